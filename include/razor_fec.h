@@ -1,0 +1,206 @@
+/*
+ * razor_fec.h -- C ABI of the MI355X-native flex-FEC engine.
+ *
+ * Two layers, both exported from librazor_fec.so:
+ *
+ *  1. Drop-in symbols with the reference signatures (link-compatible with the
+ *     callers in sim_transport/fec/flex_fec_sender.c:175,219 and
+ *     flex_fec_receiver.c:144,200):
+ *        flex_fec_generate   replaces sim_transport/fec/flex_fec_xor.h:7 (.c:4-53)
+ *        flex_fec_recover    replaces sim_transport/fec/flex_fec_xor.h:8 (.c:55-104)
+ *     Each call runs on the GPU (one launch over a zero-copy staging area).
+ *
+ *  2. A batched, device-resident API (rfec_*): many independent FEC groups laid
+ *     out structure-of-arrays in HBM, encoded / recovered by one kernel launch
+ *     each.  The plan (which segments every parity line covers) restates
+ *     flex_fec_sender_num_packets / flex_fec_sender_update
+ *     (sim_transport/fec/flex_fec_sender.c:81-135, 146-245).
+ *
+ * All pointers passed to rfec_*_batch are DEVICE pointers; `stream` is a
+ * hipStream_t passed as void* (NULL = the default stream).  Nothing in this
+ * header needs HIP headers.
+ */
+#ifndef RAZOR_FEC_H_
+#define RAZOR_FEC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Reference ABI types (sim_transport/sim_proto.h:54, 80-99, 145-174).       */
+/* When the reference's own sim_proto.h is already included, its definitions */
+/* are used and these are skipped; the layouts are identical.                */
+/* ------------------------------------------------------------------------ */
+#ifndef SIM_VIDEO_SIZE
+#define SIM_VIDEO_SIZE 1000 /* sim_proto.h:54 */
+#endif
+
+#ifndef __sim_proto_h_001__
+typedef struct {
+    uint32_t packet_id;     /* offset  0 */
+    uint32_t fid;           /* offset  4 */
+    uint32_t timestamp;     /* offset  8 */
+    uint16_t index;         /* offset 12 */
+    uint16_t total;         /* offset 14 */
+    uint8_t ftype;          /* offset 16 */
+    uint8_t payload_type;   /* offset 17 */
+    uint8_t remb;           /* offset 18 */
+    uint16_t fec_id;        /* offset 20 */
+    uint16_t send_ts;       /* offset 22 */
+    uint16_t transport_seq; /* offset 24 */
+    uint32_t send_id;       /* offset 28 */
+    uint16_t data_size;     /* offset 32 */
+    uint8_t data[SIM_VIDEO_SIZE]; /* offset 34 (not 16-B aligned) */
+} sim_segment_t;
+
+typedef struct {
+    uint32_t seq;  /* XOR of packet_id */
+    uint32_t fid;
+    uint32_t ts;   /* XOR of timestamp */
+    uint16_t index;
+    uint16_t total;
+    uint8_t ftype;
+    uint8_t payload_type;
+    uint16_t size; /* XOR of data_size */
+} sim_fec_meta_t;
+
+typedef struct {
+    uint16_t fec_id;        /* offset  0 */
+    uint8_t row;            /* offset  2 */
+    uint8_t col;            /* offset  3 */
+    uint8_t index;          /* offset  4: row r, or 0x80|c for column c */
+    uint16_t count;         /* offset  6 */
+    uint32_t base_id;       /* offset  8 */
+    uint32_t send_ts;       /* offset 12 */
+    uint16_t transport_seq; /* offset 16 */
+    sim_fec_meta_t fec_meta; /* offset 20 */
+    uint16_t fec_data_size; /* offset 40 */
+    uint8_t fec_data[SIM_VIDEO_SIZE]; /* offset 42 */
+} sim_fec_t;
+#endif /* __sim_proto_h_001__ */
+
+/* Drop-in entry points: same names, argument meaning and 0 / -1 returns as
+ * flex_fec_xor.c:4-53 and :55-104 (see DESIGN.md for the side effects kept). */
+int flex_fec_generate(sim_segment_t* segs[], int segs_count, sim_fec_t* fec);
+int flex_fec_recover(sim_segment_t* segs[], int segs_count, sim_fec_t* fec, sim_segment_t* out_seg);
+
+/* SIM_VIDEO_SIZE this library's drop-in symbols were compiled with. */
+int rfec_sim_video_size(void);
+
+/* ------------------------------------------------------------------------ */
+/* Batched device API                                                        */
+/* ------------------------------------------------------------------------ */
+#define RFEC_MAX_K 128     /* segments per group (sim_sender.c:370 flushes at 100) */
+#define RFEC_MAX_LINES 64  /* parity lines per group */
+
+#define RFEC_OK 0
+#define RFEC_EINVAL (-1)
+#define RFEC_EDEVICE (-2)
+#define RFEC_ENOMEM (-3)
+
+/* 20-byte header record.  Field order and widths are sim_fec_meta_t's, so the
+ * XOR of several records, taken as five 32-bit words, is the record of the
+ * XORed fields (flex_fec_xor.c:13-20, 37-44, 64-85). */
+typedef struct {
+    uint32_t seq;   /* packet_id */
+    uint32_t fid;
+    uint32_t ts;    /* timestamp */
+    uint16_t index;
+    uint16_t total;
+    uint8_t ftype;
+    uint8_t payload_type;
+    uint16_t size;  /* data_size */
+} rfec_hdr;
+
+/* One parity line: members first, first+stride, ..., first+(count-1)*stride. */
+typedef struct {
+    uint8_t first;
+    uint8_t stride;
+    uint8_t count;
+    uint8_t index; /* sim_fec_t.index: row r, or 0x80|c (flex_fec_sender.c:180,224) */
+} rfec_line;
+
+#define RFEC_LAYER_ROWS 1u
+#define RFEC_LAYER_COLS 2u
+
+typedef struct {
+    uint16_t k;        /* segments per group */
+    uint8_t row, col;  /* matrix shape (flex_fec_sender_t.row/.col) */
+    uint8_t rc;        /* 1 when the planner chose matrix mode */
+    uint8_t n_lines;   /* parity lines emitted (lines with <2 members dropped) */
+    uint8_t n_row_lines;
+    uint8_t reserved;
+    rfec_line line[RFEC_MAX_LINES]; /* rows first, then columns, reference order */
+} rfec_plan;
+
+/* Restates flex_fec_sender_num_packets (flex_fec_sender.c:81-135).  Writes
+ * row/col and returns rc (0 strip mode, 1 matrix mode); k==0 -> (0,0). */
+int rfec_num_packets(uint16_t k, uint8_t protect_fraction, uint8_t* row, uint8_t* col);
+
+/* Plan of flex_fec_sender_update (flex_fec_sender.c:146-245) for a group of
+ * k segments at the given protect_fraction, restricted to `layers`.  Lines
+ * whose flex_fec_generate would fail (fewer than 2 members) are dropped, as
+ * the reference drops them.  Returns RFEC_OK or RFEC_EINVAL. */
+int rfec_plan_from_fraction(uint16_t k, uint8_t protect_fraction, unsigned layers, rfec_plan* plan);
+
+/* Plan for an explicit row x col matrix over k segments (rows of `col`
+ * consecutive segments, columns strided by `col`). */
+int rfec_plan_matrix(uint16_t k, uint8_t row, uint8_t col, unsigned layers, rfec_plan* plan);
+
+/*
+ * Device layout (G groups, k segments, n = plan->n_lines):
+ *   shards  [G][k][stride] u8    payloads, bytes beyond data_size MUST be 0
+ *   hdr     [G][k]         rfec_hdr
+ *   parity  [G][n][stride] u8    fec_data; bytes beyond fec_data_size are 0
+ *   meta    [G][n]         rfec_hdr  (fec_meta)
+ *   fec_size[G][n]         u16   (fec_data_size)
+ *   status  [G][n]         i8    0, or -1 where flex_fec_generate returns -1
+ * stride is a multiple of 16 and >= capacity; capacity plays SIM_VIDEO_SIZE.
+ */
+int rfec_encode_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
+                      const uint8_t* shards, const rfec_hdr* hdr, uint8_t* parity, rfec_hdr* meta,
+                      uint16_t* fec_size, int8_t* status, void* stream);
+
+/*
+ * Peeling recovery (flex_fec_receiver.c:105-206 + the cascade of
+ * sim_receiver.c:780-804), batched:
+ *   shards/hdr       in/out: erased slots are filled with the recovered segment
+ *   present          [G][2] u64: bit i = segment i was received
+ *   parity/meta/fec_size as produced by rfec_encode_batch
+ *   parity_present   [G] u64: bit l = parity line l was received
+ *   recovered        [G][2] u64 out: bit i = segment i was recovered here
+ *   workspace        rfec_recover_workspace_size(plan, G) bytes of device memory
+ * A line recovers its single missing member only under the conditions of
+ * flex_recover_row/col and flex_fec_recover (sizes within fec_data_size).
+ */
+size_t rfec_recover_workspace_size(const rfec_plan* plan, uint32_t groups);
+int rfec_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
+                       uint8_t* shards, rfec_hdr* hdr, const uint64_t* present,
+                       const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fec_size,
+                       const uint64_t* parity_present, uint64_t* recovered, void* workspace,
+                       void* stream);
+
+/* Zero bytes [data_size, stride) of every shard (establishes the layout
+ * invariant for callers that cannot guarantee it). */
+int rfec_zero_tails(uint32_t groups, uint32_t k, uint32_t stride, uint8_t* shards,
+                    const rfec_hdr* hdr, void* stream);
+
+/* Kernel-selection knobs, for benchmarking and A/B tests (0 = defaults:
+ * specialised row kernels where the plan allows, non-temporal streaming). */
+#define RFEC_TUNE_GENERIC 1u  /* always use the generic plan-driven kernel */
+#define RFEC_TUNE_TEMPORAL 2u /* plain instead of non-temporal loads/stores */
+void rfec_set_tuning(unsigned flags);
+unsigned rfec_get_tuning(void);
+
+/* Last HIP error string seen by this thread (for diagnostics). */
+const char* rfec_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RAZOR_FEC_H_ */

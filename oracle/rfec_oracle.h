@@ -1,0 +1,73 @@
+/*
+ * rfec_oracle.h -- CPU restatement of razor's flex-FEC path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Used by tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py as the checker / CPU baseline.  The product
+ * (librazor_fec.so) never links or calls anything in oracle/.
+ *
+ * Parity pinning: checked bit-for-bit against the reference C compiled from
+ * /root/reference (oracle/Makefile -> oracle/_ref/) through the golden
+ * fixtures in tests/golden/ (generator: oracle/gen_golden.c).
+ */
+#ifndef RFEC_ORACLE_H_
+#define RFEC_ORACLE_H_
+
+#include "razor_fec.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* xorshift64* as in test/common_test.c:10-16 */
+uint64_t oracle_xs_next(uint64_t* state);
+/* cf_rand (test/common_test.c:18-26): uniform integer in [0, t] */
+uint32_t oracle_xs_rand(uint64_t* state, uint32_t t);
+
+/* Synthetic group fill.  shards [G][k][stride], hdr [G][k].
+ * ragged==0: data_size = S; else data_size = 1 + cf_rand(S-1) from a second
+ * stream, bytes beyond data_size zeroed.  seed = 0x52415A4F52464543 ^ config_id. */
+void oracle_fill_groups(uint64_t config_id, uint32_t groups, uint32_t k, uint32_t S, uint32_t stride,
+                        int ragged, uint8_t* shards, rfec_hdr* hdr);
+
+/* flex_fec_xor.c:4-53 with SIM_VIDEO_SIZE replaced by `capacity`. */
+int oracle_generate(sim_segment_t* segs[], int segs_count, sim_fec_t* fec, int capacity);
+/* flex_fec_xor.c:55-104 */
+int oracle_recover(sim_segment_t* segs[], int segs_count, sim_fec_t* fec, sim_segment_t* out_seg);
+
+/* flex_fec_sender.c:81-135 */
+int oracle_num_packets(int segs_count, int protect_fraction, int* row, int* col);
+/* flex_fec_sender.c:146-245 line layout */
+int oracle_plan_from_fraction(int k, int protect_fraction, unsigned layers, rfec_plan* plan);
+int oracle_plan_matrix(int k, int row, int col, unsigned layers, rfec_plan* plan);
+
+/* Batched restatements over the device layout (include/razor_fec.h). */
+void oracle_encode_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
+                         const uint8_t* shards, const rfec_hdr* hdr, uint8_t* parity, rfec_hdr* meta,
+                         uint16_t* fec_size, int8_t* status);
+void oracle_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
+                          uint8_t* shards, rfec_hdr* hdr, const uint64_t* present,
+                          const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fec_size,
+                          const uint64_t* parity_present, uint64_t* recovered);
+
+/* Reference-shaped CPU path for the baseline: per group, builds sim_segment_t*
+ * arrays over AoS segments (segs[G*k], each sizeof(sim_segment_t) at this
+ * build's SIM_VIDEO_SIZE) and calls oracle_generate once per plan line,
+ * exactly as flex_fec_sender_update does.  Returns parities produced. */
+long oracle_encode_aos(const rfec_plan* plan, uint32_t groups, sim_segment_t* segs, sim_fec_t* fecs);
+/* Same, split over `threads` pthreads by contiguous group ranges. */
+long oracle_encode_aos_mt(const rfec_plan* plan, uint32_t groups, sim_segment_t* segs, sim_fec_t* fecs,
+                          int threads);
+/* Per group, recover the erased segments of `present` from row/col parities
+ * with oracle_recover (canonical peel order).  Returns segments recovered. */
+long oracle_recover_aos(const rfec_plan* plan, uint32_t groups, sim_segment_t* segs,
+                        sim_fec_t* fecs, const uint64_t* present, sim_segment_t* out);
+
+int oracle_sim_video_size(void);
+size_t oracle_segment_size(void);
+size_t oracle_fec_size(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

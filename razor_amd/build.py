@@ -1,0 +1,91 @@
+"""Builds the native library librazor_fec.so (HIP kernels for gfx950 + C host
+layer) in-tree, under razor_amd/lib/.
+
+Two variants are produced; they differ only in the SIM_VIDEO_SIZE the drop-in
+symbols flex_fec_generate/flex_fec_recover are compiled with (the batched
+rfec_* API takes the payload capacity at run time):
+
+    lib/librazor_fec.so        SIM_VIDEO_SIZE 1000 (the reference default, sim_proto.h:54)
+    lib/librazor_fec_v1200.so  SIM_VIDEO_SIZE 1200 (the 1200-byte benchmark packets)
+
+Usage: python -m razor_amd.build [--force]
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+LIBDIR = PKG / "lib"
+OBJDIR = PKG / "lib" / "obj"
+INCLUDE = ROOT / "include"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("RFEC_OFFLOAD_ARCH", "gfx950")
+
+HIP_SRC = [CSRC / "rfec_kernels.hip"]
+C_SRC = [CSRC / "rfec_host.c"]
+HEADERS = [INCLUDE / "razor_fec.h", CSRC / "rfec_internal.h"]
+
+VARIANTS = {"librazor_fec.so": 1000, "librazor_fec_v1200.so": 1200}
+
+
+def _hipcc() -> str:
+    p = ROCM / "bin" / "hipcc"
+    return str(p) if p.exists() else "hipcc"
+
+
+def _stale(out: Path, deps) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"build step failed: {' '.join(map(str, cmd))}")
+    return r
+
+
+def build(force: bool = False, verbose: bool = False) -> dict:
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    OBJDIR.mkdir(parents=True, exist_ok=True)
+    built = {}
+    kobj = OBJDIR / "rfec_kernels.o"
+    if force or _stale(kobj, HIP_SRC + HEADERS):
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+              f"-I{INCLUDE}", f"-I{CSRC}", "-c", str(HIP_SRC[0]), "-o", str(kobj)])
+        if verbose:
+            print("built", kobj)
+    for name, vsize in VARIANTS.items():
+        hobj = OBJDIR / f"rfec_host_v{vsize}.o"
+        if force or _stale(hobj, C_SRC + HEADERS):
+            _run(["gcc", "-std=c99", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
+                  f"-DSIM_VIDEO_SIZE={vsize}", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}",
+                  f"-I{INCLUDE}", f"-I{CSRC}", "-c", str(C_SRC[0]), "-o", str(hobj)])
+        so = LIBDIR / name
+        if force or _stale(so, [kobj, hobj]):
+            _run([_hipcc(), "-shared", "-fPIC", str(kobj), str(hobj), "-o", str(so),
+                  f"-Wl,-soname,{name}", "-lpthread", "-lm"])
+            if verbose:
+                print("built", so)
+        built[name] = so
+    return built
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    out = build(force="--force" in argv, verbose=True)
+    for k, v in out.items():
+        print(k, v)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,509 @@
+/*
+ * rfec_host.c -- C host layer of the MI355X flex-FEC engine (C99 + the HIP
+ * runtime C API).  Three parts:
+ *
+ *  1. The planner: restates flex_fec_sender_num_packets and the row / column
+ *     line layout of flex_fec_sender_update
+ *     (sim_transport/fec/flex_fec_sender.c:81-135, :158-233).
+ *  2. The batched device API (rfec_encode_batch / rfec_recover_batch):
+ *     argument checks, then one launch through the shim in rfec_kernels.hip.
+ *  3. The drop-in flex_fec_generate / flex_fec_recover
+ *     (sim_transport/fec/flex_fec_xor.h:7-8): each call stages its segments
+ *     into a per-thread pinned, device-mapped area and runs the same kernels
+ *     on the GPU as a one-group batch.  There is no CPU compute path: without
+ *     a usable HIP device the calls print an error once and return -1.
+ */
+#define _POSIX_C_SOURCE 200809L
+#ifndef __HIP_PLATFORM_AMD__
+#define __HIP_PLATFORM_AMD__ 1
+#endif
+#include <hip/hip_runtime_api.h>
+
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "razor_fec.h"
+#include "rfec_internal.h"
+
+/* ------------------------------------------------------------------------ */
+/* errors                                                                    */
+/* ------------------------------------------------------------------------ */
+static __thread char t_err[256];
+
+static int set_err(int code, const char* what, int hip_code)
+{
+    if (hip_code)
+        snprintf(t_err, sizeof(t_err), "%s: %s (hip %d)", what, rfec_hip_error_string(hip_code), hip_code);
+    else
+        snprintf(t_err, sizeof(t_err), "%s", what);
+    return code;
+}
+
+const char* rfec_last_error(void) { return t_err; }
+
+int rfec_sim_video_size(void) { return SIM_VIDEO_SIZE; }
+
+static unsigned g_tuning = 0;
+void rfec_set_tuning(unsigned flags) { g_tuning = flags; }
+unsigned rfec_get_tuning(void) { return g_tuning; }
+
+/* ------------------------------------------------------------------------ */
+/* 1. planner                                                                */
+/* ------------------------------------------------------------------------ */
+int rfec_num_packets(uint16_t k, uint8_t protect_fraction, uint8_t* row, uint8_t* col)
+{
+    const int n = k, pf = protect_fraction;
+    uint8_t r = 0, c = 0;
+    int rc = 0;
+    if (n == 0) {
+        /* (0, 0) */
+    } else if (pf >= 10 && n >= 6) {
+        /* matrix mode: near-square, column count clamped to [3, 20] */
+        const double f = sqrt((double)n);
+        int cols = (int)f;
+        if ((float)cols + 0.1f < f)
+            cols = 1 + (int)f;
+        cols = cols < 3 ? 3 : (cols > 20 ? 20 : cols);
+        r = (uint8_t)(n / cols + (n % cols != 0));
+        c = (uint8_t)(n / r + (n % r != 0));
+        rc = 1;
+    } else if (pf > 0) {
+        /* strip mode: about n*pf/256 row parities */
+        const int lines = (n * pf + 128) >> 8;
+        if (lines == 0) {
+            r = 1;
+            c = (uint8_t)n;
+        } else {
+            c = (uint8_t)(n / lines + (n % lines > 0));
+            r = (uint8_t)(n / c + (n % c != 0));
+        }
+    }
+    if (row)
+        *row = r;
+    if (col)
+        *col = c;
+    return rc;
+}
+
+static void add_line(rfec_plan* p, int first, int stride, int count, int index)
+{
+    if (count < 2) /* flex_fec_generate refuses <2 members: no parity on the wire */
+        return;
+    rfec_line* l = &p->line[p->n_lines++];
+    l->first = (uint8_t)first;
+    l->stride = (uint8_t)stride;
+    l->count = (uint8_t)count;
+    l->index = (uint8_t)index;
+}
+
+static int build_plan(uint16_t k, uint8_t row, uint8_t col, int rc, unsigned layers, rfec_plan* p)
+{
+    if (!p)
+        return set_err(RFEC_EINVAL, "plan is NULL", 0);
+    memset(p, 0, sizeof(*p));
+    if (k < 1 || k > RFEC_MAX_K)
+        return set_err(RFEC_EINVAL, "k out of range [1, RFEC_MAX_K]", 0);
+    p->k = k;
+    p->row = row;
+    p->col = col;
+    p->rc = (uint8_t)rc;
+    if (col <= 1)
+        return RFEC_OK; /* no parity at all (flex_fec_sender.c:158) */
+    if (layers & RFEC_LAYER_ROWS) {
+        for (int r = 0; r < row; ++r) {
+            const int first = r * col;
+            const int left = (int)k - first;
+            add_line(p, first, 1, left < col ? left : col, r);
+        }
+    }
+    p->n_row_lines = p->n_lines;
+    if ((layers & RFEC_LAYER_COLS) && row > 1 && rc == 1) {
+        for (int c = 0; c < col; ++c) {
+            int count = 0;
+            while (count < row && count * col + c < (int)k)
+                ++count;
+            add_line(p, c, col, count, 0x80 | c);
+        }
+    }
+    return RFEC_OK;
+}
+
+int rfec_plan_from_fraction(uint16_t k, uint8_t protect_fraction, unsigned layers, rfec_plan* plan)
+{
+    uint8_t row, col;
+    const int rc = rfec_num_packets(k, protect_fraction, &row, &col);
+    return build_plan(k, row, col, rc, layers, plan);
+}
+
+int rfec_plan_matrix(uint16_t k, uint8_t row, uint8_t col, unsigned layers, rfec_plan* plan)
+{
+    if (row == 0 || col == 0 || (uint32_t)row * col < k)
+        return set_err(RFEC_EINVAL, "row*col must cover k", 0);
+    return build_plan(k, row, col, 1, layers, plan);
+}
+
+/* ------------------------------------------------------------------------ */
+/* 2. batched device API                                                     */
+/* ------------------------------------------------------------------------ */
+static int check_plan(const rfec_plan* p)
+{
+    if (!p)
+        return set_err(RFEC_EINVAL, "plan is NULL", 0);
+    if (p->k < 1 || p->k > RFEC_MAX_K || p->n_lines > RFEC_MAX_LINES)
+        return set_err(RFEC_EINVAL, "plan k / n_lines out of range", 0);
+    for (int l = 0; l < p->n_lines; ++l) {
+        const rfec_line* ln = &p->line[l];
+        if (ln->count < 1 || ln->stride < 1)
+            return set_err(RFEC_EINVAL, "plan line with zero count or stride", 0);
+        if ((uint32_t)ln->first + (uint32_t)(ln->count - 1) * ln->stride >= p->k)
+            return set_err(RFEC_EINVAL, "plan line member beyond k", 0);
+    }
+    return RFEC_OK;
+}
+
+static int check_geometry(uint32_t groups, uint32_t stride, uint32_t capacity, uint32_t rows_per_group)
+{
+    if (stride == 0 || stride % 16 != 0)
+        return set_err(RFEC_EINVAL, "stride must be a positive multiple of 16", 0);
+    if (capacity > stride || capacity > 65535)
+        return set_err(RFEC_EINVAL, "capacity must be <= stride and <= 65535", 0);
+    if ((uint64_t)groups * (stride / 16) >= (1ull << 31) ||
+        (uint64_t)groups * rows_per_group * (stride / 16) >= (1ull << 40))
+        return set_err(RFEC_EINVAL, "batch too large for one launch", 0);
+    return RFEC_OK;
+}
+
+int rfec_encode_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
+                      const uint8_t* shards, const rfec_hdr* hdr, uint8_t* parity, rfec_hdr* meta,
+                      uint16_t* fec_size, int8_t* status, void* stream)
+{
+    int rc = check_plan(plan);
+    if (rc)
+        return rc;
+    if ((rc = check_geometry(groups, stride, capacity, plan->k)))
+        return rc;
+    if (groups == 0 || plan->n_lines == 0)
+        return RFEC_OK;
+    if (!shards || !hdr || !parity || !meta || !fec_size)
+        return set_err(RFEC_EINVAL, "NULL buffer", 0);
+    const int e = rfec_launch_encode(plan, groups, stride, capacity, shards, hdr, parity, meta, fec_size, status,
+                                     stream, g_tuning);
+    return e ? set_err(RFEC_EDEVICE, "encode launch", e) : RFEC_OK;
+}
+
+size_t rfec_recover_workspace_size(const rfec_plan* plan, uint32_t groups)
+{
+    if (!plan)
+        return 0;
+    return (size_t)groups * (1u + plan->n_lines) * sizeof(rfec_step);
+}
+
+static void make_masks(const rfec_plan* p, rfec_kmask* M)
+{
+    memset(M, 0, sizeof(*M));
+    M->plan = *p;
+    for (int l = 0; l < p->n_lines; ++l) {
+        const rfec_line* ln = &p->line[l];
+        for (int q = 0; q < ln->count; ++q) {
+            const int i = ln->first + q * ln->stride;
+            M->mask[l][i >> 6] |= 1ull << (i & 63);
+        }
+    }
+}
+
+int rfec_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
+                       uint8_t* shards, rfec_hdr* hdr, const uint64_t* present, const uint8_t* parity,
+                       const rfec_hdr* meta, const uint16_t* fec_size, const uint64_t* parity_present,
+                       uint64_t* recovered, void* workspace, void* stream)
+{
+    int rc = check_plan(plan);
+    if (rc)
+        return rc;
+    if ((rc = check_geometry(groups, stride, capacity, plan->k)))
+        return rc;
+    if (groups == 0)
+        return RFEC_OK;
+    if (!shards || !hdr || !present || !parity_present || !recovered || !workspace ||
+        (plan->n_lines && (!parity || !meta || !fec_size)))
+        return set_err(RFEC_EINVAL, "NULL buffer", 0);
+    static __thread rfec_kmask M; /* 1.3 KB: keep it off the stack */
+    make_masks(plan, &M);
+    const int e = rfec_launch_recover(&M, groups, stride, capacity, shards, hdr, present, parity, meta, fec_size,
+                                      parity_present, recovered, workspace, 1u + plan->n_lines, stream, g_tuning);
+    return e ? set_err(RFEC_EDEVICE, "recover launch", e) : RFEC_OK;
+}
+
+int rfec_zero_tails(uint32_t groups, uint32_t k, uint32_t stride, uint8_t* shards, const rfec_hdr* hdr,
+                    void* stream)
+{
+    int rc = check_geometry(groups * k, stride, 0, 1);
+    if (rc)
+        return rc;
+    if (!shards || !hdr)
+        return set_err(RFEC_EINVAL, "NULL buffer", 0);
+    if (groups == 0 || k == 0)
+        return RFEC_OK;
+    const int e = rfec_launch_zero_tails(groups * k, stride, shards, hdr, stream);
+    return e ? set_err(RFEC_EDEVICE, "zero_tails launch", e) : RFEC_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* 3. drop-in single-call path                                               */
+/* ------------------------------------------------------------------------ */
+#define DI_STRIDE ((SIM_VIDEO_SIZE + 15) & ~15)
+#define DI_MAXK RFEC_MAX_K
+
+/* one pinned, device-mapped staging area per calling thread */
+typedef struct {
+    int device;
+    hipStream_t stream;
+    uint8_t* host;   /* host view */
+    uint8_t* dev;    /* device view of the same bytes */
+    size_t bytes;
+} di_ctx;
+
+typedef struct { /* offsets inside the staging area */
+    size_t shards, parity, hdr, meta, fsize, status, present, ppresent, recovered, ws, total;
+} di_layout;
+
+static di_layout di_offsets(void)
+{
+    di_layout L;
+    size_t o = 0;
+#define DI_TAKE(field, n)                  \
+    do {                                    \
+        L.field = o;                        \
+        o = (o + (size_t)(n) + 255) & ~(size_t)255; \
+    } while (0)
+    DI_TAKE(shards, (size_t)DI_MAXK * DI_STRIDE);
+    DI_TAKE(parity, DI_STRIDE);
+    DI_TAKE(hdr, DI_MAXK * sizeof(rfec_hdr));
+    DI_TAKE(meta, sizeof(rfec_hdr));
+    DI_TAKE(fsize, sizeof(uint16_t));
+    DI_TAKE(status, 1);
+    DI_TAKE(present, 2 * sizeof(uint64_t));
+    DI_TAKE(ppresent, sizeof(uint64_t));
+    DI_TAKE(recovered, 2 * sizeof(uint64_t));
+    DI_TAKE(ws, 2 * sizeof(rfec_step));
+#undef DI_TAKE
+    L.total = o;
+    return L;
+}
+
+static pthread_key_t di_key;
+static pthread_once_t di_once = PTHREAD_ONCE_INIT;
+static int di_reported = 0;
+
+static void di_free(void* p)
+{
+    di_ctx* c = (di_ctx*)p;
+    if (!c)
+        return;
+    if (c->host)
+        (void)hipHostFree(c->host);
+    if (c->stream)
+        (void)hipStreamDestroy(c->stream);
+    free(c);
+}
+
+static void di_make_key(void) { (void)pthread_key_create(&di_key, di_free); }
+
+static void di_loud(const char* msg)
+{
+    if (!di_reported) {
+        di_reported = 1;
+        fprintf(stderr, "razor_fec: %s -- flex_fec_generate/flex_fec_recover need a HIP device (no CPU path)\n",
+                msg);
+    }
+}
+
+static di_ctx* di_get(void)
+{
+    pthread_once(&di_once, di_make_key);
+    di_ctx* c = (di_ctx*)pthread_getspecific(di_key);
+    if (c)
+        return c;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) {
+        set_err(RFEC_EDEVICE, "no HIP device", e);
+        di_loud(t_err);
+        return NULL;
+    }
+    c = (di_ctx*)calloc(1, sizeof(*c));
+    if (!c)
+        return NULL;
+    const di_layout L = di_offsets();
+    c->bytes = L.total;
+    if ((e = hipGetDevice(&c->device)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&c->host, c->bytes, hipHostMallocMapped)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&c->dev, c->host, 0)) != hipSuccess) {
+        set_err(RFEC_EDEVICE, "staging setup", e);
+        di_loud(t_err);
+        di_free(c);
+        return NULL;
+    }
+    pthread_setspecific(di_key, c);
+    return c;
+}
+
+static void seg_to_hdr(const sim_segment_t* s, rfec_hdr* h)
+{
+    h->seq = s->packet_id;
+    h->fid = s->fid;
+    h->ts = s->timestamp;
+    h->index = s->index;
+    h->total = s->total;
+    h->ftype = s->ftype;
+    h->payload_type = s->payload_type;
+    h->size = s->data_size;
+}
+
+static void stage_payload(uint8_t* slot, const uint8_t* data, uint32_t size)
+{
+    const uint32_t n = size < SIM_VIDEO_SIZE ? size : SIM_VIDEO_SIZE;
+    memcpy(slot, data, n);
+    memset(slot + n, 0, DI_STRIDE - n);
+}
+
+static int di_sync(di_ctx* c, int launch_err, const char* what)
+{
+    if (launch_err)
+        return set_err(RFEC_EDEVICE, what, launch_err);
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    return e == hipSuccess ? RFEC_OK : set_err(RFEC_EDEVICE, what, e);
+}
+
+/* flex_fec_xor.c:4-53 on the GPU. */
+int flex_fec_generate(sim_segment_t* segs[], int segs_count, sim_fec_t* fec)
+{
+    if (segs_count <= 1) /* :9-10 */
+        return -1;
+    if (segs_count > DI_MAXK) {
+        set_err(RFEC_EINVAL, "segs_count above RFEC_MAX_K", 0);
+        return -1;
+    }
+    di_ctx* c = di_get();
+    if (!c)
+        return -1;
+    const di_layout L = di_offsets();
+    rfec_hdr* hh = (rfec_hdr*)(c->host + L.hdr);
+    for (int i = 0; i < segs_count; ++i) {
+        stage_payload(c->host + L.shards + (size_t)i * DI_STRIDE, segs[i]->data, segs[i]->data_size);
+        seg_to_hdr(segs[i], &hh[i]);
+    }
+    rfec_plan p;
+    memset(&p, 0, sizeof(p));
+    p.k = (uint16_t)segs_count;
+    p.n_lines = 1;
+    p.line[0].first = 0;
+    p.line[0].stride = 1;
+    p.line[0].count = (uint8_t)segs_count;
+    const int e = rfec_launch_encode(&p, 1, DI_STRIDE, SIM_VIDEO_SIZE, c->dev + L.shards,
+                                     (const rfec_hdr*)(c->dev + L.hdr), c->dev + L.parity,
+                                     (rfec_hdr*)(c->dev + L.meta), (uint16_t*)(c->dev + L.fsize),
+                                     (int8_t*)(c->dev + L.status), c->stream, g_tuning);
+    if (di_sync(c, e, "flex_fec_generate") != RFEC_OK) {
+        di_loud(t_err);
+        return -1;
+    }
+    const rfec_hdr* m = (const rfec_hdr*)(c->host + L.meta);
+    const uint16_t fds = *(const uint16_t*)(c->host + L.fsize);
+    const int8_t st = *(const int8_t*)(c->host + L.status);
+    fec->fec_data_size = fds;
+    if (st != 0) {
+        /* over capacity (:27-28): the reference has written seg0's header and
+         * the size by then, nothing else */
+        seg_to_hdr(segs[0], (rfec_hdr*)&fec->fec_meta);
+        return -1;
+    }
+    memcpy(&fec->fec_meta, m, sizeof(rfec_hdr));
+    memcpy(fec->fec_data, c->host + L.parity, fds);
+    /* in-place zero padding of segs[1..] to fec_data_size (:47) */
+    for (int i = 1; i < segs_count; ++i)
+        if (segs[i]->data_size < fds)
+            memset(segs[i]->data + segs[i]->data_size, 0, (size_t)(fds - segs[i]->data_size));
+    return 0;
+}
+
+/* flex_fec_xor.c:55-104 on the GPU: the n present segments plus one erased
+ * slot form a one-line group that the peel + recovery kernels repair. */
+int flex_fec_recover(sim_segment_t* segs[], int segs_count, sim_fec_t* fec, sim_segment_t* out_seg)
+{
+    if (segs_count <= 0) /* :60-61 */
+        return -1;
+    if (segs_count + 1 > DI_MAXK) {
+        set_err(RFEC_EINVAL, "segs_count above RFEC_MAX_K-1", 0);
+        return -1;
+    }
+    const uint32_t Lfec = fec->fec_data_size;
+    if (Lfec > SIM_VIDEO_SIZE) {
+        set_err(RFEC_EINVAL, "fec_data_size above SIM_VIDEO_SIZE", 0);
+        return -1;
+    }
+    di_ctx* c = di_get();
+    if (!c)
+        return -1;
+    const di_layout L = di_offsets();
+    const int k = segs_count + 1;
+    rfec_hdr* hh = (rfec_hdr*)(c->host + L.hdr);
+    for (int i = 0; i < segs_count; ++i) {
+        stage_payload(c->host + L.shards + (size_t)i * DI_STRIDE, segs[i]->data, segs[i]->data_size);
+        seg_to_hdr(segs[i], &hh[i]);
+    }
+    memset(&hh[segs_count], 0, sizeof(rfec_hdr));
+    stage_payload(c->host + L.parity, fec->fec_data, Lfec);
+    memcpy(c->host + L.meta, &fec->fec_meta, sizeof(rfec_hdr));
+    *(uint16_t*)(c->host + L.fsize) = (uint16_t)Lfec;
+    uint64_t* pres = (uint64_t*)(c->host + L.present);
+    pres[0] = pres[1] = 0;
+    for (int i = 0; i < segs_count; ++i)
+        pres[i >> 6] |= 1ull << (i & 63);
+    *(uint64_t*)(c->host + L.ppresent) = 1;
+    rfec_kmask* M = (rfec_kmask*)calloc(1, sizeof(rfec_kmask));
+    if (!M)
+        return -1;
+    M->plan.k = (uint16_t)k;
+    M->plan.n_lines = 1;
+    M->plan.line[0].first = 0;
+    M->plan.line[0].stride = 1;
+    M->plan.line[0].count = (uint8_t)k;
+    for (int i = 0; i < k; ++i)
+        M->mask[0][i >> 6] |= 1ull << (i & 63);
+    const int e = rfec_launch_recover(M, 1, DI_STRIDE, SIM_VIDEO_SIZE, c->dev + L.shards,
+                                      (rfec_hdr*)(c->dev + L.hdr), (const uint64_t*)(c->dev + L.present),
+                                      c->dev + L.parity, (const rfec_hdr*)(c->dev + L.meta),
+                                      (const uint16_t*)(c->dev + L.fsize), (const uint64_t*)(c->dev + L.ppresent),
+                                      (uint64_t*)(c->dev + L.recovered), c->dev + L.ws, 2, c->stream, g_tuning);
+    free(M);
+    if (di_sync(c, e, "flex_fec_recover") != RFEC_OK) {
+        di_loud(t_err);
+        return -1;
+    }
+    /* in-place zero padding of the present segments (:91), up to the first
+     * one the reference rejects (:88-89) */
+    for (int i = 0; i < segs_count; ++i) {
+        if (segs[i]->data_size > Lfec)
+            break;
+        memset(segs[i]->data + segs[i]->data_size, 0, (size_t)(Lfec - segs[i]->data_size));
+    }
+    const uint64_t* rec = (const uint64_t*)(c->host + L.recovered);
+    if (!((rec[segs_count >> 6] >> (segs_count & 63)) & 1ull))
+        return -1;
+    const rfec_hdr* r = &hh[segs_count];
+    out_seg->packet_id = r->seq;
+    out_seg->fid = r->fid;
+    out_seg->timestamp = r->ts;
+    out_seg->index = r->index;
+    out_seg->total = r->total;
+    out_seg->ftype = r->ftype;
+    out_seg->payload_type = r->payload_type;
+    out_seg->data_size = r->size;
+    memcpy(out_seg->data, c->host + L.shards + (size_t)segs_count * DI_STRIDE, Lfec);
+    out_seg->fec_id = fec->fec_id; /* :101 */
+    return 0;
+}

@@ -1,0 +1,244 @@
+"""Python view of the C ABI in include/razor_fec.h (ctypes).
+
+The product is librazor_fec.so (HIP kernels + C host layer).  This module only
+loads it, mirrors its structs, and passes device pointers / streams through;
+it has no compute path of its own.  Loading fails loudly when the library is
+missing, and every call checks the C return code.
+
+Reference interface mirrored (yuanrongxi/razor):
+  flex_fec_generate / flex_fec_recover      sim_transport/fec/flex_fec_xor.h:7-8
+  flex_fec_sender_num_packets (planner)     sim_transport/fec/flex_fec_sender.c:81-135
+  row/column parity lines                   sim_transport/fec/flex_fec_sender.c:158-233
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+from pathlib import Path
+
+import numpy as np
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+LIBDIR = PKG / "lib"
+HEADER = ROOT / "include" / "razor_fec.h"
+
+RFEC_MAX_K = 128
+RFEC_MAX_LINES = 64
+RFEC_LAYER_ROWS = 1
+RFEC_LAYER_COLS = 2
+RFEC_TUNE_GENERIC = 1
+RFEC_TUNE_TEMPORAL = 2
+
+# 20-byte header record == sim_fec_meta_t layout (sim_proto.h:145-155)
+HDR_DTYPE = np.dtype([("seq", "<u4"), ("fid", "<u4"), ("ts", "<u4"), ("index", "<u2"), ("total", "<u2"),
+                      ("ftype", "u1"), ("payload_type", "u1"), ("size", "<u2")])
+assert HDR_DTYPE.itemsize == 20
+
+
+class RfecError(RuntimeError):
+    pass
+
+
+class rfec_line(C.Structure):
+    _fields_ = [("first", C.c_uint8), ("stride", C.c_uint8), ("count", C.c_uint8), ("index", C.c_uint8)]
+
+
+class rfec_plan(C.Structure):
+    _fields_ = [("k", C.c_uint16), ("row", C.c_uint8), ("col", C.c_uint8), ("rc", C.c_uint8),
+                ("n_lines", C.c_uint8), ("n_row_lines", C.c_uint8), ("reserved", C.c_uint8),
+                ("line", rfec_line * RFEC_MAX_LINES)]
+
+    def lines(self):
+        return [(self.line[i].first, self.line[i].stride, self.line[i].count, self.line[i].index)
+                for i in range(self.n_lines)]
+
+    def members(self, l):
+        ln = self.line[l]
+        return [ln.first + q * ln.stride for q in range(ln.count)]
+
+    def __repr__(self):
+        return (f"rfec_plan(k={self.k}, row={self.row}, col={self.col}, rc={self.rc}, "
+                f"n_lines={self.n_lines}, lines={self.lines()})")
+
+
+def sim_types(video_size: int):
+    """ctypes mirrors of sim_segment_t / sim_fec_t (sim_proto.h:80-99, 157-174)."""
+
+    class sim_segment_t(C.Structure):
+        _fields_ = [("packet_id", C.c_uint32), ("fid", C.c_uint32), ("timestamp", C.c_uint32),
+                    ("index", C.c_uint16), ("total", C.c_uint16), ("ftype", C.c_uint8),
+                    ("payload_type", C.c_uint8), ("remb", C.c_uint8), ("fec_id", C.c_uint16),
+                    ("send_ts", C.c_uint16), ("transport_seq", C.c_uint16), ("send_id", C.c_uint32),
+                    ("data_size", C.c_uint16), ("data", C.c_uint8 * video_size)]
+
+    class sim_fec_meta_t(C.Structure):
+        _fields_ = [("seq", C.c_uint32), ("fid", C.c_uint32), ("ts", C.c_uint32), ("index", C.c_uint16),
+                    ("total", C.c_uint16), ("ftype", C.c_uint8), ("payload_type", C.c_uint8),
+                    ("size", C.c_uint16)]
+
+    class sim_fec_t(C.Structure):
+        _fields_ = [("fec_id", C.c_uint16), ("row", C.c_uint8), ("col", C.c_uint8), ("index", C.c_uint8),
+                    ("count", C.c_uint16), ("base_id", C.c_uint32), ("send_ts", C.c_uint32),
+                    ("transport_seq", C.c_uint16), ("fec_meta", sim_fec_meta_t), ("fec_data_size", C.c_uint16),
+                    ("fec_data", C.c_uint8 * video_size)]
+
+    assert C.sizeof(sim_fec_meta_t) == 20
+    assert C.sizeof(sim_segment_t) == ((34 + video_size + 3) // 4) * 4
+    return sim_segment_t, sim_fec_t
+
+
+_P = C.c_void_p
+_SIGS = {
+    "flex_fec_generate": (C.c_int, [_P, C.c_int, _P]),
+    "flex_fec_recover": (C.c_int, [_P, C.c_int, _P, _P]),
+    "rfec_sim_video_size": (C.c_int, []),
+    "rfec_num_packets": (C.c_int, [C.c_uint16, C.c_uint8, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]),
+    "rfec_plan_from_fraction": (C.c_int, [C.c_uint16, C.c_uint8, C.c_uint, C.POINTER(rfec_plan)]),
+    "rfec_plan_matrix": (C.c_int, [C.c_uint16, C.c_uint8, C.c_uint8, C.c_uint, C.POINTER(rfec_plan)]),
+    "rfec_encode_batch": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, C.c_uint32, C.c_uint32,
+                                    _P, _P, _P, _P, _P, _P, _P]),
+    "rfec_recover_workspace_size": (C.c_size_t, [C.POINTER(rfec_plan), C.c_uint32]),
+    "rfec_recover_batch": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, C.c_uint32, C.c_uint32,
+                                     _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "rfec_zero_tails": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    "rfec_set_tuning": (None, [C.c_uint]),
+    "rfec_get_tuning": (C.c_uint, []),
+    "rfec_last_error": (C.c_char_p, []),
+}
+
+
+def header_functions() -> list[str]:
+    """Every function declared in include/razor_fec.h."""
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*[A-Za-z_][\w\s\*]*?\b([a-z_][a-z0-9_]*)\s*\(", text, flags=re.M)))
+
+
+class Native:
+    """One loaded variant of librazor_fec.so."""
+
+    def __init__(self, video_size: int = 1000, path: str | os.PathLike | None = None):
+        name = "librazor_fec.so" if video_size == 1000 else f"librazor_fec_v{video_size}.so"
+        self.path = Path(path) if path else LIBDIR / name
+        if not self.path.exists():
+            raise RfecError(f"{self.path} is missing: build it with `python -m razor_amd.build` "
+                            "(there is no fallback path)")
+        self.lib = C.CDLL(str(self.path))
+        for fn, (res, args) in _SIGS.items():
+            f = getattr(self.lib, fn)
+            f.restype = res
+            f.argtypes = args
+        self.video_size = self.lib.rfec_sim_video_size()
+        if self.video_size != video_size:
+            raise RfecError(f"{self.path} was built with SIM_VIDEO_SIZE={self.video_size}")
+        self.sim_segment_t, self.sim_fec_t = sim_types(self.video_size)
+
+    # -- planner -------------------------------------------------------------
+    def num_packets(self, k: int, protect_fraction: int):
+        r, c = C.c_uint8(), C.c_uint8()
+        rc = self.lib.rfec_num_packets(k, protect_fraction, C.byref(r), C.byref(c))
+        return rc, r.value, c.value
+
+    def plan_from_fraction(self, k: int, protect_fraction: int, layers: int = RFEC_LAYER_ROWS | RFEC_LAYER_COLS):
+        p = rfec_plan()
+        self._check(self.lib.rfec_plan_from_fraction(k, protect_fraction, layers, C.byref(p)), "plan")
+        return p
+
+    def plan_matrix(self, k: int, row: int, col: int, layers: int = RFEC_LAYER_ROWS | RFEC_LAYER_COLS):
+        p = rfec_plan()
+        self._check(self.lib.rfec_plan_matrix(k, row, col, layers, C.byref(p)), "plan")
+        return p
+
+    # -- batched device API (pointers are device addresses as ints) ----------
+    def encode_batch(self, plan, groups, stride, capacity, shards, hdr, parity, meta, fec_size, status,
+                     stream=None):
+        self._check(self.lib.rfec_encode_batch(C.byref(plan), groups, stride, capacity, shards, hdr, parity,
+                                               meta, fec_size, status, stream), "rfec_encode_batch")
+
+    def workspace_size(self, plan, groups) -> int:
+        return self.lib.rfec_recover_workspace_size(C.byref(plan), groups)
+
+    def recover_batch(self, plan, groups, stride, capacity, shards, hdr, present, parity, meta, fec_size,
+                      parity_present, recovered, workspace, stream=None):
+        self._check(self.lib.rfec_recover_batch(C.byref(plan), groups, stride, capacity, shards, hdr, present,
+                                                parity, meta, fec_size, parity_present, recovered, workspace,
+                                                stream), "rfec_recover_batch")
+
+    def zero_tails(self, groups, k, stride, shards, hdr, stream=None):
+        self._check(self.lib.rfec_zero_tails(groups, k, stride, shards, hdr, stream), "rfec_zero_tails")
+
+    def set_tuning(self, flags: int):
+        self.lib.rfec_set_tuning(flags)
+
+    def get_tuning(self) -> int:
+        return self.lib.rfec_get_tuning()
+
+    # -- drop-in symbols --------------------------------------------------------
+    def flex_fec_generate(self, segs, fec) -> int:
+        arr = (C.c_void_p * max(1, len(segs)))(*[C.addressof(s) for s in segs])
+        return self.lib.flex_fec_generate(arr, len(segs), C.byref(fec))
+
+    def flex_fec_recover(self, segs, fec, out_seg, count=None) -> int:
+        arr = (C.c_void_p * max(1, len(segs)))(*[C.addressof(s) for s in segs])
+        n = len(segs) if count is None else count
+        return self.lib.flex_fec_recover(arr, n, C.byref(fec), C.byref(out_seg))
+
+    def last_error(self) -> str:
+        v = self.lib.rfec_last_error()
+        return v.decode() if v else ""
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RfecError(f"{what} failed ({rc}): {self.last_error()}")
+
+
+_CACHE: dict[int, Native] = {}
+
+
+def native(video_size: int = 1000) -> Native:
+    if video_size not in _CACHE:
+        _CACHE[video_size] = Native(video_size)
+    return _CACHE[video_size]
+
+
+# ---------------------------------------------------------------------------
+# torch helpers: a device-resident batch in the layout of include/razor_fec.h
+# ---------------------------------------------------------------------------
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+class DeviceBatch:
+    """G groups of k segments in HBM (torch tensors as the allocator only)."""
+
+    def __init__(self, plan, groups: int, payload: int, device, stride: int | None = None):
+        import torch
+
+        self.plan, self.groups, self.capacity = plan, groups, payload
+        self.stride = stride or ((payload + 15) // 16) * 16
+        self.k, self.n = plan.k, plan.n_lines
+        dev = torch.device(device)
+        u8 = torch.uint8
+        self.shards = torch.zeros((groups, self.k, self.stride), dtype=u8, device=dev)
+        self.hdr = torch.zeros((groups, self.k, 20), dtype=u8, device=dev)
+        self.parity = torch.zeros((groups, max(1, self.n), self.stride), dtype=u8, device=dev)
+        self.meta = torch.zeros((groups, max(1, self.n), 20), dtype=u8, device=dev)
+        self.fec_size = torch.zeros((groups, max(1, self.n)), dtype=torch.int16, device=dev)
+        self.status = torch.zeros((groups, max(1, self.n)), dtype=torch.int8, device=dev)
+        self.present = torch.zeros((groups, 2), dtype=torch.int64, device=dev)
+        self.parity_present = torch.zeros((groups,), dtype=torch.int64, device=dev)
+        self.recovered = torch.zeros((groups, 2), dtype=torch.int64, device=dev)
+        ws = groups * (1 + self.n) * 8  # rfec_recover_workspace_size()
+        self.workspace = torch.zeros((max(16, ws),), dtype=u8, device=dev)
+
+    def encode(self, lib: Native, stream=None):
+        lib.encode_batch(self.plan, self.groups, self.stride, self.capacity, _ptr(self.shards), _ptr(self.hdr),
+                         _ptr(self.parity), _ptr(self.meta), _ptr(self.fec_size), _ptr(self.status), stream)
+
+    def recover(self, lib: Native, stream=None):
+        lib.recover_batch(self.plan, self.groups, self.stride, self.capacity, _ptr(self.shards), _ptr(self.hdr),
+                          _ptr(self.present), _ptr(self.parity), _ptr(self.meta), _ptr(self.fec_size),
+                          _ptr(self.parity_present), _ptr(self.recovered), _ptr(self.workspace), stream)
+

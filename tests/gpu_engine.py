@@ -1,0 +1,67 @@
+"""Runs the product (librazor_fec.so, HIP kernels) on numpy inputs: uploads to
+HBM with torch (allocator only), calls the C ABI, downloads the results."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from razor_amd.fec import HDR_DTYPE, native
+
+
+def _dev(a: np.ndarray, device) -> torch.Tensor:
+    a = np.ascontiguousarray(a)
+    return torch.from_numpy(a.view(np.uint8).reshape(-1).copy()).to(device)
+
+
+def _host(t: torch.Tensor, dtype, shape) -> np.ndarray:
+    return t.cpu().numpy().view(dtype).reshape(shape)
+
+
+class GpuEngine:
+    def __init__(self, video_size=1000, device="cuda:0", tuning=0):
+        self.lib = native(video_size)
+        self.device = torch.device(device)
+        self.tuning = tuning
+
+    def encode(self, plan, shards, hdr, capacity):
+        G, k, stride = shards.shape
+        n = plan.n_lines
+        d_sh = _dev(shards, self.device)
+        d_h = _dev(hdr, self.device)
+        d_p = torch.full((G * n * stride,), 0x5A, dtype=torch.uint8, device=self.device)
+        d_m = torch.full((G * n * 20,), 0x5A, dtype=torch.uint8, device=self.device)
+        d_f = torch.zeros((G * n,), dtype=torch.int16, device=self.device)
+        d_s = torch.full((G * n,), 7, dtype=torch.int8, device=self.device)
+        self.lib.set_tuning(self.tuning)
+        try:
+            self.lib.encode_batch(plan, G, stride, capacity, d_sh.data_ptr(), d_h.data_ptr(), d_p.data_ptr(),
+                                  d_m.data_ptr(), d_f.data_ptr(), d_s.data_ptr(),
+                                  torch.cuda.current_stream(self.device).cuda_stream)
+            torch.cuda.synchronize(self.device)
+        finally:
+            self.lib.set_tuning(0)
+        return (_host(d_p, np.uint8, (G, n, stride)), _host(d_m, HDR_DTYPE, (G, n)),
+                _host(d_f, np.uint16, (G, n)), _host(d_s, np.int8, (G, n)))
+
+    def recover(self, plan, shards, hdr, present, parity, meta, fsize, pp, capacity):
+        G, k, stride = shards.shape
+        d_sh = _dev(shards, self.device)
+        d_h = _dev(hdr, self.device)
+        d_pr = _dev(np.ascontiguousarray(present, np.uint64), self.device)
+        d_p = _dev(parity, self.device)
+        d_m = _dev(meta, self.device)
+        d_f = _dev(np.ascontiguousarray(fsize, np.uint16), self.device)
+        d_pp = _dev(np.ascontiguousarray(pp, np.uint64), self.device)
+        d_rec = torch.full((G * 16,), 0xEE, dtype=torch.uint8, device=self.device)
+        ws = torch.zeros((max(16, self.lib.workspace_size(plan, G)),), dtype=torch.uint8, device=self.device)
+        self.lib.set_tuning(self.tuning)
+        try:
+            self.lib.recover_batch(plan, G, stride, capacity, d_sh.data_ptr(), d_h.data_ptr(), d_pr.data_ptr(),
+                                   d_p.data_ptr(), d_m.data_ptr(), d_f.data_ptr(), d_pp.data_ptr(),
+                                   d_rec.data_ptr(), ws.data_ptr(),
+                                   torch.cuda.current_stream(self.device).cuda_stream)
+            torch.cuda.synchronize(self.device)
+        finally:
+            self.lib.set_tuning(0)
+        return (_host(d_sh, np.uint8, (G, k, stride)), _host(d_h, HDR_DTYPE, (G, k)),
+                _host(d_rec, np.uint64, (G, 2)))

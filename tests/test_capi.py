@@ -1,0 +1,100 @@
+"""CPU: the C ABI library loads, exports every symbol include/razor_fec.h
+declares, and its host-side planner matches the reference (no GPU compute)."""
+import ctypes as C
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import pyoracle as po
+from razor_amd.fec import header_functions
+
+
+def test_header_symbols_exported(product, product1200):
+    fns = header_functions()
+    assert "flex_fec_generate" in fns and "rfec_encode_batch" in fns
+    for lib in (product, product1200):
+        for f in fns:
+            assert hasattr(lib.lib, f), f"{lib.path.name} does not export {f}"
+
+
+def test_variants(product, product1200):
+    assert product.video_size == 1000 and C.sizeof(product.sim_segment_t) == 1036
+    assert product1200.video_size == 1200 and C.sizeof(product1200.sim_segment_t) == 1236
+    assert C.sizeof(product.sim_fec_t) == 1044 and C.sizeof(product1200.sim_fec_t) == 1244
+
+
+def test_planner_table(product):
+    """rfec_num_packets == flex_fec_sender_num_packets for n<256, pf<256."""
+    t = po.plan_table()
+    for n in range(256):
+        for pf in range(256):
+            assert product.num_packets(n, pf) == tuple(int(x) for x in t[n, pf]), (n, pf)
+
+
+def test_plan_lines_match_oracle(product, oracle1000):
+    for k in range(1, 129):
+        for pf in range(0, 256, 3):
+            for layers in (1, 2, 3):
+                a = product.plan_from_fraction(k, pf, layers)
+                b = oracle1000.plan_from_fraction(k, pf, layers)
+                assert (a.k, a.row, a.col, a.rc, a.n_lines, a.n_row_lines) == \
+                       (b.k, b.row, b.col, b.rc, b.n_lines, b.n_row_lines), (k, pf, layers)
+                assert a.lines() == b.lines(), (k, pf, layers)
+
+
+def test_plan_counts_match_reference_emissions(product):
+    """Parities per group in the reference sender fixtures == plan lines."""
+    m = po.manifest()
+    for c in m["cases"]:
+        if c["kind"] == "sender":
+            p = product.plan_from_fraction(c["k"], c["protect_fraction"])
+            assert p.n_lines * c["groups"] == c["parities"], c["name"]
+        if c["kind"] == "sender_random":
+            groups = np.fromfile(po.GOLDEN / c["groups_file"], np.uint32).reshape(-1, 3)
+            for k, pf, n in groups:
+                assert product.plan_from_fraction(int(k), int(pf)).n_lines == n
+
+
+def test_argument_validation(product):
+    from razor_amd.fec import RfecError
+    plan = product.plan_from_fraction(10, 80, 1)
+    with pytest.raises(RfecError):  # stride not a multiple of 16
+        product.encode_batch(plan, 4, 1000, 1000, 1, 1, 1, 1, 1, None)
+    with pytest.raises(RfecError):  # capacity > stride
+        product.encode_batch(plan, 4, 1200, 1201, 1, 1, 1, 1, 1, None)
+    with pytest.raises(RfecError):  # NULL buffers
+        product.encode_batch(plan, 4, 1200, 1200, None, None, None, None, None, None)
+    with pytest.raises(RfecError):
+        product.plan_from_fraction(0, 80)
+    with pytest.raises(RfecError):
+        product.plan_from_fraction(129, 80)
+    with pytest.raises(RfecError):
+        product.plan_matrix(10, 2, 4)  # 2x4 does not cover 10
+    bad = product.plan_from_fraction(10, 80, 1)
+    bad.line[0].count = 20  # member beyond k
+    with pytest.raises(RfecError):
+        product.encode_batch(bad, 4, 1200, 1200, 1, 1, 1, 1, 1, None)
+    assert product.workspace_size(plan, 100) == 100 * (1 + plan.n_lines) * 8
+
+
+def test_dropin_fails_loudly_without_gpu():
+    """No CPU path: without a HIP device the drop-in symbols print and return -1."""
+    code = r'''
+import ctypes as C, sys
+sys.path.insert(0, ".")
+from razor_amd.fec import native
+lib = native(1000)
+a, b = lib.sim_segment_t(), lib.sim_segment_t()
+a.data_size = b.data_size = 10
+f = lib.sim_fec_t()
+print("RC", lib.flex_fec_generate([a, b], f))
+'''
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       cwd=str(po.ROOT))
+    assert "RC -1" in r.stdout, r.stdout + r.stderr
+    assert "razor_fec" in r.stderr

@@ -1,0 +1,248 @@
+"""GPU: the HIP path (librazor_fec.so through its C ABI) against the golden
+fixtures of the compiled reference and against the oracle, bit-exact."""
+import ctypes as C
+import json
+
+import numpy as np
+import pytest
+
+import parity_cases as pc
+import pyoracle as po
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+MANIFEST = po.manifest()
+CASES = {c["name"]: c for c in MANIFEST["cases"]}
+TUNINGS = {"default": 0, "generic": 1, "temporal": 2, "generic_temporal": 3}
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the -m gpu suite must run on an MI355X")
+    from gpu_engine import GpuEngine
+    return GpuEngine
+
+
+@pytest.mark.parametrize("tuning", list(TUNINGS))
+@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "sender"])
+def test_sender_fixture_gpu(gpu, oracle1000, name, tuning):
+    pc.check_sender_case(gpu(tuning=TUNINGS[tuning]), oracle1000, CASES[name])
+
+
+def test_sender_random_fixture_gpu(gpu, oracle1000):
+    pc.check_sender_random_case(gpu(), oracle1000, CASES["random_k"])
+
+
+@pytest.mark.parametrize("tuning", ["default", "generic"])
+@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "rows"])
+def test_rows_fixture_gpu(gpu, oracle1000, oracle1200, name, tuning):
+    c = CASES[name]
+    o = oracle1200 if c["S"] > 1000 else oracle1000
+    pc.check_rows_case(gpu(tuning=TUNINGS[tuning]), o, c, capacity=max(c["S"], 1000))
+
+
+@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures"])
+def test_erasure_fixture_gpu(gpu, oracle1000, name):
+    pc.check_erasure_case(gpu(), oracle1000, CASES[name])
+
+
+def test_single_cases_dropin_gpu(product):
+    """flex_fec_generate / flex_fec_recover (drop-in symbols) on the GPU vs the
+    reference's single-call outputs, including failures and in-place padding."""
+    from test_oracle_golden import run_single_cases
+
+    seg_t, fec_t = product.sim_segment_t, product.sim_fec_t
+    run_single_cases(lambda s, f: product.flex_fec_generate(s, f),
+                     lambda s, f, o: product.flex_fec_recover(s, f, o), seg_t, fec_t, 1000)
+
+
+def test_dropin_1200(product1200, oracle1200):
+    """The SIM_VIDEO_SIZE=1200 variant: a 1200-B row through the drop-in symbols."""
+    lib, o = product1200, oracle1200
+    shards, hdr = o.fill_groups(101, 1, 4, 1200, ragged=True)
+    segs = []
+    for i in range(4):
+        s = lib.sim_segment_t()
+        h = hdr[0, i]
+        s.packet_id, s.fid, s.timestamp = int(h["seq"]), int(h["fid"]), int(h["ts"])
+        s.index, s.total, s.ftype, s.payload_type = int(h["index"]), int(h["total"]), int(h["ftype"]), 0
+        s.data_size = int(h["size"])
+        C.memmove(C.addressof(s) + 34, shards[0, i].tobytes(), 1200)
+        segs.append(s)
+    fec = lib.sim_fec_t()
+    assert lib.flex_fec_generate(segs, fec) == 0
+    parity, meta, fsize, _ = o.encode_batch(o.plan_matrix(4, 1, 4, 1), shards, hdr, 1200)
+    L = int(fsize[0, 0])
+    assert fec.fec_data_size == L
+    assert bytes(fec.fec_data)[:L] == parity[0, 0, :L].tobytes()
+    out = lib.sim_segment_t()
+    assert lib.flex_fec_recover(segs[1:], fec, out) == 0
+    assert out.data_size == hdr[0, 0]["size"] and out.packet_id == hdr[0, 0]["seq"]
+    assert bytes(out.data)[:out.data_size] == shards[0, 0, :out.data_size].tobytes()
+
+
+# ---- full-size properties ---------------------------------------------------
+def _device_batch(G, k, S, seed, device="cuda:0"):
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    shards = torch.randint(0, 256, (G, k, S), dtype=torch.uint8, device=device, generator=g)
+    hdr = np.zeros((G, k), po.HDR_DTYPE)
+    gi = np.arange(G, dtype=np.uint32)[:, None]
+    ii = np.arange(k, dtype=np.uint32)[None, :]
+    hdr["seq"] = 1 + gi * k + ii
+    hdr["fid"] = 1 + gi
+    hdr["ts"] = 33 * gi
+    hdr["index"] = ii
+    hdr["total"] = k
+    hdr["ftype"] = (gi % 60 == 0)
+    hdr["size"] = S
+    d_hdr = torch.from_numpy(hdr.view(np.uint8).reshape(G, k, 20).copy()).to(device)
+    return shards, hdr, d_hdr
+
+
+def _run_encode(lib, plan, G, S, shards, d_hdr, tuning=0):
+    n = plan.n_lines
+    dev = shards.device
+    par = torch.empty((G, n, S), dtype=torch.uint8, device=dev)
+    meta = torch.empty((G, n, 20), dtype=torch.uint8, device=dev)
+    fs = torch.empty((G, n), dtype=torch.int16, device=dev)
+    st = torch.empty((G, n), dtype=torch.int8, device=dev)
+    lib.set_tuning(tuning)
+    try:
+        lib.encode_batch(plan, G, S, S, shards.data_ptr(), d_hdr.data_ptr(), par.data_ptr(), meta.data_ptr(),
+                         fs.data_ptr(), st.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    finally:
+        lib.set_tuning(0)
+    torch.cuda.synchronize()
+    return par, meta, fs, st
+
+
+@pytest.mark.parametrize("layers", [1, 3])
+def test_full_size_k10_roundtrip(product, oracle1200, layers):
+    """Config 2/3 shape (G=65536, k=10, 1200 B): fast == generic kernel bit for
+    bit, a sample equals the oracle, and 2 erasures per group round-trip."""
+    lib, o = product, oracle1200
+    G, k, S = 65536, 10, 1200
+    plan = lib.plan_from_fraction(k, 80, layers)
+    shards, hdr, d_hdr = _device_batch(G, k, S, 1234)
+    par, meta, fs, st = _run_encode(lib, plan, G, S, shards, d_hdr)
+    par2, meta2, fs2, st2 = _run_encode(lib, plan, G, S, shards, d_hdr, tuning=3)
+    assert torch.equal(par, par2) and torch.equal(meta, meta2) and torch.equal(fs, fs2)
+    assert int(st.abs().sum()) == 0
+    # oracle on a sample of groups
+    idx = np.r_[0:8, G // 2:G // 2 + 8, G - 8:G]
+    sh_h = shards[idx].cpu().numpy()
+    p_o, m_o, f_o, s_o = o.encode_batch(o.plan_from_fraction(k, 80, layers), sh_h, hdr[idx], 1200)
+    assert np.array_equal(par[idx].cpu().numpy(), p_o)
+    assert np.array_equal(meta[idx].cpu().numpy().view(po.HDR_DTYPE).reshape(len(idx), -1), m_o)
+    assert np.array_equal(fs[idx].cpu().numpy().view(np.uint16), f_o)
+    # erasures: 2 per group; rows only -> distinct rows (all recoverable)
+    rng = np.random.default_rng(7)
+    if layers == 1:
+        rows = [[0, 1, 2, 3], [4, 5, 6, 7], [8, 9]]
+        pairs = [(a, b) for r1 in range(3) for r2 in range(r1 + 1, 3) for a in rows[r1] for b in rows[r2]]
+        assert len(pairs) == 32
+    else:
+        pairs = [(a, b) for a in range(k) for b in range(a + 1, k)]
+        assert len(pairs) == 45
+    choice = rng.integers(0, len(pairs), G)
+    er = np.array(pairs)[choice]
+    present = np.full((G, 2), 0, np.uint64)
+    present[:, 0] = np.uint64((1 << k) - 1) & ~((np.uint64(1) << er[:, 0].astype(np.uint64)) |
+                                               (np.uint64(1) << er[:, 1].astype(np.uint64)))
+    rx = shards.clone()
+    rx_hdr = d_hdr.clone()
+    gi = torch.arange(G, device=rx.device)
+    for c in range(2):
+        e = torch.from_numpy(er[:, c]).to(rx.device)
+        rx[gi, e] = 0xA5
+        rx_hdr[gi, e] = 0
+    d_pres = torch.from_numpy(present.view(np.int64)).to(rx.device)
+    d_pp = torch.full((G,), (1 << plan.n_lines) - 1, dtype=torch.int64, device=rx.device)
+    rec = torch.empty((G, 2), dtype=torch.int64, device=rx.device)
+    ws = torch.empty((lib.workspace_size(plan, G),), dtype=torch.uint8, device=rx.device)
+    lib.recover_batch(plan, G, S, S, rx.data_ptr(), rx_hdr.data_ptr(), d_pres.data_ptr(), par.data_ptr(),
+                      meta.data_ptr(), fs.data_ptr(), d_pp.data_ptr(), rec.data_ptr(), ws.data_ptr(),
+                      torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(rx, shards)
+    assert torch.equal(rx_hdr, d_hdr)
+    exp = ((1 << er[:, 0]) | (1 << er[:, 1])).astype(np.int64)
+    assert np.array_equal(rec[:, 0].cpu().numpy(), exp)
+
+
+def test_full_size_k32_s256(product, oracle1000):
+    """Config 5 shape: k=32, 8 rows of 4, 256-B packets, G=65536."""
+    lib, o = product, oracle1000
+    G, k, S = 65536, 32, 256
+    plan = lib.plan_matrix(k, 8, 4, 1)
+    assert plan.n_lines == 8
+    shards, hdr, d_hdr = _device_batch(G, k, S, 99)
+    par, meta, fs, st = _run_encode(lib, plan, G, S, shards, d_hdr)
+    par2, *_ = _run_encode(lib, plan, G, S, shards, d_hdr, tuning=1)
+    assert torch.equal(par, par2)
+    idx = np.r_[0:4, G - 4:G]
+    p_o, m_o, f_o, _ = o.encode_batch(o.plan_matrix(k, 8, 4, 1), shards[idx].cpu().numpy(), hdr[idx], 256)
+    assert np.array_equal(par[idx].cpu().numpy(), p_o)
+    assert np.array_equal(meta[idx].cpu().numpy().view(po.HDR_DTYPE).reshape(len(idx), -1), m_o)
+
+
+def test_zero_tails(product):
+    lib = product
+    G, k, S = 37, 5, 1200
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, (G, k, S), dtype=np.uint8)
+    hdr = np.zeros((G, k), po.HDR_DTYPE)
+    hdr["size"] = rng.integers(0, S + 1, (G, k))
+    hdr["size"][0, 0] = 0
+    hdr["size"][0, 1] = S
+    hdr["size"][0, 2] = 17
+    d = torch.from_numpy(data.copy()).cuda()
+    dh = torch.from_numpy(hdr.view(np.uint8).reshape(-1).copy()).cuda()
+    lib.zero_tails(G, k, S, d.data_ptr(), dh.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    exp = data.copy()
+    for g in range(G):
+        for i in range(k):
+            exp[g, i, hdr["size"][g, i]:] = 0
+    assert np.array_equal(d.cpu().numpy(), exp)
+
+
+def test_empty_and_degenerate(product):
+    lib = product
+    s = torch.cuda.current_stream().cuda_stream
+    plan = lib.plan_from_fraction(10, 80, 1)
+    # zero groups: a no-op that returns OK
+    lib.encode_batch(plan, 0, 1200, 1200, None, None, None, None, None, None, s)
+    # a plan with no lines (pf = 0 -> col = 0)
+    p0 = lib.plan_from_fraction(10, 0, 3)
+    assert p0.n_lines == 0
+    d = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    lib.encode_batch(p0, 4, 16, 16, d.data_ptr(), d.data_ptr(), d.data_ptr(), d.data_ptr(), d.data_ptr(), None, s)
+    torch.cuda.synchronize()
+
+
+def test_capacity_status(product):
+    """status -1 where a line's fec_data_size exceeds capacity (flex_fec_xor.c:27-28)."""
+    lib = product
+    plan = lib.plan_matrix(4, 2, 2, 1)
+    G, k, S = 3, 4, 64
+    hdr = np.zeros((G, k), po.HDR_DTYPE)
+    hdr["size"] = 10
+    hdr["size"][1, 2] = 60  # group 1, row 1 over capacity 48
+    sh = torch.zeros((G, k, S), dtype=torch.uint8, device="cuda")
+    dh = torch.from_numpy(hdr.view(np.uint8).reshape(-1).copy()).cuda()
+    par = torch.empty((G, 2, S), dtype=torch.uint8, device="cuda")
+    meta = torch.empty((G, 2, 20), dtype=torch.uint8, device="cuda")
+    fs = torch.empty((G, 2), dtype=torch.int16, device="cuda")
+    st = torch.empty((G, 2), dtype=torch.int8, device="cuda")
+    lib.encode_batch(plan, G, S, 48, sh.data_ptr(), dh.data_ptr(), par.data_ptr(), meta.data_ptr(), fs.data_ptr(),
+                     st.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    exp = np.zeros((G, 2), np.int8)
+    exp[1, 1] = -1
+    assert np.array_equal(st.cpu().numpy(), exp)
+    assert fs.cpu().numpy()[1, 1] == 60

@@ -1,0 +1,189 @@
+"""CPU: the oracle (oracle/rfec_oracle.c) against the golden fixtures the
+compiled reference produced (oracle/gen_golden.c).  This pins the oracle
+before it is trusted as the checker of the HIP path."""
+import ctypes as C
+import json
+import subprocess
+
+import numpy as np
+import pytest
+
+import parity_cases as pc
+import pyoracle as po
+
+MANIFEST = po.manifest()
+CASES = {c["name"]: c for c in MANIFEST["cases"]}
+
+
+class OracleEngine:
+    def __init__(self, o):
+        self.o = o
+
+    def encode(self, plan, shards, hdr, capacity):
+        return self.o.encode_batch(plan, shards, hdr, capacity)
+
+    def recover(self, plan, shards, hdr, present, parity, meta, fsize, pp, capacity):
+        return self.o.recover_batch(plan, shards, hdr, present, parity, meta, fsize, pp, capacity)
+
+
+def test_manifest_shape():
+    assert MANIFEST["sim_video_size"] == 1000
+    assert MANIFEST["record_bytes"] == {"parity": 48, "erasure": 176}
+
+
+def test_plan_table_oracle(oracle1000):
+    """flex_fec_sender_num_packets for every n<256, pf<256 (flex_fec_sender.c:81-135)."""
+    t = po.plan_table()
+    for n in range(256):
+        for pf in range(256):
+            rc, r, c = oracle1000.num_packets(n, pf)
+            assert (rc, r, c) == tuple(int(x) for x in t[n, pf]), (n, pf)
+
+
+def test_num_fec_kat(oracle1000):
+    """test_num_fec (sim_test/fec_test/test_func.c:73-87) as printed by the reference."""
+    lines = (po.GOLDEN / "ref_fec_test_stdout.txt").read_text().splitlines()
+    kat = [l for l in lines if l.startswith("num = ")]
+    assert len(kat) == 10
+    for l in kat:
+        n = int(l.split(",")[0].split("=")[1])
+        col = int(l.split(",")[1].split("=")[1])
+        row = int(l.split(",")[2].split("=")[1])
+        _, r, c = oracle1000.num_packets(n, 80)
+        assert (c, r) == (col, row), l
+
+
+@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "sender"])
+def test_sender_fixture_oracle(oracle1000, name):
+    pc.check_sender_case(OracleEngine(oracle1000), oracle1000, CASES[name])
+
+
+def test_sender_random_fixture_oracle(oracle1000):
+    pc.check_sender_random_case(OracleEngine(oracle1000), oracle1000, CASES["random_k"])
+
+
+@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "rows"])
+def test_rows_fixture_oracle(oracle1000, oracle1200, name):
+    c = CASES[name]
+    o = oracle1200 if c["S"] > 1000 else oracle1000
+    pc.check_rows_case(OracleEngine(o), o, c, capacity=max(c["S"], 1000))
+
+
+@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures"])
+def test_erasure_fixture_oracle(oracle1000, name):
+    pc.check_erasure_case(OracleEngine(oracle1000), oracle1000, CASES[name])
+
+
+def test_erasure_counts(oracle1000):
+    """at k=10 3x4 all 45 pairs and 120 triples recover with the full
+    plan; rows only recovers 32/45 pairs and 32/120 triples."""
+    for name, exp2, exp3 in (("k10_full_le3", 45, 120), ("k10_rows_le3", 32, 32)):
+        pats = po.load_erasures(CASES[name])
+        full = lambda p: int(p["recovered"][0]) == ((~int(p["present"][0])) & 0x3FF)
+        n_erased = np.array([bin((~int(p["present"][0])) & 0x3FF).count("1") for p in pats])
+        ok = np.array([full(p) for p in pats])
+        assert ok[n_erased == 2].sum() == exp2, name
+        assert ok[n_erased == 3].sum() == exp3, name
+
+
+# ---- single-call semantics (flex_fec_xor.c) --------------------------------
+def _segs_from_case(st, c):
+    segs = []
+    for inp in c["inputs"]:
+        s = inp["seg"]
+        seg = st()
+        for f in ("packet_id", "fid", "timestamp", "index", "total", "ftype", "payload_type", "data_size",
+                  "fec_id"):
+            setattr(seg, f, s[f])
+        raw = bytes.fromhex(s["data"])
+        C.memmove(C.addressof(seg) + 34, raw, len(raw))
+        segs.append(seg)
+    return segs
+
+
+def _fnv_data(seg, vsize):
+    return "%016x" % po.fnv1a(bytes(seg.data)[:vsize])
+
+
+def run_single_cases(gen, rec, seg_t, fec_t, vsize):
+    cases = json.loads((po.GOLDEN / "single_cases.json").read_text())
+    for c in cases:
+        segs = _segs_from_case(seg_t, c)
+        fec = fec_t()
+        C.memset(C.addressof(fec), 0xCD, C.sizeof(fec))
+        fec.fec_id = 77
+        rc = gen(segs, fec)
+        assert rc == c["generate_rc"], c["name"]
+        if "fec" in c:
+            e = c["fec"]
+            assert fec.fec_data_size == e["fec_data_size"], c["name"]
+            for f in ("seq", "fid", "ts", "index", "total", "ftype", "payload_type", "size"):
+                assert getattr(fec.fec_meta, f) == e[f], (c["name"], f)
+            if rc == 0:
+                assert bytes(fec.fec_data)[:fec.fec_data_size].hex() == e["data"], c["name"]
+        assert [_fnv_data(s, vsize) for s in segs] == c["after_generate"], c["name"]
+        if "recover_rc" in c:
+            if c["corrupt"] == 1:
+                segs[1].data_size = fec.fec_data_size + 1
+            elif c["corrupt"] == 2:
+                fec.fec_meta.size ^= c["meta_size_xor"]
+            rest = [s for i, s in enumerate(segs) if i != c["drop"]]
+            out = seg_t()
+            C.memset(C.addressof(out), 0xAB, C.sizeof(out))
+            rr = rec(rest, fec, out)
+            assert rr == c["recover_rc"], c["name"]
+            if rr == 0:
+                e = c["recovered"]
+                for f in ("packet_id", "fid", "timestamp", "index", "total", "ftype", "payload_type", "data_size",
+                          "fec_id"):
+                    assert getattr(out, f) == e[f], (c["name"], f)
+                assert bytes(out.data)[:fec.fec_data_size].hex() == e["data"], c["name"]
+            assert [_fnv_data(s, vsize) for s in rest] == c["after_recover"], c["name"]
+        if "recover_n0_rc" in c:
+            out = seg_t()
+            assert rec([], fec, out) == c["recover_n0_rc"]
+
+
+def test_single_cases_oracle(oracle1000):
+    from razor_amd.fec import sim_types
+
+    seg_t, fec_t = sim_types(1000)
+    lib = oracle1000.lib
+
+    def gen(segs, fec):
+        arr = (C.c_void_p * max(1, len(segs)))(*[C.addressof(s) for s in segs])
+        return lib.oracle_generate(arr, len(segs), C.byref(fec), 1000)
+
+    def rec(segs, fec, out):
+        arr = (C.c_void_p * max(1, len(segs)))(*[C.addressof(s) for s in segs])
+        return lib.oracle_recover(arr, len(segs), C.byref(fec), C.byref(out))
+
+    run_single_cases(gen, rec, seg_t, fec_t, 1000)
+
+
+def test_reference_stdout_reproducible():
+    """The compiled reference's own tests print the golden stdout (skipped when
+    the reference build is absent, e.g. on the GPU box)."""
+    exe = po.REFDIR / "ref_fec_test"
+    if not exe.exists():
+        pytest.skip("oracle/_ref not built")
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60).stdout
+    assert out == (po.GOLDEN / "ref_fec_test_stdout.txt").read_text()
+
+
+def test_aos_path_matches_batch(oracle1200):
+    """The reference-shaped AoS path (CPU baseline) equals the batched restatement."""
+    o = oracle1200
+    shards, hdr = o.fill_groups(77, 24, 10, 1200, ragged=True)
+    plan = o.plan_from_fraction(10, 80)
+    parity, meta, fsize, status = o.encode_batch(plan, shards, hdr, 1200)
+    segs = o.to_aos(shards, hdr)
+    n, fec = o.encode_aos(plan, 24, segs, threads=3)
+    assert n == 24 * plan.n_lines
+    fec = fec.reshape(24, plan.n_lines, -1)
+    for g in range(24):
+        for l in range(plan.n_lines):
+            L = int(fsize[g, l])
+            assert int.from_bytes(fec[g, l, 40:42].tobytes(), "little") == L
+            assert fec[g, l, 20:40].tobytes() == meta[g, l].tobytes()
+            assert np.array_equal(fec[g, l, 42:42 + L], parity[g, l, :L])
