@@ -28,6 +28,7 @@ import torch
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
+from razor_amd.dist import shard_groups  # noqa: E402
 from razor_amd.fec import HDR_DTYPE, native  # noqa: E402
 
 METRIC = "FEC encode+decode GiB/s (device-resident), 1200B pkts k=10/r=3; % HBM peak"
@@ -213,7 +214,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--groups", type=int, default=65536, help="groups per GPU")
+    ap.add_argument("--groups", type=int, default=65536, help="groups per GPU (weak scaling)")
+    ap.add_argument("--total-groups", type=int, default=0,
+                    help="split this many groups over the GPUs instead (strong scaling, e.g. 1048576)")
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--payload", type=int, default=1200)
     ap.add_argument("--protect-fraction", type=int, default=80)
@@ -238,8 +241,13 @@ def main():
 
     lib = native(1000)
     lib.set_tuning(args.tuning)
-    w = Workload(lib, args.groups, args.k, args.payload, args.protect_fraction, device, rank * args.groups,
-                 seed=1000 + rank)
+    if args.total_groups:
+        group0, my_groups = shard_groups(args.total_groups, world, rank)
+        scaling = "strong"
+    else:
+        group0, my_groups = rank * args.groups, args.groups
+        scaling = "weak"
+    w = Workload(lib, my_groups, args.k, args.payload, args.protect_fraction, device, group0, seed=1000 + rank)
     stream = torch.cuda.current_stream(device)
     sp = stream.cuda_stream
     torch.cuda.synchronize(device)
@@ -278,7 +286,11 @@ def main():
         dist.all_reduce(vt, op=dist.ReduceOp.MIN)
         verified = None if args.no_verify else bool(vt.item())
 
-    step_bytes = (w.enc_bytes + w.dec_bytes) * world
+    # whole-job bytes: every rank's slice (equal slices up to one group)
+    nb = torch.tensor([w.enc_bytes + w.dec_bytes], dtype=torch.float64, device=device)
+    if dist:
+        dist.all_reduce(nb, op=dist.ReduceOp.SUM)
+    step_bytes = float(nb.item())
     value = step_bytes * args.steps / elapsed / 2**30
     enc_mean = float(t_enc.mean())
     dec_mean = float(t_dec.mean())
@@ -286,7 +298,7 @@ def main():
     res = None
     if rank == 0:
         ceiling = copy_ceiling(device)
-        workload_name = f"k{args.k}_r{w.n}_S{args.payload}_G{args.groups}"
+        workload_name = f"k{args.k}_r{w.n}_S{args.payload}_G{w.G}"
         traffic = load_traffic(workload_name)
         res = {
             "metric": METRIC,
@@ -297,11 +309,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (torch.randint payloads, sequential headers), resident in HBM before timing",
-            "config": {"workload": workload_name, "groups_per_gpu": args.groups, "k": args.k, "r": w.n,
+            "config": {"workload": workload_name, "groups_per_gpu": w.G,
+                       "total_groups": args.total_groups or args.groups * world, "k": args.k, "r": w.n,
                        "payload_bytes": args.payload, "plan": "row layer of the reference 3x4 plan, rows {4,4,2}",
                        "erasures_per_group": 2, "erasure_pairs": "uniform over the 32 distinct-row pairs",
                        "parallelism": f"batch split over {world} GPU(s), no collective",

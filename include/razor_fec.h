@@ -174,6 +174,7 @@ int rfec_encode_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, u
  *   parity_present   [G] u64: bit l = parity line l was received
  *   recovered        [G][2] u64 out: bit i = segment i was recovered here
  *   workspace        rfec_recover_workspace_size(plan, G) bytes of device memory
+ *                    (one peeling-schedule record per group)
  * A line recovers its single missing member only under the conditions of
  * flex_recover_row/col and flex_fec_recover (sizes within fec_data_size).
  */
@@ -191,10 +192,22 @@ int rfec_zero_tails(uint32_t groups, uint32_t k, uint32_t stride, uint8_t* shard
 
 /* Kernel-selection knobs, for benchmarking and A/B tests (0 = defaults:
  * specialised row kernels where the plan allows, non-temporal streaming). */
-#define RFEC_TUNE_GENERIC 1u  /* always use the generic plan-driven kernel */
-#define RFEC_TUNE_TEMPORAL 2u /* plain instead of non-temporal loads/stores */
+#define RFEC_TUNE_GENERIC 1u       /* always use the generic plan-driven kernel */
+#define RFEC_TUNE_PLAIN_LOADS 2u   /* plain instead of non-temporal payload loads */
+#define RFEC_TUNE_NT_STORES 4u     /* non-temporal instead of plain parity stores */
+#define RFEC_TUNE_ITEMS2 8u        /* two chunk columns per lane in the row kernels */
+#define RFEC_TUNE_WAVE_DECODE 16u  /* one-launch recovery, one wave per group */
+#define RFEC_TUNE_DIAG_NO_META 256u /* DIAGNOSTIC ONLY: skip fec_meta (wrong output) */
 void rfec_set_tuning(unsigned flags);
 unsigned rfec_get_tuning(void);
+
+/* HBM ceiling probes (measurement only, not on the FEC path): streaming
+ * read / copy / write of `bytes` (multiple of 16) in the FEC kernels' access
+ * shape.  flags bit0 = non-temporal, bit1 = 4 vectors per lane.  `sink` of
+ * rfec_probe_read needs 16 KiB.  Return 0 or a HIP error code. */
+int rfec_probe_read(const void* src, size_t bytes, void* sink, unsigned flags, void* stream);
+int rfec_probe_copy(const void* src, void* dst, size_t bytes, unsigned flags, void* stream);
+int rfec_probe_write(void* dst, size_t bytes, unsigned flags, void* stream);
 
 /* Last HIP error string seen by this thread (for diagnostics). */
 const char* rfec_last_error(void);

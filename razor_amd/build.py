@@ -26,7 +26,7 @@ INCLUDE = ROOT / "include"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("RFEC_OFFLOAD_ARCH", "gfx950")
 
-HIP_SRC = [CSRC / "rfec_kernels.hip"]
+HIP_SRC = [CSRC / "rfec_kernels.hip", CSRC / "rfec_probe.hip"]
 C_SRC = [CSRC / "rfec_host.c"]
 HEADERS = [INCLUDE / "razor_fec.h", CSRC / "rfec_internal.h"]
 
@@ -57,12 +57,15 @@ def build(force: bool = False, verbose: bool = False) -> dict:
     LIBDIR.mkdir(parents=True, exist_ok=True)
     OBJDIR.mkdir(parents=True, exist_ok=True)
     built = {}
-    kobj = OBJDIR / "rfec_kernels.o"
-    if force or _stale(kobj, HIP_SRC + HEADERS):
-        _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-              f"-I{INCLUDE}", f"-I{CSRC}", "-c", str(HIP_SRC[0]), "-o", str(kobj)])
-        if verbose:
-            print("built", kobj)
+    kobjs = []
+    for src in HIP_SRC:
+        kobj = OBJDIR / (src.stem + ".o")
+        if force or _stale(kobj, [src] + HEADERS):
+            _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+                  f"-I{INCLUDE}", f"-I{CSRC}", "-c", str(src), "-o", str(kobj)])
+            if verbose:
+                print("built", kobj)
+        kobjs.append(kobj)
     for name, vsize in VARIANTS.items():
         hobj = OBJDIR / f"rfec_host_v{vsize}.o"
         if force or _stale(hobj, C_SRC + HEADERS):
@@ -70,8 +73,8 @@ def build(force: bool = False, verbose: bool = False) -> dict:
                   f"-DSIM_VIDEO_SIZE={vsize}", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}",
                   f"-I{INCLUDE}", f"-I{CSRC}", "-c", str(C_SRC[0]), "-o", str(hobj)])
         so = LIBDIR / name
-        if force or _stale(so, [kobj, hobj]):
-            _run([_hipcc(), "-shared", "-fPIC", str(kobj), str(hobj), "-o", str(so),
+        if force or _stale(so, kobjs + [hobj]):
+            _run([_hipcc(), "-shared", "-fPIC", *map(str, kobjs), str(hobj), "-o", str(so),
                   f"-Wl,-soname,{name}", "-lpthread", "-lm"])
             if verbose:
                 print("built", so)

@@ -198,7 +198,7 @@ size_t rfec_recover_workspace_size(const rfec_plan* plan, uint32_t groups)
 {
     if (!plan)
         return 0;
-    return (size_t)groups * (1u + plan->n_lines) * sizeof(rfec_step);
+    return (size_t)groups * rfec_sched_record_bytes(plan->n_lines);
 }
 
 static void make_masks(const rfec_plan* p, rfec_kmask* M)
@@ -232,7 +232,7 @@ int rfec_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, 
     static __thread rfec_kmask M; /* 1.3 KB: keep it off the stack */
     make_masks(plan, &M);
     const int e = rfec_launch_recover(&M, groups, stride, capacity, shards, hdr, present, parity, meta, fec_size,
-                                      parity_present, recovered, workspace, 1u + plan->n_lines, stream, g_tuning);
+                                      parity_present, recovered, workspace, stream, g_tuning);
     return e ? set_err(RFEC_EDEVICE, "recover launch", e) : RFEC_OK;
 }
 
@@ -287,7 +287,7 @@ static di_layout di_offsets(void)
     DI_TAKE(present, 2 * sizeof(uint64_t));
     DI_TAKE(ppresent, sizeof(uint64_t));
     DI_TAKE(recovered, 2 * sizeof(uint64_t));
-    DI_TAKE(ws, 2 * sizeof(rfec_step));
+    DI_TAKE(ws, 16);
 #undef DI_TAKE
     L.total = o;
     return L;
@@ -478,7 +478,7 @@ int flex_fec_recover(sim_segment_t* segs[], int segs_count, sim_fec_t* fec, sim_
                                       (rfec_hdr*)(c->dev + L.hdr), (const uint64_t*)(c->dev + L.present),
                                       c->dev + L.parity, (const rfec_hdr*)(c->dev + L.meta),
                                       (const uint16_t*)(c->dev + L.fsize), (const uint64_t*)(c->dev + L.ppresent),
-                                      (uint64_t*)(c->dev + L.recovered), c->dev + L.ws, 2, c->stream, g_tuning);
+                                      (uint64_t*)(c->dev + L.recovered), c->dev + L.ws, c->stream, g_tuning);
     free(M);
     if (di_sync(c, e, "flex_fec_recover") != RFEC_OK) {
         di_loud(t_err);

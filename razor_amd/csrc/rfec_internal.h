@@ -17,16 +17,13 @@ typedef struct {
     uint64_t mask[RFEC_MAX_LINES][2];
 } rfec_kmask;
 
-/* one peeling step replayed by the recovery XOR kernel; slot 0 of a group's
- * record holds the step count in `first` */
-typedef struct {
-    uint8_t first, stride, count, q; /* line geometry, q = target's position on it */
-    uint8_t line, target;
-    uint8_t pad[2];
-} rfec_step;
-
-#define RFEC_KFLAG_GENERIC 1u  /* never use the specialised row kernels */
-#define RFEC_KFLAG_TEMPORAL 2u /* plain (not non-temporal) loads/stores */
+/* kernel flags == the RFEC_TUNE_* bits of razor_fec.h */
+#define RFEC_KFLAG_GENERIC RFEC_TUNE_GENERIC
+#define RFEC_KFLAG_PLAIN_LOADS RFEC_TUNE_PLAIN_LOADS
+#define RFEC_KFLAG_NT_STORES RFEC_TUNE_NT_STORES
+#define RFEC_KFLAG_WAVE_DECODE RFEC_TUNE_WAVE_DECODE
+#define RFEC_KFLAG_ITEMS2 RFEC_TUNE_ITEMS2
+#define RFEC_KFLAG_DIAG_NO_META RFEC_TUNE_DIAG_NO_META
 
 int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, uint32_t capacity,
                        const uint8_t* shards, const rfec_hdr* hdr, uint8_t* parity, rfec_hdr* meta,
@@ -34,7 +31,11 @@ int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, ui
 int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32_t capacity,
                         uint8_t* shards, rfec_hdr* hdr, const uint64_t* present, const uint8_t* parity,
                         const rfec_hdr* meta, const uint16_t* fsize, const uint64_t* parity_present,
-                        uint64_t* recovered, void* ws, uint32_t ws_stride, void* stream, unsigned flags);
+                        uint64_t* recovered, void* ws, void* stream, unsigned flags);
+
+/* bytes of one group's peeling-schedule record: step count, single-level
+ * flag, then a (line, target) byte pair per step; 16-byte multiple */
+static inline uint32_t rfec_sched_record_bytes(uint32_t n_lines) { return (2u + 2u * n_lines + 15u) & ~15u; }
 int rfec_launch_zero_tails(uint32_t slots, uint32_t stride, uint8_t* shards, const rfec_hdr* hdr, void* stream);
 const char* rfec_hip_error_string(int code);
 

@@ -8,10 +8,21 @@
 //   peeling order / conditions                             flex_fec_receiver.c:105-206
 //
 // Device layout (include/razor_fec.h): payload slots of `stride` bytes
-// (multiple of 16), zero beyond data_size; one lane owns one 16-byte chunk
-// column of one group and walks every line of that group, so all arithmetic
-// is wave64 v_xor_b32 on dwordx4 registers: no LDS, no MFMA (XOR is the only
-// operation, ~0.06 op/B -> HBM-bound).
+// (multiple of 16), zero beyond data_size.  All arithmetic is wave64
+// v_xor_b32 on dwordx4 registers (no MFMA: XOR is ~0.06 op/B, HBM-bound).
+//
+//  encode: one launch, two kinds of workgroups.
+//    * payload blocks: one lane per (group, 16-B chunk column); a lane loads
+//      the chunk of every member (all loads in flight before the first XOR)
+//      and stores one chunk per parity line -- a pure streaming pass.
+//    * meta blocks (the first ones in the grid): copy the headers of up to
+//      64 groups into LDS with coalesced dword loads, then one lane per
+//      (group, line) XORs its members' 20-byte records out of LDS.
+//  recover: one wave per group.  The wave loads the group's headers / line
+//    metadata lane-parallel, computes the peeling schedule with wave-uniform
+//    (scalar) control flow, and runs each recovery XOR over its chunk columns
+//    as soon as the line fires, so cascaded recoveries read segments this
+//    same lane has just written.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -20,6 +31,8 @@
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kWave = 64;
+constexpr int kMetaDwords = 4096; // 16 KiB of LDS for the meta blocks' header stage
 
 // CUTLASS-style fast unsigned division for dividends < 2^31.
 struct FastDiv {
@@ -35,88 +48,95 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f)
 // native 16-byte vector (the nontemporal builtins need a clang vector type)
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ v4u xor4(v4u a, v4u b) { return a ^ b; }
-
 template <bool NT>
 __device__ __forceinline__ v4u ld16(const v4u* p)
 {
-    if constexpr (NT) {
+    if constexpr (NT)
         return __builtin_nontemporal_load(p);
-    } else {
+    else
         return *p;
-    }
 }
 
 template <bool NT>
 __device__ __forceinline__ void st16(v4u* p, v4u v)
 {
-    if constexpr (NT) {
+    if constexpr (NT)
         __builtin_nontemporal_store(v, p);
-    } else {
+    else
         *p = v;
+}
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+
+// ---------------------------------------------------------------------------
+// Encode meta blocks: fec_meta = XOR of the member headers taken as five
+// dwords (field-wise XOR, flex_fec_xor.c:13-20, 37-44), fec_data_size = max
+// data_size (:22-26), status -1 where flex_fec_generate fails (:9-10, :27-28).
+// ---------------------------------------------------------------------------
+__device__ void meta_block(uint32_t mb, const uint32_t* __restrict__ hdr_dw, uint32_t* __restrict__ meta_dw,
+                           uint16_t* __restrict__ fsize, int8_t* __restrict__ status, uint32_t groups,
+                           uint32_t capacity, uint32_t gpb, const rfec_kplan& P)
+{
+    __shared__ uint32_t lds[kMetaDwords];
+    const uint32_t K = P.k, NL = P.n_lines;
+    const uint32_t g0 = mb * gpb;
+    const uint32_t ng = min(gpb, groups - g0);
+    const uint32_t ndw = ng * K * 5;
+    const uint32_t* src = hdr_dw + (size_t)g0 * K * 5;
+    for (uint32_t i = threadIdx.x; i < ndw; i += kBlock)
+        lds[i] = src[i];
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < ng * NL; o += kBlock) {
+        const uint32_t gl = o / NL, l = o - gl * NL;
+        const rfec_line ln = P.line[l];
+        const uint32_t* h = lds + gl * K * 5;
+        uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0, m4 = 0, L = 0;
+        for (uint32_t q = 0; q < ln.count; ++q) {
+            const uint32_t* r = h + (ln.first + q * ln.stride) * 5;
+            m0 ^= r[0];
+            m1 ^= r[1];
+            m2 ^= r[2];
+            m3 ^= r[3];
+            m4 ^= r[4];
+            L = max(L, r[4] >> 16);
+        }
+        const size_t out = (size_t)g0 * NL + o;
+        uint32_t* d = meta_dw + out * 5;
+        d[0] = m0;
+        d[1] = m1;
+        d[2] = m2;
+        d[3] = m3;
+        d[4] = m4;
+        fsize[out] = (uint16_t)L;
+        if (status)
+            status[out] = (ln.count <= 1 || L > capacity) ? (int8_t)-1 : (int8_t)0;
     }
 }
 
-struct Hdr5 {
-    uint32_t w[5];
+struct EncMeta {
+    const uint32_t* hdr_dw;
+    uint32_t* meta_dw;
+    uint16_t* fsize;
+    int8_t* status;
+    uint32_t groups, capacity, gpb, n_meta_blocks;
 };
 
-__device__ __forceinline__ Hdr5 ldh(const rfec_hdr* h)
+// ---------------------------------------------------------------------------
+// Encode payload, generic plan.
+// ---------------------------------------------------------------------------
+template <bool NTL, bool NTS>
+__global__ __launch_bounds__(kBlock) void k_encode(const v4u* __restrict__ shards, v4u* __restrict__ parity,
+                                                   uint32_t total, uint32_t C, FastDiv divC, EncMeta E,
+                                                   rfec_kplan P)
 {
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(h);
-    Hdr5 r;
-#pragma unroll
-    for (int i = 0; i < 5; ++i)
-        r.w[i] = p[i];
-    return r;
-}
-
-__device__ __forceinline__ void sth(rfec_hdr* h, const Hdr5& r)
-{
-    uint32_t* p = reinterpret_cast<uint32_t*>(h);
-#pragma unroll
-    for (int i = 0; i < 5; ++i)
-        p[i] = r.w[i];
-}
-
-__device__ __forceinline__ uint32_t hsize(const Hdr5& h) { return h.w[4] >> 16; }
-
-// Parity meta of line l of group g: XOR of the member headers as five dwords
-// (field-wise XOR, flex_fec_xor.c:13-20, 37-44) and L = max data_size
-// (:22-26); status -1 where flex_fec_generate fails (:9-10, :27-28).
-__device__ __forceinline__ void encode_meta(const rfec_hdr* __restrict__ hdr, rfec_hdr* __restrict__ meta,
-                                            uint16_t* __restrict__ fsize, int8_t* __restrict__ status,
-                                            uint32_t g, uint32_t l, const rfec_kplan& P, uint32_t capacity)
-{
-    const rfec_line ln = P.line[l];
-    const rfec_hdr* hg = hdr + (size_t)g * P.k;
-    Hdr5 m = {{0, 0, 0, 0, 0}};
-    uint32_t L = 0;
-    for (uint32_t q = 0; q < ln.count; ++q) {
-        Hdr5 h = ldh(hg + ln.first + q * ln.stride);
-#pragma unroll
-        for (int i = 0; i < 5; ++i)
-            m.w[i] ^= h.w[i];
-        L = max(L, hsize(h));
+    if (blockIdx.x < E.n_meta_blocks) {
+        meta_block(blockIdx.x, E.hdr_dw, E.meta_dw, E.fsize, E.status, E.groups, E.capacity, E.gpb, P);
+        return;
     }
-    const size_t o = (size_t)g * P.n_lines + l;
-    sth(meta + o, m);
-    fsize[o] = (uint16_t)L;
-    if (status)
-        status[o] = (ln.count <= 1 || L > capacity) ? (int8_t)-1 : (int8_t)0;
-}
-
-// ---------------------------------------------------------------------------
-// Encode, generic plan: one lane per (group, 16-B chunk column).
-// ---------------------------------------------------------------------------
-template <bool NT>
-__global__ __launch_bounds__(kBlock) void k_encode(const v4u* __restrict__ shards,
-                                                   const rfec_hdr* __restrict__ hdr, v4u* __restrict__ parity,
-                                                   rfec_hdr* __restrict__ meta, uint16_t* __restrict__ fsize,
-                                                   int8_t* __restrict__ status, uint32_t total, uint32_t C,
-                                                   FastDiv divC, uint32_t capacity, rfec_kplan P)
-{
-    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t t = (blockIdx.x - E.n_meta_blocks) * kBlock + threadIdx.x;
     if (t >= total)
         return;
     const uint32_t g = fdiv(t, divC);
@@ -127,120 +147,198 @@ __global__ __launch_bounds__(kBlock) void k_encode(const v4u* __restrict__ shard
         const rfec_line ln = P.line[l];
         const v4u* s = src + (size_t)ln.first * C;
         const size_t step = (size_t)ln.stride * C;
-        v4u acc = ld16<NT>(s);
+        v4u acc = ld16<NTL>(s);
         for (uint32_t q = 1; q < ln.count; ++q)
-            acc = xor4(acc, ld16<NT>(s + q * step));
-        st16<NT>(dst + (size_t)l * C, acc);
+            acc ^= ld16<NTL>(s + q * step);
+        st16<NTS>(dst + (size_t)l * C, acc);
     }
-    if (j < P.n_lines)
-        encode_meta(hdr, meta, fsize, status, g, j, P, capacity);
 }
 
 // ---------------------------------------------------------------------------
-// Encode, rows-of-COL fast path (the k=10 / rows {4,4,2} and k=32 / 8x4
-// configurations): every member offset is a compile-time constant, so all K
-// dwordx4 loads of a lane issue back to back before the first XOR.
+// Encode payload, rows-of-COL fast path (k=10 rows {4,4,2}; k=32 8x4): member
+// offsets are compile-time constants, so all K x ITEMS dwordx4 loads of a lane
+// issue back to back.  Item u of a lane is chunk t0 + u*(payload lanes), so
+// every wave instruction still covers 1 KiB of consecutive chunks.
 // ---------------------------------------------------------------------------
-template <int K, int COL, bool NT>
-__global__ __launch_bounds__(kBlock) void k_encode_rows(const v4u* __restrict__ shards,
-                                                        const rfec_hdr* __restrict__ hdr,
-                                                        v4u* __restrict__ parity, rfec_hdr* __restrict__ meta,
-                                                        uint16_t* __restrict__ fsize, int8_t* __restrict__ status,
-                                                        uint32_t total, uint32_t C, FastDiv divC,
-                                                        uint32_t capacity, rfec_kplan P)
+template <int K, int COL, bool NTL, bool NTS, int ITEMS>
+__global__ __launch_bounds__(kBlock) void k_encode_rows(const v4u* __restrict__ shards, v4u* __restrict__ parity,
+                                                        uint32_t total, uint32_t C, FastDiv divC, EncMeta E,
+                                                        rfec_kplan P)
 {
-    constexpr int R = (K + COL - 1) / COL;
-    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    if (t >= total)
+    if (blockIdx.x < E.n_meta_blocks) {
+        meta_block(blockIdx.x, E.hdr_dw, E.meta_dw, E.fsize, E.status, E.groups, E.capacity, E.gpb, P);
         return;
-    const uint32_t g = fdiv(t, divC);
-    const uint32_t j = t - g * C;
-    const v4u* src = shards + (size_t)g * K * C + j;
-    v4u* dst = parity + (size_t)g * R * C + j;
-    v4u v[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i)
-        v[i] = ld16<NT>(src + (size_t)i * C);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        v4u acc = v[r * COL];
-#pragma unroll
-        for (int q = 1; q < COL; ++q)
-            if (r * COL + q < K)
-                acc = xor4(acc, v[r * COL + q]);
-        st16<NT>(dst + (size_t)r * C, acc);
     }
-    if (j < (uint32_t)R)
-        encode_meta(hdr, meta, fsize, status, g, j, P, capacity);
+    constexpr int R = (K + COL - 1) / COL;
+    const uint32_t lanes = (gridDim.x - E.n_meta_blocks) * kBlock;
+    const uint32_t t0 = (blockIdx.x - E.n_meta_blocks) * kBlock + threadIdx.x;
+    v4u v[ITEMS][K];
+    uint32_t gi[ITEMS], ji[ITEMS];
+#pragma unroll
+    for (int u = 0; u < ITEMS; ++u) {
+        const uint32_t t = t0 + u * lanes;
+        gi[u] = fdiv(t, divC);
+        ji[u] = t - gi[u] * C;
+        if (t < total) {
+            const v4u* src = shards + (size_t)gi[u] * K * C + ji[u];
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                v[u][i] = ld16<NTL>(src + (size_t)i * C);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < ITEMS; ++u) {
+        if (t0 + u * lanes >= total)
+            continue;
+        v4u* dst = parity + (size_t)gi[u] * R * C + ji[u];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            v4u acc = v[u][r * COL];
+#pragma unroll
+            for (int q = 1; q < COL; ++q)
+                if (r * COL + q < K)
+                    acc ^= v[u][r * COL + q];
+            st16<NTS>(dst + (size_t)r * C, acc);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
-// Peeling schedule: one lane per group.  Fixpoint of flex_recover_row/col
-// (flex_fec_receiver.c:105-206) with the cascade of sim_receiver.c:780-804,
-// lines in plan order, repeated until nothing fires.  Writes the recovered
-// headers (flex_fec_xor.c:64-85) and the step list the XOR kernel replays.
+// Recover: one wave per group.
+//
+// Peeling = the fixpoint reached by flex_recover_row / flex_recover_col
+// (flex_fec_receiver.c:105-206) as segments, parities and recovered segments
+// (sim_receiver.c:780-804) arrive; canonical order: lines in plan order,
+// repeated until nothing fires.  A line fires when its parity is present,
+// exactly one member is missing, at least one is present (:133-140,
+// :189-196) and flex_fec_recover would succeed: fec_data_size within the
+// capacity, every member's data_size <= fec_data_size (flex_fec_xor.c:88-89)
+// and the recovered data_size <= fec_data_size (:98-99).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_peel(rfec_hdr* __restrict__ hdr, const uint64_t* __restrict__ present,
-                                                 const rfec_hdr* __restrict__ meta,
-                                                 const uint16_t* __restrict__ fsize,
-                                                 const uint64_t* __restrict__ parity_present,
-                                                 uint64_t* __restrict__ recovered, rfec_step* __restrict__ ws,
-                                                 uint32_t groups, uint32_t ws_stride, uint32_t capacity,
-                                                 rfec_kmask M)
+struct RecArgs {
+    v4u* shards;
+    rfec_hdr* hdr;
+    const uint64_t* present;
+    const v4u* parity;
+    const rfec_hdr* meta;
+    const uint16_t* fsize;
+    const uint64_t* parity_present;
+    uint64_t* recovered;
+    uint32_t groups, C, capacity;
+};
+
+template <bool NTL>
+__global__ __launch_bounds__(kBlock) void k_recover(RecArgs A, rfec_kmask M)
 {
-    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-    if (g >= groups)
+    const uint32_t g = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) / kWave);
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    if (g >= A.groups)
         return;
     const rfec_kplan& P = M.plan;
-    uint64_t have0 = present[2 * g], have1 = present[2 * g + 1];
-    const uint64_t pp = parity_present[g];
+    const uint32_t K = P.k, NL = P.n_lines, C = A.C;
+
+    // ---- lane-parallel loads of the group's bookkeeping -------------------
+    uint64_t have0 = A.present[2 * g], have1 = A.present[2 * g + 1];
+    const uint64_t ppm = A.parity_present[g];
+    const uint32_t* hdr_dw = reinterpret_cast<const uint32_t*>(A.hdr + (size_t)g * K);
+    const uint32_t* meta_dw = reinterpret_cast<const uint32_t*>(A.meta + (size_t)g * NL);
+    uint32_t hA[5] = {0, 0, 0, 0, 0}, hB[5] = {0, 0, 0, 0, 0}; // headers of segments lane, lane+64
+    uint32_t mL[5] = {0, 0, 0, 0, 0}, fL = 0;                  // meta / fec_data_size of line `lane`
+    if (lane < K) {
+#pragma unroll
+        for (int w = 0; w < 5; ++w)
+            hA[w] = hdr_dw[lane * 5 + w];
+    }
+    if (lane + kWave < K) {
+#pragma unroll
+        for (int w = 0; w < 5; ++w)
+            hB[w] = hdr_dw[(lane + kWave) * 5 + w];
+    }
+    if (lane < NL) {
+#pragma unroll
+        for (int w = 0; w < 5; ++w)
+            mL[w] = meta_dw[lane * 5 + w];
+        fL = A.fsize[(size_t)g * NL + lane];
+    }
+    v4u* grp = A.shards + (size_t)g * K * C;
+    const v4u* par = A.parity + (size_t)g * NL * C;
     uint64_t rec0 = 0, rec1 = 0;
-    rfec_hdr* hg = hdr + (size_t)g * P.k;
-    rfec_step* steps = ws + (size_t)g * ws_stride;
-    uint32_t n_steps = 0;
+
     bool progress = true;
     while (progress) {
         progress = false;
-        for (uint32_t l = 0; l < P.n_lines; ++l) {
-            if (!((pp >> l) & 1ull))
+        for (uint32_t l = 0; l < NL; ++l) {
+            if (!((ppm >> l) & 1ull))
                 continue;
             const uint64_t m0 = M.mask[l][0], m1 = M.mask[l][1];
             const uint64_t x0 = m0 & ~have0, x1 = m1 & ~have1;
             if (__popcll(x0) + __popcll(x1) != 1)
                 continue;
             if (((m0 & have0) | (m1 & have1)) == 0)
-                continue; // count == 0 (:134, :190)
-            const uint32_t t = x0 ? (uint32_t)__ffsll((long long)x0) - 1 : 64u + (uint32_t)__ffsll((long long)x1) - 1;
-            const size_t o = (size_t)g * P.n_lines + l;
-            const uint32_t L = fsize[o];
-            if (L > capacity)
+                continue; // count == 0
+            const uint32_t t = x0 ? (uint32_t)__ffsll((long long)x0) - 1
+                                  : 64u + (uint32_t)__ffsll((long long)x1) - 1;
+            const uint32_t L = rl(fL, l);
+            if (L > A.capacity)
                 continue;
             const rfec_line ln = P.line[l];
-            Hdr5 r = ldh(meta + o);
+            uint32_t r0 = rl(mL[0], l), r1 = rl(mL[1], l), r2 = rl(mL[2], l), r3 = rl(mL[3], l), r4 = rl(mL[4], l);
             bool ok = true;
             for (uint32_t q = 0; q < ln.count; ++q) {
                 const uint32_t i = ln.first + q * ln.stride;
                 if (i == t)
                     continue;
-                Hdr5 h = ldh(hg + i);
-#pragma unroll
-                for (int w = 0; w < 5; ++w)
-                    r.w[w] ^= h.w[w];
-                ok = ok && hsize(h) <= L; // flex_fec_xor.c:88-89
+                const bool hi = i >= kWave;
+                const uint32_t src = i & (kWave - 1);
+                r0 ^= rl(hi ? hB[0] : hA[0], src);
+                r1 ^= rl(hi ? hB[1] : hA[1], src);
+                r2 ^= rl(hi ? hB[2] : hA[2], src);
+                r3 ^= rl(hi ? hB[3] : hA[3], src);
+                const uint32_t w4 = rl(hi ? hB[4] : hA[4], src);
+                r4 ^= w4;
+                ok = ok && (w4 >> 16) <= L;
             }
-            if (!ok || hsize(r) > L) // :98-99
+            if (!ok || (r4 >> 16) > L)
                 continue;
-            sth(hg + t, r);
-            rfec_step st;
-            st.first = ln.first;
-            st.stride = ln.stride;
-            st.count = ln.count;
-            st.q = (uint8_t)((t - ln.first) / ln.stride);
-            st.line = (uint8_t)l;
-            st.target = (uint8_t)t;
-            st.pad[0] = st.pad[1] = 0;
-            steps[1 + n_steps] = st;
-            ++n_steps;
+
+            // payload: this lane's chunk columns j = lane, lane+64, ...
+            for (uint32_t j0 = 0; j0 < C; j0 += 2 * kWave) {
+                const uint32_t ja = j0 + lane, jb = j0 + kWave + lane;
+                const bool oka = ja < C, okb = jb < C;
+                v4u a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
+                const v4u* pl = par + (size_t)l * C;
+                if (oka)
+                    a = ld16<NTL>(pl + ja);
+                if (okb)
+                    b = ld16<NTL>(pl + jb);
+                for (uint32_t q = 0; q < ln.count; ++q) {
+                    const uint32_t i = ln.first + q * ln.stride;
+                    if (i == t)
+                        continue;
+                    const v4u* s = grp + (size_t)i * C;
+                    if (oka)
+                        a ^= s[ja];
+                    if (okb)
+                        b ^= s[jb];
+                }
+                v4u* d = grp + (size_t)t * C;
+                if (oka)
+                    d[ja] = a;
+                if (okb)
+                    d[jb] = b;
+            }
+            // recovered header (flex_fec_xor.c:64-85): lanes 0-4 store one dword
+            // each; the holder lane of segment t keeps it for cascaded lines
+            const uint32_t rw = lane == 0 ? r0 : lane == 1 ? r1 : lane == 2 ? r2 : lane == 3 ? r3 : r4;
+            if (lane < 5)
+                reinterpret_cast<uint32_t*>(A.hdr + (size_t)g * K + t)[lane] = rw;
+            if ((t & (kWave - 1)) == lane) {
+                if (t >= kWave) {
+                    hB[0] = r0, hB[1] = r1, hB[2] = r2, hB[3] = r3, hB[4] = r4;
+                } else {
+                    hA[0] = r0, hA[1] = r1, hA[2] = r2, hA[3] = r3, hA[4] = r4;
+                }
+            }
             if (t < 64) {
                 have0 |= 1ull << t;
                 rec0 |= 1ull << t;
@@ -251,44 +349,202 @@ __global__ __launch_bounds__(kBlock) void k_peel(rfec_hdr* __restrict__ hdr, con
             progress = true;
         }
     }
-    rfec_step head = {};
-    head.first = (uint8_t)n_steps; // step 0 slot carries the count
-    head.count = 0;
-    steps[0] = head;
-    recovered[2 * g] = rec0;
-    recovered[2 * g + 1] = rec1;
+    if (lane == 0) {
+        A.recovered[2 * g] = rec0;
+        A.recovered[2 * g + 1] = rec1;
+    }
 }
 
 // ---------------------------------------------------------------------------
-// Recovery XOR: one lane per (group, chunk column) replays the group's steps;
-// a member recovered by an earlier step was written by this same lane.
+// Recover, two-kernel form (default).
+//
+// k_peel_lds: the same peeling schedule as k_recover, one lane per group, over
+// the group's headers / line metadata staged in LDS by coalesced dword loads.
+// Writes the recovered headers and a schedule record per group:
+//   byte 0 = steps, byte 1 = 1 when no step reads a segment recovered by an
+//   earlier step (single level), then (line, target) byte pairs.
+// k_recover_flat: one lane per (group, 16-B chunk column) replays the record;
+// single-level schedules run BATCH steps with every load in flight at once.
 // ---------------------------------------------------------------------------
-template <bool NT>
-__global__ __launch_bounds__(kBlock) void k_recover(v4u* shards, const v4u* __restrict__ parity,
-                                                    const rfec_step* __restrict__ ws, uint32_t total, uint32_t C,
-                                                    FastDiv divC, uint32_t k, uint32_t n_lines,
-                                                    uint32_t ws_stride)
+constexpr int kPeelDwords = 8192; // 32 KiB of LDS per peel block
+
+struct PeelArgs {
+    rfec_hdr* hdr;
+    const uint64_t* present;
+    const rfec_hdr* meta;
+    const uint16_t* fsize;
+    const uint64_t* parity_present;
+    uint64_t* recovered;
+    uint8_t* sched;
+    uint32_t groups, capacity, gpb, rec_bytes;
+};
+
+__global__ __launch_bounds__(kBlock) void k_peel_lds(PeelArgs A, rfec_kmask M)
 {
+    __shared__ uint32_t lds[kPeelDwords];
+    const rfec_kplan& P = M.plan;
+    const uint32_t K = P.k, NL = P.n_lines;
+    const uint32_t g0 = blockIdx.x * A.gpb;
+    const uint32_t ng = min(A.gpb, A.groups - g0);
+    uint32_t* Lh = lds;               // [ng][K][5]
+    uint32_t* Lm = Lh + ng * K * 5;   // [ng][NL][5]
+    uint32_t* Lf = Lm + ng * NL * 5;  // [ng][NL]
+    const uint32_t* hsrc = reinterpret_cast<const uint32_t*>(A.hdr + (size_t)g0 * K);
+    const uint32_t* msrc = reinterpret_cast<const uint32_t*>(A.meta + (size_t)g0 * NL);
+    for (uint32_t i = threadIdx.x; i < ng * K * 5; i += kBlock)
+        Lh[i] = hsrc[i];
+    for (uint32_t i = threadIdx.x; i < ng * NL * 5; i += kBlock)
+        Lm[i] = msrc[i];
+    for (uint32_t i = threadIdx.x; i < ng * NL; i += kBlock)
+        Lf[i] = A.fsize[(size_t)g0 * NL + i];
+    __syncthreads();
+    if (threadIdx.x >= ng)
+        return;
+    const uint32_t g = g0 + threadIdx.x;
+    uint32_t* h = Lh + threadIdx.x * K * 5;
+    const uint32_t* m = Lm + threadIdx.x * NL * 5;
+    const uint32_t* f = Lf + threadIdx.x * NL;
+    uint64_t have0 = A.present[2 * g], have1 = A.present[2 * g + 1];
+    const uint64_t ppm = A.parity_present[g];
+    uint64_t rec0 = 0, rec1 = 0;
+    uint8_t* rec = A.sched + (size_t)g * A.rec_bytes;
+    uint32_t n = 0, single = 1;
+    bool progress = true;
+    while (progress) {
+        progress = false;
+        for (uint32_t l = 0; l < NL; ++l) {
+            if (!((ppm >> l) & 1ull))
+                continue;
+            const uint64_t m0 = M.mask[l][0], m1 = M.mask[l][1];
+            const uint64_t x0 = m0 & ~have0, x1 = m1 & ~have1;
+            if (__popcll(x0) + __popcll(x1) != 1)
+                continue;
+            if (((m0 & have0) | (m1 & have1)) == 0)
+                continue;
+            const uint32_t t = x0 ? (uint32_t)__ffsll((long long)x0) - 1
+                                  : 64u + (uint32_t)__ffsll((long long)x1) - 1;
+            const uint32_t L = f[l];
+            if (L > A.capacity)
+                continue;
+            uint32_t r0 = m[l * 5], r1 = m[l * 5 + 1], r2 = m[l * 5 + 2], r3 = m[l * 5 + 3], r4 = m[l * 5 + 4];
+            bool ok = true;
+            const bool reads_recovered = ((m0 & rec0) | (m1 & rec1)) != 0;
+            const rfec_line ln = P.line[l];
+            for (uint32_t q = 0; q < ln.count; ++q) {
+                const uint32_t i = ln.first + q * ln.stride;
+                if (i == t)
+                    continue;
+                const uint32_t* r = h + i * 5;
+                r0 ^= r[0];
+                r1 ^= r[1];
+                r2 ^= r[2];
+                r3 ^= r[3];
+                r4 ^= r[4];
+                ok = ok && (r[4] >> 16) <= L;
+            }
+            if (!ok || (r4 >> 16) > L)
+                continue;
+            uint32_t* ht = h + t * 5;
+            ht[0] = r0, ht[1] = r1, ht[2] = r2, ht[3] = r3, ht[4] = r4;
+            uint32_t* gh = reinterpret_cast<uint32_t*>(A.hdr + (size_t)g * K + t);
+            gh[0] = r0, gh[1] = r1, gh[2] = r2, gh[3] = r3, gh[4] = r4;
+            rec[2 + 2 * n] = (uint8_t)l;
+            rec[3 + 2 * n] = (uint8_t)t;
+            ++n;
+            if (reads_recovered)
+                single = 0;
+            if (t < 64) {
+                have0 |= 1ull << t;
+                rec0 |= 1ull << t;
+            } else {
+                have1 |= 1ull << (t - 64);
+                rec1 |= 1ull << (t - 64);
+            }
+            progress = true;
+        }
+    }
+    rec[0] = (uint8_t)n;
+    rec[1] = (uint8_t)single;
+    A.recovered[2 * g] = rec0;
+    A.recovered[2 * g + 1] = rec1;
+}
+
+__device__ __forceinline__ uint32_t rec_byte(const v4u& r, uint32_t b)
+{
+    return (r[b >> 2] >> (8 * (b & 3))) & 0xffu;
+}
+
+template <int MAXC, int BATCH, bool NTL>
+__global__ __launch_bounds__(kBlock) void k_recover_flat(v4u* shards, const v4u* __restrict__ parity,
+                                                         const uint8_t* __restrict__ sched, uint32_t total,
+                                                         uint32_t C, FastDiv divC, uint32_t rec_bytes,
+                                                         uint32_t fast_ok, rfec_kplan P)
+{
+    __shared__ uint32_t lplan[RFEC_MAX_LINES];
+    if (threadIdx.x < P.n_lines)
+        lplan[threadIdx.x] = reinterpret_cast<const uint32_t*>(P.line)[threadIdx.x];
+    __syncthreads();
     const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
     if (t >= total)
         return;
     const uint32_t g = fdiv(t, divC);
     const uint32_t j = t - g * C;
-    const rfec_step* steps = ws + (size_t)g * ws_stride;
-    const uint32_t n = steps[0].first;
-    v4u* grp = shards + (size_t)g * k * C + j;
-    const v4u* par = parity + (size_t)g * n_lines * C + j;
-    for (uint32_t s = 0; s < n; ++s) {
-        const rfec_step st = steps[1 + s];
-        v4u acc = ld16<NT>(par + (size_t)st.line * C);
-        const v4u* base = grp + (size_t)st.first * C;
-        const size_t step = (size_t)st.stride * C;
-        for (uint32_t q = 0; q < st.count; ++q) {
-            if (q == st.q)
-                continue;
-            acc = xor4(acc, base[q * step]);
+    const uint32_t K = P.k, NL = P.n_lines;
+    const uint8_t* rec = sched + (size_t)g * rec_bytes;
+    const v4u r0 = *reinterpret_cast<const v4u*>(rec);
+    const uint32_t n = rec_byte(r0, 0);
+    v4u* grp = shards + (size_t)g * K * C + j;
+    const v4u* par = parity + (size_t)g * NL * C + j;
+    uint32_t s = 0;
+    if (fast_ok && rec_byte(r0, 1)) {
+        // single level: BATCH steps at a time, all loads in flight together
+        const uint32_t nf = n < 7 ? n : 7; // steps carried in the first 16 record bytes
+        for (; s < nf; s += BATCH) {
+            v4u acc[BATCH], mv[BATCH][MAXC];
+            uint32_t tg[BATCH];
+            bool on[BATCH];
+#pragma unroll
+            for (int b = 0; b < BATCH; ++b) {
+                on[b] = s + b < nf;
+                const uint32_t l = on[b] ? rec_byte(r0, 2 + 2 * (s + b)) : 0;
+                tg[b] = rec_byte(r0, 3 + 2 * (s + b));
+                const uint32_t ln = lplan[l];
+                const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
+                acc[b] = v4u{0, 0, 0, 0};
+                if (on[b])
+                    acc[b] = ld16<NTL>(par + (size_t)l * C);
+#pragma unroll
+                for (int q = 0; q < MAXC; ++q) {
+                    const uint32_t i = first + q * stride;
+                    mv[b][q] = v4u{0, 0, 0, 0};
+                    if (on[b] && (uint32_t)q < count && i != tg[b])
+                        mv[b][q] = ld16<NTL>(grp + (size_t)i * C);
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < BATCH; ++b) {
+#pragma unroll
+                for (int q = 0; q < MAXC; ++q)
+                    acc[b] ^= mv[b][q];
+                if (on[b])
+                    grp[(size_t)tg[b] * C] = acc[b];
+            }
         }
-        grp[(size_t)st.target * C] = acc;
+        s = nf;
+    }
+    // remaining / multi-level steps, one at a time in schedule order
+    for (; s < n; ++s) {
+        const uint32_t l = s < 7 ? rec_byte(r0, 2 + 2 * s) : rec[2 + 2 * s];
+        const uint32_t tt = s < 7 ? rec_byte(r0, 3 + 2 * s) : rec[3 + 2 * s];
+        const uint32_t ln = lplan[l];
+        const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
+        v4u acc = ld16<NTL>(par + (size_t)l * C);
+        for (uint32_t q = 0; q < count; ++q) {
+            const uint32_t i = first + q * stride;
+            if (i != tt)
+                acc ^= grp[(size_t)i * C];
+        }
+        grp[(size_t)tt * C] = acc;
     }
 }
 
@@ -311,16 +567,15 @@ __global__ __launch_bounds__(kBlock) void k_zero_tails(v4u* shards, const rfec_h
         return;
     }
     v4u v = *p;
-    uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint32_t lo = b0 + 4 * i;
         if (lo >= size)
-            w[i] = 0;
+            v[i] = 0;
         else if (lo + 4 > size)
-            w[i] &= (1u << (8 * (size - lo))) - 1u;
+            v[i] &= (1u << (8 * (size - lo))) - 1u;
     }
-    *p = v4u{w[0], w[1], w[2], w[3]};
+    *p = v;
 }
 
 FastDiv make_fastdiv(uint32_t d)
@@ -337,39 +592,62 @@ FastDiv make_fastdiv(uint32_t d)
 
 inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
 
-template <bool NT>
-hipError_t launch_encode_t(const rfec_kplan* P, uint32_t groups, uint32_t stride, uint32_t capacity,
-                           const uint8_t* shards, const rfec_hdr* hdr, uint8_t* parity, rfec_hdr* meta,
-                           uint16_t* fsize, int8_t* status, hipStream_t stream, int force_generic)
+struct EncLaunch {
+    const rfec_kplan* P;
+    uint32_t groups, stride;
+    const v4u* s;
+    v4u* p;
+    EncMeta E;
+    hipStream_t stream;
+};
+
+template <int K, int COL, bool NTL, bool NTS, int ITEMS>
+hipError_t launch_rows(const EncLaunch& a)
 {
-    const uint32_t C = stride / 16;
-    const uint32_t total = groups * C;
-    const FastDiv f = make_fastdiv(C);
-    const dim3 grid(blocks_for(total)), block(kBlock);
-    const v4u* s = reinterpret_cast<const v4u*>(shards);
-    v4u* p = reinterpret_cast<v4u*>(parity);
-    // fast paths: pure row layouts, rows of COL consecutive members
+    const uint32_t C = a.stride / 16;
+    const uint32_t total = a.groups * C;
+    const uint32_t lanes = (total + ITEMS - 1) / ITEMS;
+    hipLaunchKernelGGL((k_encode_rows<K, COL, NTL, NTS, ITEMS>), dim3(a.E.n_meta_blocks + blocks_for(lanes)),
+                       dim3(kBlock), 0, a.stream, a.s, a.p, total, C, make_fastdiv(C), a.E, *a.P);
+    return hipGetLastError();
+}
+
+template <int K, int COL, bool NTL, bool NTS>
+hipError_t launch_rows_v(const EncLaunch& a, unsigned flags)
+{
+    if (flags & RFEC_KFLAG_ITEMS2)
+        return launch_rows<K, COL, NTL, NTS, 2>(a);
+    return launch_rows<K, COL, NTL, NTS, 1>(a);
+}
+
+bool is_row_layout(const rfec_kplan* P, uint32_t* col_out)
+{
     const uint32_t col = P->n_lines ? P->line[0].count : 0;
-    bool full_rows = col >= 2 && P->n_lines == (P->k + col - 1) / col;
-    for (uint32_t l = 0; l < P->n_lines && full_rows; ++l) {
+    bool rows = col >= 2 && P->n_lines == (P->k + col - 1) / col;
+    for (uint32_t l = 0; l < P->n_lines && rows; ++l) {
         const uint32_t first = l * col;
         const uint32_t count = P->k - first < col ? P->k - first : col;
-        full_rows = P->line[l].stride == 1 && P->line[l].first == first && P->line[l].count == count;
+        rows = P->line[l].stride == 1 && P->line[l].first == first && P->line[l].count == count;
     }
-    if (!force_generic && full_rows) {
-        if (P->k == 10 && col == 4) {
-            hipLaunchKernelGGL((k_encode_rows<10, 4, NT>), grid, block, 0, stream, s, hdr, p, meta, fsize, status,
-                               total, C, f, capacity, *P);
-            return hipGetLastError();
-        }
-        if (P->k == 32 && col == 4) {
-            hipLaunchKernelGGL((k_encode_rows<32, 4, NT>), grid, block, 0, stream, s, hdr, p, meta, fsize, status,
-                               total, C, f, capacity, *P);
-            return hipGetLastError();
-        }
+    *col_out = col;
+    return rows;
+}
+
+template <bool NTL, bool NTS>
+hipError_t launch_encode_t(const EncLaunch& a, unsigned flags)
+{
+    const rfec_kplan* P = a.P;
+    uint32_t col = 0;
+    if (!(flags & RFEC_KFLAG_GENERIC) && is_row_layout(P, &col)) {
+        if (P->k == 10 && col == 4)
+            return launch_rows_v<10, 4, NTL, NTS>(a, flags);
+        if (P->k == 32 && col == 4)
+            return launch_rows_v<32, 4, NTL, NTS>(a, flags);
     }
-    hipLaunchKernelGGL((k_encode<NT>), grid, block, 0, stream, s, hdr, p, meta, fsize, status, total, C, f, capacity,
-                       *P);
+    const uint32_t C = a.stride / 16;
+    const uint32_t total = a.groups * C;
+    hipLaunchKernelGGL((k_encode<NTL, NTS>), dim3(a.E.n_meta_blocks + blocks_for(total)), dim3(kBlock), 0, a.stream,
+                       a.s, a.p, total, C, make_fastdiv(C), a.E, *P);
     return hipGetLastError();
 }
 
@@ -381,41 +659,104 @@ int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, ui
                        const uint8_t* shards, const rfec_hdr* hdr, uint8_t* parity, rfec_hdr* meta,
                        uint16_t* fsize, int8_t* status, void* stream, unsigned flags)
 {
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int generic = (flags & RFEC_KFLAG_GENERIC) != 0;
-    hipError_t e = (flags & RFEC_KFLAG_TEMPORAL)
-                       ? launch_encode_t<false>(P, groups, stride, capacity, shards, hdr, parity, meta, fsize,
-                                                status, st, generic)
-                       : launch_encode_t<true>(P, groups, stride, capacity, shards, hdr, parity, meta, fsize,
-                                               status, st, generic);
+    EncMeta E;
+    E.hdr_dw = reinterpret_cast<const uint32_t*>(hdr);
+    E.meta_dw = reinterpret_cast<uint32_t*>(meta);
+    E.fsize = fsize;
+    E.status = status;
+    E.groups = groups;
+    E.capacity = capacity;
+    uint32_t gpb = kMetaDwords / (5u * P->k);
+    gpb = gpb < 1 ? 1 : (gpb > 64 ? 64 : gpb);
+    E.gpb = gpb;
+    E.n_meta_blocks = (flags & RFEC_KFLAG_DIAG_NO_META) ? 0 : (groups + gpb - 1) / gpb;
+    const EncLaunch a = {P, groups, stride, reinterpret_cast<const v4u*>(shards), reinterpret_cast<v4u*>(parity),
+                         E, reinterpret_cast<hipStream_t>(stream)};
+    const bool ntl = !(flags & RFEC_KFLAG_PLAIN_LOADS), nts = (flags & RFEC_KFLAG_NT_STORES) != 0;
+    hipError_t e;
+    if (ntl && nts)
+        e = launch_encode_t<true, true>(a, flags);
+    else if (ntl)
+        e = launch_encode_t<true, false>(a, flags);
+    else if (nts)
+        e = launch_encode_t<false, true>(a, flags);
+    else
+        e = launch_encode_t<false, false>(a, flags);
     return (int)e;
 }
 
 int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32_t capacity,
                         uint8_t* shards, rfec_hdr* hdr, const uint64_t* present, const uint8_t* parity,
                         const rfec_hdr* meta, const uint16_t* fsize, const uint64_t* parity_present,
-                        uint64_t* recovered, void* ws, uint32_t ws_stride, void* stream, unsigned flags)
+                        uint64_t* recovered, void* ws, void* stream, unsigned flags)
 {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const uint32_t C = stride / 16;
-    hipLaunchKernelGGL(k_peel, dim3(blocks_for(groups)), dim3(kBlock), 0, st, hdr, present, meta, fsize,
-                       parity_present, recovered, reinterpret_cast<rfec_step*>(ws), groups, ws_stride, capacity,
-                       *M);
+    const bool ntl = !(flags & RFEC_KFLAG_PLAIN_LOADS);
+    if (flags & RFEC_KFLAG_WAVE_DECODE) {
+        RecArgs A;
+        A.shards = reinterpret_cast<v4u*>(shards);
+        A.hdr = hdr;
+        A.present = present;
+        A.parity = reinterpret_cast<const v4u*>(parity);
+        A.meta = meta;
+        A.fsize = fsize;
+        A.parity_present = parity_present;
+        A.recovered = recovered;
+        A.groups = groups;
+        A.C = stride / 16;
+        A.capacity = capacity;
+        const dim3 grid((unsigned)(((uint64_t)groups * kWave + kBlock - 1) / kBlock));
+        if (ntl)
+            hipLaunchKernelGGL(k_recover<true>, grid, dim3(kBlock), 0, st, A, *M);
+        else
+            hipLaunchKernelGGL(k_recover<false>, grid, dim3(kBlock), 0, st, A, *M);
+        return (int)hipGetLastError();
+    }
+    const rfec_kplan& P = M->plan;
+    PeelArgs B;
+    B.hdr = hdr;
+    B.present = present;
+    B.meta = meta;
+    B.fsize = fsize;
+    B.parity_present = parity_present;
+    B.recovered = recovered;
+    B.sched = reinterpret_cast<uint8_t*>(ws);
+    B.groups = groups;
+    B.capacity = capacity;
+    const uint32_t per = 5u * P.k + 6u * P.n_lines;
+    uint32_t gpb = kPeelDwords / per;
+    B.gpb = gpb < 1 ? 1 : (gpb > (uint32_t)kBlock ? (uint32_t)kBlock : gpb);
+    B.rec_bytes = rfec_sched_record_bytes(P.n_lines);
+    hipLaunchKernelGGL(k_peel_lds, dim3((groups + B.gpb - 1) / B.gpb), dim3(kBlock), 0, st, B, *M);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return (int)e;
+    uint32_t maxc = 0;
+    for (uint32_t l = 0; l < P.n_lines; ++l)
+        maxc = P.line[l].count > maxc ? P.line[l].count : maxc;
+    const uint32_t C = stride / 16;
     const uint32_t total = groups * C;
+    const dim3 grid(blocks_for(total));
     const FastDiv f = make_fastdiv(C);
-    if (flags & RFEC_KFLAG_TEMPORAL)
-        hipLaunchKernelGGL(k_recover<false>, dim3(blocks_for(total)), dim3(kBlock), 0, st,
-                           reinterpret_cast<v4u*>(shards), reinterpret_cast<const v4u*>(parity),
-                           reinterpret_cast<const rfec_step*>(ws), total, C, f, (uint32_t)M->plan.k,
-                           (uint32_t)M->plan.n_lines, ws_stride);
-    else
-        hipLaunchKernelGGL(k_recover<true>, dim3(blocks_for(total)), dim3(kBlock), 0, st,
-                           reinterpret_cast<v4u*>(shards), reinterpret_cast<const v4u*>(parity),
-                           reinterpret_cast<const rfec_step*>(ws), total, C, f, (uint32_t)M->plan.k,
-                           (uint32_t)M->plan.n_lines, ws_stride);
+    const v4u* pp = reinterpret_cast<const v4u*>(parity);
+    v4u* sh = reinterpret_cast<v4u*>(shards);
+    const uint8_t* sc = B.sched;
+    if (maxc <= 4) {
+        if (ntl)
+            hipLaunchKernelGGL((k_recover_flat<4, 2, true>), grid, dim3(kBlock), 0, st, sh, pp, sc, total, C, f,
+                               B.rec_bytes, 1u, P);
+        else
+            hipLaunchKernelGGL((k_recover_flat<4, 2, false>), grid, dim3(kBlock), 0, st, sh, pp, sc, total, C, f,
+                               B.rec_bytes, 1u, P);
+    } else {
+        const uint32_t fast = maxc <= 8;
+        if (ntl)
+            hipLaunchKernelGGL((k_recover_flat<8, 1, true>), grid, dim3(kBlock), 0, st, sh, pp, sc, total, C, f,
+                               B.rec_bytes, fast, P);
+        else
+            hipLaunchKernelGGL((k_recover_flat<8, 1, false>), grid, dim3(kBlock), 0, st, sh, pp, sc, total, C, f,
+                               B.rec_bytes, fast, P);
+    }
     return (int)hipGetLastError();
 }
 

@@ -29,7 +29,11 @@ RFEC_MAX_LINES = 64
 RFEC_LAYER_ROWS = 1
 RFEC_LAYER_COLS = 2
 RFEC_TUNE_GENERIC = 1
-RFEC_TUNE_TEMPORAL = 2
+RFEC_TUNE_PLAIN_LOADS = 2
+RFEC_TUNE_NT_STORES = 4
+RFEC_TUNE_WAVE_DECODE = 16
+RFEC_TUNE_ITEMS2 = 8
+RFEC_TUNE_DIAG_NO_META = 256
 
 # 20-byte header record == sim_fec_meta_t layout (sim_proto.h:145-155)
 HDR_DTYPE = np.dtype([("seq", "<u4"), ("fid", "<u4"), ("ts", "<u4"), ("index", "<u2"), ("total", "<u2"),
@@ -106,6 +110,9 @@ _SIGS = {
     "rfec_set_tuning": (None, [C.c_uint]),
     "rfec_get_tuning": (C.c_uint, []),
     "rfec_last_error": (C.c_char_p, []),
+    "rfec_probe_read": (C.c_int, [_P, C.c_size_t, _P, C.c_uint, _P]),
+    "rfec_probe_copy": (C.c_int, [_P, _P, C.c_size_t, C.c_uint, _P]),
+    "rfec_probe_write": (C.c_int, [_P, C.c_size_t, C.c_uint, _P]),
 }
 
 
@@ -114,6 +121,17 @@ def header_functions() -> list[str]:
     text = HEADER.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"^\s*[A-Za-z_][\w\s\*]*?\b([a-z_][a-z0-9_]*)\s*\(", text, flags=re.M)))
+
+
+def as_plan(p) -> rfec_plan:
+    """Accepts any ctypes struct with rfec_plan's layout (e.g. the oracle's)."""
+    if isinstance(p, rfec_plan):
+        return p
+    if C.sizeof(p) != C.sizeof(rfec_plan):
+        raise TypeError("not an rfec_plan")
+    q = rfec_plan()
+    C.memmove(C.byref(q), C.byref(p), C.sizeof(q))
+    return q
 
 
 class Native:
@@ -154,15 +172,15 @@ class Native:
     # -- batched device API (pointers are device addresses as ints) ----------
     def encode_batch(self, plan, groups, stride, capacity, shards, hdr, parity, meta, fec_size, status,
                      stream=None):
-        self._check(self.lib.rfec_encode_batch(C.byref(plan), groups, stride, capacity, shards, hdr, parity,
+        self._check(self.lib.rfec_encode_batch(C.byref(as_plan(plan)), groups, stride, capacity, shards, hdr, parity,
                                                meta, fec_size, status, stream), "rfec_encode_batch")
 
     def workspace_size(self, plan, groups) -> int:
-        return self.lib.rfec_recover_workspace_size(C.byref(plan), groups)
+        return self.lib.rfec_recover_workspace_size(C.byref(as_plan(plan)), groups)
 
     def recover_batch(self, plan, groups, stride, capacity, shards, hdr, present, parity, meta, fec_size,
                       parity_present, recovered, workspace, stream=None):
-        self._check(self.lib.rfec_recover_batch(C.byref(plan), groups, stride, capacity, shards, hdr, present,
+        self._check(self.lib.rfec_recover_batch(C.byref(as_plan(plan)), groups, stride, capacity, shards, hdr, present,
                                                 parity, meta, fec_size, parity_present, recovered, workspace,
                                                 stream), "rfec_recover_batch")
 
@@ -230,7 +248,7 @@ class DeviceBatch:
         self.present = torch.zeros((groups, 2), dtype=torch.int64, device=dev)
         self.parity_present = torch.zeros((groups,), dtype=torch.int64, device=dev)
         self.recovered = torch.zeros((groups, 2), dtype=torch.int64, device=dev)
-        ws = groups * (1 + self.n) * 8  # rfec_recover_workspace_size()
+        ws = groups * ((2 + 2 * self.n + 15) // 16 * 16)  # rfec_recover_workspace_size()
         self.workspace = torch.zeros((max(16, ws),), dtype=u8, device=dev)
 
     def encode(self, lib: Native, stream=None):

@@ -76,7 +76,7 @@ def test_argument_validation(product):
     bad.line[0].count = 20  # member beyond k
     with pytest.raises(RfecError):
         product.encode_batch(bad, 4, 1200, 1200, 1, 1, 1, 1, 1, None)
-    assert product.workspace_size(plan, 100) == 100 * (1 + plan.n_lines) * 8
+    assert product.workspace_size(plan, 100) == 100 * 16  # 2 + 2*3 bytes -> 16
 
 
 def test_dropin_fails_loudly_without_gpu():

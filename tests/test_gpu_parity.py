@@ -15,7 +15,8 @@ pytestmark = pytest.mark.gpu
 
 MANIFEST = po.manifest()
 CASES = {c["name"]: c for c in MANIFEST["cases"]}
-TUNINGS = {"default": 0, "generic": 1, "temporal": 2, "generic_temporal": 3}
+TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "nt_stores": 4, "items2": 8, "wave_decode": 16,
+           "generic_plain": 3}
 
 
 @pytest.fixture(scope="module")
@@ -44,9 +45,10 @@ def test_rows_fixture_gpu(gpu, oracle1000, oracle1200, name, tuning):
     pc.check_rows_case(gpu(tuning=TUNINGS[tuning]), o, c, capacity=max(c["S"], 1000))
 
 
+@pytest.mark.parametrize("tuning", ["default", "wave_decode", "plain_loads"])
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures"])
-def test_erasure_fixture_gpu(gpu, oracle1000, name):
-    pc.check_erasure_case(gpu(), oracle1000, CASES[name])
+def test_erasure_fixture_gpu(gpu, oracle1000, name, tuning):
+    pc.check_erasure_case(gpu(tuning=TUNINGS[tuning]), oracle1000, CASES[name])
 
 
 def test_single_cases_dropin_gpu(product):
@@ -129,8 +131,10 @@ def test_full_size_k10_roundtrip(product, oracle1200, layers):
     plan = lib.plan_from_fraction(k, 80, layers)
     shards, hdr, d_hdr = _device_batch(G, k, S, 1234)
     par, meta, fs, st = _run_encode(lib, plan, G, S, shards, d_hdr)
-    par2, meta2, fs2, st2 = _run_encode(lib, plan, G, S, shards, d_hdr, tuning=3)
-    assert torch.equal(par, par2) and torch.equal(meta, meta2) and torch.equal(fs, fs2)
+    for tuning in (1, 2, 4, 8, 3):
+        par2, meta2, fs2, st2 = _run_encode(lib, plan, G, S, shards, d_hdr, tuning=tuning)
+        assert torch.equal(par, par2) and torch.equal(meta, meta2) and torch.equal(fs, fs2), tuning
+        del par2, meta2, fs2, st2
     assert int(st.abs().sum()) == 0
     # oracle on a sample of groups
     idx = np.r_[0:8, G // 2:G // 2 + 8, G - 8:G]
@@ -182,8 +186,9 @@ def test_full_size_k32_s256(product, oracle1000):
     assert plan.n_lines == 8
     shards, hdr, d_hdr = _device_batch(G, k, S, 99)
     par, meta, fs, st = _run_encode(lib, plan, G, S, shards, d_hdr)
-    par2, *_ = _run_encode(lib, plan, G, S, shards, d_hdr, tuning=1)
-    assert torch.equal(par, par2)
+    for tuning in (1, 8):
+        par2, *_ = _run_encode(lib, plan, G, S, shards, d_hdr, tuning=tuning)
+        assert torch.equal(par, par2), tuning
     idx = np.r_[0:4, G - 4:G]
     p_o, m_o, f_o, _ = o.encode_batch(o.plan_matrix(k, 8, 4, 1), shards[idx].cpu().numpy(), hdr[idx], 256)
     assert np.array_equal(par[idx].cpu().numpy(), p_o)

@@ -1,0 +1,114 @@
+"""Interleaved A/B of the encode / decode kernel variants and the HBM ceiling
+probes on one GPU, one process (cdna_hip_programming.md §5.4 rule 24).
+
+Usage (GPU box): python tools/ab_encode.py [--rounds 5] [--reps 20] [--out gpurun_out/ab.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+from bench import Workload  # noqa: E402
+from razor_amd.fec import native  # noqa: E402
+
+ENC_VARIANTS = {
+    "nt_ld+plain_st(default)": 0,
+    "nt_ld+nt_st": 4,
+    "plain_ld+plain_st": 2,
+    "plain_ld+nt_st": 6,
+    "items2": 8,
+    "generic": 1,
+    "diag_no_meta": 256,
+}
+DEC_VARIANTS = {"flat_nt_ld(default)": 0, "flat_plain_ld": 2, "wave_nt_ld": 16, "wave_plain_ld": 18}
+
+
+def timeit(fn, reps, stream):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / 1e3 / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--groups", type=int, default=65536)
+    ap.add_argument("--out", default="gpurun_out/ab.json")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    lib = native(1000)
+    w = Workload(lib, args.groups, 10, 1200, 80, dev, 0, seed=5)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    nb = 1 << 30
+    a = torch.empty(nb, dtype=torch.uint8, device=dev)
+    b = torch.empty(nb, dtype=torch.uint8, device=dev)
+    sink = torch.zeros(16384, dtype=torch.uint8, device=dev)
+    a.random_(0, 255)
+
+    def enc(flags):
+        def f():
+            lib.set_tuning(flags)
+            w.encode(sp)
+        return f
+
+    def dec(flags):
+        def f():
+            lib.set_tuning(flags)
+            w.decode(sp)
+        return f
+
+    def probe(kind, flags):
+        L = lib.lib
+        if kind == "read":
+            return lambda: L.rfec_probe_read(a.data_ptr(), nb, sink.data_ptr(), flags, sp)
+        if kind == "copy":
+            return lambda: L.rfec_probe_copy(a.data_ptr(), b.data_ptr(), nb // 2, flags, sp)
+        return lambda: L.rfec_probe_write(b.data_ptr(), nb, flags, sp)
+
+    cases = {}
+    for k, f in ENC_VARIANTS.items():
+        cases[f"enc/{k}"] = (enc(f), w.enc_bytes)
+    for k, f in DEC_VARIANTS.items():
+        cases[f"dec/{k}"] = (dec(f), w.dec_bytes)
+    for kind, bytes_ in (("read", nb), ("copy", nb), ("write", nb)):
+        for fl, name in ((0, "plain"), (1, "nt"), (2, "plain_x4"), (3, "nt_x4")):
+            cases[f"probe_{kind}/{name}"] = (probe(kind, fl), bytes_)
+    res = {k: [] for k in cases}
+    for k, (fn, _) in cases.items():  # warm
+        fn()
+    torch.cuda.synchronize()
+    for r in range(args.rounds):
+        for k, (fn, _) in cases.items():
+            res[k].append(timeit(fn, args.reps, stream))
+    lib.set_tuning(0)
+    out = {}
+    print(f"{'case':32s} {'median_us':>10s} {'min_us':>10s} {'GB/s(med)':>10s} {'frac8T':>7s}")
+    for k, (_, bytes_) in cases.items():
+        t = np.array(res[k])
+        med, mn = float(np.median(t)), float(t.min())
+        gbs = bytes_ / med / 1e9
+        out[k] = {"median_us": med * 1e6, "min_us": mn * 1e6, "GBps": gbs, "frac_of_8TBps": gbs / 8000, "bytes": bytes_}
+        print(f"{k:32s} {med * 1e6:10.1f} {mn * 1e6:10.1f} {gbs:10.1f} {gbs / 8000:7.3f}")
+    ok = w.verify()
+    print("verify", ok)
+    Path(args.out).parent.mkdir(parents=True, exist_ok=True)
+    Path(args.out).write_text(json.dumps({"results": out, "verified": ok,
+                                          "device": torch.cuda.get_device_name(0)}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
