@@ -59,17 +59,22 @@ def distinct_row_pairs(plan):
 
 
 class Workload:
-    def __init__(self, lib, G, k, S, pf, device, group0, seed):
+    def __init__(self, lib, G, k, S, pf, device, group0, seed, stride=None):
         self.lib, self.G, self.k, self.S = lib, G, k, S
+        self.stride = stride or (S + 15) // 16 * 16  # slot width in HBM (>= S, multiple of 16)
         self.plan = lib.plan_from_fraction(k, pf, 1)  # row layer: r = 3 at k = 10
         self.n = self.plan.n_lines
         dev = device
         gen = torch.Generator(device=dev)
         gen.manual_seed(seed)
-        self.shards = torch.randint(0, 256, (G, k, S), dtype=torch.uint8, device=dev, generator=gen)
+        if self.stride == S:
+            self.shards = torch.randint(0, 256, (G, k, S), dtype=torch.uint8, device=dev, generator=gen)
+        else:
+            self.shards = torch.zeros((G, k, self.stride), dtype=torch.uint8, device=dev)
+            self.shards[:, :, :S] = torch.randint(0, 256, (G, k, S), dtype=torch.uint8, device=dev, generator=gen)
         self.hdr_np = make_headers(G, k, S, group0)
         self.hdr = torch.from_numpy(self.hdr_np.view(np.uint8).reshape(G, k, 20).copy()).to(dev)
-        self.parity = torch.empty((G, self.n, S), dtype=torch.uint8, device=dev)
+        self.parity = torch.empty((G, self.n, self.stride), dtype=torch.uint8, device=dev)
         self.meta = torch.empty((G, self.n, 20), dtype=torch.uint8, device=dev)
         self.fsize = torch.empty((G, self.n), dtype=torch.int16, device=dev)
         self.status = torch.empty((G, self.n), dtype=torch.int8, device=dev)
@@ -101,18 +106,33 @@ class Workload:
         self.dec_bytes = int((sizes[self.erased[:, 0]] + 1).sum() + (sizes[self.erased[:, 1]] + 1).sum()) * S
 
     def encode(self, stream):
-        self.lib.encode_batch(self.plan, self.G, self.S, self.S, self.shards.data_ptr(), self.hdr.data_ptr(),
+        self.lib.encode_batch(self.plan, self.G, self.stride, self.S, self.shards.data_ptr(), self.hdr.data_ptr(),
                               self.parity.data_ptr(), self.meta.data_ptr(), self.fsize.data_ptr(),
                               self.status.data_ptr(), stream)
 
     def decode(self, stream):
-        self.lib.recover_batch(self.plan, self.G, self.S, self.S, self.rx.data_ptr(), self.rx_hdr.data_ptr(),
+        self.lib.recover_batch(self.plan, self.G, self.stride, self.S, self.rx.data_ptr(), self.rx_hdr.data_ptr(),
                                self.present.data_ptr(), self.parity.data_ptr(), self.meta.data_ptr(),
                                self.fsize.data_ptr(), self.parity_present.data_ptr(), self.recovered.data_ptr(),
                                self.ws.data_ptr(), stream)
 
     def verify(self):
-        ok = torch.equal(self.rx, self.shards) and torch.equal(self.rx_hdr, self.hdr)
+        """Whole-batch checks after the timed steps (not timed): every parity
+        line equals a torch XOR of its members (payload and 20-B meta record),
+        and every erased segment came back bit-exact."""
+        S = self.S
+        ok = True
+        hdr32 = self.hdr.view(torch.int32).reshape(self.G, self.k, 5)
+        meta32 = self.meta.view(torch.int32).reshape(self.G, self.n, 5)
+        for l in range(self.n):
+            mem = self.plan.members(l)
+            ref = self.shards[:, mem[0], :S].clone()
+            href = hdr32[:, mem[0]].clone()
+            for i in mem[1:]:
+                ref ^= self.shards[:, i, :S]
+                href ^= hdr32[:, i]
+            ok = ok and torch.equal(self.parity[:, l, :S], ref) and torch.equal(meta32[:, l], href)
+        ok = ok and torch.equal(self.rx[:, :, :S], self.shards[:, :, :S]) and torch.equal(self.rx_hdr, self.hdr)
         exp = ((1 << self.erased[:, 0]) | (1 << self.erased[:, 1])).astype(np.int64)
         ok = ok and np.array_equal(self.recovered[:, 0].cpu().numpy(), exp)
         ok = ok and int(self.status.abs().sum()) == 0
@@ -144,7 +164,7 @@ def cpu_baseline(w: Workload, seconds: float):
     from pyoracle import Oracle
 
     sample = min(w.G, 4096)
-    shards = w.shards[:sample].cpu().numpy()
+    shards = w.shards[:sample, :, :w.S].cpu().numpy()
     hdr = w.hdr_np[:sample]
     present = w.present_np[:sample]
     out = {}
@@ -219,6 +239,7 @@ def main():
                     help="split this many groups over the GPUs instead (strong scaling, e.g. 1048576)")
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--payload", type=int, default=1200)
+    ap.add_argument("--stride", type=int, default=0, help="HBM slot width (default: payload rounded to 16)")
     ap.add_argument("--protect-fraction", type=int, default=80)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -247,7 +268,8 @@ def main():
     else:
         group0, my_groups = rank * args.groups, args.groups
         scaling = "weak"
-    w = Workload(lib, my_groups, args.k, args.payload, args.protect_fraction, device, group0, seed=1000 + rank)
+    w = Workload(lib, my_groups, args.k, args.payload, args.protect_fraction, device, group0, seed=1000 + rank,
+                 stride=args.stride or None)
     stream = torch.cuda.current_stream(device)
     sp = stream.cuda_stream
     torch.cuda.synchronize(device)

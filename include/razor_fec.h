@@ -185,6 +185,26 @@ int rfec_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, 
                        const uint64_t* parity_present, uint64_t* recovered, void* workspace,
                        void* stream);
 
+/*
+ * Host-resident batch: the path that starts and ends in host memory (segments
+ * built from UDP socket buffers, sim_session.c).  Gathers G groups of
+ * sim_segment_t (segs[g*k + i], this library's SIM_VIDEO_SIZE layout) into a
+ * pinned structure-of-arrays staging area, copies it to HBM, runs
+ * rfec_encode_batch, copies the parities back and scatters them into the
+ * caller's sim_fec_t (fecs[g*n + l]) stamped like flex_fec_sender_update
+ * (flex_fec_sender.c:176-181, 220-225: fec_id = fec_id0 + g, base_id = the
+ * group's smallest packet_id, row, col, index, count).  A line whose
+ * flex_fec_generate would fail gets fec_data_size = 0xFFFF and no payload.
+ * `timing` (may be NULL) receives the per-stage wall times in microseconds.
+ * Staging is per calling thread and grows on demand.
+ */
+typedef struct {
+    double gather_us, h2d_us, kernel_us, d2h_us, scatter_us, total_us;
+} rfec_host_timing;
+
+int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,
+                            sim_fec_t* const* fecs, uint16_t fec_id0, rfec_host_timing* timing);
+
 /* Zero bytes [data_size, stride) of every shard (establishes the layout
  * invariant for callers that cannot guarantee it). */
 int rfec_zero_tails(uint32_t groups, uint32_t k, uint32_t stride, uint8_t* shards,
@@ -194,9 +214,14 @@ int rfec_zero_tails(uint32_t groups, uint32_t k, uint32_t stride, uint8_t* shard
  * specialised row kernels where the plan allows, non-temporal streaming). */
 #define RFEC_TUNE_GENERIC 1u       /* always use the generic plan-driven kernel */
 #define RFEC_TUNE_PLAIN_LOADS 2u   /* plain instead of non-temporal payload loads */
-#define RFEC_TUNE_NT_STORES 4u     /* non-temporal instead of plain parity stores */
+#define RFEC_TUNE_PLAIN_STORES 4u  /* plain instead of non-temporal parity / recovered stores */
 #define RFEC_TUNE_ITEMS2 8u        /* two chunk columns per lane in the row kernels */
 #define RFEC_TUNE_WAVE_DECODE 16u  /* one-launch recovery, one wave per group */
+#define RFEC_TUNE_PIPE_DECODE 32u  /* grid-stride recovery replay with record prefetch */
+#define RFEC_TUNE_WT_STORES 64u    /* write-through (sc0 sc1) parity / recovered stores */
+#define RFEC_TUNE_WT_NT 128u       /* with RFEC_TUNE_WT_STORES: sc0 sc1 nt */
+#define RFEC_TUNE_NT_STORES 512u   /* non-temporal parity / recovered stores */
+/* (defaults: parity stores write-through, recovered stores non-temporal) */
 #define RFEC_TUNE_DIAG_NO_META 256u /* DIAGNOSTIC ONLY: skip fec_meta (wrong output) */
 void rfec_set_tuning(unsigned flags);
 unsigned rfec_get_tuning(void);

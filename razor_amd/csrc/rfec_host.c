@@ -263,6 +263,12 @@ typedef struct {
     uint8_t* host;   /* host view */
     uint8_t* dev;    /* device view of the same bytes */
     size_t bytes;
+    /* rfec_host_encode_groups: pinned host staging + its HBM mirror */
+    uint8_t* bh;
+    uint8_t* bd;
+    size_t b_bytes;
+    hipEvent_t ev[4];
+    int have_ev;
 } di_ctx;
 
 typedef struct { /* offsets inside the staging area */
@@ -304,6 +310,12 @@ static void di_free(void* p)
         return;
     if (c->host)
         (void)hipHostFree(c->host);
+    if (c->bh)
+        (void)hipHostFree(c->bh);
+    if (c->bd)
+        (void)hipFree(c->bd);
+    for (int i = 0; c->have_ev && i < 4; ++i)
+        (void)hipEventDestroy(c->ev[i]);
     if (c->stream)
         (void)hipStreamDestroy(c->stream);
     free(c);
@@ -506,4 +518,162 @@ int flex_fec_recover(sim_segment_t* segs[], int segs_count, sim_fec_t* fec, sim_
     memcpy(out_seg->data, c->host + L.shards + (size_t)segs_count * DI_STRIDE, Lfec);
     out_seg->fec_id = fec->fec_id; /* :101 */
     return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* 4. host-resident batch (gather -> H2D -> encode -> D2H -> scatter)        */
+/* ------------------------------------------------------------------------ */
+#include <time.h>
+
+static double now_us(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
+typedef struct {
+    size_t shards, hdr, parity, meta, fsize, status, in_bytes, total;
+} hb_layout;
+
+static hb_layout hb_offsets(uint32_t G, uint32_t k, uint32_t n)
+{
+    hb_layout L;
+    size_t o = 0;
+#define HB_TAKE(field, bytes)                       \
+    do {                                             \
+        L.field = o;                                 \
+        o = (o + (size_t)(bytes) + 255) & ~(size_t)255; \
+    } while (0)
+    HB_TAKE(shards, (size_t)G * k * DI_STRIDE);
+    HB_TAKE(hdr, (size_t)G * k * sizeof(rfec_hdr));
+    L.in_bytes = o; /* [shards, hdr] go host -> device in one copy */
+    HB_TAKE(parity, (size_t)G * n * DI_STRIDE);
+    HB_TAKE(meta, (size_t)G * n * sizeof(rfec_hdr));
+    HB_TAKE(fsize, (size_t)G * n * sizeof(uint16_t));
+    HB_TAKE(status, (size_t)G * n);
+#undef HB_TAKE
+    L.total = o;
+    return L;
+}
+
+static int hb_reserve(di_ctx* c, size_t bytes)
+{
+    hipError_t e;
+    if (!c->have_ev) {
+        for (int i = 0; i < 4; ++i)
+            if ((e = hipEventCreate(&c->ev[i])) != hipSuccess)
+                return set_err(RFEC_EDEVICE, "event create", e);
+        c->have_ev = 1;
+    }
+    if (c->b_bytes >= bytes)
+        return RFEC_OK;
+    if (c->bh)
+        (void)hipHostFree(c->bh);
+    if (c->bd)
+        (void)hipFree(c->bd);
+    c->bh = NULL;
+    c->bd = NULL;
+    c->b_bytes = 0;
+    if ((e = hipHostMalloc((void**)&c->bh, bytes, hipHostMallocDefault)) != hipSuccess)
+        return set_err(RFEC_ENOMEM, "pinned staging", e);
+    if ((e = hipMalloc((void**)&c->bd, bytes)) != hipSuccess)
+        return set_err(RFEC_ENOMEM, "device staging", e);
+    c->b_bytes = bytes;
+    return RFEC_OK;
+}
+
+/* the sender's fec_id sequence: +1 per group, 0 skipped (flex_fec_sender.c:241-243) */
+static uint16_t fec_id_at(uint16_t id0, uint32_t g)
+{
+    const uint32_t base = id0 ? (uint32_t)id0 - 1u : 0u;
+    return (uint16_t)((base + g) % 65535u + 1u);
+}
+
+int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,
+                            sim_fec_t* const* fecs, uint16_t fec_id0, rfec_host_timing* timing)
+{
+    int rc = check_plan(plan);
+    if (rc)
+        return rc;
+    if (groups == 0 || plan->n_lines == 0)
+        return RFEC_OK;
+    if (!segs || !fecs)
+        return set_err(RFEC_EINVAL, "NULL segs / fecs", 0);
+    if ((rc = check_geometry(groups, DI_STRIDE, SIM_VIDEO_SIZE, plan->k)))
+        return rc;
+    di_ctx* c = di_get();
+    if (!c)
+        return RFEC_EDEVICE;
+    const uint32_t k = plan->k, n = plan->n_lines;
+    const hb_layout L = hb_offsets(groups, k, n);
+    if ((rc = hb_reserve(c, L.total)))
+        return rc;
+    const double t0 = now_us();
+    /* gather: AoS segments (payload at offset 34, not 16-B aligned) -> SoA slots */
+    rfec_hdr* hh = (rfec_hdr*)(c->bh + L.hdr);
+    for (size_t s = 0; s < (size_t)groups * k; ++s) {
+        const sim_segment_t* seg = segs[s];
+        stage_payload(c->bh + L.shards + s * DI_STRIDE, seg->data, seg->data_size);
+        seg_to_hdr(seg, &hh[s]);
+    }
+    const double t1 = now_us();
+    hipError_t e;
+    if ((e = hipEventRecord(c->ev[0], c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(c->bd, c->bh, L.in_bytes, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (e = hipEventRecord(c->ev[1], c->stream)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "H2D", e);
+    const int ke = rfec_launch_encode(plan, groups, DI_STRIDE, SIM_VIDEO_SIZE, c->bd + L.shards,
+                                      (const rfec_hdr*)(c->bd + L.hdr), c->bd + L.parity,
+                                      (rfec_hdr*)(c->bd + L.meta), (uint16_t*)(c->bd + L.fsize),
+                                      (int8_t*)(c->bd + L.status), c->stream, g_tuning);
+    if (ke)
+        return set_err(RFEC_EDEVICE, "encode launch", ke);
+    if ((e = hipEventRecord(c->ev[2], c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(c->bh + L.parity, c->bd + L.parity, L.total - L.parity, hipMemcpyDeviceToHost,
+                            c->stream)) != hipSuccess ||
+        (e = hipEventRecord(c->ev[3], c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "D2H", e);
+    const double t2 = now_us();
+    /* scatter into the caller's sim_fec_t, stamped as flex_fec_sender_update does */
+    const rfec_hdr* mh = (const rfec_hdr*)(c->bh + L.meta);
+    const uint16_t* fs = (const uint16_t*)(c->bh + L.fsize);
+    const int8_t* st = (const int8_t*)(c->bh + L.status);
+    for (uint32_t g = 0; g < groups; ++g) {
+        uint32_t base = hh[(size_t)g * k].seq;
+        for (uint32_t i = 1; i < k; ++i)
+            base = hh[(size_t)g * k + i].seq < base ? hh[(size_t)g * k + i].seq : base;
+        for (uint32_t l = 0; l < n; ++l) {
+            const size_t o = (size_t)g * n + l;
+            sim_fec_t* f = fecs[o];
+            f->fec_id = fec_id_at(fec_id0, g);
+            f->base_id = base;
+            f->row = plan->row;
+            f->col = plan->col;
+            f->index = plan->line[l].index;
+            f->count = plan->k;
+            if (st[o] != 0) {
+                f->fec_data_size = 0xFFFF;
+                continue;
+            }
+            memcpy(&f->fec_meta, &mh[o], sizeof(rfec_hdr));
+            f->fec_data_size = fs[o];
+            memcpy(f->fec_data, c->bh + L.parity + o * DI_STRIDE, fs[o]);
+        }
+    }
+    const double t3 = now_us();
+    if (timing) {
+        float a = 0, b = 0, d = 0;
+        (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
+        (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
+        (void)hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
+        timing->gather_us = t1 - t0;
+        timing->h2d_us = a * 1e3;
+        timing->kernel_us = b * 1e3;
+        timing->d2h_us = d * 1e3;
+        timing->scatter_us = t3 - t2;
+        timing->total_us = t3 - t0;
+    }
+    return RFEC_OK;
 }

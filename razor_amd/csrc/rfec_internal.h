@@ -20,8 +20,12 @@ typedef struct {
 /* kernel flags == the RFEC_TUNE_* bits of razor_fec.h */
 #define RFEC_KFLAG_GENERIC RFEC_TUNE_GENERIC
 #define RFEC_KFLAG_PLAIN_LOADS RFEC_TUNE_PLAIN_LOADS
-#define RFEC_KFLAG_NT_STORES RFEC_TUNE_NT_STORES
+#define RFEC_KFLAG_PLAIN_STORES RFEC_TUNE_PLAIN_STORES
 #define RFEC_KFLAG_WAVE_DECODE RFEC_TUNE_WAVE_DECODE
+#define RFEC_KFLAG_PIPE_DECODE RFEC_TUNE_PIPE_DECODE
+#define RFEC_KFLAG_WT_STORES RFEC_TUNE_WT_STORES
+#define RFEC_KFLAG_WT_NT RFEC_TUNE_WT_NT
+#define RFEC_KFLAG_NT_STORES RFEC_TUNE_NT_STORES
 #define RFEC_KFLAG_ITEMS2 RFEC_TUNE_ITEMS2
 #define RFEC_KFLAG_DIAG_NO_META RFEC_TUNE_DIAG_NO_META
 

@@ -57,11 +57,22 @@ __device__ __forceinline__ v4u ld16(const v4u* p)
         return *p;
 }
 
-template <bool NT>
+// Store cache policy: 0 plain, 1 non-temporal, 2 write-through (sc0 sc1),
+// 3 write-through + non-temporal.  2 and 3 are emitted as inline asm (hipcc
+// has no builtin for them).  hipcc neither counts nor pads an asm statement
+// (cdna_hip_programming.md §5.7): the trailing `s_nop 1` keeps the next VALU
+// from overwriting the store-data VGPRs before the dwordx4 store reads them;
+// no s_waitcnt is needed (nothing of ours waits on a store, and a later load
+// of the same address by the same lane is ordered behind it by the memory pipe).
+template <int SP>
 __device__ __forceinline__ void st16(v4u* p, v4u v)
 {
-    if constexpr (NT)
+    if constexpr (SP == 1)
         __builtin_nontemporal_store(v, p);
+    else if constexpr (SP == 2)
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (SP == 3)
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
     else
         *p = v;
 }
@@ -69,6 +80,47 @@ __device__ __forceinline__ void st16(v4u* p, v4u v)
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
 {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+
+// Copies n dwords global -> LDS with the whole block, several loads in flight
+// per lane (a plain strided loop would wait on each load before the next).
+// `lds` must be 16-byte aligned; 16-byte loads are used when `src` is too.
+__device__ __forceinline__ void stage_dwords(uint32_t* lds, const uint32_t* __restrict__ src, uint32_t n)
+{
+    constexpr int U = 4;
+    const uint32_t nv = ((reinterpret_cast<uintptr_t>(src) & 15) == 0) ? n / 4 : 0;
+    const v4u* s4 = reinterpret_cast<const v4u*>(src);
+    v4u* d4 = reinterpret_cast<v4u*>(lds);
+    for (uint32_t base = 0; base < nv; base += U * kBlock) {
+        v4u tmp[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = base + u * kBlock + threadIdx.x;
+            if (i < nv)
+                tmp[u] = s4[i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = base + u * kBlock + threadIdx.x;
+            if (i < nv)
+                d4[i] = tmp[u];
+        }
+    }
+    for (uint32_t base = nv * 4; base < n; base += 4 * U * kBlock) {
+        uint32_t tmp[4 * U];
+#pragma unroll
+        for (int u = 0; u < 4 * U; ++u) {
+            const uint32_t i = base + u * kBlock + threadIdx.x;
+            if (i < n)
+                tmp[u] = src[i];
+        }
+#pragma unroll
+        for (int u = 0; u < 4 * U; ++u) {
+            const uint32_t i = base + u * kBlock + threadIdx.x;
+            if (i < n)
+                lds[i] = tmp[u];
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -80,14 +132,11 @@ __device__ void meta_block(uint32_t mb, const uint32_t* __restrict__ hdr_dw, uin
                            uint16_t* __restrict__ fsize, int8_t* __restrict__ status, uint32_t groups,
                            uint32_t capacity, uint32_t gpb, const rfec_kplan& P)
 {
-    __shared__ uint32_t lds[kMetaDwords];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kMetaDwords];
     const uint32_t K = P.k, NL = P.n_lines;
     const uint32_t g0 = mb * gpb;
     const uint32_t ng = min(gpb, groups - g0);
-    const uint32_t ndw = ng * K * 5;
-    const uint32_t* src = hdr_dw + (size_t)g0 * K * 5;
-    for (uint32_t i = threadIdx.x; i < ndw; i += kBlock)
-        lds[i] = src[i];
+    stage_dwords(lds, hdr_dw + (size_t)g0 * K * 5, ng * K * 5);
     __syncthreads();
     for (uint32_t o = threadIdx.x; o < ng * NL; o += kBlock) {
         const uint32_t gl = o / NL, l = o - gl * NL;
@@ -127,7 +176,7 @@ struct EncMeta {
 // ---------------------------------------------------------------------------
 // Encode payload, generic plan.
 // ---------------------------------------------------------------------------
-template <bool NTL, bool NTS>
+template <bool NTL, int NTS>
 __global__ __launch_bounds__(kBlock) void k_encode(const v4u* __restrict__ shards, v4u* __restrict__ parity,
                                                    uint32_t total, uint32_t C, FastDiv divC, EncMeta E,
                                                    rfec_kplan P)
@@ -140,7 +189,7 @@ __global__ __launch_bounds__(kBlock) void k_encode(const v4u* __restrict__ shard
     if (t >= total)
         return;
     const uint32_t g = fdiv(t, divC);
-    const uint32_t j = t - g * C;
+    const uint32_t j = t - g * divC.d; // chunk column (divC.d = chunks of work per slot)
     const v4u* src = shards + (size_t)g * P.k * C + j;
     v4u* dst = parity + (size_t)g * P.n_lines * C + j;
     for (uint32_t l = 0; l < P.n_lines; ++l) {
@@ -160,7 +209,7 @@ __global__ __launch_bounds__(kBlock) void k_encode(const v4u* __restrict__ shard
 // issue back to back.  Item u of a lane is chunk t0 + u*(payload lanes), so
 // every wave instruction still covers 1 KiB of consecutive chunks.
 // ---------------------------------------------------------------------------
-template <int K, int COL, bool NTL, bool NTS, int ITEMS>
+template <int K, int COL, bool NTL, int NTS, int ITEMS>
 __global__ __launch_bounds__(kBlock) void k_encode_rows(const v4u* __restrict__ shards, v4u* __restrict__ parity,
                                                         uint32_t total, uint32_t C, FastDiv divC, EncMeta E,
                                                         rfec_kplan P)
@@ -178,7 +227,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_rows(const v4u* __restrict__ 
     for (int u = 0; u < ITEMS; ++u) {
         const uint32_t t = t0 + u * lanes;
         gi[u] = fdiv(t, divC);
-        ji[u] = t - gi[u] * C;
+        ji[u] = t - gi[u] * divC.d;
         if (t < total) {
             const v4u* src = shards + (size_t)gi[u] * K * C + ji[u];
 #pragma unroll
@@ -224,7 +273,7 @@ struct RecArgs {
     const uint16_t* fsize;
     const uint64_t* parity_present;
     uint64_t* recovered;
-    uint32_t groups, C, capacity;
+    uint32_t groups, C, Cd, capacity;
 };
 
 template <bool NTL>
@@ -302,9 +351,9 @@ __global__ __launch_bounds__(kBlock) void k_recover(RecArgs A, rfec_kmask M)
                 continue;
 
             // payload: this lane's chunk columns j = lane, lane+64, ...
-            for (uint32_t j0 = 0; j0 < C; j0 += 2 * kWave) {
+            for (uint32_t j0 = 0; j0 < A.Cd; j0 += 2 * kWave) {
                 const uint32_t ja = j0 + lane, jb = j0 + kWave + lane;
-                const bool oka = ja < C, okb = jb < C;
+                const bool oka = ja < A.Cd, okb = jb < A.Cd;
                 v4u a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
                 const v4u* pl = par + (size_t)l * C;
                 if (oka)
@@ -376,41 +425,52 @@ struct PeelArgs {
     const uint64_t* parity_present;
     uint64_t* recovered;
     uint8_t* sched;
-    uint32_t groups, capacity, gpb, rec_bytes;
+    uint32_t groups, capacity, gpb, rec_bytes, disjoint;
 };
 
 __global__ __launch_bounds__(kBlock) void k_peel_lds(PeelArgs A, rfec_kmask M)
 {
-    __shared__ uint32_t lds[kPeelDwords];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kPeelDwords];
     const rfec_kplan& P = M.plan;
     const uint32_t K = P.k, NL = P.n_lines;
     const uint32_t g0 = blockIdx.x * A.gpb;
     const uint32_t ng = min(A.gpb, A.groups - g0);
-    uint32_t* Lh = lds;               // [ng][K][5]
-    uint32_t* Lm = Lh + ng * K * 5;   // [ng][NL][5]
-    uint32_t* Lf = Lm + ng * NL * 5;  // [ng][NL]
-    const uint32_t* hsrc = reinterpret_cast<const uint32_t*>(A.hdr + (size_t)g0 * K);
-    const uint32_t* msrc = reinterpret_cast<const uint32_t*>(A.meta + (size_t)g0 * NL);
-    for (uint32_t i = threadIdx.x; i < ng * K * 5; i += kBlock)
-        Lh[i] = hsrc[i];
-    for (uint32_t i = threadIdx.x; i < ng * NL * 5; i += kBlock)
-        Lm[i] = msrc[i];
-    for (uint32_t i = threadIdx.x; i < ng * NL; i += kBlock)
-        Lf[i] = A.fsize[(size_t)g0 * NL + i];
+    const uint32_t g = g0 + threadIdx.x;
+    // this lane's masks first, so their latency overlaps the staging below
+    uint64_t have0 = 0, have1 = 0, ppm = 0;
+    if (threadIdx.x < ng) {
+        have0 = A.present[2 * g];
+        have1 = A.present[2 * g + 1];
+        ppm = A.parity_present[g];
+    }
+    const uint32_t nh = ng * K * 5, nm = ng * NL * 5, nf = ng * NL;
+    uint32_t* Lh = lds;                            // [ng][K][5]
+    uint32_t* Lm = Lh + ((nh + 3) & ~3u);          // [ng][NL][5]
+    uint16_t* Lf = reinterpret_cast<uint16_t*>(Lm + ((nm + 3) & ~3u)); // [ng][NL]
+    stage_dwords(Lh, reinterpret_cast<const uint32_t*>(A.hdr + (size_t)g0 * K), nh);
+    stage_dwords(Lm, reinterpret_cast<const uint32_t*>(A.meta + (size_t)g0 * NL), nm);
+    const uint16_t* fsrc = A.fsize + (size_t)g0 * NL;
+    if ((reinterpret_cast<uintptr_t>(fsrc) & 3) == 0) {
+        stage_dwords(reinterpret_cast<uint32_t*>(Lf), reinterpret_cast<const uint32_t*>(fsrc), nf / 2);
+        if ((nf & 1) && threadIdx.x == 0)
+            Lf[nf - 1] = fsrc[nf - 1];
+    } else {
+        for (uint32_t i = threadIdx.x; i < nf; i += kBlock)
+            Lf[i] = fsrc[i];
+    }
     __syncthreads();
     if (threadIdx.x >= ng)
         return;
-    const uint32_t g = g0 + threadIdx.x;
     uint32_t* h = Lh + threadIdx.x * K * 5;
     const uint32_t* m = Lm + threadIdx.x * NL * 5;
-    const uint32_t* f = Lf + threadIdx.x * NL;
-    uint64_t have0 = A.present[2 * g], have1 = A.present[2 * g + 1];
-    const uint64_t ppm = A.parity_present[g];
+    const uint16_t* f = Lf + threadIdx.x * NL;
     uint64_t rec0 = 0, rec1 = 0;
     uint8_t* rec = A.sched + (size_t)g * A.rec_bytes;
     uint32_t n = 0, single = 1;
+    // with pairwise-disjoint lines (e.g. the row layer alone) a recovery can
+    // never complete another line, so one pass reaches the fixpoint
     bool progress = true;
-    while (progress) {
+    for (uint32_t pass = 0; progress && !(A.disjoint && pass > 0); ++pass) {
         progress = false;
         for (uint32_t l = 0; l < NL; ++l) {
             if (!((ppm >> l) & 1ull))
@@ -474,27 +534,13 @@ __device__ __forceinline__ uint32_t rec_byte(const v4u& r, uint32_t b)
     return (r[b >> 2] >> (8 * (b & 3))) & 0xffu;
 }
 
-template <int MAXC, int BATCH, bool NTL>
-__global__ __launch_bounds__(kBlock) void k_recover_flat(v4u* shards, const v4u* __restrict__ parity,
-                                                         const uint8_t* __restrict__ sched, uint32_t total,
-                                                         uint32_t C, FastDiv divC, uint32_t rec_bytes,
-                                                         uint32_t fast_ok, rfec_kplan P)
+// Replays one group's schedule record over one chunk column: grp / par point
+// at chunk j of the group's segment / parity slots, r0 = first 16 record bytes.
+template <int MAXC, int BATCH, bool NTL, int NTS>
+__device__ __forceinline__ void replay(v4u* grp, const v4u* __restrict__ par, const uint8_t* __restrict__ rec,
+                                       const v4u r0, uint32_t C, uint32_t fast_ok, const uint32_t* lplan)
 {
-    __shared__ uint32_t lplan[RFEC_MAX_LINES];
-    if (threadIdx.x < P.n_lines)
-        lplan[threadIdx.x] = reinterpret_cast<const uint32_t*>(P.line)[threadIdx.x];
-    __syncthreads();
-    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    if (t >= total)
-        return;
-    const uint32_t g = fdiv(t, divC);
-    const uint32_t j = t - g * C;
-    const uint32_t K = P.k, NL = P.n_lines;
-    const uint8_t* rec = sched + (size_t)g * rec_bytes;
-    const v4u r0 = *reinterpret_cast<const v4u*>(rec);
     const uint32_t n = rec_byte(r0, 0);
-    v4u* grp = shards + (size_t)g * K * C + j;
-    const v4u* par = parity + (size_t)g * NL * C + j;
     uint32_t s = 0;
     if (fast_ok && rec_byte(r0, 1)) {
         // single level: BATCH steps at a time, all loads in flight together
@@ -527,7 +573,7 @@ __global__ __launch_bounds__(kBlock) void k_recover_flat(v4u* shards, const v4u*
                 for (int q = 0; q < MAXC; ++q)
                     acc[b] ^= mv[b][q];
                 if (on[b])
-                    grp[(size_t)tg[b] * C] = acc[b];
+                    st16<NTS>(grp + (size_t)tg[b] * C, acc[b]);
             }
         }
         s = nf;
@@ -544,7 +590,63 @@ __global__ __launch_bounds__(kBlock) void k_recover_flat(v4u* shards, const v4u*
             if (i != tt)
                 acc ^= grp[(size_t)i * C];
         }
-        grp[(size_t)tt * C] = acc;
+        st16<NTS>(grp + (size_t)tt * C, acc);
+    }
+}
+
+__device__ __forceinline__ void stage_plan(uint32_t* lplan, const rfec_kplan& P)
+{
+    if (threadIdx.x < P.n_lines)
+        lplan[threadIdx.x] = reinterpret_cast<const uint32_t*>(P.line)[threadIdx.x];
+    __syncthreads();
+}
+
+template <int MAXC, int BATCH, bool NTL, int NTS>
+__global__ __launch_bounds__(kBlock) void k_recover_flat(v4u* shards, const v4u* __restrict__ parity,
+                                                         const uint8_t* __restrict__ sched, uint32_t total,
+                                                         uint32_t C, FastDiv divC, uint32_t rec_bytes,
+                                                         uint32_t fast_ok, rfec_kplan P)
+{
+    __shared__ uint32_t lplan[RFEC_MAX_LINES];
+    stage_plan(lplan, P);
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= total)
+        return;
+    const uint32_t g = fdiv(t, divC);
+    const uint32_t j = t - g * divC.d; // chunk column (divC.d = chunks of work per slot)
+    const uint8_t* rec = sched + (size_t)g * rec_bytes;
+    const v4u r0 = *reinterpret_cast<const v4u*>(rec);
+    replay<MAXC, BATCH, NTL, NTS>(shards + (size_t)g * P.k * C + j, parity + (size_t)g * P.n_lines * C + j, rec, r0, C,
+                             fast_ok, lplan);
+}
+
+// Grid-stride form: each lane walks items t, t+T, t+2T, ... and loads the
+// next item's schedule record before replaying the current one, so the
+// record's latency hides under the current item's payload loads.
+template <int MAXC, int BATCH, bool NTL, int NTS>
+__global__ __launch_bounds__(kBlock) void k_recover_pipe(v4u* shards, const v4u* __restrict__ parity,
+                                                         const uint8_t* __restrict__ sched, uint32_t total,
+                                                         uint32_t C, FastDiv divC, uint32_t rec_bytes,
+                                                         uint32_t fast_ok, rfec_kplan P)
+{
+    __shared__ uint32_t lplan[RFEC_MAX_LINES];
+    stage_plan(lplan, P);
+    const uint32_t T = gridDim.x * kBlock;
+    uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= total)
+        return;
+    uint32_t g = fdiv(t, divC);
+    v4u r0 = *reinterpret_cast<const v4u*>(sched + (size_t)g * rec_bytes);
+    while (t < total) {
+        const uint32_t j = t - g * divC.d; // chunk column (divC.d = chunks of work per slot)
+        const uint32_t tn = t + T;
+        const uint32_t gn = tn < total ? fdiv(tn, divC) : g;
+        const v4u rn = *reinterpret_cast<const v4u*>(sched + (size_t)gn * rec_bytes);
+        replay<MAXC, BATCH, NTL, NTS>(shards + (size_t)g * P.k * C + j, parity + (size_t)g * P.n_lines * C + j,
+                                 sched + (size_t)g * rec_bytes, r0, C, fast_ok, lplan);
+        t = tn;
+        g = gn;
+        r0 = rn;
     }
 }
 
@@ -594,30 +696,85 @@ inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kB
 
 struct EncLaunch {
     const rfec_kplan* P;
-    uint32_t groups, stride;
+    uint32_t groups, stride, cd; // cd = 16-B chunks of work per slot, ceil(capacity / 16)
     const v4u* s;
     v4u* p;
     EncMeta E;
     hipStream_t stream;
 };
 
-template <int K, int COL, bool NTL, bool NTS, int ITEMS>
+template <int K, int COL, bool NTL, int NTS, int ITEMS>
 hipError_t launch_rows(const EncLaunch& a)
 {
     const uint32_t C = a.stride / 16;
-    const uint32_t total = a.groups * C;
+    const uint32_t total = a.groups * a.cd;
     const uint32_t lanes = (total + ITEMS - 1) / ITEMS;
     hipLaunchKernelGGL((k_encode_rows<K, COL, NTL, NTS, ITEMS>), dim3(a.E.n_meta_blocks + blocks_for(lanes)),
-                       dim3(kBlock), 0, a.stream, a.s, a.p, total, C, make_fastdiv(C), a.E, *a.P);
+                       dim3(kBlock), 0, a.stream, a.s, a.p, total, C, make_fastdiv(a.cd), a.E, *a.P);
     return hipGetLastError();
 }
 
-template <int K, int COL, bool NTL, bool NTS>
+template <int K, int COL, bool NTL, int NTS>
 hipError_t launch_rows_v(const EncLaunch& a, unsigned flags)
 {
     if (flags & RFEC_KFLAG_ITEMS2)
         return launch_rows<K, COL, NTL, NTS, 2>(a);
     return launch_rows<K, COL, NTL, NTS, 1>(a);
+}
+
+struct ReplayArgs {
+    v4u* shards;
+    const v4u* parity;
+    const uint8_t* sched;
+    uint32_t total, C;
+    FastDiv f;
+    uint32_t rec_bytes, fast_ok;
+    hipStream_t stream;
+};
+
+template <int MAXC, int BATCH, bool PIPE, bool NTL, int NTS>
+void launch_replay_t(const ReplayArgs& R, const rfec_kplan& P, dim3 grid)
+{
+    if constexpr (PIPE)
+        hipLaunchKernelGGL((k_recover_pipe<MAXC, BATCH, NTL, NTS>), grid, dim3(kBlock), 0, R.stream, R.shards,
+                           R.parity, R.sched, R.total, R.C, R.f, R.rec_bytes, R.fast_ok, P);
+    else
+        hipLaunchKernelGGL((k_recover_flat<MAXC, BATCH, NTL, NTS>), grid, dim3(kBlock), 0, R.stream, R.shards,
+                           R.parity, R.sched, R.total, R.C, R.f, R.rec_bytes, R.fast_ok, P);
+}
+
+template <int MAXC, int BATCH, bool PIPE>
+void launch_replay(const ReplayArgs& R, bool ntl, int sp, const rfec_kplan& P, dim3 grid)
+{
+    if (!ntl) {
+        launch_replay_t<MAXC, BATCH, PIPE, false, 1>(R, P, grid); // A/B only: NT stores
+        return;
+    }
+    switch (sp) {
+    case 0: launch_replay_t<MAXC, BATCH, PIPE, true, 0>(R, P, grid); break;
+    case 2: launch_replay_t<MAXC, BATCH, PIPE, true, 2>(R, P, grid); break;
+    case 3: launch_replay_t<MAXC, BATCH, PIPE, true, 3>(R, P, grid); break;
+    default: launch_replay_t<MAXC, BATCH, PIPE, true, 1>(R, P, grid); break;
+    }
+}
+
+// flags -> store cache policy of st16<SP>.  Defaults, measured in the
+// encode -> decode alternation bench.py runs (tools/ab_encode.py step mode):
+// parity stores write-through (sc0 sc1), recovered-segment stores
+// non-temporal; a decode that leaves written-back lines behind slows the
+// next write-through encode by ~45%, a non-temporal one does not.
+constexpr int kEncodeStoreDefault = 2;
+constexpr int kRecoverStoreDefault = 1;
+
+int store_policy(unsigned flags, int dflt)
+{
+    if (flags & RFEC_KFLAG_PLAIN_STORES)
+        return 0;
+    if (flags & RFEC_KFLAG_WT_STORES)
+        return (flags & RFEC_KFLAG_WT_NT) ? 3 : 2;
+    if (flags & RFEC_KFLAG_NT_STORES)
+        return 1;
+    return dflt;
 }
 
 bool is_row_layout(const rfec_kplan* P, uint32_t* col_out)
@@ -633,7 +790,7 @@ bool is_row_layout(const rfec_kplan* P, uint32_t* col_out)
     return rows;
 }
 
-template <bool NTL, bool NTS>
+template <bool NTL, int NTS>
 hipError_t launch_encode_t(const EncLaunch& a, unsigned flags)
 {
     const rfec_kplan* P = a.P;
@@ -645,9 +802,9 @@ hipError_t launch_encode_t(const EncLaunch& a, unsigned flags)
             return launch_rows_v<32, 4, NTL, NTS>(a, flags);
     }
     const uint32_t C = a.stride / 16;
-    const uint32_t total = a.groups * C;
+    const uint32_t total = a.groups * a.cd;
     hipLaunchKernelGGL((k_encode<NTL, NTS>), dim3(a.E.n_meta_blocks + blocks_for(total)), dim3(kBlock), 0, a.stream,
-                       a.s, a.p, total, C, make_fastdiv(C), a.E, *P);
+                       a.s, a.p, total, C, make_fastdiv(a.cd), a.E, *P);
     return hipGetLastError();
 }
 
@@ -668,21 +825,21 @@ int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, ui
     E.capacity = capacity;
     uint32_t gpb = kMetaDwords / (5u * P->k);
     gpb = gpb < 1 ? 1 : (gpb > 64 ? 64 : gpb);
+    if (gpb >= 4)
+        gpb &= ~3u; // keeps every block's header slice 16-byte aligned
     E.gpb = gpb;
     E.n_meta_blocks = (flags & RFEC_KFLAG_DIAG_NO_META) ? 0 : (groups + gpb - 1) / gpb;
-    const EncLaunch a = {P, groups, stride, reinterpret_cast<const v4u*>(shards), reinterpret_cast<v4u*>(parity),
+    const uint32_t cd = capacity ? (capacity + 15) / 16 : 1;
+    const EncLaunch a = {P, groups, stride, cd, reinterpret_cast<const v4u*>(shards), reinterpret_cast<v4u*>(parity),
                          E, reinterpret_cast<hipStream_t>(stream)};
-    const bool ntl = !(flags & RFEC_KFLAG_PLAIN_LOADS), nts = (flags & RFEC_KFLAG_NT_STORES) != 0;
-    hipError_t e;
-    if (ntl && nts)
-        e = launch_encode_t<true, true>(a, flags);
-    else if (ntl)
-        e = launch_encode_t<true, false>(a, flags);
-    else if (nts)
-        e = launch_encode_t<false, true>(a, flags);
-    else
-        e = launch_encode_t<false, false>(a, flags);
-    return (int)e;
+    if (flags & RFEC_KFLAG_PLAIN_LOADS) // A/B only
+        return (int)launch_encode_t<false, 1>(a, flags);
+    switch (store_policy(flags, kEncodeStoreDefault)) {
+    case 0: return (int)launch_encode_t<true, 0>(a, flags);
+    case 2: return (int)launch_encode_t<true, 2>(a, flags);
+    case 3: return (int)launch_encode_t<true, 3>(a, flags);
+    default: return (int)launch_encode_t<true, 1>(a, flags);
+    }
 }
 
 int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32_t capacity,
@@ -704,6 +861,7 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
         A.recovered = recovered;
         A.groups = groups;
         A.C = stride / 16;
+        A.Cd = capacity ? (capacity + 15) / 16 : 1;
         A.capacity = capacity;
         const dim3 grid((unsigned)(((uint64_t)groups * kWave + kBlock - 1) / kBlock));
         if (ntl)
@@ -723,10 +881,25 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
     B.sched = reinterpret_cast<uint8_t*>(ws);
     B.groups = groups;
     B.capacity = capacity;
+    // LDS per group: K + NL header records (5 dwords) + NL u16 sizes; block
+    // ranges start on 8-group boundaries so the staged slices are 16-B aligned
     const uint32_t per = 5u * P.k + 6u * P.n_lines;
-    uint32_t gpb = kPeelDwords / per;
-    B.gpb = gpb < 1 ? 1 : (gpb > (uint32_t)kBlock ? (uint32_t)kBlock : gpb);
+    // (at most 64 groups per block: the peel is one serial chain per lane, so
+    // more, smaller blocks give each SIMD more chains to interleave)
+    uint32_t gpb = (kPeelDwords - 8) / per;
+    gpb = gpb > 64u ? 64u : gpb;
+    if (gpb >= 8)
+        gpb &= ~7u;
+    B.gpb = gpb < 1 ? 1 : gpb;
     B.rec_bytes = rfec_sched_record_bytes(P.n_lines);
+    uint64_t seen0 = 0, seen1 = 0;
+    B.disjoint = 1;
+    for (uint32_t l = 0; l < P.n_lines; ++l) {
+        if ((seen0 & M->mask[l][0]) | (seen1 & M->mask[l][1]))
+            B.disjoint = 0;
+        seen0 |= M->mask[l][0];
+        seen1 |= M->mask[l][1];
+    }
     hipLaunchKernelGGL(k_peel_lds, dim3((groups + B.gpb - 1) / B.gpb), dim3(kBlock), 0, st, B, *M);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
@@ -735,28 +908,21 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
     for (uint32_t l = 0; l < P.n_lines; ++l)
         maxc = P.line[l].count > maxc ? P.line[l].count : maxc;
     const uint32_t C = stride / 16;
-    const uint32_t total = groups * C;
+    const uint32_t cd = capacity ? (capacity + 15) / 16 : 1;
+    const uint32_t total = groups * cd;
     const dim3 grid(blocks_for(total));
-    const FastDiv f = make_fastdiv(C);
+    const FastDiv f = make_fastdiv(cd);
     const v4u* pp = reinterpret_cast<const v4u*>(parity);
     v4u* sh = reinterpret_cast<v4u*>(shards);
     const uint8_t* sc = B.sched;
-    if (maxc <= 4) {
-        if (ntl)
-            hipLaunchKernelGGL((k_recover_flat<4, 2, true>), grid, dim3(kBlock), 0, st, sh, pp, sc, total, C, f,
-                               B.rec_bytes, 1u, P);
-        else
-            hipLaunchKernelGGL((k_recover_flat<4, 2, false>), grid, dim3(kBlock), 0, st, sh, pp, sc, total, C, f,
-                               B.rec_bytes, 1u, P);
-    } else {
-        const uint32_t fast = maxc <= 8;
-        if (ntl)
-            hipLaunchKernelGGL((k_recover_flat<8, 1, true>), grid, dim3(kBlock), 0, st, sh, pp, sc, total, C, f,
-                               B.rec_bytes, fast, P);
-        else
-            hipLaunchKernelGGL((k_recover_flat<8, 1, false>), grid, dim3(kBlock), 0, st, sh, pp, sc, total, C, f,
-                               B.rec_bytes, fast, P);
-    }
+    const int nts = store_policy(flags, kRecoverStoreDefault);
+    const ReplayArgs R = {sh, pp, sc, total, C, f, B.rec_bytes, maxc <= 8 ? 1u : 0u, st};
+    if (maxc <= 4 && (flags & RFEC_KFLAG_PIPE_DECODE))
+        launch_replay<4, 2, true>(R, ntl, nts, P, dim3(grid.x < 4096u ? grid.x : 4096u));
+    else if (maxc <= 4)
+        launch_replay<4, 2, false>(R, ntl, nts, P, grid);
+    else
+        launch_replay<8, 1, false>(R, ntl, nts, P, grid);
     return (int)hipGetLastError();
 }
 

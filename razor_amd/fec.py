@@ -30,8 +30,12 @@ RFEC_LAYER_ROWS = 1
 RFEC_LAYER_COLS = 2
 RFEC_TUNE_GENERIC = 1
 RFEC_TUNE_PLAIN_LOADS = 2
-RFEC_TUNE_NT_STORES = 4
+RFEC_TUNE_PLAIN_STORES = 4
 RFEC_TUNE_WAVE_DECODE = 16
+RFEC_TUNE_PIPE_DECODE = 32
+RFEC_TUNE_WT_STORES = 64
+RFEC_TUNE_WT_NT = 128
+RFEC_TUNE_NT_STORES = 512
 RFEC_TUNE_ITEMS2 = 8
 RFEC_TUNE_DIAG_NO_META = 256
 
@@ -65,6 +69,29 @@ class rfec_plan(C.Structure):
     def __repr__(self):
         return (f"rfec_plan(k={self.k}, row={self.row}, col={self.col}, rc={self.rc}, "
                 f"n_lines={self.n_lines}, lines={self.lines()})")
+
+
+class rfec_host_timing(C.Structure):
+    _fields_ = [("gather_us", C.c_double), ("h2d_us", C.c_double), ("kernel_us", C.c_double),
+                ("d2h_us", C.c_double), ("scatter_us", C.c_double), ("total_us", C.c_double)]
+
+
+def seg_dtype(video_size: int) -> np.dtype:
+    """numpy mirror of sim_segment_t (sim_proto.h:80-99)."""
+    size = ((34 + video_size + 3) // 4) * 4
+    return np.dtype({"names": ["packet_id", "fid", "timestamp", "index", "total", "ftype", "payload_type",
+                               "fec_id", "data_size", "data"],
+                     "formats": ["<u4", "<u4", "<u4", "<u2", "<u2", "u1", "u1", "<u2", "<u2", ("u1", video_size)],
+                     "offsets": [0, 4, 8, 12, 14, 16, 17, 20, 32, 34], "itemsize": size})
+
+
+def fec_dtype(video_size: int) -> np.dtype:
+    """numpy mirror of sim_fec_t (sim_proto.h:157-174)."""
+    size = ((42 + video_size + 3) // 4) * 4
+    return np.dtype({"names": ["fec_id", "row", "col", "index", "count", "base_id", "meta", "fec_data_size",
+                               "fec_data"],
+                     "formats": ["<u2", "u1", "u1", "u1", "<u2", "<u4", HDR_DTYPE, "<u2", ("u1", video_size)],
+                     "offsets": [0, 2, 3, 4, 6, 8, 20, 40, 42], "itemsize": size})
 
 
 def sim_types(video_size: int):
@@ -110,6 +137,7 @@ _SIGS = {
     "rfec_set_tuning": (None, [C.c_uint]),
     "rfec_get_tuning": (C.c_uint, []),
     "rfec_last_error": (C.c_char_p, []),
+    "rfec_host_encode_groups": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, _P, _P, C.c_uint16, _P]),
     "rfec_probe_read": (C.c_int, [_P, C.c_size_t, _P, C.c_uint, _P]),
     "rfec_probe_copy": (C.c_int, [_P, _P, C.c_size_t, C.c_uint, _P]),
     "rfec_probe_write": (C.c_int, [_P, C.c_size_t, C.c_uint, _P]),
@@ -183,6 +211,17 @@ class Native:
         self._check(self.lib.rfec_recover_batch(C.byref(as_plan(plan)), groups, stride, capacity, shards, hdr, present,
                                                 parity, meta, fec_size, parity_present, recovered, workspace,
                                                 stream), "rfec_recover_batch")
+
+    def host_encode_groups(self, plan, groups, seg_ptrs, fec_ptrs, fec_id0=1):
+        """seg_ptrs / fec_ptrs: host addresses (uint64 numpy arrays) of the
+        sim_segment_t / sim_fec_t structs; returns the per-stage timing (us)."""
+        t = rfec_host_timing()
+        seg_ptrs = np.ascontiguousarray(seg_ptrs, np.uint64)
+        fec_ptrs = np.ascontiguousarray(fec_ptrs, np.uint64)
+        self._check(self.lib.rfec_host_encode_groups(C.byref(as_plan(plan)), groups, seg_ptrs.ctypes.data,
+                                                     fec_ptrs.ctypes.data, fec_id0, C.addressof(t)),
+                    "rfec_host_encode_groups")
+        return {f: getattr(t, f) for f, _ in rfec_host_timing._fields_}
 
     def zero_tails(self, groups, k, stride, shards, hdr, stream=None):
         self._check(self.lib.rfec_zero_tails(groups, k, stride, shards, hdr, stream), "rfec_zero_tails")

@@ -15,7 +15,8 @@ pytestmark = pytest.mark.gpu
 
 MANIFEST = po.manifest()
 CASES = {c["name"]: c for c in MANIFEST["cases"]}
-TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "nt_stores": 4, "items2": 8, "wave_decode": 16,
+TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "plain_stores": 4, "items2": 8, "wave_decode": 16,
+           "pipe_decode": 32, "wt_stores": 64, "wt_nt_stores": 192, "nt_stores": 512,
            "generic_plain": 3}
 
 
@@ -45,7 +46,8 @@ def test_rows_fixture_gpu(gpu, oracle1000, oracle1200, name, tuning):
     pc.check_rows_case(gpu(tuning=TUNINGS[tuning]), o, c, capacity=max(c["S"], 1000))
 
 
-@pytest.mark.parametrize("tuning", ["default", "wave_decode", "plain_loads"])
+@pytest.mark.parametrize("tuning", ["default", "wave_decode", "pipe_decode", "plain_loads", "wt_stores",
+                                    "plain_stores", "nt_stores"])
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures"])
 def test_erasure_fixture_gpu(gpu, oracle1000, name, tuning):
     pc.check_erasure_case(gpu(tuning=TUNINGS[tuning]), oracle1000, CASES[name])
@@ -131,7 +133,7 @@ def test_full_size_k10_roundtrip(product, oracle1200, layers):
     plan = lib.plan_from_fraction(k, 80, layers)
     shards, hdr, d_hdr = _device_batch(G, k, S, 1234)
     par, meta, fs, st = _run_encode(lib, plan, G, S, shards, d_hdr)
-    for tuning in (1, 2, 4, 8, 3):
+    for tuning in (1, 2, 4, 8, 3, 64, 192, 512):
         par2, meta2, fs2, st2 = _run_encode(lib, plan, G, S, shards, d_hdr, tuning=tuning)
         assert torch.equal(par, par2) and torch.equal(meta, meta2) and torch.equal(fs, fs2), tuning
         del par2, meta2, fs2, st2
@@ -251,3 +253,35 @@ def test_capacity_status(product):
     exp[1, 1] = -1
     assert np.array_equal(st.cpu().numpy(), exp)
     assert fs.cpu().numpy()[1, 1] == 60
+
+
+def test_host_encode_groups(product1200, oracle1200):
+    """rfec_host_encode_groups (host AoS in, host sim_fec_t out) vs the oracle's
+    reference-shaped AoS path (flex_fec_generate per line + sender stamps)."""
+    from razor_amd.fec import fec_dtype, seg_dtype
+
+    lib, o = product1200, oracle1200
+    G, k, S = 37, 10, 1200
+    shards, hdr = o.fill_groups(202, G, k, S, ragged=True)
+    plan = o.plan_from_fraction(k, 80, 3)  # full 3x4 plan: 7 parities
+    segs = np.zeros(G * k, seg_dtype(1200))
+    h = hdr.reshape(-1)
+    for a, b in (("seq", "packet_id"), ("fid", "fid"), ("ts", "timestamp"), ("index", "index"),
+                 ("total", "total"), ("ftype", "ftype"), ("payload_type", "payload_type"), ("size", "data_size")):
+        segs[b] = h[a]
+    segs["data"] = shards.reshape(G * k, S)
+    n = plan.n_lines
+    fecs = np.zeros(G * n, fec_dtype(1200))
+    sp = segs.ctypes.data + np.arange(G * k, dtype=np.uint64) * segs.dtype.itemsize
+    fp = fecs.ctypes.data + np.arange(G * n, dtype=np.uint64) * fecs.dtype.itemsize
+    t = lib.host_encode_groups(plan, G, sp, fp, fec_id0=1)
+    assert t["total_us"] > 0
+    nref, ref = o.encode_aos(plan, G, o.to_aos(shards, hdr))
+    assert nref == G * n
+    ref = ref.view(fec_dtype(1200)).reshape(-1)
+    for f in ("fec_id", "row", "col", "index", "count", "base_id", "fec_data_size"):
+        assert np.array_equal(fecs[f], ref[f]), f
+    assert np.array_equal(fecs["meta"], ref["meta"])
+    for j in range(G * n):
+        L = int(ref["fec_data_size"][j])
+        assert np.array_equal(fecs["fec_data"][j, :L], ref["fec_data"][j, :L])

@@ -7,6 +7,8 @@
 #         tests = smoke + pytest -m gpu
 #         ab    = pytest -m gpu + tools/ab_encode.py
 #         bench = bench + rocprofv3 stats
+#         pmc   = FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py)
+#         all   = pytest + ab + pmc + bench + rocprofv3 stats
 set -u
 TAG=${1:-run}; MODE=${2:-full}; shift 2 || true
 OUT=gpurun_out/$TAG
@@ -28,12 +30,16 @@ case "$MODE" in
   full|tests)
     step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
     step pytest_gpu 900 python -m pytest tests -m gpu -x -q -rs ;;
-  ab)
+  ab|all)
     step pytest_gpu 900 python -m pytest tests -m gpu -x -q -rs
     step ab 600 python tools/ab_encode.py --out "$OUT/ab.json" ;;
 esac
 case "$MODE" in
-  full|bench)
+  pmc|all)
+    step pmc 900 python tools/pmc_traffic.py --out "$OUT/traffic.json" ;;
+esac
+case "$MODE" in
+  full|bench|all)
     step bench 600 python bench.py "$@"
     step rocprof_stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --no-cpu "$@" ;;
 esac
