@@ -263,11 +263,13 @@ typedef struct {
     uint8_t* host;   /* host view */
     uint8_t* dev;    /* device view of the same bytes */
     size_t bytes;
-    /* rfec_host_encode_groups: pinned host staging + its HBM mirror */
+    /* rfec_host_encode_groups: two pinned host staging slots + their HBM
+     * mirrors, one stream and four events per slot */
     uint8_t* bh;
     uint8_t* bd;
     size_t b_bytes;
-    hipEvent_t ev[4];
+    hipStream_t bstream[2];
+    hipEvent_t ev[2][4];
     int have_ev;
 } di_ctx;
 
@@ -314,8 +316,11 @@ static void di_free(void* p)
         (void)hipHostFree(c->bh);
     if (c->bd)
         (void)hipFree(c->bd);
-    for (int i = 0; c->have_ev && i < 4; ++i)
-        (void)hipEventDestroy(c->ev[i]);
+    for (int s = 0; c->have_ev && s < 2; ++s) {
+        for (int i = 0; i < 4; ++i)
+            (void)hipEventDestroy(c->ev[s][i]);
+        (void)hipStreamDestroy(c->bstream[s]);
+    }
     if (c->stream)
         (void)hipStreamDestroy(c->stream);
     free(c);
@@ -557,16 +562,20 @@ static hb_layout hb_offsets(uint32_t G, uint32_t k, uint32_t n)
     return L;
 }
 
-static int hb_reserve(di_ctx* c, size_t bytes)
+static int hb_reserve(di_ctx* c, size_t slot_bytes)
 {
     hipError_t e;
     if (!c->have_ev) {
-        for (int i = 0; i < 4; ++i)
-            if ((e = hipEventCreate(&c->ev[i])) != hipSuccess)
-                return set_err(RFEC_EDEVICE, "event create", e);
+        for (int s = 0; s < 2; ++s) {
+            if ((e = hipStreamCreateWithFlags(&c->bstream[s], hipStreamNonBlocking)) != hipSuccess)
+                return set_err(RFEC_EDEVICE, "stream create", e);
+            for (int i = 0; i < 4; ++i)
+                if ((e = hipEventCreate(&c->ev[s][i])) != hipSuccess)
+                    return set_err(RFEC_EDEVICE, "event create", e);
+        }
         c->have_ev = 1;
     }
-    if (c->b_bytes >= bytes)
+    if (c->b_bytes >= 2 * slot_bytes)
         return RFEC_OK;
     if (c->bh)
         (void)hipHostFree(c->bh);
@@ -575,11 +584,11 @@ static int hb_reserve(di_ctx* c, size_t bytes)
     c->bh = NULL;
     c->bd = NULL;
     c->b_bytes = 0;
-    if ((e = hipHostMalloc((void**)&c->bh, bytes, hipHostMallocDefault)) != hipSuccess)
+    if ((e = hipHostMalloc((void**)&c->bh, 2 * slot_bytes, hipHostMallocDefault)) != hipSuccess)
         return set_err(RFEC_ENOMEM, "pinned staging", e);
-    if ((e = hipMalloc((void**)&c->bd, bytes)) != hipSuccess)
+    if ((e = hipMalloc((void**)&c->bd, 2 * slot_bytes)) != hipSuccess)
         return set_err(RFEC_ENOMEM, "device staging", e);
-    c->b_bytes = bytes;
+    c->b_bytes = 2 * slot_bytes;
     return RFEC_OK;
 }
 
@@ -590,6 +599,114 @@ static uint16_t fec_id_at(uint16_t id0, uint32_t g)
     return (uint16_t)((base + g) % 65535u + 1u);
 }
 
+/* ---- a tiny fork/join helper for the host-side gather / scatter ---------- */
+typedef void (*pf_fn)(void* arg, size_t lo, size_t hi);
+typedef struct {
+    pf_fn fn;
+    void* arg;
+    size_t lo, hi;
+} pf_job;
+
+static void* pf_run(void* p)
+{
+    pf_job* j = (pf_job*)p;
+    j->fn(j->arg, j->lo, j->hi);
+    return NULL;
+}
+
+static int host_threads(void)
+{
+    const char* v = getenv("RFEC_HOST_THREADS");
+    int t = v ? atoi(v) : 8;
+    return t < 1 ? 1 : (t > 64 ? 64 : t);
+}
+
+static void parallel_for(size_t n, int threads, pf_fn fn, void* arg)
+{
+    if (threads <= 1 || n < 256) {
+        fn(arg, 0, n);
+        return;
+    }
+    pthread_t tid[64];
+    pf_job job[64];
+    int started = 0;
+    for (int t = 0; t < threads; ++t) {
+        job[t].fn = fn;
+        job[t].arg = arg;
+        job[t].lo = n * t / threads;
+        job[t].hi = n * (t + 1) / threads;
+        if (t == threads - 1 || pthread_create(&tid[t], NULL, pf_run, &job[t]) != 0)
+            break; /* the last share (or any share a thread could not take) runs here */
+        started++;
+    }
+    for (int t = started; t < threads; ++t)
+        fn(arg, job[t].lo, job[t].hi);
+    for (int t = 0; t < started; ++t)
+        pthread_join(tid[t], NULL);
+}
+
+typedef struct {
+    const rfec_plan* plan;
+    sim_segment_t* const* segs; /* first segment of the chunk */
+    sim_fec_t* const* fecs;     /* first parity of the chunk */
+    uint8_t* slot;              /* host staging slot */
+    hb_layout L;
+    uint32_t g0;                /* global index of the chunk's first group */
+    uint16_t fec_id0;
+} hb_chunk;
+
+/* gather: AoS segments (payload at offset 34, not 16-B aligned) -> SoA slots */
+static void hb_gather(void* arg, size_t lo, size_t hi)
+{
+    const hb_chunk* h = (const hb_chunk*)arg;
+    rfec_hdr* hh = (rfec_hdr*)(h->slot + h->L.hdr);
+    for (size_t s = lo; s < hi; ++s) {
+        const sim_segment_t* seg = h->segs[s];
+        stage_payload(h->slot + h->L.shards + s * DI_STRIDE, seg->data, seg->data_size);
+        seg_to_hdr(seg, &hh[s]);
+    }
+}
+
+/* scatter into the caller's sim_fec_t, stamped as flex_fec_sender_update does */
+static void hb_scatter(void* arg, size_t lo, size_t hi)
+{
+    const hb_chunk* h = (const hb_chunk*)arg;
+    const rfec_plan* plan = h->plan;
+    const uint32_t k = plan->k, n = plan->n_lines;
+    const rfec_hdr* hh = (const rfec_hdr*)(h->slot + h->L.hdr);
+    const rfec_hdr* mh = (const rfec_hdr*)(h->slot + h->L.meta);
+    const uint16_t* fs = (const uint16_t*)(h->slot + h->L.fsize);
+    const int8_t* st = (const int8_t*)(h->slot + h->L.status);
+    for (size_t g = lo; g < hi; ++g) {
+        uint32_t base = hh[g * k].seq;
+        for (uint32_t i = 1; i < k; ++i)
+            base = hh[g * k + i].seq < base ? hh[g * k + i].seq : base;
+        for (uint32_t l = 0; l < n; ++l) {
+            const size_t o = g * n + l;
+            sim_fec_t* f = h->fecs[o];
+            f->fec_id = fec_id_at(h->fec_id0, h->g0 + (uint32_t)g);
+            f->base_id = base;
+            f->row = plan->row;
+            f->col = plan->col;
+            f->index = plan->line[l].index;
+            f->count = plan->k;
+            if (st[o] != 0) {
+                f->fec_data_size = 0xFFFF;
+                continue;
+            }
+            memcpy(&f->fec_meta, &mh[o], sizeof(rfec_hdr));
+            f->fec_data_size = fs[o];
+            memcpy(f->fec_data, h->slot + h->L.parity + o * DI_STRIDE, fs[o]);
+        }
+    }
+}
+
+/*
+ * Chunked and double-buffered: while the GPU copies / encodes / copies back
+ * chunk c on slot c%2's stream, the CPU threads scatter chunk c-1's parities
+ * and gather chunk c+1 into the other slot, so the wall time approaches the
+ * slowest stage (the PCIe copies) instead of the sum of all five.
+ */
 int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,
                             sim_fec_t* const* fecs, uint16_t fec_id0, rfec_host_timing* timing)
 {
@@ -606,74 +723,87 @@ int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
     if (!c)
         return RFEC_EDEVICE;
     const uint32_t k = plan->k, n = plan->n_lines;
-    const hb_layout L = hb_offsets(groups, k, n);
+    uint32_t chunk = (groups + 7) / 8;
+    chunk = chunk < 2048 ? 2048 : chunk;
+    chunk = chunk > groups ? groups : chunk;
+    const uint32_t nch = (groups + chunk - 1) / chunk;
+    const hb_layout L = hb_offsets(chunk, k, n);
     if ((rc = hb_reserve(c, L.total)))
         return rc;
+    const int threads = host_threads();
+    double gather_us = 0, scatter_us = 0, h2d_us = 0, kernel_us = 0, d2h_us = 0;
+    hb_chunk job[2];
     const double t0 = now_us();
-    /* gather: AoS segments (payload at offset 34, not 16-B aligned) -> SoA slots */
-    rfec_hdr* hh = (rfec_hdr*)(c->bh + L.hdr);
-    for (size_t s = 0; s < (size_t)groups * k; ++s) {
-        const sim_segment_t* seg = segs[s];
-        stage_payload(c->bh + L.shards + s * DI_STRIDE, seg->data, seg->data_size);
-        seg_to_hdr(seg, &hh[s]);
-    }
-    const double t1 = now_us();
-    hipError_t e;
-    if ((e = hipEventRecord(c->ev[0], c->stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(c->bd, c->bh, L.in_bytes, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
-        (e = hipEventRecord(c->ev[1], c->stream)) != hipSuccess)
-        return set_err(RFEC_EDEVICE, "H2D", e);
-    const int ke = rfec_launch_encode(plan, groups, DI_STRIDE, SIM_VIDEO_SIZE, c->bd + L.shards,
-                                      (const rfec_hdr*)(c->bd + L.hdr), c->bd + L.parity,
-                                      (rfec_hdr*)(c->bd + L.meta), (uint16_t*)(c->bd + L.fsize),
-                                      (int8_t*)(c->bd + L.status), c->stream, g_tuning);
-    if (ke)
-        return set_err(RFEC_EDEVICE, "encode launch", ke);
-    if ((e = hipEventRecord(c->ev[2], c->stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(c->bh + L.parity, c->bd + L.parity, L.total - L.parity, hipMemcpyDeviceToHost,
-                            c->stream)) != hipSuccess ||
-        (e = hipEventRecord(c->ev[3], c->stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
-        return set_err(RFEC_EDEVICE, "D2H", e);
-    const double t2 = now_us();
-    /* scatter into the caller's sim_fec_t, stamped as flex_fec_sender_update does */
-    const rfec_hdr* mh = (const rfec_hdr*)(c->bh + L.meta);
-    const uint16_t* fs = (const uint16_t*)(c->bh + L.fsize);
-    const int8_t* st = (const int8_t*)(c->bh + L.status);
-    for (uint32_t g = 0; g < groups; ++g) {
-        uint32_t base = hh[(size_t)g * k].seq;
-        for (uint32_t i = 1; i < k; ++i)
-            base = hh[(size_t)g * k + i].seq < base ? hh[(size_t)g * k + i].seq : base;
-        for (uint32_t l = 0; l < n; ++l) {
-            const size_t o = (size_t)g * n + l;
-            sim_fec_t* f = fecs[o];
-            f->fec_id = fec_id_at(fec_id0, g);
-            f->base_id = base;
-            f->row = plan->row;
-            f->col = plan->col;
-            f->index = plan->line[l].index;
-            f->count = plan->k;
-            if (st[o] != 0) {
-                f->fec_data_size = 0xFFFF;
-                continue;
-            }
-            memcpy(&f->fec_meta, &mh[o], sizeof(rfec_hdr));
-            f->fec_data_size = fs[o];
-            memcpy(f->fec_data, c->bh + L.parity + o * DI_STRIDE, fs[o]);
+    for (uint32_t it = 0; it < nch + 2; ++it) {
+        if (it >= 2) { /* retire chunk it-2 */
+            const uint32_t s = (it - 2) & 1;
+            hipError_t e = hipEventSynchronize(c->ev[s][3]);
+            if (e != hipSuccess)
+                return set_err(RFEC_EDEVICE, "D2H wait", e);
+            float a = 0, b = 0, d = 0;
+            (void)hipEventElapsedTime(&a, c->ev[s][0], c->ev[s][1]);
+            (void)hipEventElapsedTime(&b, c->ev[s][1], c->ev[s][2]);
+            (void)hipEventElapsedTime(&d, c->ev[s][2], c->ev[s][3]);
+            h2d_us += a * 1e3;
+            kernel_us += b * 1e3;
+            d2h_us += d * 1e3;
+            const double ts = now_us();
+            const uint32_t ng = (it - 2 == nch - 1) ? groups - (it - 2) * chunk : chunk;
+            parallel_for(ng, threads, hb_scatter, &job[s]);
+            scatter_us += now_us() - ts;
+        }
+        if (it < nch) { /* stage chunk it */
+            const uint32_t s = it & 1;
+            const uint32_t g0 = it * chunk;
+            const uint32_t ng = (it == nch - 1) ? groups - g0 : chunk;
+            hb_chunk* h = &job[s];
+            h->plan = plan;
+            h->segs = segs + (size_t)g0 * k;
+            h->fecs = fecs + (size_t)g0 * n;
+            h->slot = c->bh + (size_t)s * L.total;
+            h->L = L;
+            h->g0 = g0;
+            h->fec_id0 = fec_id0;
+            const double tg = now_us();
+            parallel_for((size_t)ng * k, threads, hb_gather, h);
+            gather_us += now_us() - tg;
+            uint8_t* dv = c->bd + (size_t)s * L.total;
+            hipStream_t st = c->bstream[s];
+            hipError_t e;
+            /* the slot holds `chunk` groups; a short last chunk copies its own extent */
+            const hb_layout Ln = hb_offsets(ng, k, n);
+            if ((e = hipEventRecord(c->ev[s][0], st)) != hipSuccess ||
+                (e = hipMemcpyAsync(dv + L.shards, h->slot + L.shards, Ln.hdr, hipMemcpyHostToDevice, st)) !=
+                    hipSuccess ||
+                (e = hipMemcpyAsync(dv + L.hdr, h->slot + L.hdr, (size_t)ng * k * sizeof(rfec_hdr),
+                                    hipMemcpyHostToDevice, st)) != hipSuccess ||
+                (e = hipEventRecord(c->ev[s][1], st)) != hipSuccess)
+                return set_err(RFEC_EDEVICE, "H2D", e);
+            const int ke = rfec_launch_encode(plan, ng, DI_STRIDE, SIM_VIDEO_SIZE, dv + L.shards,
+                                              (const rfec_hdr*)(dv + L.hdr), dv + L.parity, (rfec_hdr*)(dv + L.meta),
+                                              (uint16_t*)(dv + L.fsize), (int8_t*)(dv + L.status), st, g_tuning);
+            if (ke)
+                return set_err(RFEC_EDEVICE, "encode launch", ke);
+            if ((e = hipEventRecord(c->ev[s][2], st)) != hipSuccess ||
+                (e = hipMemcpyAsync(h->slot + L.parity, dv + L.parity, (size_t)ng * n * DI_STRIDE,
+                                    hipMemcpyDeviceToHost, st)) != hipSuccess ||
+                (e = hipMemcpyAsync(h->slot + L.meta, dv + L.meta, (size_t)ng * n * sizeof(rfec_hdr),
+                                    hipMemcpyDeviceToHost, st)) != hipSuccess ||
+                (e = hipMemcpyAsync(h->slot + L.fsize, dv + L.fsize, (size_t)ng * n * sizeof(uint16_t),
+                                    hipMemcpyDeviceToHost, st)) != hipSuccess ||
+                (e = hipMemcpyAsync(h->slot + L.status, dv + L.status, (size_t)ng * n, hipMemcpyDeviceToHost,
+                                    st)) != hipSuccess ||
+                (e = hipEventRecord(c->ev[s][3], st)) != hipSuccess)
+                return set_err(RFEC_EDEVICE, "D2H", e);
         }
     }
-    const double t3 = now_us();
     if (timing) {
-        float a = 0, b = 0, d = 0;
-        (void)hipEventElapsedTime(&a, c->ev[0], c->ev[1]);
-        (void)hipEventElapsedTime(&b, c->ev[1], c->ev[2]);
-        (void)hipEventElapsedTime(&d, c->ev[2], c->ev[3]);
-        timing->gather_us = t1 - t0;
-        timing->h2d_us = a * 1e3;
-        timing->kernel_us = b * 1e3;
-        timing->d2h_us = d * 1e3;
-        timing->scatter_us = t3 - t2;
-        timing->total_us = t3 - t0;
+        timing->gather_us = gather_us;
+        timing->h2d_us = h2d_us;
+        timing->kernel_us = kernel_us;
+        timing->d2h_us = d2h_us;
+        timing->scatter_us = scatter_us;
+        timing->total_us = now_us() - t0;
     }
     return RFEC_OK;
 }

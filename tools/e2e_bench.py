@@ -64,7 +64,8 @@ def main():
     f = fecs.reshape(G, n)[idx]
     ok = bool(np.array_equal(f["fec_data"], par) and np.array_equal(f["meta"], meta)
               and np.array_equal(f["fec_data_size"], fs)
-              and np.all(f["fec_id"] == (idx[:, None] + 1)) and np.all(f["base_id"] == hdr["seq"][:, :1]))
+              # fec_id runs 1, 2, ... and wraps past 65535 to 1 (flex_fec_sender.c:241-243)
+              and np.all(f["fec_id"] == (idx[:, None] % 65535 + 1)) and np.all(f["base_id"] == hdr["seq"][:, :1]))
     enc_bytes = G * (k + n) * S
     res = {"groups": G, "k": k, "r": n, "payload": S, "reps": args.reps, "median_us": med,
            "enc_algorithmic_bytes": enc_bytes,
