@@ -215,16 +215,16 @@ def reps_str(d):
     return f"{d['reps']} passes ({d['seconds']:.1f} s)"
 
 
-def load_traffic(workload_name):
-    """HBM bytes per encode launch from the committed rocprofv3 PMC summary
-    (tools/pmc_traffic.py), or None."""
+def load_traffic(workload_name, kind):
+    """HBM bytes per encode / decode launch from the committed rocprofv3 PMC
+    summary (tools/pmc_traffic.py), or None."""
     p = ROOT / "profiles" / "traffic.json"
     if not p.exists():
         return None
     try:
         d = json.loads(p.read_text())
         e = d.get(workload_name)
-        return None if e is None else e.get("encode_hbm_bytes_per_launch")
+        return None if e is None else e.get(f"{kind}_hbm_bytes_per_launch")
     except (ValueError, OSError):
         return None
 
@@ -321,7 +321,7 @@ def main():
     if rank == 0:
         ceiling = copy_ceiling(device)
         workload_name = f"k{args.k}_r{w.n}_S{args.payload}_G{w.G}"
-        traffic = load_traffic(workload_name)
+        traffic = load_traffic(workload_name, "encode")
         res = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -350,7 +350,8 @@ def main():
             "decode_gibps": round(w.dec_bytes / dec_mean / 2**30, 2),
             "decode_roofline": {"achieved": round(w.dec_bytes / dec_mean / 1e9, 1), "frac":
                                 round(w.dec_bytes / dec_mean / 1e9 / HBM_PEAK_GBPS, 4),
-                                "launch_us": round(dec_mean * 1e6, 2), "kernels": "k_peel + k_recover"},
+                                "launch_us": round(dec_mean * 1e6, 2), "traffic": load_traffic(workload_name, "decode"),
+                                "kernels": "k_decode_disjoint (peel headers + payload, one launch)"},
             "copy_ceiling_GBps": round(ceiling, 1),
             "verified": verified,
             "tuning": args.tuning,

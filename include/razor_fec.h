@@ -177,6 +177,8 @@ int rfec_encode_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, u
  *                    (one peeling-schedule record per group)
  * A line recovers its single missing member only under the conditions of
  * flex_recover_row/col and flex_fec_recover (sizes within fec_data_size).
+ * `recovered` is authoritative: an erased slot whose bit stays clear holds
+ * unspecified bytes afterwards (the fused decode may have written it).
  */
 size_t rfec_recover_workspace_size(const rfec_plan* plan, uint32_t groups);
 int rfec_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
@@ -221,6 +223,8 @@ int rfec_zero_tails(uint32_t groups, uint32_t k, uint32_t stride, uint8_t* shard
 #define RFEC_TUNE_WT_STORES 64u    /* write-through (sc0 sc1) parity / recovered stores */
 #define RFEC_TUNE_WT_NT 128u       /* with RFEC_TUNE_WT_STORES: sc0 sc1 nt */
 #define RFEC_TUNE_NT_STORES 512u   /* non-temporal parity / recovered stores */
+#define RFEC_TUNE_DIAG_CONST_SCHED 1024u /* DIAGNOSTIC ONLY: replay group 0's schedule everywhere */
+#define RFEC_TUNE_TWO_KERNEL_DECODE 4096u /* peel + replay even for disjoint plans (default there: fused) */
 /* (defaults: parity stores write-through, recovered stores non-temporal) */
 #define RFEC_TUNE_DIAG_NO_META 256u /* DIAGNOSTIC ONLY: skip fec_meta (wrong output) */
 void rfec_set_tuning(unsigned flags);

@@ -730,6 +730,14 @@ int main(int argc, char** argv)
     case_erasures("k25_random", 14, 25, 256, 1, 80, 0, PAT_RANDOM, 8, 400, 0.2);
     case_erasures("k64_random", 15, 64, 128, 1, 120, 0, PAT_RANDOM, 12, 300, 0.15);
     case_erasures("k100_random", 16, 100, 64, 1, 255, 0, PAT_RANDOM, 16, 200, 0.1);
+    /* plans whose lines are pairwise disjoint: strip mode (k < 6 or pf < 10)
+     * and row parities only, the latter also replayed against a rows-only plan */
+    case_erasures("k5_strip_le3", 17, 5, 1000, 1, 80, 0, PAT_EXHAUSTIVE, 3, 0, 0.0);
+    case_erasures("k5_strip_pf200_le3", 18, 5, 1000, 1, 200, 0, PAT_EXHAUSTIVE, 3, 0, 0.0);
+    case_erasures("k40_strip_random", 19, 40, 256, 1, 8, 0, PAT_RANDOM, 4, 200, 0.1);
+    case_erasures("k10_rows_ragged_le4", 13, 10, 1000, 1, 80, 1, PAT_EXHAUSTIVE, 4, 0, 0.0);
+    case_erasures("k16_rows_random", 20, 16, 512, 1, 80, 1, PAT_RANDOM, 8, 300, 0.2);
+    case_erasures("k24_rows_random", 21, 24, 512, 1, 80, 1, PAT_RANDOM, 8, 300, 0.2);
 
     fprintf(g_manifest, "\n]}\n");
     fclose(g_manifest);

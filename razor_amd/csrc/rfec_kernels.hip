@@ -428,12 +428,15 @@ struct PeelArgs {
     uint32_t groups, capacity, gpb, rec_bytes, disjoint;
 };
 
-__global__ __launch_bounds__(kBlock) void k_peel_lds(PeelArgs A, rfec_kmask M)
+// One peel block: groups [blk*gpb, ...).  With WRITE_SCHED false (fused
+// decode of disjoint plans) only the recovered headers and masks are written.
+template <bool WRITE_SCHED, int LDSD>
+__device__ void peel_block(const PeelArgs& A, const rfec_kmask& M, uint32_t blk)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kPeelDwords];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[LDSD];
     const rfec_kplan& P = M.plan;
     const uint32_t K = P.k, NL = P.n_lines;
-    const uint32_t g0 = blockIdx.x * A.gpb;
+    const uint32_t g0 = blk * A.gpb;
     const uint32_t ng = min(A.gpb, A.groups - g0);
     const uint32_t g = g0 + threadIdx.x;
     // this lane's masks first, so their latency overlaps the staging below
@@ -508,8 +511,10 @@ __global__ __launch_bounds__(kBlock) void k_peel_lds(PeelArgs A, rfec_kmask M)
             ht[0] = r0, ht[1] = r1, ht[2] = r2, ht[3] = r3, ht[4] = r4;
             uint32_t* gh = reinterpret_cast<uint32_t*>(A.hdr + (size_t)g * K + t);
             gh[0] = r0, gh[1] = r1, gh[2] = r2, gh[3] = r3, gh[4] = r4;
-            rec[2 + 2 * n] = (uint8_t)l;
-            rec[3 + 2 * n] = (uint8_t)t;
+            if (WRITE_SCHED) {
+                rec[2 + 2 * n] = (uint8_t)l;
+                rec[3 + 2 * n] = (uint8_t)t;
+            }
             ++n;
             if (reads_recovered)
                 single = 0;
@@ -523,10 +528,17 @@ __global__ __launch_bounds__(kBlock) void k_peel_lds(PeelArgs A, rfec_kmask M)
             progress = true;
         }
     }
-    rec[0] = (uint8_t)n;
-    rec[1] = (uint8_t)single;
+    if (WRITE_SCHED) {
+        rec[0] = (uint8_t)n;
+        rec[1] = (uint8_t)single;
+    }
     A.recovered[2 * g] = rec0;
     A.recovered[2 * g + 1] = rec1;
+}
+
+__global__ __launch_bounds__(kBlock) void k_peel_lds(PeelArgs A, rfec_kmask M)
+{
+    peel_block<true, kPeelDwords>(A, M, blockIdx.x);
 }
 
 __device__ __forceinline__ uint32_t rec_byte(const v4u& r, uint32_t b)
@@ -614,10 +626,12 @@ __global__ __launch_bounds__(kBlock) void k_recover_flat(v4u* shards, const v4u*
         return;
     const uint32_t g = fdiv(t, divC);
     const uint32_t j = t - g * divC.d; // chunk column (divC.d = chunks of work per slot)
-    const uint8_t* rec = sched + (size_t)g * rec_bytes;
+    // fast_ok bit 1 (RFEC_TUNE_DIAG_CONST_SCHED, timing only): every group
+    // replays group 0's record, an L2-hot load instead of a dependent HBM one
+    const uint8_t* rec = sched + (size_t)((fast_ok & 2u) ? 0u : g) * rec_bytes;
     const v4u r0 = *reinterpret_cast<const v4u*>(rec);
     replay<MAXC, BATCH, NTL, NTS>(shards + (size_t)g * P.k * C + j, parity + (size_t)g * P.n_lines * C + j, rec, r0, C,
-                             fast_ok, lplan);
+                             fast_ok & 1u, lplan);
 }
 
 // Grid-stride form: each lane walks items t, t+T, t+2T, ... and loads the
@@ -647,6 +661,92 @@ __global__ __launch_bounds__(kBlock) void k_recover_pipe(v4u* shards, const v4u*
         t = tn;
         g = gn;
         r0 = rn;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Recover, fused form for plans whose lines are pairwise disjoint (the row
+// layer alone, strip mode).  No recovery there can complete another line, so
+// which lines fire follows from the received masks alone and no schedule has
+// to travel between kernels.  The first n_hdr blocks do the peel's header
+// work (size checks, recovered headers, the recovered mask); every other lane
+// is one (group, 16-B chunk column) that XORs each line with exactly one
+// missing member and its parity received into that member's slot.  A line the
+// header checks reject is still written, into an erased slot whose recovered
+// bit stays clear (rfec_recover_batch documents such slots as unspecified).
+// ---------------------------------------------------------------------------
+constexpr int kFusedPeelDwords = 4096; // 16 KiB: the payload blocks carry this allocation too
+
+__device__ __forceinline__ bool has_bit(uint64_t h0, uint64_t h1, uint32_t i)
+{
+    return ((i < 64 ? h0 >> i : h1 >> (i - 64)) & 1ull) != 0;
+}
+
+template <int MAXC, bool NTL, int NTS>
+__global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v4u* __restrict__ parity,
+                                                            uint32_t total, uint32_t C, FastDiv divC,
+                                                            uint32_t n_hdr_blocks, PeelArgs A, rfec_kmask M)
+{
+    if (blockIdx.x < n_hdr_blocks) {
+        peel_block<false, kFusedPeelDwords>(A, M, blockIdx.x);
+        return;
+    }
+    __shared__ uint32_t lplan[RFEC_MAX_LINES];
+    const rfec_kplan& P = M.plan;
+    stage_plan(lplan, P);
+    const uint32_t t = (blockIdx.x - n_hdr_blocks) * kBlock + threadIdx.x;
+    if (t >= total)
+        return;
+    const uint32_t g = fdiv(t, divC);
+    const uint32_t j = t - g * divC.d; // chunk column (divC.d = chunks of work per slot)
+    const uint64_t h0 = A.present[2 * g], h1 = A.present[2 * g + 1], pm = A.parity_present[g];
+    // lines with their parity received and exactly one member missing
+    // (uniform loop: the line masks stay scalar kernel-argument loads)
+    uint64_t fire = 0;
+    for (uint32_t l = 0; l < P.n_lines; ++l) {
+        const uint64_t x0 = M.mask[l][0] & ~h0, x1 = M.mask[l][1] & ~h1;
+        if (__popcll(x0) + __popcll(x1) == 1)
+            fire |= 1ull << l;
+    }
+    fire &= pm;
+    v4u* grp = shards + (size_t)g * P.k * C + j;
+    const v4u* par = parity + (size_t)g * P.n_lines * C + j;
+    while (fire) {
+        // two fired lines per round, every load of both in flight together
+        v4u acc[2], mv[2][MAXC];
+        uint32_t tg[2];
+        bool on[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            on[b] = fire != 0;
+            const uint32_t l = on[b] ? (uint32_t)__ffsll((long long)fire) - 1 : 0;
+            fire &= fire - 1;
+            const uint32_t ln = lplan[l];
+            const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
+            acc[b] = v4u{0, 0, 0, 0};
+            if (on[b])
+                acc[b] = ld16<NTL>(par + (size_t)l * C);
+            tg[b] = first;
+#pragma unroll
+            for (int q = 0; q < MAXC; ++q) {
+                const uint32_t i = first + q * stride;
+                mv[b][q] = v4u{0, 0, 0, 0};
+                if (!on[b] || (uint32_t)q >= count)
+                    continue;
+                if (has_bit(h0, h1, i))
+                    mv[b][q] = ld16<NTL>(grp + (size_t)i * C);
+                else
+                    tg[b] = i;
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+#pragma unroll
+            for (int q = 0; q < MAXC; ++q)
+                acc[b] ^= mv[b][q];
+            if (on[b])
+                st16<NTS>(grp + (size_t)tg[b] * C, acc[b]);
+        }
     }
 }
 
@@ -756,6 +856,32 @@ void launch_replay(const ReplayArgs& R, bool ntl, int sp, const rfec_kplan& P, d
     case 3: launch_replay_t<MAXC, BATCH, PIPE, true, 3>(R, P, grid); break;
     default: launch_replay_t<MAXC, BATCH, PIPE, true, 1>(R, P, grid); break;
     }
+}
+
+struct FusedArgs {
+    v4u* shards;
+    const v4u* parity;
+    uint32_t total, C;
+    FastDiv f;
+    uint32_t n_hdr;
+    hipStream_t stream;
+};
+
+// sp: store policy, -1 = plain loads + non-temporal stores (A/B only)
+template <int MAXC>
+void launch_fused(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, dim3 grid)
+{
+#define RFEC_FUSED(NTL, NTS)                                                                                     \
+    hipLaunchKernelGGL((k_decode_disjoint<MAXC, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards, F.parity, \
+                       F.total, F.C, F.f, F.n_hdr, B, M)
+    switch (sp) {
+    case -1: RFEC_FUSED(false, 1); break;
+    case 0: RFEC_FUSED(true, 0); break;
+    case 2: RFEC_FUSED(true, 2); break;
+    case 3: RFEC_FUSED(true, 3); break;
+    default: RFEC_FUSED(true, 1); break;
+    }
+#undef RFEC_FUSED
 }
 
 // flags -> store cache policy of st16<SP>.  Defaults, measured in the
@@ -881,16 +1007,6 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
     B.sched = reinterpret_cast<uint8_t*>(ws);
     B.groups = groups;
     B.capacity = capacity;
-    // LDS per group: K + NL header records (5 dwords) + NL u16 sizes; block
-    // ranges start on 8-group boundaries so the staged slices are 16-B aligned
-    const uint32_t per = 5u * P.k + 6u * P.n_lines;
-    // (at most 64 groups per block: the peel is one serial chain per lane, so
-    // more, smaller blocks give each SIMD more chains to interleave)
-    uint32_t gpb = (kPeelDwords - 8) / per;
-    gpb = gpb > 64u ? 64u : gpb;
-    if (gpb >= 8)
-        gpb &= ~7u;
-    B.gpb = gpb < 1 ? 1 : gpb;
     B.rec_bytes = rfec_sched_record_bytes(P.n_lines);
     uint64_t seen0 = 0, seen1 = 0;
     B.disjoint = 1;
@@ -900,13 +1016,22 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
         seen0 |= M->mask[l][0];
         seen1 |= M->mask[l][1];
     }
-    hipLaunchKernelGGL(k_peel_lds, dim3((groups + B.gpb - 1) / B.gpb), dim3(kBlock), 0, st, B, *M);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess)
-        return (int)e;
     uint32_t maxc = 0;
     for (uint32_t l = 0; l < P.n_lines; ++l)
         maxc = P.line[l].count > maxc ? P.line[l].count : maxc;
+    // disjoint plans (row layer alone, strip mode) decode in one launch
+    const bool fused = B.disjoint && maxc <= 8 && !(flags & (RFEC_KFLAG_TWO_KERNEL_DECODE | RFEC_KFLAG_PIPE_DECODE));
+    // LDS per group: K + NL header records (5 dwords) + NL u16 sizes; block
+    // ranges start on 8-group boundaries so the staged slices are 16-B aligned
+    const uint32_t per = 5u * P.k + 6u * P.n_lines;
+    // (at most 64 groups per block: the peel is one serial chain per lane, so
+    // more, smaller blocks give each SIMD more chains to interleave)
+    uint32_t gpb = ((fused ? kFusedPeelDwords : kPeelDwords) - 8) / per;
+    gpb = gpb > 64u ? 64u : gpb;
+    if (gpb >= 8)
+        gpb &= ~7u;
+    B.gpb = gpb < 1 ? 1 : gpb;
+    const uint32_t n_hdr = (groups + B.gpb - 1) / B.gpb;
     const uint32_t C = stride / 16;
     const uint32_t cd = capacity ? (capacity + 15) / 16 : 1;
     const uint32_t total = groups * cd;
@@ -914,9 +1039,23 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
     const FastDiv f = make_fastdiv(cd);
     const v4u* pp = reinterpret_cast<const v4u*>(parity);
     v4u* sh = reinterpret_cast<v4u*>(shards);
+    if (fused) {
+        const FusedArgs F = {sh, pp, total, C, f, n_hdr, st};
+        const int sp = ntl ? store_policy(flags, kRecoverStoreDefault) : -1;
+        if (maxc <= 4)
+            launch_fused<4>(F, sp, B, *M, dim3(n_hdr + grid.x));
+        else
+            launch_fused<8>(F, sp, B, *M, dim3(n_hdr + grid.x));
+        return (int)hipGetLastError();
+    }
+    hipLaunchKernelGGL(k_peel_lds, dim3(n_hdr), dim3(kBlock), 0, st, B, *M);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return (int)e;
     const uint8_t* sc = B.sched;
     const int nts = store_policy(flags, kRecoverStoreDefault);
-    const ReplayArgs R = {sh, pp, sc, total, C, f, B.rec_bytes, maxc <= 8 ? 1u : 0u, st};
+    const uint32_t fast = (maxc <= 8 ? 1u : 0u) | ((flags & RFEC_TUNE_DIAG_CONST_SCHED) ? 2u : 0u);
+    const ReplayArgs R = {sh, pp, sc, total, C, f, B.rec_bytes, fast, st};
     if (maxc <= 4 && (flags & RFEC_KFLAG_PIPE_DECODE))
         launch_replay<4, 2, true>(R, ntl, nts, P, dim3(grid.x < 4096u ? grid.x : 4096u));
     else if (maxc <= 4)

@@ -17,7 +17,7 @@ MANIFEST = po.manifest()
 CASES = {c["name"]: c for c in MANIFEST["cases"]}
 TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "plain_stores": 4, "items2": 8, "wave_decode": 16,
            "pipe_decode": 32, "wt_stores": 64, "wt_nt_stores": 192, "nt_stores": 512,
-           "generic_plain": 3}
+           "generic_plain": 3, "two_kernel": 4096, "two_kernel_wt": 4096 | 64}
 
 
 @pytest.fixture(scope="module")
@@ -47,10 +47,19 @@ def test_rows_fixture_gpu(gpu, oracle1000, oracle1200, name, tuning):
 
 
 @pytest.mark.parametrize("tuning", ["default", "wave_decode", "pipe_decode", "plain_loads", "wt_stores",
-                                    "plain_stores", "nt_stores"])
+                                    "plain_stores", "nt_stores", "two_kernel"])
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures"])
 def test_erasure_fixture_gpu(gpu, oracle1000, name, tuning):
     pc.check_erasure_case(gpu(tuning=TUNINGS[tuning]), oracle1000, CASES[name])
+
+
+@pytest.mark.parametrize("tuning", ["default", "wt_stores", "plain_stores", "plain_loads", "two_kernel",
+                                    "two_kernel_wt", "pipe_decode", "wave_decode"])
+@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures" and c["rows_only"]])
+def test_erasure_fixture_rows_plan_gpu(gpu, oracle1000, name, tuning):
+    """Row-parity-only fixtures against the row-layer plan (pairwise disjoint
+    lines: the fused one-launch decode applies where rows have <= 4 members)."""
+    pc.check_erasure_case(gpu(tuning=TUNINGS[tuning]), oracle1000, CASES[name], layers=1)
 
 
 def test_single_cases_dropin_gpu(product):
@@ -159,25 +168,31 @@ def test_full_size_k10_roundtrip(product, oracle1200, layers):
     present = np.full((G, 2), 0, np.uint64)
     present[:, 0] = np.uint64((1 << k) - 1) & ~((np.uint64(1) << er[:, 0].astype(np.uint64)) |
                                                (np.uint64(1) << er[:, 1].astype(np.uint64)))
-    rx = shards.clone()
-    rx_hdr = d_hdr.clone()
-    gi = torch.arange(G, device=rx.device)
-    for c in range(2):
-        e = torch.from_numpy(er[:, c]).to(rx.device)
-        rx[gi, e] = 0xA5
-        rx_hdr[gi, e] = 0
-    d_pres = torch.from_numpy(present.view(np.int64)).to(rx.device)
-    d_pp = torch.full((G,), (1 << plan.n_lines) - 1, dtype=torch.int64, device=rx.device)
-    rec = torch.empty((G, 2), dtype=torch.int64, device=rx.device)
-    ws = torch.empty((lib.workspace_size(plan, G),), dtype=torch.uint8, device=rx.device)
-    lib.recover_batch(plan, G, S, S, rx.data_ptr(), rx_hdr.data_ptr(), d_pres.data_ptr(), par.data_ptr(),
-                      meta.data_ptr(), fs.data_ptr(), d_pp.data_ptr(), rec.data_ptr(), ws.data_ptr(),
-                      torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    assert torch.equal(rx, shards)
-    assert torch.equal(rx_hdr, d_hdr)
+    gi = torch.arange(G, device=shards.device)
+    d_pres = torch.from_numpy(present.view(np.int64)).to(shards.device)
+    d_pp = torch.full((G,), (1 << plan.n_lines) - 1, dtype=torch.int64, device=shards.device)
+    ws = torch.empty((lib.workspace_size(plan, G),), dtype=torch.uint8, device=shards.device)
     exp = ((1 << er[:, 0]) | (1 << er[:, 1])).astype(np.int64)
-    assert np.array_equal(rec[:, 0].cpu().numpy(), exp)
+    # default (fused one-launch decode for the disjoint row layer), forced peel + replay
+    for dec_tuning in (0, 4096, 4096 | 64):
+        rx = shards.clone()
+        rx_hdr = d_hdr.clone()
+        for c in range(2):
+            e = torch.from_numpy(er[:, c]).to(rx.device)
+            rx[gi, e] = 0xA5
+            rx_hdr[gi, e] = 0
+        rec = torch.empty((G, 2), dtype=torch.int64, device=rx.device)
+        lib.set_tuning(dec_tuning)
+        try:
+            lib.recover_batch(plan, G, S, S, rx.data_ptr(), rx_hdr.data_ptr(), d_pres.data_ptr(), par.data_ptr(),
+                              meta.data_ptr(), fs.data_ptr(), d_pp.data_ptr(), rec.data_ptr(), ws.data_ptr(),
+                              torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+        finally:
+            lib.set_tuning(0)
+        assert torch.equal(rx, shards), dec_tuning
+        assert torch.equal(rx_hdr, d_hdr), dec_tuning
+        assert np.array_equal(rec[:, 0].cpu().numpy(), exp), dec_tuning
 
 
 def test_full_size_k32_s256(product, oracle1000):

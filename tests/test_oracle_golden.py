@@ -74,6 +74,11 @@ def test_erasure_fixture_oracle(oracle1000, name):
     pc.check_erasure_case(OracleEngine(oracle1000), oracle1000, CASES[name])
 
 
+@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures" and c["rows_only"]])
+def test_erasure_fixture_oracle_rows_plan(oracle1000, name):
+    pc.check_erasure_case(OracleEngine(oracle1000), oracle1000, CASES[name], layers=1)
+
+
 def test_erasure_counts(oracle1000):
     """at k=10 3x4 all 45 pairs and 120 triples recover with the full
     plan; rows only recovers 32/45 pairs and 32/120 triples."""

@@ -25,7 +25,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 
-KERNELS = {"encode": "k_encode", "peel": "k_peel", "recover": "k_recover"}
+KERNELS = {"encode": "k_encode", "decode": "k_decode_disjoint", "peel": "k_peel", "recover": "k_recover"}
 
 
 def run_pass(counter, outdir, bench_args, timeout):
@@ -41,7 +41,8 @@ def run_pass(counter, outdir, bench_args, timeout):
     files = glob.glob(str(d / "**" / "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
-    return files
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    return files, (json.loads(line[-1]) if line else None)
 
 
 def per_kernel(files, counter):
@@ -66,8 +67,9 @@ def main():
     args = ap.parse_args()
     bench_args = args.bench_args or ["--steps", "10", "--warmup", "2"]
     outdir = Path(args.out).parent
-    fetch = per_kernel(run_pass("FETCH_SIZE", outdir, bench_args, args.timeout), "FETCH_SIZE")
-    write = per_kernel(run_pass("WRITE_SIZE", outdir, bench_args, args.timeout), "WRITE_SIZE")
+    ffiles, bench_line = run_pass("FETCH_SIZE", outdir, bench_args, args.timeout)
+    fetch = per_kernel(ffiles, "FETCH_SIZE")
+    write = per_kernel(run_pass("WRITE_SIZE", outdir, bench_args, args.timeout)[0], "WRITE_SIZE")
     # the workload the bench ran
     groups = 65536
     for i, a in enumerate(bench_args):
@@ -90,6 +92,11 @@ def main():
         entry["encode_hbm_bytes_per_launch"] = res["encode"]["hbm_bytes"]
         entry["encode_algorithmic_bytes"] = enc_alg
         entry["encode_traffic_over_algorithmic"] = res["encode"]["hbm_bytes"] / enc_alg
+    dec_alg = (bench_line or {}).get("config", {}).get("bytes_per_step_per_gpu", {}).get("decode")
+    if "decode" in res and dec_alg:
+        entry["decode_hbm_bytes_per_launch"] = res["decode"]["hbm_bytes"]
+        entry["decode_algorithmic_bytes"] = dec_alg
+        entry["decode_traffic_over_algorithmic"] = res["decode"]["hbm_bytes"] / dec_alg
     name = f"k{k}_r{r}_S{S}_G{groups}"
     Path(args.out).write_text(json.dumps({name: entry}, indent=1))
     print(json.dumps({name: entry}, indent=1))
