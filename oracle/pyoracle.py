@@ -77,6 +77,8 @@ class Oracle:
         L = self.lib
         P = C.c_void_p
         L.oracle_fill_groups.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, P, P]
+        L.oracle_fill_stream.argtypes = [C.c_uint64, C.POINTER(C.c_uint64), C.c_uint32, C.c_uint32, C.c_uint32,
+                                         C.c_uint32, C.c_uint32, C.c_int, P, P]
         L.oracle_num_packets.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.oracle_plan_from_fraction.argtypes = [C.c_int, C.c_int, C.c_uint, C.POINTER(rfec_plan)]
         L.oracle_plan_matrix.argtypes = [C.c_int, C.c_int, C.c_int, C.c_uint, C.POINTER(rfec_plan)]
@@ -105,6 +107,21 @@ class Oracle:
         hdr = np.zeros((groups, k), HDR_DTYPE)
         self.lib.oracle_fill_groups(config_id, groups, k, S, stride, int(ragged), _np_ptr(shards), _np_ptr(hdr))
         return shards, hdr
+
+    def fill_stream(self, config_id, k, S, stride=None, ragged=False):
+        """Generator of (g0, shards, hdr) pieces of the fill_groups stream."""
+        stride = stride or ((S + 15) // 16) * 16
+        state = (C.c_uint64 * 2)(0, 0)
+        lib = self.lib
+
+        def piece(g0, groups):
+            shards = np.empty((groups, k, stride), np.uint8)
+            hdr = np.zeros((groups, k), HDR_DTYPE)
+            lib.oracle_fill_stream(config_id, state, g0, groups, k, S, stride, int(ragged), _np_ptr(shards),
+                                   _np_ptr(hdr))
+            return shards, hdr
+
+        return piece
 
     # -- planner ------------------------------------------------------------
     def num_packets(self, n, pf):

@@ -40,18 +40,35 @@ uint32_t oracle_xs_rand(uint64_t* s, uint32_t t)
 void oracle_fill_groups(uint64_t config_id, uint32_t groups, uint32_t k, uint32_t S, uint32_t stride,
                         int ragged, uint8_t* shards, rfec_hdr* hdr)
 {
-    uint64_t st = ORACLE_SEED ^ config_id;
-    uint64_t st2 = ORACLE_SEED ^ config_id ^ ORACLE_RAGGED_SALT;
-    for (uint32_t g = 0; g < groups; ++g) {
+    uint64_t state[2] = {0, 0};
+    oracle_fill_stream(config_id, state, 0, groups, k, S, stride, ragged, shards, hdr);
+}
+
+void oracle_fill_stream(uint64_t config_id, uint64_t state[2], uint32_t g0, uint32_t groups, uint32_t k,
+                        uint32_t S, uint32_t stride, int ragged, uint8_t* shards, rfec_hdr* hdr)
+{
+    if (state[0] == 0 && state[1] == 0) {
+        state[0] = ORACLE_SEED ^ config_id;
+        state[1] = ORACLE_SEED ^ config_id ^ ORACLE_RAGGED_SALT;
+    }
+    uint64_t st = state[0], st2 = state[1];
+    for (uint32_t gl = 0; gl < groups; ++gl) {
+        const uint32_t g = g0 + gl;
         for (uint32_t i = 0; i < k; ++i) {
-            uint8_t* d = shards + ((size_t)g * k + i) * stride;
-            for (uint32_t b = 0; b < S; b += 8) {
+            uint8_t* d = shards + ((size_t)gl * k + i) * stride;
+            uint32_t b = 0;
+            for (; b + 8 <= S; b += 8) { /* little-endian bytes of each output */
                 uint64_t v = oracle_xs_next(&st);
-                for (uint32_t q = 0; q < 8 && b + q < S; ++q)
+                for (uint32_t q = 0; q < 8; ++q)
+                    d[b + q] = (uint8_t)(v >> (8 * q));
+            }
+            if (b < S) {
+                uint64_t v = oracle_xs_next(&st);
+                for (uint32_t q = 0; b + q < S; ++q)
                     d[b + q] = (uint8_t)(v >> (8 * q));
             }
             memset(d + S, 0, stride - S);
-            rfec_hdr* h = &hdr[(size_t)g * k + i];
+            rfec_hdr* h = &hdr[(size_t)gl * k + i];
             h->seq = 1u + g * k + i; /* contiguous ids, sim_sender.c:338 */
             h->fid = 1u + g;
             h->ts = 33u * g;
@@ -67,6 +84,8 @@ void oracle_fill_groups(uint64_t config_id, uint32_t groups, uint32_t k, uint32_
             }
         }
     }
+    state[0] = st;
+    state[1] = st2;
 }
 
 /* ---- single-line XOR core: flex_fec_xor.c:4-53 ---------------------------- */

@@ -28,6 +28,10 @@ uint32_t oracle_xs_rand(uint64_t* state, uint32_t t);
  * stream, bytes beyond data_size zeroed.  seed = 0x52415A4F52464543 ^ config_id. */
 void oracle_fill_groups(uint64_t config_id, uint32_t groups, uint32_t k, uint32_t S, uint32_t stride,
                         int ragged, uint8_t* shards, rfec_hdr* hdr);
+/* The same stream in pieces: groups [g0, g0+groups) written at shards/hdr[0];
+ * state = {0, 0} before the first piece, carried between pieces. */
+void oracle_fill_stream(uint64_t config_id, uint64_t state[2], uint32_t g0, uint32_t groups, uint32_t k,
+                        uint32_t S, uint32_t stride, int ragged, uint8_t* shards, rfec_hdr* hdr);
 
 /* flex_fec_xor.c:4-53 with SIM_VIDEO_SIZE replaced by `capacity`. */
 int oracle_generate(sim_segment_t* segs[], int segs_count, sim_fec_t* fec, int capacity);

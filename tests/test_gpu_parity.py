@@ -300,3 +300,17 @@ def test_host_encode_groups(product1200, oracle1200):
     for j in range(G * n):
         L = int(ref["fec_data_size"][j])
         assert np.array_equal(fecs["fec_data"][j, :L], ref["fec_data"][j, :L])
+
+
+@pytest.mark.parametrize("name", ["c2_k10_rows_S1200_G65536", "c3_k10_full_S1200_G65536",
+                                  "c4_k10_rows_S1200_G1048576", "c5_k32_rows4_S256_G65536",
+                                  "k10_full_ragged_S1000_G65536"])
+def test_full_size_digest_gpu(gpu, oracle1000, name):
+    """Every group of a BASELINE-sized batch bit-exact vs the reference: the
+    SHA-256 of the HIP encode's outputs equals the digest oracle/gen_full.c took
+    of the reference's flex_fec_generate over the same PRNG inputs (config 4:
+    1,048,576 groups, encoded in 65,536-group launches)."""
+    import full_digest as fd
+
+    c = fd.cases()[name]
+    assert fd.digest(gpu().encode, oracle1000, c, chunk=65536) == c["sha256"]

@@ -192,3 +192,16 @@ def test_aos_path_matches_batch(oracle1200):
             assert int.from_bytes(fec[g, l, 40:42].tobytes(), "little") == L
             assert fec[g, l, 20:40].tobytes() == meta[g, l].tobytes()
             assert np.array_equal(fec[g, l, 42:42 + L], parity[g, l, :L])
+
+
+
+@pytest.mark.parametrize("name", ["c2_k10_rows_S1200_G65536", "c3_k10_full_S1200_G65536",
+                                  "c5_k32_rows4_S256_G65536", "k10_full_ragged_S1000_G65536"])
+def test_full_size_digest_oracle(oracle1000, name):
+    """The oracle reproduces the reference's digest of a whole BASELINE-sized
+    batch (tests/golden/full_hashes.json from oracle/gen_full.c; the 1M-group
+    config 4 digest is checked on the GPU only)."""
+    import full_digest as fd
+
+    c = fd.cases()[name]
+    assert fd.digest(oracle1000.encode_batch, oracle1000, c, chunk=16384) == c["sha256"]
