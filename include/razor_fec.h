@@ -212,6 +212,106 @@ int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
 int rfec_zero_tails(uint32_t groups, uint32_t k, uint32_t stride, uint8_t* shards,
                     const rfec_hdr* hdr, void* stream);
 
+/* ------------------------------------------------------------------------ */
+/* Wire codec, batched on the device: the SIM_FEC / SIM_SEG datagrams of     */
+/* sim_encode_msg / sim_decode_header + sim_decode_msg (sim_proto.c:13-146,  */
+/* sim_proto.inl:83-179, 244-307), big-endian fields (cf_stream.c:328-414),  */
+/* CRC32 trailer (cf_crc32.c:56-68, seed 0x0e3dfc0a, sim_proto.c:11).        */
+/*                                                                          */
+/* A datagram is: ver, mid, uid (6 B, sim_proto.c:13-18) | body | crc32 of   */
+/* everything before it, big-endian (sim_proto.c:92-94).  Datagram slots are */
+/* [N][dstride] bytes, dstride a multiple of 16 in [64, 2048]; lengths are   */
+/* u16 per slot.  Bytes of a slot beyond its length are written as 0.        */
+/* ------------------------------------------------------------------------ */
+#define RFEC_WIRE_VER 0x01        /* protocol_ver, sim_proto.h:39 */
+#define RFEC_WIRE_SEG 0x17        /* SIM_SEG, sim_proto.h:17-29 */
+#define RFEC_WIRE_FEC 0x1c        /* SIM_FEC, sim_proto.h:34 */
+#define RFEC_WIRE_MIN_MID 0x10    /* MIN_MSG_ID */
+#define RFEC_WIRE_MAX_MID 0x1d    /* MAX_MSG_ID (accepted, sim_session.c:594) */
+#define RFEC_WIRE_CRC_SEED 0x0e3dfc0au
+#define RFEC_WIRE_FEC_OVERHEAD 49 /* 6 + 17 + 20 + 2 + 4 bytes around fec_data */
+#define RFEC_WIRE_MAX_DSTRIDE 2048
+
+/* Per-datagram fields of a SIM_FEC the FEC engine does not produce: the
+ * session uid (sim_proto.c:13-18) and the sim_fec_t stamps of the sender
+ * (flex_fec_sender.c:176-181, 220-225; sim_sender.c:112-113). */
+typedef struct {
+    uint32_t uid;
+    uint32_t base_id;
+    uint32_t send_ts;
+    uint16_t fec_id;
+    uint16_t count;
+    uint16_t transport_seq;
+    uint8_t row, col, index;
+    uint8_t reserved;
+    uint8_t pad[2];
+} rfec_fec_stamp; /* 24 bytes */
+
+/* Per-datagram fields of a SIM_SEG beyond rfec_hdr (sim_sender.c:88-91, 335-351). */
+typedef struct {
+    uint32_t uid;
+    uint16_t fec_id;
+    uint16_t send_ts;
+    uint16_t transport_seq;
+    uint8_t remb;
+    uint8_t reserved;
+} rfec_seg_stamp; /* 12 bytes */
+
+/* SIM_FEC datagrams (sim_sender.c:118-119 + sim_fec_encode,
+ * sim_proto.inl:270-285) of `count` parity slots laid out as rfec_encode_batch
+ * wrote them (slot g*n + l = line l of group g): datagram i -> dgram slot i.
+ * `status` may be NULL; a slot with status -1 gets length 0 (the reference
+ * never emits that parity).  Needs fec_size <= capacity <= stride and
+ * dstride >= capacity + 49. */
+int rfec_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
+                        const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,
+                        const rfec_fec_stamp* stamps, uint32_t dstride, uint8_t* dgram, uint16_t* dlen,
+                        void* stream);
+
+/* SIM_SEG datagrams (sim_sender.c:96-97 + sim_segment_encode,
+ * sim_proto.inl:83-125; header widths follow the value ranges) of `count`
+ * segments: shards [count][stride], hdr [count].  Needs data_size <= capacity
+ * <= stride and dstride >= capacity + 36. */
+int rfec_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* shards,
+                        const rfec_hdr* hdr, const rfec_seg_stamp* stamps, uint32_t dstride, uint8_t* dgram,
+                        uint16_t* dlen, void* stream);
+
+/* Parse status (rfec_wire_rec.status). */
+#define RFEC_WIRE_OK 0         /* SIM_SEG / SIM_FEC decoded (a SEG with a bad data length decodes
+                                  with data_size 0, as sim_segment_decode does) */
+#define RFEC_WIRE_OTHER 1      /* valid control message (CONNECT, PING, ...): header only */
+#define RFEC_WIRE_EBADCRC (-1) /* sim_decode_header: CRC mismatch, or shorter than the trailer */
+#define RFEC_WIRE_EMID (-2)    /* mid outside [MIN_MSG_ID, MAX_MSG_ID] (sim_session.c:594) */
+#define RFEC_WIRE_EBODY (-3)   /* sim_fec_decode returned -1 (fec_data length invalid) */
+
+/* One parsed datagram.  SIM_SEG: hdr = the segment's header (seq=packet_id,
+ * fid, ts=timestamp, index, total, ftype, payload_type, size=data_size),
+ * fec_id, send_ts (u16 widened), transport_seq, remb.  SIM_FEC: hdr = fec_meta,
+ * the sim_fec_t fields, data_size = fec_data_size. */
+typedef struct {
+    int8_t status;
+    uint8_t ver, mid, remb;
+    uint32_t uid;
+    rfec_hdr hdr;
+    uint32_t base_id;
+    uint32_t send_ts;
+    uint16_t fec_id;
+    uint16_t count;
+    uint16_t transport_seq;
+    uint16_t data_size;
+    uint8_t row, col, index;
+    uint8_t reserved[17];
+} rfec_wire_rec; /* 64 bytes */
+
+/* Decode N received datagrams (sim_session.c:587-653 -> sim_decode_header,
+ * sim_decode_msg) into recs [N] and their payloads into slots [N][stride]
+ * (zero beyond data_size: the layout rfec_recover_batch expects).  `capacity`
+ * plays SIM_VIDEO_SIZE in the length checks (cf_stream.c:342-355,
+ * sim_proto.inl:301-305); capacity <= stride. */
+int rfec_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
+                    uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload,
+                    void* stream);
+
 /* Kernel-selection knobs, for benchmarking and A/B tests (0 = defaults:
  * specialised row kernels where the plan allows, non-temporal streaming). */
 #define RFEC_TUNE_GENERIC 1u       /* always use the generic plan-driven kernel */

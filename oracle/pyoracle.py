@@ -29,6 +29,29 @@ ERASURE_REC = np.dtype([("present", "<u8", (2,)), ("parity_present", "<u8"), ("r
                         ("group", "<u4"), ("n_recovered", "<u4"), ("hash", "<u8", (16,))])
 assert PARITY_REC.itemsize == 48 and ERASURE_REC.itemsize == 176
 
+# wire codec (include/razor_fec.h rfec_fec_stamp / rfec_seg_stamp / rfec_wire_rec)
+FEC_STAMP = np.dtype([("uid", "<u4"), ("base_id", "<u4"), ("send_ts", "<u4"), ("fec_id", "<u2"), ("count", "<u2"),
+                      ("transport_seq", "<u2"), ("row", "u1"), ("col", "u1"), ("index", "u1"), ("reserved", "u1"),
+                      ("pad", "u1", (2,))])
+SEG_STAMP = np.dtype([("uid", "<u4"), ("fec_id", "<u2"), ("send_ts", "<u2"), ("transport_seq", "<u2"), ("remb", "u1"),
+                      ("reserved", "u1")])
+WIRE_REC = np.dtype([("status", "i1"), ("ver", "u1"), ("mid", "u1"), ("remb", "u1"), ("uid", "<u4"),
+                     ("hdr", HDR_DTYPE), ("base_id", "<u4"), ("send_ts", "<u4"), ("fec_id", "<u2"), ("count", "<u2"),
+                     ("transport_seq", "<u2"), ("data_size", "<u2"), ("row", "u1"), ("col", "u1"), ("index", "u1"),
+                     ("reserved", "u1", (17,))])
+# fixture records (oracle/gen_wire.c)
+WIRE_FEC_IN = np.dtype([("uid", "<u4"), ("base_id", "<u4"), ("send_ts", "<u4"), ("fec_id", "<u2"), ("count", "<u2"),
+                        ("transport_seq", "<u2"), ("row", "u1"), ("col", "u1"), ("index", "u1"), ("pad0", "u1"),
+                        ("meta", HDR_DTYPE), ("fec_data_size", "<u2"), ("dlen", "<u2"), ("pad1", "u1", (2,))])
+WIRE_SEG_IN = np.dtype([("uid", "<u4"), ("packet_id", "<u4"), ("fid", "<u4"), ("timestamp", "<u4"), ("index", "<u2"),
+                        ("total", "<u2"), ("ftype", "u1"), ("payload_type", "u1"), ("remb", "u1"), ("pad0", "u1"),
+                        ("fec_id", "<u2"), ("send_ts", "<u2"), ("transport_seq", "<u2"), ("data_size", "<u2"),
+                        ("dlen", "<u2"), ("pad1", "u1", (2,))])
+WIRE_PARSE_IN = np.dtype([("len", "<u2"), ("kind", "u1"), ("pad", "u1", (5,)), ("rec", WIRE_REC)])
+assert FEC_STAMP.itemsize == 24 and SEG_STAMP.itemsize == 12 and WIRE_REC.itemsize == 64
+assert WIRE_FEC_IN.itemsize == 48 and WIRE_SEG_IN.itemsize == 36 and WIRE_PARSE_IN.itemsize == 72
+CRC_SEED = 0x0E3DFC0A
+
 SEED = 0x52415A4F52464543
 
 
@@ -94,6 +117,11 @@ class Oracle:
         L.oracle_encode_aos_mt.restype = C.c_long
         L.oracle_recover_aos.argtypes = [C.POINTER(rfec_plan), C.c_uint32, P, P, P, P]
         L.oracle_recover_aos.restype = C.c_long
+        L.oracle_crc32.argtypes = [C.c_uint32, P, C.c_size_t]
+        L.oracle_crc32.restype = C.c_uint32
+        L.oracle_wire_frame_fec_batch.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, P, P, P, P, P, C.c_uint32, P, P]
+        L.oracle_wire_frame_seg_batch.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, P, P, P, C.c_uint32, P, P]
+        L.oracle_wire_parse_batch.argtypes = [C.c_uint32, C.c_uint32, P, P, C.c_uint32, C.c_uint32, P, P]
         L.oracle_segment_size.restype = C.c_size_t
         L.oracle_fec_size.restype = C.c_size_t
         self.video_size = L.oracle_sim_video_size()
@@ -165,6 +193,44 @@ class Oracle:
                                       _np_ptr(np.ascontiguousarray(fsize, np.uint16)),
                                       _np_ptr(np.ascontiguousarray(parity_present, np.uint64)), _np_ptr(rec))
         return shards, hdr, rec
+
+    # -- wire codec ----------------------------------------------------------
+    def crc32(self, data: bytes, seed: int = CRC_SEED) -> int:
+        b = np.frombuffer(bytes(data), np.uint8)
+        return int(self.lib.oracle_crc32(seed, _np_ptr(b), len(b)))
+
+    def frame_fec_batch(self, parity, meta, fsize, status, stamps, capacity, dstride):
+        """parity [N][stride] (or [G][n][stride]) -> (dgram [N][dstride], dlen [N])."""
+        stride = parity.shape[-1]
+        N = parity.size // stride
+        dgram = np.zeros((N, dstride), np.uint8)
+        dlen = np.zeros(N, np.uint16)
+        st = None if status is None else _np_ptr(np.ascontiguousarray(status, np.int8))
+        self.lib.oracle_wire_frame_fec_batch(N, stride, capacity, _np_ptr(np.ascontiguousarray(parity)),
+                                             _np_ptr(np.ascontiguousarray(meta)),
+                                             _np_ptr(np.ascontiguousarray(fsize, np.uint16)), st,
+                                             _np_ptr(np.ascontiguousarray(stamps)), dstride, _np_ptr(dgram),
+                                             _np_ptr(dlen))
+        return dgram, dlen
+
+    def frame_seg_batch(self, shards, hdr, stamps, capacity, dstride):
+        stride = shards.shape[-1]
+        N = shards.size // stride
+        dgram = np.zeros((N, dstride), np.uint8)
+        dlen = np.zeros(N, np.uint16)
+        self.lib.oracle_wire_frame_seg_batch(N, stride, capacity, _np_ptr(np.ascontiguousarray(shards)),
+                                             _np_ptr(np.ascontiguousarray(hdr)), _np_ptr(np.ascontiguousarray(stamps)),
+                                             dstride, _np_ptr(dgram), _np_ptr(dlen))
+        return dgram, dlen
+
+    def parse_batch(self, dgram, dlen, stride, capacity):
+        N, dstride = dgram.shape
+        recs = np.zeros(N, WIRE_REC)
+        payload = np.zeros((N, stride), np.uint8)
+        self.lib.oracle_wire_parse_batch(N, dstride, _np_ptr(np.ascontiguousarray(dgram)),
+                                         _np_ptr(np.ascontiguousarray(dlen, np.uint16)), stride, capacity,
+                                         _np_ptr(recs), _np_ptr(payload))
+        return recs, payload
 
     # -- AoS (reference-shaped) path for the CPU baseline ---------------------
     def seg_dtype(self):
@@ -239,6 +305,44 @@ def load_parities(c: dict):
 
 def load_erasures(c: dict):
     return np.fromfile(GOLDEN / c["file"], ERASURE_REC)
+
+
+def wire_manifest() -> dict:
+    return json.loads((GOLDEN / "wire_manifest.json").read_text())
+
+
+def _walk(path, rec_dtype, count, tail):
+    """Variable-length records: fixed header, then tail(rec) -> [(name, nbytes)] byte fields."""
+    raw = np.fromfile(GOLDEN / path, np.uint8)
+    out, off = [], 0
+    for _ in range(count):
+        r = raw[off:off + rec_dtype.itemsize].copy().view(rec_dtype)[0]
+        off += rec_dtype.itemsize
+        fields = {}
+        for name, nb in tail(r):
+            fields[name] = raw[off:off + nb].copy()
+            off += nb
+        out.append((r, fields))
+    assert off == len(raw), f"{path}: {len(raw) - off} trailing bytes"
+    return out
+
+
+def load_wire_fec():
+    m = wire_manifest()["fec"]
+    return _walk(m["file"], WIRE_FEC_IN, m["count"],
+                 lambda r: [("payload", int(r["fec_data_size"])), ("dgram", int(r["dlen"]))])
+
+
+def load_wire_seg():
+    m = wire_manifest()["seg"]
+    return _walk(m["file"], WIRE_SEG_IN, m["count"],
+                 lambda r: [("payload", int(r["data_size"])), ("dgram", int(r["dlen"]))])
+
+
+def load_wire_parse():
+    m = wire_manifest()["parse"]
+    return _walk(m["file"], WIRE_PARSE_IN, m["count"],
+                 lambda r: [("dgram", int(r["len"])), ("payload", int(r["rec"]["data_size"]))])
 
 
 def plan_table() -> np.ndarray:

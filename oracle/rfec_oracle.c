@@ -510,3 +510,322 @@ long oracle_recover_aos(const rfec_plan* plan, uint32_t groups, sim_segment_t* s
     }
     return total;
 }
+
+/* ---- wire codec: sim_proto.c / sim_proto.inl / cf_stream.c / cf_crc32.c ---- */
+
+/* cf_crc32.c:56-68: reflected CRC-32 (poly 0xEDB88320), pre/post inverted;
+ * the table (cf_crc32.c:10-54) is the standard one, rebuilt here bitwise. */
+uint32_t oracle_crc32(uint32_t crc, const void* buf, size_t size)
+{
+    static uint32_t tab[256];
+    static int init;
+    if (!init) {
+        for (uint32_t b = 0; b < 256; ++b) {
+            uint32_t c = b;
+            for (int i = 0; i < 8; ++i)
+                c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+            tab[b] = c;
+        }
+        init = 1;
+    }
+    const uint8_t* p = (const uint8_t*)buf;
+    crc = crc ^ ~0u;
+    while (size--)
+        crc = tab[(crc ^ *p++) & 0xFF] ^ (crc >> 8);
+    return crc ^ ~0u;
+}
+
+/* bin_stream writers: big-endian (cf_stream.c:366-385 mach_put_2/4 on a
+ * little-endian host), mach_data_write = u16 length + bytes (:328-337) */
+typedef struct {
+    uint8_t* p;
+    size_t n;
+} wbuf;
+static void w8(wbuf* w, uint8_t v) { w->p[w->n++] = v; }
+static void w16(wbuf* w, uint16_t v)
+{
+    w8(w, (uint8_t)(v >> 8));
+    w8(w, (uint8_t)v);
+}
+static void w32(wbuf* w, uint32_t v)
+{
+    w16(w, (uint16_t)(v >> 16));
+    w16(w, (uint16_t)v);
+}
+static void wdata(wbuf* w, const uint8_t* d, size_t n)
+{
+    w16(w, (uint16_t)n);
+    memcpy(w->p + w->n, d, n);
+    w->n += n;
+}
+/* sim_proto.c:13-18 header, :92-94 CRC trailer */
+static void w_header(wbuf* w, uint8_t mid, uint32_t uid)
+{
+    w8(w, RFEC_WIRE_VER);
+    w8(w, mid);
+    w32(w, uid);
+}
+static size_t w_crc(wbuf* w)
+{
+    w32(w, oracle_crc32(RFEC_WIRE_CRC_SEED, w->p, w->n));
+    return w->n;
+}
+
+/* sim_fec_encode, sim_proto.inl:270-285 (+ sim_fec_meta_encode :244-254) */
+size_t oracle_wire_frame_fec(const sim_fec_t* f, uint32_t uid, uint8_t* out)
+{
+    wbuf w = {out, 0};
+    w_header(&w, RFEC_WIRE_FEC, uid);
+    w16(&w, f->fec_id);
+    w8(&w, f->row);
+    w8(&w, f->col);
+    w8(&w, f->index);
+    w16(&w, f->count);
+    w32(&w, f->base_id);
+    w16(&w, f->transport_seq);
+    w32(&w, f->send_ts);
+    w32(&w, f->fec_meta.seq);
+    w32(&w, f->fec_meta.fid);
+    w32(&w, f->fec_meta.ts);
+    w16(&w, f->fec_meta.index);
+    w16(&w, f->fec_meta.total);
+    w8(&w, f->fec_meta.ftype);
+    w8(&w, f->fec_meta.payload_type);
+    w16(&w, f->fec_meta.size);
+    wdata(&w, f->fec_data, f->fec_data_size);
+    return w_crc(&w);
+}
+
+/* sim_segment_encode, sim_proto.inl:83-125: field widths follow the values */
+size_t oracle_wire_frame_seg(const sim_segment_t* s, uint32_t uid, uint8_t* out)
+{
+    wbuf w = {out, 0};
+    w_header(&w, RFEC_WIRE_SEG, uid);
+    uint8_t mask = s->ftype & 0x01;
+    if (s->packet_id > 65535)
+        mask |= 1 << 7;
+    if (s->fid > 65535)
+        mask |= 1 << 6;
+    if (s->total > 255)
+        mask |= 1 << 5;
+    if (s->remb == 0)
+        mask |= 1 << 4;
+    w8(&w, mask);
+    w8(&w, s->payload_type);
+    if (s->packet_id > 65535)
+        w32(&w, s->packet_id);
+    else
+        w16(&w, (uint16_t)s->packet_id);
+    if (s->fid > 65535)
+        w32(&w, s->fid);
+    else
+        w16(&w, (uint16_t)s->fid);
+    w32(&w, s->timestamp);
+    if (s->total > 255) {
+        w16(&w, s->index);
+        w16(&w, s->total);
+    } else {
+        w8(&w, (uint8_t)s->index);
+        w8(&w, (uint8_t)s->total);
+    }
+    w16(&w, s->fec_id);
+    w16(&w, s->send_ts);
+    w16(&w, s->transport_seq);
+    wdata(&w, s->data, s->data_size);
+    return w_crc(&w);
+}
+
+/* bin_stream readers: a read past `used` yields 0 and does not advance
+ * (cf_stream.c mach_uint8/16/32_read); `used` covers the CRC trailer too. */
+typedef struct {
+    const uint8_t* p;
+    size_t used, r;
+} rbuf;
+static uint8_t r8(rbuf* b)
+{
+    if (b->used < b->r + 1)
+        return 0;
+    return b->p[b->r++];
+}
+static uint16_t r16(rbuf* b)
+{
+    if (b->used < b->r + 2)
+        return 0;
+    uint16_t v = (uint16_t)(b->p[b->r] << 8 | b->p[b->r + 1]);
+    b->r += 2;
+    return v;
+}
+static uint32_t r32(rbuf* b)
+{
+    if (b->used < b->r + 4)
+        return 0;
+    uint32_t v = (uint32_t)b->p[b->r] << 24 | (uint32_t)b->p[b->r + 1] << 16 | (uint32_t)b->p[b->r + 2] << 8 |
+                 b->p[b->r + 3];
+    b->r += 4;
+    return v;
+}
+/* mach_data_read, cf_stream.c:339-355: 0xFFFF on a bad length */
+static uint16_t rdata(rbuf* b, uint8_t* dst, size_t cap)
+{
+    uint16_t len = r16(b);
+    if (len > cap || b->r + len > b->used)
+        return 0xFFFF;
+    memcpy(dst, b->p + b->r, len);
+    b->r += len;
+    return len;
+}
+
+/* sim_session_process (sim_session.c:587-596) -> sim_decode_header
+ * (sim_proto.c:21-37) -> sim_decode_msg (:99-146) for SIM_SEG / SIM_FEC.
+ * Fills rec and payload[0:data_size) (payload zeroed to `capacity`). */
+int oracle_wire_parse(const uint8_t* d, size_t len, uint32_t capacity, rfec_wire_rec* rec, uint8_t* payload)
+{
+    memset(rec, 0, sizeof(*rec));
+    memset(payload, 0, capacity);
+    if (len < 4) { /* the reference would read before the buffer; rejected here */
+        rec->status = RFEC_WIRE_EBADCRC;
+        return rec->status;
+    }
+    const uint32_t src = (uint32_t)d[len - 4] << 24 | (uint32_t)d[len - 3] << 16 | (uint32_t)d[len - 2] << 8 |
+                         d[len - 1];
+    if (oracle_crc32(RFEC_WIRE_CRC_SEED, d, len - 4) != src) {
+        rec->status = RFEC_WIRE_EBADCRC;
+        return rec->status;
+    }
+    rbuf b = {d, len, 0};
+    rec->ver = r8(&b);
+    rec->mid = r8(&b);
+    rec->uid = r32(&b);
+    if (rec->mid < RFEC_WIRE_MIN_MID || rec->mid > RFEC_WIRE_MAX_MID) {
+        rec->status = RFEC_WIRE_EMID;
+        return rec->status;
+    }
+    if (rec->mid == RFEC_WIRE_SEG) { /* sim_segment_decode, sim_proto.inl:127-179 */
+        const uint8_t mask = r8(&b);
+        rec->hdr.payload_type = r8(&b);
+        rec->hdr.ftype = mask & 0x01;
+        rec->hdr.seq = (mask & (1 << 7)) ? r32(&b) : r16(&b);
+        rec->hdr.fid = (mask & (1 << 6)) ? r32(&b) : r16(&b);
+        rec->hdr.ts = r32(&b);
+        if (mask & (1 << 5)) {
+            rec->hdr.index = r16(&b);
+            rec->hdr.total = r16(&b);
+        } else {
+            rec->hdr.index = r8(&b);
+            rec->hdr.total = r8(&b);
+        }
+        rec->remb = (mask & (1 << 4)) ? 0 : 0xff;
+        rec->fec_id = r16(&b);
+        rec->send_ts = r16(&b);
+        rec->transport_seq = r16(&b);
+        uint16_t n = rdata(&b, payload, capacity);
+        if (n == 0xFFFF)
+            n = 0;
+        rec->data_size = n;
+        rec->hdr.size = n;
+        rec->status = RFEC_WIRE_OK;
+        return rec->status;
+    }
+    if (rec->mid == RFEC_WIRE_FEC) { /* sim_fec_decode, sim_proto.inl:287-307 */
+        rec->fec_id = r16(&b);
+        rec->row = r8(&b);
+        rec->col = r8(&b);
+        rec->index = r8(&b);
+        rec->count = r16(&b);
+        rec->base_id = r32(&b);
+        rec->transport_seq = r16(&b);
+        rec->send_ts = r32(&b);
+        rec->hdr.seq = r32(&b); /* sim_fec_meta_decode, :256-268 */
+        rec->hdr.fid = r32(&b);
+        rec->hdr.ts = r32(&b);
+        rec->hdr.index = r16(&b);
+        rec->hdr.total = r16(&b);
+        rec->hdr.ftype = r8(&b);
+        rec->hdr.payload_type = r8(&b);
+        rec->hdr.size = r16(&b);
+        uint16_t n = rdata(&b, payload, capacity);
+        if (n > capacity) {
+            rec->data_size = 0;
+            rec->status = RFEC_WIRE_EBODY;
+            return rec->status;
+        }
+        rec->data_size = n;
+        rec->status = RFEC_WIRE_OK;
+        return rec->status;
+    }
+    rec->status = RFEC_WIRE_OTHER;
+    return rec->status;
+}
+
+/* Batched forms over the product's device layout (include/razor_fec.h). */
+void oracle_wire_frame_fec_batch(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
+                                 const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,
+                                 const rfec_fec_stamp* stamps, uint32_t dstride, uint8_t* dgram, uint16_t* dlen)
+{
+    sim_fec_t* f = (sim_fec_t*)calloc(1, sizeof(sim_fec_t) + 65536);
+    for (size_t d = 0; d < count; ++d) {
+        uint8_t* out = dgram + d * dstride;
+        memset(out, 0, dstride);
+        if ((status && status[d] < 0) || fec_size[d] > capacity) {
+            dlen[d] = 0;
+            continue;
+        }
+        const rfec_fec_stamp* s = &stamps[d];
+        f->fec_id = s->fec_id;
+        f->row = s->row;
+        f->col = s->col;
+        f->index = s->index;
+        f->count = s->count;
+        f->base_id = s->base_id;
+        f->transport_seq = s->transport_seq;
+        f->send_ts = s->send_ts;
+        memcpy(&f->fec_meta, &meta[d], sizeof(rfec_hdr));
+        f->fec_data_size = fec_size[d];
+        memcpy(f->fec_data, parity + d * stride, fec_size[d]);
+        dlen[d] = (uint16_t)oracle_wire_frame_fec(f, s->uid, out);
+    }
+    free(f);
+}
+
+void oracle_wire_frame_seg_batch(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* shards,
+                                 const rfec_hdr* hdr, const rfec_seg_stamp* stamps, uint32_t dstride, uint8_t* dgram,
+                                 uint16_t* dlen)
+{
+    sim_segment_t* s = (sim_segment_t*)calloc(1, sizeof(sim_segment_t) + 65536);
+    for (size_t i = 0; i < count; ++i) {
+        uint8_t* out = dgram + i * dstride;
+        memset(out, 0, dstride);
+        const rfec_hdr* h = &hdr[i];
+        if (h->size > capacity) {
+            dlen[i] = 0;
+            continue;
+        }
+        s->packet_id = h->seq;
+        s->fid = h->fid;
+        s->timestamp = h->ts;
+        s->index = h->index;
+        s->total = h->total;
+        s->ftype = h->ftype;
+        s->payload_type = h->payload_type;
+        s->data_size = h->size;
+        s->fec_id = stamps[i].fec_id;
+        s->send_ts = stamps[i].send_ts;
+        s->transport_seq = stamps[i].transport_seq;
+        s->remb = stamps[i].remb;
+        memcpy(s->data, shards + i * stride, h->size);
+        dlen[i] = (uint16_t)oracle_wire_frame_seg(s, stamps[i].uid, out);
+    }
+    free(s);
+}
+
+void oracle_wire_parse_batch(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
+                             uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload)
+{
+    uint8_t* tmp = (uint8_t*)malloc(capacity + 1);
+    for (size_t i = 0; i < n; ++i) {
+        oracle_wire_parse(dgram + i * dstride, dlen[i], capacity, &recs[i], tmp);
+        memset(payload + i * stride, 0, stride);
+        memcpy(payload + i * stride, tmp, recs[i].data_size);
+    }
+    free(tmp);
+}

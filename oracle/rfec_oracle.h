@@ -66,6 +66,20 @@ long oracle_encode_aos_mt(const rfec_plan* plan, uint32_t groups, sim_segment_t*
 long oracle_recover_aos(const rfec_plan* plan, uint32_t groups, sim_segment_t* segs,
                         sim_fec_t* fecs, const uint64_t* present, sim_segment_t* out);
 
+/* wire codec (sim_proto.c, sim_proto.inl, cf_stream.c, cf_crc32.c) */
+uint32_t oracle_crc32(uint32_t crc, const void* buf, size_t size);
+size_t oracle_wire_frame_fec(const sim_fec_t* f, uint32_t uid, uint8_t* out);
+size_t oracle_wire_frame_seg(const sim_segment_t* s, uint32_t uid, uint8_t* out);
+int oracle_wire_parse(const uint8_t* d, size_t len, uint32_t capacity, rfec_wire_rec* rec, uint8_t* payload);
+void oracle_wire_frame_fec_batch(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
+                                 const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,
+                                 const rfec_fec_stamp* stamps, uint32_t dstride, uint8_t* dgram, uint16_t* dlen);
+void oracle_wire_frame_seg_batch(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* shards,
+                                 const rfec_hdr* hdr, const rfec_seg_stamp* stamps, uint32_t dstride, uint8_t* dgram,
+                                 uint16_t* dlen);
+void oracle_wire_parse_batch(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
+                             uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload);
+
 int oracle_sim_video_size(void);
 size_t oracle_segment_size(void);
 size_t oracle_fec_size(void);

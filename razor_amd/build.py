@@ -26,7 +26,7 @@ INCLUDE = ROOT / "include"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("RFEC_OFFLOAD_ARCH", "gfx950")
 
-HIP_SRC = [CSRC / "rfec_kernels.hip", CSRC / "rfec_probe.hip"]
+HIP_SRC = [CSRC / "rfec_kernels.hip", CSRC / "rfec_probe.hip", CSRC / "rfec_wire.hip"]
 C_SRC = [CSRC / "rfec_host.c"]
 HEADERS = [INCLUDE / "razor_fec.h", CSRC / "rfec_internal.h"]
 

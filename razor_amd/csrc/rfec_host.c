@@ -251,6 +251,71 @@ int rfec_zero_tails(uint32_t groups, uint32_t k, uint32_t stride, uint8_t* shard
 }
 
 /* ------------------------------------------------------------------------ */
+/* 2b. wire codec (sim_proto.c / sim_proto.inl), batched                     */
+/* ------------------------------------------------------------------------ */
+static int check_wire(uint32_t count, uint32_t stride, uint32_t capacity, uint32_t dstride, uint32_t overhead)
+{
+    if (stride == 0 || stride % 16 || stride > RFEC_WIRE_MAX_DSTRIDE)
+        return set_err(RFEC_EINVAL, "stride must be a positive multiple of 16, at most 2048", 0);
+    if (capacity > stride || capacity > 0xFFFE)
+        return set_err(RFEC_EINVAL, "capacity must be <= stride", 0);
+    if (dstride % 16 || dstride < 64 || dstride > RFEC_WIRE_MAX_DSTRIDE)
+        return set_err(RFEC_EINVAL, "dstride must be a multiple of 16 in [64, 2048]", 0);
+    if (overhead && capacity + overhead > dstride)
+        return set_err(RFEC_EINVAL, "dstride too small for capacity", 0);
+    if ((uint64_t)count * dstride > ((uint64_t)1 << 40))
+        return set_err(RFEC_EINVAL, "batch too large", 0);
+    return RFEC_OK;
+}
+
+int rfec_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
+                        const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,
+                        const rfec_fec_stamp* stamps, uint32_t dstride, uint8_t* dgram, uint16_t* dlen,
+                        void* stream)
+{
+    int rc = check_wire(count, stride, capacity, dstride, RFEC_WIRE_FEC_OVERHEAD);
+    if (rc)
+        return rc;
+    if (count == 0)
+        return RFEC_OK;
+    if (!parity || !meta || !fec_size || !stamps || !dgram || !dlen)
+        return set_err(RFEC_EINVAL, "NULL buffer", 0);
+    const int e = rfec_launch_wire_frame_fec(count, stride, capacity, parity, meta, fec_size, status, stamps,
+                                             dstride, dgram, dlen, stream);
+    return e ? set_err(RFEC_EDEVICE, "wire_frame_fec launch", e) : RFEC_OK;
+}
+
+int rfec_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* shards,
+                        const rfec_hdr* hdr, const rfec_seg_stamp* stamps, uint32_t dstride, uint8_t* dgram,
+                        uint16_t* dlen, void* stream)
+{
+    int rc = check_wire(count, stride, capacity, dstride, 36);
+    if (rc)
+        return rc;
+    if (count == 0)
+        return RFEC_OK;
+    if (!shards || !hdr || !stamps || !dgram || !dlen)
+        return set_err(RFEC_EINVAL, "NULL buffer", 0);
+    const int e = rfec_launch_wire_frame_seg(count, stride, capacity, shards, hdr, stamps, dstride, dgram, dlen,
+                                             stream);
+    return e ? set_err(RFEC_EDEVICE, "wire_frame_seg launch", e) : RFEC_OK;
+}
+
+int rfec_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen, uint32_t stride,
+                    uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload, void* stream)
+{
+    int rc = check_wire(n, stride, capacity, dstride, 0);
+    if (rc)
+        return rc;
+    if (n == 0)
+        return RFEC_OK;
+    if (!dgram || !dlen || !recs || !payload)
+        return set_err(RFEC_EINVAL, "NULL buffer", 0);
+    const int e = rfec_launch_wire_parse(n, dstride, dgram, dlen, stride, capacity, recs, payload, stream);
+    return e ? set_err(RFEC_EDEVICE, "wire_parse launch", e) : RFEC_OK;
+}
+
+/* ------------------------------------------------------------------------ */
 /* 3. drop-in single-call path                                               */
 /* ------------------------------------------------------------------------ */
 #define DI_STRIDE ((SIM_VIDEO_SIZE + 15) & ~15)

@@ -1,0 +1,612 @@
+// rfec_wire.hip -- CDNA4 (gfx950) kernels of the batched wire codec: SIM_FEC /
+// SIM_SEG datagrams with their CRC32 trailer, and the receive-side parse.
+//
+// Restated from the reference (yuanrongxi/razor):
+//   datagram = header (sim_proto.c:13-18) | body | crc32 BE (sim_proto.c:92-94)
+//   SIM_FEC body  sim_proto.inl:244-254, 270-285;  SIM_SEG body :83-125
+//   parse         sim_proto.c:21-37 (CRC check), sim_session.c:594 (mid range),
+//                 sim_proto.inl:127-179, 256-307; reads past the datagram end
+//                 yield 0 without advancing (cf_stream.c mach_*_read)
+//   crc32         cf_crc32.c:56-68, seed 0x0e3dfc0a (sim_proto.c:11)
+//
+// One wavefront per datagram; lane j owns bytes [32j, 32j+32) of it (so a
+// datagram slot is at most 2 KiB).  Payload bytes move through registers with
+// a wave-uniform byte funnel (no LDS staging); the header is assembled with
+// compile-time byte positions.  CRC32 is computed wave-parallel: each lane
+// takes the raw CRC of its 32 bytes with slice-by-16 tables in LDS, scales it
+// by x^(8e) mod P for the e bytes that follow its run (a 32-step carry-less
+// multiply, zlib's multmodp), and the wave XOR-reduces.  The CRC's initial
+// register is folded into the first four message bytes, so every lane runs
+// from a zero register.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rfec_internal.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr uint32_t kPoly = 0xEDB88320u; // reflected CRC-32 polynomial (cf_crc32.c table)
+constexpr int kXpBias = 32;              // xp[e + 32] = x^(8e) mod P, e in [-32, 2047]
+constexpr int kXpSize = 2080;
+
+struct CrcTables {
+    uint32_t t[16][256]; // t[s][b]: CRC register after byte b then s zero bytes, from 0
+    uint32_t xp[kXpSize];
+};
+
+constexpr uint32_t mul_x(uint32_t v) { return (v & 1u) ? (v >> 1) ^ kPoly : v >> 1; }
+constexpr uint32_t div_x(uint32_t y) { return (y & 0x80000000u) ? (((y ^ kPoly) << 1) | 1u) : (y << 1); }
+
+constexpr CrcTables make_crc_tables()
+{
+    CrcTables r{};
+    for (uint32_t b = 0; b < 256; ++b) {
+        uint32_t c = b;
+        for (int i = 0; i < 8; ++i)
+            c = mul_x(c);
+        r.t[0][b] = c;
+    }
+    for (int s = 1; s < 16; ++s)
+        for (uint32_t b = 0; b < 256; ++b)
+            r.t[s][b] = (r.t[s - 1][b] >> 8) ^ r.t[0][r.t[s - 1][b] & 0xffu];
+    uint32_t v = 0x80000000u; // the polynomial 1
+    r.xp[kXpBias] = v;
+    for (int i = kXpBias + 1; i < kXpSize; ++i) {
+        for (int q = 0; q < 8; ++q)
+            v = mul_x(v);
+        r.xp[i] = v;
+    }
+    v = 0x80000000u;
+    for (int i = kXpBias - 1; i >= 0; --i) {
+        for (int q = 0; q < 8; ++q)
+            v = div_x(v);
+        r.xp[i] = v;
+    }
+    return r;
+}
+
+__device__ const CrcTables kCrc = make_crc_tables();
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void load_tables(uint32_t* T)
+{
+    const v4u* s = reinterpret_cast<const v4u*>(&kCrc.t[0][0]);
+    v4u* d = reinterpret_cast<v4u*>(T);
+    for (int i = threadIdx.x; i < 16 * 256 / 4; i += kBlock)
+        d[i] = s[i];
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t tb(const uint32_t* T, int s, uint32_t byte) { return T[s * 256 + byte]; }
+
+// raw CRC (zero register) of 16 bytes given as LE dwords
+__device__ __forceinline__ uint32_t slice16(const uint32_t* T, uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+    return tb(T, 15, a & 0xff) ^ tb(T, 14, (a >> 8) & 0xff) ^ tb(T, 13, (a >> 16) & 0xff) ^ tb(T, 12, a >> 24) ^
+           tb(T, 11, b & 0xff) ^ tb(T, 10, (b >> 8) & 0xff) ^ tb(T, 9, (b >> 16) & 0xff) ^ tb(T, 8, b >> 24) ^
+           tb(T, 7, c & 0xff) ^ tb(T, 6, (c >> 8) & 0xff) ^ tb(T, 5, (c >> 16) & 0xff) ^ tb(T, 4, c >> 24) ^
+           tb(T, 3, d & 0xff) ^ tb(T, 2, (d >> 8) & 0xff) ^ tb(T, 1, (d >> 16) & 0xff) ^ tb(T, 0, d >> 24);
+}
+
+// a(x) * b(x) mod P in the reflected representation (zlib multmodp)
+__device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b)
+{
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        p ^= b & (0u - ((a >> (31 - i)) & 1u));
+        b = (b >> 1) ^ (kPoly & (0u - (b & 1u)));
+    }
+    return p;
+}
+
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+        v ^= (uint32_t)__shfl_xor((int)v, o, kWave);
+    return v;
+}
+
+// crc32(seed, msg[0:n)) (cf_crc32.c:56-68) of a message held lane-wise:
+// lane j has bytes [32j, 32j+32) in w (LE dwords), bytes >= n zero.
+__device__ uint32_t wave_crc32(const uint32_t* T, const uint32_t w[8], uint32_t n, uint32_t seed, uint32_t lane)
+{
+    if (n < 4) { // too short to fold the initial register into: bytewise
+        uint32_t r = ~seed;
+        for (uint32_t i = 0; i < n; ++i)
+            r = tb(T, 0, (r ^ (w[0] >> (8 * i))) & 0xffu) ^ (r >> 8);
+        return (uint32_t)__builtin_amdgcn_readfirstlane((int)~r);
+    }
+    uint32_t c = 0;
+    if (32u * lane < n) {
+        const uint32_t w0 = w[0] ^ (lane == 0 ? ~seed : 0u); // initial register folded into bytes 0-3
+        c = slice16(T, w0, w[1], w[2], w[3]);
+        c = slice16(T, w[4] ^ c, w[5], w[6], w[7]);
+        // x^(8e) for the e bytes after this lane's run (negative for the run
+        // holding the end: its zero padding is divided back out)
+        const int e = (int)n - 32 * (int)(lane + 1);
+        c = mulmod(c, kCrc.xp[e + kXpBias]);
+    }
+    return ~wave_xor(c);
+}
+
+// bytes [lo, hi) of the dword at byte position p0, as a byte mask
+__device__ __forceinline__ uint32_t range_mask(int p0, int lo, int hi)
+{
+    const int a = min(max(lo - p0, 0), 4), b = min(max(hi - p0, 0), 4);
+    const uint32_t fb = b >= 4 ? 0xffffffffu : (1u << (8 * b)) - 1u;
+    const uint32_t fa = a >= 4 ? 0xffffffffu : (1u << (8 * a)) - 1u;
+    return fb & ~fa;
+}
+
+// up to 4 LE bytes `fb` starting at byte position `pos`, seen from the dword at p0
+__device__ __forceinline__ uint32_t place(uint32_t fb, int pos, int p0)
+{
+    const int t = pos - p0;
+    if (t >= 4 || t <= -4)
+        return 0u;
+    return t >= 0 ? fb << (8 * t) : fb >> (-8 * t);
+}
+
+__device__ __forceinline__ uint32_t bswap(uint32_t v) { return __builtin_bswap32(v); }
+
+// Lane's 32 bytes of src[off + 32*lane, +32): src 16-B aligned, only chunks
+// below ceil(lim/16) are read (others read as 0); off is wave-uniform.
+__device__ __forceinline__ void load_shifted(const uint8_t* __restrict__ src, int off, uint32_t lim, uint32_t lane,
+                                             uint32_t out[8])
+{
+    const int s0 = off + 32 * (int)lane;
+    const int a = s0 >> 4; // floor
+    const uint32_t sh = (uint32_t)s0 & 15u;
+    const int nch = (int)((lim + 15u) >> 4);
+    const v4u* s = reinterpret_cast<const v4u*>(src);
+    const v4u z = v4u{0, 0, 0, 0};
+    const v4u c0 = (a >= 0 && a < nch) ? __builtin_nontemporal_load(s + a) : z;
+    const v4u c1 = (a + 1 >= 0 && a + 1 < nch) ? __builtin_nontemporal_load(s + a + 1) : z;
+    v4u c2;
+    // chunk a+2 is the next lane's c0
+    c2[0] = (uint32_t)__shfl_down((int)c0[0], 1, kWave);
+    c2[1] = (uint32_t)__shfl_down((int)c0[1], 1, kWave);
+    c2[2] = (uint32_t)__shfl_down((int)c0[2], 1, kWave);
+    c2[3] = (uint32_t)__shfl_down((int)c0[3], 1, kWave);
+    if (lane == kWave - 1)
+        c2 = (a + 2 >= 0 && a + 2 < nch) ? s[a + 2] : z;
+    const uint32_t x[12] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3], c2[0], c2[1], c2[2], c2[3]};
+    const uint32_t r = sh & 3u;
+    // q = sh >> 2 is wave-uniform: a uniform branch picks the dword window
+#define RFEC_FUNNEL(Q)                                                                         \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) out[k] =                                     \
+        __builtin_amdgcn_alignbyte(x[(Q) + k + 1], x[(Q) + k], r);
+    switch (sh >> 2) {
+    case 0: RFEC_FUNNEL(0) break;
+    case 1: RFEC_FUNNEL(1) break;
+    case 2: RFEC_FUNNEL(2) break;
+    default: RFEC_FUNNEL(3) break;
+    }
+#undef RFEC_FUNNEL
+}
+
+__device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t slot_bytes, uint32_t lane,
+                                           const uint32_t w[8])
+{
+    v4u* p = reinterpret_cast<v4u*>(slot + 32u * lane);
+    if (32u * lane < slot_bytes)
+        __builtin_nontemporal_store(v4u{w[0], w[1], w[2], w[3]}, p);
+    if (32u * lane + 16u < slot_bytes)
+        __builtin_nontemporal_store(v4u{w[4], w[5], w[6], w[7]}, p + 1);
+}
+
+// Header bytes at compile-time positions (big-endian fields, cf_stream.c:366-385)
+struct Hdr {
+    uint32_t h[12];
+};
+template <int POS, int NB>
+__device__ __forceinline__ void put(Hdr& b, uint32_t v)
+{
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int p = POS + i;
+        b.h[p >> 2] |= ((v >> (8 * (NB - 1 - i))) & 0xffu) << (8 * (p & 3));
+    }
+}
+
+// Assemble a datagram lane-wise: header bytes [0, hsize) from H, payload
+// [hsize, hsize+L) from pay, CRC32 BE at [hsize+L, hsize+L+4), zero after.
+__device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, uint32_t hsize, uint32_t L,
+                                             uint32_t pay[8], uint32_t lane, uint8_t* __restrict__ slot,
+                                             uint32_t dstride, uint16_t* dlen_out)
+{
+    uint32_t w[8];
+    const int n = (int)(hsize + L);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int p0 = 32 * (int)lane + 4 * k;
+        // header dwords live in lanes 0 and 1 (hsize <= 48)
+        const uint32_t hd = lane == 0 ? H.h[k] : (lane == 1 && k < 4 ? H.h[8 + k] : 0u);
+        w[k] = (pay[k] & range_mask(p0, (int)hsize, n)) | (hd & range_mask(p0, 0, (int)hsize));
+    }
+    const uint32_t crc = wave_crc32(T, w, (uint32_t)n, RFEC_WIRE_CRC_SEED, lane);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        w[k] |= place(bswap(crc), n, 32 * (int)lane + 4 * k);
+    store_slot(slot, dstride, lane, w);
+    if (lane == 0)
+        *dlen_out = (uint16_t)(n + 4);
+}
+
+__device__ __forceinline__ void zero_slot(uint8_t* __restrict__ slot, uint32_t dstride, uint32_t lane, uint16_t* dlen_out)
+{
+    const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    store_slot(slot, dstride, lane, z);
+    if (lane == 0)
+        *dlen_out = 0;
+}
+
+__device__ __forceinline__ uint32_t wave_id()
+{
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+}
+
+struct FecFrameArgs {
+    const uint8_t* parity;
+    const rfec_hdr* meta;
+    const uint16_t* fsize;
+    const int8_t* status;
+    const rfec_fec_stamp* stamps;
+    uint8_t* dgram;
+    uint16_t* dlen;
+    uint32_t count, stride, capacity, dstride;
+};
+
+// SIM_FEC: 45-byte header (sim_proto.c:13-18, sim_proto.inl:244-254, 270-283)
+__global__ __launch_bounds__(kBlock) void k_frame_fec(FecFrameArgs A)
+{
+    __shared__ uint32_t T[16 * 256];
+    load_tables(T);
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    for (uint32_t d = wave_id(); d < A.count; d += nw) {
+        uint8_t* slot = A.dgram + (size_t)d * A.dstride;
+        const uint32_t L = A.fsize[d];
+        const int st = A.status ? A.status[d] : 0;
+        if (st < 0 || L > A.capacity) {
+            zero_slot(slot, A.dstride, lane, A.dlen + d);
+            continue;
+        }
+        const rfec_fec_stamp s = A.stamps[d];
+        const rfec_hdr m = A.meta[d];
+        Hdr H = {};
+        put<0, 1>(H, RFEC_WIRE_VER);
+        put<1, 1>(H, RFEC_WIRE_FEC);
+        put<2, 4>(H, s.uid);
+        put<6, 2>(H, s.fec_id);
+        put<8, 1>(H, s.row);
+        put<9, 1>(H, s.col);
+        put<10, 1>(H, s.index);
+        put<11, 2>(H, s.count);
+        put<13, 4>(H, s.base_id);
+        put<17, 2>(H, s.transport_seq);
+        put<19, 4>(H, s.send_ts);
+        put<23, 4>(H, m.seq);
+        put<27, 4>(H, m.fid);
+        put<31, 4>(H, m.ts);
+        put<35, 2>(H, m.index);
+        put<37, 2>(H, m.total);
+        put<39, 1>(H, m.ftype);
+        put<40, 1>(H, m.payload_type);
+        put<41, 2>(H, m.size);
+        put<43, 2>(H, L); // mach_data_write length (cf_stream.c:328-337)
+        uint32_t pay[8];
+        load_shifted(A.parity + (size_t)d * A.stride, -45, L, lane, pay);
+        finish_frame(T, H, 45, L, pay, lane, slot, A.dstride, A.dlen + d);
+    }
+}
+
+struct SegFrameArgs {
+    const uint8_t* shards;
+    const rfec_hdr* hdr;
+    const rfec_seg_stamp* stamps;
+    uint8_t* dgram;
+    uint16_t* dlen;
+    uint32_t count, stride, capacity, dstride;
+};
+
+// SIM_SEG header, one of 8 layouts (sim_proto.inl:83-125): PW / FW = 4-byte
+// packet_id / fid, TW = 2-byte index and total.  Returns the header size.
+template <bool PW, bool FW, bool TW>
+__device__ __forceinline__ uint32_t seg_header(Hdr& H, const rfec_hdr& h, const rfec_seg_stamp& s)
+{
+    constexpr int P1 = 8 + (PW ? 4 : 2);  // after packet_id
+    constexpr int P2 = P1 + (FW ? 4 : 2); // after fid
+    constexpr int P3 = P2 + 4;            // after timestamp
+    constexpr int P4 = P3 + (TW ? 4 : 2); // after index, total
+    const uint32_t mask = (h.ftype & 1u) | (PW ? 0x80u : 0u) | (FW ? 0x40u : 0u) | (TW ? 0x20u : 0u) |
+                          (s.remb == 0 ? 0x10u : 0u);
+    put<0, 1>(H, RFEC_WIRE_VER);
+    put<1, 1>(H, RFEC_WIRE_SEG);
+    put<2, 4>(H, s.uid);
+    put<6, 1>(H, mask);
+    put<7, 1>(H, h.payload_type);
+    put<8, PW ? 4 : 2>(H, h.seq);
+    put<P1, FW ? 4 : 2>(H, h.fid);
+    put<P2, 4>(H, h.ts);
+    if constexpr (TW) {
+        put<P3, 2>(H, h.index);
+        put<P3 + 2, 2>(H, h.total);
+    } else {
+        put<P3, 1>(H, h.index);
+        put<P3 + 1, 1>(H, h.total);
+    }
+    put<P4, 2>(H, s.fec_id);
+    put<P4 + 2, 2>(H, s.send_ts);
+    put<P4 + 4, 2>(H, s.transport_seq);
+    put<P4 + 6, 2>(H, h.size);
+    return P4 + 8;
+}
+
+__global__ __launch_bounds__(kBlock) void k_frame_seg(SegFrameArgs A)
+{
+    __shared__ uint32_t T[16 * 256];
+    load_tables(T);
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    for (uint32_t d = wave_id(); d < A.count; d += nw) {
+        uint8_t* slot = A.dgram + (size_t)d * A.dstride;
+        const rfec_hdr h = A.hdr[d];
+        const uint32_t L = h.size;
+        if (L > A.capacity) {
+            zero_slot(slot, A.dstride, lane, A.dlen + d);
+            continue;
+        }
+        const rfec_seg_stamp s = A.stamps[d];
+        Hdr H = {};
+        const uint32_t layout = (h.seq > 65535u ? 4u : 0u) | (h.fid > 65535u ? 2u : 0u) | (h.total > 255u ? 1u : 0u);
+        uint32_t hs;
+        switch (layout) {
+        case 0: hs = seg_header<false, false, false>(H, h, s); break;
+        case 1: hs = seg_header<false, false, true>(H, h, s); break;
+        case 2: hs = seg_header<false, true, false>(H, h, s); break;
+        case 3: hs = seg_header<false, true, true>(H, h, s); break;
+        case 4: hs = seg_header<true, false, false>(H, h, s); break;
+        case 5: hs = seg_header<true, false, true>(H, h, s); break;
+        case 6: hs = seg_header<true, true, false>(H, h, s); break;
+        default: hs = seg_header<true, true, true>(H, h, s); break;
+        }
+        uint32_t pay[8];
+        load_shifted(A.shards + (size_t)d * A.stride, -(int)hs, L, lane, pay);
+        finish_frame(T, H, hs, L, pay, lane, slot, A.dstride, A.dlen + d);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Parse (receive side)
+// ---------------------------------------------------------------------------
+struct ParseArgs {
+    const uint8_t* dgram;
+    const uint16_t* dlen;
+    rfec_wire_rec* recs;
+    uint8_t* payload;
+    uint32_t n, dstride, stride, capacity;
+};
+
+// bin_stream reader over the first 64 bytes of the datagram (staged in LDS);
+// a read past `used` yields 0 and does not advance (cf_stream.c mach_*_read)
+struct Cursor {
+    const volatile uint8_t* b;
+    uint32_t used, pos;
+    __device__ uint32_t r8()
+    {
+        if (used < pos + 1)
+            return 0;
+        return b[pos++];
+    }
+    __device__ uint32_t r16()
+    {
+        if (used < pos + 2)
+            return 0;
+        const uint32_t v = (uint32_t)b[pos] << 8 | b[pos + 1];
+        pos += 2;
+        return v;
+    }
+    __device__ uint32_t r32()
+    {
+        if (used < pos + 4)
+            return 0;
+        const uint32_t v = (uint32_t)b[pos] << 24 | (uint32_t)b[pos + 1] << 16 | (uint32_t)b[pos + 2] << 8 | b[pos + 3];
+        pos += 4;
+        return v;
+    }
+};
+
+__device__ __forceinline__ void write_rec(rfec_wire_rec* r, const rfec_wire_rec& v, uint32_t lane)
+{
+    if (lane == 0) {
+        const v4u* s = reinterpret_cast<const v4u*>(&v);
+        v4u* d = reinterpret_cast<v4u*>(r);
+        d[0] = s[0];
+        d[1] = s[1];
+        d[2] = s[2];
+        d[3] = s[3];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_parse(ParseArgs A)
+{
+    __shared__ uint32_t T[16 * 256];
+    __shared__ uint32_t stage[kWavesPerBlock][16]; // first 64 bytes of each wave's datagram
+    load_tables(T);
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t wl = threadIdx.x >> 6;
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    for (uint32_t d = wave_id(); d < A.n; d += nw) {
+        const uint8_t* dg = A.dgram + (size_t)d * A.dstride;
+        uint8_t* slot = A.payload + (size_t)d * A.stride;
+        const uint32_t len = A.dlen[d];
+        rfec_wire_rec rec = {};
+        const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (len < 4 || len > A.dstride) {
+            rec.status = RFEC_WIRE_EBADCRC;
+            write_rec(A.recs + d, rec, lane);
+            store_slot(slot, A.stride, lane, z);
+            continue;
+        }
+        // datagram bytes [32j, 32j+32), zero from `len` on
+        uint32_t w[8];
+        load_shifted(dg, 0, len, lane, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            w[k] &= range_mask(32 * (int)lane + 4 * k, 0, (int)len);
+        if (lane < 2) {
+            volatile uint32_t* sg = stage[wl];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                sg[8 * lane + k] = w[k];
+        }
+        // CRC over [0, len-4) against the big-endian trailer (sim_proto.c:21-37)
+        uint32_t m[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            m[k] = w[k] & range_mask(32 * (int)lane + 4 * k, 0, (int)len - 4);
+        const uint32_t crc = wave_crc32(T, m, len - 4, RFEC_WIRE_CRC_SEED, lane);
+        uint32_t tr = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            // trailer bytes seen from each dword, moved to their BE place
+            const int p0 = 32 * (int)lane + 4 * k;
+            const uint32_t t = w[k] & range_mask(p0, (int)len - 4, (int)len);
+            const int sft = p0 - ((int)len - 4); // byte offset of this dword within the trailer
+            if (sft > -4 && sft < 4)
+                tr |= sft >= 0 ? t << (8 * sft) : t >> (-8 * sft);
+        }
+        tr = bswap(wave_xor(tr));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (crc != tr) {
+            rec.status = RFEC_WIRE_EBADCRC;
+            write_rec(A.recs + d, rec, lane);
+            store_slot(slot, A.stride, lane, z);
+            continue;
+        }
+        Cursor c{reinterpret_cast<const volatile uint8_t*>(stage[wl]), len, 0};
+        rec.ver = (uint8_t)c.r8();
+        rec.mid = (uint8_t)c.r8();
+        rec.uid = c.r32();
+        int data_at = -1;
+        uint32_t dsize = 0;
+        if (rec.mid < RFEC_WIRE_MIN_MID || rec.mid > RFEC_WIRE_MAX_MID) {
+            rec.status = RFEC_WIRE_EMID;
+        } else if (rec.mid == RFEC_WIRE_SEG) { // sim_segment_decode, sim_proto.inl:127-179
+            const uint32_t mask = c.r8();
+            rec.hdr.payload_type = (uint8_t)c.r8();
+            rec.hdr.ftype = (uint8_t)(mask & 1u);
+            rec.hdr.seq = (mask & 0x80u) ? c.r32() : c.r16();
+            rec.hdr.fid = (mask & 0x40u) ? c.r32() : c.r16();
+            rec.hdr.ts = c.r32();
+            if (mask & 0x20u) {
+                rec.hdr.index = (uint16_t)c.r16();
+                rec.hdr.total = (uint16_t)c.r16();
+            } else {
+                rec.hdr.index = (uint16_t)c.r8();
+                rec.hdr.total = (uint16_t)c.r8();
+            }
+            rec.remb = (mask & 0x10u) ? 0 : 0xff;
+            rec.fec_id = (uint16_t)c.r16();
+            rec.send_ts = c.r16();
+            rec.transport_seq = (uint16_t)c.r16();
+            const uint32_t n = c.r16(); // mach_data_read, cf_stream.c:339-355
+            if (n <= A.capacity && c.pos + n <= len) {
+                data_at = (int)c.pos;
+                dsize = n;
+            }
+            rec.status = RFEC_WIRE_OK; // a bad length leaves data_size 0 (:174-176)
+        } else if (rec.mid == RFEC_WIRE_FEC) { // sim_fec_decode, sim_proto.inl:287-307
+            rec.fec_id = (uint16_t)c.r16();
+            rec.row = (uint8_t)c.r8();
+            rec.col = (uint8_t)c.r8();
+            rec.index = (uint8_t)c.r8();
+            rec.count = (uint16_t)c.r16();
+            rec.base_id = c.r32();
+            rec.transport_seq = (uint16_t)c.r16();
+            rec.send_ts = c.r32();
+            rec.hdr.seq = c.r32();
+            rec.hdr.fid = c.r32();
+            rec.hdr.ts = c.r32();
+            rec.hdr.index = (uint16_t)c.r16();
+            rec.hdr.total = (uint16_t)c.r16();
+            rec.hdr.ftype = (uint8_t)c.r8();
+            rec.hdr.payload_type = (uint8_t)c.r8();
+            rec.hdr.size = (uint16_t)c.r16();
+            const uint32_t n = c.r16();
+            if (n <= A.capacity && c.pos + n <= len) {
+                data_at = (int)c.pos;
+                dsize = n;
+                rec.status = RFEC_WIRE_OK;
+            } else {
+                rec.status = RFEC_WIRE_EBODY;
+            }
+        } else {
+            rec.status = RFEC_WIRE_OTHER;
+        }
+        rec.data_size = (uint16_t)dsize;
+        if (rec.mid == RFEC_WIRE_SEG && rec.status == RFEC_WIRE_OK)
+            rec.hdr.size = (uint16_t)dsize;
+        write_rec(A.recs + d, rec, lane);
+        if (data_at < 0) {
+            store_slot(slot, A.stride, lane, z);
+            continue;
+        }
+        uint32_t pay[8];
+        load_shifted(dg, data_at, (uint32_t)data_at + dsize, lane, pay);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            pay[k] &= range_mask(32 * (int)lane + 4 * k, 0, (int)dsize);
+        store_slot(slot, A.stride, lane, pay);
+    }
+}
+
+uint32_t grid_for(uint32_t count)
+{
+    const uint32_t blocks = (count + kWavesPerBlock - 1) / kWavesPerBlock;
+    return blocks < 2048u ? (blocks ? blocks : 1u) : 2048u;
+}
+
+} // namespace
+
+extern "C" {
+
+int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
+                               const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,
+                               const rfec_fec_stamp* stamps, uint32_t dstride, uint8_t* dgram, uint16_t* dlen,
+                               void* stream)
+{
+    const FecFrameArgs A = {parity, meta, fec_size, status, stamps, dgram, dlen, count, stride, capacity, dstride};
+    hipLaunchKernelGGL(k_frame_fec, dim3(grid_for(count)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
+                       A);
+    return (int)hipGetLastError();
+}
+
+int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* shards,
+                               const rfec_hdr* hdr, const rfec_seg_stamp* stamps, uint32_t dstride, uint8_t* dgram,
+                               uint16_t* dlen, void* stream)
+{
+    const SegFrameArgs A = {shards, hdr, stamps, dgram, dlen, count, stride, capacity, dstride};
+    hipLaunchKernelGGL(k_frame_seg, dim3(grid_for(count)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
+                       A);
+    return (int)hipGetLastError();
+}
+
+int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
+                           uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload, void* stream)
+{
+    const ParseArgs A = {dgram, dlen, recs, payload, n, dstride, stride, capacity};
+    hipLaunchKernelGGL(k_parse, dim3(grid_for(n)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), A);
+    return (int)hipGetLastError();
+}
+
+} // extern "C"

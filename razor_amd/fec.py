@@ -46,6 +46,21 @@ HDR_DTYPE = np.dtype([("seq", "<u4"), ("fid", "<u4"), ("ts", "<u4"), ("index", "
                       ("ftype", "u1"), ("payload_type", "u1"), ("size", "<u2")])
 assert HDR_DTYPE.itemsize == 20
 
+# wire codec records (include/razor_fec.h)
+RFEC_WIRE_SEG = 0x17
+RFEC_WIRE_FEC = 0x1C
+RFEC_WIRE_FEC_OVERHEAD = 49
+FEC_STAMP_DTYPE = np.dtype([("uid", "<u4"), ("base_id", "<u4"), ("send_ts", "<u4"), ("fec_id", "<u2"),
+                            ("count", "<u2"), ("transport_seq", "<u2"), ("row", "u1"), ("col", "u1"), ("index", "u1"),
+                            ("reserved", "u1"), ("pad", "u1", (2,))])
+SEG_STAMP_DTYPE = np.dtype([("uid", "<u4"), ("fec_id", "<u2"), ("send_ts", "<u2"), ("transport_seq", "<u2"),
+                            ("remb", "u1"), ("reserved", "u1")])
+WIRE_REC_DTYPE = np.dtype([("status", "i1"), ("ver", "u1"), ("mid", "u1"), ("remb", "u1"), ("uid", "<u4"),
+                           ("hdr", HDR_DTYPE), ("base_id", "<u4"), ("send_ts", "<u4"), ("fec_id", "<u2"),
+                           ("count", "<u2"), ("transport_seq", "<u2"), ("data_size", "<u2"), ("row", "u1"),
+                           ("col", "u1"), ("index", "u1"), ("reserved", "u1", (17,))])
+assert FEC_STAMP_DTYPE.itemsize == 24 and SEG_STAMP_DTYPE.itemsize == 12 and WIRE_REC_DTYPE.itemsize == 64
+
 
 class RfecError(RuntimeError):
     pass
@@ -136,6 +151,10 @@ _SIGS = {
     "rfec_recover_batch": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, C.c_uint32, C.c_uint32,
                                      _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rfec_zero_tails": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    "rfec_wire_frame_fec": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint32, _P, _P,
+                                      _P]),
+    "rfec_wire_frame_seg": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_uint32, _P, _P, _P]),
+    "rfec_wire_parse": (C.c_int, [C.c_uint32, C.c_uint32, _P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
     "rfec_set_tuning": (None, [C.c_uint]),
     "rfec_get_tuning": (C.c_uint, []),
     "rfec_last_error": (C.c_char_p, []),
@@ -227,6 +246,20 @@ class Native:
 
     def zero_tails(self, groups, k, stride, shards, hdr, stream=None):
         self._check(self.lib.rfec_zero_tails(groups, k, stride, shards, hdr, stream), "rfec_zero_tails")
+
+    # -- wire codec (device pointers) -------------------------------------------
+    def wire_frame_fec(self, count, stride, capacity, parity, meta, fec_size, status, stamps, dstride, dgram, dlen,
+                       stream=None):
+        self._check(self.lib.rfec_wire_frame_fec(count, stride, capacity, parity, meta, fec_size, status, stamps,
+                                                 dstride, dgram, dlen, stream), "rfec_wire_frame_fec")
+
+    def wire_frame_seg(self, count, stride, capacity, shards, hdr, stamps, dstride, dgram, dlen, stream=None):
+        self._check(self.lib.rfec_wire_frame_seg(count, stride, capacity, shards, hdr, stamps, dstride, dgram, dlen,
+                                                 stream), "rfec_wire_frame_seg")
+
+    def wire_parse(self, n, dstride, dgram, dlen, stride, capacity, recs, payload, stream=None):
+        self._check(self.lib.rfec_wire_parse(n, dstride, dgram, dlen, stride, capacity, recs, payload, stream),
+                    "rfec_wire_parse")
 
     def set_tuning(self, flags: int):
         self.lib.rfec_set_tuning(flags)

@@ -65,3 +65,47 @@ class GpuEngine:
             self.lib.set_tuning(0)
         return (_host(d_sh, np.uint8, (G, k, stride)), _host(d_h, HDR_DTYPE, (G, k)),
                 _host(d_rec, np.uint64, (G, 2)))
+
+
+class GpuWire:
+    """The wire codec (rfec_wire_*) on numpy inputs."""
+
+    def __init__(self, video_size=1000, device="cuda:0"):
+        self.lib = native(video_size)
+        self.device = torch.device(device)
+
+    def _run(self, fn, *args):
+        fn(*args, torch.cuda.current_stream(self.device).cuda_stream)
+        torch.cuda.synchronize(self.device)
+
+    def frame_fec(self, parity, meta, fsize, status, stamps, capacity, dstride):
+        N, stride = parity.shape[0] if parity.ndim == 2 else parity.size // parity.shape[-1], parity.shape[-1]
+        d_p, d_m, d_f, d_s = (_dev(a, self.device) for a in (parity, meta, np.ascontiguousarray(fsize, np.uint16),
+                                                                stamps))
+        d_st = None if status is None else _dev(np.ascontiguousarray(status, np.int8), self.device)
+        d_g = torch.full((N * dstride,), 0xEE, dtype=torch.uint8, device=self.device)
+        d_l = torch.full((N,), 0x7777, dtype=torch.int16, device=self.device)
+        self._run(self.lib.wire_frame_fec, N, stride, capacity, d_p.data_ptr(), d_m.data_ptr(), d_f.data_ptr(),
+                  None if d_st is None else d_st.data_ptr(), d_s.data_ptr(), dstride, d_g.data_ptr(), d_l.data_ptr())
+        return _host(d_g, np.uint8, (N, dstride)), _host(d_l, np.uint16, (N,))
+
+    def frame_seg(self, shards, hdr, stamps, capacity, dstride):
+        stride = shards.shape[-1]
+        N = shards.size // stride
+        d_d, d_h, d_s = (_dev(a, self.device) for a in (shards, hdr, stamps))
+        d_g = torch.full((N * dstride,), 0xEE, dtype=torch.uint8, device=self.device)
+        d_l = torch.full((N,), 0x7777, dtype=torch.int16, device=self.device)
+        self._run(self.lib.wire_frame_seg, N, stride, capacity, d_d.data_ptr(), d_h.data_ptr(), d_s.data_ptr(),
+                  dstride, d_g.data_ptr(), d_l.data_ptr())
+        return _host(d_g, np.uint8, (N, dstride)), _host(d_l, np.uint16, (N,))
+
+    def parse(self, dgram, dlen, stride, capacity):
+        N, dstride = dgram.shape
+        d_g = _dev(dgram, self.device)
+        d_l = _dev(np.ascontiguousarray(dlen, np.uint16), self.device)
+        d_r = torch.full((N * 64,), 0xEE, dtype=torch.uint8, device=self.device)
+        d_p = torch.full((N * stride,), 0xEE, dtype=torch.uint8, device=self.device)
+        self._run(self.lib.wire_parse, N, dstride, d_g.data_ptr(), d_l.data_ptr(), stride, capacity, d_r.data_ptr(),
+                  d_p.data_ptr())
+        from razor_amd.fec import WIRE_REC_DTYPE
+        return _host(d_r, WIRE_REC_DTYPE, (N,)), _host(d_p, np.uint8, (N, stride))

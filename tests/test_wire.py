@@ -1,0 +1,144 @@
+"""Wire codec (SIM_FEC / SIM_SEG datagrams + CRC32, sim_proto.c / sim_proto.inl):
+the oracle against the reference's own encoder/decoder outputs
+(tests/golden/wire_*.bin from oracle/gen_wire.c), then the HIP kernels against
+the same fixtures and against the oracle on large random batches."""
+from __future__ import annotations
+
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+import pyoracle as po
+import wire_cases as wc
+
+
+class OracleWire:
+    def __init__(self, o):
+        self.o = o
+
+    def frame_fec(self, parity, meta, fsize, status, stamps, capacity, dstride):
+        return self.o.frame_fec_batch(parity, meta, fsize, status, stamps, capacity, dstride)
+
+    def frame_seg(self, shards, hdr, stamps, capacity, dstride):
+        return self.o.frame_seg_batch(shards, hdr, stamps, capacity, dstride)
+
+    def parse(self, dgram, dlen, stride, capacity):
+        return self.o.parse_batch(dgram, dlen, stride, capacity)
+
+
+# -- CPU: oracle pinned to the reference ---------------------------------------
+def test_wire_crc_is_zlib_crc32_with_seed(oracle1000):
+    """cf_crc32.c:56-68 == zlib crc32 continued from 0x0e3dfc0a; every fixture
+    datagram ends in it, big-endian (sim_proto.c:92-94)."""
+    for r, f in po.load_wire_fec() + po.load_wire_seg():
+        d = f["dgram"].tobytes()
+        c = zlib.crc32(d[:-4], po.CRC_SEED)
+        assert int.from_bytes(d[-4:], "big") == c == oracle1000.crc32(d[:-4])
+    for n in range(0, 9):
+        d = bytes(range(n))
+        assert oracle1000.crc32(d) == zlib.crc32(d, po.CRC_SEED)
+
+
+def test_wire_frame_fec_oracle(oracle1000):
+    wc.check_frame_fec(OracleWire(oracle1000))
+
+
+def test_wire_frame_seg_oracle(oracle1000):
+    wc.check_frame_seg(OracleWire(oracle1000))
+
+
+def test_wire_parse_oracle(oracle1000):
+    wc.check_parse(OracleWire(oracle1000))
+
+
+def test_wire_fixture_coverage():
+    m = po.wire_manifest()
+    assert m["sim_video_size"] == wc.CAP and m["crc_seed"] == po.CRC_SEED
+    kinds = np.array([int(r["kind"]) for r, _ in po.load_wire_parse()])
+    assert set(kinds.tolist()) == set(range(7))
+    segs = po.load_wire_seg()
+    masks = {(r["packet_id"] > 65535, r["fid"] > 65535, r["total"] > 255, r["remb"] == 0) for r, _ in segs}
+    assert len(masks) == 16  # every header-width / remb combination (sim_proto.inl:85-98)
+
+
+def test_wire_short_datagram_oracle(oracle1000):
+    """Shorter than the CRC trailer: rejected (the reference would read before its buffer)."""
+    dgram = np.zeros((4, 64), np.uint8)
+    recs, _ = oracle1000.parse_batch(dgram, np.array([0, 1, 2, 3], np.uint16), wc.STRIDE, wc.CAP)
+    assert (recs["status"] == -1).all()
+
+
+# -- GPU -----------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def gwire():
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the -m gpu suite must run on an MI355X")
+    from gpu_engine import GpuWire
+    return GpuWire()
+
+
+@pytest.mark.gpu
+def test_wire_frame_fec_gpu(gwire):
+    wc.check_frame_fec(gwire)
+
+
+@pytest.mark.gpu
+def test_wire_frame_seg_gpu(gwire):
+    wc.check_frame_seg(gwire)
+
+
+@pytest.mark.gpu
+def test_wire_parse_gpu(gwire):
+    wc.check_parse(gwire)
+
+
+@pytest.mark.gpu
+def test_wire_short_datagram_gpu(gwire):
+    dgram = np.full((5, 64), 0xAB, np.uint8)
+    recs, pay = gwire.parse(dgram, np.array([0, 1, 2, 3, 4], np.uint16), wc.STRIDE, wc.CAP)
+    assert (recs["status"][:4] == -1).all() and not pay.any()
+    # 4 bytes: an empty message whose trailer must equal crc32(seed, "") = seed
+    d = np.zeros((1, 64), np.uint8)
+    d[0, :4] = np.frombuffer(po.CRC_SEED.to_bytes(4, "big"), np.uint8)
+    recs, _ = gwire.parse(d, np.array([4], np.uint16), wc.STRIDE, wc.CAP)
+    # CRC accepted; ver/mid then read the trailer bytes themselves (0x0e, 0x3d): mid out of range
+    assert recs["status"][0] == -2 and recs["ver"][0] == 0x0E and recs["mid"][0] == 0x3D
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("capacity,stride", [(1000, 1008), (1200, 1200), (256, 256), (2000, 2000)])
+def test_wire_random_roundtrip_gpu(gwire, oracle1000, capacity, stride):
+    """Large random batches: HIP framing == oracle framing byte for byte, and
+    HIP parse(HIP frame(x)) returns x (fields, payload, zero tails)."""
+    rng = np.random.default_rng(capacity)
+    N = 20000
+    for seg in (False, True):
+        data, hdr, sizes, stamps = wc.random_batch(rng, N, stride, capacity, seg=seg)
+        over = 36 if seg else 49
+        dstride = min(2048, (capacity + over + 15) // 16 * 16)
+        if seg:
+            g, gl = gwire.frame_seg(data, hdr, stamps, capacity, dstride)
+            o, ol = oracle1000.frame_seg_batch(data, hdr, stamps, capacity, dstride)
+        else:
+            g, gl = gwire.frame_fec(data, hdr, sizes, None, stamps, capacity, dstride)
+            o, ol = oracle1000.frame_fec_batch(data, hdr, sizes, None, stamps, capacity, dstride)
+        assert np.array_equal(gl, ol)
+        assert np.array_equal(g, o)
+        recs, pay = gwire.parse(g, gl, stride, capacity)
+        orecs, opay = oracle1000.parse_batch(g, gl, stride, capacity)
+        assert np.array_equal(recs.view(np.uint8), orecs.view(np.uint8))
+        assert np.array_equal(pay, opay)
+        assert (recs["status"] == 0).all()
+        assert np.array_equal(recs["data_size"], sizes)
+        assert np.array_equal(pay, data)
+        assert np.array_equal(recs["uid"], stamps["uid"])
+        assert np.array_equal(recs["transport_seq"], stamps["transport_seq"])
+        if seg:
+            assert np.array_equal(recs["hdr"]["seq"], hdr["seq"]) and np.array_equal(recs["hdr"]["fid"], hdr["fid"])
+            assert np.array_equal(recs["hdr"]["ftype"], hdr["ftype"] & 1)
+            assert np.array_equal(recs["remb"], np.where(stamps["remb"] == 0, 0, 0xFF))
+        else:
+            assert recs["hdr"].tobytes() == hdr.tobytes()
+            assert np.array_equal(recs["base_id"], stamps["base_id"])
