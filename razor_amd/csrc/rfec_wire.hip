@@ -155,40 +155,38 @@ __device__ __forceinline__ uint32_t place(uint32_t fb, int pos, int p0)
 
 __device__ __forceinline__ uint32_t bswap(uint32_t v) { return __builtin_bswap32(v); }
 
-// Lane's 32 bytes of src[off + 32*lane, +32): src 16-B aligned, only chunks
-// below ceil(lim/16) are read (others read as 0); off is wave-uniform.
-__device__ __forceinline__ void load_shifted(const uint8_t* __restrict__ src, int off, uint32_t lim, uint32_t lane,
-                                             uint32_t out[8])
+// Three consecutive 16-B chunks of a slot, starting at chunk `a` (may be
+// negative); chunks outside [0, nch) read as 0.  Lane-private window.
+struct Win {
+    v4u c[3];
+};
+__device__ __forceinline__ Win load_win(const uint8_t* __restrict__ src, int a, int nch)
 {
-    const int s0 = off + 32 * (int)lane;
-    const int a = s0 >> 4; // floor
-    const uint32_t sh = (uint32_t)s0 & 15u;
-    const int nch = (int)((lim + 15u) >> 4);
     const v4u* s = reinterpret_cast<const v4u*>(src);
-    const v4u z = v4u{0, 0, 0, 0};
-    const v4u c0 = (a >= 0 && a < nch) ? __builtin_nontemporal_load(s + a) : z;
-    const v4u c1 = (a + 1 >= 0 && a + 1 < nch) ? __builtin_nontemporal_load(s + a + 1) : z;
-    v4u c2;
-    // chunk a+2 is the next lane's c0
-    c2[0] = (uint32_t)__shfl_down((int)c0[0], 1, kWave);
-    c2[1] = (uint32_t)__shfl_down((int)c0[1], 1, kWave);
-    c2[2] = (uint32_t)__shfl_down((int)c0[2], 1, kWave);
-    c2[3] = (uint32_t)__shfl_down((int)c0[3], 1, kWave);
-    if (lane == kWave - 1)
-        c2 = (a + 2 >= 0 && a + 2 < nch) ? s[a + 2] : z;
-    const uint32_t x[12] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3], c2[0], c2[1], c2[2], c2[3]};
-    const uint32_t r = sh & 3u;
-    // q = sh >> 2 is wave-uniform: a uniform branch picks the dword window
-#define RFEC_FUNNEL(Q)                                                                         \
-    _Pragma("unroll") for (int k = 0; k < 8; ++k) out[k] =                                     \
-        __builtin_amdgcn_alignbyte(x[(Q) + k + 1], x[(Q) + k], r);
-    switch (sh >> 2) {
-    case 0: RFEC_FUNNEL(0) break;
-    case 1: RFEC_FUNNEL(1) break;
-    case 2: RFEC_FUNNEL(2) break;
-    default: RFEC_FUNNEL(3) break;
-    }
-#undef RFEC_FUNNEL
+    Win w;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        w.c[i] = (a + i >= 0 && a + i < nch) ? __builtin_nontemporal_load(s + a + i) : v4u{0, 0, 0, 0};
+    return w;
+}
+
+// out[k] = dword k of the window shifted down by `sh` bytes (sh in [0, 16])
+template <int SH>
+__device__ __forceinline__ void funnel_c(const Win& w, uint32_t out[8])
+{
+    const uint32_t x[12] = {w.c[0][0], w.c[0][1], w.c[0][2], w.c[0][3], w.c[1][0], w.c[1][1],
+                            w.c[1][2], w.c[1][3], w.c[2][0], w.c[2][1], w.c[2][2], w.c[2][3]};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        out[k] = (SH & 3) ? __builtin_amdgcn_alignbyte(x[(SH >> 2) + k + 1], x[(SH >> 2) + k], SH & 3)
+                          : x[(SH >> 2) + k];
+}
+
+// byte mask of the first `keep` bytes of a dword (keep clamped to [0, 4])
+__device__ __forceinline__ uint32_t keep_mask(int keep)
+{
+    keep = min(max(keep, 0), 4);
+    return keep >= 4 ? 0xffffffffu : ~(0xffffffffu << (8 * keep));
 }
 
 __device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t slot_bytes, uint32_t lane,
@@ -215,25 +213,24 @@ __device__ __forceinline__ void put(Hdr& b, uint32_t v)
     }
 }
 
-// Assemble a datagram lane-wise: header bytes [0, hsize) from H, payload
-// [hsize, hsize+L) from pay, CRC32 BE at [hsize+L, hsize+L+4), zero after.
-__device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, uint32_t hsize, uint32_t L,
-                                             uint32_t pay[8], uint32_t lane, uint8_t* __restrict__ slot,
-                                             uint32_t dstride, uint16_t* dlen_out)
+// Datagram of header H (bytes [0, hsize), zero beyond) and payload `pay`
+// (zero below hsize): mask at n = hsize + L, CRC32 BE at [n, n+4), store.
+__device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, uint32_t n, uint32_t pay[8],
+                                             uint32_t lane, uint8_t* __restrict__ slot, uint32_t dstride,
+                                             uint16_t* dlen_out)
 {
     uint32_t w[8];
-    const int n = (int)(hsize + L);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const int p0 = 32 * (int)lane + 4 * k;
         // header dwords live in lanes 0 and 1 (hsize <= 48)
         const uint32_t hd = lane == 0 ? H.h[k] : (lane == 1 && k < 4 ? H.h[8 + k] : 0u);
-        w[k] = (pay[k] & range_mask(p0, (int)hsize, n)) | (hd & range_mask(p0, 0, (int)hsize));
+        w[k] = (pay[k] | hd) & keep_mask((int)n - p0);
     }
-    const uint32_t crc = wave_crc32(T, w, (uint32_t)n, RFEC_WIRE_CRC_SEED, lane);
+    const uint32_t crc = wave_crc32(T, w, n, RFEC_WIRE_CRC_SEED, lane);
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-        w[k] |= place(bswap(crc), n, 32 * (int)lane + 4 * k);
+        w[k] |= place(bswap(crc), (int)n, 32 * (int)lane + 4 * k);
     store_slot(slot, dstride, lane, w);
     if (lane == 0)
         *dlen_out = (uint16_t)(n + 4);
@@ -252,69 +249,77 @@ __device__ __forceinline__ uint32_t wave_id()
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
 }
 
-struct FecFrameArgs {
-    const uint8_t* parity;
-    const rfec_hdr* meta;
-    const uint16_t* fsize;
-    const int8_t* status;
-    const rfec_fec_stamp* stamps;
-    uint8_t* dgram;
-    uint16_t* dlen;
-    uint32_t count, stride, capacity, dstride;
-};
+// ---------------------------------------------------------------------------
+// Framing.  Persistent waves walk datagrams d, d + nw, ...; the payload
+// window of the next datagram is loaded before the current one is processed.
+// Lane j's window starts 48 (FEC) / 32 (SEG) bytes before its output bytes'
+// source, so the window does not depend on the per-datagram header size.
+// ---------------------------------------------------------------------------
 
 // SIM_FEC: 45-byte header (sim_proto.c:13-18, sim_proto.inl:244-254, 270-283)
-__global__ __launch_bounds__(kBlock) void k_frame_fec(FecFrameArgs A)
+__global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict__ parity,
+                                                      const rfec_hdr* __restrict__ meta,
+                                                      const uint16_t* __restrict__ fsize,
+                                                      const int8_t* __restrict__ status,
+                                                      const rfec_fec_stamp* __restrict__ stamps,
+                                                      uint8_t* __restrict__ dgram, uint16_t* __restrict__ dlen,
+                                                      uint32_t count, uint32_t stride, uint32_t capacity,
+                                                      uint32_t dstride)
 {
     __shared__ uint32_t T[16 * 256];
     load_tables(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
-    for (uint32_t d = wave_id(); d < A.count; d += nw) {
-        uint8_t* slot = A.dgram + (size_t)d * A.dstride;
-        const uint32_t L = A.fsize[d];
-        const int st = A.status ? A.status[d] : 0;
-        if (st < 0 || L > A.capacity) {
-            zero_slot(slot, A.dstride, lane, A.dlen + d);
-            continue;
+    const int nch = (int)((capacity + 15) >> 4);
+    const int a0 = 2 * (int)lane - 3; // source bytes [32j - 48, 32j): out bytes [32j, 32j+32) shifted by 3
+    uint32_t d = wave_id();
+    if (d >= count)
+        return;
+    Win cur = load_win(parity + (size_t)d * stride, a0, nch);
+    for (;;) {
+        const uint32_t dn = d + nw;
+        Win nxt = {};
+        if (dn < count)
+            nxt = load_win(parity + (size_t)dn * stride, a0, nch);
+        uint8_t* slot = dgram + (size_t)d * dstride;
+        const uint32_t L = fsize[d];
+        const int st = status ? status[d] : 0;
+        if (st < 0 || L > capacity) {
+            zero_slot(slot, dstride, lane, dlen + d);
+        } else {
+            const rfec_fec_stamp s = stamps[d];
+            const rfec_hdr m = meta[d];
+            Hdr H = {};
+            put<0, 1>(H, RFEC_WIRE_VER);
+            put<1, 1>(H, RFEC_WIRE_FEC);
+            put<2, 4>(H, s.uid);
+            put<6, 2>(H, s.fec_id);
+            put<8, 1>(H, s.row);
+            put<9, 1>(H, s.col);
+            put<10, 1>(H, s.index);
+            put<11, 2>(H, s.count);
+            put<13, 4>(H, s.base_id);
+            put<17, 2>(H, s.transport_seq);
+            put<19, 4>(H, s.send_ts);
+            put<23, 4>(H, m.seq);
+            put<27, 4>(H, m.fid);
+            put<31, 4>(H, m.ts);
+            put<35, 2>(H, m.index);
+            put<37, 2>(H, m.total);
+            put<39, 1>(H, m.ftype);
+            put<40, 1>(H, m.payload_type);
+            put<41, 2>(H, m.size);
+            put<43, 2>(H, L); // mach_data_write length (cf_stream.c:328-337)
+            uint32_t pay[8];
+            funnel_c<3>(cur, pay); // window [32j-48, 32j) -> bytes [32j-45, 32j-13)
+            finish_frame(T, H, 45 + L, pay, lane, slot, dstride, dlen + d);
         }
-        const rfec_fec_stamp s = A.stamps[d];
-        const rfec_hdr m = A.meta[d];
-        Hdr H = {};
-        put<0, 1>(H, RFEC_WIRE_VER);
-        put<1, 1>(H, RFEC_WIRE_FEC);
-        put<2, 4>(H, s.uid);
-        put<6, 2>(H, s.fec_id);
-        put<8, 1>(H, s.row);
-        put<9, 1>(H, s.col);
-        put<10, 1>(H, s.index);
-        put<11, 2>(H, s.count);
-        put<13, 4>(H, s.base_id);
-        put<17, 2>(H, s.transport_seq);
-        put<19, 4>(H, s.send_ts);
-        put<23, 4>(H, m.seq);
-        put<27, 4>(H, m.fid);
-        put<31, 4>(H, m.ts);
-        put<35, 2>(H, m.index);
-        put<37, 2>(H, m.total);
-        put<39, 1>(H, m.ftype);
-        put<40, 1>(H, m.payload_type);
-        put<41, 2>(H, m.size);
-        put<43, 2>(H, L); // mach_data_write length (cf_stream.c:328-337)
-        uint32_t pay[8];
-        load_shifted(A.parity + (size_t)d * A.stride, -45, L, lane, pay);
-        finish_frame(T, H, 45, L, pay, lane, slot, A.dstride, A.dlen + d);
+        if (dn >= count)
+            break;
+        d = dn;
+        cur = nxt;
     }
 }
-
-struct SegFrameArgs {
-    const uint8_t* shards;
-    const rfec_hdr* hdr;
-    const rfec_seg_stamp* stamps;
-    uint8_t* dgram;
-    uint16_t* dlen;
-    uint32_t count, stride, capacity, dstride;
-};
 
 // SIM_SEG header, one of 8 layouts (sim_proto.inl:83-125): PW / FW = 4-byte
 // packet_id / fid, TW = 2-byte index and total.  Returns the header size.
@@ -349,53 +354,66 @@ __device__ __forceinline__ uint32_t seg_header(Hdr& H, const rfec_hdr& h, const 
     return P4 + 8;
 }
 
-__global__ __launch_bounds__(kBlock) void k_frame_seg(SegFrameArgs A)
+__global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict__ shards,
+                                                      const rfec_hdr* __restrict__ hdr,
+                                                      const rfec_seg_stamp* __restrict__ stamps,
+                                                      uint8_t* __restrict__ dgram, uint16_t* __restrict__ dlen,
+                                                      uint32_t count, uint32_t stride, uint32_t capacity,
+                                                      uint32_t dstride)
 {
     __shared__ uint32_t T[16 * 256];
     load_tables(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
-    for (uint32_t d = wave_id(); d < A.count; d += nw) {
-        uint8_t* slot = A.dgram + (size_t)d * A.dstride;
-        const rfec_hdr h = A.hdr[d];
+    const int nch = (int)((capacity + 15) >> 4);
+    const int a0 = 2 * (int)lane - 2; // source bytes [32j - 32, 32j + 16): header sizes 26..32
+    uint32_t d = wave_id();
+    if (d >= count)
+        return;
+    Win cur = load_win(shards + (size_t)d * stride, a0, nch);
+    for (;;) {
+        const uint32_t dn = d + nw;
+        Win nxt = {};
+        if (dn < count)
+            nxt = load_win(shards + (size_t)dn * stride, a0, nch);
+        uint8_t* slot = dgram + (size_t)d * dstride;
+        const rfec_hdr h = hdr[d];
         const uint32_t L = h.size;
-        if (L > A.capacity) {
-            zero_slot(slot, A.dstride, lane, A.dlen + d);
-            continue;
+        if (L > capacity) {
+            zero_slot(slot, dstride, lane, dlen + d);
+        } else {
+            const rfec_seg_stamp s = stamps[d];
+            Hdr H = {};
+            const uint32_t layout = (h.seq > 65535u ? 4u : 0u) | (h.fid > 65535u ? 2u : 0u) |
+                                    (h.total > 255u ? 1u : 0u);
+            uint32_t hs, pay[8];
+            // window [32j-32, 32j+16) shifted by 32 - hs bytes
+            switch (layout) {
+            case 0: hs = seg_header<false, false, false>(H, h, s); funnel_c<6>(cur, pay); break;
+            case 1: hs = seg_header<false, false, true>(H, h, s); funnel_c<4>(cur, pay); break;
+            case 2: hs = seg_header<false, true, false>(H, h, s); funnel_c<4>(cur, pay); break;
+            case 3: hs = seg_header<false, true, true>(H, h, s); funnel_c<2>(cur, pay); break;
+            case 4: hs = seg_header<true, false, false>(H, h, s); funnel_c<4>(cur, pay); break;
+            case 5: hs = seg_header<true, false, true>(H, h, s); funnel_c<2>(cur, pay); break;
+            case 6: hs = seg_header<true, true, false>(H, h, s); funnel_c<2>(cur, pay); break;
+            default: hs = seg_header<true, true, true>(H, h, s); funnel_c<0>(cur, pay); break;
+            }
+            finish_frame(T, H, hs + L, pay, lane, slot, dstride, dlen + d);
         }
-        const rfec_seg_stamp s = A.stamps[d];
-        Hdr H = {};
-        const uint32_t layout = (h.seq > 65535u ? 4u : 0u) | (h.fid > 65535u ? 2u : 0u) | (h.total > 255u ? 1u : 0u);
-        uint32_t hs;
-        switch (layout) {
-        case 0: hs = seg_header<false, false, false>(H, h, s); break;
-        case 1: hs = seg_header<false, false, true>(H, h, s); break;
-        case 2: hs = seg_header<false, true, false>(H, h, s); break;
-        case 3: hs = seg_header<false, true, true>(H, h, s); break;
-        case 4: hs = seg_header<true, false, false>(H, h, s); break;
-        case 5: hs = seg_header<true, false, true>(H, h, s); break;
-        case 6: hs = seg_header<true, true, false>(H, h, s); break;
-        default: hs = seg_header<true, true, true>(H, h, s); break;
-        }
-        uint32_t pay[8];
-        load_shifted(A.shards + (size_t)d * A.stride, -(int)hs, L, lane, pay);
-        finish_frame(T, H, hs, L, pay, lane, slot, A.dstride, A.dlen + d);
+        if (dn >= count)
+            break;
+        d = dn;
+        cur = nxt;
     }
 }
 
 // ---------------------------------------------------------------------------
 // Parse (receive side)
 // ---------------------------------------------------------------------------
-struct ParseArgs {
-    const uint8_t* dgram;
-    const uint16_t* dlen;
-    rfec_wire_rec* recs;
-    uint8_t* payload;
-    uint32_t n, dstride, stride, capacity;
-};
 
 // bin_stream reader over the first 64 bytes of the datagram (staged in LDS);
-// a read past `used` yields 0 and does not advance (cf_stream.c mach_*_read)
+// a read past `used` yields 0 and does not advance (cf_stream.c mach_*_read).
+// Only for datagrams too short for their header; the rest take fixed offsets.
 struct Cursor {
     const volatile uint8_t* b;
     uint32_t used, pos;
@@ -423,6 +441,36 @@ struct Cursor {
     }
 };
 
+// big-endian field at a compile-time byte position of the (wave-uniform) header dwords
+template <int POS, int NB>
+__device__ __forceinline__ uint32_t get(const uint32_t* H)
+{
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+        v = (v << 8) | ((H[(POS + i) >> 2] >> (8 * ((POS + i) & 3))) & 0xffu);
+    return v;
+}
+
+// SIM_SEG fields at fixed offsets for one header layout; returns the data-length position
+template <bool PW, bool FW, bool TW>
+__device__ __forceinline__ uint32_t seg_fields(const uint32_t* H, rfec_wire_rec& rec)
+{
+    constexpr int P1 = 8 + (PW ? 4 : 2);
+    constexpr int P2 = P1 + (FW ? 4 : 2);
+    constexpr int P3 = P2 + 4;
+    constexpr int P4 = P3 + (TW ? 4 : 2);
+    rec.hdr.seq = get<8, PW ? 4 : 2>(H);
+    rec.hdr.fid = get<P1, FW ? 4 : 2>(H);
+    rec.hdr.ts = get<P2, 4>(H);
+    rec.hdr.index = (uint16_t)(TW ? get<P3, 2>(H) : get<P3, 1>(H));
+    rec.hdr.total = (uint16_t)(TW ? get<P3 + 2, 2>(H) : get<P3 + 1, 1>(H));
+    rec.fec_id = (uint16_t)get<P4, 2>(H);
+    rec.send_ts = get<P4 + 2, 2>(H);
+    rec.transport_seq = (uint16_t)get<P4 + 4, 2>(H);
+    return P4 + 6;
+}
+
 __device__ __forceinline__ void write_rec(rfec_wire_rec* r, const rfec_wire_rec& v, uint32_t lane)
 {
     if (lane == 0) {
@@ -435,138 +483,245 @@ __device__ __forceinline__ void write_rec(rfec_wire_rec* r, const rfec_wire_rec&
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_parse(ParseArgs A)
+// out lane j = datagram bytes [pos + 32j, pos + 32j + 32) from the lane-wise
+// datagram w (pos wave-uniform, < 64)
+__device__ __forceinline__ void shift_down_bytes(const uint32_t w[8], uint32_t pos, uint32_t out[8])
+{
+    uint32_t A[8], B[8];
+    const bool q = pos >= 32;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t n1 = (uint32_t)__shfl_down((int)w[k], 1, kWave);
+        const uint32_t n2 = q ? (uint32_t)__shfl_down((int)w[k], 2, kWave) : 0u;
+        A[k] = q ? n1 : w[k];
+        B[k] = q ? n2 : n1;
+    }
+    const uint32_t x[16] = {A[0], A[1], A[2], A[3], A[4], A[5], A[6], A[7],
+                            B[0], B[1], B[2], B[3], B[4], B[5], B[6], B[7]};
+    const uint32_t r = pos & 31u, rb = r & 3u;
+#define RFEC_SHIFT(S)                                                                                              \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) out[k] = __builtin_amdgcn_alignbyte(x[(S) + k + 1], x[(S) + k], rb);
+    switch (r >> 2) {
+    case 0: RFEC_SHIFT(0) break;
+    case 1: RFEC_SHIFT(1) break;
+    case 2: RFEC_SHIFT(2) break;
+    case 3: RFEC_SHIFT(3) break;
+    case 4: RFEC_SHIFT(4) break;
+    case 5: RFEC_SHIFT(5) break;
+    case 6: RFEC_SHIFT(6) break;
+    default: RFEC_SHIFT(7) break;
+    }
+#undef RFEC_SHIFT
+}
+
+__global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ dgram,
+                                                  const uint16_t* __restrict__ dlen,
+                                                  rfec_wire_rec* __restrict__ recs, uint8_t* __restrict__ payload,
+                                                  uint32_t n, uint32_t dstride, uint32_t stride, uint32_t capacity)
 {
     __shared__ uint32_t T[16 * 256];
-    __shared__ uint32_t stage[kWavesPerBlock][16]; // first 64 bytes of each wave's datagram
+    __shared__ uint32_t stage[kWavesPerBlock][16]; // first 64 bytes of each wave's datagram (slow path)
     load_tables(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wl = threadIdx.x >> 6;
     const uint32_t nw = gridDim.x * kWavesPerBlock;
-    for (uint32_t d = wave_id(); d < A.n; d += nw) {
-        const uint8_t* dg = A.dgram + (size_t)d * A.dstride;
-        uint8_t* slot = A.payload + (size_t)d * A.stride;
-        const uint32_t len = A.dlen[d];
+    const int nch = (int)(dstride >> 4);
+    uint32_t d = wave_id();
+    if (d >= n)
+        return;
+    Win cur = load_win(dgram + (size_t)d * dstride, 2 * (int)lane, nch);
+    const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (;;) {
+        const uint32_t dn = d + nw;
+        Win nxt = {};
+        if (dn < n)
+            nxt = load_win(dgram + (size_t)dn * dstride, 2 * (int)lane, nch);
+        uint8_t* slot = payload + (size_t)d * stride;
+        const uint32_t len = dlen[d];
         rfec_wire_rec rec = {};
-        const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (len < 4 || len > A.dstride) {
-            rec.status = RFEC_WIRE_EBADCRC;
-            write_rec(A.recs + d, rec, lane);
-            store_slot(slot, A.stride, lane, z);
-            continue;
-        }
-        // datagram bytes [32j, 32j+32), zero from `len` on
-        uint32_t w[8];
-        load_shifted(dg, 0, len, lane, w);
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            w[k] &= range_mask(32 * (int)lane + 4 * k, 0, (int)len);
-        if (lane < 2) {
-            volatile uint32_t* sg = stage[wl];
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                sg[8 * lane + k] = w[k];
-        }
-        // CRC over [0, len-4) against the big-endian trailer (sim_proto.c:21-37)
-        uint32_t m[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            m[k] = w[k] & range_mask(32 * (int)lane + 4 * k, 0, (int)len - 4);
-        const uint32_t crc = wave_crc32(T, m, len - 4, RFEC_WIRE_CRC_SEED, lane);
-        uint32_t tr = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            // trailer bytes seen from each dword, moved to their BE place
-            const int p0 = 32 * (int)lane + 4 * k;
-            const uint32_t t = w[k] & range_mask(p0, (int)len - 4, (int)len);
-            const int sft = p0 - ((int)len - 4); // byte offset of this dword within the trailer
-            if (sft > -4 && sft < 4)
-                tr |= sft >= 0 ? t << (8 * sft) : t >> (-8 * sft);
-        }
-        tr = bswap(wave_xor(tr));
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (crc != tr) {
-            rec.status = RFEC_WIRE_EBADCRC;
-            write_rec(A.recs + d, rec, lane);
-            store_slot(slot, A.stride, lane, z);
-            continue;
-        }
-        Cursor c{reinterpret_cast<const volatile uint8_t*>(stage[wl]), len, 0};
-        rec.ver = (uint8_t)c.r8();
-        rec.mid = (uint8_t)c.r8();
-        rec.uid = c.r32();
+        rec.status = RFEC_WIRE_EBADCRC;
         int data_at = -1;
         uint32_t dsize = 0;
-        if (rec.mid < RFEC_WIRE_MIN_MID || rec.mid > RFEC_WIRE_MAX_MID) {
-            rec.status = RFEC_WIRE_EMID;
-        } else if (rec.mid == RFEC_WIRE_SEG) { // sim_segment_decode, sim_proto.inl:127-179
-            const uint32_t mask = c.r8();
-            rec.hdr.payload_type = (uint8_t)c.r8();
-            rec.hdr.ftype = (uint8_t)(mask & 1u);
-            rec.hdr.seq = (mask & 0x80u) ? c.r32() : c.r16();
-            rec.hdr.fid = (mask & 0x40u) ? c.r32() : c.r16();
-            rec.hdr.ts = c.r32();
-            if (mask & 0x20u) {
-                rec.hdr.index = (uint16_t)c.r16();
-                rec.hdr.total = (uint16_t)c.r16();
-            } else {
-                rec.hdr.index = (uint16_t)c.r8();
-                rec.hdr.total = (uint16_t)c.r8();
-            }
-            rec.remb = (mask & 0x10u) ? 0 : 0xff;
-            rec.fec_id = (uint16_t)c.r16();
-            rec.send_ts = c.r16();
-            rec.transport_seq = (uint16_t)c.r16();
-            const uint32_t n = c.r16(); // mach_data_read, cf_stream.c:339-355
-            if (n <= A.capacity && c.pos + n <= len) {
-                data_at = (int)c.pos;
-                dsize = n;
-            }
-            rec.status = RFEC_WIRE_OK; // a bad length leaves data_size 0 (:174-176)
-        } else if (rec.mid == RFEC_WIRE_FEC) { // sim_fec_decode, sim_proto.inl:287-307
-            rec.fec_id = (uint16_t)c.r16();
-            rec.row = (uint8_t)c.r8();
-            rec.col = (uint8_t)c.r8();
-            rec.index = (uint8_t)c.r8();
-            rec.count = (uint16_t)c.r16();
-            rec.base_id = c.r32();
-            rec.transport_seq = (uint16_t)c.r16();
-            rec.send_ts = c.r32();
-            rec.hdr.seq = c.r32();
-            rec.hdr.fid = c.r32();
-            rec.hdr.ts = c.r32();
-            rec.hdr.index = (uint16_t)c.r16();
-            rec.hdr.total = (uint16_t)c.r16();
-            rec.hdr.ftype = (uint8_t)c.r8();
-            rec.hdr.payload_type = (uint8_t)c.r8();
-            rec.hdr.size = (uint16_t)c.r16();
-            const uint32_t n = c.r16();
-            if (n <= A.capacity && c.pos + n <= len) {
-                data_at = (int)c.pos;
-                dsize = n;
-                rec.status = RFEC_WIRE_OK;
-            } else {
-                rec.status = RFEC_WIRE_EBODY;
-            }
-        } else {
-            rec.status = RFEC_WIRE_OTHER;
-        }
-        rec.data_size = (uint16_t)dsize;
-        if (rec.mid == RFEC_WIRE_SEG && rec.status == RFEC_WIRE_OK)
-            rec.hdr.size = (uint16_t)dsize;
-        write_rec(A.recs + d, rec, lane);
-        if (data_at < 0) {
-            store_slot(slot, A.stride, lane, z);
-            continue;
-        }
-        uint32_t pay[8];
-        load_shifted(dg, data_at, (uint32_t)data_at + dsize, lane, pay);
+        if (len >= 4 && len <= dstride) {
+            // datagram bytes [32j, 32j+32), zero from `len` on
+            uint32_t w[8], m[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            pay[k] &= range_mask(32 * (int)lane + 4 * k, 0, (int)dsize);
-        store_slot(slot, A.stride, lane, pay);
+            for (int k = 0; k < 8; ++k) {
+                const int p0 = 32 * (int)lane + 4 * k;
+                w[k] = cur.c[k >> 2][k & 3] & keep_mask((int)len - p0);
+                m[k] = w[k] & keep_mask((int)len - 4 - p0);
+            }
+            // CRC over [0, len-4) against the big-endian trailer (sim_proto.c:21-37)
+            const uint32_t crc = wave_crc32(T, m, len - 4, RFEC_WIRE_CRC_SEED, lane);
+            const uint32_t tp = len - 4, tl = tp >> 5, tk = (tp & 31u) >> 2;
+            uint32_t lo = w[0], hi = w[1];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) {
+                lo = tk == (uint32_t)k ? w[k] : lo;
+                hi = tk == (uint32_t)k ? (k < 7 ? w[k + 1] : 0u) : hi;
+            }
+            const uint32_t nx = (uint32_t)__shfl_down((int)w[0], 1, kWave); // next lane's first dword
+            hi = tk == 7u ? nx : hi;
+            const uint64_t t2 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, (int)tl) << 32 |
+                                (uint32_t)__builtin_amdgcn_readlane((int)lo, (int)tl);
+            const uint32_t trailer = bswap((uint32_t)(t2 >> (8 * (tp & 3u))));
+            if (crc == trailer) {
+                uint32_t H[12];
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    H[k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 0);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    H[8 + k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 1);
+                rec.ver = (uint8_t)get<0, 1>(H);
+                rec.mid = (uint8_t)get<1, 1>(H);
+                const uint32_t mid = rec.mid;
+                const uint32_t smask = get<6, 1>(H);
+                const uint32_t seg_hl = 26u + ((smask & 0x80u) ? 2u : 0u) + ((smask & 0x40u) ? 2u : 0u) +
+                                        ((smask & 0x20u) ? 2u : 0u); // through the data length field
+                const bool fast = len >= 6 && ((mid == RFEC_WIRE_FEC && len >= 45) ||
+                                               (mid == RFEC_WIRE_SEG && len >= seg_hl) ||
+                                               (mid != RFEC_WIRE_FEC && mid != RFEC_WIRE_SEG));
+                uint32_t npos = 0, nval = 0;
+                if (fast) {
+                    rec.uid = get<2, 4>(H);
+                    if (mid < RFEC_WIRE_MIN_MID || mid > RFEC_WIRE_MAX_MID) {
+                        rec.status = RFEC_WIRE_EMID;
+                    } else if (mid == RFEC_WIRE_SEG) { // sim_segment_decode, sim_proto.inl:127-179
+                        rec.hdr.payload_type = (uint8_t)get<7, 1>(H);
+                        rec.hdr.ftype = (uint8_t)(smask & 1u);
+                        rec.remb = (smask & 0x10u) ? 0 : 0xff;
+                        switch (smask >> 5) {
+                        case 0: npos = seg_fields<false, false, false>(H, rec); break;
+                        case 1: npos = seg_fields<false, false, true>(H, rec); break;
+                        case 2: npos = seg_fields<false, true, false>(H, rec); break;
+                        case 3: npos = seg_fields<false, true, true>(H, rec); break;
+                        case 4: npos = seg_fields<true, false, false>(H, rec); break;
+                        case 5: npos = seg_fields<true, false, true>(H, rec); break;
+                        case 6: npos = seg_fields<true, true, false>(H, rec); break;
+                        default: npos = seg_fields<true, true, true>(H, rec); break;
+                        }
+                        nval = (H[npos >> 2] >> (8 * (npos & 3)) & 0xffu) << 8;
+                        nval |= H[(npos + 1) >> 2] >> (8 * ((npos + 1) & 3)) & 0xffu;
+                        rec.status = RFEC_WIRE_OK;
+                    } else if (mid == RFEC_WIRE_FEC) { // sim_fec_decode, sim_proto.inl:287-307
+                        rec.fec_id = (uint16_t)get<6, 2>(H);
+                        rec.row = (uint8_t)get<8, 1>(H);
+                        rec.col = (uint8_t)get<9, 1>(H);
+                        rec.index = (uint8_t)get<10, 1>(H);
+                        rec.count = (uint16_t)get<11, 2>(H);
+                        rec.base_id = get<13, 4>(H);
+                        rec.transport_seq = (uint16_t)get<17, 2>(H);
+                        rec.send_ts = get<19, 4>(H);
+                        rec.hdr.seq = get<23, 4>(H);
+                        rec.hdr.fid = get<27, 4>(H);
+                        rec.hdr.ts = get<31, 4>(H);
+                        rec.hdr.index = (uint16_t)get<35, 2>(H);
+                        rec.hdr.total = (uint16_t)get<37, 2>(H);
+                        rec.hdr.ftype = (uint8_t)get<39, 1>(H);
+                        rec.hdr.payload_type = (uint8_t)get<40, 1>(H);
+                        rec.hdr.size = (uint16_t)get<41, 2>(H);
+                        npos = 43;
+                        nval = get<43, 2>(H);
+                        rec.status = RFEC_WIRE_OK;
+                    } else {
+                        rec.status = RFEC_WIRE_OTHER;
+                    }
+                    npos += 2;
+                } else {
+                    // truncated header: emulate the bin_stream reader byte by byte
+                    if (lane < 2) {
+                        volatile uint32_t* sg = stage[wl];
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            sg[8 * lane + k] = w[k];
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    Cursor c{reinterpret_cast<const volatile uint8_t*>(stage[wl]), len, 0};
+                    c.r8();
+                    c.r8();
+                    rec.uid = c.r32();
+                    if (mid < RFEC_WIRE_MIN_MID || mid > RFEC_WIRE_MAX_MID) {
+                        rec.status = RFEC_WIRE_EMID;
+                    } else if (mid == RFEC_WIRE_SEG) {
+                        const uint32_t mk = c.r8();
+                        rec.hdr.payload_type = (uint8_t)c.r8();
+                        rec.hdr.ftype = (uint8_t)(mk & 1u);
+                        rec.hdr.seq = (mk & 0x80u) ? c.r32() : c.r16();
+                        rec.hdr.fid = (mk & 0x40u) ? c.r32() : c.r16();
+                        rec.hdr.ts = c.r32();
+                        if (mk & 0x20u) {
+                            rec.hdr.index = (uint16_t)c.r16();
+                            rec.hdr.total = (uint16_t)c.r16();
+                        } else {
+                            rec.hdr.index = (uint16_t)c.r8();
+                            rec.hdr.total = (uint16_t)c.r8();
+                        }
+                        rec.remb = (mk & 0x10u) ? 0 : 0xff;
+                        rec.fec_id = (uint16_t)c.r16();
+                        rec.send_ts = c.r16();
+                        rec.transport_seq = (uint16_t)c.r16();
+                        nval = c.r16();
+                        npos = c.pos;
+                        rec.status = RFEC_WIRE_OK;
+                    } else if (mid == RFEC_WIRE_FEC) {
+                        rec.fec_id = (uint16_t)c.r16();
+                        rec.row = (uint8_t)c.r8();
+                        rec.col = (uint8_t)c.r8();
+                        rec.index = (uint8_t)c.r8();
+                        rec.count = (uint16_t)c.r16();
+                        rec.base_id = c.r32();
+                        rec.transport_seq = (uint16_t)c.r16();
+                        rec.send_ts = c.r32();
+                        rec.hdr.seq = c.r32();
+                        rec.hdr.fid = c.r32();
+                        rec.hdr.ts = c.r32();
+                        rec.hdr.index = (uint16_t)c.r16();
+                        rec.hdr.total = (uint16_t)c.r16();
+                        rec.hdr.ftype = (uint8_t)c.r8();
+                        rec.hdr.payload_type = (uint8_t)c.r8();
+                        rec.hdr.size = (uint16_t)c.r16();
+                        nval = c.r16();
+                        npos = c.pos;
+                        rec.status = RFEC_WIRE_OK;
+                    } else {
+                        rec.status = RFEC_WIRE_OTHER;
+                    }
+                }
+                // mach_data_read, cf_stream.c:339-355
+                const bool data_ok = nval <= capacity && npos + nval <= len;
+                if (mid == RFEC_WIRE_SEG && rec.status == RFEC_WIRE_OK) {
+                    dsize = data_ok ? nval : 0u; // a bad length decodes as size 0 (sim_proto.inl:174-176)
+                    data_at = data_ok ? (int)npos : -1;
+                    rec.hdr.size = (uint16_t)dsize;
+                } else if (mid == RFEC_WIRE_FEC && rec.status == RFEC_WIRE_OK) {
+                    if (data_ok) {
+                        dsize = nval;
+                        data_at = (int)npos;
+                    } else {
+                        rec.status = RFEC_WIRE_EBODY; // sim_proto.inl:301-305
+                    }
+                }
+                rec.data_size = (uint16_t)dsize;
+                if (data_at >= 0) {
+                    uint32_t pay[8];
+                    shift_down_bytes(w, (uint32_t)data_at, pay);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        pay[k] &= keep_mask((int)dsize - 32 * (int)lane - 4 * k);
+                    store_slot(slot, stride, lane, pay);
+                }
+            }
+        }
+        write_rec(recs + d, rec, lane);
+        if (data_at < 0)
+            store_slot(slot, stride, lane, z);
+        if (dn >= n)
+            break;
+        d = dn;
+        cur = nxt;
     }
 }
 
@@ -585,9 +740,8 @@ int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacit
                                const rfec_fec_stamp* stamps, uint32_t dstride, uint8_t* dgram, uint16_t* dlen,
                                void* stream)
 {
-    const FecFrameArgs A = {parity, meta, fec_size, status, stamps, dgram, dlen, count, stride, capacity, dstride};
     hipLaunchKernelGGL(k_frame_fec, dim3(grid_for(count)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
-                       A);
+                       parity, meta, fec_size, status, stamps, dgram, dlen, count, stride, capacity, dstride);
     return (int)hipGetLastError();
 }
 
@@ -595,17 +749,16 @@ int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacit
                                const rfec_hdr* hdr, const rfec_seg_stamp* stamps, uint32_t dstride, uint8_t* dgram,
                                uint16_t* dlen, void* stream)
 {
-    const SegFrameArgs A = {shards, hdr, stamps, dgram, dlen, count, stride, capacity, dstride};
     hipLaunchKernelGGL(k_frame_seg, dim3(grid_for(count)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
-                       A);
+                       shards, hdr, stamps, dgram, dlen, count, stride, capacity, dstride);
     return (int)hipGetLastError();
 }
 
 int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
                            uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload, void* stream)
 {
-    const ParseArgs A = {dgram, dlen, recs, payload, n, dstride, stride, capacity};
-    hipLaunchKernelGGL(k_parse, dim3(grid_for(n)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), A);
+    hipLaunchKernelGGL(k_parse, dim3(grid_for(n)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), dgram,
+                       dlen, recs, payload, n, dstride, stride, capacity);
     return (int)hipGetLastError();
 }
 

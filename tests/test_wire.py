@@ -108,7 +108,7 @@ def test_wire_short_datagram_gpu(gwire):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("capacity,stride", [(1000, 1008), (1200, 1200), (256, 256), (2000, 2000)])
+@pytest.mark.parametrize("capacity,stride", [(1000, 1008), (1200, 1200), (256, 256), (1984, 1984), (1999, 2000)])
 def test_wire_random_roundtrip_gpu(gwire, oracle1000, capacity, stride):
     """Large random batches: HIP framing == oracle framing byte for byte, and
     HIP parse(HIP frame(x)) returns x (fields, payload, zero tails)."""

@@ -8,6 +8,7 @@
 #         ab    = pytest -m gpu + tools/ab_encode.py
 #         bench = bench + rocprofv3 stats
 #         pmc   = FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py)
+#         wire  = pytest -m gpu + tools/wire_bench.py + its rocprofv3 stats
 #         all   = pytest + ab + pmc + bench + rocprofv3 stats
 set -u
 TAG=${1:-run}; MODE=${2:-full}; shift 2 || true
@@ -33,6 +34,12 @@ case "$MODE" in
   ab|all)
     step pytest_gpu 900 python -m pytest tests -m gpu -x -q -rs
     step ab 600 python tools/ab_encode.py --out "$OUT/ab.json" ;;
+esac
+case "$MODE" in
+  wire)
+    step pytest_gpu 900 python -m pytest tests -m gpu -x -q -rs
+    step wire 300 python tools/wire_bench.py --out "$OUT/wire.json"
+    step wire_rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/wprof" -o run -- python tools/wire_bench.py ;;
 esac
 case "$MODE" in
   pmc|all)
