@@ -261,20 +261,22 @@ typedef struct {
  * sim_proto.inl:270-285) of `count` parity slots laid out as rfec_encode_batch
  * wrote them (slot g*n + l = line l of group g): datagram i -> dgram slot i.
  * `status` may be NULL; a slot with status -1 gets length 0 (the reference
- * never emits that parity).  Needs fec_size <= capacity <= stride and
- * dstride >= capacity + 49. */
+ * never emits that parity).  `order` may be NULL; otherwise datagram i is
+ * written to slot order[i] of dgram / dlen (a permutation).  Needs
+ * fec_size <= capacity <= stride and dstride >= capacity + 49. */
 int rfec_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
                         const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,
-                        const rfec_fec_stamp* stamps, uint32_t dstride, uint8_t* dgram, uint16_t* dlen,
-                        void* stream);
+                        const rfec_fec_stamp* stamps, const uint32_t* order, uint32_t dstride, uint8_t* dgram,
+                        uint16_t* dlen, void* stream);
 
 /* SIM_SEG datagrams (sim_sender.c:96-97 + sim_segment_encode,
  * sim_proto.inl:83-125; header widths follow the value ranges) of `count`
- * segments: shards [count][stride], hdr [count].  Needs data_size <= capacity
- * <= stride and dstride >= capacity + 36. */
+ * segments: shards [count][stride], hdr [count]; `order` as for
+ * rfec_wire_frame_fec.  Needs data_size <= capacity <= stride and
+ * dstride >= capacity + 36. */
 int rfec_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* shards,
-                        const rfec_hdr* hdr, const rfec_seg_stamp* stamps, uint32_t dstride, uint8_t* dgram,
-                        uint16_t* dlen, void* stream);
+                        const rfec_hdr* hdr, const rfec_seg_stamp* stamps, const uint32_t* order, uint32_t dstride,
+                        uint8_t* dgram, uint16_t* dlen, void* stream);
 
 /* Parse status (rfec_wire_rec.status). */
 #define RFEC_WIRE_OK 0         /* SIM_SEG / SIM_FEC decoded (a SEG with a bad data length decodes
@@ -311,6 +313,90 @@ typedef struct {
 int rfec_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
                     uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload,
                     void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Sender staging: sim_sender_put (sim_sender.c:306-377) with sim_split_frame */
+/* (:254-284) and the flex sender's grouping (flex_fec_sender.c:49-78,       */
+/* 137-245), as a plan over a batch of frames, then frame bytes copied       */
+/* straight into pinned structure-of-arrays slots.                          */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    const uint8_t* data;      /* frame bytes (host) */
+    uint32_t size;
+    uint8_t payload_type, ftype;
+    uint8_t protect_fraction; /* s->loss_fraction when the frame is put (sim_sender.c:291) */
+    uint8_t reserved;
+    int64_t now_ms;           /* GET_SYS_MS() during sim_sender_put */
+} rfec_frame;
+
+/* The sim_sender_t / flex_fec_sender_t fields that shape segments and groups. */
+typedef struct {
+    uint32_t packet_id_seed, send_id_seed, frame_id_seed;
+    int64_t first_ts;   /* -1 before the first frame (sim_sender.c:333-338) */
+    int64_t fec_ts;     /* flex->fec_ts (0 = unset) */
+    uint32_t base_id;   /* flex->base_id */
+    int32_t open_seg;   /* the open group's first segment, relative to the next batch (<= 0) */
+    uint16_t fec_id;    /* flex->fec_id, starts at 1, skips 0 */
+    uint16_t segs_count;
+    int32_t first;      /* flex->first */
+    uint32_t transport_seq_seed; /* sender->transport_seq_seed (sim_sender.c:90, 112), u16 on the wire */
+} rfec_sender_state;
+
+/* One segment the sender builds (sim_sender.c:341-363). */
+typedef struct {
+    uint32_t frame;        /* index into the frame batch */
+    uint32_t offset;       /* byte offset in the frame */
+    uint32_t packet_id, send_id, fid, timestamp;
+    uint16_t index, total, data_size, fec_id;
+    uint8_t ftype, payload_type;
+    uint8_t reserved[2];
+    int32_t group;         /* group index in this batch, -1 if never protected */
+} rfec_seg_plan; /* 40 bytes */
+
+/* One protected group: a flex_fec_sender_update that emitted parities. */
+typedef struct {
+    int32_t first_seg;     /* segments [first_seg, first_seg + count) of the batch; negative:
+                              the first -first_seg were planned by the previous call */
+    uint16_t count, fec_id;
+    uint32_t base_id;      /* smallest packet_id of the group */
+    uint32_t fec_send_id0; /* send ids of its parities: fec_send_id0 + line (sim_sender.c:295-296) */
+    uint32_t fec_ts;       /* now_ms - first_ts when it closed (sim_sender.c:299) */
+    uint8_t protect_fraction, n_lines;
+    uint8_t reserved[2];
+} rfec_group_plan; /* 24 bytes */
+
+void rfec_sender_init(rfec_sender_state* st);
+/* Plans `n` frames: the segments sim_sender_put builds (segs, at most
+ * max_segs) and the groups flex_fec_sender_update protects (groups, at most
+ * max_groups), in creation order; `st` carries the sender across calls.  A
+ * group still open after the last frame stays open in `st` (its segments have
+ * group -2); the call that closes it reports a negative first_seg.
+ * seg_size = the sender's SIM_VIDEO_SIZE.  Returns RFEC_OK, or RFEC_EINVAL
+ * when an output array is too small (nothing is consumed then). */
+int rfec_sender_plan(rfec_sender_state* st, const rfec_frame* frames, uint32_t n, uint32_t seg_size,
+                     rfec_seg_plan* segs, uint32_t max_segs, uint32_t* n_segs, rfec_group_plan* groups,
+                     uint32_t max_groups, uint32_t* n_groups);
+
+/* Frames in, datagrams out (host memory both ends): rfec_sender_plan, the
+ * frame bytes copied once into pinned structure-of-arrays slots (groups of
+ * one shape contiguous, so each shape is one rfec_encode_batch), one H2D
+ * copy, the encode, rfec_wire_frame_seg / _fec, one D2H copy per datagram
+ * kind.  Datagrams come out in creation order: seg_dgram[i] is segs[i]'s
+ * SIM_SEG, fec_dgram holds the parities group by group, lines in plan order.
+ * transport_seq counts datagrams in creation order (a group's parities right
+ * after the segment that closed it); send_ts is that of an immediate send
+ * (sim_sender.c:88-91, 111-113).  seg_size is this library's SIM_VIDEO_SIZE;
+ * the segments of a group still open at the end are kept (per calling thread)
+ * and encoded by the call that closes it. */
+typedef struct {
+    uint32_t n_segs, n_groups, n_parities, n_shapes;
+    double plan_us, stage_us, h2d_us, kernel_us, d2h_us, total_us;
+} rfec_send_report;
+
+int rfec_host_send_frames(rfec_sender_state* st, const rfec_frame* frames, uint32_t n_frames, uint32_t uid,
+                          rfec_seg_plan* segs, uint32_t max_segs, rfec_group_plan* groups, uint32_t max_groups,
+                          uint32_t dstride, uint8_t* seg_dgram, uint16_t* seg_dlen, uint8_t* fec_dgram,
+                          uint16_t* fec_dlen, uint32_t max_parities, rfec_send_report* report);
 
 /* Kernel-selection knobs, for benchmarking and A/B tests (0 = defaults:
  * specialised row kernels where the plan allows, non-temporal streaming). */

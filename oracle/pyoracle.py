@@ -52,6 +52,22 @@ assert FEC_STAMP.itemsize == 24 and SEG_STAMP.itemsize == 12 and WIRE_REC.itemsi
 assert WIRE_FEC_IN.itemsize == 48 and WIRE_SEG_IN.itemsize == 36 and WIRE_PARSE_IN.itemsize == 72
 CRC_SEED = 0x0E3DFC0A
 
+# sender staging (include/razor_fec.h rfec_frame / rfec_sender_state / rfec_seg_plan / rfec_group_plan)
+FRAME = np.dtype([("data", "<u8"), ("size", "<u4"), ("payload_type", "u1"), ("ftype", "u1"),
+                  ("protect_fraction", "u1"), ("reserved", "u1"), ("now_ms", "<i8")])
+SENDER_STATE = np.dtype([("packet_id_seed", "<u4"), ("send_id_seed", "<u4"), ("frame_id_seed", "<u4"),
+                         ("pad0", "<u4"), ("first_ts", "<i8"), ("fec_ts", "<i8"), ("base_id", "<u4"),
+                         ("open_seg", "<i4"), ("fec_id", "<u2"), ("segs_count", "<u2"), ("first", "<i4"),
+                         ("transport_seq_seed", "<u4"), ("pad1", "<u4")])
+SEG_PLAN = np.dtype([("frame", "<u4"), ("offset", "<u4"), ("packet_id", "<u4"), ("send_id", "<u4"), ("fid", "<u4"),
+                     ("timestamp", "<u4"), ("index", "<u2"), ("total", "<u2"), ("data_size", "<u2"),
+                     ("fec_id", "<u2"), ("ftype", "u1"), ("payload_type", "u1"), ("reserved", "u1", (2,)),
+                     ("group", "<i4")])
+GROUP_PLAN = np.dtype([("first_seg", "<i4"), ("count", "<u2"), ("fec_id", "<u2"), ("base_id", "<u4"),
+                       ("fec_send_id0", "<u4"), ("fec_ts", "<u4"), ("protect_fraction", "u1"), ("n_lines", "u1"),
+                       ("reserved", "u1", (2,))])
+assert FRAME.itemsize == 24 and SENDER_STATE.itemsize == 56 and SEG_PLAN.itemsize == 40 and GROUP_PLAN.itemsize == 24
+
 SEED = 0x52415A4F52464543
 
 
@@ -122,6 +138,8 @@ class Oracle:
         L.oracle_wire_frame_fec_batch.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, P, P, P, P, P, C.c_uint32, P, P]
         L.oracle_wire_frame_seg_batch.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, P, P, P, C.c_uint32, P, P]
         L.oracle_wire_parse_batch.argtypes = [C.c_uint32, C.c_uint32, P, P, C.c_uint32, C.c_uint32, P, P]
+        L.oracle_sender_init.argtypes = [P]
+        L.oracle_sender_plan.argtypes = [P, P, C.c_uint32, C.c_uint32, P, C.c_uint32, P, P, C.c_uint32, P]
         L.oracle_segment_size.restype = C.c_size_t
         L.oracle_fec_size.restype = C.c_size_t
         self.video_size = L.oracle_sim_video_size()
@@ -231,6 +249,23 @@ class Oracle:
                                          _np_ptr(np.ascontiguousarray(dlen, np.uint16)), stride, capacity,
                                          _np_ptr(recs), _np_ptr(payload))
         return recs, payload
+
+    # -- sender staging ----------------------------------------------------------
+    def sender_init(self):
+        st = np.zeros(1, SENDER_STATE)
+        self.lib.oracle_sender_init(_np_ptr(st))
+        return st
+
+    def sender_plan(self, st, frames, seg_size, max_segs=1 << 16, max_groups=1 << 14):
+        segs = np.zeros(max_segs, SEG_PLAN)
+        groups = np.zeros(max_groups, GROUP_PLAN)
+        ns, ng = C.c_uint32(), C.c_uint32()
+        rc = self.lib.oracle_sender_plan(_np_ptr(st), _np_ptr(np.ascontiguousarray(frames)), len(frames), seg_size,
+                                         _np_ptr(segs), max_segs, C.byref(ns), _np_ptr(groups), max_groups,
+                                         C.byref(ng))
+        if rc != 0:
+            raise ValueError("sender plan: output arrays too small")
+        return segs[:ns.value], groups[:ng.value]
 
     # -- AoS (reference-shaped) path for the CPU baseline ---------------------
     def seg_dtype(self):
@@ -343,6 +378,41 @@ def load_wire_parse():
     m = wire_manifest()["parse"]
     return _walk(m["file"], WIRE_PARSE_IN, m["count"],
                  lambda r: [("dgram", int(r["len"])), ("payload", int(r["rec"]["data_size"]))])
+
+
+def stage_fixture() -> dict:
+    return json.loads((GOLDEN / "stage.json").read_text())
+
+
+def stage_frames(scn, now_ms=1_700_000_000_000):
+    """(frames dtype FRAME with data pointers into `blob`, blob) for a stage.json scenario."""
+    sizes = [f[0] for f in scn["frames"]]
+    st = C.c_uint64(0x5354414745 ^ scn["id"])
+    blob = np.zeros(sum(sizes) + 8, np.uint8)
+    off = 0
+    for s in sizes:
+        words = (s + 7) // 8
+        v = np.array([_xs_next(st) for _ in range(words)], np.uint64).view(np.uint8)
+        blob[off:off + s] = v[:s]
+        off += s
+    frames = np.zeros(len(sizes), FRAME)
+    off = 0
+    for i, f in enumerate(scn["frames"]):
+        frames[i]["data"] = blob.ctypes.data + off
+        frames[i]["size"], frames[i]["ftype"], frames[i]["payload_type"], frames[i]["protect_fraction"] = f
+        frames[i]["now_ms"] = now_ms
+        off += f[0]
+    return frames, blob
+
+
+def _xs_next(st: C.c_uint64) -> int:
+    """xorshift64* (test/common_test.c:10-16), Python side for small inputs."""
+    x = st.value
+    x ^= x >> 12
+    x ^= (x << 25) & 0xFFFFFFFFFFFFFFFF
+    x ^= x >> 27
+    st.value = x
+    return (x * 2685821657736338717) & 0xFFFFFFFFFFFFFFFF
 
 
 def plan_table() -> np.ndarray:

@@ -829,3 +829,138 @@ void oracle_wire_parse_batch(uint32_t n, uint32_t dstride, const uint8_t* dgram,
     }
     free(tmp);
 }
+
+/* ---- sender staging: sim_sender.c:254-284, 286-377; flex_fec_sender.c ------ */
+void oracle_sender_init(rfec_sender_state* st)
+{
+    memset(st, 0, sizeof(*st));
+    st->first_ts = -1;  /* sim_sender.c:215-ish: first_ts = -1 until the first frame */
+    st->fec_id = 1;     /* flex_fec_sender_create / reset: fec_id = 1 (flex_fec_sender.c:40) */
+    st->first = 1;
+}
+
+/* sim_split_frame, sim_sender.c:254-284 */
+static uint32_t oracle_split(uint32_t size, uint32_t seg, uint32_t i, uint32_t total)
+{
+    if (size <= seg)
+        return size;
+    const uint32_t packet_size = size / total, remain = size % total;
+    return i < remain ? packet_size + 1 : packet_size;
+}
+
+/* flex_fec_sender_update (flex_fec_sender.c:146-245) called by sim_sender_fec
+ * (sim_sender.c:286-304) at time now: on flex_fec_sender_over (:137-143) it
+ * emits the group's parities (if any line has >= 2 members), resets and
+ * advances fec_id, skipping 0 (:236-243).  Returns 0, or -1 when `groups` is full. */
+static int oracle_sender_update(rfec_sender_state* s, int64_t now, uint8_t pf, rfec_seg_plan* segs, uint32_t ns,
+                                rfec_group_plan* groups, uint32_t max_groups, uint32_t* ng)
+{
+    if (!(s->fec_ts + 500 < now || s->segs_count >= 6)) /* FEC_REPAIR_WINDOW = 500 */
+        return 0;
+    rfec_plan plan;
+    int n_lines = 0;
+    if (s->segs_count > 0 &&
+        oracle_plan_from_fraction((int)s->segs_count, pf, RFEC_LAYER_ROWS | RFEC_LAYER_COLS, &plan) == 0)
+        n_lines = plan.n_lines;
+    const int32_t gid = n_lines > 0 ? (int32_t)*ng : -1;
+    if (n_lines > 0) {
+        if (*ng >= max_groups)
+            return -1;
+        rfec_group_plan* gp = &groups[(*ng)++];
+        memset(gp, 0, sizeof(*gp));
+        gp->first_seg = s->open_seg;
+        gp->count = s->segs_count;
+        gp->fec_id = s->fec_id;
+        gp->base_id = s->base_id;
+        gp->protect_fraction = pf;
+        gp->n_lines = (uint8_t)n_lines;
+        gp->fec_send_id0 = s->send_id_seed + 1; /* one send id per parity, sim_sender.c:295-296 */
+        gp->fec_ts = (uint32_t)(now - s->first_ts); /* :299 */
+        s->send_id_seed += (uint32_t)n_lines;
+    }
+    if (s->segs_count > 0)
+        for (int32_t q = s->open_seg; q < (int32_t)ns; ++q)
+            if (q >= 0)
+                segs[q].group = gid;
+    s->fec_ts = 0;
+    s->segs_count = 0;
+    s->base_id = 0;
+    s->first = 1;
+    s->fec_id++;
+    if (s->fec_id == 0)
+        s->fec_id = 1;
+    return 0;
+}
+
+int oracle_sender_plan(rfec_sender_state* st, const rfec_frame* frames, uint32_t n, uint32_t seg_size,
+                       rfec_seg_plan* segs, uint32_t max_segs, uint32_t* n_segs, rfec_group_plan* groups,
+                       uint32_t max_groups, uint32_t* n_groups)
+{
+    uint32_t ns = 0, ng = 0;
+    rfec_sender_state s = *st;
+    for (uint32_t f = 0; f < n; ++f) {
+        const rfec_frame* fr = &frames[f];
+        const uint32_t total = fr->size <= seg_size ? 1u : (fr->size + seg_size - 1) / seg_size; /* :258-265 */
+        uint32_t timestamp;
+        if (s.first_ts == -1) { /* :333-338 */
+            timestamp = 0;
+            s.first_ts = fr->now_ms;
+        } else {
+            timestamp = (uint32_t)(fr->now_ms - s.first_ts);
+        }
+        ++s.frame_id_seed; /* :341 */
+        uint32_t off = 0;
+        for (uint32_t i = 0; i < total; ++i) {
+            if (ns >= max_segs)
+                return -1;
+            rfec_seg_plan* g = &segs[ns];
+            memset(g, 0, sizeof(*g));
+            g->frame = f;
+            g->offset = off;
+            g->packet_id = ++s.packet_id_seed; /* :344-352 */
+            g->send_id = ++s.send_id_seed;
+            g->fid = s.frame_id_seed;
+            g->timestamp = timestamp;
+            g->ftype = fr->ftype;
+            g->payload_type = fr->payload_type;
+            g->index = (uint16_t)i;
+            g->total = (uint16_t)total;
+            g->data_size = (uint16_t)oracle_split(fr->size, seg_size, i, total);
+            off += g->data_size;
+            g->fec_id = s.fec_id; /* :360-362 */
+            g->group = -2;
+            /* flex_fec_sender_add_segment, flex_fec_sender.c:49-78 */
+            if (s.fec_ts == 0) {
+                s.fec_ts = fr->now_ms;
+            } else if (s.fec_ts + 500 * 4 < fr->now_ms) { /* stale: the open segments are dropped */
+                for (int32_t q = s.open_seg; q < (int32_t)ns; ++q)
+                    if (q >= 0)
+                        segs[q].group = -1;
+                s.segs_count = 0;
+                s.base_id = 0;
+                s.first = 1;
+                s.fec_ts = fr->now_ms;
+            }
+            if (s.segs_count == 0)
+                s.open_seg = (int32_t)ns;
+            s.base_id = s.first ? g->packet_id : (g->packet_id < s.base_id ? g->packet_id : s.base_id);
+            s.first = 0;
+            s.segs_count++;
+            ns++;
+            if (s.segs_count >= 100 && /* sim_sender.c:370-371 */
+                oracle_sender_update(&s, fr->now_ms, fr->protect_fraction, segs, ns, groups, max_groups, &ng))
+                return -1;
+        }
+        /* sim_sender.c:373-374: after every frame */
+        if (oracle_sender_update(&s, fr->now_ms, fr->protect_fraction, segs, ns, groups, max_groups, &ng))
+            return -1;
+    }
+    if (s.segs_count > 0)
+        s.open_seg -= (int32_t)ns;
+    else
+        s.open_seg = 0;
+    *st = s;
+    *n_segs = ns;
+    *n_groups = ng;
+    return 0;
+}

@@ -80,6 +80,12 @@ void oracle_wire_frame_seg_batch(uint32_t count, uint32_t stride, uint32_t capac
 void oracle_wire_parse_batch(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
                              uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload);
 
+/* sender staging (sim_sender.c:254-377, flex_fec_sender.c:49-245) */
+void oracle_sender_init(rfec_sender_state* st);
+int oracle_sender_plan(rfec_sender_state* st, const rfec_frame* frames, uint32_t n, uint32_t seg_size,
+                       rfec_seg_plan* segs, uint32_t max_segs, uint32_t* n_segs, rfec_group_plan* groups,
+                       uint32_t max_groups, uint32_t* n_groups);
+
 int oracle_sim_video_size(void);
 size_t oracle_segment_size(void);
 size_t oracle_fec_size(void);

@@ -43,11 +43,11 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
 static inline uint32_t rfec_sched_record_bytes(uint32_t n_lines) { return (2u + 2u * n_lines + 15u) & ~15u; }
 int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
                                const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,
-                               const rfec_fec_stamp* stamps, uint32_t dstride, uint8_t* dgram, uint16_t* dlen,
-                               void* stream);
+                               const rfec_fec_stamp* stamps, const uint32_t* order, uint32_t dstride,
+                               uint8_t* dgram, uint16_t* dlen, void* stream);
 int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* shards,
-                               const rfec_hdr* hdr, const rfec_seg_stamp* stamps, uint32_t dstride, uint8_t* dgram,
-                               uint16_t* dlen, void* stream);
+                               const rfec_hdr* hdr, const rfec_seg_stamp* stamps, const uint32_t* order,
+                               uint32_t dstride, uint8_t* dgram, uint16_t* dlen, void* stream);
 int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
                            uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload, void* stream);
 int rfec_launch_zero_tails(uint32_t slots, uint32_t stride, uint8_t* shards, const rfec_hdr* hdr, void* stream);

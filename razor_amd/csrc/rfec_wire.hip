@@ -26,19 +26,22 @@
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kBlock = 256;
+constexpr int kBlock = 1024;
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr uint32_t kPoly = 0xEDB88320u; // reflected CRC-32 polynomial (cf_crc32.c table)
-constexpr int kXpBias = 32;              // xp[e + 32] = x^(8e) mod P, e in [-32, 2047]
-constexpr int kXpSize = 2080;
 
+// LDS tables (built at compile time, copied to LDS once per block):
+//   t[s][b]         CRC register after byte b then s zero bytes, from 0 (slice-by-16)
+//   nib[i][v][j]    (nibble v at nibble position i of a register) * x^(256 (63-j)):
+//                   lane j's run, right-aligned in a 2 KiB window, carried to the
+//                   window's end.  [i][v][lane]: a lane reads only its own column,
+//                   so the 64 lanes never share an LDS bank.
 struct CrcTables {
-    uint32_t t[16][256]; // t[s][b]: CRC register after byte b then s zero bytes, from 0
-    uint32_t xp[kXpSize];
+    uint32_t t[16][256];
+    uint32_t nib[8][16][kWave];
 };
 
 constexpr uint32_t mul_x(uint32_t v) { return (v & 1u) ? (v >> 1) ^ kPoly : v >> 1; }
-constexpr uint32_t div_x(uint32_t y) { return (y & 0x80000000u) ? (((y ^ kPoly) << 1) | 1u) : (y << 1); }
 
 constexpr CrcTables make_crc_tables()
 {
@@ -52,18 +55,25 @@ constexpr CrcTables make_crc_tables()
     for (int s = 1; s < 16; ++s)
         for (uint32_t b = 0; b < 256; ++b)
             r.t[s][b] = (r.t[s - 1][b] >> 8) ^ r.t[0][r.t[s - 1][b] & 0xffu];
-    uint32_t v = 0x80000000u; // the polynomial 1
-    r.xp[kXpBias] = v;
-    for (int i = kXpBias + 1; i < kXpSize; ++i) {
-        for (int q = 0; q < 8; ++q)
+    // V_j = x^(256 (63 - j)); bit p of a register is the coefficient of x^(31-p)
+    uint32_t V = 0x80000000u; // x^0, for lane 63
+    for (int j = kWave - 1; j >= 0; --j) {
+        uint32_t basis[32]{}; // basis[e] = x^e * V_j
+        uint32_t v = V;
+        for (int e = 0; e < 32; ++e) {
+            basis[e] = v;
             v = mul_x(v);
-        r.xp[i] = v;
-    }
-    v = 0x80000000u;
-    for (int i = kXpBias - 1; i >= 0; --i) {
-        for (int q = 0; q < 8; ++q)
-            v = div_x(v);
-        r.xp[i] = v;
+        }
+        for (int i = 0; i < 8; ++i)
+            for (uint32_t nv = 0; nv < 16; ++nv) {
+                uint32_t acc = 0;
+                for (int k = 0; k < 4; ++k)
+                    if (nv & (1u << k))
+                        acc ^= basis[31 - (4 * i + k)];
+                r.nib[i][nv][j] = acc;
+            }
+        for (int q = 0; q < 256; ++q)
+            V = mul_x(V);
     }
     return r;
 }
@@ -72,11 +82,13 @@ __device__ const CrcTables kCrc = make_crc_tables();
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
+constexpr int kTabDwords = (int)(sizeof(CrcTables) / 4);
+constexpr int kNibBase = 16 * 256; // dword offset of nib in the LDS copy
 __device__ __forceinline__ void load_tables(uint32_t* T)
 {
-    const v4u* s = reinterpret_cast<const v4u*>(&kCrc.t[0][0]);
+    const v4u* s = reinterpret_cast<const v4u*>(&kCrc);
     v4u* d = reinterpret_cast<v4u*>(T);
-    for (int i = threadIdx.x; i < 16 * 256 / 4; i += kBlock)
+    for (int i = threadIdx.x; i < kTabDwords / 4; i += kBlock)
         d[i] = s[i];
     __syncthreads();
 }
@@ -92,16 +104,15 @@ __device__ __forceinline__ uint32_t slice16(const uint32_t* T, uint32_t a, uint3
            tb(T, 3, d & 0xff) ^ tb(T, 2, (d >> 8) & 0xff) ^ tb(T, 1, (d >> 16) & 0xff) ^ tb(T, 0, d >> 24);
 }
 
-// a(x) * b(x) mod P in the reflected representation (zlib multmodp)
-__device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b)
+// c * x^(256 (63 - lane)) mod P: eight nibble lookups in the lane's own column
+__device__ __forceinline__ uint32_t carry_to_end(const uint32_t* T, uint32_t c, uint32_t lane)
 {
-    uint32_t p = 0;
+    const uint32_t* nb = T + kNibBase + lane;
+    uint32_t r = 0;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-        p ^= b & (0u - ((a >> (31 - i)) & 1u));
-        b = (b >> 1) ^ (kPoly & (0u - (b & 1u)));
-    }
-    return p;
+    for (int i = 0; i < 8; ++i)
+        r ^= nb[(i * 16 + ((c >> (4 * i)) & 15u)) * kWave];
+    return r;
 }
 
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
@@ -112,8 +123,16 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
     return v;
 }
 
+__device__ __forceinline__ uint32_t from_lane(uint32_t v, int src)
+{
+    return src >= 0 ? (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v) : 0u;
+}
+
 // crc32(seed, msg[0:n)) (cf_crc32.c:56-68) of a message held lane-wise:
-// lane j has bytes [32j, 32j+32) in w (LE dwords), bytes >= n zero.
+// lane j has bytes [32j, 32j+32) in w (LE dwords), bytes >= n zero; n <= 2048.
+// The message is moved right by D = 2048 - n bytes (leading zeros do not
+// change a zero-register CRC), so lane j's run always ends 32 (63 - j) bytes
+// before the message does and its carry is a fixed per-lane multiplier.
 __device__ uint32_t wave_crc32(const uint32_t* T, const uint32_t w[8], uint32_t n, uint32_t seed, uint32_t lane)
 {
     if (n < 4) { // too short to fold the initial register into: bytewise
@@ -122,17 +141,39 @@ __device__ uint32_t wave_crc32(const uint32_t* T, const uint32_t w[8], uint32_t 
             r = tb(T, 0, (r ^ (w[0] >> (8 * i))) & 0xffu) ^ (r >> 8);
         return (uint32_t)__builtin_amdgcn_readfirstlane((int)~r);
     }
-    uint32_t c = 0;
-    if (32u * lane < n) {
-        const uint32_t w0 = w[0] ^ (lane == 0 ? ~seed : 0u); // initial register folded into bytes 0-3
-        c = slice16(T, w0, w[1], w[2], w[3]);
-        c = slice16(T, w[4] ^ c, w[5], w[6], w[7]);
-        // x^(8e) for the e bytes after this lane's run (negative for the run
-        // holding the end: its zero padding is divided back out)
-        const int e = (int)n - 32 * (int)(lane + 1);
-        c = mulmod(c, kCrc.xp[e + kXpBias]);
+    const uint32_t D = 2048u - n, q = D >> 5, rr = D & 31u;
+    // initial register folded into message bytes 0-3
+    const uint32_t w0 = w[0] ^ (lane == 0 ? ~seed : 0u);
+    // right-aligned view: lane j <- bytes [32j - D, 32j - D + 32) = the last rr
+    // bytes of lane j-q-1 and the first 32-rr bytes of lane j-q
+    const int la = (int)lane - (int)q - 1, lb = (int)lane - (int)q;
+    uint32_t X[16];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t v = k == 0 ? w0 : w[k];
+        X[k] = from_lane(v, la);
+        X[8 + k] = from_lane(v, lb);
     }
-    return ~wave_xor(c);
+    uint32_t v[8];
+    const uint32_t st = 32u - rr, rb = st & 3u;
+#define RFEC_VIEW(S)                                                                                              \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) v[k] =                                                          \
+        ((S) + k + 1 < 16) ? __builtin_amdgcn_alignbyte(X[((S) + k + 1) & 15], X[(S) + k], rb) : X[(S) + k];
+    switch (st >> 2) {
+    case 0: RFEC_VIEW(0) break;
+    case 1: RFEC_VIEW(1) break;
+    case 2: RFEC_VIEW(2) break;
+    case 3: RFEC_VIEW(3) break;
+    case 4: RFEC_VIEW(4) break;
+    case 5: RFEC_VIEW(5) break;
+    case 6: RFEC_VIEW(6) break;
+    case 7: RFEC_VIEW(7) break;
+    default: RFEC_VIEW(8) break; // rr == 0: lane j-q as it is
+    }
+#undef RFEC_VIEW
+    uint32_t c = slice16(T, v[0], v[1], v[2], v[3]);
+    c = slice16(T, v[4] ^ c, v[5], v[6], v[7]);
+    return ~wave_xor(carry_to_end(T, c, lane));
 }
 
 // bytes [lo, hi) of the dword at byte position p0, as a byte mask
@@ -144,29 +185,53 @@ __device__ __forceinline__ uint32_t range_mask(int p0, int lo, int hi)
     return fb & ~fa;
 }
 
-// up to 4 LE bytes `fb` starting at byte position `pos`, seen from the dword at p0
+// 4 LE bytes `fb` starting at byte position `pos`, seen from the dword at p0
+// (0 when they miss it): the 64-bit shift count is 0 or 64 (== 0 mod 64) off
+// the overlap, and the low half of fb:0 is zero
 __device__ __forceinline__ uint32_t place(uint32_t fb, int pos, int p0)
 {
-    const int t = pos - p0;
-    if (t >= 4 || t <= -4)
-        return 0u;
-    return t >= 0 ? fb << (8 * t) : fb >> (-8 * t);
+    const uint32_t s = (uint32_t)(32 - 8 * min(max(pos - p0, -4), 4));
+    return (uint32_t)(((uint64_t)fb << 32) >> (s & 63u));
 }
 
 __device__ __forceinline__ uint32_t bswap(uint32_t v) { return __builtin_bswap32(v); }
 
-// Three consecutive 16-B chunks of a slot, starting at chunk `a` (may be
-// negative); chunks outside [0, nch) read as 0.  Lane-private window.
+// Buffer descriptor over `bytes` bytes at p (wave-uniform inputs made
+// provably uniform): loads outside [0, bytes) return 0 without a branch.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes)
+{
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+    void* q = reinterpret_cast<void*>((uint64_t)hi << 32 | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(q, 0, (int)__builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
+}
+constexpr int kAuxNT = 2; // gfx950 cache-policy bits: nt
+
+// Up to three consecutive 16-B chunks of a slot, starting at chunk `a` (may
+// be negative); chunks outside [0, nch) read as 0.  Lane-private window; of
+// the third chunk only the first W2 dwords are loaded (what the funnel uses:
+// a dead dword of a wide load would pin its register until the load lands).
 struct Win {
     v4u c[3];
 };
+template <int W2>
 __device__ __forceinline__ Win load_win(const uint8_t* __restrict__ src, int a, int nch)
 {
-    const v4u* s = reinterpret_cast<const v4u*>(src);
-    Win w;
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-        w.c[i] = (a + i >= 0 && a + i < nch) ? __builtin_nontemporal_load(s + a + i) : v4u{0, 0, 0, 0};
+    const __amdgpu_buffer_rsrc_t r = rsrc(src, (uint32_t)nch * 16u);
+    Win w = {};
+    // a negative offset wraps past the range: 0
+    w.c[0] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)a * 16u, 0, kAuxNT));
+    w.c[1] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)(a + 1) * 16u, 0, kAuxNT));
+    if constexpr (W2 == 1) {
+        w.c[2][0] = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)(a + 2) * 16u, 0, kAuxNT);
+    } else if constexpr (W2 == 2) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)(a + 2) * 16u, 0, kAuxNT);
+        w.c[2][0] = v[0];
+        w.c[2][1] = v[1];
+    } else if constexpr (W2 == 4) {
+        w.c[2] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)(a + 2) * 16u, 0, kAuxNT));
+    }
     return w;
 }
 
@@ -185,8 +250,8 @@ __device__ __forceinline__ void funnel_c(const Win& w, uint32_t out[8])
 // byte mask of the first `keep` bytes of a dword (keep clamped to [0, 4])
 __device__ __forceinline__ uint32_t keep_mask(int keep)
 {
-    keep = min(max(keep, 0), 4);
-    return keep >= 4 ? 0xffffffffu : ~(0xffffffffu << (8 * keep));
+    const uint32_t s = 32u - 8u * (uint32_t)min(max(keep, 0), 4); // one 64-bit shift, no branch
+    return (uint32_t)(0xffffffffull >> s);
 }
 
 __device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t slot_bytes, uint32_t lane,
@@ -250,11 +315,71 @@ __device__ __forceinline__ uint32_t wave_id()
 }
 
 // ---------------------------------------------------------------------------
-// Framing.  Persistent waves walk datagrams d, d + nw, ...; the payload
-// window of the next datagram is loaded before the current one is processed.
+// Framing.  Persistent waves walk datagrams d, d + nw, ...; everything the
+// next datagram needs from memory (its payload window and, one dword per
+// lane, its header fields) is loaded before the current one is processed, so
+// no load inside an iteration waits behind the prefetch (vmcnt is in order).
 // Lane j's window starts 48 (FEC) / 32 (SEG) bytes before its output bytes'
 // source, so the window does not depend on the per-datagram header size.
 // ---------------------------------------------------------------------------
+
+// dword k of the prefetched per-datagram fields (wave-uniform)
+__device__ __forceinline__ uint32_t fld(uint32_t v, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
+
+// SIM_FEC fields, one dword per lane: 0-5 rfec_fec_stamp, 6-10 fec_meta,
+// 11 fec_data_size, 12 status (sign-extended; 0 when status is NULL)
+__device__ __forceinline__ uint32_t load_fec_fields(const rfec_fec_stamp* __restrict__ stamps,
+                                                    const rfec_hdr* __restrict__ meta,
+                                                    const uint16_t* __restrict__ fsize,
+                                                    const int8_t* __restrict__ status, uint32_t d, uint32_t lane)
+{
+    // four loads, each in range for its own lanes only (the rest read 0)
+    const uint32_t s = __builtin_amdgcn_raw_buffer_load_b32(rsrc(stamps + d, 24), 4u * lane, 0, kAuxNT);
+    const uint32_t m = __builtin_amdgcn_raw_buffer_load_b32(rsrc(meta + d, 20), 4u * (lane - 6u), 0, kAuxNT);
+    const uint32_t f = __builtin_amdgcn_raw_buffer_load_b16(rsrc(fsize + d, 2), 2u * (lane - 11u), 0, kAuxNT);
+    const uint32_t t = __builtin_amdgcn_raw_buffer_load_b8(rsrc(status ? status + d : status, status ? 1u : 0u),
+                                                           lane - 12u, 0, kAuxNT);
+    return s | m | f | (uint32_t)(int32_t)(int8_t)t;
+}
+
+// SIM_SEG fields: 0-4 rfec_hdr, 5-7 rfec_seg_stamp
+__device__ __forceinline__ uint32_t load_seg_fields(const rfec_hdr* __restrict__ hdr,
+                                                    const rfec_seg_stamp* __restrict__ stamps, uint32_t d,
+                                                    uint32_t lane)
+{
+    const uint32_t h = __builtin_amdgcn_raw_buffer_load_b32(rsrc(hdr + d, 20), 4u * lane, 0, kAuxNT);
+    const uint32_t s = __builtin_amdgcn_raw_buffer_load_b32(rsrc(stamps + d, 12), 4u * (lane - 5u), 0, kAuxNT);
+    return h | s;
+}
+
+// Ping-pong software pipeline over datagrams d0, d0 + nw, ...: the loads of
+// datagram i+1 go into the other buffer before datagram i is processed, and
+// no register copy ever waits on them (vmcnt is an in-order counter).
+template <class Pre, class Load, class Proc>
+__device__ __forceinline__ void ping_pong(uint32_t d, uint32_t count, uint32_t nw, Load load, Proc proc)
+{
+    Pre a, b;
+    load(d, a);
+    for (;;) {
+        // past the end the last datagram is loaded again (branch-free prefetch)
+        const uint32_t d1 = d + nw;
+        load(min(d1, count - 1), b);
+        proc(a, d);
+        if (d1 >= count)
+            break;
+        const uint32_t d2 = d1 + nw;
+        load(min(d2, count - 1), a);
+        proc(b, d1);
+        if (d2 >= count)
+            break;
+        d = d2;
+    }
+}
+
+struct Pre {
+    Win w;
+    uint32_t f;
+};
 
 // SIM_FEC: 45-byte header (sim_proto.c:13-18, sim_proto.inl:244-254, 270-283)
 __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict__ parity,
@@ -262,11 +387,12 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
                                                       const uint16_t* __restrict__ fsize,
                                                       const int8_t* __restrict__ status,
                                                       const rfec_fec_stamp* __restrict__ stamps,
+                                                      const uint32_t* __restrict__ order,
                                                       uint8_t* __restrict__ dgram, uint16_t* __restrict__ dlen,
                                                       uint32_t count, uint32_t stride, uint32_t capacity,
                                                       uint32_t dstride)
 {
-    __shared__ uint32_t T[16 * 256];
+    __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords];
     load_tables(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
@@ -275,50 +401,47 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
     uint32_t d = wave_id();
     if (d >= count)
         return;
-    Win cur = load_win(parity + (size_t)d * stride, a0, nch);
-    for (;;) {
-        const uint32_t dn = d + nw;
-        Win nxt = {};
-        if (dn < count)
-            nxt = load_win(parity + (size_t)dn * stride, a0, nch);
-        uint8_t* slot = dgram + (size_t)d * dstride;
-        const uint32_t L = fsize[d];
-        const int st = status ? status[d] : 0;
-        if (st < 0 || L > capacity) {
-            zero_slot(slot, dstride, lane, dlen + d);
-        } else {
-            const rfec_fec_stamp s = stamps[d];
-            const rfec_hdr m = meta[d];
-            Hdr H = {};
-            put<0, 1>(H, RFEC_WIRE_VER);
-            put<1, 1>(H, RFEC_WIRE_FEC);
-            put<2, 4>(H, s.uid);
-            put<6, 2>(H, s.fec_id);
-            put<8, 1>(H, s.row);
-            put<9, 1>(H, s.col);
-            put<10, 1>(H, s.index);
-            put<11, 2>(H, s.count);
-            put<13, 4>(H, s.base_id);
-            put<17, 2>(H, s.transport_seq);
-            put<19, 4>(H, s.send_ts);
-            put<23, 4>(H, m.seq);
-            put<27, 4>(H, m.fid);
-            put<31, 4>(H, m.ts);
-            put<35, 2>(H, m.index);
-            put<37, 2>(H, m.total);
-            put<39, 1>(H, m.ftype);
-            put<40, 1>(H, m.payload_type);
-            put<41, 2>(H, m.size);
-            put<43, 2>(H, L); // mach_data_write length (cf_stream.c:328-337)
-            uint32_t pay[8];
-            funnel_c<3>(cur, pay); // window [32j-48, 32j) -> bytes [32j-45, 32j-13)
-            finish_frame(T, H, 45 + L, pay, lane, slot, dstride, dlen + d);
-        }
-        if (dn >= count)
-            break;
-        d = dn;
-        cur = nxt;
-    }
+    ping_pong<Pre>(d, count, nw,
+                   [&](uint32_t dd, Pre& P) {
+                       P.f = load_fec_fields(stamps, meta, fsize, status, dd, lane);
+                       P.w = load_win<1>(parity + (size_t)dd * stride, a0, nch);
+                   },
+                   [&](const Pre& P, uint32_t d) {
+            const uint32_t o = order ? order[d] : d; // output slot
+            uint8_t* slot = dgram + (size_t)o * dstride;
+            const uint32_t L = fld(P.f, 11);
+            const int st = (int)fld(P.f, 12);
+            if (st < 0 || L > capacity) {
+                zero_slot(slot, dstride, lane, dlen + o);
+            } else {
+                const uint32_t s3 = fld(P.f, 3), s4 = fld(P.f, 4), s5 = fld(P.f, 5);
+                const uint32_t m3 = fld(P.f, 9), m4 = fld(P.f, 10);
+                Hdr H = {};
+                put<0, 1>(H, RFEC_WIRE_VER);
+                put<1, 1>(H, RFEC_WIRE_FEC);
+                put<2, 4>(H, fld(P.f, 0));     // uid
+                put<6, 2>(H, s3 & 0xffffu);     // fec_id
+                put<8, 1>(H, (s4 >> 16) & 0xffu); // row
+                put<9, 1>(H, s4 >> 24);         // col
+                put<10, 1>(H, s5 & 0xffu);      // index
+                put<11, 2>(H, s3 >> 16);        // count
+                put<13, 4>(H, fld(P.f, 1));    // base_id
+                put<17, 2>(H, s4 & 0xffffu);    // transport_seq
+                put<19, 4>(H, fld(P.f, 2));    // send_ts
+                put<23, 4>(H, fld(P.f, 6));    // fec_meta: seq, fid, ts, index, total, ftype, payload_type, size
+                put<27, 4>(H, fld(P.f, 7));
+                put<31, 4>(H, fld(P.f, 8));
+                put<35, 2>(H, m3 & 0xffffu);
+                put<37, 2>(H, m3 >> 16);
+                put<39, 1>(H, m4 & 0xffu);
+                put<40, 1>(H, (m4 >> 8) & 0xffu);
+                put<41, 2>(H, m4 >> 16);
+                put<43, 2>(H, L); // mach_data_write length (cf_stream.c:328-337)
+                uint32_t pay[8];
+                funnel_c<3>(P.w, pay); // window [32j-48, 32j) -> bytes [32j-45, 32j-13)
+                finish_frame(T, H, 45 + L, pay, lane, slot, dstride, dlen + o);
+            }
+                   });
 }
 
 // SIM_SEG header, one of 8 layouts (sim_proto.inl:83-125): PW / FW = 4-byte
@@ -357,11 +480,12 @@ __device__ __forceinline__ uint32_t seg_header(Hdr& H, const rfec_hdr& h, const 
 __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict__ shards,
                                                       const rfec_hdr* __restrict__ hdr,
                                                       const rfec_seg_stamp* __restrict__ stamps,
+                                                      const uint32_t* __restrict__ order,
                                                       uint8_t* __restrict__ dgram, uint16_t* __restrict__ dlen,
                                                       uint32_t count, uint32_t stride, uint32_t capacity,
                                                       uint32_t dstride)
 {
-    __shared__ uint32_t T[16 * 256];
+    __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords];
     load_tables(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
@@ -370,41 +494,58 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
     uint32_t d = wave_id();
     if (d >= count)
         return;
-    Win cur = load_win(shards + (size_t)d * stride, a0, nch);
-    for (;;) {
-        const uint32_t dn = d + nw;
-        Win nxt = {};
-        if (dn < count)
-            nxt = load_win(shards + (size_t)dn * stride, a0, nch);
-        uint8_t* slot = dgram + (size_t)d * dstride;
-        const rfec_hdr h = hdr[d];
-        const uint32_t L = h.size;
-        if (L > capacity) {
-            zero_slot(slot, dstride, lane, dlen + d);
-        } else {
-            const rfec_seg_stamp s = stamps[d];
-            Hdr H = {};
-            const uint32_t layout = (h.seq > 65535u ? 4u : 0u) | (h.fid > 65535u ? 2u : 0u) |
-                                    (h.total > 255u ? 1u : 0u);
-            uint32_t hs, pay[8];
-            // window [32j-32, 32j+16) shifted by 32 - hs bytes
-            switch (layout) {
-            case 0: hs = seg_header<false, false, false>(H, h, s); funnel_c<6>(cur, pay); break;
-            case 1: hs = seg_header<false, false, true>(H, h, s); funnel_c<4>(cur, pay); break;
-            case 2: hs = seg_header<false, true, false>(H, h, s); funnel_c<4>(cur, pay); break;
-            case 3: hs = seg_header<false, true, true>(H, h, s); funnel_c<2>(cur, pay); break;
-            case 4: hs = seg_header<true, false, false>(H, h, s); funnel_c<4>(cur, pay); break;
-            case 5: hs = seg_header<true, false, true>(H, h, s); funnel_c<2>(cur, pay); break;
-            case 6: hs = seg_header<true, true, false>(H, h, s); funnel_c<2>(cur, pay); break;
-            default: hs = seg_header<true, true, true>(H, h, s); funnel_c<0>(cur, pay); break;
+    ping_pong<Pre>(d, count, nw,
+                   [&](uint32_t dd, Pre& P) {
+                       P.f = load_seg_fields(hdr, stamps, dd, lane);
+                       P.w = load_win<2>(shards + (size_t)dd * stride, a0, nch);
+                   },
+                   [&](const Pre& P, uint32_t d) {
+            const uint32_t o = order ? order[d] : d; // output slot
+            uint8_t* slot = dgram + (size_t)o * dstride;
+            rfec_hdr h;
+            {
+                const uint32_t h3 = fld(P.f, 3), h4 = fld(P.f, 4);
+                h.seq = fld(P.f, 0);
+                h.fid = fld(P.f, 1);
+                h.ts = fld(P.f, 2);
+                h.index = (uint16_t)h3;
+                h.total = (uint16_t)(h3 >> 16);
+                h.ftype = (uint8_t)h4;
+                h.payload_type = (uint8_t)(h4 >> 8);
+                h.size = (uint16_t)(h4 >> 16);
             }
-            finish_frame(T, H, hs + L, pay, lane, slot, dstride, dlen + d);
-        }
-        if (dn >= count)
-            break;
-        d = dn;
-        cur = nxt;
-    }
+            const uint32_t L = h.size;
+            if (L > capacity) {
+                zero_slot(slot, dstride, lane, dlen + o);
+            } else {
+                rfec_seg_stamp s;
+                {
+                    const uint32_t s1 = fld(P.f, 6), s2 = fld(P.f, 7);
+                    s.uid = fld(P.f, 5);
+                    s.fec_id = (uint16_t)s1;
+                    s.send_ts = (uint16_t)(s1 >> 16);
+                    s.transport_seq = (uint16_t)s2;
+                    s.remb = (uint8_t)(s2 >> 16);
+                    s.reserved = 0;
+                }
+                Hdr H = {};
+                const uint32_t layout = (h.seq > 65535u ? 4u : 0u) | (h.fid > 65535u ? 2u : 0u) |
+                                        (h.total > 255u ? 1u : 0u);
+                uint32_t hs, pay[8];
+                // window [32j-32, 32j+16) shifted by 32 - hs bytes
+                switch (layout) {
+                case 0: hs = seg_header<false, false, false>(H, h, s); funnel_c<6>(P.w, pay); break;
+                case 1: hs = seg_header<false, false, true>(H, h, s); funnel_c<4>(P.w, pay); break;
+                case 2: hs = seg_header<false, true, false>(H, h, s); funnel_c<4>(P.w, pay); break;
+                case 3: hs = seg_header<false, true, true>(H, h, s); funnel_c<2>(P.w, pay); break;
+                case 4: hs = seg_header<true, false, false>(H, h, s); funnel_c<4>(P.w, pay); break;
+                case 5: hs = seg_header<true, false, true>(H, h, s); funnel_c<2>(P.w, pay); break;
+                case 6: hs = seg_header<true, true, false>(H, h, s); funnel_c<2>(P.w, pay); break;
+                default: hs = seg_header<true, true, true>(H, h, s); funnel_c<0>(P.w, pay); break;
+                }
+                finish_frame(T, H, hs + L, pay, lane, slot, dstride, dlen + o);
+            }
+                   });
 }
 
 // ---------------------------------------------------------------------------
@@ -519,216 +660,226 @@ __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ dg
                                                   rfec_wire_rec* __restrict__ recs, uint8_t* __restrict__ payload,
                                                   uint32_t n, uint32_t dstride, uint32_t stride, uint32_t capacity)
 {
-    __shared__ uint32_t T[16 * 256];
+    __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords];
     __shared__ uint32_t stage[kWavesPerBlock][16]; // first 64 bytes of each wave's datagram (slow path)
     load_tables(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wl = threadIdx.x >> 6;
     const uint32_t nw = gridDim.x * kWavesPerBlock;
     const int nch = (int)(dstride >> 4);
+    const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t d = wave_id();
     if (d >= n)
         return;
-    Win cur = load_win(dgram + (size_t)d * dstride, 2 * (int)lane, nch);
-    const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (;;) {
-        const uint32_t dn = d + nw;
-        Win nxt = {};
-        if (dn < n)
-            nxt = load_win(dgram + (size_t)dn * dstride, 2 * (int)lane, nch);
-        uint8_t* slot = payload + (size_t)d * stride;
-        const uint32_t len = dlen[d];
-        rfec_wire_rec rec = {};
-        rec.status = RFEC_WIRE_EBADCRC;
-        int data_at = -1;
-        uint32_t dsize = 0;
-        if (len >= 4 && len <= dstride) {
-            // datagram bytes [32j, 32j+32), zero from `len` on
-            uint32_t w[8], m[8];
+    ping_pong<Pre>(d, n, nw,
+                   [&](uint32_t dd, Pre& P) {
+                       P.f = __builtin_amdgcn_raw_buffer_load_b16(rsrc(dlen + dd, 2), 2u * lane, 0, kAuxNT);
+                       P.w = load_win<0>(dgram + (size_t)dd * dstride, 2 * (int)lane, nch);
+                   },
+                   [&](const Pre& P, uint32_t d) {
+            uint8_t* slot = payload + (size_t)d * stride;
+            const uint32_t len = fld(P.f, 0);
+            rfec_wire_rec rec = {};
+            rec.status = RFEC_WIRE_EBADCRC;
+            int data_at = -1;
+            uint32_t dsize = 0;
+            if (len >= 4 && len <= dstride) {
+                // datagram bytes [32j, 32j+32), zero from `len` on
+                uint32_t w[8], m[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int p0 = 32 * (int)lane + 4 * k;
-                w[k] = cur.c[k >> 2][k & 3] & keep_mask((int)len - p0);
-                m[k] = w[k] & keep_mask((int)len - 4 - p0);
-            }
-            // CRC over [0, len-4) against the big-endian trailer (sim_proto.c:21-37)
-            const uint32_t crc = wave_crc32(T, m, len - 4, RFEC_WIRE_CRC_SEED, lane);
-            const uint32_t tp = len - 4, tl = tp >> 5, tk = (tp & 31u) >> 2;
-            uint32_t lo = w[0], hi = w[1];
-#pragma unroll
-            for (int k = 1; k < 8; ++k) {
-                lo = tk == (uint32_t)k ? w[k] : lo;
-                hi = tk == (uint32_t)k ? (k < 7 ? w[k + 1] : 0u) : hi;
-            }
-            const uint32_t nx = (uint32_t)__shfl_down((int)w[0], 1, kWave); // next lane's first dword
-            hi = tk == 7u ? nx : hi;
-            const uint64_t t2 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, (int)tl) << 32 |
-                                (uint32_t)__builtin_amdgcn_readlane((int)lo, (int)tl);
-            const uint32_t trailer = bswap((uint32_t)(t2 >> (8 * (tp & 3u))));
-            if (crc == trailer) {
-                uint32_t H[12];
-#pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    H[k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 0);
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    H[8 + k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 1);
-                rec.ver = (uint8_t)get<0, 1>(H);
-                rec.mid = (uint8_t)get<1, 1>(H);
-                const uint32_t mid = rec.mid;
-                const uint32_t smask = get<6, 1>(H);
-                const uint32_t seg_hl = 26u + ((smask & 0x80u) ? 2u : 0u) + ((smask & 0x40u) ? 2u : 0u) +
-                                        ((smask & 0x20u) ? 2u : 0u); // through the data length field
-                const bool fast = len >= 6 && ((mid == RFEC_WIRE_FEC && len >= 45) ||
-                                               (mid == RFEC_WIRE_SEG && len >= seg_hl) ||
-                                               (mid != RFEC_WIRE_FEC && mid != RFEC_WIRE_SEG));
-                uint32_t npos = 0, nval = 0;
-                if (fast) {
-                    rec.uid = get<2, 4>(H);
-                    if (mid < RFEC_WIRE_MIN_MID || mid > RFEC_WIRE_MAX_MID) {
-                        rec.status = RFEC_WIRE_EMID;
-                    } else if (mid == RFEC_WIRE_SEG) { // sim_segment_decode, sim_proto.inl:127-179
-                        rec.hdr.payload_type = (uint8_t)get<7, 1>(H);
-                        rec.hdr.ftype = (uint8_t)(smask & 1u);
-                        rec.remb = (smask & 0x10u) ? 0 : 0xff;
-                        switch (smask >> 5) {
-                        case 0: npos = seg_fields<false, false, false>(H, rec); break;
-                        case 1: npos = seg_fields<false, false, true>(H, rec); break;
-                        case 2: npos = seg_fields<false, true, false>(H, rec); break;
-                        case 3: npos = seg_fields<false, true, true>(H, rec); break;
-                        case 4: npos = seg_fields<true, false, false>(H, rec); break;
-                        case 5: npos = seg_fields<true, false, true>(H, rec); break;
-                        case 6: npos = seg_fields<true, true, false>(H, rec); break;
-                        default: npos = seg_fields<true, true, true>(H, rec); break;
-                        }
-                        nval = (H[npos >> 2] >> (8 * (npos & 3)) & 0xffu) << 8;
-                        nval |= H[(npos + 1) >> 2] >> (8 * ((npos + 1) & 3)) & 0xffu;
-                        rec.status = RFEC_WIRE_OK;
-                    } else if (mid == RFEC_WIRE_FEC) { // sim_fec_decode, sim_proto.inl:287-307
-                        rec.fec_id = (uint16_t)get<6, 2>(H);
-                        rec.row = (uint8_t)get<8, 1>(H);
-                        rec.col = (uint8_t)get<9, 1>(H);
-                        rec.index = (uint8_t)get<10, 1>(H);
-                        rec.count = (uint16_t)get<11, 2>(H);
-                        rec.base_id = get<13, 4>(H);
-                        rec.transport_seq = (uint16_t)get<17, 2>(H);
-                        rec.send_ts = get<19, 4>(H);
-                        rec.hdr.seq = get<23, 4>(H);
-                        rec.hdr.fid = get<27, 4>(H);
-                        rec.hdr.ts = get<31, 4>(H);
-                        rec.hdr.index = (uint16_t)get<35, 2>(H);
-                        rec.hdr.total = (uint16_t)get<37, 2>(H);
-                        rec.hdr.ftype = (uint8_t)get<39, 1>(H);
-                        rec.hdr.payload_type = (uint8_t)get<40, 1>(H);
-                        rec.hdr.size = (uint16_t)get<41, 2>(H);
-                        npos = 43;
-                        nval = get<43, 2>(H);
-                        rec.status = RFEC_WIRE_OK;
-                    } else {
-                        rec.status = RFEC_WIRE_OTHER;
-                    }
-                    npos += 2;
-                } else {
-                    // truncated header: emulate the bin_stream reader byte by byte
-                    if (lane < 2) {
-                        volatile uint32_t* sg = stage[wl];
-#pragma unroll
-                        for (int k = 0; k < 8; ++k)
-                            sg[8 * lane + k] = w[k];
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    Cursor c{reinterpret_cast<const volatile uint8_t*>(stage[wl]), len, 0};
-                    c.r8();
-                    c.r8();
-                    rec.uid = c.r32();
-                    if (mid < RFEC_WIRE_MIN_MID || mid > RFEC_WIRE_MAX_MID) {
-                        rec.status = RFEC_WIRE_EMID;
-                    } else if (mid == RFEC_WIRE_SEG) {
-                        const uint32_t mk = c.r8();
-                        rec.hdr.payload_type = (uint8_t)c.r8();
-                        rec.hdr.ftype = (uint8_t)(mk & 1u);
-                        rec.hdr.seq = (mk & 0x80u) ? c.r32() : c.r16();
-                        rec.hdr.fid = (mk & 0x40u) ? c.r32() : c.r16();
-                        rec.hdr.ts = c.r32();
-                        if (mk & 0x20u) {
-                            rec.hdr.index = (uint16_t)c.r16();
-                            rec.hdr.total = (uint16_t)c.r16();
-                        } else {
-                            rec.hdr.index = (uint16_t)c.r8();
-                            rec.hdr.total = (uint16_t)c.r8();
-                        }
-                        rec.remb = (mk & 0x10u) ? 0 : 0xff;
-                        rec.fec_id = (uint16_t)c.r16();
-                        rec.send_ts = c.r16();
-                        rec.transport_seq = (uint16_t)c.r16();
-                        nval = c.r16();
-                        npos = c.pos;
-                        rec.status = RFEC_WIRE_OK;
-                    } else if (mid == RFEC_WIRE_FEC) {
-                        rec.fec_id = (uint16_t)c.r16();
-                        rec.row = (uint8_t)c.r8();
-                        rec.col = (uint8_t)c.r8();
-                        rec.index = (uint8_t)c.r8();
-                        rec.count = (uint16_t)c.r16();
-                        rec.base_id = c.r32();
-                        rec.transport_seq = (uint16_t)c.r16();
-                        rec.send_ts = c.r32();
-                        rec.hdr.seq = c.r32();
-                        rec.hdr.fid = c.r32();
-                        rec.hdr.ts = c.r32();
-                        rec.hdr.index = (uint16_t)c.r16();
-                        rec.hdr.total = (uint16_t)c.r16();
-                        rec.hdr.ftype = (uint8_t)c.r8();
-                        rec.hdr.payload_type = (uint8_t)c.r8();
-                        rec.hdr.size = (uint16_t)c.r16();
-                        nval = c.r16();
-                        npos = c.pos;
-                        rec.status = RFEC_WIRE_OK;
-                    } else {
-                        rec.status = RFEC_WIRE_OTHER;
-                    }
+                for (int k = 0; k < 8; ++k) {
+                    const int p0 = 32 * (int)lane + 4 * k;
+                    w[k] = P.w.c[k >> 2][k & 3] & keep_mask((int)len - p0);
+                    m[k] = w[k] & keep_mask((int)len - 4 - p0);
                 }
-                // mach_data_read, cf_stream.c:339-355
-                const bool data_ok = nval <= capacity && npos + nval <= len;
-                if (mid == RFEC_WIRE_SEG && rec.status == RFEC_WIRE_OK) {
-                    dsize = data_ok ? nval : 0u; // a bad length decodes as size 0 (sim_proto.inl:174-176)
-                    data_at = data_ok ? (int)npos : -1;
-                    rec.hdr.size = (uint16_t)dsize;
-                } else if (mid == RFEC_WIRE_FEC && rec.status == RFEC_WIRE_OK) {
-                    if (data_ok) {
-                        dsize = nval;
-                        data_at = (int)npos;
-                    } else {
-                        rec.status = RFEC_WIRE_EBODY; // sim_proto.inl:301-305
-                    }
+                // CRC over [0, len-4) against the big-endian trailer (sim_proto.c:21-37)
+                const uint32_t crc = wave_crc32(T, m, len - 4, RFEC_WIRE_CRC_SEED, lane);
+                const uint32_t tp = len - 4, tl = tp >> 5, tk = (tp & 31u) >> 2;
+                uint32_t lo = w[0], hi = w[1];
+#pragma unroll
+                for (int k = 1; k < 8; ++k) {
+                    lo = tk == (uint32_t)k ? w[k] : lo;
+                    hi = tk == (uint32_t)k ? (k < 7 ? w[k + 1] : 0u) : hi;
                 }
-                rec.data_size = (uint16_t)dsize;
-                if (data_at >= 0) {
-                    uint32_t pay[8];
-                    shift_down_bytes(w, (uint32_t)data_at, pay);
+                const uint32_t nx = (uint32_t)__shfl_down((int)w[0], 1, kWave); // next lane's first dword
+                hi = tk == 7u ? nx : hi;
+                const uint64_t t2 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, (int)tl) << 32 |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)lo, (int)tl);
+                const uint32_t trailer = bswap((uint32_t)(t2 >> (8 * (tp & 3u))));
+                if (crc == trailer) {
+                    uint32_t H[12];
 #pragma unroll
                     for (int k = 0; k < 8; ++k)
-                        pay[k] &= keep_mask((int)dsize - 32 * (int)lane - 4 * k);
-                    store_slot(slot, stride, lane, pay);
+                        H[k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 0);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        H[8 + k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 1);
+                    rec.ver = (uint8_t)get<0, 1>(H);
+                    rec.mid = (uint8_t)get<1, 1>(H);
+                    const uint32_t mid = rec.mid;
+                    const uint32_t smask = get<6, 1>(H);
+                    const uint32_t seg_hl = 26u + ((smask & 0x80u) ? 2u : 0u) + ((smask & 0x40u) ? 2u : 0u) +
+                                            ((smask & 0x20u) ? 2u : 0u); // through the data length field
+                    const bool fast = len >= 6 && ((mid == RFEC_WIRE_FEC && len >= 45) ||
+                                                   (mid == RFEC_WIRE_SEG && len >= seg_hl) ||
+                                                   (mid != RFEC_WIRE_FEC && mid != RFEC_WIRE_SEG));
+                    uint32_t npos = 0, nval = 0;
+                    if (fast) {
+                        rec.uid = get<2, 4>(H);
+                        if (mid < RFEC_WIRE_MIN_MID || mid > RFEC_WIRE_MAX_MID) {
+                            rec.status = RFEC_WIRE_EMID;
+                        } else if (mid == RFEC_WIRE_SEG) { // sim_segment_decode, sim_proto.inl:127-179
+                            rec.hdr.payload_type = (uint8_t)get<7, 1>(H);
+                            rec.hdr.ftype = (uint8_t)(smask & 1u);
+                            rec.remb = (smask & 0x10u) ? 0 : 0xff;
+                            switch (smask >> 5) {
+                            case 0: npos = seg_fields<false, false, false>(H, rec); break;
+                            case 1: npos = seg_fields<false, false, true>(H, rec); break;
+                            case 2: npos = seg_fields<false, true, false>(H, rec); break;
+                            case 3: npos = seg_fields<false, true, true>(H, rec); break;
+                            case 4: npos = seg_fields<true, false, false>(H, rec); break;
+                            case 5: npos = seg_fields<true, false, true>(H, rec); break;
+                            case 6: npos = seg_fields<true, true, false>(H, rec); break;
+                            default: npos = seg_fields<true, true, true>(H, rec); break;
+                            }
+                            nval = (H[npos >> 2] >> (8 * (npos & 3)) & 0xffu) << 8;
+                            nval |= H[(npos + 1) >> 2] >> (8 * ((npos + 1) & 3)) & 0xffu;
+                            rec.status = RFEC_WIRE_OK;
+                        } else if (mid == RFEC_WIRE_FEC) { // sim_fec_decode, sim_proto.inl:287-307
+                            rec.fec_id = (uint16_t)get<6, 2>(H);
+                            rec.row = (uint8_t)get<8, 1>(H);
+                            rec.col = (uint8_t)get<9, 1>(H);
+                            rec.index = (uint8_t)get<10, 1>(H);
+                            rec.count = (uint16_t)get<11, 2>(H);
+                            rec.base_id = get<13, 4>(H);
+                            rec.transport_seq = (uint16_t)get<17, 2>(H);
+                            rec.send_ts = get<19, 4>(H);
+                            rec.hdr.seq = get<23, 4>(H);
+                            rec.hdr.fid = get<27, 4>(H);
+                            rec.hdr.ts = get<31, 4>(H);
+                            rec.hdr.index = (uint16_t)get<35, 2>(H);
+                            rec.hdr.total = (uint16_t)get<37, 2>(H);
+                            rec.hdr.ftype = (uint8_t)get<39, 1>(H);
+                            rec.hdr.payload_type = (uint8_t)get<40, 1>(H);
+                            rec.hdr.size = (uint16_t)get<41, 2>(H);
+                            npos = 43;
+                            nval = get<43, 2>(H);
+                            rec.status = RFEC_WIRE_OK;
+                        } else {
+                            rec.status = RFEC_WIRE_OTHER;
+                        }
+                        npos += 2;
+                    } else {
+                        // truncated header: emulate the bin_stream reader byte by byte
+                        if (lane < 2) {
+                            volatile uint32_t* sg = stage[wl];
+#pragma unroll
+                            for (int k = 0; k < 8; ++k)
+                                sg[8 * lane + k] = w[k];
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        Cursor c{reinterpret_cast<const volatile uint8_t*>(stage[wl]), len, 0};
+                        c.r8();
+                        c.r8();
+                        rec.uid = c.r32();
+                        if (mid < RFEC_WIRE_MIN_MID || mid > RFEC_WIRE_MAX_MID) {
+                            rec.status = RFEC_WIRE_EMID;
+                        } else if (mid == RFEC_WIRE_SEG) {
+                            const uint32_t mk = c.r8();
+                            rec.hdr.payload_type = (uint8_t)c.r8();
+                            rec.hdr.ftype = (uint8_t)(mk & 1u);
+                            rec.hdr.seq = (mk & 0x80u) ? c.r32() : c.r16();
+                            rec.hdr.fid = (mk & 0x40u) ? c.r32() : c.r16();
+                            rec.hdr.ts = c.r32();
+                            if (mk & 0x20u) {
+                                rec.hdr.index = (uint16_t)c.r16();
+                                rec.hdr.total = (uint16_t)c.r16();
+                            } else {
+                                rec.hdr.index = (uint16_t)c.r8();
+                                rec.hdr.total = (uint16_t)c.r8();
+                            }
+                            rec.remb = (mk & 0x10u) ? 0 : 0xff;
+                            rec.fec_id = (uint16_t)c.r16();
+                            rec.send_ts = c.r16();
+                            rec.transport_seq = (uint16_t)c.r16();
+                            nval = c.r16();
+                            npos = c.pos;
+                            rec.status = RFEC_WIRE_OK;
+                        } else if (mid == RFEC_WIRE_FEC) {
+                            rec.fec_id = (uint16_t)c.r16();
+                            rec.row = (uint8_t)c.r8();
+                            rec.col = (uint8_t)c.r8();
+                            rec.index = (uint8_t)c.r8();
+                            rec.count = (uint16_t)c.r16();
+                            rec.base_id = c.r32();
+                            rec.transport_seq = (uint16_t)c.r16();
+                            rec.send_ts = c.r32();
+                            rec.hdr.seq = c.r32();
+                            rec.hdr.fid = c.r32();
+                            rec.hdr.ts = c.r32();
+                            rec.hdr.index = (uint16_t)c.r16();
+                            rec.hdr.total = (uint16_t)c.r16();
+                            rec.hdr.ftype = (uint8_t)c.r8();
+                            rec.hdr.payload_type = (uint8_t)c.r8();
+                            rec.hdr.size = (uint16_t)c.r16();
+                            nval = c.r16();
+                            npos = c.pos;
+                            rec.status = RFEC_WIRE_OK;
+                        } else {
+                            rec.status = RFEC_WIRE_OTHER;
+                        }
+                    }
+                    // mach_data_read, cf_stream.c:339-355
+                    const bool data_ok = nval <= capacity && npos + nval <= len;
+                    if (mid == RFEC_WIRE_SEG && rec.status == RFEC_WIRE_OK) {
+                        dsize = data_ok ? nval : 0u; // a bad length decodes as size 0 (sim_proto.inl:174-176)
+                        data_at = data_ok ? (int)npos : -1;
+                        rec.hdr.size = (uint16_t)dsize;
+                    } else if (mid == RFEC_WIRE_FEC && rec.status == RFEC_WIRE_OK) {
+                        if (data_ok) {
+                            dsize = nval;
+                            data_at = (int)npos;
+                        } else {
+                            rec.status = RFEC_WIRE_EBODY; // sim_proto.inl:301-305
+                        }
+                    }
+                    rec.data_size = (uint16_t)dsize;
+                    if (data_at >= 0) {
+                        uint32_t pay[8];
+                        shift_down_bytes(w, (uint32_t)data_at, pay);
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            pay[k] &= keep_mask((int)dsize - 32 * (int)lane - 4 * k);
+                        store_slot(slot, stride, lane, pay);
+                    }
                 }
             }
-        }
-        write_rec(recs + d, rec, lane);
-        if (data_at < 0)
-            store_slot(slot, stride, lane, z);
-        if (dn >= n)
-            break;
-        d = dn;
-        cur = nxt;
-    }
+            write_rec(recs + d, rec, lane);
+            if (data_at < 0)
+                store_slot(slot, stride, lane, z);
+                   });
 }
 
-uint32_t grid_for(uint32_t count)
+// Persistent grid: exactly the blocks that are resident at once (occupancy
+// from the kernel's registers / LDS x CUs), so no block waits for a second
+// round; fewer when the batch is small.
+template <class K>
+uint32_t grid_for(K kernel, uint32_t count)
 {
+    static int resident = 0; // blocks per device, per kernel
+    if (!resident) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || cus <= 0 ||
+            per_cu <= 0)
+            cus = 256, per_cu = 2;
+        resident = cus * per_cu;
+    }
     const uint32_t blocks = (count + kWavesPerBlock - 1) / kWavesPerBlock;
-    return blocks < 2048u ? (blocks ? blocks : 1u) : 2048u;
+    return blocks < (uint32_t)resident ? (blocks ? blocks : 1u) : (uint32_t)resident;
 }
 
 } // namespace
@@ -737,27 +888,29 @@ extern "C" {
 
 int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
                                const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,
-                               const rfec_fec_stamp* stamps, uint32_t dstride, uint8_t* dgram, uint16_t* dlen,
-                               void* stream)
+                               const rfec_fec_stamp* stamps, const uint32_t* order, uint32_t dstride,
+                               uint8_t* dgram, uint16_t* dlen, void* stream)
 {
-    hipLaunchKernelGGL(k_frame_fec, dim3(grid_for(count)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
-                       parity, meta, fec_size, status, stamps, dgram, dlen, count, stride, capacity, dstride);
+    hipLaunchKernelGGL(k_frame_fec, dim3(grid_for(k_frame_fec, count)), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), parity, meta, fec_size, status, stamps, order, dgram,
+                       dlen, count, stride, capacity, dstride);
     return (int)hipGetLastError();
 }
 
 int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* shards,
-                               const rfec_hdr* hdr, const rfec_seg_stamp* stamps, uint32_t dstride, uint8_t* dgram,
-                               uint16_t* dlen, void* stream)
+                               const rfec_hdr* hdr, const rfec_seg_stamp* stamps, const uint32_t* order,
+                               uint32_t dstride, uint8_t* dgram, uint16_t* dlen, void* stream)
 {
-    hipLaunchKernelGGL(k_frame_seg, dim3(grid_for(count)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
-                       shards, hdr, stamps, dgram, dlen, count, stride, capacity, dstride);
+    hipLaunchKernelGGL(k_frame_seg, dim3(grid_for(k_frame_seg, count)), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), shards, hdr, stamps, order, dgram, dlen, count, stride,
+                       capacity, dstride);
     return (int)hipGetLastError();
 }
 
 int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
                            uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload, void* stream)
 {
-    hipLaunchKernelGGL(k_parse, dim3(grid_for(n)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), dgram,
+    hipLaunchKernelGGL(k_parse, dim3(grid_for(k_parse, n)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), dgram,
                        dlen, recs, payload, n, dstride, stride, capacity);
     return (int)hipGetLastError();
 }

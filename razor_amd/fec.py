@@ -61,6 +61,28 @@ WIRE_REC_DTYPE = np.dtype([("status", "i1"), ("ver", "u1"), ("mid", "u1"), ("rem
                            ("col", "u1"), ("index", "u1"), ("reserved", "u1", (17,))])
 assert FEC_STAMP_DTYPE.itemsize == 24 and SEG_STAMP_DTYPE.itemsize == 12 and WIRE_REC_DTYPE.itemsize == 64
 
+# sender staging (include/razor_fec.h)
+FRAME_DTYPE = np.dtype([("data", "<u8"), ("size", "<u4"), ("payload_type", "u1"), ("ftype", "u1"),
+                        ("protect_fraction", "u1"), ("reserved", "u1"), ("now_ms", "<i8")])
+SENDER_STATE_DTYPE = np.dtype([("packet_id_seed", "<u4"), ("send_id_seed", "<u4"), ("frame_id_seed", "<u4"),
+                               ("pad0", "<u4"), ("first_ts", "<i8"), ("fec_ts", "<i8"), ("base_id", "<u4"),
+                               ("open_seg", "<i4"), ("fec_id", "<u2"), ("segs_count", "<u2"), ("first", "<i4"),
+                               ("transport_seq_seed", "<u4"), ("pad1", "<u4")])
+SEG_PLAN_DTYPE = np.dtype([("frame", "<u4"), ("offset", "<u4"), ("packet_id", "<u4"), ("send_id", "<u4"),
+                           ("fid", "<u4"), ("timestamp", "<u4"), ("index", "<u2"), ("total", "<u2"),
+                           ("data_size", "<u2"), ("fec_id", "<u2"), ("ftype", "u1"), ("payload_type", "u1"),
+                           ("reserved", "u1", (2,)), ("group", "<i4")])
+GROUP_PLAN_DTYPE = np.dtype([("first_seg", "<i4"), ("count", "<u2"), ("fec_id", "<u2"), ("base_id", "<u4"),
+                             ("fec_send_id0", "<u4"), ("fec_ts", "<u4"), ("protect_fraction", "u1"),
+                             ("n_lines", "u1"), ("reserved", "u1", (2,))])
+
+
+class rfec_send_report(C.Structure):
+    _fields_ = [("n_segs", C.c_uint32), ("n_groups", C.c_uint32), ("n_parities", C.c_uint32),
+                ("n_shapes", C.c_uint32), ("plan_us", C.c_double), ("stage_us", C.c_double),
+                ("h2d_us", C.c_double), ("kernel_us", C.c_double), ("d2h_us", C.c_double),
+                ("total_us", C.c_double)]
+
 
 class RfecError(RuntimeError):
     pass
@@ -151,10 +173,14 @@ _SIGS = {
     "rfec_recover_batch": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, C.c_uint32, C.c_uint32,
                                      _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rfec_zero_tails": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P]),
-    "rfec_wire_frame_fec": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint32, _P, _P,
-                                      _P]),
-    "rfec_wire_frame_seg": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_uint32, _P, _P, _P]),
+    "rfec_wire_frame_fec": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, _P, C.c_uint32, _P,
+                                      _P, _P]),
+    "rfec_wire_frame_seg": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, _P, C.c_uint32, _P, _P, _P]),
     "rfec_wire_parse": (C.c_int, [C.c_uint32, C.c_uint32, _P, _P, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    "rfec_sender_init": (None, [_P]),
+    "rfec_sender_plan": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, C.c_uint32, _P, _P, C.c_uint32, _P]),
+    "rfec_host_send_frames": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, C.c_uint32, _P, C.c_uint32,
+                                        C.c_uint32, _P, _P, _P, _P, C.c_uint32, C.POINTER(rfec_send_report)]),
     "rfec_set_tuning": (None, [C.c_uint]),
     "rfec_get_tuning": (C.c_uint, []),
     "rfec_last_error": (C.c_char_p, []),
@@ -249,17 +275,50 @@ class Native:
 
     # -- wire codec (device pointers) -------------------------------------------
     def wire_frame_fec(self, count, stride, capacity, parity, meta, fec_size, status, stamps, dstride, dgram, dlen,
-                       stream=None):
+                       stream=None, order=None):
         self._check(self.lib.rfec_wire_frame_fec(count, stride, capacity, parity, meta, fec_size, status, stamps,
-                                                 dstride, dgram, dlen, stream), "rfec_wire_frame_fec")
+                                                 order, dstride, dgram, dlen, stream), "rfec_wire_frame_fec")
 
-    def wire_frame_seg(self, count, stride, capacity, shards, hdr, stamps, dstride, dgram, dlen, stream=None):
-        self._check(self.lib.rfec_wire_frame_seg(count, stride, capacity, shards, hdr, stamps, dstride, dgram, dlen,
-                                                 stream), "rfec_wire_frame_seg")
+    def wire_frame_seg(self, count, stride, capacity, shards, hdr, stamps, dstride, dgram, dlen, stream=None,
+                       order=None):
+        self._check(self.lib.rfec_wire_frame_seg(count, stride, capacity, shards, hdr, stamps, order, dstride, dgram,
+                                                 dlen, stream), "rfec_wire_frame_seg")
 
     def wire_parse(self, n, dstride, dgram, dlen, stride, capacity, recs, payload, stream=None):
         self._check(self.lib.rfec_wire_parse(n, dstride, dgram, dlen, stride, capacity, recs, payload, stream),
                     "rfec_wire_parse")
+
+    # -- sender staging (host memory) -------------------------------------------
+    def sender_init(self):
+        st = np.zeros(1, SENDER_STATE_DTYPE)
+        self.lib.rfec_sender_init(st.ctypes.data)
+        return st
+
+    def sender_plan(self, st, frames, seg_size, max_segs=1 << 16, max_groups=1 << 14):
+        segs = np.zeros(max_segs, SEG_PLAN_DTYPE)
+        groups = np.zeros(max_groups, GROUP_PLAN_DTYPE)
+        ns, ng = C.c_uint32(), C.c_uint32()
+        self._check(self.lib.rfec_sender_plan(st.ctypes.data, np.ascontiguousarray(frames).ctypes.data, len(frames),
+                                              seg_size, segs.ctypes.data, max_segs, C.byref(ns), groups.ctypes.data,
+                                              max_groups, C.byref(ng)), "rfec_sender_plan")
+        return segs[:ns.value], groups[:ng.value]
+
+    def send_frames(self, st, frames, uid, dstride, max_segs=1 << 16, max_groups=1 << 14, max_parities=1 << 17):
+        """Frames -> (segs, groups, seg datagrams, seg lengths, fec datagrams, fec lengths, report)."""
+        segs = np.zeros(max_segs, SEG_PLAN_DTYPE)
+        groups = np.zeros(max_groups, GROUP_PLAN_DTYPE)
+        sdg = np.zeros((max_segs, dstride), np.uint8)
+        sdl = np.zeros(max_segs, np.uint16)
+        fdg = np.zeros((max_parities, dstride), np.uint8)
+        fdl = np.zeros(max_parities, np.uint16)
+        rep = rfec_send_report()
+        self._check(self.lib.rfec_host_send_frames(st.ctypes.data, np.ascontiguousarray(frames).ctypes.data,
+                                                   len(frames), uid, segs.ctypes.data, max_segs, groups.ctypes.data,
+                                                   max_groups, dstride, sdg.ctypes.data, sdl.ctypes.data,
+                                                   fdg.ctypes.data, fdl.ctypes.data, max_parities, C.byref(rep)),
+                    "rfec_host_send_frames")
+        ns, ng, npar = rep.n_segs, rep.n_groups, rep.n_parities
+        return segs[:ns], groups[:ng], sdg[:ns], sdl[:ns], fdg[:npar], fdl[:npar], rep
 
     def set_tuning(self, flags: int):
         self.lib.rfec_set_tuning(flags)

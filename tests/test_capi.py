@@ -98,3 +98,11 @@ print("RC", lib.flex_fec_generate([a, b], f))
                        cwd=str(po.ROOT))
     assert "RC -1" in r.stdout, r.stdout + r.stderr
     assert "razor_fec" in r.stderr
+
+
+def test_sender_plan_product(product):
+    """rfec_sender_plan (host C, no GPU needed) reproduces the reference flex
+    sender's grouping and stamps (tests/golden/stage.json)."""
+    import stage_cases as sc
+
+    sc.check_plan(product.sender_plan, product.sender_init)

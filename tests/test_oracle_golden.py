@@ -205,3 +205,11 @@ def test_full_size_digest_oracle(oracle1000, name):
 
     c = fd.cases()[name]
     assert fd.digest(oracle1000.encode_batch, oracle1000, c, chunk=16384) == c["sha256"]
+
+
+def test_sender_plan_oracle(oracle1000):
+    """oracle_sender_plan reproduces the reference flex sender's grouping,
+    stamps and fec_id sequence (tests/golden/stage.json)."""
+    import stage_cases as sc
+
+    sc.check_plan(oracle1000.sender_plan, oracle1000.sender_init)
