@@ -398,6 +398,44 @@ int rfec_host_send_frames(rfec_sender_state* st, const rfec_frame* frames, uint3
                           uint32_t dstride, uint8_t* seg_dgram, uint16_t* seg_dlen, uint8_t* fec_dgram,
                           uint16_t* fec_dlen, uint32_t max_parities, rfec_send_report* report);
 
+/* ------------------------------------------------------------------------ */
+/* Receiver ingestion: the receiver-side FEC of one session over a batch of */
+/* parsed datagrams in arrival order (sim_receiver_put / _put_fec,          */
+/* sim_receiver.c:780-838 -> sim_fec_put_segment / sim_fec_put_fec_packet,  */
+/* sim_fec.c:104-207 -> flex receiver, flex_fec_receiver.c:69-280).         */
+/* The control plane replays the reference event by event over the 64-byte  */
+/* records on the host: first-arrival dedupe, max_ts (raised by recovered   */
+/* segments too), the 3000 ms parity drop (sim_fec.c:148), flex creation    */
+/* from the first admitted parity and removal when full, and which line     */
+/* recovers which packet and when (so a packet recovered before its own     */
+/* late arrival is delivered, as the reference does).  The bytes stay on    */
+/* the device: every group is peeled by rfec_recover_batch from its arrived */
+/* members and registered parities, and the delivered rows are gathered.    */
+/* Not modelled (counted in n_unmodelled, never delivered wrong): the       */
+/* wall-clock eviction of sim_fec_evict, parity lines outside the sender's  */
+/* row/column plan, geometries the planner cannot express (count > 128 or   */
+/* row * col < count) and parities inconsistent with their members.         */
+/* Output: the recovered segments, ascending packet_id.                     */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    rfec_hdr hdr;     /* recovered header (flex_fec_xor.c:64-85) */
+    uint16_t fec_id;  /* out_seg->fec_id = fec->fec_id (:101) */
+    uint16_t reserved;
+} rfec_rx_seg; /* 24 bytes */
+
+typedef struct {
+    uint32_t n_groups, n_shapes, n_recovered, n_fec_dropped, n_unmodelled, reserved;
+    double host_us, h2d_us, kernel_us, d2h_us, total_us;
+} rfec_rx_report;
+
+/* recs / payload: DEVICE (rfec_wire_parse output), n records in arrival
+ * order, payload rows of `stride` bytes.  max_ts: in/out
+ * (sim_receiver_fec_t.max_ts).  out / out_payload: HOST, up to max_out
+ * recovered segments (payload rows of `stride`, zero beyond data_size). */
+int rfec_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payload, uint32_t stride,
+                    uint32_t capacity, uint32_t* max_ts, rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out,
+                    uint32_t* n_out, rfec_rx_report* report, void* stream);
+
 /* Kernel-selection knobs, for benchmarking and A/B tests (0 = defaults:
  * specialised row kernels where the plan allows, non-temporal streaming). */
 #define RFEC_TUNE_GENERIC 1u       /* always use the generic plan-driven kernel */

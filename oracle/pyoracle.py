@@ -67,6 +67,8 @@ GROUP_PLAN = np.dtype([("first_seg", "<i4"), ("count", "<u2"), ("fec_id", "<u2")
                        ("fec_send_id0", "<u4"), ("fec_ts", "<u4"), ("protect_fraction", "u1"), ("n_lines", "u1"),
                        ("reserved", "u1", (2,))])
 assert FRAME.itemsize == 24 and SENDER_STATE.itemsize == 56 and SEG_PLAN.itemsize == 40 and GROUP_PLAN.itemsize == 24
+RX_SEG = np.dtype([("hdr", HDR_DTYPE), ("fec_id", "<u2"), ("reserved", "<u2")])
+assert RX_SEG.itemsize == 24
 
 SEED = 0x52415A4F52464543
 
@@ -140,6 +142,7 @@ class Oracle:
         L.oracle_wire_parse_batch.argtypes = [C.c_uint32, C.c_uint32, P, P, C.c_uint32, C.c_uint32, P, P]
         L.oracle_sender_init.argtypes = [P]
         L.oracle_sender_plan.argtypes = [P, P, C.c_uint32, C.c_uint32, P, C.c_uint32, P, P, C.c_uint32, P]
+        L.oracle_rx_recover.argtypes = [C.c_uint32, P, P, C.c_uint32, C.c_uint32, P, P, P, C.c_uint32, P, P]
         L.oracle_segment_size.restype = C.c_size_t
         L.oracle_fec_size.restype = C.c_size_t
         self.video_size = L.oracle_sim_video_size()
@@ -266,6 +269,19 @@ class Oracle:
         if rc != 0:
             raise ValueError("sender plan: output arrays too small")
         return segs[:ns.value], groups[:ng.value]
+
+    # -- receiver ingestion ------------------------------------------------------
+    def rx_recover(self, recs, payload, capacity, max_ts=0, max_out=1 << 16):
+        n, stride = payload.shape
+        out = np.zeros(max_out, RX_SEG)
+        outp = np.zeros((max_out, stride), np.uint8)
+        mts, no, dropped = C.c_uint32(max_ts), C.c_uint32(), C.c_uint32()
+        rc = self.lib.oracle_rx_recover(n, _np_ptr(np.ascontiguousarray(recs)), _np_ptr(np.ascontiguousarray(payload)),
+                                        stride, capacity, C.byref(mts), _np_ptr(out), _np_ptr(outp), max_out,
+                                        C.byref(no), C.byref(dropped))
+        if rc != 0:
+            raise ValueError("rx: output too small")
+        return out[:no.value], outp[:no.value], mts.value, dropped.value
 
     # -- AoS (reference-shaped) path for the CPU baseline ---------------------
     def seg_dtype(self):
@@ -403,6 +419,68 @@ def stage_frames(scn, now_ms=1_700_000_000_000):
         frames[i]["now_ms"] = now_ms
         off += f[0]
     return frames, blob
+
+
+def rx_fixture() -> dict:
+    return json.loads((GOLDEN / "rx.json").read_text())
+
+
+def rx_stream(oracle, scn, video_size=1000):
+    """Parsed-datagram records (WIRE_REC) + payload rows, in the arrival order
+    of an rx.json scenario: segments from the sender plan (pinned by
+    stage.json), parities from the oracle encode (pinned by the enc_* fixtures)."""
+    frames, blob = stage_frames(scn)
+    st = oracle.sender_init()
+    segs, groups = oracle.sender_plan(st, frames, video_size)
+    assert [(int(g["fec_id"]), int(g["base_id"]), int(g["count"]), int(g["protect_fraction"])) for g in groups] == \
+        [tuple(g) for g in scn["groups"]]
+    stride = (video_size + 15) // 16 * 16
+    ns = len(segs)
+    seg_pay = np.zeros((ns, stride), np.uint8)
+    base = blob.ctypes.data
+    for i, s in enumerate(segs):
+        off = int(frames["data"][s["frame"]] - base) + int(s["offset"])
+        n = int(s["data_size"])
+        seg_pay[i, :n] = blob[off:off + n]
+    seg_rec = np.zeros(ns, WIRE_REC)
+    seg_rec["mid"], seg_rec["ver"] = 0x17, 1
+    for a, b in (("seq", "packet_id"), ("fid", "fid"), ("index", "index"), ("total", "total"), ("ftype", "ftype"),
+                 ("payload_type", "payload_type"), ("size", "data_size")):
+        seg_rec["hdr"][a] = segs[b]
+    seg_rec["hdr"]["ts"] = 33 * segs["frame"]  # gen_rx.c: 33 ms per frame
+    seg_rec["fec_id"] = segs["fec_id"]
+    seg_rec["data_size"] = segs["data_size"]
+    seg_rec["remb"] = 0xFF
+    par_rec, par_pay = [], []
+    for g in groups:
+        k, pf = int(g["count"]), int(g["protect_fraction"])
+        plan = oracle.plan_from_fraction(k, pf, 3)
+        mem = segs[int(g["first_seg"]):int(g["first_seg"]) + k]
+        hdr = np.zeros((1, k), HDR_DTYPE)
+        hdr[0] = seg_rec["hdr"][int(g["first_seg"]):int(g["first_seg"]) + k]
+        par, meta, fs, _ = oracle.encode_batch(plan, seg_pay[int(g["first_seg"]):int(g["first_seg"]) + k][None], hdr,
+                                               video_size)
+        close_frame = int(mem["frame"][-1])
+        for l in range(plan.n_lines):
+            r = np.zeros((), WIRE_REC)
+            r["mid"], r["ver"] = 0x1C, 1
+            r["fec_id"], r["base_id"], r["count"] = g["fec_id"], g["base_id"], k
+            r["row"], r["col"], r["index"] = plan.row, plan.col, plan.line[l].index
+            r["send_ts"] = 33 * close_frame
+            r["hdr"] = meta[0, l]
+            r["data_size"] = fs[0, l]
+            par_rec.append(r)
+            par_pay.append(par[0, l])
+    assert [(int(par_rec[p]["index"])) for p in range(len(par_rec))] == [q[1] for q in scn["parities"]]
+    arr = np.array(scn["arrivals"], np.int64).reshape(-1, 2)
+    recs = np.zeros(len(arr), WIRE_REC)
+    pay = np.zeros((len(arr), stride), np.uint8)
+    for a, (kind, idx) in enumerate(arr):
+        if kind == 0:
+            recs[a], pay[a] = seg_rec[idx], seg_pay[idx]
+        else:
+            recs[a], pay[a] = par_rec[idx], par_pay[idx]
+    return recs, pay, segs, seg_pay
 
 
 def _xs_next(st: C.c_uint64) -> int:

@@ -964,3 +964,336 @@ int oracle_sender_plan(rfec_sender_state* st, const rfec_frame* frames, uint32_t
     *n_groups = ng;
     return 0;
 }
+
+/* ---- receiver ingestion: sim_fec.c:104-207 + flex_fec_receiver.c:69-280, ----
+ * event by event (the reference's own order), with the recovery cascade of
+ * sim_receiver_recover (sim_receiver.c:780-804). */
+typedef struct { /* open-addressing u32 -> int32 map */
+    uint32_t* key;
+    int32_t* val;
+    uint32_t cap, n;
+} omap;
+
+static void om_init(omap* m, uint32_t cap)
+{
+    m->cap = 16;
+    while (m->cap < 2 * cap)
+        m->cap <<= 1;
+    m->key = (uint32_t*)calloc(m->cap, sizeof(uint32_t));
+    m->val = (int32_t*)malloc(m->cap * sizeof(int32_t));
+    for (uint32_t i = 0; i < m->cap; ++i)
+        m->val[i] = -1;
+    m->n = 0;
+}
+static void om_free(omap* m)
+{
+    free(m->key);
+    free(m->val);
+}
+static uint32_t om_slot(const omap* m, uint32_t k)
+{
+    uint32_t h = (k * 2654435761u) & (m->cap - 1);
+    while (m->val[h] != -1 && m->key[h] != k)
+        h = (h + 1) & (m->cap - 1);
+    return h;
+}
+static int32_t om_get(const omap* m, uint32_t k)
+{
+    return m->val[om_slot(m, k)];
+}
+static void om_put(omap* m, uint32_t k, int32_t v)
+{
+    const uint32_t h = om_slot(m, k);
+    if (m->val[h] == -1)
+        m->n++;
+    m->key[h] = k;
+    m->val[h] = v;
+}
+static void om_del(omap* m, uint32_t k) /* backward-shift deletion */
+{
+    uint32_t h = om_slot(m, k);
+    if (m->val[h] == -1)
+        return;
+    m->val[h] = -1;
+    m->n--;
+    uint32_t j = h;
+    for (;;) {
+        j = (j + 1) & (m->cap - 1);
+        if (m->val[j] == -1)
+            return;
+        const uint32_t want = (m->key[j] * 2654435761u) & (m->cap - 1);
+        if ((j > h && (want <= h || want > j)) || (j < h && (want <= h && want > j))) {
+            m->key[h] = m->key[j];
+            m->val[h] = m->val[j];
+            m->val[j] = -1;
+            h = j;
+        }
+    }
+}
+
+typedef struct {
+    uint16_t fec_id;
+    uint8_t row, col;
+    uint32_t base_id, count;
+    omap segs; /* packet_id -> segment pool index */
+    omap fecs; /* index -> parity record index */
+    int live;
+} oflex;
+
+typedef struct {
+    const rfec_wire_rec* recs;
+    const uint8_t* payload;
+    uint32_t stride, capacity;
+    sim_segment_t* pool; /* cached + recovered segments */
+    uint32_t pool_n, pool_cap;
+    omap seen, cache, recov;
+    omap flex_of;        /* fec_id -> flex index */
+    oflex* flex;
+    uint32_t n_flex, flex_cap;
+    uint32_t max_ts;
+    uint32_t dropped;
+} orx;
+
+static int32_t rx_pool_add(orx* R, const sim_segment_t* s)
+{
+    if (R->pool_n == R->pool_cap) {
+        R->pool_cap = R->pool_cap ? 2 * R->pool_cap : 1024;
+        R->pool = (sim_segment_t*)realloc(R->pool, (size_t)R->pool_cap * sizeof(sim_segment_t));
+    }
+    R->pool[R->pool_n] = *s;
+    return (int32_t)R->pool_n++;
+}
+
+static void rx_fec_struct(const orx* R, int32_t rec, sim_fec_t* f)
+{
+    const rfec_wire_rec* r = &R->recs[rec];
+    memset(f, 0, sizeof(*f));
+    f->fec_id = r->fec_id;
+    f->row = r->row;
+    f->col = r->col;
+    f->index = r->index;
+    f->count = r->count;
+    f->base_id = r->base_id;
+    f->send_ts = r->send_ts;
+    f->transport_seq = r->transport_seq;
+    memcpy(&f->fec_meta, &r->hdr, sizeof(rfec_hdr));
+    f->fec_data_size = r->data_size;
+    memcpy(f->fec_data, R->payload + (size_t)rec * R->stride, r->data_size < SIM_VIDEO_SIZE ? r->data_size : SIM_VIDEO_SIZE);
+}
+
+/* flex_recover_row / flex_recover_col (flex_fec_receiver.c:105-206) */
+static int rx_recover_line(orx* R, oflex* x, int is_col, uint32_t line, sim_segment_t* out)
+{
+    if (x->segs.n >= x->count)
+        return 0;
+    sim_segment_t* cache[256];
+    int cnt = 0, loss = 0;
+    const uint32_t lim = is_col ? x->row : x->col;
+    for (uint32_t i = 0; i < lim; ++i) {
+        const uint32_t key = is_col ? i * x->col + line + x->base_id : line * x->col + i + x->base_id;
+        if (key >= x->base_id + x->count)
+            break;
+        const int32_t p = om_get(&x->segs, key);
+        if (p >= 0)
+            cache[cnt++] = &R->pool[p];
+        else
+            loss++;
+    }
+    if (loss != 1 || cnt == 0)
+        return 0;
+    const int32_t fr = om_get(&x->fecs, is_col ? (line | 0x80u) : line);
+    if (fr < 0)
+        return 0;
+    static sim_fec_t fec;
+    rx_fec_struct(R, fr, &fec);
+    memset(out, 0, sizeof(*out));
+    return oracle_recover(cache, cnt, &fec, out) == 0;
+}
+
+/* sim_fec_packet_add_recover (sim_fec.c:104-119): first copy per packet_id */
+static void rx_add_recover(orx* R, const sim_segment_t* s)
+{
+    if (om_get(&R->recov, s->packet_id) >= 0)
+        return;
+    om_put(&R->recov, s->packet_id, rx_pool_add(R, s));
+}
+
+/* flex_fec_receiver_on_segment (flex_fec_receiver.c:243-280) */
+static void rx_on_segment(orx* R, oflex* x, int32_t pi, int add)
+{
+    const sim_segment_t* s = &R->pool[pi];
+    if (x->col < 2 || x->row == 0 || x->count == 0 || s->packet_id < x->base_id)
+        return;
+    if (om_get(&x->segs, s->packet_id) >= 0)
+        return;
+    om_put(&x->segs, s->packet_id, pi);
+    const uint32_t c = (s->packet_id - x->base_id) % x->col, r = (s->packet_id - x->base_id) / x->col;
+    sim_segment_t out;
+    if (rx_recover_line(R, x, 0, r, &out) && add)
+        rx_add_recover(R, &out);
+    if (rx_recover_line(R, x, 1, c, &out) && add)
+        rx_add_recover(R, &out);
+}
+
+static void rx_remove_flex(orx* R, uint32_t fi)
+{
+    oflex* x = &R->flex[fi];
+    for (uint32_t i = 0; i < x->count; ++i) /* sim_fec_evict_segment (sim_fec.c:93-102) */
+        om_del(&R->cache, x->base_id + i);
+    om_del(&R->flex_of, x->fec_id);
+    om_free(&x->segs);
+    om_free(&x->fecs);
+    x->live = 0;
+}
+
+/* sim_fec_put_segment (sim_fec.c:171-207) */
+static void rx_put_segment(orx* R, const sim_segment_t* s)
+{
+    if (s->packet_id <= 0) /* f->base_id == 0 */
+        return;
+    if (om_get(&R->cache, s->packet_id) >= 0)
+        return;
+    R->max_ts = s->timestamp > R->max_ts ? s->timestamp : R->max_ts;
+    const int32_t pi = rx_pool_add(R, s);
+    om_put(&R->cache, s->packet_id, pi);
+    const int32_t fi = om_get(&R->flex_of, s->fec_id);
+    if (fi < 0)
+        return;
+    rx_on_segment(R, &R->flex[fi], pi, 1);
+    if (R->flex[fi].segs.n >= R->flex[fi].count) /* flex_fec_receiver_full */
+        rx_remove_flex(R, (uint32_t)fi);
+}
+
+/* sim_fec_put_fec_packet (sim_fec.c:141-169) */
+static void rx_put_fec(orx* R, int32_t rec)
+{
+    const rfec_wire_rec* f = &R->recs[rec];
+    if (f->base_id + f->count < 0u + 1u || f->send_ts + 3000u < R->max_ts) { /* EVICT_FEC_DELAY */
+        R->dropped++;
+        return;
+    }
+    int32_t fi = om_get(&R->flex_of, f->fec_id);
+    if (fi < 0) {
+        if (R->n_flex == R->flex_cap) {
+            R->flex_cap = R->flex_cap ? 2 * R->flex_cap : 64;
+            R->flex = (oflex*)realloc(R->flex, R->flex_cap * sizeof(oflex));
+        }
+        fi = (int32_t)R->n_flex++;
+        oflex* x = &R->flex[fi];
+        memset(x, 0, sizeof(*x));
+        x->fec_id = f->fec_id; /* flex_fec_receiver_active (flex_fec_receiver.c:69-88) */
+        x->base_id = f->base_id;
+        x->row = f->row;
+        x->col = f->col;
+        x->count = f->count;
+        x->live = 1;
+        om_init(&x->segs, x->count + 8);
+        om_init(&x->fecs, 64);
+        om_put(&R->flex_of, f->fec_id, fi);
+        for (uint32_t i = 0; i < f->count; ++i) { /* sim_fec_add_segment_to_flex (sim_fec.c:121-138) */
+            const int32_t pi = om_get(&R->cache, f->base_id + i);
+            if (pi >= 0)
+                rx_on_segment(R, x, pi, 0);
+        }
+    }
+    oflex* x = &R->flex[fi];
+    /* flex_fec_receiver_on_fec (flex_fec_receiver.c:208-241) */
+    if (x->col < 2 || x->row == 0 || x->count == 0 || om_get(&x->fecs, f->index) >= 0)
+        return;
+    om_put(&x->fecs, f->index, rec);
+    sim_segment_t out;
+    if (rx_recover_line(R, x, (f->index & 0x80) != 0, f->index & 0x7Fu, &out))
+        rx_add_recover(R, &out);
+}
+
+int oracle_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payload, uint32_t stride,
+                      uint32_t capacity, uint32_t* max_ts, rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out,
+                      uint32_t* n_out, uint32_t* dropped)
+{
+    orx R;
+    memset(&R, 0, sizeof(R));
+    R.recs = recs;
+    R.payload = payload;
+    R.stride = stride;
+    R.capacity = capacity;
+    R.max_ts = *max_ts;
+    om_init(&R.seen, n + 16);
+    om_init(&R.cache, n + 16);
+    om_init(&R.recov, 64);
+    om_init(&R.flex_of, 1024);
+    uint32_t no = 0;
+    sim_segment_t seg;
+    for (uint32_t a = 0; a < n; ++a) {
+        const rfec_wire_rec* r = &recs[a];
+        if (r->status != RFEC_WIRE_OK)
+            continue;
+        if (r->mid == RFEC_WIRE_SEG) { /* sim_receiver_put (sim_receiver.c:811-827) */
+            if (om_get(&R.seen, r->hdr.seq) >= 0)
+                continue;
+            om_put(&R.seen, r->hdr.seq, 1);
+            if (r->fec_id == 0)
+                continue;
+            memset(&seg, 0, sizeof(seg));
+            seg.packet_id = r->hdr.seq;
+            seg.fid = r->hdr.fid;
+            seg.timestamp = r->hdr.ts;
+            seg.index = r->hdr.index;
+            seg.total = r->hdr.total;
+            seg.ftype = r->hdr.ftype;
+            seg.payload_type = r->hdr.payload_type;
+            seg.fec_id = r->fec_id;
+            seg.data_size = r->data_size;
+            memcpy(seg.data, payload + (size_t)a * stride, r->data_size < SIM_VIDEO_SIZE ? r->data_size : SIM_VIDEO_SIZE);
+            rx_put_segment(&R, &seg);
+        } else if (r->mid == RFEC_WIRE_FEC) {
+            rx_put_fec(&R, (int32_t)a);
+        }
+        /* sim_receiver_recover (sim_receiver.c:780-804): lowest packet_id first */
+        while (R.recov.n > 0) {
+            uint32_t best = 0xFFFFFFFFu;
+            for (uint32_t h = 0; h < R.recov.cap; ++h)
+                if (R.recov.val[h] != -1 && R.recov.key[h] < best)
+                    best = R.recov.key[h];
+            const int32_t pi = om_get(&R.recov, best);
+            om_del(&R.recov, best);
+            const sim_segment_t rs = R.pool[pi];
+            if (om_get(&R.seen, rs.packet_id) >= 0)
+                continue;
+            om_put(&R.seen, rs.packet_id, 1);
+            if (no < max_out) {
+                rfec_rx_seg* o = &out[no];
+                memset(o, 0, sizeof(*o));
+                o->hdr.seq = rs.packet_id;
+                o->hdr.fid = rs.fid;
+                o->hdr.ts = rs.timestamp;
+                o->hdr.index = rs.index;
+                o->hdr.total = rs.total;
+                o->hdr.ftype = rs.ftype;
+                o->hdr.payload_type = rs.payload_type;
+                o->hdr.size = rs.data_size;
+                o->fec_id = rs.fec_id;
+                memset(out_payload + (size_t)no * stride, 0, stride);
+                memcpy(out_payload + (size_t)no * stride, rs.data, rs.data_size);
+            }
+            no++;
+            rx_put_segment(&R, &rs);
+        }
+    }
+    *max_ts = R.max_ts;
+    *n_out = no;
+    if (dropped)
+        *dropped = R.dropped;
+    for (uint32_t i = 0; i < R.n_flex; ++i)
+        if (R.flex[i].live) {
+            om_free(&R.flex[i].segs);
+            om_free(&R.flex[i].fecs);
+        }
+    free(R.flex);
+    free(R.pool);
+    om_free(&R.seen);
+    om_free(&R.cache);
+    om_free(&R.recov);
+    om_free(&R.flex_of);
+    (void)capacity;
+    return no > max_out ? -1 : 0;
+}

@@ -86,6 +86,12 @@ int oracle_sender_plan(rfec_sender_state* st, const rfec_frame* frames, uint32_t
                        rfec_seg_plan* segs, uint32_t max_segs, uint32_t* n_segs, rfec_group_plan* groups,
                        uint32_t max_groups, uint32_t* n_groups);
 
+/* receiver ingestion, event by event (sim_fec.c:104-207, flex_fec_receiver.c:69-280,
+ * sim_receiver.c:780-838); out in delivery order */
+int oracle_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payload, uint32_t stride,
+                      uint32_t capacity, uint32_t* max_ts, rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out,
+                      uint32_t* n_out, uint32_t* dropped);
+
 int oracle_sim_video_size(void);
 size_t oracle_segment_size(void);
 size_t oracle_fec_size(void);

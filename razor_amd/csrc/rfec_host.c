@@ -1369,3 +1369,695 @@ out:
     rep->total_us = now_us() - t0;
     return rc;
 }
+
+/* ------------------------------------------------------------------------ */
+/* 6. receiver ingestion (semantics: include/razor_fec.h, rfec_rx_recover)  */
+/*    The control plane runs in arrival order on the host over headers only: */
+/*    admission, flex lifetime, which line recovers which packet and when    */
+/*    (so max_ts and first-arrival dedupe come out as the reference's).  The */
+/*    bytes never leave the device: the groups are peeled there by           */
+/*    rfec_recover_batch from their arrived members and registered parities. */
+/* ------------------------------------------------------------------------ */
+typedef struct { /* open addressing u32 -> u32, value 0 = empty */
+    uint32_t* k;
+    uint32_t* v;
+    uint32_t mask, n;
+} hmap;
+
+static uint32_t hm_home(const hmap* m, uint32_t k) { return (k * 0x9E3779B1u) & m->mask; }
+
+static int hm_init(hmap* m, uint32_t n)
+{
+    uint32_t cap = 64;
+    while (cap < 2 * n + 64)
+        cap <<= 1;
+    m->k = (uint32_t*)malloc(cap * sizeof(uint32_t));
+    m->v = (uint32_t*)calloc(cap, sizeof(uint32_t));
+    m->mask = cap - 1;
+    m->n = 0;
+    return m->k && m->v ? 0 : -1;
+}
+static void hm_free(hmap* m)
+{
+    free(m->k);
+    free(m->v);
+    m->k = m->v = NULL;
+}
+static uint32_t hm_slot(const hmap* m, uint32_t k)
+{
+    uint32_t h = hm_home(m, k);
+    while (m->v[h] && m->k[h] != k)
+        h = (h + 1) & m->mask;
+    return h;
+}
+static uint32_t hm_get(const hmap* m, uint32_t k) { return m->v[hm_slot(m, k)]; }
+static int hm_put(hmap* m, uint32_t k, uint32_t v)
+{
+    if (2 * (m->n + 1) > m->mask + 1) {
+        hmap g;
+        if (hm_init(&g, 2 * (m->mask + 1)))
+            return -1;
+        for (uint32_t i = 0; i <= m->mask; ++i)
+            if (m->v[i]) {
+                const uint32_t s = hm_slot(&g, m->k[i]);
+                g.k[s] = m->k[i];
+                g.v[s] = m->v[i];
+                g.n++;
+            }
+        hm_free(m);
+        *m = g;
+    }
+    const uint32_t s = hm_slot(m, k);
+    m->n += m->v[s] == 0;
+    m->k[s] = k;
+    m->v[s] = v;
+    return 0;
+}
+static void hm_del(hmap* m, uint32_t k) /* backward-shift deletion */
+{
+    uint32_t h = hm_slot(m, k);
+    if (!m->v[h])
+        return;
+    m->v[h] = 0;
+    m->n--;
+    for (uint32_t j = (h + 1) & m->mask; m->v[j]; j = (j + 1) & m->mask)
+        if (((j - hm_home(m, m->k[j])) & m->mask) >= ((j - h) & m->mask)) {
+            m->k[h] = m->k[j];
+            m->v[h] = m->v[j];
+            m->v[j] = 0;
+            h = j;
+        }
+}
+
+typedef struct {
+    uint32_t count, row, col, n_groups, n_lines, row0, prow0, group0;
+    int16_t line_of[256]; /* FEC index -> plan line, -1: none */
+    rfec_plan plan;
+} rx_shape;
+
+/* one flex receiver (flex_fec_receiver_t) from its creation to its removal */
+typedef struct {
+    uint32_t fec_id, base, count, row, col;
+    uint32_t shape;        /* UINT32_MAX: geometry the reference ignores or the planner cannot express */
+    uint32_t gslot, slot0, line0;
+    uint32_t nsegs;        /* flex->segs.n */
+    uint64_t have[2];      /* members in the flex (arrived or recovered) */
+    uint64_t arrived[2];   /* members that arrived: the device peel starts from these */
+    uint64_t ppm;          /* registered parities, by plan line */
+    int ref_ok;            /* col >= 2 && row >= 1 && count >= 1 (flex_fec_receiver.c:214, 250) */
+} rx_inst;
+
+typedef struct {
+    rfec_hdr hdr;
+    uint32_t inst;
+} rx_event; /* a recovered segment: pending, then delivered */
+
+typedef struct {
+    const rfec_wire_rec* R;
+    uint32_t capacity, max_ts, dropped, unmodelled;
+    hmap seen, cache, flex_of, shape_of;
+    rx_inst* G;
+    uint32_t ng, gcap;
+    rx_shape* S;
+    uint32_t ns, scap;
+    int32_t* slot_src; /* record of an arrived member, -1 otherwise */
+    rfec_hdr* slot_hdr;
+    uint32_t nslot, slotcap;
+    int32_t* line_par; /* record of the registered parity, -1 otherwise */
+    uint32_t nline, linecap;
+    rx_event* pend;
+    uint32_t npend, pendcap;
+    rx_event* out;
+    uint32_t nout, outcap;
+    int oom;
+} rx_sim;
+
+#define RX_GROW(ptr, n, cap, need, T)                                                   \
+    do {                                                                                \
+        if ((n) + (need) > (cap)) {                                                     \
+            uint32_t c_ = (cap) ? 2 * (cap) : 1024;                                     \
+            while (c_ < (n) + (need))                                                   \
+                c_ *= 2;                                                                \
+            T* p_ = (T*)realloc((ptr), (size_t)c_ * sizeof(T));                         \
+            if (!p_) {                                                                  \
+                X->oom = 1;                                                             \
+                break;                                                                  \
+            }                                                                           \
+            (ptr) = p_;                                                                 \
+            (cap) = c_;                                                                 \
+        }                                                                               \
+    } while (0)
+
+static rfec_hdr rec_hdr(const rfec_wire_rec* r)
+{
+    rfec_hdr h = r->hdr;
+    h.size = r->data_size; /* seg.data_size = the datagram's (sim_receiver.c) */
+    return h;
+}
+
+static void rx_pend(rx_sim* X, const rfec_hdr* h, uint32_t inst) /* sim_fec_packet_add_recover (sim_fec.c:104-119) */
+{
+    for (uint32_t i = 0; i < X->npend; ++i)
+        if (X->pend[i].hdr.seq == h->seq)
+            return;
+    RX_GROW(X->pend, X->npend, X->pendcap, 1, rx_event);
+    if (X->oom)
+        return;
+    X->pend[X->npend].hdr = *h;
+    X->pend[X->npend++].inst = inst;
+}
+
+/* flex_recover_row / flex_recover_col (flex_fec_receiver.c:105-206) over headers */
+static void rx_check_line(rx_sim* X, uint32_t ii, int l)
+{
+    const rx_inst* g = &X->G[ii];
+    if (l < 0 || g->nsegs >= g->count || !((g->ppm >> l) & 1ull))
+        return;
+    const rfec_line* ln = &X->S[g->shape].plan.line[l];
+    uint32_t loss = 0, cnt = 0;
+    for (uint32_t q = 0; q < ln->count; ++q) {
+        const uint32_t i = ln->first + q * ln->stride;
+        if ((g->have[i >> 6] >> (i & 63)) & 1ull)
+            cnt++;
+        else
+            loss++;
+    }
+    if (loss != 1 || cnt == 0)
+        return;
+    const rfec_wire_rec* f = &X->R[X->line_par[g->line0 + l]];
+    const uint32_t L = f->data_size;
+    if (L > X->capacity)
+        return;
+    rfec_hdr h = f->hdr; /* flex_fec_xor.c:64-99 */
+    for (uint32_t q = 0; q < ln->count; ++q) {
+        const uint32_t i = ln->first + q * ln->stride;
+        if (!((g->have[i >> 6] >> (i & 63)) & 1ull))
+            continue;
+        const rfec_hdr* m = &X->slot_hdr[g->slot0 + i];
+        if (L < m->size)
+            return;
+        h.seq ^= m->seq;
+        h.fid ^= m->fid;
+        h.ts ^= m->ts;
+        h.index ^= m->index;
+        h.total ^= m->total;
+        h.ftype ^= m->ftype;
+        h.payload_type ^= m->payload_type;
+        h.size ^= m->size;
+    }
+    if (h.size > L)
+        return;
+    rx_pend(X, &h, ii);
+}
+
+/* flex_fec_receiver_on_segment (flex_fec_receiver.c:243-280); src = record or -1 */
+static void rx_on_segment(rx_sim* X, uint32_t ii, const rfec_hdr* h, int32_t src, int check)
+{
+    rx_inst* g = &X->G[ii];
+    if (!g->ref_ok || h->seq < g->base)
+        return;
+    if (g->shape == UINT32_MAX) {
+        X->unmodelled++;
+        return;
+    }
+    const uint32_t t = h->seq - g->base;
+    if (t < g->count) {
+        if ((g->have[t >> 6] >> (t & 63)) & 1ull)
+            return;
+        g->have[t >> 6] |= 1ull << (t & 63);
+        X->slot_hdr[g->slot0 + t] = *h;
+        if (src >= 0) {
+            g->arrived[t >> 6] |= 1ull << (t & 63);
+            X->slot_src[g->slot0 + t] = src;
+        }
+    } else if (src < 0) {
+        X->unmodelled++; /* a recovered header outside its group: inconsistent parities */
+    }
+    g->nsegs++;
+    if (check) {
+        const rx_shape* sh = &X->S[g->shape];
+        const uint32_t r = t / g->col, c = t % g->col;
+        rx_check_line(X, ii, r < 128 ? sh->line_of[r] : -1);
+        rx_check_line(X, ii, c < 128 ? sh->line_of[0x80 | c] : -1);
+    }
+}
+
+static void rx_remove(rx_sim* X, uint32_t ii) /* sim_fec_evict_segment + flex removal (sim_fec.c:93-102, 199-205) */
+{
+    const rx_inst* g = &X->G[ii];
+    for (uint32_t i = 0; i < g->count; ++i)
+        hm_del(&X->cache, g->base + i);
+    hm_del(&X->flex_of, g->fec_id);
+}
+
+/* sim_fec_put_segment (sim_fec.c:171-207); cache values: record + 1, or 0x80000000 | delivered index */
+static void rx_put_segment(rx_sim* X, const rfec_hdr* h, uint16_t fec_id, uint32_t cval, int32_t src)
+{
+    if (h->seq == 0 || hm_get(&X->cache, h->seq))
+        return;
+    X->max_ts = h->ts > X->max_ts ? h->ts : X->max_ts;
+    if (hm_put(&X->cache, h->seq, cval)) {
+        X->oom = 1;
+        return;
+    }
+    const uint32_t fi = hm_get(&X->flex_of, fec_id);
+    if (!fi)
+        return;
+    rx_on_segment(X, fi - 1, h, src, 1);
+    if (X->G[fi - 1].nsegs >= X->G[fi - 1].count) /* flex_fec_receiver_full */
+        rx_remove(X, fi - 1);
+}
+
+static uint32_t rx_shape_of(rx_sim* X, uint32_t count, uint32_t row, uint32_t col)
+{
+    if (count > RFEC_MAX_K || row * col < count || row > 255 || col > 255)
+        return UINT32_MAX;
+    const uint32_t key = count << 16 | row << 8 | col;
+    const uint32_t s = hm_get(&X->shape_of, key);
+    if (s)
+        return s - 1;
+    RX_GROW(X->S, X->ns, X->scap, 1, rx_shape);
+    if (X->oom)
+        return UINT32_MAX;
+    rx_shape* sh = &X->S[X->ns];
+    memset(sh, 0, sizeof(*sh));
+    if (rfec_plan_matrix((uint16_t)count, (uint8_t)row, (uint8_t)col, RFEC_LAYER_ROWS | RFEC_LAYER_COLS, &sh->plan))
+        return UINT32_MAX;
+    sh->count = count;
+    sh->row = row;
+    sh->col = col;
+    sh->n_lines = sh->plan.n_lines;
+    for (int i = 0; i < 256; ++i)
+        sh->line_of[i] = -1;
+    for (uint32_t l = 0; l < sh->n_lines; ++l)
+        sh->line_of[sh->plan.line[l].index] = (int16_t)l;
+    if (hm_put(&X->shape_of, key, X->ns + 1)) {
+        X->oom = 1;
+        return UINT32_MAX;
+    }
+    return X->ns++;
+}
+
+/* sim_fec_put_fec_packet (sim_fec.c:141-169) -> flex_fec_receiver_on_fec (flex_fec_receiver.c:208-241) */
+static void rx_put_fec(rx_sim* X, uint32_t a)
+{
+    const rfec_wire_rec* f = &X->R[a];
+    if (f->base_id + f->count == 0u || f->send_ts + 3000u < X->max_ts) {
+        X->dropped++;
+        return;
+    }
+    uint32_t fi = hm_get(&X->flex_of, f->fec_id);
+    if (!fi) { /* flex_fec_receiver_active (flex_fec_receiver.c:69-88) */
+        RX_GROW(X->G, X->ng, X->gcap, 1, rx_inst);
+        if (X->oom)
+            return;
+        rx_inst* g = &X->G[X->ng];
+        memset(g, 0, sizeof(*g));
+        g->fec_id = f->fec_id;
+        g->base = f->base_id;
+        g->count = f->count;
+        g->row = f->row;
+        g->col = f->col;
+        g->ref_ok = g->col >= 2 && g->row >= 1 && g->count >= 1;
+        g->shape = g->ref_ok ? rx_shape_of(X, g->count, g->row, g->col) : UINT32_MAX;
+        if (g->shape != UINT32_MAX) {
+            rx_shape* sh = &X->S[g->shape];
+            g->gslot = sh->n_groups++;
+            RX_GROW(X->slot_src, X->nslot, X->slotcap, g->count, int32_t);
+            RX_GROW(X->slot_hdr, X->nslot, X->slotcap, g->count, rfec_hdr);
+            RX_GROW(X->line_par, X->nline, X->linecap, sh->n_lines, int32_t);
+            if (X->oom)
+                return;
+            g->slot0 = X->nslot;
+            g->line0 = X->nline;
+            for (uint32_t i = 0; i < g->count; ++i)
+                X->slot_src[X->nslot + i] = -1;
+            for (uint32_t l = 0; l < sh->n_lines; ++l)
+                X->line_par[X->nline + l] = -1;
+            X->nslot += g->count;
+            X->nline += sh->n_lines;
+        } else if (g->ref_ok) {
+            X->unmodelled++;
+        }
+        fi = ++X->ng;
+        if (hm_put(&X->flex_of, f->fec_id, fi)) {
+            X->oom = 1;
+            return;
+        }
+        for (uint32_t i = 0; i < g->count && g->shape != UINT32_MAX; ++i) { /* sim_fec_add_segment_to_flex */
+            const uint32_t c = hm_get(&X->cache, g->base + i);
+            if (!c)
+                continue;
+            if (c & 0x80000000u) {
+                rx_on_segment(X, fi - 1, &X->out[c & 0x7FFFFFFFu].hdr, -1, 0);
+            } else {
+                const rfec_hdr h = rec_hdr(&X->R[c - 1]);
+                rx_on_segment(X, fi - 1, &h, (int32_t)(c - 1), 0);
+            }
+        }
+    }
+    rx_inst* g = &X->G[fi - 1];
+    if (!g->ref_ok || g->shape == UINT32_MAX)
+        return;
+    const int l = X->S[g->shape].line_of[f->index];
+    if (l < 0) {
+        X->unmodelled++; /* a line the sender's plan does not have */
+        return;
+    }
+    if ((g->ppm >> l) & 1ull)
+        return;
+    g->ppm |= 1ull << l;
+    X->line_par[g->line0 + l] = (int32_t)a;
+    rx_check_line(X, fi - 1, l);
+}
+
+/* sim_receiver_recover (sim_receiver.c:780-804): lowest packet_id first, cascading */
+static void rx_drain(rx_sim* X)
+{
+    while (X->npend && !X->oom) {
+        uint32_t b = 0;
+        for (uint32_t i = 1; i < X->npend; ++i)
+            if (X->pend[i].hdr.seq < X->pend[b].hdr.seq)
+                b = i;
+        const rx_event e = X->pend[b];
+        X->pend[b] = X->pend[--X->npend];
+        if (hm_get(&X->seen, e.hdr.seq))
+            continue;
+        RX_GROW(X->out, X->nout, X->outcap, 1, rx_event);
+        if (X->oom || hm_put(&X->seen, e.hdr.seq, 1)) {
+            X->oom = 1;
+            return;
+        }
+        X->out[X->nout] = e;
+        const uint32_t idx = X->nout++;
+        rx_put_segment(X, &e.hdr, (uint16_t)X->G[e.inst].fec_id, 0x80000000u | idx, -1);
+    }
+}
+
+static void rx_sim_free(rx_sim* X)
+{
+    hm_free(&X->seen);
+    hm_free(&X->cache);
+    hm_free(&X->flex_of);
+    hm_free(&X->shape_of);
+    free(X->G);
+    free(X->S);
+    free(X->slot_src);
+    free(X->slot_hdr);
+    free(X->line_par);
+    free(X->pend);
+    free(X->out);
+}
+
+static int cmp_event(const void* a, const void* b)
+{
+    const uint32_t x = ((const rx_event*)a)->hdr.seq, y = ((const rx_event*)b)->hdr.seq;
+    return x < y ? -1 : x > y;
+}
+
+typedef struct {
+    uint8_t* h;
+    size_t hb;
+    uint8_t* d;
+    size_t db;
+} rx_ctx;
+static __thread rx_ctx t_rx;
+
+static int rx_reserve(size_t host_bytes, size_t dev_bytes)
+{
+    hipError_t e;
+    if (t_rx.hb < host_bytes) {
+        if (t_rx.h)
+            (void)hipHostFree(t_rx.h);
+        t_rx.h = NULL;
+        t_rx.hb = 0;
+        host_bytes += host_bytes / 4;
+        if ((e = hipHostMalloc((void**)&t_rx.h, host_bytes, hipHostMallocDefault)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "rx staging (host)", e);
+        t_rx.hb = host_bytes;
+    }
+    if (t_rx.db < dev_bytes) {
+        if (t_rx.d)
+            (void)hipFree(t_rx.d);
+        t_rx.d = NULL;
+        t_rx.db = 0;
+        dev_bytes += dev_bytes / 4;
+        if ((e = hipMalloc((void**)&t_rx.d, dev_bytes)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "rx workspace (device)", e);
+        t_rx.db = dev_bytes;
+    }
+    return RFEC_OK;
+}
+
+#define RX_ALIGN(x) (((x) + 255) & ~(size_t)255)
+
+int rfec_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payload, uint32_t stride,
+                    uint32_t capacity, uint32_t* max_ts, rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out,
+                    uint32_t* n_out, rfec_rx_report* rep, void* stream)
+{
+    const double t0 = now_us();
+    if (!max_ts || !n_out || !rep || (n && (!recs || !payload)) || (max_out && (!out || !out_payload)))
+        return set_err(RFEC_EINVAL, "rx: bad argument", 0);
+    if (stride == 0 || stride % 16 || capacity > stride)
+        return set_err(RFEC_EINVAL, "rx: stride must be a multiple of 16 and >= capacity", 0);
+    memset(rep, 0, sizeof(*rep));
+    *n_out = 0;
+    if (n == 0)
+        return RFEC_OK;
+    hipStream_t sm = (hipStream_t)stream;
+    hipError_t e;
+    int rc = RFEC_OK, ke = 0;
+    /* 1. the records to the host (headers only: 64 B each) */
+    const size_t rec_bytes = RX_ALIGN((size_t)n * sizeof(rfec_wire_rec));
+    if ((rc = rx_reserve(rec_bytes, 0)))
+        return rc;
+    double tt = now_us();
+    if ((e = hipMemcpyAsync(t_rx.h, recs, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost, sm)) !=
+            hipSuccess ||
+        (e = hipStreamSynchronize(sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx: records D2H", e);
+    rep->d2h_us += now_us() - tt;
+    /* 2. the control plane, in arrival order */
+    const double th = now_us();
+    rx_sim X;
+    memset(&X, 0, sizeof(X));
+    X.R = (const rfec_wire_rec*)t_rx.h;
+    X.capacity = capacity;
+    X.max_ts = *max_ts;
+    if (hm_init(&X.seen, n) || hm_init(&X.cache, n) || hm_init(&X.flex_of, 1024) || hm_init(&X.shape_of, 64)) {
+        rx_sim_free(&X);
+        return set_err(RFEC_ENOMEM, "rx: host tables", 0);
+    }
+    for (uint32_t a = 0; a < n && !X.oom; ++a) {
+        const rfec_wire_rec* r = &X.R[a];
+        if (r->status != RFEC_WIRE_OK)
+            continue;
+        if (r->mid == RFEC_WIRE_SEG) { /* sim_receiver_put (sim_receiver.c:811-827) */
+            if (hm_get(&X.seen, r->hdr.seq))
+                continue;
+            if (hm_put(&X.seen, r->hdr.seq, 1)) {
+                X.oom = 1;
+                break;
+            }
+            if (r->fec_id == 0)
+                continue;
+            const rfec_hdr h = rec_hdr(r);
+            rx_put_segment(&X, &h, r->fec_id, a + 1, (int32_t)a);
+        } else if (r->mid == RFEC_WIRE_FEC) {
+            rx_put_fec(&X, a);
+        }
+        rx_drain(&X);
+    }
+    if (X.oom) {
+        rx_sim_free(&X);
+        return set_err(RFEC_ENOMEM, "rx: host tables", 0);
+    }
+    qsort(X.out, X.nout, sizeof(rx_event), cmp_event);
+    *max_ts = X.max_ts;
+    rep->n_fec_dropped = X.dropped;
+    if (X.nout == 0) { /* nothing recovered: no device work */
+        rep->host_us = now_us() - th;
+        goto out;
+    }
+    /* 3. group tables, shape-major, for the groups that deliver something */
+    for (uint32_t s = 0; s < X.ns; ++s)
+        X.S[s].n_groups = 0;
+    for (uint32_t gi = 0; gi < X.ng; ++gi)
+        X.G[gi].gslot = UINT32_MAX;
+    for (uint32_t q = 0; q < X.nout; ++q) {
+        rx_inst* g = &X.G[X.out[q].inst];
+        if (g->gslot == UINT32_MAX)
+            g->gslot = X.S[g->shape].n_groups++;
+    }
+    uint32_t rows = 0, prows = 0, ngs = 0;
+    for (uint32_t s = 0; s < X.ns; ++s) {
+        rx_shape* sh = &X.S[s];
+        sh->row0 = rows;
+        sh->prow0 = prows;
+        sh->group0 = ngs;
+        rows += sh->n_groups * sh->count;
+        prows += sh->n_groups * sh->n_lines;
+        ngs += sh->n_groups;
+    }
+    const size_t o_smap = 0, o_pmap = RX_ALIGN((size_t)rows * 4), o_hdr = RX_ALIGN(o_pmap + (size_t)prows * 4);
+    const size_t o_meta = RX_ALIGN(o_hdr + (size_t)rows * sizeof(rfec_hdr));
+    const size_t o_fs = RX_ALIGN(o_meta + (size_t)prows * sizeof(rfec_hdr));
+    const size_t o_pres = RX_ALIGN(o_fs + (size_t)prows * 2), o_pp = RX_ALIGN(o_pres + (size_t)ngs * 16);
+    const size_t o_omap = RX_ALIGN(o_pp + (size_t)ngs * 8), o_in_end = RX_ALIGN(o_omap + (size_t)X.nout * 4);
+    const size_t o_rec = o_in_end, host_bytes = RX_ALIGN(o_rec + (size_t)ngs * 16);
+    size_t ws_bytes = 0;
+    for (uint32_t s = 0; s < X.ns; ++s)
+        ws_bytes += RX_ALIGN(rfec_recover_workspace_size(&X.S[s].plan, X.S[s].n_groups));
+    const size_t d_shards = o_in_end, d_par = RX_ALIGN(d_shards + (size_t)rows * stride);
+    const size_t d_ws = RX_ALIGN(d_par + (size_t)prows * stride), d_rec = RX_ALIGN(d_ws + ws_bytes);
+    const size_t d_out = RX_ALIGN(d_rec + (size_t)ngs * 16), dev_bytes = RX_ALIGN(d_out + (size_t)X.nout * stride);
+    /* the records stay at the start of the pinned block: the tables follow them */
+    uint8_t* old = t_rx.h;
+    if ((rc = rx_reserve(rec_bytes + host_bytes, dev_bytes)))
+        goto out;
+    if (t_rx.h != old) { /* grown: the records were not kept */
+        if ((e = hipMemcpyAsync(t_rx.h, recs, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost, sm)) !=
+                hipSuccess ||
+            (e = hipStreamSynchronize(sm)) != hipSuccess) {
+            rc = set_err(RFEC_EDEVICE, "rx: records D2H", e);
+            goto out;
+        }
+        X.R = (const rfec_wire_rec*)t_rx.h;
+    }
+    uint8_t* H = t_rx.h + rec_bytes;
+    memset(H, 0, o_in_end);
+    int32_t* smap = (int32_t*)(H + o_smap);
+    int32_t* pmap = (int32_t*)(H + o_pmap);
+    rfec_hdr* hh = (rfec_hdr*)(H + o_hdr);
+    rfec_hdr* mh = (rfec_hdr*)(H + o_meta);
+    uint16_t* fsz = (uint16_t*)(H + o_fs);
+    uint64_t* pres = (uint64_t*)(H + o_pres);
+    uint64_t* ppm = (uint64_t*)(H + o_pp);
+    int32_t* omap = (int32_t*)(H + o_omap);
+    for (uint32_t gi = 0; gi < X.ng; ++gi) {
+        const rx_inst* g = &X.G[gi];
+        if (g->shape == UINT32_MAX || g->gslot == UINT32_MAX)
+            continue;
+        const rx_shape* sh = &X.S[g->shape];
+        const uint32_t gg = sh->group0 + g->gslot, r0 = sh->row0 + g->gslot * sh->count;
+        const uint32_t p0 = sh->prow0 + g->gslot * sh->n_lines;
+        pres[2 * gg] = g->arrived[0];
+        pres[2 * gg + 1] = g->arrived[1];
+        ppm[gg] = g->ppm;
+        for (uint32_t i = 0; i < sh->count; ++i) {
+            const int32_t src = X.slot_src[g->slot0 + i];
+            smap[r0 + i] = src;
+            if (src >= 0)
+                hh[r0 + i] = X.slot_hdr[g->slot0 + i];
+        }
+        for (uint32_t l = 0; l < sh->n_lines; ++l) {
+            const int32_t src = X.line_par[g->line0 + l];
+            pmap[p0 + l] = src;
+            if (src >= 0) {
+                mh[p0 + l] = X.R[src].hdr;
+                fsz[p0 + l] = X.R[src].data_size;
+            }
+        }
+    }
+    /* output rows: the recovering group's slot */
+    uint32_t nok = 0;
+    for (uint32_t q = 0; q < X.nout; ++q) {
+        const rx_event* ev = &X.out[q];
+        const rx_inst* g = &X.G[ev->inst];
+        const rx_shape* sh = &X.S[g->shape];
+        const uint32_t t = ev->hdr.seq - g->base;
+        omap[q] = t < g->count ? (int32_t)(sh->row0 + g->gslot * sh->count + t) : -1;
+    }
+    rep->host_us = now_us() - th;
+    rep->n_groups = ngs;
+    for (uint32_t s = 0; s < X.ns; ++s)
+        rep->n_shapes += X.S[s].n_groups != 0;
+    /* 4. the device: rows in place, one peel per shape, the delivered rows compacted */
+    {
+        uint8_t* D = t_rx.d;
+        tt = now_us();
+        if ((e = hipMemcpyAsync(D, H, o_in_end, hipMemcpyHostToDevice, sm)) != hipSuccess) {
+            rc = set_err(RFEC_EDEVICE, "rx: H2D", e);
+            goto out;
+        }
+        ke = rfec_launch_gather_rows(D + d_shards, payload, (const int32_t*)(D + o_smap), rows, stride, sm);
+        if (!ke)
+            ke = rfec_launch_gather_rows(D + d_par, payload, (const int32_t*)(D + o_pmap), prows, stride, sm);
+        size_t wso = 0;
+        for (uint32_t s = 0; s < X.ns && !ke; ++s) {
+            const rx_shape* sh = &X.S[s];
+            if (!sh->n_groups)
+                continue;
+            rfec_kmask M;
+            make_masks(&sh->plan, &M);
+            ke = rfec_launch_recover(&M, sh->n_groups, stride, capacity, D + d_shards + (size_t)sh->row0 * stride,
+                                     (rfec_hdr*)(D + o_hdr) + sh->row0, (const uint64_t*)(D + o_pres) + 2 * sh->group0,
+                                     D + d_par + (size_t)sh->prow0 * stride, (const rfec_hdr*)(D + o_meta) + sh->prow0,
+                                     (const uint16_t*)(D + o_fs) + sh->prow0,
+                                     (const uint64_t*)(D + o_pp) + sh->group0,
+                                     (uint64_t*)(D + d_rec) + 2 * sh->group0, D + d_ws + wso, sm, g_tuning);
+            wso += RX_ALIGN(rfec_recover_workspace_size(&sh->plan, sh->n_groups));
+        }
+        if (!ke && X.nout)
+            ke = rfec_launch_gather_rows(D + d_out, D + d_shards, (const int32_t*)(D + o_omap), X.nout, stride, sm);
+        uint64_t* rec = (uint64_t*)(H + o_rec);
+        if (ke || (e = hipMemcpyAsync(rec, D + d_rec, (size_t)ngs * 16, hipMemcpyDeviceToHost, sm)) != hipSuccess ||
+            (e = hipStreamSynchronize(sm)) != hipSuccess) {
+            rc = set_err(RFEC_EDEVICE, "rx: recover", ke ? ke : e);
+            goto out;
+        }
+        rep->kernel_us = now_us() - tt;
+        /* the device peel covers every packet the arrival-order pass delivered (same lines, a superset of
+           the members at each firing); anything else is reported, not delivered */
+        *n_out = 0;
+        for (uint32_t q = 0; q < X.nout; ++q) {
+            const rx_event* ev = &X.out[q];
+            const rx_inst* g = &X.G[ev->inst];
+            const uint32_t t = ev->hdr.seq - g->base, gg = X.S[g->shape].group0 + g->gslot;
+            if (t >= g->count || !((rec[2 * gg + (t >> 6)] >> (t & 63)) & 1ull)) {
+                X.unmodelled++;
+                omap[q] = -1;
+                continue;
+            }
+            nok++;
+        }
+        if (nok > max_out) {
+            *n_out = nok;
+            rc = set_err(RFEC_EINVAL, "rx: output too small", 0);
+            goto out;
+        }
+        tt = now_us();
+        uint32_t o = 0;
+        if (nok == X.nout) { /* the usual case: one copy */
+            if (nok)
+                e = hipMemcpyAsync(out_payload, D + d_out, (size_t)nok * stride, hipMemcpyDeviceToHost, sm);
+            o = nok;
+        }
+        for (uint32_t q = 0; q < X.nout && nok != X.nout && e == hipSuccess; ++q) {
+            if (omap[q] < 0)
+                continue;
+            e = hipMemcpyAsync(out_payload + (size_t)o * stride, D + d_out + (size_t)q * stride, stride,
+                               hipMemcpyDeviceToHost, sm);
+            X.out[o++] = X.out[q];
+        }
+        for (uint32_t q = 0; q < o; ++q) {
+            out[q].hdr = X.out[q].hdr;
+            out[q].fec_id = (uint16_t)X.G[X.out[q].inst].fec_id;
+            out[q].reserved = 0;
+        }
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(sm);
+        if (e != hipSuccess) {
+            rc = set_err(RFEC_EDEVICE, "rx: output D2H", e);
+            goto out;
+        }
+        rep->d2h_us += now_us() - tt;
+        *n_out = o;
+        rep->n_recovered = o;
+    }
+out:
+    rep->n_unmodelled = X.unmodelled;
+    rx_sim_free(&X);
+    rep->total_us = now_us() - t0;
+    return rc;
+}

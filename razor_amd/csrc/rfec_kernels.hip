@@ -750,6 +750,23 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
     }
 }
 
+// dst row r <- src row map[r] (all `C` 16-B chunks), or zeros for map[r] < 0:
+// the receiver's scatter of parsed payloads into group slots and its gather
+// of recovered segments.  One lane per chunk, streaming.
+__global__ __launch_bounds__(kBlock) void k_gather_rows(v4u* __restrict__ dst, const v4u* __restrict__ src,
+                                                        const int32_t* __restrict__ map, uint32_t total, uint32_t C,
+                                                        FastDiv divC)
+{
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= total)
+        return;
+    const uint32_t r = fdiv(t, divC);
+    const uint32_t j = t - r * C;
+    const int32_t s = map[r];
+    const v4u v = s >= 0 ? __builtin_nontemporal_load(src + (size_t)s * C + j) : v4u{0, 0, 0, 0};
+    __builtin_nontemporal_store(v, dst + (size_t)r * C + j);
+}
+
 // Zero bytes [data_size, stride) of every slot.
 __global__ __launch_bounds__(kBlock) void k_zero_tails(v4u* shards, const rfec_hdr* __restrict__ hdr,
                                                        uint32_t total, uint32_t C, FastDiv divC)
@@ -1062,6 +1079,18 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
         launch_replay<4, 2, false>(R, ntl, nts, P, grid);
     else
         launch_replay<8, 1, false>(R, ntl, nts, P, grid);
+    return (int)hipGetLastError();
+}
+
+int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map, uint32_t rows, uint32_t stride,
+                            void* stream)
+{
+    const uint32_t C = stride / 16;
+    const uint32_t total = rows * C;
+    if (!total)
+        return 0;
+    hipLaunchKernelGGL(k_gather_rows, dim3(blocks_for(total)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
+                       reinterpret_cast<v4u*>(dst), reinterpret_cast<const v4u*>(src), map, total, C, make_fastdiv(C));
     return (int)hipGetLastError();
 }
 

@@ -123,9 +123,13 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
     return v;
 }
 
+// v of lane `src` (0 when src < 0).  The permute runs with every lane active
+// (a lane masked off would not supply its value to the lanes reading it);
+// only the result is selected.
 __device__ __forceinline__ uint32_t from_lane(uint32_t v, int src)
 {
-    return src >= 0 ? (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v) : 0u;
+    const uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((src < 0 ? 0 : src) << 2, (int)v);
+    return src >= 0 ? r : 0u;
 }
 
 // crc32(seed, msg[0:n)) (cf_crc32.c:56-68) of a message held lane-wise:

@@ -75,6 +75,15 @@ SEG_PLAN_DTYPE = np.dtype([("frame", "<u4"), ("offset", "<u4"), ("packet_id", "<
 GROUP_PLAN_DTYPE = np.dtype([("first_seg", "<i4"), ("count", "<u2"), ("fec_id", "<u2"), ("base_id", "<u4"),
                              ("fec_send_id0", "<u4"), ("fec_ts", "<u4"), ("protect_fraction", "u1"),
                              ("n_lines", "u1"), ("reserved", "u1", (2,))])
+RX_SEG_DTYPE = np.dtype([("hdr", HDR_DTYPE), ("fec_id", "<u2"), ("reserved", "<u2")])
+assert RX_SEG_DTYPE.itemsize == 24
+
+
+class rfec_rx_report(C.Structure):
+    _fields_ = [("n_groups", C.c_uint32), ("n_shapes", C.c_uint32), ("n_recovered", C.c_uint32),
+                ("n_fec_dropped", C.c_uint32), ("n_unmodelled", C.c_uint32), ("reserved", C.c_uint32),
+                ("host_us", C.c_double), ("h2d_us", C.c_double), ("kernel_us", C.c_double),
+                ("d2h_us", C.c_double), ("total_us", C.c_double)]
 
 
 class rfec_send_report(C.Structure):
@@ -181,6 +190,8 @@ _SIGS = {
     "rfec_sender_plan": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, C.c_uint32, _P, _P, C.c_uint32, _P]),
     "rfec_host_send_frames": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, C.c_uint32, _P, C.c_uint32,
                                         C.c_uint32, _P, _P, _P, _P, C.c_uint32, C.POINTER(rfec_send_report)]),
+    "rfec_rx_recover": (C.c_int, [C.c_uint32, _P, _P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), _P, _P,
+                                  C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(rfec_rx_report), _P]),
     "rfec_set_tuning": (None, [C.c_uint]),
     "rfec_get_tuning": (C.c_uint, []),
     "rfec_last_error": (C.c_char_p, []),
@@ -319,6 +330,18 @@ class Native:
                     "rfec_host_send_frames")
         ns, ng, npar = rep.n_segs, rep.n_groups, rep.n_parities
         return segs[:ns], groups[:ng], sdg[:ns], sdl[:ns], fdg[:npar], fdl[:npar], rep
+
+    # -- receiver ingestion ---------------------------------------------------------
+    def rx_recover(self, n, recs, payload, stride, capacity, max_ts=0, max_out=1 << 16, stream=None):
+        """recs / payload: device pointers (rfec_wire_parse output, arrival order).
+        Returns (segments, payload rows, max_ts, report), segments ascending packet_id."""
+        out = np.zeros(max_out, RX_SEG_DTYPE)
+        outp = np.zeros((max_out, stride), np.uint8)
+        mts, nout, rep = C.c_uint32(max_ts), C.c_uint32(), rfec_rx_report()
+        self._check(self.lib.rfec_rx_recover(n, recs, payload, stride, capacity, C.byref(mts), out.ctypes.data,
+                                             outp.ctypes.data, max_out, C.byref(nout), C.byref(rep), stream),
+                    "rfec_rx_recover")
+        return out[:nout.value], outp[:nout.value], mts.value, rep
 
     def set_tuning(self, flags: int):
         self.lib.rfec_set_tuning(flags)

@@ -1,0 +1,181 @@
+"""Receiver ingestion on the GPU (rfec_rx_recover): parsed datagrams in
+arrival order -> the segments the reference receiver recovers.
+
+  * the reference's own receiver on scripted lossy / reordered / duplicated
+    streams (tests/golden/rx.json, oracle/gen_rx.c over sim_fec.c);
+  * the event-by-event oracle (oracle_rx_recover, pinned by the same
+    fixtures) on larger streams the product sender emits, parsed by the
+    device wire codec, with loss, reordering, duplicates and parities late
+    enough for the 3000 ms rule;
+  * edge cases: empty batch, undecodable records only, output too small.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+import pyoracle as po
+import rx_cases as rc
+
+pytestmark = pytest.mark.gpu
+
+UID = 0x0BADF00D
+DSTRIDE = 1056
+STRIDE = 1008
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the -m gpu suite must run on an MI355X")
+    from razor_amd.fec import native
+    return native(1000)
+
+
+def _dev(a: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).cuda()
+
+
+def _rx(lib, recs, pay, max_ts=0, max_out=1 << 16):
+    dr, dp = _dev(recs), _dev(pay)
+    torch.cuda.synchronize()
+    return lib.rx_recover(len(recs), dr.data_ptr(), dp.data_ptr(), pay.shape[1], 1000, max_ts, max_out)
+
+
+def _sorted(rows):
+    return sorted(rows, key=lambda r: r[0])
+
+
+@pytest.mark.parametrize("name", ["k10_loss10", "k10_loss25_dup", "mixed_loss15", "late_parities"])
+def test_rx_reference_fixture(lib, oracle1000, name):
+    scn = {s["name"]: s for s in po.rx_fixture()["scenarios"]}[name]
+    recs, pay, _, _ = po.rx_stream(oracle1000, scn)
+    out, outp, max_ts, rep = _rx(lib, recs, pay)
+    assert _sorted(rc.got_rows(out, outp)) == _sorted(rc.expected(scn))
+    assert [int(s) for s in out["hdr"]["seq"]] == sorted(int(s) for s in out["hdr"]["seq"])
+    assert max_ts == scn["max_ts"]
+    _, _, _, dropped = oracle1000.rx_recover(recs, pay, 1000)
+    assert rep.n_fec_dropped == dropped and rep.n_unmodelled == 0
+    assert rep.n_recovered == len(scn["recovered"])
+
+
+def _sender_stream(lib, frames_n, seed, k_choices=(10,), pf=(80,)):
+    """Datagrams of the product sender in send order: each segment, and a
+    group's parities right after the segment that closes it."""
+    rng = np.random.default_rng(seed)
+    sizes = rng.choice(k_choices, frames_n) * 1000 - rng.integers(0, 900, frames_n)
+    blob = rng.integers(0, 256, int(sizes.sum()), dtype=np.uint8)
+    frames = np.zeros(frames_n, po.FRAME)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    frames["data"] = blob.ctypes.data + offs.astype(np.uint64)
+    frames["size"] = sizes
+    frames["payload_type"] = 96
+    frames["ftype"] = np.arange(frames_n) % 50 == 0
+    frames["protect_fraction"] = rng.choice(pf, frames_n)
+    frames["now_ms"] = 1_700_000_000_000 + np.arange(frames_n) * 33
+    st = lib.sender_init()
+    segs, groups, sdg, sdl, fdg, fdl, rep = lib.send_frames(st, frames, UID, DSTRIDE, max_segs=frames_n * 12 + 64,
+                                                            max_groups=frames_n + 64, max_parities=frames_n * 16 + 64)
+    closes = {}
+    p = 0
+    for g in groups:
+        nl = int(g["n_lines"])
+        if int(g["first_seg"]) >= 0:
+            closes[int(g["first_seg"]) + int(g["count"]) - 1] = (p, nl)
+        p += nl
+    order = []
+    for i in range(len(segs)):
+        order.append((0, i))
+        if i in closes:
+            p0, nl = closes[i]
+            order.extend((1, p0 + l) for l in range(nl))
+    return order, (sdg, sdl, fdg, fdl), blob
+
+
+def _network(order, rng, loss=0.12, window=40, dup=0.04, late=0.0, late_by=4000):
+    keys = []
+    for pos, item in enumerate(order):
+        if rng.random() < loss:
+            continue
+        key = pos + rng.integers(0, window)
+        if item[0] == 1 and rng.random() < late:
+            key += late_by
+        keys.append((key, pos, item))
+        if rng.random() < dup:
+            keys.append((key + rng.integers(1, 3 * window), pos, item))
+    keys.sort(key=lambda t: (t[0], t[1]))
+    return [t[2] for t in keys]
+
+
+def _arrivals(lib, arrivals, dg):
+    sdg, sdl, fdg, fdl = dg
+    n = len(arrivals)
+    dgram = np.zeros((n, DSTRIDE), np.uint8)
+    dlen = np.zeros(n, np.uint16)
+    for a, (kind, i) in enumerate(arrivals):
+        src, ln = (sdg, sdl) if kind == 0 else (fdg, fdl)
+        dgram[a], dlen[a] = src[i], ln[i]
+    from razor_amd.fec import WIRE_REC_DTYPE
+    d_dg, d_dl = _dev(dgram), _dev(dlen)
+    recs = torch.zeros(n * WIRE_REC_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    pay = torch.zeros(n * STRIDE, dtype=torch.uint8, device="cuda")
+    lib.wire_parse(n, DSTRIDE, d_dg.data_ptr(), d_dl.data_ptr(), STRIDE, 1000, recs.data_ptr(), pay.data_ptr())
+    torch.cuda.synchronize()
+    return recs, pay
+
+
+@pytest.mark.parametrize("case", ["k10", "mixed", "late", "heavy"])
+def test_rx_sender_stream_vs_oracle(lib, oracle1000, case):
+    cfg = {"k10": dict(frames=3000, k=(10,), pf=(80,), net=dict()),
+           "mixed": dict(frames=2000, k=(1, 3, 10, 24), pf=(20, 50, 80, 100), net=dict(loss=0.15, window=80)),
+           "late": dict(frames=1500, k=(10,), pf=(80,), net=dict(loss=0.1, late=0.25, late_by=1600)),
+           "heavy": dict(frames=800, k=(6, 10), pf=(100,), net=dict(loss=0.35, window=200, dup=0.2))}[case]
+    rng = np.random.default_rng({"k10": 1, "mixed": 2, "late": 3, "heavy": 4}[case])
+    order, dg, _ = _sender_stream(lib, cfg["frames"], 7, cfg["k"], cfg["pf"])
+    arrivals = _network(order, rng, **cfg["net"])
+    recs, pay = _arrivals(lib, arrivals, dg)
+    from razor_amd.fec import WIRE_REC_DTYPE
+    h_recs = recs.cpu().numpy().view(WIRE_REC_DTYPE)
+    h_pay = pay.cpu().numpy().reshape(-1, STRIDE)
+    assert (h_recs["status"] == 0).all()
+    eo, eop, emts, edrop = oracle1000.rx_recover(h_recs, h_pay, 1000, max_out=1 << 17)
+    out, outp, mts, rep = lib.rx_recover(len(h_recs), recs.data_ptr(), pay.data_ptr(), STRIDE, 1000, 0, 1 << 17)
+    idx = np.argsort(eo["hdr"]["seq"], kind="stable")
+    assert len(out) == len(eo) and len(out) > 0
+    assert np.array_equal(out["hdr"], eo["hdr"][idx]) and np.array_equal(out["fec_id"], eo["fec_id"][idx])
+    assert np.array_equal(outp, eop[idx])
+    assert mts == emts and rep.n_fec_dropped == edrop and rep.n_unmodelled == 0
+    if case == "late":
+        assert edrop > 0
+
+
+def test_rx_continues_across_calls(lib, oracle1000):
+    """max_ts carries across batches (sim_receiver_fec_t.max_ts)."""
+    order, dg, _ = _sender_stream(lib, 400, 3)
+    arrivals = _network(order, np.random.default_rng(5), loss=0.1, window=10, dup=0.0)
+    recs, pay = _arrivals(lib, arrivals, dg)
+    _, _, m1, _ = lib.rx_recover(len(arrivals), recs.data_ptr(), pay.data_ptr(), STRIDE, 1000, 0, 1 << 15)
+    assert m1 > 0
+    _, _, m2, rep = lib.rx_recover(len(arrivals), recs.data_ptr(), pay.data_ptr(), STRIDE, 1000, m1 + 10_000,
+                                   1 << 15)
+    assert m2 == m1 + 10_000 and rep.n_fec_dropped > 0  # every parity is now > 3 s old
+
+
+def test_rx_edges(lib):
+    from razor_amd.fec import RfecError, WIRE_REC_DTYPE
+    out, outp, mts, rep = lib.rx_recover(0, 0, 0, STRIDE, 1000, 77, 4)
+    assert len(out) == 0 and mts == 77
+    bad = np.zeros(8, WIRE_REC_DTYPE)
+    bad["status"] = -1
+    out, _, mts, rep = _rx(lib, bad, np.zeros((8, STRIDE), np.uint8), 5)
+    assert len(out) == 0 and mts == 5 and rep.n_groups == 0
+    order, dg, _ = _sender_stream(lib, 200, 11)
+    arrivals = _network(order, np.random.default_rng(2), loss=0.2, window=4, dup=0.0)
+    recs, pay = _arrivals(lib, arrivals, dg)
+    out, _, _, _ = lib.rx_recover(len(arrivals), recs.data_ptr(), pay.data_ptr(), STRIDE, 1000, 0, 1 << 14)
+    assert len(out) > 1
+    with pytest.raises(RfecError):
+        lib.rx_recover(len(arrivals), recs.data_ptr(), pay.data_ptr(), STRIDE, 1000, 0, len(out) - 1)
+    with pytest.raises(RfecError):
+        lib.rx_recover(len(arrivals), recs.data_ptr(), pay.data_ptr(), 1000, 1000, 0, 16)  # stride % 16
