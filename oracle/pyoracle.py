@@ -425,15 +425,11 @@ def rx_fixture() -> dict:
     return json.loads((GOLDEN / "rx.json").read_text())
 
 
-def rx_stream(oracle, scn, video_size=1000):
-    """Parsed-datagram records (WIRE_REC) + payload rows, in the arrival order
-    of an rx.json scenario: segments from the sender plan (pinned by
-    stage.json), parities from the oracle encode (pinned by the enc_* fixtures)."""
-    frames, blob = stage_frames(scn)
-    st = oracle.sender_init()
-    segs, groups = oracle.sender_plan(st, frames, video_size)
-    assert [(int(g["fec_id"]), int(g["base_id"]), int(g["count"]), int(g["protect_fraction"])) for g in groups] == \
-        [tuple(g) for g in scn["groups"]]
+def rx_items(oracle, frames, blob, segs, groups, video_size=1000):
+    """Parsed-datagram records (WIRE_REC) + payload rows of everything a sender
+    plan emits: (seg_rec, seg_pay, par_rec, par_pay, par_group).  Segment
+    headers from the plan (pinned by stage.json), timestamps 33 ms per frame as
+    gen_rx.c, parities from the oracle encode (pinned by the enc_* fixtures)."""
     stride = (video_size + 15) // 16 * 16
     ns = len(segs)
     seg_pay = np.zeros((ns, stride), np.uint8)
@@ -451,9 +447,11 @@ def rx_stream(oracle, scn, video_size=1000):
     seg_rec["fec_id"] = segs["fec_id"]
     seg_rec["data_size"] = segs["data_size"]
     seg_rec["remb"] = 0xFF
-    par_rec, par_pay = [], []
-    for g in groups:
+    par_rec, par_pay, par_group = [], [], []
+    for gi, g in enumerate(groups):
         k, pf = int(g["count"]), int(g["protect_fraction"])
+        if int(g["first_seg"]) < 0 or k == 0:
+            continue
         plan = oracle.plan_from_fraction(k, pf, 3)
         mem = segs[int(g["first_seg"]):int(g["first_seg"]) + k]
         hdr = np.zeros((1, k), HDR_DTYPE)
@@ -471,8 +469,12 @@ def rx_stream(oracle, scn, video_size=1000):
             r["data_size"] = fs[0, l]
             par_rec.append(r)
             par_pay.append(par[0, l])
-    assert [(int(par_rec[p]["index"])) for p in range(len(par_rec))] == [q[1] for q in scn["parities"]]
-    arr = np.array(scn["arrivals"], np.int64).reshape(-1, 2)
+            par_group.append(gi)
+    return seg_rec, seg_pay, par_rec, par_pay, par_group
+
+
+def _gather_arrivals(arr, items, stride):
+    seg_rec, seg_pay, par_rec, par_pay, _ = items
     recs = np.zeros(len(arr), WIRE_REC)
     pay = np.zeros((len(arr), stride), np.uint8)
     for a, (kind, idx) in enumerate(arr):
@@ -480,7 +482,51 @@ def rx_stream(oracle, scn, video_size=1000):
             recs[a], pay[a] = seg_rec[idx], seg_pay[idx]
         else:
             recs[a], pay[a] = par_rec[idx], par_pay[idx]
-    return recs, pay, segs, seg_pay
+    return recs, pay
+
+
+def rx_stream(oracle, scn, video_size=1000):
+    """Parsed-datagram records (WIRE_REC) + payload rows, in the arrival order
+    of an rx.json scenario."""
+    frames, blob = stage_frames(scn)
+    st = oracle.sender_init()
+    segs, groups = oracle.sender_plan(st, frames, video_size)
+    assert [(int(g["fec_id"]), int(g["base_id"]), int(g["count"]), int(g["protect_fraction"])) for g in groups] == \
+        [tuple(g) for g in scn["groups"]]
+    items = rx_items(oracle, frames, blob, segs, groups, video_size)
+    assert [(int(items[2][p]["index"])) for p in range(len(items[2]))] == [q[1] for q in scn["parities"]]
+    arr = np.array(scn["arrivals"], np.int64).reshape(-1, 2)
+    recs, pay = _gather_arrivals(arr, items, (video_size + 15) // 16 * 16)
+    return recs, pay, segs, items[1]
+
+
+def synth_rx_stream(oracle, frames, blob, segs, groups, rng, loss=0.12, window=40, dup=0.04, late=0.0,
+                    late_by=1600, video_size=1000):
+    """A lossy network over a sender plan: send order = each segment, and a
+    group's parities right after the segment that closes it; each datagram is
+    lost with `loss`, delayed by up to `window` positions, duplicated with
+    `dup`, and a parity is held back `late_by` positions with `late`."""
+    items = rx_items(oracle, frames, blob, segs, groups, video_size)
+    closes = {}
+    for p, gi in enumerate(items[4]):
+        g = groups[gi]
+        closes.setdefault(int(g["first_seg"]) + int(g["count"]) - 1, []).append(p)
+    order = []
+    for i in range(len(segs)):
+        order.append((0, i))
+        order.extend((1, p) for p in closes.get(i, []))
+    keys = []
+    for pos, item in enumerate(order):
+        if rng.random() < loss:
+            continue
+        key = pos + int(rng.integers(0, window))
+        if item[0] == 1 and rng.random() < late:
+            key += late_by
+        keys.append((key, pos, item))
+        if rng.random() < dup:
+            keys.append((key + int(rng.integers(1, 3 * window)), pos, item))
+    keys.sort(key=lambda t: (t[0], t[1]))
+    return _gather_arrivals([t[2] for t in keys], items, (video_size + 15) // 16 * 16)
 
 
 def _xs_next(st: C.c_uint64) -> int:

@@ -1482,7 +1482,7 @@ typedef struct {
     uint32_t ns, scap;
     int32_t* slot_src; /* record of an arrived member, -1 otherwise */
     rfec_hdr* slot_hdr;
-    uint32_t nslot, slotcap;
+    uint32_t nslot, slotcap, slothcap; /* one count, two capacities (each array grows on its own) */
     int32_t* line_par; /* record of the registered parity, -1 otherwise */
     uint32_t nline, linecap;
     rx_event* pend;
@@ -1684,7 +1684,7 @@ static void rx_put_fec(rx_sim* X, uint32_t a)
             rx_shape* sh = &X->S[g->shape];
             g->gslot = sh->n_groups++;
             RX_GROW(X->slot_src, X->nslot, X->slotcap, g->count, int32_t);
-            RX_GROW(X->slot_hdr, X->nslot, X->slotcap, g->count, rfec_hdr);
+            RX_GROW(X->slot_hdr, X->nslot, X->slothcap, g->count, rfec_hdr);
             RX_GROW(X->line_par, X->nline, X->linecap, sh->n_lines, int32_t);
             if (X->oom)
                 return;
@@ -1872,7 +1872,8 @@ int rfec_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payloa
         rx_sim_free(&X);
         return set_err(RFEC_ENOMEM, "rx: host tables", 0);
     }
-    qsort(X.out, X.nout, sizeof(rx_event), cmp_event);
+    if (X.nout)
+        qsort(X.out, X.nout, sizeof(rx_event), cmp_event);
     *max_ts = X.max_ts;
     rep->n_fec_dropped = X.dropped;
     if (X.nout == 0) { /* nothing recovered: no device work */

@@ -1,0 +1,181 @@
+/*
+ * stub_hip.c -- TEST INFRASTRUCTURE ONLY, never linked into librazor_fec.so.
+ *
+ * A host-memory stand-in for the handful of HIP runtime calls and kernel
+ * launches rfec_host.c makes, so the host control plane (receiver ingestion,
+ * sender staging, argument checks) can run on a machine without a GPU under
+ * AddressSanitizer / UBSan.  "Device" pointers are host pointers; copies are
+ * memcpy; streams and events are no-ops.
+ *
+ * The launches do no FEC arithmetic: payload-producing kernels leave their
+ * outputs untouched.  Only data movement the host code depends on for its
+ * own bookkeeping is mimicked:
+ *   - rfec_launch_gather_rows copies rows by the map (so an out-of-range map
+ *     index is an ASan report, not silent garbage);
+ *   - rfec_launch_recover marks every erased member of every line-covered
+ *     group as recovered (the host then reports what it would deliver).
+ * Results produced through this stub are never compared as FEC outputs; the
+ * tests using it check headers / bookkeeping against the oracle and that the
+ * sanitizers stay quiet.
+ */
+#define _POSIX_C_SOURCE 200809L
+#ifndef __HIP_PLATFORM_AMD__
+#define __HIP_PLATFORM_AMD__ 1
+#endif
+#include <hip/hip_runtime_api.h>
+
+#include <stdlib.h>
+#include <string.h>
+
+#include "rfec_internal.h"
+
+hipError_t hipGetDeviceCount(int* count)
+{
+    *count = 1;
+    return hipSuccess;
+}
+hipError_t hipGetDevice(int* d)
+{
+    *d = 0;
+    return hipSuccess;
+}
+hipError_t hipMalloc(void** p, size_t n)
+{
+    *p = malloc(n ? n : 1);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipFree(void* p)
+{
+    free(p);
+    return hipSuccess;
+}
+hipError_t hipHostMalloc(void** p, size_t n, unsigned int flags)
+{
+    (void)flags;
+    return hipMalloc(p, n);
+}
+hipError_t hipHostFree(void* p) { return hipFree(p); }
+hipError_t hipHostGetDevicePointer(void** d, void* h, unsigned int flags)
+{
+    (void)flags;
+    *d = h;
+    return hipSuccess;
+}
+hipError_t hipMemcpyAsync(void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t s)
+{
+    (void)kind, (void)s;
+    if (n)
+        memmove(dst, src, n);
+    return hipSuccess;
+}
+hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned int flags)
+{
+    (void)flags;
+    *s = (hipStream_t)malloc(1);
+    return hipSuccess;
+}
+hipError_t hipStreamDestroy(hipStream_t s)
+{
+    free(s);
+    return hipSuccess;
+}
+hipError_t hipStreamSynchronize(hipStream_t s)
+{
+    (void)s;
+    return hipSuccess;
+}
+hipError_t hipEventCreate(hipEvent_t* e)
+{
+    *e = (hipEvent_t)malloc(1);
+    return hipSuccess;
+}
+hipError_t hipEventDestroy(hipEvent_t e)
+{
+    free(e);
+    return hipSuccess;
+}
+hipError_t hipEventRecord(hipEvent_t e, hipStream_t s)
+{
+    (void)e, (void)s;
+    return hipSuccess;
+}
+hipError_t hipEventSynchronize(hipEvent_t e)
+{
+    (void)e;
+    return hipSuccess;
+}
+hipError_t hipEventElapsedTime(float* ms, hipEvent_t a, hipEvent_t b)
+{
+    (void)a, (void)b;
+    *ms = 0.f;
+    return hipSuccess;
+}
+
+int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, uint32_t capacity,
+                       const uint8_t* shards, const rfec_hdr* hdr, uint8_t* parity, rfec_hdr* meta,
+                       uint16_t* fsize, int8_t* status, void* stream, unsigned flags)
+{
+    return 0;
+}
+
+int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32_t capacity,
+                        uint8_t* shards, rfec_hdr* hdr, const uint64_t* present, const uint8_t* parity,
+                        const rfec_hdr* meta, const uint16_t* fsize, const uint64_t* parity_present,
+                        uint64_t* recovered, void* ws, void* stream, unsigned flags)
+{
+    uint64_t all0 = 0, all1 = 0;
+    for (uint32_t l = 0; l < M->plan.n_lines; ++l) {
+        all0 |= M->mask[l][0];
+        all1 |= M->mask[l][1];
+    }
+    for (uint32_t g = 0; g < groups; ++g) {
+        recovered[2 * g] = all0 & ~present[2 * g];
+        recovered[2 * g + 1] = all1 & ~present[2 * g + 1];
+    }
+    return 0;
+}
+
+int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
+                               const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,
+                               const rfec_fec_stamp* stamps, const uint32_t* order, uint32_t dstride,
+                               uint8_t* dgram, uint16_t* dlen, void* stream)
+{
+    return 0;
+}
+
+int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* shards,
+                               const rfec_hdr* hdr, const rfec_seg_stamp* stamps, const uint32_t* order,
+                               uint32_t dstride, uint8_t* dgram, uint16_t* dlen, void* stream)
+{
+    return 0;
+}
+
+int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
+                           uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload, void* stream)
+{
+    return 0;
+}
+
+int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map, uint32_t rows, uint32_t stride,
+                            void* stream)
+{
+    for (uint32_t r = 0; r < rows; ++r) {
+        if (map[r] >= 0)
+            memcpy(dst + (size_t)r * stride, src + (size_t)map[r] * stride, stride);
+        else
+            memset(dst + (size_t)r * stride, 0, stride);
+    }
+    return 0;
+}
+
+int rfec_launch_zero_tails(uint32_t slots, uint32_t stride, uint8_t* shards, const rfec_hdr* hdr, void* stream)
+{
+    return 0;
+}
+
+const char* rfec_hip_error_string(int code) { return code ? "stub error" : "no error"; }
+
+/* HBM probes: not available without a device */
+int rfec_probe_read(const void* src, size_t bytes, void* sink, unsigned flags, void* stream) { return 1; }
+int rfec_probe_copy(const void* src, void* dst, size_t bytes, unsigned flags, void* stream) { return 1; }
+int rfec_probe_write(void* dst, size_t bytes, unsigned flags, void* stream) { return 1; }

@@ -1,0 +1,177 @@
+"""Host control plane under AddressSanitizer + UBSan, on the CPU.
+
+rfec_host.c is compiled together with tests/host_stub/stub_hip.c (a
+host-memory stand-in for the HIP runtime and the kernel launches; test
+infrastructure only, it does no FEC arithmetic) and driven through the same
+ctypes view the GPU tests use.  What is checked here is the host side alone:
+
+  * rfec_rx_recover's arrival-order control plane (sim_fec.c:104-241,
+    flex_fec_receiver.c:208-280, sim_receiver.c:780-827) delivers the same
+    packets (headers, fec_id), max_ts and dropped-parity count as the
+    reference receiver / the oracle on the tests/golden/rx.json streams and on
+    synthetic lossy, reordered, duplicated streams;
+  * rfec_host_send_frames plans the same segments and groups as the oracle
+    sender (pinned to the reference flex sender by stage.json);
+  * argument checks and the error paths;
+  * and none of it trips a sanitizer.
+
+The payload bytes are not checked here (the stub computes none); the GPU
+suite (test_receiver.py, test_sender.py) checks them bit-exact.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+
+
+def _libasan():
+    r = subprocess.run(["gcc", "-print-file-name=libasan.so"], capture_output=True, text=True)
+    p = r.stdout.strip()
+    return p if r.returncode == 0 and os.path.isabs(p) and os.path.exists(p) else None
+
+
+@pytest.fixture(scope="module")
+def stub_lib(tmp_path_factory):
+    if _libasan() is None:
+        pytest.skip("libasan not available")
+    if not (ROCM / "include" / "hip" / "hip_runtime_api.h").exists():
+        pytest.skip("HIP headers not available")
+    out = tmp_path_factory.mktemp("hoststub") / "librazor_fec_hoststub.so"
+    inc = [f"-I{ROCM / 'include'}", f"-I{ROOT / 'include'}", f"-I{ROOT / 'razor_amd' / 'csrc'}"]
+    cmd = ["gcc", "-std=c99", "-O1", "-g", "-fPIC", "-shared", "-fno-omit-frame-pointer",
+           "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-DSIM_VIDEO_SIZE=1000",
+           "-D__HIP_PLATFORM_AMD__", *inc, str(ROOT / "razor_amd" / "csrc" / "rfec_host.c"),
+           str(ROOT / "tests" / "host_stub" / "stub_hip.c"), "-o", str(out), "-lpthread", "-lm"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return out
+
+
+CHILD = r"""
+import sys
+import numpy as np
+sys.path[:0] = [{root!r}, {root!r} + "/oracle", {root!r} + "/tests"]
+import pyoracle as po
+from razor_amd.fec import Native, RfecError, WIRE_REC_DTYPE, RFEC_WIRE_SEG, RFEC_WIRE_FEC
+
+lib = Native(1000, path={lib!r})
+o = po.Oracle(1000)
+STRIDE = 1008
+
+def rx(recs, pay, max_ts=0, max_out=1 << 16):
+    recs = np.ascontiguousarray(recs)
+    pay = np.ascontiguousarray(pay)
+    return lib.rx_recover(len(recs), recs.ctypes.data, pay.ctypes.data, pay.shape[1], 1000, max_ts, max_out)
+
+def check(recs, pay, max_ts=0):
+    out, _, mts, rep = rx(recs, pay, max_ts)
+    eo, _, emts, edrop = o.rx_recover(recs, pay, 1000, max_ts, max_out=1 << 17)
+    idx = np.argsort(eo["hdr"]["seq"], kind="stable")
+    assert len(out) == len(eo), (len(out), len(eo))
+    assert np.array_equal(out["hdr"], eo["hdr"][idx])
+    assert np.array_equal(out["fec_id"], eo["fec_id"][idx])
+    assert mts == emts and rep.n_fec_dropped == edrop and rep.n_unmodelled == 0, (mts, emts, rep.n_fec_dropped, edrop)
+    return len(out)
+
+# 1. the reference receiver's own streams
+fx = po.rx_fixture()
+for scn in fx["scenarios"]:
+    recs, pay, _, _ = po.rx_stream(o, scn)
+    out, _, mts, rep = rx(recs, pay)
+    assert len(out) == len(scn["recovered"]), scn["name"]
+    assert sorted(int(s) for s in out["hdr"]["seq"]) == sorted(r[0] for r in scn["recovered"])
+    assert mts == scn["max_ts"]
+    check(recs, pay)
+print("fixtures ok", len(fx["scenarios"]))
+
+# 2. synthetic streams: oracle sender plan, parities' headers from the oracle
+#    encode, arrival order shuffled with loss / duplicates / late parities
+def stream(seed, frames_n, ks, pfs, loss, window, dup, late):
+    rng = np.random.default_rng(seed)
+    sizes = rng.choice(ks, frames_n) * 1000 - rng.integers(0, 900, frames_n)
+    blob = rng.integers(0, 256, int(sizes.sum()) + 8, dtype=np.uint8)
+    frames = np.zeros(frames_n, po.FRAME)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    frames["data"] = blob.ctypes.data + offs.astype(np.uint64)
+    frames["size"] = sizes
+    frames["payload_type"] = 96
+    frames["ftype"] = np.arange(frames_n) % 50 == 0
+    frames["protect_fraction"] = rng.choice(pfs, frames_n)
+    frames["now_ms"] = 1_700_000_000_000 + np.arange(frames_n) * 33
+    st = o.sender_init()
+    segs, groups = o.sender_plan(st, frames, 1000, max_segs=frames_n * 12 + 64, max_groups=frames_n + 64)
+    return po.synth_rx_stream(o, frames, blob, segs, groups, rng, loss=loss, window=window, dup=dup, late=late)
+
+total = 0
+for seed, args in enumerate([(600, (10,), (80,), 0.12, 40, 0.04, 0.0),
+                             (500, (1, 3, 10, 24), (20, 50, 80, 100), 0.15, 80, 0.04, 0.0),
+                             (400, (10,), (80,), 0.1, 40, 0.04, 0.25),
+                             (300, (6, 10), (100,), 0.35, 200, 0.2, 0.0)]):
+    recs, pay = stream(seed, *args)
+    total += check(recs, pay)
+assert total > 100, total
+print("synthetic ok", total)
+
+# 3. across calls: max_ts carries in, old parities are dropped
+recs, pay = stream(9, 200, (10,), (80,), 0.1, 10, 0.0, 0.0)
+_, _, m1, _ = rx(recs, pay)
+_, _, m2, rep = rx(recs, pay, m1 + 10_000)
+assert m2 == m1 + 10_000 and rep.n_fec_dropped > 0
+
+# 4. edges
+out, _, mts, rep = lib.rx_recover(0, 0, 0, STRIDE, 1000, 77, 4)
+assert len(out) == 0 and mts == 77
+bad = np.zeros(8, WIRE_REC_DTYPE)
+bad["status"] = -1
+out, _, mts, rep = rx(bad, np.zeros((8, STRIDE), np.uint8), 5)
+assert len(out) == 0 and mts == 5 and rep.n_groups == 0
+out, _, _, _ = rx(recs, pay)
+for args in [(len(out) - 1,), ()]:
+    try:
+        if args:
+            rx(recs, pay, 0, args[0])
+        else:
+            lib.rx_recover(len(recs), recs.ctypes.data, pay.ctypes.data, 1000, 1000, 0, 16)
+        raise AssertionError("expected RfecError")
+    except RfecError:
+        pass
+print("edges ok")
+
+# 5. sender staging: plan == oracle plan; the stub frames nothing, so only the
+#    host side (plan, staging layout, report) runs
+for seed in range(3):
+    rng = np.random.default_rng(100 + seed)
+    n = 300
+    sizes = rng.choice((1, 3, 10, 24), n) * 1000 - rng.integers(0, 900, n)
+    blob = rng.integers(0, 256, int(sizes.sum()) + 8, dtype=np.uint8)
+    frames = np.zeros(n, po.FRAME)
+    frames["data"] = blob.ctypes.data + np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    frames["size"] = sizes
+    frames["payload_type"] = 96
+    frames["protect_fraction"] = rng.choice((0, 20, 80, 100), n)
+    frames["now_ms"] = 1_700_000_000_000 + np.arange(n) * 33
+    segs, groups, _, _, _, _, rep = lib.send_frames(lib.sender_init(), frames, 7, 1056, max_segs=n * 25,
+                                                    max_groups=n + 64, max_parities=n * 40)
+    es, eg = o.sender_plan(o.sender_init(), frames, 1000, max_segs=n * 25, max_groups=n + 64)
+    assert np.array_equal(segs, es) and np.array_equal(groups, eg)
+print("sender ok")
+"""
+
+
+def test_host_control_plane_under_asan(stub_lib, tmp_path):
+    script = tmp_path / "child.py"
+    script.write_text(CHILD.format(root=str(ROOT), lib=str(stub_lib)))
+    env = dict(os.environ)
+    env["LD_PRELOAD"] = _libasan()
+    env["ASAN_OPTIONS"] = "detect_leaks=0:abort_on_error=0:halt_on_error=1:exitcode=66"
+    env["UBSAN_OPTIONS"] = "print_stacktrace=1:halt_on_error=1"
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-8000:]
+    assert "sender ok" in r.stdout

@@ -31,19 +31,19 @@ step() {  # step <name> <timeout> <cmd...>
 case "$MODE" in
   full|tests)
     step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-    step pytest_gpu 900 python -m pytest tests -m gpu -x -q -rs ;;
+    step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 120 --timeout-method thread ;;
   ab|all)
-    step pytest_gpu 900 python -m pytest tests -m gpu -x -q -rs
+    step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 120 --timeout-method thread
     step ab 600 python tools/ab_encode.py --out "$OUT/ab.json" ;;
 esac
 case "$MODE" in
   wire)
-    step pytest_gpu 900 python -m pytest tests -m gpu -x -q -rs
+    step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 120 --timeout-method thread
     step wire 300 python tools/wire_bench.py --out "$OUT/wire.json"
     step send 300 python tools/send_bench.py --out "$OUT/send.json"
     step wire_rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/wprof" -o run -- python tools/wire_bench.py ;;
   rx)
-    step pytest_rx 900 python -m pytest tests/test_receiver.py tests/test_sender.py -m gpu -q -rs
+    step pytest_rx 900 python -u -m pytest tests/test_receiver.py tests/test_sender.py -m gpu -q -rs --timeout 120 --timeout-method thread
     step send 300 python tools/send_bench.py --out "$OUT/send.json"
     step rx 600 python tools/rx_bench.py --out "$OUT/rx.json" ;;
 esac
