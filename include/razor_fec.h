@@ -449,6 +449,8 @@ int rfec_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payloa
 #define RFEC_TUNE_NT_STORES 512u   /* non-temporal parity / recovered stores */
 #define RFEC_TUNE_DIAG_CONST_SCHED 1024u /* DIAGNOSTIC ONLY: replay group 0's schedule everywhere */
 #define RFEC_TUNE_TWO_KERNEL_DECODE 4096u /* peel + replay even for disjoint plans (default there: fused) */
+#define RFEC_TUNE_GROUP_WAVE 8192u  /* payload lanes mapped per wave over whole groups (not the flat chunk index) */
+#define RFEC_TUNE_XCD_SWIZZLE 16384u /* consecutive payload blocks on the same XCD */
 /* (defaults: parity stores write-through, recovered stores non-temporal) */
 #define RFEC_TUNE_DIAG_NO_META 256u /* DIAGNOSTIC ONLY: skip fec_meta (wrong output) */
 void rfec_set_tuning(unsigned flags);

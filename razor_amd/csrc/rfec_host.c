@@ -1783,17 +1783,24 @@ typedef struct {
 } rx_ctx;
 static __thread rx_ctx t_rx;
 
-static int rx_reserve(size_t host_bytes, size_t dev_bytes)
+/* Grows the per-thread pinned / device areas.  The first `keep` bytes of the
+ * pinned area survive a grow (copied into the new block before the old one is
+ * freed: the allocator may hand back the same address, so callers cannot tell
+ * a grow from the pointer). */
+static int rx_reserve(size_t host_bytes, size_t dev_bytes, size_t keep)
 {
     hipError_t e;
     if (t_rx.hb < host_bytes) {
-        if (t_rx.h)
-            (void)hipHostFree(t_rx.h);
-        t_rx.h = NULL;
-        t_rx.hb = 0;
+        uint8_t* nh = NULL;
         host_bytes += host_bytes / 4;
-        if ((e = hipHostMalloc((void**)&t_rx.h, host_bytes, hipHostMallocDefault)) != hipSuccess)
+        if ((e = hipHostMalloc((void**)&nh, host_bytes, hipHostMallocDefault)) != hipSuccess)
             return set_err(RFEC_ENOMEM, "rx staging (host)", e);
+        if (t_rx.h) {
+            if (keep)
+                memcpy(nh, t_rx.h, keep < t_rx.hb ? keep : t_rx.hb);
+            (void)hipHostFree(t_rx.h);
+        }
+        t_rx.h = nh;
         t_rx.hb = host_bytes;
     }
     if (t_rx.db < dev_bytes) {
@@ -1829,7 +1836,7 @@ int rfec_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payloa
     int rc = RFEC_OK, ke = 0;
     /* 1. the records to the host (headers only: 64 B each) */
     const size_t rec_bytes = RX_ALIGN((size_t)n * sizeof(rfec_wire_rec));
-    if ((rc = rx_reserve(rec_bytes, 0)))
+    if ((rc = rx_reserve(rec_bytes, 0, 0)))
         return rc;
     double tt = now_us();
     if ((e = hipMemcpyAsync(t_rx.h, recs, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost, sm)) !=
@@ -1912,19 +1919,10 @@ int rfec_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payloa
     const size_t d_shards = o_in_end, d_par = RX_ALIGN(d_shards + (size_t)rows * stride);
     const size_t d_ws = RX_ALIGN(d_par + (size_t)prows * stride), d_rec = RX_ALIGN(d_ws + ws_bytes);
     const size_t d_out = RX_ALIGN(d_rec + (size_t)ngs * 16), dev_bytes = RX_ALIGN(d_out + (size_t)X.nout * stride);
-    /* the records stay at the start of the pinned block: the tables follow them */
-    uint8_t* old = t_rx.h;
-    if ((rc = rx_reserve(rec_bytes + host_bytes, dev_bytes)))
+    /* the records stay at the start of the pinned block (kept across a grow): the tables follow them */
+    if ((rc = rx_reserve(rec_bytes + host_bytes, dev_bytes, (size_t)n * sizeof(rfec_wire_rec))))
         goto out;
-    if (t_rx.h != old) { /* grown: the records were not kept */
-        if ((e = hipMemcpyAsync(t_rx.h, recs, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost, sm)) !=
-                hipSuccess ||
-            (e = hipStreamSynchronize(sm)) != hipSuccess) {
-            rc = set_err(RFEC_EDEVICE, "rx: records D2H", e);
-            goto out;
-        }
-        X.R = (const rfec_wire_rec*)t_rx.h;
-    }
+    X.R = (const rfec_wire_rec*)t_rx.h;
     uint8_t* H = t_rx.h + rec_bytes;
     memset(H, 0, o_in_end);
     int32_t* smap = (int32_t*)(H + o_smap);

@@ -82,6 +82,19 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
 }
 
+// Payload-block index, optionally XCD-swizzled.  Workgroups are dispatched
+// round-robin over the 8 XCDs (block b runs on XCD b % 8, each XCD with its
+// own L2); the swizzle gives every XCD one contiguous range of logical blocks,
+// so a cache line shared by neighbouring blocks is fetched into one L2.  The
+// tail beyond the last multiple of 8 keeps the identity mapping (a bijection).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb, uint32_t swz)
+{
+    const uint32_t nb8 = nb & ~7u;
+    if (!swz || b >= nb8)
+        return b;
+    return (b & 7u) * (nb8 >> 3) + (b >> 3);
+}
+
 // Copies n dwords global -> LDS with the whole block, several loads in flight
 // per lane (a plain strided loop would wait on each load before the next).
 // `lds` must be 16-byte aligned; 16-byte loads are used when `src` is too.
@@ -238,6 +251,64 @@ __global__ __launch_bounds__(kBlock) void k_encode_rows(const v4u* __restrict__ 
 #pragma unroll
     for (int u = 0; u < ITEMS; ++u) {
         if (t0 + u * lanes >= total)
+            continue;
+        v4u* dst = parity + (size_t)gi[u] * R * C + ji[u];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            v4u acc = v[u][r * COL];
+#pragma unroll
+            for (int q = 1; q < COL; ++q)
+                if (r * COL + q < K)
+                    acc ^= v[u][r * COL + q];
+            st16<NTS>(dst + (size_t)r * C, acc);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Encode payload, rows-of-COL, group-per-wave mapping.  Every wave covers
+// whole groups (gpw = max(1, 64 / cd) of them, NI items per lane): a slot's
+// last chunk and the next slot's first chunk, which share a 128-B line when
+// the slot size is not a line multiple (1200 = 9.375 lines), are loaded by
+// the same wave, so the line is fetched from HBM once.  Under the flat
+// mapping those two chunks fall in different waves (often different XCDs)
+// and the line is fetched twice.
+// ---------------------------------------------------------------------------
+template <int K, int COL, bool NTL, int NTS, int NI>
+__global__ __launch_bounds__(kBlock) void k_encode_rows_gw(const v4u* __restrict__ shards, v4u* __restrict__ parity,
+                                                           uint32_t groups, uint32_t C, FastDiv divC, uint32_t gpw,
+                                                           uint32_t swz, EncMeta E, rfec_kplan P)
+{
+    if (blockIdx.x < E.n_meta_blocks) {
+        meta_block(blockIdx.x, E.hdr_dw, E.meta_dw, E.fsize, E.status, E.groups, E.capacity, E.gpb, P);
+        return;
+    }
+    constexpr int R = (K + COL - 1) / COL;
+    const uint32_t b = xcd_block(blockIdx.x - E.n_meta_blocks, gridDim.x - E.n_meta_blocks, swz);
+    const uint32_t wave = b * (kBlock / kWave) + threadIdx.x / kWave;
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t g0 = wave * gpw;
+    const uint32_t span = gpw * divC.d;
+    v4u v[NI][K];
+    uint32_t gi[NI], ji[NI];
+    bool on[NI];
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+        const uint32_t x = lane + u * kWave;
+        const uint32_t gl = fdiv(x, divC);
+        gi[u] = g0 + gl;
+        ji[u] = x - gl * divC.d;
+        on[u] = x < span && gi[u] < groups;
+        if (on[u]) {
+            const v4u* src = shards + (size_t)gi[u] * K * C + ji[u];
+#pragma unroll
+            for (int i = 0; i < K; ++i)
+                v[u][i] = ld16<NTL>(src + (size_t)i * C);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+        if (!on[u])
             continue;
         v4u* dst = parity + (size_t)gi[u] * R * C + ji[u];
 #pragma unroll
@@ -750,6 +821,83 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
     }
 }
 
+// Fused disjoint-plan decode, group-per-wave mapping (see k_encode_rows_gw):
+// each wave covers whole groups, NI chunk items per lane, one item at a time
+// with both fired lines' loads in flight together.
+template <int MAXC, bool NTL, int NTS, int NI>
+__global__ __launch_bounds__(kBlock) void k_decode_disjoint_gw(v4u* shards, const v4u* __restrict__ parity,
+                                                               uint32_t C, FastDiv divC, uint32_t gpw, uint32_t swz,
+                                                               uint32_t n_hdr_blocks, PeelArgs A, rfec_kmask M)
+{
+    if (blockIdx.x < n_hdr_blocks) {
+        peel_block<false, kFusedPeelDwords>(A, M, blockIdx.x);
+        return;
+    }
+    __shared__ uint32_t lplan[RFEC_MAX_LINES];
+    const rfec_kplan& P = M.plan;
+    stage_plan(lplan, P);
+    const uint32_t b = xcd_block(blockIdx.x - n_hdr_blocks, gridDim.x - n_hdr_blocks, swz);
+    const uint32_t wave = b * (kBlock / kWave) + threadIdx.x / kWave;
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t g0 = wave * gpw;
+    const uint32_t span = gpw * divC.d;
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+        const uint32_t x = lane + u * kWave;
+        const uint32_t gl = fdiv(x, divC);
+        const uint32_t g = g0 + gl;
+        const uint32_t j = x - gl * divC.d;
+        if (x >= span || g >= A.groups)
+            continue;
+        const uint64_t h0 = A.present[2 * g], h1 = A.present[2 * g + 1], pm = A.parity_present[g];
+        uint64_t fire = 0;
+        for (uint32_t l = 0; l < P.n_lines; ++l) {
+            const uint64_t x0 = M.mask[l][0] & ~h0, x1 = M.mask[l][1] & ~h1;
+            if (__popcll(x0) + __popcll(x1) == 1)
+                fire |= 1ull << l;
+        }
+        fire &= pm;
+        v4u* grp = shards + (size_t)g * P.k * C + j;
+        const v4u* par = parity + (size_t)g * P.n_lines * C + j;
+        while (fire) {
+            v4u acc[2], mv[2][MAXC];
+            uint32_t tg[2];
+            bool onb[2];
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb) {
+                onb[bb] = fire != 0;
+                const uint32_t l = onb[bb] ? (uint32_t)__ffsll((long long)fire) - 1 : 0;
+                fire &= fire - 1;
+                const uint32_t ln = lplan[l];
+                const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
+                acc[bb] = v4u{0, 0, 0, 0};
+                if (onb[bb])
+                    acc[bb] = ld16<NTL>(par + (size_t)l * C);
+                tg[bb] = first;
+#pragma unroll
+                for (int q = 0; q < MAXC; ++q) {
+                    const uint32_t i = first + q * stride;
+                    mv[bb][q] = v4u{0, 0, 0, 0};
+                    if (!onb[bb] || (uint32_t)q >= count)
+                        continue;
+                    if (has_bit(h0, h1, i))
+                        mv[bb][q] = ld16<NTL>(grp + (size_t)i * C);
+                    else
+                        tg[bb] = i;
+                }
+            }
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb) {
+#pragma unroll
+                for (int q = 0; q < MAXC; ++q)
+                    acc[bb] ^= mv[bb][q];
+                if (onb[bb])
+                    st16<NTS>(grp + (size_t)tg[bb] * C, acc[bb]);
+            }
+        }
+    }
+}
+
 // dst row r <- src row map[r] (all `C` 16-B chunks), or zeros for map[r] < 0:
 // the receiver's scatter of parsed payloads into group slots and its gather
 // of recovered segments.  One lane per chunk, streaming.
@@ -831,9 +979,43 @@ hipError_t launch_rows(const EncLaunch& a)
     return hipGetLastError();
 }
 
+// group-per-wave geometry: gpw whole groups per wave, ni chunk items per lane
+struct GwGeom {
+    uint32_t gpw, ni, blocks;
+};
+
+GwGeom gw_geom(uint32_t groups, uint32_t cd)
+{
+    GwGeom g;
+    g.gpw = cd >= (uint32_t)kWave ? 1u : (uint32_t)kWave / cd;
+    g.ni = (g.gpw * cd + kWave - 1) / kWave;
+    const uint64_t waves = ((uint64_t)groups + g.gpw - 1) / g.gpw;
+    g.blocks = (uint32_t)((waves + kBlock / kWave - 1) / (kBlock / kWave));
+    return g;
+}
+
+template <int K, int COL, bool NTL, int NTS, int NI>
+hipError_t launch_rows_gw(const EncLaunch& a, const GwGeom& g, uint32_t swz)
+{
+    const uint32_t C = a.stride / 16;
+    hipLaunchKernelGGL((k_encode_rows_gw<K, COL, NTL, NTS, NI>), dim3(a.E.n_meta_blocks + g.blocks), dim3(kBlock), 0,
+                       a.stream, a.s, a.p, a.groups, C, make_fastdiv(a.cd), g.gpw, swz, a.E, *a.P);
+    return hipGetLastError();
+}
+
 template <int K, int COL, bool NTL, int NTS>
 hipError_t launch_rows_v(const EncLaunch& a, unsigned flags)
 {
+    if (flags & RFEC_KFLAG_GROUP_WAVE) {
+        const GwGeom g = gw_geom(a.groups, a.cd);
+        const uint32_t swz = (flags & RFEC_KFLAG_XCD_SWIZZLE) ? 1u : 0u;
+        if (g.ni == 1)
+            return launch_rows_gw<K, COL, NTL, NTS, 1>(a, g, swz);
+        if constexpr (K <= 16) { // 2 x K dwordx4 loads in flight per lane
+            if (g.ni == 2)
+                return launch_rows_gw<K, COL, NTL, NTS, 2>(a, g, swz);
+        }
+    }
     if (flags & RFEC_KFLAG_ITEMS2)
         return launch_rows<K, COL, NTL, NTS, 2>(a);
     return launch_rows<K, COL, NTL, NTS, 1>(a);
@@ -883,6 +1065,24 @@ struct FusedArgs {
     uint32_t n_hdr;
     hipStream_t stream;
 };
+
+template <int MAXC, int NI>
+void launch_fused_gw(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, const GwGeom& g,
+                     uint32_t swz)
+{
+    const dim3 grid(F.n_hdr + g.blocks);
+#define RFEC_FUSED_GW(NTL, NTS)                                                                                  \
+    hipLaunchKernelGGL((k_decode_disjoint_gw<MAXC, NTL, NTS, NI>), grid, dim3(kBlock), 0, F.stream, F.shards,    \
+                       F.parity, F.C, F.f, g.gpw, swz, F.n_hdr, B, M)
+    switch (sp) {
+    case -1: RFEC_FUSED_GW(false, 1); break;
+    case 0: RFEC_FUSED_GW(true, 0); break;
+    case 2: RFEC_FUSED_GW(true, 2); break;
+    case 3: RFEC_FUSED_GW(true, 3); break;
+    default: RFEC_FUSED_GW(true, 1); break;
+    }
+#undef RFEC_FUSED_GW
+}
 
 // sp: store policy, -1 = plain loads + non-temporal stores (A/B only)
 template <int MAXC>
@@ -1059,6 +1259,19 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
     if (fused) {
         const FusedArgs F = {sh, pp, total, C, f, n_hdr, st};
         const int sp = ntl ? store_policy(flags, kRecoverStoreDefault) : -1;
+        const GwGeom gg = gw_geom(groups, cd);
+        const uint32_t swz = (flags & RFEC_KFLAG_XCD_SWIZZLE) ? 1u : 0u;
+        if ((flags & RFEC_KFLAG_GROUP_WAVE) && gg.ni <= 2) {
+            if (maxc <= 4 && gg.ni == 1)
+                launch_fused_gw<4, 1>(F, sp, B, *M, gg, swz);
+            else if (maxc <= 4)
+                launch_fused_gw<4, 2>(F, sp, B, *M, gg, swz);
+            else if (gg.ni == 1)
+                launch_fused_gw<8, 1>(F, sp, B, *M, gg, swz);
+            else
+                launch_fused_gw<8, 2>(F, sp, B, *M, gg, swz);
+            return (int)hipGetLastError();
+        }
         if (maxc <= 4)
             launch_fused<4>(F, sp, B, *M, dim3(n_hdr + grid.x));
         else

@@ -17,7 +17,8 @@ MANIFEST = po.manifest()
 CASES = {c["name"]: c for c in MANIFEST["cases"]}
 TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "plain_stores": 4, "items2": 8, "wave_decode": 16,
            "pipe_decode": 32, "wt_stores": 64, "wt_nt_stores": 192, "nt_stores": 512,
-           "generic_plain": 3, "two_kernel": 4096, "two_kernel_wt": 4096 | 64}
+           "generic_plain": 3, "two_kernel": 4096, "two_kernel_wt": 4096 | 64, "group_wave": 8192,
+           "group_wave_xcd": 8192 | 16384, "xcd": 16384}
 
 
 @pytest.fixture(scope="module")
@@ -38,7 +39,7 @@ def test_sender_random_fixture_gpu(gpu, oracle1000):
     pc.check_sender_random_case(gpu(), oracle1000, CASES["random_k"])
 
 
-@pytest.mark.parametrize("tuning", ["default", "generic"])
+@pytest.mark.parametrize("tuning", ["default", "generic", "group_wave", "group_wave_xcd"])
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "rows"])
 def test_rows_fixture_gpu(gpu, oracle1000, oracle1200, name, tuning):
     c = CASES[name]
@@ -47,14 +48,15 @@ def test_rows_fixture_gpu(gpu, oracle1000, oracle1200, name, tuning):
 
 
 @pytest.mark.parametrize("tuning", ["default", "wave_decode", "pipe_decode", "plain_loads", "wt_stores",
-                                    "plain_stores", "nt_stores", "two_kernel"])
+                                    "plain_stores", "nt_stores", "two_kernel", "group_wave_xcd"])
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures"])
 def test_erasure_fixture_gpu(gpu, oracle1000, name, tuning):
     pc.check_erasure_case(gpu(tuning=TUNINGS[tuning]), oracle1000, CASES[name])
 
 
 @pytest.mark.parametrize("tuning", ["default", "wt_stores", "plain_stores", "plain_loads", "two_kernel",
-                                    "two_kernel_wt", "pipe_decode", "wave_decode"])
+                                    "two_kernel_wt", "pipe_decode", "wave_decode", "group_wave",
+                                    "group_wave_xcd"])
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures" and c["rows_only"]])
 def test_erasure_fixture_rows_plan_gpu(gpu, oracle1000, name, tuning):
     """Row-parity-only fixtures against the row-layer plan (pairwise disjoint
@@ -142,7 +144,7 @@ def test_full_size_k10_roundtrip(product, oracle1200, layers):
     plan = lib.plan_from_fraction(k, 80, layers)
     shards, hdr, d_hdr = _device_batch(G, k, S, 1234)
     par, meta, fs, st = _run_encode(lib, plan, G, S, shards, d_hdr)
-    for tuning in (1, 2, 4, 8, 3, 64, 192, 512):
+    for tuning in (1, 2, 4, 8, 3, 64, 192, 512, 8192, 8192 | 16384, 16384):
         par2, meta2, fs2, st2 = _run_encode(lib, plan, G, S, shards, d_hdr, tuning=tuning)
         assert torch.equal(par, par2) and torch.equal(meta, meta2) and torch.equal(fs, fs2), tuning
         del par2, meta2, fs2, st2
@@ -174,7 +176,7 @@ def test_full_size_k10_roundtrip(product, oracle1200, layers):
     ws = torch.empty((lib.workspace_size(plan, G),), dtype=torch.uint8, device=shards.device)
     exp = ((1 << er[:, 0]) | (1 << er[:, 1])).astype(np.int64)
     # default (fused one-launch decode for the disjoint row layer), forced peel + replay
-    for dec_tuning in (0, 4096, 4096 | 64):
+    for dec_tuning in (0, 4096, 4096 | 64, 8192, 8192 | 16384):
         rx = shards.clone()
         rx_hdr = d_hdr.clone()
         for c in range(2):
@@ -203,7 +205,7 @@ def test_full_size_k32_s256(product, oracle1000):
     assert plan.n_lines == 8
     shards, hdr, d_hdr = _device_batch(G, k, S, 99)
     par, meta, fs, st = _run_encode(lib, plan, G, S, shards, d_hdr)
-    for tuning in (1, 8):
+    for tuning in (1, 8, 8192, 8192 | 16384):
         par2, *_ = _run_encode(lib, plan, G, S, shards, d_hdr, tuning=tuning)
         assert torch.equal(par, par2), tuning
     idx = np.r_[0:4, G - 4:G]

@@ -28,13 +28,17 @@ ENC_VARIANTS = {
     "items2": 8,
     "generic": 1,
     "diag_no_meta": 256,
+    "group_wave": 8192,
+    "group_wave_xcd": 8192 | 16384,
+    "xcd": 16384,
 }
 DEC_VARIANTS = {"fused(default nt_st)": 0, "fused_wt_st": 64, "fused_plain_st": 4, "fused_plain_ld": 2,
                 "two_kernel": 4096, "two_kernel_wt_st": 4096 | 64, "diag_const_sched": 4096 | 1024, "wave": 16,
-                "pipe": 32}
+                "pipe": 32, "fused_group_wave": 8192, "fused_group_wave_xcd": 8192 | 16384}
 # (encode flags, decode flags)
 STEP_VARIANTS = {"default (enc wt, dec nt)": (0, 0), "enc nt, dec nt": (512, 512), "enc nt, dec wt": (512, 64),
-                 "enc wt, dec wt": (64, 64), "enc items2": (8, 0), "dec pipe": (0, 32), "dec diag const sched": (0, 4096 | 1024), "dec two-kernel": (0, 4096), "dec wave": (0, 16)}
+                 "enc wt, dec wt": (64, 64), "enc items2": (8, 0), "dec pipe": (0, 32), "dec diag const sched": (0, 4096 | 1024), "dec two-kernel": (0, 4096), "dec wave": (0, 16),
+                 "group_wave both": (8192, 8192), "group_wave+xcd both": (8192 | 16384, 8192 | 16384)}
 
 
 def timeit(fn, reps, stream):
