@@ -1003,6 +1003,19 @@ static int32_t om_get(const omap* m, uint32_t k)
 }
 static void om_put(omap* m, uint32_t k, int32_t v)
 {
+    if (2 * (m->n + 1) > m->cap) { /* keep the load <= 1/2: a full table never terminates a probe */
+        omap g;
+        om_init(&g, m->cap);
+        for (uint32_t i = 0; i < m->cap; ++i)
+            if (m->val[i] != -1) {
+                const uint32_t s = om_slot(&g, m->key[i]);
+                g.key[s] = m->key[i];
+                g.val[s] = m->val[i];
+                g.n++;
+            }
+        om_free(m);
+        *m = g;
+    }
     const uint32_t h = om_slot(m, k);
     if (m->val[h] == -1)
         m->n++;

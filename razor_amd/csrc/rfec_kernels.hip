@@ -753,7 +753,7 @@ __device__ __forceinline__ bool has_bit(uint64_t h0, uint64_t h1, uint32_t i)
     return ((i < 64 ? h0 >> i : h1 >> (i - 64)) & 1ull) != 0;
 }
 
-template <int MAXC, bool NTL, int NTS>
+template <int MAXC, bool NTL, int NTS, int NI>
 __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v4u* __restrict__ parity,
                                                             uint32_t total, uint32_t C, FastDiv divC,
                                                             uint32_t n_hdr_blocks, PeelArgs A, rfec_kmask M)
@@ -765,58 +765,86 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
     __shared__ uint32_t lplan[RFEC_MAX_LINES];
     const rfec_kplan& P = M.plan;
     stage_plan(lplan, P);
-    const uint32_t t = (blockIdx.x - n_hdr_blocks) * kBlock + threadIdx.x;
-    if (t >= total)
-        return;
-    const uint32_t g = fdiv(t, divC);
-    const uint32_t j = t - g * divC.d; // chunk column (divC.d = chunks of work per slot)
-    const uint64_t h0 = A.present[2 * g], h1 = A.present[2 * g + 1], pm = A.parity_present[g];
+    // NI items per lane, item u = t0 + u * (payload lanes): every wave
+    // instruction still covers consecutive chunks, and the items' dependent
+    // mask loads -> payload loads chains overlap
+    const uint32_t lanes = (gridDim.x - n_hdr_blocks) * kBlock;
+    const uint32_t t0 = (blockIdx.x - n_hdr_blocks) * kBlock + threadIdx.x;
+    uint64_t h0[NI], h1[NI], fire[NI];
+    v4u* grp[NI];
+    const v4u* par[NI];
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+        const uint32_t t = t0 + u * lanes;
+        h0[u] = h1[u] = fire[u] = 0;
+        grp[u] = shards;
+        par[u] = parity;
+        if (t < total) {
+            const uint32_t g = fdiv(t, divC);
+            const uint32_t j = t - g * divC.d; // chunk column (divC.d = chunks of work per slot)
+            h0[u] = A.present[2 * g];
+            h1[u] = A.present[2 * g + 1];
+            fire[u] = A.parity_present[g];
+            grp[u] = shards + (size_t)g * P.k * C + j;
+            par[u] = parity + (size_t)g * P.n_lines * C + j;
+        }
+    }
     // lines with their parity received and exactly one member missing
     // (uniform loop: the line masks stay scalar kernel-argument loads)
-    uint64_t fire = 0;
-    for (uint32_t l = 0; l < P.n_lines; ++l) {
-        const uint64_t x0 = M.mask[l][0] & ~h0, x1 = M.mask[l][1] & ~h1;
-        if (__popcll(x0) + __popcll(x1) == 1)
-            fire |= 1ull << l;
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+        uint64_t f = 0;
+        for (uint32_t l = 0; l < P.n_lines; ++l) {
+            const uint64_t x0 = M.mask[l][0] & ~h0[u], x1 = M.mask[l][1] & ~h1[u];
+            if (__popcll(x0) + __popcll(x1) == 1)
+                f |= 1ull << l;
+        }
+        fire[u] &= f;
     }
-    fire &= pm;
-    v4u* grp = shards + (size_t)g * P.k * C + j;
-    const v4u* par = parity + (size_t)g * P.n_lines * C + j;
-    while (fire) {
-        // two fired lines per round, every load of both in flight together
-        v4u acc[2], mv[2][MAXC];
-        uint32_t tg[2];
-        bool on[2];
+    bool more = true;
+    while (more) {
+        // two fired lines per item per round, every load of all of them in flight together
+        v4u acc[NI][2], mv[NI][2][MAXC];
+        uint32_t tg[NI][2];
+        bool on[NI][2];
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            on[b] = fire != 0;
-            const uint32_t l = on[b] ? (uint32_t)__ffsll((long long)fire) - 1 : 0;
-            fire &= fire - 1;
-            const uint32_t ln = lplan[l];
-            const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
-            acc[b] = v4u{0, 0, 0, 0};
-            if (on[b])
-                acc[b] = ld16<NTL>(par + (size_t)l * C);
-            tg[b] = first;
+        for (int u = 0; u < NI; ++u) {
 #pragma unroll
-            for (int q = 0; q < MAXC; ++q) {
-                const uint32_t i = first + q * stride;
-                mv[b][q] = v4u{0, 0, 0, 0};
-                if (!on[b] || (uint32_t)q >= count)
-                    continue;
-                if (has_bit(h0, h1, i))
-                    mv[b][q] = ld16<NTL>(grp + (size_t)i * C);
-                else
-                    tg[b] = i;
+            for (int b = 0; b < 2; ++b) {
+                on[u][b] = fire[u] != 0;
+                const uint32_t l = on[u][b] ? (uint32_t)__ffsll((long long)fire[u]) - 1 : 0;
+                fire[u] &= fire[u] - 1;
+                const uint32_t ln = lplan[l];
+                const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
+                acc[u][b] = v4u{0, 0, 0, 0};
+                if (on[u][b])
+                    acc[u][b] = ld16<NTL>(par[u] + (size_t)l * C);
+                tg[u][b] = first;
+#pragma unroll
+                for (int q = 0; q < MAXC; ++q) {
+                    const uint32_t i = first + q * stride;
+                    mv[u][b][q] = v4u{0, 0, 0, 0};
+                    if (!on[u][b] || (uint32_t)q >= count)
+                        continue;
+                    if (has_bit(h0[u], h1[u], i))
+                        mv[u][b][q] = ld16<NTL>(grp[u] + (size_t)i * C);
+                    else
+                        tg[u][b] = i;
+                }
             }
         }
+        more = false;
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
+        for (int u = 0; u < NI; ++u) {
 #pragma unroll
-            for (int q = 0; q < MAXC; ++q)
-                acc[b] ^= mv[b][q];
-            if (on[b])
-                st16<NTS>(grp + (size_t)tg[b] * C, acc[b]);
+            for (int b = 0; b < 2; ++b) {
+#pragma unroll
+                for (int q = 0; q < MAXC; ++q)
+                    acc[u][b] ^= mv[u][b][q];
+                if (on[u][b])
+                    st16<NTS>(grp[u] + (size_t)tg[u][b] * C, acc[u][b]);
+            }
+            more = more || fire[u] != 0;
         }
     }
 }
@@ -1085,12 +1113,13 @@ void launch_fused_gw(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_k
 }
 
 // sp: store policy, -1 = plain loads + non-temporal stores (A/B only)
-template <int MAXC>
-void launch_fused(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, dim3 grid)
+template <int MAXC, int NI>
+void launch_fused(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M)
 {
+    const dim3 grid(F.n_hdr + blocks_for((F.total + NI - 1) / NI));
 #define RFEC_FUSED(NTL, NTS)                                                                                     \
-    hipLaunchKernelGGL((k_decode_disjoint<MAXC, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards, F.parity, \
-                       F.total, F.C, F.f, F.n_hdr, B, M)
+    hipLaunchKernelGGL((k_decode_disjoint<MAXC, NTL, NTS, NI>), grid, dim3(kBlock), 0, F.stream, F.shards,       \
+                       F.parity, F.total, F.C, F.f, F.n_hdr, B, M)
     switch (sp) {
     case -1: RFEC_FUSED(false, 1); break;
     case 0: RFEC_FUSED(true, 0); break;
@@ -1272,10 +1301,13 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
                 launch_fused_gw<8, 2>(F, sp, B, *M, gg, swz);
             return (int)hipGetLastError();
         }
-        if (maxc <= 4)
-            launch_fused<4>(F, sp, B, *M, dim3(n_hdr + grid.x));
+        const bool two = (flags & RFEC_KFLAG_ITEMS2) != 0;
+        if (maxc <= 4 && two)
+            launch_fused<4, 2>(F, sp, B, *M);
+        else if (maxc <= 4)
+            launch_fused<4, 1>(F, sp, B, *M);
         else
-            launch_fused<8>(F, sp, B, *M, dim3(n_hdr + grid.x));
+            launch_fused<8, 1>(F, sp, B, *M);
         return (int)hipGetLastError();
     }
     hipLaunchKernelGGL(k_peel_lds, dim3(n_hdr), dim3(kBlock), 0, st, B, *M);

@@ -113,7 +113,8 @@ total = 0
 for seed, args in enumerate([(600, (10,), (80,), 0.12, 40, 0.04, 0.0),
                              (500, (1, 3, 10, 24), (20, 50, 80, 100), 0.15, 80, 0.04, 0.0),
                              (400, (10,), (80,), 0.1, 40, 0.04, 0.25),
-                             (300, (6, 10), (100,), 0.35, 200, 0.2, 0.0)]):
+                             (300, (6, 10), (100,), 0.35, 200, 0.2, 0.0),
+                             (3000, (10,), (80,), 0.12, 40, 0.04, 0.0)]):  # > 2048 flexes left open
     recs, pay = stream(seed, *args)
     total += check(recs, pay)
 assert total > 100, total
