@@ -8,8 +8,8 @@
 #         ab    = pytest -m gpu + tools/ab_encode.py
 #         bench = bench + rocprofv3 stats
 #         pmc   = FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py)
-#         wire  = pytest -m gpu + tools/wire_bench.py + tools/send_bench.py + rocprofv3 stats of the wire bench
-#         rx    = receiver + sender tests, tools/send_bench.py, tools/rx_bench.py
+#         wire  = tools/wire_bench.py + tools/send_bench.py + rocprofv3 stats of the wire bench
+#         rx    = receiver + sender tests, tools/send_bench.py, tools/rx_bench.py, tools/e2e_bench.py
 #         all   = pytest + ab + pmc + bench + rocprofv3 stats
 set -u
 TAG=${1:-run}; MODE=${2:-full}; shift 2 || true
@@ -38,14 +38,14 @@ case "$MODE" in
 esac
 case "$MODE" in
   wire)
-    step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 120 --timeout-method thread
     step wire 300 python tools/wire_bench.py --out "$OUT/wire.json"
     step send 300 python tools/send_bench.py --out "$OUT/send.json"
     step wire_rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/wprof" -o run -- python tools/wire_bench.py ;;
   rx)
     step pytest_rx 900 python -u -m pytest tests/test_receiver.py tests/test_sender.py -m gpu -q -rs --timeout 120 --timeout-method thread
     step send 300 python tools/send_bench.py --out "$OUT/send.json"
-    step rx 600 python tools/rx_bench.py --out "$OUT/rx.json" ;;
+    step rx 600 python tools/rx_bench.py --out "$OUT/rx.json"
+    step e2e 300 python tools/e2e_bench.py --out "$OUT/e2e.json" ;;
 esac
 case "$MODE" in
   pmc|all)
