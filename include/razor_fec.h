@@ -436,6 +436,78 @@ int rfec_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payloa
                     uint32_t capacity, uint32_t* max_ts, rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out,
                     uint32_t* n_out, rfec_rx_report* report, void* stream);
 
+/* ------------------------------------------------------------------------ */
+/* Batched UDP I/O: the datagram path of sim_session (sim_session.c:286-296 */
+/* send, :321-364 receive loop) over posix.c's socket calls (su_udp_create  */
+/* :133-170, su_udp_send :240-243, su_udp_recv :245-275), moved from one    */
+/* sendto / select+recvfrom per datagram to sendmmsg / recvmmsg over the    */
+/* [N][dstride] datagram slots the wire codec reads and writes.  Host-only  */
+/* (no HIP); slot buffers are best pinned (hipHostMalloc) so the same block */
+/* is the DMA source / target of the H2D / D2H copies.                      */
+/* ------------------------------------------------------------------------ */
+#define RFEC_EAGAIN (-4)           /* the socket stayed blocked for wait_ms */
+#define RFEC_EIO (-5)              /* a socket call failed (errno in rfec_last_error) */
+#define RFEC_UDP_SERVER 1u         /* SU_SERVER build: 1 MiB buffers, non-blocking (posix.c:135-160) */
+#define RFEC_UDP_RECV_BYTES 1500u  /* receive buffer per datagram (sim_session.c:333) */
+#define RFEC_UDP_MIN_DGRAM 6u      /* SIM_HEADER_SIZE: shorter datagrams are ignored (sim_session.c:339) */
+
+typedef struct {
+    uint32_t ip;   /* host byte order */
+    uint16_t port; /* host byte order */
+    uint16_t reserved;
+} rfec_udp_addr;
+
+typedef struct {
+    uint64_t datagrams;  /* sent / received (kept) datagrams: s->scount / s->rcount */
+    uint64_t bytes;      /* their bytes: s->sbandwidth / s->rbandwidth (sim_session.c:291, 343) */
+    uint64_t skipped;    /* send: slots of length 0 (sim_session_network_send returns -1, :287-288) */
+    uint64_t dropped;    /* recv: datagrams shorter than RFEC_UDP_MIN_DGRAM */
+    uint64_t truncated;  /* recv: datagrams longer than the slot (MSG_TRUNC; their CRC then fails) */
+    uint64_t syscalls;   /* sendmmsg / recvmmsg calls */
+    uint64_t stalls;     /* send: waits for buffer space; recv: waits for data */
+} rfec_udp_stats;
+
+/* su_udp_create (posix.c:133-170): a UDP socket bound to ip:port (ip NULL or
+ * "" = INADDR_ANY, port 0 = any), SO_SNDBUF / SO_RCVBUF = buf_bytes (0 = the
+ * reference's 1 MiB with RFEC_UDP_SERVER, 128 KiB without), non-blocking
+ * with RFEC_UDP_SERVER.  `bound` (may be NULL) receives the bound address. */
+int rfec_udp_open(const char* ip, uint16_t port, unsigned flags, uint32_t buf_bytes, int* fd, rfec_udp_addr* bound);
+void rfec_udp_close(int fd);
+/* su_set_addr (posix.c:282-288) */
+int rfec_udp_addr_of(const char* ip, uint16_t port, rfec_udp_addr* addr);
+
+/* Sends slots [0, n) of dgram ([n][dstride], lengths dlen) to `peer` in slot
+ * order, up to 1024 per sendmmsg; slots of length 0 are skipped.  When the
+ * socket is full it waits for space up to wait_ms per stall (0: no wait) and
+ * then returns RFEC_EAGAIN; *n_done (may be NULL) = slots consumed so far, so
+ * the call can be resumed at that slot.  `st` (may be NULL) accumulates. */
+int rfec_udp_send_batch(int fd, const rfec_udp_addr* peer, uint32_t n, uint32_t dstride, const uint8_t* dgram,
+                        const uint16_t* dlen, uint32_t wait_ms, uint32_t* n_done, rfec_udp_stats* st);
+
+/* Receives up to `max` datagrams into consecutive slots of dgram ([max][dstride],
+ * at most RFEC_UDP_RECV_BYTES of each datagram; slot bytes past the length
+ * are not written) with their lengths in dlen and sources in `from` (may be
+ * NULL).  Waits up to wait_ms for the first datagram, as su_udp_recv's select
+ * does (0: no wait), then takes what is queued without waiting.  Datagrams
+ * shorter than RFEC_UDP_MIN_DGRAM are dropped, as the session loop does.
+ * *n = datagrams stored (0 after a quiet wait_ms: RFEC_OK). */
+int rfec_udp_recv_batch(int fd, uint32_t max, uint32_t dstride, uint8_t* dgram, uint16_t* dlen, rfec_udp_addr* from,
+                        uint32_t wait_ms, uint32_t* n, rfec_udp_stats* st);
+
+/* Received datagrams in host memory -> recovered segments in host memory: one
+ * H2D of the slots, rfec_wire_parse, rfec_rx_recover (arrival order = slot
+ * order).  recs_out (HOST, may be NULL) receives the n parse records.  The
+ * device staging is per calling thread.  rfec_rx_report.h2d_us includes the
+ * datagram H2D; parse time is in kernel_us. */
+int rfec_host_recv_datagrams(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
+                             uint32_t stride, uint32_t capacity, uint32_t* max_ts, rfec_wire_rec* recs_out,
+                             rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out,
+                             rfec_rx_report* report);
+
+/* Pinned host memory for datagram slots (hipHostMalloc / hipHostFree). */
+void* rfec_pinned_alloc(size_t bytes);
+void rfec_pinned_free(void* p);
+
 /* Kernel-selection knobs, for benchmarking and A/B tests (0 = defaults:
  * specialised row kernels where the plan allows, non-temporal streaming). */
 #define RFEC_TUNE_GENERIC 1u       /* always use the generic plan-driven kernel */

@@ -28,6 +28,7 @@ ARCH = os.environ.get("RFEC_OFFLOAD_ARCH", "gfx950")
 
 HIP_SRC = [CSRC / "rfec_kernels.hip", CSRC / "rfec_probe.hip", CSRC / "rfec_wire.hip"]
 C_SRC = [CSRC / "rfec_host.c"]
+NET_SRC = CSRC / "rfec_net.c"  # host-only (sockets), independent of SIM_VIDEO_SIZE
 HEADERS = [INCLUDE / "razor_fec.h", CSRC / "rfec_internal.h"]
 
 VARIANTS = {"librazor_fec.so": 1000, "librazor_fec_v1200.so": 1200}
@@ -66,6 +67,11 @@ def build(force: bool = False, verbose: bool = False) -> dict:
             if verbose:
                 print("built", kobj)
         kobjs.append(kobj)
+    nobj = OBJDIR / "rfec_net.o"
+    if force or _stale(nobj, [NET_SRC] + HEADERS):
+        _run(["gcc", "-std=c99", "-O2", "-fPIC", "-Wall", "-Wextra", f"-I{INCLUDE}", f"-I{CSRC}",
+              "-c", str(NET_SRC), "-o", str(nobj)])
+    kobjs.append(nobj)
     for name, vsize in VARIANTS.items():
         hobj = OBJDIR / f"rfec_host_v{vsize}.o"
         if force or _stale(hobj, C_SRC + HEADERS):

@@ -44,6 +44,16 @@ static int set_err(int code, const char* what, int hip_code)
 
 const char* rfec_last_error(void) { return t_err; }
 
+/* for the other host translation units (rfec_net.c): an OS error */
+int rfec_set_error_sys(int code, const char* what, int err)
+{
+    if (err)
+        snprintf(t_err, sizeof(t_err), "%s: %s (errno %d)", what, strerror(err), err);
+    else
+        snprintf(t_err, sizeof(t_err), "%s", what);
+    return code;
+}
+
 int rfec_sim_video_size(void) { return SIM_VIDEO_SIZE; }
 
 static unsigned g_tuning = 0;
@@ -2057,6 +2067,97 @@ int rfec_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payloa
 out:
     rep->n_unmodelled = X.unmodelled;
     rx_sim_free(&X);
+    rep->total_us = now_us() - t0;
+    return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Received datagrams (host) -> recovered segments (host)                    */
+/* ------------------------------------------------------------------------ */
+void* rfec_pinned_alloc(size_t bytes)
+{
+    void* p = NULL;
+    hipError_t e;
+    if (bytes == 0)
+        return NULL;
+    if ((e = hipHostMalloc(&p, bytes, hipHostMallocDefault)) != hipSuccess) {
+        set_err(RFEC_ENOMEM, "pinned alloc", e);
+        return NULL;
+    }
+    return p;
+}
+
+void rfec_pinned_free(void* p)
+{
+    if (p)
+        (void)hipHostFree(p);
+}
+
+typedef struct {
+    uint8_t* d;
+    size_t db;
+    hipStream_t sm;
+} rv_ctx;
+static __thread rv_ctx t_rv;
+
+int rfec_host_recv_datagrams(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
+                             uint32_t stride, uint32_t capacity, uint32_t* max_ts, rfec_wire_rec* recs_out,
+                             rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out,
+                             rfec_rx_report* rep)
+{
+    const double t0 = now_us();
+    if (!max_ts || !n_out || !rep || (n && (!dgram || !dlen)))
+        return set_err(RFEC_EINVAL, "recv: bad argument", 0);
+    memset(rep, 0, sizeof(*rep));
+    *n_out = 0;
+    if (n == 0)
+        return RFEC_OK;
+    if (dstride < 64 || dstride > RFEC_WIRE_MAX_DSTRIDE || dstride % 16 || stride == 0 || stride % 16 ||
+        capacity > stride)
+        return set_err(RFEC_EINVAL, "recv: dstride must be a multiple of 16 in [64, 2048], stride >= capacity", 0);
+    hipError_t e;
+    if (!t_rv.sm && (e = hipStreamCreateWithFlags(&t_rv.sm, hipStreamNonBlocking)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "recv: stream", e);
+    const size_t o_dl = RX_ALIGN((size_t)n * dstride), o_rec = RX_ALIGN(o_dl + (size_t)n * 2);
+    const size_t o_pay = RX_ALIGN(o_rec + (size_t)n * sizeof(rfec_wire_rec));
+    const size_t need = RX_ALIGN(o_pay + (size_t)n * stride);
+    if (t_rv.db < need) {
+        if (t_rv.d)
+            (void)hipFree(t_rv.d);
+        t_rv.d = NULL;
+        t_rv.db = 0;
+        const size_t b = need + need / 4;
+        if ((e = hipMalloc((void**)&t_rv.d, b)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "recv: device staging", e);
+        t_rv.db = b;
+    }
+    uint8_t* D = t_rv.d;
+    double tt = now_us();
+    if ((e = hipMemcpyAsync(D, dgram, (size_t)n * dstride, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess ||
+        (e = hipMemcpyAsync(D + o_dl, dlen, (size_t)n * 2, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess ||
+        (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "recv: datagrams H2D", e);
+    const double h2d = now_us() - tt;
+    tt = now_us();
+    int ke = rfec_launch_wire_parse(n, dstride, D, (const uint16_t*)(D + o_dl), stride, capacity,
+                                    (rfec_wire_rec*)(D + o_rec), D + o_pay, t_rv.sm);
+    if (ke || (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "recv: parse", ke ? ke : e);
+    const double parse = now_us() - tt;
+    if (recs_out) {
+        tt = now_us();
+        if ((e = hipMemcpyAsync(recs_out, D + o_rec, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost,
+                                t_rv.sm)) != hipSuccess ||
+            (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
+            return set_err(RFEC_EDEVICE, "recv: records D2H", e);
+        rep->d2h_us += now_us() - tt;
+    }
+    const double d2h_recs = rep->d2h_us;
+    const int rc = rfec_rx_recover(n, (const rfec_wire_rec*)(D + o_rec), D + o_pay, stride, capacity, max_ts, out,
+                                   out_payload, max_out, n_out, rep, t_rv.sm);
+    rep->h2d_us += h2d;
+    rep->kernel_us += parse;
+    rep->d2h_us += d2h_recs;
     rep->total_us = now_us() - t0;
     return rc;
 }

@@ -56,6 +56,8 @@ int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map
                             void* stream);
 int rfec_launch_zero_tails(uint32_t slots, uint32_t stride, uint8_t* shards, const rfec_hdr* hdr, void* stream);
 const char* rfec_hip_error_string(int code);
+/* sets rfec_last_error() from an errno value (0: `what` alone); returns code */
+int rfec_set_error_sys(int code, const char* what, int err);
 
 #ifdef __cplusplus
 }

@@ -95,6 +95,25 @@ class rfec_send_report(C.Structure):
                 ("total_us", C.c_double)]
 
 
+class rfec_udp_addr(C.Structure):
+    _fields_ = [("ip", C.c_uint32), ("port", C.c_uint16), ("reserved", C.c_uint16)]
+
+
+class rfec_udp_stats(C.Structure):
+    _fields_ = [("datagrams", C.c_uint64), ("bytes", C.c_uint64), ("skipped", C.c_uint64), ("dropped", C.c_uint64),
+                ("truncated", C.c_uint64), ("syscalls", C.c_uint64), ("stalls", C.c_uint64)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+RFEC_EAGAIN = -4
+RFEC_UDP_SERVER = 1
+RFEC_UDP_RECV_BYTES = 1500
+RFEC_UDP_MIN_DGRAM = 6
+UDP_ADDR_DTYPE = np.dtype([("ip", "<u4"), ("port", "<u2"), ("reserved", "<u2")])
+
+
 class RfecError(RuntimeError):
     pass
 
@@ -201,6 +220,19 @@ _SIGS = {
     "rfec_probe_read": (C.c_int, [_P, C.c_size_t, _P, C.c_uint, _P]),
     "rfec_probe_copy": (C.c_int, [_P, _P, C.c_size_t, C.c_uint, _P]),
     "rfec_probe_write": (C.c_int, [_P, C.c_size_t, C.c_uint, _P]),
+    "rfec_udp_open": (C.c_int, [C.c_char_p, C.c_uint16, C.c_uint, C.c_uint32, C.POINTER(C.c_int),
+                                C.POINTER(rfec_udp_addr)]),
+    "rfec_udp_close": (None, [C.c_int]),
+    "rfec_udp_addr_of": (C.c_int, [C.c_char_p, C.c_uint16, C.POINTER(rfec_udp_addr)]),
+    "rfec_udp_send_batch": (C.c_int, [C.c_int, C.POINTER(rfec_udp_addr), C.c_uint32, C.c_uint32, _P, _P, C.c_uint32,
+                                      C.POINTER(C.c_uint32), C.POINTER(rfec_udp_stats)]),
+    "rfec_udp_recv_batch": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_uint32,
+                                      C.POINTER(C.c_uint32), C.POINTER(rfec_udp_stats)]),
+    "rfec_host_recv_datagrams": (C.c_int, [C.c_uint32, C.c_uint32, _P, _P, C.c_uint32, C.c_uint32,
+                                           C.POINTER(C.c_uint32), _P, _P, _P, C.c_uint32, C.POINTER(C.c_uint32),
+                                           C.POINTER(rfec_rx_report)]),
+    "rfec_pinned_alloc": (_P, [C.c_size_t]),
+    "rfec_pinned_free": (None, [_P]),
 }
 
 
@@ -344,6 +376,55 @@ class Native:
                                              outp.ctypes.data, max_out, C.byref(nout), C.byref(rep), stream),
                     "rfec_rx_recover")
         return out[:nout.value], outp[:nout.value], mts.value, rep
+
+    def host_recv_datagrams(self, n, dstride, dgram, dlen, stride, capacity, max_ts=0, max_out=1 << 16,
+                            want_recs=False):
+        """dgram / dlen: HOST addresses of n received datagram slots.  Returns
+        (segments, payload rows, max_ts, report, recs or None)."""
+        out = np.zeros(max_out, RX_SEG_DTYPE)
+        outp = np.zeros((max_out, stride), np.uint8)
+        recs = np.zeros(n, WIRE_REC_DTYPE) if want_recs else None
+        mts, nout, rep = C.c_uint32(max_ts), C.c_uint32(), rfec_rx_report()
+        self._check(self.lib.rfec_host_recv_datagrams(n, dstride, dgram, dlen, stride, capacity, C.byref(mts),
+                                                      None if recs is None else recs.ctypes.data, out.ctypes.data,
+                                                      outp.ctypes.data, max_out, C.byref(nout), C.byref(rep)),
+                    "rfec_host_recv_datagrams")
+        return out[:nout.value], outp[:nout.value], mts.value, rep, recs
+
+    # -- batched UDP I/O (host memory) -------------------------------------------
+    def udp_open(self, ip="127.0.0.1", port=0, flags=RFEC_UDP_SERVER, buf_bytes=0):
+        """Returns (fd, bound rfec_udp_addr)."""
+        fd, a = C.c_int(-1), rfec_udp_addr()
+        self._check(self.lib.rfec_udp_open(ip.encode() if ip else None, port, flags, buf_bytes, C.byref(fd),
+                                           C.byref(a)), "rfec_udp_open")
+        return fd.value, a
+
+    def udp_close(self, fd):
+        self.lib.rfec_udp_close(fd)
+
+    def udp_addr(self, ip, port):
+        a = rfec_udp_addr()
+        self._check(self.lib.rfec_udp_addr_of(ip.encode(), port, C.byref(a)), "rfec_udp_addr_of")
+        return a
+
+    def udp_send(self, fd, peer, n, dstride, dgram, dlen, wait_ms=100, stats=None):
+        """dgram / dlen: host addresses.  Returns (rc, slots consumed); rc is
+        0 or RFEC_EAGAIN, other errors raise."""
+        done = C.c_uint32()
+        rc = self.lib.rfec_udp_send_batch(fd, C.byref(peer), n, dstride, dgram, dlen, wait_ms, C.byref(done),
+                                          None if stats is None else C.byref(stats))
+        if rc not in (0, RFEC_EAGAIN):
+            self._check(rc, "rfec_udp_send_batch")
+        return rc, done.value
+
+    def udp_recv(self, fd, max_n, dstride, dgram, dlen, wait_ms=5, stats=None, src=None):
+        """dgram / dlen / src (UDP_ADDR_DTYPE array or None): host addresses.
+        Returns the number of datagrams stored."""
+        n = C.c_uint32()
+        self._check(self.lib.rfec_udp_recv_batch(fd, max_n, dstride, dgram, dlen,
+                                                 None if src is None else src.ctypes.data, wait_ms, C.byref(n),
+                                                 None if stats is None else C.byref(stats)), "rfec_udp_recv_batch")
+        return n.value
 
     def set_tuning(self, flags: int):
         self.lib.rfec_set_tuning(flags)

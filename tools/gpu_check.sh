@@ -10,6 +10,7 @@
 #         pmc   = FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py)
 #         wire  = tools/wire_bench.py + tools/send_bench.py + rocprofv3 stats of the wire bench
 #         rx    = receiver + sender tests, tools/send_bench.py, tools/rx_bench.py, tools/e2e_bench.py
+#         udp   = UDP tests (CPU + GPU), tools/udp_bench.py (loopback socket -> receiver ingestion)
 #         all   = pytest + ab + pmc + bench + rocprofv3 stats
 set -u
 TAG=${1:-run}; MODE=${2:-full}; shift 2 || true
@@ -46,6 +47,9 @@ case "$MODE" in
     step send 300 python tools/send_bench.py --out "$OUT/send.json"
     step rx 600 python tools/rx_bench.py --out "$OUT/rx.json"
     step e2e 300 python tools/e2e_bench.py --out "$OUT/e2e.json" ;;
+  udp)
+    step pytest_udp 600 python -u -m pytest tests/test_udp.py -q -rs --timeout 120 --timeout-method thread
+    step udp 300 python tools/udp_bench.py --out "$OUT/udp.json" ;;
 esac
 case "$MODE" in
   pmc|all)
