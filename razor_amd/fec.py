@@ -42,6 +42,7 @@ RFEC_TUNE_DIAG_CONST_SCHED = 1024
 RFEC_TUNE_TWO_KERNEL_DECODE = 4096
 RFEC_TUNE_GROUP_WAVE = 8192
 RFEC_TUNE_XCD_SWIZZLE = 16384
+RFEC_TUNE_VECTOR_MASKS = 32768
 
 # 20-byte header record == sim_fec_meta_t layout (sim_proto.h:145-155)
 HDR_DTYPE = np.dtype([("seq", "<u4"), ("fid", "<u4"), ("ts", "<u4"), ("index", "<u2"), ("total", "<u2"),
@@ -263,6 +264,15 @@ class Native:
         if not self.path.exists():
             raise RfecError(f"{self.path} is missing: build it with `python -m razor_amd.build` "
                             "(there is no fallback path)")
+        # One HIP runtime per process: torch bundles its own libamdhip64 (soname
+        # libamdhip64.so.7, but its users link it by file name), so it must be
+        # loaded before this library, whose libamdhip64.so.7 then resolves to it.
+        # Loaded the other way round, the process holds two runtimes and the
+        # second one to initialise sees no device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         self.lib = C.CDLL(str(self.path))
         for fn, (res, args) in _SIGS.items():
             f = getattr(self.lib, fn)

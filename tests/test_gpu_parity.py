@@ -18,7 +18,7 @@ CASES = {c["name"]: c for c in MANIFEST["cases"]}
 TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "plain_stores": 4, "items2": 8, "wave_decode": 16,
            "pipe_decode": 32, "wt_stores": 64, "wt_nt_stores": 192, "nt_stores": 512,
            "generic_plain": 3, "two_kernel": 4096, "two_kernel_wt": 4096 | 64, "group_wave": 8192,
-           "group_wave_xcd": 8192 | 16384, "xcd": 16384}
+           "group_wave_xcd": 8192 | 16384, "xcd": 16384, "vector_masks": 32768}
 
 
 @pytest.fixture(scope="module")
@@ -56,7 +56,7 @@ def test_erasure_fixture_gpu(gpu, oracle1000, name, tuning):
 
 @pytest.mark.parametrize("tuning", ["default", "wt_stores", "plain_stores", "plain_loads", "two_kernel",
                                     "two_kernel_wt", "pipe_decode", "wave_decode", "group_wave",
-                                    "group_wave_xcd", "items2"])
+                                    "group_wave_xcd", "items2", "generic", "vector_masks"])
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures" and c["rows_only"]])
 def test_erasure_fixture_rows_plan_gpu(gpu, oracle1000, name, tuning):
     """Row-parity-only fixtures against the row-layer plan (pairwise disjoint
@@ -176,7 +176,7 @@ def test_full_size_k10_roundtrip(product, oracle1200, layers):
     ws = torch.empty((lib.workspace_size(plan, G),), dtype=torch.uint8, device=shards.device)
     exp = ((1 << er[:, 0]) | (1 << er[:, 1])).astype(np.int64)
     # default (fused one-launch decode for the disjoint row layer), forced peel + replay
-    for dec_tuning in (0, 4096, 4096 | 64, 8192, 8192 | 16384, 8, 8 | 64):
+    for dec_tuning in (0, 4096, 4096 | 64, 8192, 8192 | 16384, 8, 8 | 64, 1, 32768, 2, 4, 64):
         rx = shards.clone()
         rx_hdr = d_hdr.clone()
         for c in range(2):
@@ -212,6 +212,44 @@ def test_full_size_k32_s256(product, oracle1000):
     p_o, m_o, f_o, _ = o.encode_batch(o.plan_matrix(k, 8, 4, 1), shards[idx].cpu().numpy(), hdr[idx], 256)
     assert np.array_equal(par[idx].cpu().numpy(), p_o)
     assert np.array_equal(meta[idx].cpu().numpy().view(po.HDR_DTYPE).reshape(len(idx), -1), m_o)
+    # decode: up to one erasure in each of 3 random rows per group (row decode kernel, vector masks
+    # at 16 chunks per slot), some rows with their parity lost as well
+    rng = np.random.default_rng(11)
+    er_rows = np.stack([rng.permutation(8)[:3] for _ in range(G)])
+    er = er_rows * 4 + rng.integers(0, 4, (G, 3))
+    er[G // 3:G // 2, 2] = er[G // 3:G // 2, 1]  # some groups with 2 erasures only
+    present = np.uint64((1 << k) - 1) & ~np.bitwise_or.reduce(np.uint64(1) << er.astype(np.uint64), axis=1)
+    pp = np.full(G, 0xFF, np.uint64)
+    pp[::5] &= ~(np.uint64(1) << er_rows[::5, 0].astype(np.uint64))  # parity of the first erased row lost
+    exp = present.copy()
+    gi = torch.arange(G, device=shards.device)
+    for dec_tuning in (0, 1, 4096):
+        rx = shards.clone()
+        rx_hdr = d_hdr.clone()
+        for c in range(3):
+            e = torch.from_numpy(er[:, c]).to(rx.device)
+            rx[gi, e] = 0x5A
+            rx_hdr[gi, e] = 0
+        d_pres = torch.from_numpy(np.stack([present, np.zeros(G, np.uint64)], 1).view(np.int64)).to(rx.device)
+        d_pp = torch.from_numpy(pp.view(np.int64)).to(rx.device)
+        ws = torch.empty((lib.workspace_size(plan, G),), dtype=torch.uint8, device=rx.device)
+        rec = torch.empty((G, 2), dtype=torch.int64, device=rx.device)
+        lib.set_tuning(dec_tuning)
+        try:
+            lib.recover_batch(plan, G, S, S, rx.data_ptr(), rx_hdr.data_ptr(), d_pres.data_ptr(), par.data_ptr(),
+                              meta.data_ptr(), fs.data_ptr(), d_pp.data_ptr(), rec.data_ptr(), ws.data_ptr(),
+                              torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+        finally:
+            lib.set_tuning(0)
+        got = rec[:, 0].cpu().numpy().view(np.uint64)
+        lost_par = np.zeros(G, np.uint64)
+        lost_par[::5] = np.uint64(1) << er[::5, 0].astype(np.uint64)
+        want = ~present & np.uint64((1 << k) - 1) & ~lost_par
+        assert np.array_equal(got, want), dec_tuning
+        ok = torch.from_numpy(((exp | got) == np.uint64((1 << k) - 1))).to(rx.device)
+        assert ok.sum().item() == G - len(range(0, G, 5)), dec_tuning
+        assert torch.equal(rx[ok], shards[ok]) and torch.equal(rx_hdr[ok], d_hdr[ok]), dec_tuning
 
 
 def test_zero_tails(product):
