@@ -510,7 +510,7 @@ void rfec_pinned_free(void* p);
 
 /* Kernel-selection knobs, for benchmarking and A/B tests (0 = defaults:
  * specialised row kernels where the plan allows, non-temporal streaming). */
-#define RFEC_TUNE_GENERIC 1u       /* always use the generic plan-driven kernels (encode and decode) */
+#define RFEC_TUNE_GENERIC 1u       /* always use the generic plan-driven kernel */
 #define RFEC_TUNE_PLAIN_LOADS 2u   /* plain instead of non-temporal payload loads */
 #define RFEC_TUNE_PLAIN_STORES 4u  /* plain instead of non-temporal parity / recovered stores */
 #define RFEC_TUNE_ITEMS2 8u        /* two chunk columns per lane in the row kernels */
@@ -523,7 +523,6 @@ void rfec_pinned_free(void* p);
 #define RFEC_TUNE_TWO_KERNEL_DECODE 4096u /* peel + replay even for disjoint plans (default there: fused) */
 #define RFEC_TUNE_GROUP_WAVE 8192u  /* payload lanes mapped per wave over whole groups (not the flat chunk index) */
 #define RFEC_TUNE_XCD_SWIZZLE 16384u /* consecutive payload blocks on the same XCD */
-#define RFEC_TUNE_VECTOR_MASKS 32768u /* row decode: per-lane vector loads of the group masks (default: scalar when a wave spans <= 2 groups) */
 /* (defaults: parity stores write-through, recovered stores non-temporal) */
 #define RFEC_TUNE_DIAG_NO_META 256u /* DIAGNOSTIC ONLY: skip fec_meta (wrong output) */
 void rfec_set_tuning(unsigned flags);

@@ -849,82 +849,6 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
     }
 }
 
-// ---------------------------------------------------------------------------
-// Fused decode, rows-of-COL layout (k <= 64: the k=10 row layer {4,4,2}, the
-// k=32 rows of 4): k_decode_disjoint with the plan in compile-time constants.
-// Row r fires when parity r arrived and exactly one of its members is missing
-// (flex_recover_row's condition, flex_fec_receiver.c:133-140); its member
-// offsets are constants, so after the masks arrive every load of every fired
-// row issues back to back.  With SMASK (a slot has >= 63 chunks, so a wave
-// spans at most two groups) the masks of the wave's two groups come in
-// through scalar loads, off the vector-memory path the payload loads use.
-// ---------------------------------------------------------------------------
-template <int K, int COL, bool NTL, int NTS, bool SMASK>
-__global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* __restrict__ parity, uint32_t total,
-                                                        uint32_t C, FastDiv divC, uint32_t n_hdr_blocks, PeelArgs A,
-                                                        rfec_kmask M)
-{
-    if (blockIdx.x < n_hdr_blocks) {
-        peel_block<false, kFusedPeelDwords>(A, M, blockIdx.x);
-        return;
-    }
-    static_assert(K <= 64, "one mask word");
-    constexpr int R = (K + COL - 1) / COL;
-    const uint32_t t = (blockIdx.x - n_hdr_blocks) * kBlock + threadIdx.x;
-    const uint32_t g = fdiv(t, divC);
-    const uint32_t j = t - g * divC.d;
-    uint64_t have, pm;
-    if constexpr (SMASK) {
-        // wave-uniform: the group of the wave's first lane and the next one
-        const uint32_t tw = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-        if (tw >= total)
-            return;
-        const uint32_t ga = fdiv(tw, divC);
-        const uint32_t gb = min(ga + 1, A.groups - 1);
-        const uint64_t ha = A.present[2 * ga], hb = A.present[2 * gb];
-        const uint64_t pa = A.parity_present[ga], pb = A.parity_present[gb];
-        have = g == ga ? ha : hb;
-        pm = g == ga ? pa : pb;
-    } else {
-        have = t < total ? A.present[2 * g] : 0;
-        pm = t < total ? A.parity_present[g] : 0;
-    }
-    if (t >= total)
-        return;
-    v4u* grp = shards + (size_t)g * K * C + j;
-    const v4u* par = parity + (size_t)g * R * C + j;
-    bool on[R];
-    uint32_t tg[R];
-    v4u acc[R], mv[K];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int cnt = (r * COL + COL <= K) ? COL : K - r * COL;
-        const uint64_t mr = ((1ull << cnt) - 1ull) << (r * COL);
-        const uint64_t miss = mr & ~have;
-        on[r] = ((pm >> r) & 1ull) && miss != 0 && (miss & (miss - 1ull)) == 0;
-        tg[r] = (uint32_t)__ffsll((long long)miss) - 1u;
-        acc[r] = v4u{0, 0, 0, 0};
-        if (on[r])
-            acc[r] = ld16<NTL>(par + (size_t)r * C);
-#pragma unroll
-        for (int q = 0; q < cnt; ++q) {
-            const int i = r * COL + q;
-            mv[i] = v4u{0, 0, 0, 0};
-            if (on[r] && ((have >> i) & 1ull))
-                mv[i] = ld16<NTL>(grp + (size_t)i * C);
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int cnt = (r * COL + COL <= K) ? COL : K - r * COL;
-#pragma unroll
-        for (int q = 0; q < cnt; ++q)
-            acc[r] ^= mv[r * COL + q];
-        if (on[r])
-            st16<NTS>(grp + (size_t)tg[r] * C, acc[r]);
-    }
-}
-
 // Fused disjoint-plan decode, group-per-wave mapping (see k_encode_rows_gw):
 // each wave covers whole groups, NI chunk items per lane, one item at a time
 // with both fired lines' loads in flight together.
@@ -1170,28 +1094,6 @@ struct FusedArgs {
     hipStream_t stream;
 };
 
-template <int K, int COL>
-void launch_decode_rows(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, bool smask)
-{
-    const dim3 grid(F.n_hdr + blocks_for(F.total));
-#define RFEC_DROWS(NTL, NTS)                                                                                      \
-    do {                                                                                                          \
-        if (smask)                                                                                                \
-            hipLaunchKernelGGL((k_decode_rows<K, COL, NTL, NTS, true>), grid, dim3(kBlock), 0, F.stream, F.shards, \
-                               F.parity, F.total, F.C, F.f, F.n_hdr, B, M);                                       \
-        else                                                                                                      \
-            hipLaunchKernelGGL((k_decode_rows<K, COL, NTL, NTS, false>), grid, dim3(kBlock), 0, F.stream,         \
-                               F.shards, F.parity, F.total, F.C, F.f, F.n_hdr, B, M);                             \
-    } while (0)
-    switch (sp) {
-    case -1: RFEC_DROWS(false, 1); break;
-    case 0: RFEC_DROWS(true, 0); break;
-    case 2: RFEC_DROWS(true, 2); break;
-    default: RFEC_DROWS(true, 1); break;
-    }
-#undef RFEC_DROWS
-}
-
 template <int MAXC, int NI>
 void launch_fused_gw(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, const GwGeom& g,
                      uint32_t swz)
@@ -1397,16 +1299,6 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
                 launch_fused_gw<8, 1>(F, sp, B, *M, gg, swz);
             else
                 launch_fused_gw<8, 2>(F, sp, B, *M, gg, swz);
-            return (int)hipGetLastError();
-        }
-        uint32_t col = 0;
-        if (!(flags & (RFEC_KFLAG_GENERIC | RFEC_KFLAG_ITEMS2)) && is_row_layout(&P, &col) && col == 4 &&
-            (P.k == 10 || P.k == 32) && sp != 3) {
-            const bool smask = cd >= (uint32_t)kWave - 1 && !(flags & RFEC_KFLAG_VECTOR_MASKS); // <= 2 groups per wave
-            if (P.k == 10)
-                launch_decode_rows<10, 4>(F, sp, B, *M, smask);
-            else
-                launch_decode_rows<32, 4>(F, sp, B, *M, smask);
             return (int)hipGetLastError();
         }
         const bool two = (flags & RFEC_KFLAG_ITEMS2) != 0;

@@ -18,7 +18,7 @@ CASES = {c["name"]: c for c in MANIFEST["cases"]}
 TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "plain_stores": 4, "items2": 8, "wave_decode": 16,
            "pipe_decode": 32, "wt_stores": 64, "wt_nt_stores": 192, "nt_stores": 512,
            "generic_plain": 3, "two_kernel": 4096, "two_kernel_wt": 4096 | 64, "group_wave": 8192,
-           "group_wave_xcd": 8192 | 16384, "xcd": 16384, "vector_masks": 32768}
+           "group_wave_xcd": 8192 | 16384, "xcd": 16384}
 
 
 @pytest.fixture(scope="module")
@@ -56,7 +56,7 @@ def test_erasure_fixture_gpu(gpu, oracle1000, name, tuning):
 
 @pytest.mark.parametrize("tuning", ["default", "wt_stores", "plain_stores", "plain_loads", "two_kernel",
                                     "two_kernel_wt", "pipe_decode", "wave_decode", "group_wave",
-                                    "group_wave_xcd", "items2", "generic", "vector_masks"])
+                                    "group_wave_xcd", "items2"])
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures" and c["rows_only"]])
 def test_erasure_fixture_rows_plan_gpu(gpu, oracle1000, name, tuning):
     """Row-parity-only fixtures against the row-layer plan (pairwise disjoint
@@ -176,7 +176,7 @@ def test_full_size_k10_roundtrip(product, oracle1200, layers):
     ws = torch.empty((lib.workspace_size(plan, G),), dtype=torch.uint8, device=shards.device)
     exp = ((1 << er[:, 0]) | (1 << er[:, 1])).astype(np.int64)
     # default (fused one-launch decode for the disjoint row layer), forced peel + replay
-    for dec_tuning in (0, 4096, 4096 | 64, 8192, 8192 | 16384, 8, 8 | 64, 1, 32768, 2, 4, 64):
+    for dec_tuning in (0, 4096, 4096 | 64, 8192, 8192 | 16384, 8, 8 | 64, 2, 4, 64):
         rx = shards.clone()
         rx_hdr = d_hdr.clone()
         for c in range(2):
