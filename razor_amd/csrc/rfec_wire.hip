@@ -13,11 +13,14 @@
 // datagram slot is at most 2 KiB).  Payload bytes move through registers with
 // a wave-uniform byte funnel (no LDS staging); the header is assembled with
 // compile-time byte positions.  CRC32 is computed wave-parallel: each lane
-// takes the raw CRC of its 32 bytes with slice-by-16 tables in LDS, scales it
-// by x^(8e) mod P for the e bytes that follow its run (a 32-step carry-less
-// multiply, zlib's multmodp), and the wave XOR-reduces.  The CRC's initial
+// takes the raw CRC of its 32 bytes with slice-by-16 tables in LDS and scales
+// it to the end of the message by x^(8e) mod P, e = the bytes after its run.
+// With n = 2048 - 32q - r, e = 256 (63 - j - q) - 8r: the x^(256 (63 - c))
+// part is a fixed per-column multiplier (eight nibble lookups in column
+// c = j + q, zlib's multmodp tabulated), the x^(-8r) part is applied once to
+// the wave's XOR-reduced sum (one lookup per bit lane).  The CRC's initial
 // register is folded into the first four message bytes, so every lane runs
-// from a zero register.
+// from a zero register.  Cross-lane sums use DPP within rows plus readlane.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,16 +35,21 @@ constexpr uint32_t kPoly = 0xEDB88320u; // reflected CRC-32 polynomial (cf_crc32
 
 // LDS tables (built at compile time, copied to LDS once per block):
 //   t[s][b]         CRC register after byte b then s zero bytes, from 0 (slice-by-16)
-//   nib[i][v][j]    (nibble v at nibble position i of a register) * x^(256 (63-j)):
-//                   lane j's run, right-aligned in a 2 KiB window, carried to the
-//                   window's end.  [i][v][lane]: a lane reads only its own column,
-//                   so the 64 lanes never share an LDS bank.
+//   nib[i][v][c]    (nibble v at nibble position i of a register) * x^(256 (63-c)):
+//                   a 32-byte run in column c of a 2 KiB window, carried to the
+//                   window's end.  [i][v][c]: the lanes read distinct columns, so
+//                   they never share an LDS bank.
+//   inv[r][i]       x^(31-i) * x^(-8r): bit i of a register times x^(-8r)
+// (bit p of a register is the coefficient of x^(31-p))
 struct CrcTables {
     uint32_t t[16][256];
     uint32_t nib[8][16][kWave];
+    uint32_t inv[32][32];
 };
 
 constexpr uint32_t mul_x(uint32_t v) { return (v & 1u) ? (v >> 1) ^ kPoly : v >> 1; }
+// the inverse of mul_x (kPoly has bit 31 set, v >> 1 never does)
+constexpr uint32_t div_x(uint32_t v) { return (v & 0x80000000u) ? (((v ^ kPoly) << 1) | 1u) : (v << 1); }
 
 constexpr CrcTables make_crc_tables()
 {
@@ -75,6 +83,14 @@ constexpr CrcTables make_crc_tables()
         for (int q = 0; q < 256; ++q)
             V = mul_x(V);
     }
+    for (int i = 0; i < 32; ++i) {
+        uint32_t v = 1u << i; // x^(31-i)
+        for (int q = 0; q < 32; ++q) {
+            r.inv[q][i] = v;
+            for (int b = 0; b < 8; ++b)
+                v = div_x(v);
+        }
+    }
     return r;
 }
 
@@ -83,7 +99,8 @@ __device__ const CrcTables kCrc = make_crc_tables();
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 constexpr int kTabDwords = (int)(sizeof(CrcTables) / 4);
-constexpr int kNibBase = 16 * 256; // dword offset of nib in the LDS copy
+constexpr int kNibBase = 16 * 256;                 // dword offset of nib in the LDS copy
+constexpr int kInvBase = kNibBase + 8 * 16 * kWave; // dword offset of inv
 __device__ __forceinline__ void load_tables(uint32_t* T)
 {
     const v4u* s = reinterpret_cast<const v4u*>(&kCrc);
@@ -104,10 +121,10 @@ __device__ __forceinline__ uint32_t slice16(const uint32_t* T, uint32_t a, uint3
            tb(T, 3, d & 0xff) ^ tb(T, 2, (d >> 8) & 0xff) ^ tb(T, 1, (d >> 16) & 0xff) ^ tb(T, 0, d >> 24);
 }
 
-// c * x^(256 (63 - lane)) mod P: eight nibble lookups in the lane's own column
-__device__ __forceinline__ uint32_t carry_to_end(const uint32_t* T, uint32_t c, uint32_t lane)
+// c * x^(256 (63 - col)) mod P: eight nibble lookups in column `col`
+__device__ __forceinline__ uint32_t carry_to_end(const uint32_t* T, uint32_t c, uint32_t col)
 {
-    const uint32_t* nb = T + kNibBase + lane;
+    const uint32_t* nb = T + kNibBase + col;
     uint32_t r = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -115,28 +132,33 @@ __device__ __forceinline__ uint32_t carry_to_end(const uint32_t* T, uint32_t c, 
     return r;
 }
 
-__device__ __forceinline__ uint32_t wave_xor(uint32_t v)
+// DPP controls (GFX9): quad_perm [1,0,3,2], [2,3,0,1]; row_ror 4, 8
+constexpr int kDppQuadSwap1 = 0xB1, kDppQuadSwap2 = 0x4E, kDppRowRor4 = 0x124, kDppRowRor8 = 0x128;
+__device__ __forceinline__ uint32_t dpp(uint32_t v, int ctrl)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1)
-        v ^= (uint32_t)__shfl_xor((int)v, o, kWave);
-    return v;
+    switch (ctrl) { // the builtin needs a constant
+    case kDppQuadSwap1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppQuadSwap1, 0xF, 0xF, false);
+    case kDppQuadSwap2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppQuadSwap2, 0xF, 0xF, false);
+    case kDppRowRor4: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppRowRor4, 0xF, 0xF, false);
+    default: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppRowRor8, 0xF, 0xF, false);
+    }
 }
 
-// v of lane `src` (0 when src < 0).  The permute runs with every lane active
-// (a lane masked off would not supply its value to the lanes reading it);
-// only the result is selected.
-__device__ __forceinline__ uint32_t from_lane(uint32_t v, int src)
+// XOR of v over the wave (wave-uniform result): a 16-lane row reduction with
+// DPP (every lane of a row ends up with the row's XOR), then the four rows
+// through readlane.  Every lane must be active.
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v)
 {
-    const uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((src < 0 ? 0 : src) << 2, (int)v);
-    return src >= 0 ? r : 0u;
+    v ^= dpp(v, kDppQuadSwap1);
+    v ^= dpp(v, kDppQuadSwap2);
+    v ^= dpp(v, kDppRowRor4);
+    v ^= dpp(v, kDppRowRor8);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) ^ (uint32_t)__builtin_amdgcn_readlane((int)v, 16) ^
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 32) ^ (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 
 // crc32(seed, msg[0:n)) (cf_crc32.c:56-68) of a message held lane-wise:
 // lane j has bytes [32j, 32j+32) in w (LE dwords), bytes >= n zero; n <= 2048.
-// The message is moved right by D = 2048 - n bytes (leading zeros do not
-// change a zero-register CRC), so lane j's run always ends 32 (63 - j) bytes
-// before the message does and its carry is a fixed per-lane multiplier.
 __device__ uint32_t wave_crc32(const uint32_t* T, const uint32_t w[8], uint32_t n, uint32_t seed, uint32_t lane)
 {
     if (n < 4) { // too short to fold the initial register into: bytewise
@@ -148,54 +170,13 @@ __device__ uint32_t wave_crc32(const uint32_t* T, const uint32_t w[8], uint32_t 
     const uint32_t D = 2048u - n, q = D >> 5, rr = D & 31u;
     // initial register folded into message bytes 0-3
     const uint32_t w0 = w[0] ^ (lane == 0 ? ~seed : 0u);
-    // right-aligned view: lane j <- bytes [32j - D, 32j - D + 32) = the last rr
-    // bytes of lane j-q-1 and the first 32-rr bytes of lane j-q
-    const int la = (int)lane - (int)q - 1, lb = (int)lane - (int)q;
-    uint32_t X[16];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint32_t v = k == 0 ? w0 : w[k];
-        X[k] = from_lane(v, la);
-        X[8 + k] = from_lane(v, lb);
-    }
-    uint32_t v[8];
-    const uint32_t st = 32u - rr, rb = st & 3u;
-#define RFEC_VIEW(S)                                                                                              \
-    _Pragma("unroll") for (int k = 0; k < 8; ++k) v[k] =                                                          \
-        ((S) + k + 1 < 16) ? __builtin_amdgcn_alignbyte(X[((S) + k + 1) & 15], X[(S) + k], rb) : X[(S) + k];
-    switch (st >> 2) {
-    case 0: RFEC_VIEW(0) break;
-    case 1: RFEC_VIEW(1) break;
-    case 2: RFEC_VIEW(2) break;
-    case 3: RFEC_VIEW(3) break;
-    case 4: RFEC_VIEW(4) break;
-    case 5: RFEC_VIEW(5) break;
-    case 6: RFEC_VIEW(6) break;
-    case 7: RFEC_VIEW(7) break;
-    default: RFEC_VIEW(8) break; // rr == 0: lane j-q as it is
-    }
-#undef RFEC_VIEW
-    uint32_t c = slice16(T, v[0], v[1], v[2], v[3]);
-    c = slice16(T, v[4] ^ c, v[5], v[6], v[7]);
-    return ~wave_xor(carry_to_end(T, c, lane));
-}
-
-// bytes [lo, hi) of the dword at byte position p0, as a byte mask
-__device__ __forceinline__ uint32_t range_mask(int p0, int lo, int hi)
-{
-    const int a = min(max(lo - p0, 0), 4), b = min(max(hi - p0, 0), 4);
-    const uint32_t fb = b >= 4 ? 0xffffffffu : (1u << (8 * b)) - 1u;
-    const uint32_t fa = a >= 4 ? 0xffffffffu : (1u << (8 * a)) - 1u;
-    return fb & ~fa;
-}
-
-// 4 LE bytes `fb` starting at byte position `pos`, seen from the dword at p0
-// (0 when they miss it): the 64-bit shift count is 0 or 64 (== 0 mod 64) off
-// the overlap, and the low half of fb:0 is zero
-__device__ __forceinline__ uint32_t place(uint32_t fb, int pos, int p0)
-{
-    const uint32_t s = (uint32_t)(32 - 8 * min(max(pos - p0, -4), 4));
-    return (uint32_t)(((uint64_t)fb << 32) >> (s & 63u));
+    uint32_t c = slice16(T, w0, w[1], w[2], w[3]);
+    c = slice16(T, w[4] ^ c, w[5], w[6], w[7]);
+    // lanes past the message hold zeros (c == 0): their column is clamped
+    const uint32_t R = wave_xor(carry_to_end(T, c, min(lane + q, (uint32_t)kWave - 1u)));
+    // R = crc register * x^(8 rr): bit i of R times x^(31-i-8rr), summed
+    const uint32_t b = lane < 32 && ((R >> (lane & 31u)) & 1u) ? T[kInvBase + rr * 32 + (lane & 31u)] : 0u;
+    return ~wave_xor(b);
 }
 
 __device__ __forceinline__ uint32_t bswap(uint32_t v) { return __builtin_bswap32(v); }
@@ -251,11 +232,14 @@ __device__ __forceinline__ void funnel_c(const Win& w, uint32_t out[8])
                           : x[(SH >> 2) + k];
 }
 
-// byte mask of the first `keep` bytes of a dword (keep clamped to [0, 4])
-__device__ __forceinline__ uint32_t keep_mask(int keep)
+// Mask of dword k of lane `lane` for a message of nb bytes held lane-wise
+// (lane j = bytes [32j, 32j+32)): the byte position of nb is wave-uniform, so
+// per lane this is two selects of uniform values.
+__device__ __forceinline__ uint32_t len_mask(int k, uint32_t lane, uint32_t nb)
 {
-    const uint32_t s = 32u - 8u * (uint32_t)min(max(keep, 0), 4); // one 64-bit shift, no branch
-    return (uint32_t)(0xffffffffull >> s);
+    const uint32_t qd = nb >> 2, s = nb & 3u, lq = qd >> 3, kq = qd & 7u;
+    const uint32_t ck = (uint32_t)k < kq ? ~0u : ((uint32_t)k == kq ? (s ? (1u << (8 * s)) - 1u : 0u) : 0u);
+    return lane < lq ? ~0u : (lane == lq ? ck : 0u);
 }
 
 __device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t slot_bytes, uint32_t lane,
@@ -291,15 +275,22 @@ __device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, ui
     uint32_t w[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const int p0 = 32 * (int)lane + 4 * k;
         // header dwords live in lanes 0 and 1 (hsize <= 48)
         const uint32_t hd = lane == 0 ? H.h[k] : (lane == 1 && k < 4 ? H.h[8 + k] : 0u);
-        w[k] = (pay[k] | hd) & keep_mask((int)n - p0);
+        w[k] = (pay[k] | hd) & len_mask(k, lane, n);
     }
     const uint32_t crc = wave_crc32(T, w, n, RFEC_WIRE_CRC_SEED, lane);
+    // big-endian trailer at byte n: its first 4 - s bytes end dword n / 4, the
+    // rest start the next one (both positions wave-uniform)
+    const uint32_t be = bswap(crc), s = n & 3u, q0 = n >> 2, q1 = q0 + 1;
+    const uint32_t lo = be << (8 * s), hi = s ? be >> (32 - 8 * s) : 0u;
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-        w[k] |= place(bswap(crc), (int)n, 32 * (int)lane + 4 * k);
+    for (int k = 0; k < 8; ++k) {
+        if ((uint32_t)k == (q0 & 7u))
+            w[k] |= lane == (q0 >> 3) ? lo : 0u;
+        if ((uint32_t)k == (q1 & 7u))
+            w[k] |= lane == (q1 >> 3) ? hi : 0u;
+    }
     store_slot(slot, dstride, lane, w);
     if (lane == 0)
         *dlen_out = (uint16_t)(n + 4);
@@ -628,6 +619,12 @@ __device__ __forceinline__ void write_rec(rfec_wire_rec* r, const rfec_wire_rec&
     }
 }
 
+// v of lane + 1 (0 in lane 63): DPP wave_shl:1, no LDS traffic
+__device__ __forceinline__ uint32_t next_lane(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);
+}
+
 // out lane j = datagram bytes [pos + 32j, pos + 32j + 32) from the lane-wise
 // datagram w (pos wave-uniform, < 64)
 __device__ __forceinline__ void shift_down_bytes(const uint32_t w[8], uint32_t pos, uint32_t out[8])
@@ -636,8 +633,8 @@ __device__ __forceinline__ void shift_down_bytes(const uint32_t w[8], uint32_t p
     const bool q = pos >= 32;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const uint32_t n1 = (uint32_t)__shfl_down((int)w[k], 1, kWave);
-        const uint32_t n2 = q ? (uint32_t)__shfl_down((int)w[k], 2, kWave) : 0u;
+        const uint32_t n1 = next_lane(w[k]);
+        const uint32_t n2 = q ? next_lane(n1) : 0u;
         A[k] = q ? n1 : w[k];
         B[k] = q ? n2 : n1;
     }
@@ -692,9 +689,8 @@ __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ dg
                 uint32_t w[8], m[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
-                    const int p0 = 32 * (int)lane + 4 * k;
-                    w[k] = P.w.c[k >> 2][k & 3] & keep_mask((int)len - p0);
-                    m[k] = w[k] & keep_mask((int)len - 4 - p0);
+                    w[k] = P.w.c[k >> 2][k & 3] & len_mask(k, lane, len);
+                    m[k] = w[k] & len_mask(k, lane, len - 4);
                 }
                 // CRC over [0, len-4) against the big-endian trailer (sim_proto.c:21-37)
                 const uint32_t crc = wave_crc32(T, m, len - 4, RFEC_WIRE_CRC_SEED, lane);
@@ -705,7 +701,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ dg
                     lo = tk == (uint32_t)k ? w[k] : lo;
                     hi = tk == (uint32_t)k ? (k < 7 ? w[k + 1] : 0u) : hi;
                 }
-                const uint32_t nx = (uint32_t)__shfl_down((int)w[0], 1, kWave); // next lane's first dword
+                const uint32_t nx = next_lane(w[0]); // next lane's first dword
                 hi = tk == 7u ? nx : hi;
                 const uint64_t t2 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, (int)tl) << 32 |
                                     (uint32_t)__builtin_amdgcn_readlane((int)lo, (int)tl);
@@ -855,7 +851,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ dg
                         shift_down_bytes(w, (uint32_t)data_at, pay);
 #pragma unroll
                         for (int k = 0; k < 8; ++k)
-                            pay[k] &= keep_mask((int)dsize - 32 * (int)lane - 4 * k);
+                            pay[k] &= len_mask(k, lane, dsize);
                         store_slot(slot, stride, lane, pay);
                     }
                 }
