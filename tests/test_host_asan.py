@@ -48,7 +48,7 @@ def stub_lib(tmp_path_factory):
     cmd = ["gcc", "-std=c99", "-O1", "-g", "-fPIC", "-shared", "-fno-omit-frame-pointer",
            "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-DSIM_VIDEO_SIZE=1000",
            "-D__HIP_PLATFORM_AMD__", *inc, str(ROOT / "razor_amd" / "csrc" / "rfec_host.c"),
-           str(ROOT / "tests" / "host_stub" / "stub_hip.c"), "-o", str(out), "-lpthread", "-lm"]
+           str(ROOT / "razor_amd" / "csrc" / "rfec_net.c"), str(ROOT / "tests" / "host_stub" / "stub_hip.c"), "-o", str(out), "-lpthread", "-lm"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     return out
@@ -163,6 +163,33 @@ for seed in range(3):
     es, eg = o.sender_plan(o.sender_init(), frames, 1000, max_segs=n * 25, max_groups=n + 64)
     assert np.array_equal(segs, es) and np.array_equal(groups, eg)
 print("sender ok")
+
+# 6. batched UDP I/O over loopback (rfec_net.c): slots out, slots in, the
+#    reference's length rules, more than one sendmmsg / recvmmsg batch
+from razor_amd.fec import RFEC_UDP_SERVER, rfec_udp_stats
+rxfd, rxa = lib.udp_open("127.0.0.1", 0, RFEC_UDP_SERVER, 4 << 20)
+txfd, _ = lib.udp_open("127.0.0.1", 0, RFEC_UDP_SERVER, 4 << 20)
+rng = np.random.default_rng(6)
+D = 1504
+lens = rng.integers(0, 1500, 1500).astype(np.uint16)
+dg = rng.integers(0, 256, (1500, D), dtype=np.uint8)
+got = np.zeros((1500, 512), np.uint8)
+gl = np.zeros(1500, np.uint16)
+st = rfec_udp_stats()
+n_in, off = 0, 0
+while off < 1500:
+    rc, done = lib.udp_send(txfd, rxa, min(200, 1500 - off), D, dg[off:].ctypes.data, lens[off:].ctypes.data, 100)
+    off += done
+    n_in += lib.udp_recv(rxfd, 1500 - n_in, 512, got[n_in:].ctypes.data, gl[n_in:].ctypes.data, 20, st)
+for _ in range(20):
+    n_in += lib.udp_recv(rxfd, 1500 - n_in, 512, got[n_in:].ctypes.data, gl[n_in:].ctypes.data, 20, st)
+keep = lens >= 6
+assert n_in == keep.sum(), (n_in, keep.sum())
+assert np.array_equal(gl[:n_in], np.minimum(lens[keep], 512))
+assert st.truncated == (lens[keep] > 512).sum() and st.dropped == ((lens > 0) & ~keep).sum()
+lib.udp_close(rxfd)
+lib.udp_close(txfd)
+print("udp ok")
 """
 
 
@@ -175,4 +202,4 @@ def test_host_control_plane_under_asan(stub_lib, tmp_path):
     env["UBSAN_OPTIONS"] = "print_stacktrace=1:halt_on_error=1"
     r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-8000:]
-    assert "sender ok" in r.stdout
+    assert "sender ok" in r.stdout and "udp ok" in r.stdout
