@@ -11,7 +11,11 @@
  *   receiver sim_fec_put_segment / sim_fec_put_fec_packet (sim_fec.c:141-207)
  *            with the recovery cascade of sim_receiver_recover
  *            (sim_receiver.c:780-804): recovered packets drained lowest
- *            packet_id first, re-fed unless already in the receiver
+ *            packet_id first, re-fed unless already in the receiver; with
+ *            evict_every > 0, sim_fec_evict (sim_fec.c:209-241) after every
+ *            evict_every arrivals, as the session heartbeat's
+ *            sim_receiver_timer calls it (sim_receiver.c:880), its 300 ms
+ *            wall-clock gate always open
  *
  * Writes tests/golden/rx.json: per scenario the frames, the sender's groups,
  * the arrival sequence and the packets the receiver recovered, in delivery
@@ -68,8 +72,9 @@ static uint8_t seen[1 << 20]; /* packet ids already in the receiver (received or
 static FILE* js;
 static int first_case = 1;
 
-static void scenario(const char* name, uint64_t id, const frame_t* frames, int nf, uint32_t seg_loss_pm,
-                     uint32_t fec_loss_pm, uint32_t window, uint32_t dup_pm, uint32_t late_pm, int protect_tail)
+static void scenario_x(const char* name, uint64_t id, const frame_t* frames, int nf, uint32_t seg_loss_pm,
+                       uint32_t fec_loss_pm, uint32_t window, uint32_t dup_pm, uint32_t late_pm, int protect_tail,
+                       uint32_t late_seg_pm, int evict_every)
 {
     uint64_t st = 0x5354414745ull ^ id, rs = 0x52585258ull ^ id;
     flex_fec_sender_t* flex = flex_fec_sender_create();
@@ -157,6 +162,8 @@ static void scenario(const char* name, uint64_t id, const frame_t* frames, int n
         uint64_t key = (uint64_t)q * 1024 + oracle_xs_rand(&rs, window * 1024);
         if (a->kind == 1 && oracle_xs_rand(&rs, 999) < late_pm)
             key += (uint64_t)(150 + oracle_xs_rand(&rs, 200)) * 1024 * 12; /* seconds late */
+        if (late_seg_pm && a->kind == 0 && oracle_xs_rand(&rs, 999) < late_seg_pm)
+            key += (uint64_t)(100 + oracle_xs_rand(&rs, 150)) * 1024 * 12; /* segments seconds late */
         arr[na++] = (arrival_t){a->kind, a->idx, key, 0};
         if (oracle_xs_rand(&rs, 999) < dup_pm)
             arr[na++] = (arrival_t){a->kind, a->idx, key + 1 + oracle_xs_rand(&rs, window * 2048), 1};
@@ -172,6 +179,7 @@ static void scenario(const char* name, uint64_t id, const frame_t* frames, int n
     /* receiver: sim_receiver_put (sim_receiver.c:811-827) / _put_fec (:829-838) */
     memset(seen, 0, sizeof(seen));
     sim_receiver_fec_t* rx = sim_fec_create(NULL);
+    int64_t clock = rx->evict_ts;
     int nrec = 0;
     for (int a = 0; a < na; ++a) {
         if (arr[a].kind == 0) {
@@ -202,8 +210,14 @@ static void scenario(const char* name, uint64_t id, const frame_t* frames, int n
             nrec++;
             sim_fec_put_segment(NULL, rx, &in);
         }
+        if (evict_every > 0 && a % evict_every == evict_every - 1) {
+            clock += 1000; /* past EVICT_FEC_TIMER (sim_fec.c:209) */
+            sim_fec_evict(NULL, rx, clock);
+        }
     }
-    fprintf(js, "],\n   \"max_ts\": %u, \"segments\": %d, \"n_parities\": %d}", rx->max_ts, ns, np);
+    fprintf(js, "],\n   \"max_ts\": %u, \"segments\": %d, \"n_parities\": %d, \"evict_every\": %d, "
+                "\"flexes_left\": %u, \"cache_left\": %u}",
+            rx->max_ts, ns, np, evict_every, (unsigned)skiplist_size(rx->flexes), (unsigned)skiplist_size(rx->segs_cache));
     fprintf(stderr, "%-22s segments %d parities %d arrivals %d recovered %d\n", name, ns, np, na, nrec);
     sim_fec_destroy(NULL, rx);
     for (int q = 0; q < ns; ++q)
@@ -212,6 +226,12 @@ static void scenario(const char* name, uint64_t id, const frame_t* frames, int n
         free(fecs[p]);
     destroy_list(out);
     flex_fec_sender_destroy(flex);
+}
+
+static void scenario(const char* name, uint64_t id, const frame_t* frames, int nf, uint32_t seg_loss_pm,
+                     uint32_t fec_loss_pm, uint32_t window, uint32_t dup_pm, uint32_t late_pm, int protect_tail)
+{
+    scenario_x(name, id, frames, nf, seg_loss_pm, fec_loss_pm, window, dup_pm, late_pm, protect_tail, 0, 0);
 }
 
 int main(int argc, char** argv)
@@ -250,6 +270,16 @@ int main(int argc, char** argv)
     for (int i = 0; i < 400; ++i)
         fr[i] = (frame_t){(4u + (uint32_t)(i % 9)) * SIM_VIDEO_SIZE - 13u * (uint32_t)i % 97u, 0, 100, 60};
     scenario("late_parities", 4, fr, 400, 120, 50, 10, 10, 300, 1);
+    /* streams with the heartbeat's eviction between arrivals (a receiver
+     * session): segments arriving seconds late find their flex evicted
+     * (fec_ts + 3000 <= max_ts) or still open; parities lost wholesale leave
+     * cached segments to the 6 s cache rule */
+    for (int i = 0; i < 400; ++i)
+        fr[i] = (frame_t){(3u + (uint32_t)(i % 11)) * SIM_VIDEO_SIZE - 7u * (uint32_t)i % 89u,
+                          (uint8_t)(i % 40 == 0), 98, (uint8_t)(i % 7 == 0 ? 5 : 80)};
+    scenario_x("evict_late_segments", 5, fr, 400, 100, 60, 12, 10, 20, 1, 60, 40);
+    scenario_x("evict_lost_parities", 6, fr, 400, 80, 550, 8, 10, 0, 1, 20, 97);
+    scenario_x("no_evict_late_segments", 5, fr, 400, 100, 60, 12, 10, 20, 1, 60, 0);
     fprintf(js, "\n]}\n");
     fclose(js);
     return 0;

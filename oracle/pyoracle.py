@@ -143,6 +143,8 @@ class Oracle:
         L.oracle_sender_init.argtypes = [P]
         L.oracle_sender_plan.argtypes = [P, P, C.c_uint32, C.c_uint32, P, C.c_uint32, P, P, C.c_uint32, P]
         L.oracle_rx_recover.argtypes = [C.c_uint32, P, P, C.c_uint32, C.c_uint32, P, P, P, C.c_uint32, P, P]
+        L.oracle_rx_recover_ev.argtypes = [C.c_uint32, P, P, C.c_uint32, C.c_uint32, P, P, P, C.c_uint32, P, P,
+                                           C.c_uint32]
         L.oracle_segment_size.restype = C.c_size_t
         L.oracle_fec_size.restype = C.c_size_t
         self.video_size = L.oracle_sim_video_size()
@@ -271,14 +273,16 @@ class Oracle:
         return segs[:ns.value], groups[:ng.value]
 
     # -- receiver ingestion ------------------------------------------------------
-    def rx_recover(self, recs, payload, capacity, max_ts=0, max_out=1 << 16):
+    def rx_recover(self, recs, payload, capacity, max_ts=0, max_out=1 << 16, evict_every=0):
+        """evict_every > 0: sim_fec_evict after every evict_every arrivals."""
         n, stride = payload.shape
         out = np.zeros(max_out, RX_SEG)
         outp = np.zeros((max_out, stride), np.uint8)
         mts, no, dropped = C.c_uint32(max_ts), C.c_uint32(), C.c_uint32()
-        rc = self.lib.oracle_rx_recover(n, _np_ptr(np.ascontiguousarray(recs)), _np_ptr(np.ascontiguousarray(payload)),
-                                        stride, capacity, C.byref(mts), _np_ptr(out), _np_ptr(outp), max_out,
-                                        C.byref(no), C.byref(dropped))
+        rc = self.lib.oracle_rx_recover_ev(n, _np_ptr(np.ascontiguousarray(recs)),
+                                           _np_ptr(np.ascontiguousarray(payload)), stride, capacity, C.byref(mts),
+                                           _np_ptr(out), _np_ptr(outp), max_out, C.byref(no), C.byref(dropped),
+                                           evict_every)
         if rc != 0:
             raise ValueError("rx: output too small")
         return out[:no.value], outp[:no.value], mts.value, dropped.value

@@ -1048,6 +1048,7 @@ typedef struct {
     uint16_t fec_id;
     uint8_t row, col;
     uint32_t base_id, count;
+    uint32_t fec_ts;  /* flex->fec_ts: send_ts of the parity that created it (sim_fec.c:157) */
     omap segs; /* packet_id -> segment pool index */
     omap fecs; /* index -> parity record index */
     int live;
@@ -1199,6 +1200,7 @@ static void rx_put_fec(orx* R, int32_t rec)
         x->row = f->row;
         x->col = f->col;
         x->count = f->count;
+        x->fec_ts = f->send_ts;
         x->live = 1;
         om_init(&x->segs, x->count + 8);
         om_init(&x->fecs, 64);
@@ -1219,9 +1221,56 @@ static void rx_put_fec(orx* R, int32_t rec)
         rx_add_recover(R, &out);
 }
 
+static int cmp_u32(const void* a, const void* b)
+{
+    const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+/* sim_fec_evict (sim_fec.c:209-241) past its 300 ms wall-clock gate: flexes in
+ * fec_id order (the u16 skiplist) while stale (fec_ts + 3000 <= max_ts) or
+ * full, then cached segments in packet_id order while older than 6 s */
+static void rx_evict(orx* R)
+{
+    uint32_t* keys = (uint32_t*)malloc(((size_t)R->flex_of.n + R->cache.n + 1) * sizeof(uint32_t));
+    uint32_t nk = 0;
+    for (uint32_t h = 0; h < R->flex_of.cap; ++h)
+        if (R->flex_of.val[h] != -1)
+            keys[nk++] = R->flex_of.key[h];
+    qsort(keys, nk, sizeof(uint32_t), cmp_u32);
+    for (uint32_t i = 0; i < nk; ++i) {
+        const int32_t fi = om_get(&R->flex_of, keys[i]);
+        const oflex* x = &R->flex[fi];
+        if (!(x->fec_ts + 3000u <= R->max_ts || x->segs.n >= x->count))
+            break;
+        rx_remove_flex(R, (uint32_t)fi);
+    }
+    nk = 0;
+    for (uint32_t h = 0; h < R->cache.cap; ++h)
+        if (R->cache.val[h] != -1)
+            keys[nk++] = R->cache.key[h];
+    qsort(keys, nk, sizeof(uint32_t), cmp_u32);
+    for (uint32_t i = 0; i < nk; ++i) {
+        const int32_t pi = om_get(&R->cache, keys[i]);
+        if (!(R->pool[pi].timestamp + 6000u < R->max_ts))
+            break;
+        om_del(&R->cache, keys[i]);
+    }
+    free(keys);
+}
+
 int oracle_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payload, uint32_t stride,
                       uint32_t capacity, uint32_t* max_ts, rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out,
                       uint32_t* n_out, uint32_t* dropped)
+{
+    return oracle_rx_recover_ev(n, recs, payload, stride, capacity, max_ts, out, out_payload, max_out, n_out, dropped, 0);
+}
+
+/* As oracle_rx_recover, with sim_fec_evict after every evict_every arrivals
+ * (0: never), as the session heartbeat runs it between datagrams. */
+int oracle_rx_recover_ev(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payload, uint32_t stride,
+                         uint32_t capacity, uint32_t* max_ts, rfec_rx_seg* out, uint8_t* out_payload,
+                         uint32_t max_out, uint32_t* n_out, uint32_t* dropped, uint32_t evict_every)
 {
     orx R;
     memset(&R, 0, sizeof(R));
@@ -1291,6 +1340,8 @@ int oracle_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payl
             no++;
             rx_put_segment(&R, &rs);
         }
+        if (evict_every && a % evict_every == evict_every - 1)
+            rx_evict(&R);
     }
     *max_ts = R.max_ts;
     *n_out = no;

@@ -91,6 +91,10 @@ int oracle_sender_plan(rfec_sender_state* st, const rfec_frame* frames, uint32_t
 int oracle_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payload, uint32_t stride,
                       uint32_t capacity, uint32_t* max_ts, rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out,
                       uint32_t* n_out, uint32_t* dropped);
+/* the same with sim_fec_evict (sim_fec.c:209-241) after every evict_every arrivals (0: never) */
+int oracle_rx_recover_ev(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payload, uint32_t stride,
+                         uint32_t capacity, uint32_t* max_ts, rfec_rx_seg* out, uint8_t* out_payload,
+                         uint32_t max_out, uint32_t* n_out, uint32_t* dropped, uint32_t evict_every);
 
 int oracle_sim_video_size(void);
 size_t oracle_segment_size(void);

@@ -215,15 +215,17 @@ def test_sender_plan_oracle(oracle1000):
     sc.check_plan(oracle1000.sender_plan, oracle1000.sender_init)
 
 
-@pytest.mark.parametrize("name", ["k10_loss10", "k10_loss25_dup", "mixed_loss15", "late_parities"])
+@pytest.mark.parametrize("name", ["k10_loss10", "k10_loss25_dup", "mixed_loss15", "late_parities",
+                                  "evict_late_segments", "evict_lost_parities", "no_evict_late_segments"])
 def test_rx_oracle(oracle1000, name):
     """The oracle's event-by-event receiver recovers exactly what the reference
-    receiver did, in the same delivery order (tests/golden/rx.json)."""
+    receiver did, in the same delivery order (tests/golden/rx.json), with the
+    heartbeat's sim_fec_evict between arrivals where the scenario has it."""
     import rx_cases as rc
 
     scn = {s["name"]: s for s in po.rx_fixture()["scenarios"]}[name]
     recs, pay, _, _ = po.rx_stream(oracle1000, scn)
-    out, outp, max_ts, dropped = oracle1000.rx_recover(recs, pay, 1000)
+    out, outp, max_ts, dropped = oracle1000.rx_recover(recs, pay, 1000, evict_every=scn["evict_every"])
     assert rc.got_rows(out, outp) == rc.expected(scn)
     assert max_ts == scn["max_ts"]
     if name == "late_parities":
