@@ -508,6 +508,49 @@ int rfec_host_recv_datagrams(uint32_t n, uint32_t dstride, const uint8_t* dgram,
 void* rfec_pinned_alloc(size_t bytes);
 void rfec_pinned_free(void* p);
 
+/* ------------------------------------------------------------------------ */
+/* Receiver session: the receiver-side FEC state of one sim_session          */
+/* (sim_receiver_fec_t, sim_fec.c) kept from one batch of datagrams to the   */
+/* next -- open flex receivers, the segment cache, max_ts, first-arrival     */
+/* dedupe -- with every cached segment's and registered parity's payload row */
+/* held in HBM, so a group whose datagrams straddle batches recovers exactly */
+/* as in one stream.  rfec_rx_session_evict is sim_fec_evict (sim_fec.c:    */
+/* 209-241) for the caller's heartbeat (sim_receiver_timer, sim_receiver.c: */
+/* 880, every >= 300 ms): stale or full flexes in fec_id order, cached      */
+/* segments older than 6 s in packet_id order; then the held rows are       */
+/* compacted.  Pushing a stream in any batches, with evictions between      */
+/* batches, delivers what rfec_rx_recover delivers on the whole stream with */
+/* the same evictions.  One session per calling thread at a time.           */
+/* ------------------------------------------------------------------------ */
+typedef struct rfec_rx_session rfec_rx_session;
+
+typedef struct {
+    uint32_t max_ts;          /* sim_receiver_fec_t.max_ts */
+    uint32_t open_flexes;     /* skiplist_size(f->flexes) */
+    uint32_t cached_segments; /* skiplist_size(f->segs_cache) */
+    uint32_t records_held;    /* parsed records kept for open state */
+    uint32_t rows_held;       /* HBM payload rows allocated */
+    uint32_t reserved;
+} rfec_rx_session_info;
+
+/* NULL on bad arguments (stride % 16, capacity > stride) or no memory. */
+rfec_rx_session* rfec_rx_session_create(uint32_t stride, uint32_t capacity);
+void rfec_rx_session_destroy(rfec_rx_session* s);
+/* recs / payload: DEVICE (rfec_wire_parse output, rows of the session's
+ * stride), n records in arrival order; out / out_payload: HOST, the segments
+ * recovered by this batch, ascending packet_id.  As rfec_rx_recover. */
+int rfec_rx_session_push(rfec_rx_session* s, uint32_t n, const rfec_wire_rec* recs, const uint8_t* payload,
+                         rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out,
+                         rfec_rx_report* report, void* stream);
+/* Received datagram slots in HOST memory (rfec_udp_recv_batch's output):
+ * H2D, rfec_wire_parse, rfec_rx_session_push.  recs_out (HOST, may be NULL)
+ * receives the n parse records. */
+int rfec_rx_session_push_datagrams(rfec_rx_session* s, uint32_t n, uint32_t dstride, const uint8_t* dgram,
+                                   const uint16_t* dlen, rfec_wire_rec* recs_out, rfec_rx_seg* out,
+                                   uint8_t* out_payload, uint32_t max_out, uint32_t* n_out, rfec_rx_report* report);
+int rfec_rx_session_evict(rfec_rx_session* s, void* stream);
+int rfec_rx_session_get_info(const rfec_rx_session* s, rfec_rx_session_info* info);
+
 /* Kernel-selection knobs, for benchmarking and A/B tests (0 = defaults:
  * specialised row kernels where the plan allows, non-temporal streaming). */
 #define RFEC_TUNE_GENERIC 1u       /* always use the generic plan-driven kernel */

@@ -1474,6 +1474,7 @@ typedef struct {
     uint64_t have[2];      /* members in the flex (arrived or recovered) */
     uint64_t arrived[2];   /* members that arrived: the device peel starts from these */
     uint64_t ppm;          /* registered parities, by plan line */
+    uint32_t fec_ts;       /* flex->fec_ts = send_ts of the parity that created it (sim_fec.c:157) */
     int ref_ok;            /* col >= 2 && row >= 1 && count >= 1 (flex_fec_receiver.c:214, 250) */
 } rx_inst;
 
@@ -1497,8 +1498,10 @@ typedef struct {
     uint32_t nline, linecap;
     rx_event* pend;
     uint32_t npend, pendcap;
-    rx_event* out;
+    rx_event* out;         /* delivered by this call */
     uint32_t nout, outcap;
+    rfec_hdr* rh;          /* headers of delivered (recovered) segments the cache refers to */
+    uint32_t nrh, rhcap;
     int oom;
 } rx_sim;
 
@@ -1620,7 +1623,7 @@ static void rx_remove(rx_sim* X, uint32_t ii) /* sim_fec_evict_segment + flex re
     hm_del(&X->flex_of, g->fec_id);
 }
 
-/* sim_fec_put_segment (sim_fec.c:171-207); cache values: record + 1, or 0x80000000 | delivered index */
+/* sim_fec_put_segment (sim_fec.c:171-207); cache values: record + 1, or 0x80000000 | index into X->rh */
 static void rx_put_segment(rx_sim* X, const rfec_hdr* h, uint16_t fec_id, uint32_t cval, int32_t src)
 {
     if (h->seq == 0 || hm_get(&X->cache, h->seq))
@@ -1688,6 +1691,7 @@ static void rx_put_fec(rx_sim* X, uint32_t a)
         g->count = f->count;
         g->row = f->row;
         g->col = f->col;
+        g->fec_ts = f->send_ts;
         g->ref_ok = g->col >= 2 && g->row >= 1 && g->count >= 1;
         g->shape = g->ref_ok ? rx_shape_of(X, g->count, g->row, g->col) : UINT32_MAX;
         if (g->shape != UINT32_MAX) {
@@ -1719,7 +1723,7 @@ static void rx_put_fec(rx_sim* X, uint32_t a)
             if (!c)
                 continue;
             if (c & 0x80000000u) {
-                rx_on_segment(X, fi - 1, &X->out[c & 0x7FFFFFFFu].hdr, -1, 0);
+                rx_on_segment(X, fi - 1, &X->rh[c & 0x7FFFFFFFu], -1, 0);
             } else {
                 const rfec_hdr h = rec_hdr(&X->R[c - 1]);
                 rx_on_segment(X, fi - 1, &h, (int32_t)(c - 1), 0);
@@ -1754,12 +1758,14 @@ static void rx_drain(rx_sim* X)
         if (hm_get(&X->seen, e.hdr.seq))
             continue;
         RX_GROW(X->out, X->nout, X->outcap, 1, rx_event);
+        RX_GROW(X->rh, X->nrh, X->rhcap, 1, rfec_hdr);
         if (X->oom || hm_put(&X->seen, e.hdr.seq, 1)) {
             X->oom = 1;
             return;
         }
-        X->out[X->nout] = e;
-        const uint32_t idx = X->nout++;
+        X->out[X->nout++] = e;
+        X->rh[X->nrh] = e.hdr;
+        const uint32_t idx = X->nrh++;
         rx_put_segment(X, &e.hdr, (uint16_t)X->G[e.inst].fec_id, 0x80000000u | idx, -1);
     }
 }
@@ -1777,6 +1783,63 @@ static void rx_sim_free(rx_sim* X)
     free(X->line_par);
     free(X->pend);
     free(X->out);
+    free(X->rh);
+}
+
+static int cmp_u32(const void* a, const void* b)
+{
+    const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+/* keys of a map, ascending (the skiplists' iteration order); NULL on OOM */
+static uint32_t* hm_sorted_keys(const hmap* m, uint32_t* n)
+{
+    uint32_t* k = (uint32_t*)malloc(((size_t)m->n + 1) * sizeof(uint32_t));
+    *n = 0;
+    if (!k)
+        return NULL;
+    for (uint32_t i = 0; i <= m->mask; ++i)
+        if (m->v[i])
+            k[(*n)++] = m->k[i];
+    qsort(k, *n, sizeof(uint32_t), cmp_u32);
+    return k;
+}
+
+/* sim_fec_evict (sim_fec.c:209-241) past its 300 ms wall-clock gate: flexes in
+ * fec_id order while stale (fec_ts + 3000 <= max_ts) or full, removed with
+ * their members' cache entries; then cached segments in packet_id order while
+ * older than 6 s (timestamp + 6000 < max_ts).  Both walks stop at the first
+ * entry that stays, as the skiplist walks do. */
+static void rx_evict(rx_sim* X)
+{
+    uint32_t n = 0;
+    uint32_t* k = hm_sorted_keys(&X->flex_of, &n);
+    if (!k) {
+        X->oom = 1;
+        return;
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t fi = hm_get(&X->flex_of, k[i]) - 1;
+        const rx_inst* g = &X->G[fi];
+        if (!(g->fec_ts + 3000u <= X->max_ts || g->nsegs >= g->count))
+            break;
+        rx_remove(X, fi);
+    }
+    free(k);
+    k = hm_sorted_keys(&X->cache, &n);
+    if (!k) {
+        X->oom = 1;
+        return;
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t c = hm_get(&X->cache, k[i]);
+        const uint32_t ts = (c & 0x80000000u) ? X->rh[c & 0x7FFFFFFFu].ts : X->R[c - 1].hdr.ts;
+        if (!(ts + 6000u < X->max_ts))
+            break;
+        hm_del(&X->cache, k[i]);
+    }
+    free(k);
 }
 
 static int cmp_event(const void* a, const void* b)
@@ -1828,6 +1891,216 @@ static int rx_reserve(size_t host_bytes, size_t dev_bytes, size_t keep)
 
 #define RX_ALIGN(x) (((x) + 255) & ~(size_t)255)
 
+static int rx_tables_init(rx_sim* X, uint32_t n)
+{
+    return hm_init(&X->seen, n) || hm_init(&X->cache, n) || hm_init(&X->flex_of, 1024) || hm_init(&X->shape_of, 64);
+}
+
+/* The control plane, in arrival order, over records [a0, a0 + n) of X->R:
+ * sim_receiver_put / sim_receiver_put_fec and the recovery cascade. */
+static void rx_run(rx_sim* X, uint32_t a0, uint32_t n)
+{
+    for (uint32_t a = a0; a < a0 + n && !X->oom; ++a) {
+        const rfec_wire_rec* r = &X->R[a];
+        if (r->status != RFEC_WIRE_OK)
+            continue;
+        if (r->mid == RFEC_WIRE_SEG) { /* sim_receiver_put (sim_receiver.c:811-827) */
+            if (hm_get(&X->seen, r->hdr.seq))
+                continue;
+            if (hm_put(&X->seen, r->hdr.seq, 1)) {
+                X->oom = 1;
+                break;
+            }
+            if (r->fec_id == 0)
+                continue;
+            const rfec_hdr h = rec_hdr(r);
+            rx_put_segment(X, &h, r->fec_id, a + 1, (int32_t)a);
+        } else if (r->mid == RFEC_WIRE_FEC) {
+            rx_put_fec(X, a);
+        }
+        rx_drain(X);
+    }
+}
+
+/* The device side of one call: the groups that delivered something in this
+ * call, rebuilt from their arrived members and registered parities (rows of
+ * `rows`, DEVICE, indexed by record), peeled by rfec_recover_batch, and the
+ * delivered rows copied out.  The pinned tables go after the first `hoff`
+ * bytes of t_rx.h, which survive a grow (X->R may live there). */
+static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t capacity, size_t hoff,
+                     rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out, rfec_rx_report* rep,
+                     hipStream_t sm)
+{
+    hipError_t e = hipSuccess;
+    int rc = RFEC_OK, ke = 0;
+    const double th = now_us();
+    *n_out = 0;
+    if (X->nout)
+        qsort(X->out, X->nout, sizeof(rx_event), cmp_event);
+    if (X->nout == 0) { /* nothing recovered: no device work */
+        rep->host_us += now_us() - th;
+        return RFEC_OK;
+    }
+    /* group tables, shape-major, for the groups that deliver something */
+    for (uint32_t s = 0; s < X->ns; ++s)
+        X->S[s].n_groups = 0;
+    for (uint32_t gi = 0; gi < X->ng; ++gi)
+        X->G[gi].gslot = UINT32_MAX;
+    for (uint32_t q = 0; q < X->nout; ++q) {
+        rx_inst* g = &X->G[X->out[q].inst];
+        if (g->gslot == UINT32_MAX)
+            g->gslot = X->S[g->shape].n_groups++;
+    }
+    uint32_t nrows = 0, prows = 0, ngs = 0;
+    for (uint32_t s = 0; s < X->ns; ++s) {
+        rx_shape* sh = &X->S[s];
+        sh->row0 = nrows;
+        sh->prow0 = prows;
+        sh->group0 = ngs;
+        nrows += sh->n_groups * sh->count;
+        prows += sh->n_groups * sh->n_lines;
+        ngs += sh->n_groups;
+    }
+    const size_t o_smap = 0, o_pmap = RX_ALIGN((size_t)nrows * 4), o_hdr = RX_ALIGN(o_pmap + (size_t)prows * 4);
+    const size_t o_meta = RX_ALIGN(o_hdr + (size_t)nrows * sizeof(rfec_hdr));
+    const size_t o_fs = RX_ALIGN(o_meta + (size_t)prows * sizeof(rfec_hdr));
+    const size_t o_pres = RX_ALIGN(o_fs + (size_t)prows * 2), o_pp = RX_ALIGN(o_pres + (size_t)ngs * 16);
+    const size_t o_omap = RX_ALIGN(o_pp + (size_t)ngs * 8), o_in_end = RX_ALIGN(o_omap + (size_t)X->nout * 4);
+    const size_t o_rec = o_in_end, host_bytes = RX_ALIGN(o_rec + (size_t)ngs * 16);
+    size_t ws_bytes = 0;
+    for (uint32_t s = 0; s < X->ns; ++s)
+        ws_bytes += RX_ALIGN(rfec_recover_workspace_size(&X->S[s].plan, X->S[s].n_groups));
+    const size_t d_shards = o_in_end, d_par = RX_ALIGN(d_shards + (size_t)nrows * stride);
+    const size_t d_ws = RX_ALIGN(d_par + (size_t)prows * stride), d_rec = RX_ALIGN(d_ws + ws_bytes);
+    const size_t d_out = RX_ALIGN(d_rec + (size_t)ngs * 16), dev_bytes = RX_ALIGN(d_out + (size_t)X->nout * stride);
+    const int r_in_stage = (const uint8_t*)X->R == t_rx.h;
+    if ((rc = rx_reserve(hoff + host_bytes, dev_bytes, hoff)))
+        return rc;
+    if (r_in_stage)
+        X->R = (const rfec_wire_rec*)t_rx.h;
+    uint8_t* H = t_rx.h + hoff;
+    memset(H, 0, o_in_end);
+    int32_t* smap = (int32_t*)(H + o_smap);
+    int32_t* pmap = (int32_t*)(H + o_pmap);
+    rfec_hdr* hh = (rfec_hdr*)(H + o_hdr);
+    rfec_hdr* mh = (rfec_hdr*)(H + o_meta);
+    uint16_t* fsz = (uint16_t*)(H + o_fs);
+    uint64_t* pres = (uint64_t*)(H + o_pres);
+    uint64_t* ppm = (uint64_t*)(H + o_pp);
+    int32_t* omap = (int32_t*)(H + o_omap);
+    for (uint32_t gi = 0; gi < X->ng; ++gi) {
+        const rx_inst* g = &X->G[gi];
+        if (g->shape == UINT32_MAX || g->gslot == UINT32_MAX)
+            continue;
+        const rx_shape* sh = &X->S[g->shape];
+        const uint32_t gg = sh->group0 + g->gslot, r0 = sh->row0 + g->gslot * sh->count;
+        const uint32_t p0 = sh->prow0 + g->gslot * sh->n_lines;
+        pres[2 * gg] = g->arrived[0];
+        pres[2 * gg + 1] = g->arrived[1];
+        ppm[gg] = g->ppm;
+        for (uint32_t i = 0; i < sh->count; ++i) {
+            const int32_t src = X->slot_src[g->slot0 + i];
+            smap[r0 + i] = src;
+            if (src >= 0)
+                hh[r0 + i] = X->slot_hdr[g->slot0 + i];
+        }
+        for (uint32_t l = 0; l < sh->n_lines; ++l) {
+            const int32_t src = X->line_par[g->line0 + l];
+            pmap[p0 + l] = src;
+            if (src >= 0) {
+                mh[p0 + l] = X->R[src].hdr;
+                fsz[p0 + l] = X->R[src].data_size;
+            }
+        }
+    }
+    /* output rows: the recovering group's slot */
+    uint32_t nok = 0;
+    for (uint32_t q = 0; q < X->nout; ++q) {
+        const rx_event* ev = &X->out[q];
+        const rx_inst* g = &X->G[ev->inst];
+        const rx_shape* sh = &X->S[g->shape];
+        const uint32_t t = ev->hdr.seq - g->base;
+        omap[q] = t < g->count ? (int32_t)(sh->row0 + g->gslot * sh->count + t) : -1;
+    }
+    rep->host_us += now_us() - th;
+    rep->n_groups = ngs;
+    for (uint32_t s = 0; s < X->ns; ++s)
+        rep->n_shapes += X->S[s].n_groups != 0;
+    /* the device: rows in place, one peel per shape, the delivered rows compacted */
+    uint8_t* D = t_rx.d;
+    double tt = now_us();
+    if ((e = hipMemcpyAsync(D, H, o_in_end, hipMemcpyHostToDevice, sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx: H2D", e);
+    ke = rfec_launch_gather_rows(D + d_shards, rows, (const int32_t*)(D + o_smap), nrows, stride, sm);
+    if (!ke)
+        ke = rfec_launch_gather_rows(D + d_par, rows, (const int32_t*)(D + o_pmap), prows, stride, sm);
+    size_t wso = 0;
+    for (uint32_t s = 0; s < X->ns && !ke; ++s) {
+        const rx_shape* sh = &X->S[s];
+        if (!sh->n_groups)
+            continue;
+        rfec_kmask M;
+        make_masks(&sh->plan, &M);
+        ke = rfec_launch_recover(&M, sh->n_groups, stride, capacity, D + d_shards + (size_t)sh->row0 * stride,
+                                 (rfec_hdr*)(D + o_hdr) + sh->row0, (const uint64_t*)(D + o_pres) + 2 * sh->group0,
+                                 D + d_par + (size_t)sh->prow0 * stride, (const rfec_hdr*)(D + o_meta) + sh->prow0,
+                                 (const uint16_t*)(D + o_fs) + sh->prow0, (const uint64_t*)(D + o_pp) + sh->group0,
+                                 (uint64_t*)(D + d_rec) + 2 * sh->group0, D + d_ws + wso, sm, g_tuning);
+        wso += RX_ALIGN(rfec_recover_workspace_size(&sh->plan, sh->n_groups));
+    }
+    if (!ke && X->nout)
+        ke = rfec_launch_gather_rows(D + d_out, D + d_shards, (const int32_t*)(D + o_omap), X->nout, stride, sm);
+    uint64_t* rec = (uint64_t*)(H + o_rec);
+    if (ke || (e = hipMemcpyAsync(rec, D + d_rec, (size_t)ngs * 16, hipMemcpyDeviceToHost, sm)) != hipSuccess ||
+        (e = hipStreamSynchronize(sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx: recover", ke ? ke : e);
+    rep->kernel_us += now_us() - tt;
+    /* the device peel covers every packet the arrival-order pass delivered (same lines, a superset of
+       the members at each firing); anything else is reported, not delivered */
+    for (uint32_t q = 0; q < X->nout; ++q) {
+        const rx_event* ev = &X->out[q];
+        const rx_inst* g = &X->G[ev->inst];
+        const uint32_t t = ev->hdr.seq - g->base, gg = X->S[g->shape].group0 + g->gslot;
+        if (t >= g->count || !((rec[2 * gg + (t >> 6)] >> (t & 63)) & 1ull)) {
+            X->unmodelled++;
+            omap[q] = -1;
+            continue;
+        }
+        nok++;
+    }
+    if (nok > max_out) {
+        *n_out = nok;
+        return set_err(RFEC_EINVAL, "rx: output too small", 0);
+    }
+    tt = now_us();
+    uint32_t o = 0;
+    if (nok == X->nout) { /* the usual case: one copy */
+        if (nok)
+            e = hipMemcpyAsync(out_payload, D + d_out, (size_t)nok * stride, hipMemcpyDeviceToHost, sm);
+        o = nok;
+    }
+    for (uint32_t q = 0; q < X->nout && nok != X->nout && e == hipSuccess; ++q) {
+        if (omap[q] < 0)
+            continue;
+        e = hipMemcpyAsync(out_payload + (size_t)o * stride, D + d_out + (size_t)q * stride, stride,
+                           hipMemcpyDeviceToHost, sm);
+        X->out[o++] = X->out[q];
+    }
+    for (uint32_t q = 0; q < o; ++q) {
+        out[q].hdr = X->out[q].hdr;
+        out[q].fec_id = (uint16_t)X->G[X->out[q].inst].fec_id;
+        out[q].reserved = 0;
+    }
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(sm);
+    if (e != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx: output D2H", e);
+    rep->d2h_us += now_us() - tt;
+    *n_out = o;
+    rep->n_recovered = o;
+    return RFEC_OK;
+}
+
 int rfec_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payload, uint32_t stride,
                     uint32_t capacity, uint32_t* max_ts, rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out,
                     uint32_t* n_out, rfec_rx_report* rep, void* stream)
@@ -1843,7 +2116,7 @@ int rfec_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payloa
         return RFEC_OK;
     hipStream_t sm = (hipStream_t)stream;
     hipError_t e;
-    int rc = RFEC_OK, ke = 0;
+    int rc = RFEC_OK;
     /* 1. the records to the host (headers only: 64 B each) */
     const size_t rec_bytes = RX_ALIGN((size_t)n * sizeof(rfec_wire_rec));
     if ((rc = rx_reserve(rec_bytes, 0, 0)))
@@ -1861,210 +2134,20 @@ int rfec_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payloa
     X.R = (const rfec_wire_rec*)t_rx.h;
     X.capacity = capacity;
     X.max_ts = *max_ts;
-    if (hm_init(&X.seen, n) || hm_init(&X.cache, n) || hm_init(&X.flex_of, 1024) || hm_init(&X.shape_of, 64)) {
+    if (rx_tables_init(&X, n)) {
         rx_sim_free(&X);
         return set_err(RFEC_ENOMEM, "rx: host tables", 0);
     }
-    for (uint32_t a = 0; a < n && !X.oom; ++a) {
-        const rfec_wire_rec* r = &X.R[a];
-        if (r->status != RFEC_WIRE_OK)
-            continue;
-        if (r->mid == RFEC_WIRE_SEG) { /* sim_receiver_put (sim_receiver.c:811-827) */
-            if (hm_get(&X.seen, r->hdr.seq))
-                continue;
-            if (hm_put(&X.seen, r->hdr.seq, 1)) {
-                X.oom = 1;
-                break;
-            }
-            if (r->fec_id == 0)
-                continue;
-            const rfec_hdr h = rec_hdr(r);
-            rx_put_segment(&X, &h, r->fec_id, a + 1, (int32_t)a);
-        } else if (r->mid == RFEC_WIRE_FEC) {
-            rx_put_fec(&X, a);
-        }
-        rx_drain(&X);
-    }
+    rx_run(&X, 0, n);
     if (X.oom) {
         rx_sim_free(&X);
         return set_err(RFEC_ENOMEM, "rx: host tables", 0);
     }
-    if (X.nout)
-        qsort(X.out, X.nout, sizeof(rx_event), cmp_event);
     *max_ts = X.max_ts;
     rep->n_fec_dropped = X.dropped;
-    if (X.nout == 0) { /* nothing recovered: no device work */
-        rep->host_us = now_us() - th;
-        goto out;
-    }
-    /* 3. group tables, shape-major, for the groups that deliver something */
-    for (uint32_t s = 0; s < X.ns; ++s)
-        X.S[s].n_groups = 0;
-    for (uint32_t gi = 0; gi < X.ng; ++gi)
-        X.G[gi].gslot = UINT32_MAX;
-    for (uint32_t q = 0; q < X.nout; ++q) {
-        rx_inst* g = &X.G[X.out[q].inst];
-        if (g->gslot == UINT32_MAX)
-            g->gslot = X.S[g->shape].n_groups++;
-    }
-    uint32_t rows = 0, prows = 0, ngs = 0;
-    for (uint32_t s = 0; s < X.ns; ++s) {
-        rx_shape* sh = &X.S[s];
-        sh->row0 = rows;
-        sh->prow0 = prows;
-        sh->group0 = ngs;
-        rows += sh->n_groups * sh->count;
-        prows += sh->n_groups * sh->n_lines;
-        ngs += sh->n_groups;
-    }
-    const size_t o_smap = 0, o_pmap = RX_ALIGN((size_t)rows * 4), o_hdr = RX_ALIGN(o_pmap + (size_t)prows * 4);
-    const size_t o_meta = RX_ALIGN(o_hdr + (size_t)rows * sizeof(rfec_hdr));
-    const size_t o_fs = RX_ALIGN(o_meta + (size_t)prows * sizeof(rfec_hdr));
-    const size_t o_pres = RX_ALIGN(o_fs + (size_t)prows * 2), o_pp = RX_ALIGN(o_pres + (size_t)ngs * 16);
-    const size_t o_omap = RX_ALIGN(o_pp + (size_t)ngs * 8), o_in_end = RX_ALIGN(o_omap + (size_t)X.nout * 4);
-    const size_t o_rec = o_in_end, host_bytes = RX_ALIGN(o_rec + (size_t)ngs * 16);
-    size_t ws_bytes = 0;
-    for (uint32_t s = 0; s < X.ns; ++s)
-        ws_bytes += RX_ALIGN(rfec_recover_workspace_size(&X.S[s].plan, X.S[s].n_groups));
-    const size_t d_shards = o_in_end, d_par = RX_ALIGN(d_shards + (size_t)rows * stride);
-    const size_t d_ws = RX_ALIGN(d_par + (size_t)prows * stride), d_rec = RX_ALIGN(d_ws + ws_bytes);
-    const size_t d_out = RX_ALIGN(d_rec + (size_t)ngs * 16), dev_bytes = RX_ALIGN(d_out + (size_t)X.nout * stride);
-    /* the records stay at the start of the pinned block (kept across a grow): the tables follow them */
-    if ((rc = rx_reserve(rec_bytes + host_bytes, dev_bytes, (size_t)n * sizeof(rfec_wire_rec))))
-        goto out;
-    X.R = (const rfec_wire_rec*)t_rx.h;
-    uint8_t* H = t_rx.h + rec_bytes;
-    memset(H, 0, o_in_end);
-    int32_t* smap = (int32_t*)(H + o_smap);
-    int32_t* pmap = (int32_t*)(H + o_pmap);
-    rfec_hdr* hh = (rfec_hdr*)(H + o_hdr);
-    rfec_hdr* mh = (rfec_hdr*)(H + o_meta);
-    uint16_t* fsz = (uint16_t*)(H + o_fs);
-    uint64_t* pres = (uint64_t*)(H + o_pres);
-    uint64_t* ppm = (uint64_t*)(H + o_pp);
-    int32_t* omap = (int32_t*)(H + o_omap);
-    for (uint32_t gi = 0; gi < X.ng; ++gi) {
-        const rx_inst* g = &X.G[gi];
-        if (g->shape == UINT32_MAX || g->gslot == UINT32_MAX)
-            continue;
-        const rx_shape* sh = &X.S[g->shape];
-        const uint32_t gg = sh->group0 + g->gslot, r0 = sh->row0 + g->gslot * sh->count;
-        const uint32_t p0 = sh->prow0 + g->gslot * sh->n_lines;
-        pres[2 * gg] = g->arrived[0];
-        pres[2 * gg + 1] = g->arrived[1];
-        ppm[gg] = g->ppm;
-        for (uint32_t i = 0; i < sh->count; ++i) {
-            const int32_t src = X.slot_src[g->slot0 + i];
-            smap[r0 + i] = src;
-            if (src >= 0)
-                hh[r0 + i] = X.slot_hdr[g->slot0 + i];
-        }
-        for (uint32_t l = 0; l < sh->n_lines; ++l) {
-            const int32_t src = X.line_par[g->line0 + l];
-            pmap[p0 + l] = src;
-            if (src >= 0) {
-                mh[p0 + l] = X.R[src].hdr;
-                fsz[p0 + l] = X.R[src].data_size;
-            }
-        }
-    }
-    /* output rows: the recovering group's slot */
-    uint32_t nok = 0;
-    for (uint32_t q = 0; q < X.nout; ++q) {
-        const rx_event* ev = &X.out[q];
-        const rx_inst* g = &X.G[ev->inst];
-        const rx_shape* sh = &X.S[g->shape];
-        const uint32_t t = ev->hdr.seq - g->base;
-        omap[q] = t < g->count ? (int32_t)(sh->row0 + g->gslot * sh->count + t) : -1;
-    }
-    rep->host_us = now_us() - th;
-    rep->n_groups = ngs;
-    for (uint32_t s = 0; s < X.ns; ++s)
-        rep->n_shapes += X.S[s].n_groups != 0;
-    /* 4. the device: rows in place, one peel per shape, the delivered rows compacted */
-    {
-        uint8_t* D = t_rx.d;
-        tt = now_us();
-        if ((e = hipMemcpyAsync(D, H, o_in_end, hipMemcpyHostToDevice, sm)) != hipSuccess) {
-            rc = set_err(RFEC_EDEVICE, "rx: H2D", e);
-            goto out;
-        }
-        ke = rfec_launch_gather_rows(D + d_shards, payload, (const int32_t*)(D + o_smap), rows, stride, sm);
-        if (!ke)
-            ke = rfec_launch_gather_rows(D + d_par, payload, (const int32_t*)(D + o_pmap), prows, stride, sm);
-        size_t wso = 0;
-        for (uint32_t s = 0; s < X.ns && !ke; ++s) {
-            const rx_shape* sh = &X.S[s];
-            if (!sh->n_groups)
-                continue;
-            rfec_kmask M;
-            make_masks(&sh->plan, &M);
-            ke = rfec_launch_recover(&M, sh->n_groups, stride, capacity, D + d_shards + (size_t)sh->row0 * stride,
-                                     (rfec_hdr*)(D + o_hdr) + sh->row0, (const uint64_t*)(D + o_pres) + 2 * sh->group0,
-                                     D + d_par + (size_t)sh->prow0 * stride, (const rfec_hdr*)(D + o_meta) + sh->prow0,
-                                     (const uint16_t*)(D + o_fs) + sh->prow0,
-                                     (const uint64_t*)(D + o_pp) + sh->group0,
-                                     (uint64_t*)(D + d_rec) + 2 * sh->group0, D + d_ws + wso, sm, g_tuning);
-            wso += RX_ALIGN(rfec_recover_workspace_size(&sh->plan, sh->n_groups));
-        }
-        if (!ke && X.nout)
-            ke = rfec_launch_gather_rows(D + d_out, D + d_shards, (const int32_t*)(D + o_omap), X.nout, stride, sm);
-        uint64_t* rec = (uint64_t*)(H + o_rec);
-        if (ke || (e = hipMemcpyAsync(rec, D + d_rec, (size_t)ngs * 16, hipMemcpyDeviceToHost, sm)) != hipSuccess ||
-            (e = hipStreamSynchronize(sm)) != hipSuccess) {
-            rc = set_err(RFEC_EDEVICE, "rx: recover", ke ? ke : e);
-            goto out;
-        }
-        rep->kernel_us = now_us() - tt;
-        /* the device peel covers every packet the arrival-order pass delivered (same lines, a superset of
-           the members at each firing); anything else is reported, not delivered */
-        *n_out = 0;
-        for (uint32_t q = 0; q < X.nout; ++q) {
-            const rx_event* ev = &X.out[q];
-            const rx_inst* g = &X.G[ev->inst];
-            const uint32_t t = ev->hdr.seq - g->base, gg = X.S[g->shape].group0 + g->gslot;
-            if (t >= g->count || !((rec[2 * gg + (t >> 6)] >> (t & 63)) & 1ull)) {
-                X.unmodelled++;
-                omap[q] = -1;
-                continue;
-            }
-            nok++;
-        }
-        if (nok > max_out) {
-            *n_out = nok;
-            rc = set_err(RFEC_EINVAL, "rx: output too small", 0);
-            goto out;
-        }
-        tt = now_us();
-        uint32_t o = 0;
-        if (nok == X.nout) { /* the usual case: one copy */
-            if (nok)
-                e = hipMemcpyAsync(out_payload, D + d_out, (size_t)nok * stride, hipMemcpyDeviceToHost, sm);
-            o = nok;
-        }
-        for (uint32_t q = 0; q < X.nout && nok != X.nout && e == hipSuccess; ++q) {
-            if (omap[q] < 0)
-                continue;
-            e = hipMemcpyAsync(out_payload + (size_t)o * stride, D + d_out + (size_t)q * stride, stride,
-                               hipMemcpyDeviceToHost, sm);
-            X.out[o++] = X.out[q];
-        }
-        for (uint32_t q = 0; q < o; ++q) {
-            out[q].hdr = X.out[q].hdr;
-            out[q].fec_id = (uint16_t)X.G[X.out[q].inst].fec_id;
-            out[q].reserved = 0;
-        }
-        if (e == hipSuccess)
-            e = hipStreamSynchronize(sm);
-        if (e != hipSuccess) {
-            rc = set_err(RFEC_EDEVICE, "rx: output D2H", e);
-            goto out;
-        }
-        rep->d2h_us += now_us() - tt;
-        *n_out = o;
-        rep->n_recovered = o;
-    }
-out:
+    rep->host_us += now_us() - th;
+    /* 3. the device: the records stay at the start of the pinned block */
+    rc = rx_device(&X, payload, stride, capacity, rec_bytes, out, out_payload, max_out, n_out, rep, sm);
     rep->n_unmodelled = X.unmodelled;
     rx_sim_free(&X);
     rep->total_us = now_us() - t0;
@@ -2160,4 +2243,350 @@ int rfec_host_recv_datagrams(uint32_t n, uint32_t dstride, const uint8_t* dgram,
     rep->d2h_us += d2h_recs;
     rep->total_us = now_us() - t0;
     return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Receiver session: rx_sim kept across calls, records by id in a host store, */
+/* their payload rows by id in an HBM arena                                   */
+/* ------------------------------------------------------------------------ */
+struct rfec_rx_session {
+    rx_sim X;
+    rfec_wire_rec* store; /* X.R */
+    uint32_t nstore, storecap;
+    uint8_t* arena; /* [arows][stride] */
+    uint32_t arows;
+    uint32_t stride, capacity;
+};
+
+rfec_rx_session* rfec_rx_session_create(uint32_t stride, uint32_t capacity)
+{
+    if (stride == 0 || stride % 16 || capacity > stride) {
+        set_err(RFEC_EINVAL, "rx session: stride must be a multiple of 16 and >= capacity", 0);
+        return NULL;
+    }
+    rfec_rx_session* s = (rfec_rx_session*)calloc(1, sizeof(*s));
+    if (!s || rx_tables_init(&s->X, 1024)) {
+        if (s)
+            rx_sim_free(&s->X);
+        free(s);
+        set_err(RFEC_ENOMEM, "rx session: host tables", 0);
+        return NULL;
+    }
+    s->X.capacity = capacity;
+    s->stride = stride;
+    s->capacity = capacity;
+    return s;
+}
+
+void rfec_rx_session_destroy(rfec_rx_session* s)
+{
+    if (!s)
+        return;
+    rx_sim_free(&s->X);
+    free(s->store);
+    if (s->arena)
+        (void)hipFree(s->arena);
+    free(s);
+}
+
+/* Keeps only what the open state refers to: the flexes still registered (with
+ * their slot / line tables), the records of cached segments and of those
+ * flexes' members and parities (their rows gathered into a fresh arena with
+ * room for `extra` more), the headers of cached recovered segments. */
+static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
+{
+    rx_sim* X = &S->X;
+    int rc = RFEC_OK;
+    hipError_t e;
+    const uint32_t ng_live = X->flex_of.n;
+    rx_inst* NG = (rx_inst*)malloc(((size_t)ng_live + 1) * sizeof(rx_inst));
+    uint32_t nslot = 0, nline = 0;
+    for (uint32_t i = 0; i <= X->flex_of.mask; ++i)
+        if (X->flex_of.v[i]) {
+            const rx_inst* g = &X->G[X->flex_of.v[i] - 1];
+            if (g->shape != UINT32_MAX) {
+                nslot += g->count;
+                nline += X->S[g->shape].n_lines;
+            }
+        }
+    int32_t* nsrc = (int32_t*)malloc(((size_t)nslot + 1) * sizeof(int32_t));
+    rfec_hdr* nhdr = (rfec_hdr*)malloc(((size_t)nslot + 1) * sizeof(rfec_hdr));
+    int32_t* npar = (int32_t*)malloc(((size_t)nline + 1) * sizeof(int32_t));
+    uint32_t* rmap = (uint32_t*)calloc((size_t)S->nstore + 1, sizeof(uint32_t)); /* old record -> new + 1 */
+    uint32_t* hmap_ = (uint32_t*)calloc((size_t)X->nrh + 1, sizeof(uint32_t));  /* old rh -> new + 1 */
+    if (!NG || !nsrc || !nhdr || !npar || !rmap || !hmap_) {
+        rc = set_err(RFEC_ENOMEM, "rx session: compaction", 0);
+        goto done;
+    }
+    /* 1. live flexes, their tables; the records they refer to */
+    uint32_t ng = 0, ns = 0, nl = 0;
+    for (uint32_t i = 0; i <= X->flex_of.mask; ++i) {
+        if (!X->flex_of.v[i])
+            continue;
+        rx_inst g = X->G[X->flex_of.v[i] - 1];
+        if (g.shape != UINT32_MAX) {
+            const uint32_t nlines = X->S[g.shape].n_lines;
+            memcpy(nsrc + ns, X->slot_src + g.slot0, g.count * sizeof(int32_t));
+            memcpy(nhdr + ns, X->slot_hdr + g.slot0, g.count * sizeof(rfec_hdr));
+            memcpy(npar + nl, X->line_par + g.line0, nlines * sizeof(int32_t));
+            for (uint32_t q = 0; q < g.count; ++q)
+                if (nsrc[ns + q] >= 0)
+                    rmap[nsrc[ns + q]] = 1;
+            for (uint32_t q = 0; q < nlines; ++q)
+                if (npar[nl + q] >= 0)
+                    rmap[npar[nl + q]] = 1;
+            g.slot0 = ns;
+            g.line0 = nl;
+            ns += g.count;
+            nl += nlines;
+        }
+        NG[ng] = g;
+        X->flex_of.v[i] = ++ng;
+    }
+    /* 2. cached segments: arrived ones keep their record, recovered ones their header */
+    for (uint32_t i = 0; i <= X->cache.mask; ++i) {
+        const uint32_t c = X->cache.v[i];
+        if (!c)
+            continue;
+        if (c & 0x80000000u)
+            hmap_[c & 0x7FFFFFFFu] = 1;
+        else
+            rmap[c - 1] = 1;
+    }
+    /* 3. new ids, in arrival order */
+    uint32_t nr = 0, nh = 0;
+    for (uint32_t r = 0; r < S->nstore; ++r)
+        if (rmap[r])
+            rmap[r] = ++nr;
+    for (uint32_t h = 0; h < X->nrh; ++h)
+        if (hmap_[h])
+            hmap_[h] = ++nh;
+    for (uint32_t q = 0; q < ns; ++q)
+        if (nsrc[q] >= 0)
+            nsrc[q] = (int32_t)rmap[nsrc[q]] - 1;
+    for (uint32_t q = 0; q < nl; ++q)
+        if (npar[q] >= 0)
+            npar[q] = (int32_t)rmap[npar[q]] - 1;
+    for (uint32_t i = 0; i <= X->cache.mask; ++i) {
+        const uint32_t c = X->cache.v[i];
+        if (c)
+            X->cache.v[i] = (c & 0x80000000u) ? (0x80000000u | (hmap_[c & 0x7FFFFFFFu] - 1)) : rmap[c - 1];
+    }
+    /* 4. records (host) and rows (device) */
+    uint32_t* gmap = (uint32_t*)malloc(((size_t)nr + 1) * sizeof(uint32_t)); /* new -> old */
+    const uint32_t arows = 2 * (nr + extra) > 4096 ? 2 * (nr + extra) : 4096;
+    uint8_t* arena = NULL;
+    if (!gmap) {
+        rc = set_err(RFEC_ENOMEM, "rx session: compaction", 0);
+        goto done;
+    }
+    for (uint32_t r = 0; r < S->nstore; ++r)
+        if (rmap[r]) {
+            gmap[rmap[r] - 1] = r;
+            S->store[rmap[r] - 1] = S->store[r]; /* rmap[r] - 1 <= r: in place, ascending */
+        }
+    S->nstore = nr;
+    X->R = S->store;
+    for (uint32_t h = 0; h < X->nrh; ++h)
+        if (hmap_[h])
+            X->rh[hmap_[h] - 1] = X->rh[h];
+    X->nrh = nh;
+    if ((e = hipMalloc((void**)&arena, (size_t)arows * S->stride)) != hipSuccess) {
+        free(gmap);
+        rc = set_err(RFEC_ENOMEM, "rx session: arena", e);
+        goto done;
+    }
+    if (nr) {
+        int32_t* dmap = NULL;
+        int ke = 0;
+        if ((e = hipMalloc((void**)&dmap, (size_t)nr * sizeof(int32_t))) != hipSuccess ||
+            (e = hipMemcpyAsync(dmap, gmap, (size_t)nr * sizeof(int32_t), hipMemcpyHostToDevice, sm)) != hipSuccess ||
+            (ke = rfec_launch_gather_rows(arena, S->arena, dmap, nr, S->stride, sm)) != 0 ||
+            (e = hipStreamSynchronize(sm)) != hipSuccess) {
+            if (dmap)
+                (void)hipFree(dmap);
+            (void)hipFree(arena);
+            free(gmap);
+            rc = set_err(RFEC_EDEVICE, "rx session: row compaction", ke ? ke : e);
+            goto done;
+        }
+        (void)hipFree(dmap);
+    }
+    free(gmap);
+    if (S->arena)
+        (void)hipFree(S->arena);
+    S->arena = arena;
+    S->arows = arows;
+    /* 5. the group tables */
+    free(X->G);
+    free(X->slot_src);
+    free(X->slot_hdr);
+    free(X->line_par);
+    X->G = NG;
+    X->ng = X->gcap = ng;
+    X->slot_src = nsrc;
+    X->slot_hdr = nhdr;
+    X->nslot = X->slotcap = X->slothcap = ns;
+    X->line_par = npar;
+    X->nline = X->linecap = nl;
+    NG = NULL;
+    nsrc = npar = NULL;
+    nhdr = NULL;
+done:
+    free(NG);
+    free(nsrc);
+    free(nhdr);
+    free(npar);
+    free(rmap);
+    free(hmap_);
+    return rc;
+}
+
+/* records already on the host (t_rx.h[0, n)), payload rows on the device */
+static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const uint8_t* payload, rfec_rx_seg* out,
+                                  uint8_t* out_payload, uint32_t max_out, uint32_t* n_out, rfec_rx_report* rep,
+                                  hipStream_t sm)
+{
+    rx_sim* X = &S->X;
+    hipError_t e;
+    int rc;
+    /* room for n more rows: drop what the open state no longer refers to (and grow) */
+    if (S->nstore + n > S->arows && (rc = rx_compact(S, n, sm)))
+        return rc;
+    if (S->nstore + n > S->storecap) {
+        uint32_t c = S->storecap ? S->storecap : 4096;
+        while (c < S->nstore + n)
+            c *= 2;
+        rfec_wire_rec* p = (rfec_wire_rec*)realloc(S->store, (size_t)c * sizeof(rfec_wire_rec));
+        if (!p)
+            return set_err(RFEC_ENOMEM, "rx session: record store", 0);
+        S->store = p;
+        S->storecap = c;
+    }
+    X->R = S->store;
+    memcpy(S->store + S->nstore, t_rx.h, (size_t)n * sizeof(rfec_wire_rec));
+    double tt = now_us();
+    if ((e = hipMemcpyAsync(S->arena + (size_t)S->nstore * S->stride, payload, (size_t)n * S->stride,
+                            hipMemcpyDeviceToDevice, sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx session: rows", e);
+    rep->kernel_us += now_us() - tt;
+    const uint32_t a0 = S->nstore;
+    S->nstore += n;
+    const double th = now_us();
+    X->nout = 0;
+    X->dropped = 0;
+    X->unmodelled = 0;
+    rx_run(X, a0, n);
+    if (X->oom)
+        return set_err(RFEC_ENOMEM, "rx session: host tables", 0);
+    rep->n_fec_dropped = X->dropped;
+    rep->host_us += now_us() - th;
+    rc = rx_device(X, S->arena, S->stride, S->capacity, 0, out, out_payload, max_out, n_out, rep, sm);
+    rep->n_unmodelled = X->unmodelled;
+    return rc;
+}
+
+int rfec_rx_session_push(rfec_rx_session* S, uint32_t n, const rfec_wire_rec* recs, const uint8_t* payload,
+                         rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out,
+                         rfec_rx_report* rep, void* stream)
+{
+    const double t0 = now_us();
+    if (!S || !n_out || !rep || (n && (!recs || !payload)) || (max_out && (!out || !out_payload)))
+        return set_err(RFEC_EINVAL, "rx session: bad argument", 0);
+    memset(rep, 0, sizeof(*rep));
+    *n_out = 0;
+    if (n == 0)
+        return RFEC_OK;
+    hipStream_t sm = (hipStream_t)stream;
+    hipError_t e;
+    int rc;
+    if ((rc = rx_reserve(RX_ALIGN((size_t)n * sizeof(rfec_wire_rec)), 0, 0)))
+        return rc;
+    double tt = now_us();
+    if ((e = hipMemcpyAsync(t_rx.h, recs, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost, sm)) !=
+            hipSuccess ||
+        (e = hipStreamSynchronize(sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx session: records D2H", e);
+    rep->d2h_us += now_us() - tt;
+    rc = rx_session_push_staged(S, n, payload, out, out_payload, max_out, n_out, rep, sm);
+    rep->total_us = now_us() - t0;
+    return rc;
+}
+
+int rfec_rx_session_push_datagrams(rfec_rx_session* S, uint32_t n, uint32_t dstride, const uint8_t* dgram,
+                                   const uint16_t* dlen, rfec_wire_rec* recs_out, rfec_rx_seg* out,
+                                   uint8_t* out_payload, uint32_t max_out, uint32_t* n_out, rfec_rx_report* rep)
+{
+    const double t0 = now_us();
+    if (!S || !n_out || !rep || (n && (!dgram || !dlen)) || (max_out && (!out || !out_payload)))
+        return set_err(RFEC_EINVAL, "rx session: bad argument", 0);
+    memset(rep, 0, sizeof(*rep));
+    *n_out = 0;
+    if (n == 0)
+        return RFEC_OK;
+    if (dstride < 64 || dstride > RFEC_WIRE_MAX_DSTRIDE || dstride % 16)
+        return set_err(RFEC_EINVAL, "rx session: dstride must be a multiple of 16 in [64, 2048]", 0);
+    hipError_t e;
+    if (!t_rv.sm && (e = hipStreamCreateWithFlags(&t_rv.sm, hipStreamNonBlocking)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "recv: stream", e);
+    const uint32_t stride = S->stride;
+    const size_t o_dl = RX_ALIGN((size_t)n * dstride), o_rec = RX_ALIGN(o_dl + (size_t)n * 2);
+    const size_t o_pay = RX_ALIGN(o_rec + (size_t)n * sizeof(rfec_wire_rec));
+    const size_t need = RX_ALIGN(o_pay + (size_t)n * stride);
+    if (t_rv.db < need) {
+        if (t_rv.d)
+            (void)hipFree(t_rv.d);
+        t_rv.d = NULL;
+        t_rv.db = 0;
+        const size_t b = need + need / 4;
+        if ((e = hipMalloc((void**)&t_rv.d, b)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "recv: device staging", e);
+        t_rv.db = b;
+    }
+    uint8_t* D = t_rv.d;
+    int rc;
+    if ((rc = rx_reserve(RX_ALIGN((size_t)n * sizeof(rfec_wire_rec)), 0, 0)))
+        return rc;
+    double tt = now_us();
+    if ((e = hipMemcpyAsync(D, dgram, (size_t)n * dstride, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess ||
+        (e = hipMemcpyAsync(D + o_dl, dlen, (size_t)n * 2, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "recv: datagrams H2D", e);
+    const double h2d_issue = now_us() - tt;
+    int ke = rfec_launch_wire_parse(n, dstride, D, (const uint16_t*)(D + o_dl), stride, S->capacity,
+                                    (rfec_wire_rec*)(D + o_rec), D + o_pay, t_rv.sm);
+    if (ke || (e = hipMemcpyAsync(t_rx.h, D + o_rec, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost,
+                                  t_rv.sm)) != hipSuccess ||
+        (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "recv: parse", ke ? ke : e);
+    const double staged = now_us() - tt;
+    if (recs_out)
+        memcpy(recs_out, t_rx.h, (size_t)n * sizeof(rfec_wire_rec));
+    rc = rx_session_push_staged(S, n, D + o_pay, out, out_payload, max_out, n_out, rep, t_rv.sm);
+    rep->h2d_us += h2d_issue;
+    rep->kernel_us += staged - h2d_issue; /* the H2D completes inside this interval too */
+    rep->total_us = now_us() - t0;
+    return rc;
+}
+
+int rfec_rx_session_evict(rfec_rx_session* S, void* stream)
+{
+    if (!S)
+        return set_err(RFEC_EINVAL, "rx session: NULL", 0);
+    rx_evict(&S->X);
+    if (S->X.oom)
+        return set_err(RFEC_ENOMEM, "rx session: evict", 0);
+    return rx_compact(S, 0, (hipStream_t)stream);
+}
+
+int rfec_rx_session_get_info(const rfec_rx_session* S, rfec_rx_session_info* info)
+{
+    if (!S || !info)
+        return set_err(RFEC_EINVAL, "rx session: NULL", 0);
+    memset(info, 0, sizeof(*info));
+    info->max_ts = S->X.max_ts;
+    info->open_flexes = S->X.flex_of.n;
+    info->cached_segments = S->X.cache.n;
+    info->records_held = S->nstore;
+    info->rows_held = S->arows;
+    return RFEC_OK;
 }

@@ -95,6 +95,11 @@ class rfec_send_report(C.Structure):
                 ("total_us", C.c_double)]
 
 
+class rfec_rx_session_info(C.Structure):
+    _fields_ = [("max_ts", C.c_uint32), ("open_flexes", C.c_uint32), ("cached_segments", C.c_uint32),
+                ("records_held", C.c_uint32), ("rows_held", C.c_uint32), ("reserved", C.c_uint32)]
+
+
 class rfec_udp_addr(C.Structure):
     _fields_ = [("ip", C.c_uint32), ("port", C.c_uint16), ("reserved", C.c_uint16)]
 
@@ -232,6 +237,14 @@ _SIGS = {
                                            C.POINTER(C.c_uint32), _P, _P, _P, C.c_uint32, C.POINTER(C.c_uint32),
                                            C.POINTER(rfec_rx_report)]),
     "rfec_pinned_alloc": (_P, [C.c_size_t]),
+    "rfec_rx_session_create": (_P, [C.c_uint32, C.c_uint32]),
+    "rfec_rx_session_destroy": (None, [_P]),
+    "rfec_rx_session_push": (C.c_int, [_P, C.c_uint32, _P, _P, _P, _P, C.c_uint32, C.POINTER(C.c_uint32),
+                                       C.POINTER(rfec_rx_report), _P]),
+    "rfec_rx_session_push_datagrams": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint32,
+                                                 C.POINTER(C.c_uint32), C.POINTER(rfec_rx_report)]),
+    "rfec_rx_session_evict": (C.c_int, [_P, _P]),
+    "rfec_rx_session_get_info": (C.c_int, [_P, C.POINTER(rfec_rx_session_info)]),
     "rfec_pinned_free": (None, [_P]),
 }
 
@@ -400,6 +413,9 @@ class Native:
                     "rfec_host_recv_datagrams")
         return out[:nout.value], outp[:nout.value], mts.value, rep, recs
 
+    def rx_session(self, stride, capacity):
+        return RxSession(self, stride, capacity)
+
     # -- batched UDP I/O (host memory) -------------------------------------------
     def udp_open(self, ip="127.0.0.1", port=0, flags=RFEC_UDP_SERVER, buf_bytes=0):
         """Returns (fd, bound rfec_udp_addr)."""
@@ -458,6 +474,56 @@ class Native:
     def _check(self, rc, what):
         if rc != 0:
             raise RfecError(f"{what} failed ({rc}): {self.last_error()}")
+
+
+class RxSession:
+    """rfec_rx_session: receiver-side FEC state kept across batches."""
+
+    def __init__(self, native: Native, stride: int, capacity: int):
+        self.n, self.stride = native, stride
+        self.h = native.lib.rfec_rx_session_create(stride, capacity)
+        if not self.h:
+            raise RfecError(f"rfec_rx_session_create failed: {native.last_error()}")
+
+    def push(self, n, recs, payload, max_out=1 << 16, stream=None):
+        """recs / payload: DEVICE addresses.  Returns (segments, payload rows, report)."""
+        out = np.zeros(max_out, RX_SEG_DTYPE)
+        outp = np.zeros((max_out, self.stride), np.uint8)
+        nout, rep = C.c_uint32(), rfec_rx_report()
+        self.n._check(self.n.lib.rfec_rx_session_push(self.h, n, recs, payload, out.ctypes.data, outp.ctypes.data,
+                                                      max_out, C.byref(nout), C.byref(rep), stream),
+                      "rfec_rx_session_push")
+        return out[:nout.value], outp[:nout.value], rep
+
+    def push_datagrams(self, n, dstride, dgram, dlen, max_out=1 << 16, want_recs=False):
+        """dgram / dlen: HOST addresses of n datagram slots."""
+        out = np.zeros(max_out, RX_SEG_DTYPE)
+        outp = np.zeros((max_out, self.stride), np.uint8)
+        recs = np.zeros(n, WIRE_REC_DTYPE) if want_recs else None
+        nout, rep = C.c_uint32(), rfec_rx_report()
+        self.n._check(self.n.lib.rfec_rx_session_push_datagrams(
+            self.h, n, dstride, dgram, dlen, None if recs is None else recs.ctypes.data, out.ctypes.data,
+            outp.ctypes.data, max_out, C.byref(nout), C.byref(rep)), "rfec_rx_session_push_datagrams")
+        return out[:nout.value], outp[:nout.value], rep, recs
+
+    def evict(self, stream=None):
+        self.n._check(self.n.lib.rfec_rx_session_evict(self.h, stream), "rfec_rx_session_evict")
+
+    def info(self):
+        i = rfec_rx_session_info()
+        self.n._check(self.n.lib.rfec_rx_session_get_info(self.h, C.byref(i)), "rfec_rx_session_get_info")
+        return {f: getattr(i, f) for f, _ in i._fields_}
+
+    def close(self):
+        if self.h:
+            self.n.lib.rfec_rx_session_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 _CACHE: dict[int, Native] = {}

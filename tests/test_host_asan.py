@@ -164,6 +164,34 @@ for seed in range(3):
     assert np.array_equal(segs, es) and np.array_equal(groups, eg)
 print("sender ok")
 
+# 6b. receiver sessions: the fixtures pushed in batches (with the reference's
+#     evictions between them), split-invariance on a synthetic stream
+import rx_cases as rc
+def by_seq(rows):
+    return sorted(rows, key=lambda r: r[0])
+for scn in fx["scenarios"]:
+    recs, pay, _, _ = po.rx_stream(o, scn)
+    E = scn["evict_every"]
+    sess = lib.rx_session(pay.shape[1], 1000)
+    rng = np.random.default_rng(len(scn["name"]))
+    a, rows = 0, []
+    while a < len(recs):
+        b = min(len(recs), a + (E if E else int(rng.integers(1, 700))))
+        out, _, rep = sess.push(b - a, recs[a:b].ctypes.data, np.ascontiguousarray(pay[a:b]).ctypes.data)
+        rows += [tuple(int(v) for v in (h["seq"], h["fid"], h["ts"], h["index"], h["total"], h["ftype"],
+                                         h["payload_type"], h["size"])) + (int(f),) for h, f in zip(out["hdr"], out["fec_id"])]
+        if E and b - a == E:
+            sess.evict()
+        a = b
+    want = [tuple(r[:9]) for r in rc.expected(scn)]
+    assert by_seq(rows) == by_seq(want), scn["name"]
+    info = sess.info()
+    assert info["max_ts"] == scn["max_ts"], scn["name"]
+    if E:
+        assert (info["open_flexes"], info["cached_segments"]) == (scn["flexes_left"], scn["cache_left"]), (scn["name"], info)
+    sess.close()
+print("sessions ok")
+
 # 6. batched UDP I/O over loopback (rfec_net.c): slots out, slots in, the
 #    reference's length rules, more than one sendmmsg / recvmmsg batch
 from razor_amd.fec import RFEC_UDP_SERVER, rfec_udp_stats

@@ -179,3 +179,112 @@ def test_rx_edges(lib):
         lib.rx_recover(len(arrivals), recs.data_ptr(), pay.data_ptr(), STRIDE, 1000, 0, len(out) - 1)
     with pytest.raises(RfecError):
         lib.rx_recover(len(arrivals), recs.data_ptr(), pay.data_ptr(), 1000, 1000, 0, 16)  # stride % 16
+
+
+# ---------------------------------------------------------------------------
+# receiver sessions (rfec_rx_session_*): state kept across batches
+# ---------------------------------------------------------------------------
+def _rows(out, outp):
+    return sorted(rc.got_rows(out, outp), key=lambda r: r[0])
+
+
+@pytest.mark.parametrize("name", ["k10_loss10", "mixed_loss15", "late_parities", "evict_late_segments",
+                                  "evict_lost_parities", "no_evict_late_segments"])
+def test_rx_session_reference_fixture(lib, name):
+    """The reference receiver's streams pushed in batches, with sim_fec_evict
+    between batches where the scenario's heartbeat ran it: the same recovered
+    segments (bytes by FNV-1a), max_ts, and the same open flexes / cached
+    segments left as the reference's skiplists."""
+    scn = {s["name"]: s for s in po.rx_fixture()["scenarios"]}[name]
+    recs, pay, _, _ = po.rx_stream(po.Oracle(1000), scn)
+    E = scn["evict_every"]
+    sess = lib.rx_session(pay.shape[1], 1000)
+    rng = np.random.default_rng(7)
+    a, rows = 0, []
+    while a < len(recs):
+        b = min(len(recs), a + (E if E else int(rng.integers(1, 500))))
+        dr, dp = _dev(recs[a:b]), _dev(pay[a:b])
+        out, outp, rep = sess.push(b - a, dr.data_ptr(), dp.data_ptr())
+        assert rep.n_unmodelled == 0
+        rows += rc.got_rows(out, outp)
+        if E and b - a == E:
+            sess.evict()
+        a = b
+    assert sorted(rows, key=lambda r: r[0]) == sorted(rc.expected(scn), key=lambda r: r[0])
+    info = sess.info()
+    assert info["max_ts"] == scn["max_ts"]
+    if E:
+        assert (info["open_flexes"], info["cached_segments"]) == (scn["flexes_left"], scn["cache_left"])
+    sess.close()
+
+
+@pytest.mark.parametrize("evict_every", [0, 300])
+def test_rx_session_split_invariance(lib, oracle1000, evict_every):
+    """A product-sender stream pushed in random batches (evict_every == 0) or
+    in batches of evict_every with evictions between: the union of what the
+    batches deliver == the oracle on the whole stream with the same evictions
+    -- including groups whose datagrams straddle batches."""
+    order, dg, _ = _sender_stream(lib, 2500, 5, (3, 10, 24), (20, 80, 100))
+    arrivals = _network(order, np.random.default_rng(13), loss=0.15, window=60, dup=0.03, late=0.05,
+                        late_by=2500)
+    recs, pay = _arrivals(lib, arrivals, dg)
+    from razor_amd.fec import WIRE_REC_DTYPE
+    h_recs = recs.cpu().numpy().view(WIRE_REC_DTYPE)
+    h_pay = pay.cpu().numpy().reshape(-1, STRIDE)
+    n = len(h_recs)
+    eo, eop, emts, edrop = oracle1000.rx_recover(h_recs, h_pay, 1000, max_out=1 << 17, evict_every=evict_every)
+    sess = lib.rx_session(STRIDE, 1000)
+    rng = np.random.default_rng(evict_every + 1)
+    a, got, gotp, dropped = 0, [], [], 0
+    recs_u8 = recs.view(-1, WIRE_REC_DTYPE.itemsize)
+    pay_u8 = pay.view(-1, STRIDE)
+    while a < n:
+        b = min(n, a + (evict_every if evict_every else int(rng.integers(1, 3000))))
+        out, outp, rep = sess.push(b - a, recs_u8[a:b].data_ptr(), pay_u8[a:b].data_ptr(), max_out=1 << 16)
+        got.append(out)
+        gotp.append(outp)
+        dropped += rep.n_fec_dropped
+        assert rep.n_unmodelled == 0
+        if evict_every and b - a == evict_every:
+            sess.evict()
+        a = b
+    out, outp = np.concatenate(got), np.concatenate(gotp)
+    i, j = np.argsort(out["hdr"]["seq"], kind="stable"), np.argsort(eo["hdr"]["seq"], kind="stable")
+    assert len(out) == len(eo) > 0
+    assert np.array_equal(out["hdr"][i], eo["hdr"][j]) and np.array_equal(out["fec_id"][i], eo["fec_id"][j])
+    assert np.array_equal(outp[i], eop[j])
+    assert sess.info()["max_ts"] == emts and dropped == edrop
+    if evict_every:
+        info = sess.info()
+        assert info["records_held"] < n // 2  # compaction keeps only what the open state refers to
+    sess.close()
+
+
+def test_rx_session_datagrams(lib, oracle1000):
+    """Datagram slots in host memory -> session (H2D, parse, ingestion), in batches."""
+    order, (sdg, sdl, fdg, fdl), _ = _sender_stream(lib, 600, 9)
+    arrivals = _network(order, np.random.default_rng(4), loss=0.1, window=20, dup=0.02)
+    n = len(arrivals)
+    dgram = np.zeros((n, DSTRIDE), np.uint8)
+    dlen = np.zeros(n, np.uint16)
+    for a, (kind, i) in enumerate(arrivals):
+        src, ln = (sdg, sdl) if kind == 0 else (fdg, fdl)
+        dgram[a], dlen[a] = src[i], ln[i]
+    sess = lib.rx_session(STRIDE, 1000)
+    got, gotp, recs = [], [], []
+    for a in range(0, n, 777):
+        b = min(n, a + 777)
+        out, outp, rep, r = sess.push_datagrams(b - a, DSTRIDE, dgram[a:].ctypes.data, dlen[a:].ctypes.data,
+                                                want_recs=True)
+        got.append(out)
+        gotp.append(outp)
+        recs.append(r)
+    recs = np.concatenate(recs)
+    erecs, epay = oracle1000.parse_batch(dgram, dlen, STRIDE, 1000)
+    assert np.array_equal(recs.view(np.uint8), np.asarray(erecs).view(np.uint8).reshape(recs.view(np.uint8).shape))
+    eo, eop, emts, _ = oracle1000.rx_recover(erecs, epay, 1000, max_out=1 << 16)
+    out, outp = np.concatenate(got), np.concatenate(gotp)
+    i, j = np.argsort(out["hdr"]["seq"], kind="stable"), np.argsort(eo["hdr"]["seq"], kind="stable")
+    assert len(out) == len(eo) > 0 and np.array_equal(out["hdr"][i], eo["hdr"][j])
+    assert np.array_equal(outp[i], eop[j]) and sess.info()["max_ts"] == emts
+    sess.close()
