@@ -224,7 +224,7 @@ def test_rx_session_split_invariance(lib, oracle1000, evict_every):
     in batches of evict_every with evictions between: the union of what the
     batches deliver == the oracle on the whole stream with the same evictions
     -- including groups whose datagrams straddle batches."""
-    order, dg, _ = _sender_stream(lib, 2500, 5, (3, 10, 24), (20, 80, 100))
+    order, dg, _ = _sender_stream(lib, 2500, 5, (3, 6, 10), (20, 80, 100))
     arrivals = _network(order, np.random.default_rng(13), loss=0.15, window=60, dup=0.03, late=0.05,
                         late_by=2500)
     recs, pay = _arrivals(lib, arrivals, dg)
