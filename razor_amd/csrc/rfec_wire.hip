@@ -9,18 +9,22 @@
 //                 yield 0 without advancing (cf_stream.c mach_*_read)
 //   crc32         cf_crc32.c:56-68, seed 0x0e3dfc0a (sim_proto.c:11)
 //
-// One wavefront per datagram; lane j owns bytes [32j, 32j+32) of it (so a
-// datagram slot is at most 2 KiB).  Payload bytes move through registers with
-// a wave-uniform byte funnel (no LDS staging); the header is assembled with
-// compile-time byte positions.  CRC32 is computed wave-parallel: each lane
-// takes the raw CRC of its 32 bytes with slice-by-16 tables in LDS and scales
-// it to the end of the message by x^(8e) mod P, e = the bytes after its run.
-// With n = 2048 - 32q - r, e = 256 (63 - j - q) - 8r: the x^(256 (63 - c))
-// part is a fixed per-column multiplier (eight nibble lookups in column
-// c = j + q, zlib's multmodp tabulated), the x^(-8r) part is applied once to
-// the wave's XOR-reduced sum (one lookup per bit lane).  The CRC's initial
-// register is folded into the first four message bytes, so every lane runs
-// from a zero register.  Cross-lane sums use DPP within rows plus readlane.
+// One wavefront per datagram; lane j owns bytes [B j, B j + B) of it, B = 20
+// when the slot holds at most 1,280 bytes (a 1,249-byte SIM_FEC or 1,236-byte
+// SIM_SEG at 1,200-byte payloads then keeps 63 of 64 lanes busy), else B = 32
+// (slots up to 2 KiB).  Every lane load / store is a dword buffer access at a
+// dword-aligned offset, range-checked per dword against its slot.  Payload
+// bytes move through registers with a wave-uniform byte funnel (no LDS
+// staging); the header is assembled with compile-time byte positions.  CRC32
+// is computed wave-parallel: each lane takes the raw CRC of its B bytes with
+// slice-by-16 / slice-by-4 tables in LDS and scales it to the end of the
+// message by x^(8e) mod P, e = the bytes after its run.  With
+// n = 64 B - B q - r, e = 8 B (63 - j - q) - 8r: the x^(8 B (63 - c)) part is
+// a fixed per-column multiplier (eight nibble lookups in column c = j + q,
+// zlib's multmodp tabulated), the x^(-8r) part is applied once to the wave's
+// XOR-reduced sum (one lookup per bit lane).  The CRC's initial register is
+// folded into the first four message bytes, so every lane runs from a zero
+// register.  Cross-lane sums use DPP within rows plus readlane.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -33,27 +37,30 @@ constexpr int kBlock = 1024;
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr uint32_t kPoly = 0xEDB88320u; // reflected CRC-32 polynomial (cf_crc32.c table)
 
-// LDS tables (built at compile time, copied to LDS once per block):
+// LDS tables (built at compile time, copied to LDS once per block), per lane
+// width B:
 //   t[s][b]         CRC register after byte b then s zero bytes, from 0 (slice-by-16)
-//   nib[i][v][c]    (nibble v at nibble position i of a register) * x^(256 (63-c)):
-//                   a 32-byte run in column c of a 2 KiB window, carried to the
+//   nib[i][v][c]    (nibble v at nibble position i of a register) * x^(8 B (63-c)):
+//                   a B-byte run in column c of a 64 B-byte window, carried to the
 //                   window's end.  [i][v][c]: the lanes read distinct columns, so
 //                   they never share an LDS bank.
-//   inv[r][i]       x^(31-i) * x^(-8r): bit i of a register times x^(-8r)
+//   inv[r][i]       x^(31-i) * x^(-8r), r < B: bit i of a register times x^(-8r)
 // (bit p of a register is the coefficient of x^(31-p))
+template <int B>
 struct CrcTables {
     uint32_t t[16][256];
     uint32_t nib[8][16][kWave];
-    uint32_t inv[32][32];
+    uint32_t inv[B][32];
 };
 
 constexpr uint32_t mul_x(uint32_t v) { return (v & 1u) ? (v >> 1) ^ kPoly : v >> 1; }
 // the inverse of mul_x (kPoly has bit 31 set, v >> 1 never does)
 constexpr uint32_t div_x(uint32_t v) { return (v & 0x80000000u) ? (((v ^ kPoly) << 1) | 1u) : (v << 1); }
 
-constexpr CrcTables make_crc_tables()
+template <int B>
+constexpr CrcTables<B> make_crc_tables()
 {
-    CrcTables r{};
+    CrcTables<B> r{};
     for (uint32_t b = 0; b < 256; ++b) {
         uint32_t c = b;
         for (int i = 0; i < 8; ++i)
@@ -63,8 +70,8 @@ constexpr CrcTables make_crc_tables()
     for (int s = 1; s < 16; ++s)
         for (uint32_t b = 0; b < 256; ++b)
             r.t[s][b] = (r.t[s - 1][b] >> 8) ^ r.t[0][r.t[s - 1][b] & 0xffu];
-    // V_j = x^(256 (63 - j)); bit p of a register is the coefficient of x^(31-p)
-    uint32_t V = 0x80000000u; // x^0, for lane 63
+    // V_c = x^(8 B (63 - c))
+    uint32_t V = 0x80000000u; // x^0, for column 63
     for (int j = kWave - 1; j >= 0; --j) {
         uint32_t basis[32]{}; // basis[e] = x^e * V_j
         uint32_t v = V;
@@ -80,12 +87,12 @@ constexpr CrcTables make_crc_tables()
                         acc ^= basis[31 - (4 * i + k)];
                 r.nib[i][nv][j] = acc;
             }
-        for (int q = 0; q < 256; ++q)
+        for (int q = 0; q < 8 * B; ++q)
             V = mul_x(V);
     }
     for (int i = 0; i < 32; ++i) {
         uint32_t v = 1u << i; // x^(31-i)
-        for (int q = 0; q < 32; ++q) {
+        for (int q = 0; q < B; ++q) {
             r.inv[q][i] = v;
             for (int b = 0; b < 8; ++b)
                 v = div_x(v);
@@ -94,18 +101,25 @@ constexpr CrcTables make_crc_tables()
     return r;
 }
 
-__device__ const CrcTables kCrc = make_crc_tables();
+__device__ const CrcTables<20> kCrc20 = make_crc_tables<20>();
+__device__ const CrcTables<32> kCrc32 = make_crc_tables<32>();
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-constexpr int kTabDwords = (int)(sizeof(CrcTables) / 4);
+template <int B>
+constexpr int kTabDwords = (int)(sizeof(CrcTables<B>) / 4);
 constexpr int kNibBase = 16 * 256;                 // dword offset of nib in the LDS copy
 constexpr int kInvBase = kNibBase + 8 * 16 * kWave; // dword offset of inv
+template <int B>
 __device__ __forceinline__ void load_tables(uint32_t* T)
 {
-    const v4u* s = reinterpret_cast<const v4u*>(&kCrc);
+    const v4u* s;
+    if constexpr (B == 20)
+        s = reinterpret_cast<const v4u*>(&kCrc20);
+    else
+        s = reinterpret_cast<const v4u*>(&kCrc32);
     v4u* d = reinterpret_cast<v4u*>(T);
-    for (int i = threadIdx.x; i < kTabDwords / 4; i += kBlock)
+    for (int i = threadIdx.x; i < kTabDwords<B> / 4; i += kBlock)
         d[i] = s[i];
     __syncthreads();
 }
@@ -121,7 +135,24 @@ __device__ __forceinline__ uint32_t slice16(const uint32_t* T, uint32_t a, uint3
            tb(T, 3, d & 0xff) ^ tb(T, 2, (d >> 8) & 0xff) ^ tb(T, 1, (d >> 16) & 0xff) ^ tb(T, 0, d >> 24);
 }
 
-// c * x^(256 (63 - col)) mod P: eight nibble lookups in column `col`
+// raw CRC (zero register) of 4 bytes given as one LE dword
+__device__ __forceinline__ uint32_t slice4(const uint32_t* T, uint32_t a)
+{
+    return tb(T, 3, a & 0xff) ^ tb(T, 2, (a >> 8) & 0xff) ^ tb(T, 1, (a >> 16) & 0xff) ^ tb(T, 0, a >> 24);
+}
+
+// raw CRC of a lane's B bytes (w: B / 4 LE dwords, w0 replacing w[0])
+template <int B>
+__device__ __forceinline__ uint32_t lane_crc(const uint32_t* T, uint32_t w0, const uint32_t* w)
+{
+    uint32_t c = slice16(T, w0, w[1], w[2], w[3]);
+    if constexpr (B == 20)
+        return slice4(T, w[4] ^ c);
+    else
+        return slice16(T, w[4] ^ c, w[5], w[6], w[7]);
+}
+
+// c * x^(8 B (63 - col)) mod P: eight nibble lookups in column `col`
 __device__ __forceinline__ uint32_t carry_to_end(const uint32_t* T, uint32_t c, uint32_t col)
 {
     const uint32_t* nb = T + kNibBase + col;
@@ -158,8 +189,9 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
 }
 
 // crc32(seed, msg[0:n)) (cf_crc32.c:56-68) of a message held lane-wise:
-// lane j has bytes [32j, 32j+32) in w (LE dwords), bytes >= n zero; n <= 2048.
-__device__ uint32_t wave_crc32(const uint32_t* T, const uint32_t w[8], uint32_t n, uint32_t seed, uint32_t lane)
+// lane j has bytes [B j, B j + B) in w (LE dwords), bytes >= n zero; n <= 64 B.
+template <int B>
+__device__ __forceinline__ uint32_t wave_crc32(const uint32_t* T, const uint32_t* w, uint32_t n, uint32_t seed, uint32_t lane)
 {
     if (n < 4) { // too short to fold the initial register into: bytewise
         uint32_t r = ~seed;
@@ -167,11 +199,9 @@ __device__ uint32_t wave_crc32(const uint32_t* T, const uint32_t w[8], uint32_t 
             r = tb(T, 0, (r ^ (w[0] >> (8 * i))) & 0xffu) ^ (r >> 8);
         return (uint32_t)__builtin_amdgcn_readfirstlane((int)~r);
     }
-    const uint32_t D = 2048u - n, q = D >> 5, rr = D & 31u;
+    const uint32_t D = (uint32_t)(kWave * B) - n, q = D / B, rr = D - q * B;
     // initial register folded into message bytes 0-3
-    const uint32_t w0 = w[0] ^ (lane == 0 ? ~seed : 0u);
-    uint32_t c = slice16(T, w0, w[1], w[2], w[3]);
-    c = slice16(T, w[4] ^ c, w[5], w[6], w[7]);
+    const uint32_t c = lane_crc<B>(T, w[0] ^ (lane == 0 ? ~seed : 0u), w);
     // lanes past the message hold zeros (c == 0): their column is clamped
     const uint32_t R = wave_xor(carry_to_end(T, c, min(lane + q, (uint32_t)kWave - 1u)));
     // R = crc register * x^(8 rr): bit i of R times x^(31-i-8rr), summed
@@ -193,63 +223,49 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
 }
 constexpr int kAuxNT = 2; // gfx950 cache-policy bits: nt
 
-// Up to three consecutive 16-B chunks of a slot, starting at chunk `a` (may
-// be negative); chunks outside [0, nch) read as 0.  Lane-private window; of
-// the third chunk only the first W2 dwords are loaded (what the funnel uses:
-// a dead dword of a wide load would pin its register until the load lands).
-struct Win {
-    v4u c[3];
-};
-template <int W2>
-__device__ __forceinline__ Win load_win(const uint8_t* __restrict__ src, int a, int nch)
+// NX dwords at byte offset `off` (a multiple of 4, may be negative) of the
+// range r; dwords outside the range read as 0 (a negative offset wraps past it)
+template <int NX>
+__device__ __forceinline__ void load_dwords(const __amdgpu_buffer_rsrc_t r, int off, uint32_t (&x)[NX])
 {
-    const __amdgpu_buffer_rsrc_t r = rsrc(src, (uint32_t)nch * 16u);
-    Win w = {};
-    // a negative offset wraps past the range: 0
-    w.c[0] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)a * 16u, 0, kAuxNT));
-    w.c[1] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)(a + 1) * 16u, 0, kAuxNT));
-    if constexpr (W2 == 1) {
-        w.c[2][0] = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)(a + 2) * 16u, 0, kAuxNT);
-    } else if constexpr (W2 == 2) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)(a + 2) * 16u, 0, kAuxNT);
-        w.c[2][0] = v[0];
-        w.c[2][1] = v[1];
-    } else if constexpr (W2 == 4) {
-        w.c[2] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)(a + 2) * 16u, 0, kAuxNT));
-    }
-    return w;
+#pragma unroll
+    for (int k = 0; k < NX; ++k)
+        x[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)(off + 4 * k), 0, kAuxNT);
 }
 
-// out[k] = dword k of the window shifted down by `sh` bytes (sh in [0, 16])
-template <int SH>
-__device__ __forceinline__ void funnel_c(const Win& w, uint32_t out[8])
+// out[k] = dword k of the window x shifted down by SH bytes (k < ND)
+template <int ND, int SH, int NX>
+__device__ __forceinline__ void funnel(const uint32_t (&x)[NX], uint32_t* out)
 {
-    const uint32_t x[12] = {w.c[0][0], w.c[0][1], w.c[0][2], w.c[0][3], w.c[1][0], w.c[1][1],
-                            w.c[1][2], w.c[1][3], w.c[2][0], w.c[2][1], w.c[2][2], w.c[2][3]};
+    static_assert((SH >> 2) + ND + ((SH & 3) ? 1 : 0) <= NX, "window too short");
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
+    for (int k = 0; k < ND; ++k)
         out[k] = (SH & 3) ? __builtin_amdgcn_alignbyte(x[(SH >> 2) + k + 1], x[(SH >> 2) + k], SH & 3)
                           : x[(SH >> 2) + k];
 }
 
 // Mask of dword k of lane `lane` for a message of nb bytes held lane-wise
-// (lane j = bytes [32j, 32j+32)): the byte position of nb is wave-uniform, so
+// (lane j = bytes [B j, B j + B)): the byte position of nb is wave-uniform, so
 // per lane this is two selects of uniform values.
+template <int B>
 __device__ __forceinline__ uint32_t len_mask(int k, uint32_t lane, uint32_t nb)
 {
-    const uint32_t qd = nb >> 2, s = nb & 3u, lq = qd >> 3, kq = qd & 7u;
+    constexpr uint32_t ND = B / 4;
+    const uint32_t qd = nb >> 2, s = nb & 3u, lq = qd / ND, kq = qd - lq * ND;
     const uint32_t ck = (uint32_t)k < kq ? ~0u : ((uint32_t)k == kq ? (s ? (1u << (8 * s)) - 1u : 0u) : 0u);
     return lane < lq ? ~0u : (lane == lq ? ck : 0u);
 }
 
+// a lane's B bytes to [B lane, B lane + B) of a slot of slot_bytes (range
+// checked per dword: dwords past the slot are dropped)
+template <int B>
 __device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t slot_bytes, uint32_t lane,
-                                           const uint32_t w[8])
+                                           const uint32_t* w)
 {
-    v4u* p = reinterpret_cast<v4u*>(slot + 32u * lane);
-    if (32u * lane < slot_bytes)
-        __builtin_nontemporal_store(v4u{w[0], w[1], w[2], w[3]}, p);
-    if (32u * lane + 16u < slot_bytes)
-        __builtin_nontemporal_store(v4u{w[4], w[5], w[6], w[7]}, p + 1);
+    const __amdgpu_buffer_rsrc_t r = rsrc(slot, slot_bytes);
+#pragma unroll
+    for (int k = 0; k < B / 4; ++k)
+        __builtin_amdgcn_raw_buffer_store_b32(w[k], r, B * lane + 4 * k, 0, kAuxNT);
 }
 
 // Header bytes at compile-time positions (big-endian fields, cf_stream.c:366-385)
@@ -268,38 +284,47 @@ __device__ __forceinline__ void put(Hdr& b, uint32_t v)
 
 // Datagram of header H (bytes [0, hsize), zero beyond) and payload `pay`
 // (zero below hsize): mask at n = hsize + L, CRC32 BE at [n, n+4), store.
-__device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, uint32_t n, uint32_t pay[8],
+template <int B>
+__device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, uint32_t n, const uint32_t* pay,
                                              uint32_t lane, uint8_t* __restrict__ slot, uint32_t dstride,
                                              uint16_t* dlen_out)
 {
-    uint32_t w[8];
+    constexpr int ND = B / 4;
+    uint32_t w[ND];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        // header dwords live in lanes 0 and 1 (hsize <= 48)
-        const uint32_t hd = lane == 0 ? H.h[k] : (lane == 1 && k < 4 ? H.h[8 + k] : 0u);
-        w[k] = (pay[k] | hd) & len_mask(k, lane, n);
+    for (int k = 0; k < ND; ++k) {
+        // header dword i (hsize <= 48: i < 12) lives in lane i / ND
+        uint32_t hd = 0;
+#pragma unroll
+        for (int L = 0; L * ND < 12; ++L)
+            if (L * ND + k < 12)
+                hd = lane == (uint32_t)L ? H.h[L * ND + k] : hd;
+        w[k] = (pay[k] | hd) & len_mask<B>(k, lane, n);
     }
-    const uint32_t crc = wave_crc32(T, w, n, RFEC_WIRE_CRC_SEED, lane);
+    const uint32_t crc = wave_crc32<B>(T, w, n, RFEC_WIRE_CRC_SEED, lane);
     // big-endian trailer at byte n: its first 4 - s bytes end dword n / 4, the
     // rest start the next one (both positions wave-uniform)
     const uint32_t be = bswap(crc), s = n & 3u, q0 = n >> 2, q1 = q0 + 1;
     const uint32_t lo = be << (8 * s), hi = s ? be >> (32 - 8 * s) : 0u;
+    const uint32_t l0 = q0 / ND, k0 = q0 - l0 * ND, l1 = q1 / ND, k1 = q1 - l1 * ND;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        if ((uint32_t)k == (q0 & 7u))
-            w[k] |= lane == (q0 >> 3) ? lo : 0u;
-        if ((uint32_t)k == (q1 & 7u))
-            w[k] |= lane == (q1 >> 3) ? hi : 0u;
+    for (int k = 0; k < ND; ++k) {
+        if ((uint32_t)k == k0)
+            w[k] |= lane == l0 ? lo : 0u;
+        if ((uint32_t)k == k1)
+            w[k] |= lane == l1 ? hi : 0u;
     }
-    store_slot(slot, dstride, lane, w);
+    store_slot<B>(slot, dstride, lane, w);
     if (lane == 0)
         *dlen_out = (uint16_t)(n + 4);
 }
 
-__device__ __forceinline__ void zero_slot(uint8_t* __restrict__ slot, uint32_t dstride, uint32_t lane, uint16_t* dlen_out)
+template <int B>
+__device__ __forceinline__ void zero_slot(uint8_t* __restrict__ slot, uint32_t dstride, uint32_t lane,
+                                          uint16_t* dlen_out)
 {
-    const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    store_slot(slot, dstride, lane, z);
+    const uint32_t z[B / 4] = {};
+    store_slot<B>(slot, dstride, lane, z);
     if (lane == 0)
         *dlen_out = 0;
 }
@@ -371,12 +396,17 @@ __device__ __forceinline__ void ping_pong(uint32_t d, uint32_t count, uint32_t n
     }
 }
 
+template <int NX>
 struct Pre {
-    Win w;
-    uint32_t f;
+    uint32_t x[NX]; // payload window
+    uint32_t f;     // per-datagram fields, one dword per lane
 };
 
+// Lane j's window starts 48 (FEC) / 32 (SEG) bytes before the source of its
+// output bytes [B j, B j + B), so it does not depend on the header size.
+
 // SIM_FEC: 45-byte header (sim_proto.c:13-18, sim_proto.inl:244-254, 270-283)
+template <int B>
 __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict__ parity,
                                                       const rfec_hdr* __restrict__ meta,
                                                       const uint16_t* __restrict__ fsize,
@@ -387,27 +417,28 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
                                                       uint32_t count, uint32_t stride, uint32_t capacity,
                                                       uint32_t dstride)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords];
-    load_tables(T);
+    constexpr int ND = B / 4;
+    __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords<B>];
+    load_tables<B>(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
-    const int nch = (int)((capacity + 15) >> 4);
-    const int a0 = 2 * (int)lane - 3; // source bytes [32j - 48, 32j): out bytes [32j, 32j+32) shifted by 3
+    const uint32_t range = (capacity + 15u) & ~15u;
+    const int off = B * (int)lane - 48;
     uint32_t d = wave_id();
     if (d >= count)
         return;
-    ping_pong<Pre>(d, count, nw,
-                   [&](uint32_t dd, Pre& P) {
-                       P.f = load_fec_fields(stamps, meta, fsize, status, dd, lane);
-                       P.w = load_win<1>(parity + (size_t)dd * stride, a0, nch);
-                   },
-                   [&](const Pre& P, uint32_t d) {
+    ping_pong<Pre<ND + 1>>(d, count, nw,
+                           [&](uint32_t dd, Pre<ND + 1>& P) {
+                               P.f = load_fec_fields(stamps, meta, fsize, status, dd, lane);
+                               load_dwords<ND + 1>(rsrc(parity + (size_t)dd * stride, range), off, P.x);
+                           },
+                           [&](const Pre<ND + 1>& P, uint32_t d) {
             const uint32_t o = order ? order[d] : d; // output slot
             uint8_t* slot = dgram + (size_t)o * dstride;
             const uint32_t L = fld(P.f, 11);
             const int st = (int)fld(P.f, 12);
             if (st < 0 || L > capacity) {
-                zero_slot(slot, dstride, lane, dlen + o);
+                zero_slot<B>(slot, dstride, lane, dlen + o);
             } else {
                 const uint32_t s3 = fld(P.f, 3), s4 = fld(P.f, 4), s5 = fld(P.f, 5);
                 const uint32_t m3 = fld(P.f, 9), m4 = fld(P.f, 10);
@@ -432,11 +463,11 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
                 put<40, 1>(H, (m4 >> 8) & 0xffu);
                 put<41, 2>(H, m4 >> 16);
                 put<43, 2>(H, L); // mach_data_write length (cf_stream.c:328-337)
-                uint32_t pay[8];
-                funnel_c<3>(P.w, pay); // window [32j-48, 32j) -> bytes [32j-45, 32j-13)
-                finish_frame(T, H, 45 + L, pay, lane, slot, dstride, dlen + o);
+                uint32_t pay[ND];
+                funnel<ND, 3>(P.x, pay); // window [B j - 48, ...) -> bytes [B j - 45, ...)
+                finish_frame<B>(T, H, 45 + L, pay, lane, slot, dstride, dlen + o);
             }
-                   });
+                           });
 }
 
 // SIM_SEG header, one of 8 layouts (sim_proto.inl:83-125): PW / FW = 4-byte
@@ -472,6 +503,7 @@ __device__ __forceinline__ uint32_t seg_header(Hdr& H, const rfec_hdr& h, const 
     return P4 + 8;
 }
 
+template <int B>
 __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict__ shards,
                                                       const rfec_hdr* __restrict__ hdr,
                                                       const rfec_seg_stamp* __restrict__ stamps,
@@ -480,21 +512,22 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                                                       uint32_t count, uint32_t stride, uint32_t capacity,
                                                       uint32_t dstride)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords];
-    load_tables(T);
+    constexpr int ND = B / 4;
+    __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords<B>];
+    load_tables<B>(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
-    const int nch = (int)((capacity + 15) >> 4);
-    const int a0 = 2 * (int)lane - 2; // source bytes [32j - 32, 32j + 16): header sizes 26..32
+    const uint32_t range = (capacity + 15u) & ~15u;
+    const int off = B * (int)lane - 32; // header sizes 26..32
     uint32_t d = wave_id();
     if (d >= count)
         return;
-    ping_pong<Pre>(d, count, nw,
-                   [&](uint32_t dd, Pre& P) {
-                       P.f = load_seg_fields(hdr, stamps, dd, lane);
-                       P.w = load_win<2>(shards + (size_t)dd * stride, a0, nch);
-                   },
-                   [&](const Pre& P, uint32_t d) {
+    ping_pong<Pre<ND + 2>>(d, count, nw,
+                           [&](uint32_t dd, Pre<ND + 2>& P) {
+                               P.f = load_seg_fields(hdr, stamps, dd, lane);
+                               load_dwords<ND + 2>(rsrc(shards + (size_t)dd * stride, range), off, P.x);
+                           },
+                           [&](const Pre<ND + 2>& P, uint32_t d) {
             const uint32_t o = order ? order[d] : d; // output slot
             uint8_t* slot = dgram + (size_t)o * dstride;
             rfec_hdr h;
@@ -511,7 +544,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
             }
             const uint32_t L = h.size;
             if (L > capacity) {
-                zero_slot(slot, dstride, lane, dlen + o);
+                zero_slot<B>(slot, dstride, lane, dlen + o);
             } else {
                 rfec_seg_stamp s;
                 {
@@ -526,21 +559,21 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                 Hdr H = {};
                 const uint32_t layout = (h.seq > 65535u ? 4u : 0u) | (h.fid > 65535u ? 2u : 0u) |
                                         (h.total > 255u ? 1u : 0u);
-                uint32_t hs, pay[8];
-                // window [32j-32, 32j+16) shifted by 32 - hs bytes
+                uint32_t hs, pay[ND];
+                // window [B j - 32, ...) shifted by 32 - hs bytes
                 switch (layout) {
-                case 0: hs = seg_header<false, false, false>(H, h, s); funnel_c<6>(P.w, pay); break;
-                case 1: hs = seg_header<false, false, true>(H, h, s); funnel_c<4>(P.w, pay); break;
-                case 2: hs = seg_header<false, true, false>(H, h, s); funnel_c<4>(P.w, pay); break;
-                case 3: hs = seg_header<false, true, true>(H, h, s); funnel_c<2>(P.w, pay); break;
-                case 4: hs = seg_header<true, false, false>(H, h, s); funnel_c<4>(P.w, pay); break;
-                case 5: hs = seg_header<true, false, true>(H, h, s); funnel_c<2>(P.w, pay); break;
-                case 6: hs = seg_header<true, true, false>(H, h, s); funnel_c<2>(P.w, pay); break;
-                default: hs = seg_header<true, true, true>(H, h, s); funnel_c<0>(P.w, pay); break;
+                case 0: hs = seg_header<false, false, false>(H, h, s); funnel<ND, 6>(P.x, pay); break;
+                case 1: hs = seg_header<false, false, true>(H, h, s); funnel<ND, 4>(P.x, pay); break;
+                case 2: hs = seg_header<false, true, false>(H, h, s); funnel<ND, 4>(P.x, pay); break;
+                case 3: hs = seg_header<false, true, true>(H, h, s); funnel<ND, 2>(P.x, pay); break;
+                case 4: hs = seg_header<true, false, false>(H, h, s); funnel<ND, 4>(P.x, pay); break;
+                case 5: hs = seg_header<true, false, true>(H, h, s); funnel<ND, 2>(P.x, pay); break;
+                case 6: hs = seg_header<true, true, false>(H, h, s); funnel<ND, 2>(P.x, pay); break;
+                default: hs = seg_header<true, true, true>(H, h, s); funnel<ND, 0>(P.x, pay); break;
                 }
-                finish_frame(T, H, hs + L, pay, lane, slot, dstride, dlen + o);
+                finish_frame<B>(T, H, hs + L, pay, lane, slot, dstride, dlen + o);
             }
-                   });
+                           });
 }
 
 // ---------------------------------------------------------------------------
@@ -625,95 +658,105 @@ __device__ __forceinline__ uint32_t next_lane(uint32_t v)
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);
 }
 
-// out lane j = datagram bytes [pos + 32j, pos + 32j + 32) from the lane-wise
-// datagram w (pos wave-uniform, < 64)
-__device__ __forceinline__ void shift_down_bytes(const uint32_t w[8], uint32_t pos, uint32_t out[8])
+// out lane j = datagram bytes [pos + B j, pos + B j + B) from the lane-wise
+// datagram w (pos wave-uniform, < 64): lanes j + q and j + q + 1, q = pos / B,
+// brought over with DPP, then a funnel by the uniform remainder
+template <int B>
+__device__ __forceinline__ void shift_down_bytes(const uint32_t* w, uint32_t pos, uint32_t* out)
 {
-    uint32_t A[8], B[8];
-    const bool q = pos >= 32;
+    constexpr int ND = B / 4;
+    constexpr int QMAX = (63 + B - 1) / B; // q <= 63 / B
+    const uint32_t q = pos / B, r = pos - q * B;
+    uint32_t x[2 * ND];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint32_t n1 = next_lane(w[k]);
-        const uint32_t n2 = q ? next_lane(n1) : 0u;
-        A[k] = q ? n1 : w[k];
-        B[k] = q ? n2 : n1;
+    for (int k = 0; k < ND; ++k) {
+        uint32_t v = w[k];
+#pragma unroll
+        for (int t = 1; t <= QMAX; ++t) {
+            const uint32_t nv = next_lane(v); // every lane active: computed, then selected
+            v = q >= (uint32_t)t ? nv : v;
+        }
+        x[k] = v;
+        x[ND + k] = next_lane(v);
     }
-    const uint32_t x[16] = {A[0], A[1], A[2], A[3], A[4], A[5], A[6], A[7],
-                            B[0], B[1], B[2], B[3], B[4], B[5], B[6], B[7]};
-    const uint32_t r = pos & 31u, rb = r & 3u;
+    const uint32_t rb = r & 3u;
 #define RFEC_SHIFT(S)                                                                                              \
-    _Pragma("unroll") for (int k = 0; k < 8; ++k) out[k] = __builtin_amdgcn_alignbyte(x[(S) + k + 1], x[(S) + k], rb);
+    _Pragma("unroll") for (int k = 0; k < ND; ++k) out[k] = __builtin_amdgcn_alignbyte(x[(S) + k + 1], x[(S) + k], rb);
     switch (r >> 2) {
     case 0: RFEC_SHIFT(0) break;
     case 1: RFEC_SHIFT(1) break;
     case 2: RFEC_SHIFT(2) break;
     case 3: RFEC_SHIFT(3) break;
     case 4: RFEC_SHIFT(4) break;
-    case 5: RFEC_SHIFT(5) break;
-    case 6: RFEC_SHIFT(6) break;
-    default: RFEC_SHIFT(7) break;
+    case 5: if constexpr (ND > 5) { RFEC_SHIFT(5) } break;
+    case 6: if constexpr (ND > 6) { RFEC_SHIFT(6) } break;
+    default: if constexpr (ND > 7) { RFEC_SHIFT(7) } break;
     }
 #undef RFEC_SHIFT
 }
 
+// dword k of w, k wave-uniform
+template <int ND>
+__device__ __forceinline__ uint32_t pick(const uint32_t* w, uint32_t k)
+{
+    uint32_t v = w[0];
+#pragma unroll
+    for (int i = 1; i < ND; ++i)
+        v = k == (uint32_t)i ? w[i] : v;
+    return v;
+}
+
+template <int B>
 __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ dgram,
                                                   const uint16_t* __restrict__ dlen,
                                                   rfec_wire_rec* __restrict__ recs, uint8_t* __restrict__ payload,
                                                   uint32_t n, uint32_t dstride, uint32_t stride, uint32_t capacity)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords];
+    constexpr int ND = B / 4;
+    __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords<B>];
     __shared__ uint32_t stage[kWavesPerBlock][16]; // first 64 bytes of each wave's datagram (slow path)
-    load_tables(T);
+    load_tables<B>(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wl = threadIdx.x >> 6;
     const uint32_t nw = gridDim.x * kWavesPerBlock;
-    const int nch = (int)(dstride >> 4);
-    const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint32_t z[ND] = {};
     uint32_t d = wave_id();
     if (d >= n)
         return;
-    ping_pong<Pre>(d, n, nw,
-                   [&](uint32_t dd, Pre& P) {
-                       P.f = __builtin_amdgcn_raw_buffer_load_b16(rsrc(dlen + dd, 2), 2u * lane, 0, kAuxNT);
-                       P.w = load_win<0>(dgram + (size_t)dd * dstride, 2 * (int)lane, nch);
-                   },
-                   [&](const Pre& P, uint32_t d) {
+    ping_pong<Pre<ND>>(d, n, nw,
+                       [&](uint32_t dd, Pre<ND>& P) {
+                           P.f = __builtin_amdgcn_raw_buffer_load_b16(rsrc(dlen + dd, 2), 2u * lane, 0, kAuxNT);
+                           load_dwords<ND>(rsrc(dgram + (size_t)dd * dstride, dstride), B * (int)lane, P.x);
+                       },
+                       [&](const Pre<ND>& P, uint32_t d) {
             uint8_t* slot = payload + (size_t)d * stride;
             const uint32_t len = fld(P.f, 0);
             rfec_wire_rec rec = {};
             rec.status = RFEC_WIRE_EBADCRC;
             int data_at = -1;
             uint32_t dsize = 0;
-            if (len >= 4 && len <= dstride) {
-                // datagram bytes [32j, 32j+32), zero from `len` on
-                uint32_t w[8], m[8];
+            if (len >= 4 && len <= dstride && len <= (uint32_t)(kWave * B)) {
+                // datagram bytes [B j, B j + B), zero from `len` on
+                uint32_t w[ND], m[ND];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    w[k] = P.w.c[k >> 2][k & 3] & len_mask(k, lane, len);
-                    m[k] = w[k] & len_mask(k, lane, len - 4);
+                for (int k = 0; k < ND; ++k) {
+                    w[k] = P.x[k] & len_mask<B>(k, lane, len);
+                    m[k] = w[k] & len_mask<B>(k, lane, len - 4);
                 }
                 // CRC over [0, len-4) against the big-endian trailer (sim_proto.c:21-37)
-                const uint32_t crc = wave_crc32(T, m, len - 4, RFEC_WIRE_CRC_SEED, lane);
-                const uint32_t tp = len - 4, tl = tp >> 5, tk = (tp & 31u) >> 2;
-                uint32_t lo = w[0], hi = w[1];
-#pragma unroll
-                for (int k = 1; k < 8; ++k) {
-                    lo = tk == (uint32_t)k ? w[k] : lo;
-                    hi = tk == (uint32_t)k ? (k < 7 ? w[k + 1] : 0u) : hi;
-                }
-                const uint32_t nx = next_lane(w[0]); // next lane's first dword
-                hi = tk == 7u ? nx : hi;
-                const uint64_t t2 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, (int)tl) << 32 |
-                                    (uint32_t)__builtin_amdgcn_readlane((int)lo, (int)tl);
-                const uint32_t trailer = bswap((uint32_t)(t2 >> (8 * (tp & 3u))));
+                const uint32_t crc = wave_crc32<B>(T, m, len - 4, RFEC_WIRE_CRC_SEED, lane);
+                const uint32_t tp = len - 4, q0 = tp >> 2, q1 = q0 + 1;
+                const uint32_t l0 = q0 / ND, k0 = q0 - l0 * ND, l1 = q1 / ND, k1 = q1 - l1 * ND;
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)pick<ND>(w, k0), (int)l0);
+                const uint32_t hi = l1 < (uint32_t)kWave
+                                        ? (uint32_t)__builtin_amdgcn_readlane((int)pick<ND>(w, k1), (int)l1)
+                                        : 0u;
+                const uint32_t trailer = bswap((uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (tp & 3u))));
                 if (crc == trailer) {
                     uint32_t H[12];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k)
-                        H[k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 0);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        H[8 + k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k], 1);
+                    for (int k = 0; k < 12; ++k)
+                        H[k] = (uint32_t)__builtin_amdgcn_readlane((int)w[k % ND], k / ND);
                     rec.ver = (uint8_t)get<0, 1>(H);
                     rec.mid = (uint8_t)get<1, 1>(H);
                     const uint32_t mid = rec.mid;
@@ -771,11 +814,12 @@ __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ dg
                         npos += 2;
                     } else {
                         // truncated header: emulate the bin_stream reader byte by byte
-                        if (lane < 2) {
+                        if (lane * ND < 16) {
                             volatile uint32_t* sg = stage[wl];
 #pragma unroll
-                            for (int k = 0; k < 8; ++k)
-                                sg[8 * lane + k] = w[k];
+                            for (int k = 0; k < ND; ++k)
+                                if (lane * ND + k < 16)
+                                    sg[ND * lane + k] = w[k];
                         }
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                         __builtin_amdgcn_wave_barrier();
@@ -847,26 +891,26 @@ __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ dg
                     }
                     rec.data_size = (uint16_t)dsize;
                     if (data_at >= 0) {
-                        uint32_t pay[8];
-                        shift_down_bytes(w, (uint32_t)data_at, pay);
+                        uint32_t pay[ND];
+                        shift_down_bytes<B>(w, (uint32_t)data_at, pay);
 #pragma unroll
-                        for (int k = 0; k < 8; ++k)
-                            pay[k] &= len_mask(k, lane, dsize);
-                        store_slot(slot, stride, lane, pay);
+                        for (int k = 0; k < ND; ++k)
+                            pay[k] &= len_mask<B>(k, lane, dsize);
+                        store_slot<B>(slot, stride, lane, pay);
                     }
                 }
             }
             write_rec(recs + d, rec, lane);
             if (data_at < 0)
-                store_slot(slot, stride, lane, z);
-                   });
+                store_slot<B>(slot, stride, lane, z);
+                       });
 }
 
 // Persistent grid: exactly the blocks that are resident at once (occupancy
 // from the kernel's registers / LDS x CUs), so no block waits for a second
-// round; fewer when the batch is small.
-template <class K>
-uint32_t grid_for(K kernel, uint32_t count)
+// round; fewer when the batch is small.  TAG: one cache per kernel instance.
+template <int TAG>
+uint32_t grid_for(const void* kernel, uint32_t count)
 {
     static int resident = 0; // blocks per device, per kernel
     if (!resident) {
@@ -882,6 +926,9 @@ uint32_t grid_for(K kernel, uint32_t count)
     return blocks < (uint32_t)resident ? (blocks ? blocks : 1u) : (uint32_t)resident;
 }
 
+// lane width: 20 bytes while a wave of them covers the slot, else 32
+inline bool narrow(uint32_t dstride) { return dstride <= (uint32_t)(kWave * 20); }
+
 } // namespace
 
 extern "C" {
@@ -891,9 +938,13 @@ int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacit
                                const rfec_fec_stamp* stamps, const uint32_t* order, uint32_t dstride,
                                uint8_t* dgram, uint16_t* dlen, void* stream)
 {
-    hipLaunchKernelGGL(k_frame_fec, dim3(grid_for(k_frame_fec, count)), dim3(kBlock), 0,
-                       reinterpret_cast<hipStream_t>(stream), parity, meta, fec_size, status, stamps, order, dgram,
-                       dlen, count, stride, capacity, dstride);
+    hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
+    if (narrow(dstride))
+        hipLaunchKernelGGL(k_frame_fec<20>, dim3(grid_for<0>((const void*)k_frame_fec<20>, count)), dim3(kBlock), 0, sm,
+                           parity, meta, fec_size, status, stamps, order, dgram, dlen, count, stride, capacity, dstride);
+    else
+        hipLaunchKernelGGL(k_frame_fec<32>, dim3(grid_for<1>((const void*)k_frame_fec<32>, count)), dim3(kBlock), 0, sm,
+                           parity, meta, fec_size, status, stamps, order, dgram, dlen, count, stride, capacity, dstride);
     return (int)hipGetLastError();
 }
 
@@ -901,17 +952,26 @@ int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacit
                                const rfec_hdr* hdr, const rfec_seg_stamp* stamps, const uint32_t* order,
                                uint32_t dstride, uint8_t* dgram, uint16_t* dlen, void* stream)
 {
-    hipLaunchKernelGGL(k_frame_seg, dim3(grid_for(k_frame_seg, count)), dim3(kBlock), 0,
-                       reinterpret_cast<hipStream_t>(stream), shards, hdr, stamps, order, dgram, dlen, count, stride,
-                       capacity, dstride);
+    hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
+    if (narrow(dstride))
+        hipLaunchKernelGGL(k_frame_seg<20>, dim3(grid_for<2>((const void*)k_frame_seg<20>, count)), dim3(kBlock), 0, sm,
+                           shards, hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride);
+    else
+        hipLaunchKernelGGL(k_frame_seg<32>, dim3(grid_for<3>((const void*)k_frame_seg<32>, count)), dim3(kBlock), 0, sm,
+                           shards, hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride);
     return (int)hipGetLastError();
 }
 
 int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
                            uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload, void* stream)
 {
-    hipLaunchKernelGGL(k_parse, dim3(grid_for(k_parse, n)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), dgram,
-                       dlen, recs, payload, n, dstride, stride, capacity);
+    hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
+    if (narrow(dstride))
+        hipLaunchKernelGGL(k_parse<20>, dim3(grid_for<4>((const void*)k_parse<20>, n)), dim3(kBlock), 0, sm, dgram,
+                           dlen, recs, payload, n, dstride, stride, capacity);
+    else
+        hipLaunchKernelGGL(k_parse<32>, dim3(grid_for<5>((const void*)k_parse<32>, n)), dim3(kBlock), 0, sm, dgram,
+                           dlen, recs, payload, n, dstride, stride, capacity);
     return (int)hipGetLastError();
 }
 
