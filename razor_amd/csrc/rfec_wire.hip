@@ -224,13 +224,26 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
 constexpr int kAuxNT = 2; // gfx950 cache-policy bits: nt
 
 // NX dwords at byte offset `off` (a multiple of 4, may be negative) of the
-// range r; dwords outside the range read as 0 (a negative offset wraps past it)
+// range r, as 16-byte loads plus a tail (dword-aligned multi-dword buffer
+// accesses); dwords outside the range read as 0 (a negative offset wraps past it)
 template <int NX>
 __device__ __forceinline__ void load_dwords(const __amdgpu_buffer_rsrc_t r, int off, uint32_t (&x)[NX])
 {
 #pragma unroll
-    for (int k = 0; k < NX; ++k)
+    for (int k = 0; k + 4 <= NX; k += 4) {
+        const v4u v = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)(off + 4 * k), 0, kAuxNT));
+        x[k] = v[0], x[k + 1] = v[1], x[k + 2] = v[2], x[k + 3] = v[3];
+    }
+    constexpr int k = NX & ~3;
+    if constexpr (NX - k == 3) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (uint32_t)(off + 4 * k), 0, kAuxNT);
+        x[k] = v[0], x[k + 1] = v[1], x[k + 2] = v[2];
+    } else if constexpr (NX - k == 2) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)(off + 4 * k), 0, kAuxNT);
+        x[k] = v[0], x[k + 1] = v[1];
+    } else if constexpr (NX - k == 1) {
         x[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)(off + 4 * k), 0, kAuxNT);
+    }
 }
 
 // out[k] = dword k of the window x shifted down by SH bytes (k < ND)
@@ -256,16 +269,20 @@ __device__ __forceinline__ uint32_t len_mask(int k, uint32_t lane, uint32_t nb)
     return lane < lq ? ~0u : (lane == lq ? ck : 0u);
 }
 
-// a lane's B bytes to [B lane, B lane + B) of a slot of slot_bytes (range
-// checked per dword: dwords past the slot are dropped)
+// a lane's B bytes to [B lane, B lane + B) of a slot of slot_bytes (16-byte
+// stores plus a dword; range-checked: nothing lands past the slot)
 template <int B>
 __device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t slot_bytes, uint32_t lane,
                                            const uint32_t* w)
 {
     const __amdgpu_buffer_rsrc_t r = rsrc(slot, slot_bytes);
 #pragma unroll
-    for (int k = 0; k < B / 4; ++k)
-        __builtin_amdgcn_raw_buffer_store_b32(w[k], r, B * lane + 4 * k, 0, kAuxNT);
+    for (int k = 0; k + 4 <= B / 4; k += 4)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int,
+                                                                  v4u{w[k], w[k + 1], w[k + 2], w[k + 3]}),
+                                               r, B * lane + 4 * k, 0, kAuxNT);
+    if constexpr ((B / 4) % 4 == 1)
+        __builtin_amdgcn_raw_buffer_store_b32(w[B / 4 - 1], r, B * lane + B - 4, 0, kAuxNT);
 }
 
 // Header bytes at compile-time positions (big-endian fields, cf_stream.c:366-385)
