@@ -223,27 +223,45 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
 }
 constexpr int kAuxNT = 2; // gfx950 cache-policy bits: nt
 
-// NX dwords at byte offset `off` (a multiple of 4, may be negative) of the
-// range r, as 16-byte loads plus a tail (dword-aligned multi-dword buffer
-// accesses); dwords outside the range read as 0 (a negative offset wraps past it)
-template <int NX>
-__device__ __forceinline__ void load_dwords(const __amdgpu_buffer_rsrc_t r, int off, uint32_t (&x)[NX])
+// NX dwords at byte offset `off` (a multiple of 4, may be negative) of a
+// range of `bytes` at r; dwords outside the range read as 0.  16-byte loads
+// plus a tail at dword-aligned offsets; the hardware range-checks a buffer
+// access as a whole (one that straddles either end of the range reads 0), so
+// the at most two lanes whose accesses straddle an end load dword by dword.
+template <int N>
+__device__ __forceinline__ void load_piece(const __amdgpu_buffer_rsrc_t r, int o, uint32_t bytes, uint32_t* x)
 {
+    const bool whole = (o >= 0 && o + 4 * N <= (int)bytes) || o + 4 * N <= 0 || o >= (int)bytes;
+    if (whole) {
+        if constexpr (N == 4) {
+            const v4u v = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)o, 0, kAuxNT));
+            x[0] = v[0], x[1] = v[1], x[2] = v[2], x[3] = v[3];
+        } else if constexpr (N == 3) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (uint32_t)o, 0, kAuxNT);
+            x[0] = v[0], x[1] = v[1], x[2] = v[2];
+        } else if constexpr (N == 2) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)o, 0, kAuxNT);
+            x[0] = v[0], x[1] = v[1];
+        } else {
+            x[0] = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)o, 0, kAuxNT);
+        }
+    } else {
 #pragma unroll
-    for (int k = 0; k + 4 <= NX; k += 4) {
-        const v4u v = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)(off + 4 * k), 0, kAuxNT));
-        x[k] = v[0], x[k + 1] = v[1], x[k + 2] = v[2], x[k + 3] = v[3];
+        for (int k = 0; k < N; ++k)
+            x[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)(o + 4 * k), 0, kAuxNT);
     }
+}
+
+template <int NX>
+__device__ __forceinline__ void load_dwords(const uint8_t* base, uint32_t bytes, int off, uint32_t (&x)[NX])
+{
+    const __amdgpu_buffer_rsrc_t r = rsrc(base, bytes);
+#pragma unroll
+    for (int k = 0; k + 4 <= NX; k += 4)
+        load_piece<4>(r, off + 4 * k, bytes, x + k);
     constexpr int k = NX & ~3;
-    if constexpr (NX - k == 3) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (uint32_t)(off + 4 * k), 0, kAuxNT);
-        x[k] = v[0], x[k + 1] = v[1], x[k + 2] = v[2];
-    } else if constexpr (NX - k == 2) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)(off + 4 * k), 0, kAuxNT);
-        x[k] = v[0], x[k + 1] = v[1];
-    } else if constexpr (NX - k == 1) {
-        x[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)(off + 4 * k), 0, kAuxNT);
-    }
+    if constexpr (NX - k > 0)
+        load_piece<NX - k>(r, off + 4 * k, bytes, x + k);
 }
 
 // out[k] = dword k of the window x shifted down by SH bytes (k < ND)
@@ -270,17 +288,25 @@ __device__ __forceinline__ uint32_t len_mask(int k, uint32_t lane, uint32_t nb)
 }
 
 // a lane's B bytes to [B lane, B lane + B) of a slot of slot_bytes (16-byte
-// stores plus a dword; range-checked: nothing lands past the slot)
+// stores plus a dword; nothing lands past the slot: a lane whose 16-byte
+// store would straddle the slot end stores dword by dword, see load_piece)
 template <int B>
 __device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t slot_bytes, uint32_t lane,
                                            const uint32_t* w)
 {
     const __amdgpu_buffer_rsrc_t r = rsrc(slot, slot_bytes);
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-    for (int k = 0; k + 4 <= B / 4; k += 4)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int,
-                                                                  v4u{w[k], w[k + 1], w[k + 2], w[k + 3]}),
-                                               r, B * lane + 4 * k, 0, kAuxNT);
+    for (int k = 0; k + 4 <= B / 4; k += 4) {
+        const uint32_t o = B * lane + 4 * k;
+        if (o + 16 <= slot_bytes || o >= slot_bytes) {
+            __builtin_amdgcn_raw_buffer_store_b128(u4{w[k], w[k + 1], w[k + 2], w[k + 3]}, r, o, 0, kAuxNT);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                __builtin_amdgcn_raw_buffer_store_b32(w[k + q], r, o + 4 * q, 0, kAuxNT);
+        }
+    }
     if constexpr ((B / 4) % 4 == 1)
         __builtin_amdgcn_raw_buffer_store_b32(w[B / 4 - 1], r, B * lane + B - 4, 0, kAuxNT);
 }
@@ -447,7 +473,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
     ping_pong<Pre<ND + 1>>(d, count, nw,
                            [&](uint32_t dd, Pre<ND + 1>& P) {
                                P.f = load_fec_fields(stamps, meta, fsize, status, dd, lane);
-                               load_dwords<ND + 1>(rsrc(parity + (size_t)dd * stride, range), off, P.x);
+                               load_dwords<ND + 1>(parity + (size_t)dd * stride, range, off, P.x);
                            },
                            [&](const Pre<ND + 1>& P, uint32_t d) {
             const uint32_t o = order ? order[d] : d; // output slot
@@ -542,7 +568,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
     ping_pong<Pre<ND + 2>>(d, count, nw,
                            [&](uint32_t dd, Pre<ND + 2>& P) {
                                P.f = load_seg_fields(hdr, stamps, dd, lane);
-                               load_dwords<ND + 2>(rsrc(shards + (size_t)dd * stride, range), off, P.x);
+                               load_dwords<ND + 2>(shards + (size_t)dd * stride, range, off, P.x);
                            },
                            [&](const Pre<ND + 2>& P, uint32_t d) {
             const uint32_t o = order ? order[d] : d; // output slot
@@ -743,7 +769,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ dg
     ping_pong<Pre<ND>>(d, n, nw,
                        [&](uint32_t dd, Pre<ND>& P) {
                            P.f = __builtin_amdgcn_raw_buffer_load_b16(rsrc(dlen + dd, 2), 2u * lane, 0, kAuxNT);
-                           load_dwords<ND>(rsrc(dgram + (size_t)dd * dstride, dstride), B * (int)lane, P.x);
+                           load_dwords<ND>(dgram + (size_t)dd * dstride, dstride, B * (int)lane, P.x);
                        },
                        [&](const Pre<ND>& P, uint32_t d) {
             uint8_t* slot = payload + (size_t)d * stride;
