@@ -223,45 +223,45 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
 }
 constexpr int kAuxNT = 2; // gfx950 cache-policy bits: nt
 
-// NX dwords at byte offset `off` (a multiple of 4, may be negative) of a
-// range of `bytes` at r; dwords outside the range read as 0.  16-byte loads
-// plus a tail at dword-aligned offsets; the hardware range-checks a buffer
-// access as a whole (one that straddles either end of the range reads 0), so
-// the at most two lanes whose accesses straddle an end load dword by dword.
-template <int N>
-__device__ __forceinline__ void load_piece(const __amdgpu_buffer_rsrc_t r, int o, uint32_t bytes, uint32_t* x)
+// A lane window of NX dwords at byte offset `off` (a multiple of 4, may be
+// negative) of a range of `bytes` (a multiple of 16) at base; dwords outside
+// the range read as 0.  Loaded as whole 16-byte chunks at 16-byte offsets --
+// such a chunk is either inside the range or outside it (the hardware
+// range-checks a buffer access as a whole) -- into Win::c; the window starts
+// DW = (off / 4) mod 4 dwords into the first chunk (always 0 when B is a
+// multiple of 16), selected per lane by win_dwords once the loads are needed.
+template <int B, int NX>
+struct Win {
+    static constexpr bool ALIGNED = B % 16 == 0;
+    static constexpr int NC = ALIGNED ? (NX + 3) / 4 : (NX + 6) / 4;
+    uint32_t c[4 * NC];
+};
+
+template <int B, int NX>
+__device__ __forceinline__ void load_window(const uint8_t* base, uint32_t bytes, int off, Win<B, NX>& w)
 {
-    const bool whole = (o >= 0 && o + 4 * N <= (int)bytes) || o + 4 * N <= 0 || o >= (int)bytes;
-    if (whole) {
-        if constexpr (N == 4) {
-            const v4u v = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)o, 0, kAuxNT));
-            x[0] = v[0], x[1] = v[1], x[2] = v[2], x[3] = v[3];
-        } else if constexpr (N == 3) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (uint32_t)o, 0, kAuxNT);
-            x[0] = v[0], x[1] = v[1], x[2] = v[2];
-        } else if constexpr (N == 2) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)o, 0, kAuxNT);
-            x[0] = v[0], x[1] = v[1];
-        } else {
-            x[0] = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)o, 0, kAuxNT);
-        }
-    } else {
+    const __amdgpu_buffer_rsrc_t r = rsrc(base, bytes);
+    const int a = off >> 4; // floor
 #pragma unroll
-        for (int k = 0; k < N; ++k)
-            x[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)(o + 4 * k), 0, kAuxNT);
+    for (int i = 0; i < Win<B, NX>::NC; ++i) {
+        const v4u v = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)((a + i) * 16), 0, kAuxNT));
+        w.c[4 * i] = v[0], w.c[4 * i + 1] = v[1], w.c[4 * i + 2] = v[2], w.c[4 * i + 3] = v[3];
     }
 }
 
-template <int NX>
-__device__ __forceinline__ void load_dwords(const uint8_t* base, uint32_t bytes, int off, uint32_t (&x)[NX])
+template <int B, int NX>
+__device__ __forceinline__ void win_dwords(const Win<B, NX>& w, int off, uint32_t (&x)[NX])
 {
-    const __amdgpu_buffer_rsrc_t r = rsrc(base, bytes);
+    if constexpr (Win<B, NX>::ALIGNED) {
 #pragma unroll
-    for (int k = 0; k + 4 <= NX; k += 4)
-        load_piece<4>(r, off + 4 * k, bytes, x + k);
-    constexpr int k = NX & ~3;
-    if constexpr (NX - k > 0)
-        load_piece<NX - k>(r, off + 4 * k, bytes, x + k);
+        for (int i = 0; i < NX; ++i)
+            x[i] = w.c[i];
+    } else {
+        const uint32_t dw = ((uint32_t)off >> 2) & 3u;
+#pragma unroll
+        for (int i = 0; i < NX; ++i)
+            x[i] = dw == 0 ? w.c[i] : (dw == 1 ? w.c[i + 1] : (dw == 2 ? w.c[i + 2] : w.c[i + 3]));
+    }
 }
 
 // out[k] = dword k of the window x shifted down by SH bytes (k < ND)
@@ -439,10 +439,10 @@ __device__ __forceinline__ void ping_pong(uint32_t d, uint32_t count, uint32_t n
     }
 }
 
-template <int NX>
+template <int B, int NX>
 struct Pre {
-    uint32_t x[NX]; // payload window
-    uint32_t f;     // per-datagram fields, one dword per lane
+    Win<B, NX> w; // payload window
+    uint32_t f;   // per-datagram fields, one dword per lane
 };
 
 // Lane j's window starts 48 (FEC) / 32 (SEG) bytes before the source of its
@@ -470,12 +470,12 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
     uint32_t d = wave_id();
     if (d >= count)
         return;
-    ping_pong<Pre<ND + 1>>(d, count, nw,
-                           [&](uint32_t dd, Pre<ND + 1>& P) {
-                               P.f = load_fec_fields(stamps, meta, fsize, status, dd, lane);
-                               load_dwords<ND + 1>(parity + (size_t)dd * stride, range, off, P.x);
-                           },
-                           [&](const Pre<ND + 1>& P, uint32_t d) {
+    ping_pong<Pre<B, ND + 1>>(d, count, nw,
+                              [&](uint32_t dd, Pre<B, ND + 1>& P) {
+                                  P.f = load_fec_fields(stamps, meta, fsize, status, dd, lane);
+                                  load_window<B, ND + 1>(parity + (size_t)dd * stride, range, off, P.w);
+                              },
+                              [&](const Pre<B, ND + 1>& P, uint32_t d) {
             const uint32_t o = order ? order[d] : d; // output slot
             uint8_t* slot = dgram + (size_t)o * dstride;
             const uint32_t L = fld(P.f, 11);
@@ -506,11 +506,12 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
                 put<40, 1>(H, (m4 >> 8) & 0xffu);
                 put<41, 2>(H, m4 >> 16);
                 put<43, 2>(H, L); // mach_data_write length (cf_stream.c:328-337)
-                uint32_t pay[ND];
-                funnel<ND, 3>(P.x, pay); // window [B j - 48, ...) -> bytes [B j - 45, ...)
+                uint32_t pay[ND], x[ND + 1];
+                win_dwords(P.w, off, x);
+                funnel<ND, 3>(x, pay); // window [B j - 48, ...) -> bytes [B j - 45, ...)
                 finish_frame<B>(T, H, 45 + L, pay, lane, slot, dstride, dlen + o);
             }
-                           });
+                              });
 }
 
 // SIM_SEG header, one of 8 layouts (sim_proto.inl:83-125): PW / FW = 4-byte
@@ -565,12 +566,12 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
     uint32_t d = wave_id();
     if (d >= count)
         return;
-    ping_pong<Pre<ND + 2>>(d, count, nw,
-                           [&](uint32_t dd, Pre<ND + 2>& P) {
-                               P.f = load_seg_fields(hdr, stamps, dd, lane);
-                               load_dwords<ND + 2>(shards + (size_t)dd * stride, range, off, P.x);
-                           },
-                           [&](const Pre<ND + 2>& P, uint32_t d) {
+    ping_pong<Pre<B, ND + 2>>(d, count, nw,
+                              [&](uint32_t dd, Pre<B, ND + 2>& P) {
+                                  P.f = load_seg_fields(hdr, stamps, dd, lane);
+                                  load_window<B, ND + 2>(shards + (size_t)dd * stride, range, off, P.w);
+                              },
+                              [&](const Pre<B, ND + 2>& P, uint32_t d) {
             const uint32_t o = order ? order[d] : d; // output slot
             uint8_t* slot = dgram + (size_t)o * dstride;
             rfec_hdr h;
@@ -602,21 +603,22 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                 Hdr H = {};
                 const uint32_t layout = (h.seq > 65535u ? 4u : 0u) | (h.fid > 65535u ? 2u : 0u) |
                                         (h.total > 255u ? 1u : 0u);
-                uint32_t hs, pay[ND];
+                uint32_t hs, pay[ND], x[ND + 2];
+                win_dwords(P.w, off, x);
                 // window [B j - 32, ...) shifted by 32 - hs bytes
                 switch (layout) {
-                case 0: hs = seg_header<false, false, false>(H, h, s); funnel<ND, 6>(P.x, pay); break;
-                case 1: hs = seg_header<false, false, true>(H, h, s); funnel<ND, 4>(P.x, pay); break;
-                case 2: hs = seg_header<false, true, false>(H, h, s); funnel<ND, 4>(P.x, pay); break;
-                case 3: hs = seg_header<false, true, true>(H, h, s); funnel<ND, 2>(P.x, pay); break;
-                case 4: hs = seg_header<true, false, false>(H, h, s); funnel<ND, 4>(P.x, pay); break;
-                case 5: hs = seg_header<true, false, true>(H, h, s); funnel<ND, 2>(P.x, pay); break;
-                case 6: hs = seg_header<true, true, false>(H, h, s); funnel<ND, 2>(P.x, pay); break;
-                default: hs = seg_header<true, true, true>(H, h, s); funnel<ND, 0>(P.x, pay); break;
+                case 0: hs = seg_header<false, false, false>(H, h, s); funnel<ND, 6>(x, pay); break;
+                case 1: hs = seg_header<false, false, true>(H, h, s); funnel<ND, 4>(x, pay); break;
+                case 2: hs = seg_header<false, true, false>(H, h, s); funnel<ND, 4>(x, pay); break;
+                case 3: hs = seg_header<false, true, true>(H, h, s); funnel<ND, 2>(x, pay); break;
+                case 4: hs = seg_header<true, false, false>(H, h, s); funnel<ND, 4>(x, pay); break;
+                case 5: hs = seg_header<true, false, true>(H, h, s); funnel<ND, 2>(x, pay); break;
+                case 6: hs = seg_header<true, true, false>(H, h, s); funnel<ND, 2>(x, pay); break;
+                default: hs = seg_header<true, true, true>(H, h, s); funnel<ND, 0>(x, pay); break;
                 }
                 finish_frame<B>(T, H, hs + L, pay, lane, slot, dstride, dlen + o);
             }
-                           });
+                              });
 }
 
 // ---------------------------------------------------------------------------
@@ -766,12 +768,12 @@ __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ dg
     uint32_t d = wave_id();
     if (d >= n)
         return;
-    ping_pong<Pre<ND>>(d, n, nw,
-                       [&](uint32_t dd, Pre<ND>& P) {
-                           P.f = __builtin_amdgcn_raw_buffer_load_b16(rsrc(dlen + dd, 2), 2u * lane, 0, kAuxNT);
-                           load_dwords<ND>(dgram + (size_t)dd * dstride, dstride, B * (int)lane, P.x);
-                       },
-                       [&](const Pre<ND>& P, uint32_t d) {
+    ping_pong<Pre<B, ND>>(d, n, nw,
+                          [&](uint32_t dd, Pre<B, ND>& P) {
+                              P.f = __builtin_amdgcn_raw_buffer_load_b16(rsrc(dlen + dd, 2), 2u * lane, 0, kAuxNT);
+                              load_window<B, ND>(dgram + (size_t)dd * dstride, dstride, B * (int)lane, P.w);
+                          },
+                          [&](const Pre<B, ND>& P, uint32_t d) {
             uint8_t* slot = payload + (size_t)d * stride;
             const uint32_t len = fld(P.f, 0);
             rfec_wire_rec rec = {};
@@ -781,9 +783,10 @@ __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ dg
             if (len >= 4 && len <= dstride && len <= (uint32_t)(kWave * B)) {
                 // datagram bytes [B j, B j + B), zero from `len` on
                 uint32_t w[ND], m[ND];
+                win_dwords(P.w, B * (int)lane, w);
 #pragma unroll
                 for (int k = 0; k < ND; ++k) {
-                    w[k] = P.x[k] & len_mask<B>(k, lane, len);
+                    w[k] &= len_mask<B>(k, lane, len);
                     m[k] = w[k] & len_mask<B>(k, lane, len - 4);
                 }
                 // CRC over [0, len-4) against the big-endian trailer (sim_proto.c:21-37)
@@ -946,7 +949,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ dg
             write_rec(recs + d, rec, lane);
             if (data_at < 0)
                 store_slot<B>(slot, stride, lane, z);
-                       });
+                          });
 }
 
 // Persistent grid: exactly the blocks that are resident at once (occupancy
