@@ -224,43 +224,71 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
 constexpr int kAuxNT = 2; // gfx950 cache-policy bits: nt
 
 // A lane window of NX dwords at byte offset `off` (a multiple of 4, may be
-// negative) of a range of `bytes` (a multiple of 16) at base; dwords outside
-// the range read as 0.  Loaded as whole 16-byte chunks at 16-byte offsets --
-// such a chunk is either inside the range or outside it (the hardware
-// range-checks a buffer access as a whole) -- into Win::c; the window starts
-// DW = (off / 4) mod 4 dwords into the first chunk (always 0 when B is a
-// multiple of 16), selected per lane by win_dwords once the loads are needed.
-template <int B, int NX>
+// negative) of a range of `bytes` at base; dwords outside the range read as
+// 0.  16-byte loads plus a tail at dword-aligned offsets.  An access whose
+// offset is negative wraps past the range and reads 0 as a whole, so the
+// one lane of the frame kernels whose first 16-byte load would start less
+// than 16 bytes before the slot (FIX_LANE, S dwords before it) loads from 0
+// instead and win_dwords shifts its window back by S dwords.
+template <int NX>
 struct Win {
-    static constexpr bool ALIGNED = B % 16 == 0;
-    static constexpr int NC = ALIGNED ? (NX + 3) / 4 : (NX + 6) / 4;
-    uint32_t c[4 * NC];
+    uint32_t c[NX];
 };
 
-template <int B, int NX>
-__device__ __forceinline__ void load_window(const uint8_t* base, uint32_t bytes, int off, Win<B, NX>& w)
+template <int NX>
+__device__ __forceinline__ void load_window(const uint8_t* base, uint32_t bytes, int off, Win<NX>& w)
 {
     const __amdgpu_buffer_rsrc_t r = rsrc(base, bytes);
-    const int a = off >> 4; // floor
 #pragma unroll
-    for (int i = 0; i < Win<B, NX>::NC; ++i) {
-        const v4u v = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)((a + i) * 16), 0, kAuxNT));
-        w.c[4 * i] = v[0], w.c[4 * i + 1] = v[1], w.c[4 * i + 2] = v[2], w.c[4 * i + 3] = v[3];
+    for (int k = 0; k + 4 <= NX; k += 4) {
+        const v4u v = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, (uint32_t)(off + 4 * k), 0, kAuxNT));
+        w.c[k] = v[0], w.c[k + 1] = v[1], w.c[k + 2] = v[2], w.c[k + 3] = v[3];
+    }
+    constexpr int k = NX & ~3;
+    if constexpr (NX - k == 3) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (uint32_t)(off + 4 * k), 0, kAuxNT);
+        w.c[k] = v[0], w.c[k + 1] = v[1], w.c[k + 2] = v[2];
+    } else if constexpr (NX - k == 2) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)(off + 4 * k), 0, kAuxNT);
+        w.c[k] = v[0], w.c[k + 1] = v[1];
+    } else if constexpr (NX - k == 1) {
+        w.c[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)(off + 4 * k), 0, kAuxNT);
     }
 }
 
-template <int B, int NX>
-__device__ __forceinline__ void win_dwords(const Win<B, NX>& w, int off, uint32_t (&x)[NX])
+// lane windows at B j - SRC: the lane whose offset lies in (-16, 0) and is
+// not a multiple of 16 (-1 when none), and how many dwords before 0 it starts
+template <int B, int SRC>
+constexpr int fix_lane()
 {
-    if constexpr (Win<B, NX>::ALIGNED) {
+    for (int l = 0; l < 4; ++l) {
+        const int o = B * l - SRC;
+        if (o > -16 && o < 0 && o % 16 != 0)
+            return l;
+    }
+    return -1;
+}
+template <int B, int SRC>
+__device__ __forceinline__ int win_offset(uint32_t lane)
+{
+    constexpr int FL = fix_lane<B, SRC>();
+    const int off = B * (int)lane - SRC;
+    if constexpr (FL >= 0)
+        return lane == (uint32_t)FL ? 0 : off;
+    else
+        return off;
+}
+template <int B, int SRC, int NX>
+__device__ __forceinline__ void win_dwords(const Win<NX>& w, uint32_t lane, uint32_t (&x)[NX])
+{
+    constexpr int FL = fix_lane<B, SRC>();
+    constexpr int S = FL >= 0 ? (SRC - B * FL) / 4 : 0;
 #pragma unroll
-        for (int i = 0; i < NX; ++i)
+    for (int i = 0; i < NX; ++i) {
+        if constexpr (FL >= 0)
+            x[i] = lane == (uint32_t)FL ? (i >= S ? w.c[i - S] : 0u) : w.c[i];
+        else
             x[i] = w.c[i];
-    } else {
-        const uint32_t dw = ((uint32_t)off >> 2) & 3u;
-#pragma unroll
-        for (int i = 0; i < NX; ++i)
-            x[i] = dw == 0 ? w.c[i] : (dw == 1 ? w.c[i + 1] : (dw == 2 ? w.c[i + 2] : w.c[i + 3]));
     }
 }
 
@@ -439,10 +467,10 @@ __device__ __forceinline__ void ping_pong(uint32_t d, uint32_t count, uint32_t n
     }
 }
 
-template <int B, int NX>
+template <int NX>
 struct Pre {
-    Win<B, NX> w; // payload window
-    uint32_t f;   // per-datagram fields, one dword per lane
+    Win<NX> w;  // payload window
+    uint32_t f; // per-datagram fields, one dword per lane
 };
 
 // Lane j's window starts 48 (FEC) / 32 (SEG) bytes before the source of its
@@ -466,16 +494,16 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
     const uint32_t range = (capacity + 15u) & ~15u;
-    const int off = B * (int)lane - 48;
+    const int off = win_offset<B, 48>(lane);
     uint32_t d = wave_id();
     if (d >= count)
         return;
-    ping_pong<Pre<B, ND + 1>>(d, count, nw,
-                              [&](uint32_t dd, Pre<B, ND + 1>& P) {
+    ping_pong<Pre<ND + 1>>(d, count, nw,
+                              [&](uint32_t dd, Pre<ND + 1>& P) {
                                   P.f = load_fec_fields(stamps, meta, fsize, status, dd, lane);
-                                  load_window<B, ND + 1>(parity + (size_t)dd * stride, range, off, P.w);
+                                  load_window<ND + 1>(parity + (size_t)dd * stride, range, off, P.w);
                               },
-                              [&](const Pre<B, ND + 1>& P, uint32_t d) {
+                              [&](const Pre<ND + 1>& P, uint32_t d) {
             const uint32_t o = order ? order[d] : d; // output slot
             uint8_t* slot = dgram + (size_t)o * dstride;
             const uint32_t L = fld(P.f, 11);
@@ -507,7 +535,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
                 put<41, 2>(H, m4 >> 16);
                 put<43, 2>(H, L); // mach_data_write length (cf_stream.c:328-337)
                 uint32_t pay[ND], x[ND + 1];
-                win_dwords(P.w, off, x);
+                win_dwords<B, 48>(P.w, lane, x);
                 funnel<ND, 3>(x, pay); // window [B j - 48, ...) -> bytes [B j - 45, ...)
                 finish_frame<B>(T, H, 45 + L, pay, lane, slot, dstride, dlen + o);
             }
@@ -562,16 +590,16 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
     const uint32_t range = (capacity + 15u) & ~15u;
-    const int off = B * (int)lane - 32; // header sizes 26..32
+    const int off = win_offset<B, 32>(lane); // header sizes 26..32
     uint32_t d = wave_id();
     if (d >= count)
         return;
-    ping_pong<Pre<B, ND + 2>>(d, count, nw,
-                              [&](uint32_t dd, Pre<B, ND + 2>& P) {
+    ping_pong<Pre<ND + 2>>(d, count, nw,
+                              [&](uint32_t dd, Pre<ND + 2>& P) {
                                   P.f = load_seg_fields(hdr, stamps, dd, lane);
-                                  load_window<B, ND + 2>(shards + (size_t)dd * stride, range, off, P.w);
+                                  load_window<ND + 2>(shards + (size_t)dd * stride, range, off, P.w);
                               },
-                              [&](const Pre<B, ND + 2>& P, uint32_t d) {
+                              [&](const Pre<ND + 2>& P, uint32_t d) {
             const uint32_t o = order ? order[d] : d; // output slot
             uint8_t* slot = dgram + (size_t)o * dstride;
             rfec_hdr h;
@@ -604,7 +632,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                 const uint32_t layout = (h.seq > 65535u ? 4u : 0u) | (h.fid > 65535u ? 2u : 0u) |
                                         (h.total > 255u ? 1u : 0u);
                 uint32_t hs, pay[ND], x[ND + 2];
-                win_dwords(P.w, off, x);
+                win_dwords<B, 32>(P.w, lane, x);
                 // window [B j - 32, ...) shifted by 32 - hs bytes
                 switch (layout) {
                 case 0: hs = seg_header<false, false, false>(H, h, s); funnel<ND, 6>(x, pay); break;
@@ -768,12 +796,12 @@ __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ dg
     uint32_t d = wave_id();
     if (d >= n)
         return;
-    ping_pong<Pre<B, ND>>(d, n, nw,
-                          [&](uint32_t dd, Pre<B, ND>& P) {
+    ping_pong<Pre<ND>>(d, n, nw,
+                          [&](uint32_t dd, Pre<ND>& P) {
                               P.f = __builtin_amdgcn_raw_buffer_load_b16(rsrc(dlen + dd, 2), 2u * lane, 0, kAuxNT);
-                              load_window<B, ND>(dgram + (size_t)dd * dstride, dstride, B * (int)lane, P.w);
+                              load_window<ND>(dgram + (size_t)dd * dstride, dstride, B * (int)lane, P.w);
                           },
-                          [&](const Pre<B, ND>& P, uint32_t d) {
+                          [&](const Pre<ND>& P, uint32_t d) {
             uint8_t* slot = payload + (size_t)d * stride;
             const uint32_t len = fld(P.f, 0);
             rfec_wire_rec rec = {};
@@ -783,7 +811,7 @@ __global__ __launch_bounds__(kBlock) void k_parse(const uint8_t* __restrict__ dg
             if (len >= 4 && len <= dstride && len <= (uint32_t)(kWave * B)) {
                 // datagram bytes [B j, B j + B), zero from `len` on
                 uint32_t w[ND], m[ND];
-                win_dwords(P.w, B * (int)lane, w);
+                win_dwords<B, 0>(P.w, lane, w);
 #pragma unroll
                 for (int k = 0; k < ND; ++k) {
                     w[k] &= len_mask<B>(k, lane, len);
