@@ -315,9 +315,9 @@ __device__ __forceinline__ uint32_t len_mask(int k, uint32_t lane, uint32_t nb)
     return lane < lq ? ~0u : (lane == lq ? ck : 0u);
 }
 
-// a lane's B bytes to [B lane, B lane + B) of a slot of slot_bytes (16-byte
-// stores plus a dword; nothing lands past the slot: a lane whose 16-byte
-// store would straddle the slot end stores dword by dword, see load_piece)
+// a lane's B bytes to [B lane, B lane + B) of a slot of slot_bytes: 16-byte
+// stores plus a dword, range-checked by the buffer descriptor (nothing lands
+// past the slot)
 template <int B>
 __device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t slot_bytes, uint32_t lane,
                                            const uint32_t* w)
@@ -325,16 +325,8 @@ __device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t 
     const __amdgpu_buffer_rsrc_t r = rsrc(slot, slot_bytes);
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-    for (int k = 0; k + 4 <= B / 4; k += 4) {
-        const uint32_t o = B * lane + 4 * k;
-        if (o + 16 <= slot_bytes || o >= slot_bytes) {
-            __builtin_amdgcn_raw_buffer_store_b128(u4{w[k], w[k + 1], w[k + 2], w[k + 3]}, r, o, 0, kAuxNT);
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                __builtin_amdgcn_raw_buffer_store_b32(w[k + q], r, o + 4 * q, 0, kAuxNT);
-        }
-    }
+    for (int k = 0; k + 4 <= B / 4; k += 4)
+        __builtin_amdgcn_raw_buffer_store_b128(u4{w[k], w[k + 1], w[k + 2], w[k + 3]}, r, B * lane + 4 * k, 0, kAuxNT);
     if constexpr ((B / 4) % 4 == 1)
         __builtin_amdgcn_raw_buffer_store_b32(w[B / 4 - 1], r, B * lane + B - 4, 0, kAuxNT);
 }
@@ -732,13 +724,14 @@ __device__ __forceinline__ uint32_t next_lane(uint32_t v)
 }
 
 // out lane j = datagram bytes [pos + B j, pos + B j + B) from the lane-wise
-// datagram w (pos wave-uniform, < 64): lanes j + q and j + q + 1, q = pos / B,
+// datagram w (pos wave-uniform, <= 45: the data field of a SIM_FEC starts at
+// byte 45, of a SIM_SEG at <= 34): lanes j + q and j + q + 1, q = pos / B,
 // brought over with DPP, then a funnel by the uniform remainder
 template <int B>
 __device__ __forceinline__ void shift_down_bytes(const uint32_t* w, uint32_t pos, uint32_t* out)
 {
     constexpr int ND = B / 4;
-    constexpr int QMAX = (63 + B - 1) / B; // q <= 63 / B
+    constexpr int QMAX = 45 / B;
     const uint32_t q = pos / B, r = pos - q * B;
     uint32_t x[2 * ND];
 #pragma unroll
