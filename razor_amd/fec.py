@@ -370,14 +370,21 @@ class Native:
                                               max_groups, C.byref(ng)), "rfec_sender_plan")
         return segs[:ns.value], groups[:ng.value]
 
-    def send_frames(self, st, frames, uid, dstride, max_segs=1 << 16, max_groups=1 << 14, max_parities=1 << 17):
-        """Frames -> (segs, groups, seg datagrams, seg lengths, fec datagrams, fec lengths, report)."""
+    def send_frames(self, st, frames, uid, dstride, max_segs=1 << 16, max_groups=1 << 14, max_parities=1 << 17,
+                    bufs=None):
+        """Frames -> (segs, groups, seg datagrams, seg lengths, fec datagrams, fec lengths, report).
+        bufs: optional (sdg, sdl, fdg, fdl) output arrays to reuse (e.g. views of
+        pinned memory from pinned_array), sized for max_segs / max_parities."""
         segs = np.zeros(max_segs, SEG_PLAN_DTYPE)
         groups = np.zeros(max_groups, GROUP_PLAN_DTYPE)
-        sdg = np.zeros((max_segs, dstride), np.uint8)
-        sdl = np.zeros(max_segs, np.uint16)
-        fdg = np.zeros((max_parities, dstride), np.uint8)
-        fdl = np.zeros(max_parities, np.uint16)
+        if bufs is None:
+            sdg = np.zeros((max_segs, dstride), np.uint8)
+            sdl = np.zeros(max_segs, np.uint16)
+            fdg = np.zeros((max_parities, dstride), np.uint8)
+            fdl = np.zeros(max_parities, np.uint16)
+        else:
+            sdg, sdl, fdg, fdl = bufs
+            assert sdg.shape[0] >= max_segs and fdg.shape[0] >= max_parities and sdg.shape[1] == dstride
         rep = rfec_send_report()
         self._check(self.lib.rfec_host_send_frames(st.ctypes.data, np.ascontiguousarray(frames).ctypes.data,
                                                    len(frames), uid, segs.ctypes.data, max_segs, groups.ctypes.data,
@@ -412,6 +419,18 @@ class Native:
                                                       outp.ctypes.data, max_out, C.byref(nout), C.byref(rep)),
                     "rfec_host_recv_datagrams")
         return out[:nout.value], outp[:nout.value], mts.value, rep, recs
+
+    def pinned_array(self, shape, dtype):
+        """A numpy array over rfec_pinned_alloc memory (freed with the array's keeper: keep `.base` alive)."""
+        dt = np.dtype(dtype)
+        n = int(np.prod(shape)) * dt.itemsize
+        p = self.lib.rfec_pinned_alloc(max(n, 1))
+        if not p:
+            raise RfecError(f"rfec_pinned_alloc({n}) failed: {self.last_error()}")
+        keeper = _Pinned(self, p, n)
+        arr = np.frombuffer((C.c_uint8 * n).from_address(p), dtype=dt).reshape(shape)
+        keeper.arr = arr
+        return arr, keeper
 
     def rx_session(self, stride, capacity):
         return RxSession(self, stride, capacity)
@@ -474,6 +493,17 @@ class Native:
     def _check(self, rc, what):
         if rc != 0:
             raise RfecError(f"{what} failed ({rc}): {self.last_error()}")
+
+
+class _Pinned:
+    def __init__(self, native, p, n):
+        self.native, self.p, self.n = native, p, n
+
+    def __del__(self):
+        try:
+            self.native.lib.rfec_pinned_free(self.p)
+        except Exception:
+            pass
 
 
 class RxSession:
