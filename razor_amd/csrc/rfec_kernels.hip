@@ -266,6 +266,83 @@ __global__ __launch_bounds__(kBlock) void k_encode_rows(const v4u* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// Encode, rows-of-COL, header work fused into the payload lanes (no meta
+// blocks at the head of the grid).  A group has 6R header duties -- 5R meta
+// dwords (line u / 5, dword u % 5: the XOR of that dword over the line's
+// members, flex_fec_xor.c:13-20, 37-44) and R sizes / statuses (max data_size,
+// :22-28) -- spread over its cd payload lanes: lane j takes duties j, j + cd,
+// ... (at most ND of them).  A lane issues its header loads first, then its
+// payload loads, so the header values (older in the in-order vmcnt) are
+// combined and stored without waiting for the payload.
+// ---------------------------------------------------------------------------
+template <int K, int COL, bool NTL, int NTS, int ND>
+__global__ __launch_bounds__(kBlock) void k_encode_rows_fm(const v4u* __restrict__ shards, v4u* __restrict__ parity,
+                                                           uint32_t total, uint32_t C, FastDiv divC, EncMeta E)
+{
+    constexpr int R = (K + COL - 1) / COL;
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= total)
+        return;
+    const uint32_t g = fdiv(t, divC);
+    const uint32_t j = t - g * divC.d;
+    const uint32_t cd = divC.d;
+    // header duties: loads
+    const uint32_t* h = E.hdr_dw + (size_t)g * K * 5;
+    uint32_t hv[ND][COL];
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+        const uint32_t u = j + d * cd;
+        const uint32_t l = u < 5u * R ? u / 5u : u - 5u * R;
+        const uint32_t c = u < 5u * R ? u - 5u * l : 4u; // data_size: the high half of dword 4
+#pragma unroll
+        for (int q = 0; q < COL; ++q) {
+            hv[d][q] = 0;
+            if (u < 6u * R && l * COL + q < (uint32_t)K)
+                hv[d][q] = h[(l * COL + q) * 5 + c];
+        }
+    }
+    // payload loads
+    v4u v[K];
+    const v4u* src = shards + (size_t)g * K * C + j;
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        v[i] = ld16<NTL>(src + (size_t)i * C);
+    // header duties: combine, store
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+        const uint32_t u = j + d * cd;
+        if (u >= 6u * R)
+            continue;
+        const uint32_t l = u < 5u * R ? u / 5u : u - 5u * R;
+        const uint32_t cnt = min((uint32_t)COL, (uint32_t)K - l * COL);
+        uint32_t x = 0, L = 0;
+#pragma unroll
+        for (int q = 0; q < COL; ++q) {
+            x ^= hv[d][q];
+            L = max(L, hv[d][q] >> 16);
+        }
+        const size_t out = (size_t)g * R + l;
+        if (u < 5u * R) {
+            E.meta_dw[out * 5 + (u - 5u * l)] = x;
+        } else {
+            E.fsize[out] = (uint16_t)L;
+            if (E.status)
+                E.status[out] = (cnt <= 1 || L > E.capacity) ? (int8_t)-1 : (int8_t)0;
+        }
+    }
+    v4u* dst = parity + (size_t)g * R * C + j;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        v4u acc = v[r * COL];
+#pragma unroll
+        for (int q = 1; q < COL; ++q)
+            if (r * COL + q < K)
+                acc ^= v[r * COL + q];
+        st16<NTS>(dst + (size_t)r * C, acc);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Encode payload, rows-of-COL, group-per-wave mapping.  Every wave covers
 // whole groups (gpw = max(1, 64 / cd) of them, NI items per lane): a slot's
 // last chunk and the next slot's first chunk, which share a 128-B line when
@@ -1034,6 +1111,25 @@ hipError_t launch_rows_gw(const EncLaunch& a, const GwGeom& g, uint32_t swz)
 template <int K, int COL, bool NTL, int NTS>
 hipError_t launch_rows_v(const EncLaunch& a, unsigned flags)
 {
+    constexpr int R = (K + COL - 1) / COL;
+    const uint32_t duties = (6u * R + a.cd - 1) / a.cd; // header duties per payload lane
+    if (!(flags & (RFEC_KFLAG_META_BLOCKS | RFEC_KFLAG_GROUP_WAVE | RFEC_KFLAG_ITEMS2 | RFEC_KFLAG_DIAG_NO_META)) &&
+        duties <= 4) {
+        const uint32_t C = a.stride / 16;
+        const uint32_t total = a.groups * a.cd;
+        const dim3 grid(blocks_for(total));
+#define RFEC_FM(ND)                                                                                               \
+    hipLaunchKernelGGL((k_encode_rows_fm<K, COL, NTL, NTS, ND>), grid, dim3(kBlock), 0, a.stream, a.s, a.p, total, C, \
+                       make_fastdiv(a.cd), a.E)
+        switch (duties) {
+        case 1: RFEC_FM(1); break;
+        case 2: RFEC_FM(2); break;
+        case 3: RFEC_FM(3); break;
+        default: RFEC_FM(4); break;
+        }
+#undef RFEC_FM
+        return hipGetLastError();
+    }
     if (flags & RFEC_KFLAG_GROUP_WAVE) {
         const GwGeom g = gw_geom(a.groups, a.cd);
         const uint32_t swz = (flags & RFEC_KFLAG_XCD_SWIZZLE) ? 1u : 0u;
