@@ -266,91 +266,6 @@ __global__ __launch_bounds__(kBlock) void k_encode_rows(const v4u* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
-// Encode, rows-of-COL, header work fused into the payload blocks (no meta
-// blocks at the head of the grid).  A block first issues one coalesced load
-// per lane (HL per lane at most) of the header records of the groups its
-// lanes cover, then every lane's payload loads; the records go to LDS (their
-// loads are older in the in-order vmcnt, so this waits for them only), and
-// after one barrier a group's 6R header duties -- 5R meta dwords (line u / 5,
-// dword u % 5: the XOR of that dword over the line's members,
-// flex_fec_xor.c:13-20, 37-44) and R sizes / statuses (max data_size,
-// :22-28) -- are taken by its payload lanes j, j + cd, ... (ND per lane at
-// most) out of LDS while the payload loads are in flight.
-// ---------------------------------------------------------------------------
-template <int K, int COL, bool NTL, int NTS, int ND, int HL>
-__global__ __launch_bounds__(kBlock) void k_encode_rows_fm(const v4u* __restrict__ shards, v4u* __restrict__ parity,
-                                                           uint32_t total, uint32_t C, FastDiv divC, EncMeta E)
-{
-    constexpr int R = (K + COL - 1) / COL;
-    __shared__ uint32_t hl[HL * kBlock];
-    const uint32_t cd = divC.d;
-    const uint32_t tb0 = blockIdx.x * kBlock;
-    const uint32_t gb0 = fdiv(tb0, divC), gb1 = fdiv(min(tb0 + kBlock, total) - 1, divC);
-    const uint32_t ndw = (gb1 - gb0 + 1) * K * 5; // <= HL * kBlock (host check)
-    const uint32_t* hsrc = E.hdr_dw + (size_t)gb0 * K * 5;
-    uint32_t hreg[HL];
-#pragma unroll
-    for (int i = 0; i < HL; ++i) {
-        const uint32_t x = threadIdx.x + i * kBlock;
-        hreg[i] = x < ndw ? hsrc[x] : 0u;
-    }
-    const uint32_t t = tb0 + threadIdx.x;
-    const bool on = t < total;
-    const uint32_t g = fdiv(on ? t : total - 1, divC);
-    const uint32_t j = (on ? t : total - 1) - g * cd;
-    v4u v[K];
-    const v4u* src = shards + (size_t)g * K * C + j;
-    if (on) {
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-            v[i] = ld16<NTL>(src + (size_t)i * C);
-    }
-#pragma unroll
-    for (int i = 0; i < HL; ++i)
-        hl[threadIdx.x + i * kBlock] = hreg[i];
-    __syncthreads();
-    if (!on)
-        return;
-    const uint32_t* h = hl + (g - gb0) * K * 5;
-#pragma unroll
-    for (int d = 0; d < ND; ++d) {
-        const uint32_t u = j + d * cd;
-        if (u >= 6u * R)
-            continue;
-        const uint32_t l = u < 5u * R ? u / 5u : u - 5u * R;
-        const uint32_t c = u < 5u * R ? u - 5u * l : 4u; // data_size: the high half of dword 4
-        const uint32_t cnt = min((uint32_t)COL, (uint32_t)K - l * COL);
-        uint32_t x = 0, L = 0;
-#pragma unroll
-        for (int q = 0; q < COL; ++q) {
-            if ((uint32_t)q < cnt) {
-                const uint32_t w = h[(l * COL + q) * 5 + c];
-                x ^= w;
-                L = max(L, w >> 16);
-            }
-        }
-        const size_t out = (size_t)g * R + l;
-        if (u < 5u * R) {
-            E.meta_dw[out * 5 + c] = x;
-        } else {
-            E.fsize[out] = (uint16_t)L;
-            if (E.status)
-                E.status[out] = (cnt <= 1 || L > E.capacity) ? (int8_t)-1 : (int8_t)0;
-        }
-    }
-    v4u* dst = parity + (size_t)g * R * C + j;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        v4u acc = v[r * COL];
-#pragma unroll
-        for (int q = 1; q < COL; ++q)
-            if (r * COL + q < K)
-                acc ^= v[r * COL + q];
-        st16<NTS>(dst + (size_t)r * C, acc);
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Encode payload, rows-of-COL, group-per-wave mapping.  Every wave covers
 // whole groups (gpw = max(1, 64 / cd) of them, NI items per lane): a slot's
 // last chunk and the next slot's first chunk, which share a 128-B line when
@@ -1119,24 +1034,6 @@ hipError_t launch_rows_gw(const EncLaunch& a, const GwGeom& g, uint32_t swz)
 template <int K, int COL, bool NTL, int NTS>
 hipError_t launch_rows_v(const EncLaunch& a, unsigned flags)
 {
-    constexpr int R = (K + COL - 1) / COL;
-    const uint32_t duties = (6u * R + a.cd - 1) / a.cd;               // header duties per payload lane
-    const uint32_t hdw = ((kBlock - 1) / a.cd + 2) * (uint32_t)K * 5u; // header dwords a block may cover
-    if (!(flags & (RFEC_KFLAG_META_BLOCKS | RFEC_KFLAG_GROUP_WAVE | RFEC_KFLAG_ITEMS2 | RFEC_KFLAG_DIAG_NO_META)) &&
-        duties <= 2 && hdw <= 2u * kBlock) {
-        const uint32_t C = a.stride / 16;
-        const uint32_t total = a.groups * a.cd;
-        const dim3 grid(blocks_for(total));
-#define RFEC_FM(ND, HL)                                                                                           \
-    hipLaunchKernelGGL((k_encode_rows_fm<K, COL, NTL, NTS, ND, HL>), grid, dim3(kBlock), 0, a.stream, a.s, a.p, total, \
-                       C, make_fastdiv(a.cd), a.E)
-        if (duties == 1 && hdw <= (uint32_t)kBlock)
-            RFEC_FM(1, 1);
-        else
-            RFEC_FM(2, 2);
-#undef RFEC_FM
-        return hipGetLastError();
-    }
     if (flags & RFEC_KFLAG_GROUP_WAVE) {
         const GwGeom g = gw_geom(a.groups, a.cd);
         const uint32_t swz = (flags & RFEC_KFLAG_XCD_SWIZZLE) ? 1u : 0u;

@@ -42,7 +42,6 @@ RFEC_TUNE_DIAG_CONST_SCHED = 1024
 RFEC_TUNE_TWO_KERNEL_DECODE = 4096
 RFEC_TUNE_GROUP_WAVE = 8192
 RFEC_TUNE_XCD_SWIZZLE = 16384
-RFEC_TUNE_META_BLOCKS = 65536
 
 # 20-byte header record == sim_fec_meta_t layout (sim_proto.h:145-155)
 HDR_DTYPE = np.dtype([("seq", "<u4"), ("fid", "<u4"), ("ts", "<u4"), ("index", "<u2"), ("total", "<u2"),

@@ -20,8 +20,7 @@ from bench import Workload  # noqa: E402
 from razor_amd.fec import native  # noqa: E402
 
 ENC_VARIANTS = {
-    "default(fused meta, nt_ld+wt_st)": 0,
-    "meta_blocks": 65536,
+    "default(nt_ld+wt_st)": 0,
     "nt_st": 512,
     "plain_st": 4,
     "wt_nt_st": 192,
@@ -37,7 +36,7 @@ DEC_VARIANTS = {"fused(default nt_st)": 0, "fused_wt_st": 64, "fused_plain_st": 
                 "two_kernel": 4096, "two_kernel_wt_st": 4096 | 64, "diag_const_sched": 4096 | 1024, "wave": 16,
                 "pipe": 32, "fused_items2": 8, "fused_items2_wt": 8 | 64, "fused_group_wave": 8192, "fused_group_wave_xcd": 8192 | 16384}
 # (encode flags, decode flags)
-STEP_VARIANTS = {"default (enc wt, dec nt)": (0, 0), "enc meta blocks": (65536, 0), "enc nt, dec nt": (512, 512), "enc nt, dec wt": (512, 64),
+STEP_VARIANTS = {"default (enc wt, dec nt)": (0, 0), "enc nt, dec nt": (512, 512), "enc nt, dec wt": (512, 64),
                  "enc wt, dec wt": (64, 64), "enc items2": (8, 0), "dec pipe": (0, 32), "dec diag const sched": (0, 4096 | 1024), "dec two-kernel": (0, 4096), "dec wave": (0, 16),
                  "group_wave both": (8192, 8192), "dec items2": (0, 8), "dec items2 plain st": (0, 8 | 4),
                  "dec plain st": (0, 4), "group_wave+xcd both": (8192 | 16384, 8192 | 16384)}
