@@ -58,11 +58,36 @@ def distinct_row_pairs(plan):
     return [(a, b) for r1 in range(len(rows)) for r2 in range(r1 + 1, len(rows)) for a in rows[r1] for b in rows[r2]]
 
 
+def peel_bytes(plan, k, erased, S):
+    """Algorithmic decode bytes of one erasure set under the canonical peel
+    (lines in plan order, repeated to a fixpoint, as the oracle and the
+    device decoders run it): each fired line reads its other members and its
+    parity and writes the missing member, (count + 1) * S.  None when the
+    set is not recoverable."""
+    have = set(range(k)) - set(erased)
+    total, progress = 0, True
+    while progress:
+        progress = False
+        for l in range(plan.n_lines):
+            mem = plan.members(l)
+            miss = [i for i in mem if i not in have]
+            if len(miss) == 1:
+                have.add(miss[0])
+                total += (len(mem) + 1) * S
+                progress = True
+    return total if len(have) == k else None
+
+
 class Workload:
-    def __init__(self, lib, G, k, S, pf, device, group0, seed, stride=None):
+    def __init__(self, lib, G, k, S, pf, device, group0, seed, stride=None, col=0, full_plan=False):
         self.lib, self.G, self.k, self.S = lib, G, k, S
         self.stride = stride or (S + 15) // 16 * 16  # slot width in HBM (>= S, multiple of 16)
-        self.plan = lib.plan_from_fraction(k, pf, 1)  # row layer: r = 3 at k = 10
+        if col:  # explicit rows of `col` (config 5: k = 32 as 8 rows of 4)
+            self.plan = lib.plan_matrix(k, (k + col - 1) // col, col, 1)
+        elif full_plan:  # the reference sender's whole plan: rows and columns (3x4 -> 7 parities at k = 10)
+            self.plan = lib.plan_from_fraction(k, pf, 3)
+        else:
+            self.plan = lib.plan_from_fraction(k, pf, 1)  # row layer: r = 3 at k = 10
         self.n = self.plan.n_lines
         dev = device
         gen = torch.Generator(device=dev)
@@ -78,8 +103,12 @@ class Workload:
         self.meta = torch.empty((G, self.n, 20), dtype=torch.uint8, device=dev)
         self.fsize = torch.empty((G, self.n), dtype=torch.int16, device=dev)
         self.status = torch.empty((G, self.n), dtype=torch.int8, device=dev)
-        # receive side: the same groups with 2 erasures each
-        pairs = np.array(distinct_row_pairs(self.plan))
+        # receive side: the same groups with 2 erasures each (rows only: in distinct rows; full plan: any pair)
+        if full_plan:
+            pairs = np.array([(a, b) for a in range(k) for b in range(a + 1, k)
+                              if peel_bytes(self.plan, k, (a, b), S) is not None])
+        else:
+            pairs = np.array(distinct_row_pairs(self.plan))
         rng = np.random.default_rng(seed)
         self.erased = pairs[rng.integers(0, len(pairs), G)]
         present = np.zeros((G, 2), np.uint64)
@@ -100,10 +129,9 @@ class Workload:
         self.ws = torch.empty((lib.workspace_size(self.plan, G),), dtype=torch.uint8, device=dev)
         # algorithmic payload bytes (headers excluded): encode reads k*S, writes r*S
         self.enc_bytes = G * (k + self.n) * S
-        row_of = {i: l for l in range(self.n) for i in self.plan.members(l)}
-        sizes = np.array([self.plan.line[row_of[i]].count for i in range(k)])
-        # decode: per erased segment read (row size - 1) members + 1 parity, write 1
-        self.dec_bytes = int((sizes[self.erased[:, 0]] + 1).sum() + (sizes[self.erased[:, 1]] + 1).sum()) * S
+        # decode: per recovered segment read its line's other members + the parity, write 1
+        pair_bytes = {tuple(p): peel_bytes(self.plan, k, tuple(p), S) for p in pairs.tolist()}
+        self.dec_bytes = int(sum(pair_bytes[(int(a), int(b))] for a, b in self.erased))
 
     def encode(self, stream):
         self.lib.encode_batch(self.plan, self.G, self.stride, self.S, self.shards.data_ptr(), self.hdr.data_ptr(),
@@ -245,6 +273,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--tuning", type=int, default=0)
+    ap.add_argument("--col", type=int, default=0, help="rows of COL segments (config 5: --k 32 --payload 256 --col 4)")
+    ap.add_argument("--full-plan", action="store_true", help="rows + columns of the reference plan (config 3 variant)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -269,7 +299,7 @@ def main():
         group0, my_groups = rank * args.groups, args.groups
         scaling = "weak"
     w = Workload(lib, my_groups, args.k, args.payload, args.protect_fraction, device, group0, seed=1000 + rank,
-                 stride=args.stride or None)
+                 stride=args.stride or None, col=args.col, full_plan=args.full_plan)
     stream = torch.cuda.current_stream(device)
     sp = stream.cuda_stream
     torch.cuda.synchronize(device)
@@ -321,6 +351,19 @@ def main():
     if rank == 0:
         ceiling = copy_ceiling(device)
         workload_name = f"k{args.k}_r{w.n}_S{args.payload}_G{w.G}"
+        lines = [w.plan.line[l].count for l in range(w.n)]
+        rows_layout = not args.full_plan and len(set(lines[:-1])) <= 1
+        enc_kernel = (f"k_encode_rows<{args.k},{lines[0]}>" if rows_layout and (args.k, lines[0]) in ((10, 4), (32, 4))
+                      else "k_encode (plan-driven)")
+        dec_kernels = ("k_peel_lds + k_recover_flat (cascading peel: schedule, then replay)" if args.full_plan
+                       else "k_decode_disjoint (peel headers + payload, one launch)")
+        if args.full_plan:
+            plan_desc = f"full reference plan {w.plan.row}x{w.plan.col}: {w.plan.n_row_lines} rows + {w.n - w.plan.n_row_lines} columns, line sizes {lines}"
+            pairs_desc = "uniform over all recoverable pairs (peeling, with cascades)"
+        else:
+            plan_desc = ("row layer of the reference 3x4 plan, rows {4,4,2}" if (args.k, args.col) == (10, 0)
+                         else f"rows of sizes {lines}")
+            pairs_desc = f"uniform over the {len(distinct_row_pairs(w.plan))} distinct-row pairs"
         traffic = load_traffic(workload_name, "encode")
         res = {
             "metric": METRIC,
@@ -337,12 +380,12 @@ def main():
             "data": "synthetic (torch.randint payloads, sequential headers), resident in HBM before timing",
             "config": {"workload": workload_name, "groups_per_gpu": w.G,
                        "total_groups": args.total_groups or args.groups * world, "k": args.k, "r": w.n,
-                       "payload_bytes": args.payload, "plan": "row layer of the reference 3x4 plan, rows {4,4,2}",
-                       "erasures_per_group": 2, "erasure_pairs": "uniform over the 32 distinct-row pairs",
+                       "payload_bytes": args.payload, "plan": plan_desc,
+                       "erasures_per_group": 2, "erasure_pairs": pairs_desc,
                        "parallelism": f"batch split over {world} GPU(s), no collective",
                        "bytes_per_step_per_gpu": {"encode": w.enc_bytes, "decode": w.dec_bytes},
                        "algorithmic_bytes": "payload bytes read + written (20-B headers excluded)"},
-            "roofline": {"bound": "hbm", "kernel": "k_encode_rows<10,4>", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": enc_kernel, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "launch_us": round(enc_mean * 1e6, 2),
                          "algorithmic_bytes_per_launch": w.enc_bytes},
@@ -351,7 +394,7 @@ def main():
             "decode_roofline": {"achieved": round(w.dec_bytes / dec_mean / 1e9, 1), "frac":
                                 round(w.dec_bytes / dec_mean / 1e9 / HBM_PEAK_GBPS, 4),
                                 "launch_us": round(dec_mean * 1e6, 2), "traffic": load_traffic(workload_name, "decode"),
-                                "kernels": "k_decode_disjoint (peel headers + payload, one launch)"},
+                                "kernels": dec_kernels},
             "copy_ceiling_GBps": round(ceiling, 1),
             "verified": verified,
             "tuning": args.tuning,
