@@ -217,6 +217,53 @@ __global__ __launch_bounds__(kBlock) void k_encode(const v4u* __restrict__ shard
 }
 
 // ---------------------------------------------------------------------------
+// Encode payload, any plan over k <= 16 segments (e.g. the reference sender's
+// full row + column plan, flex_fec_sender.c:166-233): a lane loads the chunk
+// of every member once, all k loads in flight, and forms each line's XOR from
+// registers; the lines come as wave-uniform 16-bit member masks, so the
+// member selection is scalar control flow, not per-lane work.
+// ---------------------------------------------------------------------------
+struct LineMasks16 {
+    uint32_t n;
+    uint16_t m[RFEC_MAX_LINES];
+};
+
+template <bool NTL, int NTS>
+__global__ __launch_bounds__(kBlock) void k_encode_k16(const v4u* __restrict__ shards, v4u* __restrict__ parity,
+                                                       uint32_t total, uint32_t C, FastDiv divC, EncMeta E,
+                                                       rfec_kplan P, LineMasks16 LM)
+{
+    if (blockIdx.x < E.n_meta_blocks) {
+        meta_block(blockIdx.x, E.hdr_dw, E.meta_dw, E.fsize, E.status, E.groups, E.capacity, E.gpb, P);
+        return;
+    }
+    const uint32_t t = (blockIdx.x - E.n_meta_blocks) * kBlock + threadIdx.x;
+    if (t >= total)
+        return;
+    const uint32_t g = fdiv(t, divC);
+    const uint32_t j = t - g * divC.d;
+    const uint32_t K = P.k;
+    const v4u* src = shards + (size_t)g * K * C + j;
+    v4u* dst = parity + (size_t)g * LM.n * C + j;
+    v4u v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        v[i] = v4u{0, 0, 0, 0};
+        if ((uint32_t)i < K)
+            v[i] = ld16<NTL>(src + (size_t)i * C);
+    }
+    for (uint32_t l = 0; l < LM.n; ++l) {
+        const uint32_t m = LM.m[l];
+        v4u acc = v4u{0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if ((m >> i) & 1u)
+                acc ^= v[i];
+        st16<NTS>(dst + (size_t)l * C, acc);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Encode payload, rows-of-COL fast path (k=10 rows {4,4,2}; k=32 8x4): member
 // offsets are compile-time constants, so all K x ITEMS dwordx4 loads of a lane
 // issue back to back.  Item u of a lane is chunk t0 + u*(payload lanes), so
@@ -1175,6 +1222,19 @@ hipError_t launch_encode_t(const EncLaunch& a, unsigned flags)
     }
     const uint32_t C = a.stride / 16;
     const uint32_t total = a.groups * a.cd;
+    if (!(flags & RFEC_KFLAG_GENERIC) && P->k <= 16) {
+        LineMasks16 LM;
+        LM.n = P->n_lines;
+        for (uint32_t l = 0; l < P->n_lines; ++l) {
+            uint32_t m = 0;
+            for (uint32_t q = 0; q < P->line[l].count; ++q)
+                m |= 1u << (P->line[l].first + q * P->line[l].stride);
+            LM.m[l] = (uint16_t)m;
+        }
+        hipLaunchKernelGGL((k_encode_k16<NTL, NTS>), dim3(a.E.n_meta_blocks + blocks_for(total)), dim3(kBlock), 0,
+                           a.stream, a.s, a.p, total, C, make_fastdiv(a.cd), a.E, *P, LM);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL((k_encode<NTL, NTS>), dim3(a.E.n_meta_blocks + blocks_for(total)), dim3(kBlock), 0, a.stream,
                        a.s, a.p, total, C, make_fastdiv(a.cd), a.E, *P);
     return hipGetLastError();
