@@ -1266,7 +1266,12 @@ int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, ui
                          E, reinterpret_cast<hipStream_t>(stream)};
     if (flags & RFEC_KFLAG_PLAIN_LOADS) // A/B only
         return (int)launch_encode_t<false, 1>(a, flags);
-    switch (store_policy(flags, kEncodeStoreDefault)) {
+    // default store policy: write-through for the row layouts (kEncodeStoreDefault), non-temporal for the
+    // other plans, which write two parities per segment or more (the full row + column plan: 285 vs 312 us
+    // at k = 10, bench.py --full-plan)
+    uint32_t col = 0;
+    const int dflt = is_row_layout(P, &col) ? kEncodeStoreDefault : 1;
+    switch (store_policy(flags, dflt)) {
     case 0: return (int)launch_encode_t<true, 0>(a, flags);
     case 2: return (int)launch_encode_t<true, 2>(a, flags);
     case 3: return (int)launch_encode_t<true, 3>(a, flags);
