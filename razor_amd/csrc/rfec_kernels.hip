@@ -217,6 +217,80 @@ __global__ __launch_bounds__(kBlock) void k_encode(const v4u* __restrict__ shard
 }
 
 // ---------------------------------------------------------------------------
+// Encode payload, the reference sender's full matrix plan at small k
+// (flex_fec_sender.c:166-233: rows of COL consecutive segments, then columns
+// strided by COL, lines with fewer than 2 members dropped), member offsets
+// and line order compile-time: all K loads in flight, every line's XOR from
+// registers.  K = 6..16 (COL = 3 or 4, as flex_fec_sender_num_packets picks).
+// ---------------------------------------------------------------------------
+template <int K, int COL>
+struct MatrixShape {
+    static constexpr int R = (K + COL - 1) / COL;
+    static constexpr int row_count(int r) { return (r * COL + COL <= K) ? COL : K - r * COL; }
+    static constexpr int col_count(int c) { return (K - c + COL - 1) / COL; }
+    static constexpr int n_rows()
+    {
+        int n = 0;
+        for (int r = 0; r < R; ++r)
+            n += row_count(r) >= 2;
+        return n;
+    }
+    static constexpr int n_lines()
+    {
+        int n = n_rows();
+        for (int c = 0; c < COL; ++c)
+            n += col_count(c) >= 2;
+        return n;
+    }
+};
+
+template <int K, int COL, bool NTL, int NTS>
+__global__ __launch_bounds__(kBlock) void k_encode_matrix(const v4u* __restrict__ shards, v4u* __restrict__ parity,
+                                                          uint32_t total, uint32_t C, FastDiv divC, EncMeta E,
+                                                          rfec_kplan P)
+{
+    using Sh = MatrixShape<K, COL>;
+    if (blockIdx.x < E.n_meta_blocks) {
+        meta_block(blockIdx.x, E.hdr_dw, E.meta_dw, E.fsize, E.status, E.groups, E.capacity, E.gpb, P);
+        return;
+    }
+    const uint32_t t = (blockIdx.x - E.n_meta_blocks) * kBlock + threadIdx.x;
+    if (t >= total)
+        return;
+    const uint32_t g = fdiv(t, divC);
+    const uint32_t j = t - g * divC.d;
+    const v4u* src = shards + (size_t)g * K * C + j;
+    v4u* dst = parity + (size_t)g * Sh::n_lines() * C + j;
+    v4u v[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+        v[i] = ld16<NTL>(src + (size_t)i * C);
+    int l = 0;
+#pragma unroll
+    for (int r = 0; r < Sh::R; ++r) {
+        if (Sh::row_count(r) < 2)
+            continue;
+        v4u acc = v[r * COL];
+#pragma unroll
+        for (int q = 1; q < COL; ++q)
+            if (q < Sh::row_count(r))
+                acc ^= v[r * COL + q];
+        st16<NTS>(dst + (size_t)(l++) * C, acc);
+    }
+#pragma unroll
+    for (int c = 0; c < COL; ++c) {
+        if (Sh::col_count(c) < 2)
+            continue;
+        v4u acc = v[c];
+#pragma unroll
+        for (int q = 1; q < (K + COL - 1) / COL; ++q)
+            if (q < Sh::col_count(c))
+                acc ^= v[c + q * COL];
+        st16<NTS>(dst + (size_t)(l++) * C, acc);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Encode payload, any plan over k <= 16 segments (e.g. the reference sender's
 // full row + column plan, flex_fec_sender.c:166-233): a lane loads the chunk
 // of every member once, all k loads in flight, and forms each line's XOR from
@@ -1196,6 +1270,31 @@ int store_policy(unsigned flags, int dflt)
     return dflt;
 }
 
+// the sender's full plan of a k-segment group in rows of `col`: rows, then
+// columns, lines with fewer than 2 members dropped (flex_fec_sender.c:166-233)
+bool is_full_matrix(const rfec_kplan* P, uint32_t col)
+{
+    const uint32_t k = P->k, rows = (k + col - 1) / col;
+    uint32_t l = 0;
+    for (uint32_t r = 0; r < rows; ++r) {
+        const uint32_t cnt = k - r * col < col ? k - r * col : col;
+        if (cnt < 2)
+            continue;
+        if (l >= P->n_lines || P->line[l].first != r * col || P->line[l].stride != 1 || P->line[l].count != cnt)
+            return false;
+        ++l;
+    }
+    for (uint32_t c = 0; c < col; ++c) {
+        const uint32_t cnt = (k - c + col - 1) / col;
+        if (cnt < 2)
+            continue;
+        if (l >= P->n_lines || P->line[l].first != c || P->line[l].stride != col || P->line[l].count != cnt)
+            return false;
+        ++l;
+    }
+    return l == P->n_lines;
+}
+
 bool is_row_layout(const rfec_kplan* P, uint32_t* col_out)
 {
     const uint32_t col = P->n_lines ? P->line[0].count : 0;
@@ -1222,6 +1321,20 @@ hipError_t launch_encode_t(const EncLaunch& a, unsigned flags)
     }
     const uint32_t C = a.stride / 16;
     const uint32_t total = a.groups * a.cd;
+    if (!(flags & RFEC_KFLAG_GENERIC) && P->k >= 6 && P->k <= 16 && is_full_matrix(P, P->k <= 9 ? 3 : 4)) {
+        const dim3 grid(a.E.n_meta_blocks + blocks_for(total));
+#define RFEC_MX(KK, CC)                                                                                           \
+    case KK:                                                                                                      \
+        hipLaunchKernelGGL((k_encode_matrix<KK, CC, NTL, NTS>), grid, dim3(kBlock), 0, a.stream, a.s, a.p, total, C, \
+                           make_fastdiv(a.cd), a.E, *P);                                                          \
+        return hipGetLastError();
+        switch (P->k) {
+            RFEC_MX(6, 3) RFEC_MX(7, 3) RFEC_MX(8, 3) RFEC_MX(9, 3) RFEC_MX(10, 4) RFEC_MX(11, 4) RFEC_MX(12, 4)
+            RFEC_MX(13, 4) RFEC_MX(14, 4) RFEC_MX(15, 4) RFEC_MX(16, 4)
+        default: break;
+        }
+#undef RFEC_MX
+    }
     if (!(flags & RFEC_KFLAG_GENERIC) && P->k <= 16) {
         LineMasks16 LM;
         LM.n = P->n_lines;
