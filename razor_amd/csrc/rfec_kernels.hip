@@ -618,6 +618,7 @@ struct PeelArgs {
     uint64_t* recovered;
     uint8_t* sched;
     uint32_t groups, capacity, gpb, rec_bytes, disjoint;
+    uint32_t nlp_log2; // fused decode: > 0 = header lanes (line_headers), 0 = LDS-staged peel blocks
 };
 
 // One peel block: groups [blk*gpb, ...).  With WRITE_SCHED false (fused
@@ -874,13 +875,80 @@ __device__ __forceinline__ bool has_bit(uint64_t h0, uint64_t h1, uint32_t i)
     return ((i < 64 ? h0 >> i : h1 >> (i - 64)) & 1ull) != 0;
 }
 
+// Header work of the fused decode, one lane per (group, line): NLP = 2^nlp_log2
+// >= n_lines consecutive lanes per group.  A line fires as in peel_block (one
+// member missing, one present, its parity received, sizes within bounds); it
+// reads only its own members' headers, so a group costs the fired lines'
+// records instead of all K + NL staged.  Lines are pairwise disjoint, so the
+// lines of a group are independent; the group's recovered mask is OR-reduced
+// over its NLP lanes (all in one wave: NLP <= 64).
+__device__ void line_headers(const PeelArgs& A, const rfec_kmask& M, uint32_t blk)
+{
+    __shared__ uint32_t lplan[RFEC_MAX_LINES];
+    __shared__ uint64_t lmask[RFEC_MAX_LINES][2];
+    const rfec_kplan& P = M.plan;
+    if (threadIdx.x < P.n_lines) {
+        lmask[threadIdx.x][0] = M.mask[threadIdx.x][0];
+        lmask[threadIdx.x][1] = M.mask[threadIdx.x][1];
+    }
+    stage_plan(lplan, P);
+    const uint32_t nlp = 1u << A.nlp_log2;
+    const uint32_t hl = blk * kBlock + threadIdx.x;
+    const uint32_t g = hl >> A.nlp_log2, l = hl & (nlp - 1);
+    uint32_t rec[4] = {0, 0, 0, 0};
+    if (g < A.groups && l < P.n_lines && ((A.parity_present[g] >> l) & 1ull)) {
+        const uint64_t h0 = A.present[2 * g], h1 = A.present[2 * g + 1];
+        const uint64_t m0 = lmask[l][0], m1 = lmask[l][1];
+        const uint64_t x0 = m0 & ~h0, x1 = m1 & ~h1;
+        const uint32_t L = A.fsize[(size_t)g * P.n_lines + l];
+        if (__popcll(x0) + __popcll(x1) == 1 && ((m0 & h0) | (m1 & h1)) != 0 && L <= A.capacity) {
+            const uint32_t t = x0 ? (uint32_t)__ffsll((long long)x0) - 1 : 64u + (uint32_t)__ffsll((long long)x1) - 1;
+            const uint32_t* mr = reinterpret_cast<const uint32_t*>(A.meta + (size_t)g * P.n_lines + l);
+            uint32_t r0 = mr[0], r1 = mr[1], r2 = mr[2], r3 = mr[3], r4 = mr[4];
+            const uint32_t ln = lplan[l];
+            const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
+            const uint32_t* gh = reinterpret_cast<const uint32_t*>(A.hdr + (size_t)g * P.k);
+            bool ok = true;
+            for (uint32_t q = 0; q < count; ++q) {
+                const uint32_t i = first + q * stride;
+                if (i == t)
+                    continue;
+                const uint32_t* r = gh + i * 5;
+                r0 ^= r[0];
+                r1 ^= r[1];
+                r2 ^= r[2];
+                r3 ^= r[3];
+                const uint32_t w4 = r[4];
+                r4 ^= w4;
+                ok = ok && (w4 >> 16) <= L;
+            }
+            if (ok && (r4 >> 16) <= L) {
+                uint32_t* ht = reinterpret_cast<uint32_t*>(A.hdr + (size_t)g * P.k + t);
+                ht[0] = r0, ht[1] = r1, ht[2] = r2, ht[3] = r3, ht[4] = r4;
+                rec[t >> 5] = 1u << (t & 31);
+            }
+        }
+    }
+    for (uint32_t sh = 1; sh < nlp; sh <<= 1)
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            rec[w] |= __shfl_xor(rec[w], sh);
+    if (g < A.groups && l == 0) {
+        A.recovered[2 * g] = (uint64_t)rec[1] << 32 | rec[0];
+        A.recovered[2 * g + 1] = (uint64_t)rec[3] << 32 | rec[2];
+    }
+}
+
 template <int MAXC, bool NTL, int NTS, int NI>
 __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v4u* __restrict__ parity,
                                                             uint32_t total, uint32_t C, FastDiv divC,
                                                             uint32_t n_hdr_blocks, PeelArgs A, rfec_kmask M)
 {
     if (blockIdx.x < n_hdr_blocks) {
-        peel_block<false, kFusedPeelDwords>(A, M, blockIdx.x);
+        if (A.nlp_log2)
+            line_headers(A, M, blockIdx.x);
+        else
+            peel_block<false, kFusedPeelDwords>(A, M, blockIdx.x);
         return;
     }
     __shared__ uint32_t lplan[RFEC_MAX_LINES];
@@ -979,7 +1047,10 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint_gw(v4u* shards, cons
                                                                uint32_t n_hdr_blocks, PeelArgs A, rfec_kmask M)
 {
     if (blockIdx.x < n_hdr_blocks) {
-        peel_block<false, kFusedPeelDwords>(A, M, blockIdx.x);
+        if (A.nlp_log2)
+            line_headers(A, M, blockIdx.x);
+        else
+            peel_block<false, kFusedPeelDwords>(A, M, blockIdx.x);
         return;
     }
     __shared__ uint32_t lplan[RFEC_MAX_LINES];
@@ -1455,7 +1526,16 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
     if (gpb >= 8)
         gpb &= ~7u;
     B.gpb = gpb < 1 ? 1 : gpb;
-    const uint32_t n_hdr = (groups + B.gpb - 1) / B.gpb;
+    uint32_t n_hdr = (groups + B.gpb - 1) / B.gpb;
+    // fused decode: header lanes, one per (group, line), unless A/B asks for the LDS peel blocks
+    B.nlp_log2 = 0;
+    if (fused && !(flags & RFEC_KFLAG_LDS_HDR_PEEL)) {
+        uint32_t lg = 1;
+        while ((1u << lg) < P.n_lines)
+            ++lg;
+        B.nlp_log2 = lg;
+        n_hdr = (uint32_t)(((uint64_t)groups << lg) + kBlock - 1) / kBlock;
+    }
     const uint32_t C = stride / 16;
     const uint32_t cd = capacity ? (capacity + 15) / 16 : 1;
     const uint32_t total = groups * cd;

@@ -18,7 +18,7 @@ CASES = {c["name"]: c for c in MANIFEST["cases"]}
 TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "plain_stores": 4, "items2": 8, "wave_decode": 16,
            "pipe_decode": 32, "wt_stores": 64, "wt_nt_stores": 192, "nt_stores": 512,
            "generic_plain": 3, "two_kernel": 4096, "two_kernel_wt": 4096 | 64, "group_wave": 8192,
-           "group_wave_xcd": 8192 | 16384, "xcd": 16384}
+           "group_wave_xcd": 8192 | 16384, "xcd": 16384, "lds_hdr_peel": 32768}
 
 
 @pytest.fixture(scope="module")
@@ -56,7 +56,7 @@ def test_erasure_fixture_gpu(gpu, oracle1000, name, tuning):
 
 @pytest.mark.parametrize("tuning", ["default", "wt_stores", "plain_stores", "plain_loads", "two_kernel",
                                     "two_kernel_wt", "pipe_decode", "wave_decode", "group_wave",
-                                    "group_wave_xcd", "items2"])
+                                    "group_wave_xcd", "items2", "lds_hdr_peel"])
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures" and c["rows_only"]])
 def test_erasure_fixture_rows_plan_gpu(gpu, oracle1000, name, tuning):
     """Row-parity-only fixtures against the row-layer plan (pairwise disjoint
