@@ -77,6 +77,10 @@ def main():
             groups = int(bench_args[i + 1])
     S, k, r = 1200, 10, 3
     enc_alg = groups * (k + r) * S
+    cfg = (bench_line or {}).get("config", {})
+    if cfg.get("bytes_per_step_per_gpu", {}).get("encode"):  # the bench's own workload (any plan)
+        enc_alg = cfg["bytes_per_step_per_gpu"]["encode"]
+        S, k, r = cfg.get("payload_bytes", S), cfg.get("k", k), cfg.get("r", r)
     res = {}
     for key in KERNELS:
         f, w = fetch.get(key, []), write.get(key, [])
@@ -93,6 +97,8 @@ def main():
         entry["encode_algorithmic_bytes"] = enc_alg
         entry["encode_traffic_over_algorithmic"] = res["encode"]["hbm_bytes"] / enc_alg
     dec_alg = (bench_line or {}).get("config", {}).get("bytes_per_step_per_gpu", {}).get("decode")
+    if "recover" in res and dec_alg:  # two-kernel decode (plans with columns)
+        entry["recover_traffic_over_algorithmic"] = res["recover"]["hbm_bytes"] / dec_alg
     if "decode" in res and dec_alg:
         entry["decode_hbm_bytes_per_launch"] = res["decode"]["hbm_bytes"]
         entry["decode_algorithmic_bytes"] = dec_alg
