@@ -249,6 +249,8 @@ int rfec_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, 
 int rfec_zero_tails(uint32_t groups, uint32_t k, uint32_t stride, uint8_t* shards, const rfec_hdr* hdr,
                     void* stream)
 {
+    if ((uint64_t)groups * k > 0xFFFFFFFFull)
+        return set_err(RFEC_EINVAL, "groups * k overflows", 0);
     int rc = check_geometry(groups * k, stride, 0, 1);
     if (rc)
         return rc;

@@ -77,6 +77,8 @@ def test_argument_validation(product):
     with pytest.raises(RfecError):
         product.encode_batch(bad, 4, 1200, 1200, 1, 1, 1, 1, 1, None)
     assert product.workspace_size(plan, 100) == 100 * 16  # 2 + 2*3 bytes -> 16
+    with pytest.raises(RfecError):  # groups * k beyond 32 bits
+        product.zero_tails(1 << 30, 8, 1200, 1, 1, None)
 
 
 def test_dropin_fails_loudly_without_gpu():
