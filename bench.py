@@ -167,17 +167,26 @@ class Workload:
         return bool(ok)
 
 
-def copy_ceiling(device, nbytes=1 << 30, reps=10):
-    """Measured device-to-device copy rate (read + write bytes / time), GB/s."""
+def copy_ceiling(lib, device, nbytes=1 << 30, reps=10):
+    """Measured HBM copy rate (read + write bytes / time, GB/s) of the
+    library's streaming copy probe (rfec_probe_copy: one 16-B vector per lane,
+    non-temporal loads and stores), on torch's current stream."""
     a = torch.empty(nbytes, dtype=torch.uint8, device=device)
     b = torch.empty_like(a)
+    st = torch.cuda.current_stream(device).cuda_stream
+
+    def run():
+        rc = lib.lib.rfec_probe_copy(a.data_ptr(), b.data_ptr(), nbytes, 1, st)
+        if rc:
+            raise RuntimeError(f"rfec_probe_copy failed: {rc}")
+
     for _ in range(3):
-        b.copy_(a)
+        run()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(device)
     e0.record()
     for _ in range(reps):
-        b.copy_(a)
+        run()
     e1.record()
     torch.cuda.synchronize(device)
     t = e0.elapsed_time(e1) / 1e3 / reps
@@ -349,7 +358,7 @@ def main():
     achieved = w.enc_bytes / enc_mean / 1e9
     res = None
     if rank == 0:
-        ceiling = copy_ceiling(device)
+        ceiling = copy_ceiling(lib, device)
         workload_name = f"k{args.k}_r{w.n}_S{args.payload}_G{w.G}"
         lines = [w.plan.line[l].count for l in range(w.n)]
         rows_layout = not args.full_plan and len(set(lines[:-1])) <= 1
@@ -390,12 +399,15 @@ def main():
                          "traffic": traffic, "launch_us": round(enc_mean * 1e6, 2),
                          "algorithmic_bytes_per_launch": w.enc_bytes},
             "encode_gibps": round(w.enc_bytes / enc_mean / 2**30, 2),
+            # source bytes k*S*G over the encode time, and that as a fraction of the peak
+            "encode_source_gibps": round(w.G * w.k * w.S / enc_mean / 2**30, 2),
+            "encode_read_only_frac": round(w.G * w.k * w.S / enc_mean / 1e9 / HBM_PEAK_GBPS, 4),
             "decode_gibps": round(w.dec_bytes / dec_mean / 2**30, 2),
             "decode_roofline": {"achieved": round(w.dec_bytes / dec_mean / 1e9, 1), "frac":
                                 round(w.dec_bytes / dec_mean / 1e9 / HBM_PEAK_GBPS, 4),
                                 "launch_us": round(dec_mean * 1e6, 2), "traffic": load_traffic(workload_name, "decode"),
                                 "kernels": dec_kernels},
-            "copy_ceiling_GBps": round(ceiling, 1),
+            "copy_ceiling_GBps": round(ceiling, 1),  # rfec_probe_copy, read + write bytes
             "verified": verified,
             "tuning": args.tuning,
         }
