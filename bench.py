@@ -282,6 +282,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--tuning", type=int, default=0)
+    ap.add_argument("--sets", type=int, default=2, help="disjoint buffer sets rotated per step (MALL-proof timing)")
     ap.add_argument("--col", type=int, default=0, help="rows of COL segments (config 5: --k 32 --payload 256 --col 4)")
     ap.add_argument("--full-plan", action="store_true", help="rows + columns of the reference plan (config 3 variant)")
     args = ap.parse_args()
@@ -307,15 +308,19 @@ def main():
     else:
         group0, my_groups = rank * args.groups, args.groups
         scaling = "weak"
-    w = Workload(lib, my_groups, args.k, args.payload, args.protect_fraction, device, group0, seed=1000 + rank,
-                 stride=args.stride or None, col=args.col, full_plan=args.full_plan)
+    # rotate over disjoint buffer sets (same inputs), so that the
+    # 256 MB MALL never holds a step's operands from the previous step
+    sets = [Workload(lib, my_groups, args.k, args.payload, args.protect_fraction, device, group0, seed=1000 + rank,
+                     stride=args.stride or None, col=args.col, full_plan=args.full_plan)
+            for _ in range(max(1, args.sets))]
+    w = sets[0]
     stream = torch.cuda.current_stream(device)
     sp = stream.cuda_stream
     torch.cuda.synchronize(device)
 
-    for _ in range(args.warmup):
-        w.encode(sp)
-        w.decode(sp)
+    for i in range(args.warmup):
+        sets[i % len(sets)].encode(sp)
+        sets[i % len(sets)].decode(sp)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if dist:
@@ -324,10 +329,11 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         a, b, c = ev[i]
+        ws = sets[i % len(sets)]
         a.record(stream)
-        w.encode(sp)
+        ws.encode(sp)
         b.record(stream)
-        w.decode(sp)
+        ws.decode(sp)
         c.record(stream)
     torch.cuda.synchronize(device)
     if dist:
@@ -341,7 +347,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    verified = None if args.no_verify else w.verify()
+    verified = None if args.no_verify else all(ws.verify() for ws in sets)
     if dist:
         vt = torch.tensor([1 if verified in (None, True) else 0], dtype=torch.int32, device=device)
         dist.all_reduce(vt, op=dist.ReduceOp.MIN)
@@ -392,11 +398,13 @@ def main():
                        "payload_bytes": args.payload, "plan": plan_desc,
                        "erasures_per_group": 2, "erasure_pairs": pairs_desc,
                        "parallelism": f"batch split over {world} GPU(s), no collective",
+                       "buffer_sets": len(sets),
                        "bytes_per_step_per_gpu": {"encode": w.enc_bytes, "decode": w.dec_bytes},
                        "algorithmic_bytes": "payload bytes read + written (20-B headers excluded)"},
             "roofline": {"bound": "hbm", "kernel": enc_kernel, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "launch_us": round(enc_mean * 1e6, 2),
+                         "launch_us_median": round(float(np.median(t_enc)) * 1e6, 2),
                          "algorithmic_bytes_per_launch": w.enc_bytes},
             "encode_gibps": round(w.enc_bytes / enc_mean / 2**30, 2),
             # source bytes k*S*G over the encode time, and that as a fraction of the peak
@@ -405,7 +413,9 @@ def main():
             "decode_gibps": round(w.dec_bytes / dec_mean / 2**30, 2),
             "decode_roofline": {"achieved": round(w.dec_bytes / dec_mean / 1e9, 1), "frac":
                                 round(w.dec_bytes / dec_mean / 1e9 / HBM_PEAK_GBPS, 4),
-                                "launch_us": round(dec_mean * 1e6, 2), "traffic": load_traffic(workload_name, "decode"),
+                                "launch_us": round(dec_mean * 1e6, 2),
+                                "launch_us_median": round(float(np.median(t_dec)) * 1e6, 2),
+                                "traffic": load_traffic(workload_name, "decode"),
                                 "kernels": dec_kernels},
             "copy_ceiling_GBps": round(ceiling, 1),  # rfec_probe_copy, read + write bytes
             "verified": verified,
