@@ -208,7 +208,7 @@ size_t rfec_recover_workspace_size(const rfec_plan* plan, uint32_t groups)
 {
     if (!plan)
         return 0;
-    return (size_t)groups * rfec_sched_record_bytes(plan->n_lines);
+    return rfec_ws_bytes(plan->n_lines, groups);
 }
 
 static void make_masks(const rfec_plan* p, rfec_kmask* M)
@@ -372,7 +372,7 @@ static di_layout di_offsets(void)
     DI_TAKE(present, 2 * sizeof(uint64_t));
     DI_TAKE(ppresent, sizeof(uint64_t));
     DI_TAKE(recovered, 2 * sizeof(uint64_t));
-    DI_TAKE(ws, 16);
+    DI_TAKE(ws, 256); /* rfec_ws_bytes of one group, any plan (<= 164 B) */
 #undef DI_TAKE
     L.total = o;
     return L;

@@ -44,6 +44,16 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
 /* bytes of one group's peeling-schedule record: step count, single-level
  * flag, then a (line, target) byte pair per step; 16-byte multiple */
 static inline uint32_t rfec_sched_record_bytes(uint32_t n_lines) { return (2u + 2u * n_lines + 15u) & ~15u; }
+/* recover workspace: the schedule records, then (one-launch cascade decode) a
+ * 16-byte fix-up counter and a u32 list of the groups to replay exactly */
+static inline size_t rfec_ws_fix_offset(uint32_t n_lines, uint32_t groups)
+{
+    return ((size_t)groups * rfec_sched_record_bytes(n_lines) + 15u) & ~(size_t)15u;
+}
+static inline size_t rfec_ws_bytes(uint32_t n_lines, uint32_t groups)
+{
+    return rfec_ws_fix_offset(n_lines, groups) + 16u + 4u * (size_t)groups;
+}
 int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
                                const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,
                                const rfec_fec_stamp* stamps, const uint32_t* order, uint32_t dstride,

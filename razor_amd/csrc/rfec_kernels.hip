@@ -24,6 +24,10 @@
 //    as soon as the line fires, so cascaded recoveries read segments this
 //    same lane has just written.
 #include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <ctime>
+#include <unistd.h>
 #include <stdint.h>
 
 #include "rfec_internal.h"
@@ -608,6 +612,7 @@ __global__ __launch_bounds__(kBlock) void k_recover(RecArgs A, rfec_kmask M)
 // single-level schedules run BATCH steps with every load in flight at once.
 // ---------------------------------------------------------------------------
 constexpr int kPeelDwords = 8192; // 32 KiB of LDS per peel block
+constexpr int kFusedPeelDwords = 4096; // fused decodes: 16 KiB, the payload blocks carry this allocation too
 
 struct PeelArgs {
     rfec_hdr* hdr;
@@ -619,11 +624,33 @@ struct PeelArgs {
     uint8_t* sched;
     uint32_t groups, capacity, gpb, rec_bytes, disjoint;
     uint32_t nlp_log2; // fused decode: > 0 = header lanes (line_headers), 0 = LDS-staged peel blocks
+    // one-launch cascade decode: groups whose header checks rejected a line
+    // the masks alone would fire go to fixlist; fixc = (gen << 32) | count,
+    // a counter left from another launch (other gen) reads as 0
+    unsigned long long* fixc;
+    uint32_t* fixlist;
+    uint32_t gen;
 };
+
+__device__ __forceinline__ void fix_append(const PeelArgs& A, uint32_t g)
+{
+    unsigned long long old = *reinterpret_cast<volatile unsigned long long*>(A.fixc);
+    for (;;) {
+        const uint32_t idx = (uint32_t)(old >> 32) == A.gen ? (uint32_t)old : 0u;
+        const unsigned long long nw = ((unsigned long long)A.gen << 32) | (idx + 1u);
+        const unsigned long long seen = atomicCAS(A.fixc, old, nw);
+        if (seen == old) {
+            if (idx < A.groups)
+                A.fixlist[idx] = g;
+            return;
+        }
+        old = seen;
+    }
+}
 
 // One peel block: groups [blk*gpb, ...).  With WRITE_SCHED false (fused
 // decode of disjoint plans) only the recovered headers and masks are written.
-template <bool WRITE_SCHED, int LDSD>
+template <bool WRITE_SCHED, int LDSD, bool FIXUP = false>
 __device__ void peel_block(const PeelArgs& A, const rfec_kmask& M, uint32_t blk)
 {
     __shared__ __attribute__((aligned(16))) uint32_t lds[LDSD];
@@ -663,6 +690,7 @@ __device__ void peel_block(const PeelArgs& A, const rfec_kmask& M, uint32_t blk)
     uint64_t rec0 = 0, rec1 = 0;
     uint8_t* rec = A.sched + (size_t)g * A.rec_bytes;
     uint32_t n = 0, single = 1;
+    bool rejected = false; // a line the masks fire failed the header checks
     // with pairwise-disjoint lines (e.g. the row layer alone) a recovery can
     // never complete another line, so one pass reaches the fixpoint
     bool progress = true;
@@ -680,8 +708,10 @@ __device__ void peel_block(const PeelArgs& A, const rfec_kmask& M, uint32_t blk)
             const uint32_t t = x0 ? (uint32_t)__ffsll((long long)x0) - 1
                                   : 64u + (uint32_t)__ffsll((long long)x1) - 1;
             const uint32_t L = f[l];
-            if (L > A.capacity)
+            if (L > A.capacity) {
+                rejected = true;
                 continue;
+            }
             uint32_t r0 = m[l * 5], r1 = m[l * 5 + 1], r2 = m[l * 5 + 2], r3 = m[l * 5 + 3], r4 = m[l * 5 + 4];
             bool ok = true;
             const bool reads_recovered = ((m0 & rec0) | (m1 & rec1)) != 0;
@@ -698,8 +728,10 @@ __device__ void peel_block(const PeelArgs& A, const rfec_kmask& M, uint32_t blk)
                 r4 ^= r[4];
                 ok = ok && (r[4] >> 16) <= L;
             }
-            if (!ok || (r4 >> 16) > L)
+            if (!ok || (r4 >> 16) > L) {
+                rejected = true;
                 continue;
+            }
             uint32_t* ht = h + t * 5;
             ht[0] = r0, ht[1] = r1, ht[2] = r2, ht[3] = r3, ht[4] = r4;
             uint32_t* gh = reinterpret_cast<uint32_t*>(A.hdr + (size_t)g * K + t);
@@ -725,6 +757,8 @@ __device__ void peel_block(const PeelArgs& A, const rfec_kmask& M, uint32_t blk)
         rec[0] = (uint8_t)n;
         rec[1] = (uint8_t)single;
     }
+    if (FIXUP && rejected)
+        fix_append(A, g);
     A.recovered[2 * g] = rec0;
     A.recovered[2 * g + 1] = rec1;
 }
@@ -858,6 +892,122 @@ __global__ __launch_bounds__(kBlock) void k_recover_pipe(v4u* shards, const v4u*
 }
 
 // ---------------------------------------------------------------------------
+// Recover, one-launch form for plans with cascades (rows + columns), at most
+// 7 lines.  Header blocks at the head of the grid run the exact peel
+// (peel_block: headers, schedule records, recovered masks); every payload lane
+// (group, chunk column) derives the schedule from the received masks alone --
+// the same canonical peel without the header size checks -- and replays it.
+// The two schedules differ only where a header check rejected a line the masks
+// fire; the peel lists those groups and k_decode_fixup, launched next, replays
+// their exact records over the mask-only writes (which touched only erased
+// slots, so nothing it reads).  Replaying an exact record is idempotent.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void put_rec_byte(v4u& r, uint32_t pos, uint32_t v)
+{
+    const uint32_t w = pos >> 2, sh = 8 * (pos & 3);
+    r[0] |= w == 0 ? v << sh : 0u;
+    r[1] |= w == 1 ? v << sh : 0u;
+    r[2] |= w == 2 ? v << sh : 0u;
+    r[3] |= w == 3 ? v << sh : 0u;
+}
+
+// the canonical peel over the masks (lines in plan order to a fixpoint, as
+// peel_block without its header checks) as a record image in registers:
+// byte 0 = steps, byte 1 = single level, then (line, target) pairs
+template <bool WIDE> // WIDE: k > 64, the second mask word in play
+__device__ __forceinline__ v4u mask_schedule(const rfec_kmask& M, uint32_t NL, uint64_t h0, uint64_t h1, uint64_t ppm)
+{
+    if (!WIDE)
+        h1 = 0;
+    v4u r = {0, 0, 0, 0};
+    uint32_t n = 0, single = 1;
+    uint64_t rec0 = 0, rec1 = 0;
+    bool progress = true;
+    while (progress) {
+        progress = false;
+        for (uint32_t l = 0; l < NL; ++l) {
+            if (!((ppm >> l) & 1ull))
+                continue;
+            const uint64_t m0 = M.mask[l][0], m1 = WIDE ? M.mask[l][1] : 0;
+            const uint64_t x0 = m0 & ~h0, x1 = m1 & ~h1;
+            if (__popcll(x0) + (WIDE ? __popcll(x1) : 0) != 1 || ((m0 & h0) | (m1 & h1)) == 0)
+                continue;
+            const uint32_t t = x0 ? (uint32_t)__ffsll((long long)x0) - 1 : 64u + (uint32_t)__ffsll((long long)x1) - 1;
+            if ((m0 & rec0) | (m1 & rec1))
+                single = 0;
+            put_rec_byte(r, 2 + 2 * n, l);
+            put_rec_byte(r, 3 + 2 * n, t);
+            ++n;
+            if (t < 64) {
+                h0 |= 1ull << t;
+                rec0 |= 1ull << t;
+            } else {
+                h1 |= 1ull << (t - 64);
+                rec1 |= 1ull << (t - 64);
+            }
+            progress = true;
+        }
+    }
+    r[0] |= n | (single << 8);
+    return r;
+}
+
+template <int MAXC, int BATCH, bool NTL, int NTS>
+__global__ __launch_bounds__(kBlock) void k_decode_cascade(v4u* shards, const v4u* __restrict__ parity,
+                                                           uint32_t total, uint32_t C, FastDiv divC,
+                                                           uint32_t n_hdr_blocks, PeelArgs A, rfec_kmask M)
+{
+    if (blockIdx.x < n_hdr_blocks) {
+        peel_block<true, kFusedPeelDwords, true>(A, M, blockIdx.x);
+        return;
+    }
+    __shared__ uint32_t lplan[RFEC_MAX_LINES];
+    const rfec_kplan& P = M.plan;
+    stage_plan(lplan, P);
+    const uint32_t t = (blockIdx.x - n_hdr_blocks) * kBlock + threadIdx.x;
+    if (t >= total)
+        return;
+    const uint32_t g = fdiv(t, divC);
+    const uint32_t j = t - g * divC.d; // chunk column (divC.d = chunks of work per slot)
+    const v4u r0 = P.k <= 64 ? mask_schedule<false>(M, P.n_lines, A.present[2 * g], 0, A.parity_present[g])
+                              : mask_schedule<true>(M, P.n_lines, A.present[2 * g], A.present[2 * g + 1],
+                                                    A.parity_present[g]);
+    if ((r0[0] & 0xffu) == 0)
+        return;
+    // n_lines <= 7: every step sits in the 16 bytes of r0; the record pointer
+    // (the peel's, being written meanwhile) is valid memory but never read
+    replay<MAXC, BATCH, NTL, NTS>(shards + (size_t)g * P.k * C + j, parity + (size_t)g * P.n_lines * C + j,
+                                  A.sched + (size_t)g * A.rec_bytes, r0, C, 1u, lplan);
+}
+
+// Exact replay of the listed groups (see k_decode_cascade), grid-stride over
+// (listed group, chunk column); a counter from another launch counts 0.
+template <int MAXC, bool NTL, int NTS>
+__global__ __launch_bounds__(kBlock) void k_decode_fixup(v4u* shards, const v4u* __restrict__ parity,
+                                                         const uint8_t* __restrict__ sched,
+                                                         const unsigned long long* __restrict__ fixc,
+                                                         const uint32_t* __restrict__ fixlist, uint32_t gen,
+                                                         uint32_t groups, uint32_t C, FastDiv divC,
+                                                         uint32_t rec_bytes, rfec_kplan P)
+{
+    __shared__ uint32_t lplan[RFEC_MAX_LINES];
+    stage_plan(lplan, P);
+    const unsigned long long c = *fixc;
+    const uint32_t n = (uint32_t)(c >> 32) == gen ? min((uint32_t)c, groups) : 0u;
+    const uint32_t total = n * divC.d;
+    for (uint32_t it = blockIdx.x * kBlock + threadIdx.x; it < total; it += gridDim.x * kBlock) {
+        const uint32_t gi = fdiv(it, divC);
+        const uint32_t j = it - gi * divC.d;
+        const uint32_t g = fixlist[gi];
+        if (g >= groups)
+            continue;
+        const uint8_t* rec = sched + (size_t)g * rec_bytes;
+        replay<MAXC, 1, NTL, NTS>(shards + (size_t)g * P.k * C + j, parity + (size_t)g * P.n_lines * C + j, rec,
+                                  *reinterpret_cast<const v4u*>(rec), C, 0u, lplan);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Recover, fused form for plans whose lines are pairwise disjoint (the row
 // layer alone, strip mode).  No recovery there can complete another line, so
 // which lines fire follows from the received masks alone and no schedule has
@@ -868,7 +1018,6 @@ __global__ __launch_bounds__(kBlock) void k_recover_pipe(v4u* shards, const v4u*
 // header checks reject is still written, into an erased slot whose recovered
 // bit stays clear (rfec_recover_batch documents such slots as unspecified).
 // ---------------------------------------------------------------------------
-constexpr int kFusedPeelDwords = 4096; // 16 KiB: the payload blocks carry this allocation too
 
 __device__ __forceinline__ bool has_bit(uint64_t h0, uint64_t h1, uint32_t i)
 {
@@ -1304,6 +1453,43 @@ void launch_fused_gw(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_k
 #undef RFEC_FUSED_GW
 }
 
+// one-launch cascade decode + the fix-up replay (sp as launch_fused)
+template <int MAXC, int BATCH>
+void launch_cascade(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M)
+{
+    const dim3 grid(F.n_hdr + blocks_for(F.total));
+    // fix-up: a small grid (the list is empty unless headers disagree with the masks)
+    const uint32_t fb = blocks_for(F.total) < 128u ? blocks_for(F.total) : 128u;
+#define RFEC_CASCADE(NTL, NTS)                                                                                    \
+    hipLaunchKernelGGL((k_decode_cascade<MAXC, BATCH, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards,       \
+                       F.parity, F.total, F.C, F.f, F.n_hdr, B, M);                                               \
+    hipLaunchKernelGGL((k_decode_fixup<MAXC, NTL, NTS>), dim3(fb), dim3(kBlock), 0, F.stream, F.shards, F.parity,  \
+                       B.sched, B.fixc, B.fixlist, B.gen, B.groups, F.C, F.f, B.rec_bytes, M.plan)
+    switch (sp) {
+    case -1: RFEC_CASCADE(false, 1); break;
+    case 0: RFEC_CASCADE(true, 0); break;
+    case 2: RFEC_CASCADE(true, 2); break;
+    case 3: RFEC_CASCADE(true, 3); break;
+    default: RFEC_CASCADE(true, 1); break;
+    }
+#undef RFEC_CASCADE
+}
+
+// fix-up generation: a per-process sequence from a time/pid seed, so that a
+// workspace left by an earlier launch (or process) never matches
+uint32_t next_gen()
+{
+    static std::atomic<uint32_t> g{0};
+    uint32_t v = g.fetch_add(1, std::memory_order_relaxed);
+    if (v == 0) {
+        const uint32_t seed = (uint32_t)time(nullptr) * 2654435761u ^ (uint32_t)getpid() * 40503u;
+        uint32_t expect = 1;
+        g.compare_exchange_strong(expect, seed | 1u);
+        v = g.fetch_add(1, std::memory_order_relaxed);
+    }
+    return v;
+}
+
 // sp: store policy, -1 = plain loads + non-temporal stores (A/B only)
 template <int MAXC, int NI>
 void launch_fused(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M)
@@ -1516,12 +1702,18 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
         maxc = P.line[l].count > maxc ? P.line[l].count : maxc;
     // disjoint plans (row layer alone, strip mode) decode in one launch
     const bool fused = B.disjoint && maxc <= 8 && !(flags & (RFEC_KFLAG_TWO_KERNEL_DECODE | RFEC_KFLAG_PIPE_DECODE));
+    // plans with cascades and at most 7 lines (the sender's matrix plans up to k = 16): one launch + fix-up
+    const bool cascade = !B.disjoint && P.n_lines <= 7 && maxc <= 8 &&
+                         !(flags & (RFEC_KFLAG_TWO_KERNEL_DECODE | RFEC_KFLAG_PIPE_DECODE));
+    B.fixc = reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(ws) + rfec_ws_fix_offset(P.n_lines, groups));
+    B.fixlist = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(B.fixc) + 16);
+    B.gen = cascade ? next_gen() : 0u;
     // LDS per group: K + NL header records (5 dwords) + NL u16 sizes; block
     // ranges start on 8-group boundaries so the staged slices are 16-B aligned
     const uint32_t per = 5u * P.k + 6u * P.n_lines;
     // (at most 64 groups per block: the peel is one serial chain per lane, so
     // more, smaller blocks give each SIMD more chains to interleave)
-    uint32_t gpb = ((fused ? kFusedPeelDwords : kPeelDwords) - 8) / per;
+    uint32_t gpb = ((fused || cascade ? kFusedPeelDwords : kPeelDwords) - 8) / per;
     gpb = gpb > 64u ? 64u : gpb;
     if (gpb >= 8)
         gpb &= ~7u;
@@ -1566,6 +1758,15 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
             launch_fused<4, 1>(F, sp, B, *M);
         else
             launch_fused<8, 1>(F, sp, B, *M);
+        return (int)hipGetLastError();
+    }
+    if (cascade) {
+        const FusedArgs F = {sh, pp, total, C, f, n_hdr, st};
+        const int sp = ntl ? store_policy(flags, kRecoverStoreDefault) : -1;
+        if (maxc <= 4)
+            launch_cascade<4, 2>(F, sp, B, *M);
+        else
+            launch_cascade<8, 1>(F, sp, B, *M);
         return (int)hipGetLastError();
     }
     hipLaunchKernelGGL(k_peel_lds, dim3(n_hdr), dim3(kBlock), 0, st, B, *M);

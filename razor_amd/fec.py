@@ -592,7 +592,7 @@ class DeviceBatch:
         self.present = torch.zeros((groups, 2), dtype=torch.int64, device=dev)
         self.parity_present = torch.zeros((groups,), dtype=torch.int64, device=dev)
         self.recovered = torch.zeros((groups, 2), dtype=torch.int64, device=dev)
-        ws = groups * ((2 + 2 * self.n + 15) // 16 * 16)  # rfec_recover_workspace_size()
+        ws = (groups * ((2 + 2 * self.n + 15) // 16 * 16) + 15) // 16 * 16 + 16 + 4 * groups  # rfec_recover_workspace_size()
         self.workspace = torch.zeros((max(16, ws),), dtype=u8, device=dev)
 
     def encode(self, lib: Native, stream=None):

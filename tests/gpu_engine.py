@@ -18,10 +18,11 @@ def _host(t: torch.Tensor, dtype, shape) -> np.ndarray:
 
 
 class GpuEngine:
-    def __init__(self, video_size=1000, device="cuda:0", tuning=0):
+    def __init__(self, video_size=1000, device="cuda:0", tuning=0, random_workspace=False):
         self.lib = native(video_size)
         self.device = torch.device(device)
         self.tuning = tuning
+        self.random_workspace = random_workspace  # recover workspace starts as random bytes (not zeroed)
 
     def encode(self, plan, shards, hdr, capacity):
         G, k, stride = shards.shape
@@ -53,7 +54,9 @@ class GpuEngine:
         d_f = _dev(np.ascontiguousarray(fsize, np.uint16), self.device)
         d_pp = _dev(np.ascontiguousarray(pp, np.uint64), self.device)
         d_rec = torch.full((G * 16,), 0xEE, dtype=torch.uint8, device=self.device)
-        ws = torch.zeros((max(16, self.lib.workspace_size(plan, G)),), dtype=torch.uint8, device=self.device)
+        nws = max(16, self.lib.workspace_size(plan, G))
+        ws = (torch.randint(0, 256, (nws,), dtype=torch.uint8, device=self.device) if self.random_workspace
+              else torch.zeros((nws,), dtype=torch.uint8, device=self.device))
         self.lib.set_tuning(self.tuning)
         try:
             self.lib.recover_batch(plan, G, stride, capacity, d_sh.data_ptr(), d_h.data_ptr(), d_pr.data_ptr(),

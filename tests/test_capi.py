@@ -76,7 +76,7 @@ def test_argument_validation(product):
     bad.line[0].count = 20  # member beyond k
     with pytest.raises(RfecError):
         product.encode_batch(bad, 4, 1200, 1200, 1, 1, 1, 1, 1, None)
-    assert product.workspace_size(plan, 100) == 100 * 16  # 2 + 2*3 bytes -> 16
+    assert product.workspace_size(plan, 100) == 100 * 16 + 16 + 4 * 100  # records (2 + 2*3 -> 16 B), fix-up list
     with pytest.raises(RfecError):  # groups * k beyond 32 bits
         product.zero_tails(1 << 30, 8, 1200, 1, 1, None)
 

@@ -354,3 +354,73 @@ def test_full_size_digest_gpu(gpu, oracle1000, name):
 
     c = fd.cases()[name]
     assert fd.digest(gpu().encode, oracle1000, c, chunk=65536) == c["sha256"]
+
+
+def _mask_peel(plan, k, present, pp):
+    """Recovered mask of the canonical peel over the masks alone (no header checks)."""
+    have = int(present)
+    rec = 0
+    progress = True
+    while progress:
+        progress = False
+        for l in range(plan.n_lines):
+            if not (int(pp) >> l) & 1:
+                continue
+            mem = plan.members(l)
+            miss = [i for i in mem if not (have >> i) & 1]
+            if len(miss) == 1 and len(miss) < len(mem):
+                have |= 1 << miss[0]
+                rec |= 1 << miss[0]
+                progress = True
+    return rec
+
+
+@pytest.mark.parametrize("tuning", ["default", "two_kernel", "nt_stores"])
+def test_cascade_header_rejections_gpu(gpu, oracle1000, tuning):
+    """Full 3x4 plan groups whose headers make the exact peel reject lines the
+    masks alone would fire (fec_data_size above capacity, a member larger than
+    fec_data_size): the one-launch cascade decode replays those groups' exact
+    schedules in its fix-up pass and must equal the oracle, recovered masks,
+    headers and data.  The workspace starts as random bytes."""
+    o = oracle1000
+    k, G, S = 10, 1024, 1000
+    plan = o.plan_from_fraction(k, 80, 3)
+    assert plan.n_lines == 7
+    rng = np.random.default_rng(77)
+    shards, hdr = o.fill_groups(9, G, k, S, ragged=True)
+    cap = min(o.video_size, shards.shape[-1])
+    parity, meta, fsize, _ = o.encode_batch(plan, shards, hdr, cap)
+    present = np.zeros((G, 2), np.uint64)
+    pp = np.full(G, (1 << plan.n_lines) - 1, np.uint64)
+    shards_rx, hdr_rx, fsize_rx = shards.copy(), hdr.copy(), fsize.copy()
+    for g in range(G):
+        m = (1 << k) - 1
+        for i in rng.choice(k, int(rng.integers(1, 5)), replace=False):
+            m &= ~(1 << int(i))
+            shards_rx[g, i] = 0xA5
+            hdr_rx[g, i] = np.zeros((), po.HDR_DTYPE)
+        present[g, 0] = m
+        if rng.random() < 0.2:
+            pp[g] &= ~np.uint64(1 << int(rng.integers(plan.n_lines)))
+        r = rng.random()
+        if r < 0.25:
+            fsize_rx[g, rng.integers(plan.n_lines)] = cap + 1
+        elif r < 0.5:
+            l = int(rng.integers(plan.n_lines))
+            fsize_rx[g, l] = max(1, int(fsize_rx[g, l]) - 7)
+        elif r < 0.7:
+            i = int(rng.integers(k))
+            if (m >> i) & 1:
+                hdr_rx[g, i]["size"] = min(cap, int(hdr_rx[g, i]["size"]) + 50)
+    e_s, e_h, e_rec = o.recover_batch(plan, shards_rx, hdr_rx, present, parity, meta, fsize_rx, pp, cap)
+    rejected = sum(int(e_rec[g, 0]) != _mask_peel(plan, k, present[g, 0], pp[g]) for g in range(G))
+    assert rejected >= 20, f"only {rejected} groups where the header checks change the peel"
+    eng = gpu(tuning=TUNINGS[tuning], random_workspace=True)
+    out_s, out_h, rec = eng.recover(plan, shards_rx, hdr_rx, present, parity, meta, fsize_rx, pp, cap)
+    assert np.array_equal(rec, e_rec)
+    for g in range(G):
+        for i in range(k):
+            if (int(rec[g, 0]) >> i) & 1:
+                assert out_h[g, i] == e_h[g, i], f"group {g} segment {i}: header"
+                L = int(e_h[g, i]["size"])
+                assert np.array_equal(out_s[g, i, :L], e_s[g, i, :L]), f"group {g} segment {i}: data"
