@@ -1478,6 +1478,7 @@ typedef struct {
     uint64_t ppm;          /* registered parities, by plan line */
     uint32_t fec_ts;       /* flex->fec_ts = send_ts of the parity that created it (sim_fec.c:157) */
     int ref_ok;            /* col >= 2 && row >= 1 && count >= 1 (flex_fec_receiver.c:214, 250) */
+    uint32_t gstamp;       /* == rx_sim.epoch: gslot is this device call's group slot */
 } rx_inst;
 
 typedef struct {
@@ -1504,6 +1505,9 @@ typedef struct {
     uint32_t nout, outcap;
     rfec_hdr* rh;          /* headers of delivered (recovered) segments the cache refers to */
     uint32_t nrh, rhcap;
+    uint32_t* dl;          /* instances that deliver in this device call */
+    uint32_t ndl, dlcap;
+    uint32_t epoch;        /* device call counter (rx_inst.gstamp) */
     int oom;
 } rx_sim;
 
@@ -1786,6 +1790,7 @@ static void rx_sim_free(rx_sim* X)
     free(X->pend);
     free(X->out);
     free(X->rh);
+    free(X->dl);
 }
 
 static int cmp_u32(const void* a, const void* b)
@@ -1943,15 +1948,27 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
         rep->host_us += now_us() - th;
         return RFEC_OK;
     }
-    /* group tables, shape-major, for the groups that deliver something */
+    /* group tables, shape-major, for the groups that deliver something (work
+     * proportional to the deliveries, not to the open flexes) */
     for (uint32_t s = 0; s < X->ns; ++s)
         X->S[s].n_groups = 0;
-    for (uint32_t gi = 0; gi < X->ng; ++gi)
-        X->G[gi].gslot = UINT32_MAX;
+    if (++X->epoch == 0) { /* wrapped: no instance may carry a stale stamp */
+        for (uint32_t gi = 0; gi < X->ng; ++gi)
+            X->G[gi].gstamp = 0;
+        X->epoch = 1;
+    }
+    X->ndl = 0;
     for (uint32_t q = 0; q < X->nout; ++q) {
-        rx_inst* g = &X->G[X->out[q].inst];
-        if (g->gslot == UINT32_MAX)
+        const uint32_t gi = X->out[q].inst;
+        rx_inst* g = &X->G[gi];
+        if (g->gstamp != X->epoch) {
+            RX_GROW(X->dl, X->ndl, X->dlcap, 1, uint32_t);
+            if (X->oom)
+                return set_err(RFEC_ENOMEM, "rx: delivery list", 0);
+            g->gstamp = X->epoch;
             g->gslot = X->S[g->shape].n_groups++;
+            X->dl[X->ndl++] = gi;
+        }
     }
     uint32_t nrows = 0, prows = 0, ngs = 0;
     for (uint32_t s = 0; s < X->ns; ++s) {
@@ -1990,10 +2007,8 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
     uint64_t* pres = (uint64_t*)(H + o_pres);
     uint64_t* ppm = (uint64_t*)(H + o_pp);
     int32_t* omap = (int32_t*)(H + o_omap);
-    for (uint32_t gi = 0; gi < X->ng; ++gi) {
-        const rx_inst* g = &X->G[gi];
-        if (g->shape == UINT32_MAX || g->gslot == UINT32_MAX)
-            continue;
+    for (uint32_t d = 0; d < X->ndl; ++d) {
+        const rx_inst* g = &X->G[X->dl[d]];
         const rx_shape* sh = &X->S[g->shape];
         const uint32_t gg = sh->group0 + g->gslot, r0 = sh->row0 + g->gslot * sh->count;
         const uint32_t p0 = sh->prow0 + g->gslot * sh->n_lines;
@@ -2055,7 +2070,7 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
     uint64_t* rec = (uint64_t*)(H + o_rec);
     if (ke || (e = hipMemcpyAsync(rec, D + d_rec, (size_t)ngs * 16, hipMemcpyDeviceToHost, sm)) != hipSuccess ||
         (e = hipStreamSynchronize(sm)) != hipSuccess)
-        return set_err(RFEC_EDEVICE, "rx: recover", ke ? ke : e);
+        return set_err(RFEC_EDEVICE, "rx: recover", ke ? ke : (int)e);
     rep->kernel_us += now_us() - tt;
     /* the device peel covers every packet the arrival-order pass delivered (same lines, a superset of
        the members at each firing); anything else is reported, not delivered */
@@ -2227,7 +2242,7 @@ int rfec_host_recv_datagrams(uint32_t n, uint32_t dstride, const uint8_t* dgram,
     int ke = rfec_launch_wire_parse(n, dstride, D, (const uint16_t*)(D + o_dl), stride, capacity,
                                     (rfec_wire_rec*)(D + o_rec), D + o_pay, t_rv.sm);
     if (ke || (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
-        return set_err(RFEC_EDEVICE, "recv: parse", ke ? ke : e);
+        return set_err(RFEC_EDEVICE, "recv: parse", ke ? ke : (int)e);
     const double parse = now_us() - tt;
     if (recs_out) {
         tt = now_us();
@@ -2409,7 +2424,7 @@ static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
                 (void)hipFree(dmap);
             (void)hipFree(arena);
             free(gmap);
-            rc = set_err(RFEC_EDEVICE, "rx session: row compaction", ke ? ke : e);
+            rc = set_err(RFEC_EDEVICE, "rx session: row compaction", ke ? ke : (int)e);
             goto done;
         }
         (void)hipFree(dmap);
@@ -2559,7 +2574,7 @@ int rfec_rx_session_push_datagrams(rfec_rx_session* S, uint32_t n, uint32_t dstr
     if (ke || (e = hipMemcpyAsync(t_rx.h, D + o_rec, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost,
                                   t_rv.sm)) != hipSuccess ||
         (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
-        return set_err(RFEC_EDEVICE, "recv: parse", ke ? ke : e);
+        return set_err(RFEC_EDEVICE, "recv: parse", ke ? ke : (int)e);
     const double staged = now_us() - tt;
     if (recs_out)
         memcpy(recs_out, t_rx.h, (size_t)n * sizeof(rfec_wire_rec));
