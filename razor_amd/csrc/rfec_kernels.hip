@@ -1636,11 +1636,13 @@ int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, ui
                          E, reinterpret_cast<hipStream_t>(stream)};
     if (flags & RFEC_KFLAG_PLAIN_LOADS) // A/B only
         return (int)launch_encode_t<false, 1>(a, flags);
-    // default store policy: write-through for the row layouts (kEncodeStoreDefault), non-temporal for the
-    // other plans, which write two parities per segment or more (the full row + column plan: 285 vs 312 us
-    // at k = 10, bench.py --full-plan)
+    // default store policy (rotated-buffer benches): write-through (kEncodeStoreDefault) for the row
+    // layouts over slots that split 128-B lines (k = 10 / 1,200 B: 173 vs 177 us non-temporal),
+    // non-temporal where every parity slot is whole lines (k = 32 / 256 B: 120 vs 136 us) and for the
+    // other plans, which write two parities per segment or more (the full row + column plan: 285 vs
+    // 312 us at k = 10)
     uint32_t col = 0;
-    const int dflt = is_row_layout(P, &col) ? kEncodeStoreDefault : 1;
+    const int dflt = is_row_layout(P, &col) && stride % 128 != 0 ? kEncodeStoreDefault : 1;
     switch (store_policy(flags, dflt)) {
     case 0: return (int)launch_encode_t<true, 0>(a, flags);
     case 2: return (int)launch_encode_t<true, 2>(a, flags);
