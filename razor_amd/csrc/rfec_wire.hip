@@ -772,14 +772,14 @@ __device__ __forceinline__ uint32_t pick(const uint32_t* w, uint32_t k)
     return v;
 }
 
-// parse at 20-byte lanes: registers capped for 8 waves per SIMD (two 16-wave
-// blocks per CU; a few spills) -- 570 vs 647 us for the SIM_SEG batch at the
-// compiler's 78 VGPRs (one block per CU), tools/parse_ab.sh
-template <int B>
-constexpr int kParseWaves = B == 20 ? 8 : 1;
+// parse: registers capped for 8 waves per SIMD (two 16-wave blocks per CU; a
+// few spills of loop-invariant addresses): SIM_SEG parse 570 vs 647 us at
+// 20-byte lanes (78 VGPRs uncapped), 721 vs 748 us at 32-byte lanes (93 VGPRs,
+// 1,504-B slots), tools/parse_ab.sh, tools/parse32_ab.sh
+constexpr int kParseWaves = 8;
 
 template <int B>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWaves<B>))) void k_parse(const uint8_t* __restrict__ dgram,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWaves))) void k_parse(const uint8_t* __restrict__ dgram,
                                                   const uint16_t* __restrict__ dlen,
                                                   rfec_wire_rec* __restrict__ recs, uint8_t* __restrict__ payload,
                                                   uint32_t n, uint32_t dstride, uint32_t stride, uint32_t capacity)

@@ -48,6 +48,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--groups", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--dstride", type=int, default=0, help="datagram slot width for both kinds (e.g. 1504: 1500-B receive slots, 32-byte lanes)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     G, k, n, S = args.groups, 10, 3, 1200
@@ -82,7 +83,7 @@ def main():
     sstamp["transport_seq"] = np.arange(NS)
     to = lambda a: torch.from_numpy(a.view(np.uint8).reshape(-1).copy()).to(dev)  # noqa: E731
     d_meta, d_fs, d_fst, d_hdr, d_sst = to(meta), to(np.full(NF, S, np.uint16)), to(fstamp), to(hdr), to(sstamp)
-    DF, DS = 1264, 1248  # datagram slots: >= 1249 / >= 1236, multiples of 16
+    DF, DS = (args.dstride, args.dstride) if args.dstride else (1264, 1248)  # slots: >= 1249 / >= 1236, multiples of 16
     dg_f = torch.empty((NF, DF), dtype=torch.uint8, device=dev)
     dl_f = torch.empty((NF,), dtype=torch.int16, device=dev)
     dg_s = torch.empty((NS, DS), dtype=torch.uint8, device=dev)
