@@ -313,6 +313,15 @@ int rfec_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacity, cons
     return e ? set_err(RFEC_EDEVICE, "wire_frame_seg launch", e) : RFEC_OK;
 }
 
+/* the longest of n host-side datagram lengths (0 for none) */
+static uint32_t max_dlen(const uint16_t* dlen, uint32_t n)
+{
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        m = dlen[i] > m ? dlen[i] : m;
+    return m;
+}
+
 int rfec_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen, uint32_t stride,
                     uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload, void* stream)
 {
@@ -323,7 +332,7 @@ int rfec_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const ui
         return RFEC_OK;
     if (!dgram || !dlen || !recs || !payload)
         return set_err(RFEC_EINVAL, "NULL buffer", 0);
-    const int e = rfec_launch_wire_parse(n, dstride, dgram, dlen, stride, capacity, recs, payload, stream);
+    const int e = rfec_launch_wire_parse(n, dstride, dgram, dlen, stride, capacity, recs, payload, 0, stream);
     return e ? set_err(RFEC_EDEVICE, "wire_parse launch", e) : RFEC_OK;
 }
 
@@ -2240,7 +2249,7 @@ int rfec_host_recv_datagrams(uint32_t n, uint32_t dstride, const uint8_t* dgram,
     const double h2d = now_us() - tt;
     tt = now_us();
     int ke = rfec_launch_wire_parse(n, dstride, D, (const uint16_t*)(D + o_dl), stride, capacity,
-                                    (rfec_wire_rec*)(D + o_rec), D + o_pay, t_rv.sm);
+                                    (rfec_wire_rec*)(D + o_rec), D + o_pay, max_dlen(dlen, n), t_rv.sm);
     if (ke || (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
         return set_err(RFEC_EDEVICE, "recv: parse", ke ? ke : (int)e);
     const double parse = now_us() - tt;
@@ -2570,7 +2579,7 @@ int rfec_rx_session_push_datagrams(rfec_rx_session* S, uint32_t n, uint32_t dstr
         return set_err(RFEC_EDEVICE, "recv: datagrams H2D", e);
     const double h2d_issue = now_us() - tt;
     int ke = rfec_launch_wire_parse(n, dstride, D, (const uint16_t*)(D + o_dl), stride, S->capacity,
-                                    (rfec_wire_rec*)(D + o_rec), D + o_pay, t_rv.sm);
+                                    (rfec_wire_rec*)(D + o_rec), D + o_pay, max_dlen(dlen, n), t_rv.sm);
     if (ke || (e = hipMemcpyAsync(t_rx.h, D + o_rec, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost,
                                   t_rv.sm)) != hipSuccess ||
         (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)

@@ -61,8 +61,11 @@ int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacit
 int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* shards,
                                const rfec_hdr* hdr, const rfec_seg_stamp* stamps, const uint32_t* order,
                                uint32_t dstride, uint8_t* dgram, uint16_t* dlen, void* stream);
+/* max_len: the longest datagram when the caller knows it (host-side lengths), else 0; slots
+ * wider than 1,280 B still take the 20-byte-lane parse when every datagram fits 1,280 B */
 int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
-                           uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload, void* stream);
+                           uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload,
+                           uint32_t max_len, void* stream);
 int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map, uint32_t rows, uint32_t stride,
                             void* stream);
 int rfec_launch_zero_tails(uint32_t slots, uint32_t stride, uint8_t* shards, const rfec_hdr* hdr, void* stream);

@@ -1036,10 +1036,12 @@ int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacit
 }
 
 int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
-                           uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload, void* stream)
+                           uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload,
+                           uint32_t max_len, void* stream)
 {
     hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
-    if (narrow(dstride))
+    // 20-byte lanes cover 1,280 bytes of a slot: enough when the slot or every datagram fits
+    if (narrow(dstride) || (max_len && max_len <= (uint32_t)(kWave * 20)))
         hipLaunchKernelGGL(k_parse<20>, dim3(grid_for<4>((const void*)k_parse<20>, n)), dim3(kBlock), 0, sm, dgram,
                            dlen, recs, payload, n, dstride, stride, capacity);
     else

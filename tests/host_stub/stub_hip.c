@@ -151,7 +151,8 @@ int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacit
 }
 
 int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
-                           uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload, void* stream)
+                           uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload,
+                           uint32_t max_len, void* stream)
 {
     return 0;
 }

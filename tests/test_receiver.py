@@ -288,3 +288,46 @@ def test_rx_session_datagrams(lib, oracle1000):
     assert len(out) == len(eo) > 0 and np.array_equal(out["hdr"][i], eo["hdr"][j])
     assert np.array_equal(outp[i], eop[j]) and sess.info()["max_ts"] == emts
     sess.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("long_junk", [False, True])
+def test_recv_datagrams_wide_slots(oracle1000, long_junk):
+    """rfec_host_recv_datagrams over 1,504-B receive slots: with every datagram
+    <= 1,280 B the 20-byte-lane parse runs (the host knows the lengths), with a
+    few 1,300-1,500-B junk datagrams the 32-byte-lane one; records, recovered
+    segments and payloads equal the oracle either way."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the -m gpu suite must run on an MI355X")
+    from razor_amd.fec import WIRE_REC_DTYPE, native
+
+    W = 1504
+    lib = native(1000)
+    order, (sdg, sdl, fdg, fdl), _ = _sender_stream(lib, 300, 5)
+    arrivals = _network(order, np.random.default_rng(9), loss=0.1, window=20, dup=0.02)
+    rng = np.random.default_rng(10)
+    rows = []
+    for kind, i in arrivals:
+        src, ln = (sdg, sdl) if kind == 0 else (fdg, fdl)
+        rows.append((src[i][:ln[i]].tobytes()))
+    if long_junk:
+        for p in rng.choice(len(rows), 5, replace=False):
+            rows[p] = rng.integers(0, 256, int(rng.integers(1300, 1501)), dtype=np.uint8).tobytes()
+    n = len(rows)
+    dg = np.zeros((n, W), np.uint8)
+    dl = np.zeros(n, np.uint16)
+    for a, b in enumerate(rows):
+        dg[a, :len(b)] = np.frombuffer(b, np.uint8)
+        dl[a] = len(b)
+    out, outp, mts, rep, recs = lib.host_recv_datagrams(n, W, dg.ctypes.data, dl.ctypes.data, STRIDE, 1000, 0,
+                                                        1 << 15, want_recs=True)
+    erecs, epay = oracle1000.parse_batch(dg, dl, STRIDE, 1000)
+    assert np.array_equal(recs.view(np.uint8), np.asarray(erecs).view(np.uint8).reshape(recs.view(np.uint8).shape))
+    assert (recs["status"] != 0).sum() == (5 if long_junk else 0)
+    eo, eop, emts, edrop = oracle1000.rx_recover(recs.view(WIRE_REC_DTYPE), epay, 1000, max_out=1 << 15)
+    idx = np.argsort(eo["hdr"]["seq"], kind="stable")
+    assert len(out) == len(eo) and len(out) > 0
+    assert np.array_equal(out["hdr"], eo["hdr"][idx]) and np.array_equal(outp, eop[idx])
+    assert mts == emts
