@@ -174,7 +174,8 @@ int rfec_encode_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, u
  *   parity_present   [G] u64: bit l = parity line l was received
  *   recovered        [G][2] u64 out: bit i = segment i was recovered here
  *   workspace        rfec_recover_workspace_size(plan, G) bytes of device memory
- *                    (one peeling-schedule record per group, a fix-up list)
+ *                    (one peeling-schedule record per group, a fix-up list),
+ *                    16-byte aligned; its contents need no initialisation
  * A line recovers its single missing member only under the conditions of
  * flex_recover_row/col and flex_fec_recover (sizes within fec_data_size).
  * `recovered` is authoritative: an erased slot whose bit stays clear holds
