@@ -1,3 +1,4 @@
+# full-plan (config 3 variant) store policies: default / NT (512) / plain (4) / WT+NT (192), then rocprofv3 stats
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/c3ab

@@ -1,3 +1,5 @@
+# session push cost, old vs new host code: build/ab/librazor_fec_v1200_old.so is the previous rfec_host.c
+# linked against the current kernel objects (see DESIGN.md section 8 for how it was made and the result)
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/sab

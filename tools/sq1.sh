@@ -1,3 +1,4 @@
+# UDP tests, then the list of available rocprofv3 counters on the box
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/sq1

@@ -1,3 +1,4 @@
+# SQ counters (two passes) of the full-plan decode kernels: peel, replay, encode
 set -o pipefail
 export TMPDIR=/tmp
 A="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
