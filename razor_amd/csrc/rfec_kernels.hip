@@ -18,11 +18,17 @@
 //    * meta blocks (the first ones in the grid): copy the headers of up to
 //      64 groups into LDS with coalesced dword loads, then one lane per
 //      (group, line) XORs its members' 20-byte records out of LDS.
-//  recover: one wave per group.  The wave loads the group's headers / line
-//    metadata lane-parallel, computes the peeling schedule with wave-uniform
-//    (scalar) control flow, and runs each recovery XOR over its chunk columns
-//    as soon as the line fires, so cascaded recoveries read segments this
-//    same lane has just written.
+//  recover (rfec_launch_recover picks by plan):
+//    * disjoint lines (row layer, strip mode): k_decode_disjoint, one launch --
+//      header lanes (one per group and line) at the head of the grid, then one
+//      lane per (group, chunk column) XORing every line with one missing member;
+//    * lines that cascade (rows + columns), at most 7: k_decode_cascade, one
+//      launch -- the exact peel in header blocks, a mask-only replay of the
+//      same canonical schedule in the payload lanes -- plus k_decode_fixup for
+//      the groups whose header checks disagree with the masks;
+//    * otherwise k_peel_lds (schedule records) + k_recover_flat (replay);
+//      k_recover (one wave per group, schedule and XOR interleaved) stays as
+//      an A/B variant.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
