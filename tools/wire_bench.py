@@ -28,7 +28,7 @@ import torch
 ROOT = Path(__file__).resolve().parent.parent
 sys.path[:0] = [str(ROOT), str(ROOT / "oracle")]
 
-from razor_amd.fec import FEC_STAMP_DTYPE, SEG_STAMP_DTYPE, HDR_DTYPE, native  # noqa: E402
+from razor_amd.fec import FEC_STAMP_DTYPE, SEG_STAMP_DTYPE, HDR_DTYPE, Native, native  # noqa: E402
 
 HBM_PEAK = 8000.0
 
@@ -48,11 +48,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--groups", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--lib", default="", help="another build of the library (A/B)")
     ap.add_argument("--dstride", type=int, default=0, help="datagram slot width for both kinds (e.g. 1504: 1500-B receive slots, 32-byte lanes)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     G, k, n, S = args.groups, 10, 3, 1200
-    lib = native(1200)
+    lib = Native(1200, args.lib) if args.lib else native(1200)
     dev = torch.device("cuda:0")
     st = torch.cuda.Stream(dev)
     sp = st.cuda_stream
