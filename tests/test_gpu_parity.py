@@ -424,3 +424,40 @@ def test_cascade_header_rejections_gpu(gpu, oracle1000, tuning):
                 assert out_h[g, i] == e_h[g, i], f"group {g} segment {i}: header"
                 L = int(e_h[g, i]["size"])
                 assert np.array_equal(out_s[g, i, :L], e_s[g, i, :L]), f"group {g} segment {i}: data"
+
+
+@pytest.mark.parametrize("k", [6, 7, 9, 11, 12, 13, 15])
+@pytest.mark.parametrize("tuning", ["default", "two_kernel"])
+def test_full_plan_shapes_gpu(gpu, oracle1000, k, tuning):
+    """The sender's full plans of k = 6..15 (3 or 4 columns; up to 7 lines the
+    one-launch cascade decode runs by default, k = 15 has 8 and takes peel +
+    replay) against the oracle: 1-5 erasures and lost parities per group,
+    ragged sizes, recovered masks, headers and data bit-exact."""
+    o = oracle1000
+    plan = o.plan_from_fraction(k, 80, 3)
+    assert (plan.n_lines <= 7) == (k != 15)
+    G = 512
+    rng = np.random.default_rng(100 + k)
+    shards, hdr = o.fill_groups(20 + k, G, k, 1000, ragged=True)
+    parity, meta, fsize, _ = o.encode_batch(plan, shards, hdr, 1000)
+    present = np.zeros((G, 2), np.uint64)
+    pp = np.full(G, (1 << plan.n_lines) - 1, np.uint64)
+    rx, rh = shards.copy(), hdr.copy()
+    for g in range(G):
+        m = (1 << k) - 1
+        for i in rng.choice(k, int(rng.integers(1, 6)), replace=False):
+            m &= ~(1 << int(i))
+            rx[g, i] = 0xA5
+            rh[g, i] = np.zeros((), po.HDR_DTYPE)
+        present[g, 0] = m
+        if rng.random() < 0.25:
+            pp[g] &= ~np.uint64(1 << int(rng.integers(plan.n_lines)))
+    e_s, e_h, e_rec = o.recover_batch(plan, rx, rh, present, parity, meta, fsize, pp, 1000)
+    out_s, out_h, rec = gpu(tuning=TUNINGS[tuning]).recover(plan, rx, rh, present, parity, meta, fsize, pp, 1000)
+    assert np.array_equal(rec, e_rec)
+    assert int(sum(bin(int(x)).count("1") for x in rec[:, 0])) > G // 2
+    for g in range(G):
+        for i in range(k):
+            if (int(rec[g, 0]) >> i) & 1:
+                assert out_h[g, i] == hdr[g, i] and out_h[g, i] == e_h[g, i]
+                assert np.array_equal(out_s[g, i], shards[g, i]), f"k={k} group {g} segment {i}"
