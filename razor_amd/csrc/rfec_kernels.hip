@@ -22,7 +22,7 @@
 //    * disjoint lines (row layer, strip mode): k_decode_disjoint, one launch --
 //      header lanes (one per group and line) at the head of the grid, then one
 //      lane per (group, chunk column) XORing every line with one missing member;
-//    * lines that cascade (rows + columns), at most 7: k_decode_cascade, one
+//    * lines that cascade (rows + columns), up to 8 members: k_decode_cascade, one
 //      launch -- the exact peel in header blocks, a mask-only replay of the
 //      same canonical schedule in the payload lanes -- plus k_decode_fixup for
 //      the groups whose header checks disagree with the masks;
@@ -763,7 +763,7 @@ __device__ void peel_block(const PeelArgs& A, const rfec_kmask& M, uint32_t blk)
         rec[0] = (uint8_t)n;
         rec[1] = (uint8_t)single;
     }
-    if (FIXUP && rejected)
+    if (FIXUP && (rejected || n > 7)) // header checks disagree with the masks, or more steps than a record image
         fix_append(A, g);
     A.recovered[2 * g] = rec0;
     A.recovered[2 * g + 1] = rec1;
@@ -898,15 +898,16 @@ __global__ __launch_bounds__(kBlock) void k_recover_pipe(v4u* shards, const v4u*
 }
 
 // ---------------------------------------------------------------------------
-// Recover, one-launch form for plans with cascades (rows + columns), at most
-// 7 lines.  Header blocks at the head of the grid run the exact peel
-// (peel_block: headers, schedule records, recovered masks); every payload lane
-// (group, chunk column) derives the schedule from the received masks alone --
-// the same canonical peel without the header size checks -- and replays it.
+// Recover, one-launch form for plans with cascades (rows + columns).  Header
+// blocks at the head of the grid run the exact peel (peel_block: headers,
+// schedule records, recovered masks); every payload lane (group, chunk column)
+// derives the schedule from the received masks alone -- the same canonical
+// peel without the header size checks -- and replays up to 7 of its steps.
 // The two schedules differ only where a header check rejected a line the masks
-// fire; the peel lists those groups and k_decode_fixup, launched next, replays
-// their exact records over the mask-only writes (which touched only erased
-// slots, so nothing it reads).  Replaying an exact record is idempotent.
+// fire; the peel lists those groups, and those with more than 7 steps, and
+// k_decode_fixup, launched next, replays their exact records over the
+// mask-only writes (which touched only erased slots, so nothing it reads).
+// Replaying an exact record is idempotent.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void put_rec_byte(v4u& r, uint32_t pos, uint32_t v)
 {
@@ -939,6 +940,10 @@ __device__ __forceinline__ v4u mask_schedule(const rfec_kmask& M, uint32_t NL, u
             if (__popcll(x0) + (WIDE ? __popcll(x1) : 0) != 1 || ((m0 & h0) | (m1 & h1)) == 0)
                 continue;
             const uint32_t t = x0 ? (uint32_t)__ffsll((long long)x0) - 1 : 64u + (uint32_t)__ffsll((long long)x1) - 1;
+            if (n == 7) { // the record image holds 7 steps: the peel lists this group for the fix-up
+                r[0] |= n | (single << 8);
+                return r;
+            }
             if ((m0 & rec0) | (m1 & rec1))
                 single = 0;
             put_rec_byte(r, 2 + 2 * n, l);
@@ -980,7 +985,8 @@ __global__ __launch_bounds__(kBlock) void k_decode_cascade(v4u* shards, const v4
                                                     A.parity_present[g]);
     if ((r0[0] & 0xffu) == 0)
         return;
-    // n_lines <= 7: every step sits in the 16 bytes of r0; the record pointer
+    // at most 7 steps (mask_schedule stops there; longer schedules are the
+    // fix-up's): every step sits in the 16 bytes of r0, the record pointer
     // (the peel's, being written meanwhile) is valid memory but never read
     replay<MAXC, BATCH, NTL, NTS>(shards + (size_t)g * P.k * C + j, parity + (size_t)g * P.n_lines * C + j,
                                   A.sched + (size_t)g * A.rec_bytes, r0, C, 1u, lplan);
@@ -1710,8 +1716,8 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
         maxc = P.line[l].count > maxc ? P.line[l].count : maxc;
     // disjoint plans (row layer alone, strip mode) decode in one launch
     const bool fused = B.disjoint && maxc <= 8 && !(flags & (RFEC_KFLAG_TWO_KERNEL_DECODE | RFEC_KFLAG_PIPE_DECODE));
-    // plans with cascades and at most 7 lines (the sender's matrix plans up to k = 16): one launch + fix-up
-    const bool cascade = !B.disjoint && P.n_lines <= 7 && maxc <= 8 &&
+    // plans with cascades (the sender's matrix plans): one launch + fix-up
+    const bool cascade = !B.disjoint && maxc <= 8 &&
                          !(flags & (RFEC_KFLAG_TWO_KERNEL_DECODE | RFEC_KFLAG_PIPE_DECODE));
     B.fixc = reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(ws) + rfec_ws_fix_offset(P.n_lines, groups));
     B.fixlist = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(B.fixc) + 16);

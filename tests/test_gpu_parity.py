@@ -426,16 +426,15 @@ def test_cascade_header_rejections_gpu(gpu, oracle1000, tuning):
                 assert np.array_equal(out_s[g, i, :L], e_s[g, i, :L]), f"group {g} segment {i}: data"
 
 
-@pytest.mark.parametrize("k", [6, 7, 9, 11, 12, 13, 15])
+@pytest.mark.parametrize("k", [6, 7, 9, 11, 12, 13, 15, 16])
 @pytest.mark.parametrize("tuning", ["default", "two_kernel"])
 def test_full_plan_shapes_gpu(gpu, oracle1000, k, tuning):
-    """The sender's full plans of k = 6..15 (3 or 4 columns; up to 7 lines the
-    one-launch cascade decode runs by default, k = 15 has 8 and takes peel +
-    replay) against the oracle: 1-5 erasures and lost parities per group,
-    ragged sizes, recovered masks, headers and data bit-exact."""
+    """The sender's full plans of k = 6..15 (3 or 4 columns, 5-8 lines: the
+    one-launch cascade decode by default, peel + replay as the A/B) against
+    the oracle: 1-5 erasures and lost parities per group, ragged sizes,
+    recovered masks, headers and data bit-exact."""
     o = oracle1000
     plan = o.plan_from_fraction(k, 80, 3)
-    assert (plan.n_lines <= 7) == (k != 15)
     G = 512
     rng = np.random.default_rng(100 + k)
     shards, hdr = o.fill_groups(20 + k, G, k, 1000, ragged=True)
