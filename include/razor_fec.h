@@ -568,6 +568,8 @@ int rfec_rx_session_get_info(const rfec_rx_session* s, rfec_rx_session_info* inf
 #define RFEC_TUNE_GROUP_WAVE 8192u  /* payload lanes mapped per wave over whole groups (not the flat chunk index) */
 #define RFEC_TUNE_XCD_SWIZZLE 16384u /* consecutive payload blocks on the same XCD */
 #define RFEC_TUNE_LDS_HDR_PEEL 32768u /* fused decode: header work in LDS-staged peel blocks (default: one lane per group and line) */
+#define RFEC_TUNE_FLAT_ENCODE 65536u  /* row encode: one lane per (group, chunk column), all members (default: one lane per parity chunk) */
+#define RFEC_TUNE_META_TAIL 131072u   /* encode: header (meta) blocks at the tail of the grid instead of its head */
 /* (defaults: parity stores write-through, recovered stores non-temporal) */
 #define RFEC_TUNE_DIAG_NO_META 256u /* DIAGNOSTIC ONLY: skip fec_meta (wrong output) */
 void rfec_set_tuning(unsigned flags);

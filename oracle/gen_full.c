@@ -93,6 +93,15 @@ static void run_case(FILE* js, const full_case* fc, int first)
     sha256_ctx cref, cora;
     sha256_init(&cref);
     sha256_init(&cora);
+    /* per-rank slice digests for the multi-GPU split (razor_amd/dist.py
+     * shard_groups: rank r of N owns [G*r/N, G*(r+1)/N)), config 4 only */
+    static const uint32_t NS[3] = {2, 4, 8};
+    const int slices = fc->cfg == 4;
+    sha256_ctx cs[3][8];
+    uint32_t cur[3] = {0, 0, 0};
+    if (slices)
+        for (int a = 0; a < 3; ++a)
+            sha256_init(&cs[a][0]);
     uint64_t state[2] = {0, 0};
     for (uint32_t g0 = 0; g0 < fc->G; g0 += CHUNK) {
         const uint32_t ng = fc->G - g0 < CHUNK ? fc->G - g0 : CHUNK;
@@ -137,6 +146,12 @@ static void run_case(FILE* js, const full_case* fc, int first)
                 fs[l] = (uint16_t)L;
             }
             digest_group(&cref, par, meta, fs, n, stride);
+            for (int a = 0; slices && a < 3; ++a) {
+                const uint64_t g = (uint64_t)g0 + gl;
+                while (g >= (uint64_t)fc->G * (cur[a] + 1) / NS[a])
+                    sha256_init(&cs[a][++cur[a]]);
+                digest_group(&cs[a][cur[a]], par, meta, fs, n, stride);
+            }
         }
         oracle_encode_batch(&plan, ng, stride, S, shards, hdr, opar, ometa, ofs, ost);
         for (uint32_t gl = 0; gl < ng; ++gl) {
@@ -160,9 +175,25 @@ static void run_case(FILE* js, const full_case* fc, int first)
     fprintf(js,
             "%s  {\"name\": \"%s\", \"config_id\": %llu, \"groups\": %u, \"k\": %u, \"S\": %u, \"stride\": %u, "
             "\"ragged\": %d, \"plan\": \"%s\", \"pf\": %d, \"row\": %d, \"col\": %d, \"layers\": %u, "
-            "\"n_lines\": %u, \"window\": %u, \"sha256\": \"%s\"}",
+            "\"n_lines\": %u, \"window\": %u, \"sha256\": \"%s\"",
             first ? "" : ",\n", fc->name, (unsigned long long)fc->cfg, fc->G, k, S, stride, fc->ragged,
             fc->matrix ? "matrix" : "fraction", fc->pf, fc->row, fc->col, fc->layers, n, span, h1);
+    if (slices) {
+        fprintf(js, ", \"slices\": {");
+        for (int a = 0; a < 3; ++a) {
+            fprintf(js, "%s\"%u\": [", a ? ", " : "", NS[a]);
+            for (uint32_t r = 0; r < NS[a]; ++r) {
+                uint8_t d[32];
+                char hx[65];
+                sha256_final(&cs[a][r], d);
+                sha256_hex(d, hx);
+                fprintf(js, "%s\"%s\"", r ? ", " : "", hx);
+            }
+            fprintf(js, "]");
+        }
+        fprintf(js, "}");
+    }
+    fprintf(js, "}");
     free(shards);
     free(hdr);
     free(par);

@@ -32,6 +32,8 @@ typedef struct {
 #define RFEC_KFLAG_GROUP_WAVE RFEC_TUNE_GROUP_WAVE
 #define RFEC_KFLAG_XCD_SWIZZLE RFEC_TUNE_XCD_SWIZZLE
 #define RFEC_KFLAG_LDS_HDR_PEEL RFEC_TUNE_LDS_HDR_PEEL
+#define RFEC_KFLAG_FLAT_ENCODE RFEC_TUNE_FLAT_ENCODE
+#define RFEC_KFLAG_META_TAIL RFEC_TUNE_META_TAIL
 
 int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, uint32_t capacity,
                        const uint8_t* shards, const rfec_hdr* hdr, uint8_t* parity, rfec_hdr* meta,

@@ -397,6 +397,53 @@ __global__ __launch_bounds__(kBlock) void k_encode_rows(const v4u* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// Encode payload, rows-of-COL, output-mapped (default for row layouts): one
+// lane per PARITY chunk (group, row, chunk column), the lane loads its row's
+// COL (last row: K - (R-1)*COL) member chunks and stores one chunk.  Lane t
+// writes parity chunk t when the slots are packed (stride == capacity), so
+// every wave's store is 1 KiB of consecutive, 128-B-aligned parity bytes:
+// whole lines, never two partial writes of one line from two waves on two
+// XCDs, which the flat (group, chunk) mapping makes at every 1,200-B slot
+// edge.  Row layouts have no member in two lines, so no chunk is loaded twice.
+// tools/encode_lab.hip: 165-171 us vs 178-211 us flat at k = 10 / 1,200 B,
+// equal to a 10-read : 3-write probe over contiguous streams.
+// Meta blocks sit at the head of the grid, or at its tail (META_TAIL).
+// ---------------------------------------------------------------------------
+template <int K, int COL, bool NTL, int NTS>
+__global__ __launch_bounds__(kBlock) void k_encode_out(const v4u* __restrict__ shards, v4u* __restrict__ parity,
+                                                       uint32_t total, uint32_t C, FastDiv divC, FastDiv divRC,
+                                                       uint32_t meta_first, EncMeta E, rfec_kplan P)
+{
+    const uint32_t mb = blockIdx.x - meta_first; // meta_first: 0 (head) or the payload block count (tail)
+    if (mb < E.n_meta_blocks) {
+        meta_block(mb, E.hdr_dw, E.meta_dw, E.fsize, E.status, E.groups, E.capacity, E.gpb, P);
+        return;
+    }
+    constexpr int R = (K + COL - 1) / COL;
+    constexpr int LAST = K - (R - 1) * COL;
+    const uint32_t b = meta_first ? blockIdx.x : blockIdx.x - E.n_meta_blocks;
+    const uint32_t t = b * kBlock + threadIdx.x;
+    if (t >= total)
+        return;
+    const uint32_t g = fdiv(t, divRC);
+    const uint32_t rem = t - g * divRC.d;
+    const uint32_t r = fdiv(rem, divC);
+    const uint32_t j = rem - r * divC.d;
+    const v4u* s = shards + ((size_t)g * K + (size_t)r * COL) * C + j;
+    v4u v[COL];
+#pragma unroll
+    for (int q = 0; q < COL; ++q)
+        if (q < LAST || r < (uint32_t)(R - 1))
+            v[q] = ld16<NTL>(s + (size_t)q * C);
+    v4u acc = v[0];
+#pragma unroll
+    for (int q = 1; q < COL; ++q)
+        if (q < LAST || r < (uint32_t)(R - 1))
+            acc ^= v[q];
+    st16<NTS>(parity + ((size_t)g * R + r) * C + j, acc);
+}
+
+// ---------------------------------------------------------------------------
 // Encode payload, rows-of-COL, group-per-wave mapping.  Every wave covers
 // whole groups (gpw = max(1, 64 / cd) of them, NI items per lane): a slot's
 // last chunk and the next slot's first chunk, which share a 128-B line when
@@ -1385,8 +1432,23 @@ hipError_t launch_rows_gw(const EncLaunch& a, const GwGeom& g, uint32_t swz)
 }
 
 template <int K, int COL, bool NTL, int NTS>
+hipError_t launch_rows_out(const EncLaunch& a, unsigned flags)
+{
+    constexpr uint32_t R = (K + COL - 1) / COL;
+    const uint32_t C = a.stride / 16;
+    const uint64_t total = (uint64_t)a.groups * R * a.cd;
+    const uint32_t nb = blocks_for(total);
+    const uint32_t meta_first = (flags & RFEC_KFLAG_META_TAIL) ? nb : 0u;
+    hipLaunchKernelGGL((k_encode_out<K, COL, NTL, NTS>), dim3(a.E.n_meta_blocks + nb), dim3(kBlock), 0, a.stream, a.s,
+                       a.p, (uint32_t)total, C, make_fastdiv(a.cd), make_fastdiv(R * a.cd), meta_first, a.E, *a.P);
+    return hipGetLastError();
+}
+
+template <int K, int COL, bool NTL, int NTS>
 hipError_t launch_rows_v(const EncLaunch& a, unsigned flags)
 {
+    if (!(flags & (RFEC_KFLAG_FLAT_ENCODE | RFEC_KFLAG_GROUP_WAVE | RFEC_KFLAG_ITEMS2)))
+        return launch_rows_out<K, COL, NTL, NTS>(a, flags);
     if (flags & RFEC_KFLAG_GROUP_WAVE) {
         const GwGeom g = gw_geom(a.groups, a.cd);
         const uint32_t swz = (flags & RFEC_KFLAG_XCD_SWIZZLE) ? 1u : 0u;
@@ -1653,8 +1715,12 @@ int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, ui
     // non-temporal where every parity slot is whole lines (k = 32 / 256 B: 120 vs 136 us) and for the
     // other plans, which write two parities per segment or more (the full row + column plan: 285 vs
     // 312 us at k = 10)
+    // The output-mapped row kernel (default) writes whole lines: non-temporal
+    // (tools/step_ab.py: 172.7 us vs 185.8 write-through once the decode
+    // reads a parity set that is not MALL-resident).
     uint32_t col = 0;
-    const int dflt = is_row_layout(P, &col) && stride % 128 != 0 ? kEncodeStoreDefault : 1;
+    const int dflt =
+        (flags & RFEC_KFLAG_FLAT_ENCODE) && is_row_layout(P, &col) && stride % 128 != 0 ? kEncodeStoreDefault : 1;
     switch (store_policy(flags, dflt)) {
     case 0: return (int)launch_encode_t<true, 0>(a, flags);
     case 2: return (int)launch_encode_t<true, 2>(a, flags);

@@ -18,7 +18,8 @@ CASES = {c["name"]: c for c in MANIFEST["cases"]}
 TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "plain_stores": 4, "items2": 8, "wave_decode": 16,
            "pipe_decode": 32, "wt_stores": 64, "wt_nt_stores": 192, "nt_stores": 512,
            "generic_plain": 3, "two_kernel": 4096, "two_kernel_wt": 4096 | 64, "group_wave": 8192,
-           "group_wave_xcd": 8192 | 16384, "xcd": 16384, "lds_hdr_peel": 32768}
+           "group_wave_xcd": 8192 | 16384, "xcd": 16384, "lds_hdr_peel": 32768, "flat_encode": 65536,
+           "meta_tail": 131072, "meta_tail_nt": 131072 | 512}
 
 
 @pytest.fixture(scope="module")
@@ -39,7 +40,7 @@ def test_sender_random_fixture_gpu(gpu, oracle1000):
     pc.check_sender_random_case(gpu(), oracle1000, CASES["random_k"])
 
 
-@pytest.mark.parametrize("tuning", ["default", "generic", "group_wave", "group_wave_xcd"])
+@pytest.mark.parametrize("tuning", ["default", "generic", "group_wave", "group_wave_xcd", "flat_encode", "meta_tail"])
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "rows"])
 def test_rows_fixture_gpu(gpu, oracle1000, oracle1200, name, tuning):
     c = CASES[name]
@@ -144,7 +145,7 @@ def test_full_size_k10_roundtrip(product, oracle1200, layers):
     plan = lib.plan_from_fraction(k, 80, layers)
     shards, hdr, d_hdr = _device_batch(G, k, S, 1234)
     par, meta, fs, st = _run_encode(lib, plan, G, S, shards, d_hdr)
-    for tuning in (1, 2, 4, 8, 3, 64, 192, 512, 8192, 8192 | 16384, 16384):
+    for tuning in (1, 2, 4, 8, 3, 64, 192, 512, 8192, 8192 | 16384, 16384, 65536, 131072, 131072 | 512):
         par2, meta2, fs2, st2 = _run_encode(lib, plan, G, S, shards, d_hdr, tuning=tuning)
         assert torch.equal(par, par2) and torch.equal(meta, meta2) and torch.equal(fs, fs2), tuning
         del par2, meta2, fs2, st2
@@ -205,7 +206,7 @@ def test_full_size_k32_s256(product, oracle1000):
     assert plan.n_lines == 8
     shards, hdr, d_hdr = _device_batch(G, k, S, 99)
     par, meta, fs, st = _run_encode(lib, plan, G, S, shards, d_hdr)
-    for tuning in (1, 8, 8192, 8192 | 16384):
+    for tuning in (1, 8, 8192, 8192 | 16384, 65536, 131072):
         par2, meta2, fs2, _ = _run_encode(lib, plan, G, S, shards, d_hdr, tuning=tuning)
         assert torch.equal(par, par2) and torch.equal(meta, meta2) and torch.equal(fs, fs2), tuning
     idx = np.r_[0:4, G - 4:G]
