@@ -1,23 +1,36 @@
 """Benchmark: device-resident flex-FEC encode + decode on MI355X.
 
-Workload (BASELINE.json configs[2], the metric's config): per GPU, G = 65,536
+Workload (BASELINE.json configs[2], the metric's config, at N = 1): G = 65,536
 FEC groups of k = 10 segments of 1,200 bytes; the r = 3 row parities of the
 reference's 3x4 plan (rows {4,4,2}, flex_fec_sender.c:166-188); 2 erasures
 per group drawn from the 32 distinct-row pairs, recovered by peeling
-(flex_fec_receiver.c:105-150).  One step = encode every group, then recover
-every erased segment.  Inputs are synthetic, resident in HBM before timing.
+(flex_fec_receiver.c:105-150).  Payloads are the SURVEY §8(d) xorshift64*
+stream (config id 2, so the parity equals the reference digest c2 of
+tests/golden/full_hashes.json), generated on the device, resident in HBM
+before timing.
 
-Multi-GPU: one process per GPU (torchrun); groups are independent, so each
-rank encodes/decodes its own slice of the batch with no data-path collective
-(weak scaling); a barrier + max-over-ranks time bracket the timed steps.
+One step = encode one buffer set, then recover the set encoded one step
+earlier (receiver order: its parity arrived over the network, so it is not
+in the 256 MB MALL), over >= 2 disjoint buffer sets rotated per step.
+
+Multi-GPU (BASELINE.json configs[3]): one process per GPU; the driver starts
+them with torchrun, `bench.py --gpus N` alone starts them itself.  At
+WORLD_SIZE > 1 the default is config 4: 1,048,576 groups split into
+contiguous slices (razor_amd/dist.py), no data-path collective; the control
+plane (barrier, max-over-ranks time, byte sum) is a CPU gloo group, so no
+RCCL is brought up and several ranks may share one GPU.
 
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -33,6 +46,19 @@ from razor_amd.fec import HDR_DTYPE, native  # noqa: E402
 
 METRIC = "FEC encode+decode GiB/s (device-resident), 1200B pkts k=10/r=3; % HBM peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+GOLDEN = ROOT / "tests" / "golden" / "full_hashes.json"
+
+# name -> (k, S, plan, total groups, config id of the input stream, golden digest case)
+CONFIGS = {
+    "c3": dict(k=10, S=1200, plan="rows", groups=65536, config_id=2, golden="c2_k10_rows_S1200_G65536",
+               desc="BASELINE configs[2]: encode + decode, k=10 r=3, 1200 B, 2 erasures/group"),
+    "c3full": dict(k=10, S=1200, plan="full", groups=65536, config_id=3, golden="c3_k10_full_S1200_G65536",
+                   desc="configs[2] variant: the reference sender's full 3x4 plan (7 parities)"),
+    "c4": dict(k=10, S=1200, plan="rows", groups=1048576, config_id=4, golden="c4_k10_rows_S1200_G1048576",
+               desc="BASELINE configs[3]: 1M groups split over the GPUs, k=10 r=3, 1200 B"),
+    "c5": dict(k=32, S=256, plan="col4", groups=65536, config_id=5, golden="c5_k32_rows4_S256_G65536",
+               desc="BASELINE configs[4]: k=32 r=8 (8 rows of 4), 256 B"),
+}
 
 
 def log(*a):
@@ -40,6 +66,7 @@ def log(*a):
 
 
 def make_headers(G, k, S, group0):
+    """SURVEY §8(d) headers: contiguous packet ids (sim_sender.c:338)."""
     hdr = np.zeros((G, k), HDR_DTYPE)
     gi = (np.arange(G, dtype=np.uint64) + group0)[:, None]
     ii = np.arange(k, dtype=np.uint64)[None, :]
@@ -79,7 +106,7 @@ def peel_bytes(plan, k, erased, S):
 
 
 class Workload:
-    def __init__(self, lib, G, k, S, pf, device, group0, seed, stride=None, col=0, full_plan=False):
+    def __init__(self, lib, G, k, S, pf, device, group0, seed, stride=None, col=0, full_plan=False, config_id=2):
         self.lib, self.G, self.k, self.S = lib, G, k, S
         self.stride = stride or (S + 15) // 16 * 16  # slot width in HBM (>= S, multiple of 16)
         if col:  # explicit rows of `col` (config 5: k = 32 as 8 rows of 4)
@@ -90,13 +117,10 @@ class Workload:
             self.plan = lib.plan_from_fraction(k, pf, 1)  # row layer: r = 3 at k = 10
         self.n = self.plan.n_lines
         dev = device
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(seed)
-        if self.stride == S:
-            self.shards = torch.randint(0, 256, (G, k, S), dtype=torch.uint8, device=dev, generator=gen)
-        else:
-            self.shards = torch.zeros((G, k, self.stride), dtype=torch.uint8, device=dev)
-            self.shards[:, :, :S] = torch.randint(0, 256, (G, k, S), dtype=torch.uint8, device=dev, generator=gen)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        # SURVEY §8(d) payloads: xorshift64* stream of `config_id`, groups [group0, group0 + G)
+        self.shards = torch.empty((G, k, self.stride), dtype=torch.uint8, device=dev)
+        lib.fill_xorshift(self.shards.data_ptr(), config_id, group0, G, k, S, self.stride, st)
         self.hdr_np = make_headers(G, k, S, group0)
         self.hdr = torch.from_numpy(self.hdr_np.view(np.uint8).reshape(G, k, 20).copy()).to(dev)
         self.parity = torch.empty((G, self.n, self.stride), dtype=torch.uint8, device=dev)
@@ -166,6 +190,19 @@ class Workload:
         ok = ok and int(self.status.abs().sum()) == 0
         return bool(ok)
 
+    def digest(self, chunk=65536):
+        """SHA-256 of the encode outputs group by group, parity[n][stride] |
+        meta[n] (20 B) | fec_data_size[n] (u16 LE): the record
+        oracle/gen_full.c digests from the reference's flex_fec_generate."""
+        h = hashlib.sha256()
+        for g0 in range(0, self.G, chunk):
+            g1 = min(self.G, g0 + chunk)
+            n = g1 - g0
+            rec = torch.cat([self.parity[g0:g1].reshape(n, -1), self.meta[g0:g1].reshape(n, -1),
+                             self.fsize[g0:g1].view(torch.uint8).reshape(n, -1)], dim=1)
+            h.update(rec.cpu().numpy().tobytes())
+        return h.hexdigest()
+
 
 def copy_ceiling(lib, device, nbytes=1 << 30, reps=10):
     """Measured HBM copy rate (read + write bytes / time, GB/s) of the
@@ -194,62 +231,84 @@ def copy_ceiling(lib, device, nbytes=1 << 30, reps=10):
     return 2 * nbytes / t / 1e9
 
 
+def host_cores():
+    """(cores this process may run on, os.cpu_count()): the affinity set,
+    capped by a cgroup v2 CPU quota when one is set."""
+    n = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = n
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            avail = min(avail, max(1, math.ceil(int(q) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return avail, n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(w: Workload, seconds: float):
-    """The oracle's reference-shaped path (flex_fec_generate per line, flex_fec_recover
-    per erasure, over AoS sim_segment_t) on a bounded sample of the same groups."""
+    """The oracle's reference-shaped path (flex_fec_generate per line,
+    flex_fec_recover per erasure, over AoS sim_segment_t) on a
+    bounded sample of the same groups (the device-generated xorshift64*
+    payloads): (i) 1 core at the reference's own flags (-O0), (ii) 1 core at
+    -O2, (iii) every available core at -O2 with a pthread group split."""
     sys.path.insert(0, str(ROOT / "oracle"))
     from pyoracle import Oracle
 
-    sample = min(w.G, 4096)
+    sample = min(w.G, 16384)
     shards = w.shards[:sample, :, :w.S].cpu().numpy()
     hdr = w.hdr_np[:sample]
     present = w.present_np[:sample]
+    cores, nproc = host_cores()
     out = {}
-    for label, opt, threads in (("O2_1core", "O2", 1), ("O0_1core", "O0", 1), ("O2_16threads", "O2", 16)):
+    legs = (("O2_1core", "O2", 1, seconds), ("O0_1core", "O0", 1, seconds / 4),
+            (f"O2_{cores}threads", "O2", cores, seconds / 4))
+    for label, opt, threads, budget in legs:
         o = Oracle(1200, opt)
         segs = o.to_aos(shards, hdr)
-        budget = seconds if label == "O2_1core" else seconds / 4
+        rec_out = np.zeros_like(segs)
         t_enc = t_dec = 0.0
         reps = 0
-        fec = None
         while t_enc + t_dec < budget or reps == 0:
             t0 = time.perf_counter()
             n, fec = o.encode_aos(w.plan, sample, segs, threads=threads)
             t1 = time.perf_counter()
-            if threads == 1:
-                nrec, _ = o.recover_aos(w.plan, sample, segs, fec, present)
-                assert nrec == 2 * sample
+            nrec, _ = o.recover_aos(w.plan, sample, segs, fec, present, threads=threads, out=rec_out)
             t2 = time.perf_counter()
+            assert n == sample * w.n and nrec == 2 * sample
             t_enc += t1 - t0
             t_dec += t2 - t1
             reps += 1
         enc_b = sample * (w.k + w.n) * w.S * reps
         dec_b = w.dec_bytes * sample / w.G * reps
-        if threads == 1:
-            out[label] = {"gibps": (enc_b + dec_b) / (t_enc + t_dec) / 2**30,
-                          "encode_gibps": enc_b / t_enc / 2**30, "decode_gibps": dec_b / t_dec / 2**30,
-                          "reps": reps, "seconds": t_enc + t_dec}
-        else:
-            out[label] = {"encode_gibps": enc_b / t_enc / 2**30, "reps": reps, "seconds": t_enc}
+        out[label] = {"gibps": (enc_b + dec_b) / (t_enc + t_dec) / 2**30, "encode_gibps": enc_b / t_enc / 2**30,
+                      "decode_gibps": dec_b / t_dec / 2**30, "reps": reps, "seconds": t_enc + t_dec,
+                      "threads": threads}
     main = out["O2_1core"]
-    cpu = "unknown"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
+    allc = out[f"O2_{cores}threads"]
     return {"value": round(main["gibps"], 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{sample} groups x {reps_str(main)} of the same workload (k=10, rows {{4,4,2}}, 1200 B, "
-                      f"2 erasures/group), oracle/rfec_oracle.c at -O2 over AoS sim_segment_t, one thread",
-            "cpu": cpu, "encode_gibps": round(main["encode_gibps"], 4), "decode_gibps": round(main["decode_gibps"], 4),
+            "sample": f"{sample} groups x {main['reps']} passes ({main['seconds']:.1f} s) of the same workload "
+                      f"(k={w.k}, {w.n} parities, {w.S} B, 2 erasures/group, the device's xorshift64* payloads), "
+                      f"oracle/rfec_oracle.c at -O2 over AoS sim_segment_t, one thread",
+            "cpu": cpu_model(), "nproc": nproc, "cores_available": cores,
+            "encode_gibps": round(main["encode_gibps"], 4), "decode_gibps": round(main["decode_gibps"], 4),
             "reference_flags_O0_1core_gibps": round(out["O0_1core"]["gibps"], 4),
-            "O2_16threads_encode_gibps": round(out["O2_16threads"]["encode_gibps"], 4)}
-
-
-def reps_str(d):
-    return f"{d['reps']} passes ({d['seconds']:.1f} s)"
+            "all_cores_O2_gibps": round(allc["gibps"], 4),
+            "all_cores_O2_encode_gibps": round(allc["encode_gibps"], 4),
+            "all_cores_O2_decode_gibps": round(allc["decode_gibps"], 4),
+            "all_cores_threads": cores}
 
 
 def load_traffic(workload_name, kind):
@@ -266,16 +325,39 @@ def load_traffic(workload_name, kind):
         return None
 
 
+def golden_digest(case, world, rank):
+    """The reference's digest of this rank's slice (tests/golden/full_hashes.json)."""
+    try:
+        cases = {c["name"]: c for c in json.loads(GOLDEN.read_text())["cases"]}
+    except (OSError, ValueError):
+        return None
+    c = cases.get(case)
+    if c is None:
+        return None
+    if world == 1:
+        return c["sha256"]
+    return c.get("slices", {}).get(str(world), [None] * world)[rank]
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--groups", type=int, default=65536, help="groups per GPU (weak scaling)")
-    ap.add_argument("--total-groups", type=int, default=0,
-                    help="split this many groups over the GPUs instead (strong scaling, e.g. 1048576)")
-    ap.add_argument("--k", type=int, default=10)
-    ap.add_argument("--payload", type=int, default=1200)
+    ap.add_argument("--config", default="auto", choices=["auto"] + list(CONFIGS),
+                    help="auto: c3 at one rank, c4 (1M groups split) at WORLD_SIZE > 1")
+    ap.add_argument("--groups", type=int, default=0, help="custom: groups per GPU (weak scaling)")
+    ap.add_argument("--total-groups", type=int, default=0, help="custom: split this many groups over the GPUs")
+    ap.add_argument("--k", type=int, default=0)
+    ap.add_argument("--payload", type=int, default=0)
     ap.add_argument("--stride", type=int, default=0, help="HBM slot width (default: payload rounded to 16)")
     ap.add_argument("--protect-fraction", type=int, default=80)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
@@ -283,57 +365,94 @@ def main():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--tuning", type=int, default=0)
     ap.add_argument("--sets", type=int, default=2, help="disjoint buffer sets rotated per step (MALL-proof timing)")
-    ap.add_argument("--col", type=int, default=0, help="rows of COL segments (config 5: --k 32 --payload 256 --col 4)")
-    ap.add_argument("--full-plan", action="store_true", help="rows + columns of the reference plan (config 3 variant)")
+    ap.add_argument("--col", type=int, default=0, help="custom: rows of COL segments")
+    ap.add_argument("--full-plan", action="store_true", help="custom: rows + columns of the reference plan")
+    ap.add_argument("--hot-decode", action="store_true",
+                    help="decode the set encoded in the same step (its parity still MALL-resident)")
     args = ap.parse_args()
 
+    # --gpus N without a launcher: start N ranks under torchrun as a child
+    # process (nothing here has touched the GPU yet), exit with its code
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(Path(__file__).resolve())]
+        raise SystemExit(subprocess.call(cmd + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs a GPU")
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=device)
+        dist.init_process_group("gloo")  # control plane only: barrier, max time, byte sum
+    ndev = torch.cuda.device_count()
+    if ndev < 1 or not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU")
+    torch.cuda.set_device(local % ndev)
+    device = torch.device("cuda", local % ndev)
 
     lib = native(1000)
     lib.set_tuning(args.tuning)
-    if args.total_groups:
-        group0, my_groups = shard_groups(args.total_groups, world, rank)
-        scaling = "strong"
+    custom = args.groups or args.total_groups or args.k or args.payload or args.col or args.full_plan
+    cfg_name = args.config if args.config != "auto" else ("c4" if world > 1 else "c3")
+    cfg = dict(CONFIGS[cfg_name])
+    if args.full_plan:
+        cfg.update(plan="full", config_id=3)
+    if args.col:
+        cfg.update(plan=f"col{args.col}")
+    if args.k:
+        cfg["k"] = args.k
+    if args.payload:
+        cfg["S"] = args.payload
+    if custom:
+        cfg.update(golden=None, desc="custom")
+        cfg_name = "custom"
+    k, S = cfg["k"], cfg["S"]
+    if args.groups:
+        group0, my_groups, total, scaling = rank * args.groups, args.groups, args.groups * world, "weak"
     else:
-        group0, my_groups = rank * args.groups, args.groups
-        scaling = "weak"
-    # rotate over disjoint buffer sets (same inputs), so that the
-    # 256 MB MALL never holds a step's operands from the previous step
-    sets = [Workload(lib, my_groups, args.k, args.payload, args.protect_fraction, device, group0, seed=1000 + rank,
-                     stride=args.stride or None, col=args.col, full_plan=args.full_plan)
+        total = args.total_groups or cfg["groups"]
+        if cfg_name == "c4" or args.total_groups:
+            group0, my_groups = shard_groups(total, world, rank)
+            scaling = "strong"
+        else:  # per-GPU config (c3 / c3full / c5): every rank runs the whole config on its own groups
+            group0, my_groups, scaling = rank * total, total, "weak"
+            total *= world
+    col = int(cfg["plan"][3:]) if cfg["plan"].startswith("col") else 0
+    full_plan = cfg["plan"] == "full"
+    sets = [Workload(lib, my_groups, k, S, args.protect_fraction, device, group0, seed=1000 + rank,
+                     stride=args.stride or None, col=col, full_plan=full_plan, config_id=cfg["config_id"])
             for _ in range(max(1, args.sets))]
     w = sets[0]
+    nset = len(sets)
     stream = torch.cuda.current_stream(device)
     sp = stream.cuda_stream
     torch.cuda.synchronize(device)
 
+    def dec_set(i):
+        return sets[i % nset] if args.hot_decode else sets[(i - 1) % nset]
+
+    for ws in sets:  # every set holds its parity before the first (cold) decode
+        ws.encode(sp)
+
     for i in range(args.warmup):
-        sets[i % len(sets)].encode(sp)
-        sets[i % len(sets)].decode(sp)
+        sets[i % nset].encode(sp)
+        dec_set(i).decode(sp)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    torch.cuda.synchronize(device)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for i in range(args.steps):
         a, b, c = ev[i]
-        ws = sets[i % len(sets)]
         a.record(stream)
-        ws.encode(sp)
+        sets[(args.warmup + i) % nset].encode(sp)
         b.record(stream)
-        ws.decode(sp)
+        dec_set(args.warmup + i).decode(sp)
         c.record(stream)
     torch.cuda.synchronize(device)
     if dist:
@@ -343,21 +462,34 @@ def main():
     t_enc = np.array([a.elapsed_time(b) for a, b, _ in ev]) / 1e3
     t_dec = np.array([b.elapsed_time(c) for _, b, c in ev]) / 1e3
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    verified = None if args.no_verify else all(ws.verify() for ws in sets)
+    verified, digest_ok = None, None
+    if not args.no_verify:
+        verified = all(ws.verify() for ws in sets)
+        # the reference's digest of exactly these groups, where the golden file holds one
+        want = None
+        if cfg["golden"] and scaling == "strong":
+            want = golden_digest(cfg["golden"], world, rank)
+        elif cfg["golden"] and group0 == 0:
+            want = golden_digest(cfg["golden"], 1, 0)
+        if want is not None:
+            digest_ok = w.digest() == want
+            verified = verified and digest_ok
     if dist:
-        vt = torch.tensor([1 if verified in (None, True) else 0], dtype=torch.int32, device=device)
+        vt = torch.tensor([1 if verified in (None, True) else 0, 1 if digest_ok else 0, 1 if digest_ok is None else 0],
+                          dtype=torch.int32)
         dist.all_reduce(vt, op=dist.ReduceOp.MIN)
-        verified = None if args.no_verify else bool(vt.item())
+        verified = None if args.no_verify else bool(vt[0].item())
+        digest_ok = None if (args.no_verify or vt[2].item()) else bool(vt[1].item())
 
     # whole-job bytes: every rank's slice (equal slices up to one group)
-    nb = torch.tensor([w.enc_bytes + w.dec_bytes], dtype=torch.float64, device=device)
+    nb = torch.tensor([w.enc_bytes + w.dec_bytes, w.G], dtype=torch.float64)
     if dist:
         dist.all_reduce(nb, op=dist.ReduceOp.SUM)
-    step_bytes = float(nb.item())
+    step_bytes = float(nb[0].item())
     value = step_bytes * args.steps / elapsed / 2**30
     enc_mean = float(t_enc.mean())
     dec_mean = float(t_dec.mean())
@@ -365,18 +497,19 @@ def main():
     res = None
     if rank == 0:
         ceiling = copy_ceiling(lib, device)
-        workload_name = f"k{args.k}_r{w.n}_S{args.payload}_G{w.G}"
+        workload_name = f"k{k}_r{w.n}_S{S}_G{w.G}"
         lines = [w.plan.line[l].count for l in range(w.n)]
-        rows_layout = not args.full_plan and len(set(lines[:-1])) <= 1
-        enc_kernel = (f"k_encode_rows<{args.k},{lines[0]}>" if rows_layout and (args.k, lines[0]) in ((10, 4), (32, 4))
-                      else "k_encode (plan-driven)")
-        dec_kernels = ("k_peel_lds + k_recover_flat (cascading peel: schedule, then replay)" if args.full_plan
+        rows_layout = not full_plan and len(set(lines[:-1])) <= 1
+        enc_kernel = (f"k_encode_out<{k},{lines[0]}>" if rows_layout and (k, lines[0]) in ((10, 4), (32, 4))
+                      else (f"k_encode_matrix<{k},{w.plan.col}>" if full_plan else "k_encode (plan-driven)"))
+        dec_kernels = ("k_decode_cascade + k_decode_fixup (one launch + fix-up)" if full_plan
                        else "k_decode_disjoint (peel headers + payload, one launch)")
-        if args.full_plan:
-            plan_desc = f"full reference plan {w.plan.row}x{w.plan.col}: {w.plan.n_row_lines} rows + {w.n - w.plan.n_row_lines} columns, line sizes {lines}"
+        if full_plan:
+            plan_desc = (f"full reference plan {w.plan.row}x{w.plan.col}: {w.plan.n_row_lines} rows + "
+                         f"{w.n - w.plan.n_row_lines} columns, line sizes {lines}")
             pairs_desc = "uniform over all recoverable pairs (peeling, with cascades)"
         else:
-            plan_desc = ("row layer of the reference 3x4 plan, rows {4,4,2}" if (args.k, args.col) == (10, 0)
+            plan_desc = ("row layer of the reference 3x4 plan, rows {4,4,2}" if (k, col) == (10, 0)
                          else f"rows of sizes {lines}")
             pairs_desc = f"uniform over the {len(distinct_row_pairs(w.plan))} distinct-row pairs"
         traffic = load_traffic(workload_name, "encode")
@@ -392,13 +525,18 @@ def main():
             "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (torch.randint payloads, sequential headers), resident in HBM before timing",
-            "config": {"workload": workload_name, "groups_per_gpu": w.G,
-                       "total_groups": args.total_groups or args.groups * world, "k": args.k, "r": w.n,
-                       "payload_bytes": args.payload, "plan": plan_desc,
+            "data": (f"synthetic: SURVEY §8(d) xorshift64* payloads (config id {cfg['config_id']}, generated on the "
+                     f"device by jump-ahead), sequential headers; resident in HBM before timing"),
+            "config": {"workload": f"{cfg_name}: {workload_name}" + (f" (rank 0's slice of {total})"
+                                                                     if scaling == "strong" and world > 1 else ""),
+                       "config": cfg_name, "desc": cfg["desc"], "groups_per_gpu": w.G, "total_groups": total,
+                       "k": k, "r": w.n, "payload_bytes": S, "plan": plan_desc,
                        "erasures_per_group": 2, "erasure_pairs": pairs_desc,
-                       "parallelism": f"batch split over {world} GPU(s), no collective",
-                       "buffer_sets": len(sets),
+                       "parallelism": f"batch split over {world} GPU(s) (contiguous group slices), no collective; "
+                                      f"control plane on a CPU gloo group" if world > 1 else "1 GPU",
+                       "buffer_sets": nset,
+                       "decode_order": "hot (same step's set)" if args.hot_decode or nset == 1 else
+                                       "cold (the set encoded one step earlier)",
                        "bytes_per_step_per_gpu": {"encode": w.enc_bytes, "decode": w.dec_bytes},
                        "algorithmic_bytes": "payload bytes read + written (20-B headers excluded)"},
             "roofline": {"bound": "hbm", "kernel": enc_kernel, "achieved": round(achieved, 1),
@@ -416,9 +554,12 @@ def main():
                                 "launch_us": round(dec_mean * 1e6, 2),
                                 "launch_us_median": round(float(np.median(t_dec)) * 1e6, 2),
                                 "traffic": load_traffic(workload_name, "decode"),
-                                "kernels": dec_kernels},
+                                "kernels": dec_kernels,
+                                "parity_operand": "cold: written one step (>= 1.7 GB of traffic) before"
+                                if not (args.hot_decode or nset == 1) else "hot: written by this step's encode"},
             "copy_ceiling_GBps": round(ceiling, 1),  # rfec_probe_copy, read + write bytes
             "verified": verified,
+            "verified_vs_reference_digest": digest_ok,
             "tuning": args.tuning,
         }
         if world == 1 and not args.no_cpu:

@@ -583,6 +583,18 @@ int rfec_probe_read(const void* src, size_t bytes, void* sink, unsigned flags, v
 int rfec_probe_copy(const void* src, void* dst, size_t bytes, unsigned flags, void* stream);
 int rfec_probe_write(void* dst, size_t bytes, unsigned flags, void* stream);
 
+/* Synthetic inputs of SURVEY.md §8(d) (bench and tests only, not on the FEC
+ * path): payload slots of groups [g0, g0 + groups) of the xorshift64*
+ * stream seeded 0x52415A4F52464543 ^ config_id, filled group-major and
+ * shard-major, S bytes per slot from ceil(S / 8) outputs (little endian),
+ * zero to `stride`.  The slice is reached by jump-ahead, so a rank fills its
+ * own part of a batch without the outputs before it.  Synchronises `stream`.
+ * Returns RFEC_OK, RFEC_EINVAL or RFEC_EDEVICE. */
+int rfec_fill_xorshift(uint8_t* shards, uint64_t config_id, uint64_t g0, uint32_t groups, uint32_t k, uint32_t S,
+                       uint32_t stride, void* stream);
+/* The xorshift64* state n steps after x (GF(2) jump-ahead; host only). */
+uint64_t rfec_xorshift_jump(uint64_t x, uint64_t n);
+
 /* Last HIP error string seen by this thread (for diagnostics). */
 const char* rfec_last_error(void);
 

@@ -135,6 +135,8 @@ class Oracle:
         L.oracle_encode_aos_mt.restype = C.c_long
         L.oracle_recover_aos.argtypes = [C.POINTER(rfec_plan), C.c_uint32, P, P, P, P]
         L.oracle_recover_aos.restype = C.c_long
+        L.oracle_recover_aos_mt.argtypes = [C.POINTER(rfec_plan), C.c_uint32, P, P, P, P, C.c_int]
+        L.oracle_recover_aos_mt.restype = C.c_long
         L.oracle_crc32.argtypes = [C.c_uint32, P, C.c_size_t]
         L.oracle_crc32.restype = C.c_uint32
         L.oracle_wire_frame_fec_batch.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, P, P, P, P, P, C.c_uint32, P, P]
@@ -317,12 +319,16 @@ class Oracle:
             n = self.lib.oracle_encode_aos(C.byref(p), groups, _np_ptr(seg_bytes), _np_ptr(fec))
         return n, fec
 
-    def recover_aos(self, plan, groups, seg_bytes, fec_bytes, present):
-        out = np.zeros_like(seg_bytes)
+    def recover_aos(self, plan, groups, seg_bytes, fec_bytes, present, threads=1, out=None):
+        out = np.zeros_like(seg_bytes) if out is None else out
         assert seg_bytes.nbytes == groups * plan.k * self.segment_size
-        n = self.lib.oracle_recover_aos(C.byref(_as_oracle_plan(plan)), groups, _np_ptr(seg_bytes),
-                                        _np_ptr(fec_bytes), _np_ptr(np.ascontiguousarray(present, np.uint64)),
-                                        _np_ptr(out))
+        pres = np.ascontiguousarray(present, np.uint64)
+        if threads > 1:
+            n = self.lib.oracle_recover_aos_mt(C.byref(_as_oracle_plan(plan)), groups, _np_ptr(seg_bytes),
+                                               _np_ptr(fec_bytes), _np_ptr(pres), _np_ptr(out), threads)
+        else:
+            n = self.lib.oracle_recover_aos(C.byref(_as_oracle_plan(plan)), groups, _np_ptr(seg_bytes),
+                                            _np_ptr(fec_bytes), _np_ptr(pres), _np_ptr(out))
         return n, out
 
 

@@ -472,13 +472,13 @@ long oracle_encode_aos_mt(const rfec_plan* plan, uint32_t groups, sim_segment_t*
     return total;
 }
 
-long oracle_recover_aos(const rfec_plan* plan, uint32_t groups, sim_segment_t* segs, sim_fec_t* fecs,
-                        const uint64_t* present, sim_segment_t* out)
+static long recover_aos_range(const rfec_plan* plan, uint32_t g0, uint32_t g1, sim_segment_t* segs,
+                              sim_fec_t* fecs, const uint64_t* present, sim_segment_t* out)
 {
     const uint32_t k = plan->k, n = plan->n_lines;
     sim_segment_t* ptrs[RFEC_MAX_K];
     long total = 0;
-    for (uint32_t g = 0; g < groups; ++g) {
+    for (uint32_t g = g0; g < g1; ++g) {
         sim_segment_t* base = segs + (size_t)g * k;
         sim_segment_t* obase = out + (size_t)g * k;
         uint64_t have[2] = {present[2 * g], present[2 * g + 1]};
@@ -507,6 +507,57 @@ long oracle_recover_aos(const rfec_plan* plan, uint32_t groups, sim_segment_t* s
                 }
             }
         }
+    }
+    return total;
+}
+
+long oracle_recover_aos(const rfec_plan* plan, uint32_t groups, sim_segment_t* segs, sim_fec_t* fecs,
+                        const uint64_t* present, sim_segment_t* out)
+{
+    return recover_aos_range(plan, 0, groups, segs, fecs, present, out);
+}
+
+typedef struct {
+    const rfec_plan* plan;
+    uint32_t g0, g1;
+    sim_segment_t *segs, *out;
+    sim_fec_t* fecs;
+    const uint64_t* present;
+    long recovered;
+} rec_job;
+
+static void* rec_worker(void* p)
+{
+    rec_job* j = (rec_job*)p;
+    j->recovered = recover_aos_range(j->plan, j->g0, j->g1, j->segs, j->fecs, j->present, j->out);
+    return NULL;
+}
+
+/* the CPU baseline's all-cores leg: a pthread group split */
+long oracle_recover_aos_mt(const rfec_plan* plan, uint32_t groups, sim_segment_t* segs, sim_fec_t* fecs,
+                           const uint64_t* present, sim_segment_t* out, int threads)
+{
+    if (threads < 1)
+        threads = 1;
+    if (threads > 256)
+        threads = 256;
+    pthread_t tid[256];
+    rec_job jobs[256];
+    for (int t = 0; t < threads; ++t) {
+        jobs[t].plan = plan;
+        jobs[t].g0 = (uint32_t)((uint64_t)groups * t / threads);
+        jobs[t].g1 = (uint32_t)((uint64_t)groups * (t + 1) / threads);
+        jobs[t].segs = segs;
+        jobs[t].out = out;
+        jobs[t].fecs = fecs;
+        jobs[t].present = present;
+        jobs[t].recovered = 0;
+        pthread_create(&tid[t], NULL, rec_worker, &jobs[t]);
+    }
+    long total = 0;
+    for (int t = 0; t < threads; ++t) {
+        pthread_join(tid[t], NULL);
+        total += jobs[t].recovered;
     }
     return total;
 }

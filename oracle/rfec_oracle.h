@@ -65,6 +65,8 @@ long oracle_encode_aos_mt(const rfec_plan* plan, uint32_t groups, sim_segment_t*
  * with oracle_recover (canonical peel order).  Returns segments recovered. */
 long oracle_recover_aos(const rfec_plan* plan, uint32_t groups, sim_segment_t* segs,
                         sim_fec_t* fecs, const uint64_t* present, sim_segment_t* out);
+long oracle_recover_aos_mt(const rfec_plan* plan, uint32_t groups, sim_segment_t* segs, sim_fec_t* fecs,
+                           const uint64_t* present, sim_segment_t* out, int threads);
 
 /* wire codec (sim_proto.c, sim_proto.inl, cf_stream.c, cf_crc32.c) */
 uint32_t oracle_crc32(uint32_t crc, const void* buf, size_t size);

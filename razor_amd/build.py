@@ -26,7 +26,7 @@ INCLUDE = ROOT / "include"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("RFEC_OFFLOAD_ARCH", "gfx950")
 
-HIP_SRC = [CSRC / "rfec_kernels.hip", CSRC / "rfec_probe.hip", CSRC / "rfec_wire.hip"]
+HIP_SRC = [CSRC / "rfec_kernels.hip", CSRC / "rfec_probe.hip", CSRC / "rfec_wire.hip", CSRC / "rfec_fill.hip"]
 C_SRC = [CSRC / "rfec_host.c"]
 NET_SRC = CSRC / "rfec_net.c"  # host-only (sockets), independent of SIM_VIDEO_SIZE
 HEADERS = [INCLUDE / "razor_fec.h", CSRC / "rfec_internal.h"]

@@ -225,6 +225,8 @@ _SIGS = {
     "rfec_probe_read": (C.c_int, [_P, C.c_size_t, _P, C.c_uint, _P]),
     "rfec_probe_copy": (C.c_int, [_P, _P, C.c_size_t, C.c_uint, _P]),
     "rfec_probe_write": (C.c_int, [_P, C.c_size_t, C.c_uint, _P]),
+    "rfec_fill_xorshift": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P]),
+    "rfec_xorshift_jump": (C.c_uint64, [C.c_uint64, C.c_uint64]),
     "rfec_udp_open": (C.c_int, [C.c_char_p, C.c_uint16, C.c_uint, C.c_uint32, C.POINTER(C.c_int),
                                 C.POINTER(rfec_udp_addr)]),
     "rfec_udp_close": (None, [C.c_int]),
@@ -316,6 +318,12 @@ class Native:
                      stream=None):
         self._check(self.lib.rfec_encode_batch(C.byref(as_plan(plan)), groups, stride, capacity, shards, hdr, parity,
                                                meta, fec_size, status, stream), "rfec_encode_batch")
+
+    def fill_xorshift(self, shards, config_id, g0, groups, k, S, stride, stream=None):
+        """SURVEY §8(d) synthetic payloads of groups [g0, g0 + groups) into the
+        device slots at `shards` (bench / test inputs; jump-ahead per slot)."""
+        self._check(self.lib.rfec_fill_xorshift(shards, config_id, g0, groups, k, S, stride, stream),
+                    "rfec_fill_xorshift")
 
     def workspace_size(self, plan, groups) -> int:
         return self.lib.rfec_recover_workspace_size(C.byref(as_plan(plan)), groups)

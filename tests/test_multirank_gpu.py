@@ -1,0 +1,120 @@
+"""GPU, two ranks on the one leased GPU (CPU gloo control plane, no RCCL):
+the config-4 batch split (razor_amd/dist.py) through librazor_fec.so itself.
+
+Each rank generates its contiguous slice of the 1,048,576-group config-4
+stream on the device (jump-ahead, no outputs before its slice), encodes it
+with the product library in 65,536-group launches and digests its outputs;
+each slice digest must equal the one oracle/gen_full.c took of the
+reference's flex_fec_generate over the same groups
+(tests/golden/full_hashes.json, c4 "slices").  Groups are independent
+(flex_fec_sender.c:146-245, sim_fec.c:152-166), so the split needs no
+data-path collective.  Then bench.py --gpus 2 end to end."""
+import hashlib
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parent.parent
+GOLDEN = ROOT / "tests" / "golden" / "full_hashes.json"
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _c4():
+    return {c["name"]: c for c in json.loads(GOLDEN.read_text())["cases"]}["c4_k10_rows_S1200_G1048576"]
+
+
+def _worker(rank, world, port, outdir):
+    sys.path[:0] = [str(ROOT)]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    from bench import make_headers
+    from razor_amd.dist import shard_groups
+    from razor_amd.fec import native
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = _c4()
+    lib = native(1000)
+    dev = torch.device("cuda", 0)  # both ranks on the one leased GPU
+    torch.cuda.set_device(dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    k, S, total = c["k"], c["S"], c["groups"]
+    plan = lib.plan_from_fraction(k, c["pf"], c["layers"])
+    assert plan.n_lines == c["n_lines"]
+    lo, n = shard_groups(total, world, rank)
+    chunk = 65536
+    shards = torch.empty((chunk, k, S), dtype=torch.uint8, device=dev)
+    par = torch.empty((chunk, plan.n_lines, S), dtype=torch.uint8, device=dev)
+    meta = torch.empty((chunk, plan.n_lines, 20), dtype=torch.uint8, device=dev)
+    fs = torch.empty((chunk, plan.n_lines), dtype=torch.int16, device=dev)
+    status = torch.empty((chunk, plan.n_lines), dtype=torch.int8, device=dev)
+    h = hashlib.sha256()
+    bad = 0
+    for g in range(lo, lo + n, chunk):
+        m = min(chunk, lo + n - g)
+        lib.fill_xorshift(shards.data_ptr(), c["config_id"], g, m, k, S, S, st)
+        hdr = make_headers(m, k, S, g)
+        d_hdr = torch.from_numpy(hdr.view(np.uint8).reshape(m, k, 20).copy()).to(dev)
+        lib.encode_batch(plan, m, S, S, shards.data_ptr(), d_hdr.data_ptr(), par.data_ptr(), meta.data_ptr(),
+                         fs.data_ptr(), status.data_ptr(), st)
+        torch.cuda.synchronize(dev)
+        bad += int(status[:m].abs().sum())
+        rec = torch.cat([par[:m].reshape(m, -1), meta[:m].reshape(m, -1), fs[:m].view(torch.uint8).reshape(m, -1)],
+                        dim=1)
+        h.update(rec.cpu().numpy().tobytes())
+    res = [None] * world
+    dist.all_gather_object(res, {"lo": lo, "n": n, "digest": h.hexdigest(), "bad": bad})
+    if rank == 0:
+        Path(outdir, "result.json").write_text(json.dumps(res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_c4_split_two_ranks_one_gpu(tmp_path):
+    import torch.multiprocessing as mp
+
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    res = json.loads((tmp_path / "result.json").read_text())
+    c = _c4()
+    lo = 0
+    for r, s in enumerate(res):
+        assert s["lo"] == lo and s["bad"] == 0  # contiguous, no gap, no overlap
+        lo += s["n"]
+        assert s["digest"] == c["slices"][str(world)][r], f"rank {r} slice differs from the reference"
+    assert lo == c["groups"]
+
+
+def test_bench_two_ranks_one_gpu():
+    """bench.py --gpus 2 starts its own two ranks (torchrun, gloo control
+    plane) on the one GPU: one JSON line naming config 4, every rank's slice
+    equal to the reference digest."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--no-cpu", "--sets", "2"], capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["config"] == "c4" and d["config"]["total_groups"] == 1048576
+    assert d["config"]["workload"].startswith("c4:")
+    assert d["verified"] is True and d["verified_vs_reference_digest"] is True
+    assert d["value"] > 0
