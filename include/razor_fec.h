@@ -570,8 +570,12 @@ int rfec_rx_session_get_info(const rfec_rx_session* s, rfec_rx_session_info* inf
 #define RFEC_TUNE_LDS_HDR_PEEL 32768u /* fused decode: header work in LDS-staged peel blocks (default: one lane per group and line) */
 #define RFEC_TUNE_FLAT_ENCODE 65536u  /* row encode: one lane per (group, chunk column), all members (default: one lane per parity chunk) */
 #define RFEC_TUNE_META_TAIL 131072u   /* encode: header (meta) blocks at the tail of the grid instead of its head */
+#define RFEC_TUNE_HDR_HEAD 524288u    /* fused decodes: header blocks at the head of the grid (default: spread over it) */
+#define RFEC_TUNE_OUT_DECODE 2097152u  /* disjoint-plan decode: output-mapped also for slots under 64 chunks */
+#define RFEC_TUNE_FLAT_DECODE 262144u /* disjoint-plan decode: one lane per (group, chunk column), every fired line (default: one lane per (group, line, chunk)) */
 /* (defaults: parity stores write-through, recovered stores non-temporal) */
 #define RFEC_TUNE_DIAG_NO_META 256u /* DIAGNOSTIC ONLY: skip fec_meta (wrong output) */
+#define RFEC_TUNE_DIAG_NO_HDR 1048576u /* DIAGNOSTIC ONLY: fused decode without its header blocks (wrong output) */
 void rfec_set_tuning(unsigned flags);
 unsigned rfec_get_tuning(void);
 

@@ -241,6 +241,13 @@ int rfec_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, 
         return set_err(RFEC_EINVAL, "NULL buffer", 0);
     if ((uintptr_t)workspace % 16) /* schedule records are read as 16-B vectors, the fix-up counter atomically */
         return set_err(RFEC_EINVAL, "workspace must be 16-byte aligned", 0);
+    {   /* the fused decode's header lanes: one per (group, line slot), 32-bit lane index */
+        unsigned lg = 1;
+        while ((1u << lg) < plan->n_lines)
+            ++lg;
+        if (((uint64_t)groups << lg) >= (1ull << 32))
+            return set_err(RFEC_EINVAL, "batch too large for one launch (groups x lines)", 0);
+    }
     static __thread rfec_kmask M; /* 1.3 KB: keep it off the stack */
     make_masks(plan, &M);
     const int e = rfec_launch_recover(&M, groups, stride, capacity, shards, hdr, present, parity, meta, fec_size,

@@ -1108,27 +1108,39 @@ __device__ void line_headers(const PeelArgs& A, const rfec_kmask& M, uint32_t bl
         const uint64_t h0 = A.present[2 * g], h1 = A.present[2 * g + 1];
         const uint64_t m0 = lmask[l][0], m1 = lmask[l][1];
         const uint64_t x0 = m0 & ~h0, x1 = m1 & ~h1;
-        const uint32_t L = A.fsize[(size_t)g * P.n_lines + l];
-        if (__popcll(x0) + __popcll(x1) == 1 && ((m0 & h0) | (m1 & h1)) != 0 && L <= A.capacity) {
+        if (__popcll(x0) + __popcll(x1) == 1 && ((m0 & h0) | (m1 & h1)) != 0) {
+            // one round of loads: fec_data_size, fec_meta and the present
+            // members' records together (the size check comes after them)
             const uint32_t t = x0 ? (uint32_t)__ffsll((long long)x0) - 1 : 64u + (uint32_t)__ffsll((long long)x1) - 1;
+            const uint32_t L = A.fsize[(size_t)g * P.n_lines + l];
             const uint32_t* mr = reinterpret_cast<const uint32_t*>(A.meta + (size_t)g * P.n_lines + l);
             uint32_t r0 = mr[0], r1 = mr[1], r2 = mr[2], r3 = mr[3], r4 = mr[4];
             const uint32_t ln = lplan[l];
             const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
             const uint32_t* gh = reinterpret_cast<const uint32_t*>(A.hdr + (size_t)g * P.k);
-            bool ok = true;
-            for (uint32_t q = 0; q < count; ++q) {
+            uint32_t w[8][5];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) { // fused decodes: lines of at most 8 members
                 const uint32_t i = first + q * stride;
-                if (i == t)
-                    continue;
-                const uint32_t* r = gh + i * 5;
-                r0 ^= r[0];
-                r1 ^= r[1];
-                r2 ^= r[2];
-                r3 ^= r[3];
-                const uint32_t w4 = r[4];
-                r4 ^= w4;
-                ok = ok && (w4 >> 16) <= L;
+#pragma unroll
+                for (int d = 0; d < 5; ++d)
+                    w[q][d] = 0;
+                if ((uint32_t)q < count && i != t) {
+                    const uint32_t* r = gh + i * 5;
+#pragma unroll
+                    for (int d = 0; d < 5; ++d)
+                        w[q][d] = r[d];
+                }
+            }
+            bool ok = L <= A.capacity;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                r0 ^= w[q][0];
+                r1 ^= w[q][1];
+                r2 ^= w[q][2];
+                r3 ^= w[q][3];
+                r4 ^= w[q][4];
+                ok = ok && (w[q][4] >> 16) <= L;
             }
             if (ok && (r4 >> 16) <= L) {
                 uint32_t* ht = reinterpret_cast<uint32_t*>(A.hdr + (size_t)g * P.k + t);
@@ -1147,16 +1159,41 @@ __device__ void line_headers(const PeelArgs& A, const rfec_kmask& M, uint32_t bl
     }
 }
 
+// Header blocks of the fused decodes: the first n_hdr of the grid, or (every
+// > 0) every (every + 1)-th block until they run out, spread over the grid so
+// their latency-bound chains overlap the payload stream.  Returns true with
+// *hb = header block index, else false with *pb = payload block index.
+__device__ __forceinline__ bool header_block(uint32_t n_hdr, uint32_t every, uint32_t* hb, uint32_t* pb)
+{
+    const uint32_t b = blockIdx.x;
+    if (!every) {
+        *hb = b;
+        *pb = b - n_hdr;
+        return b < n_hdr;
+    }
+    const uint32_t per = b / (every + 1);
+    *hb = per;
+    *pb = b - min(per, n_hdr);
+    return per < n_hdr && b - per * (every + 1) == every;
+}
+
+__device__ __forceinline__ void run_header_block(const PeelArgs& A, const rfec_kmask& M, uint32_t hb)
+{
+    if (A.nlp_log2)
+        line_headers(A, M, hb);
+    else
+        peel_block<false, kFusedPeelDwords>(A, M, hb);
+}
+
 template <int MAXC, bool NTL, int NTS, int NI>
 __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v4u* __restrict__ parity,
                                                             uint32_t total, uint32_t C, FastDiv divC,
-                                                            uint32_t n_hdr_blocks, PeelArgs A, rfec_kmask M)
+                                                            uint32_t n_hdr_blocks, uint32_t hdr_every, PeelArgs A,
+                                                            rfec_kmask M)
 {
-    if (blockIdx.x < n_hdr_blocks) {
-        if (A.nlp_log2)
-            line_headers(A, M, blockIdx.x);
-        else
-            peel_block<false, kFusedPeelDwords>(A, M, blockIdx.x);
+    uint32_t hb, pb;
+    if (header_block(n_hdr_blocks, hdr_every, &hb, &pb)) {
+        run_header_block(A, M, hb);
         return;
     }
     __shared__ uint32_t lplan[RFEC_MAX_LINES];
@@ -1166,7 +1203,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
     // instruction still covers consecutive chunks, and the items' dependent
     // mask loads -> payload loads chains overlap
     const uint32_t lanes = (gridDim.x - n_hdr_blocks) * kBlock;
-    const uint32_t t0 = (blockIdx.x - n_hdr_blocks) * kBlock + threadIdx.x;
+    const uint32_t t0 = pb * kBlock + threadIdx.x;
     uint64_t h0[NI], h1[NI], fire[NI];
     v4u* grp[NI];
     const v4u* par[NI];
@@ -1244,6 +1281,112 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
             more = more || fire[u] != 0;
         }
     }
+}
+
+// Fused disjoint-plan decode, output-mapped (default): one lane per (group,
+// line, chunk column).  A lane whose line does not fire (parity missing, or
+// not exactly one member missing) exits; the others load the parity chunk
+// and the line's present members' chunks, all in flight, and store one
+// chunk of the missing member.  A wave's loads and its store each cover 1 KiB
+// of one slot, and no lane carries a second line (the flat (group, chunk)
+// form serialises two lines' loads per lane).  tools/decode_lab.hip, cold
+// parity: 142.7 us vs 157.8 us flat at k = 10 / 1,200 B.
+template <int MAXC, bool NTL, int NTS>
+__global__ __launch_bounds__(kBlock) void k_decode_out(v4u* shards, const v4u* __restrict__ parity, uint32_t total,
+                                                       uint32_t C, FastDiv divC, FastDiv divLC,
+                                                       uint32_t n_hdr_blocks, uint32_t hdr_every, PeelArgs A,
+                                                       rfec_kmask M)
+{
+    uint32_t hb, pb;
+    if (header_block(n_hdr_blocks, hdr_every, &hb, &pb)) {
+        run_header_block(A, M, hb);
+        return;
+    }
+    __shared__ uint32_t lplan[RFEC_MAX_LINES];
+    __shared__ uint64_t lmask[RFEC_MAX_LINES][2];
+    const rfec_kplan& P = M.plan;
+    if (threadIdx.x < P.n_lines) {
+        lmask[threadIdx.x][0] = M.mask[threadIdx.x][0];
+        lmask[threadIdx.x][1] = M.mask[threadIdx.x][1];
+    }
+    stage_plan(lplan, P); // ends in a barrier
+    const uint32_t t = pb * kBlock + threadIdx.x;
+    if (t >= total)
+        return;
+    const uint32_t g = fdiv(t, divLC);
+    const uint32_t rem = t - g * divLC.d;
+    const uint32_t l = fdiv(rem, divC);
+    const uint32_t j = rem - l * divC.d;
+    if (!((A.parity_present[g] >> l) & 1ull))
+        return;
+    const uint64_t h0 = A.present[2 * g], h1 = A.present[2 * g + 1];
+    const uint64_t x0 = lmask[l][0] & ~h0, x1 = lmask[l][1] & ~h1;
+    if (__popcll(x0) + __popcll(x1) != 1 || ((lmask[l][0] & h0) | (lmask[l][1] & h1)) == 0)
+        return;
+    const uint32_t tgt = x0 ? (uint32_t)__ffsll((long long)x0) - 1 : 64u + (uint32_t)__ffsll((long long)x1) - 1;
+    const uint32_t ln = lplan[l];
+    const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
+    v4u* grp = shards + (size_t)g * P.k * C + j;
+    v4u acc = ld16<NTL>(parity + ((size_t)g * P.n_lines + l) * C + j);
+    v4u mv[MAXC];
+#pragma unroll
+    for (int q = 0; q < MAXC; ++q) {
+        const uint32_t i = first + q * stride;
+        mv[q] = v4u{0, 0, 0, 0};
+        if ((uint32_t)q < count && i != tgt) // every other member of a firing line is present
+            mv[q] = ld16<NTL>(grp + (size_t)i * C);
+    }
+#pragma unroll
+    for (int q = 0; q < MAXC; ++q)
+        acc ^= mv[q];
+    st16<NTS>(grp + (size_t)tgt * C, acc);
+}
+
+// The same for the row layouts of the encode fast path (rows of COL
+// consecutive segments, K <= 64): the line masks and members are arithmetic
+// in the row index, so no plan is staged through LDS (no barrier before the
+// first load).
+template <int K, int COL, bool NTL, int NTS>
+__global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* __restrict__ parity, uint32_t total,
+                                                        uint32_t C, FastDiv divC, FastDiv divRC,
+                                                        uint32_t n_hdr_blocks, uint32_t hdr_every, PeelArgs A,
+                                                        rfec_kmask M)
+{
+    static_assert(K <= 64, "row decode keeps the present mask in one word");
+    uint32_t hb, pb;
+    if (header_block(n_hdr_blocks, hdr_every, &hb, &pb)) {
+        run_header_block(A, M, hb);
+        return;
+    }
+    constexpr int R = (K + COL - 1) / COL;
+    constexpr int LAST = K - (R - 1) * COL;
+    const uint32_t t = pb * kBlock + threadIdx.x;
+    if (t >= total)
+        return;
+    const uint32_t g = fdiv(t, divRC);
+    const uint32_t rem = t - g * divRC.d;
+    const uint32_t r = fdiv(rem, divC);
+    const uint32_t j = rem - r * divC.d;
+    const uint64_t h = A.present[2 * g];
+    const uint32_t cnt = r < (uint32_t)(R - 1) ? COL : LAST;
+    const uint64_t rm = ((1ull << cnt) - 1ull) << (r * COL);
+    const uint64_t miss = rm & ~h;
+    if (__popcll(miss) != 1 || !((A.parity_present[g] >> r) & 1ull))
+        return;
+    const uint32_t tgt = (uint32_t)__ffsll((long long)miss) - 1;
+    v4u* row = shards + ((size_t)g * K + r * COL) * C + j;
+    v4u acc = ld16<NTL>(parity + ((size_t)g * R + r) * C + j);
+    v4u mv[COL];
+#pragma unroll
+    for (int q = 0; q < COL; ++q) {
+        mv[q] = v4u{0, 0, 0, 0};
+        if ((q < LAST || r < (uint32_t)(R - 1)) && r * COL + q != tgt)
+            mv[q] = ld16<NTL>(row + (size_t)q * C);
+    }
+#pragma unroll
+    for (int q = 0; q < COL; ++q)
+        acc ^= mv[q];
+    st16<NTS>(shards + ((size_t)g * K + tgt) * C + j, acc);
 }
 
 // Fused disjoint-plan decode, group-per-wave mapping (see k_encode_rows_gw):
@@ -1447,7 +1590,9 @@ hipError_t launch_rows_out(const EncLaunch& a, unsigned flags)
 template <int K, int COL, bool NTL, int NTS>
 hipError_t launch_rows_v(const EncLaunch& a, unsigned flags)
 {
-    if (!(flags & (RFEC_KFLAG_FLAT_ENCODE | RFEC_KFLAG_GROUP_WAVE | RFEC_KFLAG_ITEMS2)))
+    constexpr uint64_t R = (K + COL - 1) / COL;
+    if (!(flags & (RFEC_KFLAG_FLAT_ENCODE | RFEC_KFLAG_GROUP_WAVE | RFEC_KFLAG_ITEMS2)) &&
+        (uint64_t)a.groups * R * a.cd < (1ull << 32))
         return launch_rows_out<K, COL, NTL, NTS>(a, flags);
     if (flags & RFEC_KFLAG_GROUP_WAVE) {
         const GwGeom g = gw_geom(a.groups, a.cd);
@@ -1507,7 +1652,18 @@ struct FusedArgs {
     FastDiv f;
     uint32_t n_hdr;
     hipStream_t stream;
+    bool spread; // header blocks spread over the grid (RFEC_TUNE_HDR_SPREAD)
 };
+
+// header_block()'s period for npay payload blocks (0: header blocks first).
+// n_hdr periods of (every + 1) blocks must fit the grid: every <= npay / n_hdr,
+// so fewer payload than header blocks keeps them at the head.
+inline uint32_t hdr_every(const FusedArgs& F, uint32_t npay)
+{
+    if (!F.spread || !F.n_hdr)
+        return 0;
+    return npay / F.n_hdr;
+}
 
 template <int MAXC, int NI>
 void launch_fused_gw(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, const GwGeom& g,
@@ -1564,6 +1720,50 @@ uint32_t next_gen()
     return v;
 }
 
+// output-mapped fused decode: one lane per (group, line, chunk column)
+template <int MAXC>
+void launch_fused_out(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, uint32_t cd)
+{
+    const uint32_t NL = M.plan.n_lines;
+    const uint32_t total = B.groups * NL * cd; // < 2^32: checked by the caller
+    const uint32_t npay = blocks_for(total);
+    const dim3 grid(F.n_hdr + npay);
+    const FastDiv dC = make_fastdiv(cd), dLC = make_fastdiv(NL * cd);
+    const uint32_t every = hdr_every(F, npay);
+#define RFEC_FUSED_OUT(NTL, NTS)                                                                                 \
+    hipLaunchKernelGGL((k_decode_out<MAXC, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards, F.parity, total, \
+                       F.C, dC, dLC, F.n_hdr, every, B, M)
+    switch (sp) {
+    case -1: RFEC_FUSED_OUT(false, 1); break;
+    case 0: RFEC_FUSED_OUT(true, 0); break;
+    case 2: RFEC_FUSED_OUT(true, 2); break;
+    case 3: RFEC_FUSED_OUT(true, 3); break;
+    default: RFEC_FUSED_OUT(true, 1); break;
+    }
+#undef RFEC_FUSED_OUT
+}
+
+// row-layout fused decode: one lane per (group, row, chunk column)
+template <int K, int COL>
+void launch_fused_rows(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, uint32_t cd)
+{
+    constexpr uint32_t R = (K + COL - 1) / COL;
+    const uint32_t total = B.groups * R * cd; // < 2^32: checked by the caller
+    const dim3 grid(F.n_hdr + blocks_for(total));
+    const FastDiv dC = make_fastdiv(cd), dRC = make_fastdiv(R * cd);
+#define RFEC_FUSED_ROWS(NTL, NTS)                                                                                \
+    hipLaunchKernelGGL((k_decode_rows<K, COL, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards, F.parity,    \
+                       total, F.C, dC, dRC, F.n_hdr, hdr_every(F, blocks_for(total)), B, M)
+    switch (sp) {
+    case -1: RFEC_FUSED_ROWS(false, 1); break;
+    case 0: RFEC_FUSED_ROWS(true, 0); break;
+    case 2: RFEC_FUSED_ROWS(true, 2); break;
+    case 3: RFEC_FUSED_ROWS(true, 3); break;
+    default: RFEC_FUSED_ROWS(true, 1); break;
+    }
+#undef RFEC_FUSED_ROWS
+}
+
 // sp: store policy, -1 = plain loads + non-temporal stores (A/B only)
 template <int MAXC, int NI>
 void launch_fused(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M)
@@ -1571,7 +1771,7 @@ void launch_fused(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmas
     const dim3 grid(F.n_hdr + blocks_for((F.total + NI - 1) / NI));
 #define RFEC_FUSED(NTL, NTS)                                                                                     \
     hipLaunchKernelGGL((k_decode_disjoint<MAXC, NTL, NTS, NI>), grid, dim3(kBlock), 0, F.stream, F.shards,       \
-                       F.parity, F.total, F.C, F.f, F.n_hdr, B, M)
+                       F.parity, F.total, F.C, F.f, F.n_hdr, hdr_every(F, grid.x - F.n_hdr), B, M)
     switch (sp) {
     case -1: RFEC_FUSED(false, 1); break;
     case 0: RFEC_FUSED(true, 0); break;
@@ -1806,8 +2006,10 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
         while ((1u << lg) < P.n_lines)
             ++lg;
         B.nlp_log2 = lg;
-        n_hdr = (uint32_t)(((uint64_t)groups << lg) + kBlock - 1) / kBlock;
+        n_hdr = (uint32_t)((((uint64_t)groups << lg) + kBlock - 1) / kBlock); // host checks groups << lg < 2^32
     }
+    if (fused && (flags & RFEC_KFLAG_DIAG_NO_HDR))
+        n_hdr = 0; // timing only: no recovered headers / masks
     const uint32_t C = stride / 16;
     const uint32_t cd = capacity ? (capacity + 15) / 16 : 1;
     const uint32_t total = groups * cd;
@@ -1816,7 +2018,9 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
     const v4u* pp = reinterpret_cast<const v4u*>(parity);
     v4u* sh = reinterpret_cast<v4u*>(shards);
     if (fused) {
-        const FusedArgs F = {sh, pp, total, C, f, n_hdr, st};
+        // header blocks spread over the grid by default (tools/step_ab.py, cold: k = 32 / 256 B flat
+        // 41.6 vs 46.9 us at the head; k = 10 / 1,200 B rows 139.4-141.1 vs 144.0-144.4 us)
+        const FusedArgs F = {sh, pp, total, C, f, n_hdr, st, !(flags & RFEC_KFLAG_HDR_HEAD)};
         const int sp = ntl ? store_policy(flags, kRecoverStoreDefault) : -1;
         const GwGeom gg = gw_geom(groups, cd);
         const uint32_t swz = (flags & RFEC_KFLAG_XCD_SWIZZLE) ? 1u : 0u;
@@ -1832,6 +2036,26 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
             return (int)hipGetLastError();
         }
         const bool two = (flags & RFEC_KFLAG_ITEMS2) != 0;
+        // output-mapped (a lane per (group, line, chunk)) where a line's slot spans at least a wave of
+        // chunks; below that most of its lanes would sit on lines that do not fire (k = 32 / 256 B, 2
+        // erasures: 6 of 8 rows idle, 60.0 vs 41.6 us flat), so the flat form
+        if (!two && !(flags & RFEC_KFLAG_FLAT_DECODE) && (cd >= (uint32_t)kWave || (flags & RFEC_KFLAG_OUT_DECODE)) &&
+            (uint64_t)groups * P.n_lines * cd < (1ull << 32)) {
+            uint32_t col = 0;
+            if (!(flags & RFEC_KFLAG_GENERIC) && is_row_layout(&P, &col) && col == 4 &&
+                (P.k == 10 || P.k == 32)) {
+                if (P.k == 10)
+                    launch_fused_rows<10, 4>(F, sp, B, *M, cd);
+                else
+                    launch_fused_rows<32, 4>(F, sp, B, *M, cd);
+                return (int)hipGetLastError();
+            }
+            if (maxc <= 4)
+                launch_fused_out<4>(F, sp, B, *M, cd);
+            else
+                launch_fused_out<8>(F, sp, B, *M, cd);
+            return (int)hipGetLastError();
+        }
         if (maxc <= 4 && two)
             launch_fused<4, 2>(F, sp, B, *M);
         else if (maxc <= 4)

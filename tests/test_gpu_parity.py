@@ -19,7 +19,8 @@ TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "plain_stores": 4, "ite
            "pipe_decode": 32, "wt_stores": 64, "wt_nt_stores": 192, "nt_stores": 512,
            "generic_plain": 3, "two_kernel": 4096, "two_kernel_wt": 4096 | 64, "group_wave": 8192,
            "group_wave_xcd": 8192 | 16384, "xcd": 16384, "lds_hdr_peel": 32768, "flat_encode": 65536,
-           "meta_tail": 131072, "meta_tail_nt": 131072 | 512}
+           "meta_tail": 131072, "meta_tail_nt": 131072 | 512, "flat_decode": 262144, "hdr_head": 524288,
+           "out_decode": 2097152, "out_decode_head": 2097152 | 524288}
 
 
 @pytest.fixture(scope="module")
@@ -57,7 +58,8 @@ def test_erasure_fixture_gpu(gpu, oracle1000, name, tuning):
 
 @pytest.mark.parametrize("tuning", ["default", "wt_stores", "plain_stores", "plain_loads", "two_kernel",
                                     "two_kernel_wt", "pipe_decode", "wave_decode", "group_wave",
-                                    "group_wave_xcd", "items2", "lds_hdr_peel"])
+                                    "group_wave_xcd", "items2", "lds_hdr_peel", "flat_decode",
+                                    "generic", "hdr_head", "out_decode", "out_decode_head"])
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures" and c["rows_only"]])
 def test_erasure_fixture_rows_plan_gpu(gpu, oracle1000, name, tuning):
     """Row-parity-only fixtures against the row-layer plan (pairwise disjoint
@@ -177,7 +179,8 @@ def test_full_size_k10_roundtrip(product, oracle1200, layers):
     ws = torch.empty((lib.workspace_size(plan, G),), dtype=torch.uint8, device=shards.device)
     exp = ((1 << er[:, 0]) | (1 << er[:, 1])).astype(np.int64)
     # default (fused one-launch decode for the disjoint row layer), forced peel + replay
-    for dec_tuning in (0, 4096, 4096 | 64, 8192, 8192 | 16384, 8, 8 | 64, 2, 4, 64):
+    for dec_tuning in (0, 4096, 4096 | 64, 8192, 8192 | 16384, 8, 8 | 64, 2, 4, 64, 262144, 524288, 1, 2097152,
+                       2097152 | 524288, 262144 | 524288):
         rx = shards.clone()
         rx_hdr = d_hdr.clone()
         for c in range(2):
@@ -224,7 +227,7 @@ def test_full_size_k32_s256(product, oracle1000):
     pp[::5] &= ~(np.uint64(1) << er_rows[::5, 0].astype(np.uint64))  # parity of the first erased row lost
     exp = present.copy()
     gi = torch.arange(G, device=shards.device)
-    for dec_tuning in (0, 1, 4096):
+    for dec_tuning in (0, 1, 4096, 262144, 524288, 2097152, 2097152 | 524288):
         rx = shards.clone()
         rx_hdr = d_hdr.clone()
         for c in range(3):
@@ -461,3 +464,57 @@ def test_full_plan_shapes_gpu(gpu, oracle1000, k, tuning):
             if (int(rec[g, 0]) >> i) & 1:
                 assert out_h[g, i] == hdr[g, i] and out_h[g, i] == e_h[g, i]
                 assert np.array_equal(out_s[g, i], shards[g, i]), f"k={k} group {g} segment {i}"
+
+
+@pytest.mark.parametrize("k,col,S", [(10, 4, 64), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 1000)])
+@pytest.mark.parametrize("tuning", ["default", "hdr_head", "out_decode", "out_decode_head", "flat_decode", "generic"])
+def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tuning):
+    """Row plans (disjoint lines: the fused decodes) with up to 6 erasures per
+    group, lost parities and corrupted headers (fec_data_size above capacity or
+    below a member's size, a member's data_size above fec_data_size): recovered
+    masks, headers and data equal the oracle's, under every fused form: the
+    flat (group, chunk) lanes (default below 64 chunks per slot), the
+    output-mapped (group, line, chunk) lanes (row kernel at k = 10 / 32,
+    plan-driven otherwise), header blocks spread over the grid or at its head."""
+    o = oracle1000
+    rows = (k + col - 1) // col
+    plan = o.plan_matrix(k, rows, col, 1)
+    G = 700
+    rng = np.random.default_rng(k * 1000 + S)
+    shards, hdr = o.fill_groups(31, G, k, S, ragged=True)
+    cap = min(o.video_size, S)
+    parity, meta, fsize, _ = o.encode_batch(plan, shards, hdr, cap)
+    present = np.zeros((G, 2), np.uint64)
+    pp = np.full(G, (1 << plan.n_lines) - 1, np.uint64)
+    rx, rh, fs_rx = shards.copy(), hdr.copy(), fsize.copy()
+    for g in range(G):
+        m = (1 << k) - 1
+        for i in rng.choice(k, int(rng.integers(0, 7)), replace=False):
+            m &= ~(1 << int(i))
+            rx[g, i] = 0xA5
+            rh[g, i] = np.zeros((), po.HDR_DTYPE)
+        present[g, 0] = m
+        if rng.random() < 0.2:
+            pp[g] &= ~np.uint64(1 << int(rng.integers(plan.n_lines)))
+        r = rng.random()
+        if r < 0.15:
+            fs_rx[g, rng.integers(plan.n_lines)] = cap + 1
+        elif r < 0.3:
+            l = int(rng.integers(plan.n_lines))
+            fs_rx[g, l] = max(1, int(fs_rx[g, l]) - 3)
+        elif r < 0.45:
+            i = int(rng.integers(k))
+            if (m >> i) & 1:
+                rh[g, i]["size"] = min(cap, int(rh[g, i]["size"]) + 5)
+    e_s, e_h, e_rec = o.recover_batch(plan, rx, rh, present, parity, meta, fs_rx, pp, cap)
+    out_s, out_h, rec = gpu(tuning=TUNINGS[tuning]).recover(plan, rx, rh, present, parity, meta, fs_rx, pp, cap)
+    assert np.array_equal(rec, e_rec)
+    assert int(sum(bin(int(x)).count("1") for x in rec[:, 0])) > G // 4
+    for g in range(G):
+        for i in range(k):
+            if (int(rec[g, 0]) >> i) & 1:
+                assert out_h[g, i] == e_h[g, i], f"group {g} segment {i}: header"
+                L = int(e_h[g, i]["size"])
+                assert np.array_equal(out_s[g, i, :L], e_s[g, i, :L]), f"group {g} segment {i}: data"
+            elif (int(present[g, 0]) >> i) & 1:
+                assert out_h[g, i] == rh[g, i] and np.array_equal(out_s[g, i], rx[g, i])

@@ -23,7 +23,7 @@ sys.path.insert(0, str(ROOT))
 from bench import Workload  # noqa: E402
 from razor_amd.fec import native  # noqa: E402
 
-FLAT, META_TAIL, NT, WT, WTNT, PLAIN = 65536, 131072, 512, 64, 64 | 128, 4
+FLAT, META_TAIL, NT, WT, WTNT, PLAIN, FLATDEC = 65536, 131072, 512, 64, 64 | 128, 4, 262144
 VARIANTS = {
     "default": (0, 0),
     "enc flat (r01 default)": (FLAT, 0),
@@ -33,6 +33,11 @@ VARIANTS = {
     "enc out meta_tail": (META_TAIL, 0),
     "enc out meta_tail nt": (META_TAIL | NT, 0),
     "enc flat nt": (FLAT | NT, 0),
+    "dec flat (r01 default)": (0, FLATDEC),
+    "dec out wt": (0, WT),
+    "dec out plain": (0, PLAIN),
+    "dec out wtnt": (0, WTNT),
+    "dec lds hdr peel": (0, 32768),
 }
 
 
@@ -52,12 +57,12 @@ def main():
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     variants = dict(VARIANTS)
-    for item in filter(None, args.extra.split(";")):
+    if args.variants:
+        variants = {k: variants[k] for k in args.variants.split(",")}
+    for item in filter(None, args.extra.split(";")):  # extras always run
         name, fl = item.split("=")
         e, d = fl.split(":")
         variants[name] = (int(e, 0), int(d, 0))
-    if args.variants:
-        variants = {k: variants[k] for k in args.variants.split(",")}
     dev = torch.device("cuda", 0)
     lib = native(1000)
     sets = [Workload(lib, args.groups, args.k, args.payload, 80, dev, 0, seed=11 + i, col=args.col,
