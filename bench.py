@@ -502,8 +502,15 @@ def main():
         rows_layout = not full_plan and len(set(lines[:-1])) <= 1
         enc_kernel = (f"k_encode_out<{k},{lines[0]}>" if rows_layout and (k, lines[0]) in ((10, 4), (32, 4))
                       else (f"k_encode_matrix<{k},{w.plan.col}>" if full_plan else "k_encode (plan-driven)"))
-        dec_kernels = ("k_decode_cascade + k_decode_fixup (one launch + fix-up)" if full_plan
-                       else "k_decode_disjoint (peel headers + payload, one launch)")
+        cd = (S + 15) // 16
+        if full_plan:
+            dec_kernels = "k_decode_cascade + k_decode_fixup (one launch + fix-up)"
+        elif cd >= 64 and rows_layout and (k, lines[0]) in ((10, 4), (32, 4)):
+            dec_kernels = f"k_decode_rows<{k},{lines[0]}> (one lane per (group, row, chunk); header blocks spread)"
+        elif cd >= 64:
+            dec_kernels = "k_decode_out (one lane per (group, line, chunk); header blocks spread)"
+        else:
+            dec_kernels = "k_decode_disjoint (one lane per (group, chunk), every fired line; header blocks spread)"
         if full_plan:
             plan_desc = (f"full reference plan {w.plan.row}x{w.plan.col}: {w.plan.n_row_lines} rows + "
                          f"{w.n - w.plan.n_row_lines} columns, line sizes {lines}")

@@ -25,7 +25,8 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 
-KERNELS = {"encode": "k_encode", "decode": "k_decode_disjoint", "peel": "k_peel", "recover": "k_recover"}
+KERNELS = {"encode": ("k_encode",), "decode": ("k_decode_rows", "k_decode_out", "k_decode_disjoint", "k_decode_cascade"),
+           "peel": ("k_peel",), "recover": ("k_recover",)}
 
 
 def run_pass(counter, outdir, bench_args, timeout):
@@ -53,8 +54,8 @@ def per_kernel(files, counter):
                 if row.get("Counter_Name") != counter:
                     continue
                 name = row.get("Kernel_Name", "")
-                for key, pat in KERNELS.items():
-                    if pat in name:
+                for key, pats in KERNELS.items():
+                    if any(p in name for p in pats):
                         vals[key].append(float(row["Counter_Value"]))
     return vals
 
@@ -78,6 +79,7 @@ def main():
     S, k, r = 1200, 10, 3
     enc_alg = groups * (k + r) * S
     cfg = (bench_line or {}).get("config", {})
+    groups = cfg.get("groups_per_gpu", groups)
     if cfg.get("bytes_per_step_per_gpu", {}).get("encode"):  # the bench's own workload (any plan)
         enc_alg = cfg["bytes_per_step_per_gpu"]["encode"]
         S, k, r = cfg.get("payload_bytes", S), cfg.get("k", k), cfg.get("r", r)
