@@ -27,9 +27,9 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("RFEC_OFFLOAD_ARCH", "gfx950")
 
 HIP_SRC = [CSRC / "rfec_kernels.hip", CSRC / "rfec_probe.hip", CSRC / "rfec_wire.hip", CSRC / "rfec_fill.hip"]
-C_SRC = [CSRC / "rfec_host.c"]
+C_SRC = [CSRC / "rfec_host.c", CSRC / "rfec_flex.c"]  # built once per SIM_VIDEO_SIZE
 NET_SRC = CSRC / "rfec_net.c"  # host-only (sockets), independent of SIM_VIDEO_SIZE
-HEADERS = [INCLUDE / "razor_fec.h", CSRC / "rfec_internal.h"]
+HEADERS = [INCLUDE / "razor_fec.h", INCLUDE / "razor_flex.h", CSRC / "rfec_internal.h"]
 
 VARIANTS = {"librazor_fec.so": 1000, "librazor_fec_v1200.so": 1200}
 
@@ -73,14 +73,17 @@ def build(force: bool = False, verbose: bool = False) -> dict:
               "-c", str(NET_SRC), "-o", str(nobj)])
     kobjs.append(nobj)
     for name, vsize in VARIANTS.items():
-        hobj = OBJDIR / f"rfec_host_v{vsize}.o"
-        if force or _stale(hobj, C_SRC + HEADERS):
-            _run(["gcc", "-std=c99", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
-                  f"-DSIM_VIDEO_SIZE={vsize}", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}",
-                  f"-I{INCLUDE}", f"-I{CSRC}", "-c", str(C_SRC[0]), "-o", str(hobj)])
+        hobjs = []
+        for src in C_SRC:
+            hobj = OBJDIR / f"{src.stem}_v{vsize}.o"
+            if force or _stale(hobj, [src] + HEADERS):
+                _run(["gcc", "-std=c99", "-O2", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
+                      f"-DSIM_VIDEO_SIZE={vsize}", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}",
+                      f"-I{INCLUDE}", f"-I{CSRC}", "-c", str(src), "-o", str(hobj)])
+            hobjs.append(hobj)
         so = LIBDIR / name
-        if force or _stale(so, kobjs + [hobj]):
-            _run([_hipcc(), "-shared", "-fPIC", *map(str, kobjs), str(hobj), "-o", str(so),
+        if force or _stale(so, kobjs + hobjs):
+            _run([_hipcc(), "-shared", "-fPIC", *map(str, kobjs), *map(str, hobjs), "-o", str(so),
                   f"-Wl,-soname,{name}", "-lpthread", "-lm"])
             if verbose:
                 print("built", so)
@@ -88,9 +91,31 @@ def build(force: bool = False, verbose: bool = False) -> dict:
     return built
 
 
+HARNESS_SRC = ROOT / "tests" / "dropin" / "fec_test_harness.c"
+HARNESS = LIBDIR / "fec_test_harness"
+GROUP_BENCH_SRC = ROOT / "tools" / "dropin_group_bench.c"  # tools/: per-group drop-in cost (GPU box)
+GROUP_BENCH = LIBDIR / "fec_dropin_group_bench"
+
+
+def build_harness(force: bool = False, verbose: bool = False) -> Path:
+    """tests/dropin/fec_test_harness.c (the reference's FEC tests replayed through
+    the drop-in symbols, own code) linked to lib/librazor_fec.so, and
+    tools/dropin_group_bench.c linked to lib/librazor_fec_v1200.so: test and
+    measurement infrastructure, built next to the library so they travel with it."""
+    for src, exe, lib, vsize in ((HARNESS_SRC, HARNESS, "librazor_fec.so", 1000),
+                                 (GROUP_BENCH_SRC, GROUP_BENCH, "librazor_fec_v1200.so", 1200)):
+        if force or _stale(exe, [src, LIBDIR / lib] + HEADERS):
+            _run(["gcc", "-std=c99", "-O2", "-Wall", "-Wextra", f"-DSIM_VIDEO_SIZE={vsize}", f"-I{INCLUDE}", str(src),
+                  "-o", str(exe), f"-L{LIBDIR}", f"-l:{lib}", "-Wl,-rpath,$ORIGIN"])
+            if verbose:
+                print("built", exe)
+    return HARNESS
+
+
 def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else argv
     out = build(force="--force" in argv, verbose=True)
+    out["fec_test_harness"] = build_harness(force="--force" in argv, verbose=True)
     for k, v in out.items():
         print(k, v)
     return 0

@@ -44,6 +44,8 @@ static int set_err(int code, const char* what, int hip_code)
 
 const char* rfec_last_error(void) { return t_err; }
 
+int rfec_set_error(int code, const char* what) { return set_err(code, what, 0); }
+
 /* for the other host translation units (rfec_net.c): an OS error */
 int rfec_set_error_sys(int code, const char* what, int err)
 {
@@ -381,16 +383,18 @@ static di_layout di_offsets(void)
         L.field = o;                        \
         o = (o + (size_t)(n) + 255) & ~(size_t)255; \
     } while (0)
+    /* a whole group (k <= RFEC_MAX_K segments, every line of its plan) for
+     * the group-level sender, or up to RFEC_DI_GROUPS one-line groups */
     DI_TAKE(shards, (size_t)DI_MAXK * DI_STRIDE);
-    DI_TAKE(parity, DI_STRIDE);
+    DI_TAKE(parity, (size_t)RFEC_MAX_LINES * DI_STRIDE);
     DI_TAKE(hdr, DI_MAXK * sizeof(rfec_hdr));
-    DI_TAKE(meta, sizeof(rfec_hdr));
-    DI_TAKE(fsize, sizeof(uint16_t));
-    DI_TAKE(status, 1);
-    DI_TAKE(present, 2 * sizeof(uint64_t));
-    DI_TAKE(ppresent, sizeof(uint64_t));
-    DI_TAKE(recovered, 2 * sizeof(uint64_t));
-    DI_TAKE(ws, 256); /* rfec_ws_bytes of one group, any plan (<= 164 B) */
+    DI_TAKE(meta, RFEC_MAX_LINES * sizeof(rfec_hdr));
+    DI_TAKE(fsize, RFEC_MAX_LINES * sizeof(uint16_t));
+    DI_TAKE(status, RFEC_MAX_LINES);
+    DI_TAKE(present, RFEC_DI_GROUPS * 2 * sizeof(uint64_t));
+    DI_TAKE(ppresent, RFEC_DI_GROUPS * sizeof(uint64_t));
+    DI_TAKE(recovered, RFEC_DI_GROUPS * 2 * sizeof(uint64_t));
+    DI_TAKE(ws, rfec_ws_bytes(RFEC_MAX_LINES, RFEC_DI_GROUPS));
 #undef DI_TAKE
     L.total = o;
     return L;
@@ -490,7 +494,67 @@ static int di_sync(di_ctx* c, int launch_err, const char* what)
     return e == hipSuccess ? RFEC_OK : set_err(RFEC_EDEVICE, what, e);
 }
 
-/* flex_fec_xor.c:4-53 on the GPU. */
+/* Every line of `plan` over segs[0..k) in one launch (flex_fec_xor.c:4-53 per
+ * line): line l's meta, fec_data_size and fec_data go to outs[l], the return
+ * value flex_fec_generate would give to rets[l].  The group-level sender
+ * (rfec_flex.c) and flex_fec_generate (a one-line plan) share it. */
+int rfec_di_generate_group(sim_segment_t* const* segs, int k, const rfec_plan* plan, sim_fec_t* const* outs,
+                           int* rets)
+{
+    if (k < 1 || k > DI_MAXK || plan->k != k || plan->n_lines > RFEC_MAX_LINES)
+        return set_err(RFEC_EINVAL, "group above RFEC_MAX_K segments / RFEC_MAX_LINES lines", 0);
+    for (int l = 0; l < plan->n_lines; ++l)
+        rets[l] = -1;
+    if (check_plan(plan) != RFEC_OK)
+        return RFEC_EINVAL;
+    if (plan->n_lines == 0)
+        return RFEC_OK;
+    di_ctx* c = di_get();
+    if (!c)
+        return RFEC_EDEVICE;
+    const di_layout L = di_offsets();
+    rfec_hdr* hh = (rfec_hdr*)(c->host + L.hdr);
+    for (int i = 0; i < k; ++i) {
+        stage_payload(c->host + L.shards + (size_t)i * DI_STRIDE, segs[i]->data, segs[i]->data_size);
+        seg_to_hdr(segs[i], &hh[i]);
+    }
+    const int e = rfec_launch_encode(plan, 1, DI_STRIDE, SIM_VIDEO_SIZE, c->dev + L.shards,
+                                     (const rfec_hdr*)(c->dev + L.hdr), c->dev + L.parity,
+                                     (rfec_hdr*)(c->dev + L.meta), (uint16_t*)(c->dev + L.fsize),
+                                     (int8_t*)(c->dev + L.status), c->stream, g_tuning);
+    if (di_sync(c, e, "group encode") != RFEC_OK) {
+        di_loud(t_err);
+        return RFEC_EDEVICE;
+    }
+    const rfec_hdr* m = (const rfec_hdr*)(c->host + L.meta);
+    const uint16_t* fds = (const uint16_t*)(c->host + L.fsize);
+    const int8_t* st = (const int8_t*)(c->host + L.status);
+    for (int l = 0; l < plan->n_lines; ++l) {
+        const rfec_line* ln = &plan->line[l];
+        sim_fec_t* f = outs[l];
+        if (ln->count <= 1) /* :9-10 */
+            continue;
+        f->fec_data_size = fds[l];
+        if (st[l] != 0) {
+            /* over capacity (:27-28): the reference has written the first
+             * member's header and the size by then, nothing else */
+            seg_to_hdr(segs[ln->first], (rfec_hdr*)&f->fec_meta);
+            continue;
+        }
+        memcpy(&f->fec_meta, &m[l], sizeof(rfec_hdr));
+        memcpy(f->fec_data, c->host + L.parity + (size_t)l * DI_STRIDE, fds[l]);
+        /* in-place zero padding of the line's members 1.. to fec_data_size (:47) */
+        for (int q = 1; q < ln->count; ++q) {
+            sim_segment_t* s = segs[ln->first + q * ln->stride];
+            if (s->data_size < fds[l])
+                memset(s->data + s->data_size, 0, (size_t)(fds[l] - s->data_size));
+        }
+        rets[l] = 0;
+    }
+    return RFEC_OK;
+}
+
+/* flex_fec_xor.c:4-53 on the GPU: a one-line group. */
 int flex_fec_generate(sim_segment_t* segs[], int segs_count, sim_fec_t* fec)
 {
     if (segs_count <= 1) /* :9-10 */
@@ -499,15 +563,6 @@ int flex_fec_generate(sim_segment_t* segs[], int segs_count, sim_fec_t* fec)
         set_err(RFEC_EINVAL, "segs_count above RFEC_MAX_K", 0);
         return -1;
     }
-    di_ctx* c = di_get();
-    if (!c)
-        return -1;
-    const di_layout L = di_offsets();
-    rfec_hdr* hh = (rfec_hdr*)(c->host + L.hdr);
-    for (int i = 0; i < segs_count; ++i) {
-        stage_payload(c->host + L.shards + (size_t)i * DI_STRIDE, segs[i]->data, segs[i]->data_size);
-        seg_to_hdr(segs[i], &hh[i]);
-    }
     rfec_plan p;
     memset(&p, 0, sizeof(p));
     p.k = (uint16_t)segs_count;
@@ -515,31 +570,127 @@ int flex_fec_generate(sim_segment_t* segs[], int segs_count, sim_fec_t* fec)
     p.line[0].first = 0;
     p.line[0].stride = 1;
     p.line[0].count = (uint8_t)segs_count;
-    const int e = rfec_launch_encode(&p, 1, DI_STRIDE, SIM_VIDEO_SIZE, c->dev + L.shards,
-                                     (const rfec_hdr*)(c->dev + L.hdr), c->dev + L.parity,
-                                     (rfec_hdr*)(c->dev + L.meta), (uint16_t*)(c->dev + L.fsize),
-                                     (int8_t*)(c->dev + L.status), c->stream, g_tuning);
-    if (di_sync(c, e, "flex_fec_generate") != RFEC_OK) {
-        di_loud(t_err);
+    int ret = -1;
+    sim_fec_t* const outs[1] = {fec};
+    if (rfec_di_generate_group(segs, segs_count, &p, outs, &ret) != RFEC_OK)
         return -1;
+    return ret;
+}
+
+/* n independent flex_fec_recover calls (flex_fec_xor.c:55-104) in as few
+ * launches as the staging area allows: job j is a one-line group of K slots,
+ * its count present members first, then zero-filled present slots (neutral
+ * for the XOR of payloads and header records, and for the size checks), the
+ * erased member last; K = 1 + the largest count of the launch.  rets[j] is
+ * what flex_fec_recover returns for the job. */
+int rfec_di_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets)
+{
+    for (int j = 0; j < n; ++j)
+        rets[j] = -1;
+    di_ctx* c = NULL;
+    const di_layout L = di_offsets();
+    int j0 = 0;
+    while (j0 < n) {
+        /* jobs [j0, j1) in one launch */
+        int j1 = j0, K = 0;
+        while (j1 < n && j1 - j0 < RFEC_DI_GROUPS) {
+            const rfec_di_recover_job* J = &jobs[j1];
+            if (J->count <= 0 || J->count + 1 > DI_MAXK || J->fec->fec_data_size > SIM_VIDEO_SIZE) {
+                if (j1 == j0) { /* refused alone: :60-61, or beyond this library's limits */
+                    if (J->count + 1 > DI_MAXK)
+                        set_err(RFEC_EINVAL, "segs_count above RFEC_MAX_K-1", 0);
+                    else if (J->count > 0)
+                        set_err(RFEC_EINVAL, "fec_data_size above SIM_VIDEO_SIZE", 0);
+                    ++j0;
+                    ++j1;
+                    continue;
+                }
+                break;
+            }
+            const int k1 = J->count + 1 > K ? J->count + 1 : K;
+            if (k1 * (j1 - j0 + 1) > DI_MAXK)
+                break;
+            K = k1;
+            ++j1;
+        }
+        if (j1 == j0)
+            continue;
+        if (!c && !(c = di_get()))
+            return RFEC_EDEVICE;
+        const int G = j1 - j0;
+        rfec_hdr* hh = (rfec_hdr*)(c->host + L.hdr);
+        uint64_t* pres = (uint64_t*)(c->host + L.present);
+        uint64_t* pp = (uint64_t*)(c->host + L.ppresent);
+        rfec_hdr* mh = (rfec_hdr*)(c->host + L.meta);
+        uint16_t* fs = (uint16_t*)(c->host + L.fsize);
+        memset(pres, 0, (size_t)G * 2 * sizeof(uint64_t));
+        for (int g = 0; g < G; ++g) {
+            const rfec_di_recover_job* J = &jobs[j0 + g];
+            uint8_t* base = c->host + L.shards + (size_t)g * K * DI_STRIDE;
+            for (int i = 0; i < K - 1; ++i) {
+                if (i < J->count) {
+                    stage_payload(base + (size_t)i * DI_STRIDE, J->segs[i]->data, J->segs[i]->data_size);
+                    seg_to_hdr(J->segs[i], &hh[g * K + i]);
+                } else {
+                    memset(base + (size_t)i * DI_STRIDE, 0, DI_STRIDE);
+                    memset(&hh[g * K + i], 0, sizeof(rfec_hdr));
+                }
+                pres[2 * g + (i >> 6)] |= 1ull << (i & 63);
+            }
+            memset(&hh[g * K + K - 1], 0, sizeof(rfec_hdr));
+            stage_payload(c->host + L.parity + (size_t)g * DI_STRIDE, J->fec->fec_data, J->fec->fec_data_size);
+            memcpy(&mh[g], &J->fec->fec_meta, sizeof(rfec_hdr));
+            fs[g] = J->fec->fec_data_size;
+            pp[g] = 1;
+        }
+        static __thread rfec_kmask M; /* 1.3 KB: keep it off the stack */
+        memset(&M, 0, sizeof(M));
+        M.plan.k = (uint16_t)K;
+        M.plan.n_lines = 1;
+        M.plan.line[0].first = 0;
+        M.plan.line[0].stride = 1;
+        M.plan.line[0].count = (uint8_t)K;
+        for (int i = 0; i < K; ++i)
+            M.mask[0][i >> 6] |= 1ull << (i & 63);
+        const int e = rfec_launch_recover(&M, (uint32_t)G, DI_STRIDE, SIM_VIDEO_SIZE, c->dev + L.shards,
+                                          (rfec_hdr*)(c->dev + L.hdr), (const uint64_t*)(c->dev + L.present),
+                                          c->dev + L.parity, (const rfec_hdr*)(c->dev + L.meta),
+                                          (const uint16_t*)(c->dev + L.fsize), (const uint64_t*)(c->dev + L.ppresent),
+                                          (uint64_t*)(c->dev + L.recovered), c->dev + L.ws, c->stream, g_tuning);
+        if (di_sync(c, e, "flex_fec_recover") != RFEC_OK) {
+            di_loud(t_err);
+            return RFEC_EDEVICE;
+        }
+        const uint64_t* rec = (const uint64_t*)(c->host + L.recovered);
+        for (int g = 0; g < G; ++g) {
+            const rfec_di_recover_job* J = &jobs[j0 + g];
+            const uint32_t Lfec = J->fec->fec_data_size;
+            /* in-place zero padding of the present segments (:91), up to the
+             * first one the reference rejects (:88-89) */
+            for (int i = 0; i < J->count; ++i) {
+                if (J->segs[i]->data_size > Lfec)
+                    break;
+                memset(J->segs[i]->data + J->segs[i]->data_size, 0, (size_t)(Lfec - J->segs[i]->data_size));
+            }
+            if (!((rec[2 * g + ((K - 1) >> 6)] >> ((K - 1) & 63)) & 1ull))
+                continue;
+            const rfec_hdr* r = &hh[g * K + K - 1];
+            sim_segment_t* o = J->out;
+            o->packet_id = r->seq;
+            o->fid = r->fid;
+            o->timestamp = r->ts;
+            o->index = r->index;
+            o->total = r->total;
+            o->ftype = r->ftype;
+            o->payload_type = r->payload_type;
+            o->data_size = r->size;
+            memcpy(o->data, c->host + L.shards + ((size_t)g * K + K - 1) * DI_STRIDE, Lfec);
+            o->fec_id = J->fec->fec_id; /* :101 */
+            rets[j0 + g] = 0;
+        }
+        j0 = j1;
     }
-    const rfec_hdr* m = (const rfec_hdr*)(c->host + L.meta);
-    const uint16_t fds = *(const uint16_t*)(c->host + L.fsize);
-    const int8_t st = *(const int8_t*)(c->host + L.status);
-    fec->fec_data_size = fds;
-    if (st != 0) {
-        /* over capacity (:27-28): the reference has written seg0's header and
-         * the size by then, nothing else */
-        seg_to_hdr(segs[0], (rfec_hdr*)&fec->fec_meta);
-        return -1;
-    }
-    memcpy(&fec->fec_meta, m, sizeof(rfec_hdr));
-    memcpy(fec->fec_data, c->host + L.parity, fds);
-    /* in-place zero padding of segs[1..] to fec_data_size (:47) */
-    for (int i = 1; i < segs_count; ++i)
-        if (segs[i]->data_size < fds)
-            memset(segs[i]->data + segs[i]->data_size, 0, (size_t)(fds - segs[i]->data_size));
-    return 0;
+    return RFEC_OK;
 }
 
 /* flex_fec_xor.c:55-104 on the GPU: the n present segments plus one erased
@@ -548,76 +699,11 @@ int flex_fec_recover(sim_segment_t* segs[], int segs_count, sim_fec_t* fec, sim_
 {
     if (segs_count <= 0) /* :60-61 */
         return -1;
-    if (segs_count + 1 > DI_MAXK) {
-        set_err(RFEC_EINVAL, "segs_count above RFEC_MAX_K-1", 0);
+    const rfec_di_recover_job J = {segs, segs_count, fec, out_seg};
+    int ret = -1;
+    if (rfec_di_recover_lines(&J, 1, &ret) != RFEC_OK)
         return -1;
-    }
-    const uint32_t Lfec = fec->fec_data_size;
-    if (Lfec > SIM_VIDEO_SIZE) {
-        set_err(RFEC_EINVAL, "fec_data_size above SIM_VIDEO_SIZE", 0);
-        return -1;
-    }
-    di_ctx* c = di_get();
-    if (!c)
-        return -1;
-    const di_layout L = di_offsets();
-    const int k = segs_count + 1;
-    rfec_hdr* hh = (rfec_hdr*)(c->host + L.hdr);
-    for (int i = 0; i < segs_count; ++i) {
-        stage_payload(c->host + L.shards + (size_t)i * DI_STRIDE, segs[i]->data, segs[i]->data_size);
-        seg_to_hdr(segs[i], &hh[i]);
-    }
-    memset(&hh[segs_count], 0, sizeof(rfec_hdr));
-    stage_payload(c->host + L.parity, fec->fec_data, Lfec);
-    memcpy(c->host + L.meta, &fec->fec_meta, sizeof(rfec_hdr));
-    *(uint16_t*)(c->host + L.fsize) = (uint16_t)Lfec;
-    uint64_t* pres = (uint64_t*)(c->host + L.present);
-    pres[0] = pres[1] = 0;
-    for (int i = 0; i < segs_count; ++i)
-        pres[i >> 6] |= 1ull << (i & 63);
-    *(uint64_t*)(c->host + L.ppresent) = 1;
-    rfec_kmask* M = (rfec_kmask*)calloc(1, sizeof(rfec_kmask));
-    if (!M)
-        return -1;
-    M->plan.k = (uint16_t)k;
-    M->plan.n_lines = 1;
-    M->plan.line[0].first = 0;
-    M->plan.line[0].stride = 1;
-    M->plan.line[0].count = (uint8_t)k;
-    for (int i = 0; i < k; ++i)
-        M->mask[0][i >> 6] |= 1ull << (i & 63);
-    const int e = rfec_launch_recover(M, 1, DI_STRIDE, SIM_VIDEO_SIZE, c->dev + L.shards,
-                                      (rfec_hdr*)(c->dev + L.hdr), (const uint64_t*)(c->dev + L.present),
-                                      c->dev + L.parity, (const rfec_hdr*)(c->dev + L.meta),
-                                      (const uint16_t*)(c->dev + L.fsize), (const uint64_t*)(c->dev + L.ppresent),
-                                      (uint64_t*)(c->dev + L.recovered), c->dev + L.ws, c->stream, g_tuning);
-    free(M);
-    if (di_sync(c, e, "flex_fec_recover") != RFEC_OK) {
-        di_loud(t_err);
-        return -1;
-    }
-    /* in-place zero padding of the present segments (:91), up to the first
-     * one the reference rejects (:88-89) */
-    for (int i = 0; i < segs_count; ++i) {
-        if (segs[i]->data_size > Lfec)
-            break;
-        memset(segs[i]->data + segs[i]->data_size, 0, (size_t)(Lfec - segs[i]->data_size));
-    }
-    const uint64_t* rec = (const uint64_t*)(c->host + L.recovered);
-    if (!((rec[segs_count >> 6] >> (segs_count & 63)) & 1ull))
-        return -1;
-    const rfec_hdr* r = &hh[segs_count];
-    out_seg->packet_id = r->seq;
-    out_seg->fid = r->fid;
-    out_seg->timestamp = r->ts;
-    out_seg->index = r->index;
-    out_seg->total = r->total;
-    out_seg->ftype = r->ftype;
-    out_seg->payload_type = r->payload_type;
-    out_seg->data_size = r->size;
-    memcpy(out_seg->data, c->host + L.shards + (size_t)segs_count * DI_STRIDE, Lfec);
-    out_seg->fec_id = fec->fec_id; /* :101 */
-    return 0;
+    return ret;
 }
 
 /* ------------------------------------------------------------------------ */

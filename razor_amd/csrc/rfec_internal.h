@@ -76,6 +76,23 @@ int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map
                             void* stream);
 int rfec_launch_zero_tails(uint32_t slots, uint32_t stride, uint8_t* shards, const rfec_hdr* hdr, void* stream);
 const char* rfec_hip_error_string(int code);
+
+/* Group-level drop-in (rfec_flex.c) over the per-thread pinned, device-mapped
+ * staging area of the single-call path (rfec_host.c): one launch and one
+ * stream sync per call.  Both return RFEC_OK once the device work is done
+ * (per-item results in rets[]), or an error code with rfec_last_error set. */
+#define RFEC_DI_GROUPS 8 /* one-line recover jobs per launch */
+typedef struct {
+    sim_segment_t* const* segs; /* the present members */
+    int count;
+    sim_fec_t* fec;
+    sim_segment_t* out;
+} rfec_di_recover_job;
+__attribute__((visibility("hidden"))) int rfec_di_generate_group(sim_segment_t* const* segs, int k,
+                                                                 const rfec_plan* plan, sim_fec_t* const* outs,
+                                                                 int* rets);
+__attribute__((visibility("hidden"))) int rfec_di_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets);
+__attribute__((visibility("hidden"))) int rfec_set_error(int code, const char* what);
 /* sets rfec_last_error() from an errno value (0: `what` alone); returns code */
 int rfec_set_error_sys(int code, const char* what, int err);
 

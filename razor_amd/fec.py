@@ -23,6 +23,7 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 LIBDIR = PKG / "lib"
 HEADER = ROOT / "include" / "razor_fec.h"
+HEADERS = sorted((ROOT / "include").glob("*.h"))
 
 RFEC_MAX_K = 128
 RFEC_MAX_LINES = 64
@@ -252,8 +253,9 @@ _SIGS = {
 
 
 def header_functions() -> list[str]:
-    """Every function declared in include/razor_fec.h."""
-    text = HEADER.read_text()
+    """Every function declared in include/*.h."""
+    text = "\n".join(h.read_text() for h in HEADERS)
+    text = re.sub(r"^\s*typedef[^;]*;", "", text, flags=re.M)  # function-pointer typedefs
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"^\s*[A-Za-z_][\w\s\*]*?\b([a-z_][a-z0-9_]*)\s*\(", text, flags=re.M)))
 

@@ -1,4 +1,4 @@
-"""CPU: the C ABI library loads, exports every symbol include/razor_fec.h
+"""CPU: the C ABI library loads, exports every symbol include/*.h
 declares, and its host-side planner matches the reference (no GPU compute)."""
 import ctypes as C
 import subprocess
@@ -13,7 +13,7 @@ from razor_amd.fec import header_functions
 
 def test_header_symbols_exported(product, product1200):
     fns = header_functions()
-    assert "flex_fec_generate" in fns and "rfec_encode_batch" in fns
+    assert "flex_fec_generate" in fns and "rfec_encode_batch" in fns and "flex_fec_sender_update" in fns
     for lib in (product, product1200):
         for f in fns:
             assert hasattr(lib.lib, f), f"{lib.path.name} does not export {f}"

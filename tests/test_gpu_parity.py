@@ -430,6 +430,59 @@ def test_cascade_header_rejections_gpu(gpu, oracle1000, tuning):
                 assert np.array_equal(out_s[g, i, :L], e_s[g, i, :L]), f"group {g} segment {i}: data"
 
 
+@pytest.mark.parametrize("k", [36, 64])
+def test_cascade_long_schedules_gpu(gpu, oracle1000, k):
+    """Schedules longer than the payload lanes' 7 replayed steps: the sender's
+    full 6x6 / 8x8 plans (one-launch cascade decode) with 8-12 erasures per
+    group, lost parities, header rejections (fec_data_size above capacity or
+    short, a member above fec_data_size) and a workspace of random bytes.  The
+    groups of > 7 steps go through the fix-up pass; masks, headers and data
+    must equal the oracle (the > 7-step path had no targeted case)."""
+    o = oracle1000
+    plan = o.plan_from_fraction(k, 80, 3)
+    assert plan.n_lines == (12 if k == 36 else 16)
+    G, S = 768, 256
+    rng = np.random.default_rng(4242 + k)
+    shards, hdr = o.fill_groups(40 + k, G, k, S, ragged=True)
+    cap = S
+    parity, meta, fsize, _ = o.encode_batch(plan, shards, hdr, cap)
+    present = np.zeros((G, 2), np.uint64)
+    pp = np.full(G, (1 << plan.n_lines) - 1, np.uint64)
+    rx, rh, fs_rx = shards.copy(), hdr.copy(), fsize.copy()
+    for g in range(G):
+        m = (1 << k) - 1
+        for i in rng.choice(k, int(rng.integers(8, 13)), replace=False):
+            m &= ~(1 << int(i))
+            rx[g, i] = 0xA5
+            rh[g, i] = np.zeros((), po.HDR_DTYPE)
+        present[g, 0] = m
+        if rng.random() < 0.15:
+            pp[g] &= ~np.uint64(1 << int(rng.integers(plan.n_lines)))
+        r = rng.random()
+        if r < 0.1:
+            fs_rx[g, rng.integers(plan.n_lines)] = cap + 1
+        elif r < 0.2:
+            l = int(rng.integers(plan.n_lines))
+            fs_rx[g, l] = max(1, int(fs_rx[g, l]) - 5)
+        elif r < 0.3:
+            i = int(rng.integers(k))
+            if (m >> i) & 1:
+                rh[g, i]["size"] = min(cap, int(rh[g, i]["size"]) + 9)
+    steps = [bin(_mask_peel(plan, k, present[g, 0], pp[g])).count("1") for g in range(G)]
+    assert sum(s > 7 for s in steps) >= G // 8, "too few groups with > 7 peel steps"
+    e_s, e_h, e_rec = o.recover_batch(plan, rx, rh, present, parity, meta, fs_rx, pp, cap)
+    rejected = sum(int(e_rec[g, 0]) != _mask_peel(plan, k, present[g, 0], pp[g]) for g in range(G))
+    assert rejected >= 10, f"only {rejected} groups where the header checks change the peel"
+    out_s, out_h, rec = gpu(random_workspace=True).recover(plan, rx, rh, present, parity, meta, fs_rx, pp, cap)
+    assert np.array_equal(rec, e_rec)
+    for g in range(G):
+        for i in range(k):
+            if (int(rec[g, 0]) >> i) & 1:
+                assert out_h[g, i] == e_h[g, i], f"group {g} segment {i}: header"
+                L = int(e_h[g, i]["size"])
+                assert np.array_equal(out_s[g, i, :L], e_s[g, i, :L]), f"group {g} segment {i}: data"
+
+
 @pytest.mark.parametrize("k", [6, 7, 9, 11, 12, 13, 15, 16])
 @pytest.mark.parametrize("tuning", ["default", "two_kernel"])
 def test_full_plan_shapes_gpu(gpu, oracle1000, k, tuning):
