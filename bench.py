@@ -106,7 +106,8 @@ def peel_bytes(plan, k, erased, S):
 
 
 class Workload:
-    def __init__(self, lib, G, k, S, pf, device, group0, seed, stride=None, col=0, full_plan=False, config_id=2):
+    def __init__(self, lib, G, k, S, pf, device, group0, seed, stride=None, col=0, full_plan=False, config_id=2,
+                 in_place=False):
         self.lib, self.G, self.k, self.S = lib, G, k, S
         self.stride = stride or (S + 15) // 16 * 16  # slot width in HBM (>= S, multiple of 16)
         if col:  # explicit rows of `col` (config 5: k = 32 as 8 rows of 4)
@@ -150,6 +151,13 @@ class Workload:
             self.rx[gi, e] = 0xA5
             self.rx_hdr[gi, e] = 0
         self.recovered = torch.empty((G, 2), dtype=torch.int64, device=dev)
+        # recovered segments: into a dense output [G][2] (rfec_recover_batch_out, as flex_fec_recover's
+        # caller-allocated out_seg) where the plan's lines are disjoint, else in place (cascades)
+        self.dense = not (in_place or full_plan)
+        if self.dense:
+            self.out_shards = torch.empty((G, 2, self.stride), dtype=torch.uint8, device=dev)
+            self.out_hdr = torch.empty((G, 2, 20), dtype=torch.uint8, device=dev)
+            self.out_index = torch.empty((G, 2), dtype=torch.uint8, device=dev)
         self.ws = torch.empty((lib.workspace_size(self.plan, G),), dtype=torch.uint8, device=dev)
         # algorithmic payload bytes (headers excluded): encode reads k*S, writes r*S
         self.enc_bytes = G * (k + self.n) * S
@@ -163,6 +171,13 @@ class Workload:
                               self.status.data_ptr(), stream)
 
     def decode(self, stream):
+        if self.dense:
+            self.lib.recover_batch_out(self.plan, self.G, self.stride, self.S, self.rx.data_ptr(),
+                                       self.rx_hdr.data_ptr(), self.present.data_ptr(), self.parity.data_ptr(),
+                                       self.meta.data_ptr(), self.fsize.data_ptr(), self.parity_present.data_ptr(),
+                                       self.recovered.data_ptr(), 2, self.out_shards.data_ptr(),
+                                       self.out_hdr.data_ptr(), self.out_index.data_ptr(), self.ws.data_ptr(), stream)
+            return
         self.lib.recover_batch(self.plan, self.G, self.stride, self.S, self.rx.data_ptr(), self.rx_hdr.data_ptr(),
                                self.present.data_ptr(), self.parity.data_ptr(), self.meta.data_ptr(),
                                self.fsize.data_ptr(), self.parity_present.data_ptr(), self.recovered.data_ptr(),
@@ -184,7 +199,15 @@ class Workload:
                 ref ^= self.shards[:, i, :S]
                 href ^= hdr32[:, i]
             ok = ok and torch.equal(self.parity[:, l, :S], ref) and torch.equal(meta32[:, l], href)
-        ok = ok and torch.equal(self.rx[:, :, :S], self.shards[:, :, :S]) and torch.equal(self.rx_hdr, self.hdr)
+        if self.dense:  # out slot e = the e-th erased segment in index order; the received set untouched
+            gi = torch.arange(self.G, device=self.shards.device)
+            for e in range(2):
+                idx = torch.from_numpy(np.sort(self.erased, axis=1)[:, e].astype(np.int64)).to(self.shards.device)
+                ok = ok and torch.equal(self.out_shards[:, e, :S], self.shards[gi, idx, :S])
+                ok = ok and torch.equal(self.out_hdr[:, e], self.hdr[gi, idx])
+                ok = ok and torch.equal(self.out_index[:, e].long(), idx)
+        else:
+            ok = ok and torch.equal(self.rx[:, :, :S], self.shards[:, :, :S]) and torch.equal(self.rx_hdr, self.hdr)
         exp = ((1 << self.erased[:, 0]) | (1 << self.erased[:, 1])).astype(np.int64)
         ok = ok and np.array_equal(self.recovered[:, 0].cpu().numpy(), exp)
         ok = ok and int(self.status.abs().sum()) == 0
@@ -367,6 +390,8 @@ def main():
     ap.add_argument("--sets", type=int, default=2, help="disjoint buffer sets rotated per step (MALL-proof timing)")
     ap.add_argument("--col", type=int, default=0, help="custom: rows of COL segments")
     ap.add_argument("--full-plan", action="store_true", help="custom: rows + columns of the reference plan")
+    ap.add_argument("--in-place", action="store_true",
+                    help="decode into the received shards (rfec_recover_batch) instead of a dense output")
     ap.add_argument("--hot-decode", action="store_true",
                     help="decode the set encoded in the same step (its parity still MALL-resident)")
     args = ap.parse_args()
@@ -423,7 +448,8 @@ def main():
     col = int(cfg["plan"][3:]) if cfg["plan"].startswith("col") else 0
     full_plan = cfg["plan"] == "full"
     sets = [Workload(lib, my_groups, k, S, args.protect_fraction, device, group0, seed=1000 + rank,
-                     stride=args.stride or None, col=col, full_plan=full_plan, config_id=cfg["config_id"])
+                     stride=args.stride or None, col=col, full_plan=full_plan, config_id=cfg["config_id"],
+                     in_place=args.in_place)
             for _ in range(max(1, args.sets))]
     w = sets[0]
     nset = len(sets)
@@ -504,7 +530,7 @@ def main():
                       else (f"k_encode_matrix<{k},{w.plan.col}>" if full_plan else "k_encode (plan-driven)"))
         cd = (S + 15) // 16
         if full_plan:
-            dec_kernels = "k_decode_cascade + k_decode_fixup (one launch + fix-up)"
+            dec_kernels = "k_decode_cascade + k_decode_fixup (one launch + fix-up, in place)"
         elif cd >= 64 and rows_layout and (k, lines[0]) in ((10, 4), (32, 4)):
             dec_kernels = f"k_decode_rows<{k},{lines[0]}> (one lane per (group, row, chunk); header blocks spread)"
         elif cd >= 64:
@@ -556,6 +582,8 @@ def main():
             "encode_source_gibps": round(w.G * w.k * w.S / enc_mean / 2**30, 2),
             "encode_read_only_frac": round(w.G * w.k * w.S / enc_mean / 1e9 / HBM_PEAK_GBPS, 4),
             "decode_gibps": round(w.dec_bytes / dec_mean / 2**30, 2),
+            "decode_output": ("dense: rfec_recover_batch_out, recovered segments to [G][2] slots (flex_fec_recover's "
+                              "out_seg); the received shards read only" if w.dense else "in place: rfec_recover_batch"),
             "decode_roofline": {"achieved": round(w.dec_bytes / dec_mean / 1e9, 1), "frac":
                                 round(w.dec_bytes / dec_mean / 1e9 / HBM_PEAK_GBPS, 4),
                                 "launch_us": round(dec_mean * 1e6, 2),

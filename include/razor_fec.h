@@ -189,6 +189,29 @@ int rfec_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, 
                        void* stream);
 
 /*
+ * Recovery into a dense output, as flex_fec_recover writes each recovered
+ * segment into a caller-allocated out_seg (flex_fec_xor.c:55-104,
+ * flex_fec_receiver.c:142-143): the shards and headers are only read.  The
+ * e-th erased segment of group g (e-th in segment-index order among the
+ * segments whose present bit is clear, e < per_group) goes to
+ *   out_shards [g*per_group + e][stride]   payload bytes [0, fec_data_size)
+ *   out_hdr    [g*per_group + e]           its recovered header record
+ *   out_index  [g*per_group + e]           its segment index, or 0xFF where
+ *                                          that erased segment was not recovered
+ * and `recovered` gets its bit as in rfec_recover_batch (erased segments of
+ * rank >= per_group are left out).  Plans whose lines are pairwise disjoint
+ * (the row layer, strip mode: no recovery feeds another) with at most 8
+ * members per line; others return RFEC_EINVAL (rfec_recover_batch recovers
+ * them in place).  Same workspace as rfec_recover_batch.
+ */
+int rfec_recover_batch_out(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
+                           const uint8_t* shards, const rfec_hdr* hdr, const uint64_t* present,
+                           const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fec_size,
+                           const uint64_t* parity_present, uint64_t* recovered, uint32_t per_group,
+                           uint8_t* out_shards, rfec_hdr* out_hdr, uint8_t* out_index, void* workspace,
+                           void* stream);
+
+/*
  * Host-resident batch: the path that starts and ends in host memory (segments
  * built from UDP socket buffers, sim_session.c).  Gathers G groups of
  * sim_segment_t (segs[g*k + i], this library's SIM_VIDEO_SIZE layout) into a

@@ -257,6 +257,51 @@ int rfec_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, 
     return e ? set_err(RFEC_EDEVICE, "recover launch", e) : RFEC_OK;
 }
 
+int rfec_recover_batch_out(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
+                           const uint8_t* shards, const rfec_hdr* hdr, const uint64_t* present,
+                           const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fec_size,
+                           const uint64_t* parity_present, uint64_t* recovered, uint32_t per_group,
+                           uint8_t* out_shards, rfec_hdr* out_hdr, uint8_t* out_index, void* workspace,
+                           void* stream)
+{
+    int rc = check_plan(plan);
+    if (rc)
+        return rc;
+    if ((rc = check_geometry(groups, stride, capacity, plan->k)))
+        return rc;
+    if (per_group == 0 || per_group > plan->k)
+        return set_err(RFEC_EINVAL, "per_group must be in [1, k]", 0);
+    if ((uint64_t)groups * per_group * (stride / 16) >= (1ull << 40))
+        return set_err(RFEC_EINVAL, "dense output too large", 0);
+    if (groups == 0)
+        return RFEC_OK;
+    if (!shards || !hdr || !present || !parity_present || !recovered || !workspace || !out_shards || !out_hdr ||
+        !out_index || (plan->n_lines && (!parity || !meta || !fec_size)))
+        return set_err(RFEC_EINVAL, "NULL buffer", 0);
+    if ((uintptr_t)workspace % 16)
+        return set_err(RFEC_EINVAL, "workspace must be 16-byte aligned", 0);
+    static __thread rfec_kmask M;
+    make_masks(plan, &M);
+    uint64_t seen0 = 0, seen1 = 0;
+    for (int l = 0; l < plan->n_lines; ++l) {
+        if (plan->line[l].count > 8 || (seen0 & M.mask[l][0]) || (seen1 & M.mask[l][1]))
+            return set_err(RFEC_EINVAL, "dense output needs pairwise disjoint lines of <= 8 members", 0);
+        seen0 |= M.mask[l][0];
+        seen1 |= M.mask[l][1];
+    }
+    {   /* header lanes: one per (group, line slot), 32-bit lane index */
+        unsigned lg = 1;
+        while ((1u << lg) < plan->n_lines)
+            ++lg;
+        if (((uint64_t)groups << lg) >= (1ull << 32))
+            return set_err(RFEC_EINVAL, "batch too large for one launch (groups x lines)", 0);
+    }
+    const rfec_dense_out D = {out_shards, out_hdr, out_index, per_group};
+    const int e = rfec_launch_recover_out(&M, groups, stride, capacity, shards, hdr, present, parity, meta, fec_size,
+                                          parity_present, recovered, workspace, stream, g_tuning, &D);
+    return e ? set_err(RFEC_EDEVICE, "recover launch", e) : RFEC_OK;
+}
+
 int rfec_zero_tails(uint32_t groups, uint32_t k, uint32_t stride, uint8_t* shards, const rfec_hdr* hdr,
                     void* stream)
 {

@@ -47,6 +47,19 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
                         const rfec_hdr* meta, const uint16_t* fsize, const uint64_t* parity_present,
                         uint64_t* recovered, void* ws, void* stream, unsigned flags);
 
+/* dense output of rfec_recover_batch_out (device pointers; per_group > 0) */
+typedef struct {
+    uint8_t* shards;  /* [G][per_group][stride] */
+    rfec_hdr* hdr;    /* [G][per_group] */
+    uint8_t* index;   /* [G][per_group] */
+    uint32_t per_group;
+} rfec_dense_out;
+int rfec_launch_recover_out(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32_t capacity,
+                            const uint8_t* shards, const rfec_hdr* hdr, const uint64_t* present,
+                            const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fsize,
+                            const uint64_t* parity_present, uint64_t* recovered, void* ws, void* stream,
+                            unsigned flags, const rfec_dense_out* out);
+
 /* bytes of one group's peeling-schedule record: step count, single-level
  * flag, then a (line, target) byte pair per step; 16-byte multiple */
 static inline uint32_t rfec_sched_record_bytes(uint32_t n_lines) { return (2u + 2u * n_lines + 15u) & ~15u; }

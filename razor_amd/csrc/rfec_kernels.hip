@@ -683,7 +683,26 @@ struct PeelArgs {
     unsigned long long* fixc;
     uint32_t* fixlist;
     uint32_t gen;
+    // dense output (rfec_recover_batch_out): recovered segment e of group g
+    // (the e-th erased one in index order, e < out_per_group) goes to
+    // out_hdr[g * out_per_group + e]; out_per_group == 0: in place
+    rfec_hdr* out_hdr;
+    uint8_t* out_index;
+    uint32_t out_per_group;
 };
+
+// Payload side of the dense output: out slot (g * E + e) of `sh` (E == 0: in place).
+struct DenseOut {
+    v4u* sh;
+    uint32_t E;
+};
+
+// rank of erased segment t among the group's erased segments (index order)
+__device__ __forceinline__ uint32_t missing_rank(uint64_t h0, uint64_t h1, uint32_t t)
+{
+    return t < 64 ? (uint32_t)__popcll(~h0 & ((1ull << t) - 1ull))
+                  : (uint32_t)__popcll(~h0) + (uint32_t)__popcll(~h1 & ((1ull << (t - 64)) - 1ull));
+}
 
 __device__ __forceinline__ void fix_append(const PeelArgs& A, uint32_t g)
 {
@@ -1143,9 +1162,18 @@ __device__ void line_headers(const PeelArgs& A, const rfec_kmask& M, uint32_t bl
                 ok = ok && (w[q][4] >> 16) <= L;
             }
             if (ok && (r4 >> 16) <= L) {
-                uint32_t* ht = reinterpret_cast<uint32_t*>(A.hdr + (size_t)g * P.k + t);
-                ht[0] = r0, ht[1] = r1, ht[2] = r2, ht[3] = r3, ht[4] = r4;
-                rec[t >> 5] = 1u << (t & 31);
+                uint32_t* ht = nullptr;
+                if (!A.out_per_group) {
+                    ht = reinterpret_cast<uint32_t*>(A.hdr + (size_t)g * P.k + t);
+                } else {
+                    const uint32_t e = missing_rank(h0, h1, t);
+                    if (e < A.out_per_group)
+                        ht = reinterpret_cast<uint32_t*>(A.out_hdr + (size_t)g * A.out_per_group + e);
+                }
+                if (ht) {
+                    ht[0] = r0, ht[1] = r1, ht[2] = r2, ht[3] = r3, ht[4] = r4;
+                    rec[t >> 5] = 1u << (t & 31);
+                }
             }
         }
     }
@@ -1156,6 +1184,26 @@ __device__ void line_headers(const PeelArgs& A, const rfec_kmask& M, uint32_t bl
     if (g < A.groups && l == 0) {
         A.recovered[2 * g] = (uint64_t)rec[1] << 32 | rec[0];
         A.recovered[2 * g + 1] = (uint64_t)rec[3] << 32 | rec[2];
+        if (A.out_per_group) {
+            // out_index: the e-th erased segment's index where it was recovered, else 0xFF
+            const uint32_t K = P.k;
+            uint64_t m0 = ~A.present[2 * g] & (K >= 64 ? ~0ull : (1ull << K) - 1ull);
+            uint64_t m1 = K <= 64 ? 0ull : ~A.present[2 * g + 1] & (K >= 128 ? ~0ull : (1ull << (K - 64)) - 1ull);
+            uint8_t* oi = A.out_index + (size_t)g * A.out_per_group;
+            for (uint32_t e = 0; e < A.out_per_group; ++e) {
+                uint32_t v = 0xFF;
+                if (m0 | m1) {
+                    const uint32_t i = m0 ? (uint32_t)__ffsll((long long)m0) - 1 : 64u + (uint32_t)__ffsll((long long)m1) - 1;
+                    if ((rec[i >> 5] >> (i & 31)) & 1u)
+                        v = i;
+                    if (m0)
+                        m0 &= m0 - 1;
+                    else
+                        m1 &= m1 - 1;
+                }
+                oi[e] = (uint8_t)v;
+            }
+        }
     }
 }
 
@@ -1189,7 +1237,7 @@ template <int MAXC, bool NTL, int NTS, int NI>
 __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v4u* __restrict__ parity,
                                                             uint32_t total, uint32_t C, FastDiv divC,
                                                             uint32_t n_hdr_blocks, uint32_t hdr_every, PeelArgs A,
-                                                            rfec_kmask M)
+                                                            rfec_kmask M, DenseOut D)
 {
     uint32_t hb, pb;
     if (header_block(n_hdr_blocks, hdr_every, &hb, &pb)) {
@@ -1206,12 +1254,14 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
     const uint32_t t0 = pb * kBlock + threadIdx.x;
     uint64_t h0[NI], h1[NI], fire[NI];
     v4u* grp[NI];
+    v4u* out[NI]; // dense output: the group's first out slot at this chunk column
     const v4u* par[NI];
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
         const uint32_t t = t0 + u * lanes;
         h0[u] = h1[u] = fire[u] = 0;
         grp[u] = shards;
+        out[u] = D.sh;
         par[u] = parity;
         if (t < total) {
             const uint32_t g = fdiv(t, divC);
@@ -1220,6 +1270,8 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
             h1[u] = A.present[2 * g + 1];
             fire[u] = A.parity_present[g];
             grp[u] = shards + (size_t)g * P.k * C + j;
+            if (D.E)
+                out[u] = D.sh + (size_t)g * D.E * C + j;
             par[u] = parity + (size_t)g * P.n_lines * C + j;
         }
     }
@@ -1275,8 +1327,15 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
 #pragma unroll
                 for (int q = 0; q < MAXC; ++q)
                     acc[u][b] ^= mv[u][b][q];
-                if (on[u][b])
-                    st16<NTS>(grp[u] + (size_t)tg[u][b] * C, acc[u][b]);
+                if (on[u][b]) {
+                    if (!D.E) {
+                        st16<NTS>(grp[u] + (size_t)tg[u][b] * C, acc[u][b]);
+                    } else {
+                        const uint32_t e = missing_rank(h0[u], h1[u], tg[u][b]);
+                        if (e < D.E)
+                            st16<NTS>(out[u] + (size_t)e * C, acc[u][b]);
+                    }
+                }
             }
             more = more || fire[u] != 0;
         }
@@ -1295,7 +1354,7 @@ template <int MAXC, bool NTL, int NTS>
 __global__ __launch_bounds__(kBlock) void k_decode_out(v4u* shards, const v4u* __restrict__ parity, uint32_t total,
                                                        uint32_t C, FastDiv divC, FastDiv divLC,
                                                        uint32_t n_hdr_blocks, uint32_t hdr_every, PeelArgs A,
-                                                       rfec_kmask M)
+                                                       rfec_kmask M, DenseOut D)
 {
     uint32_t hb, pb;
     if (header_block(n_hdr_blocks, hdr_every, &hb, &pb)) {
@@ -1324,9 +1383,16 @@ __global__ __launch_bounds__(kBlock) void k_decode_out(v4u* shards, const v4u* _
     if (__popcll(x0) + __popcll(x1) != 1 || ((lmask[l][0] & h0) | (lmask[l][1] & h1)) == 0)
         return;
     const uint32_t tgt = x0 ? (uint32_t)__ffsll((long long)x0) - 1 : 64u + (uint32_t)__ffsll((long long)x1) - 1;
+    v4u* grp = shards + (size_t)g * P.k * C + j;
+    v4u* dst = grp + (size_t)tgt * C;
+    if (D.E) {
+        const uint32_t e = missing_rank(h0, h1, tgt);
+        if (e >= D.E)
+            return;
+        dst = D.sh + ((size_t)g * D.E + e) * C + j;
+    }
     const uint32_t ln = lplan[l];
     const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
-    v4u* grp = shards + (size_t)g * P.k * C + j;
     v4u acc = ld16<NTL>(parity + ((size_t)g * P.n_lines + l) * C + j);
     v4u mv[MAXC];
 #pragma unroll
@@ -1339,7 +1405,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_out(v4u* shards, const v4u* _
 #pragma unroll
     for (int q = 0; q < MAXC; ++q)
         acc ^= mv[q];
-    st16<NTS>(grp + (size_t)tgt * C, acc);
+    st16<NTS>(dst, acc);
 }
 
 // The same for the row layouts of the encode fast path (rows of COL
@@ -1350,7 +1416,7 @@ template <int K, int COL, bool NTL, int NTS>
 __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* __restrict__ parity, uint32_t total,
                                                         uint32_t C, FastDiv divC, FastDiv divRC,
                                                         uint32_t n_hdr_blocks, uint32_t hdr_every, PeelArgs A,
-                                                        rfec_kmask M)
+                                                        rfec_kmask M, DenseOut D)
 {
     static_assert(K <= 64, "row decode keeps the present mask in one word");
     uint32_t hb, pb;
@@ -1374,6 +1440,13 @@ __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* 
     if (__popcll(miss) != 1 || !((A.parity_present[g] >> r) & 1ull))
         return;
     const uint32_t tgt = (uint32_t)__ffsll((long long)miss) - 1;
+    v4u* dst = shards + ((size_t)g * K + tgt) * C + j;
+    if (D.E) {
+        const uint32_t e = (uint32_t)__popcll(~h & ((1ull << tgt) - 1ull));
+        if (e >= D.E)
+            return;
+        dst = D.sh + ((size_t)g * D.E + e) * C + j;
+    }
     v4u* row = shards + ((size_t)g * K + r * COL) * C + j;
     v4u acc = ld16<NTL>(parity + ((size_t)g * R + r) * C + j);
     v4u mv[COL];
@@ -1386,7 +1459,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* 
 #pragma unroll
     for (int q = 0; q < COL; ++q)
         acc ^= mv[q];
-    st16<NTS>(shards + ((size_t)g * K + tgt) * C + j, acc);
+    st16<NTS>(dst, acc);
 }
 
 // Fused disjoint-plan decode, group-per-wave mapping (see k_encode_rows_gw):
@@ -1653,6 +1726,7 @@ struct FusedArgs {
     uint32_t n_hdr;
     hipStream_t stream;
     bool spread; // header blocks spread over the grid (RFEC_TUNE_HDR_SPREAD)
+    DenseOut D;  // recovered payloads in place (E == 0) or to the dense output
 };
 
 // header_block()'s period for npay payload blocks (0: header blocks first).
@@ -1732,7 +1806,7 @@ void launch_fused_out(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_
     const uint32_t every = hdr_every(F, npay);
 #define RFEC_FUSED_OUT(NTL, NTS)                                                                                 \
     hipLaunchKernelGGL((k_decode_out<MAXC, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards, F.parity, total, \
-                       F.C, dC, dLC, F.n_hdr, every, B, M)
+                       F.C, dC, dLC, F.n_hdr, every, B, M, F.D)
     switch (sp) {
     case -1: RFEC_FUSED_OUT(false, 1); break;
     case 0: RFEC_FUSED_OUT(true, 0); break;
@@ -1753,7 +1827,7 @@ void launch_fused_rows(const FusedArgs& F, int sp, const PeelArgs& B, const rfec
     const FastDiv dC = make_fastdiv(cd), dRC = make_fastdiv(R * cd);
 #define RFEC_FUSED_ROWS(NTL, NTS)                                                                                \
     hipLaunchKernelGGL((k_decode_rows<K, COL, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards, F.parity,    \
-                       total, F.C, dC, dRC, F.n_hdr, hdr_every(F, blocks_for(total)), B, M)
+                       total, F.C, dC, dRC, F.n_hdr, hdr_every(F, blocks_for(total)), B, M, F.D)
     switch (sp) {
     case -1: RFEC_FUSED_ROWS(false, 1); break;
     case 0: RFEC_FUSED_ROWS(true, 0); break;
@@ -1771,7 +1845,7 @@ void launch_fused(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmas
     const dim3 grid(F.n_hdr + blocks_for((F.total + NI - 1) / NI));
 #define RFEC_FUSED(NTL, NTS)                                                                                     \
     hipLaunchKernelGGL((k_decode_disjoint<MAXC, NTL, NTS, NI>), grid, dim3(kBlock), 0, F.stream, F.shards,       \
-                       F.parity, F.total, F.C, F.f, F.n_hdr, hdr_every(F, grid.x - F.n_hdr), B, M)
+                       F.parity, F.total, F.C, F.f, F.n_hdr, hdr_every(F, grid.x - F.n_hdr), B, M, F.D)
     switch (sp) {
     case -1: RFEC_FUSED(false, 1); break;
     case 0: RFEC_FUSED(true, 0); break;
@@ -1929,12 +2003,20 @@ int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, ui
     }
 }
 
-int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32_t capacity,
-                        uint8_t* shards, rfec_hdr* hdr, const uint64_t* present, const uint8_t* parity,
-                        const rfec_hdr* meta, const uint16_t* fsize, const uint64_t* parity_present,
-                        uint64_t* recovered, void* ws, void* stream, unsigned flags)
+} // extern "C"
+
+namespace {
+
+int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32_t capacity, uint8_t* shards,
+                   rfec_hdr* hdr, const uint64_t* present, const uint8_t* parity, const rfec_hdr* meta,
+                   const uint16_t* fsize, const uint64_t* parity_present, uint64_t* recovered, void* ws,
+                   void* stream, unsigned flags, const rfec_dense_out* out)
 {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const bool dense = out && out->per_group;
+    if (dense) // the dense-output forms: fused decodes, header lanes (the host checks the plan is disjoint)
+        flags &= ~(RFEC_KFLAG_WAVE_DECODE | RFEC_KFLAG_TWO_KERNEL_DECODE | RFEC_KFLAG_PIPE_DECODE |
+                   RFEC_KFLAG_GROUP_WAVE | RFEC_KFLAG_LDS_HDR_PEEL | RFEC_KFLAG_DIAG_NO_HDR);
     const bool ntl = !(flags & RFEC_KFLAG_PLAIN_LOADS);
     if (flags & RFEC_KFLAG_WAVE_DECODE) {
         RecArgs A;
@@ -1969,6 +2051,10 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
     B.groups = groups;
     B.capacity = capacity;
     B.rec_bytes = rfec_sched_record_bytes(P.n_lines);
+    B.out_hdr = dense ? out->hdr : nullptr;
+    B.out_index = dense ? out->index : nullptr;
+    B.out_per_group = dense ? out->per_group : 0u;
+    const DenseOut DO = {dense ? reinterpret_cast<v4u*>(out->shards) : nullptr, dense ? out->per_group : 0u};
     uint64_t seen0 = 0, seen1 = 0;
     B.disjoint = 1;
     for (uint32_t l = 0; l < P.n_lines; ++l) {
@@ -1982,6 +2068,8 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
         maxc = P.line[l].count > maxc ? P.line[l].count : maxc;
     // disjoint plans (row layer alone, strip mode) decode in one launch
     const bool fused = B.disjoint && maxc <= 8 && !(flags & (RFEC_KFLAG_TWO_KERNEL_DECODE | RFEC_KFLAG_PIPE_DECODE));
+    if (dense && !fused)
+        return (int)hipErrorInvalidValue; // rfec_recover_batch_out checks this first
     // plans with cascades (the sender's matrix plans): one launch + fix-up
     const bool cascade = !B.disjoint && maxc <= 8 &&
                          !(flags & (RFEC_KFLAG_TWO_KERNEL_DECODE | RFEC_KFLAG_PIPE_DECODE));
@@ -2020,7 +2108,7 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
     if (fused) {
         // header blocks spread over the grid by default (tools/step_ab.py, cold: k = 32 / 256 B flat
         // 41.6 vs 46.9 us at the head; k = 10 / 1,200 B rows 139.4-141.1 vs 144.0-144.4 us)
-        const FusedArgs F = {sh, pp, total, C, f, n_hdr, st, !(flags & RFEC_KFLAG_HDR_HEAD)};
+        const FusedArgs F = {sh, pp, total, C, f, n_hdr, st, !(flags & RFEC_KFLAG_HDR_HEAD), DO};
         const int sp = ntl ? store_policy(flags, kRecoverStoreDefault) : -1;
         const GwGeom gg = gw_geom(groups, cd);
         const uint32_t swz = (flags & RFEC_KFLAG_XCD_SWIZZLE) ? 1u : 0u;
@@ -2065,7 +2153,7 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
         return (int)hipGetLastError();
     }
     if (cascade) {
-        const FusedArgs F = {sh, pp, total, C, f, n_hdr, st};
+        const FusedArgs F = {sh, pp, total, C, f, n_hdr, st, false, DO};
         const int sp = ntl ? store_policy(flags, kRecoverStoreDefault) : -1;
         if (maxc <= 4)
             launch_cascade<4, 2>(F, sp, B, *M);
@@ -2088,6 +2176,30 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
     else
         launch_replay<8, 1, false>(R, ntl, nts, P, grid);
     return (int)hipGetLastError();
+}
+
+} // namespace
+
+extern "C" {
+
+int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32_t capacity,
+                        uint8_t* shards, rfec_hdr* hdr, const uint64_t* present, const uint8_t* parity,
+                        const rfec_hdr* meta, const uint16_t* fsize, const uint64_t* parity_present,
+                        uint64_t* recovered, void* ws, void* stream, unsigned flags)
+{
+    return launch_recover(M, groups, stride, capacity, shards, hdr, present, parity, meta, fsize, parity_present,
+                          recovered, ws, stream, flags, nullptr);
+}
+
+int rfec_launch_recover_out(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32_t capacity,
+                            const uint8_t* shards, const rfec_hdr* hdr, const uint64_t* present,
+                            const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fsize,
+                            const uint64_t* parity_present, uint64_t* recovered, void* ws, void* stream,
+                            unsigned flags, const rfec_dense_out* out)
+{
+    // the fused decodes only read the shards and headers when the output is dense
+    return launch_recover(M, groups, stride, capacity, const_cast<uint8_t*>(shards), const_cast<rfec_hdr*>(hdr),
+                          present, parity, meta, fsize, parity_present, recovered, ws, stream, flags, out);
 }
 
 int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map, uint32_t rows, uint32_t stride,

@@ -208,6 +208,8 @@ _SIGS = {
     "rfec_recover_workspace_size": (C.c_size_t, [C.POINTER(rfec_plan), C.c_uint32]),
     "rfec_recover_batch": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, C.c_uint32, C.c_uint32,
                                      _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "rfec_recover_batch_out": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, C.c_uint32, C.c_uint32,
+                                         _P, _P, _P, _P, _P, _P, _P, _P, C.c_uint32, _P, _P, _P, _P, _P]),
     "rfec_zero_tails": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P]),
     "rfec_wire_frame_fec": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, _P, C.c_uint32, _P,
                                       _P, _P]),
@@ -340,6 +342,14 @@ class Native:
         self._check(self.lib.rfec_recover_batch(C.byref(as_plan(plan)), groups, stride, capacity, shards, hdr, present,
                                                 parity, meta, fec_size, parity_present, recovered, workspace,
                                                 stream), "rfec_recover_batch")
+
+    def recover_batch_out(self, plan, groups, stride, capacity, shards, hdr, present, parity, meta, fec_size,
+                          parity_present, recovered, per_group, out_shards, out_hdr, out_index, workspace,
+                          stream=None):
+        self._check(self.lib.rfec_recover_batch_out(C.byref(as_plan(plan)), groups, stride, capacity, shards, hdr,
+                                                    present, parity, meta, fec_size, parity_present, recovered,
+                                                    per_group, out_shards, out_hdr, out_index, workspace, stream),
+                    "rfec_recover_batch_out")
 
     def host_encode_groups(self, plan, groups, seg_ptrs, fec_ptrs, fec_id0=1):
         """seg_ptrs / fec_ptrs: host addresses (uint64 numpy arrays) of the

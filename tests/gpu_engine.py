@@ -69,6 +69,40 @@ class GpuEngine:
         return (_host(d_sh, np.uint8, (G, k, stride)), _host(d_h, HDR_DTYPE, (G, k)),
                 _host(d_rec, np.uint64, (G, 2)))
 
+    def recover_out(self, plan, shards, hdr, present, parity, meta, fsize, pp, capacity, per_group):
+        """rfec_recover_batch_out: returns (out_shards [G][E][stride], out_hdr
+        [G][E], out_index [G][E], recovered [G][2]) and checks that the inputs
+        were left untouched."""
+        G, k, stride = shards.shape
+        E = per_group
+        d_sh = _dev(shards, self.device)
+        d_h = _dev(hdr, self.device)
+        d_pr = _dev(np.ascontiguousarray(present, np.uint64), self.device)
+        d_p = _dev(parity, self.device)
+        d_m = _dev(meta, self.device)
+        d_f = _dev(np.ascontiguousarray(fsize, np.uint16), self.device)
+        d_pp = _dev(np.ascontiguousarray(pp, np.uint64), self.device)
+        d_rec = torch.full((G * 16,), 0xEE, dtype=torch.uint8, device=self.device)
+        o_sh = torch.full((G * E * stride,), 0x3C, dtype=torch.uint8, device=self.device)
+        o_h = torch.full((G * E * 20,), 0x3C, dtype=torch.uint8, device=self.device)
+        o_i = torch.full((G * E,), 0x3C, dtype=torch.uint8, device=self.device)
+        nws = max(16, self.lib.workspace_size(plan, G))
+        ws = (torch.randint(0, 256, (nws,), dtype=torch.uint8, device=self.device) if self.random_workspace
+              else torch.zeros((nws,), dtype=torch.uint8, device=self.device))
+        self.lib.set_tuning(self.tuning)
+        try:
+            self.lib.recover_batch_out(plan, G, stride, capacity, d_sh.data_ptr(), d_h.data_ptr(), d_pr.data_ptr(),
+                                       d_p.data_ptr(), d_m.data_ptr(), d_f.data_ptr(), d_pp.data_ptr(),
+                                       d_rec.data_ptr(), E, o_sh.data_ptr(), o_h.data_ptr(), o_i.data_ptr(),
+                                       ws.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
+            torch.cuda.synchronize(self.device)
+        finally:
+            self.lib.set_tuning(0)
+        assert np.array_equal(_host(d_sh, np.uint8, (G, k, stride)), shards), "shards written"
+        assert np.array_equal(_host(d_h, HDR_DTYPE, (G, k)), hdr), "headers written"
+        return (_host(o_sh, np.uint8, (G, E, stride)), _host(o_h, HDR_DTYPE, (G, E)), _host(o_i, np.uint8, (G, E)),
+                _host(d_rec, np.uint64, (G, 2)))
+
 
 class GpuWire:
     """The wire codec (rfec_wire_*) on numpy inputs."""

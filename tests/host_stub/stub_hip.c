@@ -135,6 +135,18 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
     return 0;
 }
 
+/* dense output form: not used by the host control plane; refused */
+int rfec_launch_recover_out(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32_t capacity,
+                            const uint8_t* shards, const rfec_hdr* hdr, const uint64_t* present,
+                            const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fsize,
+                            const uint64_t* parity_present, uint64_t* recovered, void* ws, void* stream,
+                            unsigned flags, const rfec_dense_out* out)
+{
+    (void)M, (void)groups, (void)stride, (void)capacity, (void)shards, (void)hdr, (void)present, (void)parity;
+    (void)meta, (void)fsize, (void)parity_present, (void)recovered, (void)ws, (void)stream, (void)flags, (void)out;
+    return (int)hipErrorInvalidValue;
+}
+
 int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
                                const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,
                                const rfec_fec_stamp* stamps, const uint32_t* order, uint32_t dstride,

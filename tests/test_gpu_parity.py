@@ -571,3 +571,73 @@ def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tunin
                 assert np.array_equal(out_s[g, i, :L], e_s[g, i, :L]), f"group {g} segment {i}: data"
             elif (int(present[g, 0]) >> i) & 1:
                 assert out_h[g, i] == rh[g, i] and np.array_equal(out_s[g, i], rx[g, i])
+
+
+@pytest.mark.parametrize("k,col,S", [(10, 4, 1200), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 64)])
+@pytest.mark.parametrize("tuning", ["default", "flat_decode", "out_decode", "hdr_head", "generic"])
+def test_dense_output_decode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning):
+    """rfec_recover_batch_out (recovered segments into a dense output, as
+    flex_fec_recover's caller-allocated out_seg): row plans with up to 6
+    erasures per group, lost parities and header rejections.  Out slot e of a
+    group holds its e-th erased segment: index, header and bytes equal the
+    oracle's in-place recovery, 0xFF where it was not recovered; erased
+    segments beyond per_group are left out of the recovered mask; the inputs
+    stay untouched (checked in recover_out)."""
+    o = oracle1200 if S > 1000 else oracle1000
+    rows = (k + col - 1) // col
+    plan = o.plan_matrix(k, rows, col, 1)
+    G = 600
+    rng = np.random.default_rng(k * 77 + S)
+    shards, hdr = o.fill_groups(51, G, k, S, ragged=True)
+    cap = min(o.video_size, S)
+    parity, meta, fsize, _ = o.encode_batch(plan, shards, hdr, cap)
+    present = np.zeros((G, 2), np.uint64)
+    pp = np.full(G, (1 << plan.n_lines) - 1, np.uint64)
+    rx, rh, fs_rx = shards.copy(), hdr.copy(), fsize.copy()
+    for g in range(G):
+        m = (1 << k) - 1
+        for i in rng.choice(k, int(rng.integers(0, 7)), replace=False):
+            m &= ~(1 << int(i))
+            rx[g, i] = 0xA5
+            rh[g, i] = np.zeros((), po.HDR_DTYPE)
+        present[g, 0] = m
+        if rng.random() < 0.2:
+            pp[g] &= ~np.uint64(1 << int(rng.integers(plan.n_lines)))
+        r = rng.random()
+        if r < 0.15:
+            fs_rx[g, rng.integers(plan.n_lines)] = cap + 1
+        elif r < 0.3:
+            l = int(rng.integers(plan.n_lines))
+            fs_rx[g, l] = max(1, int(fs_rx[g, l]) - 3)
+        elif r < 0.45:
+            i = int(rng.integers(k))
+            if (m >> i) & 1:
+                rh[g, i]["size"] = min(cap, int(rh[g, i]["size"]) + 5)
+    e_s, e_h, e_rec = o.recover_batch(plan, rx, rh, present, parity, meta, fs_rx, pp, cap)
+    for E in (1, 3):
+        out_s, out_h, out_i, rec = gpu(tuning=TUNINGS[tuning]).recover_out(plan, rx, rh, present, parity, meta,
+                                                                           fs_rx, pp, cap, E)
+        n_rec = 0
+        for g in range(G):
+            missing = [i for i in range(k) if not (int(present[g, 0]) >> i) & 1]
+            want_mask = 0
+            for e in range(E):
+                if e >= len(missing) or not (int(e_rec[g, 0]) >> missing[e]) & 1:
+                    assert out_i[g, e] == 0xFF, (g, e)
+                    continue
+                i = missing[e]
+                want_mask |= 1 << i
+                n_rec += 1
+                assert out_i[g, e] == i, (g, e)
+                assert out_h[g, e] == e_h[g, i], f"group {g} out {e}: header"
+                L = int(e_h[g, i]["size"])
+                assert np.array_equal(out_s[g, e, :L], e_s[g, i, :L]), f"group {g} out {e}: data"
+            assert int(rec[g, 0]) == want_mask and int(rec[g, 1]) == 0, g
+        assert n_rec > G // 4
+
+
+def test_dense_output_rejects_cascading_plans(product):
+    """A plan with columns (recoveries feed each other) is refused before any launch."""
+    plan = product.plan_from_fraction(10, 80, 3)
+    with pytest.raises(Exception):
+        product.recover_batch_out(plan, 1, 1008, 1000, 16, 16, 16, 16, 16, 16, 16, 16, 2, 16, 16, 16, 16)
