@@ -2016,7 +2016,7 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
     const bool dense = out && out->per_group;
     if (dense) // the dense-output forms: fused decodes, header lanes (the host checks the plan is disjoint)
         flags &= ~(RFEC_KFLAG_WAVE_DECODE | RFEC_KFLAG_TWO_KERNEL_DECODE | RFEC_KFLAG_PIPE_DECODE |
-                   RFEC_KFLAG_GROUP_WAVE | RFEC_KFLAG_LDS_HDR_PEEL | RFEC_KFLAG_DIAG_NO_HDR);
+                   RFEC_KFLAG_GROUP_WAVE | RFEC_KFLAG_LDS_HDR_PEEL);
     const bool ntl = !(flags & RFEC_KFLAG_PLAIN_LOADS);
     if (flags & RFEC_KFLAG_WAVE_DECODE) {
         RecArgs A;
