@@ -1342,6 +1342,139 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
     }
 }
 
+// Fused disjoint-plan decode for small slots (CD = 16 or 32 chunks, a group's
+// lanes inside one wave), header work folded into the payload lanes: no
+// header blocks.  Lane (g, j) runs the fired lines two at a time as
+// k_decode_disjoint does; for line b of the pair, lanes j = 5b .. 5b + 4 also
+// take dword j - 5b of its meta and of its present members' header records
+// (the record of the erased member is their XOR), lane 5b + 4 the sizes and
+// the checks of line_headers / peel_block (fec_data_size <= capacity, every
+// present member and the recovered size within fec_data_size).  The verdict
+// reaches the group's other lanes by one ds_bpermute, so every lane keeps the
+// group's recovered mask and lane j == 0 writes it.
+template <int CD, bool WIDE, bool NTL, int NTS>
+__global__ __launch_bounds__(kBlock) void k_decode_small(v4u* shards, const v4u* __restrict__ parity, uint32_t C,
+                                                         PeelArgs A, rfec_kmask M, DenseOut D)
+{
+    static_assert(CD == 16 || CD == 32, "a group's lanes must sit in one wave");
+    constexpr int MAXC = 4;
+    __shared__ uint32_t lplan[RFEC_MAX_LINES];
+    const rfec_kplan& P = M.plan;
+    stage_plan(lplan, P);
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t g = t / CD, j = t % CD;
+    const uint32_t lane = threadIdx.x & (kWave - 1);
+    const uint32_t base = lane - j; // the group's first lane in this wave
+    const bool valid = g < A.groups;
+    const uint32_t gg = valid ? g : 0u;
+    const uint64_t h0 = valid ? A.present[2 * gg] : ~0ull;
+    const uint64_t h1 = valid && WIDE ? A.present[2 * gg + 1] : ~0ull;
+    uint64_t fire = valid ? A.parity_present[gg] : 0ull;
+    {
+        uint64_t f = 0;
+        for (uint32_t l = 0; l < P.n_lines; ++l) {
+            const uint64_t m0 = M.mask[l][0], m1 = WIDE ? M.mask[l][1] : 0ull;
+            const uint64_t x0 = m0 & ~h0, x1 = m1 & ~h1;
+            if (__popcll(x0) + (WIDE ? __popcll(x1) : 0) == 1 && ((m0 & h0) | (m1 & h1)) != 0)
+                f |= 1ull << l;
+        }
+        fire &= f;
+    }
+    v4u* grp = shards + (size_t)gg * P.k * C + j;
+    const v4u* par = parity + (size_t)gg * P.n_lines * C + j;
+    const uint32_t* gh = reinterpret_cast<const uint32_t*>(A.hdr + (size_t)gg * P.k);
+    const uint32_t hb = j / 5, hd = j - 5 * hb; // header lane of pair slot hb, dword hd
+    uint32_t rec[4] = {0, 0, 0, 0};
+    while (fire) { // uniform within the group: all its lanes loop alike
+        v4u acc[2], mv[2][MAXC];
+        uint32_t tg[2], hx[2], L[2], hsz[2];
+        bool on[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            on[b] = fire != 0;
+            const uint32_t l = on[b] ? (uint32_t)__ffsll((long long)fire) - 1 : 0;
+            fire &= fire - 1;
+            const uint32_t ln = lplan[l];
+            const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
+            const bool hl = on[b] && hb == (uint32_t)b; // header lane of this line
+            acc[b] = v4u{0, 0, 0, 0};
+            hx[b] = 0;
+            L[b] = 0;
+            hsz[b] = 0; // max present member size
+            if (on[b]) {
+                acc[b] = ld16<NTL>(par + (size_t)l * C);
+                if (hl) {
+                    hx[b] = reinterpret_cast<const uint32_t*>(A.meta + (size_t)gg * P.n_lines + l)[hd];
+                    if (hd == 4)
+                        L[b] = A.fsize[(size_t)gg * P.n_lines + l];
+                }
+            }
+            tg[b] = first;
+#pragma unroll
+            for (int q = 0; q < MAXC; ++q) {
+                const uint32_t i = first + q * stride;
+                mv[b][q] = v4u{0, 0, 0, 0};
+                if (!on[b] || (uint32_t)q >= count)
+                    continue;
+                if (has_bit(h0, h1, i)) {
+                    mv[b][q] = ld16<NTL>(grp + (size_t)i * C);
+                    if (hl) {
+                        const uint32_t w = gh[i * 5 + hd];
+                        hx[b] ^= w;
+                        hsz[b] = max(hsz[b], w >> 16);
+                    }
+                } else {
+                    tg[b] = i;
+                }
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+#pragma unroll
+            for (int q = 0; q < MAXC; ++q)
+                acc[b] ^= mv[b][q];
+            const uint32_t e = D.E ? missing_rank(h0, h1, tg[b]) : 0u;
+            if (on[b] && (!D.E || e < D.E))
+                st16<NTS>(D.E ? D.sh + ((size_t)gg * D.E + e) * C + j : grp + (size_t)tg[b] * C, acc[b]);
+            // the checks in lane 5b + 4 (sizes in the high half of dword 4), to the group's lanes
+            const uint32_t okv = (hb == (uint32_t)b && hd == 4 && L[b] <= A.capacity && hsz[b] <= L[b] &&
+                                  (hx[b] >> 16) <= L[b]) ? 1u : 0u;
+            const uint32_t ok = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (base + 5u * b + 4u)), (int)okv);
+            if (on[b] && ok && (!D.E || e < D.E)) { // (beyond the dense output: not recovered)
+                rec[tg[b] >> 5] |= 1u << (tg[b] & 31);
+                if (hb == (uint32_t)b) {
+                    uint32_t* ht = D.E ? reinterpret_cast<uint32_t*>(A.out_hdr + (size_t)gg * D.E + e)
+                                       : reinterpret_cast<uint32_t*>(A.hdr + (size_t)gg * P.k + tg[b]);
+                    ht[hd] = hx[b];
+                }
+            }
+        }
+    }
+    if (valid && j == 0) {
+        A.recovered[2 * g] = (uint64_t)rec[1] << 32 | rec[0];
+        A.recovered[2 * g + 1] = (uint64_t)rec[3] << 32 | rec[2];
+        if (D.E) {
+            const uint32_t K = P.k;
+            uint64_t m0 = ~h0 & (K >= 64 ? ~0ull : (1ull << K) - 1ull);
+            uint64_t m1 = K <= 64 ? 0ull : ~h1 & (K >= 128 ? ~0ull : (1ull << (K - 64)) - 1ull);
+            uint8_t* oi = A.out_index + (size_t)g * D.E;
+            for (uint32_t e = 0; e < D.E; ++e) {
+                uint32_t v = 0xFF;
+                if (m0 | m1) {
+                    const uint32_t i = m0 ? (uint32_t)__ffsll((long long)m0) - 1 : 64u + (uint32_t)__ffsll((long long)m1) - 1;
+                    if ((rec[i >> 5] >> (i & 31)) & 1u)
+                        v = i;
+                    if (m0)
+                        m0 &= m0 - 1;
+                    else
+                        m1 &= m1 - 1;
+                }
+                oi[e] = (uint8_t)v;
+            }
+        }
+    }
+}
+
 // Fused disjoint-plan decode, output-mapped (default): one lane per (group,
 // line, chunk column).  A lane whose line does not fire (parity missing, or
 // not exactly one member missing) exits; the others load the parity chunk
@@ -1838,6 +1971,24 @@ void launch_fused_rows(const FusedArgs& F, int sp, const PeelArgs& B, const rfec
 #undef RFEC_FUSED_ROWS
 }
 
+// small-slot fused decode with the header work in the payload lanes (cd = CD)
+template <int CD, bool WIDE>
+void launch_small(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M)
+{
+    const dim3 grid(blocks_for(B.groups * CD)); // groups * CD < 2^31: check_geometry
+#define RFEC_SMALL(NTL, NTS)                                                                                     \
+    hipLaunchKernelGGL((k_decode_small<CD, WIDE, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards, F.parity, \
+                       F.C, B, M, F.D)
+    switch (sp) {
+    case -1: RFEC_SMALL(false, 1); break;
+    case 0: RFEC_SMALL(true, 0); break;
+    case 2: RFEC_SMALL(true, 2); break;
+    case 3: RFEC_SMALL(true, 3); break;
+    default: RFEC_SMALL(true, 1); break;
+    }
+#undef RFEC_SMALL
+}
+
 // sp: store policy, -1 = plain loads + non-temporal stores (A/B only)
 template <int MAXC, int NI>
 void launch_fused(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M)
@@ -2124,6 +2275,18 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
             return (int)hipGetLastError();
         }
         const bool two = (flags & RFEC_KFLAG_ITEMS2) != 0;
+        // slots of 16 or 32 chunks, lines of <= 4: header work in the payload lanes (c5, k = 32 / 256 B:
+        // no header blocks)
+        if (!two && (cd == 16 || cd == 32) && maxc <= 4 &&
+            !(flags & (RFEC_KFLAG_SPLIT_HDR | RFEC_KFLAG_FLAT_DECODE | RFEC_KFLAG_OUT_DECODE | RFEC_KFLAG_LDS_HDR_PEEL |
+                       RFEC_KFLAG_HDR_HEAD | RFEC_KFLAG_DIAG_NO_HDR))) {
+            const bool wide = P.k > 64;
+            if (cd == 16)
+                wide ? launch_small<16, true>(F, sp, B, *M) : launch_small<16, false>(F, sp, B, *M);
+            else
+                wide ? launch_small<32, true>(F, sp, B, *M) : launch_small<32, false>(F, sp, B, *M);
+            return (int)hipGetLastError();
+        }
         // output-mapped (a lane per (group, line, chunk)) where a line's slot spans at least a wave of
         // chunks; below that most of its lanes would sit on lines that do not fire (k = 32 / 256 B, 2
         // erasures: 6 of 8 rows idle, 60.0 vs 41.6 us flat), so the flat form

@@ -20,7 +20,7 @@ TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "plain_stores": 4, "ite
            "generic_plain": 3, "two_kernel": 4096, "two_kernel_wt": 4096 | 64, "group_wave": 8192,
            "group_wave_xcd": 8192 | 16384, "xcd": 16384, "lds_hdr_peel": 32768, "flat_encode": 65536,
            "meta_tail": 131072, "meta_tail_nt": 131072 | 512, "flat_decode": 262144, "hdr_head": 524288,
-           "out_decode": 2097152, "out_decode_head": 2097152 | 524288}
+           "out_decode": 2097152, "out_decode_head": 2097152 | 524288, "split_hdr": 4194304}
 
 
 @pytest.fixture(scope="module")
@@ -360,6 +360,11 @@ def test_full_size_digest_gpu(gpu, oracle1000, name):
     assert fd.digest(gpu().encode, oracle1000, c, chunk=65536) == c["sha256"]
 
 
+def _w(a, g):
+    """A [G][2] u64 mask array's row g as one int (bit i = segment i, k <= 128)."""
+    return int(a[g, 0]) | int(a[g, 1]) << 64
+
+
 def _mask_peel(plan, k, present, pp):
     """Recovered mask of the canonical peel over the masks alone (no header checks)."""
     have = int(present)
@@ -519,8 +524,10 @@ def test_full_plan_shapes_gpu(gpu, oracle1000, k, tuning):
                 assert np.array_equal(out_s[g, i], shards[g, i]), f"k={k} group {g} segment {i}"
 
 
-@pytest.mark.parametrize("k,col,S", [(10, 4, 64), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 1000)])
-@pytest.mark.parametrize("tuning", ["default", "hdr_head", "out_decode", "out_decode_head", "flat_decode", "generic"])
+@pytest.mark.parametrize("k,col,S", [(10, 4, 64), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 1000),
+                                     (96, 4, 512), (20, 3, 256)])
+@pytest.mark.parametrize("tuning", ["default", "hdr_head", "out_decode", "out_decode_head", "flat_decode", "generic",
+                                    "split_hdr"])
 def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tuning):
     """Row plans (disjoint lines: the fused decodes) with up to 6 erasures per
     group, lost parities and corrupted headers (fec_data_size above capacity or
@@ -546,7 +553,7 @@ def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tunin
             m &= ~(1 << int(i))
             rx[g, i] = 0xA5
             rh[g, i] = np.zeros((), po.HDR_DTYPE)
-        present[g, 0] = m
+        present[g, 0], present[g, 1] = m & (2**64 - 1), m >> 64
         if rng.random() < 0.2:
             pp[g] &= ~np.uint64(1 << int(rng.integers(plan.n_lines)))
         r = rng.random()
@@ -562,19 +569,20 @@ def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tunin
     e_s, e_h, e_rec = o.recover_batch(plan, rx, rh, present, parity, meta, fs_rx, pp, cap)
     out_s, out_h, rec = gpu(tuning=TUNINGS[tuning]).recover(plan, rx, rh, present, parity, meta, fs_rx, pp, cap)
     assert np.array_equal(rec, e_rec)
-    assert int(sum(bin(int(x)).count("1") for x in rec[:, 0])) > G // 4
+    assert sum(bin(_w(rec, g)).count("1") for g in range(G)) > G // 4
     for g in range(G):
         for i in range(k):
-            if (int(rec[g, 0]) >> i) & 1:
+            if (_w(rec, g) >> i) & 1:
                 assert out_h[g, i] == e_h[g, i], f"group {g} segment {i}: header"
                 L = int(e_h[g, i]["size"])
                 assert np.array_equal(out_s[g, i, :L], e_s[g, i, :L]), f"group {g} segment {i}: data"
-            elif (int(present[g, 0]) >> i) & 1:
+            elif (_w(present, g) >> i) & 1:
                 assert out_h[g, i] == rh[g, i] and np.array_equal(out_s[g, i], rx[g, i])
 
 
-@pytest.mark.parametrize("k,col,S", [(10, 4, 1200), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 64)])
-@pytest.mark.parametrize("tuning", ["default", "flat_decode", "out_decode", "hdr_head", "generic"])
+@pytest.mark.parametrize("k,col,S", [(10, 4, 1200), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 64),
+                                     (96, 4, 512), (20, 3, 256)])
+@pytest.mark.parametrize("tuning", ["default", "flat_decode", "out_decode", "hdr_head", "generic", "split_hdr"])
 def test_dense_output_decode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning):
     """rfec_recover_batch_out (recovered segments into a dense output, as
     flex_fec_recover's caller-allocated out_seg): row plans with up to 6
@@ -600,7 +608,7 @@ def test_dense_output_decode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning)
             m &= ~(1 << int(i))
             rx[g, i] = 0xA5
             rh[g, i] = np.zeros((), po.HDR_DTYPE)
-        present[g, 0] = m
+        present[g, 0], present[g, 1] = m & (2**64 - 1), m >> 64
         if rng.random() < 0.2:
             pp[g] &= ~np.uint64(1 << int(rng.integers(plan.n_lines)))
         r = rng.random()
@@ -619,10 +627,10 @@ def test_dense_output_decode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning)
                                                                            fs_rx, pp, cap, E)
         n_rec = 0
         for g in range(G):
-            missing = [i for i in range(k) if not (int(present[g, 0]) >> i) & 1]
+            missing = [i for i in range(k) if not (_w(present, g) >> i) & 1]
             want_mask = 0
             for e in range(E):
-                if e >= len(missing) or not (int(e_rec[g, 0]) >> missing[e]) & 1:
+                if e >= len(missing) or not (_w(e_rec, g) >> missing[e]) & 1:
                     assert out_i[g, e] == 0xFF, (g, e)
                     continue
                 i = missing[e]
@@ -632,7 +640,7 @@ def test_dense_output_decode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning)
                 assert out_h[g, e] == e_h[g, i], f"group {g} out {e}: header"
                 L = int(e_h[g, i]["size"])
                 assert np.array_equal(out_s[g, e, :L], e_s[g, i, :L]), f"group {g} out {e}: data"
-            assert int(rec[g, 0]) == want_mask and int(rec[g, 1]) == 0, g
+            assert _w(rec, g) == want_mask, g
         assert n_rec > G // 4
 
 
