@@ -39,6 +39,7 @@ typedef struct {
 #define RFEC_KFLAG_OUT_DECODE RFEC_TUNE_OUT_DECODE
 #define RFEC_KFLAG_DIAG_NO_HDR RFEC_TUNE_DIAG_NO_HDR
 #define RFEC_KFLAG_SPLIT_HDR RFEC_TUNE_SPLIT_HDR
+#define RFEC_KFLAG_SMALL_B2 RFEC_TUNE_SMALL_B2
 
 int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, uint32_t capacity,
                        const uint8_t* shards, const rfec_hdr* hdr, uint8_t* parity, rfec_hdr* meta,

@@ -1122,7 +1122,7 @@ __device__ void line_headers(const PeelArgs& A, const rfec_kmask& M, uint32_t bl
     const uint32_t nlp = 1u << A.nlp_log2;
     const uint32_t hl = blk * kBlock + threadIdx.x;
     const uint32_t g = hl >> A.nlp_log2, l = hl & (nlp - 1);
-    uint32_t rec[4] = {0, 0, 0, 0};
+    uint64_t rec0 = 0, rec1 = 0; // recovered mask (no dynamic register index: no scratch)
     if (g < A.groups && l < P.n_lines && ((A.parity_present[g] >> l) & 1ull)) {
         const uint64_t h0 = A.present[2 * g], h1 = A.present[2 * g + 1];
         const uint64_t m0 = lmask[l][0], m1 = lmask[l][1];
@@ -1172,18 +1172,21 @@ __device__ void line_headers(const PeelArgs& A, const rfec_kmask& M, uint32_t bl
                 }
                 if (ht) {
                     ht[0] = r0, ht[1] = r1, ht[2] = r2, ht[3] = r3, ht[4] = r4;
-                    rec[t >> 5] = 1u << (t & 31);
+                    if (t < 64)
+                        rec0 = 1ull << t;
+                    else
+                        rec1 = 1ull << (t - 64);
                 }
             }
         }
     }
-    for (uint32_t sh = 1; sh < nlp; sh <<= 1)
-#pragma unroll
-        for (int w = 0; w < 4; ++w)
-            rec[w] |= __shfl_xor(rec[w], sh);
+    for (uint32_t sh = 1; sh < nlp; sh <<= 1) {
+        rec0 |= __shfl_xor(rec0, sh);
+        rec1 |= __shfl_xor(rec1, sh);
+    }
     if (g < A.groups && l == 0) {
-        A.recovered[2 * g] = (uint64_t)rec[1] << 32 | rec[0];
-        A.recovered[2 * g + 1] = (uint64_t)rec[3] << 32 | rec[2];
+        A.recovered[2 * g] = rec0;
+        A.recovered[2 * g + 1] = rec1;
         if (A.out_per_group) {
             // out_index: the e-th erased segment's index where it was recovered, else 0xFF
             const uint32_t K = P.k;
@@ -1194,7 +1197,7 @@ __device__ void line_headers(const PeelArgs& A, const rfec_kmask& M, uint32_t bl
                 uint32_t v = 0xFF;
                 if (m0 | m1) {
                     const uint32_t i = m0 ? (uint32_t)__ffsll((long long)m0) - 1 : 64u + (uint32_t)__ffsll((long long)m1) - 1;
-                    if ((rec[i >> 5] >> (i & 31)) & 1u)
+                    if (has_bit(rec0, rec1, i))
                         v = i;
                     if (m0)
                         m0 &= m0 - 1;
@@ -1352,7 +1355,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
 // present member and the recovered size within fec_data_size).  The verdict
 // reaches the group's other lanes by one ds_bpermute, so every lane keeps the
 // group's recovered mask and lane j == 0 writes it.
-template <int CD, bool WIDE, bool NTL, int NTS>
+template <int CD, int BATCH, bool WIDE, bool NTL, int NTS>
 __global__ __launch_bounds__(kBlock) void k_decode_small(v4u* shards, const v4u* __restrict__ parity, uint32_t C,
                                                          PeelArgs A, rfec_kmask M, DenseOut D)
 {
@@ -1384,13 +1387,13 @@ __global__ __launch_bounds__(kBlock) void k_decode_small(v4u* shards, const v4u*
     const v4u* par = parity + (size_t)gg * P.n_lines * C + j;
     const uint32_t* gh = reinterpret_cast<const uint32_t*>(A.hdr + (size_t)gg * P.k);
     const uint32_t hb = j / 5, hd = j - 5 * hb; // header lane of pair slot hb, dword hd
-    uint32_t rec[4] = {0, 0, 0, 0};
+    uint64_t rec0 = 0, rec1 = 0;
     while (fire) { // uniform within the group: all its lanes loop alike
-        v4u acc[2], mv[2][MAXC];
-        uint32_t tg[2], hx[2], L[2], hsz[2];
-        bool on[2];
+        v4u acc[BATCH], mv[BATCH][MAXC];
+        uint32_t tg[BATCH], hx[BATCH], L[BATCH], hsz[BATCH];
+        bool on[BATCH];
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
+        for (int b = 0; b < BATCH; ++b) {
             on[b] = fire != 0;
             const uint32_t l = on[b] ? (uint32_t)__ffsll((long long)fire) - 1 : 0;
             fire &= fire - 1;
@@ -1429,7 +1432,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_small(v4u* shards, const v4u*
             }
         }
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
+        for (int b = 0; b < BATCH; ++b) {
 #pragma unroll
             for (int q = 0; q < MAXC; ++q)
                 acc[b] ^= mv[b][q];
@@ -1441,7 +1444,10 @@ __global__ __launch_bounds__(kBlock) void k_decode_small(v4u* shards, const v4u*
                                   (hx[b] >> 16) <= L[b]) ? 1u : 0u;
             const uint32_t ok = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (base + 5u * b + 4u)), (int)okv);
             if (on[b] && ok && (!D.E || e < D.E)) { // (beyond the dense output: not recovered)
-                rec[tg[b] >> 5] |= 1u << (tg[b] & 31);
+                if (tg[b] < 64)
+                    rec0 |= 1ull << tg[b];
+                else
+                    rec1 |= 1ull << (tg[b] - 64);
                 if (hb == (uint32_t)b) {
                     uint32_t* ht = D.E ? reinterpret_cast<uint32_t*>(A.out_hdr + (size_t)gg * D.E + e)
                                        : reinterpret_cast<uint32_t*>(A.hdr + (size_t)gg * P.k + tg[b]);
@@ -1451,8 +1457,8 @@ __global__ __launch_bounds__(kBlock) void k_decode_small(v4u* shards, const v4u*
         }
     }
     if (valid && j == 0) {
-        A.recovered[2 * g] = (uint64_t)rec[1] << 32 | rec[0];
-        A.recovered[2 * g + 1] = (uint64_t)rec[3] << 32 | rec[2];
+        A.recovered[2 * g] = rec0;
+        A.recovered[2 * g + 1] = rec1;
         if (D.E) {
             const uint32_t K = P.k;
             uint64_t m0 = ~h0 & (K >= 64 ? ~0ull : (1ull << K) - 1ull);
@@ -1462,7 +1468,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_small(v4u* shards, const v4u*
                 uint32_t v = 0xFF;
                 if (m0 | m1) {
                     const uint32_t i = m0 ? (uint32_t)__ffsll((long long)m0) - 1 : 64u + (uint32_t)__ffsll((long long)m1) - 1;
-                    if ((rec[i >> 5] >> (i & 31)) & 1u)
+                    if (has_bit(rec0, rec1, i))
                         v = i;
                     if (m0)
                         m0 &= m0 - 1;
@@ -1972,13 +1978,13 @@ void launch_fused_rows(const FusedArgs& F, int sp, const PeelArgs& B, const rfec
 }
 
 // small-slot fused decode with the header work in the payload lanes (cd = CD)
-template <int CD, bool WIDE>
+template <int CD, int BATCH, bool WIDE>
 void launch_small(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M)
 {
     const dim3 grid(blocks_for(B.groups * CD)); // groups * CD < 2^31: check_geometry
 #define RFEC_SMALL(NTL, NTS)                                                                                     \
-    hipLaunchKernelGGL((k_decode_small<CD, WIDE, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards, F.parity, \
-                       F.C, B, M, F.D)
+    hipLaunchKernelGGL((k_decode_small<CD, BATCH, WIDE, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards,    \
+                       F.parity, F.C, B, M, F.D)
     switch (sp) {
     case -1: RFEC_SMALL(false, 1); break;
     case 0: RFEC_SMALL(true, 0); break;
@@ -2280,11 +2286,13 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
         if (!two && (cd == 16 || cd == 32) && maxc <= 4 &&
             !(flags & (RFEC_KFLAG_SPLIT_HDR | RFEC_KFLAG_FLAT_DECODE | RFEC_KFLAG_OUT_DECODE | RFEC_KFLAG_LDS_HDR_PEEL |
                        RFEC_KFLAG_HDR_HEAD | RFEC_KFLAG_DIAG_NO_HDR))) {
-            const bool wide = P.k > 64;
-            if (cd == 16)
-                wide ? launch_small<16, true>(F, sp, B, *M) : launch_small<16, false>(F, sp, B, *M);
+            const bool wide = P.k > 64, b2 = (flags & RFEC_KFLAG_SMALL_B2) != 0;
+            if (cd == 16 && !b2)
+                wide ? launch_small<16, 1, true>(F, sp, B, *M) : launch_small<16, 1, false>(F, sp, B, *M);
+            else if (cd == 16)
+                wide ? launch_small<16, 2, true>(F, sp, B, *M) : launch_small<16, 2, false>(F, sp, B, *M);
             else
-                wide ? launch_small<32, true>(F, sp, B, *M) : launch_small<32, false>(F, sp, B, *M);
+                wide ? launch_small<32, 1, true>(F, sp, B, *M) : launch_small<32, 1, false>(F, sp, B, *M);
             return (int)hipGetLastError();
         }
         // output-mapped (a lane per (group, line, chunk)) where a line's slot spans at least a wave of
