@@ -1612,6 +1612,7 @@ static void hm_del(hmap* m, uint32_t k) /* backward-shift deletion */
 
 typedef struct {
     uint32_t count, row, col, n_groups, n_lines, row0, prow0, group0;
+    uint64_t xcol[2];     /* columns c >= col a peer's parities named (bit c) */
     int16_t line_of[256]; /* FEC index -> plan line, -1: none */
     rfec_plan plan;
 } rx_shape;
@@ -1796,34 +1797,134 @@ static void rx_put_segment(rx_sim* X, const rfec_hdr* h, uint16_t fec_id, uint32
         rx_remove(X, fi - 1);
 }
 
-static uint32_t rx_shape_of(rx_sim* X, uint32_t count, uint32_t row, uint32_t col)
+/* members of the reference's line `index` of a (count, row, col) flex:
+ * flex_recover_row walks i < col, flex_recover_col i < row, both stopping at
+ * the first position >= count (flex_fec_receiver.c:118-126, 175-183) */
+static uint32_t rx_line_members(uint32_t count, uint32_t row, uint32_t col, uint32_t index, uint32_t* first,
+                                uint32_t* stride)
 {
-    if (count > RFEC_MAX_K || row * col < count || row > 255 || col > 255)
+    const uint32_t x = index & 0x7Fu;
+    uint32_t n = 0;
+    if (index & 0x80u) {
+        while (n < row && n * col + x < count)
+            ++n;
+        *first = x;
+        *stride = col;
+    } else {
+        while (n < col && x * col + n < count)
+            ++n;
+        *first = x * col;
+        *stride = 1;
+    }
+    return n;
+}
+
+/* The device plan of a flex geometry: every row with 2+ members (also rows
+ * at and beyond `row` when row * col < count: the reference bounds rows by
+ * count only), every column c < col with 2+ members, and the extra columns
+ * c >= col of xcol.  Lines of fewer than 2 members can never recover (one
+ * missing member leaves none present).  Standard geometry (row * col >=
+ * count, no extra columns) is exactly rfec_plan_matrix's plan. */
+static int rx_build_plan(uint32_t count, uint32_t row, uint32_t col, const uint64_t* xcol, rfec_plan* p)
+{
+    if (row * col >= count && !xcol[0] && !xcol[1])
+        return rfec_plan_matrix((uint16_t)count, (uint8_t)row, (uint8_t)col, RFEC_LAYER_ROWS | RFEC_LAYER_COLS, p);
+    memset(p, 0, sizeof(*p));
+    p->k = (uint16_t)count;
+    p->row = (uint8_t)row;
+    p->col = (uint8_t)col;
+    p->rc = 1;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (uint32_t x = 0; x < 128; ++x) {
+            if (pass == 1 && x >= col && !((xcol[x >> 6] >> (x & 63)) & 1ull))
+                continue;
+            uint32_t first, stride;
+            const uint32_t n = rx_line_members(count, row, col, pass ? (0x80u | x) : x, &first, &stride);
+            if (n < 2)
+                continue;
+            if (p->n_lines >= RFEC_MAX_LINES)
+                return RFEC_EINVAL;
+            rfec_line* l = &p->line[p->n_lines++];
+            l->first = (uint8_t)first;
+            l->stride = (uint8_t)stride;
+            l->count = (uint8_t)n;
+            l->index = (uint8_t)(pass ? (0x80u | x) : x);
+        }
+        if (pass == 0)
+            p->n_row_lines = p->n_lines;
+    }
+    return RFEC_OK;
+}
+
+static uint32_t rx_shape_of(rx_sim* X, uint32_t count, uint32_t row, uint32_t col, const uint64_t* xcol)
+{
+    if (count > RFEC_MAX_K || row > 255 || col > 255)
         return UINT32_MAX;
+    const int extended = xcol[0] || xcol[1];
     const uint32_t key = count << 16 | row << 8 | col;
-    const uint32_t s = hm_get(&X->shape_of, key);
-    if (s)
-        return s - 1;
+    if (!extended) {
+        const uint32_t s = hm_get(&X->shape_of, key);
+        if (s)
+            return s - 1;
+    } else { /* rare (a peer's extra columns): a scan */
+        for (uint32_t s = 0; s < X->ns; ++s)
+            if (X->S[s].count == count && X->S[s].row == row && X->S[s].col == col && X->S[s].xcol[0] == xcol[0] &&
+                X->S[s].xcol[1] == xcol[1])
+                return s;
+    }
     RX_GROW(X->S, X->ns, X->scap, 1, rx_shape);
     if (X->oom)
         return UINT32_MAX;
     rx_shape* sh = &X->S[X->ns];
     memset(sh, 0, sizeof(*sh));
-    if (rfec_plan_matrix((uint16_t)count, (uint8_t)row, (uint8_t)col, RFEC_LAYER_ROWS | RFEC_LAYER_COLS, &sh->plan))
+    if (rx_build_plan(count, row, col, xcol, &sh->plan))
         return UINT32_MAX;
     sh->count = count;
     sh->row = row;
     sh->col = col;
+    sh->xcol[0] = xcol[0];
+    sh->xcol[1] = xcol[1];
     sh->n_lines = sh->plan.n_lines;
     for (int i = 0; i < 256; ++i)
         sh->line_of[i] = -1;
     for (uint32_t l = 0; l < sh->n_lines; ++l)
         sh->line_of[sh->plan.line[l].index] = (int16_t)l;
-    if (hm_put(&X->shape_of, key, X->ns + 1)) {
+    if (!extended && hm_put(&X->shape_of, key, X->ns + 1)) {
         X->oom = 1;
         return UINT32_MAX;
     }
     return X->ns++;
+}
+
+/* A parity for a column c >= col of flex ii (a peer's plan, not razor's
+ * sender): the flex moves to the shape with that column added, its
+ * registered parities carried over by index.  Returns the column's line in
+ * the new shape, or -1 (no room: the parity stays unmodelled). */
+static int rx_extend(rx_sim* X, uint32_t ii, uint32_t c)
+{
+    rx_inst* g = &X->G[ii];
+    uint64_t xcol[2] = {X->S[g->shape].xcol[0], X->S[g->shape].xcol[1]};
+    xcol[c >> 6] |= 1ull << (c & 63);
+    const uint32_t ns = rx_shape_of(X, g->count, g->row, g->col, xcol);
+    if (ns == UINT32_MAX)
+        return -1;
+    const rx_shape* nsh = &X->S[ns]; /* (X->S may have moved) */
+    const rx_shape* osh = &X->S[g->shape];
+    RX_GROW(X->line_par, X->nline, X->linecap, nsh->n_lines, int32_t);
+    if (X->oom)
+        return -1;
+    uint64_t ppm = 0;
+    for (uint32_t l = 0; l < nsh->n_lines; ++l) {
+        const int ol = osh->line_of[nsh->plan.line[l].index];
+        X->line_par[X->nline + l] = ol >= 0 ? X->line_par[g->line0 + ol] : -1;
+        if (ol >= 0 && ((g->ppm >> ol) & 1ull))
+            ppm |= 1ull << l;
+    }
+    g->line0 = X->nline;
+    X->nline += nsh->n_lines;
+    g->ppm = ppm;
+    g->shape = ns;
+    return nsh->line_of[0x80u | c];
 }
 
 /* sim_fec_put_fec_packet (sim_fec.c:141-169) -> flex_fec_receiver_on_fec (flex_fec_receiver.c:208-241) */
@@ -1848,7 +1949,8 @@ static void rx_put_fec(rx_sim* X, uint32_t a)
         g->col = f->col;
         g->fec_ts = f->send_ts;
         g->ref_ok = g->col >= 2 && g->row >= 1 && g->count >= 1;
-        g->shape = g->ref_ok ? rx_shape_of(X, g->count, g->row, g->col) : UINT32_MAX;
+        static const uint64_t no_xcol[2] = {0, 0};
+        g->shape = g->ref_ok ? rx_shape_of(X, g->count, g->row, g->col, no_xcol) : UINT32_MAX;
         if (g->shape != UINT32_MAX) {
             rx_shape* sh = &X->S[g->shape];
             g->gslot = sh->n_groups++;
@@ -1888,10 +1990,17 @@ static void rx_put_fec(rx_sim* X, uint32_t a)
     rx_inst* g = &X->G[fi - 1];
     if (!g->ref_ok || g->shape == UINT32_MAX)
         return;
-    const int l = X->S[g->shape].line_of[f->index];
+    int l = X->S[g->shape].line_of[f->index];
     if (l < 0) {
-        X->unmodelled++; /* a line the sender's plan does not have */
-        return;
+        uint32_t first, stride;
+        if (rx_line_members(g->count, g->row, g->col, f->index, &first, &stride) < 2)
+            return; /* a line that can never recover (flex_fec_receiver.c:133-134, 189-190) */
+        /* a column c >= col (razor's sender never emits one; a peer may) */
+        if ((l = rx_extend(X, fi - 1, f->index & 0x7Fu)) < 0) {
+            X->unmodelled++;
+            return;
+        }
+        g = &X->G[fi - 1];
     }
     if ((g->ppm >> l) & 1ull)
         return;

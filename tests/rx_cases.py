@@ -21,3 +21,98 @@ def got_rows(out, pay):
                      int(h["payload_type"]), n, int(o["fec_id"]), f"{po.fnv1a(p[:n].tobytes()):016x}"))
         assert not p[n:].any()
     return rows
+
+
+def _peer_plan(k, row, col, xcols):
+    """The lines the reference receiver walks for a (count = k, row, col) flex
+    (flex_fec_receiver.c:118-126 rows of col, :175-183 columns of row, both
+    cut at count): every row, the columns c < col, and the extra columns
+    `xcols` (c >= col); lines of fewer than 2 members dropped."""
+    p = po.rfec_plan()
+    p.k, p.row, p.col, p.rc = k, row, col, 1
+    lines = []
+    r = 0
+    while r * col < k:
+        n = min(col, k - r * col)
+        if n >= 2:
+            lines.append((r * col, 1, n, r))
+        r += 1
+    for c in list(range(col)) + sorted(xcols):
+        n = 0
+        while n < row and n * col + c < k:
+            n += 1
+        if n >= 2:
+            lines.append((c, col, n, 0x80 | c))
+    assert len(lines) <= 64
+    for i, (f, s, n, idx) in enumerate(lines):
+        p.line[i].first, p.line[i].stride, p.line[i].count, p.line[i].index = f, s, n, idx
+    p.n_lines = len(lines)
+    p.n_row_lines = sum(1 for ln in lines if ln[3] < 0x80)
+    return p
+
+
+def peer_stream(oracle, rng, n_groups=90, video_size=1000):
+    """Parsed-datagram records + payload rows of FEC groups in geometries
+    razor's own sender never emits but a peer may: parities of columns
+    c >= col, and row * col < count (members past the matrix, reachable by
+    rows only).  Per group its datagrams arrive shuffled, 15% of the segments
+    and 10% of the parities lost."""
+    stride = (video_size + 15) // 16 * 16
+    recs, pays = [], []
+    pid, ts = 1, 0
+    for g in range(n_groups):
+        kind = g % 3
+        if kind == 0:  # extra columns
+            col = int(rng.integers(3, 7))
+            k = int(rng.integers(col + 2, 40))
+            row = -(-k // col)
+            xc = [c for c in range(col, min(k, 100)) if rng.random() < 0.3][:12]
+        elif kind == 1:  # rows past the matrix
+            col = int(rng.integers(2, 6))
+            row = int(rng.integers(1, 4))
+            k = row * col + int(rng.integers(1, 2 * col + 1))
+            xc = [c for c in range(col, min(k, 100)) if rng.random() < 0.2][:6]
+        else:  # razor's own geometry
+            col = int(rng.integers(3, 6))
+            k = int(rng.integers(6, 30))
+            row = -(-k // col)
+            xc = []
+        plan = _peer_plan(k, row, col, xc)
+        hdr = np.zeros((1, k), po.HDR_DTYPE)
+        hdr["seq"] = pid + np.arange(k)
+        hdr["fid"] = 1 + g
+        hdr["ts"] = ts
+        hdr["index"] = np.arange(k)
+        hdr["total"] = k
+        hdr["payload_type"] = 96
+        hdr["size"] = rng.integers(1, video_size + 1, k)
+        sh = np.zeros((1, k, stride), np.uint8)
+        for i in range(k):
+            sh[0, i, :int(hdr["size"][0, i])] = rng.integers(0, 256, int(hdr["size"][0, i]), dtype=np.uint8)
+        par, meta, fs, st = oracle.encode_batch(plan, sh, hdr, video_size)
+        items = []
+        for i in range(k):
+            if rng.random() < 0.15:
+                continue
+            r = np.zeros((), po.WIRE_REC)
+            r["mid"], r["ver"], r["remb"] = 0x17, 1, 0xFF
+            r["hdr"] = hdr[0, i]
+            r["fec_id"], r["data_size"] = 1 + g, hdr["size"][0, i]
+            items.append((r, sh[0, i]))
+        for l in range(plan.n_lines):
+            if rng.random() < 0.10 or st[0, l] != 0:
+                continue
+            r = np.zeros((), po.WIRE_REC)
+            r["mid"], r["ver"] = 0x1C, 1
+            r["fec_id"], r["base_id"], r["count"] = 1 + g, pid, k
+            r["row"], r["col"], r["index"] = row, col, plan.line[l].index
+            r["send_ts"] = ts
+            r["hdr"] = meta[0, l]
+            r["data_size"] = fs[0, l]
+            items.append((r, par[0, l]))
+        for j in rng.permutation(len(items)):
+            recs.append(items[j][0])
+            pays.append(items[j][1])
+        pid += k
+        ts += 33
+    return np.array(recs, po.WIRE_REC), np.array(pays, np.uint8)

@@ -120,6 +120,16 @@ for seed, args in enumerate([(600, (10,), (80,), 0.12, 40, 0.04, 0.0),
 assert total > 100, total
 print("synthetic ok", total)
 
+# 2b. a peer's geometries razor's sender never emits (columns c >= col, rows
+#     past row * col): modelled like the reference receiver, none unmodelled
+import rx_cases as rc0
+npeer = 0
+for seed in range(3):
+    recs, pay = rc0.peer_stream(o, np.random.default_rng(40 + seed))
+    npeer += check(recs, pay)
+assert npeer > 300, npeer
+print("peer geometry ok", npeer)
+
 # 3. across calls: max_ts carries in, old parities are dropped
 recs, pay = stream(9, 200, (10,), (80,), 0.1, 10, 0.0, 0.0)
 _, _, m1, _ = rx(recs, pay)

@@ -331,3 +331,33 @@ def test_recv_datagrams_wide_slots(oracle1000, long_junk):
     assert len(out) == len(eo) and len(out) > 0
     assert np.array_equal(out["hdr"], eo["hdr"][idx]) and np.array_equal(outp, eop[idx])
     assert mts == emts
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_rx_peer_geometry(lib, oracle1000, seed):
+    """Groups a peer may send that razor's own sender never does (parities of
+    columns c >= col; row * col < count, members past the matrix): the batched
+    receiver models them as the reference flex receiver does (it takes row,
+    col, count and index straight from the parity, flex_fec_receiver.c:69-88,
+    105-206) and delivers exactly the oracle's segments, bytes included;
+    nothing is left unmodelled.  Then the same stream pushed into a session in
+    random batches."""
+    recs, pay = rc.peer_stream(oracle1000, np.random.default_rng(70 + seed))
+    out, outp, max_ts, rep = _rx(lib, recs, pay)
+    eo, ep, emts, edrop = oracle1000.rx_recover(recs, pay, 1000)
+    assert rep.n_unmodelled == 0 and len(eo) > 100
+    assert _sorted(rc.got_rows(out, outp)) == _sorted(rc.got_rows(eo, ep))
+    assert max_ts == emts
+    sess = lib.rx_session(pay.shape[1], 1000)
+    rng = np.random.default_rng(seed)
+    a, rows = 0, []
+    while a < len(recs):
+        b = min(len(recs), a + int(rng.integers(1, 400)))
+        dr, dp = _dev(recs[a:b]), _dev(pay[a:b])
+        torch.cuda.synchronize()
+        o, op, r = sess.push(b - a, dr.data_ptr(), dp.data_ptr())
+        rows += rc.got_rows(o, op)
+        assert r.n_unmodelled == 0
+        a = b
+    sess.close()
+    assert _sorted(rows) == _sorted(rc.got_rows(eo, ep))
