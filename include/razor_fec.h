@@ -595,8 +595,8 @@ int rfec_rx_session_get_info(const rfec_rx_session* s, rfec_rx_session_info* inf
 #define RFEC_TUNE_META_TAIL 131072u   /* encode: header (meta) blocks at the tail of the grid instead of its head */
 #define RFEC_TUNE_HDR_HEAD 524288u    /* fused decodes: header blocks at the head of the grid (default: spread over it) */
 #define RFEC_TUNE_OUT_DECODE 2097152u  /* disjoint-plan decode: output-mapped also for slots under 64 chunks */
-#define RFEC_TUNE_SPLIT_HDR 4194304u   /* small-slot disjoint decode (16 / 32 chunks): header blocks, not header work in the payload lanes */
-#define RFEC_TUNE_SMALL_B2 8388608u    /* small-slot disjoint decode: two fired lines per lane and pass (16-chunk slots) */
+#define RFEC_TUNE_SMALL_FUSED 4194304u /* small-slot disjoint decode (16 / 32 chunks): header checks in the payload lanes (k_decode_small), no header blocks */
+#define RFEC_TUNE_SMALL_B2 8388608u    /* with RFEC_TUNE_SMALL_FUSED: two fired lines per lane and pass (16-chunk slots) */
 #define RFEC_TUNE_FLAT_DECODE 262144u /* disjoint-plan decode: one lane per (group, chunk column), every fired line (default: one lane per (group, line, chunk)) */
 /* (defaults: parity stores write-through, recovered stores non-temporal) */
 #define RFEC_TUNE_DIAG_NO_META 256u /* DIAGNOSTIC ONLY: skip fec_meta (wrong output) */

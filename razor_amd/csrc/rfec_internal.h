@@ -38,7 +38,7 @@ typedef struct {
 #define RFEC_KFLAG_HDR_HEAD RFEC_TUNE_HDR_HEAD
 #define RFEC_KFLAG_OUT_DECODE RFEC_TUNE_OUT_DECODE
 #define RFEC_KFLAG_DIAG_NO_HDR RFEC_TUNE_DIAG_NO_HDR
-#define RFEC_KFLAG_SPLIT_HDR RFEC_TUNE_SPLIT_HDR
+#define RFEC_KFLAG_SMALL_FUSED RFEC_TUNE_SMALL_FUSED
 #define RFEC_KFLAG_SMALL_B2 RFEC_TUNE_SMALL_B2
 
 int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, uint32_t capacity,

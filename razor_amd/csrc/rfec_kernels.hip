@@ -2281,11 +2281,10 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
             return (int)hipGetLastError();
         }
         const bool two = (flags & RFEC_KFLAG_ITEMS2) != 0;
-        // slots of 16 or 32 chunks, lines of <= 4: header work in the payload lanes (c5, k = 32 / 256 B:
-        // no header blocks)
-        if (!two && (cd == 16 || cd == 32) && maxc <= 4 &&
-            !(flags & (RFEC_KFLAG_SPLIT_HDR | RFEC_KFLAG_FLAT_DECODE | RFEC_KFLAG_OUT_DECODE | RFEC_KFLAG_LDS_HDR_PEEL |
-                       RFEC_KFLAG_HDR_HEAD | RFEC_KFLAG_DIAG_NO_HDR))) {
+        // A/B: slots of 16 or 32 chunks, lines of <= 4, header work in the payload lanes (k_decode_small).
+        // Slower than header blocks + the flat lanes at c5 (k = 32 / 256 B, cold parity, tools/gpu_v4.sh:
+        // 40.8 us one line per pass, 48.1 us two, vs 35.9 us), so not the default.
+        if ((flags & RFEC_KFLAG_SMALL_FUSED) && !two && (cd == 16 || cd == 32) && maxc <= 4) {
             const bool wide = P.k > 64, b2 = (flags & RFEC_KFLAG_SMALL_B2) != 0;
             if (cd == 16 && !b2)
                 wide ? launch_small<16, 1, true>(F, sp, B, *M) : launch_small<16, 1, false>(F, sp, B, *M);

@@ -20,7 +20,7 @@ TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "plain_stores": 4, "ite
            "generic_plain": 3, "two_kernel": 4096, "two_kernel_wt": 4096 | 64, "group_wave": 8192,
            "group_wave_xcd": 8192 | 16384, "xcd": 16384, "lds_hdr_peel": 32768, "flat_encode": 65536,
            "meta_tail": 131072, "meta_tail_nt": 131072 | 512, "flat_decode": 262144, "hdr_head": 524288,
-           "out_decode": 2097152, "out_decode_head": 2097152 | 524288, "split_hdr": 4194304, "small_b2": 8388608}
+           "out_decode": 2097152, "out_decode_head": 2097152 | 524288, "small_fused": 4194304, "small_b2": 4194304 | 8388608}
 
 
 @pytest.fixture(scope="module")
@@ -527,7 +527,7 @@ def test_full_plan_shapes_gpu(gpu, oracle1000, k, tuning):
 @pytest.mark.parametrize("k,col,S", [(10, 4, 64), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 1000),
                                      (96, 4, 512), (20, 3, 256)])
 @pytest.mark.parametrize("tuning", ["default", "hdr_head", "out_decode", "out_decode_head", "flat_decode", "generic",
-                                    "split_hdr", "small_b2"])
+                                    "small_fused", "small_b2"])
 def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tuning):
     """Row plans (disjoint lines: the fused decodes) with up to 6 erasures per
     group, lost parities and corrupted headers (fec_data_size above capacity or
@@ -582,7 +582,7 @@ def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tunin
 
 @pytest.mark.parametrize("k,col,S", [(10, 4, 1200), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 64),
                                      (96, 4, 512), (20, 3, 256)])
-@pytest.mark.parametrize("tuning", ["default", "flat_decode", "out_decode", "hdr_head", "generic", "split_hdr",
+@pytest.mark.parametrize("tuning", ["default", "flat_decode", "out_decode", "hdr_head", "generic", "small_fused",
                                     "small_b2"])
 def test_dense_output_decode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning):
     """rfec_recover_batch_out (recovered segments into a dense output, as
