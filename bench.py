@@ -214,14 +214,14 @@ class Workload:
         return bool(ok)
 
     def digest(self, chunk=65536):
-        """SHA-256 of the encode outputs group by group, parity[n][stride] |
+        """SHA-256 of the encode outputs group by group, parity[n][S] |
         meta[n] (20 B) | fec_data_size[n] (u16 LE): the record
         oracle/gen_full.c digests from the reference's flex_fec_generate."""
         h = hashlib.sha256()
         for g0 in range(0, self.G, chunk):
             g1 = min(self.G, g0 + chunk)
             n = g1 - g0
-            rec = torch.cat([self.parity[g0:g1].reshape(n, -1), self.meta[g0:g1].reshape(n, -1),
+            rec = torch.cat([self.parity[g0:g1, :, :self.S].reshape(n, -1), self.meta[g0:g1].reshape(n, -1),
                              self.fsize[g0:g1].view(torch.uint8).reshape(n, -1)], dim=1)
             h.update(rec.cpu().numpy().tobytes())
         return h.hexdigest()
