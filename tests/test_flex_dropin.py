@@ -52,15 +52,19 @@ class flex_fec_sender_t(C.Structure):  # flex_fec_sender.h:7-24
 
 
 def list_pop(lst: base_list_t):
-    u = lst.head
-    if not u:
+    """list_pop (common/cf_list.c): the head unit's data; the unit is freed.
+    (A POINTER field read from a ctypes Structure aliases the field, so the
+    unit's address is taken as an integer before the head moves.)"""
+    addr = C.cast(lst.head, C.c_void_p).value
+    if not addr:
         return None
-    d = u.contents.pdata
-    lst.head = u.contents.next
-    if not lst.head:
+    u = base_list_unit_t.from_address(addr)
+    d, nxt = u.pdata, C.cast(u.next, C.c_void_p).value
+    lst.head = C.cast(nxt, C.POINTER(base_list_unit_t)) if nxt else None
+    if not nxt:
         lst.tailer = None
     lst.size -= 1
-    libc.free(C.cast(u, C.c_void_p))
+    libc.free(addr)
     return d
 
 
