@@ -412,7 +412,7 @@ __global__ __launch_bounds__(kBlock) void k_encode_rows(const v4u* __restrict__ 
 template <int K, int COL, bool NTL, int NTS>
 __global__ __launch_bounds__(kBlock) void k_encode_out(const v4u* __restrict__ shards, v4u* __restrict__ parity,
                                                        uint32_t total, uint32_t C, FastDiv divC, FastDiv divRC,
-                                                       uint32_t meta_first, EncMeta E, rfec_kplan P)
+                                                       uint32_t meta_first, uint32_t swz_head, EncMeta E, rfec_kplan P)
 {
     const uint32_t mb = blockIdx.x - meta_first; // meta_first: 0 (head) or the payload block count (tail)
     if (mb < E.n_meta_blocks) {
@@ -421,7 +421,12 @@ __global__ __launch_bounds__(kBlock) void k_encode_out(const v4u* __restrict__ s
     }
     constexpr int R = (K + COL - 1) / COL;
     constexpr int LAST = K - (R - 1) * COL;
-    const uint32_t b = meta_first ? blockIdx.x : blockIdx.x - E.n_meta_blocks;
+    uint32_t b = meta_first ? blockIdx.x : blockIdx.x - E.n_meta_blocks;
+    if (swz_head) { // XCD swizzle (A/B): swz_head = meta + padding blocks, a multiple of 8
+        if (blockIdx.x < swz_head)
+            return;
+        b = xcd_block(blockIdx.x - swz_head, gridDim.x - swz_head, 1);
+    }
     const uint32_t t = b * kBlock + threadIdx.x;
     if (t >= total)
         return;
@@ -1555,11 +1560,18 @@ template <int K, int COL, bool NTL, int NTS>
 __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* __restrict__ parity, uint32_t total,
                                                         uint32_t C, FastDiv divC, FastDiv divRC,
                                                         uint32_t n_hdr_blocks, uint32_t hdr_every, PeelArgs A,
-                                                        rfec_kmask M, DenseOut D)
+                                                        rfec_kmask M, DenseOut D, uint32_t swz_head)
 {
     static_assert(K <= 64, "row decode keeps the present mask in one word");
     uint32_t hb, pb;
-    if (header_block(n_hdr_blocks, hdr_every, &hb, &pb)) {
+    if (swz_head) { // XCD swizzle (A/B): header blocks first, padded to a multiple of 8 (swz_head)
+        if (blockIdx.x < swz_head) {
+            if (blockIdx.x < n_hdr_blocks)
+                run_header_block(A, M, blockIdx.x);
+            return;
+        }
+        pb = xcd_block(blockIdx.x - swz_head, gridDim.x - swz_head, 1);
+    } else if (header_block(n_hdr_blocks, hdr_every, &hb, &pb)) {
         run_header_block(A, M, hb);
         return;
     }
@@ -1793,9 +1805,13 @@ hipError_t launch_rows_out(const EncLaunch& a, unsigned flags)
     const uint32_t C = a.stride / 16;
     const uint64_t total = (uint64_t)a.groups * R * a.cd;
     const uint32_t nb = blocks_for(total);
-    const uint32_t meta_first = (flags & RFEC_KFLAG_META_TAIL) ? nb : 0u;
-    hipLaunchKernelGGL((k_encode_out<K, COL, NTL, NTS>), dim3(a.E.n_meta_blocks + nb), dim3(kBlock), 0, a.stream, a.s,
-                       a.p, (uint32_t)total, C, make_fastdiv(a.cd), make_fastdiv(R * a.cd), meta_first, a.E, *a.P);
+    const bool swz = (flags & RFEC_KFLAG_XCD_SWIZZLE) != 0;
+    const uint32_t meta_first = (flags & RFEC_KFLAG_META_TAIL) && !swz ? nb : 0u;
+    // swizzle: meta blocks at the head, padded to a multiple of 8 so payload block p runs on XCD p % 8
+    const uint32_t head = swz ? (a.E.n_meta_blocks + 7u) & ~7u : 0u;
+    hipLaunchKernelGGL((k_encode_out<K, COL, NTL, NTS>), dim3((swz ? head : a.E.n_meta_blocks) + nb), dim3(kBlock), 0,
+                       a.stream, a.s, a.p, (uint32_t)total, C, make_fastdiv(a.cd), make_fastdiv(R * a.cd), meta_first,
+                       head, a.E, *a.P);
     return hipGetLastError();
 }
 
@@ -1958,15 +1974,16 @@ void launch_fused_out(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_
 
 // row-layout fused decode: one lane per (group, row, chunk column)
 template <int K, int COL>
-void launch_fused_rows(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, uint32_t cd)
+void launch_fused_rows(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, uint32_t cd, bool swz)
 {
     constexpr uint32_t R = (K + COL - 1) / COL;
     const uint32_t total = B.groups * R * cd; // < 2^32: checked by the caller
-    const dim3 grid(F.n_hdr + blocks_for(total));
+    const uint32_t head = swz ? (F.n_hdr + 7u) & ~7u : 0u;
+    const dim3 grid((swz ? head : F.n_hdr) + blocks_for(total));
     const FastDiv dC = make_fastdiv(cd), dRC = make_fastdiv(R * cd);
 #define RFEC_FUSED_ROWS(NTL, NTS)                                                                                \
     hipLaunchKernelGGL((k_decode_rows<K, COL, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards, F.parity,    \
-                       total, F.C, dC, dRC, F.n_hdr, hdr_every(F, blocks_for(total)), B, M, F.D)
+                       total, F.C, dC, dRC, F.n_hdr, hdr_every(F, blocks_for(total)), B, M, F.D, head)
     switch (sp) {
     case -1: RFEC_FUSED_ROWS(false, 1); break;
     case 0: RFEC_FUSED_ROWS(true, 0); break;
@@ -2302,10 +2319,11 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
             uint32_t col = 0;
             if (!(flags & RFEC_KFLAG_GENERIC) && is_row_layout(&P, &col) && col == 4 &&
                 (P.k == 10 || P.k == 32)) {
+                const bool swz = (flags & RFEC_KFLAG_XCD_SWIZZLE) != 0;
                 if (P.k == 10)
-                    launch_fused_rows<10, 4>(F, sp, B, *M, cd);
+                    launch_fused_rows<10, 4>(F, sp, B, *M, cd, swz);
                 else
-                    launch_fused_rows<32, 4>(F, sp, B, *M, cd);
+                    launch_fused_rows<32, 4>(F, sp, B, *M, cd, swz);
                 return (int)hipGetLastError();
             }
             if (maxc <= 4)

@@ -527,7 +527,7 @@ def test_full_plan_shapes_gpu(gpu, oracle1000, k, tuning):
 @pytest.mark.parametrize("k,col,S", [(10, 4, 64), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 1000),
                                      (96, 4, 512), (20, 3, 256)])
 @pytest.mark.parametrize("tuning", ["default", "hdr_head", "out_decode", "out_decode_head", "flat_decode", "generic",
-                                    "small_fused", "small_b2"])
+                                    "small_fused", "small_b2", "xcd"])
 def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tuning):
     """Row plans (disjoint lines: the fused decodes) with up to 6 erasures per
     group, lost parities and corrupted headers (fec_data_size above capacity or
@@ -583,7 +583,7 @@ def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tunin
 @pytest.mark.parametrize("k,col,S", [(10, 4, 1200), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 64),
                                      (96, 4, 512), (20, 3, 256)])
 @pytest.mark.parametrize("tuning", ["default", "flat_decode", "out_decode", "hdr_head", "generic", "small_fused",
-                                    "small_b2"])
+                                    "small_b2", "xcd"])
 def test_dense_output_decode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning):
     """rfec_recover_batch_out (recovered segments into a dense output, as
     flex_fec_recover's caller-allocated out_seg): row plans with up to 6
