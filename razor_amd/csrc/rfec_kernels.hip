@@ -1233,6 +1233,36 @@ __device__ __forceinline__ bool header_block(uint32_t n_hdr, uint32_t every, uin
     return per < n_hdr && b - per * (every + 1) == every;
 }
 
+// The same spread in rounds of 8 blocks (one per XCD: block b runs on XCD
+// b % 8) for the XCD-swizzled decodes: every (every + 1)-th round is a round
+// of 8 header blocks until n_hr of them ran, so the payload blocks fill whole
+// rounds and payload block p (in payload order) runs on XCD p % 8; it then
+// takes logical block xcd_block(p): consecutive logical blocks share an XCD's
+// L2 (the 128-B lines split between neighbouring slots are fetched once).
+// npay8: payload blocks rounded up to a multiple of 8.
+__device__ __forceinline__ bool header_block_xcd(uint32_t n_hr, uint32_t every, uint32_t npay8, uint32_t* hb,
+                                                 uint32_t* pb)
+{
+    const uint32_t R = blockIdx.x >> 3, x = blockIdx.x & 7u;
+    uint32_t pr;
+    if (!every) {
+        if (R < n_hr) {
+            *hb = R * 8u + x;
+            return true;
+        }
+        pr = R - n_hr;
+    } else {
+        const uint32_t per = R / (every + 1);
+        if (per < n_hr && R - per * (every + 1) == every) {
+            *hb = per * 8u + x;
+            return true;
+        }
+        pr = R - min(per, n_hr);
+    }
+    *pb = xcd_block(pr * 8u + x, npay8, 1);
+    return false;
+}
+
 __device__ __forceinline__ void run_header_block(const PeelArgs& A, const rfec_kmask& M, uint32_t hb)
 {
     if (A.nlp_log2)
@@ -1560,17 +1590,16 @@ template <int K, int COL, bool NTL, int NTS>
 __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* __restrict__ parity, uint32_t total,
                                                         uint32_t C, FastDiv divC, FastDiv divRC,
                                                         uint32_t n_hdr_blocks, uint32_t hdr_every, PeelArgs A,
-                                                        rfec_kmask M, DenseOut D, uint32_t swz_head)
+                                                        rfec_kmask M, DenseOut D, uint32_t swz_npay8)
 {
     static_assert(K <= 64, "row decode keeps the present mask in one word");
     uint32_t hb, pb;
-    if (swz_head) { // XCD swizzle (A/B): header blocks first, padded to a multiple of 8 (swz_head)
-        if (blockIdx.x < swz_head) {
-            if (blockIdx.x < n_hdr_blocks)
-                run_header_block(A, M, blockIdx.x);
+    if (swz_npay8) { // XCD swizzle: rounds of 8 blocks, header rounds spread (hdr_every in rounds)
+        if (header_block_xcd((n_hdr_blocks + 7u) >> 3, hdr_every, swz_npay8, &hb, &pb)) {
+            if (hb < n_hdr_blocks)
+                run_header_block(A, M, hb);
             return;
         }
-        pb = xcd_block(blockIdx.x - swz_head, gridDim.x - swz_head, 1);
     } else if (header_block(n_hdr_blocks, hdr_every, &hb, &pb)) {
         run_header_block(A, M, hb);
         return;
@@ -1978,12 +2007,14 @@ void launch_fused_rows(const FusedArgs& F, int sp, const PeelArgs& B, const rfec
 {
     constexpr uint32_t R = (K + COL - 1) / COL;
     const uint32_t total = B.groups * R * cd; // < 2^32: checked by the caller
-    const uint32_t head = swz ? (F.n_hdr + 7u) & ~7u : 0u;
-    const dim3 grid((swz ? head : F.n_hdr) + blocks_for(total));
+    const uint32_t npay = blocks_for(total), npay8 = (npay + 7u) & ~7u, nhr = (F.n_hdr + 7u) >> 3;
+    // swizzled: rounds of 8 blocks, nhr header rounds spread over npay8 / 8 payload rounds
+    const dim3 grid(swz ? 8u * nhr + npay8 : F.n_hdr + npay);
+    const uint32_t every = swz ? (F.spread && nhr ? (npay8 >> 3) / nhr : 0u) : hdr_every(F, npay);
     const FastDiv dC = make_fastdiv(cd), dRC = make_fastdiv(R * cd);
 #define RFEC_FUSED_ROWS(NTL, NTS)                                                                                \
     hipLaunchKernelGGL((k_decode_rows<K, COL, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards, F.parity,    \
-                       total, F.C, dC, dRC, F.n_hdr, hdr_every(F, blocks_for(total)), B, M, F.D, head)
+                       total, F.C, dC, dRC, F.n_hdr, every, B, M, F.D, swz ? npay8 : 0u)
     switch (sp) {
     case -1: RFEC_FUSED_ROWS(false, 1); break;
     case 0: RFEC_FUSED_ROWS(true, 0); break;
