@@ -1834,7 +1834,9 @@ hipError_t launch_rows_out(const EncLaunch& a, unsigned flags)
     const uint32_t C = a.stride / 16;
     const uint64_t total = (uint64_t)a.groups * R * a.cd;
     const uint32_t nb = blocks_for(total);
-    const bool swz = (flags & RFEC_KFLAG_XCD_SWIZZLE) != 0;
+    // XCD-swizzled block order by default (tools/gpu_xcd.sh, cold: 168.1-168.4 vs 172.1 us linear, HBM
+    // traffic 1.029 vs 1.059 x algorithmic: a 128-B line split between neighbouring slots is fetched once)
+    const bool swz = !(flags & (RFEC_KFLAG_LINEAR_BLOCKS | RFEC_KFLAG_META_TAIL));
     const uint32_t meta_first = (flags & RFEC_KFLAG_META_TAIL) && !swz ? nb : 0u;
     // swizzle: meta blocks at the head, padded to a multiple of 8 so payload block p runs on XCD p % 8
     const uint32_t head = swz ? (a.E.n_meta_blocks + 7u) & ~7u : 0u;
@@ -2350,7 +2352,9 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
             uint32_t col = 0;
             if (!(flags & RFEC_KFLAG_GENERIC) && is_row_layout(&P, &col) && col == 4 &&
                 (P.k == 10 || P.k == 32)) {
-                const bool swz = (flags & RFEC_KFLAG_XCD_SWIZZLE) != 0;
+                // XCD-swizzled by default: decode traffic 1.077 vs 1.107 x algorithmic at k = 10 / 1,200 B,
+                // time within noise (130.0-130.4 vs 129.2 us, tools/gpu_xcd.sh)
+                const bool swz = !(flags & RFEC_KFLAG_LINEAR_BLOCKS);
                 if (P.k == 10)
                     launch_fused_rows<10, 4>(F, sp, B, *M, cd, swz);
                 else

@@ -20,7 +20,7 @@ TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "plain_stores": 4, "ite
            "generic_plain": 3, "two_kernel": 4096, "two_kernel_wt": 4096 | 64, "group_wave": 8192,
            "group_wave_xcd": 8192 | 16384, "xcd": 16384, "lds_hdr_peel": 32768, "flat_encode": 65536,
            "meta_tail": 131072, "meta_tail_nt": 131072 | 512, "flat_decode": 262144, "hdr_head": 524288,
-           "out_decode": 2097152, "out_decode_head": 2097152 | 524288, "small_fused": 4194304, "small_b2": 4194304 | 8388608}
+           "out_decode": 2097152, "out_decode_head": 2097152 | 524288, "small_fused": 4194304, "small_b2": 4194304 | 8388608, "linear": 16777216}
 
 
 @pytest.fixture(scope="module")
@@ -41,7 +41,8 @@ def test_sender_random_fixture_gpu(gpu, oracle1000):
     pc.check_sender_random_case(gpu(), oracle1000, CASES["random_k"])
 
 
-@pytest.mark.parametrize("tuning", ["default", "generic", "group_wave", "group_wave_xcd", "flat_encode", "meta_tail"])
+@pytest.mark.parametrize("tuning", ["default", "generic", "group_wave", "group_wave_xcd", "flat_encode", "meta_tail",
+                                    "linear"])
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "rows"])
 def test_rows_fixture_gpu(gpu, oracle1000, oracle1200, name, tuning):
     c = CASES[name]
@@ -59,7 +60,7 @@ def test_erasure_fixture_gpu(gpu, oracle1000, name, tuning):
 @pytest.mark.parametrize("tuning", ["default", "wt_stores", "plain_stores", "plain_loads", "two_kernel",
                                     "two_kernel_wt", "pipe_decode", "wave_decode", "group_wave",
                                     "group_wave_xcd", "items2", "lds_hdr_peel", "flat_decode",
-                                    "generic", "hdr_head", "out_decode", "out_decode_head"])
+                                    "generic", "hdr_head", "out_decode", "out_decode_head", "linear"])
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures" and c["rows_only"]])
 def test_erasure_fixture_rows_plan_gpu(gpu, oracle1000, name, tuning):
     """Row-parity-only fixtures against the row-layer plan (pairwise disjoint
@@ -147,7 +148,7 @@ def test_full_size_k10_roundtrip(product, oracle1200, layers):
     plan = lib.plan_from_fraction(k, 80, layers)
     shards, hdr, d_hdr = _device_batch(G, k, S, 1234)
     par, meta, fs, st = _run_encode(lib, plan, G, S, shards, d_hdr)
-    for tuning in (1, 2, 4, 8, 3, 64, 192, 512, 8192, 8192 | 16384, 16384, 65536, 131072, 131072 | 512):
+    for tuning in (1, 2, 4, 8, 3, 64, 192, 512, 8192, 8192 | 16384, 16384, 65536, 131072, 131072 | 512, 16777216):
         par2, meta2, fs2, st2 = _run_encode(lib, plan, G, S, shards, d_hdr, tuning=tuning)
         assert torch.equal(par, par2) and torch.equal(meta, meta2) and torch.equal(fs, fs2), tuning
         del par2, meta2, fs2, st2
@@ -527,7 +528,7 @@ def test_full_plan_shapes_gpu(gpu, oracle1000, k, tuning):
 @pytest.mark.parametrize("k,col,S", [(10, 4, 64), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 1000),
                                      (96, 4, 512), (20, 3, 256)])
 @pytest.mark.parametrize("tuning", ["default", "hdr_head", "out_decode", "out_decode_head", "flat_decode", "generic",
-                                    "small_fused", "small_b2", "xcd"])
+                                    "small_fused", "small_b2", "xcd", "linear"])
 def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tuning):
     """Row plans (disjoint lines: the fused decodes) with up to 6 erasures per
     group, lost parities and corrupted headers (fec_data_size above capacity or
@@ -583,7 +584,7 @@ def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tunin
 @pytest.mark.parametrize("k,col,S", [(10, 4, 1200), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 64),
                                      (96, 4, 512), (20, 3, 256)])
 @pytest.mark.parametrize("tuning", ["default", "flat_decode", "out_decode", "hdr_head", "generic", "small_fused",
-                                    "small_b2", "xcd"])
+                                    "small_b2", "xcd", "linear"])
 def test_dense_output_decode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning):
     """rfec_recover_batch_out (recovered segments into a dense output, as
     flex_fec_recover's caller-allocated out_seg): row plans with up to 6
