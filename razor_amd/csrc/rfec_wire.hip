@@ -330,10 +330,41 @@ __device__ __forceinline__ uint32_t len_mask(int k, uint32_t lane, uint32_t nb)
 // a lane's B bytes to [B lane, B lane + B) of a slot of slot_bytes: 16-byte
 // stores plus a dword, range-checked by the buffer descriptor (nothing lands
 // past the slot)
+// A 20-byte-lane message stored as 16-byte lanes: the lanes' dwords go through
+// this wave's LDS buffer wb (320 dwords; dword 5j + k from lane j: banks 5j + k
+// mod 32, distinct over a 32-lane group) and come back as 16-byte chunks, so
+// each global store is 1 KiB (then 256 B) of consecutive 16-byte-aligned
+// bytes.  The direct form stores 16 + 4 bytes per lane at a 20-byte stride:
+// misaligned vectors that cost the frame kernels ~140 of their ~460 us
+// (tools/wire_lab.sh, DIAG_NO_STORE).
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int B>
 __device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t slot_bytes, uint32_t lane,
-                                           const uint32_t* w)
+                                           const uint32_t* w, uint32_t* wb = nullptr)
 {
+    if constexpr (B == 20) {
+        if (wb) {
+            typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+            const __amdgpu_buffer_rsrc_t r = rsrc(slot, slot_bytes);
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+                wb[5 * lane + k] = w[k];
+            wave_lds_sync();
+            const v4u a = *reinterpret_cast<const v4u*>(wb + 4 * lane);
+            const v4u c = *reinterpret_cast<const v4u*>(wb + 256 + 4 * (lane & 15u));
+            wave_lds_sync(); // the buffer is refilled by the next message
+            __builtin_amdgcn_raw_buffer_store_b128(u4{a[0], a[1], a[2], a[3]}, r, 16 * lane, 0, kAuxNT);
+            if (lane < 16)
+                __builtin_amdgcn_raw_buffer_store_b128(u4{c[0], c[1], c[2], c[3]}, r, 1024 + 16 * lane, 0, kAuxNT);
+            return;
+        }
+    }
 #if defined(RFEC_WIRE_DIAG_NO_STORE)
     uint32_t x = 0;
 #pragma unroll
@@ -371,7 +402,7 @@ __device__ __forceinline__ void put(Hdr& b, uint32_t v)
 template <int B>
 __device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, uint32_t n, const uint32_t* pay,
                                              uint32_t lane, uint8_t* __restrict__ slot, uint32_t dstride,
-                                             uint16_t* dlen_out)
+                                             uint16_t* dlen_out, uint32_t* wb)
 {
     constexpr int ND = B / 4;
     uint32_t w[ND];
@@ -398,17 +429,17 @@ __device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, ui
         if ((uint32_t)k == k1)
             w[k] |= lane == l1 ? hi : 0u;
     }
-    store_slot<B>(slot, dstride, lane, w);
+    store_slot<B>(slot, dstride, lane, w, wb);
     if (lane == 0)
         *dlen_out = (uint16_t)(n + 4);
 }
 
 template <int B>
 __device__ __forceinline__ void zero_slot(uint8_t* __restrict__ slot, uint32_t dstride, uint32_t lane,
-                                          uint16_t* dlen_out)
+                                          uint16_t* dlen_out, uint32_t* wb)
 {
     const uint32_t z[B / 4] = {};
-    store_slot<B>(slot, dstride, lane, z);
+    store_slot<B>(slot, dstride, lane, z, wb);
     if (lane == 0)
         *dlen_out = 0;
 }
@@ -503,6 +534,8 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
 {
     constexpr int ND = B / 4;
     __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords<B>];
+    __shared__ __attribute__((aligned(16))) uint32_t WB[kWavesPerBlock][B == 20 ? 16 * B : 4]; // store transposes
+    uint32_t* wb = B == 20 ? WB[threadIdx.x >> 6] : nullptr;
     load_tables<B>(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
@@ -522,7 +555,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
             const uint32_t L = fld(P.f, 11);
             const int st = (int)fld(P.f, 12);
             if (st < 0 || L > capacity) {
-                zero_slot<B>(slot, dstride, lane, dlen + o);
+                zero_slot<B>(slot, dstride, lane, dlen + o, wb);
             } else {
                 const uint32_t s3 = fld(P.f, 3), s4 = fld(P.f, 4), s5 = fld(P.f, 5);
                 const uint32_t m3 = fld(P.f, 9), m4 = fld(P.f, 10);
@@ -550,7 +583,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
                 uint32_t pay[ND], x[ND + 1];
                 win_dwords<B, 48>(P.w, lane, x);
                 funnel<ND, 3>(x, pay); // window [B j - 48, ...) -> bytes [B j - 45, ...)
-                finish_frame<B>(T, H, 45 + L, pay, lane, slot, dstride, dlen + o);
+                finish_frame<B>(T, H, 45 + L, pay, lane, slot, dstride, dlen + o, wb);
             }
                               });
 }
@@ -599,6 +632,8 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
 {
     constexpr int ND = B / 4;
     __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords<B>];
+    __shared__ __attribute__((aligned(16))) uint32_t WB[kWavesPerBlock][B == 20 ? 16 * B : 4]; // store transposes
+    uint32_t* wb = B == 20 ? WB[threadIdx.x >> 6] : nullptr;
     load_tables<B>(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
@@ -629,7 +664,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
             }
             const uint32_t L = h.size;
             if (L > capacity) {
-                zero_slot<B>(slot, dstride, lane, dlen + o);
+                zero_slot<B>(slot, dstride, lane, dlen + o, wb);
             } else {
                 rfec_seg_stamp s;
                 {
@@ -657,7 +692,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                 case 6: hs = seg_header<true, true, false>(H, h, s); funnel<ND, 2>(x, pay); break;
                 default: hs = seg_header<true, true, true>(H, h, s); funnel<ND, 0>(x, pay); break;
                 }
-                finish_frame<B>(T, H, hs + L, pay, lane, slot, dstride, dlen + o);
+                finish_frame<B>(T, H, hs + L, pay, lane, slot, dstride, dlen + o, wb);
             }
                               });
 }
@@ -808,6 +843,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
     constexpr int ND = B / 4;
     __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords<B>];
     __shared__ uint32_t stage[kWavesPerBlock][16]; // first 64 bytes of each wave's datagram (slow path)
+    __shared__ __attribute__((aligned(16))) uint32_t WB[kWavesPerBlock][B == 20 ? 16 * B : 4]; // store transposes
+    uint32_t* wb = B == 20 ? WB[threadIdx.x >> 6] : nullptr;
     load_tables<B>(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wl = threadIdx.x >> 6;
@@ -990,13 +1027,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
 #pragma unroll
                         for (int k = 0; k < ND; ++k)
                             pay[k] &= len_mask<B>(k, lane, dsize);
-                        store_slot<B>(slot, stride, lane, pay);
+                        store_slot<B>(slot, stride, lane, pay, wb);
                     }
                 }
             }
             write_rec(recs + d, rec, lane);
             if (data_at < 0)
-                store_slot<B>(slot, stride, lane, z);
+                store_slot<B>(slot, stride, lane, z, wb);
                           });
 }
 
