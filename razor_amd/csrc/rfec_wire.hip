@@ -348,6 +348,15 @@ template <int B>
 __device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t slot_bytes, uint32_t lane,
                                            const uint32_t* w, uint32_t* wb = nullptr)
 {
+#if defined(RFEC_WIRE_DIAG_NO_STORE)
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < B / 4; ++k)
+        x ^= w[k];
+    if (x == 0x9E3779B9u && lane == 63u) // keeps the work alive, stores (almost) nothing
+        slot[0] = (uint8_t)x;
+    return;
+#endif
     if constexpr (B == 20) {
         if (wb) {
             typedef unsigned int u4 __attribute__((ext_vector_type(4)));
@@ -365,15 +374,6 @@ __device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t 
             return;
         }
     }
-#if defined(RFEC_WIRE_DIAG_NO_STORE)
-    uint32_t x = 0;
-#pragma unroll
-    for (int k = 0; k < B / 4; ++k)
-        x ^= w[k];
-    if (x == 0x9E3779B9u && lane == 63u) // keeps the work alive, stores (almost) nothing
-        slot[0] = (uint8_t)x;
-    return;
-#endif
     const __amdgpu_buffer_rsrc_t r = rsrc(slot, slot_bytes);
     typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 #pragma unroll
@@ -511,11 +511,59 @@ __device__ __forceinline__ void ping_pong(uint32_t d, uint32_t count, uint32_t n
     }
 }
 
-template <int NX>
+template <class W>
 struct Pre {
-    Win<NX> w;  // payload window
+    W w;        // payload: a lane window (Win) or aligned chunks (Chunks)
     uint32_t f; // per-datagram fields, one dword per lane
 };
+
+template <bool C, class A, class B_>
+struct Sel {
+    using T = A;
+};
+template <class A, class B_>
+struct Sel<false, A, B_> {
+    using T = B_;
+};
+
+// 20-byte lanes, staged: the slot's first 1,280 bytes as aligned 16-byte
+// chunks (chunk j in lane j, chunk 64 + j in lane j < 16), coalesced 1 KiB
+// loads; stage_window() turns them into the lanes' windows through this
+// wave's LDS buffer (the direct window loads are 16 + 12-byte vectors at a
+// 20-byte stride: misaligned).
+struct Chunks {
+    v4u c0, c1;
+};
+
+__device__ __forceinline__ void load_chunks(const uint8_t* base, uint32_t bytes, uint32_t lane, Chunks& ch)
+{
+    const __amdgpu_buffer_rsrc_t r = rsrc(base, bytes);
+    ch.c0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * lane, 0, kAuxNT));
+    ch.c1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, 1024u + 16u * (lane & 15u), 0, kAuxNT));
+}
+
+// x[k] = dword k of the window at slot byte 20 lane - SRC (SRC a multiple of
+// 16; bytes before the slot and past the loaded range read 0).  LDS: bytes
+// [0, SRC) zero, then the 1,280 staged bytes; the reads, dword 5 lane + k,
+// hit 32 distinct banks per 32-lane group.
+template <int SRC, int NX>
+__device__ __forceinline__ void stage_window(const Chunks& ch, uint32_t lane, uint32_t* wb, uint32_t (&x)[NX])
+{
+    static_assert(SRC % 16 == 0 && 5 * 63 + NX <= SRC / 4 + 320, "window past the staged bytes");
+    v4u* w4 = reinterpret_cast<v4u*>(wb);
+    w4[SRC / 16 + lane] = ch.c0;
+    if (lane < 16)
+        w4[SRC / 16 + 64 + lane] = ch.c1;
+    if (lane < SRC / 16)
+        w4[lane] = v4u{0, 0, 0, 0};
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < NX; ++k)
+        x[k] = wb[5 * lane + k];
+    wave_lds_sync(); // the buffer is reused by the store
+}
+
+constexpr int kWaveBuf = 336; // dwords per wave: 48 + 1,280 bytes staged, or 1,280 stored
 
 // Lane j's window starts 48 (FEC) / 32 (SEG) bytes before the source of its
 // output bytes [B j, B j + B), so it does not depend on the header size.
@@ -534,7 +582,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
 {
     constexpr int ND = B / 4;
     __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords<B>];
-    __shared__ __attribute__((aligned(16))) uint32_t WB[kWavesPerBlock][B == 20 ? 16 * B : 4]; // store transposes
+    __shared__ __attribute__((aligned(16))) uint32_t WB[kWavesPerBlock][B == 20 ? kWaveBuf : 4]; // staging
     uint32_t* wb = B == 20 ? WB[threadIdx.x >> 6] : nullptr;
     load_tables<B>(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -544,12 +592,16 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
     uint32_t d = wave_id();
     if (d >= count)
         return;
-    ping_pong<Pre<ND + 1>>(d, count, nw,
-                              [&](uint32_t dd, Pre<ND + 1>& P) {
+    using PW = Pre<typename Sel<B == 20, Chunks, Win<ND + 1>>::T>;
+    ping_pong<PW>(d, count, nw,
+                              [&](uint32_t dd, PW& P) {
                                   P.f = load_fec_fields(stamps, meta, fsize, status, dd, lane);
-                                  load_window<ND + 1>(parity + (size_t)dd * stride, range, off, P.w);
+                                  if constexpr (B == 20)
+                                      load_chunks(parity + (size_t)dd * stride, range, lane, P.w);
+                                  else
+                                      load_window<ND + 1>(parity + (size_t)dd * stride, range, off, P.w);
                               },
-                              [&](const Pre<ND + 1>& P, uint32_t d) {
+                              [&](const PW& P, uint32_t d) {
             const uint32_t o = order ? order[d] : d; // output slot
             uint8_t* slot = dgram + (size_t)o * dstride;
             const uint32_t L = fld(P.f, 11);
@@ -581,7 +633,10 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
                 put<41, 2>(H, m4 >> 16);
                 put<43, 2>(H, L); // mach_data_write length (cf_stream.c:328-337)
                 uint32_t pay[ND], x[ND + 1];
-                win_dwords<B, 48>(P.w, lane, x);
+                if constexpr (B == 20)
+                    stage_window<48, ND + 1>(P.w, lane, wb, x);
+                else
+                    win_dwords<B, 48>(P.w, lane, x);
                 funnel<ND, 3>(x, pay); // window [B j - 48, ...) -> bytes [B j - 45, ...)
                 finish_frame<B>(T, H, 45 + L, pay, lane, slot, dstride, dlen + o, wb);
             }
@@ -632,7 +687,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
 {
     constexpr int ND = B / 4;
     __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords<B>];
-    __shared__ __attribute__((aligned(16))) uint32_t WB[kWavesPerBlock][B == 20 ? 16 * B : 4]; // store transposes
+    __shared__ __attribute__((aligned(16))) uint32_t WB[kWavesPerBlock][B == 20 ? kWaveBuf : 4]; // staging
     uint32_t* wb = B == 20 ? WB[threadIdx.x >> 6] : nullptr;
     load_tables<B>(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
@@ -642,12 +697,16 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
     uint32_t d = wave_id();
     if (d >= count)
         return;
-    ping_pong<Pre<ND + 2>>(d, count, nw,
-                              [&](uint32_t dd, Pre<ND + 2>& P) {
+    using PW = Pre<typename Sel<B == 20, Chunks, Win<ND + 2>>::T>;
+    ping_pong<PW>(d, count, nw,
+                              [&](uint32_t dd, PW& P) {
                                   P.f = load_seg_fields(hdr, stamps, dd, lane);
-                                  load_window<ND + 2>(shards + (size_t)dd * stride, range, off, P.w);
+                                  if constexpr (B == 20)
+                                      load_chunks(shards + (size_t)dd * stride, range, lane, P.w);
+                                  else
+                                      load_window<ND + 2>(shards + (size_t)dd * stride, range, off, P.w);
                               },
-                              [&](const Pre<ND + 2>& P, uint32_t d) {
+                              [&](const PW& P, uint32_t d) {
             const uint32_t o = order ? order[d] : d; // output slot
             uint8_t* slot = dgram + (size_t)o * dstride;
             rfec_hdr h;
@@ -680,7 +739,10 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                 const uint32_t layout = (h.seq > 65535u ? 4u : 0u) | (h.fid > 65535u ? 2u : 0u) |
                                         (h.total > 255u ? 1u : 0u);
                 uint32_t hs, pay[ND], x[ND + 2];
-                win_dwords<B, 32>(P.w, lane, x);
+                if constexpr (B == 20)
+                    stage_window<32, ND + 2>(P.w, lane, wb, x);
+                else
+                    win_dwords<B, 32>(P.w, lane, x);
                 // window [B j - 32, ...) shifted by 32 - hs bytes
                 switch (layout) {
                 case 0: hs = seg_header<false, false, false>(H, h, s); funnel<ND, 6>(x, pay); break;
@@ -843,8 +905,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
     constexpr int ND = B / 4;
     __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords<B>];
     __shared__ uint32_t stage[kWavesPerBlock][16]; // first 64 bytes of each wave's datagram (slow path)
-    __shared__ __attribute__((aligned(16))) uint32_t WB[kWavesPerBlock][B == 20 ? 16 * B : 4]; // store transposes
-    uint32_t* wb = B == 20 ? WB[threadIdx.x >> 6] : nullptr;
+    uint32_t* wb = nullptr; // direct stores: the LDS transpose measured slower in the parse (608 vs 568 us)
     load_tables<B>(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wl = threadIdx.x >> 6;
@@ -853,12 +914,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
     uint32_t d = wave_id();
     if (d >= n)
         return;
-    ping_pong<Pre<ND>>(d, n, nw,
-                          [&](uint32_t dd, Pre<ND>& P) {
+    ping_pong<Pre<Win<ND>>>(d, n, nw,
+                          [&](uint32_t dd, Pre<Win<ND>>& P) {
                               P.f = __builtin_amdgcn_raw_buffer_load_b16(rsrc(dlen + dd, 2), 2u * lane, 0, kAuxNT);
                               load_window<ND>(dgram + (size_t)dd * dstride, dstride, B * (int)lane, P.w);
                           },
-                          [&](const Pre<ND>& P, uint32_t d) {
+                          [&](const Pre<Win<ND>>& P, uint32_t d) {
             uint8_t* slot = payload + (size_t)d * stride;
             const uint32_t len = fld(P.f, 0);
             rfec_wire_rec rec = {};
