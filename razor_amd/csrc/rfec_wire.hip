@@ -511,6 +511,31 @@ __device__ __forceinline__ void ping_pong(uint32_t d, uint32_t count, uint32_t n
     }
 }
 
+// Three-deep form: two datagrams' loads in flight while one is processed
+// (the frame kernels' staged chunks are 8 dwords, so a third buffer fits the
+// register budget of 8 waves per SIMD).
+template <class Pre_, class Load, class Proc>
+__device__ __forceinline__ void pipeline3(uint32_t d, uint32_t count, uint32_t nw, Load load, Proc proc)
+{
+    Pre_ a, b, c;
+    load(d, a);
+    load(min(d + nw, count - 1), b);
+    for (;;) {
+        load(min(d + 2 * nw, count - 1), c);
+        proc(a, d);
+        if ((d += nw) >= count)
+            break;
+        load(min(d + 2 * nw, count - 1), a);
+        proc(b, d);
+        if ((d += nw) >= count)
+            break;
+        load(min(d + 2 * nw, count - 1), b);
+        proc(c, d);
+        if ((d += nw) >= count)
+            break;
+    }
+}
+
 template <class W>
 struct Pre {
     W w;        // payload: a lane window (Win) or aligned chunks (Chunks)
@@ -564,6 +589,9 @@ __device__ __forceinline__ void stage_window(const Chunks& ch, uint32_t lane, ui
 }
 
 constexpr int kWaveBuf = 336; // dwords per wave: 48 + 1,280 bytes staged, or 1,280 stored
+#ifndef RFEC_WIRE_PIPE
+#define RFEC_WIRE_PIPE ping_pong // frame kernels' datagram pipeline (the lab's DEPTH3 build: pipeline3)
+#endif
 
 // Lane j's window starts 48 (FEC) / 32 (SEG) bytes before the source of its
 // output bytes [B j, B j + B), so it does not depend on the header size.
@@ -593,7 +621,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
     if (d >= count)
         return;
     using PW = Pre<typename Sel<B == 20, Chunks, Win<ND + 1>>::T>;
-    ping_pong<PW>(d, count, nw,
+    RFEC_WIRE_PIPE<PW>(d, count, nw,
                               [&](uint32_t dd, PW& P) {
                                   P.f = load_fec_fields(stamps, meta, fsize, status, dd, lane);
                                   if constexpr (B == 20)
@@ -698,7 +726,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
     if (d >= count)
         return;
     using PW = Pre<typename Sel<B == 20, Chunks, Win<ND + 2>>::T>;
-    ping_pong<PW>(d, count, nw,
+    RFEC_WIRE_PIPE<PW>(d, count, nw,
                               [&](uint32_t dd, PW& P) {
                                   P.f = load_seg_fields(hdr, stamps, dd, lane);
                                   if constexpr (B == 20)
