@@ -933,7 +933,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
     constexpr int ND = B / 4;
     __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords<B>];
     __shared__ uint32_t stage[kWavesPerBlock][16]; // first 64 bytes of each wave's datagram (slow path)
-    uint32_t* wb = nullptr; // direct stores: the LDS transpose measured slower in the parse (608 vs 568 us)
+    // 20-byte lanes: the datagram comes in as aligned 16-byte chunks, staged
+    // in this wave's LDS buffer; the lanes' windows and the payload's output
+    // dwords are read from there
+    __shared__ __attribute__((aligned(16))) uint32_t WB[kWavesPerBlock][B == 20 ? kWaveBuf : 4];
+    uint32_t* wb = WB[threadIdx.x >> 6];
     load_tables<B>(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t wl = threadIdx.x >> 6;
@@ -942,22 +946,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
     uint32_t d = wave_id();
     if (d >= n)
         return;
-    ping_pong<Pre<Win<ND>>>(d, n, nw,
-                          [&](uint32_t dd, Pre<Win<ND>>& P) {
+    using PW = Pre<typename Sel<B == 20, Chunks, Win<ND>>::T>;
+    ping_pong<PW>(d, n, nw,
+                          [&](uint32_t dd, PW& P) {
                               P.f = __builtin_amdgcn_raw_buffer_load_b16(rsrc(dlen + dd, 2), 2u * lane, 0, kAuxNT);
-                              load_window<ND>(dgram + (size_t)dd * dstride, dstride, B * (int)lane, P.w);
+                              if constexpr (B == 20)
+                                  load_chunks(dgram + (size_t)dd * dstride, dstride, lane, P.w);
+                              else
+                                  load_window<ND>(dgram + (size_t)dd * dstride, dstride, B * (int)lane, P.w);
                           },
-                          [&](const Pre<Win<ND>>& P, uint32_t d) {
+                          [&](const PW& P, uint32_t d) {
             uint8_t* slot = payload + (size_t)d * stride;
             const uint32_t len = fld(P.f, 0);
             rfec_wire_rec rec = {};
             rec.status = RFEC_WIRE_EBADCRC;
             int data_at = -1;
             uint32_t dsize = 0;
+            if constexpr (B == 20) { // stage the datagram: LDS dwords [0, 320)
+                v4u* w4 = reinterpret_cast<v4u*>(wb);
+                w4[lane] = P.w.c0;
+                if (lane < 16)
+                    w4[64 + lane] = P.w.c1;
+                wave_lds_sync();
+            }
             if (len >= 4 && len <= dstride && len <= (uint32_t)(kWave * B)) {
                 // datagram bytes [B j, B j + B), zero from `len` on
                 uint32_t w[ND], m[ND];
-                win_dwords<B, 0>(P.w, lane, w);
+                if constexpr (B == 20) {
+#pragma unroll
+                    for (int k = 0; k < ND; ++k)
+                        w[k] = wb[ND * lane + k];
+                } else {
+                    win_dwords<B, 0>(P.w, lane, w);
+                }
 #pragma unroll
                 for (int k = 0; k < ND; ++k) {
                     w[k] &= len_mask<B>(k, lane, len);
@@ -1111,18 +1132,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
                     }
                     rec.data_size = (uint16_t)dsize;
                     if (data_at >= 0) {
-                        uint32_t pay[ND];
-                        shift_down_bytes<B>(w, (uint32_t)data_at, pay);
+                        if constexpr (B == 20) {
+                            // payload dword q = datagram bytes [data_at + 4q, +4) from the staged
+                            // copy, zero from dsize on; 64 consecutive dwords per store
+                            const __amdgpu_buffer_rsrc_t r = rsrc(slot, stride);
+                            const uint32_t c = (uint32_t)data_at >> 2, sh = (uint32_t)data_at & 3u;
+                            for (uint32_t q0 = 0; q0 < stride / 4; q0 += kWave) {
+                                const uint32_t q = q0 + lane, i = min(c + q, (uint32_t)kWaveBuf - 2);
+                                uint32_t v = __builtin_amdgcn_alignbyte(wb[i + 1], wb[i], sh);
+                                v = 4 * q + 4 <= dsize ? v : (4 * q < dsize ? v & ((1u << (8 * (dsize - 4 * q))) - 1u) : 0u);
+                                __builtin_amdgcn_raw_buffer_store_b32(v, r, 4 * q, 0, kAuxNT);
+                            }
+                        } else {
+                            uint32_t pay[ND];
+                            shift_down_bytes<B>(w, (uint32_t)data_at, pay);
 #pragma unroll
-                        for (int k = 0; k < ND; ++k)
-                            pay[k] &= len_mask<B>(k, lane, dsize);
-                        store_slot<B>(slot, stride, lane, pay, wb);
+                            for (int k = 0; k < ND; ++k)
+                                pay[k] &= len_mask<B>(k, lane, dsize);
+                            store_slot<B>(slot, stride, lane, pay);
+                        }
                     }
                 }
             }
             write_rec(recs + d, rec, lane);
-            if (data_at < 0)
-                store_slot<B>(slot, stride, lane, z, wb);
+            if (data_at < 0) {
+                if constexpr (B == 20) { // aligned 16-byte zeros
+                    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+                    const __amdgpu_buffer_rsrc_t r = rsrc(slot, stride);
+                    for (uint32_t q0 = 0; q0 < stride / 16; q0 += kWave)
+                        __builtin_amdgcn_raw_buffer_store_b128(u4{0, 0, 0, 0}, r, 16 * (q0 + lane), 0, kAuxNT);
+                } else {
+                    store_slot<B>(slot, stride, lane, z);
+                }
+            }
+            if constexpr (B == 20)
+                wave_lds_sync(); // the buffer is refilled by the next datagram
                           });
 }
 
