@@ -3,7 +3,7 @@
 #   bash tools/wire_lab.sh build      # here: hipcc, tools/bin/wire_lab_*
 #   bash tools/wire_lab.sh run        # GPU box
 set -u
-V="base: nocrc:-DRFEC_WIRE_DIAG_NO_CRC nocarry:-DRFEC_WIRE_DIAG_NO_CARRY nostore:-DRFEC_WIRE_DIAG_NO_STORE nocrc_nostore:-DRFEC_WIRE_DIAG_NO_CRC_-DRFEC_WIRE_DIAG_NO_STORE depth3:-DRFEC_WIRE_PIPE=pipeline3 depth3_nocrc_nostore:-DRFEC_WIRE_PIPE=pipeline3_-DRFEC_WIRE_DIAG_NO_CRC_-DRFEC_WIRE_DIAG_NO_STORE"
+V="base: nocrc:-DRFEC_WIRE_DIAG_NO_CRC nocrc_nostore:-DRFEC_WIRE_DIAG_NO_CRC_-DRFEC_WIRE_DIAG_NO_STORE loadonly:-DRFEC_WIRE_DIAG_LOAD_ONLY nopass1:-DRFEC_WIRE_DIAG_NO_PASS1 pass1_noload:-DRFEC_WIRE_DIAG_PASS1_NOLOAD"
 if [ "${1:-run}" = build ]; then
   for v in $V; do
     name=${v%%:*}; flags=${v#*:}; flags=${flags//_-D/ -D}
