@@ -2,7 +2,7 @@
 # The round's standard GPU measurement pass (GPU box, repo root):
 #   bash tools/measure.sh <tag>
 # pytest -m gpu, smoke, drop-in harness + group bench, bench (c3, then c5),
-# rocprofv3 kernel stats of the bench, PMC traffic passes (FETCH_SIZE /
+# rocprofv3 kernel stats of the bench, wire bench + its kernel stats, PMC traffic passes (FETCH_SIZE /
 # WRITE_SIZE) for c3 and c5.  Every GPU step has its own limit; a crash /
 # fault / timeout stops the script.
 set -u
@@ -28,6 +28,8 @@ step bench 400 python bench.py --steps 20 --warmup 5
 step bench_c5 400 python bench.py --config c5 --steps 20 --warmup 5 --no-cpu
 step rocprof_stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --no-cpu --steps 20 --warmup 5
 step rocprof_stats_c5 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5" -o run -- python bench.py --config c5 --no-cpu --steps 20 --warmup 5
+step wire_bench 300 python tools/wire_bench.py --out "$OUT/wire.json"
+step rocprof_wire 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_wire" -o run -- python tools/wire_bench.py --reps 5
 step pmc_c3 600 python tools/pmc_traffic.py --out "$OUT/traffic_c3.json" -- --steps 10 --warmup 2
 step pmc_c5 600 python tools/pmc_traffic.py --out "$OUT/traffic_c5.json" -- --config c5 --steps 10 --warmup 2
 echo done | tee -a "$OUT/steps.log"

@@ -6,7 +6,7 @@
 // build (tools/wire_lab.sh does all variants):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Irazor_amd/csrc [-DRFEC_WIRE_DIAG_NO_CRC ...] \
 //         tools/wire_lab.hip -o tools/bin/wire_lab_<variant>
-// run:   tools/bin/wire_lab_<variant> [reps=20]
+// run:   tools/bin/wire_lab_<variant> [reps=20] [dstride=1248]
 #include "../razor_amd/csrc/rfec_wire.hip"
 
 #include <algorithm>
@@ -27,7 +27,7 @@
 int main(int argc, char** argv)
 {
     const int reps = argc > 1 ? atoi(argv[1]) : 20;
-    const uint32_t N = 655360, S = 1200, DS = 1248;
+    const uint32_t N = 655360, S = 1200, DS = argc > 2 ? (uint32_t)atoi(argv[2]) : 1248; // datagram slot stride
     std::vector<uint8_t> sh((size_t)N * S);
     uint64_t x = 0x52415A4F52464543ull;
     for (size_t i = 0; i < sh.size(); i += 8) {
