@@ -2114,12 +2114,28 @@ static int cmp_event(const void* a, const void* b)
 }
 
 typedef struct {
-    uint8_t* h;
+    uint8_t* h;  /* pinned, device-mapped */
+    uint8_t* hd; /* h as the device addresses it */
     size_t hb;
     uint8_t* d;
     size_t db;
 } rx_ctx;
 static __thread rx_ctx t_rx;
+
+/* The device address of host memory the device can read directly (pinned:
+ * rfec_pinned_alloc, hipHostMalloc, registered), else NULL (pageable: the
+ * caller copies).  A failed query leaves no pending HIP error behind. */
+static const uint8_t* host_mapped(const void* p)
+{
+    hipPointerAttribute_t a;
+    void* d = NULL;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost ||
+        hipHostGetDevicePointer(&d, (void*)p, 0) != hipSuccess || !d) {
+        (void)hipGetLastError();
+        return NULL;
+    }
+    return (const uint8_t*)d;
+}
 
 /* Grows the per-thread pinned / device areas.  The first `keep` bytes of the
  * pinned area survive a grow (copied into the new block before the old one is
@@ -2131,14 +2147,20 @@ static int rx_reserve(size_t host_bytes, size_t dev_bytes, size_t keep)
     if (t_rx.hb < host_bytes) {
         uint8_t* nh = NULL;
         host_bytes += host_bytes / 4;
-        if ((e = hipHostMalloc((void**)&nh, host_bytes, hipHostMallocDefault)) != hipSuccess)
+        void* nd = NULL;
+        if ((e = hipHostMalloc((void**)&nh, host_bytes, hipHostMallocMapped)) != hipSuccess)
             return set_err(RFEC_ENOMEM, "rx staging (host)", e);
+        if ((e = hipHostGetDevicePointer(&nd, nh, 0)) != hipSuccess) {
+            (void)hipHostFree(nh);
+            return set_err(RFEC_EDEVICE, "rx staging (host): device view", e);
+        }
         if (t_rx.h) {
             if (keep)
                 memcpy(nh, t_rx.h, keep < t_rx.hb ? keep : t_rx.hb);
             (void)hipHostFree(t_rx.h);
         }
         t_rx.h = nh;
+        t_rx.hd = (uint8_t*)nd;
         t_rx.hb = host_bytes;
     }
     if (t_rx.db < dev_bytes) {
@@ -2323,8 +2345,13 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
                                  (uint64_t*)(D + d_rec) + 2 * sh->group0, D + d_ws + wso, sm, g_tuning);
         wso += RX_ALIGN(rfec_recover_workspace_size(&sh->plan, sh->n_groups));
     }
+    /* delivered rows: straight into the caller's output when it is pinned and
+       large enough (no second round trip; rows the peel did not cover are
+       squeezed out on the host below), else into the device staging */
+    uint8_t* outd = X->nout && X->nout <= max_out ? (uint8_t*)host_mapped(out_payload) : NULL;
     if (!ke && X->nout)
-        ke = rfec_launch_gather_rows(D + d_out, D + d_shards, (const int32_t*)(D + o_omap), X->nout, stride, sm);
+        ke = rfec_launch_gather_rows(outd ? outd : D + d_out, D + d_shards, (const int32_t*)(D + o_omap), X->nout,
+                                     stride, sm);
     uint64_t* rec = (uint64_t*)(H + o_rec);
     if (ke || (e = hipMemcpyAsync(rec, D + d_rec, (size_t)ngs * 16, hipMemcpyDeviceToHost, sm)) != hipSuccess ||
         (e = hipStreamSynchronize(sm)) != hipSuccess)
@@ -2349,12 +2376,20 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
     }
     tt = now_us();
     uint32_t o = 0;
-    if (nok == X->nout) { /* the usual case: one copy */
+    if (outd) { /* the rows are in out_payload already (the sync above) */
+        for (uint32_t q = 0; q < X->nout; ++q) {
+            if (omap[q] < 0)
+                continue;
+            if (o != q)
+                memmove(out_payload + (size_t)o * stride, out_payload + (size_t)q * stride, stride);
+            X->out[o++] = X->out[q];
+        }
+    } else if (nok == X->nout) { /* the usual case: one copy */
         if (nok)
             e = hipMemcpyAsync(out_payload, D + d_out, (size_t)nok * stride, hipMemcpyDeviceToHost, sm);
         o = nok;
     }
-    for (uint32_t q = 0; q < X->nout && nok != X->nout && e == hipSuccess; ++q) {
+    for (uint32_t q = 0; q < X->nout && !outd && nok != X->nout && e == hipSuccess; ++q) {
         if (omap[q] < 0)
             continue;
         e = hipMemcpyAsync(out_payload + (size_t)o * stride, D + d_out + (size_t)q * stride, stride,
@@ -2366,7 +2401,7 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
         out[q].fec_id = (uint16_t)X->G[X->out[q].inst].fec_id;
         out[q].reserved = 0;
     }
-    if (e == hipSuccess)
+    if (e == hipSuccess && !outd)
         e = hipStreamSynchronize(sm);
     if (e != hipSuccess)
         return set_err(RFEC_EDEVICE, "rx: output D2H", e);
@@ -2717,15 +2752,11 @@ done:
     return rc;
 }
 
-/* records already on the host (t_rx.h[0, n)), payload rows on the device */
-static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const uint8_t* payload, rfec_rx_seg* out,
-                                  uint8_t* out_payload, uint32_t max_out, uint32_t* n_out, rfec_rx_report* rep,
-                                  hipStream_t sm)
+/* room for n more arena rows and records: drop what the open state no longer
+ * refers to (and grow) */
+static int rx_session_room(rfec_rx_session* S, uint32_t n, hipStream_t sm)
 {
-    rx_sim* X = &S->X;
-    hipError_t e;
     int rc;
-    /* room for n more rows: drop what the open state no longer refers to (and grow) */
     if (S->nstore + n > S->arows && (rc = rx_compact(S, n, sm)))
         return rc;
     if (S->nstore + n > S->storecap) {
@@ -2738,13 +2769,30 @@ static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const uint8_t*
         S->store = p;
         S->storecap = c;
     }
+    return RFEC_OK;
+}
+
+/* records already on the host (t_rx.h[0, n)), payload rows on the device at
+ * `payload`, or already in the arena's next n rows (payload NULL; the caller
+ * made the room) */
+static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const uint8_t* payload, rfec_rx_seg* out,
+                                  uint8_t* out_payload, uint32_t max_out, uint32_t* n_out, rfec_rx_report* rep,
+                                  hipStream_t sm)
+{
+    rx_sim* X = &S->X;
+    hipError_t e;
+    int rc;
+    if (payload && (rc = rx_session_room(S, n, sm)))
+        return rc;
     X->R = S->store;
     memcpy(S->store + S->nstore, t_rx.h, (size_t)n * sizeof(rfec_wire_rec));
-    double tt = now_us();
-    if ((e = hipMemcpyAsync(S->arena + (size_t)S->nstore * S->stride, payload, (size_t)n * S->stride,
-                            hipMemcpyDeviceToDevice, sm)) != hipSuccess)
-        return set_err(RFEC_EDEVICE, "rx session: rows", e);
-    rep->kernel_us += now_us() - tt;
+    if (payload) {
+        double tt = now_us();
+        if ((e = hipMemcpyAsync(S->arena + (size_t)S->nstore * S->stride, payload, (size_t)n * S->stride,
+                                hipMemcpyDeviceToDevice, sm)) != hipSuccess)
+            return set_err(RFEC_EDEVICE, "rx session: rows", e);
+        rep->kernel_us += now_us() - tt;
+    }
     const uint32_t a0 = S->nstore;
     S->nstore += n;
     const double th = now_us();
@@ -2805,9 +2853,7 @@ int rfec_rx_session_push_datagrams(rfec_rx_session* S, uint32_t n, uint32_t dstr
     if (!t_rv.sm && (e = hipStreamCreateWithFlags(&t_rv.sm, hipStreamNonBlocking)) != hipSuccess)
         return set_err(RFEC_EDEVICE, "recv: stream", e);
     const uint32_t stride = S->stride;
-    const size_t o_dl = RX_ALIGN((size_t)n * dstride), o_rec = RX_ALIGN(o_dl + (size_t)n * 2);
-    const size_t o_pay = RX_ALIGN(o_rec + (size_t)n * sizeof(rfec_wire_rec));
-    const size_t need = RX_ALIGN(o_pay + (size_t)n * stride);
+    const size_t o_dl = RX_ALIGN((size_t)n * dstride), need = RX_ALIGN(o_dl + (size_t)n * 2);
     if (t_rv.db < need) {
         if (t_rv.d)
             (void)hipFree(t_rv.d);
@@ -2822,21 +2868,32 @@ int rfec_rx_session_push_datagrams(rfec_rx_session* S, uint32_t n, uint32_t dstr
     int rc;
     if ((rc = rx_reserve(RX_ALIGN((size_t)n * sizeof(rfec_wire_rec)), 0, 0)))
         return rc;
+    /* the payload rows are parsed straight into the arena's next n rows */
+    if ((rc = rx_session_room(S, n, t_rv.sm)))
+        return rc;
     double tt = now_us();
-    if ((e = hipMemcpyAsync(D, dgram, (size_t)n * dstride, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess ||
-        (e = hipMemcpyAsync(D + o_dl, dlen, (size_t)n * 2, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess)
-        return set_err(RFEC_EDEVICE, "recv: datagrams H2D", e);
+    /* datagrams in pinned memory (the UDP batch slots) are read by the parse
+     * itself; pageable ones are copied first.  The records go straight to the
+     * pinned staging area. */
+    const uint8_t* dg = host_mapped(dgram);
+    const uint8_t* dl = host_mapped(dlen);
+    if (!dg || !dl) {
+        if ((e = hipMemcpyAsync(D, dgram, (size_t)n * dstride, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess ||
+            (e = hipMemcpyAsync(D + o_dl, dlen, (size_t)n * 2, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess)
+            return set_err(RFEC_EDEVICE, "recv: datagrams H2D", e);
+        dg = D;
+        dl = D + o_dl;
+    }
     const double h2d_issue = now_us() - tt;
-    int ke = rfec_launch_wire_parse(n, dstride, D, (const uint16_t*)(D + o_dl), stride, S->capacity,
-                                    (rfec_wire_rec*)(D + o_rec), D + o_pay, max_dlen(dlen, n), t_rv.sm);
-    if (ke || (e = hipMemcpyAsync(t_rx.h, D + o_rec, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost,
-                                  t_rv.sm)) != hipSuccess ||
-        (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
+    int ke = rfec_launch_wire_parse(n, dstride, dg, (const uint16_t*)dl, stride, S->capacity,
+                                    (rfec_wire_rec*)t_rx.hd, S->arena + (size_t)S->nstore * stride,
+                                    max_dlen(dlen, n), t_rv.sm);
+    if (ke || (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
         return set_err(RFEC_EDEVICE, "recv: parse", ke ? ke : (int)e);
     const double staged = now_us() - tt;
     if (recs_out)
         memcpy(recs_out, t_rx.h, (size_t)n * sizeof(rfec_wire_rec));
-    rc = rx_session_push_staged(S, n, D + o_pay, out, out_payload, max_out, n_out, rep, t_rv.sm);
+    rc = rx_session_push_staged(S, n, NULL, out, out_payload, max_out, n_out, rep, t_rv.sm);
     rep->h2d_us += h2d_issue;
     rep->kernel_us += staged - h2d_issue; /* the H2D completes inside this interval too */
     rep->total_us = now_us() - t0;

@@ -550,16 +550,22 @@ class RxSession:
                       "rfec_rx_session_push")
         return out[:nout.value], outp[:nout.value], rep
 
-    def push_datagrams(self, n, dstride, dgram, dlen, max_out=1 << 16, want_recs=False):
-        """dgram / dlen: HOST addresses of n datagram slots."""
+    def push_datagrams(self, n, dstride, dgram, dlen, max_out=1 << 16, want_recs=False, pinned_out=False):
+        """dgram / dlen: HOST addresses of n datagram slots.  pinned_out: the
+        payload output in pinned memory (the library gathers into it directly)."""
         out = np.zeros(max_out, RX_SEG_DTYPE)
-        outp = np.zeros((max_out, self.stride), np.uint8)
+        keep = None
+        if pinned_out:
+            outp, keep = self.n.pinned_array((max_out, self.stride), np.uint8)
+        else:
+            outp = np.zeros((max_out, self.stride), np.uint8)
         recs = np.zeros(n, WIRE_REC_DTYPE) if want_recs else None
         nout, rep = C.c_uint32(), rfec_rx_report()
         self.n._check(self.n.lib.rfec_rx_session_push_datagrams(
             self.h, n, dstride, dgram, dlen, None if recs is None else recs.ctypes.data, out.ctypes.data,
             outp.ctypes.data, max_out, C.byref(nout), C.byref(rep)), "rfec_rx_session_push_datagrams")
-        return out[:nout.value], outp[:nout.value], rep, recs
+        rows = outp[:nout.value].copy() if keep is not None else outp[:nout.value]
+        return out[:nout.value], rows, rep, recs
 
     def evict(self, stream=None):
         self.n._check(self.n.lib.rfec_rx_session_evict(self.h, stream), "rfec_rx_session_evict")

@@ -260,13 +260,25 @@ def test_rx_session_split_invariance(lib, oracle1000, evict_every):
     sess.close()
 
 
-def test_rx_session_datagrams(lib, oracle1000):
-    """Datagram slots in host memory -> session (H2D, parse, ingestion), in batches."""
+@pytest.mark.parametrize("pinned", [False, True])
+def test_rx_session_datagrams(lib, oracle1000, pinned):
+    """Datagram slots in host memory -> session (parse, ingestion), in batches.
+    Pageable slots are copied to the device first; pinned ones (the UDP batch
+    slots) are read by the parse kernel itself, and a pinned payload output is
+    gathered into directly."""
     order, (sdg, sdl, fdg, fdl), _ = _sender_stream(lib, 600, 9)
     arrivals = _network(order, np.random.default_rng(4), loss=0.1, window=20, dup=0.02)
     n = len(arrivals)
-    dgram = np.zeros((n, DSTRIDE), np.uint8)
-    dlen = np.zeros(n, np.uint16)
+    keep = []
+    if pinned:
+        dgram, k1 = lib.pinned_array((n, DSTRIDE), np.uint8)
+        dlen, k2 = lib.pinned_array((n,), np.uint16)
+        keep += [k1, k2]
+        dgram[:] = 0
+        dlen[:] = 0
+    else:
+        dgram = np.zeros((n, DSTRIDE), np.uint8)
+        dlen = np.zeros(n, np.uint16)
     for a, (kind, i) in enumerate(arrivals):
         src, ln = (sdg, sdl) if kind == 0 else (fdg, fdl)
         dgram[a], dlen[a] = src[i], ln[i]
@@ -275,7 +287,7 @@ def test_rx_session_datagrams(lib, oracle1000):
     for a in range(0, n, 777):
         b = min(n, a + 777)
         out, outp, rep, r = sess.push_datagrams(b - a, DSTRIDE, dgram[a:].ctypes.data, dlen[a:].ctypes.data,
-                                                want_recs=True)
+                                                want_recs=True, max_out=4096, pinned_out=pinned)
         got.append(out)
         gotp.append(outp)
         recs.append(r)

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--batches", default="256,1024,4096")
     ap.add_argument("--evict-every", type=int, default=8)
     ap.add_argument("--lib", default="")
+    ap.add_argument("--pageable-out", action="store_true", help="payload output in pageable memory")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     lib = Native(1200, args.lib or None)
@@ -41,11 +42,15 @@ def main():
     lens = np.ctypeslib.as_array((C.c_uint16 * n).from_address(pin + n * DSTRIDE))
     slots[:] = dgram
     lens[:] = dlen
-    res = {"datagrams": n, "lib": args.lib or "in-tree", "evict_every": args.evict_every, "batches": {}}
+    res = {"datagrams": n, "lib": args.lib or "in-tree", "evict_every": args.evict_every,
+           "output": "pageable" if args.pageable_out else "pinned", "batches": {}}
     for B in [int(x) for x in args.batches.split(",")]:
         cap = B + 256
         out = np.zeros(cap, RX_SEG_DTYPE)
-        outp = np.zeros((cap, STRIDE), np.uint8)
+        if args.pageable_out:
+            outp = np.zeros((cap, STRIDE), np.uint8)
+        else:  # pinned, as a receive loop would keep its output rows
+            outp, keep = lib.pinned_array((cap, STRIDE), np.uint8)
         h = lib.lib.rfec_rx_session_create(STRIDE, S)
         nout, rep = C.c_uint32(), rfec_rx_report()
         tot = {"host_us": 0.0, "kernel_us": 0.0, "d2h_us": 0.0}
