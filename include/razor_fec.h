@@ -567,11 +567,25 @@ int rfec_rx_session_push(rfec_rx_session* s, uint32_t n, const rfec_wire_rec* re
                          rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out,
                          rfec_rx_report* report, void* stream);
 /* Received datagram slots in HOST memory (rfec_udp_recv_batch's output):
- * H2D, rfec_wire_parse, rfec_rx_session_push.  recs_out (HOST, may be NULL)
- * receives the n parse records. */
+ * rfec_wire_parse, rfec_rx_session_push.  Pinned slots (rfec_pinned_alloc)
+ * are read by the parse kernel itself, pageable ones copied first; a pinned
+ * out_payload is gathered into directly.  recs_out (HOST, may be NULL)
+ * receives the n parse records.  Refused while a pipelined batch is pending. */
 int rfec_rx_session_push_datagrams(rfec_rx_session* s, uint32_t n, uint32_t dstride, const uint8_t* dgram,
                                    const uint16_t* dlen, rfec_wire_rec* recs_out, rfec_rx_seg* out,
                                    uint8_t* out_payload, uint32_t max_out, uint32_t* n_out, rfec_rx_report* report);
+/* Pipelined form, one batch of latency: starts the parse of these n
+ * datagrams on the session's own stream, then ingests the batch the previous
+ * call started (control plane, peel) while the device parses this one, and
+ * returns THAT batch's recovered segments (recs_out: its records).  dgram /
+ * dlen must stay unchanged until the next call on the session returns.
+ * n == 0 only ingests the pending batch (the flush).  Deliveries, in total
+ * and in order, equal rfec_rx_session_push_datagrams over the same batches;
+ * rfec_rx_session_evict may come between calls. */
+int rfec_rx_session_push_datagrams_async(rfec_rx_session* s, uint32_t n, uint32_t dstride, const uint8_t* dgram,
+                                         const uint16_t* dlen, rfec_wire_rec* recs_out, rfec_rx_seg* out,
+                                         uint8_t* out_payload, uint32_t max_out, uint32_t* n_out,
+                                         rfec_rx_report* report);
 int rfec_rx_session_evict(rfec_rx_session* s, void* stream);
 int rfec_rx_session_get_info(const rfec_rx_session* s, rfec_rx_session_info* info);
 

@@ -2559,13 +2559,28 @@ int rfec_host_recv_datagrams(uint32_t n, uint32_t dstride, const uint8_t* dgram,
 /* Receiver session: rx_sim kept across calls, records by id in a host store, */
 /* their payload rows by id in an HBM arena                                   */
 /* ------------------------------------------------------------------------ */
+/* a batch of the pipelined push: its parse in flight on the session's stream */
+typedef struct {
+    rfec_wire_rec* rec;  /* pinned, device-mapped records */
+    rfec_wire_rec* recd; /* rec as the device addresses it */
+    uint32_t reccap;
+    uint8_t* dg; /* device copy of pageable datagram slots + lengths */
+    size_t dgb;
+    hipEvent_t done;
+} rx_stage;
+
 struct rfec_rx_session {
     rx_sim X;
     rfec_wire_rec* store; /* X.R */
     uint32_t nstore, storecap;
-    uint8_t* arena; /* [arows][stride] */
+    uint8_t* arena; /* [arows][stride]: rows [0, nstore) ingested, then the pending batch's */
     uint32_t arows;
     uint32_t stride, capacity;
+    /* pipelined push (rfec_rx_session_push_datagrams_async) */
+    hipStream_t sa;
+    rx_stage st[2];
+    uint32_t pend_n; /* rows of the pending batch (arena rows [nstore, nstore + pend_n)) */
+    int pend;        /* its stage, -1: none */
 };
 
 rfec_rx_session* rfec_rx_session_create(uint32_t stride, uint32_t capacity)
@@ -2585,6 +2600,7 @@ rfec_rx_session* rfec_rx_session_create(uint32_t stride, uint32_t capacity)
     s->X.capacity = capacity;
     s->stride = stride;
     s->capacity = capacity;
+    s->pend = -1;
     return s;
 }
 
@@ -2592,6 +2608,18 @@ void rfec_rx_session_destroy(rfec_rx_session* s)
 {
     if (!s)
         return;
+    if (s->sa) /* a pending parse still writes into the arena */
+        (void)hipStreamSynchronize(s->sa);
+    for (int i = 0; i < 2; ++i) {
+        if (s->st[i].rec)
+            (void)hipHostFree(s->st[i].rec);
+        if (s->st[i].dg)
+            (void)hipFree(s->st[i].dg);
+        if (s->st[i].done)
+            (void)hipEventDestroy(s->st[i].done);
+    }
+    if (s->sa)
+        (void)hipStreamDestroy(s->sa);
     rx_sim_free(&s->X);
     free(s->store);
     if (s->arena)
@@ -2602,12 +2630,17 @@ void rfec_rx_session_destroy(rfec_rx_session* s)
 /* Keeps only what the open state refers to: the flexes still registered (with
  * their slot / line tables), the records of cached segments and of those
  * flexes' members and parities (their rows gathered into a fresh arena with
- * room for `extra` more), the headers of cached recovered segments. */
+ * room for `extra` more), the headers of cached recovered segments.  The rows
+ * of a pending pipelined batch (parsed, not ingested) move along behind the
+ * kept ones. */
 static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
 {
+    const uint32_t tail = S->pend >= 0 ? S->pend_n : 0;
+    hipError_t e;
+    if (tail && (e = hipEventSynchronize(S->st[S->pend].done)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx session: pending parse", e);
     rx_sim* X = &S->X;
     int rc = RFEC_OK;
-    hipError_t e;
     const uint32_t ng_live = X->flex_of.n;
     rx_inst* NG = (rx_inst*)malloc(((size_t)ng_live + 1) * sizeof(rx_inst));
     uint32_t nslot = 0, nline = 0;
@@ -2683,8 +2716,8 @@ static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
             X->cache.v[i] = (c & 0x80000000u) ? (0x80000000u | (hmap_[c & 0x7FFFFFFFu] - 1)) : rmap[c - 1];
     }
     /* 4. records (host) and rows (device) */
-    uint32_t* gmap = (uint32_t*)malloc(((size_t)nr + 1) * sizeof(uint32_t)); /* new -> old */
-    const uint32_t arows = 2 * (nr + extra) > 4096 ? 2 * (nr + extra) : 4096;
+    uint32_t* gmap = (uint32_t*)malloc(((size_t)nr + tail + 1) * sizeof(uint32_t)); /* new -> old */
+    const uint32_t arows = 2 * (nr + tail + extra) > 4096 ? 2 * (nr + tail + extra) : 4096;
     uint8_t* arena = NULL;
     if (!gmap) {
         rc = set_err(RFEC_ENOMEM, "rx session: compaction", 0);
@@ -2695,6 +2728,8 @@ static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
             gmap[rmap[r] - 1] = r;
             S->store[rmap[r] - 1] = S->store[r]; /* rmap[r] - 1 <= r: in place, ascending */
         }
+    for (uint32_t t = 0; t < tail; ++t)
+        gmap[nr + t] = S->nstore + t;
     S->nstore = nr;
     X->R = S->store;
     for (uint32_t h = 0; h < X->nrh; ++h)
@@ -2706,12 +2741,13 @@ static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
         rc = set_err(RFEC_ENOMEM, "rx session: arena", e);
         goto done;
     }
-    if (nr) {
+    if (nr + tail) {
         int32_t* dmap = NULL;
         int ke = 0;
-        if ((e = hipMalloc((void**)&dmap, (size_t)nr * sizeof(int32_t))) != hipSuccess ||
-            (e = hipMemcpyAsync(dmap, gmap, (size_t)nr * sizeof(int32_t), hipMemcpyHostToDevice, sm)) != hipSuccess ||
-            (ke = rfec_launch_gather_rows(arena, S->arena, dmap, nr, S->stride, sm)) != 0 ||
+        const uint32_t nm = nr + tail;
+        if ((e = hipMalloc((void**)&dmap, (size_t)nm * sizeof(int32_t))) != hipSuccess ||
+            (e = hipMemcpyAsync(dmap, gmap, (size_t)nm * sizeof(int32_t), hipMemcpyHostToDevice, sm)) != hipSuccess ||
+            (ke = rfec_launch_gather_rows(arena, S->arena, dmap, nm, S->stride, sm)) != 0 ||
             (e = hipStreamSynchronize(sm)) != hipSuccess) {
             if (dmap)
                 (void)hipFree(dmap);
@@ -2757,11 +2793,12 @@ done:
 static int rx_session_room(rfec_rx_session* S, uint32_t n, hipStream_t sm)
 {
     int rc;
-    if (S->nstore + n > S->arows && (rc = rx_compact(S, n, sm)))
+    const uint32_t tail = S->pend >= 0 ? S->pend_n : 0; /* a pending pipelined batch's rows */
+    if (S->nstore + tail + n > S->arows && (rc = rx_compact(S, n, sm)))
         return rc;
-    if (S->nstore + n > S->storecap) {
+    if (S->nstore + tail + n > S->storecap) {
         uint32_t c = S->storecap ? S->storecap : 4096;
-        while (c < S->nstore + n)
+        while (c < S->nstore + tail + n)
             c *= 2;
         rfec_wire_rec* p = (rfec_wire_rec*)realloc(S->store, (size_t)c * sizeof(rfec_wire_rec));
         if (!p)
@@ -2772,12 +2809,12 @@ static int rx_session_room(rfec_rx_session* S, uint32_t n, hipStream_t sm)
     return RFEC_OK;
 }
 
-/* records already on the host (t_rx.h[0, n)), payload rows on the device at
+/* records already on the host (rh[0, n)), payload rows on the device at
  * `payload`, or already in the arena's next n rows (payload NULL; the caller
  * made the room) */
-static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const uint8_t* payload, rfec_rx_seg* out,
-                                  uint8_t* out_payload, uint32_t max_out, uint32_t* n_out, rfec_rx_report* rep,
-                                  hipStream_t sm)
+static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const rfec_wire_rec* rh, const uint8_t* payload,
+                                  rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out,
+                                  rfec_rx_report* rep, hipStream_t sm)
 {
     rx_sim* X = &S->X;
     hipError_t e;
@@ -2785,7 +2822,7 @@ static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const uint8_t*
     if (payload && (rc = rx_session_room(S, n, sm)))
         return rc;
     X->R = S->store;
-    memcpy(S->store + S->nstore, t_rx.h, (size_t)n * sizeof(rfec_wire_rec));
+    memcpy(S->store + S->nstore, rh, (size_t)n * sizeof(rfec_wire_rec));
     if (payload) {
         double tt = now_us();
         if ((e = hipMemcpyAsync(S->arena + (size_t)S->nstore * S->stride, payload, (size_t)n * S->stride,
@@ -2816,6 +2853,8 @@ int rfec_rx_session_push(rfec_rx_session* S, uint32_t n, const rfec_wire_rec* re
     const double t0 = now_us();
     if (!S || !n_out || !rep || (n && (!recs || !payload)) || (max_out && (!out || !out_payload)))
         return set_err(RFEC_EINVAL, "rx session: bad argument", 0);
+    if (S->pend >= 0)
+        return set_err(RFEC_EINVAL, "rx session: a pipelined batch is pending (flush it: async push with n = 0)", 0);
     memset(rep, 0, sizeof(*rep));
     *n_out = 0;
     if (n == 0)
@@ -2831,7 +2870,8 @@ int rfec_rx_session_push(rfec_rx_session* S, uint32_t n, const rfec_wire_rec* re
         (e = hipStreamSynchronize(sm)) != hipSuccess)
         return set_err(RFEC_EDEVICE, "rx session: records D2H", e);
     rep->d2h_us += now_us() - tt;
-    rc = rx_session_push_staged(S, n, payload, out, out_payload, max_out, n_out, rep, sm);
+    rc = rx_session_push_staged(S, n, (const rfec_wire_rec*)t_rx.h, payload, out, out_payload, max_out, n_out, rep,
+                                sm);
     rep->total_us = now_us() - t0;
     return rc;
 }
@@ -2843,6 +2883,8 @@ int rfec_rx_session_push_datagrams(rfec_rx_session* S, uint32_t n, uint32_t dstr
     const double t0 = now_us();
     if (!S || !n_out || !rep || (n && (!dgram || !dlen)) || (max_out && (!out || !out_payload)))
         return set_err(RFEC_EINVAL, "rx session: bad argument", 0);
+    if (S->pend >= 0)
+        return set_err(RFEC_EINVAL, "rx session: a pipelined batch is pending (flush it: async push with n = 0)", 0);
     memset(rep, 0, sizeof(*rep));
     *n_out = 0;
     if (n == 0)
@@ -2893,11 +2935,117 @@ int rfec_rx_session_push_datagrams(rfec_rx_session* S, uint32_t n, uint32_t dstr
     const double staged = now_us() - tt;
     if (recs_out)
         memcpy(recs_out, t_rx.h, (size_t)n * sizeof(rfec_wire_rec));
-    rc = rx_session_push_staged(S, n, NULL, out, out_payload, max_out, n_out, rep, t_rv.sm);
+    rc = rx_session_push_staged(S, n, (const rfec_wire_rec*)t_rx.h, NULL, out, out_payload, max_out, n_out, rep,
+                                t_rv.sm);
     rep->h2d_us += h2d_issue;
     rep->kernel_us += staged - h2d_issue; /* the H2D completes inside this interval too */
     rep->total_us = now_us() - t0;
     return rc;
+}
+
+/* The pipelined push: this call starts batch i (H2D if pageable, parse into
+ * the arena's rows after the pending batch's, records into its stage's mapped
+ * area, on the session's own stream) and then ingests batch i-1 (control
+ * plane, peel on the thread's stream) while the device parses batch i. */
+static int rx_stage_reserve(rx_stage* st, uint32_t n, size_t dg_bytes)
+{
+    hipError_t e;
+    if (!st->done && (e = hipEventCreateWithFlags(&st->done, hipEventDisableTiming)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx session: event", e);
+    if (st->reccap < n) {
+        const uint32_t c = n + n / 4 + 64;
+        void* h = NULL;
+        void* d = NULL;
+        if ((e = hipHostMalloc(&h, (size_t)c * sizeof(rfec_wire_rec), hipHostMallocMapped)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "rx session: record stage", e);
+        if ((e = hipHostGetDevicePointer(&d, h, 0)) != hipSuccess) {
+            (void)hipHostFree(h);
+            return set_err(RFEC_EDEVICE, "rx session: record stage device view", e);
+        }
+        if (st->rec)
+            (void)hipHostFree(st->rec);
+        st->rec = (rfec_wire_rec*)h;
+        st->recd = (rfec_wire_rec*)d;
+        st->reccap = c;
+    }
+    if (dg_bytes > st->dgb) {
+        if (st->dg)
+            (void)hipFree(st->dg);
+        st->dg = NULL;
+        st->dgb = 0;
+        const size_t b = dg_bytes + dg_bytes / 4;
+        if ((e = hipMalloc((void**)&st->dg, b)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "rx session: datagram stage", e);
+        st->dgb = b;
+    }
+    return RFEC_OK;
+}
+
+int rfec_rx_session_push_datagrams_async(rfec_rx_session* S, uint32_t n, uint32_t dstride, const uint8_t* dgram,
+                                         const uint16_t* dlen, rfec_wire_rec* recs_out, rfec_rx_seg* out,
+                                         uint8_t* out_payload, uint32_t max_out, uint32_t* n_out, rfec_rx_report* rep)
+{
+    const double t0 = now_us();
+    if (!S || !n_out || !rep || (n && (!dgram || !dlen)) || (max_out && (!out || !out_payload)))
+        return set_err(RFEC_EINVAL, "rx session: bad argument", 0);
+    memset(rep, 0, sizeof(*rep));
+    *n_out = 0;
+    if (n && (dstride < 64 || dstride > RFEC_WIRE_MAX_DSTRIDE || dstride % 16))
+        return set_err(RFEC_EINVAL, "rx session: dstride must be a multiple of 16 in [64, 2048]", 0);
+    hipError_t e;
+    int rc;
+    if (!t_rv.sm && (e = hipStreamCreateWithFlags(&t_rv.sm, hipStreamNonBlocking)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "recv: stream", e);
+    if (!S->sa && (e = hipStreamCreateWithFlags(&S->sa, hipStreamNonBlocking)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx session: stream", e);
+    const int prev = S->pend;
+    const uint32_t p = prev >= 0 ? S->pend_n : 0;
+    int cur = -1;
+    if (n) {
+        /* 1. start batch i behind the pending one's rows */
+        cur = prev == 0 ? 1 : 0;
+        rx_stage* st = &S->st[cur];
+        const size_t o_dl = RX_ALIGN((size_t)n * dstride);
+        if ((rc = rx_session_room(S, n, t_rv.sm)) || (rc = rx_stage_reserve(st, n, o_dl + (size_t)n * 2)))
+            return rc;
+        double tt = now_us();
+        const uint8_t* dg = host_mapped(dgram);
+        const uint8_t* dl = host_mapped(dlen);
+        if (!dg || !dl) {
+            if ((e = hipMemcpyAsync(st->dg, dgram, (size_t)n * dstride, hipMemcpyHostToDevice, S->sa)) != hipSuccess ||
+                (e = hipMemcpyAsync(st->dg + o_dl, dlen, (size_t)n * 2, hipMemcpyHostToDevice, S->sa)) != hipSuccess)
+                return set_err(RFEC_EDEVICE, "rx session: datagrams H2D", e);
+            dg = st->dg;
+            dl = st->dg + o_dl;
+        }
+        rep->h2d_us += now_us() - tt;
+        const int ke = rfec_launch_wire_parse(n, dstride, dg, (const uint16_t*)dl, S->stride, S->capacity, st->recd,
+                                              S->arena + (size_t)(S->nstore + p) * S->stride, max_dlen(dlen, n),
+                                              S->sa);
+        if (ke || (e = hipEventRecord(st->done, S->sa)) != hipSuccess)
+            return set_err(RFEC_EDEVICE, "rx session: parse", ke ? ke : (int)e);
+    }
+    /* 2. ingest batch i-1 while the device parses batch i */
+    if (prev >= 0) {
+        rx_stage* ps = &S->st[prev];
+        double tt = now_us();
+        if ((e = hipEventSynchronize(ps->done)) != hipSuccess)
+            return set_err(RFEC_EDEVICE, "rx session: parse", e);
+        rep->kernel_us += now_us() - tt;
+        if (recs_out)
+            memcpy(recs_out, ps->rec, (size_t)p * sizeof(rfec_wire_rec));
+        S->pend = -1; /* its rows are the arena's next p rows now */
+        rc = rx_session_push_staged(S, p, ps->rec, NULL, out, out_payload, max_out, n_out, rep, t_rv.sm);
+        if (rc) {
+            S->pend = cur; /* batch i stays pending behind whatever was ingested */
+            S->pend_n = n;
+            return rc;
+        }
+    }
+    S->pend = cur;
+    S->pend_n = n;
+    rep->total_us = now_us() - t0;
+    return RFEC_OK;
 }
 
 int rfec_rx_session_evict(rfec_rx_session* S, void* stream)

@@ -248,6 +248,8 @@ _SIGS = {
                                        C.POINTER(rfec_rx_report), _P]),
     "rfec_rx_session_push_datagrams": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint32,
                                                  C.POINTER(C.c_uint32), C.POINTER(rfec_rx_report)]),
+    "rfec_rx_session_push_datagrams_async": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint32,
+                                                       C.POINTER(C.c_uint32), C.POINTER(rfec_rx_report)]),
     "rfec_rx_session_evict": (C.c_int, [_P, _P]),
     "rfec_rx_session_get_info": (C.c_int, [_P, C.POINTER(rfec_rx_session_info)]),
     "rfec_pinned_free": (None, [_P]),
@@ -564,6 +566,27 @@ class RxSession:
         self.n._check(self.n.lib.rfec_rx_session_push_datagrams(
             self.h, n, dstride, dgram, dlen, None if recs is None else recs.ctypes.data, out.ctypes.data,
             outp.ctypes.data, max_out, C.byref(nout), C.byref(rep)), "rfec_rx_session_push_datagrams")
+        rows = outp[:nout.value].copy() if keep is not None else outp[:nout.value]
+        return out[:nout.value], rows, rep, recs
+
+    def push_datagrams_async(self, n, dstride, dgram, dlen, max_out=1 << 16, want_recs=False, pinned_out=False):
+        """The pipelined push: starts these n datagrams (n = 0: flush) and returns
+        the PREVIOUS batch's (segments, payload rows, report, its records).  The
+        slots at dgram / dlen must stay unchanged until the next call."""
+        out = np.zeros(max_out, RX_SEG_DTYPE)
+        keep = None
+        if pinned_out:
+            outp, keep = self.n.pinned_array((max_out, self.stride), np.uint8)
+        else:
+            outp = np.zeros((max_out, self.stride), np.uint8)
+        prev = getattr(self, "_pend_n", 0)
+        recs = np.zeros(prev, WIRE_REC_DTYPE) if want_recs else None
+        nout, rep = C.c_uint32(), rfec_rx_report()
+        self.n._check(self.n.lib.rfec_rx_session_push_datagrams_async(
+            self.h, n, dstride, dgram, dlen, None if recs is None or prev == 0 else recs.ctypes.data,
+            out.ctypes.data, outp.ctypes.data, max_out, C.byref(nout), C.byref(rep)),
+            "rfec_rx_session_push_datagrams_async")
+        self._pend_n = n
         rows = outp[:nout.value].copy() if keep is not None else outp[:nout.value]
         return out[:nout.value], rows, rep, recs
 

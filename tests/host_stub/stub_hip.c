@@ -97,6 +97,11 @@ hipError_t hipEventCreate(hipEvent_t* e)
     *e = (hipEvent_t)malloc(1);
     return hipSuccess;
 }
+hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned flags)
+{
+    (void)flags;
+    return hipEventCreate(e);
+}
 hipError_t hipEventDestroy(hipEvent_t e)
 {
     free(e);

@@ -302,6 +302,79 @@ def test_rx_session_datagrams(lib, oracle1000, pinned):
     sess.close()
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+def test_rx_session_datagrams_async(lib, oracle1000, pinned):
+    """The pipelined push (rfec_rx_session_push_datagrams_async): random batch
+    sizes, evictions between calls (compaction with a parsed, not ingested
+    batch behind the kept rows), then the flush.  Deliveries, records and
+    payloads equal the synchronous push over the same batches with each
+    eviction at the same point of ingestion; a synchronous push is refused
+    while a batch is pending."""
+    order, (sdg, sdl, fdg, fdl), _ = _sender_stream(lib, 600, 9)
+    arrivals = _network(order, np.random.default_rng(5), loss=0.1, window=20, dup=0.02)
+    n = len(arrivals)
+    keep = []
+    if pinned:
+        dgram, k1 = lib.pinned_array((n, DSTRIDE), np.uint8)
+        dlen, k2 = lib.pinned_array((n,), np.uint16)
+        keep += [k1, k2]
+    else:
+        dgram = np.zeros((n, DSTRIDE), np.uint8)
+        dlen = np.zeros(n, np.uint16)
+    for a, (kind, i) in enumerate(arrivals):
+        src, ln = (sdg, sdl) if kind == 0 else (fdg, fdl)
+        dgram[a], dlen[a] = src[i], ln[i]
+    rng = np.random.default_rng(6)
+    cuts, a = [], 0
+    while a < n:
+        b = min(n, a + int(rng.integers(1, 1500)))
+        cuts.append((a, b))
+        a = b
+    evict_after = {j for j in range(len(cuts)) if rng.random() < 0.3}  # evict once batch j is ingested
+
+    def collect(parts):
+        out = np.concatenate([p[0] for p in parts])
+        outp = np.concatenate([p[1] for p in parts])
+        recs = np.concatenate([p[2] for p in parts if p[2] is not None and len(p[2])])
+        return out, outp, recs
+
+    # synchronous reference
+    sess = lib.rx_session(STRIDE, 1000)
+    ref = []
+    for j, (a, b) in enumerate(cuts):
+        out, outp, rep, r = sess.push_datagrams(b - a, DSTRIDE, dgram[a:].ctypes.data, dlen[a:].ctypes.data,
+                                                want_recs=True, max_out=4096)
+        ref.append((out, outp, r))
+        if j in evict_after:
+            sess.evict()
+    ref_info = sess.info()
+    sess.close()
+    # pipelined: call j starts batch j and ingests batch j - 1
+    sess = lib.rx_session(STRIDE, 1000)
+    got = []
+    for j, (a, b) in enumerate(cuts):
+        out, outp, rep, r = sess.push_datagrams_async(b - a, DSTRIDE, dgram[a:].ctypes.data, dlen[a:].ctypes.data,
+                                                      want_recs=True, max_out=4096, pinned_out=pinned)
+        got.append((out, outp, r))
+        if j == 0:
+            with pytest.raises(Exception):
+                sess.push_datagrams(1, DSTRIDE, dgram.ctypes.data, dlen.ctypes.data)
+        if j - 1 in evict_after:
+            sess.evict()
+    out, outp, rep, r = sess.push_datagrams_async(0, DSTRIDE, 0, 0, want_recs=True, max_out=4096,
+                                                  pinned_out=pinned)
+    got.append((out, outp, r))
+    if len(cuts) - 1 in evict_after:
+        sess.evict()
+    eo, eop, erecs = collect(ref)
+    go, gop, grecs = collect(got)
+    assert len(go) == len(eo) > 0
+    assert np.array_equal(go.view(np.uint8), eo.view(np.uint8)) and np.array_equal(gop, eop)
+    assert np.array_equal(grecs.view(np.uint8), erecs.view(np.uint8))
+    assert sess.info()["max_ts"] == ref_info["max_ts"]
+    sess.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("long_junk", [False, True])
 def test_recv_datagrams_wide_slots(oracle1000, long_junk):

@@ -5,7 +5,7 @@ session's eviction called every --evict-every pushes.  Reports per-push time
 and the report's host / device / D2H split; the recovered count must not depend
 on the batch size.  --lib loads another build of the library (A/B).
 
-Usage (GPU box): python tools/session_bench.py [--batches 256,1024,4096] [--lib path] [--out file.json]
+Usage (GPU box): python tools/session_bench.py [--batches 256,1024,4096] [--pipelined] [--lib path] [--out file.json]
 """
 from __future__ import annotations
 
@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--evict-every", type=int, default=8)
     ap.add_argument("--lib", default="")
     ap.add_argument("--pageable-out", action="store_true", help="payload output in pageable memory")
+    ap.add_argument("--pipelined", action="store_true",
+                    help="rfec_rx_session_push_datagrams_async: each call ingests the previous batch")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     lib = Native(1200, args.lib or None)
@@ -43,7 +45,8 @@ def main():
     slots[:] = dgram
     lens[:] = dlen
     res = {"datagrams": n, "lib": args.lib or "in-tree", "evict_every": args.evict_every,
-           "output": "pageable" if args.pageable_out else "pinned", "batches": {}}
+           "output": "pageable" if args.pageable_out else "pinned",
+           "push": "pipelined" if args.pipelined else "synchronous", "batches": {}}
     for B in [int(x) for x in args.batches.split(",")]:
         cap = B + 256
         out = np.zeros(cap, RX_SEG_DTYPE)
@@ -56,18 +59,19 @@ def main():
         tot = {"host_us": 0.0, "kernel_us": 0.0, "d2h_us": 0.0}
         recovered, pushes = 0, 0
         t0 = time.perf_counter()
-        for a in range(0, n, B):
-            m = min(B, n - a)
-            rc = lib.lib.rfec_rx_session_push_datagrams(h, m, DSTRIDE, slots[a:].ctypes.data, lens[a:].ctypes.data,
-                                                        None, out.ctypes.data, outp.ctypes.data, cap,
-                                                        C.byref(nout), C.byref(rep))
+        push = (lib.lib.rfec_rx_session_push_datagrams_async if args.pipelined else
+                lib.lib.rfec_rx_session_push_datagrams)
+        for a in list(range(0, n, B)) + ([n] if args.pipelined else []):
+            m = min(B, n - a)  # pipelined: a last call with m = 0 flushes
+            rc = push(h, m, DSTRIDE, slots[a:].ctypes.data if m else None, lens[a:].ctypes.data if m else None,
+                      None, out.ctypes.data, outp.ctypes.data, cap, C.byref(nout), C.byref(rep))
             if rc:
                 raise SystemExit(f"push failed: {lib.last_error()}")
             recovered += nout.value
             for f in tot:
                 tot[f] += getattr(rep, f)
-            pushes += 1
-            if args.evict_every and pushes % args.evict_every == 0:
+            pushes += m > 0
+            if m and args.evict_every and pushes % args.evict_every == 0:
                 lib.lib.rfec_rx_session_evict(h, None)
         dt = time.perf_counter() - t0
         lib.lib.rfec_rx_session_destroy(h)
