@@ -612,6 +612,7 @@ int rfec_rx_session_get_info(const rfec_rx_session* s, rfec_rx_session_info* inf
 #define RFEC_TUNE_SMALL_FUSED 4194304u /* small-slot disjoint decode (16 / 32 chunks): header checks in the payload lanes (k_decode_small), no header blocks */
 #define RFEC_TUNE_SMALL_B2 8388608u    /* with RFEC_TUNE_SMALL_FUSED: two fired lines per lane and pass (16-chunk slots) */
 #define RFEC_TUNE_LINEAR_BLOCKS 16777216u /* output-mapped row encode / decode: linear block order (default: XCD-swizzled) */
+#define RFEC_TUNE_LINE_LANES 33554432u /* row decode into a dense output: one lane per (group, row, chunk) (default: per (group, output slot, chunk)) */
 #define RFEC_TUNE_FLAT_DECODE 262144u /* disjoint-plan decode: one lane per (group, chunk column), every fired line (default: one lane per (group, line, chunk)) */
 /* (defaults: parity stores write-through, recovered stores non-temporal) */
 #define RFEC_TUNE_DIAG_NO_META 256u /* DIAGNOSTIC ONLY: skip fec_meta (wrong output) */

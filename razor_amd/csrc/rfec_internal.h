@@ -41,6 +41,7 @@ typedef struct {
 #define RFEC_KFLAG_SMALL_FUSED RFEC_TUNE_SMALL_FUSED
 #define RFEC_KFLAG_SMALL_B2 RFEC_TUNE_SMALL_B2
 #define RFEC_KFLAG_LINEAR_BLOCKS RFEC_TUNE_LINEAR_BLOCKS
+#define RFEC_KFLAG_LINE_LANES RFEC_TUNE_LINE_LANES
 
 int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, uint32_t capacity,
                        const uint8_t* shards, const rfec_hdr* hdr, uint8_t* parity, rfec_hdr* meta,

@@ -1585,8 +1585,11 @@ __global__ __launch_bounds__(kBlock) void k_decode_out(v4u* shards, const v4u* _
 // The same for the row layouts of the encode fast path (rows of COL
 // consecutive segments, K <= 64): the line masks and members are arithmetic
 // in the row index, so no plan is staged through LDS (no barrier before the
-// first load).
-template <int K, int COL, bool NTL, int NTS>
+// first load).  SLOTS (dense output): one lane per (group, output slot e,
+// chunk) instead of (group, row, chunk): slot e's target is the group's e-th
+// erased segment, recovered when its row fires, so no lane sits on a row
+// that does not (divRC divides by E C then).
+template <int K, int COL, bool NTL, int NTS, bool SLOTS>
 __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* __restrict__ parity, uint32_t total,
                                                         uint32_t C, FastDiv divC, FastDiv divRC,
                                                         uint32_t n_hdr_blocks, uint32_t hdr_every, PeelArgs A,
@@ -1611,17 +1614,32 @@ __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* 
         return;
     const uint32_t g = fdiv(t, divRC);
     const uint32_t rem = t - g * divRC.d;
-    const uint32_t r = fdiv(rem, divC);
-    const uint32_t j = rem - r * divC.d;
+    const uint32_t q0 = fdiv(rem, divC); // row, or output slot (SLOTS)
+    const uint32_t j = rem - q0 * divC.d;
     const uint64_t h = A.present[2 * g];
+    uint32_t r, tgt;
+    if constexpr (SLOTS) {
+        uint64_t m = ~h & (K == 64 ? ~0ull : (1ull << K) - 1ull);
+        for (uint32_t u = 0; u < q0; ++u) // the q0-th erased segment
+            m &= m - 1ull;
+        if (!m)
+            return;
+        tgt = (uint32_t)__ffsll((long long)m) - 1;
+        r = tgt / COL;
+    } else {
+        r = q0;
+    }
     const uint32_t cnt = r < (uint32_t)(R - 1) ? COL : LAST;
     const uint64_t rm = ((1ull << cnt) - 1ull) << (r * COL);
     const uint64_t miss = rm & ~h;
     if (__popcll(miss) != 1 || !((A.parity_present[g] >> r) & 1ull))
         return;
-    const uint32_t tgt = (uint32_t)__ffsll((long long)miss) - 1;
+    if constexpr (!SLOTS)
+        tgt = (uint32_t)__ffsll((long long)miss) - 1;
     v4u* dst = shards + ((size_t)g * K + tgt) * C + j;
-    if (D.E) {
+    if constexpr (SLOTS) {
+        dst = D.sh + ((size_t)g * D.E + q0) * C + j;
+    } else if (D.E) {
         const uint32_t e = (uint32_t)__popcll(~h & ((1ull << tgt) - 1ull));
         if (e >= D.E)
             return;
@@ -2003,20 +2021,27 @@ void launch_fused_out(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_
 #undef RFEC_FUSED_OUT
 }
 
-// row-layout fused decode: one lane per (group, row, chunk column)
+// row-layout fused decode: one lane per (group, row, chunk column), or per
+// (group, dense output slot, chunk column) when `slots`
 template <int K, int COL>
-void launch_fused_rows(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, uint32_t cd, bool swz)
+void launch_fused_rows(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, uint32_t cd, bool swz,
+                       bool slots)
 {
     constexpr uint32_t R = (K + COL - 1) / COL;
-    const uint32_t total = B.groups * R * cd; // < 2^32: checked by the caller
+    const uint32_t per = slots ? F.D.E : R;
+    const uint32_t total = B.groups * per * cd; // < 2^32: checked by the caller
     const uint32_t npay = blocks_for(total), npay8 = (npay + 7u) & ~7u, nhr = (F.n_hdr + 7u) >> 3;
     // swizzled: rounds of 8 blocks, nhr header rounds spread over npay8 / 8 payload rounds
     const dim3 grid(swz ? 8u * nhr + npay8 : F.n_hdr + npay);
     const uint32_t every = swz ? (F.spread && nhr ? (npay8 >> 3) / nhr : 0u) : hdr_every(F, npay);
-    const FastDiv dC = make_fastdiv(cd), dRC = make_fastdiv(R * cd);
+    const FastDiv dC = make_fastdiv(cd), dRC = make_fastdiv(per * cd);
 #define RFEC_FUSED_ROWS(NTL, NTS)                                                                                \
-    hipLaunchKernelGGL((k_decode_rows<K, COL, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards, F.parity,    \
-                       total, F.C, dC, dRC, F.n_hdr, every, B, M, F.D, swz ? npay8 : 0u)
+    if (slots)                                                                                                   \
+        hipLaunchKernelGGL((k_decode_rows<K, COL, NTL, NTS, true>), grid, dim3(kBlock), 0, F.stream, F.shards,    \
+                           F.parity, total, F.C, dC, dRC, F.n_hdr, every, B, M, F.D, swz ? npay8 : 0u);          \
+    else                                                                                                         \
+        hipLaunchKernelGGL((k_decode_rows<K, COL, NTL, NTS, false>), grid, dim3(kBlock), 0, F.stream, F.shards,   \
+                           F.parity, total, F.C, dC, dRC, F.n_hdr, every, B, M, F.D, swz ? npay8 : 0u)
     switch (sp) {
     case -1: RFEC_FUSED_ROWS(false, 1); break;
     case 0: RFEC_FUSED_ROWS(true, 0); break;
@@ -2355,10 +2380,12 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
                 // XCD-swizzled by default: decode traffic 1.077 vs 1.107 x algorithmic at k = 10 / 1,200 B,
                 // time within noise (130.0-130.4 vs 129.2 us, tools/gpu_xcd.sh)
                 const bool swz = !(flags & RFEC_KFLAG_LINEAR_BLOCKS);
+                // dense output: lanes per output slot (no lane on a row that does not fire)
+                const bool slots = F.D.E && F.D.E <= P.n_lines && !(flags & RFEC_KFLAG_LINE_LANES);
                 if (P.k == 10)
-                    launch_fused_rows<10, 4>(F, sp, B, *M, cd, swz);
+                    launch_fused_rows<10, 4>(F, sp, B, *M, cd, swz, slots);
                 else
-                    launch_fused_rows<32, 4>(F, sp, B, *M, cd, swz);
+                    launch_fused_rows<32, 4>(F, sp, B, *M, cd, swz, slots);
                 return (int)hipGetLastError();
             }
             if (maxc <= 4)

@@ -20,7 +20,8 @@ TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "plain_stores": 4, "ite
            "generic_plain": 3, "two_kernel": 4096, "two_kernel_wt": 4096 | 64, "group_wave": 8192,
            "group_wave_xcd": 8192 | 16384, "xcd": 16384, "lds_hdr_peel": 32768, "flat_encode": 65536,
            "meta_tail": 131072, "meta_tail_nt": 131072 | 512, "flat_decode": 262144, "hdr_head": 524288,
-           "out_decode": 2097152, "out_decode_head": 2097152 | 524288, "small_fused": 4194304, "small_b2": 4194304 | 8388608, "linear": 16777216}
+           "out_decode": 2097152, "out_decode_head": 2097152 | 524288, "small_fused": 4194304, "small_b2": 4194304 | 8388608, "linear": 16777216,
+           "line_lanes": 33554432}
 
 
 @pytest.fixture(scope="module")
@@ -584,7 +585,7 @@ def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tunin
 @pytest.mark.parametrize("k,col,S", [(10, 4, 1200), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 64),
                                      (96, 4, 512), (20, 3, 256)])
 @pytest.mark.parametrize("tuning", ["default", "flat_decode", "out_decode", "hdr_head", "generic", "small_fused",
-                                    "small_b2", "xcd", "linear"])
+                                    "small_b2", "xcd", "linear", "line_lanes"])
 def test_dense_output_decode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning):
     """rfec_recover_batch_out (recovered segments into a dense output, as
     flex_fec_recover's caller-allocated out_seg): row plans with up to 6
@@ -624,7 +625,7 @@ def test_dense_output_decode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning)
             if (m >> i) & 1:
                 rh[g, i]["size"] = min(cap, int(rh[g, i]["size"]) + 5)
     e_s, e_h, e_rec = o.recover_batch(plan, rx, rh, present, parity, meta, fs_rx, pp, cap)
-    for E in (1, 3):
+    for E in (1, 2, 3):
         out_s, out_h, out_i, rec = gpu(tuning=TUNINGS[tuning]).recover_out(plan, rx, rh, present, parity, meta,
                                                                            fs_rx, pp, cap, E)
         n_rec = 0
