@@ -448,6 +448,49 @@ __global__ __launch_bounds__(kBlock) void k_encode_out(const v4u* __restrict__ s
     st16<NTS>(parity + ((size_t)g * R + r) * C + j, acc);
 }
 
+// The same for any row layout with rows of at most CMAX members (k, col
+// runtime: the strip-mode plans of flex_fec_sender_num_packets, :112-132);
+// the lane's member loads stay unrolled, predicated on the row's size.
+template <int CMAX, bool NTL, int NTS>
+__global__ __launch_bounds__(kBlock) void k_encode_out_rt(const v4u* __restrict__ shards, v4u* __restrict__ parity,
+                                                          uint32_t total, uint32_t C, FastDiv divC, FastDiv divRC,
+                                                          uint32_t K, uint32_t COL, uint32_t swz_head, EncMeta E,
+                                                          rfec_kplan P)
+{
+    if (blockIdx.x < E.n_meta_blocks) {
+        meta_block(blockIdx.x, E.hdr_dw, E.meta_dw, E.fsize, E.status, E.groups, E.capacity, E.gpb, P);
+        return;
+    }
+    uint32_t b = blockIdx.x - E.n_meta_blocks;
+    if (swz_head) { // XCD swizzle: swz_head = meta + padding blocks, a multiple of 8
+        if (blockIdx.x < swz_head)
+            return;
+        b = xcd_block(blockIdx.x - swz_head, gridDim.x - swz_head, 1);
+    }
+    const uint32_t t = b * kBlock + threadIdx.x;
+    if (t >= total)
+        return;
+    const uint32_t R = divRC.d / divC.d;
+    const uint32_t g = fdiv(t, divRC);
+    const uint32_t rem = t - g * divRC.d;
+    const uint32_t r = fdiv(rem, divC);
+    const uint32_t j = rem - r * divC.d;
+    const uint32_t cnt = r + 1 < R ? COL : K - (R - 1) * COL;
+    const v4u* s = shards + ((size_t)g * K + (size_t)r * COL) * C + j;
+    v4u v[CMAX];
+#pragma unroll
+    for (int q = 0; q < CMAX; ++q) {
+        v[q] = v4u{0, 0, 0, 0};
+        if ((uint32_t)q < cnt)
+            v[q] = ld16<NTL>(s + (size_t)q * C);
+    }
+    v4u acc = v[0];
+#pragma unroll
+    for (int q = 1; q < CMAX; ++q)
+        acc ^= v[q];
+    st16<NTS>(parity + ((size_t)g * R + r) * C + j, acc);
+}
+
 // ---------------------------------------------------------------------------
 // Encode payload, rows-of-COL, group-per-wave mapping.  Every wave covers
 // whole groups (gpw = max(1, 64 / cd) of them, NI items per lane): a slot's
@@ -1524,7 +1567,11 @@ __global__ __launch_bounds__(kBlock) void k_decode_small(v4u* shards, const v4u*
 // of one slot, and no lane carries a second line (the flat (group, chunk)
 // form serialises two lines' loads per lane).  tools/decode_lab.hip, cold
 // parity: 142.7 us vs 157.8 us flat at k = 10 / 1,200 B.
-template <int MAXC, bool NTL, int NTS>
+// SLOTS (dense output): one lane per (group, output slot e, chunk column)
+// instead: slot e's target is the group's e-th erased segment and its line
+// comes from a segment -> line table (disjoint plan), so no lane sits on a
+// line that does not fire (divLC divides by E C then).
+template <int MAXC, bool NTL, int NTS, bool SLOTS>
 __global__ __launch_bounds__(kBlock) void k_decode_out(v4u* shards, const v4u* __restrict__ parity, uint32_t total,
                                                        uint32_t C, FastDiv divC, FastDiv divLC,
                                                        uint32_t n_hdr_blocks, uint32_t hdr_every, PeelArgs A,
@@ -1537,10 +1584,22 @@ __global__ __launch_bounds__(kBlock) void k_decode_out(v4u* shards, const v4u* _
     }
     __shared__ uint32_t lplan[RFEC_MAX_LINES];
     __shared__ uint64_t lmask[RFEC_MAX_LINES][2];
+    __shared__ uint8_t sline[SLOTS ? RFEC_MAX_K : 1]; // segment -> its line (0xFF: none)
     const rfec_kplan& P = M.plan;
     if (threadIdx.x < P.n_lines) {
         lmask[threadIdx.x][0] = M.mask[threadIdx.x][0];
         lmask[threadIdx.x][1] = M.mask[threadIdx.x][1];
+    }
+    if constexpr (SLOTS) {
+        if (threadIdx.x < P.k) {
+            const uint32_t i = threadIdx.x;
+            uint32_t li = 0xFF;
+            for (uint32_t q = 0; q < P.n_lines; ++q) { // (uniform loads of the line masks)
+                const uint64_t w = i < 64 ? M.mask[q][0] : M.mask[q][1];
+                li = (w >> (i & 63)) & 1ull ? q : li;
+            }
+            sline[i] = (uint8_t)li;
+        }
     }
     stage_plan(lplan, P); // ends in a barrier
     const uint32_t t = pb * kBlock + threadIdx.x;
@@ -1548,18 +1607,37 @@ __global__ __launch_bounds__(kBlock) void k_decode_out(v4u* shards, const v4u* _
         return;
     const uint32_t g = fdiv(t, divLC);
     const uint32_t rem = t - g * divLC.d;
-    const uint32_t l = fdiv(rem, divC);
-    const uint32_t j = rem - l * divC.d;
+    const uint32_t q0 = fdiv(rem, divC); // line, or output slot (SLOTS)
+    const uint32_t j = rem - q0 * divC.d;
+    const uint64_t h0 = A.present[2 * g], h1 = A.present[2 * g + 1];
+    uint32_t l = q0, tgt = 0;
+    if constexpr (SLOTS) { // the q0-th erased segment among [0, k)
+        const uint32_t k = P.k;
+        uint64_t m0 = ~h0 & (k >= 64 ? ~0ull : (1ull << k) - 1ull);
+        uint64_t m1 = k > 64 ? ~h1 & (k >= 128 ? ~0ull : (1ull << (k - 64)) - 1ull) : 0ull;
+        const uint32_t c0 = (uint32_t)__popcll(m0);
+        uint64_t m = q0 < c0 ? m0 : m1;
+        for (uint32_t u = 0, ue = q0 < c0 ? q0 : q0 - c0; u < ue; ++u)
+            m &= m - 1ull;
+        if (!m)
+            return;
+        tgt = (q0 < c0 ? 0u : 64u) + (uint32_t)__ffsll((long long)m) - 1;
+        l = sline[tgt];
+        if (l == 0xFFu)
+            return;
+    }
     if (!((A.parity_present[g] >> l) & 1ull))
         return;
-    const uint64_t h0 = A.present[2 * g], h1 = A.present[2 * g + 1];
     const uint64_t x0 = lmask[l][0] & ~h0, x1 = lmask[l][1] & ~h1;
     if (__popcll(x0) + __popcll(x1) != 1 || ((lmask[l][0] & h0) | (lmask[l][1] & h1)) == 0)
         return;
-    const uint32_t tgt = x0 ? (uint32_t)__ffsll((long long)x0) - 1 : 64u + (uint32_t)__ffsll((long long)x1) - 1;
+    if constexpr (!SLOTS)
+        tgt = x0 ? (uint32_t)__ffsll((long long)x0) - 1 : 64u + (uint32_t)__ffsll((long long)x1) - 1;
     v4u* grp = shards + (size_t)g * P.k * C + j;
     v4u* dst = grp + (size_t)tgt * C;
-    if (D.E) {
+    if constexpr (SLOTS) {
+        dst = D.sh + ((size_t)g * D.E + q0) * C + j;
+    } else if (D.E) {
         const uint32_t e = missing_rank(h0, h1, tgt);
         if (e >= D.E)
             return;
@@ -1864,6 +1942,20 @@ hipError_t launch_rows_out(const EncLaunch& a, unsigned flags)
     return hipGetLastError();
 }
 
+template <int CMAX, bool NTL, int NTS>
+hipError_t launch_rows_out_rt(const EncLaunch& a, unsigned flags, uint32_t col)
+{
+    const uint32_t K = a.P->k, R = (K + col - 1) / col;
+    const uint64_t total = (uint64_t)a.groups * R * a.cd; // < 2^32: checked by the caller
+    const uint32_t nb = blocks_for(total);
+    const bool swz = !(flags & RFEC_KFLAG_LINEAR_BLOCKS);
+    const uint32_t head = swz ? (a.E.n_meta_blocks + 7u) & ~7u : 0u;
+    hipLaunchKernelGGL((k_encode_out_rt<CMAX, NTL, NTS>), dim3((swz ? head : a.E.n_meta_blocks) + nb), dim3(kBlock),
+                       0, a.stream, a.s, a.p, (uint32_t)total, a.stride / 16, make_fastdiv(a.cd),
+                       make_fastdiv(R * a.cd), K, col, head, a.E, *a.P);
+    return hipGetLastError();
+}
+
 template <int K, int COL, bool NTL, int NTS>
 hipError_t launch_rows_v(const EncLaunch& a, unsigned flags)
 {
@@ -2000,17 +2092,21 @@ uint32_t next_gen()
 
 // output-mapped fused decode: one lane per (group, line, chunk column)
 template <int MAXC>
-void launch_fused_out(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, uint32_t cd)
+void launch_fused_out(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, uint32_t cd, bool slots)
 {
-    const uint32_t NL = M.plan.n_lines;
-    const uint32_t total = B.groups * NL * cd; // < 2^32: checked by the caller
+    const uint32_t per = slots ? F.D.E : M.plan.n_lines;
+    const uint32_t total = B.groups * per * cd; // < 2^32: checked by the caller
     const uint32_t npay = blocks_for(total);
     const dim3 grid(F.n_hdr + npay);
-    const FastDiv dC = make_fastdiv(cd), dLC = make_fastdiv(NL * cd);
+    const FastDiv dC = make_fastdiv(cd), dLC = make_fastdiv(per * cd);
     const uint32_t every = hdr_every(F, npay);
 #define RFEC_FUSED_OUT(NTL, NTS)                                                                                 \
-    hipLaunchKernelGGL((k_decode_out<MAXC, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards, F.parity, total, \
-                       F.C, dC, dLC, F.n_hdr, every, B, M, F.D)
+    if (slots)                                                                                                   \
+        hipLaunchKernelGGL((k_decode_out<MAXC, NTL, NTS, true>), grid, dim3(kBlock), 0, F.stream, F.shards,       \
+                           F.parity, total, F.C, dC, dLC, F.n_hdr, every, B, M, F.D);                           \
+    else                                                                                                         \
+        hipLaunchKernelGGL((k_decode_out<MAXC, NTL, NTS, false>), grid, dim3(kBlock), 0, F.stream, F.shards,      \
+                           F.parity, total, F.C, dC, dLC, F.n_hdr, every, B, M, F.D)
     switch (sp) {
     case -1: RFEC_FUSED_OUT(false, 1); break;
     case 0: RFEC_FUSED_OUT(true, 0); break;
@@ -2155,6 +2251,15 @@ hipError_t launch_encode_t(const EncLaunch& a, unsigned flags)
             return launch_rows_v<10, 4, NTL, NTS>(a, flags);
         if (P->k == 32 && col == 4)
             return launch_rows_v<32, 4, NTL, NTS>(a, flags);
+        // other row layouts: the same output-mapped lanes with k and col at run time
+        if (!(flags & (RFEC_KFLAG_FLAT_ENCODE | RFEC_KFLAG_GROUP_WAVE | RFEC_KFLAG_ITEMS2)) && col <= 16 &&
+            (uint64_t)a.groups * ((P->k + col - 1) / col) * a.cd < (1ull << 32)) {
+            // (an 8-wide instantiation compiled to 230 VGPRs, two waves per SIMD: 0.33 of 8 TB/s at k = 20,
+            // col = 5, so rows of 5..16 take the 16-wide one, 74 VGPRs)
+            if (col <= 4)
+                return launch_rows_out_rt<4, NTL, NTS>(a, flags, col);
+            return launch_rows_out_rt<16, NTL, NTS>(a, flags, col);
+        }
     }
     const uint32_t C = a.stride / 16;
     const uint32_t total = a.groups * a.cd;
@@ -2375,13 +2480,13 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
         if (!two && !(flags & RFEC_KFLAG_FLAT_DECODE) && (cd >= (uint32_t)kWave || (flags & RFEC_KFLAG_OUT_DECODE)) &&
             (uint64_t)groups * P.n_lines * cd < (1ull << 32)) {
             uint32_t col = 0;
+            // dense output: lanes per output slot (no lane on a line that does not fire)
+            const bool slots = F.D.E && F.D.E <= P.n_lines && !(flags & RFEC_KFLAG_LINE_LANES);
             if (!(flags & RFEC_KFLAG_GENERIC) && is_row_layout(&P, &col) && col == 4 &&
                 (P.k == 10 || P.k == 32)) {
                 // XCD-swizzled by default: decode traffic 1.077 vs 1.107 x algorithmic at k = 10 / 1,200 B,
                 // time within noise (130.0-130.4 vs 129.2 us, tools/gpu_xcd.sh)
                 const bool swz = !(flags & RFEC_KFLAG_LINEAR_BLOCKS);
-                // dense output: lanes per output slot (no lane on a row that does not fire)
-                const bool slots = F.D.E && F.D.E <= P.n_lines && !(flags & RFEC_KFLAG_LINE_LANES);
                 if (P.k == 10)
                     launch_fused_rows<10, 4>(F, sp, B, *M, cd, swz, slots);
                 else
@@ -2389,9 +2494,9 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
                 return (int)hipGetLastError();
             }
             if (maxc <= 4)
-                launch_fused_out<4>(F, sp, B, *M, cd);
+                launch_fused_out<4>(F, sp, B, *M, cd, slots);
             else
-                launch_fused_out<8>(F, sp, B, *M, cd);
+                launch_fused_out<8>(F, sp, B, *M, cd, slots);
             return (int)hipGetLastError();
         }
         if (maxc <= 4 && two)

@@ -21,7 +21,7 @@ TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "plain_stores": 4, "ite
            "group_wave_xcd": 8192 | 16384, "xcd": 16384, "lds_hdr_peel": 32768, "flat_encode": 65536,
            "meta_tail": 131072, "meta_tail_nt": 131072 | 512, "flat_decode": 262144, "hdr_head": 524288,
            "out_decode": 2097152, "out_decode_head": 2097152 | 524288, "small_fused": 4194304, "small_b2": 4194304 | 8388608, "linear": 16777216,
-           "line_lanes": 33554432}
+           "line_lanes": 33554432, "out_decode_lines": 2097152 | 33554432}
 
 
 @pytest.fixture(scope="module")
@@ -585,7 +585,7 @@ def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tunin
 @pytest.mark.parametrize("k,col,S", [(10, 4, 1200), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 64),
                                      (96, 4, 512), (20, 3, 256)])
 @pytest.mark.parametrize("tuning", ["default", "flat_decode", "out_decode", "hdr_head", "generic", "small_fused",
-                                    "small_b2", "xcd", "linear", "line_lanes"])
+                                    "small_b2", "xcd", "linear", "line_lanes", "out_decode_lines"])
 def test_dense_output_decode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning):
     """rfec_recover_batch_out (recovered segments into a dense output, as
     flex_fec_recover's caller-allocated out_seg): row plans with up to 6
@@ -652,3 +652,30 @@ def test_dense_output_rejects_cascading_plans(product):
     plan = product.plan_from_fraction(10, 80, 3)
     with pytest.raises(Exception):
         product.recover_batch_out(plan, 1, 1008, 1000, 16, 16, 16, 16, 16, 16, 16, 16, 2, 16, 16, 16, 16)
+
+
+@pytest.mark.parametrize("k,col,S", [(12, 4, 1200), (24, 4, 1200), (12, 2, 16), (16, 8, 128), (20, 3, 256),
+                                     (96, 4, 512), (50, 16, 1000), (7, 7, 1000), (100, 20, 64)])
+@pytest.mark.parametrize("tuning", ["default", "linear", "generic"])
+def test_row_plan_encode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning):
+    """Row layouts other than the compiled k = 10 / 32 ones (strip-mode plans,
+    flex_fec_sender.c:112-132) through the run-time-k output-mapped encode
+    (rows of up to 16 members; wider rows take the plan-driven kernel):
+    parity bytes, meta records, sizes and status equal the oracle's on ragged
+    segments."""
+    o = oracle1200 if S > 1000 else oracle1000
+    rows = (k + col - 1) // col
+    plan = o.plan_matrix(k, rows, col, 1)
+    G = 300
+    shards, hdr = o.fill_groups(61 + k, G, k, S, ragged=True)
+    cap = min(o.video_size, S)
+    e_p, e_m, e_f, e_s = o.encode_batch(plan, shards, hdr, cap)
+    p, m, f, s = gpu(tuning=TUNINGS[tuning]).encode(plan, shards, hdr, cap)
+    assert np.array_equal(s, e_s) and np.array_equal(f, e_f)
+    ok = e_s == 0
+    assert np.array_equal(m[ok], e_m[ok])
+    for g in range(G):
+        for l in range(plan.n_lines):
+            if ok[g, l]:
+                L = int(e_f[g, l])
+                assert np.array_equal(p[g, l, :L], e_p[g, l, :L]), f"group {g} line {l}"
