@@ -527,14 +527,17 @@ def main():
         lines = [w.plan.line[l].count for l in range(w.n)]
         rows_layout = not full_plan and len(set(lines[:-1])) <= 1
         enc_kernel = (f"k_encode_out<{k},{lines[0]}>" if rows_layout and (k, lines[0]) in ((10, 4), (32, 4))
-                      else (f"k_encode_matrix<{k},{w.plan.col}>" if full_plan else "k_encode (plan-driven)"))
+                      else ("k_encode_out_rt (run-time k, col)" if rows_layout and lines[0] <= 16
+                            else (f"k_encode_matrix<{k},{w.plan.col}>" if full_plan else "k_encode (plan-driven)")))
         cd = (S + 15) // 16
+        per = ("one lane per (group, output slot, chunk)" if w.dense and 2 <= len(lines)
+               else "one lane per (group, line, chunk)")
         if full_plan:
             dec_kernels = "k_decode_cascade + k_decode_fixup (one launch + fix-up, in place)"
         elif cd >= 64 and rows_layout and (k, lines[0]) in ((10, 4), (32, 4)):
-            dec_kernels = f"k_decode_rows<{k},{lines[0]}> (one lane per (group, row, chunk); header blocks spread)"
+            dec_kernels = f"k_decode_rows<{k},{lines[0]}> ({per}; header blocks spread)"
         elif cd >= 64:
-            dec_kernels = "k_decode_out (one lane per (group, line, chunk); header blocks spread)"
+            dec_kernels = f"k_decode_out ({per}; header blocks spread)"
         else:
             dec_kernels = "k_decode_disjoint (one lane per (group, chunk), every fired line; header blocks spread)"
         if full_plan:
