@@ -6,7 +6,7 @@
 // build (tools/wire_lab.sh does all variants):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Irazor_amd/csrc [-DRFEC_WIRE_DIAG_NO_CRC ...] \
 //         tools/wire_lab.hip -o tools/bin/wire_lab_<variant>
-// run:   tools/bin/wire_lab_<variant> [reps=20] [dstride=1248]
+// run:   tools/bin/wire_lab_<variant> [reps=20] [dstride=1248] [payload stride=1200]
 #include "../razor_amd/csrc/rfec_wire.hip"
 
 #include <algorithm>
@@ -28,6 +28,7 @@ int main(int argc, char** argv)
 {
     const int reps = argc > 1 ? atoi(argv[1]) : 20;
     const uint32_t N = 655360, S = 1200, DS = argc > 2 ? (uint32_t)atoi(argv[2]) : 1248; // datagram slot stride
+    const uint32_t PS = argc > 3 ? (uint32_t)atoi(argv[3]) : S;                       // parse payload slot stride
     std::vector<uint8_t> sh((size_t)N * S);
     uint64_t x = 0x52415A4F52464543ull;
     for (size_t i = 0; i < sh.size(); i += 8) {
@@ -58,7 +59,7 @@ int main(int argc, char** argv)
     rfec_wire_rec* d_rec;
     CK(hipMalloc(&d_sh, sh.size()));
     CK(hipMalloc(&d_dg, (size_t)N * DS));
-    CK(hipMalloc(&d_pay, (size_t)N * S));
+    CK(hipMalloc(&d_pay, (size_t)N * PS));
     CK(hipMalloc(&d_hdr, N * sizeof(rfec_hdr)));
     CK(hipMalloc(&d_st, N * sizeof(rfec_seg_stamp)));
     CK(hipMalloc(&d_len, N * 2));
@@ -91,7 +92,7 @@ int main(int argc, char** argv)
         CK((hipError_t)rfec_launch_wire_frame_seg(N, S, S, d_sh, d_hdr, d_st, nullptr, DS, d_dg, d_len, sm));
     });
     const float tp = time([&] {
-        CK((hipError_t)rfec_launch_wire_parse(N, DS, d_dg, d_len, S, S, d_rec, d_pay, 0, sm));
+        CK((hipError_t)rfec_launch_wire_parse(N, DS, d_dg, d_len, PS, S, d_rec, d_pay, 0, sm));
     });
     const double bf = (double)N * ((S + 32) + (S + 36 + 2)), bp = (double)N * ((S + 36 + 2) + (64 + S));
     printf("frame_seg %8.1f us %6.4f   parse_seg %8.1f us %6.4f\n", tf, bf / tf / 1e3 / 8000, tp,
