@@ -1667,11 +1667,14 @@ __global__ __launch_bounds__(kBlock) void k_decode_out(v4u* shards, const v4u* _
 // chunk) instead of (group, row, chunk): slot e's target is the group's e-th
 // erased segment, recovered when its row fires, so no lane sits on a row
 // that does not (divRC divides by E C then).
+// K = 0: k and col at run time (k_rt <= 64, col_rt <= COL), the member loads
+// unrolled to COL and predicated on the row's size (the strip-mode plans).
 template <int K, int COL, bool NTL, int NTS, bool SLOTS>
 __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* __restrict__ parity, uint32_t total,
                                                         uint32_t C, FastDiv divC, FastDiv divRC,
                                                         uint32_t n_hdr_blocks, uint32_t hdr_every, PeelArgs A,
-                                                        rfec_kmask M, DenseOut D, uint32_t swz_npay8)
+                                                        rfec_kmask M, DenseOut D, uint32_t swz_npay8, uint32_t k_rt,
+                                                        uint32_t col_rt, FastDiv divCol)
 {
     static_assert(K <= 64, "row decode keeps the present mask in one word");
     uint32_t hb, pb;
@@ -1685,8 +1688,8 @@ __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* 
         run_header_block(A, M, hb);
         return;
     }
-    constexpr int R = (K + COL - 1) / COL;
-    constexpr int LAST = K - (R - 1) * COL;
+    const uint32_t KK = K ? (uint32_t)K : k_rt, CC = K ? (uint32_t)COL : col_rt;
+    const uint32_t R = (KK + CC - 1) / CC, LAST = KK - (R - 1) * CC;
     const uint32_t t = pb * kBlock + threadIdx.x;
     if (t >= total)
         return;
@@ -1697,24 +1700,24 @@ __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* 
     const uint64_t h = A.present[2 * g];
     uint32_t r, tgt;
     if constexpr (SLOTS) {
-        uint64_t m = ~h & (K == 64 ? ~0ull : (1ull << K) - 1ull);
+        uint64_t m = ~h & (KK == 64 ? ~0ull : (1ull << KK) - 1ull);
         for (uint32_t u = 0; u < q0; ++u) // the q0-th erased segment
             m &= m - 1ull;
         if (!m)
             return;
         tgt = (uint32_t)__ffsll((long long)m) - 1;
-        r = tgt / COL;
+        r = K ? tgt / (uint32_t)COL : fdiv(tgt, divCol);
     } else {
         r = q0;
     }
-    const uint32_t cnt = r < (uint32_t)(R - 1) ? COL : LAST;
-    const uint64_t rm = ((1ull << cnt) - 1ull) << (r * COL);
+    const uint32_t cnt = r + 1 < R ? CC : LAST;
+    const uint64_t rm = ((1ull << cnt) - 1ull) << (r * CC);
     const uint64_t miss = rm & ~h;
     if (__popcll(miss) != 1 || !((A.parity_present[g] >> r) & 1ull))
         return;
     if constexpr (!SLOTS)
         tgt = (uint32_t)__ffsll((long long)miss) - 1;
-    v4u* dst = shards + ((size_t)g * K + tgt) * C + j;
+    v4u* dst = shards + ((size_t)g * KK + tgt) * C + j;
     if constexpr (SLOTS) {
         dst = D.sh + ((size_t)g * D.E + q0) * C + j;
     } else if (D.E) {
@@ -1723,13 +1726,13 @@ __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* 
             return;
         dst = D.sh + ((size_t)g * D.E + e) * C + j;
     }
-    v4u* row = shards + ((size_t)g * K + r * COL) * C + j;
+    v4u* row = shards + ((size_t)g * KK + r * CC) * C + j;
     v4u acc = ld16<NTL>(parity + ((size_t)g * R + r) * C + j);
     v4u mv[COL];
 #pragma unroll
     for (int q = 0; q < COL; ++q) {
         mv[q] = v4u{0, 0, 0, 0};
-        if ((q < LAST || r < (uint32_t)(R - 1)) && r * COL + q != tgt)
+        if ((uint32_t)q < cnt && r * CC + q != tgt)
             mv[q] = ld16<NTL>(row + (size_t)q * C);
     }
 #pragma unroll
@@ -2121,23 +2124,26 @@ void launch_fused_out(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_
 // (group, dense output slot, chunk column) when `slots`
 template <int K, int COL>
 void launch_fused_rows(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmask& M, uint32_t cd, bool swz,
-                       bool slots)
+                       bool slots, uint32_t col_rt = 0)
 {
-    constexpr uint32_t R = (K + COL - 1) / COL;
+    const uint32_t kk = K ? (uint32_t)K : M.plan.k, cc = K ? (uint32_t)COL : col_rt;
+    const uint32_t R = (kk + cc - 1) / cc;
     const uint32_t per = slots ? F.D.E : R;
     const uint32_t total = B.groups * per * cd; // < 2^32: checked by the caller
     const uint32_t npay = blocks_for(total), npay8 = (npay + 7u) & ~7u, nhr = (F.n_hdr + 7u) >> 3;
     // swizzled: rounds of 8 blocks, nhr header rounds spread over npay8 / 8 payload rounds
     const dim3 grid(swz ? 8u * nhr + npay8 : F.n_hdr + npay);
     const uint32_t every = swz ? (F.spread && nhr ? (npay8 >> 3) / nhr : 0u) : hdr_every(F, npay);
-    const FastDiv dC = make_fastdiv(cd), dRC = make_fastdiv(per * cd);
+    const FastDiv dC = make_fastdiv(cd), dRC = make_fastdiv(per * cd), dCol = make_fastdiv(cc);
 #define RFEC_FUSED_ROWS(NTL, NTS)                                                                                \
     if (slots)                                                                                                   \
         hipLaunchKernelGGL((k_decode_rows<K, COL, NTL, NTS, true>), grid, dim3(kBlock), 0, F.stream, F.shards,    \
-                           F.parity, total, F.C, dC, dRC, F.n_hdr, every, B, M, F.D, swz ? npay8 : 0u);          \
+                           F.parity, total, F.C, dC, dRC, F.n_hdr, every, B, M, F.D, swz ? npay8 : 0u, kk, cc,   \
+                           dCol);                                                                                \
     else                                                                                                         \
         hipLaunchKernelGGL((k_decode_rows<K, COL, NTL, NTS, false>), grid, dim3(kBlock), 0, F.stream, F.shards,   \
-                           F.parity, total, F.C, dC, dRC, F.n_hdr, every, B, M, F.D, swz ? npay8 : 0u)
+                           F.parity, total, F.C, dC, dRC, F.n_hdr, every, B, M, F.D, swz ? npay8 : 0u, kk, cc,   \
+                           dCol)
     switch (sp) {
     case -1: RFEC_FUSED_ROWS(false, 1); break;
     case 0: RFEC_FUSED_ROWS(true, 0); break;
@@ -2491,6 +2497,11 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
                     launch_fused_rows<10, 4>(F, sp, B, *M, cd, swz, slots);
                 else
                     launch_fused_rows<32, 4>(F, sp, B, *M, cd, swz, slots);
+                return (int)hipGetLastError();
+            }
+            // other row layouts of k <= 64, rows of <= 4 members: the same kernel with k and col at run time
+            if (!(flags & RFEC_KFLAG_GENERIC) && is_row_layout(&P, &col) && col <= 4 && P.k <= 64) {
+                launch_fused_rows<0, 4>(F, sp, B, *M, cd, !(flags & RFEC_KFLAG_LINEAR_BLOCKS), slots, col);
                 return (int)hipGetLastError();
             }
             if (maxc <= 4)

@@ -527,7 +527,7 @@ def test_full_plan_shapes_gpu(gpu, oracle1000, k, tuning):
 
 
 @pytest.mark.parametrize("k,col,S", [(10, 4, 64), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 1000),
-                                     (96, 4, 512), (20, 3, 256)])
+                                     (96, 4, 512), (20, 3, 256), (24, 4, 1000), (13, 2, 1000)])
 @pytest.mark.parametrize("tuning", ["default", "hdr_head", "out_decode", "out_decode_head", "flat_decode", "generic",
                                     "small_fused", "small_b2", "xcd", "linear"])
 def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tuning):
@@ -583,7 +583,7 @@ def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tunin
 
 
 @pytest.mark.parametrize("k,col,S", [(10, 4, 1200), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 64),
-                                     (96, 4, 512), (20, 3, 256)])
+                                     (96, 4, 512), (20, 3, 256), (24, 4, 1200), (20, 3, 1200), (64, 4, 1024)])
 @pytest.mark.parametrize("tuning", ["default", "flat_decode", "out_decode", "hdr_head", "generic", "small_fused",
                                     "small_b2", "xcd", "linear", "line_lanes", "out_decode_lines"])
 def test_dense_output_decode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning):
