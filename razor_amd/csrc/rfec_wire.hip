@@ -822,268 +822,6 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// Framing with 16-byte lanes (slots of <= 1,280 bytes): the datagram is 80
-// aligned 16-byte runs, run j in lane j and run 64 + j in lane j < 16, so
-// every lane's output is one aligned b128 store and no LDS transpose sits in
-// the chain.  Lane j loads the payload chunk A / 16 runs before its own (A
-// bytes: 16 SEG, 32 FEC) and its left neighbour's chunk arrives by a
-// wave-shift DPP move: the two chunks cover the payload bytes of its run for
-// every header size (SEG 26-32, FEC 45).  The CRC is the 20-byte-lane
-// scheme's over 80 columns: each run's raw CRC (slice-by-16) carried to the
-// message end by its column's multiplier x^(128 (79 - c)), the wave's XOR
-// corrected once by x^(-8 rr).
-// ---------------------------------------------------------------------------
-constexpr int kRuns = 80;     // 16-byte runs of a 1,280-byte slot
-struct CrcTables16 {
-    uint32_t t[16][256];           // slice-by-16, as CrcTables
-    uint32_t nib[8][16][kRuns];    // nibble v at position i times x^(128 (79 - c)), column c
-    uint32_t inv[16][32];          // x^(31-i) * x^(-8r), r < 16
-};
-
-constexpr CrcTables16 make_crc_tables16()
-{
-    CrcTables16 r{};
-    const CrcTables<20> base = make_crc_tables<20>();
-    for (int s = 0; s < 16; ++s)
-        for (int b = 0; b < 256; ++b)
-            r.t[s][b] = base.t[s][b];
-    uint32_t V = 0x80000000u; // x^0, column 79
-    for (int j = kRuns - 1; j >= 0; --j) {
-        uint32_t basis[32]{};
-        uint32_t v = V;
-        for (int e = 0; e < 32; ++e) {
-            basis[e] = v;
-            v = mul_x(v);
-        }
-        for (int i = 0; i < 8; ++i)
-            for (uint32_t nv = 0; nv < 16; ++nv) {
-                uint32_t acc = 0;
-                for (int k = 0; k < 4; ++k)
-                    if (nv & (1u << k))
-                        acc ^= basis[31 - (4 * i + k)];
-                r.nib[i][nv][j] = acc;
-            }
-        for (int q = 0; q < 8 * 16; ++q)
-            V = mul_x(V);
-    }
-    for (int i = 0; i < 32; ++i) {
-        uint32_t v = 1u << i;
-        for (int q = 0; q < 16; ++q) {
-            r.inv[q][i] = v;
-            for (int b = 0; b < 8; ++b)
-                v = div_x(v);
-        }
-    }
-    return r;
-}
-
-__device__ const CrcTables16 kCrc16 = make_crc_tables16();
-constexpr int kTab16Dwords = (int)(sizeof(CrcTables16) / 4);
-constexpr int kNib16Base = 16 * 256;
-constexpr int kInv16Base = kNib16Base + 8 * 16 * kRuns;
-
-__device__ __forceinline__ void load_tables16(uint32_t* T)
-{
-    const v4u* s = reinterpret_cast<const v4u*>(&kCrc16);
-    v4u* d = reinterpret_cast<v4u*>(T);
-    for (int i = threadIdx.x; i < kTab16Dwords / 4; i += kBlock)
-        d[i] = s[i];
-    __syncthreads();
-}
-
-__device__ __forceinline__ uint32_t carry16(const uint32_t* T, uint32_t c, uint32_t col)
-{
-    const uint32_t* nb = T + kNib16Base + col;
-    uint32_t r = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-        r ^= nb[(i * 16 + ((c >> (4 * i)) & 15u)) * kRuns];
-    return r;
-}
-
-// DPP wave shifts (GFX9): lane l takes lane l - 1's value; shr: lane 0 gets 0, ror: lane 63's
-__device__ __forceinline__ uint32_t wave_shr1(uint32_t v)
-{
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);
-}
-__device__ __forceinline__ uint32_t wave_ror1(uint32_t v)
-{
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x13C, 0xF, 0xF, false);
-}
-
-// mask of dword k of a run (run index r) for a message of nb bytes
-__device__ __forceinline__ uint32_t run_mask(int k, uint32_t r, uint32_t nb)
-{
-    const uint32_t q = 4u * r + (uint32_t)k, qd = nb >> 2, s = nb & 3u;
-    return q < qd ? ~0u : (q == qd && s ? (1u << (8 * s)) - 1u : 0u);
-}
-
-// Payload chunks of a 16-byte-lane frame: c0 = payload chunk (16 lane - A) / 16,
-// c1 = chunk (1024 - A) / 16 + lane (lanes < 16 use it); bytes past `bytes`
-// read 0, negative offsets wrap and read 0.
-template <int A>
-__device__ __forceinline__ void load_chunks16(const uint8_t* base, uint32_t bytes, uint32_t lane, Chunks& ch)
-{
-    const __amdgpu_buffer_rsrc_t r = rsrc(base, bytes);
-    ch.c0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * lane - A, 0, kAuxNT));
-    ch.c1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, 1024u - A + 16u * lane, 0, kAuxNT));
-}
-
-// The two 8-dword windows (runs lane and 64 + lane): payload chunks
-// [prev, own] of each run, prev by a wave shift
-__device__ __forceinline__ void windows16(const Chunks& ch, uint32_t lane, uint32_t (&x1)[8], uint32_t (&x2)[8])
-{
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        x1[4 + k] = ch.c0[k];
-        x1[k] = wave_shr1(ch.c0[k]);
-        const uint32_t y = lane < 16 ? ch.c1[k] : ch.c0[k];
-        x2[4 + k] = ch.c1[k];
-        x2[k] = wave_ror1(y);
-    }
-}
-
-// Header H (bytes [0, hsize), dwords 0-11 in runs 0-2), payload dwords p1 / p2
-// of runs lane / 64 + lane (zero below hsize): masked at n, CRC32 BE at n,
-// both runs stored as aligned 16-byte lanes.
-__device__ __forceinline__ void finish_frame16(const uint32_t* T, const Hdr& H, uint32_t n, const uint32_t* p1,
-                                               const uint32_t* p2, uint32_t lane, uint8_t* __restrict__ slot,
-                                               uint32_t dstride, uint16_t* dlen_out)
-{
-    uint32_t w[4], v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t hd = lane == 0 ? H.h[k] : (lane == 1 ? H.h[4 + k] : (lane == 2 ? H.h[8 + k] : 0u));
-        w[k] = (p1[k] | hd) & run_mask(k, lane, n);
-        v[k] = lane < 16 ? p2[k] & run_mask(k, 64u + lane, n) : 0u;
-    }
-    // raw CRC of each run from a zero register, the initial register folded into bytes 0-3 (n >= 26)
-    const uint32_t c1 = slice16(T, w[0] ^ (lane == 0 ? ~RFEC_WIRE_CRC_SEED : 0u), w[1], w[2], w[3]);
-    uint32_t c2 = 0;
-    if (lane < 16)
-        c2 = slice16(T, v[0], v[1], v[2], v[3]);
-    const uint32_t D = (uint32_t)(kRuns * 16) - n, q = D >> 4, rr = D & 15u;
-    uint32_t cr = carry16(T, c1, min(lane + q, (uint32_t)kRuns - 1u));
-    if (lane < 16)
-        cr ^= carry16(T, c2, min(64u + lane + q, (uint32_t)kRuns - 1u));
-    const uint32_t R = wave_xor(cr);
-    const uint32_t b = lane < 32 && ((R >> (lane & 31u)) & 1u) ? T[kInv16Base + rr * 32 + (lane & 31u)] : 0u;
-    const uint32_t crc = ~wave_xor(b);
-    // big-endian trailer at byte n (positions wave-uniform)
-    const uint32_t be = bswap(crc), s = n & 3u, q0 = n >> 2, q1 = q0 + 1;
-    const uint32_t lo = be << (8 * s), hi = s ? be >> (32 - 8 * s) : 0u;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if ((q0 & 3u) == (uint32_t)k) {
-            w[k] |= lane == (q0 >> 2) ? lo : 0u;
-            v[k] |= lane + 64u == (q0 >> 2) ? lo : 0u;
-        }
-        if ((q1 & 3u) == (uint32_t)k) {
-            w[k] |= lane == (q1 >> 2) ? hi : 0u;
-            v[k] |= lane + 64u == (q1 >> 2) ? hi : 0u;
-        }
-    }
-    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-    const __amdgpu_buffer_rsrc_t r = rsrc(slot, dstride);
-    __builtin_amdgcn_raw_buffer_store_b128(u4{w[0], w[1], w[2], w[3]}, r, 16 * lane, 0, kAuxST);
-    if (lane < 16)
-        __builtin_amdgcn_raw_buffer_store_b128(u4{v[0], v[1], v[2], v[3]}, r, 1024 + 16 * lane, 0, kAuxST);
-    if (lane == 0)
-        *dlen_out = (uint16_t)(n + 4);
-}
-
-__device__ __forceinline__ void zero_slot16(uint8_t* __restrict__ slot, uint32_t dstride, uint32_t lane,
-                                            uint16_t* dlen_out)
-{
-    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-    const __amdgpu_buffer_rsrc_t r = rsrc(slot, dstride);
-    __builtin_amdgcn_raw_buffer_store_b128(u4{0, 0, 0, 0}, r, 16 * lane, 0, kAuxST);
-    if (lane < 16)
-        __builtin_amdgcn_raw_buffer_store_b128(u4{0, 0, 0, 0}, r, 1024 + 16 * lane, 0, kAuxST);
-    if (lane == 0)
-        *dlen_out = 0;
-}
-
-// SIM_SEG with 16-byte lanes (k_frame_seg's header and fields)
-__global__ __launch_bounds__(kBlock) void k_frame_seg16(const uint8_t* __restrict__ shards,
-                                                        const rfec_hdr* __restrict__ hdr,
-                                                        const rfec_seg_stamp* __restrict__ stamps,
-                                                        const uint32_t* __restrict__ order,
-                                                        uint8_t* __restrict__ dgram, uint16_t* __restrict__ dlen,
-                                                        uint32_t count, uint32_t stride, uint32_t capacity,
-                                                        uint32_t dstride)
-{
-    __shared__ __attribute__((aligned(16))) uint32_t T[kTab16Dwords];
-    load_tables16(T);
-    const uint32_t lane = threadIdx.x & (kWave - 1);
-    const uint32_t nw = gridDim.x * kWavesPerBlock;
-    const uint32_t range = (capacity + 15u) & ~15u;
-    uint32_t d = wave_id();
-    if (d >= count)
-        return;
-    using PW = Pre<Chunks>;
-    RFEC_WIRE_PIPE<PW>(d, count, nw,
-                       [&](uint32_t dd, PW& P) {
-                           P.f = load_seg_fields(hdr, stamps, dd, lane);
-                           load_chunks16<16>(shards + (size_t)dd * stride, range, lane, P.w);
-                       },
-                       [&](const PW& P, uint32_t d) {
-            const uint32_t o = order ? order[d] : d; // output slot
-            uint8_t* slot = dgram + (size_t)o * dstride;
-            rfec_hdr h;
-            {
-                const uint32_t h3 = fld(P.f, 3), h4 = fld(P.f, 4);
-                h.seq = fld(P.f, 0);
-                h.fid = fld(P.f, 1);
-                h.ts = fld(P.f, 2);
-                h.index = (uint16_t)h3;
-                h.total = (uint16_t)(h3 >> 16);
-                h.ftype = (uint8_t)h4;
-                h.payload_type = (uint8_t)(h4 >> 8);
-                h.size = (uint16_t)(h4 >> 16);
-            }
-            const uint32_t L = h.size;
-            if (L > capacity) {
-                zero_slot16(slot, dstride, lane, dlen + o);
-            } else {
-                rfec_seg_stamp s;
-                {
-                    const uint32_t s1 = fld(P.f, 6), s2 = fld(P.f, 7);
-                    s.uid = fld(P.f, 5);
-                    s.fec_id = (uint16_t)s1;
-                    s.send_ts = (uint16_t)(s1 >> 16);
-                    s.transport_seq = (uint16_t)s2;
-                    s.remb = (uint8_t)(s2 >> 16);
-                    s.reserved = 0;
-                }
-                Hdr H = {};
-                const uint32_t layout = (h.seq > 65535u ? 4u : 0u) | (h.fid > 65535u ? 2u : 0u) |
-                                        (h.total > 255u ? 1u : 0u);
-                uint32_t hs, x1[8], x2[8], p1[4], p2[4];
-                windows16(P.w, lane, x1, x2);
-                // windows [16 j - 32, 16 j) of the payload: run j's bytes start 32 - hs in
-#define RFEC_SEG16(PW_, FW_, TW_, SH)                                                                              \
-    hs = seg_header<PW_, FW_, TW_>(H, h, s);                                                                     \
-    funnel<4, SH>(x1, p1);                                                                                         \
-    funnel<4, SH>(x2, p2);                                                                                         \
-    break;
-                switch (layout) {
-                case 0: RFEC_SEG16(false, false, false, 6)
-                case 1: RFEC_SEG16(false, false, true, 4)
-                case 2: RFEC_SEG16(false, true, false, 4)
-                case 3: RFEC_SEG16(false, true, true, 2)
-                case 4: RFEC_SEG16(true, false, false, 4)
-                case 5: RFEC_SEG16(true, false, true, 2)
-                case 6: RFEC_SEG16(true, true, false, 2)
-                default: RFEC_SEG16(true, true, true, 0)
-                }
-#undef RFEC_SEG16
-                finish_frame16(T, H, hs + L, p1, p2, lane, slot, dstride, dlen + o);
-            }
-                       });
-}
-
-// ---------------------------------------------------------------------------
 // Parse (receive side)
 //
 // Two passes per batch of up to 64 of a wave's datagrams d_i = base + i nw:
@@ -1590,11 +1328,6 @@ uint32_t grid_for(const void* kernel, uint32_t count)
 
 // lane width: 20 bytes while a wave of them covers the slot, else 32
 inline bool narrow(uint32_t dstride) { return dstride <= (uint32_t)(kWave * 20); }
-// frame kernels at slots of <= 1,280 bytes: 16-byte lanes (0: the 20-byte-lane kernels, A/B builds)
-#ifndef RFEC_WIRE_LANES16
-#define RFEC_WIRE_LANES16 0
-#endif
-constexpr bool kLanes16 = RFEC_WIRE_LANES16 != 0;
 
 } // namespace
 
@@ -1620,10 +1353,7 @@ int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacit
                                uint32_t dstride, uint8_t* dgram, uint16_t* dlen, void* stream)
 {
     hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
-    if (narrow(dstride) && kLanes16)
-        hipLaunchKernelGGL(k_frame_seg16, dim3(grid_for<6>((const void*)k_frame_seg16, count)), dim3(kBlock), 0, sm,
-                           shards, hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride);
-    else if (narrow(dstride))
+    if (narrow(dstride))
         hipLaunchKernelGGL(k_frame_seg<20>, dim3(grid_for<2>((const void*)k_frame_seg<20>, count)), dim3(kBlock), 0, sm,
                            shards, hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride);
     else
