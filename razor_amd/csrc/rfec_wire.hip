@@ -862,10 +862,15 @@ constexpr int kHdrDwords = 12; // 48 bytes: the longest header read, SIM_FEC's, 
 // byte p (< 48, per lane) of the header dwords
 __device__ __forceinline__ uint32_t byte_at(const uint32_t (&H)[kHdrDwords], uint32_t p)
 {
-    uint32_t v = H[0];
+    // the dwords pass an empty asm first: a select chain over plain loads of H
+    // is folded into one indexed load, which puts the header array in scratch
+    uint32_t v = 0;
 #pragma unroll
-    for (int k = 1; k < kHdrDwords; ++k)
-        v = (p >> 2) == (uint32_t)k ? H[k] : v;
+    for (int k = 0; k < kHdrDwords; ++k) {
+        uint32_t h = H[k];
+        __asm__("" : "+v"(h));
+        v = (p >> 2) == (uint32_t)k ? h : v;
+    }
     return (v >> (8 * (p & 3u))) & 0xffu;
 }
 
