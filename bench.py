@@ -20,6 +20,15 @@ contiguous slices (razor_amd/dist.py), no data-path collective; the control
 plane (barrier, max-over-ranks time, byte sum) is a CPU gloo group, so no
 RCCL is brought up and several ranks may share one GPU.
 
+Timing: `value` is the wall clock of the K timed steps (barrier + device
+synchronize on both sides, max over ranks).  The roofline's launch duration
+is each kernel's own start / stop, HIP events bound to the launch itself
+(rfec_timing_events -> hipExtLaunchKernel, on the launch stream), which is
+what rocprofv3 reports per kernel; no event marker sits between the launches
+then.  `--timing bracket` records stream events around each call instead
+(the window then also holds the command processor's dispatch gap, 3-4 µs per
+launch, and the markers cost the step time a little).
+
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
@@ -370,6 +379,12 @@ def free_port():
     return p
 
 
+TIMING_OWN = ("the kernel's own start / stop: HIP events bound to the launch (rfec_timing_events -> "
+              "hipExtLaunchKernel) on the launch stream, mean over the timed steps")
+TIMING_BRACKET = ("HIP events recorded on the launch stream before and after the call (holds the dispatch "
+                  "gap; --timing bracket, or a call that launches more than one kernel)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -387,6 +402,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--tuning", type=int, default=0)
+    ap.add_argument("--timing", choices=("own", "bracket"), default="own",
+                    help="roofline launch duration: the kernel's own start/stop events (hipExtLaunchKernel) or "
+                         "stream events around the call")
     ap.add_argument("--sets", type=int, default=2, help="disjoint buffer sets rotated per step (MALL-proof timing)")
     ap.add_argument("--col", type=int, default=0, help="custom: rows of COL segments")
     ap.add_argument("--full-plan", action="store_true", help="custom: rows + columns of the reference plan")
@@ -468,25 +486,50 @@ def main():
         dec_set(i).decode(sp)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # the kernels' own start / stop (rfec_timing_events -> hipExtLaunchKernel on the launch stream):
+    # the roofline's launch duration, without the dispatch gap the stream-event bracket also holds
+    kev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(args.steps)]
+    for q in kev:
+        for e in q:
+            e.record(stream)  # creates the event (torch allocates it at its first record)
+    # does each call launch exactly one kernel (then its own window is its launch duration)?
+    lib.timing_events(kev[0][0].cuda_event, kev[0][1].cuda_event)
+    sets[0].encode(sp)
+    n_enc = lib.timing_launches()
+    lib.timing_events(kev[0][2].cuda_event, kev[0][3].cuda_event)
+    dec_set(1).decode(sp)
+    n_dec = lib.timing_launches()
+    own = args.timing == "own" and n_enc == 1 and n_dec == 1
     torch.cuda.synchronize(device)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        a, b, c = ev[i]
-        a.record(stream)
-        sets[(args.warmup + i) % nset].encode(sp)
-        b.record(stream)
-        dec_set(args.warmup + i).decode(sp)
-        c.record(stream)
+        if own:  # the kernels' own events only: no marker between the launches
+            ka, kb, kc, kd = kev[i]
+            lib.timing_events(ka.cuda_event, kb.cuda_event)
+            sets[(args.warmup + i) % nset].encode(sp)
+            lib.timing_events(kc.cuda_event, kd.cuda_event)
+            dec_set(args.warmup + i).decode(sp)
+        else:
+            a, b, c = ev[i]
+            a.record(stream)
+            sets[(args.warmup + i) % nset].encode(sp)
+            b.record(stream)
+            dec_set(args.warmup + i).decode(sp)
+            c.record(stream)
     torch.cuda.synchronize(device)
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    t_enc = np.array([a.elapsed_time(b) for a, b, _ in ev]) / 1e3
-    t_dec = np.array([b.elapsed_time(c) for _, b, c in ev]) / 1e3
+    if own:
+        t_enc = np.array([q[0].elapsed_time(q[1]) for q in kev]) / 1e3
+        t_dec = np.array([q[2].elapsed_time(q[3]) for q in kev]) / 1e3
+    else:
+        t_enc = np.array([a.elapsed_time(b) for a, b, _ in ev]) / 1e3
+        t_dec = np.array([b.elapsed_time(c) for _, b, c in ev]) / 1e3
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -579,6 +622,7 @@ def main():
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "launch_us": round(enc_mean * 1e6, 2),
                          "launch_us_median": round(float(np.median(t_enc)) * 1e6, 2),
+                         "timing": TIMING_OWN if own else TIMING_BRACKET,
                          "algorithmic_bytes_per_launch": w.enc_bytes},
             "encode_gibps": round(w.enc_bytes / enc_mean / 2**30, 2),
             # source bytes k*S*G over the encode time, and that as a fraction of the peak
@@ -591,6 +635,7 @@ def main():
                                 round(w.dec_bytes / dec_mean / 1e9 / HBM_PEAK_GBPS, 4),
                                 "launch_us": round(dec_mean * 1e6, 2),
                                 "launch_us_median": round(float(np.median(t_dec)) * 1e6, 2),
+                                "timing": TIMING_OWN if own else TIMING_BRACKET,
                                 "traffic": load_traffic(workload_name, "decode"),
                                 "kernels": dec_kernels,
                                 "parity_operand": "cold: written one step (>= 1.7 GB of traffic) before"

@@ -231,6 +231,16 @@ typedef struct {
 int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,
                             sim_fec_t* const* fecs, uint16_t fec_id0, rfec_host_timing* timing);
 
+/* Kernel timing for benches: the next kernel this thread launches through the
+ * batched API (rfec_encode_batch, rfec_recover_batch[_out], rfec_zero_tails)
+ * records its own start / stop on these hipEvent_t (either may be NULL), via
+ * hipExtLaunchKernel; the setting is consumed by that launch.
+ * rfec_timing_launches: kernels launched by this thread since the last
+ * rfec_timing_events (a call that launched more than one kernel timed only
+ * its first). */
+int rfec_timing_events(void* start, void* stop);
+uint32_t rfec_timing_launches(void);
+
 /* Zero bytes [data_size, stride) of every shard (establishes the layout
  * invariant for callers that cannot guarantee it). */
 int rfec_zero_tails(uint32_t groups, uint32_t k, uint32_t stride, uint8_t* shards,

@@ -38,6 +38,27 @@
 
 #include "rfec_internal.h"
 
+#include <hip/hip_ext.h>
+
+// Kernel timing (rfec_timing_events): the next launch of the calling thread
+// records its own start and stop on the caller's events (hipExtLaunchKernel:
+// the kernel's dispatch timestamps), so the measured window is the kernel
+// alone, without the dispatch gap a stream-event bracket around the call
+// also holds.  t_launches counts the launches since the events were set.
+static thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
+static thread_local uint32_t t_launches = 0;
+#define RFEC_LAUNCH(K, G, B, SH, ST, ...)                                                                          \
+    do {                                                                                                           \
+        ++t_launches;                                                                                              \
+        if (t_ev_start || t_ev_stop) {                                                                             \
+            const hipEvent_t ev_a_ = t_ev_start, ev_z_ = t_ev_stop;                                                \
+            t_ev_start = t_ev_stop = nullptr;                                                                      \
+            hipExtLaunchKernelGGL(K, G, B, SH, ST, ev_a_, ev_z_, 0u, __VA_ARGS__);                                 \
+        } else {                                                                                                   \
+            hipLaunchKernelGGL(K, G, B, SH, ST, __VA_ARGS__);                                                      \
+        }                                                                                                          \
+    } while (0)
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -1897,7 +1918,7 @@ hipError_t launch_rows(const EncLaunch& a)
     const uint32_t C = a.stride / 16;
     const uint32_t total = a.groups * a.cd;
     const uint32_t lanes = (total + ITEMS - 1) / ITEMS;
-    hipLaunchKernelGGL((k_encode_rows<K, COL, NTL, NTS, ITEMS>), dim3(a.E.n_meta_blocks + blocks_for(lanes)),
+    RFEC_LAUNCH((k_encode_rows<K, COL, NTL, NTS, ITEMS>), dim3(a.E.n_meta_blocks + blocks_for(lanes)),
                        dim3(kBlock), 0, a.stream, a.s, a.p, total, C, make_fastdiv(a.cd), a.E, *a.P);
     return hipGetLastError();
 }
@@ -1921,7 +1942,7 @@ template <int K, int COL, bool NTL, int NTS, int NI>
 hipError_t launch_rows_gw(const EncLaunch& a, const GwGeom& g, uint32_t swz)
 {
     const uint32_t C = a.stride / 16;
-    hipLaunchKernelGGL((k_encode_rows_gw<K, COL, NTL, NTS, NI>), dim3(a.E.n_meta_blocks + g.blocks), dim3(kBlock), 0,
+    RFEC_LAUNCH((k_encode_rows_gw<K, COL, NTL, NTS, NI>), dim3(a.E.n_meta_blocks + g.blocks), dim3(kBlock), 0,
                        a.stream, a.s, a.p, a.groups, C, make_fastdiv(a.cd), g.gpw, swz, a.E, *a.P);
     return hipGetLastError();
 }
@@ -1939,7 +1960,7 @@ hipError_t launch_rows_out(const EncLaunch& a, unsigned flags)
     const uint32_t meta_first = (flags & RFEC_KFLAG_META_TAIL) && !swz ? nb : 0u;
     // swizzle: meta blocks at the head, padded to a multiple of 8 so payload block p runs on XCD p % 8
     const uint32_t head = swz ? (a.E.n_meta_blocks + 7u) & ~7u : 0u;
-    hipLaunchKernelGGL((k_encode_out<K, COL, NTL, NTS>), dim3((swz ? head : a.E.n_meta_blocks) + nb), dim3(kBlock), 0,
+    RFEC_LAUNCH((k_encode_out<K, COL, NTL, NTS>), dim3((swz ? head : a.E.n_meta_blocks) + nb), dim3(kBlock), 0,
                        a.stream, a.s, a.p, (uint32_t)total, C, make_fastdiv(a.cd), make_fastdiv(R * a.cd), meta_first,
                        head, a.E, *a.P);
     return hipGetLastError();
@@ -1953,7 +1974,7 @@ hipError_t launch_rows_out_rt(const EncLaunch& a, unsigned flags, uint32_t col)
     const uint32_t nb = blocks_for(total);
     const bool swz = !(flags & RFEC_KFLAG_LINEAR_BLOCKS);
     const uint32_t head = swz ? (a.E.n_meta_blocks + 7u) & ~7u : 0u;
-    hipLaunchKernelGGL((k_encode_out_rt<CMAX, NTL, NTS>), dim3((swz ? head : a.E.n_meta_blocks) + nb), dim3(kBlock),
+    RFEC_LAUNCH((k_encode_out_rt<CMAX, NTL, NTS>), dim3((swz ? head : a.E.n_meta_blocks) + nb), dim3(kBlock),
                        0, a.stream, a.s, a.p, (uint32_t)total, a.stride / 16, make_fastdiv(a.cd),
                        make_fastdiv(R * a.cd), K, col, head, a.E, *a.P);
     return hipGetLastError();
@@ -1995,10 +2016,10 @@ template <int MAXC, int BATCH, bool PIPE, bool NTL, int NTS>
 void launch_replay_t(const ReplayArgs& R, const rfec_kplan& P, dim3 grid)
 {
     if constexpr (PIPE)
-        hipLaunchKernelGGL((k_recover_pipe<MAXC, BATCH, NTL, NTS>), grid, dim3(kBlock), 0, R.stream, R.shards,
+        RFEC_LAUNCH((k_recover_pipe<MAXC, BATCH, NTL, NTS>), grid, dim3(kBlock), 0, R.stream, R.shards,
                            R.parity, R.sched, R.total, R.C, R.f, R.rec_bytes, R.fast_ok, P);
     else
-        hipLaunchKernelGGL((k_recover_flat<MAXC, BATCH, NTL, NTS>), grid, dim3(kBlock), 0, R.stream, R.shards,
+        RFEC_LAUNCH((k_recover_flat<MAXC, BATCH, NTL, NTS>), grid, dim3(kBlock), 0, R.stream, R.shards,
                            R.parity, R.sched, R.total, R.C, R.f, R.rec_bytes, R.fast_ok, P);
 }
 
@@ -2044,7 +2065,7 @@ void launch_fused_gw(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_k
 {
     const dim3 grid(F.n_hdr + g.blocks);
 #define RFEC_FUSED_GW(NTL, NTS)                                                                                  \
-    hipLaunchKernelGGL((k_decode_disjoint_gw<MAXC, NTL, NTS, NI>), grid, dim3(kBlock), 0, F.stream, F.shards,    \
+    RFEC_LAUNCH((k_decode_disjoint_gw<MAXC, NTL, NTS, NI>), grid, dim3(kBlock), 0, F.stream, F.shards,    \
                        F.parity, F.C, F.f, g.gpw, swz, F.n_hdr, B, M)
     switch (sp) {
     case -1: RFEC_FUSED_GW(false, 1); break;
@@ -2064,9 +2085,9 @@ void launch_cascade(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_km
     // fix-up: a small grid (the list is empty unless headers disagree with the masks)
     const uint32_t fb = blocks_for(F.total) < 128u ? blocks_for(F.total) : 128u;
 #define RFEC_CASCADE(NTL, NTS)                                                                                    \
-    hipLaunchKernelGGL((k_decode_cascade<MAXC, BATCH, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards,       \
+    RFEC_LAUNCH((k_decode_cascade<MAXC, BATCH, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards,       \
                        F.parity, F.total, F.C, F.f, F.n_hdr, B, M);                                               \
-    hipLaunchKernelGGL((k_decode_fixup<MAXC, NTL, NTS>), dim3(fb), dim3(kBlock), 0, F.stream, F.shards, F.parity,  \
+    RFEC_LAUNCH((k_decode_fixup<MAXC, NTL, NTS>), dim3(fb), dim3(kBlock), 0, F.stream, F.shards, F.parity,  \
                        B.sched, B.fixc, B.fixlist, B.gen, B.groups, F.C, F.f, B.rec_bytes, M.plan)
     switch (sp) {
     case -1: RFEC_CASCADE(false, 1); break;
@@ -2105,10 +2126,10 @@ void launch_fused_out(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_
     const uint32_t every = hdr_every(F, npay);
 #define RFEC_FUSED_OUT(NTL, NTS)                                                                                 \
     if (slots)                                                                                                   \
-        hipLaunchKernelGGL((k_decode_out<MAXC, NTL, NTS, true>), grid, dim3(kBlock), 0, F.stream, F.shards,       \
+        RFEC_LAUNCH((k_decode_out<MAXC, NTL, NTS, true>), grid, dim3(kBlock), 0, F.stream, F.shards,       \
                            F.parity, total, F.C, dC, dLC, F.n_hdr, every, B, M, F.D);                           \
     else                                                                                                         \
-        hipLaunchKernelGGL((k_decode_out<MAXC, NTL, NTS, false>), grid, dim3(kBlock), 0, F.stream, F.shards,      \
+        RFEC_LAUNCH((k_decode_out<MAXC, NTL, NTS, false>), grid, dim3(kBlock), 0, F.stream, F.shards,      \
                            F.parity, total, F.C, dC, dLC, F.n_hdr, every, B, M, F.D)
     switch (sp) {
     case -1: RFEC_FUSED_OUT(false, 1); break;
@@ -2137,11 +2158,11 @@ void launch_fused_rows(const FusedArgs& F, int sp, const PeelArgs& B, const rfec
     const FastDiv dC = make_fastdiv(cd), dRC = make_fastdiv(per * cd), dCol = make_fastdiv(cc);
 #define RFEC_FUSED_ROWS(NTL, NTS)                                                                                \
     if (slots)                                                                                                   \
-        hipLaunchKernelGGL((k_decode_rows<K, COL, NTL, NTS, true>), grid, dim3(kBlock), 0, F.stream, F.shards,    \
+        RFEC_LAUNCH((k_decode_rows<K, COL, NTL, NTS, true>), grid, dim3(kBlock), 0, F.stream, F.shards,    \
                            F.parity, total, F.C, dC, dRC, F.n_hdr, every, B, M, F.D, swz ? npay8 : 0u, kk, cc,   \
                            dCol);                                                                                \
     else                                                                                                         \
-        hipLaunchKernelGGL((k_decode_rows<K, COL, NTL, NTS, false>), grid, dim3(kBlock), 0, F.stream, F.shards,   \
+        RFEC_LAUNCH((k_decode_rows<K, COL, NTL, NTS, false>), grid, dim3(kBlock), 0, F.stream, F.shards,   \
                            F.parity, total, F.C, dC, dRC, F.n_hdr, every, B, M, F.D, swz ? npay8 : 0u, kk, cc,   \
                            dCol)
     switch (sp) {
@@ -2160,7 +2181,7 @@ void launch_small(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmas
 {
     const dim3 grid(blocks_for(B.groups * CD)); // groups * CD < 2^31: check_geometry
 #define RFEC_SMALL(NTL, NTS)                                                                                     \
-    hipLaunchKernelGGL((k_decode_small<CD, BATCH, WIDE, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards,    \
+    RFEC_LAUNCH((k_decode_small<CD, BATCH, WIDE, NTL, NTS>), grid, dim3(kBlock), 0, F.stream, F.shards,    \
                        F.parity, F.C, B, M, F.D)
     switch (sp) {
     case -1: RFEC_SMALL(false, 1); break;
@@ -2178,7 +2199,7 @@ void launch_fused(const FusedArgs& F, int sp, const PeelArgs& B, const rfec_kmas
 {
     const dim3 grid(F.n_hdr + blocks_for((F.total + NI - 1) / NI));
 #define RFEC_FUSED(NTL, NTS)                                                                                     \
-    hipLaunchKernelGGL((k_decode_disjoint<MAXC, NTL, NTS, NI>), grid, dim3(kBlock), 0, F.stream, F.shards,       \
+    RFEC_LAUNCH((k_decode_disjoint<MAXC, NTL, NTS, NI>), grid, dim3(kBlock), 0, F.stream, F.shards,       \
                        F.parity, F.total, F.C, F.f, F.n_hdr, hdr_every(F, grid.x - F.n_hdr), B, M, F.D)
     switch (sp) {
     case -1: RFEC_FUSED(false, 1); break;
@@ -2273,7 +2294,7 @@ hipError_t launch_encode_t(const EncLaunch& a, unsigned flags)
         const dim3 grid(a.E.n_meta_blocks + blocks_for(total));
 #define RFEC_MX(KK, CC)                                                                                           \
     case KK:                                                                                                      \
-        hipLaunchKernelGGL((k_encode_matrix<KK, CC, NTL, NTS>), grid, dim3(kBlock), 0, a.stream, a.s, a.p, total, C, \
+        RFEC_LAUNCH((k_encode_matrix<KK, CC, NTL, NTS>), grid, dim3(kBlock), 0, a.stream, a.s, a.p, total, C, \
                            make_fastdiv(a.cd), a.E, *P);                                                          \
         return hipGetLastError();
         switch (P->k) {
@@ -2292,16 +2313,26 @@ hipError_t launch_encode_t(const EncLaunch& a, unsigned flags)
                 m |= 1u << (P->line[l].first + q * P->line[l].stride);
             LM.m[l] = (uint16_t)m;
         }
-        hipLaunchKernelGGL((k_encode_k16<NTL, NTS>), dim3(a.E.n_meta_blocks + blocks_for(total)), dim3(kBlock), 0,
+        RFEC_LAUNCH((k_encode_k16<NTL, NTS>), dim3(a.E.n_meta_blocks + blocks_for(total)), dim3(kBlock), 0,
                            a.stream, a.s, a.p, total, C, make_fastdiv(a.cd), a.E, *P, LM);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL((k_encode<NTL, NTS>), dim3(a.E.n_meta_blocks + blocks_for(total)), dim3(kBlock), 0, a.stream,
+    RFEC_LAUNCH((k_encode<NTL, NTS>), dim3(a.E.n_meta_blocks + blocks_for(total)), dim3(kBlock), 0, a.stream,
                        a.s, a.p, total, C, make_fastdiv(a.cd), a.E, *P);
     return hipGetLastError();
 }
 
 } // namespace
+
+extern "C" int rfec_timing_events(void* start, void* stop)
+{
+    t_ev_start = reinterpret_cast<hipEvent_t>(start);
+    t_ev_stop = reinterpret_cast<hipEvent_t>(stop);
+    t_launches = 0;
+    return 0;
+}
+
+extern "C" uint32_t rfec_timing_launches(void) { return t_launches; }
 
 extern "C" {
 
@@ -2377,9 +2408,9 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
         A.capacity = capacity;
         const dim3 grid((unsigned)(((uint64_t)groups * kWave + kBlock - 1) / kBlock));
         if (ntl)
-            hipLaunchKernelGGL(k_recover<true>, grid, dim3(kBlock), 0, st, A, *M);
+            RFEC_LAUNCH(k_recover<true>, grid, dim3(kBlock), 0, st, A, *M);
         else
-            hipLaunchKernelGGL(k_recover<false>, grid, dim3(kBlock), 0, st, A, *M);
+            RFEC_LAUNCH(k_recover<false>, grid, dim3(kBlock), 0, st, A, *M);
         return (int)hipGetLastError();
     }
     const rfec_kplan& P = M->plan;
@@ -2527,7 +2558,7 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
             launch_cascade<8, 1>(F, sp, B, *M);
         return (int)hipGetLastError();
     }
-    hipLaunchKernelGGL(k_peel_lds, dim3(n_hdr), dim3(kBlock), 0, st, B, *M);
+    RFEC_LAUNCH(k_peel_lds, dim3(n_hdr), dim3(kBlock), 0, st, B, *M);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess)
         return (int)e;
@@ -2575,7 +2606,7 @@ int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map
     const uint32_t total = rows * C;
     if (!total)
         return 0;
-    hipLaunchKernelGGL(k_gather_rows, dim3(blocks_for(total)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
+    RFEC_LAUNCH(k_gather_rows, dim3(blocks_for(total)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
                        reinterpret_cast<v4u*>(dst), reinterpret_cast<const v4u*>(src), map, total, C, make_fastdiv(C));
     return (int)hipGetLastError();
 }
@@ -2584,7 +2615,7 @@ int rfec_launch_zero_tails(uint32_t slots, uint32_t stride, uint8_t* shards, con
 {
     const uint32_t C = stride / 16;
     const uint32_t total = slots * C;
-    hipLaunchKernelGGL(k_zero_tails, dim3(blocks_for(total)), dim3(kBlock), 0,
+    RFEC_LAUNCH(k_zero_tails, dim3(blocks_for(total)), dim3(kBlock), 0,
                        reinterpret_cast<hipStream_t>(stream), reinterpret_cast<v4u*>(shards), hdr, total, C,
                        make_fastdiv(C));
     return (int)hipGetLastError();

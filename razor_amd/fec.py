@@ -211,6 +211,8 @@ _SIGS = {
     "rfec_recover_batch_out": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, C.c_uint32, C.c_uint32,
                                          _P, _P, _P, _P, _P, _P, _P, _P, C.c_uint32, _P, _P, _P, _P, _P]),
     "rfec_zero_tails": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    "rfec_timing_events": (C.c_int, [_P, _P]),
+    "rfec_timing_launches": (C.c_uint32, []),
     "rfec_wire_frame_fec": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, _P, C.c_uint32, _P,
                                       _P, _P]),
     "rfec_wire_frame_seg": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, _P, C.c_uint32, _P, _P, _P]),
@@ -363,6 +365,14 @@ class Native:
                                                      fec_ptrs.ctypes.data, fec_id0, C.addressof(t)),
                     "rfec_host_encode_groups")
         return {f: getattr(t, f) for f, _ in rfec_host_timing._fields_}
+
+    def timing_events(self, start, stop):
+        """The next kernel this thread launches records its own start / stop on
+        these hipEvent_t handles (rfec_timing_events)."""
+        self.lib.rfec_timing_events(start, stop)
+
+    def timing_launches(self) -> int:
+        return int(self.lib.rfec_timing_launches())
 
     def zero_tails(self, groups, k, stride, shards, hdr, stream=None):
         self._check(self.lib.rfec_zero_tails(groups, k, stride, shards, hdr, stream), "rfec_zero_tails")
