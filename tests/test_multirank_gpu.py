@@ -118,3 +118,6 @@ def test_bench_two_ranks_one_gpu():
     assert d["config"]["workload"].startswith("c4:")
     assert d["verified"] is True and d["verified_vs_reference_digest"] is True
     assert d["value"] > 0
+    # one kernel per call: the roofline takes each kernel's own start / stop events
+    for key in ("roofline", "decode_roofline"):
+        assert d[key]["timing"].startswith("the kernel's own") and d[key]["launch_us"] > 0
