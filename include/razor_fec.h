@@ -232,8 +232,8 @@ int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
                             sim_fec_t* const* fecs, uint16_t fec_id0, rfec_host_timing* timing);
 
 /* Kernel timing for benches: the next kernel this thread launches through the
- * batched API (rfec_encode_batch, rfec_recover_batch[_out], rfec_zero_tails)
- * records its own start / stop on these hipEvent_t (either may be NULL), via
+ * batched API (rfec_encode_batch, rfec_recover_batch[_out], rfec_zero_tails,
+ * rfec_wire_frame_fec / _seg, rfec_wire_parse) records its own start / stop on these hipEvent_t (either may be NULL), via
  * hipExtLaunchKernel; the setting is consumed by that launch.
  * rfec_timing_launches: kernels launched by this thread since the last
  * rfec_timing_events (a call that launched more than one kernel timed only

@@ -29,7 +29,7 @@ ARCH = os.environ.get("RFEC_OFFLOAD_ARCH", "gfx950")
 HIP_SRC = [CSRC / "rfec_kernels.hip", CSRC / "rfec_probe.hip", CSRC / "rfec_wire.hip", CSRC / "rfec_fill.hip"]
 C_SRC = [CSRC / "rfec_host.c", CSRC / "rfec_flex.c"]  # built once per SIM_VIDEO_SIZE
 NET_SRC = CSRC / "rfec_net.c"  # host-only (sockets), independent of SIM_VIDEO_SIZE
-HEADERS = [INCLUDE / "razor_fec.h", INCLUDE / "razor_flex.h", CSRC / "rfec_internal.h"]
+HEADERS = [INCLUDE / "razor_fec.h", INCLUDE / "razor_flex.h", CSRC / "rfec_internal.h", CSRC / "rfec_launch.h"]
 
 VARIANTS = {"librazor_fec.so": 1000, "librazor_fec_v1200.so": 1200}
 

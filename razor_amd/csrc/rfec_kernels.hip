@@ -38,26 +38,21 @@
 
 #include "rfec_internal.h"
 
-#include <hip/hip_ext.h>
+#include "rfec_launch.h"
 
-// Kernel timing (rfec_timing_events): the next launch of the calling thread
-// records its own start and stop on the caller's events (hipExtLaunchKernel:
-// the kernel's dispatch timestamps), so the measured window is the kernel
-// alone, without the dispatch gap a stream-event bracket around the call
-// also holds.  t_launches counts the launches since the events were set.
 static thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
-static thread_local uint32_t t_launches = 0;
-#define RFEC_LAUNCH(K, G, B, SH, ST, ...)                                                                          \
-    do {                                                                                                           \
-        ++t_launches;                                                                                              \
-        if (t_ev_start || t_ev_stop) {                                                                             \
-            const hipEvent_t ev_a_ = t_ev_start, ev_z_ = t_ev_stop;                                                \
-            t_ev_start = t_ev_stop = nullptr;                                                                      \
-            hipExtLaunchKernelGGL(K, G, B, SH, ST, ev_a_, ev_z_, 0u, __VA_ARGS__);                                 \
-        } else {                                                                                                   \
-            hipLaunchKernelGGL(K, G, B, SH, ST, __VA_ARGS__);                                                      \
-        }                                                                                                          \
-    } while (0)
+static thread_local uint32_t t_launches = 0; // launches since rfec_timing_events
+
+bool rfec_timing_take(hipEvent_t* start, hipEvent_t* stop)
+{
+    ++t_launches;
+    if (!t_ev_start && !t_ev_stop)
+        return false;
+    *start = t_ev_start;
+    *stop = t_ev_stop;
+    t_ev_start = t_ev_stop = nullptr;
+    return true;
+}
 
 namespace {
 

@@ -29,6 +29,7 @@
 #include <stdint.h>
 
 #include "rfec_internal.h"
+#include "rfec_launch.h"
 
 namespace {
 
@@ -1345,10 +1346,10 @@ int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacit
 {
     hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
     if (narrow(dstride))
-        hipLaunchKernelGGL(k_frame_fec<20>, dim3(grid_for<0>((const void*)k_frame_fec<20>, count)), dim3(kBlock), 0, sm,
+        RFEC_LAUNCH(k_frame_fec<20>, dim3(grid_for<0>((const void*)k_frame_fec<20>, count)), dim3(kBlock), 0, sm,
                            parity, meta, fec_size, status, stamps, order, dgram, dlen, count, stride, capacity, dstride);
     else
-        hipLaunchKernelGGL(k_frame_fec<32>, dim3(grid_for<1>((const void*)k_frame_fec<32>, count)), dim3(kBlock), 0, sm,
+        RFEC_LAUNCH(k_frame_fec<32>, dim3(grid_for<1>((const void*)k_frame_fec<32>, count)), dim3(kBlock), 0, sm,
                            parity, meta, fec_size, status, stamps, order, dgram, dlen, count, stride, capacity, dstride);
     return (int)hipGetLastError();
 }
@@ -1359,10 +1360,10 @@ int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacit
 {
     hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
     if (narrow(dstride))
-        hipLaunchKernelGGL(k_frame_seg<20>, dim3(grid_for<2>((const void*)k_frame_seg<20>, count)), dim3(kBlock), 0, sm,
+        RFEC_LAUNCH(k_frame_seg<20>, dim3(grid_for<2>((const void*)k_frame_seg<20>, count)), dim3(kBlock), 0, sm,
                            shards, hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride);
     else
-        hipLaunchKernelGGL(k_frame_seg<32>, dim3(grid_for<3>((const void*)k_frame_seg<32>, count)), dim3(kBlock), 0, sm,
+        RFEC_LAUNCH(k_frame_seg<32>, dim3(grid_for<3>((const void*)k_frame_seg<32>, count)), dim3(kBlock), 0, sm,
                            shards, hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride);
     return (int)hipGetLastError();
 }
@@ -1374,10 +1375,10 @@ int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, c
     hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
     // 20-byte lanes cover 1,280 bytes of a slot: enough when the slot or every datagram fits
     if (narrow(dstride) || (max_len && max_len <= (uint32_t)(kWave * 20)))
-        hipLaunchKernelGGL(k_parse<20>, dim3(grid_for<4>((const void*)k_parse<20>, n)), dim3(kBlock), 0, sm, dgram,
+        RFEC_LAUNCH(k_parse<20>, dim3(grid_for<4>((const void*)k_parse<20>, n)), dim3(kBlock), 0, sm, dgram,
                            dlen, recs, payload, n, dstride, stride, capacity);
     else
-        hipLaunchKernelGGL(k_parse<32>, dim3(grid_for<5>((const void*)k_parse<32>, n)), dim3(kBlock), 0, sm, dgram,
+        RFEC_LAUNCH(k_parse<32>, dim3(grid_for<5>((const void*)k_parse<32>, n)), dim3(kBlock), 0, sm, dgram,
                            dlen, recs, payload, n, dstride, stride, capacity);
     return (int)hipGetLastError();
 }

@@ -33,12 +33,24 @@ from razor_amd.fec import FEC_STAMP_DTYPE, SEG_STAMP_DTYPE, HDR_DTYPE, Native, n
 HBM_PEAK = 8000.0
 
 
-def timed(fn, reps, stream):
+def timed(fn, reps, stream, lib=None):
+    """Median / mean kernel time: the kernel's own start / stop (rfec_timing_events, as bench.py)
+    when the library has it, else stream events around each call."""
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    own = lib is not None and hasattr(lib.lib, "rfec_timing_events")
+    if own:
+        for a, b in ev:  # torch creates an event at its first record
+            a.record(stream)
+            b.record(stream)
+        torch.cuda.synchronize()
     for a, b in ev:
-        a.record(stream)
-        fn()
-        b.record(stream)
+        if own:
+            lib.timing_events(a.cuda_event, b.cuda_event)
+            fn()
+        else:
+            a.record(stream)
+            fn()
+            b.record(stream)
     torch.cuda.synchronize()
     t = np.array([a.elapsed_time(b) * 1e-3 for a, b in ev])
     return float(np.median(t)), float(t.mean())
@@ -121,7 +133,7 @@ def main():
                "parse_seg": NS * ((lens + 2) + (64 + S))}
         for name, f in (("frame_fec", frame_fec), ("frame_seg", frame_seg), ("parse_fec", parse_f),
                         ("parse_seg", parse_s)):
-            med, mean = timed(f, args.reps, st)
+            med, mean = timed(f, args.reps, st, lib)
             res[name] = {"median_us": round(med * 1e6, 2), "mean_us": round(mean * 1e6, 2),
                          "algorithmic_bytes": alg[name], "GBps": round(alg[name] / med / 1e9, 1),
                          "frac_of_hbm_peak": round(alg[name] / med / 1e9 / HBM_PEAK, 4)}
@@ -142,7 +154,9 @@ def main():
     og, ol = o.frame_seg_batch(shards[idx].cpu().numpy(), hdr[idx], sstamp[idx], S, DS)
     ok = ok and bool(np.array_equal(dg_s[idx].cpu().numpy(), og))
     out = {"groups": G, "k": k, "r": n, "payload": S, "fec_datagrams": NF, "seg_datagrams": NS,
-           "dstride": {"fec": DF, "seg": DS}, "kernels": res, "verified": ok}
+           "dstride": {"fec": DF, "seg": DS}, "kernels": res, "verified": ok,
+           "timing": ("the kernel's own start / stop (rfec_timing_events)" if hasattr(lib.lib, "rfec_timing_events")
+                      else "stream events around each call")}
     print(json.dumps(out, indent=1))
     if args.out:
         Path(args.out).write_text(json.dumps(out, indent=1))
