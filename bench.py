@@ -484,8 +484,7 @@ def main():
     for i in range(args.warmup):
         sets[i % nset].encode(sp)
         dec_set(i).decode(sp)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(args.steps)]
     # the kernels' own start / stop (rfec_timing_events -> hipExtLaunchKernel on the launch stream):
     # the roofline's launch duration, without the dispatch gap the stream-event bracket also holds
     kev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(args.steps)]
@@ -499,37 +498,38 @@ def main():
     lib.timing_events(kev[0][2].cuda_event, kev[0][3].cuda_event)
     dec_set(1).decode(sp)
     n_dec = lib.timing_launches()
-    own = args.timing == "own" and n_enc == 1 and n_dec == 1
+    own_enc = args.timing == "own" and n_enc == 1
+    own_dec = args.timing == "own" and n_dec == 1
     torch.cuda.synchronize(device)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if own:  # the kernels' own events only: no marker between the launches
-            ka, kb, kc, kd = kev[i]
+        # the kernels' own events where a call is one launch (no marker between launches), else a bracket
+        ka, kb, kc, kd = kev[i]
+        a, b, c, d = ev[i]
+        if own_enc:
             lib.timing_events(ka.cuda_event, kb.cuda_event)
-            sets[(args.warmup + i) % nset].encode(sp)
-            lib.timing_events(kc.cuda_event, kd.cuda_event)
-            dec_set(args.warmup + i).decode(sp)
         else:
-            a, b, c = ev[i]
             a.record(stream)
-            sets[(args.warmup + i) % nset].encode(sp)
+        sets[(args.warmup + i) % nset].encode(sp)
+        if not own_enc:
             b.record(stream)
-            dec_set(args.warmup + i).decode(sp)
+        if own_dec:
+            lib.timing_events(kc.cuda_event, kd.cuda_event)
+        else:
             c.record(stream)
+        dec_set(args.warmup + i).decode(sp)
+        if not own_dec:
+            d.record(stream)
     torch.cuda.synchronize(device)
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    if own:
-        t_enc = np.array([q[0].elapsed_time(q[1]) for q in kev]) / 1e3
-        t_dec = np.array([q[2].elapsed_time(q[3]) for q in kev]) / 1e3
-    else:
-        t_enc = np.array([a.elapsed_time(b) for a, b, _ in ev]) / 1e3
-        t_dec = np.array([b.elapsed_time(c) for _, b, c in ev]) / 1e3
+    t_enc = np.array([(q if own_enc else e)[0].elapsed_time((q if own_enc else e)[1]) for q, e in zip(kev, ev)]) / 1e3
+    t_dec = np.array([(q if own_dec else e)[2].elapsed_time((q if own_dec else e)[3]) for q, e in zip(kev, ev)]) / 1e3
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -622,7 +622,7 @@ def main():
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "launch_us": round(enc_mean * 1e6, 2),
                          "launch_us_median": round(float(np.median(t_enc)) * 1e6, 2),
-                         "timing": TIMING_OWN if own else TIMING_BRACKET,
+                         "timing": TIMING_OWN if own_enc else TIMING_BRACKET,
                          "algorithmic_bytes_per_launch": w.enc_bytes},
             "encode_gibps": round(w.enc_bytes / enc_mean / 2**30, 2),
             # source bytes k*S*G over the encode time, and that as a fraction of the peak
@@ -635,7 +635,7 @@ def main():
                                 round(w.dec_bytes / dec_mean / 1e9 / HBM_PEAK_GBPS, 4),
                                 "launch_us": round(dec_mean * 1e6, 2),
                                 "launch_us_median": round(float(np.median(t_dec)) * 1e6, 2),
-                                "timing": TIMING_OWN if own else TIMING_BRACKET,
+                                "timing": TIMING_OWN if own_dec else TIMING_BRACKET,
                                 "traffic": load_traffic(workload_name, "decode"),
                                 "kernels": dec_kernels,
                                 "parity_operand": "cold: written one step (>= 1.7 GB of traffic) before"
