@@ -234,6 +234,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
     void* q = reinterpret_cast<void*>((uint64_t)hi << 32 | lo);
     return __builtin_amdgcn_make_buffer_rsrc(q, 0, (int)__builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
 }
+// Frame kernels: wave priority 3 over 1 = the CRC, 2 = finish_frame (CRC,
+// trailer, store staging), 3 = a whole datagram's processing; 0 = none
+#ifndef RFEC_WIRE_FRAME_PRIO
+#define RFEC_WIRE_FRAME_PRIO 2
+#endif
 constexpr int kAuxNT = 2; // gfx950 cache-policy bits: nt
 #ifndef RFEC_WIRE_STORE_AUX
 #define RFEC_WIRE_STORE_AUX 2 // stores' cache policy (the lab's ST0 build: 0)
@@ -409,6 +414,9 @@ __device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, ui
                                              uint32_t lane, uint8_t* __restrict__ slot, uint32_t dstride,
                                              uint16_t* dlen_out, uint32_t* wb)
 {
+#if RFEC_WIRE_FRAME_PRIO == 2
+    __builtin_amdgcn_s_setprio(3);
+#endif
     constexpr int ND = B / 4;
     uint32_t w[ND];
 #pragma unroll
@@ -421,7 +429,13 @@ __device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, ui
                 hd = lane == (uint32_t)L ? H.h[L * ND + k] : hd;
         w[k] = (pay[k] | hd) & len_mask<B>(k, lane, n);
     }
+#if RFEC_WIRE_FRAME_PRIO == 1
+    __builtin_amdgcn_s_setprio(3); // the CRC's dependent LDS / DPP chain ahead of the other waves' work
+#endif
     const uint32_t crc = wave_crc32<B>(T, w, n, RFEC_WIRE_CRC_SEED, lane);
+#if RFEC_WIRE_FRAME_PRIO == 1
+    __builtin_amdgcn_s_setprio(0);
+#endif
     // big-endian trailer at byte n: its first 4 - s bytes end dword n / 4, the
     // rest start the next one (both positions wave-uniform)
     const uint32_t be = bswap(crc), s = n & 3u, q0 = n >> 2, q1 = q0 + 1;
@@ -437,6 +451,9 @@ __device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, ui
     store_slot<B>(slot, dstride, lane, w, wb);
     if (lane == 0)
         *dlen_out = (uint16_t)(n + 4);
+#if RFEC_WIRE_FRAME_PRIO == 2
+    __builtin_amdgcn_s_setprio(0);
+#endif
 }
 
 template <int B>
@@ -492,6 +509,14 @@ __device__ __forceinline__ uint32_t load_seg_fields(const rfec_hdr* __restrict__
     return h | s;
 }
 
+// end of a datagram's processing under RFEC_WIRE_FRAME_PRIO == 3
+__device__ __forceinline__ void frame_prio_end()
+{
+#if RFEC_WIRE_FRAME_PRIO == 3
+    __builtin_amdgcn_s_setprio(0);
+#endif
+}
+
 // Ping-pong software pipeline over datagrams d0, d0 + nw, ...: the loads of
 // datagram i+1 go into the other buffer before datagram i is processed, and
 // no register copy ever waits on them (vmcnt is an in-order counter).
@@ -505,11 +530,13 @@ __device__ __forceinline__ void ping_pong(uint32_t d, uint32_t count, uint32_t n
         const uint32_t d1 = d + nw;
         load(min(d1, count - 1), b);
         proc(a, d);
+        frame_prio_end();
         if (d1 >= count)
             break;
         const uint32_t d2 = d1 + nw;
         load(min(d2, count - 1), a);
         proc(b, d1);
+        frame_prio_end();
         if (d2 >= count)
             break;
         d = d2;
@@ -659,6 +686,9 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
                                       load_window<ND + 1>(parity + (size_t)dd * stride, range, off, P.w);
                               },
                               [&](const PW& P, uint32_t d) {
+#if RFEC_WIRE_FRAME_PRIO == 3
+            __builtin_amdgcn_s_setprio(3);
+#endif
             const uint32_t o = order ? order[d] : d; // output slot
             uint8_t* slot = dgram + (size_t)o * dstride;
             const uint32_t L = fld(P.f, 11);
@@ -764,6 +794,9 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                                       load_window<ND + 2>(shards + (size_t)dd * stride, range, off, P.w);
                               },
                               [&](const PW& P, uint32_t d) {
+#if RFEC_WIRE_FRAME_PRIO == 3
+            __builtin_amdgcn_s_setprio(3);
+#endif
             RFEC_DIAG_LOAD_ONLY(diag_fold(P.w) ^ P.f, dgram)
             const uint32_t o = order ? order[d] : d; // output slot
             uint8_t* slot = dgram + (size_t)o * dstride;
