@@ -234,6 +234,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
     void* q = reinterpret_cast<void*>((uint64_t)hi << 32 | lo);
     return __builtin_amdgcn_make_buffer_rsrc(q, 0, (int)__builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
 }
+// Parse: wave priority 3 over 1 = the payload store, 2 = a datagram's
+// processing, 3 = the batch header pass, 4 = 1 and 3; 0 = none
+#ifndef RFEC_WIRE_PARSE_PRIO
+#define RFEC_WIRE_PARSE_PRIO 4
+#endif
 // Frame kernels: wave priority 3 over 1 = the CRC, 2 = finish_frame (CRC,
 // trailer, store staging), 3 = a whole datagram's processing; 0 = none
 #ifndef RFEC_WIRE_FRAME_PRIO
@@ -1242,6 +1247,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
     uint32_t pk = 0, i = kWave; // i: the datagram's index in its batch (kWave: a batch starts)
     auto proc = [&](const PW& P, uint32_t d) {
         const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)pk, (int)i++);
+#if RFEC_WIRE_PARSE_PRIO == 2
+        __builtin_amdgcn_s_setprio(3);
+#endif
         RFEC_DIAG_LOAD_ONLY(diag_fold(P) ^ f, payload)
         const uint32_t len = f & 0xfffu, at1 = (f >> 12) & 63u, dsize = (f >> 18) & 0xfffu;
         bool ok = false;
@@ -1298,8 +1306,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
         const uint32_t dsz = ok && at1 ? dsize : 0u, at = at1 ? at1 - 1u : 0u;
         uint8_t* slot = payload + (size_t)d * stride;
         if constexpr (B == 20) {
+#if RFEC_WIRE_PARSE_PRIO == 1 || RFEC_WIRE_PARSE_PRIO == 4
+            __builtin_amdgcn_s_setprio(3);
+#endif
             store_payload20(wb, slot, stride, at, dsz, lane);
             wave_lds_sync(); // the buffer is refilled by the next datagram
+#if RFEC_WIRE_PARSE_PRIO == 1 || RFEC_WIRE_PARSE_PRIO == 2 || RFEC_WIRE_PARSE_PRIO == 4
+            __builtin_amdgcn_s_setprio(0);
+#endif
         } else {
             uint32_t pay[ND];
             shift_down_bytes<B>(w, at, pay);
@@ -1328,8 +1342,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
                 in.H[k] = (k == 0 ? 0x1701u : k == 6 ? 0xB004u : 0u) + (dstride >> 16);
             pk = decode_header<B>(in, recs, dl, lane < cnt, dstride, capacity);
 #else
+#if RFEC_WIRE_PARSE_PRIO == 3 || RFEC_WIRE_PARSE_PRIO == 4
+            __builtin_amdgcn_s_setprio(3);
+#endif
             load_header(dgram, dlen, dl, lane < cnt, dstride, in);
             pk = decode_header<B>(in, recs, dl, lane < cnt, dstride, capacity);
+#if RFEC_WIRE_PARSE_PRIO == 3 || RFEC_WIRE_PARSE_PRIO == 4
+            __builtin_amdgcn_s_setprio(0);
+#endif
 #endif
             i = 0;
         }
