@@ -51,7 +51,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 from razor_amd.dist import shard_groups  # noqa: E402
-from razor_amd.fec import HDR_DTYPE, native  # noqa: E402
+from razor_amd.fec import HDR_DTYPE, Native, native  # noqa: E402
 
 METRIC = "FEC encode+decode GiB/s (device-resident), 1200B pkts k=10/r=3; % HBM peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -402,6 +402,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--tuning", type=int, default=0)
+    ap.add_argument("--lib", default="", help="A/B only: another build of librazor_fec.so")
     ap.add_argument("--timing", choices=("own", "bracket"), default="own",
                     help="roofline launch duration: the kernel's own start/stop events (hipExtLaunchKernel) or "
                          "stream events around the call")
@@ -436,7 +437,7 @@ def main():
     torch.cuda.set_device(local % ndev)
     device = torch.device("cuda", local % ndev)
 
-    lib = native(1000)
+    lib = Native(1000, args.lib) if args.lib else native(1000)
     lib.set_tuning(args.tuning)
     custom = args.groups or args.total_groups or args.k or args.payload or args.col or args.full_plan
     cfg_name = args.config if args.config != "auto" else ("c4" if world > 1 else "c3")
