@@ -240,7 +240,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
 #define RFEC_WIRE_PARSE_PRIO 4
 #endif
 // Frame kernels: wave priority 3 over 1 = the CRC, 2 = finish_frame (CRC,
-// trailer, store staging), 3 = a whole datagram's processing; 0 = none
+// trailer, store staging), 3 = a whole datagram's processing, 4 = the header
+// bytes and finish_frame; 0 = none
 #ifndef RFEC_WIRE_FRAME_PRIO
 #define RFEC_WIRE_FRAME_PRIO 2
 #endif
@@ -456,7 +457,7 @@ __device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, ui
     store_slot<B>(slot, dstride, lane, w, wb);
     if (lane == 0)
         *dlen_out = (uint16_t)(n + 4);
-#if RFEC_WIRE_FRAME_PRIO == 2
+#if RFEC_WIRE_FRAME_PRIO == 2 || RFEC_WIRE_FRAME_PRIO == 4
     __builtin_amdgcn_s_setprio(0);
 #endif
 }
@@ -729,6 +730,9 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
                     stage_window<48, ND + 1>(P.w, lane, wb, x);
                 else
                     win_dwords<B, 48>(P.w, lane, x);
+#if RFEC_WIRE_FRAME_PRIO == 4
+                __builtin_amdgcn_s_setprio(3);
+#endif
                 funnel<ND, 3>(x, pay); // window [B j - 48, ...) -> bytes [B j - 45, ...)
                 finish_frame<B>(T, H, 45 + L, pay, lane, slot, dstride, dlen + o, wb);
             }
@@ -839,6 +843,9 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                     stage_window<32, ND + 2>(P.w, lane, wb, x);
                 else
                     win_dwords<B, 32>(P.w, lane, x);
+#if RFEC_WIRE_FRAME_PRIO == 4
+                __builtin_amdgcn_s_setprio(3);
+#endif
                 // window [B j - 32, ...) shifted by 32 - hs bytes
 #if defined(RFEC_WIRE_DIAG_NO_HDR) // lab: header bytes left zero, one layout
                 hs = 26, H.h[0] = layout ^ s.uid;
