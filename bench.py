@@ -13,12 +13,17 @@ One step = encode one buffer set, then recover the set encoded one step
 earlier (receiver order: its parity arrived over the network, so it is not
 in the 256 MB MALL), over >= 2 disjoint buffer sets rotated per step.
 
-Multi-GPU (BASELINE.json configs[3]): one process per GPU; the driver starts
-them with torchrun, `bench.py --gpus N` alone starts them itself.  At
-WORLD_SIZE > 1 the default is config 4: 1,048,576 groups split into
-contiguous slices (razor_amd/dist.py), no data-path collective; the control
-plane (barrier, max-over-ranks time, byte sum) is a CPU gloo group, so no
-RCCL is brought up and several ranks may share one GPU.
+Multi-GPU: one process per GPU; the driver starts them with torchrun,
+`bench.py --gpus N` alone starts them itself.  FEC groups are independent, so
+the default at every N is weak scaling of config 3: rank r runs groups
+[r * 65,536, (r + 1) * 65,536) of the same stream -- the N = 1 workload per GPU,
+so value(N) / (N * value(1)) is a scaling efficiency.  `--config c4` is
+BASELINE.json configs[3] at any N (N = 1 included): 1,048,576 groups split
+into contiguous slices (razor_amd/dist.py), strong scaling.  No data-path
+collective; the control plane (barrier, max-over-ranks time, byte sum) is a
+CPU gloo group, so no RCCL is brought up and several ranks may share one GPU.
+Every rank checks its slice against the reference's digest of exactly those
+groups (tests/golden/full_hashes.json: c2 / the weak chunks, the c4 slices).
 
 Timing: `value` is the wall clock of the K timed steps (barrier + device
 synchronize on both sides, max over ranks).  The roofline's launch duration
@@ -60,6 +65,7 @@ GOLDEN = ROOT / "tests" / "golden" / "full_hashes.json"
 # name -> (k, S, plan, total groups, config id of the input stream, golden digest case)
 CONFIGS = {
     "c3": dict(k=10, S=1200, plan="rows", groups=65536, config_id=2, golden="c2_k10_rows_S1200_G65536",
+               weak_golden="c3_weak_k10_rows_S1200_G524288",
                desc="BASELINE configs[2]: encode + decode, k=10 r=3, 1200 B, 2 erasures/group"),
     "c3full": dict(k=10, S=1200, plan="full", groups=65536, config_id=3, golden="c3_k10_full_S1200_G65536",
                    desc="configs[2] variant: the reference sender's full 3x4 plan (7 parities)"),
@@ -161,8 +167,8 @@ class Workload:
             self.rx_hdr[gi, e] = 0
         self.recovered = torch.empty((G, 2), dtype=torch.int64, device=dev)
         # recovered segments: into a dense output [G][2] (rfec_recover_batch_out, as flex_fec_recover's
-        # caller-allocated out_seg) where the plan's lines are disjoint, else in place (cascades)
-        self.dense = not (in_place or full_plan)
+        # caller-allocated out_seg), or in place (rfec_recover_batch, --in-place)
+        self.dense = not in_place
         if self.dense:
             self.out_shards = torch.empty((G, 2, self.stride), dtype=torch.uint8, device=dev)
             self.out_hdr = torch.empty((G, 2, 20), dtype=torch.uint8, device=dev)
@@ -357,8 +363,11 @@ def load_traffic(workload_name, kind):
         return None
 
 
-def golden_digest(case, world, rank):
-    """The reference's digest of this rank's slice (tests/golden/full_hashes.json)."""
+def golden_digest(case, world, rank, chunk=0):
+    """The reference's digest of this rank's groups (tests/golden/full_hashes.json):
+    the whole case at world 1; the strong-scaling slice [G r / N, G (r + 1) / N)
+    ("slices"); with `chunk`, the weak-scaling slice [r chunk, (r + 1) chunk)
+    ("chunks")."""
     try:
         cases = {c["name"]: c for c in json.loads(GOLDEN.read_text())["cases"]}
     except (OSError, ValueError):
@@ -366,6 +375,9 @@ def golden_digest(case, world, rank):
     c = cases.get(case)
     if c is None:
         return None
+    if chunk:
+        ch = c.get("chunks", [])
+        return ch[rank] if c.get("chunk") == chunk and rank < len(ch) else None
     if world == 1:
         return c["sha256"]
     return c.get("slices", {}).get(str(world), [None] * world)[rank]
@@ -390,8 +402,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="auto", choices=["auto"] + list(CONFIGS),
-                    help="auto: c3 at one rank, c4 (1M groups split) at WORLD_SIZE > 1")
+    ap.add_argument("--config", default="c3", choices=list(CONFIGS),
+                    help="c3 (default): weak scaling, 65,536 groups per GPU; c4: 1M groups split over the GPUs")
     ap.add_argument("--groups", type=int, default=0, help="custom: groups per GPU (weak scaling)")
     ap.add_argument("--total-groups", type=int, default=0, help="custom: split this many groups over the GPUs")
     ap.add_argument("--k", type=int, default=0)
@@ -440,7 +452,7 @@ def main():
     lib = Native(1000, args.lib) if args.lib else native(1000)
     lib.set_tuning(args.tuning)
     custom = args.groups or args.total_groups or args.k or args.payload or args.col or args.full_plan
-    cfg_name = args.config if args.config != "auto" else ("c4" if world > 1 else "c3")
+    cfg_name = args.config
     cfg = dict(CONFIGS[cfg_name])
     if args.full_plan:
         cfg.update(plan="full", config_id=3)
@@ -545,15 +557,19 @@ def main():
             want = golden_digest(cfg["golden"], world, rank)
         elif cfg["golden"] and group0 == 0:
             want = golden_digest(cfg["golden"], 1, 0)
+        elif cfg.get("weak_golden"):  # weak scaling: this rank's chunk of the stream
+            want = golden_digest(cfg["weak_golden"], world, rank, chunk=w.G)
         if want is not None:
             digest_ok = w.digest() == want
             verified = verified and digest_ok
     if dist:
-        vt = torch.tensor([1 if verified in (None, True) else 0, 1 if digest_ok else 0, 1 if digest_ok is None else 0],
-                          dtype=torch.int32)
+        # verified: every rank's checks held; digest: True only when every rank had a reference digest for
+        # its groups and matched it, False when any rank mismatched, None when some rank had none
+        vt = torch.tensor([1 if verified in (None, True) else 0, 0 if digest_ok is False else 1,
+                           1 if digest_ok is True else 0], dtype=torch.int32)
         dist.all_reduce(vt, op=dist.ReduceOp.MIN)
         verified = None if args.no_verify else bool(vt[0].item())
-        digest_ok = None if (args.no_verify or vt[2].item()) else bool(vt[1].item())
+        digest_ok = None if args.no_verify else (False if not vt[1].item() else (True if vt[2].item() else None))
 
     # whole-job bytes: every rank's slice (equal slices up to one group)
     nb = torch.tensor([w.enc_bytes + w.dec_bytes, w.G], dtype=torch.float64)
@@ -577,7 +593,9 @@ def main():
         per = ("one lane per (group, output slot, chunk)" if w.dense and 2 <= len(lines)
                else "one lane per (group, line, chunk)")
         if full_plan:
-            dec_kernels = "k_decode_cascade + k_decode_fixup (one launch + fix-up, in place)"
+            dec_kernels = ("k_decode_cascade (one launch; one lane per (group, " +
+                           ("output slot" if w.dense else "schedule step") + ", chunk), schedule and header checks "
+                           "per lane)")
         elif cd >= 64 and rows_layout and (k, lines[0]) in ((10, 4), (32, 4)):
             dec_kernels = f"k_decode_rows<{k},{lines[0]}> ({per}; header blocks spread)"
         elif cd >= 64:
@@ -607,8 +625,14 @@ def main():
             "dtype": "u8",
             "data": (f"synthetic: SURVEY §8(d) xorshift64* payloads (config id {cfg['config_id']}, generated on the "
                      f"device by jump-ahead), sequential headers; resident in HBM before timing"),
-            "config": {"workload": f"{cfg_name}: {workload_name}" + (f" (rank 0's slice of {total})"
-                                                                     if scaling == "strong" and world > 1 else ""),
+            "config": {"workload": f"{cfg_name}: {workload_name}" + (
+                           (f" (rank 0's slice of {total})" if scaling == "strong" else
+                            f" per GPU x {world} (weak scaling: rank r runs groups [r*{w.G}, (r+1)*{w.G}))")
+                           if world > 1 else ""),
+                       "scaling_rule": ("weak: every GPU runs the N = 1 workload on its own groups, value = all "
+                                        "ranks' bytes / max-over-ranks time" if scaling == "weak" else
+                                        "strong: the config's groups split over the GPUs (--config c4 at N = 1 "
+                                        "runs all of them on one GPU)"),
                        "config": cfg_name, "desc": cfg["desc"], "groups_per_gpu": w.G, "total_groups": total,
                        "k": k, "r": w.n, "payload_bytes": S, "plan": plan_desc,
                        "erasures_per_group": 2, "erasure_pairs": pairs_desc,

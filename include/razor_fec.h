@@ -174,8 +174,9 @@ int rfec_encode_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, u
  *   parity_present   [G] u64: bit l = parity line l was received
  *   recovered        [G][2] u64 out: bit i = segment i was recovered here
  *   workspace        rfec_recover_workspace_size(plan, G) bytes of device memory
- *                    (one peeling-schedule record per group, a fix-up list),
- *                    16-byte aligned; its contents need no initialisation
+ *                    (one peeling-schedule record per group, used by the
+ *                    generic peel + replay), 16-byte aligned; its contents
+ *                    need no initialisation
  * A line recovers its single missing member only under the conditions of
  * flex_recover_row/col and flex_fec_recover (sizes within fec_data_size).
  * `recovered` is authoritative: an erased slot whose bit stays clear holds
@@ -198,11 +199,13 @@ int rfec_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, 
  *   out_hdr    [g*per_group + e]           its recovered header record
  *   out_index  [g*per_group + e]           its segment index, or 0xFF where
  *                                          that erased segment was not recovered
- * and `recovered` gets its bit as in rfec_recover_batch (erased segments of
- * rank >= per_group are left out).  Plans whose lines are pairwise disjoint
- * (the row layer, strip mode: no recovery feeds another) with at most 8
- * members per line; others return RFEC_EINVAL (rfec_recover_batch recovers
- * them in place).  Same workspace as rfec_recover_batch.
+ * and `recovered` gets its bit as in rfec_recover_batch.  Any plan: where
+ * lines cascade (rows + columns), a recovered segment feeds the lines after
+ * it as in place.  Only erased segments of rank < per_group are recovered
+ * (they are the ones with an output slot), so with per_group at least the
+ * group's erasure count the result is rfec_recover_batch's; with fewer slots
+ * the peel runs as if the segments of higher rank could not be recovered.
+ * Same workspace as rfec_recover_batch.
  */
 int rfec_recover_batch_out(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
                            const uint8_t* shards, const rfec_hdr* hdr, const uint64_t* present,
@@ -599,34 +602,12 @@ int rfec_rx_session_push_datagrams_async(rfec_rx_session* s, uint32_t n, uint32_
 int rfec_rx_session_evict(rfec_rx_session* s, void* stream);
 int rfec_rx_session_get_info(const rfec_rx_session* s, rfec_rx_session_info* info);
 
-/* Kernel-selection knobs, for benchmarking and A/B tests (0 = defaults:
- * specialised row kernels where the plan allows, non-temporal streaming). */
-#define RFEC_TUNE_GENERIC 1u       /* always use the generic plan-driven kernel */
-#define RFEC_TUNE_PLAIN_LOADS 2u   /* plain instead of non-temporal payload loads */
-#define RFEC_TUNE_PLAIN_STORES 4u  /* plain instead of non-temporal parity / recovered stores */
-#define RFEC_TUNE_ITEMS2 8u        /* two chunk columns per lane in the row kernels */
-#define RFEC_TUNE_WAVE_DECODE 16u  /* one-launch recovery, one wave per group */
-#define RFEC_TUNE_PIPE_DECODE 32u  /* grid-stride recovery replay with record prefetch */
-#define RFEC_TUNE_WT_STORES 64u    /* write-through (sc0 sc1) parity / recovered stores */
-#define RFEC_TUNE_WT_NT 128u       /* with RFEC_TUNE_WT_STORES: sc0 sc1 nt */
-#define RFEC_TUNE_NT_STORES 512u   /* non-temporal parity / recovered stores */
-#define RFEC_TUNE_DIAG_CONST_SCHED 1024u /* DIAGNOSTIC ONLY: replay group 0's schedule everywhere */
-#define RFEC_TUNE_TWO_KERNEL_DECODE 4096u /* peel + replay even for disjoint plans (default there: fused) */
-#define RFEC_TUNE_GROUP_WAVE 8192u  /* payload lanes mapped per wave over whole groups (not the flat chunk index) */
-#define RFEC_TUNE_XCD_SWIZZLE 16384u /* consecutive payload blocks on the same XCD */
-#define RFEC_TUNE_LDS_HDR_PEEL 32768u /* fused decode: header work in LDS-staged peel blocks (default: one lane per group and line) */
-#define RFEC_TUNE_FLAT_ENCODE 65536u  /* row encode: one lane per (group, chunk column), all members (default: one lane per parity chunk) */
-#define RFEC_TUNE_META_TAIL 131072u   /* encode: header (meta) blocks at the tail of the grid instead of its head */
-#define RFEC_TUNE_HDR_HEAD 524288u    /* fused decodes: header blocks at the head of the grid (default: spread over it) */
-#define RFEC_TUNE_OUT_DECODE 2097152u  /* disjoint-plan decode: output-mapped also for slots under 64 chunks */
-#define RFEC_TUNE_SMALL_FUSED 4194304u /* small-slot disjoint decode (16 / 32 chunks): header checks in the payload lanes (k_decode_small), no header blocks */
-#define RFEC_TUNE_SMALL_B2 8388608u    /* with RFEC_TUNE_SMALL_FUSED: two fired lines per lane and pass (16-chunk slots) */
-#define RFEC_TUNE_LINEAR_BLOCKS 16777216u /* output-mapped row encode / decode: linear block order (default: XCD-swizzled) */
-#define RFEC_TUNE_LINE_LANES 33554432u /* row decode into a dense output: one lane per (group, row, chunk) (default: per (group, output slot, chunk)) */
-#define RFEC_TUNE_FLAT_DECODE 262144u /* disjoint-plan decode: one lane per (group, chunk column), every fired line (default: one lane per (group, line, chunk)) */
-/* (defaults: parity stores write-through, recovered stores non-temporal) */
-#define RFEC_TUNE_DIAG_NO_META 256u /* DIAGNOSTIC ONLY: skip fec_meta (wrong output) */
-#define RFEC_TUNE_DIAG_NO_HDR 1048576u /* DIAGNOSTIC ONLY: fused decode without its header blocks (wrong output) */
+/* Kernel selection, for tests: 0 = the default kernels (specialised where the
+ * plan allows); RFEC_TUNE_GENERIC = the plan-driven kernels for every plan
+ * (encode: one lane per (group, chunk column) over the plan's lines; recover
+ * in place: the LDS peel + schedule replay), the cross-check of the
+ * specialised ones.  Other bits are ignored. */
+#define RFEC_TUNE_GENERIC 1u
 void rfec_set_tuning(unsigned flags);
 unsigned rfec_get_tuning(void);
 

@@ -45,6 +45,7 @@ typedef struct {
     int matrix; /* 0: plan_from_fraction(k, pf, layers); 1: plan_matrix(k, row, col, layers) */
     int pf, row, col;
     unsigned layers;
+    uint32_t chunk; /* > 0: also a digest of every `chunk` groups (the weak-scaling ranks' slices) */
 } full_case;
 
 enum { CHUNK = 4096 };
@@ -102,6 +103,11 @@ static void run_case(FILE* js, const full_case* fc, int first)
     if (slices)
         for (int a = 0; a < 3; ++a)
             sha256_init(&cs[a][0]);
+    /* weak scaling (bench.py at N > 1): rank r runs groups [r * chunk, (r + 1) * chunk) */
+    const uint32_t nchunks = fc->chunk ? fc->G / fc->chunk : 0;
+    sha256_ctx* cc = nchunks ? (sha256_ctx*)malloc(sizeof(sha256_ctx) * nchunks) : NULL;
+    for (uint32_t c = 0; c < nchunks; ++c)
+        sha256_init(&cc[c]);
     uint64_t state[2] = {0, 0};
     for (uint32_t g0 = 0; g0 < fc->G; g0 += CHUNK) {
         const uint32_t ng = fc->G - g0 < CHUNK ? fc->G - g0 : CHUNK;
@@ -146,6 +152,8 @@ static void run_case(FILE* js, const full_case* fc, int first)
                 fs[l] = (uint16_t)L;
             }
             digest_group(&cref, par, meta, fs, n, stride);
+            if (nchunks)
+                digest_group(&cc[(g0 + gl) / fc->chunk], par, meta, fs, n, stride);
             for (int a = 0; slices && a < 3; ++a) {
                 const uint64_t g = (uint64_t)g0 + gl;
                 while (g >= (uint64_t)fc->G * (cur[a] + 1) / NS[a])
@@ -178,6 +186,18 @@ static void run_case(FILE* js, const full_case* fc, int first)
             "\"n_lines\": %u, \"window\": %u, \"sha256\": \"%s\"",
             first ? "" : ",\n", fc->name, (unsigned long long)fc->cfg, fc->G, k, S, stride, fc->ragged,
             fc->matrix ? "matrix" : "fraction", fc->pf, fc->row, fc->col, fc->layers, n, span, h1);
+    if (nchunks) {
+        fprintf(js, ", \"chunk\": %u, \"chunks\": [", fc->chunk);
+        for (uint32_t c = 0; c < nchunks; ++c) {
+            uint8_t d[32];
+            char hx[65];
+            sha256_final(&cc[c], d);
+            sha256_hex(d, hx);
+            fprintf(js, "%s\"%s\"", c ? ", " : "", hx);
+        }
+        fprintf(js, "]");
+        free(cc);
+    }
     if (slices) {
         fprintf(js, ", \"slices\": {");
         for (int a = 0; a < 3; ++a) {
@@ -218,6 +238,8 @@ int main(int argc, char** argv)
         {"c4_k10_rows_S1200_G1048576", 4, 1048576, 10, 1200, 0, 0, 80, 0, 0, RFEC_LAYER_ROWS},
         {"c5_k32_rows4_S256_G65536", 5, 65536, 32, 256, 0, 1, 0, 8, 4, RFEC_LAYER_ROWS},
         {"k10_full_ragged_S1000_G65536", 6, 65536, 10, 1000, 1, 0, 80, 0, 0, RFEC_LAYER_ROWS | RFEC_LAYER_COLS},
+        /* the c3 stream continued: the weak-scaling ranks' slices of 65,536 groups, N <= 8 */
+        {"c3_weak_k10_rows_S1200_G524288", 2, 524288, 10, 1200, 0, 0, 80, 0, 0, RFEC_LAYER_ROWS, 65536},
     };
     FILE* js = fopen(argv[1], "w");
     if (!js) {

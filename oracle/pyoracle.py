@@ -127,6 +127,8 @@ class Oracle:
                                           P, P, P, P, P, P]
         L.oracle_recover_batch.argtypes = [C.POINTER(rfec_plan), C.c_uint32, C.c_uint32, C.c_uint32,
                                            P, P, P, P, P, P, P, P]
+        L.oracle_recover_batch_out.argtypes = [C.POINTER(rfec_plan), C.c_uint32, C.c_uint32, C.c_uint32,
+                                               P, P, P, P, P, P, P, P, C.c_uint32, P, P, P]
         L.oracle_generate.argtypes = [P, C.c_int, P, C.c_int]
         L.oracle_recover.argtypes = [P, C.c_int, P, P]
         L.oracle_encode_aos.argtypes = [C.POINTER(rfec_plan), C.c_uint32, P, P]
@@ -218,6 +220,26 @@ class Oracle:
                                       _np_ptr(np.ascontiguousarray(fsize, np.uint16)),
                                       _np_ptr(np.ascontiguousarray(parity_present, np.uint64)), _np_ptr(rec))
         return shards, hdr, rec
+
+    def recover_batch_out(self, plan, shards, hdr, present, parity, meta, fsize, parity_present, capacity,
+                          per_group):
+        """rfec_recover_batch_out's semantics: returns (out_shards [G][E][stride],
+        out_hdr [G][E], out_index [G][E], recovered [G][2])."""
+        shards = np.ascontiguousarray(shards)
+        hdr = np.ascontiguousarray(hdr)
+        G, k, stride = shards.shape
+        E = per_group
+        rec = np.zeros((G, 2), np.uint64)
+        o_s = np.zeros((G, E, stride), np.uint8)
+        o_h = np.zeros((G, E), HDR_DTYPE)
+        o_i = np.zeros((G, E), np.uint8)
+        self.lib.oracle_recover_batch_out(C.byref(_as_oracle_plan(plan)), G, stride, capacity, _np_ptr(shards),
+                                          _np_ptr(hdr), _np_ptr(np.ascontiguousarray(present, np.uint64)),
+                                          _np_ptr(np.ascontiguousarray(parity)), _np_ptr(np.ascontiguousarray(meta)),
+                                          _np_ptr(np.ascontiguousarray(fsize, np.uint16)),
+                                          _np_ptr(np.ascontiguousarray(parity_present, np.uint64)), _np_ptr(rec), E,
+                                          _np_ptr(o_s), _np_ptr(o_h), _np_ptr(o_i))
+        return o_s, o_h, o_i, rec
 
     # -- wire codec ----------------------------------------------------------
     def crc32(self, data: bytes, seed: int = CRC_SEED) -> int:

@@ -327,10 +327,22 @@ void oracle_encode_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride
  * (member sizes <= fec_data_size, recovered size <= fec_data_size;
  * flex_fec_xor.c:88-89, 98-99).
  */
-void oracle_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
-                          uint8_t* shards, rfec_hdr* hdr, const uint64_t* present,
-                          const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fec_size,
-                          const uint64_t* parity_present, uint64_t* recovered)
+/* rank of erased segment t among the group's erased segments (index order) */
+static uint32_t erased_rank(const uint64_t pres[2], uint32_t t)
+{
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < t; ++i)
+        r += !BIT_GET(pres, i);
+    return r;
+}
+
+/* The canonical peel (flex_fec_receiver.c:105-206 to a fixpoint, lines in plan
+ * order; flex_fec_xor.c:55-104 per line) in place.  max_rank > 0: only erased
+ * segments of rank < max_rank may be recovered (the dense output's slots). */
+static void recover_batch_ranked(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
+                                 uint8_t* shards, rfec_hdr* hdr, const uint64_t* present,
+                                 const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fec_size,
+                                 const uint64_t* parity_present, uint64_t* recovered, uint32_t max_rank)
 {
     const uint32_t k = plan->k, n = plan->n_lines;
     for (uint32_t g = 0; g < groups; ++g) {
@@ -356,6 +368,8 @@ void oracle_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t strid
                     }
                 }
                 if (miss != 1 || got == 0)
+                    continue;
+                if (max_rank && erased_rank(&present[2 * g], t) >= max_rank)
                     continue;
                 size_t o = (size_t)g * n + l;
                 uint32_t L = fec_size[o];
@@ -393,6 +407,52 @@ void oracle_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t strid
         recovered[2 * g] = rec[0];
         recovered[2 * g + 1] = rec[1];
     }
+}
+
+void oracle_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
+                          uint8_t* shards, rfec_hdr* hdr, const uint64_t* present,
+                          const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fec_size,
+                          const uint64_t* parity_present, uint64_t* recovered)
+{
+    recover_batch_ranked(plan, groups, stride, capacity, shards, hdr, present, parity, meta, fec_size,
+                         parity_present, recovered, 0);
+}
+
+void oracle_recover_batch_out(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
+                              const uint8_t* shards, const rfec_hdr* hdr, const uint64_t* present,
+                              const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fec_size,
+                              const uint64_t* parity_present, uint64_t* recovered, uint32_t per_group,
+                              uint8_t* out_shards, rfec_hdr* out_hdr, uint8_t* out_index)
+{
+    const uint32_t k = plan->k;
+    uint8_t* sh = malloc((size_t)k * stride);
+    rfec_hdr* hd = malloc(sizeof(rfec_hdr) * k);
+    for (uint32_t g = 0; g < groups; ++g) {
+        memcpy(sh, shards + (size_t)g * k * stride, (size_t)k * stride);
+        memcpy(hd, hdr + (size_t)g * k, sizeof(rfec_hdr) * k);
+        /* one group at a time over copies: the plan's per-group arrays offset by g */
+        recover_batch_ranked(plan, 1, stride, capacity, sh, hd, present + 2 * g, parity + (size_t)g * plan->n_lines * stride,
+                             meta + (size_t)g * plan->n_lines, fec_size + (size_t)g * plan->n_lines,
+                             parity_present + g, recovered + 2 * g, per_group);
+        uint32_t e = 0;
+        for (uint32_t i = 0; i < k && e < per_group; ++i) {
+            if (BIT_GET(&present[2 * g], i))
+                continue;
+            const size_t o = (size_t)g * per_group + e;
+            if (BIT_GET(&recovered[2 * g], i)) {
+                memcpy(out_shards + o * stride, sh + (size_t)i * stride, stride);
+                out_hdr[o] = hd[i];
+                out_index[o] = (uint8_t)i;
+            } else {
+                out_index[o] = 0xFF;
+            }
+            ++e;
+        }
+        for (; e < per_group; ++e)
+            out_index[(size_t)g * per_group + e] = 0xFF;
+    }
+    free(sh);
+    free(hd);
 }
 
 /* ---- reference-shaped AoS path (CPU baseline) ------------------------------ */

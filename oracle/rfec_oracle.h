@@ -52,6 +52,14 @@ void oracle_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t strid
                           uint8_t* shards, rfec_hdr* hdr, const uint64_t* present,
                           const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fec_size,
                           const uint64_t* parity_present, uint64_t* recovered);
+/* rfec_recover_batch_out's semantics (include/razor_fec.h): the same peel on a
+ * copy of each group in which only erased segments of rank < per_group may be
+ * recovered; out slot e = the e-th erased segment (bytes, header, index or 0xFF). */
+void oracle_recover_batch_out(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
+                              const uint8_t* shards, const rfec_hdr* hdr, const uint64_t* present,
+                              const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fec_size,
+                              const uint64_t* parity_present, uint64_t* recovered, uint32_t per_group,
+                              uint8_t* out_shards, rfec_hdr* out_hdr, uint8_t* out_index);
 
 /* Reference-shaped CPU path for the baseline: per group, builds sim_segment_t*
  * arrays over AoS segments (segs[G*k], each sizeof(sim_segment_t) at this

@@ -89,8 +89,11 @@ int rfec_num_packets(uint16_t k, uint8_t protect_fraction, uint8_t* row, uint8_t
             r = 1;
             c = (uint8_t)n;
         } else {
+            /* the reference stores col in a uint8_t before dividing by it: a group of
+             * >= 256 segments can truncate it to 0 and divide by zero there
+             * (flex_fec_sender.c:122-126); here such a group gets no parity */
             c = (uint8_t)(n / lines + (n % lines > 0));
-            r = (uint8_t)(n / c + (n % c != 0));
+            r = c ? (uint8_t)(n / c + (n % c != 0)) : 0;
         }
     }
     if (row)
@@ -241,7 +244,7 @@ int rfec_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, 
     if (!shards || !hdr || !present || !parity_present || !recovered || !workspace ||
         (plan->n_lines && (!parity || !meta || !fec_size)))
         return set_err(RFEC_EINVAL, "NULL buffer", 0);
-    if ((uintptr_t)workspace % 16) /* schedule records are read as 16-B vectors, the fix-up counter atomically */
+    if ((uintptr_t)workspace % 16) /* schedule records are read as 16-B vectors */
         return set_err(RFEC_EINVAL, "workspace must be 16-byte aligned", 0);
     {   /* the fused decode's header lanes: one per (group, line slot), 32-bit lane index */
         unsigned lg = 1;
@@ -282,13 +285,6 @@ int rfec_recover_batch_out(const rfec_plan* plan, uint32_t groups, uint32_t stri
         return set_err(RFEC_EINVAL, "workspace must be 16-byte aligned", 0);
     static __thread rfec_kmask M;
     make_masks(plan, &M);
-    uint64_t seen0 = 0, seen1 = 0;
-    for (int l = 0; l < plan->n_lines; ++l) {
-        if (plan->line[l].count > 8 || (seen0 & M.mask[l][0]) || (seen1 & M.mask[l][1]))
-            return set_err(RFEC_EINVAL, "dense output needs pairwise disjoint lines of <= 8 members", 0);
-        seen0 |= M.mask[l][0];
-        seen1 |= M.mask[l][1];
-    }
     {   /* header lanes: one per (group, line slot), 32-bit lane index */
         unsigned lg = 1;
         while ((1u << lg) < plan->n_lines)

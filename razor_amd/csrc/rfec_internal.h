@@ -19,29 +19,6 @@ typedef struct {
 
 /* kernel flags == the RFEC_TUNE_* bits of razor_fec.h */
 #define RFEC_KFLAG_GENERIC RFEC_TUNE_GENERIC
-#define RFEC_KFLAG_PLAIN_LOADS RFEC_TUNE_PLAIN_LOADS
-#define RFEC_KFLAG_PLAIN_STORES RFEC_TUNE_PLAIN_STORES
-#define RFEC_KFLAG_WAVE_DECODE RFEC_TUNE_WAVE_DECODE
-#define RFEC_KFLAG_PIPE_DECODE RFEC_TUNE_PIPE_DECODE
-#define RFEC_KFLAG_WT_STORES RFEC_TUNE_WT_STORES
-#define RFEC_KFLAG_WT_NT RFEC_TUNE_WT_NT
-#define RFEC_KFLAG_NT_STORES RFEC_TUNE_NT_STORES
-#define RFEC_KFLAG_ITEMS2 RFEC_TUNE_ITEMS2
-#define RFEC_KFLAG_DIAG_NO_META RFEC_TUNE_DIAG_NO_META
-#define RFEC_KFLAG_TWO_KERNEL_DECODE RFEC_TUNE_TWO_KERNEL_DECODE
-#define RFEC_KFLAG_GROUP_WAVE RFEC_TUNE_GROUP_WAVE
-#define RFEC_KFLAG_XCD_SWIZZLE RFEC_TUNE_XCD_SWIZZLE
-#define RFEC_KFLAG_LDS_HDR_PEEL RFEC_TUNE_LDS_HDR_PEEL
-#define RFEC_KFLAG_FLAT_ENCODE RFEC_TUNE_FLAT_ENCODE
-#define RFEC_KFLAG_META_TAIL RFEC_TUNE_META_TAIL
-#define RFEC_KFLAG_FLAT_DECODE RFEC_TUNE_FLAT_DECODE
-#define RFEC_KFLAG_HDR_HEAD RFEC_TUNE_HDR_HEAD
-#define RFEC_KFLAG_OUT_DECODE RFEC_TUNE_OUT_DECODE
-#define RFEC_KFLAG_DIAG_NO_HDR RFEC_TUNE_DIAG_NO_HDR
-#define RFEC_KFLAG_SMALL_FUSED RFEC_TUNE_SMALL_FUSED
-#define RFEC_KFLAG_SMALL_B2 RFEC_TUNE_SMALL_B2
-#define RFEC_KFLAG_LINEAR_BLOCKS RFEC_TUNE_LINEAR_BLOCKS
-#define RFEC_KFLAG_LINE_LANES RFEC_TUNE_LINE_LANES
 
 int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, uint32_t capacity,
                        const uint8_t* shards, const rfec_hdr* hdr, uint8_t* parity, rfec_hdr* meta,
@@ -67,15 +44,10 @@ int rfec_launch_recover_out(const rfec_kmask* M, uint32_t groups, uint32_t strid
 /* bytes of one group's peeling-schedule record: step count, single-level
  * flag, then a (line, target) byte pair per step; 16-byte multiple */
 static inline uint32_t rfec_sched_record_bytes(uint32_t n_lines) { return (2u + 2u * n_lines + 15u) & ~15u; }
-/* recover workspace: the schedule records, then (one-launch cascade decode) a
- * 16-byte fix-up counter and a u32 list of the groups to replay exactly */
-static inline size_t rfec_ws_fix_offset(uint32_t n_lines, uint32_t groups)
-{
-    return ((size_t)groups * rfec_sched_record_bytes(n_lines) + 15u) & ~(size_t)15u;
-}
+/* recover workspace: the schedule records of the generic peel + replay */
 static inline size_t rfec_ws_bytes(uint32_t n_lines, uint32_t groups)
 {
-    return rfec_ws_fix_offset(n_lines, groups) + 16u + 4u * (size_t)groups;
+    return (size_t)groups * rfec_sched_record_bytes(n_lines);
 }
 int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
                                const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,

@@ -30,19 +30,6 @@ RFEC_MAX_LINES = 64
 RFEC_LAYER_ROWS = 1
 RFEC_LAYER_COLS = 2
 RFEC_TUNE_GENERIC = 1
-RFEC_TUNE_PLAIN_LOADS = 2
-RFEC_TUNE_PLAIN_STORES = 4
-RFEC_TUNE_WAVE_DECODE = 16
-RFEC_TUNE_PIPE_DECODE = 32
-RFEC_TUNE_WT_STORES = 64
-RFEC_TUNE_WT_NT = 128
-RFEC_TUNE_NT_STORES = 512
-RFEC_TUNE_ITEMS2 = 8
-RFEC_TUNE_DIAG_NO_META = 256
-RFEC_TUNE_DIAG_CONST_SCHED = 1024
-RFEC_TUNE_TWO_KERNEL_DECODE = 4096
-RFEC_TUNE_GROUP_WAVE = 8192
-RFEC_TUNE_XCD_SWIZZLE = 16384
 
 # 20-byte header record == sim_fec_meta_t layout (sim_proto.h:145-155)
 HDR_DTYPE = np.dtype([("seq", "<u4"), ("fid", "<u4"), ("ts", "<u4"), ("index", "<u2"), ("total", "<u2"),

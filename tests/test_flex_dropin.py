@@ -68,10 +68,8 @@ def list_pop(lst: base_list_t):
     return d
 
 
-@pytest.fixture(scope="module")
-def flex(product):
-    if not torch.cuda.is_available():
-        pytest.fail("no GPU visible: the -m gpu suite must run on an MI355X")
+def bind_flex(product):
+    """Declares the razor_flex.h symbols on the product's ctypes handle."""
     L = product.lib
     P = C.c_void_p
     for fn, res, args in (("flex_fec_sender_create", C.POINTER(flex_fec_sender_t), []),
@@ -88,6 +86,13 @@ def flex(product):
         f = getattr(L, fn)
         f.restype, f.argtypes = res, args
     return product
+
+
+@pytest.fixture(scope="module")
+def flex(product):
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the -m gpu suite must run on an MI355X")
+    return bind_flex(product)
 
 
 def make_segments(lib, shards, hdr):

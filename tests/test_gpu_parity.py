@@ -15,13 +15,7 @@ pytestmark = pytest.mark.gpu
 
 MANIFEST = po.manifest()
 CASES = {c["name"]: c for c in MANIFEST["cases"]}
-TUNINGS = {"default": 0, "generic": 1, "plain_loads": 2, "plain_stores": 4, "items2": 8, "wave_decode": 16,
-           "pipe_decode": 32, "wt_stores": 64, "wt_nt_stores": 192, "nt_stores": 512,
-           "generic_plain": 3, "two_kernel": 4096, "two_kernel_wt": 4096 | 64, "group_wave": 8192,
-           "group_wave_xcd": 8192 | 16384, "xcd": 16384, "lds_hdr_peel": 32768, "flat_encode": 65536,
-           "meta_tail": 131072, "meta_tail_nt": 131072 | 512, "flat_decode": 262144, "hdr_head": 524288,
-           "out_decode": 2097152, "out_decode_head": 2097152 | 524288, "small_fused": 4194304, "small_b2": 4194304 | 8388608, "linear": 16777216,
-           "line_lanes": 33554432, "out_decode_lines": 2097152 | 33554432}
+TUNINGS = {"default": 0, "generic": 1}  # RFEC_TUNE_GENERIC: the plan-driven kernels as the cross-check
 
 
 @pytest.fixture(scope="module")
@@ -42,8 +36,7 @@ def test_sender_random_fixture_gpu(gpu, oracle1000):
     pc.check_sender_random_case(gpu(), oracle1000, CASES["random_k"])
 
 
-@pytest.mark.parametrize("tuning", ["default", "generic", "group_wave", "group_wave_xcd", "flat_encode", "meta_tail",
-                                    "linear"])
+@pytest.mark.parametrize("tuning", list(TUNINGS))
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "rows"])
 def test_rows_fixture_gpu(gpu, oracle1000, oracle1200, name, tuning):
     c = CASES[name]
@@ -51,17 +44,18 @@ def test_rows_fixture_gpu(gpu, oracle1000, oracle1200, name, tuning):
     pc.check_rows_case(gpu(tuning=TUNINGS[tuning]), o, c, capacity=max(c["S"], 1000))
 
 
-@pytest.mark.parametrize("tuning", ["default", "wave_decode", "pipe_decode", "plain_loads", "wt_stores",
-                                    "plain_stores", "nt_stores", "two_kernel", "group_wave_xcd"])
+@pytest.mark.parametrize("output", ["in_place", "dense"])
+@pytest.mark.parametrize("tuning", list(TUNINGS))
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures"])
-def test_erasure_fixture_gpu(gpu, oracle1000, name, tuning):
-    pc.check_erasure_case(gpu(tuning=TUNINGS[tuning]), oracle1000, CASES[name])
+def test_erasure_fixture_gpu(gpu, oracle1000, name, tuning, output):
+    """The reference receiver's verdicts and segment hashes (era_*.bin) through
+    rfec_recover_batch (in place) and rfec_recover_batch_out (a slot per
+    segment, scattered back): every plan, the full 3x4 plan's cascades too."""
+    eng = gpu(tuning=TUNINGS[tuning])
+    pc.check_erasure_case(eng if output == "in_place" else pc.DenseAsInPlace(eng), oracle1000, CASES[name])
 
 
-@pytest.mark.parametrize("tuning", ["default", "wt_stores", "plain_stores", "plain_loads", "two_kernel",
-                                    "two_kernel_wt", "pipe_decode", "wave_decode", "group_wave",
-                                    "group_wave_xcd", "items2", "lds_hdr_peel", "flat_decode",
-                                    "generic", "hdr_head", "out_decode", "out_decode_head", "linear"])
+@pytest.mark.parametrize("tuning", list(TUNINGS))
 @pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "erasures" and c["rows_only"]])
 def test_erasure_fixture_rows_plan_gpu(gpu, oracle1000, name, tuning):
     """Row-parity-only fixtures against the row-layer plan (pairwise disjoint
@@ -149,7 +143,7 @@ def test_full_size_k10_roundtrip(product, oracle1200, layers):
     plan = lib.plan_from_fraction(k, 80, layers)
     shards, hdr, d_hdr = _device_batch(G, k, S, 1234)
     par, meta, fs, st = _run_encode(lib, plan, G, S, shards, d_hdr)
-    for tuning in (1, 2, 4, 8, 3, 64, 192, 512, 8192, 8192 | 16384, 16384, 65536, 131072, 131072 | 512, 16777216):
+    for tuning in (1,):
         par2, meta2, fs2, st2 = _run_encode(lib, plan, G, S, shards, d_hdr, tuning=tuning)
         assert torch.equal(par, par2) and torch.equal(meta, meta2) and torch.equal(fs, fs2), tuning
         del par2, meta2, fs2, st2
@@ -181,8 +175,7 @@ def test_full_size_k10_roundtrip(product, oracle1200, layers):
     ws = torch.empty((lib.workspace_size(plan, G),), dtype=torch.uint8, device=shards.device)
     exp = ((1 << er[:, 0]) | (1 << er[:, 1])).astype(np.int64)
     # default (fused one-launch decode for the disjoint row layer), forced peel + replay
-    for dec_tuning in (0, 4096, 4096 | 64, 8192, 8192 | 16384, 8, 8 | 64, 2, 4, 64, 262144, 524288, 1, 2097152,
-                       2097152 | 524288, 262144 | 524288):
+    for dec_tuning in (0, 1):
         rx = shards.clone()
         rx_hdr = d_hdr.clone()
         for c in range(2):
@@ -211,7 +204,7 @@ def test_full_size_k32_s256(product, oracle1000):
     assert plan.n_lines == 8
     shards, hdr, d_hdr = _device_batch(G, k, S, 99)
     par, meta, fs, st = _run_encode(lib, plan, G, S, shards, d_hdr)
-    for tuning in (1, 8, 8192, 8192 | 16384, 65536, 131072):
+    for tuning in (1,):
         par2, meta2, fs2, _ = _run_encode(lib, plan, G, S, shards, d_hdr, tuning=tuning)
         assert torch.equal(par, par2) and torch.equal(meta, meta2) and torch.equal(fs, fs2), tuning
     idx = np.r_[0:4, G - 4:G]
@@ -229,7 +222,7 @@ def test_full_size_k32_s256(product, oracle1000):
     pp[::5] &= ~(np.uint64(1) << er_rows[::5, 0].astype(np.uint64))  # parity of the first erased row lost
     exp = present.copy()
     gi = torch.arange(G, device=shards.device)
-    for dec_tuning in (0, 1, 4096, 262144, 524288, 2097152, 2097152 | 524288):
+    for dec_tuning in (0, 1):
         rx = shards.clone()
         rx_hdr = d_hdr.clone()
         for c in range(3):
@@ -386,7 +379,7 @@ def _mask_peel(plan, k, present, pp):
     return rec
 
 
-@pytest.mark.parametrize("tuning", ["default", "two_kernel", "nt_stores"])
+@pytest.mark.parametrize("tuning", list(TUNINGS))
 def test_cascade_header_rejections_gpu(gpu, oracle1000, tuning):
     """Full 3x4 plan groups whose headers make the exact peel reject lines the
     masks alone would fire (fec_data_size above capacity, a member larger than
@@ -491,7 +484,7 @@ def test_cascade_long_schedules_gpu(gpu, oracle1000, k):
 
 
 @pytest.mark.parametrize("k", [6, 7, 9, 11, 12, 13, 15, 16])
-@pytest.mark.parametrize("tuning", ["default", "two_kernel"])
+@pytest.mark.parametrize("tuning", list(TUNINGS))
 def test_full_plan_shapes_gpu(gpu, oracle1000, k, tuning):
     """The sender's full plans of k = 6..15 (3 or 4 columns, 5-8 lines: the
     one-launch cascade decode by default, peel + replay as the A/B) against
@@ -528,8 +521,7 @@ def test_full_plan_shapes_gpu(gpu, oracle1000, k, tuning):
 
 @pytest.mark.parametrize("k,col,S", [(10, 4, 64), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 1000),
                                      (96, 4, 512), (20, 3, 256), (24, 4, 1000), (13, 2, 1000)])
-@pytest.mark.parametrize("tuning", ["default", "hdr_head", "out_decode", "out_decode_head", "flat_decode", "generic",
-                                    "small_fused", "small_b2", "xcd", "linear"])
+@pytest.mark.parametrize("tuning", list(TUNINGS))
 def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tuning):
     """Row plans (disjoint lines: the fused decodes) with up to 6 erasures per
     group, lost parities and corrupted headers (fec_data_size above capacity or
@@ -584,8 +576,7 @@ def test_disjoint_decode_header_rejections_gpu(gpu, oracle1000, k, col, S, tunin
 
 @pytest.mark.parametrize("k,col,S", [(10, 4, 1200), (32, 4, 256), (12, 2, 16), (16, 8, 128), (10, 4, 64),
                                      (96, 4, 512), (20, 3, 256), (24, 4, 1200), (20, 3, 1200), (64, 4, 1024)])
-@pytest.mark.parametrize("tuning", ["default", "flat_decode", "out_decode", "hdr_head", "generic", "small_fused",
-                                    "small_b2", "xcd", "linear", "line_lanes", "out_decode_lines"])
+@pytest.mark.parametrize("tuning", list(TUNINGS))
 def test_dense_output_decode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning):
     """rfec_recover_batch_out (recovered segments into a dense output, as
     flex_fec_recover's caller-allocated out_seg): row plans with up to 6
@@ -647,16 +638,102 @@ def test_dense_output_decode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning)
         assert n_rec > G // 4
 
 
-def test_dense_output_rejects_cascading_plans(product):
-    """A plan with columns (recoveries feed each other) is refused before any launch."""
-    plan = product.plan_from_fraction(10, 80, 3)
-    with pytest.raises(Exception):
-        product.recover_batch_out(plan, 1, 1008, 1000, 16, 16, 16, 16, 16, 16, 16, 16, 2, 16, 16, 16, 16)
+def _lossy_rx(o, plan, k, G, S, rng, n_erase, p_lost_parity=0.2, corrupt=0.45):
+    """A received batch: n_erase(rng) erasures per group, a lost parity with
+    probability p_lost_parity, and (probability `corrupt`) header corruptions
+    that make the exact peel reject lines: fec_data_size above capacity or
+    below a member's size, a member's data_size above fec_data_size."""
+    shards, hdr = o.fill_groups(71 + k, G, k, S, ragged=True)
+    cap = min(o.video_size, S)
+    parity, meta, fsize, _ = o.encode_batch(plan, shards, hdr, cap)
+    present = np.zeros((G, 2), np.uint64)
+    pp = np.full(G, (1 << plan.n_lines) - 1, np.uint64)
+    rx, rh, fs_rx = shards.copy(), hdr.copy(), fsize.copy()
+    for g in range(G):
+        m = (1 << k) - 1
+        for i in rng.choice(k, int(n_erase(rng)), replace=False):
+            m &= ~(1 << int(i))
+            rx[g, i] = 0xA5
+            rh[g, i] = np.zeros((), po.HDR_DTYPE)
+        present[g, 0], present[g, 1] = m & (2**64 - 1), m >> 64
+        if rng.random() < p_lost_parity:
+            pp[g] &= ~np.uint64(1 << int(rng.integers(plan.n_lines)))
+        r = rng.random() / corrupt if corrupt else 1.0
+        if r < 1 / 3:
+            fs_rx[g, rng.integers(plan.n_lines)] = cap + 1
+        elif r < 2 / 3:
+            l = int(rng.integers(plan.n_lines))
+            fs_rx[g, l] = max(1, int(fs_rx[g, l]) - 3)
+        elif r < 1:
+            i = int(rng.integers(k))
+            if (m >> i) & 1:
+                rh[g, i]["size"] = min(cap, int(rh[g, i]["size"]) + 5)
+    return shards, hdr, rx, rh, present, parity, meta, fs_rx, pp, cap
+
+
+def _check_dense(got, exp, G, E, where):
+    o_s, o_h, o_i, rec = got
+    e_s, e_h, e_i, e_rec = exp
+    assert np.array_equal(rec, e_rec), f"{where}: recovered masks"
+    assert np.array_equal(o_i, e_i), f"{where}: out_index"
+    n = 0
+    for g in range(G):
+        for e in range(E):
+            if e_i[g, e] == 0xFF:
+                continue
+            n += 1
+            assert o_h[g, e] == e_h[g, e], f"{where}: group {g} out {e}: header"
+            L = int(e_h[g, e]["size"])
+            assert np.array_equal(o_s[g, e, :L], e_s[g, e, :L]), f"{where}: group {g} out {e}: data"
+    return n
+
+
+@pytest.mark.parametrize("k", [6, 9, 10, 12, 16])
+@pytest.mark.parametrize("tuning", list(TUNINGS))
+def test_dense_output_cascade_gpu(gpu, oracle1000, k, tuning):
+    """rfec_recover_batch_out over the sender's full plans (rows + columns,
+    recoveries cascade): 1-6 erasures per group, lost parities and header
+    rejections, E = 1..4 output slots and E = k; out slots, headers, indices and
+    recovered masks equal the oracle's dense restatement (only erased segments
+    of rank < E recoverable; E >= the erasure count gives the in-place peel).
+    Default: the one-launch register-schedule cascade decode; generic: the
+    LDS peel + replay into the dense output."""
+    o = oracle1000
+    plan = o.plan_from_fraction(k, 80, 3)
+    G, S = 500, 1000 if k <= 10 else 256
+    rng = np.random.default_rng(500 + k)
+    _, _, rx, rh, present, parity, meta, fs, pp, cap = _lossy_rx(o, plan, k, G, S, rng,
+                                                                 lambda r: r.integers(1, 7))
+    e_s, e_h, e_rec = o.recover_batch(plan, rx, rh, present, parity, meta, fs, pp, cap)
+    for E in (1, 2, 3, 4, k):
+        exp = o.recover_batch_out(plan, rx, rh, present, parity, meta, fs, pp, cap, E)
+        got = gpu(tuning=TUNINGS[tuning]).recover_out(plan, rx, rh, present, parity, meta, fs, pp, cap, E)
+        n = _check_dense(got, exp, G, E, f"k={k} E={E}")
+        assert n > G // 3, (E, n)
+        if E == k:  # every erased segment has a slot: the in-place peel's result
+            assert np.array_equal(exp[3], e_rec)
+
+
+@pytest.mark.parametrize("k", [36, 64])
+def test_dense_output_long_schedules_gpu(gpu, oracle1000, k):
+    """Full plans with more than 8 lines (generic peel + replay into the dense
+    output): 8-12 erasures, cascades that read recovered segments back from
+    their out slots."""
+    o = oracle1000
+    plan = o.plan_from_fraction(k, 80, 3)
+    G, S = 300, 256
+    rng = np.random.default_rng(900 + k)
+    _, _, rx, rh, present, parity, meta, fs, pp, cap = _lossy_rx(o, plan, k, G, S, rng,
+                                                                 lambda r: r.integers(8, 13), corrupt=0.3)
+    for E in (3, 12):
+        exp = o.recover_batch_out(plan, rx, rh, present, parity, meta, fs, pp, cap, E)
+        got = gpu().recover_out(plan, rx, rh, present, parity, meta, fs, pp, cap, E)
+        assert _check_dense(got, exp, G, E, f"k={k} E={E}") > G
 
 
 @pytest.mark.parametrize("k,col,S", [(12, 4, 1200), (24, 4, 1200), (12, 2, 16), (16, 8, 128), (20, 3, 256),
                                      (96, 4, 512), (50, 16, 1000), (7, 7, 1000), (100, 20, 64)])
-@pytest.mark.parametrize("tuning", ["default", "linear", "generic"])
+@pytest.mark.parametrize("tuning", list(TUNINGS))
 def test_row_plan_encode_gpu(gpu, oracle1000, oracle1200, k, col, S, tuning):
     """Row layouts other than the compiled k = 10 / 32 ones (strip-mode plans,
     flex_fec_sender.c:112-132) through the run-time-k output-mapped encode

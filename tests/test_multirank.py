@@ -93,3 +93,22 @@ def test_shard_groups_cover():
             assert sum(n for _, n in spans) == total
             assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(world - 1))
             assert max(n for _, n in spans) - min(n for _, n in spans) <= 1
+
+
+def test_bench_digest_rules():
+    """bench.py's reference digest per rank: the whole case at N = 1, the
+    strong-scaling slices of config 4, the weak-scaling chunks of the config 3
+    stream (chunk 0 is config 3's own digest)."""
+    sys.path[:0] = [str(ROOT)]
+    import bench
+
+    cases = {c["name"]: c for c in json.loads(bench.GOLDEN.read_text())["cases"]}
+    c2, weak, c4 = (cases["c2_k10_rows_S1200_G65536"], cases["c3_weak_k10_rows_S1200_G524288"],
+                    cases["c4_k10_rows_S1200_G1048576"])
+    assert bench.golden_digest("c2_k10_rows_S1200_G65536", 1, 0) == c2["sha256"]
+    assert weak["chunk"] == 65536 and len(weak["chunks"]) == 8 and weak["chunks"][0] == c2["sha256"]
+    for r in range(8):
+        assert bench.golden_digest(bench.CONFIGS["c3"]["weak_golden"], 8, r, chunk=65536) == weak["chunks"][r]
+    assert bench.golden_digest(bench.CONFIGS["c3"]["weak_golden"], 2, 1, chunk=4096) is None
+    for n in (2, 4, 8):
+        assert [bench.golden_digest("c4_k10_rows_S1200_G1048576", n, r) for r in range(n)] == c4["slices"][str(n)]

@@ -101,23 +101,47 @@ def test_c4_split_two_ranks_one_gpu(tmp_path):
     assert lo == c["groups"]
 
 
-def test_bench_two_ranks_one_gpu():
-    """bench.py --gpus 2 starts its own two ranks (torchrun, gloo control
-    plane) on the one GPU: one JSON line naming config 4, every rank's slice
-    equal to the reference digest."""
+def _bench(*args, timeout=600):
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
-    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-                        "--no-cpu", "--sets", "2"], capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
-    d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
-    assert d["config"]["config"] == "c4" and d["config"]["total_groups"] == 1048576
-    assert d["config"]["workload"].startswith("c4:")
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_one_gpu():
+    """bench.py --gpus 2 starts its own two ranks (torchrun, gloo control
+    plane) on the one GPU: one JSON line, weak scaling of config 3 (the N = 1
+    workload on each rank's own 65,536 groups), every rank's groups equal to
+    the reference digest of exactly those groups."""
+    d = _bench("--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu", "--sets", "2")
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert d["config"]["config"] == "c3" and d["config"]["groups_per_gpu"] == 65536
+    assert d["config"]["total_groups"] == 2 * 65536
+    assert d["config"]["workload"].startswith("c3: k10_r3_S1200_G65536 per GPU x 2")
     assert d["verified"] is True and d["verified_vs_reference_digest"] is True
     assert d["value"] > 0
     # one kernel per call: the roofline takes each kernel's own start / stop events
     for key in ("roofline", "decode_roofline"):
         assert d[key]["timing"].startswith("the kernel's own") and d[key]["launch_us"] > 0
+
+
+@pytest.mark.timeout(900)
+def test_bench_c4_strong_scaling_lines():
+    """--config c4 at N = 1 and N = 2 (two ranks on the one GPU): both lines
+    name config 4 over the same 1,048,576 groups (strong scaling), so their
+    ratio is an efficiency of the same workload; N = 2 checks each rank's
+    slice against the reference's slice digest."""
+    one = _bench("--gpus", "1", "--config", "c4", "--steps", "3", "--warmup", "1", "--no-cpu", "--sets", "1",
+                 "--no-verify")
+    two = _bench("--gpus", "2", "--config", "c4", "--steps", "3", "--warmup", "1", "--no-cpu", "--sets", "1")
+    for d, n in ((one, 1), (two, 2)):
+        assert d["n_gpus"] == n and d["scaling"] == "strong"
+        assert d["config"]["config"] == "c4" and d["config"]["total_groups"] == 1048576
+        assert d["config"]["workload"].startswith("c4: k10_r3_S1200_G")
+        assert d["value"] > 0
+    assert one["config"]["groups_per_gpu"] == 1048576 and two["config"]["groups_per_gpu"] == 524288
+    assert two["verified"] is True and two["verified_vs_reference_digest"] is True
