@@ -213,7 +213,7 @@ size_t rfec_recover_workspace_size(const rfec_plan* plan, uint32_t groups)
 {
     if (!plan)
         return 0;
-    return rfec_ws_bytes(plan->n_lines, groups);
+    return rfec_ws_bytes(plan->k, plan->n_lines, groups);
 }
 
 static void make_masks(const rfec_plan* p, rfec_kmask* M)
@@ -435,7 +435,7 @@ static di_layout di_offsets(void)
     DI_TAKE(present, RFEC_DI_GROUPS * 2 * sizeof(uint64_t));
     DI_TAKE(ppresent, RFEC_DI_GROUPS * sizeof(uint64_t));
     DI_TAKE(recovered, RFEC_DI_GROUPS * 2 * sizeof(uint64_t));
-    DI_TAKE(ws, rfec_ws_bytes(RFEC_MAX_LINES, RFEC_DI_GROUPS));
+    DI_TAKE(ws, rfec_ws_bytes(RFEC_MAX_K, RFEC_MAX_LINES, RFEC_DI_GROUPS));
 #undef DI_TAKE
     L.total = o;
     return L;

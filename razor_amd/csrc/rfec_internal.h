@@ -41,13 +41,18 @@ int rfec_launch_recover_out(const rfec_kmask* M, uint32_t groups, uint32_t strid
                             const uint64_t* parity_present, uint64_t* recovered, void* ws, void* stream,
                             unsigned flags, const rfec_dense_out* out);
 
-/* bytes of one group's peeling-schedule record: step count, single-level
- * flag, then a (line, target) byte pair per step; 16-byte multiple */
-static inline uint32_t rfec_sched_record_bytes(uint32_t n_lines) { return (2u + 2u * n_lines + 15u) & ~15u; }
-/* recover workspace: the schedule records of the generic peel + replay */
-static inline size_t rfec_ws_bytes(uint32_t n_lines, uint32_t groups)
+/* recover workspace, per group: the generic peel's schedule record (step
+ * count, single-level flag, then a (line, target) byte pair per step), or the
+ * cascade decode's 16-byte schedule record followed by one 4-byte task word
+ * per output slot (max(k, n_lines) of them); 16-byte multiple */
+static inline uint32_t rfec_sched_record_bytes(uint32_t k, uint32_t n_lines)
 {
-    return (size_t)groups * rfec_sched_record_bytes(n_lines);
+    const uint32_t peel = 2u + 2u * n_lines, casc = 16u + 4u * (k > n_lines ? k : n_lines);
+    return ((peel > casc ? peel : casc) + 15u) & ~15u;
+}
+static inline size_t rfec_ws_bytes(uint32_t k, uint32_t n_lines, uint32_t groups)
+{
+    return (size_t)groups * rfec_sched_record_bytes(k, n_lines);
 }
 int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
                                const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,

@@ -721,7 +721,16 @@ struct CascArgs {
     uint32_t E;               // dense slots per group; 0 = in place
     uint32_t groups, total, C, capacity;
     FastDiv divC, divQC;      // cd, Q * cd (Q = slots per group)
+    uint8_t* ws;              // per group (ws_stride bytes): the schedule record, then Q task words
+    uint32_t ws_stride, Q;
 };
+
+// A slot's task (the checker writes one per output slot of every group): the
+// line and target of the step that recovers the slot's segment (dense: the
+// slot's erased segment; in place: the slot-th step), bit 31 = there is one,
+// bit 30 = it reads a segment recovered by an earlier step (a cascade: the
+// payload lane then replays from the schedule record).
+constexpr uint32_t kTaskValid = 1u << 31, kTaskCascade = 1u << 30;
 
 // A schedule: step s = (line, target), packed so that no register array is
 // indexed at run time (no scratch).  Which earlier steps a step reads follows
@@ -999,17 +1008,29 @@ __device__ v4u cascade_check_lanes(const CascArgs& A, const rfec_kmask& M, uint3
                 rm |= 1ull << cs_tg(X, s2);
         A.recovered[2 * g] = rm;
         A.recovered[2 * g + 1] = 0;
-        if (A.E) { // out_index: the e-th erased segment's index where it was recovered, else 0xFF
-            uint64_t m = (uint64_t)erased;
-            for (uint32_t e = 0; e < A.E; ++e) {
-                uint32_t v = 0xFF;
-                if (m) {
-                    const uint32_t i = (uint32_t)__ffsll((long long)m) - 1;
-                    v = (rm >> i) & 1ull ? i : 0xFFu;
-                    m &= m - 1;
-                }
-                A.out_index[(size_t)g * A.E + e] = (uint8_t)v;
+        // the slots' tasks (and out_index: the e-th erased segment's index where it was recovered)
+        uint32_t* task = reinterpret_cast<uint32_t*>(A.ws + (size_t)g * A.ws_stride + 16);
+        uint64_t m = (uint64_t)erased;
+        for (uint32_t q = 0; q < A.Q; ++q) {
+            uint32_t ss = 8;
+            if (A.E) {
+                const uint32_t i = m ? (uint32_t)__ffsll((long long)m) - 1 : 0xFFu;
+                m &= m - 1;
+#pragma unroll
+                for (int s2 = 0; s2 < 8; ++s2)
+                    if ((uint32_t)s2 < X.n && cs_tg(X, s2) == i)
+                        ss = s2;
+                A.out_index[(size_t)g * A.E + q] = (uint8_t)(ss < 8 ? i : 0xFFu);
+            } else if (q < X.n) {
+                ss = q;
             }
+            uint32_t w = 0;
+            if (ss < 8) {
+                const uint32_t tl = cs_line(X, ss), tt = cs_tg(X, ss);
+                const bool casc = (M.mask[tl][0] & (uint64_t)erased & ~(1ull << tt)) != 0;
+                w = kTaskValid | (casc ? kTaskCascade : 0u) | tl | (tt << 8);
+            }
+            task[q] = w;
         }
     }
     return cs_pack(X);
@@ -1023,7 +1044,7 @@ __device__ v4u cascade_check_lanes(const CascArgs& A, const rfec_kmask& M, uint3
 constexpr int kCheckLanes = 4;
 
 template <typename MT>
-__global__ __launch_bounds__(kBlock) void k_cascade_check(CascArgs A, rfec_kmask M, v4u* __restrict__ recs)
+__global__ __launch_bounds__(kBlock) void k_cascade_check(CascArgs A, rfec_kmask M)
 {
     const uint32_t gt = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t g = gt / kCheckLanes, s = gt % kCheckLanes;
@@ -1031,14 +1052,15 @@ __global__ __launch_bounds__(kBlock) void k_cascade_check(CascArgs A, rfec_kmask
     const v4u r = cascade_check_lanes<MT, kCheckLanes>(A, M, live ? g : 0u, live, s,
                                                        (threadIdx.x & (kWave - 1)) & ~(uint32_t)(kCheckLanes - 1));
     if (live && s == 0)
-        recs[g] = r;
+        *reinterpret_cast<v4u*>(A.ws + (size_t)g * A.ws_stride) = r;
 }
 
-// The payload kernel: lane (group, slot, chunk column) reads its group's
-// received mask and schedule record in one round of loads, finds its step and
-// replays it (and, in a cascade, the steps it reads).  Like the row decode,
-// no lane does header work.
-__global__ __launch_bounds__(kBlock) void k_decode_cascade(CascArgs A, rfec_kmask M, const v4u* __restrict__ recs)
+// The payload kernel: lane (group, slot, chunk column) reads its slot's task
+// word and, for a single-level step (the common case), loads the line's
+// parity and other members, all in flight, and stores the recovered chunk --
+// no mask work, one dependent load before the payload loads.  A cascade step
+// replays the steps it reads from the group's schedule record.
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_decode_cascade(CascArgs A, rfec_kmask M)
 {
     __shared__ uint32_t lplan[RFEC_MAX_LINES];
     __shared__ uint64_t lmask[8];
@@ -1055,44 +1077,55 @@ __global__ __launch_bounds__(kBlock) void k_decode_cascade(CascArgs A, rfec_kmas
     const uint32_t q = fdiv(rem, A.divC);
     const uint32_t j = rem - q * A.divC.d;
     const uint32_t K = P.k, NL = P.n_lines, C = A.C;
+    const uint8_t* wg = A.ws + (size_t)g * A.ws_stride;
+    const uint32_t task = reinterpret_cast<const uint32_t*>(wg + 16)[q];
+    if (!(task & kTaskValid))
+        return;
+    const uint32_t l = task & 15u, tgt = (task >> 8) & 0xffu;
+    const v4u* grp = A.shards + (size_t)g * K * C + j;
+    const v4u* par = A.parity + (size_t)g * NL * C + j;
+    v4u* slot0 = A.E ? A.out_sh + (size_t)g * A.E * C + j : A.shards + (size_t)g * K * C + j;
+    v4u* dst = slot0 + (size_t)(A.E ? q : tgt) * C;
+    KCHECK(tgt < K && l < NL && j < C, "casc g %u q %u j %u: line %u target %u\n", g, q, j, l, tgt);
+    if (!(task & kTaskCascade)) { // single level: every other member arrived
+        const uint32_t ln = lplan[l];
+        const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
+        v4u acc = ld16(par + (size_t)l * C);
+        v4u mv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = first + u * stride;
+            mv[u] = v4u{0, 0, 0, 0};
+            if ((uint32_t)u < count && i != tgt)
+                mv[u] = ld16(grp + (size_t)i * C);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            acc ^= mv[u];
+        st16(dst, acc);
+        return;
+    }
+    // a cascade: the steps it reads, transitively (a step's erased members other than its target were
+    // recovered by earlier steps), replayed from the schedule record
     const uint64_t kmask = K >= 64 ? ~0ull : (1ull << K) - 1ull;
     const uint64_t erased = ~A.present[2 * g] & kmask;
-    const CSched S = cs_unpack(recs[g]);
-    uint32_t ss = 8; // this slot's step
-    if (A.E) {       // the step whose target is the q-th erased segment
-        uint64_t m = erased;
-        for (uint32_t u = 0; u < q; ++u)
-            m &= m - 1ull;
-        const uint32_t tq = m ? (uint32_t)__ffsll((long long)m) - 1 : 0xFFu;
+    const CSched S = cs_unpack(*reinterpret_cast<const v4u*>(wg));
+    uint32_t ss = 0;
 #pragma unroll
-        for (int s = 0; s < 8; ++s)
-            if ((uint32_t)s < S.n && cs_tg(S, s) == tq)
-                ss = s;
-    } else if (q < S.n) {
-        ss = q;
-    }
-    if (ss >= 8)
-        return;
-    // the steps it reads, transitively: a step's erased members other than its target were
-    // recovered by earlier steps (single level -- the common case -- when there are none)
+    for (int s = 0; s < 8; ++s)
+        if ((uint32_t)s < S.n && cs_tg(S, s) == tgt)
+            ss = s;
     uint32_t need = 1u << ss;
-    if (lmask[cs_line(S, ss)] & erased & ~(1ull << cs_tg(S, ss))) {
 #pragma unroll 1
-        for (int s = (int)ss; s >= 0; --s) {
-            if (!((need >> s) & 1u))
-                continue;
-            const uint64_t dm = lmask[cs_line(S, s)] & erased & ~(1ull << cs_tg(S, s));
-            for (int s2 = 0; s2 < s; ++s2)
-                if ((dm >> cs_tg(S, s2)) & 1ull)
-                    need |= 1u << s2;
-        }
+    for (int s = (int)ss; s >= 0; --s) {
+        if (!((need >> s) & 1u))
+            continue;
+        const uint64_t dm = lmask[cs_line(S, s)] & erased & ~(1ull << cs_tg(S, s));
+        for (int s2 = 0; s2 < s; ++s2)
+            if ((dm >> cs_tg(S, s2)) & 1ull)
+                need |= 1u << s2;
     }
-    v4u* slot0 = A.E ? A.out_sh + (size_t)g * A.E * C + j : A.shards + (size_t)g * K * C + j;
-    const v4u res = cascade_replay(S, need, ss, erased, A.shards + (size_t)g * K * C + j,
-                                   A.parity + (size_t)g * NL * C + j, slot0, A.E, C, lplan);
-    const uint32_t tgt = cs_tg(S, ss);
-    KCHECK(tgt < K && j < C, "casc g %u q %u j %u: ss %u target %u\n", g, q, j, ss, tgt);
-    st16(slot0 + (size_t)cs_slot(A.E, erased, tgt) * C, res);
+    st16(dst, cascade_replay(S, need, ss, erased, grp, par, slot0, A.E, C, lplan));
 }
 
 // ---------------------------------------------------------------------------
@@ -1714,23 +1747,25 @@ struct FusedArgs {
 // payload than header blocks keeps them at the head.
 inline uint32_t hdr_every(const FusedArgs& F, uint32_t npay) { return F.n_hdr ? npay / F.n_hdr : 0; }
 
-// cascade decode: the checker (schedule records into the workspace), then the payload lanes, Q slots
-// per group (dense: E, in place: one per possible step)
-void launch_cascade(CascArgs A, const rfec_kmask& M, uint32_t groups, uint32_t cd, void* ws, hipStream_t st)
+// cascade decode: the checker (schedule records and task words into the workspace), then the payload
+// lanes, Q slots per group (dense: E, in place: one per possible step)
+void launch_cascade(CascArgs A, const rfec_kmask& M, uint32_t groups, uint32_t cd, void* ws, uint32_t ws_stride,
+                    hipStream_t st)
 {
-    const uint32_t Q = A.E ? A.E : (M.plan.n_lines < M.plan.k ? M.plan.n_lines : M.plan.k);
+    A.Q = A.E ? A.E : (M.plan.n_lines < M.plan.k ? M.plan.n_lines : M.plan.k);
     A.groups = groups;
-    A.total = groups * Q * cd; // < 2^32: checked by the caller
+    A.total = groups * A.Q * cd; // < 2^32: checked by the caller
     A.divC = make_fastdiv(cd);
-    A.divQC = make_fastdiv(Q * cd);
-    v4u* recs = reinterpret_cast<v4u*>(ws);
+    A.divQC = make_fastdiv(A.Q * cd);
+    A.ws = reinterpret_cast<uint8_t*>(ws);
+    A.ws_stride = ws_stride;
     const dim3 gc(blocks_for((uint64_t)groups * kCheckLanes));
     if (M.plan.k <= 32)
-        RFEC_LAUNCH(k_cascade_check<uint32_t>, gc, dim3(kBlock), 0, st, A, M, recs);
+        RFEC_LAUNCH(k_cascade_check<uint32_t>, gc, dim3(kBlock), 0, st, A, M);
     else
-        RFEC_LAUNCH(k_cascade_check<uint64_t>, gc, dim3(kBlock), 0, st, A, M, recs);
+        RFEC_LAUNCH(k_cascade_check<uint64_t>, gc, dim3(kBlock), 0, st, A, M);
     const uint32_t nb = (blocks_for(A.total) + 7u) & ~7u; // whole rounds of 8 (XCD swizzle)
-    RFEC_LAUNCH(k_decode_cascade, dim3(nb), dim3(kBlock), 0, st, A, M, recs);
+    RFEC_LAUNCH(k_decode_cascade, dim3(nb), dim3(kBlock), 0, st, A, M);
 }
 
 // output-mapped fused decode: one lane per (group, line or output slot, chunk column)
@@ -1842,7 +1877,7 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
     B.sched = reinterpret_cast<uint8_t*>(ws);
     B.groups = groups;
     B.capacity = capacity;
-    B.rec_bytes = rfec_sched_record_bytes(P.n_lines);
+    B.rec_bytes = rfec_sched_record_bytes(P.k, P.n_lines);
     B.out_hdr = dense ? out->hdr : nullptr;
     B.out_index = dense ? out->index : nullptr;
     B.out_per_group = dense ? out->per_group : 0u;
@@ -1936,7 +1971,7 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
         A.E = DO.E;
         A.C = C;
         A.capacity = capacity;
-        launch_cascade(A, *M, groups, cd, ws, st);
+        launch_cascade(A, *M, groups, cd, ws, B.rec_bytes, st);
         return (int)hipGetLastError();
     }
     RFEC_LAUNCH(k_peel_lds, dim3(n_hdr), dim3(kBlock), 0, st, B, *M);

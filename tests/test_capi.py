@@ -76,7 +76,7 @@ def test_argument_validation(product):
     bad.line[0].count = 20  # member beyond k
     with pytest.raises(RfecError):
         product.encode_batch(bad, 4, 1200, 1200, 1, 1, 1, 1, 1, None)
-    assert product.workspace_size(plan, 100) == 100 * 16  # schedule records (2 + 2*3 -> 16 B)
+    assert product.workspace_size(plan, 100) == 100 * 64  # per group: schedule record + task words (16 + 4*10 -> 64 B)
     with pytest.raises(RfecError):  # workspace not 16-byte aligned (checked before any launch)
         product.recover_batch(plan, 4, 1200, 1200, 16, 16, 16, 16, 16, 16, 16, 16, 24, None)
     with pytest.raises(RfecError):  # groups * k beyond 32 bits
