@@ -94,7 +94,9 @@ int rfec_sim_video_size(void);
 /* ------------------------------------------------------------------------ */
 /* Batched device API                                                        */
 /* ------------------------------------------------------------------------ */
-#define RFEC_MAX_K 128     /* segments per group (sim_sender.c:370 flushes at 100) */
+#define RFEC_MAX_K 128     /* segments per group in recovery (sim_sender.c:370 flushes at 100) */
+#define RFEC_MAX_K_ENCODE 255 /* segments per group in an encode plan (rfec_line's 8-bit fields; razor's
+                                 flex sender keeps row and col in uint8_t, so no line exceeds it) */
 #define RFEC_MAX_LINES 64  /* parity lines per group */
 
 #define RFEC_OK 0
@@ -567,7 +569,8 @@ typedef struct {
     uint32_t cached_segments; /* skiplist_size(f->segs_cache) */
     uint32_t records_held;    /* parsed records kept for open state */
     uint32_t rows_held;       /* HBM payload rows allocated */
-    uint32_t reserved;
+    uint32_t pending;         /* datagrams of the batch the last _async call
+                                 started: the records its next call writes */
 } rfec_rx_session_info;
 
 /* NULL on bad arguments (stride % 16, capacity > stride) or no memory. */
@@ -590,7 +593,9 @@ int rfec_rx_session_push_datagrams(rfec_rx_session* s, uint32_t n, uint32_t dstr
 /* Pipelined form, one batch of latency: starts the parse of these n
  * datagrams on the session's own stream, then ingests the batch the previous
  * call started (control plane, peel) while the device parses this one, and
- * returns THAT batch's recovered segments (recs_out: its records).  dgram /
+ * returns THAT batch's recovered segments.  recs_out (HOST, may be NULL)
+ * receives THAT batch's records too, so it must hold the PREVIOUS call's n
+ * records (rfec_rx_session_get_info's `pending`), not this call's.  dgram /
  * dlen must stay unchanged until the next call on the session returns.
  * n == 0 only ingests the pending batch (the flush).  Deliveries, in total
  * and in order, equal rfec_rx_session_push_datagrams over the same batches;

@@ -217,8 +217,8 @@ static void write_parity(FILE* f, const sim_fec_t* p, uint32_t g, uint32_t line,
 }
 
 /* ---- encode cases driven by the reference sender --------------------------- */
-static void case_sender(const char* name, uint64_t cfg, uint32_t G, uint32_t k, uint32_t S, int ragged,
-                        uint8_t pf)
+static void case_sender_kind(const char* name, const char* kind, uint64_t cfg, uint32_t G, uint32_t k, uint32_t S,
+                             int ragged, uint8_t pf)
 {
     char fn[256];
     snprintf(fn, sizeof(fn), "enc_%s.bin", name);
@@ -243,10 +243,15 @@ static void case_sender(const char* name, uint64_t cfg, uint32_t G, uint32_t k, 
     fclose(f);
     char js[512];
     snprintf(js, sizeof(js),
-             "{\"name\": \"%s\", \"kind\": \"sender\", \"file\": \"%s\", \"config_id\": %llu, \"groups\": %u, "
+             "{\"name\": \"%s\", \"kind\": \"%s\", \"file\": \"%s\", \"config_id\": %llu, \"groups\": %u, "
              "\"k\": %u, \"S\": %u, \"ragged\": %d, \"protect_fraction\": %u, \"parities\": %ld}",
-             name, fn, (unsigned long long)cfg, G, k, S, ragged, pf, total);
+             name, kind, fn, (unsigned long long)cfg, G, k, S, ragged, pf, total);
     manifest_case(js);
+}
+
+static void case_sender(const char* name, uint64_t cfg, uint32_t G, uint32_t k, uint32_t S, int ragged, uint8_t pf)
+{
+    case_sender_kind(name, "sender", cfg, G, k, S, ragged, pf);
 }
 
 /* Random k / random protect fraction per group, one sender across groups. */
@@ -718,6 +723,14 @@ int main(int argc, char** argv)
     case_sender("k21_pf80_S104", 5, 8, 21, 104, 1, 80);   /* test_flex_sender shape: 9 parities */
     case_sender("k25_pf80_S256", 6, 8, 25, 256, 1, 80);   /* test_flex_receiver shape: 10 parities */
     case_sender("k100_pf200_S512", 7, 4, 100, 512, 1, 200);
+    /* groups above the batched recovery's 128 segments, through the reference sender; the group-level
+     * drop-in's large-group paths (one launch up to 255 segments, line by line above) */
+    case_sender_kind("k200_pf10_S104", "sender_large", 71, 2, 200, 104, 1, 10);   /* 14 x 15 matrix, 29 lines */
+    case_sender_kind("k200_pf5_S104", "sender_large", 72, 2, 200, 104, 1, 5);     /* strip: 4 rows of 50 */
+    case_sender_kind("k300_pf10_S64", "sender_large", 73, 1, 300, 64, 1, 10);     /* 17 x 18 matrix */
+    case_sender_kind("k1100_pf255_S64", "sender_large", 74, 1, 1100, 64, 1, 255); /* 55 x 20 matrix, 75 lines */
+    /* strip mode with col truncated by the uint8_t field: 275 -> 19, 58 rows of 19 */
+    case_sender_kind("k1100_pf1_S64", "sender_large", 75, 1, 1100, 64, 1, 1);
     case_sender_random("random_k", 8, 64, 328);
     /* encode: explicit rows (config 5 shape, and 1200-B payloads in 600-B windows) */
     case_rows("k32_rows4_S256", 9, 16, 32, 256, 0, 4, 256);

@@ -226,7 +226,7 @@ static int plan_lines(rfec_plan* p, int k, int row, int col, int rc, unsigned la
     p->row = (uint8_t)row;
     p->col = (uint8_t)col;
     p->rc = (uint8_t)rc;
-    if (k < 1 || k > RFEC_MAX_K)
+    if (k < 1 || k > RFEC_MAX_K_ENCODE)
         return -1;
     if (col <= 1) /* :158 */
         return 0;

@@ -156,9 +156,12 @@ typedef struct {
     int first[2 * 256], stride[2 * 256], count[2 * 256], index[2 * 256];
 } line_list;
 
+/* row and col are uint8_t in flex_fec_sender_t (the reference truncates the
+ * planner's values the same way), so at most 255 + 255 lines fit line_list */
 static void sender_lines(const flex_fec_sender_t* f, int rc, line_list* L)
 {
     const int n = f->segs_count, row = f->row, col = f->col;
+    _Static_assert(sizeof(f->row) == 1 && sizeof(f->col) == 1, "line_list holds 2 x 256 lines");
     L->n_lines = 0;
     for (int r = 0; r < row; ++r) {
         const int left = n - r * col;
@@ -222,7 +225,7 @@ void flex_fec_sender_update(flex_fec_sender_t* f, uint8_t protect_fraction, base
                 break;
         if (n_out == L.n_lines) {
             const int n = f->segs_count;
-            if (n <= RFEC_MAX_K && L.n_lines <= RFEC_MAX_LINES) {
+            if (n <= RFEC_MAX_K_ENCODE && L.n_lines <= RFEC_MAX_LINES) {
                 /* the whole group in one launch */
                 rfec_plan p;
                 memset(&p, 0, sizeof(p));
@@ -244,13 +247,9 @@ void flex_fec_sender_update(flex_fec_sender_t* f, uint8_t protect_fraction, base
                         rets[l] = -1;
             } else {
                 /* a group above the staging area: line by line */
-                sim_segment_t* mem[RFEC_MAX_K];
+                sim_segment_t* mem[RFEC_MAX_K_ENCODE]; /* a line has at most 255 members (uint8 row / col) */
                 for (int l = 0; l < L.n_lines; ++l) {
                     rets[l] = -1;
-                    if (L.count[l] > RFEC_MAX_K) {
-                        rfec_set_error(RFEC_EINVAL, "flex line above RFEC_MAX_K members");
-                        continue;
-                    }
                     for (int q = 0; q < L.count[l]; ++q)
                         mem[q] = f->segs[L.first[l] + q * L.stride[l]];
                     rets[l] = flex_fec_generate(mem, L.count[l], outs[l]);

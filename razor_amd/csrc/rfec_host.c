@@ -119,8 +119,8 @@ static int build_plan(uint16_t k, uint8_t row, uint8_t col, int rc, unsigned lay
     if (!p)
         return set_err(RFEC_EINVAL, "plan is NULL", 0);
     memset(p, 0, sizeof(*p));
-    if (k < 1 || k > RFEC_MAX_K)
-        return set_err(RFEC_EINVAL, "k out of range [1, RFEC_MAX_K]", 0);
+    if (k < 1 || k > RFEC_MAX_K_ENCODE)
+        return set_err(RFEC_EINVAL, "k out of range [1, RFEC_MAX_K_ENCODE]", 0);
     p->k = k;
     p->row = row;
     p->col = col;
@@ -163,11 +163,12 @@ int rfec_plan_matrix(uint16_t k, uint8_t row, uint8_t col, unsigned layers, rfec
 /* ------------------------------------------------------------------------ */
 /* 2. batched device API                                                     */
 /* ------------------------------------------------------------------------ */
-static int check_plan(const rfec_plan* p)
+/* max_k: RFEC_MAX_K_ENCODE for encode plans, RFEC_MAX_K for recovery (128-bit masks) */
+static int check_plan(const rfec_plan* p, uint32_t max_k)
 {
     if (!p)
         return set_err(RFEC_EINVAL, "plan is NULL", 0);
-    if (p->k < 1 || p->k > RFEC_MAX_K || p->n_lines > RFEC_MAX_LINES)
+    if (p->k < 1 || p->k > max_k || p->n_lines > RFEC_MAX_LINES)
         return set_err(RFEC_EINVAL, "plan k / n_lines out of range", 0);
     for (int l = 0; l < p->n_lines; ++l) {
         const rfec_line* ln = &p->line[l];
@@ -195,7 +196,7 @@ int rfec_encode_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, u
                       const uint8_t* shards, const rfec_hdr* hdr, uint8_t* parity, rfec_hdr* meta,
                       uint16_t* fec_size, int8_t* status, void* stream)
 {
-    int rc = check_plan(plan);
+    int rc = check_plan(plan, RFEC_MAX_K_ENCODE);
     if (rc)
         return rc;
     if ((rc = check_geometry(groups, stride, capacity, plan->k)))
@@ -234,7 +235,7 @@ int rfec_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, 
                        const rfec_hdr* meta, const uint16_t* fec_size, const uint64_t* parity_present,
                        uint64_t* recovered, void* workspace, void* stream)
 {
-    int rc = check_plan(plan);
+    int rc = check_plan(plan, RFEC_MAX_K);
     if (rc)
         return rc;
     if ((rc = check_geometry(groups, stride, capacity, plan->k)))
@@ -267,7 +268,7 @@ int rfec_recover_batch_out(const rfec_plan* plan, uint32_t groups, uint32_t stri
                            uint8_t* out_shards, rfec_hdr* out_hdr, uint8_t* out_index, void* workspace,
                            void* stream)
 {
-    int rc = check_plan(plan);
+    int rc = check_plan(plan, RFEC_MAX_K);
     if (rc)
         return rc;
     if ((rc = check_geometry(groups, stride, capacity, plan->k)))
@@ -392,7 +393,7 @@ int rfec_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const ui
 /* 3. drop-in single-call path                                               */
 /* ------------------------------------------------------------------------ */
 #define DI_STRIDE ((SIM_VIDEO_SIZE + 15) & ~15)
-#define DI_MAXK RFEC_MAX_K
+#define DI_MAXK RFEC_MAX_K_ENCODE /* staging slots: a whole encode group, or the recover jobs' slots */
 
 /* one pinned, device-mapped staging area per calling thread */
 typedef struct {
@@ -546,7 +547,7 @@ int rfec_di_generate_group(sim_segment_t* const* segs, int k, const rfec_plan* p
         return set_err(RFEC_EINVAL, "group above RFEC_MAX_K segments / RFEC_MAX_LINES lines", 0);
     for (int l = 0; l < plan->n_lines; ++l)
         rets[l] = -1;
-    if (check_plan(plan) != RFEC_OK)
+    if (check_plan(plan, RFEC_MAX_K_ENCODE) != RFEC_OK)
         return RFEC_EINVAL;
     if (plan->n_lines == 0)
         return RFEC_OK;
@@ -601,7 +602,7 @@ int flex_fec_generate(sim_segment_t* segs[], int segs_count, sim_fec_t* fec)
     if (segs_count <= 1) /* :9-10 */
         return -1;
     if (segs_count > DI_MAXK) {
-        set_err(RFEC_EINVAL, "segs_count above RFEC_MAX_K", 0);
+        set_err(RFEC_EINVAL, "segs_count above RFEC_MAX_K_ENCODE", 0);
         return -1;
     }
     rfec_plan p;
@@ -636,9 +637,9 @@ int rfec_di_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets)
         int j1 = j0, K = 0;
         while (j1 < n && j1 - j0 < RFEC_DI_GROUPS) {
             const rfec_di_recover_job* J = &jobs[j1];
-            if (J->count <= 0 || J->count + 1 > DI_MAXK || J->fec->fec_data_size > SIM_VIDEO_SIZE) {
+            if (J->count <= 0 || J->count + 1 > RFEC_MAX_K || J->fec->fec_data_size > SIM_VIDEO_SIZE) {
                 if (j1 == j0) { /* refused alone: :60-61, or beyond this library's limits */
-                    if (J->count + 1 > DI_MAXK)
+                    if (J->count + 1 > RFEC_MAX_K)
                         set_err(RFEC_EINVAL, "segs_count above RFEC_MAX_K-1", 0);
                     else if (J->count > 0)
                         set_err(RFEC_EINVAL, "fec_data_size above SIM_VIDEO_SIZE", 0);
@@ -649,7 +650,7 @@ int rfec_di_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets)
                 break;
             }
             const int k1 = J->count + 1 > K ? J->count + 1 : K;
-            if (k1 * (j1 - j0 + 1) > DI_MAXK)
+            if (k1 * (j1 - j0 + 1) > RFEC_MAX_K)
                 break;
             K = k1;
             ++j1;
@@ -932,7 +933,7 @@ static void hb_scatter(void* arg, size_t lo, size_t hi)
 int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,
                             sim_fec_t* const* fecs, uint16_t fec_id0, rfec_host_timing* timing)
 {
-    int rc = check_plan(plan);
+    int rc = check_plan(plan, RFEC_MAX_K_ENCODE);
     if (rc)
         return rc;
     if (groups == 0 || plan->n_lines == 0)
@@ -3064,5 +3065,6 @@ int rfec_rx_session_get_info(const rfec_rx_session* S, rfec_rx_session_info* inf
     info->cached_segments = S->X.cache.n;
     info->records_held = S->nstore;
     info->rows_held = S->arows;
+    info->pending = S->pend >= 0 ? S->pend_n : 0;
     return RFEC_OK;
 }

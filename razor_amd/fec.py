@@ -85,7 +85,7 @@ class rfec_send_report(C.Structure):
 
 class rfec_rx_session_info(C.Structure):
     _fields_ = [("max_ts", C.c_uint32), ("open_flexes", C.c_uint32), ("cached_segments", C.c_uint32),
-                ("records_held", C.c_uint32), ("rows_held", C.c_uint32), ("reserved", C.c_uint32)]
+                ("records_held", C.c_uint32), ("rows_held", C.c_uint32), ("pending", C.c_uint32)]
 
 
 class rfec_udp_addr(C.Structure):
@@ -576,14 +576,13 @@ class RxSession:
             outp, keep = self.n.pinned_array((max_out, self.stride), np.uint8)
         else:
             outp = np.zeros((max_out, self.stride), np.uint8)
-        prev = getattr(self, "_pend_n", 0)
+        prev = self.info()["pending"]  # the batch this call ingests
         recs = np.zeros(prev, WIRE_REC_DTYPE) if want_recs else None
         nout, rep = C.c_uint32(), rfec_rx_report()
         self.n._check(self.n.lib.rfec_rx_session_push_datagrams_async(
             self.h, n, dstride, dgram, dlen, None if recs is None or prev == 0 else recs.ctypes.data,
             out.ctypes.data, outp.ctypes.data, max_out, C.byref(nout), C.byref(rep)),
             "rfec_rx_session_push_datagrams_async")
-        self._pend_n = n
         rows = outp[:nout.value].copy() if keep is not None else outp[:nout.value]
         return out[:nout.value], rows, rep, recs
 

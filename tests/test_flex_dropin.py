@@ -130,7 +130,7 @@ def sender_group(lib, snd, segs, pf):
     return fecs
 
 
-@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "sender"])
+@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] in ("sender", "sender_large")])
 def test_flex_sender_fixture(flex, oracle1000, name):
     c = CASES[name]
     lib = flex

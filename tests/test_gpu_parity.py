@@ -27,7 +27,8 @@ def gpu():
 
 
 @pytest.mark.parametrize("tuning", list(TUNINGS))
-@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "sender"])
+@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"]
+                                  if c["kind"] == "sender" or (c["kind"] == "sender_large" and c["k"] <= 255)])
 def test_sender_fixture_gpu(gpu, oracle1000, name, tuning):
     pc.check_sender_case(gpu(tuning=TUNINGS[tuning]), oracle1000, CASES[name])
 

@@ -56,7 +56,8 @@ def test_num_fec_kat(oracle1000):
         assert (c, r) == (col, row), l
 
 
-@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"] if c["kind"] == "sender"])
+@pytest.mark.parametrize("name", [c["name"] for c in MANIFEST["cases"]
+                                  if c["kind"] == "sender" or (c["kind"] == "sender_large" and c["k"] <= 255)])
 def test_sender_fixture_oracle(oracle1000, name):
     pc.check_sender_case(OracleEngine(oracle1000), oracle1000, CASES[name])
 

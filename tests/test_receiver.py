@@ -356,6 +356,7 @@ def test_rx_session_datagrams_async(lib, oracle1000, pinned):
         out, outp, rep, r = sess.push_datagrams_async(b - a, DSTRIDE, dgram[a:].ctypes.data, dlen[a:].ctypes.data,
                                                       want_recs=True, max_out=4096, pinned_out=pinned)
         got.append((out, outp, r))
+        assert sess.info()["pending"] == b - a and (j == 0 or len(r) == cuts[j - 1][1] - cuts[j - 1][0])
         if j == 0:
             with pytest.raises(Exception):
                 sess.push_datagrams(1, DSTRIDE, dgram.ctypes.data, dlen.ctypes.data)
@@ -364,6 +365,7 @@ def test_rx_session_datagrams_async(lib, oracle1000, pinned):
     out, outp, rep, r = sess.push_datagrams_async(0, DSTRIDE, 0, 0, want_recs=True, max_out=4096,
                                                   pinned_out=pinned)
     got.append((out, outp, r))
+    assert sess.info()["pending"] == 0
     if len(cuts) - 1 in evict_after:
         sess.evict()
     eo, eop, erecs = collect(ref)
