@@ -613,8 +613,25 @@ int rfec_rx_session_get_info(const rfec_rx_session* s, rfec_rx_session_info* inf
  * in place: the LDS peel + schedule replay), the cross-check of the
  * specialised ones.  Other bits are ignored. */
 #define RFEC_TUNE_GENERIC 1u
+/* RFEC_TUNE_NO_SERVICE: the drop-in symbols (flex_fec_generate / _recover, the
+ * group-level sender and receiver) launch their kernels per call instead of
+ * posting to the resident service (process-wide; also RFEC_SERVICE=0 in the
+ * environment). */
+#define RFEC_TUNE_NO_SERVICE 2u
 void rfec_set_tuning(unsigned flags);
 unsigned rfec_get_tuning(void);
+
+/* The drop-in's resident service: one workgroup that stays on the device and
+ * takes the drop-in symbols' jobs from a doorbell in pinned, host-coherent
+ * memory (no launch, no stream synchronisation per call).  It starts on the
+ * first drop-in call and leaves the device by itself after RFEC_SERVICE_IDLE_US
+ * (default 20000) microseconds without a job, after one second in total (the
+ * next call starts it again) and at exit.  rfec_service_stop() makes it leave
+ * now and waits for it; it returns RFEC_OK (also when it was not running) or
+ * RFEC_EDEVICE.  rfec_service_stats reports the calls served and the
+ * launches made so far (either pointer may be NULL). */
+int rfec_service_stop(void);
+void rfec_service_stats(uint64_t* jobs, uint64_t* launches);
 
 /* HBM ceiling probes (measurement only, not on the FEC path): streaming
  * read / copy / write of `bytes` (multiple of 16) in the FEC kernels' access

@@ -26,7 +26,8 @@ INCLUDE = ROOT / "include"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("RFEC_OFFLOAD_ARCH", "gfx950")
 
-HIP_SRC = [CSRC / "rfec_kernels.hip", CSRC / "rfec_probe.hip", CSRC / "rfec_wire.hip", CSRC / "rfec_fill.hip"]
+HIP_SRC = [CSRC / "rfec_kernels.hip", CSRC / "rfec_probe.hip", CSRC / "rfec_wire.hip", CSRC / "rfec_fill.hip",
+           CSRC / "rfec_service.hip"]
 C_SRC = [CSRC / "rfec_host.c", CSRC / "rfec_flex.c"]  # built once per SIM_VIDEO_SIZE
 NET_SRC = CSRC / "rfec_net.c"  # host-only (sockets), independent of SIM_VIDEO_SIZE
 HEADERS = [INCLUDE / "razor_fec.h", INCLUDE / "razor_flex.h", CSRC / "rfec_internal.h", CSRC / "rfec_launch.h"]

@@ -536,6 +536,215 @@ static int di_sync(di_ctx* c, int launch_err, const char* what)
     return e == hipSuccess ? RFEC_OK : set_err(RFEC_EDEVICE, what, e);
 }
 
+static double now_us(void);
+
+/* ---- resident service (rfec_service.hip) --------------------------------
+ * The drop-in symbols are called once per group under razor's session mutex
+ * (sim_session.c:241, sim_sender.c:286-304), so their cost is latency: a
+ * launch plus hipStreamSynchronize is ~15-20 us before any work.  Instead ONE
+ * workgroup stays on the device and polls a doorbell in pinned, host-coherent
+ * memory; a call stages its segments next to the doorbell, bumps `req` and
+ * spins on `done` (a few PCIe round trips).  The workgroup leaves after
+ * RFEC_SERVICE_IDLE_US without a job, after one second in total, on `stop`
+ * (rfec_service_stop, atexit); a call that finds `alive` == 0 launches it
+ * again.  One service per process, calls serialised by its mutex. */
+typedef struct {
+    pthread_mutex_t mu;
+    int state; /* 0 not set up, 1 ready, -1 unavailable (per-call launches) */
+    hipStream_t stream;
+    rfec_svc_ctl* ctl;   /* host view; the staging slots follow it */
+    uint8_t* dev;        /* device view of the same allocation */
+    size_t o_shards, o_parity;
+    uint32_t seq;
+    uint64_t idle_ticks, life_ticks;
+    uint64_t jobs, launches;
+} svc_state;
+static svc_state g_svc = {PTHREAD_MUTEX_INITIALIZER, 0, NULL, NULL, NULL, 0, 0, 0, 0, 0, 0, 0};
+
+static void svc_pause(void)
+{
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#endif
+}
+
+/* mutex held; leaves the workgroup off the device */
+static int svc_stop_locked(void)
+{
+    if (g_svc.state != 1)
+        return RFEC_OK;
+    __atomic_store_n(&g_svc.ctl->stop, 1u, __ATOMIC_RELEASE);
+    const hipError_t e = hipStreamSynchronize(g_svc.stream);
+    __atomic_store_n(&g_svc.ctl->stop, 0u, __ATOMIC_RELEASE);
+    g_svc.ctl->alive = 0;
+    return e == hipSuccess ? RFEC_OK : set_err(RFEC_EDEVICE, "service stop", e);
+}
+
+int rfec_service_stop(void)
+{
+    pthread_mutex_lock(&g_svc.mu);
+    const int rc = svc_stop_locked();
+    pthread_mutex_unlock(&g_svc.mu);
+    return rc;
+}
+
+void rfec_service_stats(uint64_t* jobs, uint64_t* launches)
+{
+    pthread_mutex_lock(&g_svc.mu);
+    if (jobs)
+        *jobs = g_svc.jobs;
+    if (launches)
+        *launches = g_svc.launches;
+    pthread_mutex_unlock(&g_svc.mu);
+}
+
+static void svc_atexit(void) { (void)rfec_service_stop(); }
+
+static size_t svc_align(size_t x) { return (x + 255) & ~(size_t)255; }
+
+/* Locks the service and returns 1 when calls should go through it (set up on
+ * first use), else 0 with the mutex released. */
+static int svc_acquire(void)
+{
+    if (g_tuning & RFEC_TUNE_NO_SERVICE)
+        return 0;
+    pthread_mutex_lock(&g_svc.mu);
+    if (g_svc.state == 0) {
+        g_svc.state = -1;
+        const char* env = getenv("RFEC_SERVICE");
+        int dev = 0, khz = 0, n = 0;
+        hipError_t e;
+        if (env && env[0] == '0') {
+            pthread_mutex_unlock(&g_svc.mu);
+            return 0;
+        }
+        const size_t o_shards = svc_align(sizeof(rfec_svc_ctl));
+        const size_t o_parity = o_shards + svc_align((size_t)DI_MAXK * DI_STRIDE);
+        const size_t bytes = o_parity + svc_align((size_t)RFEC_MAX_LINES * DI_STRIDE);
+        void* h = NULL;
+        if ((e = hipGetDeviceCount(&n)) != hipSuccess || n == 0 || (e = hipGetDevice(&dev)) != hipSuccess ||
+            (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev)) != hipSuccess || khz <= 0 ||
+            (e = hipStreamCreateWithFlags(&g_svc.stream, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void**)&g_svc.dev, h, 0)) != hipSuccess) {
+            set_err(RFEC_EDEVICE, "service setup", e);
+            if (h)
+                (void)hipHostFree(h);
+            pthread_mutex_unlock(&g_svc.mu);
+            return 0;
+        }
+        memset(h, 0, bytes);
+        g_svc.ctl = (rfec_svc_ctl*)h;
+        g_svc.o_shards = o_shards;
+        g_svc.o_parity = o_parity;
+        const char* idle = getenv("RFEC_SERVICE_IDLE_US");
+        const double idle_us = idle && atof(idle) > 0 ? atof(idle) : 20000.0;
+        g_svc.idle_ticks = (uint64_t)(idle_us * khz / 1000.0);
+        g_svc.life_ticks = (uint64_t)khz * 1000u; /* one second */
+        g_svc.state = 1;
+        atexit(svc_atexit);
+    }
+    if (g_svc.state != 1) {
+        pthread_mutex_unlock(&g_svc.mu);
+        return 0;
+    }
+    return 1;
+}
+
+static uint8_t* svc_shard(uint32_t i) { return (uint8_t*)g_svc.ctl + g_svc.o_shards + (size_t)i * DI_STRIDE; }
+static uint8_t* svc_parity(uint32_t i) { return (uint8_t*)g_svc.ctl + g_svc.o_parity + (size_t)i * DI_STRIDE; }
+
+/* a payload into a service slot: the bytes, zero to the end of their last 16-byte chunk; returns the chunks */
+static uint8_t svc_stage(uint8_t* slot, const uint8_t* data, uint32_t size)
+{
+    const uint32_t n = size < SIM_VIDEO_SIZE ? size : SIM_VIDEO_SIZE, nck = (n + 15) / 16;
+    memcpy(slot, data, n);
+    memset(slot + n, 0, (size_t)nck * 16 - n);
+    return (uint8_t)nck;
+}
+
+/* mutex held, the job written: post it, (re)launch the workgroup when it is
+ * gone, wait for `done` */
+static int svc_run(void)
+{
+    rfec_svc_ctl* q = g_svc.ctl;
+    const uint32_t seq = ++g_svc.seq;
+    __atomic_store_n(&q->req, seq, __ATOMIC_RELEASE);
+    const double t0 = now_us();
+    for (uint64_t spin = 0;; ++spin) {
+        if (__atomic_load_n(&q->done, __ATOMIC_ACQUIRE) == seq)
+            break;
+        if (__atomic_load_n(&q->alive, __ATOMIC_ACQUIRE) == 0) {
+            /* gone (or leaving): a new launch runs after it and takes the job */
+            q->alive = 1;
+            __atomic_thread_fence(__ATOMIC_SEQ_CST);
+            const int ke = rfec_launch_service(q, g_svc.dev + g_svc.o_shards, g_svc.dev + g_svc.o_parity, DI_STRIDE,
+                                               g_svc.idle_ticks, g_svc.life_ticks, g_svc.stream);
+            if (ke) {
+                q->alive = 0;
+                g_svc.state = -1;
+                return set_err(RFEC_EDEVICE, "service launch", ke);
+            }
+            ++g_svc.launches;
+        }
+        if ((spin & 4095) == 4095 && now_us() - t0 > 5e6) {
+            /* no answer in 5 s: stop using the service (the workgroup leaves
+             * within its one-second lifetime) */
+            g_svc.state = -1;
+            return set_err(RFEC_EDEVICE, "service timeout", 0);
+        }
+        svc_pause();
+    }
+    ++g_svc.jobs;
+    return RFEC_OK;
+}
+
+/* the group encode of rfec_di_generate_group through the service (mutex held) */
+static int svc_generate_group(sim_segment_t* const* segs, int k, const rfec_plan* plan)
+{
+    rfec_svc_job* J = &g_svc.ctl->job;
+    J->op = RFEC_SVC_ENCODE;
+    J->n_slots = (uint32_t)k;
+    J->groups = 1;
+    J->capacity = SIM_VIDEO_SIZE;
+    J->plan = *plan;
+    for (int i = 0; i < k; ++i) {
+        J->slot_src[i] = (uint16_t)i;
+        J->slot_nck[i] = svc_stage(svc_shard((uint32_t)i), segs[i]->data, segs[i]->data_size);
+        seg_to_hdr(segs[i], (rfec_hdr*)&J->hdr[5 * i]);
+    }
+    return svc_run();
+}
+
+/* a group encode's results (line l: meta m[l], fec_data_size fds[l], status
+ * st[l], payload at parity + l * DI_STRIDE) into the callers' sim_fec_t */
+static void di_take_group(sim_segment_t* const* segs, const rfec_plan* plan, sim_fec_t* const* outs, int* rets,
+                          const rfec_hdr* m, const uint16_t* fds, const int8_t* st, const uint8_t* parity)
+{
+    for (int l = 0; l < plan->n_lines; ++l) {
+        const rfec_line* ln = &plan->line[l];
+        sim_fec_t* f = outs[l];
+        if (ln->count <= 1) /* :9-10 */
+            continue;
+        f->fec_data_size = fds[l];
+        if (st[l] != 0) {
+            /* over capacity (:27-28): the reference has written the first
+             * member's header and the size by then, nothing else */
+            seg_to_hdr(segs[ln->first], (rfec_hdr*)&f->fec_meta);
+            continue;
+        }
+        memcpy(&f->fec_meta, &m[l], sizeof(rfec_hdr));
+        memcpy(f->fec_data, parity + (size_t)l * DI_STRIDE, fds[l]);
+        /* in-place zero padding of the line's members 1.. to fec_data_size (:47) */
+        for (int q = 1; q < ln->count; ++q) {
+            sim_segment_t* s = segs[ln->first + q * ln->stride];
+            if (s->data_size < fds[l])
+                memset(s->data + s->data_size, 0, (size_t)(fds[l] - s->data_size));
+        }
+        rets[l] = 0;
+    }
+}
+
 /* Every line of `plan` over segs[0..k) in one launch (flex_fec_xor.c:4-53 per
  * line): line l's meta, fec_data_size and fec_data go to outs[l], the return
  * value flex_fec_generate would give to rets[l].  The group-level sender
@@ -551,6 +760,17 @@ int rfec_di_generate_group(sim_segment_t* const* segs, int k, const rfec_plan* p
         return RFEC_EINVAL;
     if (plan->n_lines == 0)
         return RFEC_OK;
+    if (svc_acquire()) {
+        const int rc = svc_generate_group(segs, k, plan);
+        if (rc == RFEC_OK) {
+            const rfec_svc_ctl* q = g_svc.ctl;
+            di_take_group(segs, plan, outs, rets, (const rfec_hdr*)q->out.meta, q->out.fsize, q->out.status,
+                          svc_parity(0));
+        }
+        pthread_mutex_unlock(&g_svc.mu);
+        if (rc == RFEC_OK)
+            return RFEC_OK; /* else: the per-call launch below */
+    }
     di_ctx* c = di_get();
     if (!c)
         return RFEC_EDEVICE;
@@ -568,31 +788,8 @@ int rfec_di_generate_group(sim_segment_t* const* segs, int k, const rfec_plan* p
         di_loud(t_err);
         return RFEC_EDEVICE;
     }
-    const rfec_hdr* m = (const rfec_hdr*)(c->host + L.meta);
-    const uint16_t* fds = (const uint16_t*)(c->host + L.fsize);
-    const int8_t* st = (const int8_t*)(c->host + L.status);
-    for (int l = 0; l < plan->n_lines; ++l) {
-        const rfec_line* ln = &plan->line[l];
-        sim_fec_t* f = outs[l];
-        if (ln->count <= 1) /* :9-10 */
-            continue;
-        f->fec_data_size = fds[l];
-        if (st[l] != 0) {
-            /* over capacity (:27-28): the reference has written the first
-             * member's header and the size by then, nothing else */
-            seg_to_hdr(segs[ln->first], (rfec_hdr*)&f->fec_meta);
-            continue;
-        }
-        memcpy(&f->fec_meta, &m[l], sizeof(rfec_hdr));
-        memcpy(f->fec_data, c->host + L.parity + (size_t)l * DI_STRIDE, fds[l]);
-        /* in-place zero padding of the line's members 1.. to fec_data_size (:47) */
-        for (int q = 1; q < ln->count; ++q) {
-            sim_segment_t* s = segs[ln->first + q * ln->stride];
-            if (s->data_size < fds[l])
-                memset(s->data + s->data_size, 0, (size_t)(fds[l] - s->data_size));
-        }
-        rets[l] = 0;
-    }
+    di_take_group(segs, plan, outs, rets, (const rfec_hdr*)(c->host + L.meta), (const uint16_t*)(c->host + L.fsize),
+                  (const int8_t*)(c->host + L.status), c->host + L.parity);
     return RFEC_OK;
 }
 
@@ -625,10 +822,116 @@ int flex_fec_generate(sim_segment_t* segs[], int segs_count, sim_fec_t* fec)
  * for the XOR of payloads and header records, and for the size checks), the
  * erased member last; K = 1 + the largest count of the launch.  rets[j] is
  * what flex_fec_recover returns for the job. */
+/* a recover job's in-place zero padding of its present segments (:91), up to
+ * the first one the reference rejects (:88-89) */
+static void di_pad_members(const rfec_di_recover_job* J)
+{
+    const uint32_t Lfec = J->fec->fec_data_size;
+    for (int i = 0; i < J->count; ++i) {
+        if (J->segs[i]->data_size > Lfec)
+            break;
+        memset(J->segs[i]->data + J->segs[i]->data_size, 0, (size_t)(Lfec - J->segs[i]->data_size));
+    }
+}
+
+/* a recovered segment (header r, payload data) into the job's out_seg (:64-73, :101) */
+static void di_take_recovered(const rfec_di_recover_job* J, const rfec_hdr* r, const uint8_t* data)
+{
+    sim_segment_t* o = J->out;
+    o->packet_id = r->seq;
+    o->fid = r->fid;
+    o->timestamp = r->ts;
+    o->index = r->index;
+    o->total = r->total;
+    o->ftype = r->ftype;
+    o->payload_type = r->payload_type;
+    o->data_size = r->size;
+    memcpy(o->data, data, J->fec->fec_data_size);
+    o->fec_id = J->fec->fec_id;
+}
+
+/* a recover job the drop-in refuses alone: flex_fec_recover's own refusal
+ * (:60-61) or this library's limits */
+static int di_refused(const rfec_di_recover_job* J)
+{
+    if (J->count <= 0)
+        return 1;
+    if (J->count + 1 > RFEC_MAX_K) {
+        set_err(RFEC_EINVAL, "segs_count above RFEC_MAX_K-1", 0);
+        return 1;
+    }
+    if (J->fec->fec_data_size > SIM_VIDEO_SIZE) {
+        set_err(RFEC_EINVAL, "fec_data_size above SIM_VIDEO_SIZE", 0);
+        return 1;
+    }
+    return 0;
+}
+
+/* rfec_di_recover_lines through the service (mutex held): up to
+ * RFEC_DI_GROUPS jobs per post, each its members then its parity in LDS */
+static int svc_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets)
+{
+    rfec_svc_ctl* q = g_svc.ctl;
+    rfec_svc_job* S = &q->job;
+    int j = 0;
+    while (j < n) {
+        int idx[RFEC_DI_GROUPS];
+        uint32_t G = 0, ns = 0;
+        for (; j < n && G < RFEC_DI_GROUPS; ++j) {
+            const rfec_di_recover_job* J = &jobs[j];
+            if (di_refused(J))
+                continue;
+            const uint32_t c = (uint32_t)J->count;
+            if (ns + c + 1 > RFEC_SVC_SLOTS || ns + c + 1 > DI_MAXK)
+                break;
+            S->slot0[G] = S->hdr0[G] = (uint16_t)ns;
+            S->count[G] = (uint16_t)c;
+            S->fsize[G] = J->fec->fec_data_size;
+            memcpy(&S->hdr[5 * ns], &J->fec->fec_meta, sizeof(rfec_hdr));
+            for (uint32_t i = 0; i < c; ++i) {
+                S->slot_src[ns + i] = (uint16_t)(ns + i);
+                S->slot_nck[ns + i] = svc_stage(svc_shard(ns + i), J->segs[i]->data, J->segs[i]->data_size);
+                seg_to_hdr(J->segs[i], (rfec_hdr*)&S->hdr[5 * (ns + 1 + i)]);
+            }
+            S->slot_src[ns + c] = (uint16_t)(G | RFEC_SVC_PARITY_SLOT);
+            S->slot_nck[ns + c] = svc_stage(svc_parity(G), J->fec->fec_data, J->fec->fec_data_size);
+            S->out_slot[G] = (uint16_t)(ns + c); /* the shards slot next to the members: free */
+            idx[G++] = j;
+            ns += c + 1;
+        }
+        if (G == 0)
+            continue;
+        S->op = RFEC_SVC_RECOVER;
+        S->n_slots = ns;
+        S->groups = G;
+        S->capacity = SIM_VIDEO_SIZE;
+        const int rc = svc_run();
+        if (rc != RFEC_OK)
+            return rc;
+        for (uint32_t g = 0; g < G; ++g) {
+            const rfec_di_recover_job* J = &jobs[idx[g]];
+            di_pad_members(J);
+            if (q->out.status[g] != 0)
+                continue;
+            di_take_recovered(J, (const rfec_hdr*)q->out.meta[g], svc_shard(S->out_slot[g]));
+            rets[idx[g]] = 0;
+        }
+    }
+    return RFEC_OK;
+}
+
 int rfec_di_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets)
 {
     for (int j = 0; j < n; ++j)
         rets[j] = -1;
+    if (n > 0 && svc_acquire()) {
+        const int rc = svc_recover_lines(jobs, n, rets);
+        pthread_mutex_unlock(&g_svc.mu);
+        if (rc == RFEC_OK)
+            return RFEC_OK;
+        for (int j = 0; j < n; ++j) /* the per-call launches below redo them all */
+            rets[j] = -1;
+    }
     di_ctx* c = NULL;
     const di_layout L = di_offsets();
     int j0 = 0;
@@ -639,10 +942,7 @@ int rfec_di_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets)
             const rfec_di_recover_job* J = &jobs[j1];
             if (J->count <= 0 || J->count + 1 > RFEC_MAX_K || J->fec->fec_data_size > SIM_VIDEO_SIZE) {
                 if (j1 == j0) { /* refused alone: :60-61, or beyond this library's limits */
-                    if (J->count + 1 > RFEC_MAX_K)
-                        set_err(RFEC_EINVAL, "segs_count above RFEC_MAX_K-1", 0);
-                    else if (J->count > 0)
-                        set_err(RFEC_EINVAL, "fec_data_size above SIM_VIDEO_SIZE", 0);
+                    (void)di_refused(J);
                     ++j0;
                     ++j1;
                     continue;
@@ -706,28 +1006,10 @@ int rfec_di_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets)
         const uint64_t* rec = (const uint64_t*)(c->host + L.recovered);
         for (int g = 0; g < G; ++g) {
             const rfec_di_recover_job* J = &jobs[j0 + g];
-            const uint32_t Lfec = J->fec->fec_data_size;
-            /* in-place zero padding of the present segments (:91), up to the
-             * first one the reference rejects (:88-89) */
-            for (int i = 0; i < J->count; ++i) {
-                if (J->segs[i]->data_size > Lfec)
-                    break;
-                memset(J->segs[i]->data + J->segs[i]->data_size, 0, (size_t)(Lfec - J->segs[i]->data_size));
-            }
+            di_pad_members(J);
             if (!((rec[2 * g + ((K - 1) >> 6)] >> ((K - 1) & 63)) & 1ull))
                 continue;
-            const rfec_hdr* r = &hh[g * K + K - 1];
-            sim_segment_t* o = J->out;
-            o->packet_id = r->seq;
-            o->fid = r->fid;
-            o->timestamp = r->ts;
-            o->index = r->index;
-            o->total = r->total;
-            o->ftype = r->ftype;
-            o->payload_type = r->payload_type;
-            o->data_size = r->size;
-            memcpy(o->data, c->host + L.shards + ((size_t)g * K + K - 1) * DI_STRIDE, Lfec);
-            o->fec_id = J->fec->fec_id; /* :101 */
+            di_take_recovered(J, &hh[g * K + K - 1], c->host + L.shards + ((size_t)g * K + K - 1) * DI_STRIDE);
             rets[j0 + g] = 0;
         }
         j0 = j1;

@@ -86,6 +86,39 @@ __attribute__((visibility("hidden"))) int rfec_di_generate_group(sim_segment_t* 
                                                                  const rfec_plan* plan, sim_fec_t* const* outs,
                                                                  int* rets);
 __attribute__((visibility("hidden"))) int rfec_di_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets);
+/* The resident service (rfec_service.hip): one workgroup polling a doorbell in
+ * pinned, host-coherent memory for the drop-in's jobs.  Slot codes name a
+ * staging slot: shards slot i, or parity slot i | RFEC_SVC_PARITY_SLOT. */
+#define RFEC_SVC_ENCODE 1u
+#define RFEC_SVC_RECOVER 2u
+#define RFEC_SVC_PARITY_SLOT 0x8000u
+#define RFEC_SVC_SLOTS 264 /* an encode group (<= 255 members) or the recover jobs' members + parities */
+typedef struct {
+    uint32_t op, n_slots, groups, capacity;
+    rfec_kplan plan;                   /* encode: the group's lines over slots 0..k-1 */
+    uint16_t slot0[RFEC_DI_GROUPS];    /* recover job g: its members' first LDS slot, its parity right after */
+    uint16_t count[RFEC_DI_GROUPS];    /* present members */
+    uint16_t fsize[RFEC_DI_GROUPS];    /* fec_data_size */
+    uint16_t hdr0[RFEC_DI_GROUPS];     /* first header record: the parity's meta, then the members' */
+    uint16_t out_slot[RFEC_DI_GROUPS]; /* shards slot of the recovered payload */
+    uint16_t slot_src[RFEC_SVC_SLOTS]; /* LDS slot s <- staging slot code */
+    uint8_t slot_nck[RFEC_SVC_SLOTS];  /* 16-byte chunks of the slot that may be non-zero */
+    uint32_t hdr[RFEC_SVC_SLOTS * 5];  /* encode: member i at 5 i; recover: as hdr0 */
+} rfec_svc_job;
+typedef struct {
+    uint32_t req, stop, pad0[14];  /* host-written line: job sequence number, leave now */
+    uint32_t done, pad1[15];       /* device-written: the last job finished */
+    uint32_t alive, pad2[15];      /* 1 set by the host before a launch, 0 by the workgroup as it leaves */
+    struct {
+        uint32_t meta[RFEC_MAX_LINES][5]; /* encode: line l's meta; recover: job g's recovered header */
+        uint16_t fsize[RFEC_MAX_LINES];
+        int8_t status[RFEC_MAX_LINES];    /* flex_fec_generate / flex_fec_recover's 0 / -1 */
+    } out;
+    rfec_svc_job job;
+} rfec_svc_ctl;
+int rfec_launch_service(rfec_svc_ctl* ctl, const uint8_t* shards, uint8_t* parity, uint32_t stride,
+                        uint64_t idle_ticks, uint64_t life_ticks, void* stream);
+
 __attribute__((visibility("hidden"))) int rfec_set_error(int code, const char* what);
 /* sets rfec_last_error() from an errno value (0: `what` alone); returns code */
 int rfec_set_error_sys(int code, const char* what, int err);

@@ -223,7 +223,13 @@ __global__ __launch_bounds__(kBlock) void k_encode(const v4u* __restrict__ shard
         const v4u* s = src + (size_t)ln.first * C;
         const size_t step = (size_t)ln.stride * C;
         v4u acc = ld16(s);
-        for (uint32_t q = 1; q < ln.count; ++q)
+        uint32_t q = 1;
+        for (; q + 4 <= ln.count; q += 4) { // four loads in flight
+            const v4u a = ld16(s + q * step), b = ld16(s + (q + 1) * step);
+            const v4u c = ld16(s + (q + 2) * step), d = ld16(s + (q + 3) * step);
+            acc ^= (a ^ b) ^ (c ^ d);
+        }
+        for (; q < ln.count; ++q)
             acc ^= ld16(s + q * step);
         st16(dst + (size_t)l * C, acc);
     }
@@ -302,6 +308,52 @@ __global__ __launch_bounds__(kBlock) void k_encode_matrix(const v4u* __restrict_
         st16(dst + (size_t)(l++) * C, acc);
     }
 }
+
+#ifdef RFEC_MATRIX_OUT
+// Output-mapped form of the full matrix encode: one lane per PARITY chunk
+// (group, line, chunk column), as k_encode_out, so that every wave's store is
+// 1 KiB of consecutive parity bytes (whole 128-B lines when the slots are
+// packed) instead of seven 1 KiB runs that start and end inside lines shared
+// with the neighbouring waves.  Each member is loaded by its row's lanes and
+// again by its column's lanes one block or so later, on the same XCD, so HBM
+// should still see every member once.  Row l < NR: members l COL + q; column c = l - NR: c + q COL
+// (K >= 2 COL here, so no column has fewer than 2 members).  Loads take the
+// default policy: the column lanes' second reads are meant to hit L2.
+template <int K, int COL>
+__global__ __launch_bounds__(kBlock) void k_encode_matrix_out(const v4u* __restrict__ shards,
+                                                              v4u* __restrict__ parity, uint32_t total, uint32_t C,
+                                                              FastDiv divC, FastDiv divLC, uint32_t head, EncMeta E,
+                                                              rfec_kplan P)
+{
+    using Sh = MatrixShape<K, COL>;
+    constexpr int NR = Sh::n_rows(), R = Sh::R, M = COL > R ? COL : R;
+    static_assert(K >= 2 * COL && Sh::n_lines() == NR + COL, "every column has >= 2 members");
+    uint32_t b;
+    if (!enc_payload_block(E, head, P, &b))
+        return;
+    const uint32_t t = b * kBlock + threadIdx.x;
+    if (t >= total)
+        return;
+    const uint32_t g = fdiv(t, divLC);
+    const uint32_t rem = t - g * divLC.d;
+    const uint32_t l = fdiv(rem, divC);
+    const uint32_t j = rem - l * divC.d;
+    const bool row = l < (uint32_t)NR;
+    const uint32_t c = l - NR;
+    const uint32_t first = row ? l * COL : c, step = row ? 1u : (uint32_t)COL;
+    const uint32_t count = row ? min((uint32_t)COL, K - l * COL) : (K - c + COL - 1) / COL;
+    const v4u* s = shards + ((size_t)g * K + first) * C + j;
+    v4u v[M];
+#pragma unroll
+    for (int q = 0; q < M; ++q) // unconditional (an unused slot re-reads member 0), default policy
+        v[q] = s[(uint32_t)q < count ? (size_t)q * step * C : 0];
+    v4u acc = v[0];
+#pragma unroll
+    for (int q = 1; q < M; ++q)
+        acc ^= (uint32_t)q < count ? v[q] : v4u{0, 0, 0, 0};
+    st16(parity + ((size_t)g * (NR + COL) + l) * C + j, acc);
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // Encode payload, rows-of-COL, output-mapped (default for row layouts): one
@@ -593,32 +645,34 @@ __device__ __forceinline__ void replay(v4u* grp, const v4u* __restrict__ par, co
         // single level: BATCH steps at a time, all loads in flight together
         const uint32_t nf = n < 7 ? n : 7; // steps carried in the first 16 record bytes
         for (; s < nf; s += BATCH) {
+            // (unconditional loads, see k_decode_rows; an off step re-reads
+            // the first step's parity chunk)
             v4u acc[BATCH], mv[BATCH][MAXC];
-            uint32_t tg[BATCH];
-            bool on[BATCH];
+            uint32_t tg[BATCH], l0 = 0;
+            bool on[BATCH], use[BATCH][MAXC];
 #pragma unroll
             for (int b = 0; b < BATCH; ++b) {
                 on[b] = s + b < nf;
-                const uint32_t l = on[b] ? rec_byte(r0, 2 + 2 * (s + b)) : 0;
+                const uint32_t l = on[b] ? rec_byte(r0, 2 + 2 * (s + b)) : l0;
+                l0 = l;
                 tg[b] = rec_byte(r0, 3 + 2 * (s + b));
                 const uint32_t ln = lplan[l];
                 const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
-                acc[b] = v4u{0, 0, 0, 0};
-                if (on[b])
-                    acc[b] = ld16(par + (size_t)l * C);
+                const v4u* pl = par + (size_t)l * C;
+                acc[b] = ld16(pl);
+                const ptrdiff_t to_par = pl - grp;
 #pragma unroll
                 for (int q = 0; q < MAXC; ++q) {
                     const uint32_t i = first + q * stride;
-                    mv[b][q] = v4u{0, 0, 0, 0};
-                    if (on[b] && (uint32_t)q < count && i != tg[b])
-                        mv[b][q] = ld16(grp + (size_t)i * C);
+                    use[b][q] = on[b] && (uint32_t)q < count && i != tg[b];
+                    mv[b][q] = ld16(grp + (use[b][q] ? (ptrdiff_t)i * C : to_par));
                 }
             }
 #pragma unroll
             for (int b = 0; b < BATCH; ++b) {
 #pragma unroll
                 for (int q = 0; q < MAXC; ++q)
-                    acc[b] ^= mv[b][q];
+                    acc[b] ^= use[b][q] ? mv[b][q] : v4u{0, 0, 0, 0};
                 if (on[b])
                     st16(out ? out + (size_t)missing_rank(h0, h1, tg[b]) * C : grp + (size_t)tg[b] * C, acc[b]);
             }
@@ -1308,6 +1362,10 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
                                                             uint32_t n_hdr_blocks, uint32_t hdr_every, PeelArgs A,
                                                             rfec_kmask M, DenseOut D)
 {
+#ifdef RFEC_DEC_LDS_PAD
+    __shared__ uint32_t lds_pad[RFEC_DEC_LDS_PAD / 4];
+    asm volatile("" ::"v"(lds_pad));
+#endif
     uint32_t hb, pb;
     if (header_block(n_hdr_blocks, hdr_every, &hb, &pb)) {
         line_headers(A, M, hb);
@@ -1338,37 +1396,38 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
     }
     while (fire) {
         // two fired lines per round, every load of both in flight together
+        // (every load unconditional: a member slot the line does not use
+        // re-reads its parity chunk and is masked, see k_decode_rows)
         v4u acc[2], mv[2][MAXC];
         uint32_t tg[2];
-        bool on[2];
+        bool on[2], use[2][MAXC];
+        uint32_t l0 = 0;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            on[b] = fire != 0;
-            const uint32_t l = on[b] ? (uint32_t)__ffsll((long long)fire) - 1 : 0;
+            on[b] = fire != 0; // (the first always: the loop runs while lines fire)
+            const uint32_t l = on[b] ? (uint32_t)__ffsll((long long)fire) - 1 : l0; // off: the first's, re-read
+            l0 = l;
             fire &= fire - 1;
             const uint32_t ln = lplan[l];
             const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
-            acc[b] = v4u{0, 0, 0, 0};
-            if (on[b])
-                acc[b] = ld16(par + (size_t)l * C);
+            const v4u* pl = par + (size_t)l * C;
+            acc[b] = ld16(pl);
+            const ptrdiff_t to_par = pl - grp;
             tg[b] = first;
 #pragma unroll
             for (int q = 0; q < MAXC; ++q) {
                 const uint32_t i = first + q * stride;
-                mv[b][q] = v4u{0, 0, 0, 0};
-                if (!on[b] || (uint32_t)q >= count)
-                    continue;
-                if (has_bit(h0, h1, i))
-                    mv[b][q] = ld16(grp + (size_t)i * C);
-                else
-                    tg[b] = i;
+                const bool in = on[b] && (uint32_t)q < count, have = has_bit(h0, h1, i);
+                use[b][q] = in && have;
+                tg[b] = in && !have ? i : tg[b];
+                mv[b][q] = ld16(grp + (use[b][q] ? (ptrdiff_t)i * C : to_par));
             }
         }
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
 #pragma unroll
             for (int q = 0; q < MAXC; ++q)
-                acc[b] ^= mv[b][q];
+                acc[b] ^= use[b][q] ? mv[b][q] : v4u{0, 0, 0, 0};
             if (on[b]) {
                 if (!D.E) {
                     st16(grp + (size_t)tg[b] * C, acc[b]);
@@ -1466,18 +1525,20 @@ __global__ __launch_bounds__(kBlock) void k_decode_out(v4u* shards, const v4u* _
     }
     const uint32_t ln = lplan[l];
     const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
-    v4u acc = ld16(parity + ((size_t)g * P.n_lines + l) * C + j);
+    const v4u* pl = parity + ((size_t)g * P.n_lines + l) * C + j;
+    v4u acc = ld16(pl);
+    const ptrdiff_t to_par = pl - grp;
     v4u mv[MAXC];
+    bool use[MAXC];
 #pragma unroll
-    for (int q = 0; q < MAXC; ++q) {
+    for (int q = 0; q < MAXC; ++q) { // (unconditional loads, see k_decode_rows)
         const uint32_t i = first + q * stride;
-        mv[q] = v4u{0, 0, 0, 0};
-        if ((uint32_t)q < count && i != tgt) // every other member of a firing line is present
-            mv[q] = ld16(grp + (size_t)i * C);
+        use[q] = (uint32_t)q < count && i != tgt; // every other member of a firing line is present
+        mv[q] = ld16(grp + (use[q] ? (ptrdiff_t)i * C : to_par));
     }
 #pragma unroll
     for (int q = 0; q < MAXC; ++q)
-        acc ^= mv[q];
+        acc ^= use[q] ? mv[q] : v4u{0, 0, 0, 0};
     st16(dst, acc);
 }
 
@@ -1499,6 +1560,10 @@ __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* 
                                                         uint32_t col_rt, FastDiv divCol)
 {
     static_assert(K <= 64, "row decode keeps the present mask in one word");
+#ifdef RFEC_DEC_LDS_PAD // A/B (tools/build_ab.sh): a block's LDS allocation as round 2's
+    __shared__ uint32_t lds_pad[RFEC_DEC_LDS_PAD / 4];
+    asm volatile("" ::"v"(lds_pad));
+#endif
     uint32_t hb, pb;
     if (header_block_xcd((n_hdr_blocks + 7u) >> 3, hdr_every, npay8, &hb, &pb)) {
         if (hb < n_hdr_blocks)
@@ -1544,17 +1609,23 @@ __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* 
         dst = D.sh + ((size_t)g * D.E + e) * C + j;
     }
     v4u* row = shards + ((size_t)g * KK + r * CC) * C + j;
-    v4u acc = ld16(parity + ((size_t)g * R + r) * C + j);
+    const v4u* par = parity + ((size_t)g * R + r) * C + j;
+    v4u acc = ld16(par);
+    // Every member load is issued unconditionally (a slot the row does not
+    // use re-reads the parity chunk, an L2 hit, and is masked after): under
+    // per-load branches hipcc waited on each load before the next one
+    // (vmcnt(0) between them: 130 vs 121 us at c3).
     v4u mv[COL];
+    bool use[COL];
+    const ptrdiff_t to_par = par - row; // (a select of two pointers loses the nt hint)
 #pragma unroll
     for (int q = 0; q < COL; ++q) {
-        mv[q] = v4u{0, 0, 0, 0};
-        if ((uint32_t)q < cnt && r * CC + q != tgt)
-            mv[q] = ld16(row + (size_t)q * C);
+        use[q] = (uint32_t)q < cnt && r * CC + q != tgt;
+        mv[q] = ld16(row + (use[q] ? (ptrdiff_t)q * C : to_par));
     }
 #pragma unroll
     for (int q = 0; q < COL; ++q)
-        acc ^= mv[q];
+        acc ^= use[q] ? mv[q] : v4u{0, 0, 0, 0};
     st16(dst, acc);
 }
 
@@ -1715,11 +1786,21 @@ hipError_t launch_encode(const EncLaunch& a, unsigned flags)
     if (!generic && P->k >= 6 && P->k <= 16 && is_full_matrix(P, P->k <= 9 ? 3 : 4)) {
         const uint32_t head = enc_head(a);
         const dim3 grid(head + blocks_for(total));
+#ifdef RFEC_MATRIX_OUT // A/B: the output-mapped form
+        const uint32_t nl = P->n_lines, tot = a.groups * nl * a.cd;
+        const dim3 grid_o(head + blocks_for(tot));
+#define RFEC_MX(KK, CC)                                                                                           \
+    case KK:                                                                                                      \
+        RFEC_LAUNCH((k_encode_matrix_out<KK, CC>), grid_o, dim3(kBlock), 0, a.stream, a.s, a.p, tot, C,          \
+                    make_fastdiv(a.cd), make_fastdiv(nl * a.cd), head, a.E, *P);                                  \
+        return hipGetLastError();
+#else
 #define RFEC_MX(KK, CC)                                                                                           \
     case KK:                                                                                                      \
         RFEC_LAUNCH((k_encode_matrix<KK, CC>), grid, dim3(kBlock), 0, a.stream, a.s, a.p, total, C,               \
                     make_fastdiv(a.cd), head, a.E, *P);                                                           \
         return hipGetLastError();
+#endif
         switch (P->k) {
             RFEC_MX(6, 3) RFEC_MX(7, 3) RFEC_MX(8, 3) RFEC_MX(9, 3) RFEC_MX(10, 4) RFEC_MX(11, 4) RFEC_MX(12, 4)
             RFEC_MX(13, 4) RFEC_MX(14, 4) RFEC_MX(15, 4) RFEC_MX(16, 4)

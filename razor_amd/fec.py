@@ -30,6 +30,7 @@ RFEC_MAX_LINES = 64
 RFEC_LAYER_ROWS = 1
 RFEC_LAYER_COLS = 2
 RFEC_TUNE_GENERIC = 1
+RFEC_TUNE_NO_SERVICE = 2
 
 # 20-byte header record == sim_fec_meta_t layout (sim_proto.h:145-155)
 HDR_DTYPE = np.dtype([("seq", "<u4"), ("fid", "<u4"), ("ts", "<u4"), ("index", "<u2"), ("total", "<u2"),
@@ -212,6 +213,8 @@ _SIGS = {
                                   C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(rfec_rx_report), _P]),
     "rfec_set_tuning": (None, [C.c_uint]),
     "rfec_get_tuning": (C.c_uint, []),
+    "rfec_service_stop": (C.c_int, []),
+    "rfec_service_stats": (None, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "rfec_last_error": (C.c_char_p, []),
     "rfec_host_encode_groups": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, _P, _P, C.c_uint16, _P]),
     "rfec_probe_read": (C.c_int, [_P, C.c_size_t, _P, C.c_uint, _P]),

@@ -13,6 +13,7 @@ flex_fec_xor.c (`make dropin`), and the reference's tests with librazor_fec.so
 in place of flex_fec_xor.c, flex_fec_sender.c and flex_fec_receiver.c
 (`make dropin_flex`).  A link check only: running them needs the GPU.
 """
+import os
 import subprocess
 from pathlib import Path
 
@@ -25,10 +26,18 @@ HARNESS = ROOT / "razor_amd" / "lib" / "fec_test_harness"
 REFERENCE = Path("/root/reference")
 
 
+# the resident service (default), with a relaunch before every call (a 1 us
+# idle window races the workgroup's exit against the next post), and kernel
+# launches per call
+SERVICE_ENVS = {"service": {}, "service_relaunch": {"RFEC_SERVICE_IDLE_US": "1"}, "launch": {"RFEC_SERVICE": "0"}}
+
+
 @pytest.mark.gpu
-def test_reference_tests_through_dropin_symbols():
+@pytest.mark.parametrize("mode", list(SERVICE_ENVS))
+def test_reference_tests_through_dropin_symbols(mode):
     assert HARNESS.exists(), "razor_amd/lib/fec_test_harness not built (python -m razor_amd.build)"
-    r = subprocess.run([str(HARNESS)], capture_output=True, text=True, timeout=120)
+    env = dict(os.environ, **SERVICE_ENVS[mode])
+    r = subprocess.run([str(HARNESS)], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout == (po.GOLDEN / "ref_fec_test_stdout.txt").read_text()
 

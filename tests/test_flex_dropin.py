@@ -22,6 +22,7 @@ import torch
 
 import parity_cases as pc
 import pyoracle as po
+from razor_amd.fec import RFEC_TUNE_NO_SERVICE
 
 pytestmark = pytest.mark.gpu
 
@@ -88,11 +89,29 @@ def bind_flex(product):
     return product
 
 
-@pytest.fixture(scope="module")
-def flex(product):
+@pytest.fixture(scope="module", params=["service", "launch"])
+def flex(product, request):
+    """The drop-in both ways: posted to the resident service (the default) and
+    with a kernel launch per call (RFEC_TUNE_NO_SERVICE)."""
     if not torch.cuda.is_available():
         pytest.fail("no GPU visible: the -m gpu suite must run on an MI355X")
-    return bind_flex(product)
+    L = product.lib
+    before = _svc_stats(L)
+    L.rfec_set_tuning(0 if request.param == "service" else RFEC_TUNE_NO_SERVICE)
+    yield bind_flex(product)
+    L.rfec_set_tuning(0)
+    jobs = _svc_stats(L)[0] - before[0]
+    assert L.rfec_service_stop() == 0
+    if request.param == "service":
+        assert jobs > 0, "no drop-in call reached the resident service"
+    else:
+        assert jobs == 0, "a drop-in call reached the service under RFEC_TUNE_NO_SERVICE"
+
+
+def _svc_stats(L):
+    j, n = C.c_uint64(), C.c_uint64()
+    L.rfec_service_stats(C.byref(j), C.byref(n))
+    return j.value, n.value
 
 
 def make_segments(lib, shards, hdr):
