@@ -619,7 +619,7 @@ static int svc_acquire(void)
             return 0;
         }
         const size_t o_shards = svc_align(sizeof(rfec_svc_ctl));
-        const size_t o_parity = o_shards + svc_align((size_t)DI_MAXK * DI_STRIDE);
+        const size_t o_parity = o_shards + svc_align((size_t)RFEC_SVC_SLOTS * DI_STRIDE);
         const size_t bytes = o_parity + svc_align((size_t)RFEC_MAX_LINES * DI_STRIDE);
         void* h = NULL;
         if ((e = hipGetDeviceCount(&n)) != hipSuccess || n == 0 || (e = hipGetDevice(&dev)) != hipSuccess ||
@@ -652,9 +652,11 @@ static int svc_acquire(void)
 }
 
 static uint8_t* svc_shard(uint32_t i) { return (uint8_t*)g_svc.ctl + g_svc.o_shards + (size_t)i * DI_STRIDE; }
-static uint8_t* svc_parity(uint32_t i) { return (uint8_t*)g_svc.ctl + g_svc.o_parity + (size_t)i * DI_STRIDE; }
+static uint8_t* svc_out(uint32_t i) { return (uint8_t*)g_svc.ctl + g_svc.o_parity + (size_t)i * DI_STRIDE; }
 
-/* a payload into a service slot: the bytes, zero to the end of their last 16-byte chunk; returns the chunks */
+/* a payload into a service slot: the bytes, zero to the end of their last
+ * 16-byte chunk (chunks past it are stale: the device masks them); returns
+ * the chunks */
 static uint8_t svc_stage(uint8_t* slot, const uint8_t* data, uint32_t size)
 {
     const uint32_t n = size < SIM_VIDEO_SIZE ? size : SIM_VIDEO_SIZE, nck = (n + 15) / 16;
@@ -663,13 +665,13 @@ static uint8_t svc_stage(uint8_t* slot, const uint8_t* data, uint32_t size)
     return (uint8_t)nck;
 }
 
-/* mutex held, the job written: post it, (re)launch the workgroup when it is
- * gone, wait for `done` */
-static int svc_run(void)
+/* mutex held, the job written: ring the doorbell, (re)launch the workgroup
+ * when it is gone, wait for `done` */
+static int svc_run(uint32_t n_slots, uint32_t op)
 {
     rfec_svc_ctl* q = g_svc.ctl;
     const uint32_t seq = ++g_svc.seq;
-    __atomic_store_n(&q->req, seq, __ATOMIC_RELEASE);
+    __atomic_store_n(&q->bell, RFEC_SVC_BELL(seq, n_slots, op), __ATOMIC_RELEASE);
     const double t0 = now_us();
     for (uint64_t spin = 0;; ++spin) {
         if (__atomic_load_n(&q->done, __ATOMIC_ACQUIRE) == seq)
@@ -709,11 +711,10 @@ static int svc_generate_group(sim_segment_t* const* segs, int k, const rfec_plan
     J->capacity = SIM_VIDEO_SIZE;
     J->plan = *plan;
     for (int i = 0; i < k; ++i) {
-        J->slot_src[i] = (uint16_t)i;
         J->slot_nck[i] = svc_stage(svc_shard((uint32_t)i), segs[i]->data, segs[i]->data_size);
         seg_to_hdr(segs[i], (rfec_hdr*)&J->hdr[5 * i]);
     }
-    return svc_run();
+    return svc_run((uint32_t)k, RFEC_SVC_ENCODE);
 }
 
 /* a group encode's results (line l: meta m[l], fec_data_size fds[l], status
@@ -765,7 +766,7 @@ int rfec_di_generate_group(sim_segment_t* const* segs, int k, const rfec_plan* p
         if (rc == RFEC_OK) {
             const rfec_svc_ctl* q = g_svc.ctl;
             di_take_group(segs, plan, outs, rets, (const rfec_hdr*)q->out.meta, q->out.fsize, q->out.status,
-                          svc_parity(0));
+                          svc_out(0));
         }
         pthread_mutex_unlock(&g_svc.mu);
         if (rc == RFEC_OK)
@@ -868,7 +869,8 @@ static int di_refused(const rfec_di_recover_job* J)
 }
 
 /* rfec_di_recover_lines through the service (mutex held): up to
- * RFEC_DI_GROUPS jobs per post, each its members then its parity in LDS */
+ * RFEC_DI_GROUPS jobs per post, each its members then its parity in
+ * consecutive slots, its recovered payload to output slot g */
 static int svc_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets)
 {
     rfec_svc_ctl* q = g_svc.ctl;
@@ -884,18 +886,15 @@ static int svc_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets)
             const uint32_t c = (uint32_t)J->count;
             if (ns + c + 1 > RFEC_SVC_SLOTS || ns + c + 1 > DI_MAXK)
                 break;
-            S->slot0[G] = S->hdr0[G] = (uint16_t)ns;
+            S->slot0[G] = (uint16_t)ns;
             S->count[G] = (uint16_t)c;
             S->fsize[G] = J->fec->fec_data_size;
             memcpy(&S->hdr[5 * ns], &J->fec->fec_meta, sizeof(rfec_hdr));
             for (uint32_t i = 0; i < c; ++i) {
-                S->slot_src[ns + i] = (uint16_t)(ns + i);
                 S->slot_nck[ns + i] = svc_stage(svc_shard(ns + i), J->segs[i]->data, J->segs[i]->data_size);
                 seg_to_hdr(J->segs[i], (rfec_hdr*)&S->hdr[5 * (ns + 1 + i)]);
             }
-            S->slot_src[ns + c] = (uint16_t)(G | RFEC_SVC_PARITY_SLOT);
-            S->slot_nck[ns + c] = svc_stage(svc_parity(G), J->fec->fec_data, J->fec->fec_data_size);
-            S->out_slot[G] = (uint16_t)(ns + c); /* the shards slot next to the members: free */
+            S->slot_nck[ns + c] = svc_stage(svc_shard(ns + c), J->fec->fec_data, J->fec->fec_data_size);
             idx[G++] = j;
             ns += c + 1;
         }
@@ -905,7 +904,7 @@ static int svc_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets)
         S->n_slots = ns;
         S->groups = G;
         S->capacity = SIM_VIDEO_SIZE;
-        const int rc = svc_run();
+        const int rc = svc_run(ns, RFEC_SVC_RECOVER);
         if (rc != RFEC_OK)
             return rc;
         for (uint32_t g = 0; g < G; ++g) {
@@ -913,7 +912,7 @@ static int svc_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets)
             di_pad_members(J);
             if (q->out.status[g] != 0)
                 continue;
-            di_take_recovered(J, (const rfec_hdr*)q->out.meta[g], svc_shard(S->out_slot[g]));
+            di_take_recovered(J, (const rfec_hdr*)q->out.meta[g], svc_out(g));
             rets[idx[g]] = 0;
         }
     }

@@ -87,26 +87,28 @@ __attribute__((visibility("hidden"))) int rfec_di_generate_group(sim_segment_t* 
                                                                  int* rets);
 __attribute__((visibility("hidden"))) int rfec_di_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets);
 /* The resident service (rfec_service.hip): one workgroup polling a doorbell in
- * pinned, host-coherent memory for the drop-in's jobs.  Slot codes name a
- * staging slot: shards slot i, or parity slot i | RFEC_SVC_PARITY_SLOT. */
+ * pinned, host-coherent memory for the drop-in's jobs.  A job's payloads sit
+ * in staging slots 0..n_slots-1 (LDS slot s = staging slot s); its outputs go
+ * to the output slots (encode: line l, recover: job g). */
 #define RFEC_SVC_ENCODE 1u
 #define RFEC_SVC_RECOVER 2u
-#define RFEC_SVC_PARITY_SLOT 0x8000u
 #define RFEC_SVC_SLOTS 264 /* an encode group (<= 255 members) or the recover jobs' members + parities */
+/* the doorbell word: job sequence number | n_slots << 32 | op << 48 */
+#define RFEC_SVC_BELL(seq, ns, op) ((uint64_t)(uint32_t)(seq) | (uint64_t)(ns) << 32 | (uint64_t)(op) << 48)
 typedef struct {
     uint32_t op, n_slots, groups, capacity;
     rfec_kplan plan;                   /* encode: the group's lines over slots 0..k-1 */
-    uint16_t slot0[RFEC_DI_GROUPS];    /* recover job g: its members' first LDS slot, its parity right after */
+    uint16_t slot0[RFEC_DI_GROUPS];    /* recover job g: its first slot (members, then its parity) and the
+                                        * first of its header records (the parity's meta, then the members') */
     uint16_t count[RFEC_DI_GROUPS];    /* present members */
     uint16_t fsize[RFEC_DI_GROUPS];    /* fec_data_size */
-    uint16_t hdr0[RFEC_DI_GROUPS];     /* first header record: the parity's meta, then the members' */
-    uint16_t out_slot[RFEC_DI_GROUPS]; /* shards slot of the recovered payload */
-    uint16_t slot_src[RFEC_SVC_SLOTS]; /* LDS slot s <- staging slot code */
-    uint8_t slot_nck[RFEC_SVC_SLOTS];  /* 16-byte chunks of the slot that may be non-zero */
-    uint32_t hdr[RFEC_SVC_SLOTS * 5];  /* encode: member i at 5 i; recover: as hdr0 */
+    uint16_t pad[RFEC_DI_GROUPS];
+    uint8_t slot_nck[RFEC_SVC_SLOTS];  /* 16-byte chunks of the slot that hold its bytes (the rest: stale) */
+    uint32_t hdr[RFEC_SVC_SLOTS * 5];  /* encode: member i at 5 i; recover: as slot0 */
 } rfec_svc_job;
 typedef struct {
-    uint32_t req, stop, pad0[14];  /* host-written line: job sequence number, leave now */
+    uint64_t bell;                 /* host-written: RFEC_SVC_BELL, written last */
+    uint32_t stop, pad0[13];       /* host-written: leave now */
     uint32_t done, pad1[15];       /* device-written: the last job finished */
     uint32_t alive, pad2[15];      /* 1 set by the host before a launch, 0 by the workgroup as it leaves */
     struct {
@@ -116,7 +118,7 @@ typedef struct {
     } out;
     rfec_svc_job job;
 } rfec_svc_ctl;
-int rfec_launch_service(rfec_svc_ctl* ctl, const uint8_t* shards, uint8_t* parity, uint32_t stride,
+int rfec_launch_service(rfec_svc_ctl* ctl, const uint8_t* shards, uint8_t* out, uint32_t stride,
                         uint64_t idle_ticks, uint64_t life_ticks, void* stream);
 
 __attribute__((visibility("hidden"))) int rfec_set_error(int code, const char* what);

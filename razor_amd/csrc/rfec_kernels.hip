@@ -17,8 +17,9 @@
 //  header records of up to 64 groups staged in LDS, one lane per (group, line)):
 //    * row layouts (the sender's row layer, strip mode): k_encode_out, one
 //      lane per PARITY chunk loading its row's members, XCD-swizzled blocks;
-//    * the sender's full rows + columns plan (k = 6..16): k_encode_matrix, one
-//      lane per (group, chunk column), every member loaded once;
+//    * the sender's full rows + columns plan (k = 6..16): k_encode_matrix_out,
+//      one lane per PARITY chunk (group, line, chunk), member loads at the
+//      default policy so a column's lanes re-read its members from L2;
 //    * any other plan: k_encode (plan-driven).
 //  recover (rfec_launch_recover picks by plan):
 //    * pairwise disjoint lines (row layer, strip mode), one launch: header
@@ -80,6 +81,28 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 // payload streams: non-temporal loads and stores (every byte is touched once)
 __device__ __forceinline__ v4u ld16(const v4u* p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ void st16(v4u* p, v4u v) { __builtin_nontemporal_store(v, p); }
+
+// Predicated member loads of the decodes: a buffer descriptor over the wave's
+// first group (wave-uniform base, made provably uniform by readfirstlane) and
+// per-lane byte offsets; a load that is not wanted takes kNoLoad, past the
+// descriptor's range, and returns zeros without touching memory.  No branch
+// and no redundant request: with per-load branches hipcc waited on each load
+// before the next (c3 decode 130 us), with loads redirected to an address
+// already in flight it issued 25-150 % more requests (127 us).
+constexpr uint32_t kNoLoad = 0x7FFFFFF0u;
+constexpr int kAuxNT = 2; // gfx950 cache-policy bits: nt
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* p)
+{
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uint64_t)hi << 32 | lo), 0, (int)kNoLoad,
+                                             0x00020000);
+}
+__device__ __forceinline__ v4u bld16(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxNT));
+}
 
 // Payload-block index, XCD-swizzled.  Workgroups are dispatched round-robin
 // over the 8 XCDs (block b runs on XCD b % 8, each XCD with its own L2); the
@@ -309,7 +332,6 @@ __global__ __launch_bounds__(kBlock) void k_encode_matrix(const v4u* __restrict_
     }
 }
 
-#ifdef RFEC_MATRIX_OUT
 // Output-mapped form of the full matrix encode: one lane per PARITY chunk
 // (group, line, chunk column), as k_encode_out, so that every wave's store is
 // 1 KiB of consecutive parity bytes (whole 128-B lines when the slots are
@@ -353,7 +375,6 @@ __global__ __launch_bounds__(kBlock) void k_encode_matrix_out(const v4u* __restr
         acc ^= (uint32_t)q < count ? v[q] : v4u{0, 0, 0, 0};
     st16(parity + ((size_t)g * (NR + COL) + l) * C + j, acc);
 }
-#endif
 
 // ---------------------------------------------------------------------------
 // Encode payload, rows-of-COL, output-mapped (default for row layouts): one
@@ -1362,10 +1383,6 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
                                                             uint32_t n_hdr_blocks, uint32_t hdr_every, PeelArgs A,
                                                             rfec_kmask M, DenseOut D)
 {
-#ifdef RFEC_DEC_LDS_PAD
-    __shared__ uint32_t lds_pad[RFEC_DEC_LDS_PAD / 4];
-    asm volatile("" ::"v"(lds_pad));
-#endif
     uint32_t hb, pb;
     if (header_block(n_hdr_blocks, hdr_every, &hb, &pb)) {
         line_headers(A, M, hb);
@@ -1383,7 +1400,11 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
     uint64_t fire = A.parity_present[g];
     v4u* grp = shards + (size_t)g * P.k * C + j;
     v4u* out = D.E ? D.sh + (size_t)g * D.E * C + j : nullptr;
-    const v4u* par = parity + (size_t)g * P.n_lines * C + j;
+    // descriptors over the wave's first group (its lanes span a few groups)
+    const uint32_t gb = (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
+    const __amdgpu_buffer_rsrc_t rs = wave_rsrc(shards + (size_t)gb * P.k * C);
+    const __amdgpu_buffer_rsrc_t rp = wave_rsrc(parity + (size_t)gb * P.n_lines * C);
+    const uint32_t grp0 = ((g - gb) * P.k * C + j) * 16u, par0 = ((g - gb) * P.n_lines * C + j) * 16u;
     {   // lines with their parity received and exactly one member missing
         // (uniform loop: the line masks stay scalar kernel-argument loads)
         uint64_t f = 0;
@@ -1396,38 +1417,32 @@ __global__ __launch_bounds__(kBlock) void k_decode_disjoint(v4u* shards, const v
     }
     while (fire) {
         // two fired lines per round, every load of both in flight together
-        // (every load unconditional: a member slot the line does not use
-        // re-reads its parity chunk and is masked, see k_decode_rows)
+        // (predicated loads through the wave's descriptors, see wave_rsrc)
         v4u acc[2], mv[2][MAXC];
         uint32_t tg[2];
-        bool on[2], use[2][MAXC];
-        uint32_t l0 = 0;
+        bool on[2];
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            on[b] = fire != 0; // (the first always: the loop runs while lines fire)
-            const uint32_t l = on[b] ? (uint32_t)__ffsll((long long)fire) - 1 : l0; // off: the first's, re-read
-            l0 = l;
+            on[b] = fire != 0;
+            const uint32_t l = on[b] ? (uint32_t)__ffsll((long long)fire) - 1 : 0;
             fire &= fire - 1;
             const uint32_t ln = lplan[l];
             const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
-            const v4u* pl = par + (size_t)l * C;
-            acc[b] = ld16(pl);
-            const ptrdiff_t to_par = pl - grp;
+            acc[b] = bld16(rp, on[b] ? par0 + l * C * 16u : kNoLoad);
             tg[b] = first;
 #pragma unroll
             for (int q = 0; q < MAXC; ++q) {
                 const uint32_t i = first + q * stride;
                 const bool in = on[b] && (uint32_t)q < count, have = has_bit(h0, h1, i);
-                use[b][q] = in && have;
                 tg[b] = in && !have ? i : tg[b];
-                mv[b][q] = ld16(grp + (use[b][q] ? (ptrdiff_t)i * C : to_par));
+                mv[b][q] = bld16(rs, in && have ? grp0 + i * C * 16u : kNoLoad);
             }
         }
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
 #pragma unroll
             for (int q = 0; q < MAXC; ++q)
-                acc[b] ^= use[b][q] ? mv[b][q] : v4u{0, 0, 0, 0};
+                acc[b] ^= mv[b][q];
             if (on[b]) {
                 if (!D.E) {
                     st16(grp + (size_t)tg[b] * C, acc[b]);
@@ -1560,10 +1575,6 @@ __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* 
                                                         uint32_t col_rt, FastDiv divCol)
 {
     static_assert(K <= 64, "row decode keeps the present mask in one word");
-#ifdef RFEC_DEC_LDS_PAD // A/B (tools/build_ab.sh): a block's LDS allocation as round 2's
-    __shared__ uint32_t lds_pad[RFEC_DEC_LDS_PAD / 4];
-    asm volatile("" ::"v"(lds_pad));
-#endif
     uint32_t hb, pb;
     if (header_block_xcd((n_hdr_blocks + 7u) >> 3, hdr_every, npay8, &hb, &pb)) {
         if (hb < n_hdr_blocks)
@@ -1608,24 +1619,18 @@ __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* 
             return;
         dst = D.sh + ((size_t)g * D.E + e) * C + j;
     }
-    v4u* row = shards + ((size_t)g * KK + r * CC) * C + j;
-    const v4u* par = parity + ((size_t)g * R + r) * C + j;
-    v4u acc = ld16(par);
-    // Every member load is issued unconditionally (a slot the row does not
-    // use re-reads the parity chunk, an L2 hit, and is masked after): under
-    // per-load branches hipcc waited on each load before the next one
-    // (vmcnt(0) between them: 130 vs 121 us at c3).
+    // members through a descriptor over the wave's first group (wave_rsrc)
+    const uint32_t gb = (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
+    const __amdgpu_buffer_rsrc_t rs = wave_rsrc(shards + (size_t)gb * KK * C);
+    const uint32_t row0 = (((g - gb) * KK + r * CC) * C + j) * 16u;
+    v4u acc = ld16(parity + ((size_t)g * R + r) * C + j);
     v4u mv[COL];
-    bool use[COL];
-    const ptrdiff_t to_par = par - row; // (a select of two pointers loses the nt hint)
-#pragma unroll
-    for (int q = 0; q < COL; ++q) {
-        use[q] = (uint32_t)q < cnt && r * CC + q != tgt;
-        mv[q] = ld16(row + (use[q] ? (ptrdiff_t)q * C : to_par));
-    }
 #pragma unroll
     for (int q = 0; q < COL; ++q)
-        acc ^= use[q] ? mv[q] : v4u{0, 0, 0, 0};
+        mv[q] = bld16(rs, (uint32_t)q < cnt && r * CC + q != tgt ? row0 + (uint32_t)q * C * 16u : kNoLoad);
+#pragma unroll
+    for (int q = 0; q < COL; ++q)
+        acc ^= mv[q];
     st16(dst, acc);
 }
 
@@ -1786,7 +1791,7 @@ hipError_t launch_encode(const EncLaunch& a, unsigned flags)
     if (!generic && P->k >= 6 && P->k <= 16 && is_full_matrix(P, P->k <= 9 ? 3 : 4)) {
         const uint32_t head = enc_head(a);
         const dim3 grid(head + blocks_for(total));
-#ifdef RFEC_MATRIX_OUT // A/B: the output-mapped form
+#ifndef RFEC_MATRIX_REG // the output-mapped form (A/B -DRFEC_MATRIX_REG: one lane per (group, chunk column))
         const uint32_t nl = P->n_lines, tot = a.groups * nl * a.cd;
         const dim3 grid_o(head + blocks_for(tot));
 #define RFEC_MX(KK, CC)                                                                                           \
@@ -1977,7 +1982,9 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
     const uint32_t C = stride / 16;
     const uint32_t cd = capacity ? (capacity + 15) / 16 : 1;
     // disjoint plans (row layer alone, strip mode), lines of <= 8 members: one launch, header lanes
-    const bool fused = B.disjoint && maxc <= 8 && !generic;
+    // (the fused kernels address a wave's groups through one buffer descriptor: offsets < kNoLoad)
+    const bool fused = B.disjoint && maxc <= 8 && !generic &&
+                       (uint64_t)(kWave + 1) * (P.k > P.n_lines ? P.k : P.n_lines) * stride < kNoLoad;
     // plans with cascades within the register schedule (the sender's matrix plans): one launch
     const uint32_t Q = dense ? out->per_group : (P.n_lines < P.k ? P.n_lines : P.k);
     const bool cascade = !B.disjoint && maxc <= 4 && P.n_lines <= 8 && P.k <= 64 && !generic &&
