@@ -621,17 +621,27 @@ int rfec_rx_session_get_info(const rfec_rx_session* s, rfec_rx_session_info* inf
 void rfec_set_tuning(unsigned flags);
 unsigned rfec_get_tuning(void);
 
-/* The drop-in's resident service: one workgroup that stays on the device and
- * takes the drop-in symbols' jobs from a doorbell in pinned, host-coherent
- * memory (no launch, no stream synchronisation per call).  It starts on the
+/* The drop-in's resident service: RFEC_SERVICE_GROUPS (default 4, at most 8)
+ * workgroups that stay on the device and take the drop-in symbols' jobs from
+ * a doorbell in pinned, host-coherent memory (no launch, no stream
+ * synchronisation per call), each on its share of a job's 16-byte columns.  It starts on the
  * first drop-in call and leaves the device by itself after RFEC_SERVICE_IDLE_US
  * (default 20000) microseconds without a job, after one second in total (the
  * next call starts it again) and at exit.  rfec_service_stop() makes it leave
  * now and waits for it; it returns RFEC_OK (also when it was not running) or
- * RFEC_EDEVICE.  rfec_service_stats reports the calls served and the
- * launches made so far (either pointer may be NULL). */
+ * RFEC_EDEVICE.  rfec_service_get_info reports the calls served, the
+ * launches made and where a call's time goes (means over the calls served). */
+typedef struct {
+    uint64_t jobs;       /* drop-in calls served */
+    uint64_t launches;   /* workgroup launches (the first call, then after each idle exit) */
+    double stage_host_us; /* mean, per job: the host copying the segments next to the doorbell */
+    double wait_us;      /* doorbell written -> `done` seen by the host */
+    double dev_stage_us; /* on the device: doorbell seen -> the job's slots in LDS (one PCIe round trip) */
+    double dev_work_us;  /* -> results stored */
+    double dev_release_us; /* -> the system-scope release before `done` */
+} rfec_service_info;
 int rfec_service_stop(void);
-void rfec_service_stats(uint64_t* jobs, uint64_t* launches);
+int rfec_service_get_info(rfec_service_info* info);
 
 /* HBM ceiling probes (measurement only, not on the FEC path): streaming
  * read / copy / write of `bytes` (multiple of 16) in the FEC kernels' access

@@ -555,11 +555,13 @@ typedef struct {
     rfec_svc_ctl* ctl;   /* host view; the staging slots follow it */
     uint8_t* dev;        /* device view of the same allocation */
     size_t o_shards, o_parity;
-    uint32_t seq;
+    uint32_t seq, groups;
     uint64_t idle_ticks, life_ticks;
     uint64_t jobs, launches;
+    double tick_us;                                  /* s_memrealtime period */
+    double t_stage, t_wait, t_dstage, t_dwork, t_drel; /* sums over the jobs, us */
 } svc_state;
-static svc_state g_svc = {PTHREAD_MUTEX_INITIALIZER, 0, NULL, NULL, NULL, 0, 0, 0, 0, 0, 0, 0};
+static svc_state g_svc = {PTHREAD_MUTEX_INITIALIZER, 0, NULL, NULL, NULL, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
 static void svc_pause(void)
 {
@@ -577,6 +579,7 @@ static int svc_stop_locked(void)
     const hipError_t e = hipStreamSynchronize(g_svc.stream);
     __atomic_store_n(&g_svc.ctl->stop, 0u, __ATOMIC_RELEASE);
     g_svc.ctl->alive = 0;
+    g_svc.ctl->quit = 0;
     return e == hipSuccess ? RFEC_OK : set_err(RFEC_EDEVICE, "service stop", e);
 }
 
@@ -588,14 +591,24 @@ int rfec_service_stop(void)
     return rc;
 }
 
-void rfec_service_stats(uint64_t* jobs, uint64_t* launches)
+int rfec_service_get_info(rfec_service_info* info)
 {
+    if (!info)
+        return set_err(RFEC_EINVAL, "service info: NULL", 0);
     pthread_mutex_lock(&g_svc.mu);
-    if (jobs)
-        *jobs = g_svc.jobs;
-    if (launches)
-        *launches = g_svc.launches;
+    memset(info, 0, sizeof(*info));
+    info->jobs = g_svc.jobs;
+    info->launches = g_svc.launches;
+    if (g_svc.jobs) {
+        const double n = (double)g_svc.jobs;
+        info->stage_host_us = g_svc.t_stage / n;
+        info->wait_us = g_svc.t_wait / n;
+        info->dev_stage_us = g_svc.t_dstage / n;
+        info->dev_work_us = g_svc.t_dwork / n;
+        info->dev_release_us = g_svc.t_drel / n;
+    }
     pthread_mutex_unlock(&g_svc.mu);
+    return RFEC_OK;
 }
 
 static void svc_atexit(void) { (void)rfec_service_stop(); }
@@ -640,6 +653,10 @@ static int svc_acquire(void)
         const char* idle = getenv("RFEC_SERVICE_IDLE_US");
         const double idle_us = idle && atof(idle) > 0 ? atof(idle) : 20000.0;
         g_svc.idle_ticks = (uint64_t)(idle_us * khz / 1000.0);
+        g_svc.tick_us = 1000.0 / khz;
+        const char* grp = getenv("RFEC_SERVICE_GROUPS");
+        const int ng = grp ? atoi(grp) : 4;
+        g_svc.groups = ng >= 1 && ng <= RFEC_SVC_MAX_GROUPS ? (uint32_t)ng : 4u;
         g_svc.life_ticks = (uint64_t)khz * 1000u; /* one second */
         g_svc.state = 1;
         atexit(svc_atexit);
@@ -667,21 +684,33 @@ static uint8_t svc_stage(uint8_t* slot, const uint8_t* data, uint32_t size)
 
 /* mutex held, the job written: ring the doorbell, (re)launch the workgroup
  * when it is gone, wait for `done` */
-static int svc_run(uint32_t n_slots, uint32_t op)
+static int svc_run(uint32_t n_slots, uint32_t op, double t_begin)
 {
     rfec_svc_ctl* q = g_svc.ctl;
     const uint32_t seq = ++g_svc.seq;
-    __atomic_store_n(&q->bell, RFEC_SVC_BELL(seq, n_slots, op), __ATOMIC_RELEASE);
     const double t0 = now_us();
+    __atomic_store_n(&q->bell, RFEC_SVC_BELL(seq, n_slots, op), __ATOMIC_RELEASE);
     for (uint64_t spin = 0;; ++spin) {
-        if (__atomic_load_n(&q->done, __ATOMIC_ACQUIRE) == seq)
+        uint32_t w = 0;
+        while (w < g_svc.groups && __atomic_load_n(&q->done[w], __ATOMIC_ACQUIRE) == seq)
+            ++w;
+        if (w == g_svc.groups)
             break;
         if (__atomic_load_n(&q->alive, __ATOMIC_ACQUIRE) == 0) {
-            /* gone (or leaving): a new launch runs after it and takes the job */
+            /* gone (or leaving): wait until every workgroup of the old launch
+             * has left (they leave on `quit`; a part of this job one of them
+             * answered stays answered in its done[w]), then launch again: the
+             * new workgroups take the parts still missing */
+            hipError_t se = hipStreamSynchronize(g_svc.stream);
+            if (se != hipSuccess) {
+                g_svc.state = -1;
+                return set_err(RFEC_EDEVICE, "service relaunch", se);
+            }
+            q->quit = 0;
             q->alive = 1;
             __atomic_thread_fence(__ATOMIC_SEQ_CST);
             const int ke = rfec_launch_service(q, g_svc.dev + g_svc.o_shards, g_svc.dev + g_svc.o_parity, DI_STRIDE,
-                                               g_svc.idle_ticks, g_svc.life_ticks, g_svc.stream);
+                                               g_svc.idle_ticks, g_svc.life_ticks, g_svc.groups, g_svc.stream);
             if (ke) {
                 q->alive = 0;
                 g_svc.state = -1;
@@ -697,13 +726,21 @@ static int svc_run(uint32_t n_slots, uint32_t op)
         }
         svc_pause();
     }
+    const double t1 = now_us();
+    const uint64_t* t = q->out.t;
     ++g_svc.jobs;
+    g_svc.t_stage += t0 - t_begin;
+    g_svc.t_wait += t1 - t0;
+    g_svc.t_dstage += (double)(t[1] - t[0]) * g_svc.tick_us;
+    g_svc.t_dwork += (double)(t[2] - t[1]) * g_svc.tick_us;
+    g_svc.t_drel += (double)(t[3] - t[2]) * g_svc.tick_us;
     return RFEC_OK;
 }
 
 /* the group encode of rfec_di_generate_group through the service (mutex held) */
 static int svc_generate_group(sim_segment_t* const* segs, int k, const rfec_plan* plan)
 {
+    const double t_begin = now_us();
     rfec_svc_job* J = &g_svc.ctl->job;
     J->op = RFEC_SVC_ENCODE;
     J->n_slots = (uint32_t)k;
@@ -714,7 +751,7 @@ static int svc_generate_group(sim_segment_t* const* segs, int k, const rfec_plan
         J->slot_nck[i] = svc_stage(svc_shard((uint32_t)i), segs[i]->data, segs[i]->data_size);
         seg_to_hdr(segs[i], (rfec_hdr*)&J->hdr[5 * i]);
     }
-    return svc_run((uint32_t)k, RFEC_SVC_ENCODE);
+    return svc_run((uint32_t)k, RFEC_SVC_ENCODE, t_begin);
 }
 
 /* a group encode's results (line l: meta m[l], fec_data_size fds[l], status
@@ -879,6 +916,7 @@ static int svc_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets)
     while (j < n) {
         int idx[RFEC_DI_GROUPS];
         uint32_t G = 0, ns = 0;
+        const double t_begin = now_us();
         for (; j < n && G < RFEC_DI_GROUPS; ++j) {
             const rfec_di_recover_job* J = &jobs[j];
             if (di_refused(J))
@@ -904,7 +942,7 @@ static int svc_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets)
         S->n_slots = ns;
         S->groups = G;
         S->capacity = SIM_VIDEO_SIZE;
-        const int rc = svc_run(ns, RFEC_SVC_RECOVER);
+        const int rc = svc_run(ns, RFEC_SVC_RECOVER, t_begin);
         if (rc != RFEC_OK)
             return rc;
         for (uint32_t g = 0; g < G; ++g) {

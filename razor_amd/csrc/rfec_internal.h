@@ -93,6 +93,7 @@ __attribute__((visibility("hidden"))) int rfec_di_recover_lines(const rfec_di_re
 #define RFEC_SVC_ENCODE 1u
 #define RFEC_SVC_RECOVER 2u
 #define RFEC_SVC_SLOTS 264 /* an encode group (<= 255 members) or the recover jobs' members + parities */
+#define RFEC_SVC_MAX_GROUPS 8 /* workgroups of the service, each on its share of the chunk columns */
 /* the doorbell word: job sequence number | n_slots << 32 | op << 48 */
 #define RFEC_SVC_BELL(seq, ns, op) ((uint64_t)(uint32_t)(seq) | (uint64_t)(ns) << 32 | (uint64_t)(op) << 48)
 typedef struct {
@@ -109,17 +110,19 @@ typedef struct {
 typedef struct {
     uint64_t bell;                 /* host-written: RFEC_SVC_BELL, written last */
     uint32_t stop, pad0[13];       /* host-written: leave now */
-    uint32_t done, pad1[15];       /* device-written: the last job finished */
-    uint32_t alive, pad2[15];      /* 1 set by the host before a launch, 0 by the workgroup as it leaves */
+    uint32_t done[RFEC_SVC_MAX_GROUPS], pad1[16 - RFEC_SVC_MAX_GROUPS]; /* device-written: workgroup w's last job */
+    uint32_t alive, quit, pad2[14]; /* alive: 1 set by the host before a launch, 0 by workgroup 0 as it leaves;
+                                     * quit: set by workgroup 0 before that, the others leave on it */
     struct {
         uint32_t meta[RFEC_MAX_LINES][5]; /* encode: line l's meta; recover: job g's recovered header */
         uint16_t fsize[RFEC_MAX_LINES];
         int8_t status[RFEC_MAX_LINES];    /* flex_fec_generate / flex_fec_recover's 0 / -1 */
+        uint64_t t[4];                    /* s_memrealtime: bell seen, job staged, results stored, done */
     } out;
     rfec_svc_job job;
 } rfec_svc_ctl;
 int rfec_launch_service(rfec_svc_ctl* ctl, const uint8_t* shards, uint8_t* out, uint32_t stride,
-                        uint64_t idle_ticks, uint64_t life_ticks, void* stream);
+                        uint64_t idle_ticks, uint64_t life_ticks, uint32_t groups, void* stream);
 
 __attribute__((visibility("hidden"))) int rfec_set_error(int code, const char* what);
 /* sets rfec_last_error() from an errno value (0: `what` alone); returns code */

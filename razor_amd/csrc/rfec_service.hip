@@ -18,8 +18,9 @@
 // control block), then the doorbell word (sequence number, slot count, op);
 // lane 0 of the workgroup polls it (relaxed system-scope loads + s_sleep), the
 // workgroup loads the job description and its payload slots into LDS in ONE
-// burst of loads (one PCIe round trip), XORs, stores the results to the
-// output slots, releases at system scope and writes `done`.  The
+// burst of system-coherent loads (one PCIe round trip), XORs, stores the
+// results to the output slots with system-coherent stores, waits for their
+// acknowledgements and writes `done`.  The
 // workgroup returns when `stop` is set, after `idle_ticks` without a job, or
 // after `life_ticks` in total (every wave leaves through the same uniform
 // test); the host relaunches it when a job finds it gone.
@@ -51,33 +52,77 @@ __device__ __forceinline__ uint32_t poll_u32(const uint32_t* p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The results are written with system-coherent buffer stores (sc0 sc1: past
+// this CU's L1 and the XCD's L2, to the host memory itself) and drained
+// before `done`, so no L2 write-back release is needed (0.4 vs 1.0 us).
+constexpr int kSys = 1 | 16; // gfx950 cache-policy bits: sc0 | sc1
+// The job's bytes are read with plain loads behind a system-scope acquire
+// (tools/svc_ab.sh, a k = 10 group encode: 3.0-3.3 us from the doorbell to the
+// job in LDS; the same with the invalidate issued at the end of the previous
+// job instead, or with an agent-scope acquire; sc1 loads without an acquire
+// 6.0 us; sc0 loads read stale lines from L1).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(const void* p, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ v4u ld_job(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void st_sys(__amdgpu_buffer_rsrc_t r, uint32_t off, v4u v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kSys);
+}
+__device__ __forceinline__ void st_sys32(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, kSys);
+}
+__device__ __forceinline__ void st_sys16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint16_t v)
+{
+    __builtin_amdgcn_raw_buffer_store_b16(v, r, off, 0, kSys);
+}
+__device__ __forceinline__ void st_sys8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint8_t v)
+{
+    __builtin_amdgcn_raw_buffer_store_b8(v, r, off, 0, kSys);
+}
+#define CTL_OFF(field) ((uint32_t)offsetof(rfec_svc_ctl, field))
+
 // Chunk columns [j0, j0 + tj) of slots [0, ns) into lds (slot s at s tj), all
 // loads issued before the first LDS store; stale chunks (past a slot's bytes)
 // come along and are masked by the readers.  With `J` (the job description
 // copy, first tile), its loads go out in the same burst: one PCIe round trip.
 __device__ __forceinline__ void stage_tile(const SvcArgs& A, uint32_t ns, uint32_t j0, uint32_t tj, v4u* lds,
-                                           const rfec_svc_job* jsrc, rfec_svc_job* jdst)
+                                           bool jsrc, rfec_svc_job* jdst)
 {
-    constexpr uint32_t nj = sizeof(rfec_svc_job) / 16, UJ = (nj + kSvcBlock - 1) / kSvcBlock;
-    static_assert(sizeof(rfec_svc_job) % 16 == 0 && offsetof(rfec_svc_ctl, job) % 16 == 0, "job layout");
+    constexpr uint32_t njmax = sizeof(rfec_svc_job) / 16, UJ = (njmax + kSvcBlock - 1) / kSvcBlock;
+    static_assert(sizeof(rfec_svc_job) % 16 == 0 && offsetof(rfec_svc_ctl, job) % 16 == 0 &&
+                      offsetof(rfec_svc_job, hdr) % 16 == 0, "job layout");
+    // the job description up to its ns header records only
+    const uint32_t nj = offsetof(rfec_svc_job, hdr) / 16 + (5 * ns + 3) / 4;
     const uint32_t items = max(ns * tj, 1u);
     v4u v[kSvcU], t[UJ];
     // (unconditional loads at clamped indices: under per-load branches hipcc
     // waits on each load before issuing the next)
-    const v4u* js = reinterpret_cast<const v4u*>(jsrc ? jsrc : &A.ctl->job);
+    const __amdgpu_buffer_rsrc_t rc = sys_rsrc(A.ctl, sizeof(rfec_svc_ctl));
+    const __amdgpu_buffer_rsrc_t rs = sys_rsrc(A.shards, RFEC_SVC_SLOTS * A.C * 16u);
+#ifdef RFEC_SVC_FULL_JOB // A/B: the whole description
+    const uint32_t njr = njmax;
+#else
+    const uint32_t njr = nj;
+#endif
 #pragma unroll
     for (uint32_t u = 0; u < UJ; ++u)
-        t[u] = js[min(u * kSvcBlock + threadIdx.x, nj - 1)];
+        t[u] = ld_job(rc, CTL_OFF(job) + 16u * min(u * kSvcBlock + threadIdx.x, njr - 1));
 #pragma unroll
     for (int u = 0; u < kSvcU; ++u) {
         const uint32_t it = min(u * kSvcBlock + threadIdx.x, items - 1);
-        const uint32_t s = it / tj;
-        v[u] = A.shards[(size_t)s * A.C + j0 + (it - s * tj)];
+        const uint32_t s = it / max(tj, 1u);
+        v[u] = ld_job(rs, 16u * (s * A.C + j0 + (it - s * tj)));
     }
     if (jsrc) {
 #pragma unroll
         for (uint32_t u = 0; u < UJ; ++u)
-            if (u * kSvcBlock + threadIdx.x < nj)
+            if (u * kSvcBlock + threadIdx.x < njr)
                 reinterpret_cast<v4u*>(jdst)[u * kSvcBlock + threadIdx.x] = t[u];
     }
 #pragma unroll
@@ -89,10 +134,12 @@ __device__ __forceinline__ void stage_tile(const SvcArgs& A, uint32_t ns, uint32
 }
 
 // encode: line l's meta / fec_data_size / status from the member headers (the
-// job's hdr words, member i at 5 i), flex_fec_xor.c:9-28
-__device__ void svc_encode_meta(const SvcArgs& A, const rfec_svc_job& J, uint16_t* fsz)
+// job's hdr words, member i at 5 i), flex_fec_xor.c:9-28; every workgroup
+// needs the sizes (fsz), workgroup 0 writes the results
+__device__ void svc_encode_meta(const SvcArgs& A, const rfec_svc_job& J, uint16_t* fsz, bool write)
 {
     const rfec_kplan& P = J.plan;
+    const __amdgpu_buffer_rsrc_t rc = sys_rsrc(A.ctl, sizeof(rfec_svc_ctl));
     for (uint32_t l = threadIdx.x; l < P.n_lines; l += kSvcBlock) {
         const rfec_line ln = P.line[l];
         uint32_t m[5] = {0, 0, 0, 0, 0}, L = 0;
@@ -103,20 +150,23 @@ __device__ void svc_encode_meta(const SvcArgs& A, const rfec_svc_job& J, uint16_
                 m[d] ^= r[d];
             L = max(L, r[4] >> 16);
         }
+        fsz[l] = (uint16_t)L;
+        if (!write)
+            continue;
 #pragma unroll
         for (int d = 0; d < 5; ++d)
-            A.ctl->out.meta[l][d] = m[d];
-        A.ctl->out.fsize[l] = (uint16_t)L;
-        A.ctl->out.status[l] = (ln.count <= 1 || L > J.capacity) ? (int8_t)-1 : (int8_t)0;
-        fsz[l] = (uint16_t)L;
+            st_sys32(rc, CTL_OFF(out.meta) + 20u * l + 4u * d, m[d]);
+        st_sys16(rc, CTL_OFF(out.fsize) + 2u * l, (uint16_t)L);
+        st_sys8(rc, CTL_OFF(out.status) + l, (ln.count <= 1 || L > J.capacity) ? 0xFFu : 0u);
     }
 }
 
 // recover: job g's recovered header (meta ^ members) and verdict,
 // flex_fec_xor.c:64-71, 75-99; the job's hdr words: the parity's meta at
-// 5 slot0[g], then its members'
+// 5 slot0[g], then its members' (workgroup 0)
 __device__ void svc_recover_meta(const SvcArgs& A, const rfec_svc_job& J)
 {
+    const __amdgpu_buffer_rsrc_t rc = sys_rsrc(A.ctl, sizeof(rfec_svc_ctl));
     for (uint32_t g = threadIdx.x; g < J.groups; g += kSvcBlock) {
         const uint32_t* r = J.hdr + 5u * J.slot0[g];
         const uint32_t L = J.fsize[g];
@@ -134,8 +184,8 @@ __device__ void svc_recover_meta(const SvcArgs& A, const rfec_svc_job& J)
         ok = ok && (m[4] >> 16) <= L;
 #pragma unroll
         for (int d = 0; d < 5; ++d)
-            A.ctl->out.meta[g][d] = m[d];
-        A.ctl->out.status[g] = ok ? (int8_t)0 : (int8_t)-1;
+            st_sys32(rc, CTL_OFF(out.meta) + 20u * g + 4u * d, m[d]);
+        st_sys8(rc, CTL_OFF(out.status) + g, ok ? 0u : 0xFFu);
     }
 }
 
@@ -145,22 +195,27 @@ __device__ __forceinline__ v4u chunk(const v4u* lds, const rfec_svc_job& J, uint
     return j < J.slot_nck[s] ? lds[s * tj + jj] : v4u{0, 0, 0, 0};
 }
 
-// one job: slots [0, ns) staged tile by tile (the first tile together with
-// the job description), the lines (encode) or jobs (recover) XORed from LDS
-__device__ void svc_job(const SvcArgs& A, uint32_t ns, v4u* lds, rfec_svc_job& J, uint16_t* fsz)
+// One job, this workgroup's chunk columns [c0, c1) of every slot: staged
+// tile by tile (the first tile together with the job description), the
+// lines (encode) or jobs (recover) XORed from LDS.
+__device__ void svc_job(const SvcArgs& A, uint32_t ns, uint32_t c0, uint32_t c1, bool leader, v4u* lds,
+                        rfec_svc_job& J, uint16_t* fsz, uint64_t* t1)
 {
     const uint32_t C = A.C;
-    const uint32_t tmax = ns ? min(C, (uint32_t)kSvcLdsChunks / ns) : C;
-    for (uint32_t j0 = 0; j0 < C; j0 += tmax) {
-        const uint32_t tj = min(tmax, C - j0);
-        if (j0)
+    const uint32_t tmax = ns ? max(1u, min(c1 - c0, (uint32_t)kSvcLdsChunks / ns)) : c1 - c0;
+    const __amdgpu_buffer_rsrc_t ro = sys_rsrc(A.out, RFEC_MAX_LINES * C * 16u);
+    for (uint32_t j0 = c0, first = 1; first || j0 < c1; j0 += tmax, first = 0) {
+        const uint32_t tj = j0 < c1 ? min(tmax, c1 - j0) : 0u;
+        if (!first)
             __syncthreads(); // the previous tile's readers are done
-        stage_tile(A, ns, j0, tj, lds, j0 ? nullptr : &A.ctl->job, &J);
+        stage_tile(A, ns, j0, tj, lds, first, &J);
         __syncthreads();
-        if (j0 == 0) { // the headers' work, once J has landed
+        if (first) { // the headers' work, once J has landed
+            if (leader && threadIdx.x == 0)
+                *t1 = __builtin_amdgcn_s_memrealtime();
             if (J.op == RFEC_SVC_ENCODE)
-                svc_encode_meta(A, J, fsz);
-            else
+                svc_encode_meta(A, J, fsz, leader);
+            else if (leader)
                 svc_recover_meta(A, J);
             __syncthreads(); // fsz
         }
@@ -174,7 +229,7 @@ __device__ void svc_job(const SvcArgs& A, uint32_t ns, v4u* lds, rfec_svc_job& J
                 v4u acc = chunk(lds, J, ln.first, tj, jj, j);
                 for (uint32_t q = 1; q < ln.count; ++q)
                     acc ^= chunk(lds, J, ln.first + q * ln.stride, tj, jj, j);
-                A.out[(size_t)l * C + j] = acc;
+                st_sys(ro, 16u * (l * C + j), acc);
             }
         } else {
             for (uint32_t it = threadIdx.x; it < J.groups * tj; it += kSvcBlock) {
@@ -185,42 +240,57 @@ __device__ void svc_job(const SvcArgs& A, uint32_t ns, v4u* lds, rfec_svc_job& J
                 v4u acc = chunk(lds, J, s0 + n, tj, jj, j); // the parity slot follows the members
                 for (uint32_t q = 0; q < n; ++q)
                     acc ^= chunk(lds, J, s0 + q, tj, jj, j);
-                A.out[(size_t)g * C + j] = acc;
+                st_sys(ro, 16u * (g * C + j), acc);
             }
         }
+        if (tj == 0)
+            break;
     }
 }
 
+// gridDim.x workgroups (<= RFEC_SVC_MAX_GROUPS), workgroup w on chunk columns
+// [C w / n, C (w + 1) / n) of every job: the PCIe round trips of a job's
+// staging spread over several CUs.  Workgroup 0 leads: it writes the header
+// results and the timing, and it alone decides to leave (idle / lifetime):
+// `quit`, then `alive` = 0; the others leave on `quit` or `stop` (and, as a
+// backstop, 0.1 s after the lifetime).  Every workgroup answers in done[w].
 __global__ __launch_bounds__(kSvcBlock) void k_service(SvcArgs A)
 {
     __shared__ __attribute__((aligned(16))) v4u lds[kSvcLdsChunks];
     __shared__ uint32_t s_ns, s_exit, s_seq;
+    __shared__ uint64_t s_t1;
     __shared__ uint16_t fsz[RFEC_MAX_LINES];
     __shared__ __attribute__((aligned(16))) rfec_svc_job J; // the job description, copied per job
+    const uint32_t w = blockIdx.x, nw = gridDim.x;
+    const bool leader = w == 0;
+    const uint32_t c0 = A.C * w / nw, c1 = A.C * (w + 1) / nw;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    const uint64_t life = leader ? A.life_ticks : A.life_ticks + A.life_ticks / 10;
     uint64_t t_last = t_start;
-    uint32_t done = poll_u32(&A.ctl->done);
+    uint32_t done = poll_u32(&A.ctl->done[w]);
     for (;;) {
         if (threadIdx.x == 0) {
             uint32_t ex = 0;
             uint64_t bell = 0;
             for (;;) {
                 bell = __hip_atomic_load(&A.ctl->bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (poll_u32(&A.ctl->stop)) {
+                if (poll_u32(&A.ctl->stop) || (!leader && poll_u32(&A.ctl->quit))) {
                     ex = 1;
                     break;
                 }
                 if ((uint32_t)bell != done)
                     break;
                 const uint64_t now = __builtin_amdgcn_s_memrealtime();
-                if (now - t_last > A.idle_ticks || now - t_start > A.life_ticks) {
+                if ((leader && now - t_last > A.idle_ticks) || now - t_start > life) {
                     ex = 1;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
-            if (ex) // a job posted after the poll above finds alive == 0 and relaunches
+            if (ex && leader) { // a job posted after the poll above finds alive == 0 and relaunches
+                __hip_atomic_store(&A.ctl->quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(&A.ctl->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             s_seq = (uint32_t)bell;
             s_ns = (uint32_t)(bell >> 32) & 0xffffu;
             s_exit = ex;
@@ -229,13 +299,25 @@ __global__ __launch_bounds__(kSvcBlock) void k_service(SvcArgs A)
         if (s_exit) // uniform: every wave leaves here
             return;
         const uint32_t seq = s_seq;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the job's bytes, written before the bell
-        svc_job(A, min(s_ns, (uint32_t)RFEC_SVC_SLOTS), lds, J, fsz);
-        // every wave's stores complete and visible to the host before `done`
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the job's bytes, written before the doorbell
+        svc_job(A, min(s_ns, (uint32_t)RFEC_SVC_SLOTS), c0, c1, leader, lds, J, fsz, &s_t1);
+        const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+        // every wave's system-coherent stores acknowledged before `done`
+        __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
-        if (threadIdx.x == 0)
-            __hip_atomic_store(&A.ctl->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (threadIdx.x == 0) {
+            if (leader) { // timing of this job (rfec_service_get_info), before `done`
+                const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
+                const __amdgpu_buffer_rsrc_t rc = sys_rsrc(A.ctl, sizeof(rfec_svc_ctl));
+                st_sys(rc, CTL_OFF(out.t),
+                       v4u{(uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)s_t1, (uint32_t)(s_t1 >> 32)});
+                st_sys(rc, CTL_OFF(out.t) + 16u,
+                       v4u{(uint32_t)t2, (uint32_t)(t2 >> 32), (uint32_t)t3, (uint32_t)(t3 >> 32)});
+                __builtin_amdgcn_s_waitcnt(0);
+            }
+            __hip_atomic_store(&A.ctl->done[w], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         done = seq;
         t_last = __builtin_amdgcn_s_memrealtime();
     }
@@ -244,12 +326,12 @@ __global__ __launch_bounds__(kSvcBlock) void k_service(SvcArgs A)
 } // namespace
 
 extern "C" int rfec_launch_service(rfec_svc_ctl* ctl, const uint8_t* shards, uint8_t* out, uint32_t stride,
-                                   uint64_t idle_ticks, uint64_t life_ticks, void* stream)
+                                   uint64_t idle_ticks, uint64_t life_ticks, uint32_t groups, void* stream)
 {
-    if (stride % 16 || stride / 16 > 255)
+    if (stride % 16 || stride / 16 > 255 || groups < 1 || groups > RFEC_SVC_MAX_GROUPS)
         return (int)hipErrorInvalidValue;
     SvcArgs A{ctl, reinterpret_cast<const v4u*>(shards), reinterpret_cast<v4u*>(out), stride / 16, idle_ticks,
               life_ticks};
-    hipLaunchKernelGGL(k_service, dim3(1), dim3(kSvcBlock), 0, (hipStream_t)stream, A);
+    hipLaunchKernelGGL(k_service, dim3(groups), dim3(kSvcBlock), 0, (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }

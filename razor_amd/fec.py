@@ -89,6 +89,12 @@ class rfec_rx_session_info(C.Structure):
                 ("records_held", C.c_uint32), ("rows_held", C.c_uint32), ("pending", C.c_uint32)]
 
 
+class rfec_service_info(C.Structure):
+    _fields_ = [("jobs", C.c_uint64), ("launches", C.c_uint64), ("stage_host_us", C.c_double),
+                ("wait_us", C.c_double), ("dev_stage_us", C.c_double), ("dev_work_us", C.c_double),
+                ("dev_release_us", C.c_double)]
+
+
 class rfec_udp_addr(C.Structure):
     _fields_ = [("ip", C.c_uint32), ("port", C.c_uint16), ("reserved", C.c_uint16)]
 
@@ -214,7 +220,7 @@ _SIGS = {
     "rfec_set_tuning": (None, [C.c_uint]),
     "rfec_get_tuning": (C.c_uint, []),
     "rfec_service_stop": (C.c_int, []),
-    "rfec_service_stats": (None, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "rfec_service_get_info": (C.c_int, [C.c_void_p]),
     "rfec_last_error": (C.c_char_p, []),
     "rfec_host_encode_groups": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, _P, _P, C.c_uint16, _P]),
     "rfec_probe_read": (C.c_int, [_P, C.c_size_t, _P, C.c_uint, _P]),

@@ -49,9 +49,10 @@ hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t a, int d)
     return hipErrorNotSupported;
 }
 int rfec_launch_service(rfec_svc_ctl* ctl, const uint8_t* shards, uint8_t* out, uint32_t stride,
-                        uint64_t idle_ticks, uint64_t life_ticks, void* stream)
+                        uint64_t idle_ticks, uint64_t life_ticks, uint32_t groups, void* stream)
 {
-    (void)ctl, (void)shards, (void)out, (void)stride, (void)idle_ticks, (void)life_ticks, (void)stream;
+    (void)ctl, (void)shards, (void)out, (void)stride, (void)idle_ticks, (void)life_ticks, (void)groups,
+        (void)stream;
     return (int)hipErrorNotSupported;
 }
 hipError_t hipMalloc(void** p, size_t n)

@@ -109,9 +109,10 @@ def flex(product, request):
 
 
 def _svc_stats(L):
-    j, n = C.c_uint64(), C.c_uint64()
-    L.rfec_service_stats(C.byref(j), C.byref(n))
-    return j.value, n.value
+    from razor_amd.fec import rfec_service_info
+    i = rfec_service_info()
+    assert L.rfec_service_get_info(C.byref(i)) == 0
+    return i.jobs, i.launches
 
 
 def make_segments(lib, shards, hdr):
@@ -272,3 +273,4 @@ def test_flex_sender_random_fixture(flex, oracle1000):
                 assert bytes(f.fec_data)[:L] == pays[ri][:L].tobytes()
     finally:
         lib.lib.flex_fec_sender_destroy(snd)
+

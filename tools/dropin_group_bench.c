@@ -100,6 +100,10 @@ int main(int argc, char** argv)
         flex_fec_sender_release(fs, &out);
     }
 
+    rfec_service_info si; /* the resident service's breakdown of the group-level sender calls */
+    memset(&si, 0, sizeof(si));
+    rfec_service_get_info(&si);
+
     /* sender, line level: the same 7 lines (3 x 4 plan) as 7 calls */
     static const int first[7] = {0, 4, 8, 0, 1, 2, 3}, stride[7] = {1, 1, 1, 4, 4, 4, 4}, count[7] = {4, 4, 2, 3, 3, 2, 2};
     sim_fec_t* fl = (sim_fec_t*)malloc(7 * sizeof(sim_fec_t));
@@ -196,9 +200,12 @@ int main(int argc, char** argv)
            " \"sender_line_level_us_per_group\": %.2f,\n"
            " \"receiver_on_segment_row_and_col_us\": %.2f,\n"
            " \"receiver_two_flex_fec_recover_us\": %.2f,\n"
-           " \"outputs_equal\": %s}\n",
+           " \"outputs_equal\": %s,\n"
+           " \"service_sender\": {\"jobs\": %llu, \"launches\": %llu, \"stage_host_us\": %.2f, \"wait_us\": %.2f,"
+           " \"dev_stage_us\": %.2f, \"dev_work_us\": %.2f, \"dev_release_us\": %.2f}}\n",
            groups, K, SIM_VIDEO_SIZE, t_group / groups, t_line / groups, t_rx / rx_groups, t_rx2 / rx_groups,
-           ok ? "true" : "false");
+           ok ? "true" : "false", (unsigned long long)si.jobs, (unsigned long long)si.launches, si.stage_host_us,
+           si.wait_us, si.dev_stage_us, si.dev_work_us, si.dev_release_us);
     drain(&out);
     flex_fec_sender_destroy(fs);
     free(fl);
