@@ -621,7 +621,7 @@ int rfec_rx_session_get_info(const rfec_rx_session* s, rfec_rx_session_info* inf
 void rfec_set_tuning(unsigned flags);
 unsigned rfec_get_tuning(void);
 
-/* The drop-in's resident service: RFEC_SERVICE_GROUPS (default 4, at most 8)
+/* The drop-in's resident service: RFEC_SERVICE_GROUPS (default 1, at most 8)
  * workgroups that stay on the device and take the drop-in symbols' jobs from
  * a doorbell in pinned, host-coherent memory (no launch, no stream
  * synchronisation per call), each on its share of a job's 16-byte columns.  It starts on the

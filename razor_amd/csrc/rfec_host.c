@@ -654,9 +654,12 @@ static int svc_acquire(void)
         const double idle_us = idle && atof(idle) > 0 ? atof(idle) : 20000.0;
         g_svc.idle_ticks = (uint64_t)(idle_us * khz / 1000.0);
         g_svc.tick_us = 1000.0 / khz;
+        /* workgroups: 1 (tools/svc_groups.sh: 1 / 2 / 4 / 8 took 12.8 / 15.9 / 12.8 / 14.4 us per group
+         * encode on one box; more CUs shorten the XOR + stores, 2.0 -> 1.35 us, but not the PCIe round
+         * trip of the staging, 3.0-3.4 us, and the host then waits on more answers) */
         const char* grp = getenv("RFEC_SERVICE_GROUPS");
-        const int ng = grp ? atoi(grp) : 4;
-        g_svc.groups = ng >= 1 && ng <= RFEC_SVC_MAX_GROUPS ? (uint32_t)ng : 4u;
+        const int ng = grp ? atoi(grp) : 1;
+        g_svc.groups = ng >= 1 && ng <= RFEC_SVC_MAX_GROUPS ? (uint32_t)ng : 1u;
         g_svc.life_ticks = (uint64_t)khz * 1000u; /* one second */
         g_svc.state = 1;
         atexit(svc_atexit);

@@ -25,8 +25,8 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 
-KERNELS = {"encode": ("k_encode",), "decode": ("k_decode_rows", "k_decode_out", "k_decode_disjoint", "k_decode_cascade", "k_decode_small"),
-           "peel": ("k_peel",), "recover": ("k_recover",)}
+KERNELS = {"encode": ("k_encode",), "decode": ("k_decode_rows", "k_decode_out", "k_decode_disjoint", "k_decode_cascade"),
+           "check": ("k_cascade_check",), "peel": ("k_peel",), "recover": ("k_recover",)}
 
 
 def run_pass(counter, outdir, bench_args, timeout):
@@ -105,6 +105,9 @@ def main():
         entry["decode_hbm_bytes_per_launch"] = res["decode"]["hbm_bytes"]
         entry["decode_algorithmic_bytes"] = dec_alg
         entry["decode_traffic_over_algorithmic"] = res["decode"]["hbm_bytes"] / dec_alg
+        if "check" in res:  # the cascade decode's two launches together
+            entry["decode_with_check_traffic_over_algorithmic"] = (res["decode"]["hbm_bytes"] +
+                                                                   res["check"]["hbm_bytes"]) / dec_alg
     name = f"k{k}_r{r}_S{S}_G{groups}"
     Path(args.out).write_text(json.dumps({name: entry}, indent=1))
     print(json.dumps({name: entry}, indent=1))
