@@ -234,17 +234,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
     void* q = reinterpret_cast<void*>((uint64_t)hi << 32 | lo);
     return __builtin_amdgcn_make_buffer_rsrc(q, 0, (int)__builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
 }
-// Parse: wave priority 3 over 1 = the payload store, 2 = a datagram's
-// processing, 3 = the batch header pass, 4 = 1 and 3; 0 = none
-#ifndef RFEC_WIRE_PARSE_PRIO
-#define RFEC_WIRE_PARSE_PRIO 4
-#endif
-// Frame kernels: wave priority 3 over 1 = the CRC, 2 = finish_frame (CRC,
-// trailer, store staging), 3 = a whole datagram's processing, 4 = the header
-// bytes and finish_frame; 0 = none
-#ifndef RFEC_WIRE_FRAME_PRIO
-#define RFEC_WIRE_FRAME_PRIO 2
-#endif
+// Wave priority (s_setprio 3, measured against the other placements in round
+// 2): the frame kernels raise it over finish_frame (the CRC,
+// the trailer, the store staging), the parse over its payload store and over
+// the batch header pass; each raise is dropped again before the next phase.
 constexpr int kAuxNT = 2; // gfx950 cache-policy bits: nt
 #ifndef RFEC_WIRE_STORE_AUX
 #define RFEC_WIRE_STORE_AUX 2 // stores' cache policy (the lab's ST0 build: 0)
@@ -420,9 +413,7 @@ __device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, ui
                                              uint32_t lane, uint8_t* __restrict__ slot, uint32_t dstride,
                                              uint16_t* dlen_out, uint32_t* wb)
 {
-#if RFEC_WIRE_FRAME_PRIO == 2
     __builtin_amdgcn_s_setprio(3);
-#endif
     constexpr int ND = B / 4;
     uint32_t w[ND];
 #pragma unroll
@@ -435,13 +426,7 @@ __device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, ui
                 hd = lane == (uint32_t)L ? H.h[L * ND + k] : hd;
         w[k] = (pay[k] | hd) & len_mask<B>(k, lane, n);
     }
-#if RFEC_WIRE_FRAME_PRIO == 1
-    __builtin_amdgcn_s_setprio(3); // the CRC's dependent LDS / DPP chain ahead of the other waves' work
-#endif
     const uint32_t crc = wave_crc32<B>(T, w, n, RFEC_WIRE_CRC_SEED, lane);
-#if RFEC_WIRE_FRAME_PRIO == 1
-    __builtin_amdgcn_s_setprio(0);
-#endif
     // big-endian trailer at byte n: its first 4 - s bytes end dword n / 4, the
     // rest start the next one (both positions wave-uniform)
     const uint32_t be = bswap(crc), s = n & 3u, q0 = n >> 2, q1 = q0 + 1;
@@ -457,9 +442,7 @@ __device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, ui
     store_slot<B>(slot, dstride, lane, w, wb);
     if (lane == 0)
         *dlen_out = (uint16_t)(n + 4);
-#if RFEC_WIRE_FRAME_PRIO == 2 || RFEC_WIRE_FRAME_PRIO == 4
     __builtin_amdgcn_s_setprio(0);
-#endif
 }
 
 template <int B>
@@ -515,14 +498,6 @@ __device__ __forceinline__ uint32_t load_seg_fields(const rfec_hdr* __restrict__
     return h | s;
 }
 
-// end of a datagram's processing under RFEC_WIRE_FRAME_PRIO == 3
-__device__ __forceinline__ void frame_prio_end()
-{
-#if RFEC_WIRE_FRAME_PRIO == 3
-    __builtin_amdgcn_s_setprio(0);
-#endif
-}
-
 // Ping-pong software pipeline over datagrams d0, d0 + nw, ...: the loads of
 // datagram i+1 go into the other buffer before datagram i is processed, and
 // no register copy ever waits on them (vmcnt is an in-order counter).
@@ -536,13 +511,11 @@ __device__ __forceinline__ void ping_pong(uint32_t d, uint32_t count, uint32_t n
         const uint32_t d1 = d + nw;
         load(min(d1, count - 1), b);
         proc(a, d);
-        frame_prio_end();
         if (d1 >= count)
             break;
         const uint32_t d2 = d1 + nw;
         load(min(d2, count - 1), a);
         proc(b, d1);
-        frame_prio_end();
         if (d2 >= count)
             break;
         d = d2;
@@ -692,9 +665,6 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
                                       load_window<ND + 1>(parity + (size_t)dd * stride, range, off, P.w);
                               },
                               [&](const PW& P, uint32_t d) {
-#if RFEC_WIRE_FRAME_PRIO == 3
-            __builtin_amdgcn_s_setprio(3);
-#endif
             const uint32_t o = order ? order[d] : d; // output slot
             uint8_t* slot = dgram + (size_t)o * dstride;
             const uint32_t L = fld(P.f, 11);
@@ -730,9 +700,6 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
                     stage_window<48, ND + 1>(P.w, lane, wb, x);
                 else
                     win_dwords<B, 48>(P.w, lane, x);
-#if RFEC_WIRE_FRAME_PRIO == 4
-                __builtin_amdgcn_s_setprio(3);
-#endif
                 funnel<ND, 3>(x, pay); // window [B j - 48, ...) -> bytes [B j - 45, ...)
                 finish_frame<B>(T, H, 45 + L, pay, lane, slot, dstride, dlen + o, wb);
             }
@@ -803,9 +770,6 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                                       load_window<ND + 2>(shards + (size_t)dd * stride, range, off, P.w);
                               },
                               [&](const PW& P, uint32_t d) {
-#if RFEC_WIRE_FRAME_PRIO == 3
-            __builtin_amdgcn_s_setprio(3);
-#endif
             RFEC_DIAG_LOAD_ONLY(diag_fold(P.w) ^ P.f, dgram)
             const uint32_t o = order ? order[d] : d; // output slot
             uint8_t* slot = dgram + (size_t)o * dstride;
@@ -843,9 +807,6 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                     stage_window<32, ND + 2>(P.w, lane, wb, x);
                 else
                     win_dwords<B, 32>(P.w, lane, x);
-#if RFEC_WIRE_FRAME_PRIO == 4
-                __builtin_amdgcn_s_setprio(3);
-#endif
                 // window [B j - 32, ...) shifted by 32 - hs bytes
 #if defined(RFEC_WIRE_DIAG_NO_HDR) // lab: header bytes left zero, one layout
                 hs = 26, H.h[0] = layout ^ s.uid;
@@ -1254,9 +1215,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
     uint32_t pk = 0, i = kWave; // i: the datagram's index in its batch (kWave: a batch starts)
     auto proc = [&](const PW& P, uint32_t d) {
         const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)pk, (int)i++);
-#if RFEC_WIRE_PARSE_PRIO == 2
-        __builtin_amdgcn_s_setprio(3);
-#endif
         RFEC_DIAG_LOAD_ONLY(diag_fold(P) ^ f, payload)
         const uint32_t len = f & 0xfffu, at1 = (f >> 12) & 63u, dsize = (f >> 18) & 0xfffu;
         bool ok = false;
@@ -1313,14 +1271,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
         const uint32_t dsz = ok && at1 ? dsize : 0u, at = at1 ? at1 - 1u : 0u;
         uint8_t* slot = payload + (size_t)d * stride;
         if constexpr (B == 20) {
-#if RFEC_WIRE_PARSE_PRIO == 1 || RFEC_WIRE_PARSE_PRIO == 4
             __builtin_amdgcn_s_setprio(3);
-#endif
             store_payload20(wb, slot, stride, at, dsz, lane);
             wave_lds_sync(); // the buffer is refilled by the next datagram
-#if RFEC_WIRE_PARSE_PRIO == 1 || RFEC_WIRE_PARSE_PRIO == 2 || RFEC_WIRE_PARSE_PRIO == 4
             __builtin_amdgcn_s_setprio(0);
-#endif
         } else {
             uint32_t pay[ND];
             shift_down_bytes<B>(w, at, pay);
@@ -1349,14 +1303,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
                 in.H[k] = (k == 0 ? 0x1701u : k == 6 ? 0xB004u : 0u) + (dstride >> 16);
             pk = decode_header<B>(in, recs, dl, lane < cnt, dstride, capacity);
 #else
-#if RFEC_WIRE_PARSE_PRIO == 3 || RFEC_WIRE_PARSE_PRIO == 4
             __builtin_amdgcn_s_setprio(3);
-#endif
             load_header(dgram, dlen, dl, lane < cnt, dstride, in);
             pk = decode_header<B>(in, recs, dl, lane < cnt, dstride, capacity);
-#if RFEC_WIRE_PARSE_PRIO == 3 || RFEC_WIRE_PARSE_PRIO == 4
             __builtin_amdgcn_s_setprio(0);
-#endif
 #endif
             i = 0;
         }
