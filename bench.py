@@ -588,7 +588,7 @@ def main():
         rows_layout = not full_plan and len(set(lines[:-1])) <= 1
         enc_kernel = (f"k_encode_out<{k},{lines[0]}>" if rows_layout and (k, lines[0]) in ((10, 4), (32, 4))
                       else ("k_encode_out_rt (run-time k, col)" if rows_layout and lines[0] <= 16
-                            else (f"k_encode_matrix<{k},{w.plan.col}>" if full_plan else "k_encode (plan-driven)")))
+                            else (f"k_encode_matrix_out<{k},{w.plan.col}>" if full_plan else "k_encode (plan-driven)")))
         cd = (S + 15) // 16
         per = ("one lane per (group, output slot, chunk)" if w.dense and 2 <= len(lines)
                else "one lane per (group, line, chunk)")

@@ -71,6 +71,9 @@ static uint8_t seen[1 << 20]; /* packet ids already in the receiver (received or
 
 static FILE* js;
 static int first_case = 1;
+/* the sender closes a group at this many segments (sim_sender.c:370: 100);
+ * a foreign peer's sender may close them later */
+static int g_flush_at = 100;
 
 static void scenario_x(const char* name, uint64_t id, const frame_t* frames, int nf, uint32_t seg_loss_pm,
                        uint32_t fec_loss_pm, uint32_t window, uint32_t dup_pm, uint32_t late_pm, int protect_tail,
@@ -84,8 +87,10 @@ static void scenario_x(const char* name, uint64_t id, const frame_t* frames, int
     /* sender order: segments, each group's parities right after its closing segment */
     static arrival_t order[MAXS + MAXP];
     int no = 0;
-    fprintf(js, "%s  {\"name\": \"%s\", \"id\": %llu, \"frames\": [", first_case ? "" : ",\n", name,
-            (unsigned long long)id);
+    fprintf(js, "%s  {\"name\": \"%s\", \"id\": %llu, ", first_case ? "" : ",\n", name, (unsigned long long)id);
+    if (g_flush_at != 100)
+        fprintf(js, "\"flush_at\": %d, ", g_flush_at);
+    fprintf(js, "\"frames\": [");
     first_case = 0;
     for (int f = 0; f < nf; ++f)
         fprintf(js, "%s[%u, %u, %u, %u]", f ? ", " : "", frames[f].size, frames[f].ftype, frames[f].payload_type,
@@ -124,7 +129,7 @@ static void scenario_x(const char* name, uint64_t id, const frame_t* frames, int
             order[no++] = (arrival_t){0, ns, 0, 0};
             ns++;
             for (int pass = 0; pass < 2; ++pass) {
-                if (pass == 0 ? flex->segs_count < 100 : i + 1 < total)
+                if (pass == 0 ? flex->segs_count < g_flush_at : i + 1 < total)
                     continue;
                 const uint16_t gid = flex->fec_id;
                 const uint32_t base = flex->base_id;
@@ -280,6 +285,15 @@ int main(int argc, char** argv)
     scenario_x("evict_late_segments", 5, fr, 400, 100, 60, 12, 10, 20, 1, 60, 40);
     scenario_x("evict_lost_parities", 6, fr, 400, 80, 550, 8, 10, 0, 1, 20, 97);
     scenario_x("no_evict_late_segments", 5, fr, 400, 100, 60, 12, 10, 20, 1, 60, 0);
+    /* a foreign peer's groups above 128 segments (one group per frame of 130-200
+     * segments): razor's own sender closes groups at 100, the flex receiver
+     * takes any count (flex_fec_receiver.c:69-88) */
+    g_flush_at = 256;
+    for (int i = 0; i < 40; ++i)
+        fr[i] = (frame_t){(130u + (uint32_t)(i * 37 % 71)) * SIM_VIDEO_SIZE - 11u * (uint32_t)i, (uint8_t)(i % 20 == 0),
+                          97, (uint8_t)(i % 5 == 0 ? 30 : 80)};
+    scenario("peer_large_groups", 7, fr, 40, 60, 80, 24, 10, 0, 1);
+    g_flush_at = 100;
     fprintf(js, "\n]}\n");
     fclose(js);
     return 0;

@@ -517,12 +517,31 @@ def _gather_arrivals(arr, items, stride):
     return recs, pay
 
 
+def _peer_groups(segs, listed):
+    """GROUP_PLAN rows for listed [fec_id, base_id, count, protect_fraction]
+    groups over the planned segments (their fec_id / group fields set)."""
+    groups = np.zeros(len(listed), GROUP_PLAN)
+    first = {int(pid): i for i, pid in enumerate(segs["packet_id"])}
+    segs["group"] = -1
+    for gi, (fec_id, base_id, count, pf) in enumerate(listed):
+        f = first[int(base_id)]
+        groups[gi]["first_seg"], groups[gi]["count"], groups[gi]["fec_id"] = f, count, fec_id
+        groups[gi]["base_id"], groups[gi]["protect_fraction"] = base_id, pf
+        segs["fec_id"][f:f + count] = fec_id
+        segs["group"][f:f + count] = gi
+    return groups
+
+
 def rx_stream(oracle, scn, video_size=1000):
     """Parsed-datagram records (WIRE_REC) + payload rows, in the arrival order
     of an rx.json scenario."""
     frames, blob = stage_frames(scn)
     st = oracle.sender_init()
     segs, groups = oracle.sender_plan(st, frames, video_size)
+    if int(scn.get("flush_at", 100)) != 100:
+        # a foreign peer's sender that closes groups later than razor's 100 (gen_rx.c g_flush_at):
+        # the segments are split as razor's, the groups are the scenario's
+        groups = _peer_groups(segs, scn["groups"])
     assert [(int(g["fec_id"]), int(g["base_id"]), int(g["count"]), int(g["protect_fraction"])) for g in groups] == \
         [tuple(g) for g in scn["groups"]]
     items = rx_items(oracle, frames, blob, segs, groups, video_size)
