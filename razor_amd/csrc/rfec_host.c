@@ -1942,8 +1942,8 @@ typedef struct {
     uint32_t shape;        /* UINT32_MAX: geometry the reference ignores or the planner cannot express */
     uint32_t gslot, slot0, line0;
     uint32_t nsegs;        /* flex->segs.n */
-    uint64_t have[2];      /* members in the flex (arrived or recovered) */
-    uint64_t arrived[2];   /* members that arrived: the device peel starts from these */
+    uint64_t have[4];      /* members in the flex (arrived or recovered), count <= RX_MAX_COUNT */
+    uint64_t arrived[4];   /* members that arrived: the device peel starts from these */
     uint64_t ppm;          /* registered parities, by plan line */
     uint32_t fec_ts;       /* flex->fec_ts = send_ts of the parity that created it (sim_fec.c:157) */
     int ref_ok;            /* col >= 2 && row >= 1 && count >= 1 (flex_fec_receiver.c:214, 250) */
@@ -1976,6 +1976,12 @@ typedef struct {
     uint32_t nrh, rhcap;
     uint32_t* dl;          /* instances that deliver in this device call */
     uint32_t ndl, dlcap;
+    rfec_line_job* jobs;   /* groups above RFEC_MAX_K: this call's line jobs (rx_big_peel) */
+    uint32_t njobs, jobcap;
+    uint16_t* jlevel;      /* a job's dependency level (1 = arrived members only) */
+    uint32_t jlevelcap;
+    int32_t* jmem;         /* member codes: record >= 0, job j as -1 - j */
+    uint32_t njmem, jmemcap;
     uint32_t epoch;        /* device call counter (rx_inst.gstamp) */
     int oom;
 } rx_sim;
@@ -2175,9 +2181,14 @@ static int rx_build_plan(uint32_t count, uint32_t row, uint32_t col, const uint6
     return RFEC_OK;
 }
 
+/* flexes of up to 255 segments are modelled (a plan's lines have 8-bit
+ * members); above RFEC_MAX_K the device recovery takes line jobs (rx_big_peel)
+ * instead of the batched peel, whose masks hold 128 members */
+#define RX_MAX_COUNT 255u
+
 static uint32_t rx_shape_of(rx_sim* X, uint32_t count, uint32_t row, uint32_t col, const uint64_t* xcol)
 {
-    if (count > RFEC_MAX_K || row > 255 || col > 255)
+    if (count > RX_MAX_COUNT || row > 255 || col > 255)
         return UINT32_MAX;
     const int extended = xcol[0] || xcol[1];
     const uint32_t key = count << 16 | row << 8 | col;
@@ -2368,6 +2379,9 @@ static void rx_sim_free(rx_sim* X)
     free(X->out);
     free(X->rh);
     free(X->dl);
+    free(X->jobs);
+    free(X->jlevel);
+    free(X->jmem);
 }
 
 static int cmp_u32(const void* a, const void* b)
@@ -2528,6 +2542,98 @@ static void rx_run(rx_sim* X, uint32_t a0, uint32_t n)
     }
 }
 
+/* A group above RFEC_MAX_K segments (a foreign peer's flex): the canonical
+ * peel (lines in plan order to a fixpoint, with flex_fec_recover's header
+ * checks, flex_fec_xor.c:60-99) from its arrived members and registered
+ * parities, over headers on the host; each firing becomes a line job the
+ * device runs (rfec_launch_line_jobs).  job_of[t]: the job recovering member
+ * t, or -1. */
+static void rx_big_peel(rx_sim* X, uint32_t gi, int32_t* job_of)
+{
+    const rx_inst* g = &X->G[gi];
+    const rfec_plan* P = &X->S[g->shape].plan;
+    const uint32_t k = g->count;
+    uint64_t have[4] = {g->arrived[0], g->arrived[1], g->arrived[2], g->arrived[3]};
+    static __thread rfec_hdr hd[RX_MAX_COUNT];
+    static __thread int32_t src[RX_MAX_COUNT];
+    static __thread uint16_t lvl[RX_MAX_COUNT];
+    for (uint32_t i = 0; i < k; ++i) {
+        job_of[i] = -1;
+        lvl[i] = 0;
+        src[i] = X->slot_src[g->slot0 + i];
+        if ((have[i >> 6] >> (i & 63)) & 1ull)
+            hd[i] = X->slot_hdr[g->slot0 + i];
+    }
+    for (int progress = 1; progress && !X->oom;) {
+        progress = 0;
+        for (uint32_t l = 0; l < P->n_lines && !X->oom; ++l) {
+            if (!((g->ppm >> l) & 1ull))
+                continue;
+            const rfec_line* ln = &P->line[l];
+            uint32_t miss = 0, present = 0, t = 0;
+            for (uint32_t q = 0; q < ln->count; ++q) {
+                const uint32_t i = ln->first + q * ln->stride;
+                if ((have[i >> 6] >> (i & 63)) & 1ull) {
+                    present++;
+                } else {
+                    miss++;
+                    t = i;
+                }
+            }
+            if (miss != 1 || present == 0)
+                continue;
+            const rfec_wire_rec* f = &X->R[X->line_par[g->line0 + l]];
+            const uint32_t L = f->data_size;
+            if (L > X->capacity)
+                continue;
+            rfec_hdr h = f->hdr;
+            int ok = 1;
+            uint16_t level = 0;
+            for (uint32_t q = 0; q < ln->count && ok; ++q) {
+                const uint32_t i = ln->first + q * ln->stride;
+                if (i == t)
+                    continue;
+                const rfec_hdr* m = &hd[i];
+                ok = m->size <= L;
+                h.seq ^= m->seq;
+                h.fid ^= m->fid;
+                h.ts ^= m->ts;
+                h.index ^= m->index;
+                h.total ^= m->total;
+                h.ftype ^= m->ftype;
+                h.payload_type ^= m->payload_type;
+                h.size ^= m->size;
+                level = lvl[i] > level ? lvl[i] : level;
+            }
+            if (!ok || h.size > L)
+                continue;
+            RX_GROW(X->jobs, X->njobs, X->jobcap, 1, rfec_line_job);
+            RX_GROW(X->jlevel, X->njobs, X->jlevelcap, 1, uint16_t);
+            RX_GROW(X->jmem, X->njmem, X->jmemcap, present, int32_t);
+            if (X->oom)
+                return;
+            rfec_line_job* J = &X->jobs[X->njobs];
+            J->out = (int32_t)X->njobs;
+            J->parity = X->line_par[g->line0 + l];
+            J->member0 = X->njmem;
+            J->n_members = present;
+            for (uint32_t q = 0; q < ln->count; ++q) {
+                const uint32_t i = ln->first + q * ln->stride;
+                if (i != t)
+                    X->jmem[X->njmem++] = src[i];
+            }
+            X->jlevel[X->njobs] = (uint16_t)(level + 1);
+            job_of[t] = (int32_t)X->njobs;
+            src[t] = -1 - (int32_t)X->njobs;
+            lvl[t] = (uint16_t)(level + 1);
+            hd[t] = h;
+            have[t >> 6] |= 1ull << (t & 63);
+            X->njobs++;
+            progress = 1;
+        }
+    }
+}
+
 /* The device side of one call: the groups that delivered something in this
  * call, rebuilt from their arrived members and registered parities (rows of
  * `rows`, DEVICE, indexed by record), peeled by rfec_recover_batch, and the
@@ -2575,25 +2681,91 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
         sh->row0 = nrows;
         sh->prow0 = prows;
         sh->group0 = ngs;
+        if (sh->count > RFEC_MAX_K) /* line jobs instead (below) */
+            continue;
         nrows += sh->n_groups * sh->count;
         prows += sh->n_groups * sh->n_lines;
         ngs += sh->n_groups;
+    }
+    /* groups above RFEC_MAX_K: the host peel's line jobs, output rows after
+     * the batched peel's rows, launched level by level (jobs sorted by level) */
+    X->njobs = X->njmem = 0;
+    uint32_t nbig = 0, maxlvl = 0;
+    for (uint32_t d = 0; d < X->ndl; ++d)
+        if (X->S[X->G[X->dl[d]].shape].count > RFEC_MAX_K)
+            nbig += X->G[X->dl[d]].count;
+    int32_t* job_of = nbig ? (int32_t*)malloc((size_t)nbig * sizeof(int32_t)) : NULL;
+    uint32_t* jperm = NULL;
+    if (nbig && !job_of)
+        return set_err(RFEC_ENOMEM, "rx: large groups", 0);
+    for (uint32_t d = 0, off = 0; d < X->ndl; ++d) {
+        rx_inst* g = &X->G[X->dl[d]];
+        if (X->S[g->shape].count <= RFEC_MAX_K)
+            continue;
+        g->gslot = off; /* (a large group's slot: its job_of range) */
+        rx_big_peel(X, X->dl[d], job_of + off);
+        off += g->count;
+    }
+    if (X->oom) {
+        free(job_of);
+        return set_err(RFEC_ENOMEM, "rx: line jobs", 0);
+    }
+    uint32_t lvl_n[65] = {0};
+    if (X->njobs) { /* stable sort by level; codes and job_of follow */
+        for (uint32_t j = 0; j < X->njobs; ++j) {
+            if (X->jlevel[j] > 64) { /* deeper than any plan of <= 64 lines cascades */
+                free(job_of);
+                return set_err(RFEC_EINVAL, "rx: line job chain too deep", 0);
+            }
+            maxlvl = X->jlevel[j] > maxlvl ? X->jlevel[j] : maxlvl;
+            lvl_n[X->jlevel[j]]++;
+        }
+        uint32_t start[66] = {0};
+        for (uint32_t v = 1; v <= maxlvl; ++v)
+            start[v + 1] = start[v] + lvl_n[v];
+        jperm = (uint32_t*)malloc((size_t)X->njobs * sizeof(uint32_t));
+        rfec_line_job* sorted = (rfec_line_job*)malloc((size_t)X->njobs * sizeof(rfec_line_job));
+        if (!jperm || !sorted) {
+            free(jperm);
+            free(sorted);
+            free(job_of);
+            return set_err(RFEC_ENOMEM, "rx: line jobs", 0);
+        }
+        for (uint32_t j = 0; j < X->njobs; ++j)
+            jperm[j] = start[X->jlevel[j]]++;
+        for (uint32_t j = 0; j < X->njobs; ++j) {
+            sorted[jperm[j]] = X->jobs[j];
+            sorted[jperm[j]].out = (int32_t)jperm[j];
+        }
+        memcpy(X->jobs, sorted, (size_t)X->njobs * sizeof(rfec_line_job));
+        free(sorted);
+        for (uint32_t m = 0; m < X->njmem; ++m)
+            if (X->jmem[m] < 0)
+                X->jmem[m] = -1 - (int32_t)jperm[-1 - X->jmem[m]];
+        for (uint32_t i = 0; i < nbig; ++i)
+            if (job_of[i] >= 0)
+                job_of[i] = (int32_t)jperm[job_of[i]];
     }
     const size_t o_smap = 0, o_pmap = RX_ALIGN((size_t)nrows * 4), o_hdr = RX_ALIGN(o_pmap + (size_t)prows * 4);
     const size_t o_meta = RX_ALIGN(o_hdr + (size_t)nrows * sizeof(rfec_hdr));
     const size_t o_fs = RX_ALIGN(o_meta + (size_t)prows * sizeof(rfec_hdr));
     const size_t o_pres = RX_ALIGN(o_fs + (size_t)prows * 2), o_pp = RX_ALIGN(o_pres + (size_t)ngs * 16);
-    const size_t o_omap = RX_ALIGN(o_pp + (size_t)ngs * 8), o_in_end = RX_ALIGN(o_omap + (size_t)X->nout * 4);
+    const size_t o_omap = RX_ALIGN(o_pp + (size_t)ngs * 8), o_jobs = RX_ALIGN(o_omap + (size_t)X->nout * 4);
+    const size_t o_jmem = RX_ALIGN(o_jobs + (size_t)X->njobs * sizeof(rfec_line_job));
+    const size_t o_in_end = RX_ALIGN(o_jmem + (size_t)X->njmem * 4);
     const size_t o_rec = o_in_end, host_bytes = RX_ALIGN(o_rec + (size_t)ngs * 16);
     size_t ws_bytes = 0;
     for (uint32_t s = 0; s < X->ns; ++s)
         ws_bytes += RX_ALIGN(rfec_recover_workspace_size(&X->S[s].plan, X->S[s].n_groups));
-    const size_t d_shards = o_in_end, d_par = RX_ALIGN(d_shards + (size_t)nrows * stride);
+    const size_t d_shards = o_in_end, d_par = RX_ALIGN(d_shards + ((size_t)nrows + X->njobs) * stride);
     const size_t d_ws = RX_ALIGN(d_par + (size_t)prows * stride), d_rec = RX_ALIGN(d_ws + ws_bytes);
     const size_t d_out = RX_ALIGN(d_rec + (size_t)ngs * 16), dev_bytes = RX_ALIGN(d_out + (size_t)X->nout * stride);
     const int r_in_stage = (const uint8_t*)X->R == t_rx.h;
-    if ((rc = rx_reserve(hoff + host_bytes, dev_bytes, hoff)))
+    if ((rc = rx_reserve(hoff + host_bytes, dev_bytes, hoff))) {
+        free(job_of);
+        free(jperm);
         return rc;
+    }
     if (r_in_stage)
         X->R = (const rfec_wire_rec*)t_rx.h;
     uint8_t* H = t_rx.h + hoff;
@@ -2606,9 +2778,15 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
     uint64_t* pres = (uint64_t*)(H + o_pres);
     uint64_t* ppm = (uint64_t*)(H + o_pp);
     int32_t* omap = (int32_t*)(H + o_omap);
+    if (X->njobs) {
+        memcpy(H + o_jobs, X->jobs, (size_t)X->njobs * sizeof(rfec_line_job));
+        memcpy(H + o_jmem, X->jmem, (size_t)X->njmem * 4);
+    }
     for (uint32_t d = 0; d < X->ndl; ++d) {
         const rx_inst* g = &X->G[X->dl[d]];
         const rx_shape* sh = &X->S[g->shape];
+        if (sh->count > RFEC_MAX_K)
+            continue;
         const uint32_t gg = sh->group0 + g->gslot, r0 = sh->row0 + g->gslot * sh->count;
         const uint32_t p0 = sh->prow0 + g->gslot * sh->n_lines;
         pres[2 * gg] = g->arrived[0];
@@ -2636,8 +2814,13 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
         const rx_inst* g = &X->G[ev->inst];
         const rx_shape* sh = &X->S[g->shape];
         const uint32_t t = ev->hdr.seq - g->base;
-        omap[q] = t < g->count ? (int32_t)(sh->row0 + g->gslot * sh->count + t) : -1;
+        if (sh->count > RFEC_MAX_K) /* the job that recovers t */
+            omap[q] = t < g->count && job_of[g->gslot + t] >= 0 ? (int32_t)(nrows + (uint32_t)job_of[g->gslot + t]) : -1;
+        else
+            omap[q] = t < g->count ? (int32_t)(sh->row0 + g->gslot * sh->count + t) : -1;
     }
+    free(job_of);
+    free(jperm);
     rep->host_us += now_us() - th;
     rep->n_groups = ngs;
     for (uint32_t s = 0; s < X->ns; ++s)
@@ -2650,10 +2833,13 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
     ke = rfec_launch_gather_rows(D + d_shards, rows, (const int32_t*)(D + o_smap), nrows, stride, sm);
     if (!ke)
         ke = rfec_launch_gather_rows(D + d_par, rows, (const int32_t*)(D + o_pmap), prows, stride, sm);
+    for (uint32_t v = 1, lo = 0; v <= maxlvl && !ke; lo += lvl_n[v], ++v) /* the large groups' line jobs */
+        ke = rfec_launch_line_jobs((const rfec_line_job*)(D + o_jobs) + lo, lvl_n[v], (const int32_t*)(D + o_jmem),
+                                   rows, D + d_shards + (size_t)nrows * stride, stride, sm);
     size_t wso = 0;
     for (uint32_t s = 0; s < X->ns && !ke; ++s) {
         const rx_shape* sh = &X->S[s];
-        if (!sh->n_groups)
+        if (!sh->n_groups || sh->count > RFEC_MAX_K)
             continue;
         rfec_kmask M;
         make_masks(&sh->plan, &M);
@@ -2682,7 +2868,8 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
         const rx_event* ev = &X->out[q];
         const rx_inst* g = &X->G[ev->inst];
         const uint32_t t = ev->hdr.seq - g->base, gg = X->S[g->shape].group0 + g->gslot;
-        if (t >= g->count || !((rec[2 * gg + (t >> 6)] >> (t & 63)) & 1ull)) {
+        const int big = X->S[g->shape].count > RFEC_MAX_K;
+        if (big ? omap[q] < 0 : t >= g->count || !((rec[2 * gg + (t >> 6)] >> (t & 63)) & 1ull)) {
             X->unmodelled++;
             omap[q] = -1;
             continue;

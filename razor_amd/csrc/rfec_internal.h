@@ -68,6 +68,15 @@ int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, c
                            uint32_t max_len, void* stream);
 int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map, uint32_t rows, uint32_t stride,
                             void* stream);
+/* receiver groups above RFEC_MAX_K segments: out row = parity row ^ member rows (one dependency level per call) */
+typedef struct {
+    int32_t out;       /* output row */
+    int32_t parity;    /* row of `rows` holding the line's parity */
+    uint32_t member0;  /* first member code in the member list */
+    uint32_t n_members;
+} rfec_line_job;
+int rfec_launch_line_jobs(const rfec_line_job* jobs, uint32_t n_jobs, const int32_t* members, const uint8_t* rows,
+                          uint8_t* outrows, uint32_t stride, void* stream);
 int rfec_launch_zero_tails(uint32_t slots, uint32_t stride, uint8_t* shards, const rfec_hdr* hdr, void* stream);
 const char* rfec_hip_error_string(int code);
 

@@ -1651,6 +1651,41 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows(v4u* __restrict__ dst, c
     st16(dst + (size_t)r * C + j, v);
 }
 
+// Receiver groups above RFEC_MAX_K segments (a foreign peer's flexes): one
+// line job per recovered segment, recovered = parity ^ the line's present
+// members (flex_fec_xor.c:73-95), the host's peel in dependency levels (one
+// launch per level: a job reads only arrived rows and outputs of earlier
+// levels).  One lane per (job, 16-byte column); member code m >= 0: row m of
+// `rows`, m < 0: output row -1 - m.
+__global__ __launch_bounds__(kBlock) void k_line_jobs(const rfec_line_job* __restrict__ jobs,
+                                                      const int32_t* __restrict__ members,
+                                                      const v4u* __restrict__ rows, v4u* outrows, uint32_t total,
+                                                      uint32_t C, FastDiv divC)
+{
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= total)
+        return;
+    const uint32_t q = fdiv(t, divC);
+    const uint32_t j = t - q * C;
+    const rfec_line_job J = jobs[q];
+    v4u acc = ld16(rows + (size_t)J.parity * C + j);
+    uint32_t i = 0;
+    for (; i + 4 <= J.n_members; i += 4) { // four loads in flight
+        v4u v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int32_t m = members[J.member0 + i + u];
+            v[u] = m >= 0 ? rows[(size_t)m * C + j] : outrows[(size_t)(-1 - m) * C + j];
+        }
+        acc ^= (v[0] ^ v[1]) ^ (v[2] ^ v[3]);
+    }
+    for (; i < J.n_members; ++i) {
+        const int32_t m = members[J.member0 + i];
+        acc ^= m >= 0 ? rows[(size_t)m * C + j] : outrows[(size_t)(-1 - m) * C + j];
+    }
+    outrows[(size_t)J.out * C + j] = acc;
+}
+
 // Zero bytes [data_size, stride) of every slot.
 __global__ __launch_bounds__(kBlock) void k_zero_tails(v4u* shards, const rfec_hdr* __restrict__ hdr,
                                                        uint32_t total, uint32_t C, FastDiv divC)
@@ -2099,6 +2134,18 @@ int rfec_launch_recover_out(const rfec_kmask* M, uint32_t groups, uint32_t strid
     // the fused decodes only read the shards and headers when the output is dense
     return launch_recover(M, groups, stride, capacity, const_cast<uint8_t*>(shards), const_cast<rfec_hdr*>(hdr),
                           present, parity, meta, fsize, parity_present, recovered, ws, stream, flags, out);
+}
+
+int rfec_launch_line_jobs(const rfec_line_job* jobs, uint32_t n_jobs, const int32_t* members, const uint8_t* rows,
+                          uint8_t* outrows, uint32_t stride, void* stream)
+{
+    if (n_jobs == 0)
+        return 0;
+    const uint32_t C = stride / 16, total = n_jobs * C; // n_jobs * C < 2^32: host-bounded
+    RFEC_LAUNCH(k_line_jobs, dim3(blocks_for(total)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), jobs,
+                members, reinterpret_cast<const v4u*>(rows), reinterpret_cast<v4u*>(outrows), total, C,
+                make_fastdiv(C));
+    return (int)hipGetLastError();
 }
 
 int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map, uint32_t rows, uint32_t stride,

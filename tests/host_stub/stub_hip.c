@@ -55,6 +55,22 @@ int rfec_launch_service(rfec_svc_ctl* ctl, const uint8_t* shards, uint8_t* out, 
         (void)stream;
     return (int)hipErrorNotSupported;
 }
+/* the large-group line jobs: copied through, as the gathers (no FEC arithmetic) */
+int rfec_launch_line_jobs(const rfec_line_job* jobs, uint32_t n_jobs, const int32_t* members, const uint8_t* rows,
+                          uint8_t* outrows, uint32_t stride, void* stream)
+{
+    (void)stream;
+    for (uint32_t q = 0; q < n_jobs; ++q) {
+        const rfec_line_job* J = &jobs[q];
+        memcpy(outrows + (size_t)J->out * stride, rows + (size_t)J->parity * stride, stride);
+        for (uint32_t i = 0; i < J->n_members; ++i) { /* every member code must address a valid row */
+            const int32_t m = members[J->member0 + i];
+            const uint8_t* src = m >= 0 ? rows + (size_t)m * stride : outrows + (size_t)(-1 - m) * stride;
+            outrows[(size_t)J->out * stride] ^= src[0];
+        }
+    }
+    return 0;
+}
 hipError_t hipMalloc(void** p, size_t n)
 {
     *p = malloc(n ? n : 1);

@@ -47,7 +47,8 @@ def _sorted(rows):
     return sorted(rows, key=lambda r: r[0])
 
 
-@pytest.mark.parametrize("name", ["k10_loss10", "k10_loss25_dup", "mixed_loss15", "late_parities"])
+@pytest.mark.parametrize("name", ["k10_loss10", "k10_loss25_dup", "mixed_loss15", "late_parities",
+                                  "peer_large_groups"])  # (flexes of 130-200 segments: line jobs)
 def test_rx_reference_fixture(lib, oracle1000, name):
     scn = {s["name"]: s for s in po.rx_fixture()["scenarios"]}[name]
     recs, pay, _, _ = po.rx_stream(oracle1000, scn)
@@ -189,7 +190,7 @@ def _rows(out, outp):
 
 
 @pytest.mark.parametrize("name", ["k10_loss10", "mixed_loss15", "late_parities", "evict_late_segments",
-                                  "evict_lost_parities", "no_evict_late_segments"])
+                                  "evict_lost_parities", "no_evict_late_segments", "peer_large_groups"])
 def test_rx_session_reference_fixture(lib, name):
     """The reference receiver's streams pushed in batches, with sim_fec_evict
     between batches where the scenario's heartbeat ran it: the same recovered
