@@ -165,13 +165,15 @@ __device__ __forceinline__ uint32_t carry_to_end(const uint32_t* T, uint32_t c, 
 }
 
 // DPP controls (GFX9): quad_perm [1,0,3,2], [2,3,0,1]; row_ror 4, 8
-constexpr int kDppQuadSwap1 = 0xB1, kDppQuadSwap2 = 0x4E, kDppRowRor4 = 0x124, kDppRowRor8 = 0x128;
+constexpr int kDppQuadSwap1 = 0xB1, kDppQuadSwap2 = 0x4E, kDppRowRor4 = 0x124, kDppRowRor8 = 0x128,
+              kDppRowRor15 = 0x12F; // row_ror:15: lane i of a 16-lane row reads lane (i + 1) mod 16
 __device__ __forceinline__ uint32_t dpp(uint32_t v, int ctrl)
 {
     switch (ctrl) { // the builtin needs a constant
     case kDppQuadSwap1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppQuadSwap1, 0xF, 0xF, false);
     case kDppQuadSwap2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppQuadSwap2, 0xF, 0xF, false);
     case kDppRowRor4: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppRowRor4, 0xF, 0xF, false);
+    case kDppRowRor15: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppRowRor15, 0xF, 0xF, false);
     default: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppRowRor8, 0xF, 0xF, false);
     }
 }
@@ -1322,6 +1324,366 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
     }
 }
 
+// ---------------------------------------------------------------------------
+// Quarter-wave SIM_SEG framing (slots of at most 1,280 bytes).  A wave frames
+// four consecutive datagrams, 16 lanes each: lane s of group g owns 16-byte
+// chunks c = 16 k + s (k = 0..4) of datagram 4 q + g, so every per-datagram
+// quantity (header layout and size, length, CRC alignment, trailer position)
+// is a per-lane value computed once for four datagrams, the payload moves
+// from its slot to the datagram with one byte funnel per chunk and no LDS
+// staging, and a load or store instruction covers 256 contiguous bytes of
+// each of the four slots.  (The wave-per-datagram kernels above spend most
+// of their ~400 instructions per datagram on wave-uniform scalar work, LDS
+// transposes and cross-lane reductions: DESIGN.md §5.1.)
+//
+// Headers: a per-lane pass builds the 32 header bytes of 64 datagrams at once
+// (the wave's next 16 quads, lane 4 t + g = quad t's datagram g), from which
+// each quad takes its own with ds_bpermute.
+//
+// CRC32 over the datagram's n bytes: lane s's five chunks are folded by
+// Horner's rule over the rows (acc = acc * x^(8 * 256) + raw CRC of the next
+// chunk; slice-by-16 for a chunk, four byte lookups for the multiply), then
+// carried from the end of its row-4 chunk (byte 1,040 + 16 s) to the end of
+// the message: x^(8 (240 - 16 s - D)) with D = 1280 - n = 16 Dq + Dr, as
+// column s + Dq of the nibble tables (columns past 15 hold the negative
+// powers a lane needs when its row-4 chunk lies past the message) and one
+// x^(-8 Dr) correction of the group's XOR-reduced sum (bit tables, two bits
+// per lane).  Row-level DPP reduces the 16 lanes.
+// ---------------------------------------------------------------------------
+constexpr int kQLanes = 16, kQRows = 5, kQChunks = kQLanes * kQRows; // 80 chunks = 1,280 bytes
+constexpr uint32_t kQWindow = 16u * kQChunks;
+constexpr int kQCols = kQLanes + kQChunks; // carry columns s + Dq, Dq <= 80
+
+struct CrcQTables {
+    uint32_t t[16][256];         // slice-by-16, as CrcTables
+    uint32_t m[4][256];          // (byte v at byte position b of a register) * x^(8 * 256)
+    uint32_t nib[8][16][kQCols]; // (nibble v at nibble position i) * x^(8 (240 - 16 j))
+    uint32_t inv[16][32];        // x^(31-i) * x^(-8 r)
+};
+
+constexpr CrcQTables make_crcq_tables()
+{
+    CrcQTables r{};
+    for (uint32_t b = 0; b < 256; ++b) {
+        uint32_t c = b;
+        for (int i = 0; i < 8; ++i)
+            c = mul_x(c);
+        r.t[0][b] = c;
+    }
+    for (int s = 1; s < 16; ++s)
+        for (uint32_t b = 0; b < 256; ++b)
+            r.t[s][b] = (r.t[s - 1][b] >> 8) ^ r.t[0][r.t[s - 1][b] & 0xffu];
+    {
+        uint32_t Y = 0x80000000u; // x^0
+        for (int q = 0; q < 8 * 256; ++q)
+            Y = mul_x(Y);
+        uint32_t bas[32]{}; // x^e * x^2048
+        for (int e = 0; e < 32; ++e) {
+            bas[e] = Y;
+            Y = mul_x(Y);
+        }
+        for (int b = 0; b < 4; ++b)
+            for (uint32_t v = 0; v < 256; ++v) {
+                uint32_t acc = 0;
+                for (int i = 0; i < 8; ++i)
+                    if (v & (1u << i))
+                        acc ^= bas[31 - (8 * b + i)];
+                r.m[b][v] = acc;
+            }
+    }
+    uint32_t Vj = 0x80000000u; // x^(8 (240 - 16 j)), from x^1920 at j = 0 down by x^128 per column
+    for (int q = 0; q < 8 * 240; ++q)
+        Vj = mul_x(Vj);
+    for (int j = 0; j < kQCols; ++j) {
+        uint32_t V = Vj;
+        for (int q = 0; q < 128; ++q)
+            Vj = div_x(Vj);
+        uint32_t basis[32]{};
+        for (int e = 0; e < 32; ++e) {
+            basis[e] = V;
+            V = mul_x(V);
+        }
+        for (int i = 0; i < 8; ++i)
+            for (uint32_t nv = 0; nv < 16; ++nv) {
+                uint32_t acc = 0;
+                for (int k = 0; k < 4; ++k)
+                    if (nv & (1u << k))
+                        acc ^= basis[31 - (4 * i + k)];
+                r.nib[i][nv][j] = acc;
+            }
+    }
+    for (int i = 0; i < 32; ++i) {
+        uint32_t v = 1u << i;
+        for (int q = 0; q < 16; ++q) {
+            r.inv[q][i] = v;
+            for (int b = 0; b < 8; ++b)
+                v = div_x(v);
+        }
+    }
+    return r;
+}
+
+__device__ const CrcQTables kCrcQ = make_crcq_tables();
+constexpr int kQTabDwords = (int)(sizeof(CrcQTables) / 4);
+constexpr int kQM = 16 * 256, kQNib = kQM + 4 * 256, kQInv = kQNib + 8 * 16 * kQCols;
+
+// v * x^(8 * 256): four byte lookups
+__device__ __forceinline__ uint32_t mul_row(const uint32_t* T, uint32_t v)
+{
+    return T[kQM + (v & 0xffu)] ^ T[kQM + 256 + ((v >> 8) & 0xffu)] ^ T[kQM + 512 + ((v >> 16) & 0xffu)] ^
+           T[kQM + 768 + (v >> 24)];
+}
+
+// XOR of v over each 16-lane row (every lane of the row gets its row's XOR)
+__device__ __forceinline__ uint32_t row_xor(uint32_t v)
+{
+    v ^= dpp(v, kDppQuadSwap1);
+    v ^= dpp(v, kDppQuadSwap2);
+    v ^= dpp(v, kDppRowRor4);
+    v ^= dpp(v, kDppRowRor8);
+    return v;
+}
+
+// chunk c's raw CRC r carried by column col of the nibble tables
+__device__ __forceinline__ uint32_t carry_q(const uint32_t* T, uint32_t r, uint32_t col)
+{
+    const uint32_t* nb = T + kQNib + col;
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        x ^= nb[(i * 16 + ((r >> (4 * i)) & 15u)) * kQCols];
+    return x;
+}
+
+// SIM_SEG header of one datagram (sim_proto.inl:83-125), per lane: the
+// header's bytes as 8 LE dwords (zero past hs) and m = valid << 31 | hs << 16
+// | data_size.  The maximal layout (4-byte packet_id and fid, 2-byte index /
+// total) in 16-bit big-endian units, then the narrow fields' units removed
+// from the back (each removal is one select per later unit).
+struct SegHdrQ {
+    uint32_t h[8];
+    uint32_t m;
+};
+
+__device__ __forceinline__ SegHdrQ seg_header_q(const rfec_hdr* __restrict__ hdr,
+                                                const rfec_seg_stamp* __restrict__ stamps, uint32_t d, bool act,
+                                                uint32_t capacity)
+{
+    const uint32_t* hp = reinterpret_cast<const uint32_t*>(hdr + d);
+    const uint32_t* sp = reinterpret_cast<const uint32_t*>(stamps + d);
+    const uint32_t seq = hp[0], fid = hp[1], ts = hp[2], h3 = hp[3], h4 = hp[4];
+    const uint32_t uid = sp[0], s1 = sp[1], s2 = sp[2];
+    const uint32_t idx = h3 & 0xffffu, tot = h3 >> 16, L = h4 >> 16;
+    const bool PW = seq > 65535u, FW = fid > 65535u, TW = tot > 255u;
+    const uint32_t mask = (h4 & 1u) | (PW ? 0x80u : 0u) | (FW ? 0x40u : 0u) | (TW ? 0x20u : 0u) |
+                          (((s2 >> 16) & 0xffu) == 0 ? 0x10u : 0u);
+    uint32_t u[17];
+    u[0] = (RFEC_WIRE_VER << 8) | RFEC_WIRE_SEG;
+    u[1] = uid >> 16;
+    u[2] = uid & 0xffffu;
+    u[3] = (mask << 8) | ((h4 >> 8) & 0xffu);
+    // maximal tail: seq 2, fid 2, ts 2, index, total, fec_id, send_ts, transport_seq, size
+    u[4] = seq >> 16, u[5] = seq & 0xffffu, u[6] = fid >> 16, u[7] = fid & 0xffffu;
+    u[8] = ts >> 16, u[9] = ts & 0xffffu, u[10] = idx, u[11] = tot;
+    u[12] = s1 & 0xffffu, u[13] = s1 >> 16, u[14] = s2 & 0xffffu, u[15] = L, u[16] = 0;
+    // 1-byte index and total: one unit (index low byte, total low byte)
+    u[10] = TW ? u[10] : ((idx & 0xffu) << 8) | (tot & 0xffu);
+#pragma unroll
+    for (int r = 11; r < 16; ++r)
+        u[r] = TW ? u[r] : u[r + 1];
+    // 2-byte fid: drop its high unit
+#pragma unroll
+    for (int r = 6; r < 16; ++r)
+        u[r] = FW ? u[r] : u[r + 1];
+    // 2-byte packet_id
+#pragma unroll
+    for (int r = 4; r < 16; ++r)
+        u[r] = PW ? u[r] : u[r + 1];
+    SegHdrQ H;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) // bytes of unit 2k, then of unit 2k + 1 (big-endian each)
+        H.h[k] = __builtin_amdgcn_perm(u[2 * k + 1], u[2 * k], 0x04050001u);
+    const uint32_t hs = 26u + 2u * ((uint32_t)PW + (uint32_t)FW + (uint32_t)TW);
+    // units past hs / 2 were shifted in from u[16] = 0: the bytes past hs are zero
+    H.m = (act && L <= capacity ? 0x80000000u : 0u) | hs << 16 | L;
+    return H;
+}
+
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane)
+{
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane * 4u), (int)v);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc64(const void* p, uint64_t bytes)
+{
+    return rsrc(p, bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)bytes);
+}
+
+// bytes >= m of a quarter-wave's chunks to zero (rows that some lane's range ends in or before)
+__device__ __forceinline__ void mask_q(uint32_t (&x)[kQRows][4], uint32_t m, uint32_t s)
+{
+#pragma unroll
+    for (int k = 0; k < kQRows; ++k) {
+        const int e = (int)m - (int)(16u * (16u * k + s));
+        if (__builtin_amdgcn_ballot_w64(e < 16) != 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { // keep min(max(e - 4 j, 0), 4) bytes of dword j
+                const uint32_t t8 = 8u * (uint32_t)min(max(e - 4 * j, 0), 4);
+                x[k][j] &= ~(uint32_t)(0xFFFFFFFFull << t8);
+            }
+        }
+    }
+}
+
+// payload windows of a quad's datagram for its five chunk rows: chunk c
+// needs payload bytes [16 c - hs, 16 c - hs + 16), read from the dword below
+// (for c < 2, from payload byte 0: see the row-0 fix-up)
+__device__ __forceinline__ void load_rows_q(__amdgpu_buffer_rsrc_t rin, uint32_t pbase, uint32_t m, uint32_t s,
+                                            v4u (&W)[kQRows])
+{
+    const uint32_t hs = (m >> 16) & 63u, sh = hs & 2u;
+#pragma unroll
+    for (int k = 0; k < kQRows; ++k) {
+        const uint32_t c = 16u * k + s;
+        const uint32_t off = pbase + (c >= 2 ? 16u * c - hs - sh : 0u);
+        W[k] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, kAuxNT));
+    }
+}
+
+// (registers capped for 8 waves per SIMD, two blocks per CU: the LDS tables
+// allow two; 4 waves per SIMD with a software-pipelined next quad took 452 vs
+// 381 us, the same pipeline capped at 64 registers spilled: 680 us)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_frame_seg_q(
+    const uint8_t* __restrict__ shards, const rfec_hdr* __restrict__ hdr, const rfec_seg_stamp* __restrict__ stamps,
+    const uint32_t* __restrict__ order, uint8_t* __restrict__ dgram, uint16_t* __restrict__ dlen, uint32_t count,
+    uint32_t stride, uint32_t capacity, uint32_t dstride)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t T[kQTabDwords];
+    {
+        const v4u* src = reinterpret_cast<const v4u*>(&kCrcQ);
+        v4u* dst = reinterpret_cast<v4u*>(T);
+        for (int i = threadIdx.x; i < kQTabDwords / 4; i += kBlock)
+            dst[i] = src[i];
+        __syncthreads();
+    }
+    const uint32_t lane = threadIdx.x & (kWave - 1), g = lane >> 4, s = lane & 15u;
+    const uint32_t nquads = (count + 3u) / 4u;
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    uint32_t q = wave_id();
+    if (q >= nquads)
+        return;
+    const __amdgpu_buffer_rsrc_t rin = rsrc64(shards, (uint64_t)count * stride);
+    const __amdgpu_buffer_rsrc_t rout = rsrc64(dgram, (uint64_t)count * dstride);
+    // the batch: lane 4 t + g holds quad q + t nw's datagram g
+    SegHdrQ B;
+    auto pass = [&](uint32_t q0) {
+        const uint32_t dd = 4u * (q0 + (lane >> 2) * nw) + (lane & 3u);
+        const bool a = dd < count;
+        B = seg_header_q(hdr, stamps, a ? dd : 0u, a, capacity);
+    };
+    uint32_t bt = 16;
+    for (;;) {
+        if (bt == 16) { // the next 16 quads' headers
+            pass(q);
+            bt = 0;
+        }
+        const uint32_t src = 4u * bt + g;
+        const uint32_t mc = bperm(B.m, src);
+        v4u W[kQRows];
+        load_rows_q(rin, (4u * q + g) * stride, mc, s, W);
+        const uint32_t oc = order ? order[min(4u * q + g, count - 1u)] : 4u * q + g;
+        uint32_t Hd[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            Hd[j] = bperm(B.h[j], src);
+        ++bt;
+        const uint32_t d = 4u * q + g;
+        const bool act = d < count;
+        const uint32_t hs = (mc >> 16) & 63u, L = mc & 0xffffu;
+        const bool valid = (mc >> 31) != 0;
+        const uint32_t n = valid ? hs + L : 0u; // invalid: every byte masked, length 0
+        const uint32_t sh = hs & 2u;             // (16 c - hs) mod 4 for an even hs
+        const uint32_t o = oc;
+        // datagram chunks from the payload windows; a window's fifth dword is
+        // the next chunk's first (lane s + 1's, for s = 15 lane 0's in the next
+        // row; chunk 79's lies past any message)
+        uint32_t out[kQRows][4];
+        {
+            uint32_t nx[kQRows];
+#pragma unroll
+            for (int k = 0; k < kQRows; ++k)
+                nx[k] = dpp(W[k][0], kDppRowRor15);
+#pragma unroll
+            for (int k = 0; k < kQRows; ++k) {
+                uint32_t w[5] = {W[k][0], W[k][1], W[k][2], W[k][3], s == 15 ? (k + 1 < kQRows ? nx[k + 1 < kQRows ? k + 1 : k] : 0u) : nx[k]};
+                if (k == 0) {
+                    // lane 0: header bytes 0-15; lane 1: header bytes 16-31 over
+                    // the payload's first 32 - hs bytes (loaded from payload byte 0,
+                    // they start 3 or 4 dwords into the window)
+                    const bool z3 = hs + sh == 28u;
+                    const uint32_t p0 = w[0], p1 = w[1];
+                    w[0] = s > 1 ? w[0] : 0u;
+                    w[1] = s > 1 ? w[1] : 0u;
+                    w[2] = s > 1 ? w[2] : 0u;
+                    w[3] = s > 1 ? w[3] : (s == 1 && z3 ? p0 : 0u);
+                    w[4] = s > 1 ? w[4] : (s == 1 ? (z3 ? p1 : p0) : 0u);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    out[k][j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            out[0][j] |= s == 0 ? Hd[j] : (s == 1 ? Hd[4 + j] : 0u);
+        mask_q(out, n, s);
+        // CRC32 (Horner over the rows, seed folded into the first dword)
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < kQRows; ++k) {
+            const uint32_t x0 = out[k][0] ^ (k == 0 && s == 0 ? ~RFEC_WIRE_CRC_SEED : 0u);
+            acc = (k ? mul_row(T, acc) : 0u) ^ slice16(T, x0, out[k][1], out[k][2], out[k][3]);
+        }
+        const uint32_t D = kQWindow - n, Dq = D >> 4, Dr = D & 15u;
+        const uint32_t R = row_xor(carry_q(T, acc, s + Dq));
+        const uint32_t* iv = T + kQInv + Dr * 32u;
+        const uint32_t b = (((R >> s) & 1u) ? iv[s] : 0u) ^ (((R >> (s + 16u)) & 1u) ? iv[s + 16u] : 0u);
+        const uint32_t crc = ~row_xor(b);
+        // big-endian trailer at byte n: dwords n / 4 and n / 4 + 1.  (Storing
+        // the rows as they are hashed and holding back the trailer's chunks
+        // took registers the CRC needs: spills, 495 vs 381 us.)
+        if (valid) {
+            const uint32_t be = bswap(crc), s4 = n & 3u, q0 = n >> 2;
+            const uint32_t lo = be << (8 * s4), hi = s4 ? be >> (32 - 8 * s4) : 0u;
+            const int x0 = (int)q0 - (int)(4u * s); // relative to the lane's row-0 chunk
+#pragma unroll
+            for (int k = 0; k < kQRows; ++k) {
+                const int x = x0 - 64 * k;
+                if (__builtin_amdgcn_ballot_w64(x >= -1 && x < 4) == 0)
+                    continue; // (wave-uniform: no lane's trailer in this row)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    out[k][j] |= x == j ? lo : (x == j - 1 ? hi : 0u);
+            }
+        }
+        if (act) {
+            const uint32_t obase = o * dstride;
+#pragma unroll
+            for (int k = 0; k < kQRows; ++k) {
+                const uint32_t c = 16u * k + s;
+                if (16u * c < dstride)
+                    __builtin_amdgcn_raw_buffer_store_b128(v4u{out[k][0], out[k][1], out[k][2], out[k][3]}, rout,
+                                                           obase + 16u * c, 0, kAuxST);
+            }
+            if (s == 0)
+                dlen[o] = (uint16_t)(valid ? n + 4u : 0u);
+        }
+        q += nw;
+        if (q >= nquads)
+            break;
+    }
+}
+
 // Persistent grid: exactly the blocks that are resident at once (occupancy
 // from the kernel's registers / LDS x CUs), so no block waits for a second
 // round; fewer when the batch is small.  TAG: one cache per kernel instance.
@@ -1344,6 +1706,15 @@ uint32_t grid_for(const void* kernel, uint32_t count)
 
 // lane width: 20 bytes while a wave of them covers the slot, else 32
 inline bool narrow(uint32_t dstride) { return dstride <= (uint32_t)(kWave * 20); }
+
+// quarter-wave framing: datagram slots of 16-byte multiples up to 1,280 bytes,
+// dword-aligned payload slots, both arrays addressable by 32-bit buffer offsets
+inline bool quarter_ok(uint32_t count, uint32_t stride, uint32_t dstride)
+{
+    return dstride <= kQWindow && dstride % 16 == 0 && stride % 4 == 0 &&
+           ((uint64_t)count + 4) * stride + kQWindow < 0xFFFFFFF0ull && (uint64_t)count * dstride < 0xFFFFFFF0ull;
+}
+
 
 } // namespace
 
@@ -1369,7 +1740,11 @@ int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacit
                                uint32_t dstride, uint8_t* dgram, uint16_t* dlen, void* stream)
 {
     hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
-    if (narrow(dstride))
+    if (quarter_ok(count, stride, dstride)) {
+        const uint32_t quads = (count + 3u) / 4u;
+        RFEC_LAUNCH(k_frame_seg_q, dim3(grid_for<6>((const void*)k_frame_seg_q, quads)), dim3(kBlock), 0, sm, shards,
+                    hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride);
+    } else if (narrow(dstride))
         RFEC_LAUNCH(k_frame_seg<20>, dim3(grid_for<2>((const void*)k_frame_seg<20>, count)), dim3(kBlock), 0, sm,
                            shards, hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride);
     else

@@ -126,14 +126,16 @@ class GpuWire:
                   None if d_st is None else d_st.data_ptr(), d_s.data_ptr(), dstride, d_g.data_ptr(), d_l.data_ptr())
         return _host(d_g, np.uint8, (N, dstride)), _host(d_l, np.uint16, (N,))
 
-    def frame_seg(self, shards, hdr, stamps, capacity, dstride):
+    def frame_seg(self, shards, hdr, stamps, capacity, dstride, order=None):
         stride = shards.shape[-1]
         N = shards.size // stride
         d_d, d_h, d_s = (_dev(a, self.device) for a in (shards, hdr, stamps))
+        d_o = None if order is None else _dev(np.ascontiguousarray(order, np.uint32), self.device)
         d_g = torch.full((N * dstride,), 0xEE, dtype=torch.uint8, device=self.device)
         d_l = torch.full((N,), 0x7777, dtype=torch.int16, device=self.device)
-        self._run(self.lib.wire_frame_seg, N, stride, capacity, d_d.data_ptr(), d_h.data_ptr(), d_s.data_ptr(),
-                  dstride, d_g.data_ptr(), d_l.data_ptr())
+        fn = lambda *a: self.lib.wire_frame_seg(*a, order=None if d_o is None else d_o.data_ptr())  # noqa: E731
+        self._run(fn, N, stride, capacity, d_d.data_ptr(), d_h.data_ptr(), d_s.data_ptr(), dstride, d_g.data_ptr(),
+                  d_l.data_ptr())
         return _host(d_g, np.uint8, (N, dstride)), _host(d_l, np.uint16, (N,))
 
     def parse(self, dgram, dlen, stride, capacity):

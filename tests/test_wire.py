@@ -142,3 +142,33 @@ def test_wire_random_roundtrip_gpu(gwire, oracle1000, capacity, stride):
         else:
             assert recs["hdr"].tobytes() == hdr.tobytes()
             assert np.array_equal(recs["base_id"], stamps["base_id"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("capacity,stride,dstride", [(1200, 1200, 1248), (1200, 1216, 1264), (1000, 1008, 1280),
+                                                     (1201, 1216, 1248), (1240, 1248, 1280), (230, 240, 272),
+                                                     (1300, 1312, 1344)])
+def test_wire_frame_seg_edges_gpu(gwire, oracle1000, capacity, stride, dstride):
+    """SIM_SEG framing against the oracle where the quarter-wave kernel must
+    mask and place bytes itself: garbage past each segment's data (other
+    bytes of its slot), sizes above capacity (zero datagram, length 0),
+    every header width, an output permutation (`order`), and slot widths
+    on both sides of the quarter-wave path's condition (datagram slots up
+    to 1,280 B; wider ones take the 32-byte lanes)."""
+    rng = np.random.default_rng(capacity * 7 + stride + dstride)
+    N = 4099  # not a multiple of 4: the last quad is partial
+    data, hdr, sizes, stamps = wc.random_batch(rng, N, stride, capacity, seg=True)
+    garbage = rng.integers(0, 256, data.shape, dtype=np.uint8)
+    tail = np.arange(stride)[None, :] >= sizes[:, None]
+    data = np.where(tail, garbage, data)
+    big = rng.random(N) < 0.02
+    hdr["size"][big] = capacity + 1 + rng.integers(0, 50, int(big.sum()))
+    o, ol = oracle1000.frame_seg_batch(data, hdr, stamps, capacity, dstride)
+    assert (ol[big] == 0).all() and not o[big].any()
+    g, gl = gwire.frame_seg(data, hdr, stamps, capacity, dstride)
+    assert np.array_equal(gl, ol)
+    assert np.array_equal(g, o)
+    perm = rng.permutation(N).astype(np.uint32)
+    g2, gl2 = gwire.frame_seg(data, hdr, stamps, capacity, dstride, order=perm)
+    assert np.array_equal(gl2[perm], ol)
+    assert np.array_equal(g2[perm], o)
