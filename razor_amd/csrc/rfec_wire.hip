@@ -1684,6 +1684,164 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
 }
 
+// Quarter-wave SIM_FEC framing, as k_frame_seg_q: the 45-byte header
+// (sim_proto.c:13-18, sim_proto.inl:244-254, 270-283) has one layout, so no
+// header pass: lane i < 13 of a group loads field dword i of its datagram
+// (0-5 rfec_fec_stamp, 6-10 fec_meta, 11 fec_data_size, 12 status), every
+// lane takes the 13 with ds_bpermute, and lanes 0-2 byte-permute them into
+// header dwords 0-11.  The payload starts at byte 45: chunk c >= 3 takes
+// payload bytes [16 (c - 3), 16 (c - 2)) plus the next chunk's first dword
+// shifted by 3 bytes; chunk 2 holds the header's last 13 bytes and payload
+// bytes 0-2.
+__device__ __forceinline__ uint32_t fec_hdr_dword(const uint32_t (&F)[13], int m)
+{
+    // header bytes 4 m .. 4 m + 3 from big-endian fields (v_perm: selector
+    // bytes 0-3 pick from the second operand, 4-7 from the first, 12 = zero)
+    switch (m) {
+    case 0: return __builtin_amdgcn_perm(0u, F[0], 0x02030C0Cu) | (RFEC_WIRE_FEC << 8) | RFEC_WIRE_VER;
+    case 1: return __builtin_amdgcn_perm(F[3], F[0], 0x04050001u);
+    case 2: return __builtin_amdgcn_perm(F[5], F[4], 0x07040302u) & 0x00FFFFFFu | (F[3] >> 24) << 24;
+    case 3: return __builtin_amdgcn_perm(F[1], F[3], 0x05060702u);
+    case 4: return __builtin_amdgcn_perm(F[4], F[1], 0x07040500u) & 0x00FFFFFFu | (F[2] >> 24) << 24;
+    case 5: return __builtin_amdgcn_perm(F[6], F[2], 0x07000102u);
+    case 6: return __builtin_amdgcn_perm(F[7], F[6], 0x07000102u);
+    case 7: return __builtin_amdgcn_perm(F[8], F[7], 0x07000102u);
+    case 8: return __builtin_amdgcn_perm(F[9], F[8], 0x05000102u);
+    case 9: return __builtin_amdgcn_perm(F[10], F[9], 0x04020300u);
+    case 10: return __builtin_amdgcn_perm(F[11], F[10], 0x05020301u);
+    default: return F[11] & 0xffu;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_frame_fec_q(
+    const uint8_t* __restrict__ parity, const rfec_hdr* __restrict__ meta, const uint16_t* __restrict__ fsize,
+    const int8_t* __restrict__ status, const rfec_fec_stamp* __restrict__ stamps, const uint32_t* __restrict__ order,
+    uint8_t* __restrict__ dgram, uint16_t* __restrict__ dlen, uint32_t count, uint32_t stride, uint32_t capacity,
+    uint32_t dstride)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t T[kQTabDwords];
+    {
+        const v4u* src = reinterpret_cast<const v4u*>(&kCrcQ);
+        v4u* dst = reinterpret_cast<v4u*>(T);
+        for (int i = threadIdx.x; i < kQTabDwords / 4; i += kBlock)
+            dst[i] = src[i];
+        __syncthreads();
+    }
+    const uint32_t lane = threadIdx.x & (kWave - 1), g = lane >> 4, s = lane & 15u;
+    const uint32_t nquads = (count + 3u) / 4u;
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    uint32_t q = wave_id();
+    if (q >= nquads)
+        return;
+    const __amdgpu_buffer_rsrc_t rin = rsrc64(parity, (uint64_t)count * stride);
+    const __amdgpu_buffer_rsrc_t rout = rsrc64(dgram, (uint64_t)count * dstride);
+    // field descriptors over the whole arrays: a lane's offset past the end reads 0
+    const __amdgpu_buffer_rsrc_t rst = rsrc64(stamps, (uint64_t)count * sizeof(rfec_fec_stamp));
+    const __amdgpu_buffer_rsrc_t rme = rsrc64(meta, (uint64_t)count * sizeof(rfec_hdr));
+    const __amdgpu_buffer_rsrc_t rfs = rsrc64(fsize, (uint64_t)count * 2u);
+    const __amdgpu_buffer_rsrc_t rsu = rsrc64(status, status ? count : 0u);
+    constexpr uint32_t kOut = 0xFFFFFFF0u;
+    for (;;) {
+        const uint32_t d = 4u * q + g;
+        const bool act = d < count;
+        // payload windows (chunk c >= 3: payload bytes from 16 (c - 3); chunk 2: from 0)
+        v4u W[kQRows];
+        const uint32_t pbase = d * stride;
+#pragma unroll
+        for (int k = 0; k < kQRows; ++k) {
+            const uint32_t c = 16u * k + s;
+            W[k] = __builtin_bit_cast(
+                v4u, __builtin_amdgcn_raw_buffer_load_b128(rin, pbase + (c >= 3 ? 16u * (c - 3) : 0u), 0, kAuxNT));
+        }
+        uint32_t fv = __builtin_amdgcn_raw_buffer_load_b32(rst, s < 6 ? 24u * d + 4u * s : kOut, 0, kAuxNT);
+        fv |= __builtin_amdgcn_raw_buffer_load_b32(rme, s - 6u < 5u ? 20u * d + 4u * (s - 6u) : kOut, 0, kAuxNT);
+        fv |= __builtin_amdgcn_raw_buffer_load_b16(rfs, s == 11 ? 2u * d : kOut, 0, kAuxNT);
+        fv |= (uint32_t)(int32_t)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(rsu, s == 12 ? d : kOut, 0, kAuxNT);
+        const uint32_t o = order ? order[act ? d : 0u] : d;
+        uint32_t F[13];
+#pragma unroll
+        for (int i = 0; i < 13; ++i)
+            F[i] = bperm(fv, 16u * g + i);
+        const uint32_t L = F[11];
+        const bool valid = (int32_t)F[12] >= 0 && L <= capacity;
+        const uint32_t n = valid ? 45u + L : 0u;
+        // header dwords 4 s .. 4 s + 3 for lanes 0-2
+        uint32_t Hd[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t h0 = fec_hdr_dword(F, j), h1 = fec_hdr_dword(F, 4 + j), h2 = fec_hdr_dword(F, 8 + j);
+            Hd[j] = s == 0 ? h0 : (s == 1 ? h1 : (s == 2 ? h2 : 0u));
+        }
+        uint32_t out[kQRows][4];
+        {
+            uint32_t nx[kQRows];
+#pragma unroll
+            for (int k = 0; k < kQRows; ++k)
+                nx[k] = dpp(W[k][0], kDppRowRor15);
+#pragma unroll
+            for (int k = 0; k < kQRows; ++k) {
+                uint32_t w[5] = {W[k][0], W[k][1], W[k][2], W[k][3],
+                                 s == 15 ? (k + 1 < kQRows ? nx[k + 1 < kQRows ? k + 1 : k] : 0u) : nx[k]};
+                if (k == 0) { // lanes 0-1: header only; lane 2: payload bytes 0-2 at its end
+                    const uint32_t p0 = w[0];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        w[j] = s > 2 ? w[j] : 0u;
+                    w[4] = s > 2 ? w[4] : (s == 2 ? p0 : 0u);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    out[k][j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], 3);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            out[0][j] |= Hd[j];
+        mask_q(out, n, s);
+        // CRC32 (Horner over the rows, seed folded into the first dword)
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < kQRows; ++k) {
+            const uint32_t x0 = out[k][0] ^ (k == 0 && s == 0 ? ~RFEC_WIRE_CRC_SEED : 0u);
+            acc = (k ? mul_row(T, acc) : 0u) ^ slice16(T, x0, out[k][1], out[k][2], out[k][3]);
+        }
+        const uint32_t D = kQWindow - n, Dq = D >> 4, Dr = D & 15u;
+        const uint32_t R = row_xor(carry_q(T, acc, s + Dq));
+        const uint32_t* iv = T + kQInv + Dr * 32u;
+        const uint32_t b = (((R >> s) & 1u) ? iv[s] : 0u) ^ (((R >> (s + 16u)) & 1u) ? iv[s + 16u] : 0u);
+        const uint32_t crc = ~row_xor(b);
+        if (valid) { // big-endian trailer at byte n
+            const uint32_t be = bswap(crc), s4 = n & 3u, q0 = n >> 2;
+            const uint32_t lo = be << (8 * s4), hi = s4 ? be >> (32 - 8 * s4) : 0u;
+            const int x0 = (int)q0 - (int)(4u * s);
+#pragma unroll
+            for (int k = 0; k < kQRows; ++k) {
+                const int x = x0 - 64 * k;
+                if (__builtin_amdgcn_ballot_w64(x >= -1 && x < 4) == 0)
+                    continue;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    out[k][j] |= x == j ? lo : (x == j - 1 ? hi : 0u);
+            }
+        }
+        if (act) {
+            const uint32_t obase = o * dstride;
+#pragma unroll
+            for (int k = 0; k < kQRows; ++k) {
+                const uint32_t c = 16u * k + s;
+                if (16u * c < dstride)
+                    __builtin_amdgcn_raw_buffer_store_b128(v4u{out[k][0], out[k][1], out[k][2], out[k][3]}, rout,
+                                                           obase + 16u * c, 0, kAuxST);
+            }
+            if (s == 0)
+                dlen[o] = (uint16_t)(valid ? n + 4u : 0u);
+        }
+        q += nw;
+        if (q >= nquads)
+            break;
+    }
+}
+
 // Persistent grid: exactly the blocks that are resident at once (occupancy
 // from the kernel's registers / LDS x CUs), so no block waits for a second
 // round; fewer when the batch is small.  TAG: one cache per kernel instance.
@@ -1726,7 +1884,11 @@ int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacit
                                uint8_t* dgram, uint16_t* dlen, void* stream)
 {
     hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
-    if (narrow(dstride))
+    if (quarter_ok(count, stride, dstride)) {
+        const uint32_t quads = (count + 3u) / 4u;
+        RFEC_LAUNCH(k_frame_fec_q, dim3(grid_for<7>((const void*)k_frame_fec_q, quads)), dim3(kBlock), 0, sm, parity,
+                    meta, fec_size, status, stamps, order, dgram, dlen, count, stride, capacity, dstride);
+    } else if (narrow(dstride))
         RFEC_LAUNCH(k_frame_fec<20>, dim3(grid_for<0>((const void*)k_frame_fec<20>, count)), dim3(kBlock), 0, sm,
                            parity, meta, fec_size, status, stamps, order, dgram, dlen, count, stride, capacity, dstride);
     else
