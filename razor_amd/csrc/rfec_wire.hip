@@ -338,16 +338,6 @@ __device__ __forceinline__ uint32_t len_mask(int k, uint32_t lane, uint32_t nb)
     return lane < lq ? ~0u : (lane == lq ? ck : 0u);
 }
 
-// a lane's B bytes to [B lane, B lane + B) of a slot of slot_bytes: 16-byte
-// stores plus a dword, range-checked by the buffer descriptor (nothing lands
-// past the slot)
-// A 20-byte-lane message stored as 16-byte lanes: the lanes' dwords go through
-// this wave's LDS buffer wb (320 dwords; dword 5j + k from lane j: banks 5j + k
-// mod 32, distinct over a 32-lane group) and come back as 16-byte chunks, so
-// each global store is 1 KiB (then 256 B) of consecutive 16-byte-aligned
-// bytes.  The direct form stores 16 + 4 bytes per lane at a 20-byte stride:
-// misaligned vectors that cost the frame kernels ~140 of their ~460 us
-// (tools/wire_lab.sh, DIAG_NO_STORE).
 __device__ __forceinline__ void wave_lds_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -355,10 +345,14 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// a lane's B bytes (B = 32) to [B lane, B lane + B) of a slot of slot_bytes:
+// 16-byte stores range-checked by the buffer descriptor (nothing lands past
+// the slot)
 template <int B>
 __device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t slot_bytes, uint32_t lane,
-                                           const uint32_t* w, uint32_t* wb = nullptr)
+                                           const uint32_t* w)
 {
+    static_assert(B % 16 == 0, "whole 16-byte stores");
 #if defined(RFEC_WIRE_DIAG_NO_STORE)
     uint32_t x = 0;
 #pragma unroll
@@ -368,30 +362,10 @@ __device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t 
         slot[0] = (uint8_t)x;
     return;
 #endif
-    if constexpr (B == 20) {
-        if (wb) {
-            typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-            const __amdgpu_buffer_rsrc_t r = rsrc(slot, slot_bytes);
-#pragma unroll
-            for (int k = 0; k < 5; ++k)
-                wb[5 * lane + k] = w[k];
-            wave_lds_sync();
-            const v4u a = *reinterpret_cast<const v4u*>(wb + 4 * lane);
-            const v4u c = *reinterpret_cast<const v4u*>(wb + 256 + 4 * (lane & 15u));
-            wave_lds_sync(); // the buffer is refilled by the next message
-            __builtin_amdgcn_raw_buffer_store_b128(u4{a[0], a[1], a[2], a[3]}, r, 16 * lane, 0, kAuxST);
-            if (lane < 16)
-                __builtin_amdgcn_raw_buffer_store_b128(u4{c[0], c[1], c[2], c[3]}, r, 1024 + 16 * lane, 0, kAuxST);
-            return;
-        }
-    }
     const __amdgpu_buffer_rsrc_t r = rsrc(slot, slot_bytes);
-    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int k = 0; k + 4 <= B / 4; k += 4)
-        __builtin_amdgcn_raw_buffer_store_b128(u4{w[k], w[k + 1], w[k + 2], w[k + 3]}, r, B * lane + 4 * k, 0, kAuxST);
-    if constexpr ((B / 4) % 4 == 1)
-        __builtin_amdgcn_raw_buffer_store_b32(w[B / 4 - 1], r, B * lane + B - 4, 0, kAuxST);
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{w[k], w[k + 1], w[k + 2], w[k + 3]}, r, B * lane + 4 * k, 0, kAuxST);
 }
 
 // Header bytes at compile-time positions (big-endian fields, cf_stream.c:366-385)
@@ -413,7 +387,7 @@ __device__ __forceinline__ void put(Hdr& b, uint32_t v)
 template <int B>
 __device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, uint32_t n, const uint32_t* pay,
                                              uint32_t lane, uint8_t* __restrict__ slot, uint32_t dstride,
-                                             uint16_t* dlen_out, uint32_t* wb)
+                                             uint16_t* dlen_out)
 {
     __builtin_amdgcn_s_setprio(3);
     constexpr int ND = B / 4;
@@ -441,7 +415,7 @@ __device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, ui
         if ((uint32_t)k == k1)
             w[k] |= lane == l1 ? hi : 0u;
     }
-    store_slot<B>(slot, dstride, lane, w, wb);
+    store_slot<B>(slot, dstride, lane, w);
     if (lane == 0)
         *dlen_out = (uint16_t)(n + 4);
     __builtin_amdgcn_s_setprio(0);
@@ -449,10 +423,10 @@ __device__ __forceinline__ void finish_frame(const uint32_t* T, const Hdr& H, ui
 
 template <int B>
 __device__ __forceinline__ void zero_slot(uint8_t* __restrict__ slot, uint32_t dstride, uint32_t lane,
-                                          uint16_t* dlen_out, uint32_t* wb)
+                                          uint16_t* dlen_out)
 {
     const uint32_t z[B / 4] = {};
-    store_slot<B>(slot, dstride, lane, z, wb);
+    store_slot<B>(slot, dstride, lane, z);
     if (lane == 0)
         *dlen_out = 0;
 }
@@ -564,11 +538,9 @@ struct Sel<false, A, B_> {
     using T = B_;
 };
 
-// 20-byte lanes, staged: the slot's first 1,280 bytes as aligned 16-byte
-// chunks (chunk j in lane j, chunk 64 + j in lane j < 16), coalesced 1 KiB
-// loads; stage_window() turns them into the lanes' windows through this
-// wave's LDS buffer (the direct window loads are 16 + 12-byte vectors at a
-// 20-byte stride: misaligned).
+// 20-byte lanes (the parse), staged: the slot's first 1,280 bytes as aligned
+// 16-byte chunks (chunk j in lane j, chunk 64 + j in lane j < 16), coalesced
+// 1 KiB loads, then through the wave's LDS buffer.
 struct Chunks {
     v4u c0, c1;
 };
@@ -578,27 +550,6 @@ __device__ __forceinline__ void load_chunks(const uint8_t* base, uint32_t bytes,
     const __amdgpu_buffer_rsrc_t r = rsrc(base, bytes);
     ch.c0 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * lane, 0, kAuxNT));
     ch.c1 = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, 1024u + 16u * (lane & 15u), 0, kAuxNT));
-}
-
-// x[k] = dword k of the window at slot byte 20 lane - SRC (SRC a multiple of
-// 16; bytes before the slot and past the loaded range read 0).  LDS: bytes
-// [0, SRC) zero, then the 1,280 staged bytes; the reads, dword 5 lane + k,
-// hit 32 distinct banks per 32-lane group.
-template <int SRC, int NX>
-__device__ __forceinline__ void stage_window(const Chunks& ch, uint32_t lane, uint32_t* wb, uint32_t (&x)[NX])
-{
-    static_assert(SRC % 16 == 0 && 5 * 63 + NX <= SRC / 4 + 320, "window past the staged bytes");
-    v4u* w4 = reinterpret_cast<v4u*>(wb);
-    w4[SRC / 16 + lane] = ch.c0;
-    if (lane < 16)
-        w4[SRC / 16 + 64 + lane] = ch.c1;
-    if (lane < SRC / 16)
-        w4[lane] = v4u{0, 0, 0, 0};
-    wave_lds_sync();
-#pragma unroll
-    for (int k = 0; k < NX; ++k)
-        x[k] = wb[5 * lane + k];
-    wave_lds_sync(); // the buffer is reused by the store
 }
 
 constexpr int kWaveBuf = 336; // dwords per wave: 48 + 1,280 bytes staged, or 1,280 stored
@@ -646,9 +597,8 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
                                                       uint32_t dstride)
 {
     constexpr int ND = B / 4;
+    static_assert(B == 32, "slots up to 1,280 bytes take k_frame_fec_q");
     __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords<B>];
-    __shared__ __attribute__((aligned(16))) uint32_t WB[kWavesPerBlock][B == 20 ? kWaveBuf : 4]; // staging
-    uint32_t* wb = B == 20 ? WB[threadIdx.x >> 6] : nullptr;
     load_tables<B>(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
@@ -657,14 +607,11 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
     uint32_t d = wave_id();
     if (d >= count)
         return;
-    using PW = Pre<typename Sel<B == 20, Chunks, Win<ND + 1>>::T>;
+    using PW = Pre<Win<ND + 1>>;
     RFEC_WIRE_PIPE<PW>(d, count, nw,
                               [&](uint32_t dd, PW& P) {
                                   P.f = load_fec_fields(stamps, meta, fsize, status, dd, lane);
-                                  if constexpr (B == 20)
-                                      load_chunks(parity + (size_t)dd * stride, range, lane, P.w);
-                                  else
-                                      load_window<ND + 1>(parity + (size_t)dd * stride, range, off, P.w);
+                                  load_window<ND + 1>(parity + (size_t)dd * stride, range, off, P.w);
                               },
                               [&](const PW& P, uint32_t d) {
             const uint32_t o = order ? order[d] : d; // output slot
@@ -672,7 +619,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
             const uint32_t L = fld(P.f, 11);
             const int st = (int)fld(P.f, 12);
             if (st < 0 || L > capacity) {
-                zero_slot<B>(slot, dstride, lane, dlen + o, wb);
+                zero_slot<B>(slot, dstride, lane, dlen + o);
             } else {
                 const uint32_t s3 = fld(P.f, 3), s4 = fld(P.f, 4), s5 = fld(P.f, 5);
                 const uint32_t m3 = fld(P.f, 9), m4 = fld(P.f, 10);
@@ -698,12 +645,9 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
                 put<41, 2>(H, m4 >> 16);
                 put<43, 2>(H, L); // mach_data_write length (cf_stream.c:328-337)
                 uint32_t pay[ND], x[ND + 1];
-                if constexpr (B == 20)
-                    stage_window<48, ND + 1>(P.w, lane, wb, x);
-                else
-                    win_dwords<B, 48>(P.w, lane, x);
+                win_dwords<B, 48>(P.w, lane, x);
                 funnel<ND, 3>(x, pay); // window [B j - 48, ...) -> bytes [B j - 45, ...)
-                finish_frame<B>(T, H, 45 + L, pay, lane, slot, dstride, dlen + o, wb);
+                finish_frame<B>(T, H, 45 + L, pay, lane, slot, dstride, dlen + o);
             }
                               });
 }
@@ -751,9 +695,8 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                                                       uint32_t dstride)
 {
     constexpr int ND = B / 4;
+    static_assert(B == 32, "slots up to 1,280 bytes take k_frame_seg_q");
     __shared__ __attribute__((aligned(16))) uint32_t T[kTabDwords<B>];
-    __shared__ __attribute__((aligned(16))) uint32_t WB[kWavesPerBlock][B == 20 ? kWaveBuf : 4]; // staging
-    uint32_t* wb = B == 20 ? WB[threadIdx.x >> 6] : nullptr;
     load_tables<B>(T);
     const uint32_t lane = threadIdx.x & (kWave - 1);
     const uint32_t nw = gridDim.x * kWavesPerBlock;
@@ -762,14 +705,11 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
     uint32_t d = wave_id();
     if (d >= count)
         return;
-    using PW = Pre<typename Sel<B == 20, Chunks, Win<ND + 2>>::T>;
+    using PW = Pre<Win<ND + 2>>;
     RFEC_WIRE_PIPE<PW>(d, count, nw,
                               [&](uint32_t dd, PW& P) {
                                   P.f = load_seg_fields(hdr, stamps, dd, lane);
-                                  if constexpr (B == 20)
-                                      load_chunks(shards + (size_t)dd * stride, range, lane, P.w);
-                                  else
-                                      load_window<ND + 2>(shards + (size_t)dd * stride, range, off, P.w);
+                                  load_window<ND + 2>(shards + (size_t)dd * stride, range, off, P.w);
                               },
                               [&](const PW& P, uint32_t d) {
             RFEC_DIAG_LOAD_ONLY(diag_fold(P.w) ^ P.f, dgram)
@@ -789,7 +729,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
             }
             const uint32_t L = h.size;
             if (L > capacity) {
-                zero_slot<B>(slot, dstride, lane, dlen + o, wb);
+                zero_slot<B>(slot, dstride, lane, dlen + o);
             } else {
                 rfec_seg_stamp s;
                 {
@@ -805,10 +745,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                 const uint32_t layout = (h.seq > 65535u ? 4u : 0u) | (h.fid > 65535u ? 2u : 0u) |
                                         (h.total > 255u ? 1u : 0u);
                 uint32_t hs, pay[ND], x[ND + 2];
-                if constexpr (B == 20)
-                    stage_window<32, ND + 2>(P.w, lane, wb, x);
-                else
-                    win_dwords<B, 32>(P.w, lane, x);
+                win_dwords<B, 32>(P.w, lane, x);
                 // window [B j - 32, ...) shifted by 32 - hs bytes
 #if defined(RFEC_WIRE_DIAG_NO_HDR) // lab: header bytes left zero, one layout
                 hs = 26, H.h[0] = layout ^ s.uid;
@@ -825,7 +762,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                 case 6: hs = seg_header<true, true, false>(H, h, s); funnel<ND, 2>(x, pay); break;
                 default: hs = seg_header<true, true, true>(H, h, s); funnel<ND, 0>(x, pay); break;
                 }
-                finish_frame<B>(T, H, hs + L, pay, lane, slot, dstride, dlen + o, wb);
+                finish_frame<B>(T, H, hs + L, pay, lane, slot, dstride, dlen + o);
             }
                               });
 }
@@ -1700,9 +1637,9 @@ __device__ __forceinline__ uint32_t fec_hdr_dword(const uint32_t (&F)[13], int m
     switch (m) {
     case 0: return __builtin_amdgcn_perm(0u, F[0], 0x02030C0Cu) | (RFEC_WIRE_FEC << 8) | RFEC_WIRE_VER;
     case 1: return __builtin_amdgcn_perm(F[3], F[0], 0x04050001u);
-    case 2: return __builtin_amdgcn_perm(F[5], F[4], 0x07040302u) & 0x00FFFFFFu | (F[3] >> 24) << 24;
+    case 2: return (__builtin_amdgcn_perm(F[5], F[4], 0x07040302u) & 0x00FFFFFFu) | (F[3] >> 24) << 24;
     case 3: return __builtin_amdgcn_perm(F[1], F[3], 0x05060702u);
-    case 4: return __builtin_amdgcn_perm(F[4], F[1], 0x07040500u) & 0x00FFFFFFu | (F[2] >> 24) << 24;
+    case 4: return (__builtin_amdgcn_perm(F[4], F[1], 0x07040500u) & 0x00FFFFFFu) | (F[2] >> 24) << 24;
     case 5: return __builtin_amdgcn_perm(F[6], F[2], 0x07000102u);
     case 6: return __builtin_amdgcn_perm(F[7], F[6], 0x07000102u);
     case 7: return __builtin_amdgcn_perm(F[8], F[7], 0x07000102u);
@@ -1888,10 +1825,7 @@ int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacit
         const uint32_t quads = (count + 3u) / 4u;
         RFEC_LAUNCH(k_frame_fec_q, dim3(grid_for<7>((const void*)k_frame_fec_q, quads)), dim3(kBlock), 0, sm, parity,
                     meta, fec_size, status, stamps, order, dgram, dlen, count, stride, capacity, dstride);
-    } else if (narrow(dstride))
-        RFEC_LAUNCH(k_frame_fec<20>, dim3(grid_for<0>((const void*)k_frame_fec<20>, count)), dim3(kBlock), 0, sm,
-                           parity, meta, fec_size, status, stamps, order, dgram, dlen, count, stride, capacity, dstride);
-    else
+    } else // slots above 1,280 bytes (or a batch past 32-bit buffer offsets): 32-byte lanes
         RFEC_LAUNCH(k_frame_fec<32>, dim3(grid_for<1>((const void*)k_frame_fec<32>, count)), dim3(kBlock), 0, sm,
                            parity, meta, fec_size, status, stamps, order, dgram, dlen, count, stride, capacity, dstride);
     return (int)hipGetLastError();
@@ -1906,10 +1840,7 @@ int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacit
         const uint32_t quads = (count + 3u) / 4u;
         RFEC_LAUNCH(k_frame_seg_q, dim3(grid_for<6>((const void*)k_frame_seg_q, quads)), dim3(kBlock), 0, sm, shards,
                     hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride);
-    } else if (narrow(dstride))
-        RFEC_LAUNCH(k_frame_seg<20>, dim3(grid_for<2>((const void*)k_frame_seg<20>, count)), dim3(kBlock), 0, sm,
-                           shards, hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride);
-    else
+    } else // slots above 1,280 bytes (or a batch past 32-bit buffer offsets): 32-byte lanes
         RFEC_LAUNCH(k_frame_seg<32>, dim3(grid_for<3>((const void*)k_frame_seg<32>, count)), dim3(kBlock), 0, sm,
                            shards, hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride);
     return (int)hipGetLastError();
