@@ -172,3 +172,27 @@ def test_wire_frame_seg_edges_gpu(gwire, oracle1000, capacity, stride, dstride):
     g2, gl2 = gwire.frame_seg(data, hdr, stamps, capacity, dstride, order=perm)
     assert np.array_equal(gl2[perm], ol)
     assert np.array_equal(g2[perm], o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("capacity,stride,dstride", [(1200, 1200, 1264), (1200, 1216, 1280), (1000, 1008, 1056),
+                                                     (230, 240, 288), (1300, 1312, 1360)])
+def test_wire_frame_fec_edges_gpu(gwire, oracle1000, capacity, stride, dstride):
+    """SIM_FEC framing against the oracle with garbage past each line's
+    fec_data_size, status -1 and oversize lines (zero datagram, length 0),
+    random stamps and meta, a partial last quad and an output permutation,
+    on both sides of the quarter-wave path's slot limit (1,280 B)."""
+    rng = np.random.default_rng(capacity * 5 + stride + dstride)
+    N = 4097
+    data, meta, sizes, stamps = wc.random_batch(rng, N, stride, capacity, seg=False)
+    garbage = rng.integers(0, 256, data.shape, dtype=np.uint8)
+    data = np.where(np.arange(stride)[None, :] >= sizes[:, None], garbage, data)
+    sizes = sizes.astype(np.uint16)
+    big = rng.random(N) < 0.02
+    sizes[big] = capacity + 1 + rng.integers(0, 40, int(big.sum()))
+    status = np.where(rng.random(N) < 0.05, -1, 0).astype(np.int8)
+    o, ol = oracle1000.frame_fec_batch(data, meta, sizes, status, stamps, capacity, dstride)
+    assert (ol[big | (status < 0)] == 0).all()
+    g, gl = gwire.frame_fec(data, meta, sizes, status, stamps, capacity, dstride)
+    assert np.array_equal(gl, ol)
+    assert np.array_equal(g, o)
