@@ -9,10 +9,13 @@
 //                 yield 0 without advancing (cf_stream.c mach_*_read)
 //   crc32         cf_crc32.c:56-68, seed 0x0e3dfc0a (sim_proto.c:11)
 //
-// One wavefront per datagram; lane j owns bytes [B j, B j + B) of it, B = 20
-// when the slot holds at most 1,280 bytes (a 1,249-byte SIM_FEC or 1,236-byte
-// SIM_SEG at 1,200-byte payloads then keeps 63 of 64 lanes busy), else B = 32
-// (slots up to 2 KiB).  Every lane load / store is a dword buffer access at a
+// Framing into datagram slots of at most 1,280 bytes: the quarter-wave
+// kernels at the end of this file (k_frame_seg_q, k_frame_fec_q: 16 lanes per
+// datagram, four datagrams per wave).  The parse, and framing into wider
+// slots: one wavefront per datagram; lane j owns bytes [B j, B j + B) of it,
+// B = 20 when the slot holds at most 1,280 bytes (a 1,249-byte SIM_FEC or
+// 1,236-byte SIM_SEG at 1,200-byte payloads then keeps 63 of 64 lanes busy),
+// else B = 32 (slots up to 2 KiB).  Every lane load / store is a dword buffer access at a
 // dword-aligned offset, range-checked per dword against its slot.  Payload
 // bytes move through registers with a wave-uniform byte funnel (no LDS
 // staging); the header is assembled with compile-time byte positions.  CRC32
