@@ -593,9 +593,9 @@ def main():
         per = ("one lane per (group, output slot, chunk)" if w.dense and 2 <= len(lines)
                else "one lane per (group, line, chunk)")
         if full_plan:
-            dec_kernels = ("k_decode_cascade (one launch; one lane per (group, " +
-                           ("output slot" if w.dense else "schedule step") + ", chunk), schedule and header checks "
-                           "per lane)")
+            dec_kernels = ("k_decode_cascade_dense (one launch: checker blocks spread over the payload lanes, one "
+                           "lane per (group, output slot, chunk))" if w.dense else
+                           "k_cascade_check + k_decode_cascade (one lane per (group, schedule step, chunk))")
         elif cd >= 64 and rows_layout and (k, lines[0]) in ((10, 4), (32, 4)):
             dec_kernels = f"k_decode_rows<{k},{lines[0]}> ({per}; header blocks spread)"
         elif cd >= 64:

@@ -201,6 +201,8 @@ int rfec_recover_batch(const rfec_plan* plan, uint32_t groups, uint32_t stride, 
  *   out_hdr    [g*per_group + e]           its recovered header record
  *   out_index  [g*per_group + e]           its segment index, or 0xFF where
  *                                          that erased segment was not recovered
+ *                                          (its out_shards slot then holds
+ *                                          unspecified bytes)
  * and `recovered` gets its bit as in rfec_recover_batch.  Any plan: where
  * lines cascade (rows + columns), a recovered segment feeds the lines after
  * it as in place.  Only erased segments of rank < per_group are recovered

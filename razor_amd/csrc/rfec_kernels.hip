@@ -993,7 +993,7 @@ __device__ __forceinline__ CSched cs_unpack(const v4u r)
 // schedule packed.  A group of more than LPG steps (more than LPG erasures
 // recovered) takes the serial exact peel.  Dead lanes (live false) join the
 // shuffles only.
-template <typename MT, int LPG>
+template <typename MT, int LPG, bool kTasks = true>
 __device__ v4u cascade_check_lanes(const CascArgs& A, const rfec_kmask& M, uint32_t g, bool live, uint32_t s,
                                    uint32_t base)
 {
@@ -1084,7 +1084,7 @@ __device__ v4u cascade_check_lanes(const CascArgs& A, const rfec_kmask& M, uint3
         A.recovered[2 * g] = rm;
         A.recovered[2 * g + 1] = 0;
         // the slots' tasks (and out_index: the e-th erased segment's index where it was recovered)
-        uint32_t* task = reinterpret_cast<uint32_t*>(A.ws + (size_t)g * A.ws_stride + 16);
+        uint32_t* task = kTasks ? reinterpret_cast<uint32_t*>(A.ws + (size_t)g * A.ws_stride + 16) : nullptr;
         uint64_t m = (uint64_t)erased;
         for (uint32_t q = 0; q < A.Q; ++q) {
             uint32_t ss = 8;
@@ -1105,7 +1105,8 @@ __device__ v4u cascade_check_lanes(const CascArgs& A, const rfec_kmask& M, uint3
                 const bool casc = (M.mask[tl][0] & (uint64_t)erased & ~(1ull << tt)) != 0;
                 w = kTaskValid | (casc ? kTaskCascade : 0u) | tl | (tt << 8);
             }
-            task[q] = w;
+            if (kTasks)
+                task[q] = w;
         }
     }
     return cs_pack(X);
@@ -1190,6 +1191,113 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     for (int s = 0; s < 8; ++s)
         if ((uint32_t)s < S.n && cs_tg(S, s) == tgt)
             ss = s;
+    uint32_t need = 1u << ss;
+#pragma unroll 1
+    for (int s = (int)ss; s >= 0; --s) {
+        if (!((need >> s) & 1u))
+            continue;
+        const uint64_t dm = lmask[cs_line(S, s)] & erased & ~(1ull << cs_tg(S, s));
+        for (int s2 = 0; s2 < s; ++s2)
+            if ((dm >> cs_tg(S, s2)) & 1ull)
+                need |= 1u << s2;
+    }
+    st16(dst, cascade_replay(S, need, ss, erased, grp, par, slot0, A.E, C, lplan));
+}
+
+// Dense output, one launch: rounds of 8 checker blocks spread over the grid
+// (header_block_xcd; they write the headers, recovered masks and out_index, no
+// task words) between the payload lanes' rounds, which need nothing from them: lane
+// (group, slot q, chunk column) recovers the group's q-th erased segment
+// through a line that fires at once for it (parity received, every other
+// member present) or, when none does, replays the group's mask schedule
+// (cascade_schedule without the header checks).  Any line that recovers a
+// segment gives its bytes, so the data equal the exact peel's wherever it
+// recovers; a segment it leaves unrecovered (a rejected line) may still be
+// written, its out_index 0xFF.  The checker's latency-bound work overlaps the
+// payload traffic instead of preceding it: c3 full 129.4-130.3 vs 131.5-131.8
+// us for check + k_decode_cascade (A/B on one box; the checker's blocks all at
+// the head of the grid: 134.6 us; the line search through LDS copies of the
+// masks instead of the kernel arguments: 131 us).  The payload lanes wait on
+// the masks (HBM) where k_decode_cascade waited on its task word (L2).
+__device__ __forceinline__ bool header_block_xcd(uint32_t n_hr, uint32_t every, uint32_t npay8, uint32_t* hb,
+                                                 uint32_t* pb);
+
+template <typename MT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_decode_cascade_dense(
+    CascArgs A, rfec_kmask M, uint32_t n_hr, uint32_t every, uint32_t npay8)
+{
+    uint32_t hb = 0, pb = 0;
+    if (header_block_xcd(n_hr, every, npay8, &hb, &pb)) {
+        const uint32_t gt = hb * kBlock + threadIdx.x;
+        const uint32_t g = gt / kCheckLanes, s = gt % kCheckLanes;
+        const bool live = g < A.groups;
+        cascade_check_lanes<MT, kCheckLanes, false>(A, M, live ? g : 0u, live, s,
+                                                    (threadIdx.x & (kWave - 1)) & ~(uint32_t)(kCheckLanes - 1));
+        return;
+    }
+    __shared__ uint32_t lplan[RFEC_MAX_LINES];
+    __shared__ uint64_t lmask[8];
+    const rfec_kplan& P = M.plan;
+    if (threadIdx.x < 8)
+        lmask[threadIdx.x] = threadIdx.x < P.n_lines ? M.mask[threadIdx.x][0] : 0ull;
+    stage_plan(lplan, P); // (ends in a barrier)
+    const uint32_t t = pb * kBlock + threadIdx.x; // (XCD-swizzled: a group's lanes share one L2)
+    if (t >= A.total)
+        return;
+    const uint32_t g = fdiv(t, A.divQC);
+    const uint32_t rem = t - g * A.divQC.d;
+    const uint32_t q = fdiv(rem, A.divC);
+    const uint32_t j = rem - q * A.divC.d;
+    const uint32_t K = P.k, NL = P.n_lines, C = A.C;
+    const uint64_t kmask = K >= 64 ? ~0ull : (1ull << K) - 1ull;
+    const uint64_t have = A.present[2 * g] & kmask, erased = ~have & kmask;
+    const uint64_t ppm = A.parity_present[g];
+    uint64_t e = erased; // slot q: the q-th erased segment
+    for (uint32_t i = 0; i < q; ++i)
+        e &= e - 1;
+    if (!e)
+        return;
+    const uint32_t tgt = (uint32_t)__ffsll((long long)e) - 1;
+    // the first line that fires at once for it (masks and line records from the
+    // kernel arguments: scalar loads, no LDS round trips before the payload loads)
+    uint32_t l = 0xFFu, ln = 0;
+#pragma unroll
+    for (int x = 7; x >= 0; --x) {
+        const uint64_t lm = M.mask[x][0];
+        if ((uint32_t)x < NL && ((ppm >> x) & 1ull) && (lm & erased) == (1ull << tgt) && (lm & have)) {
+            l = (uint32_t)x;
+            ln = reinterpret_cast<const uint32_t*>(P.line)[x];
+        }
+    }
+    const v4u* grp = A.shards + (size_t)g * K * C + j;
+    const v4u* par = A.parity + (size_t)g * NL * C + j;
+    v4u* slot0 = A.out_sh + (size_t)g * A.E * C + j;
+    v4u* dst = slot0 + (size_t)q * C;
+    if (l != 0xFFu) { // single level
+        const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
+        v4u acc = ld16(par + (size_t)l * C);
+        v4u mv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = first + u * stride;
+            mv[u] = v4u{0, 0, 0, 0};
+            if ((uint32_t)u < count && i != tgt)
+                mv[u] = ld16(grp + (size_t)i * C);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            acc ^= mv[u];
+        st16(dst, acc);
+        return;
+    }
+    const CSched S = cascade_schedule<MT>(M, NL, (MT)have, ppm, 0u, (MT)erased, A.E);
+    uint32_t ss = 8;
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+        if ((uint32_t)s < S.n && cs_tg(S, s) == tgt)
+            ss = s;
+    if (ss == 8)
+        return; // not recoverable
     uint32_t need = 1u << ss;
 #pragma unroll 1
     for (int s = (int)ss; s >= 0; --s) {
@@ -1868,8 +1976,8 @@ struct FusedArgs {
 // payload than header blocks keeps them at the head.
 inline uint32_t hdr_every(const FusedArgs& F, uint32_t npay) { return F.n_hdr ? npay / F.n_hdr : 0; }
 
-// cascade decode: the checker (schedule records and task words into the workspace), then the payload
-// lanes, Q slots per group (dense: E, in place: one per possible step)
+// cascade decode, dense: one launch (k_decode_cascade_dense); in place: the checker (schedule records and
+// task words into the workspace), then the payload lanes, Q slots per group (one per possible step)
 void launch_cascade(CascArgs A, const rfec_kmask& M, uint32_t groups, uint32_t cd, void* ws, uint32_t ws_stride,
                     hipStream_t st)
 {
@@ -1880,6 +1988,17 @@ void launch_cascade(CascArgs A, const rfec_kmask& M, uint32_t groups, uint32_t c
     A.divQC = make_fastdiv(A.Q * cd);
     A.ws = reinterpret_cast<uint8_t*>(ws);
     A.ws_stride = ws_stride;
+    if (A.E) { // dense: one launch, the checker's blocks spread over the payload's
+        const uint32_t n_hr = (blocks_for((uint64_t)groups * kCheckLanes) + 7u) >> 3; // rounds of 8 check blocks
+        const uint32_t npay8 = (blocks_for(A.total) + 7u) & ~7u;
+        const uint32_t every = n_hr ? (npay8 >> 3) / n_hr : 0u;
+        const dim3 grid(8u * n_hr + npay8);
+        if (M.plan.k <= 32)
+            RFEC_LAUNCH(k_decode_cascade_dense<uint32_t>, grid, dim3(kBlock), 0, st, A, M, n_hr, every, npay8);
+        else
+            RFEC_LAUNCH(k_decode_cascade_dense<uint64_t>, grid, dim3(kBlock), 0, st, A, M, n_hr, every, npay8);
+        return;
+    }
     const dim3 gc(blocks_for((uint64_t)groups * kCheckLanes));
     if (M.plan.k <= 32)
         RFEC_LAUNCH(k_cascade_check<uint32_t>, gc, dim3(kBlock), 0, st, A, M);
