@@ -1219,15 +1219,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
 // the head of the grid: 134.6 us; the line search through LDS copies of the
 // masks instead of the kernel arguments: 131 us).  The payload lanes wait on
 // the masks (HBM) where k_decode_cascade waited on its task word (L2).
-__device__ __forceinline__ bool header_block_xcd(uint32_t n_hr, uint32_t every, uint32_t npay8, uint32_t* hb,
-                                                 uint32_t* pb);
-
 template <typename MT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_decode_cascade_dense(
     CascArgs A, rfec_kmask M, uint32_t n_hr, uint32_t every, uint32_t npay8)
 {
-    uint32_t hb = 0, pb = 0;
-    if (header_block_xcd(n_hr, every, npay8, &hb, &pb)) {
+    // Round R of 8 blocks (block x of a round runs on XCD x): the first round
+    // of every (every + 1) is a checker round while n_hr of them remain.  XCD x
+    // takes check blocks x n_hr + 0, 1, ... in order, the groups its payload
+    // rounds reach next (payload block p runs logical block xcd_block(p): XCD
+    // x's payload sweeps its eighth of the groups in order), so the checker's
+    // reads of the masks are the same XCD's and come just before the payload's.
+    const uint32_t R = blockIdx.x >> 3, x = blockIdx.x & 7u;
+    const uint32_t per = every ? R / (every + 1u) : R;
+    const bool check = per < n_hr && (every ? R == per * (every + 1u) : true);
+    if (check) {
+        const uint32_t hb = x * n_hr + per;
         const uint32_t gt = hb * kBlock + threadIdx.x;
         const uint32_t g = gt / kCheckLanes, s = gt % kCheckLanes;
         const bool live = g < A.groups;
@@ -1241,7 +1247,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     if (threadIdx.x < 8)
         lmask[threadIdx.x] = threadIdx.x < P.n_lines ? M.mask[threadIdx.x][0] : 0ull;
     stage_plan(lplan, P); // (ends in a barrier)
-    const uint32_t t = pb * kBlock + threadIdx.x; // (XCD-swizzled: a group's lanes share one L2)
+    const uint32_t pr = R - (every ? min(per + 1u, n_hr) : n_hr);
+    const uint32_t t = xcd_block(pr * 8u + x, npay8) * kBlock + threadIdx.x; // (a group's lanes share one L2)
     if (t >= A.total)
         return;
     const uint32_t g = fdiv(t, A.divQC);
