@@ -1214,11 +1214,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
 // segment gives its bytes, so the data equal the exact peel's wherever it
 // recovers; a segment it leaves unrecovered (a rejected line) may still be
 // written, its out_index 0xFF.  The checker's latency-bound work overlaps the
-// payload traffic instead of preceding it: c3 full 129.4-130.3 vs 131.5-131.8
-// us for check + k_decode_cascade (A/B on one box; the checker's blocks all at
-// the head of the grid: 134.6 us; the line search through LDS copies of the
-// masks instead of the kernel arguments: 131 us).  The payload lanes wait on
-// the masks (HBM) where k_decode_cascade waited on its task word (L2).
+// payload traffic instead of preceding it: c3 full 128.3-128.8 us vs 131.5-131.8
+// us for check + k_decode_cascade (A/Bs on one box; the checker's blocks all at
+// the head of the grid: 134.6 us; spread but not XCD-aligned with the payload:
+// 129.4-130.3 us; the line search through LDS copies of the masks instead of
+// the kernel arguments: 131 us; checker rounds 3 or 8 rounds further ahead: no
+// change).  The payload lanes wait on the masks where k_decode_cascade waited
+// on its task word (L2).
 template <typename MT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_decode_cascade_dense(
     CascArgs A, rfec_kmask M, uint32_t n_hr, uint32_t every, uint32_t npay8)
