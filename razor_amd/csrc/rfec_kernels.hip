@@ -1221,21 +1221,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
 // the kernel arguments: 131 us; checker rounds 3 or 8 rounds further ahead: no
 // change).  The payload lanes wait on the masks where k_decode_cascade waited
 // on its task word (L2).
+__device__ __forceinline__ bool header_block_xcd(uint32_t n_hr, uint32_t every, uint32_t npay8, uint32_t* hb,
+                                                 uint32_t* pb);
+
 template <typename MT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_decode_cascade_dense(
     CascArgs A, rfec_kmask M, uint32_t n_hr, uint32_t every, uint32_t npay8)
 {
-    // Round R of 8 blocks (block x of a round runs on XCD x): the first round
-    // of every (every + 1) is a checker round while n_hr of them remain.  XCD x
-    // takes check blocks x n_hr + 0, 1, ... in order, the groups its payload
-    // rounds reach next (payload block p runs logical block xcd_block(p): XCD
-    // x's payload sweeps its eighth of the groups in order), so the checker's
-    // reads of the masks are the same XCD's and come just before the payload's.
-    const uint32_t R = blockIdx.x >> 3, x = blockIdx.x & 7u;
-    const uint32_t per = every ? R / (every + 1u) : R;
-    const bool check = per < n_hr && (every ? R == per * (every + 1u) : true);
-    if (check) {
-        const uint32_t hb = x * n_hr + per;
+    uint32_t hb = 0, pb = 0;
+    if (header_block_xcd(n_hr, every, npay8, &hb, &pb)) { // (checker blocks XCD-aligned with the payload sweep)
         const uint32_t gt = hb * kBlock + threadIdx.x;
         const uint32_t g = gt / kCheckLanes, s = gt % kCheckLanes;
         const bool live = g < A.groups;
@@ -1249,8 +1243,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     if (threadIdx.x < 8)
         lmask[threadIdx.x] = threadIdx.x < P.n_lines ? M.mask[threadIdx.x][0] : 0ull;
     stage_plan(lplan, P); // (ends in a barrier)
-    const uint32_t pr = R - (every ? min(per + 1u, n_hr) : n_hr);
-    const uint32_t t = xcd_block(pr * 8u + x, npay8) * kBlock + threadIdx.x; // (a group's lanes share one L2)
+    const uint32_t t = pb * kBlock + threadIdx.x; // (XCD-swizzled: a group's lanes share one L2)
     if (t >= A.total)
         return;
     const uint32_t g = fdiv(t, A.divQC);
@@ -1462,11 +1455,16 @@ __device__ __forceinline__ bool header_block(uint32_t n_hdr, uint32_t every, uin
 }
 
 // The same spread in rounds of 8 blocks (one per XCD: block b runs on XCD
-// b % 8) for the XCD-swizzled decodes: every (every + 1)-th round is a round
-// of 8 header blocks until n_hr of them ran, so the payload blocks fill whole
-// rounds and payload block p (in payload order) runs on XCD p % 8; it then
-// takes logical block xcd_block(p): consecutive logical blocks share an XCD's
-// L2 (the 128-B lines split between neighbouring slots are fetched once).
+// b % 8) for the XCD-swizzled decodes: the first round of every (every + 1) is
+// a round of 8 header blocks until n_hr of them ran, so the payload blocks fill
+// whole rounds and payload block p (in payload order) runs on XCD p % 8; it
+// then takes logical block xcd_block(p): consecutive logical blocks share an
+// XCD's L2 (the 128-B lines split between neighbouring slots are fetched once)
+// and XCD x sweeps its eighth of the groups in order.  XCD x's header blocks
+// are x n_hr + 0, 1, ...: the groups its own payload rounds reach next, so the
+// header blocks' reads of the masks come in through the same L2 just before
+// the payload lanes read them (the cascade decode: 128.3-128.8 vs 129.4-130.3
+// us with header block per * 8 + x, last in each period).
 // npay8: payload blocks rounded up to a multiple of 8.
 __device__ __forceinline__ bool header_block_xcd(uint32_t n_hr, uint32_t every, uint32_t npay8, uint32_t* hb,
                                                  uint32_t* pb)
@@ -1475,17 +1473,17 @@ __device__ __forceinline__ bool header_block_xcd(uint32_t n_hr, uint32_t every, 
     uint32_t pr;
     if (!every) {
         if (R < n_hr) {
-            *hb = R * 8u + x;
+            *hb = x * n_hr + R;
             return true;
         }
         pr = R - n_hr;
     } else {
         const uint32_t per = R / (every + 1);
-        if (per < n_hr && R - per * (every + 1) == every) {
-            *hb = per * 8u + x;
+        if (per < n_hr && R == per * (every + 1)) {
+            *hb = x * n_hr + per;
             return true;
         }
-        pr = R - min(per, n_hr);
+        pr = R - min(per + 1, n_hr);
     }
     *pb = xcd_block(pr * 8u + x, npay8);
     return false;
