@@ -150,7 +150,8 @@ class Workload:
         else:
             pairs = np.array(distinct_row_pairs(self.plan))
         rng = np.random.default_rng(seed)
-        self.erased = pairs[rng.integers(0, len(pairs), G)]
+        pick = rng.integers(0, len(pairs), G)
+        self.erased = pairs[pick]
         present = np.zeros((G, 2), np.uint64)
         full = np.uint64((1 << k) - 1)
         present[:, 0] = full & ~((np.uint64(1) << self.erased[:, 0].astype(np.uint64)) |
@@ -177,8 +178,8 @@ class Workload:
         # algorithmic payload bytes (headers excluded): encode reads k*S, writes r*S
         self.enc_bytes = G * (k + self.n) * S
         # decode: per recovered segment read its line's other members + the parity, write 1
-        pair_bytes = {tuple(p): peel_bytes(self.plan, k, tuple(p), S) for p in pairs.tolist()}
-        self.dec_bytes = int(sum(pair_bytes[(int(a), int(b))] for a, b in self.erased))
+        pair_bytes = np.array([peel_bytes(self.plan, k, tuple(p), S) for p in pairs.tolist()], np.int64)
+        self.dec_bytes = int(pair_bytes[pick].sum())
 
     def encode(self, stream):
         self.lib.encode_batch(self.plan, self.G, self.stride, self.S, self.shards.data_ptr(), self.hdr.data_ptr(),
@@ -267,6 +268,47 @@ def copy_ceiling(lib, device, nbytes=1 << 30, reps=10):
     t = e0.elapsed_time(e1) / 1e3 / reps
     del a, b
     return 2 * nbytes / t / 1e9
+
+
+def mix_ceiling(lib, device, r, w, stream_bytes, reps=10):
+    """Measured HBM rate (GB/s, read + write bytes / time) of the library's
+    r : w streaming probe (rfec_probe_mix: r read streams XORed into w write
+    streams, one 16-B vector per lane, non-temporal) over the encode's own
+    byte volume, two rotated buffer sets: the ceiling of the encode's read /
+    write mix (writes cost HBM more than reads: 10 : 3 streams at ~0.77 of
+    8 TB/s, 10 : 7 at ~0.71)."""
+    st = torch.cuda.current_stream(device).cuda_stream
+    sets = [(torch.empty(r * stream_bytes, dtype=torch.uint8, device=device),
+             torch.empty(w * stream_bytes, dtype=torch.uint8, device=device)) for _ in range(2)]
+
+    def run(i):
+        a, b = sets[i % 2]
+        rc = lib.lib.rfec_probe_mix(a.data_ptr(), b.data_ptr(), stream_bytes, r, w, st)
+        if rc:
+            raise RuntimeError(f"rfec_probe_mix {r}:{w} failed: {rc}")
+
+    for i in range(4):
+        run(i)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(device)
+    e0.record()
+    for i in range(reps):
+        run(i)
+    e1.record()
+    torch.cuda.synchronize(device)
+    t = e0.elapsed_time(e1) / 1e3 / reps
+    del sets
+    return (r + w) * stream_bytes / t / 1e9
+
+
+def encode_mix(w):
+    """(reads, writes, stream bytes) of the probe with the encode's byte mix, or None."""
+    lines = [w.plan.line[l].count for l in range(w.n)]
+    if w.k == 10 and w.n in (3, 7):  # rows {4,4,2} (10 : 3), the full 3 x 4 plan (10 : 7)
+        return 10, w.n, w.G * w.S
+    if len(set(lines)) == 1 and lines[0] == 4 and w.k == 4 * w.n:  # rows of 4 (c5: 4 : 1)
+        return 4, 1, w.G * w.n * w.S
+    return None
 
 
 def host_cores():
@@ -397,6 +439,129 @@ TIMING_BRACKET = ("HIP events recorded on the launch stream before and after the
                   "gap; --timing bracket, or a call that launches more than one kernel)")
 
 
+def time_steps(lib, sets, steps, warmup, stream, dist, timing, hot):
+    """Primes every set's parity, runs `warmup` untimed steps, then times
+    `steps` steps (encode one set, decode the set encoded one step earlier, or
+    the same set when `hot` or one set) between a barrier + device
+    synchronize on both sides.  Returns (elapsed wall seconds, max over ranks;
+    per-step encode / decode launch seconds; whether each is the kernel's own
+    window)."""
+    nset = len(sets)
+    sp = stream.cuda_stream
+    device = stream.device
+
+    def dec_set(i):
+        return sets[i % nset] if hot else sets[(i - 1) % nset]
+
+    for ws in sets:  # every set holds its parity before the first (cold) decode
+        ws.encode(sp)
+    for i in range(warmup):
+        sets[i % nset].encode(sp)
+        dec_set(i).decode(sp)
+    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(steps)]
+    # the kernels' own start / stop (rfec_timing_events -> hipExtLaunchKernel on the launch stream):
+    # the roofline's launch duration, without the dispatch gap the stream-event bracket also holds
+    kev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(steps)]
+    for q in kev:
+        for e in q:
+            e.record(stream)  # creates the event (torch allocates it at its first record)
+    # does each call launch exactly one kernel (then its own window is its launch duration)?
+    lib.timing_events(kev[0][0].cuda_event, kev[0][1].cuda_event)
+    sets[0].encode(sp)
+    n_enc = lib.timing_launches()
+    lib.timing_events(kev[0][2].cuda_event, kev[0][3].cuda_event)
+    dec_set(1).decode(sp)
+    n_dec = lib.timing_launches()
+    own_enc = timing == "own" and n_enc == 1
+    own_dec = timing == "own" and n_dec == 1
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        # the kernels' own events where a call is one launch (no marker between launches), else a bracket
+        ka, kb, kc, kd = kev[i]
+        a, b, c, d = ev[i]
+        if own_enc:
+            lib.timing_events(ka.cuda_event, kb.cuda_event)
+        else:
+            a.record(stream)
+        sets[(warmup + i) % nset].encode(sp)
+        if not own_enc:
+            b.record(stream)
+        if own_dec:
+            lib.timing_events(kc.cuda_event, kd.cuda_event)
+        else:
+            c.record(stream)
+        dec_set(warmup + i).decode(sp)
+        if not own_dec:
+            d.record(stream)
+    torch.cuda.synchronize(device)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t_enc = np.array([(q if own_enc else e)[0].elapsed_time((q if own_enc else e)[1]) for q, e in zip(kev, ev)]) / 1e3
+    t_dec = np.array([(q if own_dec else e)[2].elapsed_time((q if own_dec else e)[3]) for q, e in zip(kev, ev)]) / 1e3
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    return elapsed, t_enc, t_dec, own_enc, own_dec
+
+
+def c4_strong(lib, device, stream, dist, world, rank, pf, steps, warmup, verify):
+    """BASELINE configs[3] beside the weak-scaling headline: the 1,048,576
+    groups of config 4 split into contiguous slices over the ranks
+    (razor_amd/dist.shard_groups; all of them on one GPU at N = 1), `steps`
+    timed encode + decode steps of one buffer set (at 12.6 GB of shards per
+    GPU at N = 1 nothing of a step stays in the 256 MB MALL).  Every rank
+    checks its slice against the reference's digest of exactly those groups
+    (full_hashes.json: the whole case at N = 1, "slices" at N = 2 / 4 / 8).
+    Returns the sub-object on rank 0 (None elsewhere); value = all ranks'
+    bytes / max-over-ranks time, so value(N) / value(1) is the strong-scaling
+    speedup."""
+    cfg = CONFIGS["c4"]
+    total = cfg["groups"]
+    group0, my = shard_groups(total, world, rank)
+    w = Workload(lib, my, cfg["k"], cfg["S"], pf, device, group0, seed=3000 + rank, config_id=cfg["config_id"])
+    elapsed, t_enc, t_dec, own_enc, own_dec = time_steps(lib, [w], steps, warmup, stream, dist, "own", True)
+    verified = digest_ok = None
+    if verify:
+        verified = w.verify()
+        want = golden_digest(cfg["golden"], world, rank)
+        if want is not None:
+            digest_ok = w.digest() == want
+            verified = verified and digest_ok
+    per_rank = torch.tensor([w.G, w.enc_bytes + w.dec_bytes, float(t_enc.mean()) * 1e6, float(t_dec.mean()) * 1e6,
+                             -1 if verified is None else int(verified), -1 if digest_ok is None else int(digest_ok)],
+                            dtype=torch.float64)
+    rows = [per_rank]
+    if dist:
+        rows = [torch.zeros_like(per_rank) for _ in range(world)]
+        dist.all_gather(rows, per_rank)
+    del w
+    torch.cuda.empty_cache()
+    if rank != 0:
+        return None
+    step_bytes = sum(float(r[1]) for r in rows)
+    enc_b = rows[0][0].item() * (cfg["k"] + 3) * cfg["S"]
+    flags = [(int(r[4]), int(r[5])) for r in rows]
+    return {"workload": f"c4: k10_r3_S1200_G{total} split into {world} contiguous slice(s) "
+                        f"[r*{total}/{world}, (r+1)*{total}/{world})",
+            "scaling": "strong", "value": round(step_bytes * steps / elapsed / 2**30, 3), "unit": "GiB/s",
+            "steps": steps, "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "buffer_sets": 1, "decode_order": "hot (the set this step encoded; at this size not MALL-resident)",
+            "groups_per_rank": [int(r[0]) for r in rows],
+            "encode_launch_us_per_rank": [round(float(r[2]), 2) for r in rows],
+            "decode_launch_us_per_rank": [round(float(r[3]), 2) for r in rows],
+            "rank0_encode_frac_of_peak": round(enc_b / (float(rows[0][2]) * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+            "timing": (TIMING_OWN if own_enc and own_dec else TIMING_BRACKET),
+            "verified": None if not verify else all(f[0] == 1 for f in flags),
+            "verified_vs_reference_digest": None if not verify else (
+                False if any(f[1] == 0 for f in flags) else (True if all(f[1] == 1 for f in flags) else None))}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -425,6 +590,8 @@ def main():
                     help="decode into the received shards (rfec_recover_batch) instead of a dense output")
     ap.add_argument("--hot-decode", action="store_true",
                     help="decode the set encoded in the same step (its parity still MALL-resident)")
+    ap.add_argument("--c4-steps", type=int, default=10,
+                    help="timed steps of the c4_strong sub-object (config c3 only; 0 = skip it)")
     args = ap.parse_args()
 
     # --gpus N without a launcher: start N ranks under torchrun as a child
@@ -488,65 +655,8 @@ def main():
     sp = stream.cuda_stream
     torch.cuda.synchronize(device)
 
-    def dec_set(i):
-        return sets[i % nset] if args.hot_decode else sets[(i - 1) % nset]
-
-    for ws in sets:  # every set holds its parity before the first (cold) decode
-        ws.encode(sp)
-
-    for i in range(args.warmup):
-        sets[i % nset].encode(sp)
-        dec_set(i).decode(sp)
-    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(args.steps)]
-    # the kernels' own start / stop (rfec_timing_events -> hipExtLaunchKernel on the launch stream):
-    # the roofline's launch duration, without the dispatch gap the stream-event bracket also holds
-    kev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(args.steps)]
-    for q in kev:
-        for e in q:
-            e.record(stream)  # creates the event (torch allocates it at its first record)
-    # does each call launch exactly one kernel (then its own window is its launch duration)?
-    lib.timing_events(kev[0][0].cuda_event, kev[0][1].cuda_event)
-    sets[0].encode(sp)
-    n_enc = lib.timing_launches()
-    lib.timing_events(kev[0][2].cuda_event, kev[0][3].cuda_event)
-    dec_set(1).decode(sp)
-    n_dec = lib.timing_launches()
-    own_enc = args.timing == "own" and n_enc == 1
-    own_dec = args.timing == "own" and n_dec == 1
-    torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        # the kernels' own events where a call is one launch (no marker between launches), else a bracket
-        ka, kb, kc, kd = kev[i]
-        a, b, c, d = ev[i]
-        if own_enc:
-            lib.timing_events(ka.cuda_event, kb.cuda_event)
-        else:
-            a.record(stream)
-        sets[(args.warmup + i) % nset].encode(sp)
-        if not own_enc:
-            b.record(stream)
-        if own_dec:
-            lib.timing_events(kc.cuda_event, kd.cuda_event)
-        else:
-            c.record(stream)
-        dec_set(args.warmup + i).decode(sp)
-        if not own_dec:
-            d.record(stream)
-    torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    t_enc = np.array([(q if own_enc else e)[0].elapsed_time((q if own_enc else e)[1]) for q, e in zip(kev, ev)]) / 1e3
-    t_dec = np.array([(q if own_dec else e)[2].elapsed_time((q if own_dec else e)[3]) for q, e in zip(kev, ev)]) / 1e3
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed, t_enc, t_dec, own_enc, own_dec = time_steps(lib, sets, args.steps, args.warmup, stream, dist,
+                                                         args.timing, args.hot_decode)
 
     verified, digest_ok = None, None
     if not args.no_verify:
@@ -571,6 +681,15 @@ def main():
         verified = None if args.no_verify else bool(vt[0].item())
         digest_ok = None if args.no_verify else (False if not vt[1].item() else (True if vt[2].item() else None))
 
+    # BASELINE configs[3] beside the weak headline (default run only): the 1M-group strong split
+    c4 = None
+    if cfg_name == "c3" and args.c4_steps > 0 and not args.lib:
+        log("c4 strong split ...")
+        c4 = c4_strong(lib, device, stream, dist, world, rank, args.protect_fraction, args.c4_steps, 2,
+                       not args.no_verify)
+        if c4 and c4["verified"] is False:
+            verified = False
+
     # whole-job bytes: every rank's slice (equal slices up to one group)
     nb = torch.tensor([w.enc_bytes + w.dec_bytes, w.G], dtype=torch.float64)
     if dist:
@@ -583,12 +702,14 @@ def main():
     res = None
     if rank == 0:
         ceiling = copy_ceiling(lib, device)
+        mix = encode_mix(w)
+        mix_gbps = mix_ceiling(lib, device, *mix) if mix else None
         workload_name = f"k{k}_r{w.n}_S{S}_G{w.G}"
         lines = [w.plan.line[l].count for l in range(w.n)]
         rows_layout = not full_plan and len(set(lines[:-1])) <= 1
         enc_kernel = (f"k_encode_out<{k},{lines[0]}>" if rows_layout and (k, lines[0]) in ((10, 4), (32, 4))
                       else ("k_encode_out_rt (run-time k, col)" if rows_layout and lines[0] <= 16
-                            else (f"k_encode_matrix_out<{k},{w.plan.col}>" if full_plan else "k_encode (plan-driven)")))
+                            else (f"k_encode_matrix_lds<{k},{w.plan.col}>" if full_plan else "k_encode (plan-driven)")))
         cd = (S + 15) // 16
         per = ("one lane per (group, output slot, chunk)" if w.dense and 2 <= len(lines)
                else "one lane per (group, line, chunk)")
@@ -648,7 +769,12 @@ def main():
                          "traffic": traffic, "launch_us": round(enc_mean * 1e6, 2),
                          "launch_us_median": round(float(np.median(t_enc)) * 1e6, 2),
                          "timing": TIMING_OWN if own_enc else TIMING_BRACKET,
-                         "algorithmic_bytes_per_launch": w.enc_bytes},
+                         "algorithmic_bytes_per_launch": w.enc_bytes,
+                         "mix_ceiling": None if not mix else {
+                             "probe": f"rfec_probe_mix {mix[0]} reads : {mix[1]} writes, {mix[2]} B per stream "
+                                      f"(the encode's byte mix and volume, contiguous streams)",
+                             "GBps": round(mix_gbps, 1), "frac_of_peak": round(mix_gbps / HBM_PEAK_GBPS, 4),
+                             "kernel_vs_ceiling": round(achieved / mix_gbps, 4)}},
             "encode_gibps": round(w.enc_bytes / enc_mean / 2**30, 2),
             # source bytes k*S*G over the encode time, and that as a fraction of the peak
             "encode_source_gibps": round(w.G * w.k * w.S / enc_mean / 2**30, 2),
@@ -670,6 +796,8 @@ def main():
             "verified_vs_reference_digest": digest_ok,
             "tuning": args.tuning,
         }
+        if c4 is not None:
+            res["c4_strong"] = c4
         if world == 1 and not args.no_cpu:
             log("cpu baseline ...")
             res["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)

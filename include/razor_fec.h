@@ -652,6 +652,11 @@ int rfec_service_get_info(rfec_service_info* info);
 int rfec_probe_read(const void* src, size_t bytes, void* sink, unsigned flags, void* stream);
 int rfec_probe_copy(const void* src, void* dst, size_t bytes, unsigned flags, void* stream);
 int rfec_probe_write(void* dst, size_t bytes, unsigned flags, void* stream);
+/* r read streams : w write streams of stream_bytes each (src holds r, dst w
+ * streams back to back), lane i XORs chunk i of every read stream into chunk
+ * i of every write stream, non-temporal: the ceiling of the encodes' read /
+ * write mixes.  (r, w) in {(10, 3), (10, 7), (4, 1), (1, 1)}, else -1. */
+int rfec_probe_mix(const void* src, void* dst, size_t stream_bytes, unsigned r, unsigned w, void* stream);
 
 /* Synthetic inputs of SURVEY.md §8(d) (bench and tests only, not on the FEC
  * path): payload slots of groups [g0, g0 + groups) of the xorshift64*

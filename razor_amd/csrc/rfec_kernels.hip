@@ -19,7 +19,8 @@
 //      lane per PARITY chunk loading its row's members, XCD-swizzled blocks;
 //    * the sender's full rows + columns plan (k = 6..16): k_encode_matrix_out,
 //      one lane per PARITY chunk (group, line, chunk), member loads at the
-//      default policy so a column's lanes re-read its members from L2;
+//      default policy so a column's lanes re-read its members from L2 (at the
+//      10 : 7 read / write mix's streaming ceiling, rfec_probe_mix);
 //    * any other plan: k_encode (plan-driven).
 //  recover (rfec_launch_recover picks by plan):
 //    * pairwise disjoint lines (row layer, strip mode), one launch: header
@@ -117,41 +118,48 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
     return (b & 7u) * (nb8 >> 3) + (b >> 3);
 }
 
-// Copies n dwords global -> LDS with the whole block, several loads in flight
-// per lane (a plain strided loop would wait on each load before the next).
-// `lds` must be 16-byte aligned; 16-byte loads are used when `src` is too.
-__device__ __forceinline__ void stage_dwords(uint32_t* lds, const uint32_t* __restrict__ src, uint32_t n)
+// Copies n dwords global -> LDS with the whole block (nt lanes), several loads
+// in flight per lane: the loads go through a buffer descriptor over exactly
+// the n dwords, so a lane past the end reads zeros with no branch around the
+// load (hipcc waited on each guarded load before issuing the next).  `lds`
+// must be 16-byte aligned; 16-byte loads are used when `src` is too.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t span_rsrc(const void* p, uint32_t nbytes)
+{
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((uint64_t)hi << 32 | lo), 0,
+                                             (int)__builtin_amdgcn_readfirstlane((int)nbytes), 0x00020000);
+}
+
+__device__ __forceinline__ void stage_dwords(uint32_t* lds, const uint32_t* __restrict__ src, uint32_t n,
+                                             uint32_t nt = kBlock)
 {
     constexpr int U = 4;
+    const __amdgpu_buffer_rsrc_t r = span_rsrc(src, n * 4u);
     const uint32_t nv = ((reinterpret_cast<uintptr_t>(src) & 15) == 0) ? n / 4 : 0;
-    const v4u* s4 = reinterpret_cast<const v4u*>(src);
     v4u* d4 = reinterpret_cast<v4u*>(lds);
-    for (uint32_t base = 0; base < nv; base += U * kBlock) {
+    for (uint32_t base = 0; base < nv; base += U * nt) {
         v4u tmp[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t i = base + u * kBlock + threadIdx.x;
-            if (i < nv)
-                tmp[u] = s4[i];
-        }
+        for (int u = 0; u < U; ++u)
+            tmp[u] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 r, (base + u * nt + threadIdx.x) * 16u, 0, 0));
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t i = base + u * kBlock + threadIdx.x;
+            const uint32_t i = base + u * nt + threadIdx.x;
             if (i < nv)
                 d4[i] = tmp[u];
         }
     }
-    for (uint32_t base = nv * 4; base < n; base += 4 * U * kBlock) {
+    for (uint32_t base = nv * 4; base < n; base += 4 * U * nt) {
         uint32_t tmp[4 * U];
 #pragma unroll
-        for (int u = 0; u < 4 * U; ++u) {
-            const uint32_t i = base + u * kBlock + threadIdx.x;
-            if (i < n)
-                tmp[u] = src[i];
-        }
+        for (int u = 0; u < 4 * U; ++u)
+            tmp[u] = __builtin_amdgcn_raw_buffer_load_b32(r, (base + u * nt + threadIdx.x) * 4u, 0, 0);
 #pragma unroll
         for (int u = 0; u < 4 * U; ++u) {
-            const uint32_t i = base + u * kBlock + threadIdx.x;
+            const uint32_t i = base + u * nt + threadIdx.x;
             if (i < n)
                 lds[i] = tmp[u];
         }
@@ -163,17 +171,18 @@ __device__ __forceinline__ void stage_dwords(uint32_t* lds, const uint32_t* __re
 // dwords (field-wise XOR, flex_fec_xor.c:13-20, 37-44), fec_data_size = max
 // data_size (:22-26), status -1 where flex_fec_generate fails (:9-10, :27-28).
 // ---------------------------------------------------------------------------
-__device__ void meta_block(uint32_t mb, const uint32_t* __restrict__ hdr_dw, uint32_t* __restrict__ meta_dw,
-                           uint16_t* __restrict__ fsize, int8_t* __restrict__ status, uint32_t groups,
-                           uint32_t capacity, uint32_t gpb, const rfec_kplan& P)
+// (lds: kMetaDwords, 16-byte aligned; nt: the block's threads)
+__device__ void meta_block_in(uint32_t* lds, uint32_t nt, uint32_t mb, const uint32_t* __restrict__ hdr_dw,
+                              uint32_t* __restrict__ meta_dw, uint16_t* __restrict__ fsize,
+                              int8_t* __restrict__ status, uint32_t groups, uint32_t capacity, uint32_t gpb,
+                              const rfec_kplan& P)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kMetaDwords];
     const uint32_t K = P.k, NL = P.n_lines;
     const uint32_t g0 = mb * gpb;
     const uint32_t ng = min(gpb, groups - g0);
-    stage_dwords(lds, hdr_dw + (size_t)g0 * K * 5, ng * K * 5);
+    stage_dwords(lds, hdr_dw + (size_t)g0 * K * 5, ng * K * 5, nt);
     __syncthreads();
-    for (uint32_t o = threadIdx.x; o < ng * NL; o += kBlock) {
+    for (uint32_t o = threadIdx.x; o < ng * NL; o += nt) {
         const uint32_t gl = o / NL, l = o - gl * NL;
         const rfec_line ln = P.line[l];
         const uint32_t* h = lds + gl * K * 5;
@@ -198,6 +207,14 @@ __device__ void meta_block(uint32_t mb, const uint32_t* __restrict__ hdr_dw, uin
         if (status)
             status[out] = (ln.count <= 1 || L > capacity) ? (int8_t)-1 : (int8_t)0;
     }
+}
+
+__device__ void meta_block(uint32_t mb, const uint32_t* __restrict__ hdr_dw, uint32_t* __restrict__ meta_dw,
+                           uint16_t* __restrict__ fsize, int8_t* __restrict__ status, uint32_t groups,
+                           uint32_t capacity, uint32_t gpb, const rfec_kplan& P)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kMetaDwords];
+    meta_block_in(lds, kBlock, mb, hdr_dw, meta_dw, fsize, status, groups, capacity, gpb, P);
 }
 
 struct EncMeta {
@@ -261,10 +278,9 @@ __global__ __launch_bounds__(kBlock) void k_encode(const v4u* __restrict__ shard
 // ---------------------------------------------------------------------------
 // Encode payload, the reference sender's full matrix plan at small k
 // (flex_fec_sender.c:166-233: rows of COL consecutive segments, then columns
-// strided by COL, lines with fewer than 2 members dropped), member offsets
-// and line order compile-time: all K loads in flight, every line's XOR from
-// registers.  K = 6..16 (COL = 3 or 4, as flex_fec_sender_num_packets picks).
-// One lane per (group, chunk column), XCD-swizzled blocks.
+// strided by COL, lines with fewer than 2 members dropped), K = 6..16 (COL =
+// 3 or 4, as flex_fec_sender_num_packets picks); MatrixShape = its compile-time
+// line layout.
 // ---------------------------------------------------------------------------
 template <int K, int COL>
 struct MatrixShape {
@@ -287,60 +303,23 @@ struct MatrixShape {
     }
 };
 
-template <int K, int COL>
-__global__ __launch_bounds__(kBlock) void k_encode_matrix(const v4u* __restrict__ shards, v4u* __restrict__ parity,
-                                                          uint32_t total, uint32_t C, FastDiv divC, uint32_t head,
-                                                          EncMeta E, rfec_kplan P)
-{
-    using Sh = MatrixShape<K, COL>;
-    uint32_t b;
-    if (!enc_payload_block(E, head, P, &b))
-        return;
-    const uint32_t t = b * kBlock + threadIdx.x;
-    if (t >= total)
-        return;
-    const uint32_t g = fdiv(t, divC);
-    const uint32_t j = t - g * divC.d;
-    const v4u* src = shards + (size_t)g * K * C + j;
-    v4u* dst = parity + (size_t)g * Sh::n_lines() * C + j;
-    v4u v[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i)
-        v[i] = ld16(src + (size_t)i * C);
-    int l = 0;
-#pragma unroll
-    for (int r = 0; r < Sh::R; ++r) {
-        if (Sh::row_count(r) < 2)
-            continue;
-        v4u acc = v[r * COL];
-#pragma unroll
-        for (int q = 1; q < COL; ++q)
-            if (q < Sh::row_count(r))
-                acc ^= v[r * COL + q];
-        st16(dst + (size_t)(l++) * C, acc);
-    }
-#pragma unroll
-    for (int c = 0; c < COL; ++c) {
-        if (Sh::col_count(c) < 2)
-            continue;
-        v4u acc = v[c];
-#pragma unroll
-        for (int q = 1; q < (K + COL - 1) / COL; ++q)
-            if (q < Sh::col_count(c))
-                acc ^= v[c + q * COL];
-        st16(dst + (size_t)(l++) * C, acc);
-    }
-}
-
 // Output-mapped form of the full matrix encode: one lane per PARITY chunk
 // (group, line, chunk column), as k_encode_out, so that every wave's store is
 // 1 KiB of consecutive parity bytes (whole 128-B lines when the slots are
 // packed) instead of seven 1 KiB runs that start and end inside lines shared
 // with the neighbouring waves.  Each member is loaded by its row's lanes and
 // again by its column's lanes one block or so later, on the same XCD, so HBM
-// should still see every member once.  Row l < NR: members l COL + q; column c = l - NR: c + q COL
-// (K >= 2 COL here, so no column has fewer than 2 members).  Loads take the
-// default policy: the column lanes' second reads are meant to hit L2.
+// should still see every member once (PMC: 1.018 x algorithmic).  Row l <
+// NR: members l COL + q; column c = l - NR: c + q COL (K >= 2 COL here, so no
+// column has fewer than 2 members).  Loads take the default policy: the
+// column lanes' second reads are meant to hit L2.  At c3 full (10 reads : 7
+// writes per group) 233-235 us, the time of a 10 : 7 streaming probe over
+// contiguous streams (rfec_probe_mix: 235 us): the mix's HBM ceiling.
+// Measured slower: one lane per (group, chunk) loading each member once, all
+// seven parity chunks through LDS and stored as one contiguous run per block
+// (238-239 us, round 4); the same with seven direct stores per lane (252-260
+// us, round 2: every 1-KiB store run starts and ends inside lines that the
+// neighbouring waves write).
 template <int K, int COL>
 __global__ __launch_bounds__(kBlock) void k_encode_matrix_out(const v4u* __restrict__ shards,
                                                               v4u* __restrict__ parity, uint32_t total, uint32_t C,
@@ -1278,13 +1257,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     if (l != 0xFFu) { // single level
         const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
         v4u acc = ld16(par + (size_t)l * C);
+        // members through a descriptor over the first active lane's group (wave_rsrc: no per-load
+        // branch, all four loads in flight; with `if (used) load` hipcc waited on each load in turn)
+        const uint32_t gb = (uint32_t)__builtin_amdgcn_readfirstlane((int)g); // lanes' groups ascend
+        const __amdgpu_buffer_rsrc_t rs = wave_rsrc(A.shards + (size_t)gb * K * C);
+        const uint32_t grp0 = ((g - gb) * K * C + j) * 16u;
         v4u mv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t i = first + u * stride;
-            mv[u] = v4u{0, 0, 0, 0};
-            if ((uint32_t)u < count && i != tgt)
-                mv[u] = ld16(grp + (size_t)i * C);
+            mv[u] = bld16(rs, (uint32_t)u < count && i != tgt ? grp0 + i * C * 16u : kNoLoad);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -1940,8 +1922,6 @@ hipError_t launch_encode(const EncLaunch& a, unsigned flags)
     const uint32_t total = a.groups * a.cd;
     if (!generic && P->k >= 6 && P->k <= 16 && is_full_matrix(P, P->k <= 9 ? 3 : 4)) {
         const uint32_t head = enc_head(a);
-        const dim3 grid(head + blocks_for(total));
-#ifndef RFEC_MATRIX_REG // the output-mapped form (A/B -DRFEC_MATRIX_REG: one lane per (group, chunk column))
         const uint32_t nl = P->n_lines, tot = a.groups * nl * a.cd;
         const dim3 grid_o(head + blocks_for(tot));
 #define RFEC_MX(KK, CC)                                                                                           \
@@ -1949,13 +1929,6 @@ hipError_t launch_encode(const EncLaunch& a, unsigned flags)
         RFEC_LAUNCH((k_encode_matrix_out<KK, CC>), grid_o, dim3(kBlock), 0, a.stream, a.s, a.p, tot, C,          \
                     make_fastdiv(a.cd), make_fastdiv(nl * a.cd), head, a.E, *P);                                  \
         return hipGetLastError();
-#else
-#define RFEC_MX(KK, CC)                                                                                           \
-    case KK:                                                                                                      \
-        RFEC_LAUNCH((k_encode_matrix<KK, CC>), grid, dim3(kBlock), 0, a.stream, a.s, a.p, total, C,               \
-                    make_fastdiv(a.cd), head, a.E, *P);                                                           \
-        return hipGetLastError();
-#endif
         switch (P->k) {
             RFEC_MX(6, 3) RFEC_MX(7, 3) RFEC_MX(8, 3) RFEC_MX(9, 3) RFEC_MX(10, 4) RFEC_MX(11, 4) RFEC_MX(12, 4)
             RFEC_MX(13, 4) RFEC_MX(14, 4) RFEC_MX(15, 4) RFEC_MX(16, 4)
@@ -2149,7 +2122,7 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
     // plans with cascades within the register schedule (the sender's matrix plans): one launch
     const uint32_t Q = dense ? out->per_group : (P.n_lines < P.k ? P.n_lines : P.k);
     const bool cascade = !B.disjoint && maxc <= 4 && P.n_lines <= 8 && P.k <= 64 && !generic &&
-                         (uint64_t)groups * Q * cd < (1ull << 32);
+                         (uint64_t)groups * Q * cd < (1ull << 32) && (uint64_t)(kWave + 1) * P.k * stride < kNoLoad;
     // everything else (and RFEC_TUNE_GENERIC): the LDS peel + schedule replay, in place or dense
     // LDS per group: K + NL header records (5 dwords) + NL u16 sizes; block
     // ranges start on 8-group boundaries so the staged slices are 16-B aligned

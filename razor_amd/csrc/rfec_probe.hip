@@ -81,6 +81,30 @@ __global__ __launch_bounds__(kBlock) void k_write(v4u* __restrict__ dst, size_t 
     }
 }
 
+// R read streams : W write streams (the FEC kernels' read / write mixes:
+// 10 : 3 for the row encode, 10 : 7 for the full 3 x 4 plan, 4 : 1 for rows
+// of 4 as at k = 32): lane i loads
+// chunk i of each read stream (all in flight), stores their XOR to chunk i of
+// each write stream; non-temporal both ways.
+template <int R, int W>
+__global__ __launch_bounds__(kBlock) void k_mix(const v4u* __restrict__ src, v4u* __restrict__ dst, size_t n)
+{
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    v4u v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        v[r] = ld<true>(src + r * n + i);
+    v4u acc = v[0];
+#pragma unroll
+    for (int r = 1; r < R; ++r)
+        acc ^= v[r];
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+        st<true>(dst + w * n + i, acc);
+}
+
 inline dim3 grid_for(size_t n, int items)
 {
     const size_t lanes = (n + items - 1) / items;
@@ -151,6 +175,28 @@ int rfec_probe_write(void* dst, size_t bytes, unsigned flags, void* stream)
         else
             hipLaunchKernelGGL((k_write<false, 1>), grid_for(n, 1), dim3(kBlock), 0, s, b, n);
     }
+    return (int)hipGetLastError();
+}
+
+/* R : W streaming mix (see k_mix), stream_bytes per stream; (r, w) in
+   {(10, 3), (10, 7), (4, 1), (1, 1)}; -1 for another pair */
+int rfec_probe_mix(const void* src, void* dst, size_t stream_bytes, unsigned r, unsigned w, void* stream)
+{
+    const size_t n = stream_bytes / 16;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const v4u* a = reinterpret_cast<const v4u*>(src);
+    v4u* b = reinterpret_cast<v4u*>(dst);
+    const dim3 g = grid_for(n, 1);
+    if (r == 10 && w == 3)
+        hipLaunchKernelGGL((k_mix<10, 3>), g, dim3(kBlock), 0, s, a, b, n);
+    else if (r == 10 && w == 7)
+        hipLaunchKernelGGL((k_mix<10, 7>), g, dim3(kBlock), 0, s, a, b, n);
+    else if (r == 4 && w == 1)
+        hipLaunchKernelGGL((k_mix<4, 1>), g, dim3(kBlock), 0, s, a, b, n);
+    else if (r == 1 && w == 1)
+        hipLaunchKernelGGL((k_mix<1, 1>), g, dim3(kBlock), 0, s, a, b, n);
+    else
+        return -1;
     return (int)hipGetLastError();
 }
 

@@ -226,6 +226,7 @@ _SIGS = {
     "rfec_probe_read": (C.c_int, [_P, C.c_size_t, _P, C.c_uint, _P]),
     "rfec_probe_copy": (C.c_int, [_P, _P, C.c_size_t, C.c_uint, _P]),
     "rfec_probe_write": (C.c_int, [_P, C.c_size_t, C.c_uint, _P]),
+    "rfec_probe_mix": (C.c_int, [_P, _P, C.c_size_t, C.c_uint, C.c_uint, _P]),
     "rfec_fill_xorshift": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P]),
     "rfec_xorshift_jump": (C.c_uint64, [C.c_uint64, C.c_uint64]),
     "rfec_udp_open": (C.c_int, [C.c_char_p, C.c_uint16, C.c_uint, C.c_uint32, C.POINTER(C.c_int),

@@ -117,7 +117,7 @@ def test_bench_two_ranks_one_gpu():
     plane) on the one GPU: one JSON line, weak scaling of config 3 (the N = 1
     workload on each rank's own 65,536 groups), every rank's groups equal to
     the reference digest of exactly those groups."""
-    d = _bench("--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu", "--sets", "2")
+    d = _bench("--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu", "--sets", "2", "--c4-steps", "2")
     assert d["n_gpus"] == 2 and d["scaling"] == "weak"
     assert d["config"]["config"] == "c3" and d["config"]["groups_per_gpu"] == 65536
     assert d["config"]["total_groups"] == 2 * 65536
@@ -127,6 +127,29 @@ def test_bench_two_ranks_one_gpu():
     # one kernel per call: the roofline takes each kernel's own start / stop events
     for key in ("roofline", "decode_roofline"):
         assert d[key]["timing"].startswith("the kernel's own") and d[key]["launch_us"] > 0
+    _check_c4_strong(d["c4_strong"], 2)
+
+
+def _check_c4_strong(c4, n):
+    """The driver's default line carries BASELINE configs[3] too: the 1M
+    groups split over the n ranks, each slice equal to the reference's."""
+    assert c4["scaling"] == "strong" and c4["workload"].startswith("c4: k10_r3_S1200_G1048576")
+    assert c4["groups_per_rank"] == [1048576 // n] * n
+    assert c4["verified"] is True and c4["verified_vs_reference_digest"] is True
+    assert c4["value"] > 0 and len(c4["encode_launch_us_per_rank"]) == n
+    assert all(t > 0 for t in c4["encode_launch_us_per_rank"] + c4["decode_launch_us_per_rank"])
+
+
+@pytest.mark.timeout(600)
+def test_bench_one_gpu_c4_strong():
+    """The default N = 1 line: weak c3 as `value`, plus the c4_strong object
+    over all 1,048,576 groups on the one GPU (the N = 1 point of the strong
+    curve), bit-exact against the reference's c4 digest."""
+    d = _bench("--gpus", "1", "--steps", "3", "--warmup", "1", "--no-cpu", "--c4-steps", "2")
+    assert d["n_gpus"] == 1 and d["scaling"] == "weak" and d["config"]["config"] == "c3"
+    assert d["verified_vs_reference_digest"] is True
+    _check_c4_strong(d["c4_strong"], 1)
+    assert d["roofline"]["mix_ceiling"]["probe"].startswith("rfec_probe_mix 10 reads : 3 writes")
 
 
 @pytest.mark.timeout(900)
