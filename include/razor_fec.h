@@ -618,8 +618,9 @@ int rfec_rx_session_get_info(const rfec_rx_session* s, rfec_rx_session_info* inf
 /* RFEC_TUNE_NO_SERVICE: the drop-in symbols (flex_fec_generate / _recover, the
  * group-level sender and receiver) launch their kernels per call instead of
  * posting to the resident service (process-wide; also RFEC_SERVICE=0 in the
- * environment). */
-#define RFEC_TUNE_NO_SERVICE 2u
+ * environment).  Bit 30, so that no value of the round-1/2 tuning bits
+ * (1u << 1 .. 1u << 24, now ignored) turns the service off. */
+#define RFEC_TUNE_NO_SERVICE (1u << 30)
 void rfec_set_tuning(unsigned flags);
 unsigned rfec_get_tuning(void);
 

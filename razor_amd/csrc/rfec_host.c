@@ -545,12 +545,22 @@ static double now_us(void);
  * workgroup stays on the device and polls a doorbell in pinned, host-coherent
  * memory; a call stages its segments next to the doorbell, bumps `req` and
  * spins on `done` (a few PCIe round trips).  The workgroup leaves after
- * RFEC_SERVICE_IDLE_US without a job, after one second in total, on `stop`
- * (rfec_service_stop, atexit); a call that finds `alive` == 0 launches it
- * again.  One service per process, calls serialised by its mutex. */
+ * RFEC_SERVICE_IDLE_US (default 2 ms) without a job, after
+ * RFEC_SERVICE_LIFE_US (default 4 ms) in total, on `stop` (rfec_service_stop,
+ * atexit); a call that finds `alive` == 0 launches it again (~10-20 us for
+ * that call).  The lifetime bounds what the resident kernel can hold up: a
+ * device-wide synchronize (hipDeviceSynchronize, torch.cuda.synchronize)
+ * waits for it, and so would any kernel queued behind it on a shared
+ * hardware queue -- which is why its stream is created with a CU mask: a
+ * CU-masked stream gets a hardware queue of its own (the mask is a queue
+ * property), so no other stream's kernels sit behind the service
+ * (tests/test_service.py times torch kernels while it is resident).  One
+ * service per process, calls serialised by its mutex. */
 typedef struct {
     pthread_mutex_t mu;
-    int state; /* 0 not set up, 1 ready, -1 unavailable (per-call launches) */
+    int state;     /* 0 not set up, 1 ready, -1 unavailable (per-call launches), -2 timed out: a launch may
+                      still be live (stop set); retried after 1 s once its stream is idle */
+    double t_fail; /* when it timed out */
     hipStream_t stream;
     rfec_svc_ctl* ctl;   /* host view; the staging slots follow it */
     uint8_t* dev;        /* device view of the same allocation */
@@ -561,7 +571,8 @@ typedef struct {
     double tick_us;                                  /* s_memrealtime period */
     double t_stage, t_wait, t_dstage, t_dwork, t_drel; /* sums over the jobs, us */
 } svc_state;
-static svc_state g_svc = {PTHREAD_MUTEX_INITIALIZER, 0, NULL, NULL, NULL, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+static svc_state g_svc = {PTHREAD_MUTEX_INITIALIZER, 0, 0, NULL, NULL, NULL, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                          0};
 
 static void svc_pause(void)
 {
@@ -573,7 +584,7 @@ static void svc_pause(void)
 /* mutex held; leaves the workgroup off the device */
 static int svc_stop_locked(void)
 {
-    if (g_svc.state != 1)
+    if (g_svc.state != 1 && g_svc.state != -2)
         return RFEC_OK;
     __atomic_store_n(&g_svc.ctl->stop, 1u, __ATOMIC_RELEASE);
     const hipError_t e = hipStreamSynchronize(g_svc.stream);
@@ -635,9 +646,24 @@ static int svc_acquire(void)
         const size_t o_parity = o_shards + svc_align((size_t)RFEC_SVC_SLOTS * DI_STRIDE);
         const size_t bytes = o_parity + svc_align((size_t)RFEC_MAX_LINES * DI_STRIDE);
         void* h = NULL;
+        int ncu = 0;
         if ((e = hipGetDeviceCount(&n)) != hipSuccess || n == 0 || (e = hipGetDevice(&dev)) != hipSuccess ||
             (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev)) != hipSuccess || khz <= 0 ||
-            (e = hipStreamCreateWithFlags(&g_svc.stream, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) {
+            set_err(RFEC_EDEVICE, "service setup", e);
+            pthread_mutex_unlock(&g_svc.mu);
+            return 0;
+        }
+        /* a hardware queue of its own: a stream with a CU mask (every CU) */
+        uint32_t mask[32];
+        const uint32_t nw = ncu > 0 && ncu <= 1024 ? ((uint32_t)ncu + 31) / 32 : 0;
+        for (uint32_t i = 0; i < nw; ++i)
+            mask[i] = (uint32_t)ncu >= 32 * (i + 1) ? 0xFFFFFFFFu : (1u << ((uint32_t)ncu - 32 * i)) - 1u;
+        if (!nw || hipExtStreamCreateWithCUMask(&g_svc.stream, nw, mask) != hipSuccess) {
+            (void)hipGetLastError();
+            g_svc.stream = NULL;
+        }
+        if ((!g_svc.stream && (e = hipStreamCreateWithFlags(&g_svc.stream, hipStreamNonBlocking)) != hipSuccess) ||
             (e = hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
             (e = hipHostGetDevicePointer((void**)&g_svc.dev, h, 0)) != hipSuccess) {
             set_err(RFEC_EDEVICE, "service setup", e);
@@ -651,8 +677,11 @@ static int svc_acquire(void)
         g_svc.o_shards = o_shards;
         g_svc.o_parity = o_parity;
         const char* idle = getenv("RFEC_SERVICE_IDLE_US");
-        const double idle_us = idle && atof(idle) > 0 ? atof(idle) : 20000.0;
+        const char* life = getenv("RFEC_SERVICE_LIFE_US");
+        const double idle_us = idle && atof(idle) > 0 ? atof(idle) : 2000.0;
+        const double life_us = life && atof(life) > 0 ? atof(life) : 4000.0;
         g_svc.idle_ticks = (uint64_t)(idle_us * khz / 1000.0);
+        g_svc.life_ticks = (uint64_t)(life_us * khz / 1000.0);
         g_svc.tick_us = 1000.0 / khz;
         /* workgroups: 1 (tools/svc_groups.sh: 1 / 2 / 4 / 8 took 12.8 / 15.9 / 12.8 / 14.4 us per group
          * encode on one box; more CUs shorten the XOR + stores, 2.0 -> 1.35 us, but not the PCIe round
@@ -660,9 +689,16 @@ static int svc_acquire(void)
         const char* grp = getenv("RFEC_SERVICE_GROUPS");
         const int ng = grp ? atoi(grp) : 1;
         g_svc.groups = ng >= 1 && ng <= RFEC_SVC_MAX_GROUPS ? (uint32_t)ng : 1u;
-        g_svc.life_ticks = (uint64_t)khz * 1000u; /* one second */
         g_svc.state = 1;
         atexit(svc_atexit);
+    }
+    if (g_svc.state == -2 && now_us() - g_svc.t_fail > 1e6 && hipStreamQuery(g_svc.stream) == hipSuccess) {
+        /* the timed-out launch has left: take the service up again */
+        g_svc.ctl->stop = 0;
+        g_svc.ctl->quit = 0;
+        g_svc.ctl->alive = 0;
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
+        g_svc.state = 1;
     }
     if (g_svc.state != 1) {
         pthread_mutex_unlock(&g_svc.mu);
@@ -722,9 +758,12 @@ static int svc_run(uint32_t n_slots, uint32_t op, double t_begin)
             ++g_svc.launches;
         }
         if ((spin & 4095) == 4095 && now_us() - t0 > 5e6) {
-            /* no answer in 5 s: stop using the service (the workgroup leaves
-             * within its one-second lifetime) */
-            g_svc.state = -1;
+            /* no answer in 5 s: tell any live launch to leave (it may still
+             * take the job; rfec_service_stop / atexit synchronise its
+             * stream), fall back to per-call launches, retry in 1 s */
+            __atomic_store_n(&q->stop, 1u, __ATOMIC_RELEASE);
+            g_svc.state = -2;
+            g_svc.t_fail = now_us();
             return set_err(RFEC_EDEVICE, "service timeout", 0);
         }
         svc_pause();

@@ -105,11 +105,7 @@ __device__ __forceinline__ void stage_tile(const SvcArgs& A, uint32_t ns, uint32
     // waits on each load before issuing the next)
     const __amdgpu_buffer_rsrc_t rc = sys_rsrc(A.ctl, sizeof(rfec_svc_ctl));
     const __amdgpu_buffer_rsrc_t rs = sys_rsrc(A.shards, RFEC_SVC_SLOTS * A.C * 16u);
-#ifdef RFEC_SVC_FULL_JOB // A/B: the whole description
-    const uint32_t njr = njmax;
-#else
     const uint32_t njr = nj;
-#endif
 #pragma unroll
     for (uint32_t u = 0; u < UJ; ++u)
         t[u] = ld_job(rc, CTL_OFF(job) + 16u * min(u * kSvcBlock + threadIdx.x, njr - 1));
@@ -253,7 +249,8 @@ __device__ void svc_job(const SvcArgs& A, uint32_t ns, uint32_t c0, uint32_t c1,
 // staging spread over several CUs.  Workgroup 0 leads: it writes the header
 // results and the timing, and it alone decides to leave (idle / lifetime):
 // `quit`, then `alive` = 0; the others leave on `quit` or `stop` (and, as a
-// backstop, 0.1 s after the lifetime).  Every workgroup answers in done[w].
+// backstop only, after ten lifetimes: a non-leader that started late must not
+// leave while `alive` is 1).  Every workgroup answers in done[w].
 __global__ __launch_bounds__(kSvcBlock) void k_service(SvcArgs A)
 {
     __shared__ __attribute__((aligned(16))) v4u lds[kSvcLdsChunks];
@@ -265,7 +262,7 @@ __global__ __launch_bounds__(kSvcBlock) void k_service(SvcArgs A)
     const bool leader = w == 0;
     const uint32_t c0 = A.C * w / nw, c1 = A.C * (w + 1) / nw;
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    const uint64_t life = leader ? A.life_ticks : A.life_ticks + A.life_ticks / 10;
+    const uint64_t life = leader ? A.life_ticks : 10 * A.life_ticks;
     uint64_t t_last = t_start;
     uint32_t done = poll_u32(&A.ctl->done[w]);
     for (;;) {

@@ -30,7 +30,7 @@ RFEC_MAX_LINES = 64
 RFEC_LAYER_ROWS = 1
 RFEC_LAYER_COLS = 2
 RFEC_TUNE_GENERIC = 1
-RFEC_TUNE_NO_SERVICE = 2
+RFEC_TUNE_NO_SERVICE = 1 << 30
 
 # 20-byte header record == sim_fec_meta_t layout (sim_proto.h:145-155)
 HDR_DTYPE = np.dtype([("seq", "<u4"), ("fid", "<u4"), ("ts", "<u4"), ("index", "<u2"), ("total", "<u2"),

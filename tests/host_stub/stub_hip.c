@@ -124,6 +124,18 @@ hipError_t hipStreamSynchronize(hipStream_t s)
     (void)s;
     return hipSuccess;
 }
+hipError_t hipStreamQuery(hipStream_t s)
+{
+    (void)s;
+    return hipSuccess;
+}
+hipError_t hipExtStreamCreateWithCUMask(hipStream_t* s, uint32_t n, const uint32_t* mask)
+{
+    (void)n;
+    (void)mask;
+    *s = (hipStream_t)malloc(1);
+    return hipSuccess;
+}
 hipError_t hipEventCreate(hipEvent_t* e)
 {
     *e = (hipEvent_t)malloc(1);

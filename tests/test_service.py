@@ -42,3 +42,75 @@ def test_service_stop_and_relaunch(product, oracle1000):
     finally:
         L.flex_fec_sender_destroy(snd)
         assert L.rfec_service_stop() == 0
+
+
+_HOL_SCRIPT = r"""
+import json, sys, time
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import torch
+import pyoracle as po
+from razor_amd.fec import native
+from test_flex_dropin import CASES, bind_flex, make_segments, sender_group
+
+lib = bind_flex(native(1000))
+L = lib.lib
+c = CASES["k10_pf80_S1000"]
+shards, hdr = po.Oracle(1000).fill_groups(c["config_id"], 1, c["k"], c["S"], ragged=c["ragged"])
+snd = L.flex_fec_sender_create()
+dev = torch.device("cuda", 0)
+x = torch.ones(1 << 20, device=dev)
+streams = [torch.cuda.Stream(dev) for _ in range(8)]
+for s in streams:  # warm every stream up before the service is resident
+    with torch.cuda.stream(s):
+        x.mul_(1.0)
+    s.synchronize()
+t_call = time.perf_counter()
+sender_group(lib, snd, make_segments(lib, shards[0], hdr[0]), c["protect_fraction"])
+waits = []
+for s in streams + [torch.cuda.current_stream(dev)]:
+    t0 = time.perf_counter()
+    with torch.cuda.stream(s):
+        x.mul_(1.0)
+    s.synchronize()
+    waits.append(time.perf_counter() - t0)
+t0 = time.perf_counter()
+torch.cuda.synchronize()
+sync = time.perf_counter() - t0
+L.flex_fec_sender_destroy(snd)
+assert L.rfec_service_stop() == 0
+print(json.dumps({"stream_waits_s": waits, "device_sync_s": sync, "since_call_s": time.perf_counter() - t_call}))
+"""
+
+
+@pytest.mark.parametrize("life_us", [1_500_000, None])
+def test_service_does_not_hold_other_streams(tmp_path, life_us):
+    """While the resident service runs, kernels on other streams (8 torch
+    streams and the current one: more than the GPU_MAX_HW_QUEUES = 4 hardware
+    queues they share) still finish at once -- the service has a CU-masked
+    stream, i.e. a hardware queue of its own.  A device-wide synchronize does
+    wait for it: with a 1.5-s lifetime it takes about that long, with the
+    default lifetime (4 ms) a few ms at most."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ)
+    env.pop("RFEC_SERVICE", None)
+    if life_us:
+        env.update(RFEC_SERVICE_LIFE_US=str(life_us), RFEC_SERVICE_IDLE_US=str(life_us))
+    else:
+        env.pop("RFEC_SERVICE_LIFE_US", None)
+        env.pop("RFEC_SERVICE_IDLE_US", None)
+    r = subprocess.run([sys.executable, "-c", _HOL_SCRIPT, str(root), str(root / "tests"),
+                        ], capture_output=True, text=True, timeout=120, env=env,
+                       cwd=str(root / "oracle"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert max(d["stream_waits_s"]) < 0.1, d
+    if life_us:
+        assert 0.5 < d["since_call_s"] < 5.0, d  # the service really was resident meanwhile
+    else:
+        assert d["device_sync_s"] < 0.05, d
