@@ -98,7 +98,7 @@ static void scenario_x(const char* name, uint64_t id, const frame_t* frames, int
     fprintf(js, "],\n   \"groups\": [");
     for (int f = 0; f < nf; ++f) {
         const frame_t* fr = &frames[f];
-        static uint8_t fbuf[200 * SIM_VIDEO_SIZE];
+        static uint8_t fbuf[1100 * SIM_VIDEO_SIZE];
         for (uint32_t b = 0; b < fr->size; b += 8) {
             uint64_t v = oracle_xs_next(&st);
             for (uint32_t q = 0; q < 8 && b + q < fr->size; ++q)
@@ -293,6 +293,15 @@ int main(int argc, char** argv)
         fr[i] = (frame_t){(130u + (uint32_t)(i * 37 % 71)) * SIM_VIDEO_SIZE - 11u * (uint32_t)i, (uint8_t)(i % 20 == 0),
                           97, (uint8_t)(i % 5 == 0 ? 30 : 80)};
     scenario("peer_large_groups", 7, fr, 40, 60, 80, 24, 10, 0, 1);
+    /* a foreign peer's groups above 255 segments (one group per frame of
+     * 300-1,000 segments): planes of up to 50 rows x 20 columns, 70 lines at
+     * 1,000 (flex_fec_sender.c:81-135 clamps the column count to 20), deep
+     * row / column cascades */
+    g_flush_at = 1100;
+    for (int i = 0; i < 10; ++i)
+        fr[i] = (frame_t){(300u + (uint32_t)(i * 131 % 701)) * SIM_VIDEO_SIZE - 17u * (uint32_t)i, (uint8_t)(i == 0),
+                          97, 80};
+    scenario("peer_huge_groups", 8, fr, 10, 50, 60, 30, 10, 0, 0);
     g_flush_at = 100;
     fprintf(js, "\n]}\n");
     fclose(js);

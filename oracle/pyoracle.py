@@ -484,6 +484,12 @@ def rx_items(oracle, frames, blob, segs, groups, video_size=1000):
         k, pf = int(g["count"]), int(g["protect_fraction"])
         if int(g["first_seg"]) < 0 or k == 0:
             continue
+        if k > 255:  # above the 8-bit plan lines: the sender's lines restated here
+            for r in _big_group_parities(oracle, seg_rec, seg_pay, g, k, pf):
+                par_rec.append(r[0])
+                par_pay.append(r[1])
+                par_group.append(gi)
+            continue
         plan = oracle.plan_from_fraction(k, pf, 3)
         mem = segs[int(g["first_seg"]):int(g["first_seg"]) + k]
         hdr = np.zeros((1, k), HDR_DTYPE)
@@ -503,6 +509,43 @@ def rx_items(oracle, frames, blob, segs, groups, video_size=1000):
             par_pay.append(par[0, l])
             par_group.append(gi)
     return seg_rec, seg_pay, par_rec, par_pay, par_group
+
+
+def _big_group_parities(oracle, seg_rec, seg_pay, g, k, pf):
+    """The parities flex_fec_sender_update emits for a group of k > 255
+    segments (flex_fec_sender.c:146-245): the planner's (row, col)
+    (oracle_num_packets, :81-135); with col > 1, one parity per row over
+    segments [r col, min(k, (r + 1) col)), index r (:157-188), and in matrix
+    mode with row > 1 one per column over r col + c < k, index 0x80 | c
+    (:199-233); a
+    line of fewer than 2 members emits none (flex_fec_xor.c:9-10).  Each
+    parity = flex_fec_generate: payload XOR zero-padded to L = max data_size,
+    meta = XOR of the 20-byte headers (flex_fec_xor.c:13-50)."""
+    rc, row, col = oracle.num_packets(k, pf)
+    f0 = int(g["first_seg"])
+    hdr32 = seg_rec["hdr"][f0:f0 + k].copy().view(np.uint32).reshape(k, 5)
+    pay = seg_pay[f0:f0 + k]
+    sizes = seg_rec["data_size"][f0:f0 + k].astype(np.int64)
+    lines = [(list(range(r * col, min(k, (r + 1) * col))), r) for r in range(row)] if col > 1 else []
+    if col > 1 and row > 1 and rc == 1:
+        lines += [([r * col + c for r in range(row) if r * col + c < k], 0x80 | c) for c in range(col)]
+    out = []
+    for mem, index in lines:
+        if len(mem) < 2:
+            continue
+        L = int(sizes[mem].max())
+        pp = np.bitwise_xor.reduce(pay[mem], axis=0)
+        pp[L:] = 0
+        m = np.bitwise_xor.reduce(hdr32[mem], axis=0)
+        r = np.zeros((), WIRE_REC)
+        r["mid"], r["ver"] = 0x1C, 1
+        r["fec_id"], r["base_id"], r["count"] = g["fec_id"], g["base_id"], k
+        r["row"], r["col"], r["index"] = row, col, index
+        r["send_ts"] = 33 * int(seg_rec["hdr"]["ts"][f0 + k - 1] // 33)
+        r["hdr"] = m.view(r["hdr"].dtype)[0]
+        r["data_size"] = L
+        out.append((r, pp))
+    return out
 
 
 def _gather_arrivals(arr, items, stride):

@@ -659,7 +659,15 @@ static int svc_acquire(void)
         const uint32_t nw = ncu > 0 && ncu <= 1024 ? ((uint32_t)ncu + 31) / 32 : 0;
         for (uint32_t i = 0; i < nw; ++i)
             mask[i] = (uint32_t)ncu >= 32 * (i + 1) ? 0xFFFFFFFFu : (1u << ((uint32_t)ncu - 32 * i)) - 1u;
-        if (!nw || hipExtStreamCreateWithCUMask(&g_svc.stream, nw, mask) != hipSuccess) {
+        const char* sk = getenv("RFEC_SERVICE_STREAM"); /* LAB: cumask | prio | plain */
+        if (sk && sk[0] == 'p' && sk[1] == 'r') {
+            int lo = 0, hi = 0;
+            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+                hipStreamCreateWithPriority(&g_svc.stream, hipStreamNonBlocking, hi) != hipSuccess) {
+                (void)hipGetLastError();
+                g_svc.stream = NULL;
+            }
+        } else if ((!sk || sk[0] == 'c') && (!nw || hipExtStreamCreateWithCUMask(&g_svc.stream, nw, mask) != hipSuccess)) {
             (void)hipGetLastError();
             g_svc.stream = NULL;
         }
@@ -1970,6 +1978,9 @@ static void hm_del(hmap* m, uint32_t k) /* backward-shift deletion */
 
 typedef struct {
     uint32_t count, row, col, n_groups, n_lines, row0, prow0, group0;
+    uint32_t huge;        /* count > RX_MAX_COUNT or more than RFEC_MAX_LINES lines: no plan; line l = FEC
+                             index l (members by rx_line_members), n_lines 256, peeled by the host into
+                             line jobs (rx_big_peel) */
     uint64_t xcol[2];     /* columns c >= col a peer's parities named (bit c) */
     int16_t line_of[256]; /* FEC index -> plan line, -1: none */
     rfec_plan plan;
@@ -1978,12 +1989,12 @@ typedef struct {
 /* one flex receiver (flex_fec_receiver_t) from its creation to its removal */
 typedef struct {
     uint32_t fec_id, base, count, row, col;
-    uint32_t shape;        /* UINT32_MAX: geometry the reference ignores or the planner cannot express */
+    uint32_t shape;        /* UINT32_MAX: geometry the reference ignores (col < 2, row 0, count 0) */
     uint32_t gslot, slot0, line0;
     uint32_t nsegs;        /* flex->segs.n */
-    uint64_t have[4];      /* members in the flex (arrived or recovered), count <= RX_MAX_COUNT */
-    uint64_t arrived[4];   /* members that arrived: the device peel starts from these */
-    uint64_t ppm;          /* registered parities, by plan line */
+    uint64_t have[4];      /* members in the flex (arrived or recovered); huge shapes: rx_has */
+    uint64_t arrived[4];   /* members that arrived: the device peel starts from these (huge: slot_src) */
+    uint64_t ppm;          /* registered parities, by plan line (huge: line_par >= 0) */
     uint32_t fec_ts;       /* flex->fec_ts = send_ts of the parity that created it (sim_fec.c:157) */
     int ref_ok;            /* col >= 2 && row >= 1 && count >= 1 (flex_fec_receiver.c:214, 250) */
     uint32_t gstamp;       /* == rx_sim.epoch: gslot is this device call's group slot */
@@ -2048,6 +2059,52 @@ static rfec_hdr rec_hdr(const rfec_wire_rec* r)
     return h;
 }
 
+/* members of the reference's line `index` of a (count, row, col) flex:
+ * flex_recover_row walks i < col, flex_recover_col i < row, both stopping at
+ * the first position >= count (flex_fec_receiver.c:118-126, 175-183) */
+static uint32_t rx_line_members(uint32_t count, uint32_t row, uint32_t col, uint32_t index, uint32_t* first,
+                                uint32_t* stride)
+{
+    const uint32_t x = index & 0x7Fu;
+    uint32_t n = 0;
+    if (index & 0x80u) {
+        while (n < row && n * col + x < count)
+            ++n;
+        *first = x;
+        *stride = col;
+    } else {
+        while (n < col && x * col + n < count)
+            ++n;
+        *first = x * col;
+        *stride = 1;
+    }
+    return n;
+}
+
+/* line l of flex g: its members and whether its parity is registered */
+static uint32_t rx_line(const rx_sim* X, const rx_inst* g, uint32_t l, uint32_t* first, uint32_t* stride, int* reg)
+{
+    const rx_shape* sh = &X->S[g->shape];
+    if (sh->huge) {
+        *reg = X->line_par[g->line0 + l] >= 0;
+        return rx_line_members(g->count, g->row, g->col, l, first, stride);
+    }
+    const rfec_line* ln = &sh->plan.line[l];
+    *reg = (int)((g->ppm >> l) & 1ull);
+    *first = ln->first;
+    *stride = ln->stride;
+    return ln->count;
+}
+
+/* member t of flex g is in it (arrived or recovered); a huge flex's slot
+ * header holds the member's seq once it is in, ~(base + t) before */
+static int rx_has(const rx_sim* X, const rx_inst* g, uint32_t t)
+{
+    if (X->S[g->shape].huge)
+        return X->slot_hdr[g->slot0 + t].seq == g->base + t;
+    return (int)((g->have[t >> 6] >> (t & 63)) & 1ull);
+}
+
 static void rx_pend(rx_sim* X, const rfec_hdr* h, uint32_t inst) /* sim_fec_packet_add_recover (sim_fec.c:104-119) */
 {
     for (uint32_t i = 0; i < X->npend; ++i)
@@ -2064,13 +2121,16 @@ static void rx_pend(rx_sim* X, const rfec_hdr* h, uint32_t inst) /* sim_fec_pack
 static void rx_check_line(rx_sim* X, uint32_t ii, int l)
 {
     const rx_inst* g = &X->G[ii];
-    if (l < 0 || g->nsegs >= g->count || !((g->ppm >> l) & 1ull))
+    if (l < 0 || g->nsegs >= g->count)
         return;
-    const rfec_line* ln = &X->S[g->shape].plan.line[l];
+    uint32_t first, stride;
+    int reg;
+    const uint32_t n = rx_line(X, g, (uint32_t)l, &first, &stride, &reg);
+    if (!reg)
+        return;
     uint32_t loss = 0, cnt = 0;
-    for (uint32_t q = 0; q < ln->count; ++q) {
-        const uint32_t i = ln->first + q * ln->stride;
-        if ((g->have[i >> 6] >> (i & 63)) & 1ull)
+    for (uint32_t q = 0; q < n; ++q) {
+        if (rx_has(X, g, first + q * stride))
             cnt++;
         else
             loss++;
@@ -2082,9 +2142,9 @@ static void rx_check_line(rx_sim* X, uint32_t ii, int l)
     if (L > X->capacity)
         return;
     rfec_hdr h = f->hdr; /* flex_fec_xor.c:64-99 */
-    for (uint32_t q = 0; q < ln->count; ++q) {
-        const uint32_t i = ln->first + q * ln->stride;
-        if (!((g->have[i >> 6] >> (i & 63)) & 1ull))
+    for (uint32_t q = 0; q < n; ++q) {
+        const uint32_t i = first + q * stride;
+        if (!rx_has(X, g, i))
             continue;
         const rfec_hdr* m = &X->slot_hdr[g->slot0 + i];
         if (L < m->size)
@@ -2115,12 +2175,14 @@ static void rx_on_segment(rx_sim* X, uint32_t ii, const rfec_hdr* h, int32_t src
     }
     const uint32_t t = h->seq - g->base;
     if (t < g->count) {
-        if ((g->have[t >> 6] >> (t & 63)) & 1ull)
+        if (rx_has(X, g, t))
             return;
-        g->have[t >> 6] |= 1ull << (t & 63);
+        if (!X->S[g->shape].huge)
+            g->have[t >> 6] |= 1ull << (t & 63);
         X->slot_hdr[g->slot0 + t] = *h;
         if (src >= 0) {
-            g->arrived[t >> 6] |= 1ull << (t & 63);
+            if (!X->S[g->shape].huge)
+                g->arrived[t >> 6] |= 1ull << (t & 63);
             X->slot_src[g->slot0 + t] = src;
         }
     } else if (src < 0) {
@@ -2161,28 +2223,6 @@ static void rx_put_segment(rx_sim* X, const rfec_hdr* h, uint16_t fec_id, uint32
         rx_remove(X, fi - 1);
 }
 
-/* members of the reference's line `index` of a (count, row, col) flex:
- * flex_recover_row walks i < col, flex_recover_col i < row, both stopping at
- * the first position >= count (flex_fec_receiver.c:118-126, 175-183) */
-static uint32_t rx_line_members(uint32_t count, uint32_t row, uint32_t col, uint32_t index, uint32_t* first,
-                                uint32_t* stride)
-{
-    const uint32_t x = index & 0x7Fu;
-    uint32_t n = 0;
-    if (index & 0x80u) {
-        while (n < row && n * col + x < count)
-            ++n;
-        *first = x;
-        *stride = col;
-    } else {
-        while (n < col && x * col + n < count)
-            ++n;
-        *first = x * col;
-        *stride = 1;
-    }
-    return n;
-}
-
 /* The device plan of a flex geometry: every row with 2+ members (also rows
  * at and beyond `row` when row * col < count: the reference bounds rows by
  * count only), every column c < col with 2+ members, and the extra columns
@@ -2220,14 +2260,17 @@ static int rx_build_plan(uint32_t count, uint32_t row, uint32_t col, const uint6
     return RFEC_OK;
 }
 
-/* flexes of up to 255 segments are modelled (a plan's lines have 8-bit
+/* flexes of up to 255 segments and 64 lines have a device plan (8-bit
  * members); above RFEC_MAX_K the device recovery takes line jobs (rx_big_peel)
- * instead of the batched peel, whose masks hold 128 members */
+ * instead of the batched peel, whose masks hold 128 members.  Larger flexes
+ * (a foreign peer's: the reference receiver takes any uint16_t count,
+ * flex_fec_receiver.c:69-88, and up to 128 rows and 128 columns of FEC
+ * indices) are huge shapes: line = FEC index, line jobs too. */
 #define RX_MAX_COUNT 255u
 
 static uint32_t rx_shape_of(rx_sim* X, uint32_t count, uint32_t row, uint32_t col, const uint64_t* xcol)
 {
-    if (count > RX_MAX_COUNT || row > 255 || col > 255)
+    if (row > 255 || col > 255)
         return UINT32_MAX;
     const int extended = xcol[0] || xcol[1];
     const uint32_t key = count << 16 | row << 8 | col;
@@ -2246,18 +2289,23 @@ static uint32_t rx_shape_of(rx_sim* X, uint32_t count, uint32_t row, uint32_t co
         return UINT32_MAX;
     rx_shape* sh = &X->S[X->ns];
     memset(sh, 0, sizeof(*sh));
-    if (rx_build_plan(count, row, col, xcol, &sh->plan))
-        return UINT32_MAX;
     sh->count = count;
     sh->row = row;
     sh->col = col;
     sh->xcol[0] = xcol[0];
     sh->xcol[1] = xcol[1];
-    sh->n_lines = sh->plan.n_lines;
-    for (int i = 0; i < 256; ++i)
-        sh->line_of[i] = -1;
-    for (uint32_t l = 0; l < sh->n_lines; ++l)
-        sh->line_of[sh->plan.line[l].index] = (int16_t)l;
+    sh->huge = count > RX_MAX_COUNT || rx_build_plan(count, row, col, xcol, &sh->plan) != RFEC_OK;
+    if (sh->huge) { /* every FEC index is a line */
+        sh->n_lines = 256;
+        for (int i = 0; i < 256; ++i)
+            sh->line_of[i] = (int16_t)i;
+    } else {
+        sh->n_lines = sh->plan.n_lines;
+        for (int i = 0; i < 256; ++i)
+            sh->line_of[i] = -1;
+        for (uint32_t l = 0; l < sh->n_lines; ++l)
+            sh->line_of[sh->plan.line[l].index] = (int16_t)l;
+    }
     if (!extended && hm_put(&X->shape_of, key, X->ns + 1)) {
         X->oom = 1;
         return UINT32_MAX;
@@ -2284,11 +2332,15 @@ static int rx_extend(rx_sim* X, uint32_t ii, uint32_t c)
         return -1;
     uint64_t ppm = 0;
     for (uint32_t l = 0; l < nsh->n_lines; ++l) {
-        const int ol = osh->line_of[nsh->plan.line[l].index];
-        X->line_par[X->nline + l] = ol >= 0 ? X->line_par[g->line0 + ol] : -1;
-        if (ol >= 0 && ((g->ppm >> ol) & 1ull))
+        const int ol = osh->line_of[nsh->huge ? l : nsh->plan.line[l].index];
+        X->line_par[X->nline + l] = ol >= 0 && ((g->ppm >> ol) & 1ull) ? X->line_par[g->line0 + ol] : -1;
+        if (ol >= 0 && ((g->ppm >> ol) & 1ull) && !nsh->huge)
             ppm |= 1ull << l;
     }
+    if (nsh->huge) /* more than RFEC_MAX_LINES lines now: membership moves to the slot headers (rx_has) */
+        for (uint32_t t = 0; t < g->count; ++t)
+            if (!((g->have[t >> 6] >> (t & 63)) & 1ull))
+                X->slot_hdr[g->slot0 + t].seq = ~(g->base + t);
     g->line0 = X->nline;
     X->nline += nsh->n_lines;
     g->ppm = ppm;
@@ -2330,8 +2382,10 @@ static void rx_put_fec(rx_sim* X, uint32_t a)
                 return;
             g->slot0 = X->nslot;
             g->line0 = X->nline;
-            for (uint32_t i = 0; i < g->count; ++i)
+            for (uint32_t i = 0; i < g->count; ++i) {
                 X->slot_src[X->nslot + i] = -1;
+                X->slot_hdr[X->nslot + i].seq = ~(g->base + i); /* rx_has: not in the flex */
+            }
             for (uint32_t l = 0; l < sh->n_lines; ++l)
                 X->line_par[X->nline + l] = -1;
             X->nslot += g->count;
@@ -2360,6 +2414,15 @@ static void rx_put_fec(rx_sim* X, uint32_t a)
     if (!g->ref_ok || g->shape == UINT32_MAX)
         return;
     int l = X->S[g->shape].line_of[f->index];
+    if (X->S[g->shape].huge) { /* line = index; the parity registered once */
+        uint32_t first, stride;
+        if (rx_line_members(g->count, g->row, g->col, f->index, &first, &stride) < 2 ||
+            X->line_par[g->line0 + l] >= 0)
+            return;
+        X->line_par[g->line0 + l] = (int32_t)a;
+        rx_check_line(X, fi - 1, l);
+        return;
+    }
     if (l < 0) {
         uint32_t first, stride;
         if (rx_line_members(g->count, g->row, g->col, f->index, &first, &stride) < 2)
@@ -2371,9 +2434,14 @@ static void rx_put_fec(rx_sim* X, uint32_t a)
         }
         g = &X->G[fi - 1];
     }
-    if ((g->ppm >> l) & 1ull)
-        return;
-    g->ppm |= 1ull << l;
+    if (X->S[g->shape].huge) { /* (the extension took it past RFEC_MAX_LINES lines) */
+        if (X->line_par[g->line0 + l] >= 0)
+            return;
+    } else {
+        if ((g->ppm >> l) & 1ull)
+            return;
+        g->ppm |= 1ull << l;
+    }
     X->line_par[g->line0 + l] = (int32_t)a;
     rx_check_line(X, fi - 1, l);
 }
@@ -2582,37 +2650,47 @@ static void rx_run(rx_sim* X, uint32_t a0, uint32_t n)
 }
 
 /* A group above RFEC_MAX_K segments (a foreign peer's flex): the canonical
- * peel (lines in plan order to a fixpoint, with flex_fec_recover's header
- * checks, flex_fec_xor.c:60-99) from its arrived members and registered
- * parities, over headers on the host; each firing becomes a line job the
- * device runs (rfec_launch_line_jobs).  job_of[t]: the job recovering member
- * t, or -1. */
-static void rx_big_peel(rx_sim* X, uint32_t gi, int32_t* job_of)
+ * peel (lines in plan order -- rows, then columns -- to a fixpoint, with
+ * flex_fec_recover's header checks, flex_fec_xor.c:60-99) from its arrived
+ * members and registered parities, over headers on the host; each firing
+ * becomes a line job the device runs (rfec_launch_line_jobs).  job_of[t]: the
+ * job recovering member t, or -1.  Returns -1 when out of memory. */
+static int rx_big_peel(rx_sim* X, uint32_t gi, int32_t* job_of)
 {
     const rx_inst* g = &X->G[gi];
-    const rfec_plan* P = &X->S[g->shape].plan;
-    const uint32_t k = g->count;
-    uint64_t have[4] = {g->arrived[0], g->arrived[1], g->arrived[2], g->arrived[3]};
-    static __thread rfec_hdr hd[RX_MAX_COUNT];
-    static __thread int32_t src[RX_MAX_COUNT];
-    static __thread uint16_t lvl[RX_MAX_COUNT];
+    const rx_shape* sh = &X->S[g->shape];
+    const uint32_t k = g->count, NL = sh->n_lines;
+    rfec_hdr* hd = (rfec_hdr*)malloc((size_t)k * sizeof(rfec_hdr));
+    int32_t* src = (int32_t*)malloc((size_t)k * sizeof(int32_t));
+    uint16_t* lvl = (uint16_t*)malloc((size_t)k * sizeof(uint16_t));
+    uint8_t* have = (uint8_t*)malloc(k);
+    if (!hd || !src || !lvl || !have) {
+        free(hd);
+        free(src);
+        free(lvl);
+        free(have);
+        return -1;
+    }
     for (uint32_t i = 0; i < k; ++i) {
         job_of[i] = -1;
         lvl[i] = 0;
         src[i] = X->slot_src[g->slot0 + i];
-        if ((have[i >> 6] >> (i & 63)) & 1ull)
+        have[i] = src[i] >= 0; /* the peel starts from the arrived members */
+        if (have[i])
             hd[i] = X->slot_hdr[g->slot0 + i];
     }
     for (int progress = 1; progress && !X->oom;) {
         progress = 0;
-        for (uint32_t l = 0; l < P->n_lines && !X->oom; ++l) {
-            if (!((g->ppm >> l) & 1ull))
+        for (uint32_t l = 0; l < NL && !X->oom; ++l) {
+            uint32_t first, stride;
+            int reg;
+            const uint32_t n = rx_line(X, g, l, &first, &stride, &reg);
+            if (!reg)
                 continue;
-            const rfec_line* ln = &P->line[l];
             uint32_t miss = 0, present = 0, t = 0;
-            for (uint32_t q = 0; q < ln->count; ++q) {
-                const uint32_t i = ln->first + q * ln->stride;
-                if ((have[i >> 6] >> (i & 63)) & 1ull) {
+            for (uint32_t q = 0; q < n; ++q) {
+                const uint32_t i = first + q * stride;
+                if (have[i]) {
                     present++;
                 } else {
                     miss++;
@@ -2628,8 +2706,8 @@ static void rx_big_peel(rx_sim* X, uint32_t gi, int32_t* job_of)
             rfec_hdr h = f->hdr;
             int ok = 1;
             uint16_t level = 0;
-            for (uint32_t q = 0; q < ln->count && ok; ++q) {
-                const uint32_t i = ln->first + q * ln->stride;
+            for (uint32_t q = 0; q < n && ok; ++q) {
+                const uint32_t i = first + q * stride;
                 if (i == t)
                     continue;
                 const rfec_hdr* m = &hd[i];
@@ -2650,14 +2728,14 @@ static void rx_big_peel(rx_sim* X, uint32_t gi, int32_t* job_of)
             RX_GROW(X->jlevel, X->njobs, X->jlevelcap, 1, uint16_t);
             RX_GROW(X->jmem, X->njmem, X->jmemcap, present, int32_t);
             if (X->oom)
-                return;
+                break;
             rfec_line_job* J = &X->jobs[X->njobs];
             J->out = (int32_t)X->njobs;
             J->parity = X->line_par[g->line0 + l];
             J->member0 = X->njmem;
             J->n_members = present;
-            for (uint32_t q = 0; q < ln->count; ++q) {
-                const uint32_t i = ln->first + q * ln->stride;
+            for (uint32_t q = 0; q < n; ++q) {
+                const uint32_t i = first + q * stride;
                 if (i != t)
                     X->jmem[X->njmem++] = src[i];
             }
@@ -2666,12 +2744,19 @@ static void rx_big_peel(rx_sim* X, uint32_t gi, int32_t* job_of)
             src[t] = -1 - (int32_t)X->njobs;
             lvl[t] = (uint16_t)(level + 1);
             hd[t] = h;
-            have[t >> 6] |= 1ull << (t & 63);
+            have[t] = 1;
             X->njobs++;
             progress = 1;
         }
     }
+    free(hd);
+    free(src);
+    free(lvl);
+    free(have);
+    return X->oom ? -1 : 0;
 }
+
+#define RX_MAX_LEVEL 256u
 
 /* The device side of one call: the groups that delivered something in this
  * call, rebuilt from their arrived members and registered parities (rows of
@@ -2742,24 +2827,26 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
         if (X->S[g->shape].count <= RFEC_MAX_K)
             continue;
         g->gslot = off; /* (a large group's slot: its job_of range) */
-        rx_big_peel(X, X->dl[d], job_of + off);
+        if (rx_big_peel(X, X->dl[d], job_of + off))
+            X->oom = 1;
         off += g->count;
     }
     if (X->oom) {
         free(job_of);
         return set_err(RFEC_ENOMEM, "rx: line jobs", 0);
     }
-    uint32_t lvl_n[65] = {0};
+    /* a line fires at most once, so a chain is at most as deep as a group has lines (256 FEC indices) */
+    uint32_t lvl_n[RX_MAX_LEVEL + 1] = {0};
     if (X->njobs) { /* stable sort by level; codes and job_of follow */
         for (uint32_t j = 0; j < X->njobs; ++j) {
-            if (X->jlevel[j] > 64) { /* deeper than any plan of <= 64 lines cascades */
+            if (X->jlevel[j] > RX_MAX_LEVEL) {
                 free(job_of);
                 return set_err(RFEC_EINVAL, "rx: line job chain too deep", 0);
             }
             maxlvl = X->jlevel[j] > maxlvl ? X->jlevel[j] : maxlvl;
             lvl_n[X->jlevel[j]]++;
         }
-        uint32_t start[66] = {0};
+        uint32_t start[RX_MAX_LEVEL + 2] = {0};
         for (uint32_t v = 1; v <= maxlvl; ++v)
             start[v + 1] = start[v] + lvl_n[v];
         jperm = (uint32_t*)malloc((size_t)X->njobs * sizeof(uint32_t));

@@ -129,6 +129,19 @@ hipError_t hipStreamQuery(hipStream_t s)
     (void)s;
     return hipSuccess;
 }
+hipError_t hipDeviceGetStreamPriorityRange(int* lo, int* hi)
+{
+    *lo = 0;
+    *hi = -1;
+    return hipSuccess;
+}
+hipError_t hipStreamCreateWithPriority(hipStream_t* s, unsigned int flags, int prio)
+{
+    (void)flags;
+    (void)prio;
+    *s = (hipStream_t)malloc(1);
+    return hipSuccess;
+}
 hipError_t hipExtStreamCreateWithCUMask(hipStream_t* s, uint32_t n, const uint32_t* mask)
 {
     (void)n;

@@ -116,3 +116,59 @@ def peer_stream(oracle, rng, n_groups=90, video_size=1000):
         pid += k
         ts += 33
     return np.array(recs, po.WIRE_REC), np.array(pays, np.uint8)
+
+
+def single_group_stream(oracle, k, pf, erase, tamper=None, seed=0, video_size=1000):
+    """One flex of k segments (packet ids 1..k, ragged sizes) and every parity
+    the reference sender emits for it (k <= 255: the oracle's plan + encode;
+    above: pyoracle's restatement of flex_fec_sender_update), arriving after
+    the segments not in `erase`.  tamper = (parity index, data_size): that
+    parity's fec_data_size is cut below a member's size, so flex_fec_recover
+    rejects its line (flex_fec_xor.c:88-89).  Returns (recs, pay)."""
+    rng = np.random.default_rng(seed)
+    stride = (video_size + 15) // 16 * 16
+    sizes = rng.integers(video_size // 2, video_size + 1, k)
+    pay = np.zeros((k, stride), np.uint8)
+    for i in range(k):
+        pay[i, :sizes[i]] = rng.integers(0, 256, sizes[i], dtype=np.uint8)
+    seg = np.zeros(k, po.WIRE_REC)
+    seg["mid"], seg["ver"], seg["remb"] = 0x17, 1, 0xFF
+    seg["hdr"]["seq"] = 1 + np.arange(k)
+    seg["hdr"]["fid"] = 1 + np.arange(k) // 10
+    seg["hdr"]["ts"] = 33 * (np.arange(k) // 10)
+    seg["hdr"]["index"] = np.arange(k) % 10
+    seg["hdr"]["total"] = 10
+    seg["hdr"]["payload_type"] = 96
+    seg["hdr"]["size"] = sizes
+    seg["data_size"] = sizes
+    seg["fec_id"] = 7
+    g = np.zeros((), po.GROUP_PLAN)
+    g["first_seg"], g["count"], g["fec_id"], g["base_id"], g["protect_fraction"] = 0, k, 7, 1, pf
+    if k > 255:
+        pars = po._big_group_parities(oracle, seg, pay, g, k, pf)
+    else:
+        plan = oracle.plan_from_fraction(k, pf, 3)
+        hdr = np.zeros((1, k), po.HDR_DTYPE)
+        hdr[0] = seg["hdr"]
+        par, meta, fs, _ = oracle.encode_batch(plan, pay[None], hdr, video_size)
+        pars = []
+        for l in range(plan.n_lines):
+            r = np.zeros((), po.WIRE_REC)
+            r["mid"], r["ver"] = 0x1C, 1
+            r["fec_id"], r["base_id"], r["count"] = 7, 1, k
+            r["row"], r["col"], r["index"] = plan.row, plan.col, plan.line[l].index
+            r["send_ts"] = int(seg["hdr"]["ts"][-1])
+            r["hdr"], r["data_size"] = meta[0, l], fs[0, l]
+            pars.append((r, par[0, l]))
+    recs, rows = [], []
+    for i in range(k):
+        if i not in erase:
+            recs.append(seg[i])
+            rows.append(pay[i])
+    for r, p in pars:
+        if tamper is not None and int(r["index"]) == tamper[0]:
+            r = r.copy()
+            r["data_size"] = tamper[1]
+        recs.append(r)
+        rows.append(p)
+    return np.array(recs, po.WIRE_REC), np.array(rows, np.uint8)

@@ -48,7 +48,7 @@ def _sorted(rows):
 
 
 @pytest.mark.parametrize("name", ["k10_loss10", "k10_loss25_dup", "mixed_loss15", "late_parities",
-                                  "peer_large_groups"])  # (flexes of 130-200 segments: line jobs)
+                                  "peer_large_groups", "peer_huge_groups"])  # (flexes of 130-200 and 300-1,000 segments: line jobs)
 def test_rx_reference_fixture(lib, oracle1000, name):
     scn = {s["name"]: s for s in po.rx_fixture()["scenarios"]}[name]
     recs, pay, _, _ = po.rx_stream(oracle1000, scn)
@@ -190,7 +190,7 @@ def _rows(out, outp):
 
 
 @pytest.mark.parametrize("name", ["k10_loss10", "mixed_loss15", "late_parities", "evict_late_segments",
-                                  "evict_lost_parities", "no_evict_late_segments", "peer_large_groups"])
+                                  "evict_lost_parities", "no_evict_late_segments", "peer_large_groups", "peer_huge_groups"])
 def test_rx_session_reference_fixture(lib, name):
     """The reference receiver's streams pushed in batches, with sim_fec_evict
     between batches where the scenario's heartbeat ran it: the same recovered
@@ -449,3 +449,24 @@ def test_rx_peer_geometry(lib, oracle1000, seed):
         a = b
     sess.close()
     assert _sorted(rows) == _sorted(rc.got_rows(eo, ep))
+
+
+@pytest.mark.parametrize("k,pf", [(200, 80), (600, 80), (1000, 80)])
+def test_rx_large_group_cascades_and_rejection(lib, oracle1000, k, pf):
+    """Flexes above RFEC_MAX_K (line jobs; above 255 segments and 64 lines:
+    huge shapes, lines by FEC index): a recovery two levels deep (members 0
+    and 1 of row 0 lost with member `col` of row 1: row 1 recovers `col`, then
+    column 0 recovers 0 -- column 1 recovers 1 directly), a row parity whose
+    fec_data_size is cut below a member's size (flex_fec_xor.c:88-89: its
+    line is rejected, its lost member comes back through its column), and
+    scattered single losses.  Delivered rows equal the event-by-event
+    oracle's, nothing unmodelled."""
+    _, row, col = oracle1000.num_packets(k, pf)
+    erase = {0, 1, col, 2 * col + 3, 5 * col + 7, 9 * col + 1}
+    recs, pay = rc.single_group_stream(oracle1000, k, pf, erase, tamper=(2, 1), seed=k)
+    out, outp, _, rep = _rx(lib, recs, pay)
+    o_out, o_pay, _, _ = oracle1000.rx_recover(recs, pay, 1000)
+    assert rep.n_unmodelled == 0
+    assert _sorted(rc.got_rows(out, outp)) == _sorted(rc.got_rows(o_out, o_pay))
+    got = {int(s) for s in out["hdr"]["seq"]}
+    assert {1, 2, col + 1, 2 * col + 4} <= got  # the two-level chain and the rejected row's member
