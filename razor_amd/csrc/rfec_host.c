@@ -551,11 +551,11 @@ static double now_us(void);
  * that call).  The lifetime bounds what the resident kernel can hold up: a
  * device-wide synchronize (hipDeviceSynchronize, torch.cuda.synchronize)
  * waits for it, and so would any kernel queued behind it on a shared
- * hardware queue -- which is why its stream is created with a CU mask: a
- * CU-masked stream gets a hardware queue of its own (the mask is a queue
- * property), so no other stream's kernels sit behind the service
- * (tests/test_service.py times torch kernels while it is resident).  One
- * service per process, calls serialised by its mutex. */
+ * hardware queue -- which is why its stream is a non-blocking stream of the
+ * highest priority: a queue of its own, so no other stream's kernels sit
+ * behind the service (tests/test_service.py times torch kernels on 9 streams
+ * while it is resident).  One service per process, calls serialised by its
+ * mutex. */
 typedef struct {
     pthread_mutex_t mu;
     int state;     /* 0 not set up, 1 ready, -1 unavailable (per-call launches), -2 timed out: a launch may
@@ -646,28 +646,22 @@ static int svc_acquire(void)
         const size_t o_parity = o_shards + svc_align((size_t)RFEC_SVC_SLOTS * DI_STRIDE);
         const size_t bytes = o_parity + svc_align((size_t)RFEC_MAX_LINES * DI_STRIDE);
         void* h = NULL;
-        int ncu = 0;
         if ((e = hipGetDeviceCount(&n)) != hipSuccess || n == 0 || (e = hipGetDevice(&dev)) != hipSuccess ||
-            (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev)) != hipSuccess || khz <= 0 ||
-            (e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) {
+            (e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev)) != hipSuccess || khz <= 0) {
             set_err(RFEC_EDEVICE, "service setup", e);
             pthread_mutex_unlock(&g_svc.mu);
             return 0;
         }
-        /* a hardware queue of its own: a stream with a CU mask (every CU) */
-        uint32_t mask[32];
-        const uint32_t nw = ncu > 0 && ncu <= 1024 ? ((uint32_t)ncu + 31) / 32 : 0;
-        for (uint32_t i = 0; i < nw; ++i)
-            mask[i] = (uint32_t)ncu >= 32 * (i + 1) ? 0xFFFFFFFFu : (1u << ((uint32_t)ncu - 32 * i)) - 1u;
-        const char* sk = getenv("RFEC_SERVICE_STREAM"); /* LAB: cumask | prio | plain */
-        if (sk && sk[0] == 'p' && sk[1] == 'r') {
-            int lo = 0, hi = 0;
-            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
-                hipStreamCreateWithPriority(&g_svc.stream, hipStreamNonBlocking, hi) != hipSuccess) {
-                (void)hipGetLastError();
-                g_svc.stream = NULL;
-            }
-        } else if ((!sk || sk[0] == 'c') && (!nw || hipExtStreamCreateWithCUMask(&g_svc.stream, nw, mask) != hipSuccess)) {
+        /* a hardware queue of its own: a non-blocking stream of the highest
+         * priority (the runtime keeps a queue pool per priority, and the
+         * application's streams are normal priority; measured on the MI355X
+         * with 8 torch streams + the default one held up for the service's
+         * whole lifetime: a normal-priority stream shared a queue with one of
+         * them, a CU-masked stream -- blocking -- held the legacy default
+         * stream, the high-priority one held none) */
+        int prio_lo = 0, prio_hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
+            hipStreamCreateWithPriority(&g_svc.stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
             (void)hipGetLastError();
             g_svc.stream = NULL;
         }

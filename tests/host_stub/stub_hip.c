@@ -142,13 +142,6 @@ hipError_t hipStreamCreateWithPriority(hipStream_t* s, unsigned int flags, int p
     *s = (hipStream_t)malloc(1);
     return hipSuccess;
 }
-hipError_t hipExtStreamCreateWithCUMask(hipStream_t* s, uint32_t n, const uint32_t* mask)
-{
-    (void)n;
-    (void)mask;
-    *s = (hipStream_t)malloc(1);
-    return hipSuccess;
-}
 hipError_t hipEventCreate(hipEvent_t* e)
 {
     *e = (hipEvent_t)malloc(1);
