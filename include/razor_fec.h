@@ -238,6 +238,26 @@ typedef struct {
 int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,
                             sim_fec_t* const* fecs, uint16_t fec_id0, rfec_host_timing* timing);
 
+/*
+ * The receive direction of rfec_host_encode_groups: G groups in host memory,
+ * segs[g*k + i] the received sim_segment_t of member i or NULL where it was
+ * lost, fecs[g*n + l] the received sim_fec_t of line l or NULL.  Gathers them
+ * into the pinned staging (payload slots, header records, the present and
+ * parity-present masks, the parities' meta / fec_data_size / payload), copies
+ * it to HBM, runs rfec_recover_batch_out with per_group dense slots, copies
+ * the recovered slots back and scatters them like flex_fec_recover's out_seg
+ * (flex_fec_xor.c:64-101): out[g*per_group + e] receives the group's e-th
+ * erased segment (index order) when the peel recovered it -- header fields,
+ * data_size, SIM_VIDEO_SIZE bytes of data (zero past the recovering line's
+ * fec_data_size), fec_id of the group's parities -- and out_index[g*per_group
+ * + e] its member index, 0xFF when it was not recovered (out[...] untouched).
+ * recovered (may be NULL): [G][2] masks.  Chunked and double-buffered as the
+ * encode; k <= RFEC_MAX_K.  timing: gather = staging, scatter = delivery.
+ */
+int rfec_host_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,
+                             sim_fec_t* const* fecs, uint32_t per_group, sim_segment_t* const* out,
+                             uint8_t* out_index, uint64_t* recovered, rfec_host_timing* timing);
+
 /* Kernel timing for benches: the next kernel this thread launches through the
  * batched API (rfec_encode_batch, rfec_recover_batch[_out], rfec_zero_tails,
  * rfec_wire_frame_fec / _seg, rfec_wire_parse) records its own start / stop on these hipEvent_t (either may be NULL), via

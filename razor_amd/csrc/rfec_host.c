@@ -1394,6 +1394,243 @@ int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
     return RFEC_OK;
 }
 
+/* ---- the receive direction: rfec_host_recover_groups --------------------- */
+typedef struct {
+    size_t shards, hdr, present, parity, meta, fsize, ppm, in_bytes; /* host -> device, one copy */
+    size_t out_shards, out_hdr, out_index, recovered, out_bytes;      /* device -> host */
+    size_t ws, total;                                                /* device workspace */
+} hr_layout;
+
+static hr_layout hr_offsets(const rfec_plan* plan, uint32_t G, uint32_t E)
+{
+    const uint32_t k = plan->k, n = plan->n_lines;
+    hr_layout L;
+    size_t o = 0;
+#define HR_TAKE(field, bytes)                           \
+    do {                                                \
+        L.field = o;                                    \
+        o = (o + (size_t)(bytes) + 255) & ~(size_t)255; \
+    } while (0)
+    HR_TAKE(shards, (size_t)G * k * DI_STRIDE);
+    HR_TAKE(hdr, (size_t)G * k * sizeof(rfec_hdr));
+    HR_TAKE(present, (size_t)G * 16);
+    HR_TAKE(parity, (size_t)G * n * DI_STRIDE);
+    HR_TAKE(meta, (size_t)G * n * sizeof(rfec_hdr));
+    HR_TAKE(fsize, (size_t)G * n * sizeof(uint16_t));
+    HR_TAKE(ppm, (size_t)G * 8);
+    L.in_bytes = o;
+    HR_TAKE(out_shards, (size_t)G * E * DI_STRIDE);
+    HR_TAKE(out_hdr, (size_t)G * E * sizeof(rfec_hdr));
+    HR_TAKE(out_index, (size_t)G * E);
+    HR_TAKE(recovered, (size_t)G * 16);
+    L.out_bytes = o - L.out_shards;
+    HR_TAKE(ws, rfec_recover_workspace_size(plan, G));
+#undef HR_TAKE
+    L.total = o;
+    return L;
+}
+
+typedef struct {
+    const rfec_plan* plan;
+    sim_segment_t* const* segs; /* the chunk's first group */
+    sim_fec_t* const* fecs;
+    sim_segment_t* const* out;
+    uint8_t* out_index;
+    uint64_t* recovered;
+    uint8_t* slot;
+    hr_layout L;
+    uint32_t E;
+} hr_chunk;
+
+/* gather one group per index: received payloads / headers (a lost member's
+ * slot zero, its header zero), masks, received parities */
+static void hr_gather(void* arg, size_t lo, size_t hi)
+{
+    const hr_chunk* h = (const hr_chunk*)arg;
+    const uint32_t k = h->plan->k, n = h->plan->n_lines;
+    rfec_hdr* hh = (rfec_hdr*)(h->slot + h->L.hdr);
+    uint64_t* pres = (uint64_t*)(h->slot + h->L.present);
+    rfec_hdr* mh = (rfec_hdr*)(h->slot + h->L.meta);
+    uint16_t* fs = (uint16_t*)(h->slot + h->L.fsize);
+    uint64_t* ppm = (uint64_t*)(h->slot + h->L.ppm);
+    for (size_t g = lo; g < hi; ++g) {
+        uint64_t m0 = 0, m1 = 0, pm = 0;
+        for (uint32_t i = 0; i < k; ++i) {
+            const size_t s = g * k + i;
+            const sim_segment_t* seg = h->segs[s];
+            uint8_t* slot = h->slot + h->L.shards + s * DI_STRIDE;
+            if (!seg) {
+                memset(slot, 0, DI_STRIDE);
+                memset(&hh[s], 0, sizeof(rfec_hdr));
+                continue;
+            }
+            stage_payload(slot, seg->data, seg->data_size);
+            seg_to_hdr(seg, &hh[s]);
+            if (i < 64)
+                m0 |= 1ull << i;
+            else
+                m1 |= 1ull << (i - 64);
+        }
+        for (uint32_t l = 0; l < n; ++l) {
+            const size_t o = g * n + l;
+            const sim_fec_t* f = h->fecs[o];
+            if (!f) {
+                fs[o] = 0;
+                continue;
+            }
+            pm |= 1ull << l;
+            memcpy(&mh[o], &f->fec_meta, sizeof(rfec_hdr));
+            fs[o] = f->fec_data_size;
+            stage_payload(h->slot + h->L.parity + o * DI_STRIDE, f->fec_data,
+                          f->fec_data_size < SIM_VIDEO_SIZE ? f->fec_data_size : SIM_VIDEO_SIZE);
+        }
+        pres[2 * g] = m0;
+        pres[2 * g + 1] = m1;
+        ppm[g] = pm;
+    }
+}
+
+/* the recovered segments into the callers' sim_segment_t (flex_fec_recover's out_seg) */
+static void hr_scatter(void* arg, size_t lo, size_t hi)
+{
+    const hr_chunk* h = (const hr_chunk*)arg;
+    const uint32_t n = h->plan->n_lines, E = h->E;
+    const rfec_hdr* oh = (const rfec_hdr*)(h->slot + h->L.out_hdr);
+    const uint8_t* oi = h->slot + h->L.out_index;
+    const uint64_t* rec = (const uint64_t*)(h->slot + h->L.recovered);
+    for (size_t g = lo; g < hi; ++g) {
+        uint16_t fec_id = 0;
+        for (uint32_t l = 0; l < n; ++l)
+            if (h->fecs[g * n + l]) {
+                fec_id = h->fecs[g * n + l]->fec_id;
+                break;
+            }
+        for (uint32_t e = 0; e < E; ++e) {
+            const size_t o = g * E + e;
+            if (h->out_index)
+                h->out_index[o] = oi[o];
+            if (oi[o] == 0xFF || !h->out[o])
+                continue;
+            sim_segment_t* s = h->out[o];
+            const rfec_hdr* r = &oh[o];
+            s->packet_id = r->seq;
+            s->fid = r->fid;
+            s->timestamp = r->ts;
+            s->index = r->index;
+            s->total = r->total;
+            s->ftype = r->ftype;
+            s->payload_type = r->payload_type;
+            s->data_size = r->size;
+            memcpy(s->data, h->slot + h->L.out_shards + o * DI_STRIDE, SIM_VIDEO_SIZE);
+            s->fec_id = fec_id;
+        }
+        if (h->recovered) {
+            h->recovered[2 * g] = rec[2 * g];
+            h->recovered[2 * g + 1] = rec[2 * g + 1];
+        }
+    }
+}
+
+int rfec_host_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,
+                             sim_fec_t* const* fecs, uint32_t per_group, sim_segment_t* const* out,
+                             uint8_t* out_index, uint64_t* recovered, rfec_host_timing* timing)
+{
+    int rc = check_plan(plan, RFEC_MAX_K);
+    if (rc)
+        return rc;
+    if (groups == 0 || plan->n_lines == 0 || per_group == 0)
+        return RFEC_OK;
+    if (!segs || !fecs || !out)
+        return set_err(RFEC_EINVAL, "NULL segs / fecs / out", 0);
+    if (per_group > plan->k)
+        return set_err(RFEC_EINVAL, "per_group above k", 0);
+    if ((rc = check_geometry(groups, DI_STRIDE, SIM_VIDEO_SIZE, plan->k)))
+        return rc;
+    di_ctx* c = di_get();
+    if (!c)
+        return RFEC_EDEVICE;
+    const uint32_t k = plan->k, E = per_group;
+    uint32_t chunk = (groups + 7) / 8;
+    chunk = chunk < 2048 ? 2048 : chunk;
+    chunk = chunk > groups ? groups : chunk;
+    const uint32_t nch = (groups + chunk - 1) / chunk;
+    const hr_layout L = hr_offsets(plan, chunk, E);
+    if ((rc = hb_reserve(c, L.total)))
+        return rc;
+    rfec_kmask M;
+    make_masks(plan, &M);
+    const int threads = host_threads();
+    double gather_us = 0, scatter_us = 0, h2d_us = 0, kernel_us = 0, d2h_us = 0;
+    hr_chunk job[2];
+    const double t0 = now_us();
+    for (uint32_t it = 0; it < nch + 2; ++it) {
+        if (it >= 2) { /* retire chunk it-2 */
+            const uint32_t s = (it - 2) & 1;
+            hipError_t e = hipEventSynchronize(c->ev[s][3]);
+            if (e != hipSuccess)
+                return set_err(RFEC_EDEVICE, "D2H wait", e);
+            float a = 0, b = 0, d = 0;
+            (void)hipEventElapsedTime(&a, c->ev[s][0], c->ev[s][1]);
+            (void)hipEventElapsedTime(&b, c->ev[s][1], c->ev[s][2]);
+            (void)hipEventElapsedTime(&d, c->ev[s][2], c->ev[s][3]);
+            h2d_us += a * 1e3;
+            kernel_us += b * 1e3;
+            d2h_us += d * 1e3;
+            const double ts = now_us();
+            const uint32_t ng = (it - 2 == nch - 1) ? groups - (it - 2) * chunk : chunk;
+            parallel_for(ng, threads, hr_scatter, &job[s]);
+            scatter_us += now_us() - ts;
+        }
+        if (it < nch) { /* stage chunk it */
+            const uint32_t s = it & 1;
+            const uint32_t g0 = it * chunk;
+            const uint32_t ng = (it == nch - 1) ? groups - g0 : chunk;
+            hr_chunk* h = &job[s];
+            h->plan = plan;
+            h->segs = segs + (size_t)g0 * k;
+            h->fecs = fecs + (size_t)g0 * plan->n_lines;
+            h->out = out + (size_t)g0 * E;
+            h->out_index = out_index ? out_index + (size_t)g0 * E : NULL;
+            h->recovered = recovered ? recovered + (size_t)g0 * 2 : NULL;
+            h->slot = c->bh + (size_t)s * L.total;
+            h->L = L;
+            h->E = E;
+            const double tg = now_us();
+            parallel_for(ng, threads, hr_gather, h);
+            gather_us += now_us() - tg;
+            uint8_t* dv = c->bd + (size_t)s * L.total;
+            hipStream_t st = c->bstream[s];
+            hipError_t e;
+            if ((e = hipEventRecord(c->ev[s][0], st)) != hipSuccess ||
+                (e = hipMemcpyAsync(dv, h->slot, L.in_bytes, hipMemcpyHostToDevice, st)) != hipSuccess ||
+                (e = hipEventRecord(c->ev[s][1], st)) != hipSuccess)
+                return set_err(RFEC_EDEVICE, "H2D", e);
+            const rfec_dense_out D = {dv + L.out_shards, (rfec_hdr*)(dv + L.out_hdr), dv + L.out_index, E};
+            const int ke = rfec_launch_recover_out(
+                &M, ng, DI_STRIDE, SIM_VIDEO_SIZE, dv + L.shards, (const rfec_hdr*)(dv + L.hdr),
+                (const uint64_t*)(dv + L.present), dv + L.parity, (const rfec_hdr*)(dv + L.meta),
+                (const uint16_t*)(dv + L.fsize), (const uint64_t*)(dv + L.ppm), (uint64_t*)(dv + L.recovered),
+                dv + L.ws, st, g_tuning, &D);
+            if (ke)
+                return set_err(RFEC_EDEVICE, "recover launch", ke);
+            if ((e = hipEventRecord(c->ev[s][2], st)) != hipSuccess ||
+                (e = hipMemcpyAsync(h->slot + L.out_shards, dv + L.out_shards, L.out_bytes, hipMemcpyDeviceToHost,
+                                    st)) != hipSuccess ||
+                (e = hipEventRecord(c->ev[s][3], st)) != hipSuccess)
+                return set_err(RFEC_EDEVICE, "D2H", e);
+        }
+    }
+    if (timing) {
+        timing->gather_us = gather_us;
+        timing->h2d_us = h2d_us;
+        timing->kernel_us = kernel_us;
+        timing->d2h_us = d2h_us;
+        timing->scatter_us = scatter_us;
+        timing->total_us = now_us() - t0;
+    }
+    return RFEC_OK;
+}
+
 /* ------------------------------------------------------------------------ */
 /* 5. sender staging: sim_sender_put (sim_sender.c:254-377) + the flex sender */
 /*    grouping (flex_fec_sender.c:49-245), frames -> datagrams                */

@@ -747,18 +747,6 @@ __global__ __launch_bounds__(kBlock) void k_recover_flat(v4u* shards, const v4u*
 // kept in registers (a cascade costs loads, never another launch nor a round
 // trip through another lane's output).
 // ---------------------------------------------------------------------------
-// lab builds only (tools/build_ab.sh NAME -DRFEC_KDEBUG): index checks that print and bail out
-#ifdef RFEC_KDEBUG
-#define KCHECK(c, ...)                                                                                            \
-    do {                                                                                                          \
-        if (!(c)) {                                                                                               \
-            printf(__VA_ARGS__);                                                                                  \
-            return;                                                                                               \
-        }                                                                                                         \
-    } while (0)
-#else
-#define KCHECK(c, ...) ((void)0)
-#endif
 
 struct CascArgs {
     v4u* shards;              // in place: the erased slots are written; dense: read only
@@ -1141,7 +1129,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     const v4u* par = A.parity + (size_t)g * NL * C + j;
     v4u* slot0 = A.E ? A.out_sh + (size_t)g * A.E * C + j : A.shards + (size_t)g * K * C + j;
     v4u* dst = slot0 + (size_t)(A.E ? q : tgt) * C;
-    KCHECK(tgt < K && l < NL && j < C, "casc g %u q %u j %u: line %u target %u\n", g, q, j, l, tgt);
     if (!(task & kTaskCascade)) { // single level: every other member arrived
         const uint32_t ln = lplan[l];
         const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;

@@ -196,18 +196,9 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
 
 // crc32(seed, msg[0:n)) (cf_crc32.c:56-68) of a message held lane-wise:
 // lane j has bytes [B j, B j + B) in w (LE dwords), bytes >= n zero; n <= 64 B.
-// RFEC_WIRE_DIAG_*: measurement-only builds of tools/wire_lab.hip (cost
-// breakdown of the wire kernels; never defined in the product library)
 template <int B>
 __device__ __forceinline__ uint32_t wave_crc32(const uint32_t* T, const uint32_t* w, uint32_t n, uint32_t seed, uint32_t lane)
 {
-#if defined(RFEC_WIRE_DIAG_NO_CRC)
-    uint32_t x = n ^ seed;
-#pragma unroll
-    for (int k = 0; k < B / 4; ++k)
-        x ^= w[k];
-    return wave_xor(x);
-#endif
     if (n < 4) { // too short to fold the initial register into: bytewise
         uint32_t r = ~seed;
         for (uint32_t i = 0; i < n; ++i)
@@ -217,9 +208,6 @@ __device__ __forceinline__ uint32_t wave_crc32(const uint32_t* T, const uint32_t
     const uint32_t D = (uint32_t)(kWave * B) - n, q = D / B, rr = D - q * B;
     // initial register folded into message bytes 0-3
     const uint32_t c = lane_crc<B>(T, w[0] ^ (lane == 0 ? ~seed : 0u), w);
-#if defined(RFEC_WIRE_DIAG_NO_CARRY)
-    return wave_xor(c ^ q ^ rr);
-#endif
     // lanes past the message hold zeros (c == 0): their column is clamped
     const uint32_t R = wave_xor(carry_to_end(T, c, min(lane + q, (uint32_t)kWave - 1u)));
     // R = crc register * x^(8 rr): bit i of R times x^(31-i-8rr), summed
@@ -244,10 +232,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
 // the trailer, the store staging), the parse over its payload store and over
 // the batch header pass; each raise is dropped again before the next phase.
 constexpr int kAuxNT = 2; // gfx950 cache-policy bits: nt
-#ifndef RFEC_WIRE_STORE_AUX
-#define RFEC_WIRE_STORE_AUX 2 // stores' cache policy (the lab's ST0 build: 0)
-#endif
-constexpr int kAuxST = RFEC_WIRE_STORE_AUX;
+constexpr int kAuxST = kAuxNT; // datagram / payload stores: non-temporal
 
 // A lane window of NX dwords at byte offset `off` (a multiple of 4, may be
 // negative) of a range of `bytes` at base; dwords outside the range read as
@@ -356,15 +341,6 @@ __device__ __forceinline__ void store_slot(uint8_t* __restrict__ slot, uint32_t 
                                            const uint32_t* w)
 {
     static_assert(B % 16 == 0, "whole 16-byte stores");
-#if defined(RFEC_WIRE_DIAG_NO_STORE)
-    uint32_t x = 0;
-#pragma unroll
-    for (int k = 0; k < B / 4; ++k)
-        x ^= w[k];
-    if (x == 0x9E3779B9u && lane == 63u) // keeps the work alive, stores (almost) nothing
-        slot[0] = (uint8_t)x;
-    return;
-#endif
     const __amdgpu_buffer_rsrc_t r = rsrc(slot, slot_bytes);
 #pragma unroll
     for (int k = 0; k + 4 <= B / 4; k += 4)
@@ -504,28 +480,6 @@ __device__ __forceinline__ void ping_pong(uint32_t d, uint32_t count, uint32_t n
 // Three-deep form: two datagrams' loads in flight while one is processed
 // (the frame kernels' staged chunks are 8 dwords, so a third buffer fits the
 // register budget of 8 waves per SIMD).
-template <class Pre_, class Load, class Proc>
-__device__ __forceinline__ void pipeline3(uint32_t d, uint32_t count, uint32_t nw, Load load, Proc proc)
-{
-    Pre_ a, b, c;
-    load(d, a);
-    load(min(d + nw, count - 1), b);
-    for (;;) {
-        load(min(d + 2 * nw, count - 1), c);
-        proc(a, d);
-        if ((d += nw) >= count)
-            break;
-        load(min(d + 2 * nw, count - 1), a);
-        proc(b, d);
-        if ((d += nw) >= count)
-            break;
-        load(min(d + 2 * nw, count - 1), b);
-        proc(c, d);
-        if ((d += nw) >= count)
-            break;
-    }
-}
-
 template <class W>
 struct Pre {
     W w;        // payload: a lane window (Win) or aligned chunks (Chunks)
@@ -557,32 +511,6 @@ __device__ __forceinline__ void load_chunks(const uint8_t* base, uint32_t bytes,
 
 constexpr int kWaveBuf = 336; // dwords per wave: 48 + 1,280 bytes staged, or 1,280 stored
 
-#if defined(RFEC_WIRE_DIAG_LOAD_ONLY)
-// lab: the prefetched datagram folded to one dword, nothing else done
-__device__ __forceinline__ uint32_t diag_fold(const Chunks& c)
-{
-    return c.c0[0] ^ c.c0[1] ^ c.c0[2] ^ c.c0[3] ^ c.c1[0] ^ c.c1[1] ^ c.c1[2] ^ c.c1[3];
-}
-template <int NX>
-__device__ __forceinline__ uint32_t diag_fold(const Win<NX>& w)
-{
-    uint32_t x = 0;
-    for (int k = 0; k < NX; ++k)
-        x ^= w.c[k];
-    return x;
-}
-#define RFEC_DIAG_LOAD_ONLY(x, out)                                                                                  \
-    {                                                                                                                \
-        if ((x) == 0x9E3779B9u)                                                                                      \
-            (out)[0] = 1;                                                                                            \
-        return;                                                                                                      \
-    }
-#else
-#define RFEC_DIAG_LOAD_ONLY(x, out)
-#endif
-#ifndef RFEC_WIRE_PIPE
-#define RFEC_WIRE_PIPE ping_pong // frame kernels' datagram pipeline (the lab's DEPTH3 build: pipeline3)
-#endif
 
 // Lane j's window starts 48 (FEC) / 32 (SEG) bytes before the source of its
 // output bytes [B j, B j + B), so it does not depend on the header size.
@@ -611,7 +539,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_fec(const uint8_t* __restrict_
     if (d >= count)
         return;
     using PW = Pre<Win<ND + 1>>;
-    RFEC_WIRE_PIPE<PW>(d, count, nw,
+    ping_pong<PW>(d, count, nw,
                               [&](uint32_t dd, PW& P) {
                                   P.f = load_fec_fields(stamps, meta, fsize, status, dd, lane);
                                   load_window<ND + 1>(parity + (size_t)dd * stride, range, off, P.w);
@@ -709,13 +637,12 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
     if (d >= count)
         return;
     using PW = Pre<Win<ND + 2>>;
-    RFEC_WIRE_PIPE<PW>(d, count, nw,
+    ping_pong<PW>(d, count, nw,
                               [&](uint32_t dd, PW& P) {
                                   P.f = load_seg_fields(hdr, stamps, dd, lane);
                                   load_window<ND + 2>(shards + (size_t)dd * stride, range, off, P.w);
                               },
                               [&](const PW& P, uint32_t d) {
-            RFEC_DIAG_LOAD_ONLY(diag_fold(P.w) ^ P.f, dgram)
             const uint32_t o = order ? order[d] : d; // output slot
             uint8_t* slot = dgram + (size_t)o * dstride;
             rfec_hdr h;
@@ -750,11 +677,6 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                 uint32_t hs, pay[ND], x[ND + 2];
                 win_dwords<B, 32>(P.w, lane, x);
                 // window [B j - 32, ...) shifted by 32 - hs bytes
-#if defined(RFEC_WIRE_DIAG_NO_HDR) // lab: header bytes left zero, one layout
-                hs = 26, H.h[0] = layout ^ s.uid;
-                funnel<ND, 6>(x, pay);
-                if (0)
-#endif
                 switch (layout) {
                 case 0: hs = seg_header<false, false, false>(H, h, s); funnel<ND, 6>(x, pay); break;
                 case 1: hs = seg_header<false, false, true>(H, h, s); funnel<ND, 4>(x, pay); break;
@@ -1123,10 +1045,7 @@ __device__ __forceinline__ void store_payload20(const uint32_t* wb, uint8_t* __r
 }
 
 // parse: registers capped for 8 waves per SIMD (two 16-wave blocks per CU)
-#ifndef RFEC_PARSE_WAVES
-#define RFEC_PARSE_WAVES 8 // the lab's W6 build: 6
-#endif
-constexpr int kParseWaves = RFEC_PARSE_WAVES;
+constexpr int kParseWaves = 8;
 
 template <int B>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWaves))) void k_parse(const uint8_t* __restrict__ dgram,
@@ -1157,7 +1076,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
     uint32_t pk = 0, i = kWave; // i: the datagram's index in its batch (kWave: a batch starts)
     auto proc = [&](const PW& P, uint32_t d) {
         const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)pk, (int)i++);
-        RFEC_DIAG_LOAD_ONLY(diag_fold(P) ^ f, payload)
         const uint32_t len = f & 0xfffu, at1 = (f >> 12) & 63u, dsize = (f >> 18) & 0xfffu;
         bool ok = false;
         if constexpr (B == 20) { // stage the datagram: LDS dwords [0, 320)
@@ -1236,20 +1154,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
             const uint32_t cnt = min((uint32_t)kWave, (n - 1 - d) / nw + 1);
             HdrIn in;
             const uint32_t dl = d + lane * nw;
-#if defined(RFEC_WIRE_DIAG_NO_PASS1) // lab: every datagram a 1,236-byte SIM_SEG, data at 30
-            pk = kPkValid | 1236u | 31u << 12 | 1200u << 18;
-            (void)in, (void)dl;
-#elif defined(RFEC_WIRE_DIAG_PASS1_NOLOAD) // lab: the header pass on a fixed header
-            in.len = 1236u + (dstride >> 16); // (dstride < 64 KiB: opaque zeros)
-            for (int k = 0; k < kHdrDwords; ++k)
-                in.H[k] = (k == 0 ? 0x1701u : k == 6 ? 0xB004u : 0u) + (dstride >> 16);
-            pk = decode_header<B>(in, recs, dl, lane < cnt, dstride, capacity);
-#else
             __builtin_amdgcn_s_setprio(3);
             load_header(dgram, dlen, dl, lane < cnt, dstride, in);
             pk = decode_header<B>(in, recs, dl, lane < cnt, dstride, capacity);
             __builtin_amdgcn_s_setprio(0);
-#endif
             i = 0;
         }
         load(min(d1, n - 1), nxt); // past the end: the last datagram again (branch-free)

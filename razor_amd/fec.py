@@ -223,6 +223,7 @@ _SIGS = {
     "rfec_service_get_info": (C.c_int, [C.c_void_p]),
     "rfec_last_error": (C.c_char_p, []),
     "rfec_host_encode_groups": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, _P, _P, C.c_uint16, _P]),
+    "rfec_host_recover_groups": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, _P, _P, C.c_uint32, _P, _P, _P, _P]),
     "rfec_probe_read": (C.c_int, [_P, C.c_size_t, _P, C.c_uint, _P]),
     "rfec_probe_copy": (C.c_int, [_P, _P, C.c_size_t, C.c_uint, _P]),
     "rfec_probe_write": (C.c_int, [_P, C.c_size_t, C.c_uint, _P]),
@@ -362,6 +363,23 @@ class Native:
                                                      fec_ptrs.ctypes.data, fec_id0, C.addressof(t)),
                     "rfec_host_encode_groups")
         return {f: getattr(t, f) for f, _ in rfec_host_timing._fields_}
+
+    def host_recover_groups(self, plan, groups, seg_ptrs, fec_ptrs, per_group, out_ptrs):
+        """rfec_host_recover_groups: seg_ptrs [G*k] / fec_ptrs [G*n] host addresses of
+        the received sim_segment_t / sim_fec_t (0 = lost), out_ptrs [G*per_group] the
+        out_seg structs; returns (out_index [G][per_group] u8, recovered [G][2] u64,
+        per-stage timing in us)."""
+        t = rfec_host_timing()
+        seg_ptrs = np.ascontiguousarray(seg_ptrs, np.uint64)
+        fec_ptrs = np.ascontiguousarray(fec_ptrs, np.uint64)
+        out_ptrs = np.ascontiguousarray(out_ptrs, np.uint64)
+        oi = np.zeros((groups, per_group), np.uint8)
+        rec = np.zeros((groups, 2), np.uint64)
+        self._check(self.lib.rfec_host_recover_groups(C.byref(as_plan(plan)), groups, seg_ptrs.ctypes.data,
+                                                      fec_ptrs.ctypes.data, per_group, out_ptrs.ctypes.data,
+                                                      oi.ctypes.data, rec.ctypes.data, C.addressof(t)),
+                    "rfec_host_recover_groups")
+        return oi, rec, {f: getattr(t, f) for f, _ in rfec_host_timing._fields_}
 
     def timing_events(self, start, stop):
         """The next kernel this thread launches records its own start / stop on

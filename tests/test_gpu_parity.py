@@ -342,6 +342,73 @@ def test_host_encode_groups(product1200, oracle1200):
         assert np.array_equal(fecs["fec_data"][j, :L], ref["fec_data"][j, :L])
 
 
+@pytest.mark.parametrize("layers", [1, 3])
+def test_host_recover_groups(product1200, oracle1200, layers):
+    """rfec_host_recover_groups (host AoS in, flex_fec_recover-style out_seg
+    out): groups encoded by rfec_host_encode_groups (checked above), 1-3
+    segments and 0-2 parities of each lost; out_index / recovered masks equal
+    the oracle's rfec_recover_batch_out restatement, every recovered out_seg
+    equals the lost segment (header fields, data_size, data, zero past it)
+    and carries the group's fec_id."""
+    from razor_amd.fec import fec_dtype, seg_dtype
+
+    lib, o = product1200, oracle1200
+    G, k, S, E = 301, 10, 1200, 3
+    shards, hdr = o.fill_groups(203, G, k, S, ragged=True)
+    plan = o.plan_from_fraction(k, 80, layers)
+    n = plan.n_lines
+    segs = np.zeros(G * k, seg_dtype(1200))
+    h = hdr.reshape(-1)
+    for a, b in (("seq", "packet_id"), ("fid", "fid"), ("ts", "timestamp"), ("index", "index"),
+                 ("total", "total"), ("ftype", "ftype"), ("payload_type", "payload_type"), ("size", "data_size")):
+        segs[b] = h[a]
+    segs["data"] = shards.reshape(G * k, S)
+    fecs = np.zeros(G * n, fec_dtype(1200))
+    sp = segs.ctypes.data + np.arange(G * k, dtype=np.uint64) * segs.dtype.itemsize
+    fp = fecs.ctypes.data + np.arange(G * n, dtype=np.uint64) * fecs.dtype.itemsize
+    lib.host_encode_groups(plan, G, sp, fp, fec_id0=1)
+    rng = np.random.default_rng(layers)
+    present = np.zeros((G, 2), np.uint64)
+    ppm = np.zeros(G, np.uint64)
+    sp_rx, fp_rx = sp.copy(), fp.copy()
+    for g in range(G):
+        lost = rng.choice(k, int(rng.integers(1, 4)), replace=False)
+        sp_rx[g * k + lost] = 0
+        present[g, 0] = sum(1 << i for i in range(k) if i not in lost)
+        plost = rng.choice(n, int(rng.integers(0, 3)), replace=False)
+        fp_rx[g * n + plost] = 0
+        ppm[g] = sum(1 << l for l in range(n) if l not in plost)
+    out = np.zeros(G * E, seg_dtype(1200))
+    op = out.ctypes.data + np.arange(G * E, dtype=np.uint64) * out.dtype.itemsize
+    oi, rec, t = lib.host_recover_groups(plan, G, sp_rx, fp_rx, E, op)
+    assert t["total_us"] > 0
+    # the oracle on the same received set (lost members' slots / headers zero)
+    rx_sh = shards.copy()
+    rx_h = hdr.copy()
+    for g in range(G):
+        for i in range(k):
+            if not (int(present[g, 0]) >> i) & 1:
+                rx_sh[g, i] = 0
+                rx_h[g, i] = 0
+    par = fecs["fec_data"].reshape(G, n, S)
+    meta = np.ascontiguousarray(fecs["meta"].reshape(G, n))
+    fsz = fecs["fec_data_size"].reshape(G, n)
+    _, _, o_i, o_rec = o.recover_batch_out(plan, rx_sh, rx_h, present, par, meta, fsz, ppm, 1200, E)
+    assert np.array_equal(oi, o_i) and np.array_equal(rec, o_rec)
+    assert (oi != 0xFF).sum() > G  # most losses came back
+    for g in range(G):
+        for e in range(E):
+            i = int(oi[g, e])
+            if i == 0xFF:
+                continue
+            got, want = out[g * E + e], segs[g * k + i]
+            for f in ("packet_id", "fid", "timestamp", "index", "total", "ftype", "payload_type", "data_size"):
+                assert got[f] == want[f], (g, e, f)
+            nb = int(want["data_size"])
+            assert np.array_equal(got["data"][:nb], want["data"][:nb]) and not got["data"][nb:].any()
+            assert got["fec_id"] == fecs["fec_id"][g * n]
+
+
 @pytest.mark.parametrize("name", ["c2_k10_rows_S1200_G65536", "c3_k10_full_S1200_G65536",
                                   "c4_k10_rows_S1200_G1048576", "c5_k32_rows4_S256_G65536",
                                   "k10_full_ragged_S1000_G65536"])

@@ -1,5 +1,5 @@
 """Lab: one cascade-decode call on the inputs of a GPU test, against a chosen
-library build (e.g. a -DRFEC_KDEBUG one from tools/build_ab.sh), serialised.
+library build (e.g. an A/B build from tools/build_ab.sh), serialised.
 Usage: python tools/dbg_cascade.py LIB [k] [G] [mode]   (mode: in_place | dense)"""
 import sys
 from pathlib import Path

@@ -7,7 +7,10 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Irazor_amd/csrc [-DRFEC_WIRE_DIAG_NO_CRC ...] \
 //         tools/wire_lab.hip -o tools/bin/wire_lab_<variant>
 // run:   tools/bin/wire_lab_<variant> [reps=20] [dstride=1248] [payload stride=1200]
-#include "../razor_amd/csrc/rfec_wire.hip"
+#include "bin/wire_lab_src/rfec_wire.hip"
+
+// (the product's kernel-own timing hook, rfec_kernels.hip: no events here)
+bool rfec_timing_take(hipEvent_t*, hipEvent_t*) { return false; }
 
 #include <algorithm>
 #include <cstring>
