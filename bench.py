@@ -122,8 +122,9 @@ def peel_bytes(plan, k, erased, S):
 
 class Workload:
     def __init__(self, lib, G, k, S, pf, device, group0, seed, stride=None, col=0, full_plan=False, config_id=2,
-                 in_place=False):
+                 in_place=False, launch_groups=0):
         self.lib, self.G, self.k, self.S = lib, G, k, S
+        self.launch_groups = launch_groups
         self.stride = stride or (S + 15) // 16 * 16  # slot width in HBM (>= S, multiple of 16)
         if col:  # explicit rows of `col` (config 5: k = 32 as 8 rows of 4)
             self.plan = lib.plan_matrix(k, (k + col - 1) // col, col, 1)
@@ -174,30 +175,45 @@ class Workload:
             self.out_shards = torch.empty((G, 2, self.stride), dtype=torch.uint8, device=dev)
             self.out_hdr = torch.empty((G, 2, 20), dtype=torch.uint8, device=dev)
             self.out_index = torch.empty((G, 2), dtype=torch.uint8, device=dev)
-        self.ws = torch.empty((lib.workspace_size(self.plan, G),), dtype=torch.uint8, device=dev)
+        self.ws = torch.empty((lib.workspace_size(self.plan, launch_groups or G),), dtype=torch.uint8, device=dev)
         # algorithmic payload bytes (headers excluded): encode reads k*S, writes r*S
         self.enc_bytes = G * (k + self.n) * S
         # decode: per recovered segment read its line's other members + the parity, write 1
         pair_bytes = np.array([peel_bytes(self.plan, k, tuple(p), S) for p in pairs.tolist()], np.int64)
         self.dec_bytes = int(pair_bytes[pick].sum())
 
+    def _chunks(self):
+        """(first group, groups) of each launch: the whole batch, or launches of
+        `self.launch_groups` groups (the c4 sub-object: every launch the size of
+        the headline's, so per-kernel rocprofv3 averages stay comparable)."""
+        c = self.launch_groups or self.G
+        return [(g0, min(c, self.G - g0)) for g0 in range(0, self.G, c)]
+
     def encode(self, stream):
-        self.lib.encode_batch(self.plan, self.G, self.stride, self.S, self.shards.data_ptr(), self.hdr.data_ptr(),
-                              self.parity.data_ptr(), self.meta.data_ptr(), self.fsize.data_ptr(),
-                              self.status.data_ptr(), stream)
+        k, n, st = self.k, self.n, self.stride
+        for g0, g in self._chunks():
+            self.lib.encode_batch(self.plan, g, st, self.S, self.shards.data_ptr() + g0 * k * st,
+                                  self.hdr.data_ptr() + g0 * k * 20, self.parity.data_ptr() + g0 * n * st,
+                                  self.meta.data_ptr() + g0 * n * 20, self.fsize.data_ptr() + g0 * n * 2,
+                                  self.status.data_ptr() + g0 * n, stream)
 
     def decode(self, stream):
-        if self.dense:
-            self.lib.recover_batch_out(self.plan, self.G, self.stride, self.S, self.rx.data_ptr(),
-                                       self.rx_hdr.data_ptr(), self.present.data_ptr(), self.parity.data_ptr(),
-                                       self.meta.data_ptr(), self.fsize.data_ptr(), self.parity_present.data_ptr(),
-                                       self.recovered.data_ptr(), 2, self.out_shards.data_ptr(),
-                                       self.out_hdr.data_ptr(), self.out_index.data_ptr(), self.ws.data_ptr(), stream)
-            return
-        self.lib.recover_batch(self.plan, self.G, self.stride, self.S, self.rx.data_ptr(), self.rx_hdr.data_ptr(),
-                               self.present.data_ptr(), self.parity.data_ptr(), self.meta.data_ptr(),
-                               self.fsize.data_ptr(), self.parity_present.data_ptr(), self.recovered.data_ptr(),
-                               self.ws.data_ptr(), stream)
+        k, n, st = self.k, self.n, self.stride
+        for g0, g in self._chunks():
+            if self.dense:
+                self.lib.recover_batch_out(self.plan, g, st, self.S, self.rx.data_ptr() + g0 * k * st,
+                                           self.rx_hdr.data_ptr() + g0 * k * 20, self.present.data_ptr() + g0 * 16,
+                                           self.parity.data_ptr() + g0 * n * st, self.meta.data_ptr() + g0 * n * 20,
+                                           self.fsize.data_ptr() + g0 * n * 2, self.parity_present.data_ptr() + g0 * 8,
+                                           self.recovered.data_ptr() + g0 * 16, 2,
+                                           self.out_shards.data_ptr() + g0 * 2 * st, self.out_hdr.data_ptr() + g0 * 40,
+                                           self.out_index.data_ptr() + g0 * 2, self.ws.data_ptr(), stream)
+            else:
+                self.lib.recover_batch(self.plan, g, st, self.S, self.rx.data_ptr() + g0 * k * st,
+                                       self.rx_hdr.data_ptr() + g0 * k * 20, self.present.data_ptr() + g0 * 16,
+                                       self.parity.data_ptr() + g0 * n * st, self.meta.data_ptr() + g0 * n * 20,
+                                       self.fsize.data_ptr() + g0 * n * 2, self.parity_present.data_ptr() + g0 * 8,
+                                       self.recovered.data_ptr() + g0 * 16, self.ws.data_ptr(), stream)
 
     def verify(self):
         """Whole-batch checks after the timed steps (not timed): every parity
@@ -515,7 +531,9 @@ def c4_strong(lib, device, stream, dist, world, rank, pf, steps, warmup, verify)
     groups of config 4 split into contiguous slices over the ranks
     (razor_amd/dist.shard_groups; all of them on one GPU at N = 1), `steps`
     timed encode + decode steps of one buffer set (at 12.6 GB of shards per
-    GPU at N = 1 nothing of a step stays in the 256 MB MALL).  Every rank
+    GPU at N = 1 nothing of a step stays in the 256 MB MALL), each direction
+    as launches of 65,536 groups (the headline's launch size: the kernels'
+    rocprofv3 averages over a whole bench run stay those of one size).  Every rank
     checks its slice against the reference's digest of exactly those groups
     (full_hashes.json: the whole case at N = 1, "slices" at N = 2 / 4 / 8).
     Returns the sub-object on rank 0 (None elsewhere); value = all ranks'
@@ -524,7 +542,8 @@ def c4_strong(lib, device, stream, dist, world, rank, pf, steps, warmup, verify)
     cfg = CONFIGS["c4"]
     total = cfg["groups"]
     group0, my = shard_groups(total, world, rank)
-    w = Workload(lib, my, cfg["k"], cfg["S"], pf, device, group0, seed=3000 + rank, config_id=cfg["config_id"])
+    w = Workload(lib, my, cfg["k"], cfg["S"], pf, device, group0, seed=3000 + rank, config_id=cfg["config_id"],
+                 launch_groups=CONFIGS["c3"]["groups"])
     elapsed, t_enc, t_dec, own_enc, own_dec = time_steps(lib, [w], steps, warmup, stream, dist, "own", True)
     verified = digest_ok = None
     if verify:
@@ -553,10 +572,11 @@ def c4_strong(lib, device, stream, dist, world, rank, pf, steps, warmup, verify)
             "steps": steps, "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 4),
             "buffer_sets": 1, "decode_order": "hot (the set this step encoded; at this size not MALL-resident)",
             "groups_per_rank": [int(r[0]) for r in rows],
-            "encode_launch_us_per_rank": [round(float(r[2]), 2) for r in rows],
-            "decode_launch_us_per_rank": [round(float(r[3]), 2) for r in rows],
+            "launch_groups": CONFIGS["c3"]["groups"],
+            "encode_us_per_rank": [round(float(r[2]), 2) for r in rows],
+            "decode_us_per_rank": [round(float(r[3]), 2) for r in rows],
             "rank0_encode_frac_of_peak": round(enc_b / (float(rows[0][2]) * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
-            "timing": (TIMING_OWN if own_enc and own_dec else TIMING_BRACKET),
+            "timing": ("per step and direction: " + (TIMING_OWN if own_enc and own_dec else TIMING_BRACKET)),
             "verified": None if not verify else all(f[0] == 1 for f in flags),
             "verified_vs_reference_digest": None if not verify else (
                 False if any(f[1] == 0 for f in flags) else (True if all(f[1] == 1 for f in flags) else None))}

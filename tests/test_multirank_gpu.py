@@ -136,8 +136,8 @@ def _check_c4_strong(c4, n):
     assert c4["scaling"] == "strong" and c4["workload"].startswith("c4: k10_r3_S1200_G1048576")
     assert c4["groups_per_rank"] == [1048576 // n] * n
     assert c4["verified"] is True and c4["verified_vs_reference_digest"] is True
-    assert c4["value"] > 0 and len(c4["encode_launch_us_per_rank"]) == n
-    assert all(t > 0 for t in c4["encode_launch_us_per_rank"] + c4["decode_launch_us_per_rank"])
+    assert c4["value"] > 0 and len(c4["encode_us_per_rank"]) == n and c4["launch_groups"] == 65536
+    assert all(t > 0 for t in c4["encode_us_per_rank"] + c4["decode_us_per_rank"])
 
 
 @pytest.mark.timeout(600)
