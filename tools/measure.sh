@@ -1,9 +1,9 @@
 #!/bin/bash
 # The round's standard GPU measurement pass (GPU box, repo root):
 #   bash tools/measure.sh <tag>
-# pytest -m gpu, smoke, drop-in harness + group bench, bench (c3, then c5),
-# rocprofv3 kernel stats of the bench, wire bench + its kernel stats, PMC traffic passes (FETCH_SIZE /
-# WRITE_SIZE) for c3 and c5.  Every GPU step has its own limit; a crash /
+# pytest -m gpu, smoke, drop-in group bench, the default bench (the driver's command) and the
+# rocprofv3 kernel stats of that same command, c3full / c5 lines + stats, the r:w mix probe, the
+# end-to-end step, wire bench + stats, PMC traffic passes (FETCH_SIZE / WRITE_SIZE) for c3, c5, c3full.  Every GPU step has its own limit; a crash /
 # fault / timeout stops the script.
 set -u
 TAG=${1:-m}; OUT=gpurun_out/$TAG
@@ -21,18 +21,20 @@ step() {  # step <name> <timeout> <cmd...>
   fi
   return 0
 }
-step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 120 --timeout-method thread
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step group_bench 200 ./razor_amd/lib/fec_dropin_group_bench 2000
-step bench 400 python bench.py --steps 20 --warmup 5
-step bench_c5 400 python bench.py --config c5 --steps 20 --warmup 5 --no-cpu
-step bench_c3full 400 python bench.py --config c3full --steps 20 --warmup 5 --no-cpu
-step rocprof_stats 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py --no-cpu --steps 20 --warmup 5
-step rocprof_stats_c5 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5" -o run -- python bench.py --config c5 --no-cpu --steps 20 --warmup 5
+step bench 400 python bench.py
+step rocprof_stats 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py
+step bench_c3full 400 python bench.py --config c3full --no-cpu
+step bench_c5 400 python bench.py --config c5 --no-cpu
 step rocprof_stats_c3full 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c3full" -o run -- python bench.py --config c3full --no-cpu --steps 20 --warmup 5
+step rocprof_stats_c5 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5" -o run -- python bench.py --config c5 --no-cpu --steps 20 --warmup 5
+step mix 200 python tools/mix_probe.py
+step e2e 400 python tools/e2e_step.py
 step wire_bench 300 python tools/wire_bench.py --out "$OUT/wire.json"
 step rocprof_wire 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_wire" -o run -- python tools/wire_bench.py --reps 5
-step pmc_c3 600 python tools/pmc_traffic.py --out "$OUT/traffic_c3.json" -- --steps 10 --warmup 2
+step pmc_c3 600 python tools/pmc_traffic.py --out "$OUT/traffic_c3.json" -- --steps 10 --warmup 2 --c4-steps 0
 step pmc_c5 600 python tools/pmc_traffic.py --out "$OUT/traffic_c5.json" -- --config c5 --steps 10 --warmup 2
 step pmc_c3full 600 python tools/pmc_traffic.py --out "$OUT/traffic_c3full.json" -- --config c3full --steps 10 --warmup 2
 echo done | tee -a "$OUT/steps.log"
