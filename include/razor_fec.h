@@ -649,8 +649,11 @@ unsigned rfec_get_tuning(void);
  * a doorbell in pinned, host-coherent memory (no launch, no stream
  * synchronisation per call), each on its share of a job's 16-byte columns.  It starts on the
  * first drop-in call and leaves the device by itself after RFEC_SERVICE_IDLE_US
- * (default 20000) microseconds without a job, after one second in total (the
- * next call starts it again) and at exit.  rfec_service_stop() makes it leave
+ * (default 2000) microseconds without a job, after RFEC_SERVICE_LIFE_US (default
+ * 4000) in total (the next call starts it again) and at exit.  The request side
+ * (doorbell, job, staged segments) sits in device memory the host writes
+ * through its mapping when the runtime maps it (large-BAR hosts), else in
+ * pinned host memory (also with RFEC_SERVICE_STAGE=host).  rfec_service_stop() makes it leave
  * now and waits for it; it returns RFEC_OK (also when it was not running) or
  * RFEC_EDEVICE.  rfec_service_get_info reports the calls served, the
  * launches made and where a call's time goes (means over the calls served). */
@@ -659,9 +662,11 @@ typedef struct {
     uint64_t launches;   /* workgroup launches (the first call, then after each idle exit) */
     double stage_host_us; /* mean, per job: the host copying the segments next to the doorbell */
     double wait_us;      /* doorbell written -> `done` seen by the host */
-    double dev_stage_us; /* on the device: doorbell seen -> the job's slots in LDS (one PCIe round trip) */
+    double dev_stage_us; /* on the device: doorbell seen -> the job's slots in LDS */
     double dev_work_us;  /* -> results stored */
-    double dev_release_us; /* -> the system-scope release before `done` */
+    double dev_release_us; /* -> the results' stores acknowledged, before `done` */
+    uint32_t request_in_device; /* 1: the request side is in host-mapped device memory */
+    uint32_t reserved;
 } rfec_service_info;
 int rfec_service_stop(void);
 int rfec_service_get_info(rfec_service_info* info);

@@ -562,17 +562,92 @@ typedef struct {
                       still be live (stop set); retried after 1 s once its stream is idle */
     double t_fail; /* when it timed out */
     hipStream_t stream;
-    rfec_svc_ctl* ctl;   /* host view; the staging slots follow it */
+    rfec_svc_ctl* ctl;   /* results side (done / alive / out), pinned host memory; the output slots follow it */
     uint8_t* dev;        /* device view of the same allocation */
+    rfec_svc_ctl* in;    /* request side (bell / stop / quit / job), the staging slots follow it: device memory
+                            the host writes through its mapping when it can (in_vram), else == ctl */
+    uint8_t* in_dev;     /* device view of `in` */
+    void* vram;          /* the device allocation behind `in`, or NULL */
+    rfec_svc_ctl* req;   /* where a call composes its job and staged slots: `in` itself, or with `vram` a
+                            host shadow of it copied over in whole lines before the doorbell */
     size_t o_shards, o_parity;
     uint32_t seq, groups;
     uint64_t idle_ticks, life_ticks;
-    uint64_t jobs, launches;
+    uint64_t jobs, launches, dev_jobs;
     double tick_us;                                  /* s_memrealtime period */
     double t_stage, t_wait, t_dstage, t_dwork, t_drel; /* sums over the jobs, us */
 } svc_state;
-static svc_state g_svc = {PTHREAD_MUTEX_INITIALIZER, 0, 0, NULL, NULL, NULL, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                          0};
+static svc_state g_svc = {.mu = PTHREAD_MUTEX_INITIALIZER};
+
+/* host stores into device memory go through a write-combining mapping: drain
+ * them (the staged job before its doorbell, the doorbell itself) */
+static void svc_flush(void)
+{
+    if (!g_svc.vram)
+        return;
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_sfence();
+#else
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+#endif
+}
+
+/* 1 when [p, p + n) lies in one readable and writable mapping of this
+ * process (/proc/self/maps) */
+static int host_mapped_rw(const void* p, size_t n)
+{
+    FILE* f = fopen("/proc/self/maps", "r");
+    if (!f)
+        return 0;
+    char line[512];
+    int ok = 0;
+    const uintptr_t a = (uintptr_t)p;
+    while (!ok && fgets(line, sizeof(line), f)) {
+        unsigned long lo = 0, hi = 0;
+        char perm[5] = {0};
+        if (sscanf(line, "%lx-%lx %4s", &lo, &hi, perm) == 3 && a >= lo && a + n <= hi)
+            ok = perm[0] == 'r' && perm[1] == 'w';
+    }
+    fclose(f);
+    return ok;
+}
+
+/* The request side (doorbell, stop / quit, the job and its staging slots) in
+ * device memory the host writes through its BAR mapping: a call's staging is
+ * posted writes, and the workgroup polls and reads device memory, instead of
+ * reading the job over PCIe after the doorbell (one PCIe read round trip per
+ * call).  Fine-grained device memory, used when the runtime
+ * has mapped it into this process at the same address (a large-BAR host;
+ * /proc/self/maps says so); otherwise (or RFEC_SERVICE_STAGE=host) the request
+ * side stays in the pinned host block.  `bytes`: control block + staging
+ * slots. */
+static void svc_map_request_side(size_t bytes)
+{
+    const char* env = getenv("RFEC_SERVICE_STAGE");
+    if (env && strcmp(env, "host") == 0)
+        return;
+    void* d = NULL;
+    if (hipExtMallocWithFlags(&d, bytes, hipDeviceMallocFinegrained) != hipSuccess || !d) {
+        (void)hipGetLastError();
+        return;
+    }
+    if (!host_mapped_rw(d, bytes)) {
+        (void)hipFree(d);
+        return;
+    }
+    void* sh = NULL;
+    if (posix_memalign(&sh, 64, bytes) != 0) {
+        (void)hipFree(d);
+        return;
+    }
+    memset(sh, 0, bytes);
+    g_svc.vram = d;
+    g_svc.in = (rfec_svc_ctl*)d;
+    g_svc.in_dev = (uint8_t*)d;
+    g_svc.req = (rfec_svc_ctl*)sh;
+    memset(g_svc.in, 0, bytes);
+    svc_flush();
+}
 
 static void svc_pause(void)
 {
@@ -586,11 +661,13 @@ static int svc_stop_locked(void)
 {
     if (g_svc.state != 1 && g_svc.state != -2)
         return RFEC_OK;
-    __atomic_store_n(&g_svc.ctl->stop, 1u, __ATOMIC_RELEASE);
+    __atomic_store_n(&g_svc.in->stop, 1u, __ATOMIC_RELEASE);
+    svc_flush();
     const hipError_t e = hipStreamSynchronize(g_svc.stream);
-    __atomic_store_n(&g_svc.ctl->stop, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(&g_svc.in->stop, 0u, __ATOMIC_RELEASE);
+    g_svc.in->quit = 0;
+    svc_flush();
     g_svc.ctl->alive = 0;
-    g_svc.ctl->quit = 0;
     return e == hipSuccess ? RFEC_OK : set_err(RFEC_EDEVICE, "service stop", e);
 }
 
@@ -610,10 +687,14 @@ int rfec_service_get_info(rfec_service_info* info)
     memset(info, 0, sizeof(*info));
     info->jobs = g_svc.jobs;
     info->launches = g_svc.launches;
+    info->request_in_device = g_svc.vram != NULL;
     if (g_svc.jobs) {
         const double n = (double)g_svc.jobs;
         info->stage_host_us = g_svc.t_stage / n;
         info->wait_us = g_svc.t_wait / n;
+    }
+    if (g_svc.dev_jobs) {
+        const double n = (double)g_svc.dev_jobs;
         info->dev_stage_us = g_svc.t_dstage / n;
         info->dev_work_us = g_svc.t_dwork / n;
         info->dev_release_us = g_svc.t_drel / n;
@@ -678,6 +759,10 @@ static int svc_acquire(void)
         g_svc.ctl = (rfec_svc_ctl*)h;
         g_svc.o_shards = o_shards;
         g_svc.o_parity = o_parity;
+        g_svc.in = g_svc.ctl;
+        g_svc.in_dev = g_svc.dev;
+        g_svc.req = g_svc.ctl;
+        svc_map_request_side(o_parity);
         const char* idle = getenv("RFEC_SERVICE_IDLE_US");
         const char* life = getenv("RFEC_SERVICE_LIFE_US");
         const double idle_us = idle && atof(idle) > 0 ? atof(idle) : 2000.0;
@@ -696,8 +781,9 @@ static int svc_acquire(void)
     }
     if (g_svc.state == -2 && now_us() - g_svc.t_fail > 1e6 && hipStreamQuery(g_svc.stream) == hipSuccess) {
         /* the timed-out launch has left: take the service up again */
-        g_svc.ctl->stop = 0;
-        g_svc.ctl->quit = 0;
+        g_svc.in->stop = 0;
+        g_svc.in->quit = 0;
+        svc_flush();
         g_svc.ctl->alive = 0;
         __atomic_thread_fence(__ATOMIC_SEQ_CST);
         g_svc.state = 1;
@@ -709,7 +795,7 @@ static int svc_acquire(void)
     return 1;
 }
 
-static uint8_t* svc_shard(uint32_t i) { return (uint8_t*)g_svc.ctl + g_svc.o_shards + (size_t)i * DI_STRIDE; }
+static uint8_t* svc_shard(uint32_t i) { return (uint8_t*)g_svc.req + g_svc.o_shards + (size_t)i * DI_STRIDE; }
 static uint8_t* svc_out(uint32_t i) { return (uint8_t*)g_svc.ctl + g_svc.o_parity + (size_t)i * DI_STRIDE; }
 
 /* a payload into a service slot: the bytes, zero to the end of their last
@@ -729,8 +815,19 @@ static int svc_run(uint32_t n_slots, uint32_t op, double t_begin)
 {
     rfec_svc_ctl* q = g_svc.ctl;
     const uint32_t seq = ++g_svc.seq;
+    if (g_svc.vram) {
+        /* the job description up to its n_slots header records, and the slots, from the shadow in whole
+         * lines (scattered partial writes through the write-combining mapping cost ~3 us a call) */
+        const size_t oj = offsetof(rfec_svc_ctl, job);
+        const size_t nj = (offsetof(rfec_svc_job, hdr) + 20u * (size_t)n_slots + 63u) & ~(size_t)63u;
+        memcpy((uint8_t*)g_svc.in + oj, (const uint8_t*)g_svc.req + oj, nj);
+        memcpy((uint8_t*)g_svc.in + g_svc.o_shards, (const uint8_t*)g_svc.req + g_svc.o_shards,
+               (size_t)n_slots * DI_STRIDE);
+    }
+    svc_flush(); /* the staged job lands before its doorbell */
     const double t0 = now_us();
-    __atomic_store_n(&q->bell, RFEC_SVC_BELL(seq, n_slots, op), __ATOMIC_RELEASE);
+    __atomic_store_n(&g_svc.in->bell, RFEC_SVC_BELL(seq, n_slots, op), __ATOMIC_RELEASE);
+    svc_flush();
     for (uint64_t spin = 0;; ++spin) {
         uint32_t w = 0;
         while (w < g_svc.groups && __atomic_load_n(&q->done[w], __ATOMIC_ACQUIRE) == seq)
@@ -747,10 +844,12 @@ static int svc_run(uint32_t n_slots, uint32_t op, double t_begin)
                 g_svc.state = -1;
                 return set_err(RFEC_EDEVICE, "service relaunch", se);
             }
-            q->quit = 0;
+            g_svc.in->quit = 0;
+            svc_flush();
             q->alive = 1;
             __atomic_thread_fence(__ATOMIC_SEQ_CST);
-            const int ke = rfec_launch_service(q, g_svc.dev + g_svc.o_shards, g_svc.dev + g_svc.o_parity, DI_STRIDE,
+            const int ke = rfec_launch_service((rfec_svc_ctl*)g_svc.dev, (rfec_svc_ctl*)g_svc.in_dev,
+                                               g_svc.in_dev + g_svc.o_shards, g_svc.dev + g_svc.o_parity, DI_STRIDE,
                                                g_svc.idle_ticks, g_svc.life_ticks, g_svc.groups, g_svc.stream);
             if (ke) {
                 q->alive = 0;
@@ -763,7 +862,8 @@ static int svc_run(uint32_t n_slots, uint32_t op, double t_begin)
             /* no answer in 5 s: tell any live launch to leave (it may still
              * take the job; rfec_service_stop / atexit synchronise its
              * stream), fall back to per-call launches, retry in 1 s */
-            __atomic_store_n(&q->stop, 1u, __ATOMIC_RELEASE);
+            __atomic_store_n(&g_svc.in->stop, 1u, __ATOMIC_RELEASE);
+            svc_flush();
             g_svc.state = -2;
             g_svc.t_fail = now_us();
             return set_err(RFEC_EDEVICE, "service timeout", 0);
@@ -771,13 +871,18 @@ static int svc_run(uint32_t n_slots, uint32_t op, double t_begin)
         svc_pause();
     }
     const double t1 = now_us();
-    const uint64_t* t = q->out.t;
     ++g_svc.jobs;
     g_svc.t_stage += t0 - t_begin;
     g_svc.t_wait += t1 - t0;
-    g_svc.t_dstage += (double)(t[1] - t[0]) * g_svc.tick_us;
-    g_svc.t_dwork += (double)(t[2] - t[1]) * g_svc.tick_us;
-    g_svc.t_drel += (double)(t[3] - t[2]) * g_svc.tick_us;
+    if (seq > 1) { /* the previous job's device timing: written after its `done`, landed before this one's */
+        const uint64_t* t = q->out.t[(seq - 1) & 1u];
+        if (t[0] && t[3] >= t[0]) {
+            ++g_svc.dev_jobs;
+            g_svc.t_dstage += (double)(t[1] - t[0]) * g_svc.tick_us;
+            g_svc.t_dwork += (double)(t[2] - t[1]) * g_svc.tick_us;
+            g_svc.t_drel += (double)(t[3] - t[2]) * g_svc.tick_us;
+        }
+    }
     return RFEC_OK;
 }
 
@@ -785,7 +890,7 @@ static int svc_run(uint32_t n_slots, uint32_t op, double t_begin)
 static int svc_generate_group(sim_segment_t* const* segs, int k, const rfec_plan* plan)
 {
     const double t_begin = now_us();
-    rfec_svc_job* J = &g_svc.ctl->job;
+    rfec_svc_job* J = &g_svc.req->job;
     J->op = RFEC_SVC_ENCODE;
     J->n_slots = (uint32_t)k;
     J->groups = 1;
@@ -954,8 +1059,8 @@ static int di_refused(const rfec_di_recover_job* J)
  * consecutive slots, its recovered payload to output slot g */
 static int svc_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets)
 {
-    rfec_svc_ctl* q = g_svc.ctl;
-    rfec_svc_job* S = &q->job;
+    const rfec_svc_ctl* q = g_svc.ctl;
+    rfec_svc_job* S = &g_svc.req->job;
     int j = 0;
     while (j < n) {
         int idx[RFEC_DI_GROUPS];

@@ -126,11 +126,12 @@ typedef struct {
         uint32_t meta[RFEC_MAX_LINES][5]; /* encode: line l's meta; recover: job g's recovered header */
         uint16_t fsize[RFEC_MAX_LINES];
         int8_t status[RFEC_MAX_LINES];    /* flex_fec_generate / flex_fec_recover's 0 / -1 */
-        uint64_t t[4];                    /* s_memrealtime: bell seen, job staged, results stored, done */
+        uint64_t t[2][4]; /* s_memrealtime of job seq at [seq & 1]: bell seen, job staged, results stored,
+                           * drained; written after its `done` (the next job's drain lands it) */
     } out;
     rfec_svc_job job;
 } rfec_svc_ctl;
-int rfec_launch_service(rfec_svc_ctl* ctl, const uint8_t* shards, uint8_t* out, uint32_t stride,
+int rfec_launch_service(rfec_svc_ctl* ctl, rfec_svc_ctl* in, const uint8_t* shards, uint8_t* out, uint32_t stride,
                         uint64_t idle_ticks, uint64_t life_ticks, uint32_t groups, void* stream);
 
 __attribute__((visibility("hidden"))) int rfec_set_error(int code, const char* what);

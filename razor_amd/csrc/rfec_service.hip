@@ -39,7 +39,9 @@ constexpr int kSvcU = (kSvcLdsChunks + kSvcBlock - 1) / kSvcBlock; // chunk load
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 struct SvcArgs {
-    rfec_svc_ctl* ctl;   // control block (device view of host memory)
+    rfec_svc_ctl* ctl;   // control block, results side: done / alive / out (device view of host memory)
+    rfec_svc_ctl* in;    // control block, request side: bell / stop / quit / job (host-written device
+                         // memory when the host can map it, else == ctl)
     const v4u* shards;   // staging slots (device view), C chunks each
     v4u* out;            // output slots
     uint32_t C;          // chunks per slot
@@ -103,7 +105,7 @@ __device__ __forceinline__ void stage_tile(const SvcArgs& A, uint32_t ns, uint32
     v4u v[kSvcU], t[UJ];
     // (unconditional loads at clamped indices: under per-load branches hipcc
     // waits on each load before issuing the next)
-    const __amdgpu_buffer_rsrc_t rc = sys_rsrc(A.ctl, sizeof(rfec_svc_ctl));
+    const __amdgpu_buffer_rsrc_t rc = sys_rsrc(A.in, sizeof(rfec_svc_ctl));
     const __amdgpu_buffer_rsrc_t rs = sys_rsrc(A.shards, RFEC_SVC_SLOTS * A.C * 16u);
     const uint32_t njr = nj;
 #pragma unroll
@@ -270,8 +272,8 @@ __global__ __launch_bounds__(kSvcBlock) void k_service(SvcArgs A)
             uint32_t ex = 0;
             uint64_t bell = 0;
             for (;;) {
-                bell = __hip_atomic_load(&A.ctl->bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (poll_u32(&A.ctl->stop) || (!leader && poll_u32(&A.ctl->quit))) {
+                bell = __hip_atomic_load(&A.in->bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (poll_u32(&A.in->stop) || (!leader && poll_u32(&A.in->quit))) {
                     ex = 1;
                     break;
                 }
@@ -285,7 +287,7 @@ __global__ __launch_bounds__(kSvcBlock) void k_service(SvcArgs A)
                 __builtin_amdgcn_s_sleep(2);
             }
             if (ex && leader) { // a job posted after the poll above finds alive == 0 and relaunches
-                __hip_atomic_store(&A.ctl->quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&A.in->quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(&A.ctl->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             s_seq = (uint32_t)bell;
@@ -304,16 +306,14 @@ __global__ __launch_bounds__(kSvcBlock) void k_service(SvcArgs A)
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
         if (threadIdx.x == 0) {
-            if (leader) { // timing of this job (rfec_service_get_info), before `done`
-                const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
-                const __amdgpu_buffer_rsrc_t rc = sys_rsrc(A.ctl, sizeof(rfec_svc_ctl));
-                st_sys(rc, CTL_OFF(out.t),
-                       v4u{(uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)s_t1, (uint32_t)(s_t1 >> 32)});
-                st_sys(rc, CTL_OFF(out.t) + 16u,
-                       v4u{(uint32_t)t2, (uint32_t)(t2 >> 32), (uint32_t)t3, (uint32_t)(t3 >> 32)});
-                __builtin_amdgcn_s_waitcnt(0);
-            }
+            const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
             __hip_atomic_store(&A.ctl->done[w], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (leader) { // this job's timing (rfec_service_get_info) after `done`: off the call's path
+                const __amdgpu_buffer_rsrc_t rc = sys_rsrc(A.ctl, sizeof(rfec_svc_ctl));
+                const uint32_t o = CTL_OFF(out.t) + 32u * (seq & 1u);
+                st_sys(rc, o, v4u{(uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)s_t1, (uint32_t)(s_t1 >> 32)});
+                st_sys(rc, o + 16u, v4u{(uint32_t)t2, (uint32_t)(t2 >> 32), (uint32_t)t3, (uint32_t)(t3 >> 32)});
+            }
         }
         done = seq;
         t_last = __builtin_amdgcn_s_memrealtime();
@@ -322,12 +322,13 @@ __global__ __launch_bounds__(kSvcBlock) void k_service(SvcArgs A)
 
 } // namespace
 
-extern "C" int rfec_launch_service(rfec_svc_ctl* ctl, const uint8_t* shards, uint8_t* out, uint32_t stride,
-                                   uint64_t idle_ticks, uint64_t life_ticks, uint32_t groups, void* stream)
+extern "C" int rfec_launch_service(rfec_svc_ctl* ctl, rfec_svc_ctl* in, const uint8_t* shards, uint8_t* out,
+                                   uint32_t stride, uint64_t idle_ticks, uint64_t life_ticks, uint32_t groups,
+                                   void* stream)
 {
     if (stride % 16 || stride / 16 > 255 || groups < 1 || groups > RFEC_SVC_MAX_GROUPS)
         return (int)hipErrorInvalidValue;
-    SvcArgs A{ctl, reinterpret_cast<const v4u*>(shards), reinterpret_cast<v4u*>(out), stride / 16, idle_ticks,
+    SvcArgs A{ctl, in, reinterpret_cast<const v4u*>(shards), reinterpret_cast<v4u*>(out), stride / 16, idle_ticks,
               life_ticks};
     hipLaunchKernelGGL(k_service, dim3(groups), dim3(kSvcBlock), 0, (hipStream_t)stream, A);
     return (int)hipGetLastError();

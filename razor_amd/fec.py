@@ -92,7 +92,7 @@ class rfec_rx_session_info(C.Structure):
 class rfec_service_info(C.Structure):
     _fields_ = [("jobs", C.c_uint64), ("launches", C.c_uint64), ("stage_host_us", C.c_double),
                 ("wait_us", C.c_double), ("dev_stage_us", C.c_double), ("dev_work_us", C.c_double),
-                ("dev_release_us", C.c_double)]
+                ("dev_release_us", C.c_double), ("request_in_device", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class rfec_udp_addr(C.Structure):

@@ -48,10 +48,10 @@ hipError_t hipDeviceGetAttribute(int* v, hipDeviceAttribute_t a, int d)
     *v = 0;
     return hipErrorNotSupported;
 }
-int rfec_launch_service(rfec_svc_ctl* ctl, const uint8_t* shards, uint8_t* out, uint32_t stride,
+int rfec_launch_service(rfec_svc_ctl* ctl, rfec_svc_ctl* in, const uint8_t* shards, uint8_t* out, uint32_t stride,
                         uint64_t idle_ticks, uint64_t life_ticks, uint32_t groups, void* stream)
 {
-    (void)ctl, (void)shards, (void)out, (void)stride, (void)idle_ticks, (void)life_ticks, (void)groups,
+    (void)ctl, (void)in, (void)shards, (void)out, (void)stride, (void)idle_ticks, (void)life_ticks, (void)groups,
         (void)stream;
     return (int)hipErrorNotSupported;
 }
@@ -80,6 +80,13 @@ hipError_t hipFree(void* p)
 {
     free(p);
     return hipSuccess;
+}
+/* device memory the host could map: none here (the service keeps its request side in host memory) */
+hipError_t hipExtMallocWithFlags(void** p, size_t n, unsigned int flags)
+{
+    (void)n, (void)flags;
+    *p = NULL;
+    return hipErrorOutOfMemory;
 }
 hipError_t hipHostMalloc(void** p, size_t n, unsigned int flags)
 {

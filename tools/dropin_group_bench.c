@@ -202,10 +202,10 @@ int main(int argc, char** argv)
            " \"receiver_two_flex_fec_recover_us\": %.2f,\n"
            " \"outputs_equal\": %s,\n"
            " \"service_sender\": {\"jobs\": %llu, \"launches\": %llu, \"stage_host_us\": %.2f, \"wait_us\": %.2f,"
-           " \"dev_stage_us\": %.2f, \"dev_work_us\": %.2f, \"dev_release_us\": %.2f}}\n",
+           " \"dev_stage_us\": %.2f, \"dev_work_us\": %.2f, \"dev_release_us\": %.2f, \"request_in_device\": %u}}\n",
            groups, K, SIM_VIDEO_SIZE, t_group / groups, t_line / groups, t_rx / rx_groups, t_rx2 / rx_groups,
            ok ? "true" : "false", (unsigned long long)si.jobs, (unsigned long long)si.launches, si.stage_host_us,
-           si.wait_us, si.dev_stage_us, si.dev_work_us, si.dev_release_us);
+           si.wait_us, si.dev_stage_us, si.dev_work_us, si.dev_release_us, si.request_in_device);
     drain(&out);
     flex_fec_sender_destroy(fs);
     free(fl);

@@ -8,8 +8,8 @@ VARIANTS=${1:-}; R=${2:-2}
 mkdir -p gpurun_out/svcab
 for r in $(seq 1 "$R"); do
   for v in cur $VARIANTS; do
-    LP=""; [ "$v" != cur ] && LP="tools/bin/ab/$v"
-    LD_LIBRARY_PATH=$LP timeout -k 10 60 ./razor_amd/lib/fec_dropin_group_bench 2000 > "gpurun_out/svcab/$v.$r.json"
+    LP=""; EV=""; case "$v" in cur) ;; env:*) EV=${v#env:} ;; *) LP="tools/bin/ab/$v" ;; esac
+    env $EV LD_LIBRARY_PATH=$LP timeout -k 10 60 ./razor_amd/lib/fec_dropin_group_bench 2000 > "gpurun_out/svcab/$v.$r.json"
     rc=$?
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "$v: rc=$rc"; exit $rc; fi  # 1: outputs differ (reported)
     python3 - "$v" "$r" <<'PY'
@@ -18,7 +18,7 @@ v, r = sys.argv[1], sys.argv[2]
 d = json.load(open(f"gpurun_out/svcab/{v}.{r}.json"))
 s = d["service_sender"]
 print(v, r, d["outputs_equal"], d["sender_group_level_us_per_group"], d["receiver_on_segment_row_and_col_us"],
-      s["wait_us"], s["dev_stage_us"], s["dev_work_us"], s["dev_release_us"])
+      s["wait_us"], s["dev_stage_us"], s["dev_work_us"], s["dev_release_us"], s.get("request_in_device"))
 PY
   done
 done
