@@ -798,14 +798,14 @@ static int svc_acquire(void)
 static uint8_t* svc_shard(uint32_t i) { return (uint8_t*)g_svc.req + g_svc.o_shards + (size_t)i * DI_STRIDE; }
 static uint8_t* svc_out(uint32_t i) { return (uint8_t*)g_svc.ctl + g_svc.o_parity + (size_t)i * DI_STRIDE; }
 
-/* a payload into a service slot: the bytes, zero to the end of their last
- * 16-byte chunk (chunks past it are stale: the device masks them); returns
- * the chunks */
+/* a payload into a service slot: the bytes, zeros to the end of the slot (the
+ * zero padding of flex_fec_xor.c:30-32, 84-86: the device XORs whole slots);
+ * returns the 16-byte chunks that hold the bytes */
 static uint8_t svc_stage(uint8_t* slot, const uint8_t* data, uint32_t size)
 {
     const uint32_t n = size < SIM_VIDEO_SIZE ? size : SIM_VIDEO_SIZE, nck = (n + 15) / 16;
     memcpy(slot, data, n);
-    memset(slot + n, 0, (size_t)nck * 16 - n);
+    memset(slot + n, 0, (size_t)DI_STRIDE - n);
     return (uint8_t)nck;
 }
 

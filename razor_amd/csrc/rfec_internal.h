@@ -113,7 +113,7 @@ typedef struct {
     uint16_t count[RFEC_DI_GROUPS];    /* present members */
     uint16_t fsize[RFEC_DI_GROUPS];    /* fec_data_size */
     uint16_t pad[RFEC_DI_GROUPS];
-    uint8_t slot_nck[RFEC_SVC_SLOTS];  /* 16-byte chunks of the slot that hold its bytes (the rest: stale) */
+    uint8_t slot_nck[RFEC_SVC_SLOTS];  /* 16-byte chunks of the slot that hold its bytes (zeros follow) */
     uint32_t hdr[RFEC_SVC_SLOTS * 5];  /* encode: member i at 5 i; recover: as slot0 */
 } rfec_svc_job;
 typedef struct {

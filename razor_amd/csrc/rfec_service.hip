@@ -131,114 +131,116 @@ __device__ __forceinline__ void stage_tile(const SvcArgs& A, uint32_t ns, uint32
     }
 }
 
-// encode: line l's meta / fec_data_size / status from the member headers (the
-// job's hdr words, member i at 5 i), flex_fec_xor.c:9-28; every workgroup
-// needs the sizes (fsz), workgroup 0 writes the results
-__device__ void svc_encode_meta(const SvcArgs& A, const rfec_svc_job& J, uint16_t* fsz, bool write)
-{
-    const rfec_kplan& P = J.plan;
-    const __amdgpu_buffer_rsrc_t rc = sys_rsrc(A.ctl, sizeof(rfec_svc_ctl));
-    for (uint32_t l = threadIdx.x; l < P.n_lines; l += kSvcBlock) {
-        const rfec_line ln = P.line[l];
-        uint32_t m[5] = {0, 0, 0, 0, 0}, L = 0;
-        for (uint32_t q = 0; q < ln.count; ++q) {
-            const uint32_t* r = J.hdr + 5u * (ln.first + q * ln.stride);
-#pragma unroll
-            for (int d = 0; d < 5; ++d)
-                m[d] ^= r[d];
-            L = max(L, r[4] >> 16);
-        }
-        fsz[l] = (uint16_t)L;
-        if (!write)
-            continue;
-#pragma unroll
-        for (int d = 0; d < 5; ++d)
-            st_sys32(rc, CTL_OFF(out.meta) + 20u * l + 4u * d, m[d]);
-        st_sys16(rc, CTL_OFF(out.fsize) + 2u * l, (uint16_t)L);
-        st_sys8(rc, CTL_OFF(out.status) + l, (ln.count <= 1 || L > J.capacity) ? 0xFFu : 0u);
-    }
-}
+constexpr int kSvcWaves = kSvcBlock / 64;
+constexpr int kSvcMemU = 4; // member loads in flight per lane
 
-// recover: job g's recovered header (meta ^ members) and verdict,
-// flex_fec_xor.c:64-71, 75-99; the job's hdr words: the parity's meta at
-// 5 slot0[g], then its members' (workgroup 0)
-__device__ void svc_recover_meta(const SvcArgs& A, const rfec_svc_job& J)
+// One XOR line of a tile, on one wave: slots s_q = first + q * stride (q <
+// count), lane t on tile columns jb + t and jb + 64 + t.  The host stages
+// every slot zero-filled to its end (the zero padding of flex_fec_xor.c:30-32,
+// 46-49, 84-86), so whole slots are XORed.  With `hdr_lanes`, lanes 0-4 also
+// XOR header word `lane` of the records at hrec + q * hstride and keep the
+// largest upper half (the size on lane 4).  nck: the longest member's chunks.
+// The loads of a pass of kSvcMemU members go out together: one LDS round trip
+// per pass.
+struct LineAcc {
+    v4u a[2];
+    uint32_t h, L, nck;
+};
+__device__ __forceinline__ void line_pass(const rfec_svc_job& J, const v4u* lds, uint32_t tj, uint32_t jb,
+                                          uint32_t first, uint32_t stride, uint32_t count, uint32_t hrec,
+                                          uint32_t hstride, bool hdr_lanes, LineAcc& R)
 {
-    const __amdgpu_buffer_rsrc_t rc = sys_rsrc(A.ctl, sizeof(rfec_svc_ctl));
-    for (uint32_t g = threadIdx.x; g < J.groups; g += kSvcBlock) {
-        const uint32_t* r = J.hdr + 5u * J.slot0[g];
-        const uint32_t L = J.fsize[g];
-        uint32_t m[5];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t c0 = min(jb + lane, tj - 1u), c1 = min(jb + 64u + lane, tj - 1u);
+    for (uint32_t q0 = 0; q0 < count; q0 += kSvcMemU) {
 #pragma unroll
-        for (int d = 0; d < 5; ++d)
-            m[d] = r[d];
-        bool ok = L <= J.capacity;
-        for (uint32_t q = 1; q <= J.count[g]; ++q) {
-#pragma unroll
-            for (int d = 0; d < 5; ++d)
-                m[d] ^= r[5 * q + d];
-            ok = ok && (r[5 * q + 4] >> 16) <= L;
+        for (int u = 0; u < kSvcMemU; ++u) {
+            const uint32_t q = q0 + u;
+            if (q < count) { // (uniform)
+                const uint32_t sl = first + q * stride;
+                R.nck = max(R.nck, (uint32_t)J.slot_nck[sl]);
+                R.a[0] ^= lds[sl * tj + c0];
+                R.a[1] ^= lds[sl * tj + c1];
+                if (hdr_lanes && lane < 5u) {
+                    const uint32_t r = J.hdr[5u * (hrec + q * hstride) + lane];
+                    R.h ^= r;
+                    R.L = max(R.L, r >> 16);
+                }
+            }
         }
-        ok = ok && (m[4] >> 16) <= L;
-#pragma unroll
-        for (int d = 0; d < 5; ++d)
-            st_sys32(rc, CTL_OFF(out.meta) + 20u * g + 4u * d, m[d]);
-        st_sys8(rc, CTL_OFF(out.status) + g, ok ? 0u : 0xFFu);
     }
-}
-
-__device__ __forceinline__ v4u chunk(const v4u* lds, const rfec_svc_job& J, uint32_t s, uint32_t tj, uint32_t jj,
-                                     uint32_t j)
-{
-    return j < J.slot_nck[s] ? lds[s * tj + jj] : v4u{0, 0, 0, 0};
 }
 
 // One job, this workgroup's chunk columns [c0, c1) of every slot: staged
-// tile by tile (the first tile together with the job description), the
-// lines (encode) or jobs (recover) XORed from LDS.
+// tile by tile (the first tile together with the job description), then one
+// wave per line (encode) or per recover job, from LDS.  The header results
+// (workgroup 0, first tile) ride along on lanes 0-4 of the same passes:
+//   encode line l: meta = XOR of the member records, fec_data_size = the
+//     largest member size, status -1 for a single member or a size over
+//     capacity (flex_fec_xor.c:9-28)
+//   recover job g: recovered record = the parity's meta ^ the members'
+//     (records slot0[g], then its members'), status -1 when fec_data_size is
+//     over capacity or a member or the recovered size exceeds it
+//     (flex_fec_xor.c:64-71, 75-99)
 __device__ void svc_job(const SvcArgs& A, uint32_t ns, uint32_t c0, uint32_t c1, bool leader, v4u* lds,
-                        rfec_svc_job& J, uint16_t* fsz, uint64_t* t1)
+                        rfec_svc_job& J, uint64_t* t1)
 {
     const uint32_t C = A.C;
     const uint32_t tmax = ns ? max(1u, min(c1 - c0, (uint32_t)kSvcLdsChunks / ns)) : c1 - c0;
     const __amdgpu_buffer_rsrc_t ro = sys_rsrc(A.out, RFEC_MAX_LINES * C * 16u);
+    const __amdgpu_buffer_rsrc_t rc = sys_rsrc(A.ctl, sizeof(rfec_svc_ctl));
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     for (uint32_t j0 = c0, first = 1; first || j0 < c1; j0 += tmax, first = 0) {
         const uint32_t tj = j0 < c1 ? min(tmax, c1 - j0) : 0u;
         if (!first)
             __syncthreads(); // the previous tile's readers are done
         stage_tile(A, ns, j0, tj, lds, first, &J);
         __syncthreads();
-        if (first) { // the headers' work, once J has landed
-            if (leader && threadIdx.x == 0)
-                *t1 = __builtin_amdgcn_s_memrealtime();
-            if (J.op == RFEC_SVC_ENCODE)
-                svc_encode_meta(A, J, fsz, leader);
-            else if (leader)
-                svc_recover_meta(A, J);
-            __syncthreads(); // fsz
-        }
-        if (J.op == RFEC_SVC_ENCODE) {
-            const rfec_kplan& P = J.plan;
-            for (uint32_t it = threadIdx.x; it < P.n_lines * tj; it += kSvcBlock) {
-                const uint32_t l = it / tj, jj = it - l * tj, j = j0 + jj;
-                const rfec_line ln = P.line[l];
-                if (j >= (fsz[l] + 15u) / 16u) // past fec_data_size: never read back
-                    continue;
-                v4u acc = chunk(lds, J, ln.first, tj, jj, j);
-                for (uint32_t q = 1; q < ln.count; ++q)
-                    acc ^= chunk(lds, J, ln.first + q * ln.stride, tj, jj, j);
-                st_sys(ro, 16u * (l * C + j), acc);
+        if (first && leader && threadIdx.x == 0)
+            *t1 = __builtin_amdgcn_s_memrealtime();
+        const bool hdr = first && leader;
+        const bool enc = J.op == RFEC_SVC_ENCODE;
+        const uint32_t nitems = enc ? (uint32_t)J.plan.n_lines : J.groups;
+        for (uint32_t x = wv; x < nitems; x += kSvcWaves) {
+            uint32_t sf, sstr, cnt, hrec, hstr, bound;
+            LineAcc R{{v4u{0, 0, 0, 0}, v4u{0, 0, 0, 0}}, 0u, 0u, 0u};
+            if (enc) {
+                const rfec_line ln = J.plan.line[x];
+                sf = ln.first, sstr = ln.stride, cnt = ln.count, hrec = ln.first, hstr = ln.stride;
+            } else { // the members, then the parity slot; records: the parity's, then the members'
+                sf = J.slot0[x], sstr = 1u, cnt = J.count[x] + 1u, hrec = J.slot0[x], hstr = 1u;
             }
-        } else {
-            for (uint32_t it = threadIdx.x; it < J.groups * tj; it += kSvcBlock) {
-                const uint32_t g = it / tj, jj = it - g * tj, j = j0 + jj;
-                if (j >= (J.fsize[g] + 15u) / 16u)
-                    continue;
-                const uint32_t s0 = J.slot0[g], n = J.count[g];
-                v4u acc = chunk(lds, J, s0 + n, tj, jj, j); // the parity slot follows the members
-                for (uint32_t q = 0; q < n; ++q)
-                    acc ^= chunk(lds, J, s0 + q, tj, jj, j);
-                st_sys(ro, 16u * (g * C + j), acc);
+            for (uint32_t jb = 0; jb < max(tj, 1u); jb += 128u) {
+                R.a[0] = R.a[1] = v4u{0, 0, 0, 0};
+                if (tj || hdr) // (no columns in this workgroup: the records alone)
+                    line_pass(J, lds, max(tj, 1u), jb, sf, sstr, cnt, hrec, hstr, hdr && jb == 0, R);
+                bound = enc ? R.nck : (J.fsize[x] + 15u) / 16u; // past fec_data_size: never read back
+                if (!tj)
+                    break;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t jj = jb + 64u * h + lane;
+                    if (jj < tj && j0 + jj < bound)
+                        st_sys(ro, 16u * (x * C + j0 + jj), R.a[h]);
+                }
+            }
+            if (hdr && lane < 5u) {
+                st_sys32(rc, CTL_OFF(out.meta) + 20u * x + 4u * lane, R.h);
+                if (lane == 4u) {
+                    if (enc) {
+                        st_sys16(rc, CTL_OFF(out.fsize) + 2u * x, (uint16_t)R.L);
+                        st_sys8(rc, CTL_OFF(out.status) + x, (cnt <= 1u || R.L > J.capacity) ? 0xFFu : 0u);
+                    } else {
+                        // R.L: the largest of the parity's and the members' sizes; R.h: the recovered
+                        // record's size word.  The parity's own size field is fec_meta's XOR, not a
+                        // length: check the members and the recovered size against fec_data_size.
+                        const uint32_t L = J.fsize[x];
+                        bool ok = L <= J.capacity && (R.h >> 16) <= L;
+                        for (uint32_t q = 1; q < cnt; ++q)
+                            ok = ok && (J.hdr[5u * (hrec + q) + 4u] >> 16) <= L;
+                        st_sys8(rc, CTL_OFF(out.status) + x, ok ? 0u : 0xFFu);
+                    }
+                }
             }
         }
         if (tj == 0)
@@ -258,7 +260,6 @@ __global__ __launch_bounds__(kSvcBlock) void k_service(SvcArgs A)
     __shared__ __attribute__((aligned(16))) v4u lds[kSvcLdsChunks];
     __shared__ uint32_t s_ns, s_exit, s_seq;
     __shared__ uint64_t s_t1;
-    __shared__ uint16_t fsz[RFEC_MAX_LINES];
     __shared__ __attribute__((aligned(16))) rfec_svc_job J; // the job description, copied per job
     const uint32_t w = blockIdx.x, nw = gridDim.x;
     const bool leader = w == 0;
@@ -300,7 +301,7 @@ __global__ __launch_bounds__(kSvcBlock) void k_service(SvcArgs A)
         const uint32_t seq = s_seq;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the job's bytes, written before the doorbell
-        svc_job(A, min(s_ns, (uint32_t)RFEC_SVC_SLOTS), c0, c1, leader, lds, J, fsz, &s_t1);
+        svc_job(A, min(s_ns, (uint32_t)RFEC_SVC_SLOTS), c0, c1, leader, lds, J, &s_t1);
         const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
         // every wave's system-coherent stores acknowledged before `done`
         __builtin_amdgcn_s_waitcnt(0);

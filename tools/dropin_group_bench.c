@@ -28,6 +28,21 @@
 
 #define K 10
 
+static int cmp_d(const void* a, const void* b)
+{
+    const double x = *(const double*)a, y = *(const double*)b;
+    return x < y ? -1 : x > y;
+}
+
+/* the q-quantile of n samples (sorts them) */
+static double quantile(double* v, int n, double q)
+{
+    if (n <= 0)
+        return 0;
+    qsort(v, (size_t)n, sizeof(double), cmp_d);
+    return v[(int)(q * (n - 1) + 0.5)];
+}
+
 static double now_us(void)
 {
     struct timespec ts;
@@ -86,6 +101,7 @@ int main(int argc, char** argv)
 
     /* sender, group level (first group: staging set-up, untimed) */
     double t_group = 0;
+    double* tg = (double*)malloc((size_t)groups * sizeof(double));
     for (int g = -1; g < groups; ++g) {
         fill(segs, 1 + (uint32_t)(g + 1) * K);
         const double t0 = now_us();
@@ -93,8 +109,10 @@ int main(int argc, char** argv)
             flex_fec_sender_add_segment(fs, segs[i]);
         flex_fec_sender_update(fs, 80, &out);
         const double t1 = now_us();
-        if (g >= 0)
+        if (g >= 0) {
             t_group += t1 - t0;
+            tg[g] = t1 - t0;
+        }
         if (out.size != 7)
             ok = 0;
         flex_fec_sender_release(fs, &out);
@@ -141,6 +159,7 @@ int main(int argc, char** argv)
      * and 9 (column 1) lost, segment 5 (row 1, column 1 of the 3 x 4 matrix)
      * arrives last: its arrival recovers both */
     double t_rx = 0, t_rx2 = 0;
+    double* tr = (double*)malloc(500 * sizeof(double));
     const int rx_groups = groups < 500 ? groups : 500;
     for (int g = -1; g < rx_groups; ++g) {
         flex_fec_receiver_t* r = flex_fec_receiver_create(NULL, NULL, NULL);
@@ -164,8 +183,10 @@ int main(int argc, char** argv)
         const double t0 = now_us();
         flex_fec_receiver_on_segment(r, segs[5], &got);
         const double t1 = now_us();
-        if (g >= 0)
+        if (g >= 0) {
             t_rx += t1 - t0;
+            tr[g] = t1 - t0;
+        }
         if (got.size != 2 || ((sim_segment_t*)got.head->pdata)->packet_id != segs[4]->packet_id ||
             ((sim_segment_t*)got.tailer->pdata)->packet_id != segs[9]->packet_id ||
             memcmp(((sim_segment_t*)got.head->pdata)->data, segs[4]->data, SIM_VIDEO_SIZE) != 0 ||
@@ -199,11 +220,14 @@ int main(int argc, char** argv)
            " \"sender_group_level_us_per_group\": %.2f,\n"
            " \"sender_line_level_us_per_group\": %.2f,\n"
            " \"receiver_on_segment_row_and_col_us\": %.2f,\n"
+           " \"sender_group_level_us_median\": %.2f, \"sender_group_level_us_p10\": %.2f,"
+           " \"receiver_on_segment_us_median\": %.2f,\n"
            " \"receiver_two_flex_fec_recover_us\": %.2f,\n"
            " \"outputs_equal\": %s,\n"
            " \"service_sender\": {\"jobs\": %llu, \"launches\": %llu, \"stage_host_us\": %.2f, \"wait_us\": %.2f,"
            " \"dev_stage_us\": %.2f, \"dev_work_us\": %.2f, \"dev_release_us\": %.2f, \"request_in_device\": %u}}\n",
-           groups, K, SIM_VIDEO_SIZE, t_group / groups, t_line / groups, t_rx / rx_groups, t_rx2 / rx_groups,
+           groups, K, SIM_VIDEO_SIZE, t_group / groups, t_line / groups, t_rx / rx_groups,
+           quantile(tg, groups, 0.5), quantile(tg, groups, 0.1), quantile(tr, rx_groups, 0.5), t_rx2 / rx_groups,
            ok ? "true" : "false", (unsigned long long)si.jobs, (unsigned long long)si.launches, si.stage_host_us,
            si.wait_us, si.dev_stage_us, si.dev_work_us, si.dev_release_us, si.request_in_device);
     drain(&out);
