@@ -1500,10 +1500,17 @@ int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
 }
 
 /* ---- the receive direction: rfec_host_recover_groups --------------------- */
+/* Host -> device in one copy: the headers, masks and maps, then only the
+ * RECEIVED payloads, packed (`packed`, last, so the copy ends at the last
+ * used slot; lost segments and parities are not shipped).  On the device two
+ * row gathers expand them into the dense slot arrays the recover kernels read
+ * (`shards`, `parity`, device-only; a lost slot zero), then the recover
+ * kernel, then the recovered rows back. */
 typedef struct {
-    size_t shards, hdr, present, parity, meta, fsize, ppm, in_bytes; /* host -> device, one copy */
-    size_t out_shards, out_hdr, out_index, recovered, out_bytes;      /* device -> host */
-    size_t ws, total;                                                /* device workspace */
+    size_t hdr, present, meta, fsize, ppm, smap, pmap, packed; /* host -> device: [0, packed + used slots) */
+    size_t shards, parity;                                       /* device only: the dense slots */
+    size_t out_shards, out_hdr, out_index, recovered, out_bytes; /* device -> host */
+    size_t ws, total;                                            /* device workspace */
 } hr_layout;
 
 static hr_layout hr_offsets(const rfec_plan* plan, uint32_t G, uint32_t E)
@@ -1516,14 +1523,16 @@ static hr_layout hr_offsets(const rfec_plan* plan, uint32_t G, uint32_t E)
         L.field = o;                                    \
         o = (o + (size_t)(bytes) + 255) & ~(size_t)255; \
     } while (0)
-    HR_TAKE(shards, (size_t)G * k * DI_STRIDE);
     HR_TAKE(hdr, (size_t)G * k * sizeof(rfec_hdr));
     HR_TAKE(present, (size_t)G * 16);
-    HR_TAKE(parity, (size_t)G * n * DI_STRIDE);
     HR_TAKE(meta, (size_t)G * n * sizeof(rfec_hdr));
     HR_TAKE(fsize, (size_t)G * n * sizeof(uint16_t));
     HR_TAKE(ppm, (size_t)G * 8);
-    L.in_bytes = o;
+    HR_TAKE(smap, (size_t)G * k * sizeof(int32_t));
+    HR_TAKE(pmap, (size_t)G * n * sizeof(int32_t));
+    HR_TAKE(packed, (size_t)G * (k + n) * DI_STRIDE);
+    HR_TAKE(shards, (size_t)G * k * DI_STRIDE);
+    HR_TAKE(parity, (size_t)G * n * DI_STRIDE);
     HR_TAKE(out_shards, (size_t)G * E * DI_STRIDE);
     HR_TAKE(out_hdr, (size_t)G * E * sizeof(rfec_hdr));
     HR_TAKE(out_index, (size_t)G * E);
@@ -1543,12 +1552,29 @@ typedef struct {
     uint8_t* out_index;
     uint64_t* recovered;
     uint8_t* slot;
+    uint32_t* base; /* group g's first packed slot (prefix sums of the received counts) */
     hr_layout L;
     uint32_t E;
 } hr_chunk;
 
-/* gather one group per index: received payloads / headers (a lost member's
- * slot zero, its header zero), masks, received parities */
+/* received segments + parities of each group (the first pass: packed offsets) */
+static void hr_count(void* arg, size_t lo, size_t hi)
+{
+    const hr_chunk* h = (const hr_chunk*)arg;
+    const uint32_t k = h->plan->k, n = h->plan->n_lines;
+    for (size_t g = lo; g < hi; ++g) {
+        uint32_t c = 0;
+        for (uint32_t i = 0; i < k; ++i)
+            c += h->segs[g * k + i] != NULL;
+        for (uint32_t l = 0; l < n; ++l)
+            c += h->fecs[g * n + l] != NULL;
+        h->base[g] = c;
+    }
+}
+
+/* gather one group per index: received payloads into the packed slots from
+ * base[g] on (members, then parities) with their rows in the maps (-1: lost,
+ * a zero row on the device), headers (a lost member's zero), masks */
 static void hr_gather(void* arg, size_t lo, size_t hi)
 {
     const hr_chunk* h = (const hr_chunk*)arg;
@@ -1558,18 +1584,22 @@ static void hr_gather(void* arg, size_t lo, size_t hi)
     rfec_hdr* mh = (rfec_hdr*)(h->slot + h->L.meta);
     uint16_t* fs = (uint16_t*)(h->slot + h->L.fsize);
     uint64_t* ppm = (uint64_t*)(h->slot + h->L.ppm);
+    int32_t* smap = (int32_t*)(h->slot + h->L.smap);
+    int32_t* pmap = (int32_t*)(h->slot + h->L.pmap);
+    uint8_t* packed = h->slot + h->L.packed;
     for (size_t g = lo; g < hi; ++g) {
         uint64_t m0 = 0, m1 = 0, pm = 0;
+        uint32_t r = h->base[g];
         for (uint32_t i = 0; i < k; ++i) {
             const size_t s = g * k + i;
             const sim_segment_t* seg = h->segs[s];
-            uint8_t* slot = h->slot + h->L.shards + s * DI_STRIDE;
             if (!seg) {
-                memset(slot, 0, DI_STRIDE);
+                smap[s] = -1;
                 memset(&hh[s], 0, sizeof(rfec_hdr));
                 continue;
             }
-            stage_payload(slot, seg->data, seg->data_size);
+            smap[s] = (int32_t)r;
+            stage_payload(packed + (size_t)r++ * DI_STRIDE, seg->data, seg->data_size);
             seg_to_hdr(seg, &hh[s]);
             if (i < 64)
                 m0 |= 1ull << i;
@@ -1580,13 +1610,15 @@ static void hr_gather(void* arg, size_t lo, size_t hi)
             const size_t o = g * n + l;
             const sim_fec_t* f = h->fecs[o];
             if (!f) {
+                pmap[o] = -1;
                 fs[o] = 0;
                 continue;
             }
             pm |= 1ull << l;
             memcpy(&mh[o], &f->fec_meta, sizeof(rfec_hdr));
             fs[o] = f->fec_data_size;
-            stage_payload(h->slot + h->L.parity + o * DI_STRIDE, f->fec_data,
+            pmap[o] = (int32_t)r;
+            stage_payload(packed + (size_t)r++ * DI_STRIDE, f->fec_data,
                           f->fec_data_size < SIM_VIDEO_SIZE ? f->fec_data_size : SIM_VIDEO_SIZE);
         }
         pres[2 * g] = m0;
@@ -1655,8 +1687,8 @@ int rfec_host_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
     if (!c)
         return RFEC_EDEVICE;
     const uint32_t k = plan->k, E = per_group;
-    uint32_t chunk = (groups + 7) / 8;
-    chunk = chunk < 2048 ? 2048 : chunk;
+    uint32_t chunk = (groups + 7) / 8; /* 2,048-16,384 groups a step: ~1 GiB of pinned staging at most */
+    chunk = chunk < 2048 ? 2048 : chunk > 16384 ? 16384 : chunk;
     chunk = chunk > groups ? groups : chunk;
     const uint32_t nch = (groups + chunk - 1) / chunk;
     const hr_layout L = hr_offsets(plan, chunk, E);
@@ -1667,13 +1699,19 @@ int rfec_host_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
     const int threads = host_threads();
     double gather_us = 0, scatter_us = 0, h2d_us = 0, kernel_us = 0, d2h_us = 0;
     hr_chunk job[2];
+    uint32_t* base = (uint32_t*)malloc(2 * (size_t)chunk * sizeof(uint32_t));
+    if (!base)
+        return set_err(RFEC_ENOMEM, "recover offsets", 0);
+    rc = RFEC_OK;
     const double t0 = now_us();
     for (uint32_t it = 0; it < nch + 2; ++it) {
         if (it >= 2) { /* retire chunk it-2 */
             const uint32_t s = (it - 2) & 1;
             hipError_t e = hipEventSynchronize(c->ev[s][3]);
-            if (e != hipSuccess)
-                return set_err(RFEC_EDEVICE, "D2H wait", e);
+            if (e != hipSuccess) {
+                rc = set_err(RFEC_EDEVICE, "D2H wait", e);
+                break;
+            }
             float a = 0, b = 0, d = 0;
             (void)hipEventElapsedTime(&a, c->ev[s][0], c->ev[s][1]);
             (void)hipEventElapsedTime(&b, c->ev[s][1], c->ev[s][2]);
@@ -1698,32 +1736,60 @@ int rfec_host_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
             h->out_index = out_index ? out_index + (size_t)g0 * E : NULL;
             h->recovered = recovered ? recovered + (size_t)g0 * 2 : NULL;
             h->slot = c->bh + (size_t)s * L.total;
+            h->base = base + (size_t)s * chunk;
             h->L = L;
             h->E = E;
             const double tg = now_us();
+            parallel_for(ng, threads, hr_count, h);
+            uint32_t used = 0;
+            for (uint32_t g = 0; g < ng; ++g) { /* counts -> first packed slots */
+                const uint32_t cg = h->base[g];
+                h->base[g] = used;
+                used += cg;
+            }
             parallel_for(ng, threads, hr_gather, h);
             gather_us += now_us() - tg;
             uint8_t* dv = c->bd + (size_t)s * L.total;
             hipStream_t st = c->bstream[s];
             hipError_t e;
             if ((e = hipEventRecord(c->ev[s][0], st)) != hipSuccess ||
-                (e = hipMemcpyAsync(dv, h->slot, L.in_bytes, hipMemcpyHostToDevice, st)) != hipSuccess ||
-                (e = hipEventRecord(c->ev[s][1], st)) != hipSuccess)
-                return set_err(RFEC_EDEVICE, "H2D", e);
+                (e = hipMemcpyAsync(dv, h->slot, L.packed + (size_t)used * DI_STRIDE, hipMemcpyHostToDevice, st)) !=
+                    hipSuccess ||
+                (e = hipEventRecord(c->ev[s][1], st)) != hipSuccess) {
+                rc = set_err(RFEC_EDEVICE, "H2D", e);
+                break;
+            }
+            int ke = rfec_launch_gather_rows(dv + L.shards, dv + L.packed, (const int32_t*)(dv + L.smap), ng * k,
+                                             DI_STRIDE, st);
+            if (!ke)
+                ke = rfec_launch_gather_rows(dv + L.parity, dv + L.packed, (const int32_t*)(dv + L.pmap),
+                                             ng * plan->n_lines, DI_STRIDE, st);
             const rfec_dense_out D = {dv + L.out_shards, (rfec_hdr*)(dv + L.out_hdr), dv + L.out_index, E};
-            const int ke = rfec_launch_recover_out(
+            if (!ke)
+                ke = rfec_launch_recover_out(
                 &M, ng, DI_STRIDE, SIM_VIDEO_SIZE, dv + L.shards, (const rfec_hdr*)(dv + L.hdr),
                 (const uint64_t*)(dv + L.present), dv + L.parity, (const rfec_hdr*)(dv + L.meta),
                 (const uint16_t*)(dv + L.fsize), (const uint64_t*)(dv + L.ppm), (uint64_t*)(dv + L.recovered),
                 dv + L.ws, st, g_tuning, &D);
-            if (ke)
-                return set_err(RFEC_EDEVICE, "recover launch", ke);
+            if (ke) {
+                rc = set_err(RFEC_EDEVICE, "recover launch", ke);
+                break;
+            }
             if ((e = hipEventRecord(c->ev[s][2], st)) != hipSuccess ||
                 (e = hipMemcpyAsync(h->slot + L.out_shards, dv + L.out_shards, L.out_bytes, hipMemcpyDeviceToHost,
                                     st)) != hipSuccess ||
-                (e = hipEventRecord(c->ev[s][3], st)) != hipSuccess)
-                return set_err(RFEC_EDEVICE, "D2H", e);
+                (e = hipEventRecord(c->ev[s][3], st)) != hipSuccess) {
+                rc = set_err(RFEC_EDEVICE, "D2H", e);
+                break;
+            }
         }
+    }
+    free(base);
+    if (rc != RFEC_OK) {
+        /* a failed step: the other buffer's work drains before its staging is reused */
+        (void)hipStreamSynchronize(c->bstream[0]);
+        (void)hipStreamSynchronize(c->bstream[1]);
+        return rc;
     }
     if (timing) {
         timing->gather_us = gather_us;
