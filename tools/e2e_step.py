@@ -87,8 +87,10 @@ def run(lib, G, full, reps):
             "encode_e2e_gibps": round(enc_bytes / (e_t["total_us"] * 1e-6) / 2**30, 2),
             "decode_e2e_gibps": round(dec_bytes / (d_t["total_us"] * 1e-6) / 2**30, 2),
             "step_e2e_gibps": round((enc_bytes + dec_bytes) / (wall * 1e-6) / 2**30, 2),
+            # decode H2D: the received payloads only, in 1,216-B slots (2 of k lost), + headers, masks, row maps
             "pcie_bytes": {"encode_h2d": G * k * (S + 20), "encode_d2h": G * n * (S + 23),
-                           "decode_h2d": G * (k * (S + 20) + n * (S + 22) + 24), "decode_d2h": G * 2 * (S + 21) + 16 * G},
+                           "decode_h2d": G * ((k - 2 + n) * 1216 + k * 20 + n * 22 + 24 + (k + n) * 4),
+                           "decode_d2h": G * 2 * (S + 21) + 16 * G},
             "bytes": {"encode": enc_bytes, "decode": dec_bytes}, "reps": reps, "verified": ok}
 
 
