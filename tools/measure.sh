@@ -23,7 +23,9 @@ step() {  # step <name> <timeout> <cmd...>
 }
 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step group_bench 200 ./razor_amd/lib/fec_dropin_group_bench 2000
+LOCAL=$(bash tools/gpu_local_cpus.sh)  # the drop-in bench pinned to the GPU's NUMA node
+if [ -n "$LOCAL" ]; then step group_bench 200 taskset -c "$LOCAL" ./razor_amd/lib/fec_dropin_group_bench 2000
+else step group_bench 200 ./razor_amd/lib/fec_dropin_group_bench 2000; fi
 step bench 400 python bench.py
 step rocprof_stats 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python bench.py
 step bench_c3full 400 python bench.py --config c3full --no-cpu
