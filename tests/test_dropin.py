@@ -26,10 +26,12 @@ HARNESS = ROOT / "razor_amd" / "lib" / "fec_test_harness"
 REFERENCE = Path("/root/reference")
 
 
-# the resident service (default), with a relaunch before every call (a 1 us
-# idle window races the workgroup's exit against the next post), and kernel
-# launches per call
-SERVICE_ENVS = {"service": {}, "service_relaunch": {"RFEC_SERVICE_IDLE_US": "1"}, "launch": {"RFEC_SERVICE": "0"}}
+# the resident service (default: its request side in host-mapped device
+# memory where the host maps it), the same with the request side in pinned host
+# memory, with a relaunch before every call (a 1 us idle window races the
+# workgroup's exit against the next post), and kernel launches per call
+SERVICE_ENVS = {"service": {}, "service_host_staged": {"RFEC_SERVICE_STAGE": "host"},
+                "service_relaunch": {"RFEC_SERVICE_IDLE_US": "1"}, "launch": {"RFEC_SERVICE": "0"}}
 
 
 @pytest.mark.gpu

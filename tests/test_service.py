@@ -117,3 +117,34 @@ def test_service_does_not_hold_other_streams(tmp_path, life_us):
         assert 0.5 < d["since_call_s"] < 5.0, d  # the service really was resident meanwhile
     else:
         assert d["device_sync_s"] < 0.05, d
+
+
+@pytest.mark.parametrize("stage", ["default", "host"])
+def test_group_dropin_request_side(stage):
+    """tools/dropin_group_bench.c (built with the library): 300 group-level
+    sender updates and receiver recoveries through the service, their outputs
+    equal to the line-level drop-in's, with the request side (doorbell, job,
+    staged segments) in host-mapped device memory (default, where the host maps
+    it) or in pinned host memory (RFEC_SERVICE_STAGE=host)."""
+    import json
+    import os
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parent.parent / "razor_amd" / "lib" / "fec_dropin_group_bench"
+    assert exe.exists(), "razor_amd/lib/fec_dropin_group_bench not built"
+    env = dict(os.environ)
+    env.pop("RFEC_SERVICE", None)
+    if stage == "host":
+        env["RFEC_SERVICE_STAGE"] = "host"
+    else:
+        env.pop("RFEC_SERVICE_STAGE", None)
+    r = subprocess.run([str(exe), "300"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout)
+    assert d["outputs_equal"] is True
+    svc = d["service_sender"]
+    assert svc["jobs"] >= 300
+    if stage == "host":
+        assert svc["request_in_device"] == 0
+    else:
+        assert svc["request_in_device"] in (0, 1)
