@@ -32,7 +32,10 @@ is each kernel's own start / stop, HIP events bound to the launch itself
 what rocprofv3 reports per kernel; no event marker sits between the launches
 then.  `--timing bracket` records stream events around each call instead
 (the window then also holds the command processor's dispatch gap, 3-4 µs per
-launch, and the markers cost the step time a little).
+launch).  Either kind is recorded on every 8th timed step only: an event pair
+around a launch adds ~4.6 µs of dispatch gap to its step (tools/gap_probe.py:
+0.2888 ms per c3 step without events, 0.2981 with the kernels' own events on
+every step), which would otherwise be charged to `value`.
 
 Prints ONE JSON line (rank 0).
 """
@@ -450,9 +453,19 @@ def free_port():
 
 
 TIMING_OWN = ("the kernel's own start / stop: HIP events bound to the launch (rfec_timing_events -> "
-              "hipExtLaunchKernel) on the launch stream, mean over the timed steps")
-TIMING_BRACKET = ("HIP events recorded on the launch stream before and after the call (holds the dispatch "
-                  "gap; --timing bracket, or a call that launches more than one kernel)")
+              "hipExtLaunchKernel) on the launch stream, mean over every 8th timed step (events on every step "
+              "would add ~4.6 us of dispatch gap per launch to the timed region)")
+TIMING_BRACKET = ("HIP events recorded on the launch stream before and after the call on every 8th timed step "
+                  "(holds the dispatch gap; --timing bracket, or a call that launches more than one kernel)")
+
+
+# Kernel windows are recorded on every TIMING_EVERY-th timed step only: an
+# event pair around a launch (hipExtLaunchKernel's or the stream's) costs the
+# step ~4.6 us of dispatch gap (tools/gap_probe.py: 0.2888 ms per step with no
+# events, 0.2981 with the kernels' own events on every step, 0.3035 with
+# stream events); the windows are still those of launches inside the timed
+# region.
+TIMING_EVERY = 8
 
 
 def time_steps(lib, sets, steps, warmup, stream, dist, timing, hot):
@@ -460,8 +473,8 @@ def time_steps(lib, sets, steps, warmup, stream, dist, timing, hot):
     `steps` steps (encode one set, decode the set encoded one step earlier, or
     the same set when `hot` or one set) between a barrier + device
     synchronize on both sides.  Returns (elapsed wall seconds, max over ranks;
-    per-step encode / decode launch seconds; whether each is the kernel's own
-    window)."""
+    encode / decode launch seconds of the sampled steps (every TIMING_EVERY-th,
+    from the first); whether each is the kernel's own window)."""
     nset = len(sets)
     sp = stream.cuda_stream
     device = stream.device
@@ -496,29 +509,32 @@ def time_steps(lib, sets, steps, warmup, stream, dist, timing, hot):
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for i in range(steps):
-        # the kernels' own events where a call is one launch (no marker between launches), else a bracket
+        # sampled steps: the kernels' own events where a call is one launch (no marker between launches),
+        # else a bracket
+        smp = i % TIMING_EVERY == 0
         ka, kb, kc, kd = kev[i]
         a, b, c, d = ev[i]
-        if own_enc:
+        if smp and own_enc:
             lib.timing_events(ka.cuda_event, kb.cuda_event)
-        else:
+        elif smp:
             a.record(stream)
         sets[(warmup + i) % nset].encode(sp)
-        if not own_enc:
+        if smp and not own_enc:
             b.record(stream)
-        if own_dec:
+        if smp and own_dec:
             lib.timing_events(kc.cuda_event, kd.cuda_event)
-        else:
+        elif smp:
             c.record(stream)
         dec_set(warmup + i).decode(sp)
-        if not own_dec:
+        if smp and not own_dec:
             d.record(stream)
     torch.cuda.synchronize(device)
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    t_enc = np.array([(q if own_enc else e)[0].elapsed_time((q if own_enc else e)[1]) for q, e in zip(kev, ev)]) / 1e3
-    t_dec = np.array([(q if own_dec else e)[2].elapsed_time((q if own_dec else e)[3]) for q, e in zip(kev, ev)]) / 1e3
+    sampled = list(zip(kev, ev))[::TIMING_EVERY]
+    t_enc = np.array([(q if own_enc else e)[0].elapsed_time((q if own_enc else e)[1]) for q, e in sampled]) / 1e3
+    t_dec = np.array([(q if own_dec else e)[2].elapsed_time((q if own_dec else e)[3]) for q, e in sampled]) / 1e3
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
