@@ -646,8 +646,8 @@ unsigned rfec_get_tuning(void);
 
 /* The drop-in's resident service: RFEC_SERVICE_GROUPS (default 1, at most 8)
  * workgroups that stay on the device and take the drop-in symbols' jobs from
- * a doorbell in pinned, host-coherent memory (no launch, no stream
- * synchronisation per call), each on its share of a job's 16-byte columns.  It starts on the
+ * a doorbell (no launch, no stream synchronisation per call), each on its
+ * share of a job's 16-byte columns.  It starts on the
  * first drop-in call and leaves the device by itself after RFEC_SERVICE_IDLE_US
  * (default 2000) microseconds without a job, after RFEC_SERVICE_LIFE_US (default
  * 4000) in total (the next call starts it again) and at exit.  The request side

@@ -542,9 +542,10 @@ static double now_us(void);
  * The drop-in symbols are called once per group under razor's session mutex
  * (sim_session.c:241, sim_sender.c:286-304), so their cost is latency: a
  * launch plus hipStreamSynchronize is ~15-20 us before any work.  Instead ONE
- * workgroup stays on the device and polls a doorbell in pinned, host-coherent
- * memory; a call stages its segments next to the doorbell, bumps `req` and
- * spins on `done` (a few PCIe round trips).  The workgroup leaves after
+ * workgroup stays on the device and polls a doorbell; a call stages its job
+ * and segments next to the doorbell (host-mapped device memory when the host
+ * maps it, else pinned host memory: svc_map_request_side), rings it and spins
+ * on `done` in pinned host memory (a PCIe write each way).  The workgroup leaves after
  * RFEC_SERVICE_IDLE_US (default 2 ms) without a job, after
  * RFEC_SERVICE_LIFE_US (default 4 ms) in total, on `stop` (rfec_service_stop,
  * atexit); a call that finds `alive` == 0 launches it again (~10-20 us for

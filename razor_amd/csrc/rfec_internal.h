@@ -95,9 +95,13 @@ __attribute__((visibility("hidden"))) int rfec_di_generate_group(sim_segment_t* 
                                                                  const rfec_plan* plan, sim_fec_t* const* outs,
                                                                  int* rets);
 __attribute__((visibility("hidden"))) int rfec_di_recover_lines(const rfec_di_recover_job* jobs, int n, int* rets);
-/* The resident service (rfec_service.hip): one workgroup polling a doorbell in
- * pinned, host-coherent memory for the drop-in's jobs.  A job's payloads sit
- * in staging slots 0..n_slots-1 (LDS slot s = staging slot s); its outputs go
+/* The resident service (rfec_service.hip): one workgroup polling a doorbell for
+ * the drop-in's jobs.  Two control blocks of this layout: the request side
+ * (bell, stop, quit, job; the staging slots follow it) in host-mapped device
+ * memory or pinned host memory, the results side (done, alive, out; the output
+ * slots follow it) in pinned host memory; with a host-memory request side
+ * they are one block.  A job's payloads sit in staging slots 0..n_slots-1
+ * (LDS slot s = staging slot s), zero-filled to the slot's end; its outputs go
  * to the output slots (encode: line l, recover: job g). */
 #define RFEC_SVC_ENCODE 1u
 #define RFEC_SVC_RECOVER 2u

@@ -15,12 +15,14 @@
 //
 // Protocol (rfec_svc_ctl, razor_amd/csrc/rfec_internal.h): the host writes a
 // job (payload slots into the staging area, the job description into the
-// control block), then the doorbell word (sequence number, slot count, op);
-// lane 0 of the workgroup polls it (relaxed system-scope loads + s_sleep), the
-// workgroup loads the job description and its payload slots into LDS in ONE
-// burst of system-coherent loads (one PCIe round trip), XORs, stores the
-// results to the output slots with system-coherent stores, waits for their
-// acknowledgements and writes `done`.  The
+// request-side control block -- host-mapped device memory, or pinned host
+// memory where the host cannot map it), then the doorbell word (sequence
+// number, slot count, op); lane 0 of the workgroup polls it (relaxed
+// system-scope loads + s_sleep), the workgroup loads the job description and
+// its payload slots into LDS in ONE burst (one device-memory or PCIe round
+// trip), XORs one wave per line, stores the results to the output slots in
+// pinned host memory with system-coherent stores, waits for their
+// acknowledgements and writes `done`; the job's timestamps follow `done`.  The
 // workgroup returns when `stop` is set, after `idle_ticks` without a job, or
 // after `life_ticks` in total (every wave leaves through the same uniform
 // test); the host relaunches it when a job finds it gone.
