@@ -29,7 +29,26 @@ __global__ __launch_bounds__(64) void k_clock(uint64_t* out, uint32_t reps)
             out[2 * k + 1] = c1 - c0;
         }
     }
-    if (x == 12345.f)
+    // latency of a dependent chain of 64 s_memrealtime / s_memtime (shader clocks each)
+    uint64_t acc = 0;
+    const uint64_t m0 = __builtin_amdgcn_s_memtime();
+    for (int i = 0; i < 64; ++i) { // each value consumed before the next is read
+        const uint64_t v = __builtin_amdgcn_s_memrealtime();
+        __asm__ volatile("; use %0" ::"s"(v));
+        acc += v & 1u;
+    }
+    const uint64_t m1 = __builtin_amdgcn_s_memtime();
+    for (int i = 0; i < 64; ++i) {
+        const uint64_t v = __builtin_amdgcn_s_memtime();
+        __asm__ volatile("; use %0" ::"s"(v));
+        acc += v & 1u;
+    }
+    const uint64_t m2 = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) {
+        out[8] = (m1 - m0) / 64;
+        out[9] = (m2 - m1) / 64;
+    }
+    if (x == 12345.f || acc == 12345)
         out[15] = 1;
 }
 
@@ -68,7 +87,8 @@ int main()
         for (int k = 0; k < 4; ++k)
             printf("%s\"%s_MHz\": %.0f", k ? ", " : "", names[k],
                    h[2 * k] ? 100.0 * (double)h[2 * k + 1] / (double)h[2 * k] : 0.0);
-        printf("}");
+        printf(", \"memrealtime_clk\": %llu, \"memtime_clk\": %llu}", (unsigned long long)h[8],
+               (unsigned long long)h[9]);
     }
     printf("}\n");
     return 0;

@@ -132,8 +132,9 @@ static int host_can_write(volatile uint32_t* p)
     return ok;
 }
 
-int main()
+int main(int argc, char** argv)
 {
+    const int want = argc > 1 ? atoi(argv[1]) : -1; // VRAM allocation to use: 0 hipMalloc, 1 fine-grained, 2 uncached
     const uint32_t bytes = 12288, nch = bytes / 16;
     // host side: bell, answer, payload
     uint8_t* h = nullptr;
@@ -170,7 +171,7 @@ int main()
         }
         printf("%s\"%s\": {\"allocated\": %d, \"host_pointer_attr\": %d, \"host_write\": %d}", c ? ", " : "",
                cand[c].name, cand[c].p != nullptr, hostp, cand[c].ok);
-        if (cand[c].ok && pick < 0 && c > 0)
+        if (cand[c].ok && pick < 0 && (want < 0 ? c > 0 : c == want))
             pick = c;
     }
     printf("}");
