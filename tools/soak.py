@@ -7,6 +7,10 @@ the exact peel reject lines, the generic or the default kernels -- and checks:
   encode: parities, metas, fec_data_size, status == oracle
   recover (in place): recovered masks, headers and data == oracle's peel
   recover_out (dense, E random): out slots, headers, indices, masks == oracle
+and, every other iteration, the wire codec on a random batch (SIM_SEG or
+SIM_FEC, capacity 16-1999, 1-20k datagrams): framed bytes and lengths ==
+oracle, then parse of the datagrams with random bytes flipped in ~5 % of them
+(records, statuses, payload slots == oracle; the intact ones round-trip).
 Runs for --seconds (default 120), prints one line per iteration (so a hang
 is visible), and writes a JSON summary; exit 1 on any mismatch.
 
@@ -27,7 +31,42 @@ sys.path[:0] = [str(ROOT), str(ROOT / "oracle"), str(ROOT / "tests")]
 
 import pyoracle as po  # noqa: E402
 from gpu_engine import GpuEngine  # noqa: E402
+from gpu_engine import GpuWire  # noqa: E402
 from test_gpu_parity import _lossy_rx  # noqa: E402
+import wire_cases as wc  # noqa: E402
+
+
+def check_wire(o, gw, rng):
+    capacity = int(rng.integers(16, 2000))
+    stride = (capacity + 15) // 16 * 16 + 16 * int(rng.integers(0, 3))
+    N = int(rng.integers(1, 20001))
+    seg = bool(rng.random() < 0.5)
+    data, hdr, sizes, stamps = wc.random_batch(rng, N, stride, capacity, seg=seg)
+    over = 36 if seg else 49
+    dstride = min(2048, (capacity + over + 15) // 16 * 16)
+    if seg:
+        g, gl = gw.frame_seg(data, hdr, stamps, capacity, dstride)
+        e, el = o.frame_seg_batch(data, hdr, stamps, capacity, dstride)
+    else:
+        g, gl = gw.frame_fec(data, hdr, sizes, None, stamps, capacity, dstride)
+        e, el = o.frame_fec_batch(data, hdr, sizes, None, stamps, capacity, dstride)
+    if not (np.array_equal(gl, el) and np.array_equal(g, e)):
+        return f"frame {'seg' if seg else 'fec'} N={N} cap={capacity}", (capacity, N, seg)
+    bad = rng.random(N) < 0.05
+    for i in np.nonzero(bad)[0]:
+        L = int(gl[i])
+        if L:
+            g[i, int(rng.integers(L))] ^= np.uint8(1 << int(rng.integers(8)))
+    recs, pay = gw.parse(g, gl, stride, capacity)
+    orecs, opay = o.parse_batch(g, gl, stride, capacity)
+    if not (np.array_equal(recs.view(np.uint8), orecs.view(np.uint8)) and np.array_equal(pay, opay)):
+        return f"parse N={N} cap={capacity}", (capacity, N, seg)
+    ok = ~bad
+    if not (np.array_equal(pay[ok], data.reshape(N, -1)[ok]) and (recs["status"][ok] == 0).all()):
+        return f"roundtrip N={N} cap={capacity}", (capacity, N, seg)
+    if bad.any() and not (recs["status"][bad] != 0).all():
+        return f"a flipped bit passed the CRC N={N}", (capacity, N, seg)
+    return None, (capacity, N, seg)
 
 
 def check_encode(o, eng, plan, shards, hdr, cap):
@@ -95,9 +134,20 @@ def main():
     rng = np.random.default_rng(args.seed)
     o = po.Oracle(1000)
     engines = {t: GpuEngine(1000, tuning=t) for t in (0, 1)}
+    gw = GpuWire(1000)
     t0 = time.time()
-    it, fails, groups, cfgs = 0, [], 0, set()
+    it, fails, groups, cfgs, wit, dgrams = 0, [], 0, set(), 0, 0
     while time.time() - t0 < args.seconds:
+        if (it + wit) % 2 == 1:
+            what, (cap_w, N, seg) = check_wire(o, gw, rng)
+            wit += 1
+            dgrams += N
+            line = f"wire {wit} {'SIM_SEG' if seg else 'SIM_FEC'} cap={cap_w} N={N} " + ("ok" if not what
+                                                                                     else "FAIL " + what)
+            print(line, flush=True)
+            if what:
+                fails.append(line)
+            continue
         k = int(rng.integers(2, 65))
         pf = int(rng.choice([5, 10, 20, 40, 80, 120, 200, 255]))
         plan = o.plan_from_fraction(k, pf, 3)
@@ -123,8 +173,8 @@ def main():
         print(line, flush=True)
         if what:
             fails.append(line)
-    out = {"iterations": it, "groups": groups, "distinct_k_lines": len(cfgs), "seconds": round(time.time() - t0, 1),
-           "seed": args.seed, "failures": fails}
+    out = {"iterations": it, "groups": groups, "distinct_k_lines": len(cfgs), "wire_iterations": wit,
+           "datagrams": dgrams, "seconds": round(time.time() - t0, 1), "seed": args.seed, "failures": fails}
     print(json.dumps(out))
     if args.out:
         Path(args.out).write_text(json.dumps(out, indent=1))
