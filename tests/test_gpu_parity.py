@@ -342,18 +342,19 @@ def test_host_encode_groups(product1200, oracle1200):
         assert np.array_equal(fecs["fec_data"][j, :L], ref["fec_data"][j, :L])
 
 
-@pytest.mark.parametrize("layers", [1, 3])
-def test_host_recover_groups(product1200, oracle1200, layers):
+@pytest.mark.parametrize("layers,G", [(1, 301), (3, 301), (3, 4500)])
+def test_host_recover_groups(product1200, oracle1200, layers, G):
     """rfec_host_recover_groups (host AoS in, flex_fec_recover-style out_seg
     out): groups encoded by rfec_host_encode_groups (checked above), 1-3
     segments and 0-2 parities of each lost; out_index / recovered masks equal
     the oracle's rfec_recover_batch_out restatement, every recovered out_seg
     equals the lost segment (header fields, data_size, data, zero past it)
-    and carries the group's fec_id."""
+    and carries the group's fec_id.  4,500 groups: three double-buffered
+    chunks of packed received rows (2,048, 2,048, 404)."""
     from razor_amd.fec import fec_dtype, seg_dtype
 
     lib, o = product1200, oracle1200
-    G, k, S, E = 301, 10, 1200, 3
+    k, S, E = 10, 1200, 3
     shards, hdr = o.fill_groups(203, G, k, S, ragged=True)
     plan = o.plan_from_fraction(k, 80, layers)
     n = plan.n_lines
