@@ -28,9 +28,12 @@ REFERENCE = Path("/root/reference")
 
 # the resident service (default: its request side in host-mapped device
 # memory where the host maps it), the same with the request side in pinned host
-# memory, with a relaunch before every call (a 1 us idle window races the
-# workgroup's exit against the next post), and kernel launches per call
+# memory, with four workgroups on column shares (the others leave on `quit`),
+# with a relaunch before every call (a 1 us idle window races the workgroup's
+# exit against the next post), and kernel launches per call
 SERVICE_ENVS = {"service": {}, "service_host_staged": {"RFEC_SERVICE_STAGE": "host"},
+                "service_4_workgroups": {"RFEC_SERVICE_GROUPS": "4"},
+                "service_4_workgroups_relaunch": {"RFEC_SERVICE_GROUPS": "4", "RFEC_SERVICE_IDLE_US": "1"},
                 "service_relaunch": {"RFEC_SERVICE_IDLE_US": "1"}, "launch": {"RFEC_SERVICE": "0"}}
 
 
