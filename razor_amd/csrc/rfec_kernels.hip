@@ -1229,12 +1229,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     // the first line that fires at once for it (masks and line records from the
     // kernel arguments: scalar loads, no LDS round trips before the payload loads)
     uint32_t l = 0xFFu, ln = 0;
+    { // (MT: 32-bit masks for k <= 32)
+        const MT er = (MT)erased, hv = (MT)have, tb = (MT)1 << tgt;
+        const uint32_t pp = (uint32_t)ppm;
 #pragma unroll
-    for (int x = 7; x >= 0; --x) {
-        const uint64_t lm = M.mask[x][0];
-        if ((uint32_t)x < NL && ((ppm >> x) & 1ull) && (lm & erased) == (1ull << tgt) && (lm & have)) {
-            l = (uint32_t)x;
-            ln = reinterpret_cast<const uint32_t*>(P.line)[x];
+        for (int x = 7; x >= 0; --x) {
+            const MT lm = (MT)M.mask[x][0];
+            if ((uint32_t)x < NL && ((pp >> x) & 1u) && (lm & er) == tb && (lm & hv)) {
+                l = (uint32_t)x;
+                ln = reinterpret_cast<const uint32_t*>(P.line)[x];
+            }
         }
     }
     const v4u* grp = A.shards + (size_t)g * K * C + j;
