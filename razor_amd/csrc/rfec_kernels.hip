@@ -1217,20 +1217,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     const uint32_t q = fdiv(rem, A.divC);
     const uint32_t j = rem - q * A.divC.d;
     const uint32_t K = P.k, NL = P.n_lines, C = A.C;
-    const uint64_t kmask = K >= 64 ? ~0ull : (1ull << K) - 1ull;
-    const uint64_t have = A.present[2 * g] & kmask, erased = ~have & kmask;
-    const uint64_t ppm = A.parity_present[g];
-    uint64_t e = erased; // slot q: the q-th erased segment
+    // (MT: 32-bit masks for k <= 32, the low words of present / parity_present)
+    constexpr uint32_t MB = 8 * sizeof(MT);
+    const MT kmaskM = K >= MB ? ~(MT)0 : (((MT)1 << K) - 1);
+    const MT hv = (MT)A.present[2 * g] & kmaskM, er = ~hv & kmaskM;
+    const uint64_t have = hv, erased = er, ppm = (uint32_t)A.parity_present[g]; // (NL <= 8 here)
+    MT e = er; // slot q: the q-th erased segment
     for (uint32_t i = 0; i < q; ++i)
         e &= e - 1;
     if (!e)
         return;
-    const uint32_t tgt = (uint32_t)__ffsll((long long)e) - 1;
+    const uint32_t tgt = MB == 32 ? (uint32_t)__ffs((int)e) - 1 : (uint32_t)__ffsll((long long)e) - 1;
     // the first line that fires at once for it (masks and line records from the
     // kernel arguments: scalar loads, no LDS round trips before the payload loads)
     uint32_t l = 0xFFu, ln = 0;
-    { // (MT: 32-bit masks for k <= 32)
-        const MT er = (MT)erased, hv = (MT)have, tb = (MT)1 << tgt;
+    {
+        const MT tb = (MT)1 << tgt;
         const uint32_t pp = (uint32_t)ppm;
 #pragma unroll
         for (int x = 7; x >= 0; --x) {
