@@ -599,6 +599,104 @@ def c4_strong(lib, device, stream, dist, world, rank, pf, steps, warmup, verify)
                 False if any(f[1] == 0 for f in flags) else (True if all(f[1] == 1 for f in flags) else None))}
 
 
+def kernel_desc(w, k, S, full_plan):
+    """(encode kernel, decode kernels) the library launches for this workload
+    (rfec_launch_encode / rfec_launch_recover_out dispatch, rfec_kernels.hip)."""
+    lines = [w.plan.line[l].count for l in range(w.n)]
+    rows_layout = not full_plan and len(set(lines[:-1])) <= 1
+    if rows_layout and (k, lines[0]) in ((10, 4), (32, 4)):
+        enc_kernel = f"k_encode_out<{k},{lines[0]}>"
+    elif rows_layout and lines[0] <= 16:
+        enc_kernel = "k_encode_out_rt (run-time k, col)"
+    elif full_plan:
+        enc_kernel = f"k_encode_matrix_out<{k},{w.plan.col}>"
+    else:
+        enc_kernel = "k_encode (plan-driven)"
+    cd = (S + 15) // 16
+    per = ("one lane per (group, output slot, chunk)" if w.dense and 2 <= len(lines)
+           else "one lane per (group, line, chunk)")
+    if full_plan:
+        dense_k = (f"k_decode_matrix_dense<{k},{w.plan.col}>" if 6 <= k <= 16 and w.plan.col == (3 if k <= 9 else 4)
+                   else "k_decode_cascade_dense")
+        dec_kernels = (f"{dense_k} (one launch: checker blocks spread over the payload lanes, one "
+                       "lane per (group, output slot, chunk))" if w.dense else
+                       "k_cascade_check + k_decode_cascade (one lane per (group, schedule step, chunk))")
+    elif cd >= 64 and rows_layout and (k, lines[0]) in ((10, 4), (32, 4)):
+        dec_kernels = f"k_decode_rows<{k},{lines[0]}> ({per}; header blocks spread)"
+    elif cd >= 64:
+        dec_kernels = f"k_decode_out ({per}; header blocks spread)"
+    else:
+        dec_kernels = "k_decode_disjoint (one lane per (group, chunk), every fired line; header blocks spread)"
+    return enc_kernel, dec_kernels, lines, rows_layout
+
+
+def config_sub(lib, name, device, stream, dist, world, rank, pf, steps, warmup, verify):
+    """A BASELINE configuration beside the c3 headline on the driver's default
+    line (c5 = configs[4]; c3full = configs[2] under the sender's whole 3 x 4
+    plan, the plan it really emits under loss): every rank runs the config's
+    65,536 groups on its own slice of the config's stream (groups
+    [r * 65,536, (r + 1) * 65,536), weak, as the headline), `steps` timed
+    encode + decode steps over two buffer sets with the headline's timing
+    discipline.  Every rank checks its outputs (torch XOR of every line, every
+    erased segment back bit-exact); rank 0's groups are the reference's
+    full-size digest case (full_hashes.json).  Returns the sub-object on rank
+    0 (None elsewhere)."""
+    cfg = CONFIGS[name]
+    k, S, G = cfg["k"], cfg["S"], cfg["groups"]
+    col = int(cfg["plan"][3:]) if cfg["plan"].startswith("col") else 0
+    full_plan = cfg["plan"] == "full"
+    sets = [Workload(lib, G, k, S, pf, device, rank * G, seed=2000 + 17 * rank, col=col, full_plan=full_plan,
+                     config_id=cfg["config_id"]) for _ in range(2)]
+    w = sets[0]
+    elapsed, t_enc, t_dec, own_enc, own_dec = time_steps(lib, sets, steps, warmup, stream, dist, "own", False)
+    verified = digest_ok = None
+    if verify:
+        verified = all(ws.verify() for ws in sets)
+        if rank == 0:
+            want = golden_digest(cfg["golden"], 1, 0)
+            digest_ok = None if want is None else w.digest() == want
+            verified = verified and digest_ok is not False
+    per_rank = torch.tensor([w.enc_bytes + w.dec_bytes, float(t_enc.mean()) * 1e6, float(t_dec.mean()) * 1e6,
+                             -1 if verified is None else int(verified)], dtype=torch.float64)
+    rows = [per_rank]
+    if dist:
+        rows = [torch.zeros_like(per_rank) for _ in range(world)]
+        dist.all_gather(rows, per_rank)
+    res = None
+    if rank == 0:
+        enc_kernel, dec_kernels, lines, _ = kernel_desc(w, k, S, full_plan)
+        mix = encode_mix(w)
+        mix_gbps = mix_ceiling(lib, device, *mix) if mix else None
+        enc_us, dec_us = float(rows[0][1]), float(rows[0][2])
+        ach = w.enc_bytes / (enc_us * 1e-6) / 1e9
+        wn = f"k{k}_r{w.n}_S{S}_G{G}"
+        res = {"workload": f"{name}: {wn}" + (f" per GPU x {world} (weak)" if world > 1 else ""),
+               "desc": cfg["desc"], "scaling": "weak",
+               "value": round(sum(float(r[0]) for r in rows) * steps / elapsed / 2**30, 3), "unit": "GiB/s",
+               "steps": steps, "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 4),
+               "buffer_sets": 2, "decode_order": "cold (the set encoded one step earlier), as the headline",
+               "plan_lines": lines, "bytes_per_step_per_gpu": {"encode": w.enc_bytes, "decode": w.dec_bytes},
+               "encode": {"kernel": enc_kernel, "launch_us": round(enc_us, 2),
+                          "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": load_traffic(wn, "encode"),
+                          "mix_ceiling": None if not mix else {
+                              "probe": f"rfec_probe_mix {mix[0]} reads : {mix[1]} writes, {mix[2]} B per stream",
+                              "GBps": round(mix_gbps, 1), "frac_of_peak": round(mix_gbps / HBM_PEAK_GBPS, 4),
+                              "kernel_vs_ceiling": round(ach / mix_gbps, 4)}},
+               "decode": {"kernels": dec_kernels, "launch_us": round(dec_us, 2),
+                          "frac": round(w.dec_bytes / (dec_us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+                          "traffic": load_traffic(wn, "decode")},
+               "encode_us_per_rank": [round(float(r[1]), 2) for r in rows],
+               "decode_us_per_rank": [round(float(r[2]), 2) for r in rows],
+               "timing": "per launch: " + (TIMING_OWN if own_enc and own_dec else TIMING_BRACKET),
+               "verified": None if not verify else all(int(r[3]) == 1 for r in rows),
+               "verified_vs_reference_digest": digest_ok,
+               "digest_scope": "rank 0's groups [0, 65,536) = the reference's full-size digest case "
+                               f"{cfg['golden']}; the other ranks' groups are checked by the torch XOR checks"}
+    del w, sets
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -629,6 +727,8 @@ def main():
                     help="decode the set encoded in the same step (its parity still MALL-resident)")
     ap.add_argument("--c4-steps", type=int, default=10,
                     help="timed steps of the c4_strong sub-object (config c3 only; 0 = skip it)")
+    ap.add_argument("--sub-steps", type=int, default=20,
+                    help="timed steps of the c5 / c3full sub-objects (config c3 only; 0 = skip them)")
     args = ap.parse_args()
 
     # --gpus N without a launcher: start N ranks under torchrun as a child
@@ -726,6 +826,15 @@ def main():
                        not args.no_verify)
         if c4 and c4["verified"] is False:
             verified = False
+    # BASELINE configs[4] (c5) and the sender's full plan (c3full) on the same line (default run only)
+    subs = {}
+    if cfg_name == "c3" and args.sub_steps > 0 and not args.lib:
+        for sub in ("c5", "c3full"):
+            log(f"{sub} ...")
+            subs[sub] = config_sub(lib, sub, device, stream, dist, world, rank, args.protect_fraction,
+                                   args.sub_steps, 2, not args.no_verify)
+            if subs[sub] and subs[sub]["verified"] is False:
+                verified = False
 
     # whole-job bytes: every rank's slice (equal slices up to one group)
     nb = torch.tensor([w.enc_bytes + w.dec_bytes, w.G], dtype=torch.float64)
@@ -742,24 +851,7 @@ def main():
         mix = encode_mix(w)
         mix_gbps = mix_ceiling(lib, device, *mix) if mix else None
         workload_name = f"k{k}_r{w.n}_S{S}_G{w.G}"
-        lines = [w.plan.line[l].count for l in range(w.n)]
-        rows_layout = not full_plan and len(set(lines[:-1])) <= 1
-        enc_kernel = (f"k_encode_out<{k},{lines[0]}>" if rows_layout and (k, lines[0]) in ((10, 4), (32, 4))
-                      else ("k_encode_out_rt (run-time k, col)" if rows_layout and lines[0] <= 16
-                            else (f"k_encode_matrix_lds<{k},{w.plan.col}>" if full_plan else "k_encode (plan-driven)")))
-        cd = (S + 15) // 16
-        per = ("one lane per (group, output slot, chunk)" if w.dense and 2 <= len(lines)
-               else "one lane per (group, line, chunk)")
-        if full_plan:
-            dec_kernels = ("k_decode_cascade_dense (one launch: checker blocks spread over the payload lanes, one "
-                           "lane per (group, output slot, chunk))" if w.dense else
-                           "k_cascade_check + k_decode_cascade (one lane per (group, schedule step, chunk))")
-        elif cd >= 64 and rows_layout and (k, lines[0]) in ((10, 4), (32, 4)):
-            dec_kernels = f"k_decode_rows<{k},{lines[0]}> ({per}; header blocks spread)"
-        elif cd >= 64:
-            dec_kernels = f"k_decode_out ({per}; header blocks spread)"
-        else:
-            dec_kernels = "k_decode_disjoint (one lane per (group, chunk), every fired line; header blocks spread)"
+        enc_kernel, dec_kernels, lines, _ = kernel_desc(w, k, S, full_plan)
         if full_plan:
             plan_desc = (f"full reference plan {w.plan.row}x{w.plan.col}: {w.plan.n_row_lines} rows + "
                          f"{w.n - w.plan.n_row_lines} columns, line sizes {lines}")
@@ -835,6 +927,9 @@ def main():
         }
         if c4 is not None:
             res["c4_strong"] = c4
+        for sub, d in subs.items():
+            if d is not None:
+                res[sub] = d
         if world == 1 and not args.no_cpu:
             log("cpu baseline ...")
             res["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)

@@ -633,8 +633,12 @@ int rfec_rx_session_get_info(const rfec_rx_session* s, rfec_rx_session_info* inf
  * plan allows); RFEC_TUNE_GENERIC = the plan-driven kernels for every plan
  * (encode: one lane per (group, chunk column) over the plan's lines; recover
  * in place: the LDS peel + schedule replay), the cross-check of the
- * specialised ones.  Other bits are ignored. */
+ * specialised ones.  Other bits: below, or ignored. */
 #define RFEC_TUNE_GENERIC 1u
+/* RFEC_TUNE_PLAN_CASCADE: a dense recover of the sender's matrix plan
+ * (k = 6..16) takes the plan-driven cascade kernel instead of the one
+ * compiled for its shape (the A/B and cross-check of the latter). */
+#define RFEC_TUNE_PLAN_CASCADE (1u << 2)
 /* RFEC_TUNE_NO_SERVICE: the drop-in symbols (flex_fec_generate / _recover, the
  * group-level sender and receiver) launch their kernels per call instead of
  * posting to the resident service (process-wide; also RFEC_SERVICE=0 in the

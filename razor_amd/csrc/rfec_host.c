@@ -24,6 +24,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include "razor_fec.h"
 #include "rfec_internal.h"
@@ -103,15 +104,19 @@ int rfec_num_packets(uint16_t k, uint8_t protect_fraction, uint8_t* row, uint8_t
     return rc;
 }
 
-static void add_line(rfec_plan* p, int first, int stride, int count, int index)
+/* returns -1 when the plan would exceed RFEC_MAX_LINES lines */
+static int add_line(rfec_plan* p, int first, int stride, int count, int index)
 {
     if (count < 2) /* flex_fec_generate refuses <2 members: no parity on the wire */
-        return;
+        return 0;
+    if (p->n_lines >= RFEC_MAX_LINES)
+        return -1;
     rfec_line* l = &p->line[p->n_lines++];
     l->first = (uint8_t)first;
     l->stride = (uint8_t)stride;
     l->count = (uint8_t)count;
     l->index = (uint8_t)index;
+    return 0;
 }
 
 static int build_plan(uint16_t k, uint8_t row, uint8_t col, int rc, unsigned layers, rfec_plan* p)
@@ -131,7 +136,8 @@ static int build_plan(uint16_t k, uint8_t row, uint8_t col, int rc, unsigned lay
         for (int r = 0; r < row; ++r) {
             const int first = r * col;
             const int left = (int)k - first;
-            add_line(p, first, 1, left < col ? left : col, r);
+            if (add_line(p, first, 1, left < col ? left : col, r))
+                return set_err(RFEC_EINVAL, "plan above RFEC_MAX_LINES lines", 0);
         }
     }
     p->n_row_lines = p->n_lines;
@@ -140,7 +146,8 @@ static int build_plan(uint16_t k, uint8_t row, uint8_t col, int rc, unsigned lay
             int count = 0;
             while (count < row && count * col + c < (int)k)
                 ++count;
-            add_line(p, c, col, count, 0x80 | c);
+            if (add_line(p, c, col, count, 0x80 | c))
+                return set_err(RFEC_EINVAL, "plan above RFEC_MAX_LINES lines", 0);
         }
     }
     return RFEC_OK;
@@ -406,7 +413,7 @@ typedef struct {
      * mirrors, one stream and four events per slot */
     uint8_t* bh;
     uint8_t* bd;
-    size_t b_bytes;
+    size_t bh_bytes, bd_bytes; /* the two pinned / device staging slots, together */
     hipStream_t bstream[2];
     hipEvent_t ev[2][4];
     int have_ev;
@@ -573,6 +580,7 @@ typedef struct {
                             host shadow of it copied over in whole lines before the doorbell */
     size_t o_shards, o_parity;
     uint32_t seq, groups;
+    uint32_t last_ok; /* the seq of the last job answered through the service (its timing record is valid) */
     uint64_t idle_ticks, life_ticks;
     uint64_t jobs, launches, dev_jobs;
     double tick_us;                                  /* s_memrealtime period */
@@ -657,14 +665,29 @@ static void svc_pause(void)
 #endif
 }
 
-/* mutex held; leaves the workgroup off the device */
+/* mutex held; leaves the workgroup off the device.  The workgroup polls
+ * `stop` and leaves within microseconds (its lifetime is 4 ms anyway), so the
+ * wait is bounded: a launch still live after RFEC_SVC_STOP_US is wedged, and
+ * this reports it instead of blocking in hipStreamSynchronize for good (the
+ * service then stays unavailable). */
+#define RFEC_SVC_STOP_US 2e6
 static int svc_stop_locked(void)
 {
     if (g_svc.state != 1 && g_svc.state != -2)
         return RFEC_OK;
     __atomic_store_n(&g_svc.in->stop, 1u, __ATOMIC_RELEASE);
     svc_flush();
-    const hipError_t e = hipStreamSynchronize(g_svc.stream);
+    const double t0 = now_us();
+    hipError_t e;
+    while ((e = hipStreamQuery(g_svc.stream)) == hipErrorNotReady) {
+        if (now_us() - t0 > RFEC_SVC_STOP_US) {
+            g_svc.state = -1;
+            fprintf(stderr, "razor_fec: the resident FEC service did not leave within %.0f s of stop\n",
+                    RFEC_SVC_STOP_US / 1e6);
+            return set_err(RFEC_EDEVICE, "service stop: the resident workgroup did not leave", 0);
+        }
+        svc_pause();
+    }
     __atomic_store_n(&g_svc.in->stop, 0u, __ATOMIC_RELEASE);
     g_svc.in->quit = 0;
     svc_flush();
@@ -704,7 +727,16 @@ int rfec_service_get_info(rfec_service_info* info)
     return RFEC_OK;
 }
 
-static void svc_atexit(void) { (void)rfec_service_stop(); }
+/* at exit: a wedged workgroup would hold the process in the runtime's
+ * teardown; leave with a failure status instead */
+static void svc_atexit(void)
+{
+    if (rfec_service_stop() != RFEC_OK && g_svc.state == -1 && hipStreamQuery(g_svc.stream) == hipErrorNotReady) {
+        fflush(stdout);
+        fflush(stderr);
+        _exit(70);
+    }
+}
 
 static size_t svc_align(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -875,7 +907,12 @@ static int svc_run(uint32_t n_slots, uint32_t op, double t_begin)
     ++g_svc.jobs;
     g_svc.t_stage += t0 - t_begin;
     g_svc.t_wait += t1 - t0;
-    if (seq > 1) { /* the previous job's device timing: written after its `done`, landed before this one's */
+    /* the previous job's device timing: written after its `done`, landed
+     * before this one's -- when that job was answered here (a timed-out job
+     * leaves its slot holding seq - 3's record) */
+    const int prev_ok = seq > 1 && g_svc.last_ok == seq - 1;
+    g_svc.last_ok = seq;
+    if (prev_ok) {
         const uint64_t* t = q->out.t[(seq - 1) & 1u];
         if (t[0] && t[3] >= t[0]) {
             ++g_svc.dev_jobs;
@@ -1254,7 +1291,10 @@ static hb_layout hb_offsets(uint32_t G, uint32_t k, uint32_t n)
     return L;
 }
 
-static int hb_reserve(di_ctx* c, size_t slot_bytes)
+/* two staging slots: host_slot bytes of pinned memory and dev_slot bytes of
+ * device memory each (the recover path keeps device-only regions past the
+ * host-mirrored ones, so dev_slot >= host_slot there) */
+static int hb_reserve(di_ctx* c, size_t host_slot, size_t dev_slot)
 {
     hipError_t e;
     if (!c->have_ev) {
@@ -1267,20 +1307,24 @@ static int hb_reserve(di_ctx* c, size_t slot_bytes)
         }
         c->have_ev = 1;
     }
-    if (c->b_bytes >= 2 * slot_bytes)
-        return RFEC_OK;
-    if (c->bh)
-        (void)hipHostFree(c->bh);
-    if (c->bd)
-        (void)hipFree(c->bd);
-    c->bh = NULL;
-    c->bd = NULL;
-    c->b_bytes = 0;
-    if ((e = hipHostMalloc((void**)&c->bh, 2 * slot_bytes, hipHostMallocDefault)) != hipSuccess)
-        return set_err(RFEC_ENOMEM, "pinned staging", e);
-    if ((e = hipMalloc((void**)&c->bd, 2 * slot_bytes)) != hipSuccess)
-        return set_err(RFEC_ENOMEM, "device staging", e);
-    c->b_bytes = 2 * slot_bytes;
+    if (c->bh_bytes < 2 * host_slot) {
+        if (c->bh)
+            (void)hipHostFree(c->bh);
+        c->bh = NULL;
+        c->bh_bytes = 0;
+        if ((e = hipHostMalloc((void**)&c->bh, 2 * host_slot, hipHostMallocDefault)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "pinned staging", e);
+        c->bh_bytes = 2 * host_slot;
+    }
+    if (c->bd_bytes < 2 * dev_slot) {
+        if (c->bd)
+            (void)hipFree(c->bd);
+        c->bd = NULL;
+        c->bd_bytes = 0;
+        if ((e = hipMalloc((void**)&c->bd, 2 * dev_slot)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "device staging", e);
+        c->bd_bytes = 2 * dev_slot;
+    }
     return RFEC_OK;
 }
 
@@ -1420,7 +1464,7 @@ int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
     chunk = chunk > groups ? groups : chunk;
     const uint32_t nch = (groups + chunk - 1) / chunk;
     const hb_layout L = hb_offsets(chunk, k, n);
-    if ((rc = hb_reserve(c, L.total)))
+    if ((rc = hb_reserve(c, L.total, L.total)))
         return rc;
     const int threads = host_threads();
     double gather_us = 0, scatter_us = 0, h2d_us = 0, kernel_us = 0, d2h_us = 0;
@@ -1506,13 +1550,17 @@ int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
  * used slot; lost segments and parities are not shipped).  On the device two
  * row gathers expand them into the dense slot arrays the recover kernels read
  * (`shards`, `parity`, device-only; a lost slot zero), then the recover
- * kernel, then the recovered rows back. */
+ * kernel, then the recovered rows back.  The pinned slot mirrors the regions
+ * that cross PCIe only ([0, host_total)); the device-only regions follow them
+ * in the device slot. */
 typedef struct {
     size_t hdr, present, meta, fsize, ppm, smap, pmap, packed; /* host -> device: [0, packed + used slots) */
-    size_t shards, parity;                                       /* device only: the dense slots */
     size_t out_shards, out_hdr, out_index, recovered, out_bytes; /* device -> host */
-    size_t ws, total;                                            /* device workspace */
+    size_t host_total;                                           /* the pinned slot */
+    size_t shards, parity, ws, total;                            /* device only: dense slots, workspace */
 } hr_layout;
+
+#define RFEC_HR_SLOT_BYTES ((size_t)640 << 20)
 
 static hr_layout hr_offsets(const rfec_plan* plan, uint32_t G, uint32_t E)
 {
@@ -1532,13 +1580,14 @@ static hr_layout hr_offsets(const rfec_plan* plan, uint32_t G, uint32_t E)
     HR_TAKE(smap, (size_t)G * k * sizeof(int32_t));
     HR_TAKE(pmap, (size_t)G * n * sizeof(int32_t));
     HR_TAKE(packed, (size_t)G * (k + n) * DI_STRIDE);
-    HR_TAKE(shards, (size_t)G * k * DI_STRIDE);
-    HR_TAKE(parity, (size_t)G * n * DI_STRIDE);
     HR_TAKE(out_shards, (size_t)G * E * DI_STRIDE);
     HR_TAKE(out_hdr, (size_t)G * E * sizeof(rfec_hdr));
     HR_TAKE(out_index, (size_t)G * E);
     HR_TAKE(recovered, (size_t)G * 16);
     L.out_bytes = o - L.out_shards;
+    L.host_total = o;
+    HR_TAKE(shards, (size_t)G * k * DI_STRIDE);
+    HR_TAKE(parity, (size_t)G * n * DI_STRIDE);
     HR_TAKE(ws, rfec_recover_workspace_size(plan, G));
 #undef HR_TAKE
     L.total = o;
@@ -1688,12 +1737,18 @@ int rfec_host_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
     if (!c)
         return RFEC_EDEVICE;
     const uint32_t k = plan->k, E = per_group;
-    uint32_t chunk = (groups + 7) / 8; /* 2,048-16,384 groups a step: ~1 GiB of pinned staging at most */
+    /* 2,048-16,384 groups a step, and at most RFEC_HR_SLOT_BYTES of device
+     * staging per slot (its pinned mirror is smaller): at k = 10 / 3 lines a
+     * 16,384-group slot takes ~570 MB, at k = 128 / 64 lines ~470 KB a group */
+    const size_t group_bytes = hr_offsets(plan, 1024, E).total / 1024 + 1;
+    const size_t by_bytes = RFEC_HR_SLOT_BYTES / group_bytes;
+    uint32_t chunk = (groups + 7) / 8;
     chunk = chunk < 2048 ? 2048 : chunk > 16384 ? 16384 : chunk;
+    chunk = (size_t)chunk > by_bytes ? (uint32_t)(by_bytes ? by_bytes : 1) : chunk;
     chunk = chunk > groups ? groups : chunk;
     const uint32_t nch = (groups + chunk - 1) / chunk;
     const hr_layout L = hr_offsets(plan, chunk, E);
-    if ((rc = hb_reserve(c, L.total)))
+    if ((rc = hb_reserve(c, L.host_total, L.total)))
         return rc;
     rfec_kmask M;
     make_masks(plan, &M);
@@ -1736,7 +1791,7 @@ int rfec_host_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
             h->out = out + (size_t)g0 * E;
             h->out_index = out_index ? out_index + (size_t)g0 * E : NULL;
             h->recovered = recovered ? recovered + (size_t)g0 * 2 : NULL;
-            h->slot = c->bh + (size_t)s * L.total;
+            h->slot = c->bh + (size_t)s * L.host_total;
             h->base = base + (size_t)s * chunk;
             h->L = L;
             h->E = E;
@@ -3052,7 +3107,8 @@ static void rx_run(rx_sim* X, uint32_t a0, uint32_t n)
     }
 }
 
-/* A group above RFEC_MAX_K segments (a foreign peer's flex): the canonical
+/* A group recovered by line jobs (rx_line_jobs: above RFEC_MAX_K segments or a
+ * huge shape -- a foreign peer's flex): the canonical
  * peel (lines in plan order -- rows, then columns -- to a fixpoint, with
  * flex_fec_recover's header checks, flex_fec_xor.c:60-99) from its arrived
  * members and registered parities, over headers on the host; each firing
@@ -3161,6 +3217,13 @@ static int rx_big_peel(rx_sim* X, uint32_t gi, int32_t* job_of)
 
 #define RX_MAX_LEVEL 256u
 
+/* A group whose device recovery runs as the host peel's line jobs: above
+ * RFEC_MAX_K segments (the batched peel's masks hold 128 members), or a huge
+ * shape of any count (no device plan: more than RFEC_MAX_LINES lines, e.g. a
+ * peer's 128-segment flex of 64 rows x 2 columns, or one rx_extend took past
+ * 64 lines; its parity rows sit at a 256-line stride). */
+static int rx_line_jobs(const rx_shape* sh) { return sh->count > RFEC_MAX_K || sh->huge; }
+
 /* The device side of one call: the groups that delivered something in this
  * call, rebuilt from their arrived members and registered parities (rows of
  * `rows`, DEVICE, indexed by record), peeled by rfec_recover_batch, and the
@@ -3208,7 +3271,7 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
         sh->row0 = nrows;
         sh->prow0 = prows;
         sh->group0 = ngs;
-        if (sh->count > RFEC_MAX_K) /* line jobs instead (below) */
+        if (rx_line_jobs(sh)) /* line jobs instead (below) */
             continue;
         nrows += sh->n_groups * sh->count;
         prows += sh->n_groups * sh->n_lines;
@@ -3219,7 +3282,7 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
     X->njobs = X->njmem = 0;
     uint32_t nbig = 0, maxlvl = 0;
     for (uint32_t d = 0; d < X->ndl; ++d)
-        if (X->S[X->G[X->dl[d]].shape].count > RFEC_MAX_K)
+        if (rx_line_jobs(&X->S[X->G[X->dl[d]].shape]))
             nbig += X->G[X->dl[d]].count;
     int32_t* job_of = nbig ? (int32_t*)malloc((size_t)nbig * sizeof(int32_t)) : NULL;
     uint32_t* jperm = NULL;
@@ -3227,7 +3290,7 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
         return set_err(RFEC_ENOMEM, "rx: large groups", 0);
     for (uint32_t d = 0, off = 0; d < X->ndl; ++d) {
         rx_inst* g = &X->G[X->dl[d]];
-        if (X->S[g->shape].count <= RFEC_MAX_K)
+        if (!rx_line_jobs(&X->S[g->shape]))
             continue;
         g->gslot = off; /* (a large group's slot: its job_of range) */
         if (rx_big_peel(X, X->dl[d], job_of + off))
@@ -3285,7 +3348,8 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
     const size_t o_rec = o_in_end, host_bytes = RX_ALIGN(o_rec + (size_t)ngs * 16);
     size_t ws_bytes = 0;
     for (uint32_t s = 0; s < X->ns; ++s)
-        ws_bytes += RX_ALIGN(rfec_recover_workspace_size(&X->S[s].plan, X->S[s].n_groups));
+        if (!rx_line_jobs(&X->S[s]))
+            ws_bytes += RX_ALIGN(rfec_recover_workspace_size(&X->S[s].plan, X->S[s].n_groups));
     const size_t d_shards = o_in_end, d_par = RX_ALIGN(d_shards + ((size_t)nrows + X->njobs) * stride);
     const size_t d_ws = RX_ALIGN(d_par + (size_t)prows * stride), d_rec = RX_ALIGN(d_ws + ws_bytes);
     const size_t d_out = RX_ALIGN(d_rec + (size_t)ngs * 16), dev_bytes = RX_ALIGN(d_out + (size_t)X->nout * stride);
@@ -3314,7 +3378,7 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
     for (uint32_t d = 0; d < X->ndl; ++d) {
         const rx_inst* g = &X->G[X->dl[d]];
         const rx_shape* sh = &X->S[g->shape];
-        if (sh->count > RFEC_MAX_K)
+        if (rx_line_jobs(sh))
             continue;
         const uint32_t gg = sh->group0 + g->gslot, r0 = sh->row0 + g->gslot * sh->count;
         const uint32_t p0 = sh->prow0 + g->gslot * sh->n_lines;
@@ -3343,7 +3407,7 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
         const rx_inst* g = &X->G[ev->inst];
         const rx_shape* sh = &X->S[g->shape];
         const uint32_t t = ev->hdr.seq - g->base;
-        if (sh->count > RFEC_MAX_K) /* the job that recovers t */
+        if (rx_line_jobs(sh)) /* the job that recovers t */
             omap[q] = t < g->count && job_of[g->gslot + t] >= 0 ? (int32_t)(nrows + (uint32_t)job_of[g->gslot + t]) : -1;
         else
             omap[q] = t < g->count ? (int32_t)(sh->row0 + g->gslot * sh->count + t) : -1;
@@ -3368,7 +3432,7 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
     size_t wso = 0;
     for (uint32_t s = 0; s < X->ns && !ke; ++s) {
         const rx_shape* sh = &X->S[s];
-        if (!sh->n_groups || sh->count > RFEC_MAX_K)
+        if (!sh->n_groups || rx_line_jobs(sh))
             continue;
         rfec_kmask M;
         make_masks(&sh->plan, &M);
@@ -3397,7 +3461,7 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
         const rx_event* ev = &X->out[q];
         const rx_inst* g = &X->G[ev->inst];
         const uint32_t t = ev->hdr.seq - g->base, gg = X->S[g->shape].group0 + g->gslot;
-        const int big = X->S[g->shape].count > RFEC_MAX_K;
+        const int big = rx_line_jobs(&X->S[g->shape]);
         if (big ? omap[q] < 0 : t >= g->count || !((rec[2 * gg + (t >> 6)] >> (t & 63)) & 1ull)) {
             X->unmodelled++;
             omap[q] = -1;

@@ -19,6 +19,7 @@ typedef struct {
 
 /* kernel flags == the RFEC_TUNE_* bits of razor_fec.h */
 #define RFEC_KFLAG_GENERIC RFEC_TUNE_GENERIC
+#define RFEC_KFLAG_MATRIX_GENERIC RFEC_TUNE_PLAN_CASCADE
 
 int rfec_launch_encode(const rfec_kplan* P, uint32_t groups, uint32_t stride, uint32_t capacity,
                        const uint8_t* shards, const rfec_hdr* hdr, uint8_t* parity, rfec_hdr* meta,

@@ -902,16 +902,26 @@ __device__ CSched cascade_check(const CascArgs& A, const rfec_kmask& M, uint32_t
 // own slot in place -- which this lane writes first (the slot's owner lane
 // writes the same bytes; a lane's later load of an address it stored is
 // ordered behind the store).
+// Line records and masks for the replay: staged in LDS (any plan), or
+// arithmetic in the line index (the sender's matrix shapes, MatLines below).
+struct LdsLines {
+    const uint32_t* lplan;
+    const uint64_t* lmask;
+    __device__ uint32_t rec(uint32_t l) const { return lplan[l]; }
+    __device__ uint64_t mask(uint32_t l) const { return lmask[l]; }
+};
+
+template <class Lines>
 __device__ __forceinline__ v4u cascade_replay(const CSched& S, uint32_t need, uint32_t ss, uint64_t erased,
                                               const v4u* grp, const v4u* par, v4u* slot0, uint32_t E, uint32_t C,
-                                              const uint32_t* lplan)
+                                              const Lines& LL)
 {
     v4u res = {0, 0, 0, 0};
 #pragma unroll 1
     for (uint32_t s = 0; s < 8; ++s) {
         if (!((need >> s) & 1u))
             continue;
-        const uint32_t l = cs_line(S, s), t = cs_tg(S, s), ln = lplan[l];
+        const uint32_t l = cs_line(S, s), t = cs_tg(S, s), ln = LL.rec(l);
         const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
         v4u acc = ld16(par + (size_t)l * C);
         v4u mv[4];
@@ -1167,7 +1177,36 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             if ((dm >> cs_tg(S, s2)) & 1ull)
                 need |= 1u << s2;
     }
-    st16(dst, cascade_replay(S, need, ss, erased, grp, par, slot0, A.E, C, lplan));
+    st16(dst, cascade_replay(S, need, ss, erased, grp, par, slot0, A.E, C, LdsLines{lplan, lmask}));
+}
+
+// A dense payload lane whose target no line recovers at once (a cascade):
+// the group's mask schedule (cascade_schedule without the header checks),
+// the steps the target's step reads, transitively, replayed in registers.
+template <typename MT, class Lines>
+__device__ __forceinline__ void cascade_dense_tail(const CascArgs& A, const rfec_kmask& M, uint32_t NL, uint64_t have,
+                                                   uint64_t erased, uint64_t ppm, uint32_t tgt, const v4u* grp,
+                                                   const v4u* par, v4u* slot0, v4u* dst, const Lines& LL)
+{
+    const CSched S = cascade_schedule<MT>(M, NL, (MT)have, ppm, 0u, (MT)erased, A.E);
+    uint32_t ss = 8;
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+        if ((uint32_t)s < S.n && cs_tg(S, s) == tgt)
+            ss = s;
+    if (ss == 8)
+        return; // not recoverable
+    uint32_t need = 1u << ss;
+#pragma unroll 1
+    for (int s = (int)ss; s >= 0; --s) {
+        if (!((need >> s) & 1u))
+            continue;
+        const uint64_t dm = LL.mask(cs_line(S, s)) & erased & ~(1ull << cs_tg(S, s));
+        for (int s2 = 0; s2 < s; ++s2)
+            if ((dm >> cs_tg(S, s2)) & 1ull)
+                need |= 1u << s2;
+    }
+    st16(dst, cascade_replay(S, need, ss, erased, grp, par, slot0, A.E, A.C, LL));
 }
 
 // Dense output, one launch: rounds of 8 checker blocks spread over the grid
@@ -1267,25 +1306,113 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         st16(dst, acc);
         return;
     }
-    const CSched S = cascade_schedule<MT>(M, NL, (MT)have, ppm, 0u, (MT)erased, A.E);
-    uint32_t ss = 8;
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-        if ((uint32_t)s < S.n && cs_tg(S, s) == tgt)
-            ss = s;
-    if (ss == 8)
-        return; // not recoverable
-    uint32_t need = 1u << ss;
-#pragma unroll 1
-    for (int s = (int)ss; s >= 0; --s) {
-        if (!((need >> s) & 1u))
-            continue;
-        const uint64_t dm = lmask[cs_line(S, s)] & erased & ~(1ull << cs_tg(S, s));
-        for (int s2 = 0; s2 < s; ++s2)
-            if ((dm >> cs_tg(S, s2)) & 1ull)
-                need |= 1u << s2;
+    cascade_dense_tail<MT>(A, M, NL, have, erased, ppm, tgt, grp, par, slot0, dst, LdsLines{lplan, lmask});
+}
+
+// The sender's full matrix plans (rows of COL consecutive segments, then the
+// columns, flex_fec_sender.c:166-233), K = 6..16 as
+// flex_fec_sender_num_packets picks them (COL 3 for K <= 9, else 4): the dense
+// cascade decode with the plan folded into the code.  A payload lane's target
+// lies in exactly one row and one column, so the first line that fires at
+// once for it (plan order: rows first) is its row, else its column -- two
+// mask tests on masks that are shifts of constants, instead of the generic
+// kernel's search over eight kernel-argument masks and line records; the
+// q-th erased segment is found by clearing q low bits without a run-time
+// loop for q < 4.  Cascades (no line fires at once) replay the mask schedule
+// as the generic kernel does, with the line records computed from the index.
+template <int K, int COL>
+struct MatLines {
+    using Sh = MatrixShape<K, COL>;
+    static constexpr int NR = Sh::n_rows();
+    static constexpr uint32_t KM = (1u << K) - 1u, ROW = (1u << COL) - 1u;
+    static constexpr uint32_t col0()
+    {
+        uint32_t m = 0;
+        for (int r = 0; r < Sh::R; ++r)
+            m |= 1u << (r * COL);
+        return m;
     }
-    st16(dst, cascade_replay(S, need, ss, erased, grp, par, slot0, A.E, C, lplan));
+    static constexpr uint32_t COL0 = col0();
+    // line l: first | stride << 8 | count << 16 (rows l < NR, then column l - NR)
+    __device__ uint32_t rec(uint32_t l) const
+    {
+        const bool row = l < (uint32_t)NR;
+        const uint32_t c = l - NR;
+        const uint32_t first = row ? l * COL : c, stride = row ? 1u : (uint32_t)COL;
+        const uint32_t count = row ? min((uint32_t)COL, K - l * COL) : (K - c + COL - 1) / COL;
+        return first | stride << 8 | count << 16;
+    }
+    __device__ uint64_t mask(uint32_t l) const
+    {
+        return l < (uint32_t)NR ? (ROW << (l * COL)) & KM : (COL0 << (l - NR)) & KM;
+    }
+};
+
+template <int K, int COL>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_decode_matrix_dense(
+    CascArgs A, rfec_kmask M, uint32_t n_hr, uint32_t every, uint32_t npay8)
+{
+    using LL = MatLines<K, COL>;
+    constexpr int NR = LL::NR, NL = NR + COL, R = MatrixShape<K, COL>::R, MX = COL > R ? COL : R;
+    static_assert(K >= 2 * COL && K <= 16 && NL <= 8 && MX <= 4, "the cascade kernels' shapes");
+    uint32_t hb = 0, pb = 0;
+    if (header_block_xcd(n_hr, every, npay8, &hb, &pb)) { // the checker blocks, as the generic kernel's
+        const uint32_t gt = hb * kBlock + threadIdx.x;
+        const uint32_t g = gt / kCheckLanes, s = gt % kCheckLanes;
+        const bool live = g < A.groups;
+        cascade_check_lanes<uint32_t, kCheckLanes, false>(A, M, live ? g : 0u, live, s,
+                                                          (threadIdx.x & (kWave - 1)) & ~(uint32_t)(kCheckLanes - 1));
+        return;
+    }
+    const uint32_t t = pb * kBlock + threadIdx.x; // (XCD-swizzled: a group's lanes share one L2)
+    if (t >= A.total)
+        return;
+    const uint32_t g = fdiv(t, A.divQC);
+    const uint32_t rem = t - g * A.divQC.d;
+    const uint32_t q = fdiv(rem, A.divC);
+    const uint32_t j = rem - q * A.divC.d;
+    const uint32_t C = A.C;
+    const uint32_t hv = (uint32_t)A.present[2 * g] & LL::KM, er = ~hv & LL::KM;
+    const uint32_t pp = (uint32_t)A.parity_present[g];
+    uint32_t e = er; // slot q: the q-th erased segment
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        e = (uint32_t)i < q ? e & (e - 1u) : e;
+    for (uint32_t i = 3; i < q; ++i)
+        e &= e - 1u;
+    if (!e)
+        return;
+    const uint32_t tgt = (uint32_t)__ffs((int)e) - 1, tb = 1u << tgt;
+    const uint32_t r = tgt / COL, c = tgt - r * COL;
+    const uint32_t rm = (LL::ROW << (r * COL)) & LL::KM, cm = (LL::COL0 << c) & LL::KM;
+    const bool row_fires = r < (uint32_t)NR && ((pp >> r) & 1u) && (rm & er) == tb && (rm & hv);
+    const bool col_fires = ((pp >> (NR + c)) & 1u) && (cm & er) == tb && (cm & hv);
+    const v4u* grp = A.shards + (size_t)g * K * C + j;
+    const v4u* par = A.parity + (size_t)g * NL * C + j;
+    v4u* slot0 = A.out_sh + (size_t)g * A.E * C + j;
+    v4u* dst = slot0 + (size_t)q * C;
+    if (row_fires || col_fires) { // single level
+        const uint32_t l = row_fires ? r : NR + c;
+        const uint32_t first = row_fires ? r * COL : c, stride = row_fires ? 1u : (uint32_t)COL;
+        const uint32_t count = row_fires ? min((uint32_t)COL, K - r * COL) : (K - c + COL - 1) / COL;
+        v4u acc = ld16(par + (size_t)l * C);
+        // members through a descriptor over the first active lane's group (see k_decode_cascade_dense)
+        const uint32_t gb = (uint32_t)__builtin_amdgcn_readfirstlane((int)g); // lanes' groups ascend
+        const __amdgpu_buffer_rsrc_t rs = wave_rsrc(A.shards + (size_t)gb * K * C);
+        const uint32_t grp0 = ((g - gb) * K * C + j) * 16u;
+        v4u mv[MX];
+#pragma unroll
+        for (int u = 0; u < MX; ++u) {
+            const uint32_t i = first + u * stride;
+            mv[u] = bld16(rs, (uint32_t)u < count && i != tgt ? grp0 + i * C * 16u : kNoLoad);
+        }
+#pragma unroll
+        for (int u = 0; u < MX; ++u)
+            acc ^= mv[u];
+        st16(dst, acc);
+        return;
+    }
+    cascade_dense_tail<uint32_t>(A, M, NL, hv, er, pp, tgt, grp, par, slot0, dst, LL{});
 }
 
 // ---------------------------------------------------------------------------
@@ -1951,8 +2078,10 @@ inline uint32_t hdr_every(const FusedArgs& F, uint32_t npay) { return F.n_hdr ? 
 
 // cascade decode, dense: one launch (k_decode_cascade_dense); in place: the checker (schedule records and
 // task words into the workspace), then the payload lanes, Q slots per group (one per possible step)
+bool is_full_matrix(const rfec_kplan* P, uint32_t col);
+
 void launch_cascade(CascArgs A, const rfec_kmask& M, uint32_t groups, uint32_t cd, void* ws, uint32_t ws_stride,
-                    hipStream_t st)
+                    hipStream_t st, bool generic)
 {
     A.Q = A.E ? A.E : (M.plan.n_lines < M.plan.k ? M.plan.n_lines : M.plan.k);
     A.groups = groups;
@@ -1966,6 +2095,19 @@ void launch_cascade(CascArgs A, const rfec_kmask& M, uint32_t groups, uint32_t c
         const uint32_t npay8 = (blocks_for(A.total) + 7u) & ~7u;
         const uint32_t every = n_hr ? (npay8 >> 3) / n_hr : 0u;
         const dim3 grid(8u * n_hr + npay8);
+        const uint32_t k = M.plan.k;
+        if (!generic && k >= 6 && k <= 16 && is_full_matrix(&M.plan, k <= 9 ? 3 : 4)) {
+#define RFEC_MD(KK, CC)                                                                                           \
+    case KK:                                                                                                      \
+        RFEC_LAUNCH((k_decode_matrix_dense<KK, CC>), grid, dim3(kBlock), 0, st, A, M, n_hr, every, npay8);        \
+        return;
+            switch (k) {
+                RFEC_MD(6, 3) RFEC_MD(7, 3) RFEC_MD(8, 3) RFEC_MD(9, 3) RFEC_MD(10, 4) RFEC_MD(11, 4) RFEC_MD(12, 4)
+                RFEC_MD(13, 4) RFEC_MD(14, 4) RFEC_MD(15, 4) RFEC_MD(16, 4)
+            default: break;
+            }
+#undef RFEC_MD
+        }
         if (M.plan.k <= 32)
             RFEC_LAUNCH(k_decode_cascade_dense<uint32_t>, grid, dim3(kBlock), 0, st, A, M, n_hr, every, npay8);
         else
@@ -2186,7 +2328,7 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
         A.E = DO.E;
         A.C = C;
         A.capacity = capacity;
-        launch_cascade(A, *M, groups, cd, ws, B.rec_bytes, st);
+        launch_cascade(A, *M, groups, cd, ws, B.rec_bytes, st, (flags & RFEC_KFLAG_MATRIX_GENERIC) != 0);
         return (int)hipGetLastError();
     }
     RFEC_LAUNCH(k_peel_lds, dim3(n_hdr), dim3(kBlock), 0, st, B, *M);

@@ -118,13 +118,44 @@ def peer_stream(oracle, rng, n_groups=90, video_size=1000):
     return np.array(recs, po.WIRE_REC), np.array(pays, np.uint8)
 
 
-def single_group_stream(oracle, k, pf, erase, tamper=None, seed=0, video_size=1000):
+def matrix_parities(seg, pay, fec_id, base_id, k, row, col):
+    """A foreign peer's flex of `row` rows x `col` columns (not razor's
+    planner): one parity per row over [r col, min(k, (r + 1) col)), index r,
+    and one per column over r col + c < k, index 0x80 | c
+    (flex_fec_sender.c:157-233 with the peer's row / col), each one
+    flex_fec_generate (flex_fec_xor.c:13-50): payloads XORed zero-padded to
+    L = max data_size, meta = XOR of the 20-byte headers."""
+    hdr32 = seg["hdr"][:k].copy().view(np.uint32).reshape(k, 5)
+    sizes = seg["data_size"][:k].astype(np.int64)
+    lines = [(list(range(r * col, min(k, (r + 1) * col))), r) for r in range(row)]
+    lines += [([r * col + c for r in range(row) if r * col + c < k], 0x80 | c) for c in range(col)]
+    out = []
+    for mem, index in lines:
+        if len(mem) < 2:
+            continue
+        L = int(sizes[mem].max())
+        pp = np.bitwise_xor.reduce(pay[mem], axis=0)
+        pp[L:] = 0
+        r = np.zeros((), po.WIRE_REC)
+        r["mid"], r["ver"] = 0x1C, 1
+        r["fec_id"], r["base_id"], r["count"] = fec_id, base_id, k
+        r["row"], r["col"], r["index"] = row, col, index
+        r["send_ts"] = int(seg["hdr"]["ts"][k - 1])
+        r["hdr"] = np.bitwise_xor.reduce(hdr32[mem], axis=0).view(r["hdr"].dtype)[0]
+        r["data_size"] = L
+        out.append((r, pp))
+    return out
+
+
+def single_group_stream(oracle, k, pf, erase, tamper=None, seed=0, video_size=1000, shape=None):
     """One flex of k segments (packet ids 1..k, ragged sizes) and every parity
     the reference sender emits for it (k <= 255: the oracle's plan + encode;
     above: pyoracle's restatement of flex_fec_sender_update), arriving after
     the segments not in `erase`.  tamper = (parity index, data_size): that
     parity's fec_data_size is cut below a member's size, so flex_fec_recover
-    rejects its line (flex_fec_xor.c:88-89).  Returns (recs, pay)."""
+    rejects its line (flex_fec_xor.c:88-89).  shape = (row, col): a peer's
+    matrix flex of that shape instead of the sender's plan for pf.  Returns
+    (recs, pay)."""
     rng = np.random.default_rng(seed)
     stride = (video_size + 15) // 16 * 16
     sizes = rng.integers(video_size // 2, video_size + 1, k)
@@ -144,7 +175,9 @@ def single_group_stream(oracle, k, pf, erase, tamper=None, seed=0, video_size=10
     seg["fec_id"] = 7
     g = np.zeros((), po.GROUP_PLAN)
     g["first_seg"], g["count"], g["fec_id"], g["base_id"], g["protect_fraction"] = 0, k, 7, 1, pf
-    if k > 255:
+    if shape is not None:
+        pars = matrix_parities(seg, pay, 7, 1, k, *shape)
+    elif k > 255:
         pars = po._big_group_parities(oracle, seg, pay, g, k, pf)
     else:
         plan = oracle.plan_from_fraction(k, pf, 3)

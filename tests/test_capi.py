@@ -72,6 +72,10 @@ def test_argument_validation(product):
         product.plan_from_fraction(256, 80)  # above RFEC_MAX_K_ENCODE
     with pytest.raises(RfecError):
         product.plan_matrix(10, 2, 4)  # 2x4 does not cover 10
+    for row, col in ((64, 2), (2, 64)):  # 66 lines: above RFEC_MAX_LINES (the plan holds 64)
+        with pytest.raises(RfecError):
+            product.plan_matrix(128, row, col)
+    assert product.plan_matrix(124, 62, 2).n_lines == 64
     bad = product.plan_from_fraction(10, 80, 1)
     bad.line[0].count = 20  # member beyond k
     with pytest.raises(RfecError):

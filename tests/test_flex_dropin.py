@@ -104,8 +104,39 @@ def flex(product, request):
     assert L.rfec_service_stop() == 0
     if request.param == "service":
         assert jobs > 0, "no drop-in call reached the resident service"
+        # the module's sender and (ragged) receiver fixtures ran through the
+        # request side in device memory wherever the host maps it
+        assert request_in_device(L) == int(bar_host_mapped())
     else:
         assert jobs == 0, "a drop-in call reached the service under RFEC_TUNE_NO_SERVICE"
+
+
+def bar_host_mapped() -> bool:
+    """Independent of the library: is fine-grained device memory mapped
+    read-write into this process at its device address (/proc/self/maps)?
+    That is the condition under which the service puts its request side
+    (doorbell, job, staged segments) in device memory (svc_map_request_side)."""
+    hip = C.CDLL("libamdhip64.so")
+    p = C.c_void_p()
+    n = 1 << 20
+    if hip.hipExtMallocWithFlags(C.byref(p), C.c_size_t(n), C.c_uint(1)) != 0 or not p.value:  # Finegrained
+        return False
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                lo, hi = (int(x, 16) for x in line.split()[0].split("-"))
+                if lo <= p.value and p.value + n <= hi:
+                    return line.split()[1].startswith("rw")
+        return False
+    finally:
+        hip.hipFree(p)
+
+
+def request_in_device(L) -> int:
+    from razor_amd.fec import rfec_service_info
+    i = rfec_service_info()
+    assert L.rfec_service_get_info(C.byref(i)) == 0
+    return int(i.request_in_device)
 
 
 def _svc_stats(L):

@@ -342,21 +342,24 @@ def test_host_encode_groups(product1200, oracle1200):
         assert np.array_equal(fecs["fec_data"][j, :L], ref["fec_data"][j, :L])
 
 
-@pytest.mark.parametrize("layers,G", [(1, 301), (3, 301), (3, 4500)])
-def test_host_recover_groups(product1200, oracle1200, layers, G):
+@pytest.mark.parametrize("k,layers,G", [(10, 1, 301), (10, 3, 301), (10, 3, 4500), (128, 1, 3000)])
+def test_host_recover_groups(product1200, oracle1200, k, layers, G):
     """rfec_host_recover_groups (host AoS in, flex_fec_recover-style out_seg
     out): groups encoded by rfec_host_encode_groups (checked above), 1-3
     segments and 0-2 parities of each lost; out_index / recovered masks equal
     the oracle's rfec_recover_batch_out restatement, every recovered out_seg
     equals the lost segment (header fields, data_size, data, zero past it)
     and carries the group's fec_id.  4,500 groups: three double-buffered
-    chunks of packed received rows (2,048, 2,048, 404)."""
+    chunks of packed received rows (2,048, 2,048, 404).  k = 128 with a
+    64-line plan (64 rows of 2): chunks sized by bytes (~1,400 groups of
+    ~470 KB device staging each), not by the group count alone."""
     from razor_amd.fec import fec_dtype, seg_dtype
 
     lib, o = product1200, oracle1200
-    k, S, E = 10, 1200, 3
+    S, E = 1200, 3
     shards, hdr = o.fill_groups(203, G, k, S, ragged=True)
-    plan = o.plan_from_fraction(k, 80, layers)
+    plan = o.plan_from_fraction(k, 80, layers) if k <= 10 else o.plan_matrix(k, 64, 2, layers)
+    assert plan.n_lines == ({1: 3, 3: 7}[layers] if k == 10 else 64)
     n = plan.n_lines
     segs = np.zeros(G * k, seg_dtype(1200))
     h = hdr.reshape(-1)
@@ -375,7 +378,8 @@ def test_host_recover_groups(product1200, oracle1200, layers, G):
     for g in range(G):
         lost = rng.choice(k, int(rng.integers(1, 4)), replace=False)
         sp_rx[g * k + lost] = 0
-        present[g, 0] = sum(1 << i for i in range(k) if i not in lost)
+        pm = sum(1 << i for i in range(k) if i not in lost)
+        present[g, 0], present[g, 1] = pm & (2**64 - 1), pm >> 64
         plost = rng.choice(n, int(rng.integers(0, 3)), replace=False)
         fp_rx[g * n + plost] = 0
         ppm[g] = sum(1 << l for l in range(n) if l not in plost)
@@ -388,7 +392,7 @@ def test_host_recover_groups(product1200, oracle1200, layers, G):
     rx_h = hdr.copy()
     for g in range(G):
         for i in range(k):
-            if not (int(present[g, 0]) >> i) & 1:
+            if not (int(present[g, i >> 6]) >> (i & 63)) & 1:
                 rx_sh[g, i] = 0
                 rx_h[g, i] = 0
     par = fecs["fec_data"].reshape(G, n, S)
@@ -757,16 +761,23 @@ def _check_dense(got, exp, G, E, where):
     return n
 
 
-@pytest.mark.parametrize("k", [6, 9, 10, 12, 16])
-@pytest.mark.parametrize("tuning", list(TUNINGS))
+# the dense cascade decode of the sender's matrix plans: the kernel compiled for the shape (default), the
+# plan-driven cascade kernel (RFEC_TUNE_PLAN_CASCADE) and the LDS peel + replay (RFEC_TUNE_GENERIC)
+CASC_TUNINGS = {"default": 0, "plan_cascade": 1 << 2, "generic": 1}
+
+
+@pytest.mark.parametrize("k", list(range(6, 17)))
+@pytest.mark.parametrize("tuning", list(CASC_TUNINGS))
 def test_dense_output_cascade_gpu(gpu, oracle1000, k, tuning):
     """rfec_recover_batch_out over the sender's full plans (rows + columns,
     recoveries cascade): 1-6 erasures per group, lost parities and header
     rejections, E = 1..4 output slots and E = k; out slots, headers, indices and
     recovered masks equal the oracle's dense restatement (only erased segments
     of rank < E recoverable; E >= the erasure count gives the in-place peel).
-    Default: the one-launch register-schedule cascade decode; generic: the
-    LDS peel + replay into the dense output."""
+    Default: the one-launch cascade decode compiled for the plan's shape
+    (k_decode_matrix_dense<k, col>, k = 6..16); plan_cascade: the plan-driven
+    one-launch cascade decode; generic: the LDS peel + replay into the dense
+    output."""
     o = oracle1000
     plan = o.plan_from_fraction(k, 80, 3)
     G, S = 500, 1000 if k <= 10 else 256
@@ -776,7 +787,7 @@ def test_dense_output_cascade_gpu(gpu, oracle1000, k, tuning):
     e_s, e_h, e_rec = o.recover_batch(plan, rx, rh, present, parity, meta, fs, pp, cap)
     for E in (1, 2, 3, 4, k):
         exp = o.recover_batch_out(plan, rx, rh, present, parity, meta, fs, pp, cap, E)
-        got = gpu(tuning=TUNINGS[tuning]).recover_out(plan, rx, rh, present, parity, meta, fs, pp, cap, E)
+        got = gpu(tuning=CASC_TUNINGS[tuning]).recover_out(plan, rx, rh, present, parity, meta, fs, pp, cap, E)
         n = _check_dense(got, exp, G, E, f"k={k} E={E}")
         assert n > G // 3, (E, n)
         if E == k:  # every erased segment has a slot: the in-place peel's result

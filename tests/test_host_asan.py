@@ -130,6 +130,16 @@ for seed in range(3):
 assert npeer > 300, npeer
 print("peer geometry ok", npeer)
 
+# 2c. a peer's flex of <= 128 segments with more than 64 lines (a huge shape:
+#     line jobs, not the batched peel), and the same counts with a device plan
+nhuge = 0
+for k, row, col in [(128, 64, 2), (128, 2, 64), (100, 50, 2)]:
+    recs, pay = rc0.single_group_stream(o, k, 80, {{0, 1, 3, 2 * col + 1, 7 * col, k - 2}}, seed=k + row,
+                                        shape=(row, col))
+    nhuge += check(recs, pay)
+assert nhuge >= 12, nhuge
+print("huge small-count ok", nhuge)
+
 # 3. across calls: max_ts carries in, old parities are dropped
 recs, pay = stream(9, 200, (10,), (80,), 0.1, 10, 0.0, 0.0)
 _, _, m1, _ = rx(recs, pay)

@@ -140,16 +140,57 @@ def _check_c4_strong(c4, n):
     assert all(t > 0 for t in c4["encode_us_per_rank"] + c4["decode_us_per_rank"])
 
 
+def _check_subs(d, n):
+    """The default line carries BASELINE configs[4] (c5) and the sender's full
+    3 x 4 plan (c3full) too: driver-timed, each rank on its own 65,536 groups,
+    rank 0's outputs equal to the reference's full-size digest."""
+    for name, enc, lines in (("c5", "k_encode_out<32,4>", [4] * 8),
+                             ("c3full", "k_encode_matrix_out<10,4>", [4, 4, 2, 3, 3, 2, 2])):
+        c = d[name]
+        assert c["workload"].startswith(f"{name}: ") and c["scaling"] == "weak"
+        assert c["plan_lines"] == lines and c["encode"]["kernel"] == enc
+        assert c["verified"] is True and c["verified_vs_reference_digest"] is True
+        assert c["value"] > 0 and len(c["encode_us_per_rank"]) == n
+        assert all(t > 0 for t in c["encode_us_per_rank"] + c["decode_us_per_rank"])
+        assert 0 < c["encode"]["frac"] < 1 and 0 < c["decode"]["frac"] < 1
+        assert c["encode"]["mix_ceiling"]["kernel_vs_ceiling"] > 0
+    assert d["c3full"]["decode"]["kernels"].startswith("k_decode_matrix_dense<10,4>")
+    assert d["c5"]["encode"]["mix_ceiling"]["probe"].startswith("rfec_probe_mix 4 reads : 1 writes")
+    assert d["c3full"]["encode"]["mix_ceiling"]["probe"].startswith("rfec_probe_mix 10 reads : 7 writes")
+
+
 @pytest.mark.timeout(600)
 def test_bench_one_gpu_c4_strong():
     """The default N = 1 line: weak c3 as `value`, plus the c4_strong object
     over all 1,048,576 groups on the one GPU (the N = 1 point of the strong
-    curve), bit-exact against the reference's c4 digest."""
-    d = _bench("--gpus", "1", "--steps", "3", "--warmup", "1", "--no-cpu", "--c4-steps", "2")
+    curve), bit-exact against the reference's c4 digest, and the c5 / c3full
+    objects."""
+    d = _bench("--gpus", "1", "--steps", "3", "--warmup", "1", "--no-cpu", "--c4-steps", "2", "--sub-steps", "3")
     assert d["n_gpus"] == 1 and d["scaling"] == "weak" and d["config"]["config"] == "c3"
     assert d["verified_vs_reference_digest"] is True
     _check_c4_strong(d["c4_strong"], 1)
+    _check_subs(d, 1)
     assert d["roofline"]["mix_ceiling"]["probe"].startswith("rfec_probe_mix 10 reads : 3 writes")
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("n", [4, 8])
+def test_bench_n_ranks_one_gpu(n):
+    """The driver's N = 4 / N = 8 launch path before an 8-GPU node runs it:
+    bench.py --gpus n starts n ranks under torchrun on the one leased GPU
+    (LOCAL_RANK % device_count), one JSON line; every rank's weak c3 chunk
+    equals the reference digest of exactly its 65,536 groups (full_hashes.json
+    c3_weak chunks[0..n)), c4_strong's slices equal the reference's n-way
+    slice digests, groups_per_rank = 1,048,576 / n each.  Groups are
+    independent (sim_fec.c:152-166): no data-path collective."""
+    d = _bench("--gpus", str(n), "--steps", "2", "--warmup", "1", "--no-cpu", "--c4-steps", "2", "--sub-steps", "2",
+               timeout=840)
+    assert d["n_gpus"] == n and d["scaling"] == "weak"
+    assert d["config"]["total_groups"] == n * 65536
+    assert d["config"]["workload"].startswith(f"c3: k10_r3_S1200_G65536 per GPU x {n}")
+    assert d["verified"] is True and d["verified_vs_reference_digest"] is True
+    _check_c4_strong(d["c4_strong"], n)
+    _check_subs(d, n)
 
 
 @pytest.mark.timeout(900)

@@ -451,6 +451,24 @@ def test_rx_peer_geometry(lib, oracle1000, seed):
     assert _sorted(rows) == _sorted(rc.got_rows(eo, ep))
 
 
+@pytest.mark.parametrize("k,row,col", [(128, 64, 2), (128, 2, 64), (100, 50, 2), (96, 3, 32)])
+def test_rx_huge_shape_small_count(lib, oracle1000, k, row, col):
+    """A peer's flex of at most RFEC_MAX_K segments with more than 64 lines
+    (128 = 64 x 2 or 2 x 64: 66 lines) is a huge shape: its recovery runs as
+    line jobs, not through the batched peel (whose plans hold 64 lines).
+    50 x 2 and 3 x 32 (52 / 35 lines) keep a device plan.  Losses: row 0
+    whole, member 3 (its row), member 1 two levels deep where the shape
+    allows, scattered singles.  Delivered rows equal the event-by-event
+    oracle's, nothing unmodelled."""
+    erase = {0, 1, 3, 2 * col + 1, 7 * col, k - 2}
+    recs, pay = rc.single_group_stream(oracle1000, k, 80, erase, seed=k + row, shape=(row, col))
+    out, outp, _, rep = _rx(lib, recs, pay)
+    o_out, o_pay, _, _ = oracle1000.rx_recover(recs, pay, 1000)
+    assert rep.n_unmodelled == 0
+    assert len(o_out) >= 4
+    assert _sorted(rc.got_rows(out, outp)) == _sorted(rc.got_rows(o_out, o_pay))
+
+
 @pytest.mark.parametrize("k,pf", [(200, 80), (600, 80), (1000, 80)])
 def test_rx_large_group_cascades_and_rejection(lib, oracle1000, k, pf):
     """Flexes above RFEC_MAX_K (line jobs; above 255 segments and 64 lines:

@@ -10,7 +10,7 @@ import pytest
 import torch
 
 import pyoracle as po
-from test_flex_dropin import CASES, _svc_stats, bind_flex, make_segments, sender_group
+from test_flex_dropin import CASES, _svc_stats, bar_host_mapped, bind_flex, make_segments, sender_group
 
 pytestmark = pytest.mark.gpu
 
@@ -146,5 +146,7 @@ def test_group_dropin_request_side(stage):
     assert svc["jobs"] >= 300
     if stage == "host":
         assert svc["request_in_device"] == 0
+    elif not bar_host_mapped():
+        pytest.skip("device memory is not host-mapped here (small BAR): the request side stays in pinned memory")
     else:
-        assert svc["request_in_device"] in (0, 1)
+        assert svc["request_in_device"] == 1

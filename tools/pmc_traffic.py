@@ -25,7 +25,8 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 
-KERNELS = {"encode": ("k_encode",), "decode": ("k_decode_rows", "k_decode_out", "k_decode_disjoint", "k_decode_cascade"),
+KERNELS = {"encode": ("k_encode",), "decode": ("k_decode_rows", "k_decode_out", "k_decode_disjoint", "k_decode_cascade",
+                                              "k_decode_matrix"),
            "check": ("k_cascade_check",), "peel": ("k_peel",), "recover": ("k_recover",)}
 
 
