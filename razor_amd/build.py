@@ -28,9 +28,14 @@ ARCH = os.environ.get("RFEC_OFFLOAD_ARCH", "gfx950")
 
 HIP_SRC = [CSRC / "rfec_kernels.hip", CSRC / "rfec_probe.hip", CSRC / "rfec_wire.hip", CSRC / "rfec_fill.hip",
            CSRC / "rfec_service.hip"]
-C_SRC = [CSRC / "rfec_host.c", CSRC / "rfec_flex.c"]  # built once per SIM_VIDEO_SIZE
+# built once per SIM_VIDEO_SIZE: the C host layer, by concern (rfec_host.c: errors, planner, batched device
+# and wire API; rfec_dropin.c: drop-in symbols + resident service; rfec_hostmem.c: host-memory batches;
+# rfec_sender.c: sender staging; rfec_rx.c: receiver ingestion and sessions), and the flex drop-in
+HOST_SRC = ["rfec_host.c", "rfec_dropin.c", "rfec_hostmem.c", "rfec_sender.c", "rfec_rx.c"]
+C_SRC = [CSRC / f for f in HOST_SRC] + [CSRC / "rfec_flex.c"]
 NET_SRC = CSRC / "rfec_net.c"  # host-only (sockets), independent of SIM_VIDEO_SIZE
-HEADERS = [INCLUDE / "razor_fec.h", INCLUDE / "razor_flex.h", CSRC / "rfec_internal.h", CSRC / "rfec_launch.h"]
+HEADERS = [INCLUDE / "razor_fec.h", INCLUDE / "razor_flex.h", CSRC / "rfec_internal.h", CSRC / "rfec_launch.h",
+           CSRC / "rfec_host_internal.h"]
 
 VARIANTS = {"librazor_fec.so": 1000, "librazor_fec_v1200.so": 1200}
 

@@ -1,0 +1,572 @@
+/*
+ * rfec_hostmem.c -- the host-memory batch paths: rfec_host_encode_groups
+ * (sim_segment_t in, sim_fec_t out) and rfec_host_recover_groups (received
+ * sim_segment_t / sim_fec_t in, recovered segments out), chunked and
+ * double-buffered over two streams (gather -> H2D -> kernels -> D2H -> scatter).
+ */
+#define _POSIX_C_SOURCE 200809L
+#ifndef __HIP_PLATFORM_AMD__
+#define __HIP_PLATFORM_AMD__ 1
+#endif
+#include <hip/hip_runtime_api.h>
+
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "razor_fec.h"
+#include "rfec_internal.h"
+#include "rfec_host_internal.h"
+
+/* ------------------------------------------------------------------------ */
+/* 4. host-resident batch (gather -> H2D -> encode -> D2H -> scatter)        */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    size_t shards, hdr, parity, meta, fsize, status, in_bytes, total;
+} hb_layout;
+
+static hb_layout hb_offsets(uint32_t G, uint32_t k, uint32_t n)
+{
+    hb_layout L;
+    size_t o = 0;
+#define HB_TAKE(field, bytes)                       \
+    do {                                             \
+        L.field = o;                                 \
+        o = (o + (size_t)(bytes) + 255) & ~(size_t)255; \
+    } while (0)
+    HB_TAKE(shards, (size_t)G * k * DI_STRIDE);
+    HB_TAKE(hdr, (size_t)G * k * sizeof(rfec_hdr));
+    L.in_bytes = o; /* [shards, hdr] go host -> device in one copy */
+    HB_TAKE(parity, (size_t)G * n * DI_STRIDE);
+    HB_TAKE(meta, (size_t)G * n * sizeof(rfec_hdr));
+    HB_TAKE(fsize, (size_t)G * n * sizeof(uint16_t));
+    HB_TAKE(status, (size_t)G * n);
+#undef HB_TAKE
+    L.total = o;
+    return L;
+}
+
+/* two staging slots: host_slot bytes of pinned memory and dev_slot bytes of
+ * device memory each (the recover path keeps device-only regions past the
+ * host-mirrored ones, so dev_slot >= host_slot there) */
+static int hb_reserve(di_ctx* c, size_t host_slot, size_t dev_slot)
+{
+    hipError_t e;
+    if (!c->have_ev) {
+        for (int s = 0; s < 2; ++s) {
+            if ((e = hipStreamCreateWithFlags(&c->bstream[s], hipStreamNonBlocking)) != hipSuccess)
+                return set_err(RFEC_EDEVICE, "stream create", e);
+            for (int i = 0; i < 4; ++i)
+                if ((e = hipEventCreate(&c->ev[s][i])) != hipSuccess)
+                    return set_err(RFEC_EDEVICE, "event create", e);
+        }
+        c->have_ev = 1;
+    }
+    if (c->bh_bytes < 2 * host_slot) {
+        if (c->bh)
+            (void)hipHostFree(c->bh);
+        c->bh = NULL;
+        c->bh_bytes = 0;
+        if ((e = hipHostMalloc((void**)&c->bh, 2 * host_slot, hipHostMallocDefault)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "pinned staging", e);
+        c->bh_bytes = 2 * host_slot;
+    }
+    if (c->bd_bytes < 2 * dev_slot) {
+        if (c->bd)
+            (void)hipFree(c->bd);
+        c->bd = NULL;
+        c->bd_bytes = 0;
+        if ((e = hipMalloc((void**)&c->bd, 2 * dev_slot)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "device staging", e);
+        c->bd_bytes = 2 * dev_slot;
+    }
+    return RFEC_OK;
+}
+
+/* the sender's fec_id sequence: +1 per group, 0 skipped (flex_fec_sender.c:241-243) */
+static uint16_t fec_id_at(uint16_t id0, uint32_t g)
+{
+    const uint32_t base = id0 ? (uint32_t)id0 - 1u : 0u;
+    return (uint16_t)((base + g) % 65535u + 1u);
+}
+
+typedef struct {
+    const rfec_plan* plan;
+    sim_segment_t* const* segs; /* first segment of the chunk */
+    sim_fec_t* const* fecs;     /* first parity of the chunk */
+    uint8_t* slot;              /* host staging slot */
+    hb_layout L;
+    uint32_t g0;                /* global index of the chunk's first group */
+    uint16_t fec_id0;
+} hb_chunk;
+
+/* gather: AoS segments (payload at offset 34, not 16-B aligned) -> SoA slots */
+static void hb_gather(void* arg, size_t lo, size_t hi)
+{
+    const hb_chunk* h = (const hb_chunk*)arg;
+    rfec_hdr* hh = (rfec_hdr*)(h->slot + h->L.hdr);
+    for (size_t s = lo; s < hi; ++s) {
+        const sim_segment_t* seg = h->segs[s];
+        stage_payload(h->slot + h->L.shards + s * DI_STRIDE, seg->data, seg->data_size);
+        seg_to_hdr(seg, &hh[s]);
+    }
+}
+
+/* scatter into the caller's sim_fec_t, stamped as flex_fec_sender_update does */
+static void hb_scatter(void* arg, size_t lo, size_t hi)
+{
+    const hb_chunk* h = (const hb_chunk*)arg;
+    const rfec_plan* plan = h->plan;
+    const uint32_t k = plan->k, n = plan->n_lines;
+    const rfec_hdr* hh = (const rfec_hdr*)(h->slot + h->L.hdr);
+    const rfec_hdr* mh = (const rfec_hdr*)(h->slot + h->L.meta);
+    const uint16_t* fs = (const uint16_t*)(h->slot + h->L.fsize);
+    const int8_t* st = (const int8_t*)(h->slot + h->L.status);
+    for (size_t g = lo; g < hi; ++g) {
+        uint32_t base = hh[g * k].seq;
+        for (uint32_t i = 1; i < k; ++i)
+            base = hh[g * k + i].seq < base ? hh[g * k + i].seq : base;
+        for (uint32_t l = 0; l < n; ++l) {
+            const size_t o = g * n + l;
+            sim_fec_t* f = h->fecs[o];
+            f->fec_id = fec_id_at(h->fec_id0, h->g0 + (uint32_t)g);
+            f->base_id = base;
+            f->row = plan->row;
+            f->col = plan->col;
+            f->index = plan->line[l].index;
+            f->count = plan->k;
+            if (st[o] != 0) {
+                f->fec_data_size = 0xFFFF;
+                continue;
+            }
+            memcpy(&f->fec_meta, &mh[o], sizeof(rfec_hdr));
+            f->fec_data_size = fs[o];
+            memcpy(f->fec_data, h->slot + h->L.parity + o * DI_STRIDE, fs[o]);
+        }
+    }
+}
+
+/*
+ * Chunked and double-buffered: while the GPU copies / encodes / copies back
+ * chunk c on slot c%2's stream, the CPU threads scatter chunk c-1's parities
+ * and gather chunk c+1 into the other slot, so the wall time approaches the
+ * slowest stage (the PCIe copies) instead of the sum of all five.
+ */
+int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,
+                            sim_fec_t* const* fecs, uint16_t fec_id0, rfec_host_timing* timing)
+{
+    int rc = check_plan(plan, RFEC_MAX_K_ENCODE);
+    if (rc)
+        return rc;
+    if (groups == 0 || plan->n_lines == 0)
+        return RFEC_OK;
+    if (!segs || !fecs)
+        return set_err(RFEC_EINVAL, "NULL segs / fecs", 0);
+    if ((rc = check_geometry(groups, DI_STRIDE, SIM_VIDEO_SIZE, plan->k)))
+        return rc;
+    di_ctx* c = di_get();
+    if (!c)
+        return RFEC_EDEVICE;
+    const uint32_t k = plan->k, n = plan->n_lines;
+    uint32_t chunk = (groups + 7) / 8;
+    chunk = chunk < 2048 ? 2048 : chunk;
+    chunk = chunk > groups ? groups : chunk;
+    const uint32_t nch = (groups + chunk - 1) / chunk;
+    const hb_layout L = hb_offsets(chunk, k, n);
+    if ((rc = hb_reserve(c, L.total, L.total)))
+        return rc;
+    const int threads = host_threads();
+    double gather_us = 0, scatter_us = 0, h2d_us = 0, kernel_us = 0, d2h_us = 0;
+    hb_chunk job[2];
+    const double t0 = now_us();
+    for (uint32_t it = 0; it < nch + 2; ++it) {
+        if (it >= 2) { /* retire chunk it-2 */
+            const uint32_t s = (it - 2) & 1;
+            hipError_t e = hipEventSynchronize(c->ev[s][3]);
+            if (e != hipSuccess)
+                return set_err(RFEC_EDEVICE, "D2H wait", e);
+            float a = 0, b = 0, d = 0;
+            (void)hipEventElapsedTime(&a, c->ev[s][0], c->ev[s][1]);
+            (void)hipEventElapsedTime(&b, c->ev[s][1], c->ev[s][2]);
+            (void)hipEventElapsedTime(&d, c->ev[s][2], c->ev[s][3]);
+            h2d_us += a * 1e3;
+            kernel_us += b * 1e3;
+            d2h_us += d * 1e3;
+            const double ts = now_us();
+            const uint32_t ng = (it - 2 == nch - 1) ? groups - (it - 2) * chunk : chunk;
+            parallel_for(ng, threads, hb_scatter, &job[s]);
+            scatter_us += now_us() - ts;
+        }
+        if (it < nch) { /* stage chunk it */
+            const uint32_t s = it & 1;
+            const uint32_t g0 = it * chunk;
+            const uint32_t ng = (it == nch - 1) ? groups - g0 : chunk;
+            hb_chunk* h = &job[s];
+            h->plan = plan;
+            h->segs = segs + (size_t)g0 * k;
+            h->fecs = fecs + (size_t)g0 * n;
+            h->slot = c->bh + (size_t)s * L.total;
+            h->L = L;
+            h->g0 = g0;
+            h->fec_id0 = fec_id0;
+            const double tg = now_us();
+            parallel_for((size_t)ng * k, threads, hb_gather, h);
+            gather_us += now_us() - tg;
+            uint8_t* dv = c->bd + (size_t)s * L.total;
+            hipStream_t st = c->bstream[s];
+            hipError_t e;
+            /* the slot holds `chunk` groups; a short last chunk copies its own extent */
+            const hb_layout Ln = hb_offsets(ng, k, n);
+            if ((e = hipEventRecord(c->ev[s][0], st)) != hipSuccess ||
+                (e = hipMemcpyAsync(dv + L.shards, h->slot + L.shards, Ln.hdr, hipMemcpyHostToDevice, st)) !=
+                    hipSuccess ||
+                (e = hipMemcpyAsync(dv + L.hdr, h->slot + L.hdr, (size_t)ng * k * sizeof(rfec_hdr),
+                                    hipMemcpyHostToDevice, st)) != hipSuccess ||
+                (e = hipEventRecord(c->ev[s][1], st)) != hipSuccess)
+                return set_err(RFEC_EDEVICE, "H2D", e);
+            const int ke = rfec_launch_encode(plan, ng, DI_STRIDE, SIM_VIDEO_SIZE, dv + L.shards,
+                                              (const rfec_hdr*)(dv + L.hdr), dv + L.parity, (rfec_hdr*)(dv + L.meta),
+                                              (uint16_t*)(dv + L.fsize), (int8_t*)(dv + L.status), st, g_tuning);
+            if (ke)
+                return set_err(RFEC_EDEVICE, "encode launch", ke);
+            if ((e = hipEventRecord(c->ev[s][2], st)) != hipSuccess ||
+                (e = hipMemcpyAsync(h->slot + L.parity, dv + L.parity, (size_t)ng * n * DI_STRIDE,
+                                    hipMemcpyDeviceToHost, st)) != hipSuccess ||
+                (e = hipMemcpyAsync(h->slot + L.meta, dv + L.meta, (size_t)ng * n * sizeof(rfec_hdr),
+                                    hipMemcpyDeviceToHost, st)) != hipSuccess ||
+                (e = hipMemcpyAsync(h->slot + L.fsize, dv + L.fsize, (size_t)ng * n * sizeof(uint16_t),
+                                    hipMemcpyDeviceToHost, st)) != hipSuccess ||
+                (e = hipMemcpyAsync(h->slot + L.status, dv + L.status, (size_t)ng * n, hipMemcpyDeviceToHost,
+                                    st)) != hipSuccess ||
+                (e = hipEventRecord(c->ev[s][3], st)) != hipSuccess)
+                return set_err(RFEC_EDEVICE, "D2H", e);
+        }
+    }
+    if (timing) {
+        timing->gather_us = gather_us;
+        timing->h2d_us = h2d_us;
+        timing->kernel_us = kernel_us;
+        timing->d2h_us = d2h_us;
+        timing->scatter_us = scatter_us;
+        timing->total_us = now_us() - t0;
+    }
+    return RFEC_OK;
+}
+
+/* ---- the receive direction: rfec_host_recover_groups --------------------- */
+/* Host -> device in one copy: the headers, masks and maps, then only the
+ * RECEIVED payloads, packed (`packed`, last, so the copy ends at the last
+ * used slot; lost segments and parities are not shipped).  On the device two
+ * row gathers expand them into the dense slot arrays the recover kernels read
+ * (`shards`, `parity`, device-only; a lost slot zero), then the recover
+ * kernel, then the recovered rows back.  The pinned slot mirrors the regions
+ * that cross PCIe only ([0, host_total)); the device-only regions follow them
+ * in the device slot. */
+typedef struct {
+    size_t hdr, present, meta, fsize, ppm, smap, pmap, packed; /* host -> device: [0, packed + used slots) */
+    size_t out_shards, out_hdr, out_index, recovered, out_bytes; /* device -> host */
+    size_t host_total;                                           /* the pinned slot */
+    size_t shards, parity, ws, total;                            /* device only: dense slots, workspace */
+} hr_layout;
+
+#define RFEC_HR_SLOT_BYTES ((size_t)640 << 20)
+
+static hr_layout hr_offsets(const rfec_plan* plan, uint32_t G, uint32_t E)
+{
+    const uint32_t k = plan->k, n = plan->n_lines;
+    hr_layout L;
+    size_t o = 0;
+#define HR_TAKE(field, bytes)                           \
+    do {                                                \
+        L.field = o;                                    \
+        o = (o + (size_t)(bytes) + 255) & ~(size_t)255; \
+    } while (0)
+    HR_TAKE(hdr, (size_t)G * k * sizeof(rfec_hdr));
+    HR_TAKE(present, (size_t)G * 16);
+    HR_TAKE(meta, (size_t)G * n * sizeof(rfec_hdr));
+    HR_TAKE(fsize, (size_t)G * n * sizeof(uint16_t));
+    HR_TAKE(ppm, (size_t)G * 8);
+    HR_TAKE(smap, (size_t)G * k * sizeof(int32_t));
+    HR_TAKE(pmap, (size_t)G * n * sizeof(int32_t));
+    HR_TAKE(packed, (size_t)G * (k + n) * DI_STRIDE);
+    HR_TAKE(out_shards, (size_t)G * E * DI_STRIDE);
+    HR_TAKE(out_hdr, (size_t)G * E * sizeof(rfec_hdr));
+    HR_TAKE(out_index, (size_t)G * E);
+    HR_TAKE(recovered, (size_t)G * 16);
+    L.out_bytes = o - L.out_shards;
+    L.host_total = o;
+    HR_TAKE(shards, (size_t)G * k * DI_STRIDE);
+    HR_TAKE(parity, (size_t)G * n * DI_STRIDE);
+    HR_TAKE(ws, rfec_recover_workspace_size(plan, G));
+#undef HR_TAKE
+    L.total = o;
+    return L;
+}
+
+typedef struct {
+    const rfec_plan* plan;
+    sim_segment_t* const* segs; /* the chunk's first group */
+    sim_fec_t* const* fecs;
+    sim_segment_t* const* out;
+    uint8_t* out_index;
+    uint64_t* recovered;
+    uint8_t* slot;
+    uint32_t* base; /* group g's first packed slot (prefix sums of the received counts) */
+    hr_layout L;
+    uint32_t E;
+} hr_chunk;
+
+/* received segments + parities of each group (the first pass: packed offsets) */
+static void hr_count(void* arg, size_t lo, size_t hi)
+{
+    const hr_chunk* h = (const hr_chunk*)arg;
+    const uint32_t k = h->plan->k, n = h->plan->n_lines;
+    for (size_t g = lo; g < hi; ++g) {
+        uint32_t c = 0;
+        for (uint32_t i = 0; i < k; ++i)
+            c += h->segs[g * k + i] != NULL;
+        for (uint32_t l = 0; l < n; ++l)
+            c += h->fecs[g * n + l] != NULL;
+        h->base[g] = c;
+    }
+}
+
+/* gather one group per index: received payloads into the packed slots from
+ * base[g] on (members, then parities) with their rows in the maps (-1: lost,
+ * a zero row on the device), headers (a lost member's zero), masks */
+static void hr_gather(void* arg, size_t lo, size_t hi)
+{
+    const hr_chunk* h = (const hr_chunk*)arg;
+    const uint32_t k = h->plan->k, n = h->plan->n_lines;
+    rfec_hdr* hh = (rfec_hdr*)(h->slot + h->L.hdr);
+    uint64_t* pres = (uint64_t*)(h->slot + h->L.present);
+    rfec_hdr* mh = (rfec_hdr*)(h->slot + h->L.meta);
+    uint16_t* fs = (uint16_t*)(h->slot + h->L.fsize);
+    uint64_t* ppm = (uint64_t*)(h->slot + h->L.ppm);
+    int32_t* smap = (int32_t*)(h->slot + h->L.smap);
+    int32_t* pmap = (int32_t*)(h->slot + h->L.pmap);
+    uint8_t* packed = h->slot + h->L.packed;
+    for (size_t g = lo; g < hi; ++g) {
+        uint64_t m0 = 0, m1 = 0, pm = 0;
+        uint32_t r = h->base[g];
+        for (uint32_t i = 0; i < k; ++i) {
+            const size_t s = g * k + i;
+            const sim_segment_t* seg = h->segs[s];
+            if (!seg) {
+                smap[s] = -1;
+                memset(&hh[s], 0, sizeof(rfec_hdr));
+                continue;
+            }
+            smap[s] = (int32_t)r;
+            stage_payload(packed + (size_t)r++ * DI_STRIDE, seg->data, seg->data_size);
+            seg_to_hdr(seg, &hh[s]);
+            if (i < 64)
+                m0 |= 1ull << i;
+            else
+                m1 |= 1ull << (i - 64);
+        }
+        for (uint32_t l = 0; l < n; ++l) {
+            const size_t o = g * n + l;
+            const sim_fec_t* f = h->fecs[o];
+            if (!f) {
+                pmap[o] = -1;
+                fs[o] = 0;
+                continue;
+            }
+            pm |= 1ull << l;
+            memcpy(&mh[o], &f->fec_meta, sizeof(rfec_hdr));
+            fs[o] = f->fec_data_size;
+            pmap[o] = (int32_t)r;
+            stage_payload(packed + (size_t)r++ * DI_STRIDE, f->fec_data,
+                          f->fec_data_size < SIM_VIDEO_SIZE ? f->fec_data_size : SIM_VIDEO_SIZE);
+        }
+        pres[2 * g] = m0;
+        pres[2 * g + 1] = m1;
+        ppm[g] = pm;
+    }
+}
+
+/* the recovered segments into the callers' sim_segment_t (flex_fec_recover's out_seg) */
+static void hr_scatter(void* arg, size_t lo, size_t hi)
+{
+    const hr_chunk* h = (const hr_chunk*)arg;
+    const uint32_t n = h->plan->n_lines, E = h->E;
+    const rfec_hdr* oh = (const rfec_hdr*)(h->slot + h->L.out_hdr);
+    const uint8_t* oi = h->slot + h->L.out_index;
+    const uint64_t* rec = (const uint64_t*)(h->slot + h->L.recovered);
+    for (size_t g = lo; g < hi; ++g) {
+        uint16_t fec_id = 0;
+        for (uint32_t l = 0; l < n; ++l)
+            if (h->fecs[g * n + l]) {
+                fec_id = h->fecs[g * n + l]->fec_id;
+                break;
+            }
+        for (uint32_t e = 0; e < E; ++e) {
+            const size_t o = g * E + e;
+            if (h->out_index)
+                h->out_index[o] = oi[o];
+            if (oi[o] == 0xFF || !h->out[o])
+                continue;
+            sim_segment_t* s = h->out[o];
+            const rfec_hdr* r = &oh[o];
+            s->packet_id = r->seq;
+            s->fid = r->fid;
+            s->timestamp = r->ts;
+            s->index = r->index;
+            s->total = r->total;
+            s->ftype = r->ftype;
+            s->payload_type = r->payload_type;
+            s->data_size = r->size;
+            memcpy(s->data, h->slot + h->L.out_shards + o * DI_STRIDE, SIM_VIDEO_SIZE);
+            s->fec_id = fec_id;
+        }
+        if (h->recovered) {
+            h->recovered[2 * g] = rec[2 * g];
+            h->recovered[2 * g + 1] = rec[2 * g + 1];
+        }
+    }
+}
+
+int rfec_host_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,
+                             sim_fec_t* const* fecs, uint32_t per_group, sim_segment_t* const* out,
+                             uint8_t* out_index, uint64_t* recovered, rfec_host_timing* timing)
+{
+    int rc = check_plan(plan, RFEC_MAX_K);
+    if (rc)
+        return rc;
+    if (groups == 0 || plan->n_lines == 0 || per_group == 0)
+        return RFEC_OK;
+    if (!segs || !fecs || !out)
+        return set_err(RFEC_EINVAL, "NULL segs / fecs / out", 0);
+    if (per_group > plan->k)
+        return set_err(RFEC_EINVAL, "per_group above k", 0);
+    if ((rc = check_geometry(groups, DI_STRIDE, SIM_VIDEO_SIZE, plan->k)))
+        return rc;
+    di_ctx* c = di_get();
+    if (!c)
+        return RFEC_EDEVICE;
+    const uint32_t k = plan->k, E = per_group;
+    /* 2,048-16,384 groups a step, and at most RFEC_HR_SLOT_BYTES of device
+     * staging per slot (its pinned mirror is smaller): at k = 10 / 3 lines a
+     * 16,384-group slot takes ~570 MB, at k = 128 / 64 lines ~470 KB a group */
+    const size_t group_bytes = hr_offsets(plan, 1024, E).total / 1024 + 1;
+    const size_t by_bytes = RFEC_HR_SLOT_BYTES / group_bytes;
+    uint32_t chunk = (groups + 7) / 8;
+    chunk = chunk < 2048 ? 2048 : chunk > 16384 ? 16384 : chunk;
+    chunk = (size_t)chunk > by_bytes ? (uint32_t)(by_bytes ? by_bytes : 1) : chunk;
+    chunk = chunk > groups ? groups : chunk;
+    const uint32_t nch = (groups + chunk - 1) / chunk;
+    const hr_layout L = hr_offsets(plan, chunk, E);
+    if ((rc = hb_reserve(c, L.host_total, L.total)))
+        return rc;
+    rfec_kmask M;
+    make_masks(plan, &M);
+    const int threads = host_threads();
+    double gather_us = 0, scatter_us = 0, h2d_us = 0, kernel_us = 0, d2h_us = 0;
+    hr_chunk job[2];
+    uint32_t* base = (uint32_t*)malloc(2 * (size_t)chunk * sizeof(uint32_t));
+    if (!base)
+        return set_err(RFEC_ENOMEM, "recover offsets", 0);
+    rc = RFEC_OK;
+    const double t0 = now_us();
+    for (uint32_t it = 0; it < nch + 2; ++it) {
+        if (it >= 2) { /* retire chunk it-2 */
+            const uint32_t s = (it - 2) & 1;
+            hipError_t e = hipEventSynchronize(c->ev[s][3]);
+            if (e != hipSuccess) {
+                rc = set_err(RFEC_EDEVICE, "D2H wait", e);
+                break;
+            }
+            float a = 0, b = 0, d = 0;
+            (void)hipEventElapsedTime(&a, c->ev[s][0], c->ev[s][1]);
+            (void)hipEventElapsedTime(&b, c->ev[s][1], c->ev[s][2]);
+            (void)hipEventElapsedTime(&d, c->ev[s][2], c->ev[s][3]);
+            h2d_us += a * 1e3;
+            kernel_us += b * 1e3;
+            d2h_us += d * 1e3;
+            const double ts = now_us();
+            const uint32_t ng = (it - 2 == nch - 1) ? groups - (it - 2) * chunk : chunk;
+            parallel_for(ng, threads, hr_scatter, &job[s]);
+            scatter_us += now_us() - ts;
+        }
+        if (it < nch) { /* stage chunk it */
+            const uint32_t s = it & 1;
+            const uint32_t g0 = it * chunk;
+            const uint32_t ng = (it == nch - 1) ? groups - g0 : chunk;
+            hr_chunk* h = &job[s];
+            h->plan = plan;
+            h->segs = segs + (size_t)g0 * k;
+            h->fecs = fecs + (size_t)g0 * plan->n_lines;
+            h->out = out + (size_t)g0 * E;
+            h->out_index = out_index ? out_index + (size_t)g0 * E : NULL;
+            h->recovered = recovered ? recovered + (size_t)g0 * 2 : NULL;
+            h->slot = c->bh + (size_t)s * L.host_total;
+            h->base = base + (size_t)s * chunk;
+            h->L = L;
+            h->E = E;
+            const double tg = now_us();
+            parallel_for(ng, threads, hr_count, h);
+            uint32_t used = 0;
+            for (uint32_t g = 0; g < ng; ++g) { /* counts -> first packed slots */
+                const uint32_t cg = h->base[g];
+                h->base[g] = used;
+                used += cg;
+            }
+            parallel_for(ng, threads, hr_gather, h);
+            gather_us += now_us() - tg;
+            uint8_t* dv = c->bd + (size_t)s * L.total;
+            hipStream_t st = c->bstream[s];
+            hipError_t e;
+            if ((e = hipEventRecord(c->ev[s][0], st)) != hipSuccess ||
+                (e = hipMemcpyAsync(dv, h->slot, L.packed + (size_t)used * DI_STRIDE, hipMemcpyHostToDevice, st)) !=
+                    hipSuccess ||
+                (e = hipEventRecord(c->ev[s][1], st)) != hipSuccess) {
+                rc = set_err(RFEC_EDEVICE, "H2D", e);
+                break;
+            }
+            int ke = rfec_launch_gather_rows(dv + L.shards, dv + L.packed, (const int32_t*)(dv + L.smap), ng * k,
+                                             DI_STRIDE, st);
+            if (!ke)
+                ke = rfec_launch_gather_rows(dv + L.parity, dv + L.packed, (const int32_t*)(dv + L.pmap),
+                                             ng * plan->n_lines, DI_STRIDE, st);
+            const rfec_dense_out D = {dv + L.out_shards, (rfec_hdr*)(dv + L.out_hdr), dv + L.out_index, E};
+            if (!ke)
+                ke = rfec_launch_recover_out(
+                &M, ng, DI_STRIDE, SIM_VIDEO_SIZE, dv + L.shards, (const rfec_hdr*)(dv + L.hdr),
+                (const uint64_t*)(dv + L.present), dv + L.parity, (const rfec_hdr*)(dv + L.meta),
+                (const uint16_t*)(dv + L.fsize), (const uint64_t*)(dv + L.ppm), (uint64_t*)(dv + L.recovered),
+                dv + L.ws, st, g_tuning, &D);
+            if (ke) {
+                rc = set_err(RFEC_EDEVICE, "recover launch", ke);
+                break;
+            }
+            if ((e = hipEventRecord(c->ev[s][2], st)) != hipSuccess ||
+                (e = hipMemcpyAsync(h->slot + L.out_shards, dv + L.out_shards, L.out_bytes, hipMemcpyDeviceToHost,
+                                    st)) != hipSuccess ||
+                (e = hipEventRecord(c->ev[s][3], st)) != hipSuccess) {
+                rc = set_err(RFEC_EDEVICE, "D2H", e);
+                break;
+            }
+        }
+    }
+    free(base);
+    if (rc != RFEC_OK) {
+        /* a failed step: the other buffer's work drains before its staging is reused */
+        (void)hipStreamSynchronize(c->bstream[0]);
+        (void)hipStreamSynchronize(c->bstream[1]);
+        return rc;
+    }
+    if (timing) {
+        timing->gather_us = gather_us;
+        timing->h2d_us = h2d_us;
+        timing->kernel_us = kernel_us;
+        timing->d2h_us = d2h_us;
+        timing->scatter_us = scatter_us;
+        timing->total_us = now_us() - t0;
+    }
+    return RFEC_OK;
+}

@@ -1,0 +1,1839 @@
+/*
+ * rfec_rx.c -- receiver ingestion: rfec_rx_recover, the receiver sessions
+ * (rfec_rx_session_*) and rfec_host_recv_datagrams.  The arrival-order control
+ * plane of sim_fec.c:104-241 / flex_fec_receiver.c:69-280 runs on the host
+ * over headers; the bytes are peeled on the device.
+ */
+#define _POSIX_C_SOURCE 200809L
+#ifndef __HIP_PLATFORM_AMD__
+#define __HIP_PLATFORM_AMD__ 1
+#endif
+#include <hip/hip_runtime_api.h>
+
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "razor_fec.h"
+#include "rfec_internal.h"
+#include "rfec_host_internal.h"
+
+/* ------------------------------------------------------------------------ */
+/* 6. receiver ingestion (semantics: include/razor_fec.h, rfec_rx_recover)  */
+/*    The control plane runs in arrival order on the host over headers only: */
+/*    admission, flex lifetime, which line recovers which packet and when    */
+/*    (so max_ts and first-arrival dedupe come out as the reference's).  The */
+/*    bytes never leave the device: the groups are peeled there by           */
+/*    rfec_recover_batch from their arrived members and registered parities. */
+/* ------------------------------------------------------------------------ */
+typedef struct { /* open addressing u32 -> u32, value 0 = empty */
+    uint32_t* k;
+    uint32_t* v;
+    uint32_t mask, n;
+} hmap;
+
+static uint32_t hm_home(const hmap* m, uint32_t k) { return (k * 0x9E3779B1u) & m->mask; }
+
+static int hm_init(hmap* m, uint32_t n)
+{
+    uint32_t cap = 64;
+    while (cap < 2 * n + 64)
+        cap <<= 1;
+    m->k = (uint32_t*)malloc(cap * sizeof(uint32_t));
+    m->v = (uint32_t*)calloc(cap, sizeof(uint32_t));
+    m->mask = cap - 1;
+    m->n = 0;
+    return m->k && m->v ? 0 : -1;
+}
+static void hm_free(hmap* m)
+{
+    free(m->k);
+    free(m->v);
+    m->k = m->v = NULL;
+}
+static uint32_t hm_slot(const hmap* m, uint32_t k)
+{
+    uint32_t h = hm_home(m, k);
+    while (m->v[h] && m->k[h] != k)
+        h = (h + 1) & m->mask;
+    return h;
+}
+static uint32_t hm_get(const hmap* m, uint32_t k) { return m->v[hm_slot(m, k)]; }
+static int hm_put(hmap* m, uint32_t k, uint32_t v)
+{
+    if (2 * (m->n + 1) > m->mask + 1) {
+        hmap g;
+        if (hm_init(&g, 2 * (m->mask + 1)))
+            return -1;
+        for (uint32_t i = 0; i <= m->mask; ++i)
+            if (m->v[i]) {
+                const uint32_t s = hm_slot(&g, m->k[i]);
+                g.k[s] = m->k[i];
+                g.v[s] = m->v[i];
+                g.n++;
+            }
+        hm_free(m);
+        *m = g;
+    }
+    const uint32_t s = hm_slot(m, k);
+    m->n += m->v[s] == 0;
+    m->k[s] = k;
+    m->v[s] = v;
+    return 0;
+}
+static void hm_del(hmap* m, uint32_t k) /* backward-shift deletion */
+{
+    uint32_t h = hm_slot(m, k);
+    if (!m->v[h])
+        return;
+    m->v[h] = 0;
+    m->n--;
+    for (uint32_t j = (h + 1) & m->mask; m->v[j]; j = (j + 1) & m->mask)
+        if (((j - hm_home(m, m->k[j])) & m->mask) >= ((j - h) & m->mask)) {
+            m->k[h] = m->k[j];
+            m->v[h] = m->v[j];
+            m->v[j] = 0;
+            h = j;
+        }
+}
+
+typedef struct {
+    uint32_t count, row, col, n_groups, n_lines, row0, prow0, group0;
+    uint32_t huge;        /* count > RX_MAX_COUNT or more than RFEC_MAX_LINES lines: no plan; line l = FEC
+                             index l (members by rx_line_members), n_lines 256, peeled by the host into
+                             line jobs (rx_big_peel) */
+    uint64_t xcol[2];     /* columns c >= col a peer's parities named (bit c) */
+    int16_t line_of[256]; /* FEC index -> plan line, -1: none */
+    rfec_plan plan;
+} rx_shape;
+
+/* one flex receiver (flex_fec_receiver_t) from its creation to its removal */
+typedef struct {
+    uint32_t fec_id, base, count, row, col;
+    uint32_t shape;        /* UINT32_MAX: geometry the reference ignores (col < 2, row 0, count 0) */
+    uint32_t gslot, slot0, line0;
+    uint32_t nsegs;        /* flex->segs.n */
+    uint64_t have[4];      /* members in the flex (arrived or recovered); huge shapes: rx_has */
+    uint64_t arrived[4];   /* members that arrived: the device peel starts from these (huge: slot_src) */
+    uint64_t ppm;          /* registered parities, by plan line (huge: line_par >= 0) */
+    uint32_t fec_ts;       /* flex->fec_ts = send_ts of the parity that created it (sim_fec.c:157) */
+    int ref_ok;            /* col >= 2 && row >= 1 && count >= 1 (flex_fec_receiver.c:214, 250) */
+    uint32_t gstamp;       /* == rx_sim.epoch: gslot is this device call's group slot */
+} rx_inst;
+
+typedef struct {
+    rfec_hdr hdr;
+    uint32_t inst;
+} rx_event; /* a recovered segment: pending, then delivered */
+
+typedef struct {
+    const rfec_wire_rec* R;
+    uint32_t capacity, max_ts, dropped, unmodelled;
+    hmap seen, cache, flex_of, shape_of;
+    rx_inst* G;
+    uint32_t ng, gcap;
+    rx_shape* S;
+    uint32_t ns, scap;
+    int32_t* slot_src; /* record of an arrived member, -1 otherwise */
+    rfec_hdr* slot_hdr;
+    uint32_t nslot, slotcap, slothcap; /* one count, two capacities (each array grows on its own) */
+    int32_t* line_par; /* record of the registered parity, -1 otherwise */
+    uint32_t nline, linecap;
+    rx_event* pend;
+    uint32_t npend, pendcap;
+    rx_event* out;         /* delivered by this call */
+    uint32_t nout, outcap;
+    rfec_hdr* rh;          /* headers of delivered (recovered) segments the cache refers to */
+    uint32_t nrh, rhcap;
+    uint32_t* dl;          /* instances that deliver in this device call */
+    uint32_t ndl, dlcap;
+    rfec_line_job* jobs;   /* groups above RFEC_MAX_K: this call's line jobs (rx_big_peel) */
+    uint32_t njobs, jobcap;
+    uint16_t* jlevel;      /* a job's dependency level (1 = arrived members only) */
+    uint32_t jlevelcap;
+    int32_t* jmem;         /* member codes: record >= 0, job j as -1 - j */
+    uint32_t njmem, jmemcap;
+    uint32_t epoch;        /* device call counter (rx_inst.gstamp) */
+    int oom;
+} rx_sim;
+
+#define RX_GROW(ptr, n, cap, need, T)                                                   \
+    do {                                                                                \
+        if ((n) + (need) > (cap)) {                                                     \
+            uint32_t c_ = (cap) ? 2 * (cap) : 1024;                                     \
+            while (c_ < (n) + (need))                                                   \
+                c_ *= 2;                                                                \
+            T* p_ = (T*)realloc((ptr), (size_t)c_ * sizeof(T));                         \
+            if (!p_) {                                                                  \
+                X->oom = 1;                                                             \
+                break;                                                                  \
+            }                                                                           \
+            (ptr) = p_;                                                                 \
+            (cap) = c_;                                                                 \
+        }                                                                               \
+    } while (0)
+
+static rfec_hdr rec_hdr(const rfec_wire_rec* r)
+{
+    rfec_hdr h = r->hdr;
+    h.size = r->data_size; /* seg.data_size = the datagram's (sim_receiver.c) */
+    return h;
+}
+
+/* members of the reference's line `index` of a (count, row, col) flex:
+ * flex_recover_row walks i < col, flex_recover_col i < row, both stopping at
+ * the first position >= count (flex_fec_receiver.c:118-126, 175-183) */
+static uint32_t rx_line_members(uint32_t count, uint32_t row, uint32_t col, uint32_t index, uint32_t* first,
+                                uint32_t* stride)
+{
+    const uint32_t x = index & 0x7Fu;
+    uint32_t n = 0;
+    if (index & 0x80u) {
+        while (n < row && n * col + x < count)
+            ++n;
+        *first = x;
+        *stride = col;
+    } else {
+        while (n < col && x * col + n < count)
+            ++n;
+        *first = x * col;
+        *stride = 1;
+    }
+    return n;
+}
+
+/* line l of flex g: its members and whether its parity is registered */
+static uint32_t rx_line(const rx_sim* X, const rx_inst* g, uint32_t l, uint32_t* first, uint32_t* stride, int* reg)
+{
+    const rx_shape* sh = &X->S[g->shape];
+    if (sh->huge) {
+        *reg = X->line_par[g->line0 + l] >= 0;
+        return rx_line_members(g->count, g->row, g->col, l, first, stride);
+    }
+    const rfec_line* ln = &sh->plan.line[l];
+    *reg = (int)((g->ppm >> l) & 1ull);
+    *first = ln->first;
+    *stride = ln->stride;
+    return ln->count;
+}
+
+/* member t of flex g is in it (arrived or recovered); a huge flex's slot
+ * header holds the member's seq once it is in, ~(base + t) before */
+static int rx_has(const rx_sim* X, const rx_inst* g, uint32_t t)
+{
+    if (X->S[g->shape].huge)
+        return X->slot_hdr[g->slot0 + t].seq == g->base + t;
+    return (int)((g->have[t >> 6] >> (t & 63)) & 1ull);
+}
+
+static void rx_pend(rx_sim* X, const rfec_hdr* h, uint32_t inst) /* sim_fec_packet_add_recover (sim_fec.c:104-119) */
+{
+    for (uint32_t i = 0; i < X->npend; ++i)
+        if (X->pend[i].hdr.seq == h->seq)
+            return;
+    RX_GROW(X->pend, X->npend, X->pendcap, 1, rx_event);
+    if (X->oom)
+        return;
+    X->pend[X->npend].hdr = *h;
+    X->pend[X->npend++].inst = inst;
+}
+
+/* flex_recover_row / flex_recover_col (flex_fec_receiver.c:105-206) over headers */
+static void rx_check_line(rx_sim* X, uint32_t ii, int l)
+{
+    const rx_inst* g = &X->G[ii];
+    if (l < 0 || g->nsegs >= g->count)
+        return;
+    uint32_t first, stride;
+    int reg;
+    const uint32_t n = rx_line(X, g, (uint32_t)l, &first, &stride, &reg);
+    if (!reg)
+        return;
+    uint32_t loss = 0, cnt = 0;
+    for (uint32_t q = 0; q < n; ++q) {
+        if (rx_has(X, g, first + q * stride))
+            cnt++;
+        else
+            loss++;
+    }
+    if (loss != 1 || cnt == 0)
+        return;
+    const rfec_wire_rec* f = &X->R[X->line_par[g->line0 + l]];
+    const uint32_t L = f->data_size;
+    if (L > X->capacity)
+        return;
+    rfec_hdr h = f->hdr; /* flex_fec_xor.c:64-99 */
+    for (uint32_t q = 0; q < n; ++q) {
+        const uint32_t i = first + q * stride;
+        if (!rx_has(X, g, i))
+            continue;
+        const rfec_hdr* m = &X->slot_hdr[g->slot0 + i];
+        if (L < m->size)
+            return;
+        h.seq ^= m->seq;
+        h.fid ^= m->fid;
+        h.ts ^= m->ts;
+        h.index ^= m->index;
+        h.total ^= m->total;
+        h.ftype ^= m->ftype;
+        h.payload_type ^= m->payload_type;
+        h.size ^= m->size;
+    }
+    if (h.size > L)
+        return;
+    rx_pend(X, &h, ii);
+}
+
+/* flex_fec_receiver_on_segment (flex_fec_receiver.c:243-280); src = record or -1 */
+static void rx_on_segment(rx_sim* X, uint32_t ii, const rfec_hdr* h, int32_t src, int check)
+{
+    rx_inst* g = &X->G[ii];
+    if (!g->ref_ok || h->seq < g->base)
+        return;
+    if (g->shape == UINT32_MAX) {
+        X->unmodelled++;
+        return;
+    }
+    const uint32_t t = h->seq - g->base;
+    if (t < g->count) {
+        if (rx_has(X, g, t))
+            return;
+        if (!X->S[g->shape].huge)
+            g->have[t >> 6] |= 1ull << (t & 63);
+        X->slot_hdr[g->slot0 + t] = *h;
+        if (src >= 0) {
+            if (!X->S[g->shape].huge)
+                g->arrived[t >> 6] |= 1ull << (t & 63);
+            X->slot_src[g->slot0 + t] = src;
+        }
+    } else if (src < 0) {
+        X->unmodelled++; /* a recovered header outside its group: inconsistent parities */
+    }
+    g->nsegs++;
+    if (check) {
+        const rx_shape* sh = &X->S[g->shape];
+        const uint32_t r = t / g->col, c = t % g->col;
+        rx_check_line(X, ii, r < 128 ? sh->line_of[r] : -1);
+        rx_check_line(X, ii, c < 128 ? sh->line_of[0x80 | c] : -1);
+    }
+}
+
+static void rx_remove(rx_sim* X, uint32_t ii) /* sim_fec_evict_segment + flex removal (sim_fec.c:93-102, 199-205) */
+{
+    const rx_inst* g = &X->G[ii];
+    for (uint32_t i = 0; i < g->count; ++i)
+        hm_del(&X->cache, g->base + i);
+    hm_del(&X->flex_of, g->fec_id);
+}
+
+/* sim_fec_put_segment (sim_fec.c:171-207); cache values: record + 1, or 0x80000000 | index into X->rh */
+static void rx_put_segment(rx_sim* X, const rfec_hdr* h, uint16_t fec_id, uint32_t cval, int32_t src)
+{
+    if (h->seq == 0 || hm_get(&X->cache, h->seq))
+        return;
+    X->max_ts = h->ts > X->max_ts ? h->ts : X->max_ts;
+    if (hm_put(&X->cache, h->seq, cval)) {
+        X->oom = 1;
+        return;
+    }
+    const uint32_t fi = hm_get(&X->flex_of, fec_id);
+    if (!fi)
+        return;
+    rx_on_segment(X, fi - 1, h, src, 1);
+    if (X->G[fi - 1].nsegs >= X->G[fi - 1].count) /* flex_fec_receiver_full */
+        rx_remove(X, fi - 1);
+}
+
+/* The device plan of a flex geometry: every row with 2+ members (also rows
+ * at and beyond `row` when row * col < count: the reference bounds rows by
+ * count only), every column c < col with 2+ members, and the extra columns
+ * c >= col of xcol.  Lines of fewer than 2 members can never recover (one
+ * missing member leaves none present).  Standard geometry (row * col >=
+ * count, no extra columns) is exactly rfec_plan_matrix's plan. */
+static int rx_build_plan(uint32_t count, uint32_t row, uint32_t col, const uint64_t* xcol, rfec_plan* p)
+{
+    if (row * col >= count && !xcol[0] && !xcol[1])
+        return rfec_plan_matrix((uint16_t)count, (uint8_t)row, (uint8_t)col, RFEC_LAYER_ROWS | RFEC_LAYER_COLS, p);
+    memset(p, 0, sizeof(*p));
+    p->k = (uint16_t)count;
+    p->row = (uint8_t)row;
+    p->col = (uint8_t)col;
+    p->rc = 1;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (uint32_t x = 0; x < 128; ++x) {
+            if (pass == 1 && x >= col && !((xcol[x >> 6] >> (x & 63)) & 1ull))
+                continue;
+            uint32_t first, stride;
+            const uint32_t n = rx_line_members(count, row, col, pass ? (0x80u | x) : x, &first, &stride);
+            if (n < 2)
+                continue;
+            if (p->n_lines >= RFEC_MAX_LINES)
+                return RFEC_EINVAL;
+            rfec_line* l = &p->line[p->n_lines++];
+            l->first = (uint8_t)first;
+            l->stride = (uint8_t)stride;
+            l->count = (uint8_t)n;
+            l->index = (uint8_t)(pass ? (0x80u | x) : x);
+        }
+        if (pass == 0)
+            p->n_row_lines = p->n_lines;
+    }
+    return RFEC_OK;
+}
+
+/* flexes of up to 255 segments and 64 lines have a device plan (8-bit
+ * members); above RFEC_MAX_K the device recovery takes line jobs (rx_big_peel)
+ * instead of the batched peel, whose masks hold 128 members.  Larger flexes
+ * (a foreign peer's: the reference receiver takes any uint16_t count,
+ * flex_fec_receiver.c:69-88, and up to 128 rows and 128 columns of FEC
+ * indices) are huge shapes: line = FEC index, line jobs too. */
+#define RX_MAX_COUNT 255u
+
+static uint32_t rx_shape_of(rx_sim* X, uint32_t count, uint32_t row, uint32_t col, const uint64_t* xcol)
+{
+    if (row > 255 || col > 255)
+        return UINT32_MAX;
+    const int extended = xcol[0] || xcol[1];
+    const uint32_t key = count << 16 | row << 8 | col;
+    if (!extended) {
+        const uint32_t s = hm_get(&X->shape_of, key);
+        if (s)
+            return s - 1;
+    } else { /* rare (a peer's extra columns): a scan */
+        for (uint32_t s = 0; s < X->ns; ++s)
+            if (X->S[s].count == count && X->S[s].row == row && X->S[s].col == col && X->S[s].xcol[0] == xcol[0] &&
+                X->S[s].xcol[1] == xcol[1])
+                return s;
+    }
+    RX_GROW(X->S, X->ns, X->scap, 1, rx_shape);
+    if (X->oom)
+        return UINT32_MAX;
+    rx_shape* sh = &X->S[X->ns];
+    memset(sh, 0, sizeof(*sh));
+    sh->count = count;
+    sh->row = row;
+    sh->col = col;
+    sh->xcol[0] = xcol[0];
+    sh->xcol[1] = xcol[1];
+    sh->huge = count > RX_MAX_COUNT || rx_build_plan(count, row, col, xcol, &sh->plan) != RFEC_OK;
+    if (sh->huge) { /* every FEC index is a line */
+        sh->n_lines = 256;
+        for (int i = 0; i < 256; ++i)
+            sh->line_of[i] = (int16_t)i;
+    } else {
+        sh->n_lines = sh->plan.n_lines;
+        for (int i = 0; i < 256; ++i)
+            sh->line_of[i] = -1;
+        for (uint32_t l = 0; l < sh->n_lines; ++l)
+            sh->line_of[sh->plan.line[l].index] = (int16_t)l;
+    }
+    if (!extended && hm_put(&X->shape_of, key, X->ns + 1)) {
+        X->oom = 1;
+        return UINT32_MAX;
+    }
+    return X->ns++;
+}
+
+/* A parity for a column c >= col of flex ii (a peer's plan, not razor's
+ * sender): the flex moves to the shape with that column added, its
+ * registered parities carried over by index.  Returns the column's line in
+ * the new shape, or -1 (no room: the parity stays unmodelled). */
+static int rx_extend(rx_sim* X, uint32_t ii, uint32_t c)
+{
+    rx_inst* g = &X->G[ii];
+    uint64_t xcol[2] = {X->S[g->shape].xcol[0], X->S[g->shape].xcol[1]};
+    xcol[c >> 6] |= 1ull << (c & 63);
+    const uint32_t ns = rx_shape_of(X, g->count, g->row, g->col, xcol);
+    if (ns == UINT32_MAX)
+        return -1;
+    const rx_shape* nsh = &X->S[ns]; /* (X->S may have moved) */
+    const rx_shape* osh = &X->S[g->shape];
+    RX_GROW(X->line_par, X->nline, X->linecap, nsh->n_lines, int32_t);
+    if (X->oom)
+        return -1;
+    uint64_t ppm = 0;
+    for (uint32_t l = 0; l < nsh->n_lines; ++l) {
+        const int ol = osh->line_of[nsh->huge ? l : nsh->plan.line[l].index];
+        X->line_par[X->nline + l] = ol >= 0 && ((g->ppm >> ol) & 1ull) ? X->line_par[g->line0 + ol] : -1;
+        if (ol >= 0 && ((g->ppm >> ol) & 1ull) && !nsh->huge)
+            ppm |= 1ull << l;
+    }
+    if (nsh->huge) /* more than RFEC_MAX_LINES lines now: membership moves to the slot headers (rx_has) */
+        for (uint32_t t = 0; t < g->count; ++t)
+            if (!((g->have[t >> 6] >> (t & 63)) & 1ull))
+                X->slot_hdr[g->slot0 + t].seq = ~(g->base + t);
+    g->line0 = X->nline;
+    X->nline += nsh->n_lines;
+    g->ppm = ppm;
+    g->shape = ns;
+    return nsh->line_of[0x80u | c];
+}
+
+/* sim_fec_put_fec_packet (sim_fec.c:141-169) -> flex_fec_receiver_on_fec (flex_fec_receiver.c:208-241) */
+static void rx_put_fec(rx_sim* X, uint32_t a)
+{
+    const rfec_wire_rec* f = &X->R[a];
+    if (f->base_id + f->count == 0u || f->send_ts + 3000u < X->max_ts) {
+        X->dropped++;
+        return;
+    }
+    uint32_t fi = hm_get(&X->flex_of, f->fec_id);
+    if (!fi) { /* flex_fec_receiver_active (flex_fec_receiver.c:69-88) */
+        RX_GROW(X->G, X->ng, X->gcap, 1, rx_inst);
+        if (X->oom)
+            return;
+        rx_inst* g = &X->G[X->ng];
+        memset(g, 0, sizeof(*g));
+        g->fec_id = f->fec_id;
+        g->base = f->base_id;
+        g->count = f->count;
+        g->row = f->row;
+        g->col = f->col;
+        g->fec_ts = f->send_ts;
+        g->ref_ok = g->col >= 2 && g->row >= 1 && g->count >= 1;
+        static const uint64_t no_xcol[2] = {0, 0};
+        g->shape = g->ref_ok ? rx_shape_of(X, g->count, g->row, g->col, no_xcol) : UINT32_MAX;
+        if (g->shape != UINT32_MAX) {
+            rx_shape* sh = &X->S[g->shape];
+            g->gslot = sh->n_groups++;
+            RX_GROW(X->slot_src, X->nslot, X->slotcap, g->count, int32_t);
+            RX_GROW(X->slot_hdr, X->nslot, X->slothcap, g->count, rfec_hdr);
+            RX_GROW(X->line_par, X->nline, X->linecap, sh->n_lines, int32_t);
+            if (X->oom)
+                return;
+            g->slot0 = X->nslot;
+            g->line0 = X->nline;
+            for (uint32_t i = 0; i < g->count; ++i) {
+                X->slot_src[X->nslot + i] = -1;
+                X->slot_hdr[X->nslot + i].seq = ~(g->base + i); /* rx_has: not in the flex */
+            }
+            for (uint32_t l = 0; l < sh->n_lines; ++l)
+                X->line_par[X->nline + l] = -1;
+            X->nslot += g->count;
+            X->nline += sh->n_lines;
+        } else if (g->ref_ok) {
+            X->unmodelled++;
+        }
+        fi = ++X->ng;
+        if (hm_put(&X->flex_of, f->fec_id, fi)) {
+            X->oom = 1;
+            return;
+        }
+        for (uint32_t i = 0; i < g->count && g->shape != UINT32_MAX; ++i) { /* sim_fec_add_segment_to_flex */
+            const uint32_t c = hm_get(&X->cache, g->base + i);
+            if (!c)
+                continue;
+            if (c & 0x80000000u) {
+                rx_on_segment(X, fi - 1, &X->rh[c & 0x7FFFFFFFu], -1, 0);
+            } else {
+                const rfec_hdr h = rec_hdr(&X->R[c - 1]);
+                rx_on_segment(X, fi - 1, &h, (int32_t)(c - 1), 0);
+            }
+        }
+    }
+    rx_inst* g = &X->G[fi - 1];
+    if (!g->ref_ok || g->shape == UINT32_MAX)
+        return;
+    int l = X->S[g->shape].line_of[f->index];
+    if (X->S[g->shape].huge) { /* line = index; the parity registered once */
+        uint32_t first, stride;
+        if (rx_line_members(g->count, g->row, g->col, f->index, &first, &stride) < 2 ||
+            X->line_par[g->line0 + l] >= 0)
+            return;
+        X->line_par[g->line0 + l] = (int32_t)a;
+        rx_check_line(X, fi - 1, l);
+        return;
+    }
+    if (l < 0) {
+        uint32_t first, stride;
+        if (rx_line_members(g->count, g->row, g->col, f->index, &first, &stride) < 2)
+            return; /* a line that can never recover (flex_fec_receiver.c:133-134, 189-190) */
+        /* a column c >= col (razor's sender never emits one; a peer may) */
+        if ((l = rx_extend(X, fi - 1, f->index & 0x7Fu)) < 0) {
+            X->unmodelled++;
+            return;
+        }
+        g = &X->G[fi - 1];
+    }
+    if (X->S[g->shape].huge) { /* (the extension took it past RFEC_MAX_LINES lines) */
+        if (X->line_par[g->line0 + l] >= 0)
+            return;
+    } else {
+        if ((g->ppm >> l) & 1ull)
+            return;
+        g->ppm |= 1ull << l;
+    }
+    X->line_par[g->line0 + l] = (int32_t)a;
+    rx_check_line(X, fi - 1, l);
+}
+
+/* sim_receiver_recover (sim_receiver.c:780-804): lowest packet_id first, cascading */
+static void rx_drain(rx_sim* X)
+{
+    while (X->npend && !X->oom) {
+        uint32_t b = 0;
+        for (uint32_t i = 1; i < X->npend; ++i)
+            if (X->pend[i].hdr.seq < X->pend[b].hdr.seq)
+                b = i;
+        const rx_event e = X->pend[b];
+        X->pend[b] = X->pend[--X->npend];
+        if (hm_get(&X->seen, e.hdr.seq))
+            continue;
+        RX_GROW(X->out, X->nout, X->outcap, 1, rx_event);
+        RX_GROW(X->rh, X->nrh, X->rhcap, 1, rfec_hdr);
+        if (X->oom || hm_put(&X->seen, e.hdr.seq, 1)) {
+            X->oom = 1;
+            return;
+        }
+        X->out[X->nout++] = e;
+        X->rh[X->nrh] = e.hdr;
+        const uint32_t idx = X->nrh++;
+        rx_put_segment(X, &e.hdr, (uint16_t)X->G[e.inst].fec_id, 0x80000000u | idx, -1);
+    }
+}
+
+static void rx_sim_free(rx_sim* X)
+{
+    hm_free(&X->seen);
+    hm_free(&X->cache);
+    hm_free(&X->flex_of);
+    hm_free(&X->shape_of);
+    free(X->G);
+    free(X->S);
+    free(X->slot_src);
+    free(X->slot_hdr);
+    free(X->line_par);
+    free(X->pend);
+    free(X->out);
+    free(X->rh);
+    free(X->dl);
+    free(X->jobs);
+    free(X->jlevel);
+    free(X->jmem);
+}
+
+static int cmp_u32(const void* a, const void* b)
+{
+    const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+/* keys of a map, ascending (the skiplists' iteration order); NULL on OOM */
+static uint32_t* hm_sorted_keys(const hmap* m, uint32_t* n)
+{
+    uint32_t* k = (uint32_t*)malloc(((size_t)m->n + 1) * sizeof(uint32_t));
+    *n = 0;
+    if (!k)
+        return NULL;
+    for (uint32_t i = 0; i <= m->mask; ++i)
+        if (m->v[i])
+            k[(*n)++] = m->k[i];
+    qsort(k, *n, sizeof(uint32_t), cmp_u32);
+    return k;
+}
+
+/* sim_fec_evict (sim_fec.c:209-241) past its 300 ms wall-clock gate: flexes in
+ * fec_id order while stale (fec_ts + 3000 <= max_ts) or full, removed with
+ * their members' cache entries; then cached segments in packet_id order while
+ * older than 6 s (timestamp + 6000 < max_ts).  Both walks stop at the first
+ * entry that stays, as the skiplist walks do. */
+static void rx_evict(rx_sim* X)
+{
+    uint32_t n = 0;
+    uint32_t* k = hm_sorted_keys(&X->flex_of, &n);
+    if (!k) {
+        X->oom = 1;
+        return;
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t fi = hm_get(&X->flex_of, k[i]) - 1;
+        const rx_inst* g = &X->G[fi];
+        if (!(g->fec_ts + 3000u <= X->max_ts || g->nsegs >= g->count))
+            break;
+        rx_remove(X, fi);
+    }
+    free(k);
+    k = hm_sorted_keys(&X->cache, &n);
+    if (!k) {
+        X->oom = 1;
+        return;
+    }
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t c = hm_get(&X->cache, k[i]);
+        const uint32_t ts = (c & 0x80000000u) ? X->rh[c & 0x7FFFFFFFu].ts : X->R[c - 1].hdr.ts;
+        if (!(ts + 6000u < X->max_ts))
+            break;
+        hm_del(&X->cache, k[i]);
+    }
+    free(k);
+}
+
+static int cmp_event(const void* a, const void* b)
+{
+    const uint32_t x = ((const rx_event*)a)->hdr.seq, y = ((const rx_event*)b)->hdr.seq;
+    return x < y ? -1 : x > y;
+}
+
+typedef struct {
+    uint8_t* h;  /* pinned, device-mapped */
+    uint8_t* hd; /* h as the device addresses it */
+    size_t hb;
+    uint8_t* d;
+    size_t db;
+} rx_ctx;
+static __thread rx_ctx t_rx;
+
+/* The device address of host memory the device can read directly (pinned:
+ * rfec_pinned_alloc, hipHostMalloc, registered), else NULL (pageable: the
+ * caller copies).  A failed query leaves no pending HIP error behind. */
+static const uint8_t* host_mapped(const void* p)
+{
+    hipPointerAttribute_t a;
+    void* d = NULL;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost ||
+        hipHostGetDevicePointer(&d, (void*)p, 0) != hipSuccess || !d) {
+        (void)hipGetLastError();
+        return NULL;
+    }
+    return (const uint8_t*)d;
+}
+
+/* Grows the per-thread pinned / device areas.  The first `keep` bytes of the
+ * pinned area survive a grow (copied into the new block before the old one is
+ * freed: the allocator may hand back the same address, so callers cannot tell
+ * a grow from the pointer). */
+static int rx_reserve(size_t host_bytes, size_t dev_bytes, size_t keep)
+{
+    hipError_t e;
+    if (t_rx.hb < host_bytes) {
+        uint8_t* nh = NULL;
+        host_bytes += host_bytes / 4;
+        void* nd = NULL;
+        if ((e = hipHostMalloc((void**)&nh, host_bytes, hipHostMallocMapped)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "rx staging (host)", e);
+        if ((e = hipHostGetDevicePointer(&nd, nh, 0)) != hipSuccess) {
+            (void)hipHostFree(nh);
+            return set_err(RFEC_EDEVICE, "rx staging (host): device view", e);
+        }
+        if (t_rx.h) {
+            if (keep)
+                memcpy(nh, t_rx.h, keep < t_rx.hb ? keep : t_rx.hb);
+            (void)hipHostFree(t_rx.h);
+        }
+        t_rx.h = nh;
+        t_rx.hd = (uint8_t*)nd;
+        t_rx.hb = host_bytes;
+    }
+    if (t_rx.db < dev_bytes) {
+        if (t_rx.d)
+            (void)hipFree(t_rx.d);
+        t_rx.d = NULL;
+        t_rx.db = 0;
+        dev_bytes += dev_bytes / 4;
+        if ((e = hipMalloc((void**)&t_rx.d, dev_bytes)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "rx workspace (device)", e);
+        t_rx.db = dev_bytes;
+    }
+    return RFEC_OK;
+}
+
+#define RX_ALIGN(x) (((x) + 255) & ~(size_t)255)
+
+static int rx_tables_init(rx_sim* X, uint32_t n)
+{
+    return hm_init(&X->seen, n) || hm_init(&X->cache, n) || hm_init(&X->flex_of, 1024) || hm_init(&X->shape_of, 64);
+}
+
+/* The control plane, in arrival order, over records [a0, a0 + n) of X->R:
+ * sim_receiver_put / sim_receiver_put_fec and the recovery cascade. */
+static void rx_run(rx_sim* X, uint32_t a0, uint32_t n)
+{
+    for (uint32_t a = a0; a < a0 + n && !X->oom; ++a) {
+        const rfec_wire_rec* r = &X->R[a];
+        if (r->status != RFEC_WIRE_OK)
+            continue;
+        if (r->mid == RFEC_WIRE_SEG) { /* sim_receiver_put (sim_receiver.c:811-827) */
+            if (hm_get(&X->seen, r->hdr.seq))
+                continue;
+            if (hm_put(&X->seen, r->hdr.seq, 1)) {
+                X->oom = 1;
+                break;
+            }
+            if (r->fec_id == 0)
+                continue;
+            const rfec_hdr h = rec_hdr(r);
+            rx_put_segment(X, &h, r->fec_id, a + 1, (int32_t)a);
+        } else if (r->mid == RFEC_WIRE_FEC) {
+            rx_put_fec(X, a);
+        }
+        rx_drain(X);
+    }
+}
+
+/* A group recovered by line jobs (rx_line_jobs: above RFEC_MAX_K segments or a
+ * huge shape -- a foreign peer's flex): the canonical
+ * peel (lines in plan order -- rows, then columns -- to a fixpoint, with
+ * flex_fec_recover's header checks, flex_fec_xor.c:60-99) from its arrived
+ * members and registered parities, over headers on the host; each firing
+ * becomes a line job the device runs (rfec_launch_line_jobs).  job_of[t]: the
+ * job recovering member t, or -1.  Returns -1 when out of memory. */
+static int rx_big_peel(rx_sim* X, uint32_t gi, int32_t* job_of)
+{
+    const rx_inst* g = &X->G[gi];
+    const rx_shape* sh = &X->S[g->shape];
+    const uint32_t k = g->count, NL = sh->n_lines;
+    rfec_hdr* hd = (rfec_hdr*)malloc((size_t)k * sizeof(rfec_hdr));
+    int32_t* src = (int32_t*)malloc((size_t)k * sizeof(int32_t));
+    uint16_t* lvl = (uint16_t*)malloc((size_t)k * sizeof(uint16_t));
+    uint8_t* have = (uint8_t*)malloc(k);
+    if (!hd || !src || !lvl || !have) {
+        free(hd);
+        free(src);
+        free(lvl);
+        free(have);
+        return -1;
+    }
+    for (uint32_t i = 0; i < k; ++i) {
+        job_of[i] = -1;
+        lvl[i] = 0;
+        src[i] = X->slot_src[g->slot0 + i];
+        have[i] = src[i] >= 0; /* the peel starts from the arrived members */
+        if (have[i])
+            hd[i] = X->slot_hdr[g->slot0 + i];
+    }
+    for (int progress = 1; progress && !X->oom;) {
+        progress = 0;
+        for (uint32_t l = 0; l < NL && !X->oom; ++l) {
+            uint32_t first, stride;
+            int reg;
+            const uint32_t n = rx_line(X, g, l, &first, &stride, &reg);
+            if (!reg)
+                continue;
+            uint32_t miss = 0, present = 0, t = 0;
+            for (uint32_t q = 0; q < n; ++q) {
+                const uint32_t i = first + q * stride;
+                if (have[i]) {
+                    present++;
+                } else {
+                    miss++;
+                    t = i;
+                }
+            }
+            if (miss != 1 || present == 0)
+                continue;
+            const rfec_wire_rec* f = &X->R[X->line_par[g->line0 + l]];
+            const uint32_t L = f->data_size;
+            if (L > X->capacity)
+                continue;
+            rfec_hdr h = f->hdr;
+            int ok = 1;
+            uint16_t level = 0;
+            for (uint32_t q = 0; q < n && ok; ++q) {
+                const uint32_t i = first + q * stride;
+                if (i == t)
+                    continue;
+                const rfec_hdr* m = &hd[i];
+                ok = m->size <= L;
+                h.seq ^= m->seq;
+                h.fid ^= m->fid;
+                h.ts ^= m->ts;
+                h.index ^= m->index;
+                h.total ^= m->total;
+                h.ftype ^= m->ftype;
+                h.payload_type ^= m->payload_type;
+                h.size ^= m->size;
+                level = lvl[i] > level ? lvl[i] : level;
+            }
+            if (!ok || h.size > L)
+                continue;
+            RX_GROW(X->jobs, X->njobs, X->jobcap, 1, rfec_line_job);
+            RX_GROW(X->jlevel, X->njobs, X->jlevelcap, 1, uint16_t);
+            RX_GROW(X->jmem, X->njmem, X->jmemcap, present, int32_t);
+            if (X->oom)
+                break;
+            rfec_line_job* J = &X->jobs[X->njobs];
+            J->out = (int32_t)X->njobs;
+            J->parity = X->line_par[g->line0 + l];
+            J->member0 = X->njmem;
+            J->n_members = present;
+            for (uint32_t q = 0; q < n; ++q) {
+                const uint32_t i = first + q * stride;
+                if (i != t)
+                    X->jmem[X->njmem++] = src[i];
+            }
+            X->jlevel[X->njobs] = (uint16_t)(level + 1);
+            job_of[t] = (int32_t)X->njobs;
+            src[t] = -1 - (int32_t)X->njobs;
+            lvl[t] = (uint16_t)(level + 1);
+            hd[t] = h;
+            have[t] = 1;
+            X->njobs++;
+            progress = 1;
+        }
+    }
+    free(hd);
+    free(src);
+    free(lvl);
+    free(have);
+    return X->oom ? -1 : 0;
+}
+
+#define RX_MAX_LEVEL 256u
+
+/* A group whose device recovery runs as the host peel's line jobs: above
+ * RFEC_MAX_K segments (the batched peel's masks hold 128 members), or a huge
+ * shape of any count (no device plan: more than RFEC_MAX_LINES lines, e.g. a
+ * peer's 128-segment flex of 64 rows x 2 columns, or one rx_extend took past
+ * 64 lines; its parity rows sit at a 256-line stride). */
+static int rx_line_jobs(const rx_shape* sh) { return sh->count > RFEC_MAX_K || sh->huge; }
+
+/* The device side of one call: the groups that delivered something in this
+ * call, rebuilt from their arrived members and registered parities (rows of
+ * `rows`, DEVICE, indexed by record), peeled by rfec_recover_batch, and the
+ * delivered rows copied out.  The pinned tables go after the first `hoff`
+ * bytes of t_rx.h, which survive a grow (X->R may live there). */
+static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t capacity, size_t hoff,
+                     rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out, rfec_rx_report* rep,
+                     hipStream_t sm)
+{
+    hipError_t e = hipSuccess;
+    int rc = RFEC_OK, ke = 0;
+    const double th = now_us();
+    *n_out = 0;
+    if (X->nout)
+        qsort(X->out, X->nout, sizeof(rx_event), cmp_event);
+    if (X->nout == 0) { /* nothing recovered: no device work */
+        rep->host_us += now_us() - th;
+        return RFEC_OK;
+    }
+    /* group tables, shape-major, for the groups that deliver something (work
+     * proportional to the deliveries, not to the open flexes) */
+    for (uint32_t s = 0; s < X->ns; ++s)
+        X->S[s].n_groups = 0;
+    if (++X->epoch == 0) { /* wrapped: no instance may carry a stale stamp */
+        for (uint32_t gi = 0; gi < X->ng; ++gi)
+            X->G[gi].gstamp = 0;
+        X->epoch = 1;
+    }
+    X->ndl = 0;
+    for (uint32_t q = 0; q < X->nout; ++q) {
+        const uint32_t gi = X->out[q].inst;
+        rx_inst* g = &X->G[gi];
+        if (g->gstamp != X->epoch) {
+            RX_GROW(X->dl, X->ndl, X->dlcap, 1, uint32_t);
+            if (X->oom)
+                return set_err(RFEC_ENOMEM, "rx: delivery list", 0);
+            g->gstamp = X->epoch;
+            g->gslot = X->S[g->shape].n_groups++;
+            X->dl[X->ndl++] = gi;
+        }
+    }
+    uint32_t nrows = 0, prows = 0, ngs = 0;
+    for (uint32_t s = 0; s < X->ns; ++s) {
+        rx_shape* sh = &X->S[s];
+        sh->row0 = nrows;
+        sh->prow0 = prows;
+        sh->group0 = ngs;
+        if (rx_line_jobs(sh)) /* line jobs instead (below) */
+            continue;
+        nrows += sh->n_groups * sh->count;
+        prows += sh->n_groups * sh->n_lines;
+        ngs += sh->n_groups;
+    }
+    /* groups above RFEC_MAX_K: the host peel's line jobs, output rows after
+     * the batched peel's rows, launched level by level (jobs sorted by level) */
+    X->njobs = X->njmem = 0;
+    uint32_t nbig = 0, maxlvl = 0;
+    for (uint32_t d = 0; d < X->ndl; ++d)
+        if (rx_line_jobs(&X->S[X->G[X->dl[d]].shape]))
+            nbig += X->G[X->dl[d]].count;
+    int32_t* job_of = nbig ? (int32_t*)malloc((size_t)nbig * sizeof(int32_t)) : NULL;
+    uint32_t* jperm = NULL;
+    if (nbig && !job_of)
+        return set_err(RFEC_ENOMEM, "rx: large groups", 0);
+    for (uint32_t d = 0, off = 0; d < X->ndl; ++d) {
+        rx_inst* g = &X->G[X->dl[d]];
+        if (!rx_line_jobs(&X->S[g->shape]))
+            continue;
+        g->gslot = off; /* (a large group's slot: its job_of range) */
+        if (rx_big_peel(X, X->dl[d], job_of + off))
+            X->oom = 1;
+        off += g->count;
+    }
+    if (X->oom) {
+        free(job_of);
+        return set_err(RFEC_ENOMEM, "rx: line jobs", 0);
+    }
+    /* a line fires at most once, so a chain is at most as deep as a group has lines (256 FEC indices) */
+    uint32_t lvl_n[RX_MAX_LEVEL + 1] = {0};
+    if (X->njobs) { /* stable sort by level; codes and job_of follow */
+        for (uint32_t j = 0; j < X->njobs; ++j) {
+            if (X->jlevel[j] > RX_MAX_LEVEL) {
+                free(job_of);
+                return set_err(RFEC_EINVAL, "rx: line job chain too deep", 0);
+            }
+            maxlvl = X->jlevel[j] > maxlvl ? X->jlevel[j] : maxlvl;
+            lvl_n[X->jlevel[j]]++;
+        }
+        uint32_t start[RX_MAX_LEVEL + 2] = {0};
+        for (uint32_t v = 1; v <= maxlvl; ++v)
+            start[v + 1] = start[v] + lvl_n[v];
+        jperm = (uint32_t*)malloc((size_t)X->njobs * sizeof(uint32_t));
+        rfec_line_job* sorted = (rfec_line_job*)malloc((size_t)X->njobs * sizeof(rfec_line_job));
+        if (!jperm || !sorted) {
+            free(jperm);
+            free(sorted);
+            free(job_of);
+            return set_err(RFEC_ENOMEM, "rx: line jobs", 0);
+        }
+        for (uint32_t j = 0; j < X->njobs; ++j)
+            jperm[j] = start[X->jlevel[j]]++;
+        for (uint32_t j = 0; j < X->njobs; ++j) {
+            sorted[jperm[j]] = X->jobs[j];
+            sorted[jperm[j]].out = (int32_t)jperm[j];
+        }
+        memcpy(X->jobs, sorted, (size_t)X->njobs * sizeof(rfec_line_job));
+        free(sorted);
+        for (uint32_t m = 0; m < X->njmem; ++m)
+            if (X->jmem[m] < 0)
+                X->jmem[m] = -1 - (int32_t)jperm[-1 - X->jmem[m]];
+        for (uint32_t i = 0; i < nbig; ++i)
+            if (job_of[i] >= 0)
+                job_of[i] = (int32_t)jperm[job_of[i]];
+    }
+    const size_t o_smap = 0, o_pmap = RX_ALIGN((size_t)nrows * 4), o_hdr = RX_ALIGN(o_pmap + (size_t)prows * 4);
+    const size_t o_meta = RX_ALIGN(o_hdr + (size_t)nrows * sizeof(rfec_hdr));
+    const size_t o_fs = RX_ALIGN(o_meta + (size_t)prows * sizeof(rfec_hdr));
+    const size_t o_pres = RX_ALIGN(o_fs + (size_t)prows * 2), o_pp = RX_ALIGN(o_pres + (size_t)ngs * 16);
+    const size_t o_omap = RX_ALIGN(o_pp + (size_t)ngs * 8), o_jobs = RX_ALIGN(o_omap + (size_t)X->nout * 4);
+    const size_t o_jmem = RX_ALIGN(o_jobs + (size_t)X->njobs * sizeof(rfec_line_job));
+    const size_t o_in_end = RX_ALIGN(o_jmem + (size_t)X->njmem * 4);
+    const size_t o_rec = o_in_end, host_bytes = RX_ALIGN(o_rec + (size_t)ngs * 16);
+    size_t ws_bytes = 0;
+    for (uint32_t s = 0; s < X->ns; ++s)
+        if (!rx_line_jobs(&X->S[s]))
+            ws_bytes += RX_ALIGN(rfec_recover_workspace_size(&X->S[s].plan, X->S[s].n_groups));
+    const size_t d_shards = o_in_end, d_par = RX_ALIGN(d_shards + ((size_t)nrows + X->njobs) * stride);
+    const size_t d_ws = RX_ALIGN(d_par + (size_t)prows * stride), d_rec = RX_ALIGN(d_ws + ws_bytes);
+    const size_t d_out = RX_ALIGN(d_rec + (size_t)ngs * 16), dev_bytes = RX_ALIGN(d_out + (size_t)X->nout * stride);
+    const int r_in_stage = (const uint8_t*)X->R == t_rx.h;
+    if ((rc = rx_reserve(hoff + host_bytes, dev_bytes, hoff))) {
+        free(job_of);
+        free(jperm);
+        return rc;
+    }
+    if (r_in_stage)
+        X->R = (const rfec_wire_rec*)t_rx.h;
+    uint8_t* H = t_rx.h + hoff;
+    memset(H, 0, o_in_end);
+    int32_t* smap = (int32_t*)(H + o_smap);
+    int32_t* pmap = (int32_t*)(H + o_pmap);
+    rfec_hdr* hh = (rfec_hdr*)(H + o_hdr);
+    rfec_hdr* mh = (rfec_hdr*)(H + o_meta);
+    uint16_t* fsz = (uint16_t*)(H + o_fs);
+    uint64_t* pres = (uint64_t*)(H + o_pres);
+    uint64_t* ppm = (uint64_t*)(H + o_pp);
+    int32_t* omap = (int32_t*)(H + o_omap);
+    if (X->njobs) {
+        memcpy(H + o_jobs, X->jobs, (size_t)X->njobs * sizeof(rfec_line_job));
+        memcpy(H + o_jmem, X->jmem, (size_t)X->njmem * 4);
+    }
+    for (uint32_t d = 0; d < X->ndl; ++d) {
+        const rx_inst* g = &X->G[X->dl[d]];
+        const rx_shape* sh = &X->S[g->shape];
+        if (rx_line_jobs(sh))
+            continue;
+        const uint32_t gg = sh->group0 + g->gslot, r0 = sh->row0 + g->gslot * sh->count;
+        const uint32_t p0 = sh->prow0 + g->gslot * sh->n_lines;
+        pres[2 * gg] = g->arrived[0];
+        pres[2 * gg + 1] = g->arrived[1];
+        ppm[gg] = g->ppm;
+        for (uint32_t i = 0; i < sh->count; ++i) {
+            const int32_t src = X->slot_src[g->slot0 + i];
+            smap[r0 + i] = src;
+            if (src >= 0)
+                hh[r0 + i] = X->slot_hdr[g->slot0 + i];
+        }
+        for (uint32_t l = 0; l < sh->n_lines; ++l) {
+            const int32_t src = X->line_par[g->line0 + l];
+            pmap[p0 + l] = src;
+            if (src >= 0) {
+                mh[p0 + l] = X->R[src].hdr;
+                fsz[p0 + l] = X->R[src].data_size;
+            }
+        }
+    }
+    /* output rows: the recovering group's slot */
+    uint32_t nok = 0;
+    for (uint32_t q = 0; q < X->nout; ++q) {
+        const rx_event* ev = &X->out[q];
+        const rx_inst* g = &X->G[ev->inst];
+        const rx_shape* sh = &X->S[g->shape];
+        const uint32_t t = ev->hdr.seq - g->base;
+        if (rx_line_jobs(sh)) /* the job that recovers t */
+            omap[q] = t < g->count && job_of[g->gslot + t] >= 0 ? (int32_t)(nrows + (uint32_t)job_of[g->gslot + t]) : -1;
+        else
+            omap[q] = t < g->count ? (int32_t)(sh->row0 + g->gslot * sh->count + t) : -1;
+    }
+    free(job_of);
+    free(jperm);
+    rep->host_us += now_us() - th;
+    rep->n_groups = ngs;
+    for (uint32_t s = 0; s < X->ns; ++s)
+        rep->n_shapes += X->S[s].n_groups != 0;
+    /* the device: rows in place, one peel per shape, the delivered rows compacted */
+    uint8_t* D = t_rx.d;
+    double tt = now_us();
+    if ((e = hipMemcpyAsync(D, H, o_in_end, hipMemcpyHostToDevice, sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx: H2D", e);
+    ke = rfec_launch_gather_rows(D + d_shards, rows, (const int32_t*)(D + o_smap), nrows, stride, sm);
+    if (!ke)
+        ke = rfec_launch_gather_rows(D + d_par, rows, (const int32_t*)(D + o_pmap), prows, stride, sm);
+    for (uint32_t v = 1, lo = 0; v <= maxlvl && !ke; lo += lvl_n[v], ++v) /* the large groups' line jobs */
+        ke = rfec_launch_line_jobs((const rfec_line_job*)(D + o_jobs) + lo, lvl_n[v], (const int32_t*)(D + o_jmem),
+                                   rows, D + d_shards + (size_t)nrows * stride, stride, sm);
+    size_t wso = 0;
+    for (uint32_t s = 0; s < X->ns && !ke; ++s) {
+        const rx_shape* sh = &X->S[s];
+        if (!sh->n_groups || rx_line_jobs(sh))
+            continue;
+        rfec_kmask M;
+        make_masks(&sh->plan, &M);
+        ke = rfec_launch_recover(&M, sh->n_groups, stride, capacity, D + d_shards + (size_t)sh->row0 * stride,
+                                 (rfec_hdr*)(D + o_hdr) + sh->row0, (const uint64_t*)(D + o_pres) + 2 * sh->group0,
+                                 D + d_par + (size_t)sh->prow0 * stride, (const rfec_hdr*)(D + o_meta) + sh->prow0,
+                                 (const uint16_t*)(D + o_fs) + sh->prow0, (const uint64_t*)(D + o_pp) + sh->group0,
+                                 (uint64_t*)(D + d_rec) + 2 * sh->group0, D + d_ws + wso, sm, g_tuning);
+        wso += RX_ALIGN(rfec_recover_workspace_size(&sh->plan, sh->n_groups));
+    }
+    /* delivered rows: straight into the caller's output when it is pinned and
+       large enough (no second round trip; rows the peel did not cover are
+       squeezed out on the host below), else into the device staging */
+    uint8_t* outd = X->nout && X->nout <= max_out ? (uint8_t*)host_mapped(out_payload) : NULL;
+    if (!ke && X->nout)
+        ke = rfec_launch_gather_rows(outd ? outd : D + d_out, D + d_shards, (const int32_t*)(D + o_omap), X->nout,
+                                     stride, sm);
+    uint64_t* rec = (uint64_t*)(H + o_rec);
+    if (ke || (e = hipMemcpyAsync(rec, D + d_rec, (size_t)ngs * 16, hipMemcpyDeviceToHost, sm)) != hipSuccess ||
+        (e = hipStreamSynchronize(sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx: recover", ke ? ke : (int)e);
+    rep->kernel_us += now_us() - tt;
+    /* the device peel covers every packet the arrival-order pass delivered (same lines, a superset of
+       the members at each firing); anything else is reported, not delivered */
+    for (uint32_t q = 0; q < X->nout; ++q) {
+        const rx_event* ev = &X->out[q];
+        const rx_inst* g = &X->G[ev->inst];
+        const uint32_t t = ev->hdr.seq - g->base, gg = X->S[g->shape].group0 + g->gslot;
+        const int big = rx_line_jobs(&X->S[g->shape]);
+        if (big ? omap[q] < 0 : t >= g->count || !((rec[2 * gg + (t >> 6)] >> (t & 63)) & 1ull)) {
+            X->unmodelled++;
+            omap[q] = -1;
+            continue;
+        }
+        nok++;
+    }
+    if (nok > max_out) {
+        *n_out = nok;
+        return set_err(RFEC_EINVAL, "rx: output too small", 0);
+    }
+    tt = now_us();
+    uint32_t o = 0;
+    if (outd) { /* the rows are in out_payload already (the sync above) */
+        for (uint32_t q = 0; q < X->nout; ++q) {
+            if (omap[q] < 0)
+                continue;
+            if (o != q)
+                memmove(out_payload + (size_t)o * stride, out_payload + (size_t)q * stride, stride);
+            X->out[o++] = X->out[q];
+        }
+    } else if (nok == X->nout) { /* the usual case: one copy */
+        if (nok)
+            e = hipMemcpyAsync(out_payload, D + d_out, (size_t)nok * stride, hipMemcpyDeviceToHost, sm);
+        o = nok;
+    }
+    for (uint32_t q = 0; q < X->nout && !outd && nok != X->nout && e == hipSuccess; ++q) {
+        if (omap[q] < 0)
+            continue;
+        e = hipMemcpyAsync(out_payload + (size_t)o * stride, D + d_out + (size_t)q * stride, stride,
+                           hipMemcpyDeviceToHost, sm);
+        X->out[o++] = X->out[q];
+    }
+    for (uint32_t q = 0; q < o; ++q) {
+        out[q].hdr = X->out[q].hdr;
+        out[q].fec_id = (uint16_t)X->G[X->out[q].inst].fec_id;
+        out[q].reserved = 0;
+    }
+    if (e == hipSuccess && !outd)
+        e = hipStreamSynchronize(sm);
+    if (e != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx: output D2H", e);
+    rep->d2h_us += now_us() - tt;
+    *n_out = o;
+    rep->n_recovered = o;
+    return RFEC_OK;
+}
+
+int rfec_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payload, uint32_t stride,
+                    uint32_t capacity, uint32_t* max_ts, rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out,
+                    uint32_t* n_out, rfec_rx_report* rep, void* stream)
+{
+    const double t0 = now_us();
+    if (!max_ts || !n_out || !rep || (n && (!recs || !payload)) || (max_out && (!out || !out_payload)))
+        return set_err(RFEC_EINVAL, "rx: bad argument", 0);
+    if (stride == 0 || stride % 16 || capacity > stride)
+        return set_err(RFEC_EINVAL, "rx: stride must be a multiple of 16 and >= capacity", 0);
+    memset(rep, 0, sizeof(*rep));
+    *n_out = 0;
+    if (n == 0)
+        return RFEC_OK;
+    hipStream_t sm = (hipStream_t)stream;
+    hipError_t e;
+    int rc = RFEC_OK;
+    /* 1. the records to the host (headers only: 64 B each) */
+    const size_t rec_bytes = RX_ALIGN((size_t)n * sizeof(rfec_wire_rec));
+    if ((rc = rx_reserve(rec_bytes, 0, 0)))
+        return rc;
+    double tt = now_us();
+    if ((e = hipMemcpyAsync(t_rx.h, recs, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost, sm)) !=
+            hipSuccess ||
+        (e = hipStreamSynchronize(sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx: records D2H", e);
+    rep->d2h_us += now_us() - tt;
+    /* 2. the control plane, in arrival order */
+    const double th = now_us();
+    rx_sim X;
+    memset(&X, 0, sizeof(X));
+    X.R = (const rfec_wire_rec*)t_rx.h;
+    X.capacity = capacity;
+    X.max_ts = *max_ts;
+    if (rx_tables_init(&X, n)) {
+        rx_sim_free(&X);
+        return set_err(RFEC_ENOMEM, "rx: host tables", 0);
+    }
+    rx_run(&X, 0, n);
+    if (X.oom) {
+        rx_sim_free(&X);
+        return set_err(RFEC_ENOMEM, "rx: host tables", 0);
+    }
+    *max_ts = X.max_ts;
+    rep->n_fec_dropped = X.dropped;
+    rep->host_us += now_us() - th;
+    /* 3. the device: the records stay at the start of the pinned block */
+    rc = rx_device(&X, payload, stride, capacity, rec_bytes, out, out_payload, max_out, n_out, rep, sm);
+    rep->n_unmodelled = X.unmodelled;
+    rx_sim_free(&X);
+    rep->total_us = now_us() - t0;
+    return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Received datagrams (host) -> recovered segments (host)                    */
+/* ------------------------------------------------------------------------ */
+void* rfec_pinned_alloc(size_t bytes)
+{
+    void* p = NULL;
+    hipError_t e;
+    if (bytes == 0)
+        return NULL;
+    if ((e = hipHostMalloc(&p, bytes, hipHostMallocDefault)) != hipSuccess) {
+        set_err(RFEC_ENOMEM, "pinned alloc", e);
+        return NULL;
+    }
+    return p;
+}
+
+void rfec_pinned_free(void* p)
+{
+    if (p)
+        (void)hipHostFree(p);
+}
+
+typedef struct {
+    uint8_t* d;
+    size_t db;
+    hipStream_t sm;
+} rv_ctx;
+static __thread rv_ctx t_rv;
+
+int rfec_host_recv_datagrams(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
+                             uint32_t stride, uint32_t capacity, uint32_t* max_ts, rfec_wire_rec* recs_out,
+                             rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out,
+                             rfec_rx_report* rep)
+{
+    const double t0 = now_us();
+    if (!max_ts || !n_out || !rep || (n && (!dgram || !dlen)))
+        return set_err(RFEC_EINVAL, "recv: bad argument", 0);
+    memset(rep, 0, sizeof(*rep));
+    *n_out = 0;
+    if (n == 0)
+        return RFEC_OK;
+    if (dstride < 64 || dstride > RFEC_WIRE_MAX_DSTRIDE || dstride % 16 || stride == 0 || stride % 16 ||
+        capacity > stride)
+        return set_err(RFEC_EINVAL, "recv: dstride must be a multiple of 16 in [64, 2048], stride >= capacity", 0);
+    hipError_t e;
+    if (!t_rv.sm && (e = hipStreamCreateWithFlags(&t_rv.sm, hipStreamNonBlocking)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "recv: stream", e);
+    const size_t o_dl = RX_ALIGN((size_t)n * dstride), o_rec = RX_ALIGN(o_dl + (size_t)n * 2);
+    const size_t o_pay = RX_ALIGN(o_rec + (size_t)n * sizeof(rfec_wire_rec));
+    const size_t need = RX_ALIGN(o_pay + (size_t)n * stride);
+    if (t_rv.db < need) {
+        if (t_rv.d)
+            (void)hipFree(t_rv.d);
+        t_rv.d = NULL;
+        t_rv.db = 0;
+        const size_t b = need + need / 4;
+        if ((e = hipMalloc((void**)&t_rv.d, b)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "recv: device staging", e);
+        t_rv.db = b;
+    }
+    uint8_t* D = t_rv.d;
+    double tt = now_us();
+    if ((e = hipMemcpyAsync(D, dgram, (size_t)n * dstride, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess ||
+        (e = hipMemcpyAsync(D + o_dl, dlen, (size_t)n * 2, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess ||
+        (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "recv: datagrams H2D", e);
+    const double h2d = now_us() - tt;
+    tt = now_us();
+    int ke = rfec_launch_wire_parse(n, dstride, D, (const uint16_t*)(D + o_dl), stride, capacity,
+                                    (rfec_wire_rec*)(D + o_rec), D + o_pay, max_dlen(dlen, n), t_rv.sm);
+    if (ke || (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "recv: parse", ke ? ke : (int)e);
+    const double parse = now_us() - tt;
+    if (recs_out) {
+        tt = now_us();
+        if ((e = hipMemcpyAsync(recs_out, D + o_rec, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost,
+                                t_rv.sm)) != hipSuccess ||
+            (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
+            return set_err(RFEC_EDEVICE, "recv: records D2H", e);
+        rep->d2h_us += now_us() - tt;
+    }
+    const double d2h_recs = rep->d2h_us;
+    const int rc = rfec_rx_recover(n, (const rfec_wire_rec*)(D + o_rec), D + o_pay, stride, capacity, max_ts, out,
+                                   out_payload, max_out, n_out, rep, t_rv.sm);
+    rep->h2d_us += h2d;
+    rep->kernel_us += parse;
+    rep->d2h_us += d2h_recs;
+    rep->total_us = now_us() - t0;
+    return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Receiver session: rx_sim kept across calls, records by id in a host store, */
+/* their payload rows by id in an HBM arena                                   */
+/* ------------------------------------------------------------------------ */
+/* a batch of the pipelined push: its parse in flight on the session's stream */
+typedef struct {
+    rfec_wire_rec* rec;  /* pinned, device-mapped records */
+    rfec_wire_rec* recd; /* rec as the device addresses it */
+    uint32_t reccap;
+    uint8_t* dg; /* device copy of pageable datagram slots + lengths */
+    size_t dgb;
+    hipEvent_t done;
+} rx_stage;
+
+struct rfec_rx_session {
+    rx_sim X;
+    rfec_wire_rec* store; /* X.R */
+    uint32_t nstore, storecap;
+    uint8_t* arena; /* [arows][stride]: rows [0, nstore) ingested, then the pending batch's */
+    uint32_t arows;
+    uint32_t stride, capacity;
+    /* pipelined push (rfec_rx_session_push_datagrams_async) */
+    hipStream_t sa;
+    rx_stage st[2];
+    uint32_t pend_n; /* rows of the pending batch (arena rows [nstore, nstore + pend_n)) */
+    int pend;        /* its stage, -1: none */
+};
+
+rfec_rx_session* rfec_rx_session_create(uint32_t stride, uint32_t capacity)
+{
+    if (stride == 0 || stride % 16 || capacity > stride) {
+        set_err(RFEC_EINVAL, "rx session: stride must be a multiple of 16 and >= capacity", 0);
+        return NULL;
+    }
+    rfec_rx_session* s = (rfec_rx_session*)calloc(1, sizeof(*s));
+    if (!s || rx_tables_init(&s->X, 1024)) {
+        if (s)
+            rx_sim_free(&s->X);
+        free(s);
+        set_err(RFEC_ENOMEM, "rx session: host tables", 0);
+        return NULL;
+    }
+    s->X.capacity = capacity;
+    s->stride = stride;
+    s->capacity = capacity;
+    s->pend = -1;
+    return s;
+}
+
+void rfec_rx_session_destroy(rfec_rx_session* s)
+{
+    if (!s)
+        return;
+    if (s->sa) /* a pending parse still writes into the arena */
+        (void)hipStreamSynchronize(s->sa);
+    for (int i = 0; i < 2; ++i) {
+        if (s->st[i].rec)
+            (void)hipHostFree(s->st[i].rec);
+        if (s->st[i].dg)
+            (void)hipFree(s->st[i].dg);
+        if (s->st[i].done)
+            (void)hipEventDestroy(s->st[i].done);
+    }
+    if (s->sa)
+        (void)hipStreamDestroy(s->sa);
+    rx_sim_free(&s->X);
+    free(s->store);
+    if (s->arena)
+        (void)hipFree(s->arena);
+    free(s);
+}
+
+/* Keeps only what the open state refers to: the flexes still registered (with
+ * their slot / line tables), the records of cached segments and of those
+ * flexes' members and parities (their rows gathered into a fresh arena with
+ * room for `extra` more), the headers of cached recovered segments.  The rows
+ * of a pending pipelined batch (parsed, not ingested) move along behind the
+ * kept ones. */
+static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
+{
+    const uint32_t tail = S->pend >= 0 ? S->pend_n : 0;
+    hipError_t e;
+    if (tail && (e = hipEventSynchronize(S->st[S->pend].done)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx session: pending parse", e);
+    rx_sim* X = &S->X;
+    int rc = RFEC_OK;
+    const uint32_t ng_live = X->flex_of.n;
+    rx_inst* NG = (rx_inst*)malloc(((size_t)ng_live + 1) * sizeof(rx_inst));
+    uint32_t nslot = 0, nline = 0;
+    for (uint32_t i = 0; i <= X->flex_of.mask; ++i)
+        if (X->flex_of.v[i]) {
+            const rx_inst* g = &X->G[X->flex_of.v[i] - 1];
+            if (g->shape != UINT32_MAX) {
+                nslot += g->count;
+                nline += X->S[g->shape].n_lines;
+            }
+        }
+    int32_t* nsrc = (int32_t*)malloc(((size_t)nslot + 1) * sizeof(int32_t));
+    rfec_hdr* nhdr = (rfec_hdr*)malloc(((size_t)nslot + 1) * sizeof(rfec_hdr));
+    int32_t* npar = (int32_t*)malloc(((size_t)nline + 1) * sizeof(int32_t));
+    uint32_t* rmap = (uint32_t*)calloc((size_t)S->nstore + 1, sizeof(uint32_t)); /* old record -> new + 1 */
+    uint32_t* hmap_ = (uint32_t*)calloc((size_t)X->nrh + 1, sizeof(uint32_t));  /* old rh -> new + 1 */
+    if (!NG || !nsrc || !nhdr || !npar || !rmap || !hmap_) {
+        rc = set_err(RFEC_ENOMEM, "rx session: compaction", 0);
+        goto done;
+    }
+    /* 1. live flexes, their tables; the records they refer to */
+    uint32_t ng = 0, ns = 0, nl = 0;
+    for (uint32_t i = 0; i <= X->flex_of.mask; ++i) {
+        if (!X->flex_of.v[i])
+            continue;
+        rx_inst g = X->G[X->flex_of.v[i] - 1];
+        if (g.shape != UINT32_MAX) {
+            const uint32_t nlines = X->S[g.shape].n_lines;
+            memcpy(nsrc + ns, X->slot_src + g.slot0, g.count * sizeof(int32_t));
+            memcpy(nhdr + ns, X->slot_hdr + g.slot0, g.count * sizeof(rfec_hdr));
+            memcpy(npar + nl, X->line_par + g.line0, nlines * sizeof(int32_t));
+            for (uint32_t q = 0; q < g.count; ++q)
+                if (nsrc[ns + q] >= 0)
+                    rmap[nsrc[ns + q]] = 1;
+            for (uint32_t q = 0; q < nlines; ++q)
+                if (npar[nl + q] >= 0)
+                    rmap[npar[nl + q]] = 1;
+            g.slot0 = ns;
+            g.line0 = nl;
+            ns += g.count;
+            nl += nlines;
+        }
+        NG[ng] = g;
+        X->flex_of.v[i] = ++ng;
+    }
+    /* 2. cached segments: arrived ones keep their record, recovered ones their header */
+    for (uint32_t i = 0; i <= X->cache.mask; ++i) {
+        const uint32_t c = X->cache.v[i];
+        if (!c)
+            continue;
+        if (c & 0x80000000u)
+            hmap_[c & 0x7FFFFFFFu] = 1;
+        else
+            rmap[c - 1] = 1;
+    }
+    /* 3. new ids, in arrival order */
+    uint32_t nr = 0, nh = 0;
+    for (uint32_t r = 0; r < S->nstore; ++r)
+        if (rmap[r])
+            rmap[r] = ++nr;
+    for (uint32_t h = 0; h < X->nrh; ++h)
+        if (hmap_[h])
+            hmap_[h] = ++nh;
+    for (uint32_t q = 0; q < ns; ++q)
+        if (nsrc[q] >= 0)
+            nsrc[q] = (int32_t)rmap[nsrc[q]] - 1;
+    for (uint32_t q = 0; q < nl; ++q)
+        if (npar[q] >= 0)
+            npar[q] = (int32_t)rmap[npar[q]] - 1;
+    for (uint32_t i = 0; i <= X->cache.mask; ++i) {
+        const uint32_t c = X->cache.v[i];
+        if (c)
+            X->cache.v[i] = (c & 0x80000000u) ? (0x80000000u | (hmap_[c & 0x7FFFFFFFu] - 1)) : rmap[c - 1];
+    }
+    /* 4. records (host) and rows (device) */
+    uint32_t* gmap = (uint32_t*)malloc(((size_t)nr + tail + 1) * sizeof(uint32_t)); /* new -> old */
+    const uint32_t arows = 2 * (nr + tail + extra) > 4096 ? 2 * (nr + tail + extra) : 4096;
+    uint8_t* arena = NULL;
+    if (!gmap) {
+        rc = set_err(RFEC_ENOMEM, "rx session: compaction", 0);
+        goto done;
+    }
+    for (uint32_t r = 0; r < S->nstore; ++r)
+        if (rmap[r]) {
+            gmap[rmap[r] - 1] = r;
+            S->store[rmap[r] - 1] = S->store[r]; /* rmap[r] - 1 <= r: in place, ascending */
+        }
+    for (uint32_t t = 0; t < tail; ++t)
+        gmap[nr + t] = S->nstore + t;
+    S->nstore = nr;
+    X->R = S->store;
+    for (uint32_t h = 0; h < X->nrh; ++h)
+        if (hmap_[h])
+            X->rh[hmap_[h] - 1] = X->rh[h];
+    X->nrh = nh;
+    if ((e = hipMalloc((void**)&arena, (size_t)arows * S->stride)) != hipSuccess) {
+        free(gmap);
+        rc = set_err(RFEC_ENOMEM, "rx session: arena", e);
+        goto done;
+    }
+    if (nr + tail) {
+        int32_t* dmap = NULL;
+        int ke = 0;
+        const uint32_t nm = nr + tail;
+        if ((e = hipMalloc((void**)&dmap, (size_t)nm * sizeof(int32_t))) != hipSuccess ||
+            (e = hipMemcpyAsync(dmap, gmap, (size_t)nm * sizeof(int32_t), hipMemcpyHostToDevice, sm)) != hipSuccess ||
+            (ke = rfec_launch_gather_rows(arena, S->arena, dmap, nm, S->stride, sm)) != 0 ||
+            (e = hipStreamSynchronize(sm)) != hipSuccess) {
+            if (dmap)
+                (void)hipFree(dmap);
+            (void)hipFree(arena);
+            free(gmap);
+            rc = set_err(RFEC_EDEVICE, "rx session: row compaction", ke ? ke : (int)e);
+            goto done;
+        }
+        (void)hipFree(dmap);
+    }
+    free(gmap);
+    if (S->arena)
+        (void)hipFree(S->arena);
+    S->arena = arena;
+    S->arows = arows;
+    /* 5. the group tables */
+    free(X->G);
+    free(X->slot_src);
+    free(X->slot_hdr);
+    free(X->line_par);
+    X->G = NG;
+    X->ng = X->gcap = ng;
+    X->slot_src = nsrc;
+    X->slot_hdr = nhdr;
+    X->nslot = X->slotcap = X->slothcap = ns;
+    X->line_par = npar;
+    X->nline = X->linecap = nl;
+    NG = NULL;
+    nsrc = npar = NULL;
+    nhdr = NULL;
+done:
+    free(NG);
+    free(nsrc);
+    free(nhdr);
+    free(npar);
+    free(rmap);
+    free(hmap_);
+    return rc;
+}
+
+/* room for n more arena rows and records: drop what the open state no longer
+ * refers to (and grow) */
+static int rx_session_room(rfec_rx_session* S, uint32_t n, hipStream_t sm)
+{
+    int rc;
+    const uint32_t tail = S->pend >= 0 ? S->pend_n : 0; /* a pending pipelined batch's rows */
+    if (S->nstore + tail + n > S->arows && (rc = rx_compact(S, n, sm)))
+        return rc;
+    if (S->nstore + tail + n > S->storecap) {
+        uint32_t c = S->storecap ? S->storecap : 4096;
+        while (c < S->nstore + tail + n)
+            c *= 2;
+        rfec_wire_rec* p = (rfec_wire_rec*)realloc(S->store, (size_t)c * sizeof(rfec_wire_rec));
+        if (!p)
+            return set_err(RFEC_ENOMEM, "rx session: record store", 0);
+        S->store = p;
+        S->storecap = c;
+    }
+    return RFEC_OK;
+}
+
+/* records already on the host (rh[0, n)), payload rows on the device at
+ * `payload`, or already in the arena's next n rows (payload NULL; the caller
+ * made the room) */
+static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const rfec_wire_rec* rh, const uint8_t* payload,
+                                  rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out,
+                                  rfec_rx_report* rep, hipStream_t sm)
+{
+    rx_sim* X = &S->X;
+    hipError_t e;
+    int rc;
+    if (payload && (rc = rx_session_room(S, n, sm)))
+        return rc;
+    X->R = S->store;
+    memcpy(S->store + S->nstore, rh, (size_t)n * sizeof(rfec_wire_rec));
+    if (payload) {
+        double tt = now_us();
+        if ((e = hipMemcpyAsync(S->arena + (size_t)S->nstore * S->stride, payload, (size_t)n * S->stride,
+                                hipMemcpyDeviceToDevice, sm)) != hipSuccess)
+            return set_err(RFEC_EDEVICE, "rx session: rows", e);
+        rep->kernel_us += now_us() - tt;
+    }
+    const uint32_t a0 = S->nstore;
+    S->nstore += n;
+    const double th = now_us();
+    X->nout = 0;
+    X->dropped = 0;
+    X->unmodelled = 0;
+    rx_run(X, a0, n);
+    if (X->oom)
+        return set_err(RFEC_ENOMEM, "rx session: host tables", 0);
+    rep->n_fec_dropped = X->dropped;
+    rep->host_us += now_us() - th;
+    rc = rx_device(X, S->arena, S->stride, S->capacity, 0, out, out_payload, max_out, n_out, rep, sm);
+    rep->n_unmodelled = X->unmodelled;
+    return rc;
+}
+
+int rfec_rx_session_push(rfec_rx_session* S, uint32_t n, const rfec_wire_rec* recs, const uint8_t* payload,
+                         rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out,
+                         rfec_rx_report* rep, void* stream)
+{
+    const double t0 = now_us();
+    if (!S || !n_out || !rep || (n && (!recs || !payload)) || (max_out && (!out || !out_payload)))
+        return set_err(RFEC_EINVAL, "rx session: bad argument", 0);
+    if (S->pend >= 0)
+        return set_err(RFEC_EINVAL, "rx session: a pipelined batch is pending (flush it: async push with n = 0)", 0);
+    memset(rep, 0, sizeof(*rep));
+    *n_out = 0;
+    if (n == 0)
+        return RFEC_OK;
+    hipStream_t sm = (hipStream_t)stream;
+    hipError_t e;
+    int rc;
+    if ((rc = rx_reserve(RX_ALIGN((size_t)n * sizeof(rfec_wire_rec)), 0, 0)))
+        return rc;
+    double tt = now_us();
+    if ((e = hipMemcpyAsync(t_rx.h, recs, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost, sm)) !=
+            hipSuccess ||
+        (e = hipStreamSynchronize(sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx session: records D2H", e);
+    rep->d2h_us += now_us() - tt;
+    rc = rx_session_push_staged(S, n, (const rfec_wire_rec*)t_rx.h, payload, out, out_payload, max_out, n_out, rep,
+                                sm);
+    rep->total_us = now_us() - t0;
+    return rc;
+}
+
+int rfec_rx_session_push_datagrams(rfec_rx_session* S, uint32_t n, uint32_t dstride, const uint8_t* dgram,
+                                   const uint16_t* dlen, rfec_wire_rec* recs_out, rfec_rx_seg* out,
+                                   uint8_t* out_payload, uint32_t max_out, uint32_t* n_out, rfec_rx_report* rep)
+{
+    const double t0 = now_us();
+    if (!S || !n_out || !rep || (n && (!dgram || !dlen)) || (max_out && (!out || !out_payload)))
+        return set_err(RFEC_EINVAL, "rx session: bad argument", 0);
+    if (S->pend >= 0)
+        return set_err(RFEC_EINVAL, "rx session: a pipelined batch is pending (flush it: async push with n = 0)", 0);
+    memset(rep, 0, sizeof(*rep));
+    *n_out = 0;
+    if (n == 0)
+        return RFEC_OK;
+    if (dstride < 64 || dstride > RFEC_WIRE_MAX_DSTRIDE || dstride % 16)
+        return set_err(RFEC_EINVAL, "rx session: dstride must be a multiple of 16 in [64, 2048]", 0);
+    hipError_t e;
+    if (!t_rv.sm && (e = hipStreamCreateWithFlags(&t_rv.sm, hipStreamNonBlocking)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "recv: stream", e);
+    const uint32_t stride = S->stride;
+    const size_t o_dl = RX_ALIGN((size_t)n * dstride), need = RX_ALIGN(o_dl + (size_t)n * 2);
+    if (t_rv.db < need) {
+        if (t_rv.d)
+            (void)hipFree(t_rv.d);
+        t_rv.d = NULL;
+        t_rv.db = 0;
+        const size_t b = need + need / 4;
+        if ((e = hipMalloc((void**)&t_rv.d, b)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "recv: device staging", e);
+        t_rv.db = b;
+    }
+    uint8_t* D = t_rv.d;
+    int rc;
+    if ((rc = rx_reserve(RX_ALIGN((size_t)n * sizeof(rfec_wire_rec)), 0, 0)))
+        return rc;
+    /* the payload rows are parsed straight into the arena's next n rows */
+    if ((rc = rx_session_room(S, n, t_rv.sm)))
+        return rc;
+    double tt = now_us();
+    /* datagrams in pinned memory (the UDP batch slots) are read by the parse
+     * itself; pageable ones are copied first.  The records go straight to the
+     * pinned staging area. */
+    const uint8_t* dg = host_mapped(dgram);
+    const uint8_t* dl = host_mapped(dlen);
+    if (!dg || !dl) {
+        if ((e = hipMemcpyAsync(D, dgram, (size_t)n * dstride, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess ||
+            (e = hipMemcpyAsync(D + o_dl, dlen, (size_t)n * 2, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess)
+            return set_err(RFEC_EDEVICE, "recv: datagrams H2D", e);
+        dg = D;
+        dl = D + o_dl;
+    }
+    const double h2d_issue = now_us() - tt;
+    int ke = rfec_launch_wire_parse(n, dstride, dg, (const uint16_t*)dl, stride, S->capacity,
+                                    (rfec_wire_rec*)t_rx.hd, S->arena + (size_t)S->nstore * stride,
+                                    max_dlen(dlen, n), t_rv.sm);
+    if (ke || (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "recv: parse", ke ? ke : (int)e);
+    const double staged = now_us() - tt;
+    if (recs_out)
+        memcpy(recs_out, t_rx.h, (size_t)n * sizeof(rfec_wire_rec));
+    rc = rx_session_push_staged(S, n, (const rfec_wire_rec*)t_rx.h, NULL, out, out_payload, max_out, n_out, rep,
+                                t_rv.sm);
+    rep->h2d_us += h2d_issue;
+    rep->kernel_us += staged - h2d_issue; /* the H2D completes inside this interval too */
+    rep->total_us = now_us() - t0;
+    return rc;
+}
+
+/* The pipelined push: this call starts batch i (H2D if pageable, parse into
+ * the arena's rows after the pending batch's, records into its stage's mapped
+ * area, on the session's own stream) and then ingests batch i-1 (control
+ * plane, peel on the thread's stream) while the device parses batch i. */
+static int rx_stage_reserve(rx_stage* st, uint32_t n, size_t dg_bytes)
+{
+    hipError_t e;
+    if (!st->done && (e = hipEventCreateWithFlags(&st->done, hipEventDisableTiming)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx session: event", e);
+    if (st->reccap < n) {
+        const uint32_t c = n + n / 4 + 64;
+        void* h = NULL;
+        void* d = NULL;
+        if ((e = hipHostMalloc(&h, (size_t)c * sizeof(rfec_wire_rec), hipHostMallocMapped)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "rx session: record stage", e);
+        if ((e = hipHostGetDevicePointer(&d, h, 0)) != hipSuccess) {
+            (void)hipHostFree(h);
+            return set_err(RFEC_EDEVICE, "rx session: record stage device view", e);
+        }
+        if (st->rec)
+            (void)hipHostFree(st->rec);
+        st->rec = (rfec_wire_rec*)h;
+        st->recd = (rfec_wire_rec*)d;
+        st->reccap = c;
+    }
+    if (dg_bytes > st->dgb) {
+        if (st->dg)
+            (void)hipFree(st->dg);
+        st->dg = NULL;
+        st->dgb = 0;
+        const size_t b = dg_bytes + dg_bytes / 4;
+        if ((e = hipMalloc((void**)&st->dg, b)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "rx session: datagram stage", e);
+        st->dgb = b;
+    }
+    return RFEC_OK;
+}
+
+int rfec_rx_session_push_datagrams_async(rfec_rx_session* S, uint32_t n, uint32_t dstride, const uint8_t* dgram,
+                                         const uint16_t* dlen, rfec_wire_rec* recs_out, rfec_rx_seg* out,
+                                         uint8_t* out_payload, uint32_t max_out, uint32_t* n_out, rfec_rx_report* rep)
+{
+    const double t0 = now_us();
+    if (!S || !n_out || !rep || (n && (!dgram || !dlen)) || (max_out && (!out || !out_payload)))
+        return set_err(RFEC_EINVAL, "rx session: bad argument", 0);
+    memset(rep, 0, sizeof(*rep));
+    *n_out = 0;
+    if (n && (dstride < 64 || dstride > RFEC_WIRE_MAX_DSTRIDE || dstride % 16))
+        return set_err(RFEC_EINVAL, "rx session: dstride must be a multiple of 16 in [64, 2048]", 0);
+    hipError_t e;
+    int rc;
+    if (!t_rv.sm && (e = hipStreamCreateWithFlags(&t_rv.sm, hipStreamNonBlocking)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "recv: stream", e);
+    if (!S->sa && (e = hipStreamCreateWithFlags(&S->sa, hipStreamNonBlocking)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx session: stream", e);
+    const int prev = S->pend;
+    const uint32_t p = prev >= 0 ? S->pend_n : 0;
+    int cur = -1;
+    if (n) {
+        /* 1. start batch i behind the pending one's rows */
+        cur = prev == 0 ? 1 : 0;
+        rx_stage* st = &S->st[cur];
+        const size_t o_dl = RX_ALIGN((size_t)n * dstride);
+        if ((rc = rx_session_room(S, n, t_rv.sm)) || (rc = rx_stage_reserve(st, n, o_dl + (size_t)n * 2)))
+            return rc;
+        double tt = now_us();
+        const uint8_t* dg = host_mapped(dgram);
+        const uint8_t* dl = host_mapped(dlen);
+        if (!dg || !dl) {
+            if ((e = hipMemcpyAsync(st->dg, dgram, (size_t)n * dstride, hipMemcpyHostToDevice, S->sa)) != hipSuccess ||
+                (e = hipMemcpyAsync(st->dg + o_dl, dlen, (size_t)n * 2, hipMemcpyHostToDevice, S->sa)) != hipSuccess)
+                return set_err(RFEC_EDEVICE, "rx session: datagrams H2D", e);
+            dg = st->dg;
+            dl = st->dg + o_dl;
+        }
+        rep->h2d_us += now_us() - tt;
+        const int ke = rfec_launch_wire_parse(n, dstride, dg, (const uint16_t*)dl, S->stride, S->capacity, st->recd,
+                                              S->arena + (size_t)(S->nstore + p) * S->stride, max_dlen(dlen, n),
+                                              S->sa);
+        if (ke || (e = hipEventRecord(st->done, S->sa)) != hipSuccess)
+            return set_err(RFEC_EDEVICE, "rx session: parse", ke ? ke : (int)e);
+    }
+    /* 2. ingest batch i-1 while the device parses batch i */
+    if (prev >= 0) {
+        rx_stage* ps = &S->st[prev];
+        double tt = now_us();
+        if ((e = hipEventSynchronize(ps->done)) != hipSuccess)
+            return set_err(RFEC_EDEVICE, "rx session: parse", e);
+        rep->kernel_us += now_us() - tt;
+        if (recs_out)
+            memcpy(recs_out, ps->rec, (size_t)p * sizeof(rfec_wire_rec));
+        S->pend = -1; /* its rows are the arena's next p rows now */
+        rc = rx_session_push_staged(S, p, ps->rec, NULL, out, out_payload, max_out, n_out, rep, t_rv.sm);
+        if (rc) {
+            S->pend = cur; /* batch i stays pending behind whatever was ingested */
+            S->pend_n = n;
+            return rc;
+        }
+    }
+    S->pend = cur;
+    S->pend_n = n;
+    rep->total_us = now_us() - t0;
+    return RFEC_OK;
+}
+
+int rfec_rx_session_evict(rfec_rx_session* S, void* stream)
+{
+    if (!S)
+        return set_err(RFEC_EINVAL, "rx session: NULL", 0);
+    rx_evict(&S->X);
+    if (S->X.oom)
+        return set_err(RFEC_ENOMEM, "rx session: evict", 0);
+    return rx_compact(S, 0, (hipStream_t)stream);
+}
+
+int rfec_rx_session_get_info(const rfec_rx_session* S, rfec_rx_session_info* info)
+{
+    if (!S || !info)
+        return set_err(RFEC_EINVAL, "rx session: NULL", 0);
+    memset(info, 0, sizeof(*info));
+    info->max_ts = S->X.max_ts;
+    info->open_flexes = S->X.flex_of.n;
+    info->cached_segments = S->X.cache.n;
+    info->records_held = S->nstore;
+    info->rows_held = S->arows;
+    info->pending = S->pend >= 0 ? S->pend_n : 0;
+    return RFEC_OK;
+}

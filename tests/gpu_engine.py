@@ -107,9 +107,10 @@ class GpuEngine:
 class GpuWire:
     """The wire codec (rfec_wire_*) on numpy inputs."""
 
-    def __init__(self, video_size=1000, device="cuda:0"):
+    def __init__(self, video_size=1000, device="cuda:0", tuning=0):
         self.lib = native(video_size)
         self.device = torch.device(device)
+        self.tuning = tuning  # RFEC_TUNE_WAVE_PARSE: the wave-per-datagram parse
 
     def _run(self, fn, *args):
         fn(*args, torch.cuda.current_stream(self.device).cuda_stream)
@@ -144,7 +145,11 @@ class GpuWire:
         d_l = _dev(np.ascontiguousarray(dlen, np.uint16), self.device)
         d_r = torch.full((N * 64,), 0xEE, dtype=torch.uint8, device=self.device)
         d_p = torch.full((N * stride,), 0xEE, dtype=torch.uint8, device=self.device)
-        self._run(self.lib.wire_parse, N, dstride, d_g.data_ptr(), d_l.data_ptr(), stride, capacity, d_r.data_ptr(),
-                  d_p.data_ptr())
+        self.lib.set_tuning(self.tuning)
+        try:
+            self._run(self.lib.wire_parse, N, dstride, d_g.data_ptr(), d_l.data_ptr(), stride, capacity,
+                      d_r.data_ptr(), d_p.data_ptr())
+        finally:
+            self.lib.set_tuning(0)
         from razor_amd.fec import WIRE_REC_DTYPE
         return _host(d_r, WIRE_REC_DTYPE, (N,)), _host(d_p, np.uint8, (N, stride))

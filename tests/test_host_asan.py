@@ -1,6 +1,8 @@
 """Host control plane under AddressSanitizer + UBSan, on the CPU.
 
-rfec_host.c is compiled together with tests/host_stub/stub_hip.c (a
+The C host layer (razor_amd/build.py HOST_SRC: rfec_host.c, rfec_dropin.c,
+rfec_hostmem.c, rfec_sender.c, rfec_rx.c) is compiled together with
+tests/host_stub/stub_hip.c (a
 host-memory stand-in for the HIP runtime and the kernel launches; test
 infrastructure only, it does no FEC arithmetic) and driven through the same
 ctypes view the GPU tests use.  What is checked here is the host side alone:
@@ -28,6 +30,9 @@ from pathlib import Path
 import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+from razor_amd.build import HOST_SRC  # noqa: E402  (the C host layer's translation units)
+
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 
 
@@ -47,7 +52,7 @@ def stub_lib(tmp_path_factory):
     inc = [f"-I{ROCM / 'include'}", f"-I{ROOT / 'include'}", f"-I{ROOT / 'razor_amd' / 'csrc'}"]
     cmd = ["gcc", "-std=c99", "-O1", "-g", "-fPIC", "-shared", "-fno-omit-frame-pointer",
            "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-DSIM_VIDEO_SIZE=1000",
-           "-D__HIP_PLATFORM_AMD__", *inc, str(ROOT / "razor_amd" / "csrc" / "rfec_host.c"),
+           "-D__HIP_PLATFORM_AMD__", *inc, *(str(ROOT / "razor_amd" / "csrc" / f) for f in HOST_SRC),
            str(ROOT / "razor_amd" / "csrc" / "rfec_net.c"), str(ROOT / "tests" / "host_stub" / "stub_hip.c"), "-o", str(out), "-lpthread", "-lm"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr

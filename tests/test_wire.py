@@ -79,6 +79,19 @@ def gwire():
     return GpuWire()
 
 
+RFEC_TUNE_WAVE_PARSE = 1 << 3
+
+
+@pytest.fixture(params=["quarter", "wave"])
+def pwire(request):
+    """The parse both ways: the quarter-wave kernel (default) and the
+    wave-per-datagram one (RFEC_TUNE_WAVE_PARSE), the cross-check."""
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the -m gpu suite must run on an MI355X")
+    from gpu_engine import GpuWire
+    return GpuWire(tuning=0 if request.param == "quarter" else RFEC_TUNE_WAVE_PARSE)
+
+
 @pytest.mark.gpu
 def test_wire_frame_fec_gpu(gwire):
     wc.check_frame_fec(gwire)
@@ -90,12 +103,13 @@ def test_wire_frame_seg_gpu(gwire):
 
 
 @pytest.mark.gpu
-def test_wire_parse_gpu(gwire):
-    wc.check_parse(gwire)
+def test_wire_parse_gpu(pwire):
+    wc.check_parse(pwire)
 
 
 @pytest.mark.gpu
-def test_wire_short_datagram_gpu(gwire):
+def test_wire_short_datagram_gpu(pwire):
+    gwire = pwire
     dgram = np.full((5, 64), 0xAB, np.uint8)
     recs, pay = gwire.parse(dgram, np.array([0, 1, 2, 3, 4], np.uint16), wc.STRIDE, wc.CAP)
     assert (recs["status"][:4] == -1).all() and not pay.any()
@@ -105,6 +119,60 @@ def test_wire_short_datagram_gpu(gwire):
     recs, _ = gwire.parse(d, np.array([4], np.uint16), wc.STRIDE, wc.CAP)
     # CRC accepted; ver/mid then read the trailer bytes themselves (0x0e, 0x3d): mid out of range
     assert recs["status"][0] == -2 and recs["ver"][0] == 0x0E and recs["mid"][0] == 0x3D
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("capacity,stride,dstride,N", [(1200, 1200, 1248, 4097), (1200, 1216, 1264, 4099),
+                                                       (1000, 1008, 1056, 3001), (230, 240, 288, 2051),
+                                                       (1200, 1280, 1280, 2050), (1200, 1200, 1504, 2049),
+                                                       (1300, 1312, 1360, 1025)])
+def test_wire_parse_mixed_gpu(pwire, oracle1000, capacity, stride, dstride, N):
+    """The parse against the oracle on batches that mix SIM_SEG (every header
+    width: data at bytes 26-32) and SIM_FEC (data at 45) datagrams in random
+    order -- a quarter-wave quad holds datagrams with different data offsets
+    -- with flipped bytes (CRC mismatches: record EBADCRC, slot zero), lengths
+    cut short or past the slot, data sizes that overrun the datagram, control
+    messages and bad message ids; slots of 1,248-1,504 bytes (wider than 1,280:
+    the datagrams still fit, the quarter-wave parse reads the first 1,280),
+    payload slots up to 1,280 bytes, N not a multiple of 4."""
+    rng = np.random.default_rng(capacity + stride * 3 + dstride * 7 + N)
+    frames, lens = [], []
+    for seg in (True, False):
+        data, hdr, sizes, stamps = wc.random_batch(rng, N, stride, capacity, seg=seg)
+        over = 36 if seg else 49
+        ds = max(dstride, (capacity + over + 15) // 16 * 16)
+        if seg:
+            g, gl = oracle1000.frame_seg_batch(data, hdr, stamps, capacity, ds)
+        else:
+            g, gl = oracle1000.frame_fec_batch(data, hdr, sizes, None, stamps, capacity, ds)
+        frames.append(g[:, :dstride] if ds > dstride else np.pad(g, ((0, 0), (0, dstride - ds))))
+        lens.append(np.minimum(gl, dstride).astype(np.uint16))
+    dgram = np.concatenate(frames)
+    dlen = np.concatenate(lens)
+    pick = rng.permutation(len(dgram))[:N]
+    dgram, dlen = dgram[pick].copy(), dlen[pick].copy()
+    n = len(dgram)
+    flip = rng.random(n) < 0.08  # a flipped byte inside the message
+    for i in np.nonzero(flip & (dlen > 8))[0]:
+        dgram[i, rng.integers(0, int(dlen[i]))] ^= 1 << int(rng.integers(8))
+    cut = rng.random(n) < 0.04  # cut short (the trailer then sits elsewhere: a CRC mismatch)
+    dlen[cut] = rng.integers(0, 60, int(cut.sum()))
+    over = rng.random(n) < 0.02  # longer than the slot
+    dlen[over] = dstride + 1 + rng.integers(0, 100, int(over.sum()))
+    mid = rng.random(n) < 0.03  # another message id, CRC recomputed (a control message or a bad id)
+    for i in np.nonzero(mid & (dlen >= 10) & (dlen <= dstride))[0]:
+        L = int(dlen[i])
+        dgram[i, 1] = rng.choice([0x10, 0x12, 0x1D, 0x05, 0x40])
+        crc = oracle1000.crc32(dgram[i, :L - 4].tobytes())
+        dgram[i, L - 4:L] = np.frombuffer(crc.to_bytes(4, "big"), np.uint8)
+    recs, pay = pwire.parse(dgram, dlen, stride, capacity)
+    orecs, opay = oracle1000.parse_batch(dgram, dlen, stride, capacity)
+    bad = np.nonzero((recs.view(np.uint8).reshape(n, 64) != orecs.view(np.uint8).reshape(n, 64)).any(1))[0]
+    assert len(bad) == 0, (bad[:8], recs[bad[:2]], orecs[bad[:2]])
+    bad = np.nonzero((pay != opay).any(1))[0]
+    assert len(bad) == 0, (bad[:8], recs[bad[:4]]["status"], recs[bad[:4]]["data_size"])
+    st = set(int(x) for x in recs["status"])
+    assert {0, -1} <= st and (recs["status"] == 0).sum() > n // 2
 
 
 @pytest.mark.gpu

@@ -63,9 +63,12 @@ def main():
     ap.add_argument("--lib", default="", help="another build of the library (A/B)")
     ap.add_argument("--dstride", type=int, default=0, help="datagram slot width for both kinds (e.g. 1504: 1500-B receive slots, 32-byte lanes)")
     ap.add_argument("--out", default="")
+    ap.add_argument("--tuning", type=int, default=0, help="rfec_set_tuning bits (8: the wave-per-datagram parse)")
+    ap.add_argument("--only", default="", help="comma list of kernels to time (frame_fec,frame_seg,parse_fec,parse_seg)")
     args = ap.parse_args()
     G, k, n, S = args.groups, 10, 3, 1200
     lib = Native(1200, args.lib) if args.lib else native(1200)
+    lib.set_tuning(args.tuning)
     dev = torch.device("cuda:0")
     st = torch.cuda.Stream(dev)
     sp = st.cuda_stream
@@ -133,6 +136,8 @@ def main():
                "parse_seg": NS * ((lens + 2) + (64 + S))}
         for name, f in (("frame_fec", frame_fec), ("frame_seg", frame_seg), ("parse_fec", parse_f),
                         ("parse_seg", parse_s)):
+            if args.only and name not in args.only.split(","):
+                continue
             med, mean = timed(f, args.reps, st, lib)
             res[name] = {"median_us": round(med * 1e6, 2), "mean_us": round(mean * 1e6, 2),
                          "algorithmic_bytes": alg[name], "GBps": round(alg[name] / med / 1e9, 1),
