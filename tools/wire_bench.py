@@ -63,7 +63,7 @@ def main():
     ap.add_argument("--lib", default="", help="another build of the library (A/B)")
     ap.add_argument("--dstride", type=int, default=0, help="datagram slot width for both kinds (e.g. 1504: 1500-B receive slots, 32-byte lanes)")
     ap.add_argument("--out", default="")
-    ap.add_argument("--tuning", type=int, default=0, help="rfec_set_tuning bits (8: the wave-per-datagram parse)")
+    ap.add_argument("--tuning", type=int, default=0, help="rfec_set_tuning bits")
     ap.add_argument("--only", default="", help="comma list of kernels to time (frame_fec,frame_seg,parse_fec,parse_seg)")
     args = ap.parse_args()
     G, k, n, S = args.groups, 10, 3, 1200
