@@ -230,9 +230,16 @@ int rfec_recover_batch_out(const rfec_plan* plan, uint32_t groups, uint32_t stri
  * flex_fec_generate would fail gets fec_data_size = 0xFFFF and no payload.
  * `timing` (may be NULL) receives the per-stage wall times in microseconds.
  * Staging is per calling thread and grows on demand.
+ *
+ * Zero copy: when every segs / fecs pointer lies inside one block from
+ * rfec_pinned_alloc (and RFEC_HOST_ZEROCOPY is not "0"), no host gather or
+ * scatter runs -- the device reads the sim_segment_t and writes the sim_fec_t
+ * through the block's device mapping over PCIe, and only the pointer tables
+ * are staged (timing->zero_copy = 1; gather_us is then the table build).
  */
 typedef struct {
     double gather_us, h2d_us, kernel_us, d2h_us, scatter_us, total_us;
+    uint32_t zero_copy, reserved;
 } rfec_host_timing;
 
 int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,

@@ -27,7 +27,7 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("RFEC_OFFLOAD_ARCH", "gfx950")
 
 HIP_SRC = [CSRC / "rfec_kernels.hip", CSRC / "rfec_probe.hip", CSRC / "rfec_wire.hip", CSRC / "rfec_fill.hip",
-           CSRC / "rfec_service.hip"]
+           CSRC / "rfec_service.hip", CSRC / "rfec_hostio.hip"]
 # built once per SIM_VIDEO_SIZE: the C host layer, by concern (rfec_host.c: errors, planner, batched device
 # and wire API; rfec_dropin.c: drop-in symbols + resident service; rfec_hostmem.c: host-memory batches;
 # rfec_sender.c: sender staging; rfec_rx.c: receiver ingestion and sessions), and the flex drop-in

@@ -87,6 +87,108 @@ static int hb_reserve(di_ctx* c, size_t host_slot, size_t dev_slot)
     return RFEC_OK;
 }
 
+#define RFEC_HR_SLOT_BYTES ((size_t)640 << 20)
+
+/* ---- pinned blocks the device maps ---------------------------------------
+ * rfec_pinned_alloc registers each block (host range and the device address
+ * of its first byte), so that the host-memory batch paths can tell that every
+ * struct of a call lies in memory the device reads and writes itself: then
+ * the zero-copy form runs (rfec_hostio.hip kernels read the callers' structs
+ * over PCIe and write the results into theirs; no host gather / scatter, no
+ * bulk copies).  Any struct outside a registered block keeps the staged form. */
+typedef struct {
+    uintptr_t lo, hi;
+    intptr_t delta; /* device address - host address */
+} pin_block;
+static pin_block* g_pin;
+static size_t g_npin, g_pincap;
+static pthread_mutex_t g_pin_mu = PTHREAD_MUTEX_INITIALIZER;
+
+void* rfec_pinned_alloc(size_t bytes)
+{
+    void* p = NULL;
+    void* d = NULL;
+    hipError_t e;
+    if (bytes == 0)
+        return NULL;
+    if ((e = hipHostMalloc(&p, bytes, hipHostMallocDefault)) != hipSuccess) {
+        set_err(RFEC_ENOMEM, "pinned alloc", e);
+        return NULL;
+    }
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess || !d) {
+        (void)hipGetLastError();
+        return p; /* pinned, but not registered for the zero-copy paths */
+    }
+    pthread_mutex_lock(&g_pin_mu);
+    if (g_npin == g_pincap) {
+        const size_t cap = g_pincap ? 2 * g_pincap : 16;
+        pin_block* nb = (pin_block*)realloc(g_pin, cap * sizeof(pin_block));
+        if (nb) {
+            g_pin = nb;
+            g_pincap = cap;
+        }
+    }
+    if (g_npin < g_pincap)
+        g_pin[g_npin++] = (pin_block){(uintptr_t)p, (uintptr_t)p + bytes, (intptr_t)((uintptr_t)d - (uintptr_t)p)};
+    pthread_mutex_unlock(&g_pin_mu);
+    return p;
+}
+
+void rfec_pinned_free(void* p)
+{
+    if (!p)
+        return;
+    pthread_mutex_lock(&g_pin_mu);
+    for (size_t i = 0; i < g_npin; ++i)
+        if (g_pin[i].lo == (uintptr_t)p) {
+            g_pin[i] = g_pin[--g_npin];
+            break;
+        }
+    pthread_mutex_unlock(&g_pin_mu);
+    (void)hipHostFree(p);
+}
+
+/* 1 when every non-NULL pointer of ptrs[0, n) addresses `obj` bytes inside one
+ * registered block (its device offset in *delta); 1 with delta 0 when all are
+ * NULL */
+static int pinned_span(const void* const* ptrs, size_t n, size_t obj, intptr_t* delta)
+{
+    uintptr_t lo = UINTPTR_MAX, hi = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const uintptr_t a = (uintptr_t)ptrs[i];
+        if (!a)
+            continue;
+        lo = a < lo ? a : lo;
+        hi = a > hi ? a : hi;
+    }
+    *delta = 0;
+    if (lo == UINTPTR_MAX)
+        return 1;
+    hi += obj;
+    int ok = 0;
+    pthread_mutex_lock(&g_pin_mu);
+    for (size_t i = 0; i < g_npin && !ok; ++i)
+        if (lo >= g_pin[i].lo && hi <= g_pin[i].hi) {
+            ok = 1;
+            *delta = g_pin[i].delta;
+        }
+    pthread_mutex_unlock(&g_pin_mu);
+    return ok;
+}
+
+static int zerocopy_enabled(void)
+{
+    const char* v = getenv("RFEC_HOST_ZEROCOPY");
+    return !(v && v[0] == '0');
+}
+
+/* device addresses of structs (0 for NULL) into a pinned table */
+static void dev_ptrs(uint64_t* out, const void* const* ptrs, size_t n, intptr_t delta)
+{
+    for (size_t i = 0; i < n; ++i)
+        out[i] = ptrs[i] ? (uint64_t)((uintptr_t)ptrs[i] + (uintptr_t)delta) : 0u;
+}
+
 /* the sender's fec_id sequence: +1 per group, 0 skipped (flex_fec_sender.c:241-243) */
 static uint16_t fec_id_at(uint16_t id0, uint32_t g)
 {
@@ -150,6 +252,126 @@ static void hb_scatter(void* arg, size_t lo, size_t hi)
     }
 }
 
+/* The zero-copy encode: per chunk on slot s's stream, the pointer tables
+ * H2D, then on the device the segments gathered from the callers' structs,
+ * the encode, the parities scattered into the callers' sim_fec_t.  Chunks
+ * alternate between two streams, so one chunk's PCIe reads overlap the
+ * previous one's PCIe writes. */
+typedef struct {
+    size_t sp, fp, shards, hdr, parity, meta, fsize, status, total, host_total;
+} hz_layout;
+
+static hz_layout hz_offsets(uint32_t G, uint32_t k, uint32_t n)
+{
+    hz_layout L;
+    size_t o = 0;
+#define HZ_TAKE(field, bytes)                           \
+    do {                                                \
+        L.field = o;                                    \
+        o = (o + (size_t)(bytes) + 255) & ~(size_t)255; \
+    } while (0)
+    HZ_TAKE(sp, (size_t)G * k * 8);
+    HZ_TAKE(fp, (size_t)G * n * 8);
+    L.host_total = o; /* the pointer tables: pinned, copied H2D */
+    HZ_TAKE(shards, (size_t)G * k * DI_STRIDE);
+    HZ_TAKE(hdr, (size_t)G * k * sizeof(rfec_hdr));
+    HZ_TAKE(parity, (size_t)G * n * DI_STRIDE);
+    HZ_TAKE(meta, (size_t)G * n * sizeof(rfec_hdr));
+    HZ_TAKE(fsize, (size_t)G * n * sizeof(uint16_t));
+    HZ_TAKE(status, (size_t)G * n);
+#undef HZ_TAKE
+    L.total = o;
+    return L;
+}
+
+static int zc_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,
+                            sim_fec_t* const* fecs, uint16_t fec_id0, rfec_host_timing* timing, intptr_t ds,
+                            intptr_t df)
+{
+    di_ctx* c = di_get();
+    if (!c)
+        return RFEC_EDEVICE;
+    const uint32_t k = plan->k, n = plan->n_lines;
+    uint32_t chunk = (groups + 7) / 8;
+    chunk = chunk < 2048 ? 2048 : chunk;
+    chunk = chunk > groups ? groups : chunk;
+    const uint32_t nch = (groups + chunk - 1) / chunk;
+    const hz_layout L = hz_offsets(chunk, k, n);
+    int rc = hb_reserve(c, L.host_total, L.total);
+    if (rc)
+        return rc;
+    double tab_us = 0, h2d_us = 0, kernel_us = 0, d2h_us = 0;
+    const double t0 = now_us();
+    for (uint32_t it = 0; it < nch + 2 && rc == RFEC_OK; ++it) {
+        if (it >= 2) { /* retire chunk it - 2: its slot may be refilled */
+            const uint32_t s = (it - 2) & 1;
+            const hipError_t e = hipEventSynchronize(c->ev[s][3]);
+            if (e != hipSuccess) {
+                rc = set_err(RFEC_EDEVICE, "zero-copy encode wait", e);
+                break;
+            }
+            float a = 0, b = 0, d = 0;
+            (void)hipEventElapsedTime(&a, c->ev[s][0], c->ev[s][1]);
+            (void)hipEventElapsedTime(&b, c->ev[s][1], c->ev[s][2]);
+            (void)hipEventElapsedTime(&d, c->ev[s][2], c->ev[s][3]);
+            h2d_us += a * 1e3;
+            kernel_us += b * 1e3;
+            d2h_us += d * 1e3;
+        }
+        if (it >= nch)
+            continue;
+        const uint32_t s = it & 1, g0 = it * chunk, ng = it == nch - 1 ? groups - g0 : chunk;
+        uint8_t* h = c->bh + (size_t)s * L.host_total;
+        uint8_t* dv = c->bd + (size_t)s * L.total;
+        hipStream_t st = c->bstream[s];
+        const double tt = now_us();
+        dev_ptrs((uint64_t*)(h + L.sp), (const void* const*)(segs + (size_t)g0 * k), (size_t)ng * k, ds);
+        dev_ptrs((uint64_t*)(h + L.fp), (const void* const*)(fecs + (size_t)g0 * n), (size_t)ng * n, df);
+        tab_us += now_us() - tt;
+        hipError_t e;
+        int ke = 0;
+        if ((e = hipEventRecord(c->ev[s][0], st)) != hipSuccess ||
+            (e = hipMemcpyAsync(dv, h, L.host_total, hipMemcpyHostToDevice, st)) != hipSuccess ||
+            (e = hipEventRecord(c->ev[s][1], st)) != hipSuccess) {
+            rc = set_err(RFEC_EDEVICE, "zero-copy encode H2D", e);
+            break;
+        }
+        ke = rfec_launch_host_gather(0, (const uint64_t*)(dv + L.sp), ng * k, DI_STRIDE, dv + L.shards,
+                                     (rfec_hdr*)(dv + L.hdr), NULL, NULL, SIM_VIDEO_SIZE, st);
+        if (!ke)
+            ke = rfec_launch_encode(plan, ng, DI_STRIDE, SIM_VIDEO_SIZE, dv + L.shards, (const rfec_hdr*)(dv + L.hdr),
+                                    dv + L.parity, (rfec_hdr*)(dv + L.meta), (uint16_t*)(dv + L.fsize),
+                                    (int8_t*)(dv + L.status), st, g_tuning);
+        if (!ke && (e = hipEventRecord(c->ev[s][2], st)) != hipSuccess)
+            ke = (int)e;
+        if (!ke)
+            ke = rfec_launch_host_scatter_fec((const uint64_t*)(dv + L.fp), ng, plan, DI_STRIDE, dv + L.parity,
+                                              (const rfec_hdr*)(dv + L.meta), (const uint16_t*)(dv + L.fsize),
+                                              (const int8_t*)(dv + L.status), (const rfec_hdr*)(dv + L.hdr), fec_id0,
+                                              g0, SIM_VIDEO_SIZE, st);
+        if (ke || (e = hipEventRecord(c->ev[s][3], st)) != hipSuccess) {
+            rc = set_err(RFEC_EDEVICE, "zero-copy encode launch", ke ? ke : (int)e);
+            break;
+        }
+    }
+    if (rc != RFEC_OK) {
+        (void)hipStreamSynchronize(c->bstream[0]);
+        (void)hipStreamSynchronize(c->bstream[1]);
+        return rc;
+    }
+    if (timing) { /* gather: the host's pointer tables; kernel: device gather + encode; d2h: the scatter */
+        timing->gather_us = tab_us;
+        timing->h2d_us = h2d_us;
+        timing->kernel_us = kernel_us;
+        timing->d2h_us = d2h_us;
+        timing->scatter_us = 0;
+        timing->total_us = now_us() - t0;
+        timing->zero_copy = 1;
+        timing->reserved = 0;
+    }
+    return RFEC_OK;
+}
+
 /*
  * Chunked and double-buffered: while the GPU copies / encodes / copies back
  * chunk c on slot c%2's stream, the CPU threads scatter chunk c-1's parities
@@ -168,6 +390,17 @@ int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
         return set_err(RFEC_EINVAL, "NULL segs / fecs", 0);
     if ((rc = check_geometry(groups, DI_STRIDE, SIM_VIDEO_SIZE, plan->k)))
         return rc;
+    intptr_t ds = 0, df = 0;
+    if (zerocopy_enabled() && pinned_span((const void* const*)segs, (size_t)groups * plan->k, sizeof(sim_segment_t), &ds) &&
+        pinned_span((const void* const*)fecs, (size_t)groups * plan->n_lines, sizeof(sim_fec_t), &df)) {
+        for (size_t i = 0; i < (size_t)groups * plan->k; ++i)
+            if (!segs[i])
+                return set_err(RFEC_EINVAL, "NULL segment", 0);
+        for (size_t i = 0; i < (size_t)groups * plan->n_lines; ++i)
+            if (!fecs[i])
+                return set_err(RFEC_EINVAL, "NULL parity", 0);
+        return zc_encode_groups(plan, groups, segs, fecs, fec_id0, timing, ds, df);
+    }
     di_ctx* c = di_get();
     if (!c)
         return RFEC_EDEVICE;
@@ -253,6 +486,8 @@ int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
         timing->d2h_us = d2h_us;
         timing->scatter_us = scatter_us;
         timing->total_us = now_us() - t0;
+        timing->zero_copy = 0;
+        timing->reserved = 0;
     }
     return RFEC_OK;
 }
@@ -273,7 +508,6 @@ typedef struct {
     size_t shards, parity, ws, total;                            /* device only: dense slots, workspace */
 } hr_layout;
 
-#define RFEC_HR_SLOT_BYTES ((size_t)640 << 20)
 
 static hr_layout hr_offsets(const rfec_plan* plan, uint32_t G, uint32_t E)
 {
@@ -431,6 +665,204 @@ static void hr_scatter(void* arg, size_t lo, size_t hi)
     }
 }
 
+/* The zero-copy recover: per chunk, the pointer tables and the received
+ * masks (from which pointers are NULL) H2D; on the device the received
+ * segments and parities gathered from the callers' structs into the dense
+ * slots (a lost one zero), the dense decode, the recovered segments scattered
+ * into the callers' out_seg structs; out_index and the recovered masks D2H. */
+typedef struct {
+    size_t sp, fp, op, present, ppm, in_bytes;       /* host -> device */
+    size_t oidx, rec, host_total;                    /* device -> host (pinned) */
+    size_t shards, hdr, parity, meta, fsize, fecid;  /* device only */
+    size_t out_shards, out_hdr, out_index, recovered, ws, total;
+} hy_layout;
+
+static hy_layout hy_offsets(const rfec_plan* plan, uint32_t G, uint32_t E)
+{
+    const uint32_t k = plan->k, n = plan->n_lines;
+    hy_layout L;
+    size_t o = 0;
+#define HY_TAKE(field, bytes)                           \
+    do {                                                \
+        L.field = o;                                    \
+        o = (o + (size_t)(bytes) + 255) & ~(size_t)255; \
+    } while (0)
+    HY_TAKE(sp, (size_t)G * k * 8);
+    HY_TAKE(fp, (size_t)G * n * 8);
+    HY_TAKE(op, (size_t)G * E * 8);
+    HY_TAKE(present, (size_t)G * 16);
+    HY_TAKE(ppm, (size_t)G * 8);
+    L.in_bytes = o;
+    HY_TAKE(oidx, (size_t)G * E);
+    HY_TAKE(rec, (size_t)G * 16);
+    L.host_total = o;
+    HY_TAKE(shards, (size_t)G * k * DI_STRIDE);
+    HY_TAKE(hdr, (size_t)G * k * sizeof(rfec_hdr));
+    HY_TAKE(parity, (size_t)G * n * DI_STRIDE);
+    HY_TAKE(meta, (size_t)G * n * sizeof(rfec_hdr));
+    HY_TAKE(fsize, (size_t)G * n * sizeof(uint16_t));
+    HY_TAKE(fecid, (size_t)G * n * sizeof(uint16_t));
+    HY_TAKE(out_shards, (size_t)G * E * DI_STRIDE);
+    HY_TAKE(out_hdr, (size_t)G * E * sizeof(rfec_hdr));
+    HY_TAKE(out_index, (size_t)G * E);
+    HY_TAKE(recovered, (size_t)G * 16);
+    HY_TAKE(ws, rfec_recover_workspace_size(plan, G));
+#undef HY_TAKE
+    L.total = o;
+    return L;
+}
+
+static int zc_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,
+                             sim_fec_t* const* fecs, uint32_t E, sim_segment_t* const* out, uint8_t* out_index,
+                             uint64_t* recovered, rfec_host_timing* timing, intptr_t ds, intptr_t df, intptr_t dout)
+{
+    di_ctx* c = di_get();
+    if (!c)
+        return RFEC_EDEVICE;
+    const uint32_t k = plan->k, n = plan->n_lines;
+    const size_t group_bytes = hy_offsets(plan, 1024, E).total / 1024 + 1;
+    const size_t by_bytes = RFEC_HR_SLOT_BYTES / group_bytes;
+    uint32_t chunk = (groups + 7) / 8;
+    chunk = chunk < 2048 ? 2048 : chunk > 16384 ? 16384 : chunk;
+    chunk = (size_t)chunk > by_bytes ? (uint32_t)(by_bytes ? by_bytes : 1) : chunk;
+    chunk = chunk > groups ? groups : chunk;
+    const uint32_t nch = (groups + chunk - 1) / chunk;
+    const hy_layout L = hy_offsets(plan, chunk, E);
+    int rc = hb_reserve(c, L.host_total, L.total);
+    if (rc)
+        return rc;
+    rfec_kmask M;
+    make_masks(plan, &M);
+    double tab_us = 0, h2d_us = 0, kernel_us = 0, d2h_us = 0, out_us = 0;
+    const double t0 = now_us();
+    for (uint32_t it = 0; it < nch + 2 && rc == RFEC_OK; ++it) {
+        if (it >= 2) { /* retire chunk it - 2: its out_index / recovered masks to the caller */
+            const uint32_t s = (it - 2) & 1, g0 = (it - 2) * chunk;
+            const uint32_t ng = it - 2 == nch - 1 ? groups - g0 : chunk;
+            const hipError_t e = hipEventSynchronize(c->ev[s][3]);
+            if (e != hipSuccess) {
+                rc = set_err(RFEC_EDEVICE, "zero-copy recover wait", e);
+                break;
+            }
+            float a = 0, b = 0, d = 0;
+            (void)hipEventElapsedTime(&a, c->ev[s][0], c->ev[s][1]);
+            (void)hipEventElapsedTime(&b, c->ev[s][1], c->ev[s][2]);
+            (void)hipEventElapsedTime(&d, c->ev[s][2], c->ev[s][3]);
+            h2d_us += a * 1e3;
+            kernel_us += b * 1e3;
+            d2h_us += d * 1e3;
+            const double to = now_us();
+            const uint8_t* h = c->bh + (size_t)s * L.host_total;
+            if (out_index)
+                memcpy(out_index + (size_t)g0 * E, h + L.oidx, (size_t)ng * E);
+            if (recovered)
+                memcpy(recovered + (size_t)g0 * 2, h + L.rec, (size_t)ng * 16);
+            out_us += now_us() - to;
+        }
+        if (it >= nch)
+            continue;
+        const uint32_t s = it & 1, g0 = it * chunk, ng = it == nch - 1 ? groups - g0 : chunk;
+        uint8_t* h = c->bh + (size_t)s * L.host_total;
+        uint8_t* dv = c->bd + (size_t)s * L.total;
+        hipStream_t st = c->bstream[s];
+        const double tt = now_us();
+        sim_segment_t* const* sg = segs + (size_t)g0 * k;
+        sim_fec_t* const* fg = fecs + (size_t)g0 * n;
+        dev_ptrs((uint64_t*)(h + L.sp), (const void* const*)sg, (size_t)ng * k, ds);
+        dev_ptrs((uint64_t*)(h + L.fp), (const void* const*)fg, (size_t)ng * n, df);
+        dev_ptrs((uint64_t*)(h + L.op), (const void* const*)(out + (size_t)g0 * E), (size_t)ng * E, dout);
+        uint64_t* pres = (uint64_t*)(h + L.present);
+        uint64_t* ppm = (uint64_t*)(h + L.ppm);
+        uint64_t* spt = (uint64_t*)(h + L.sp);
+        uint64_t* fpt = (uint64_t*)(h + L.fp);
+        for (uint32_t g = 0; g < ng; ++g) {
+            uint64_t m0 = 0, m1 = 0, pm = 0;
+            for (uint32_t i = 0; i < k; ++i)
+                if (sg[(size_t)g * k + i]) {
+                    if (i < 64)
+                        m0 |= 1ull << i;
+                    else
+                        m1 |= 1ull << (i - 64);
+                }
+            for (uint32_t l = 0; l < n; ++l)
+                if (fg[(size_t)g * n + l])
+                    pm |= 1ull << l;
+            pres[2 * g] = m0;
+            pres[2 * g + 1] = m1;
+            ppm[g] = pm;
+            /* A line fires only to rebuild a member it lacks, so the decode
+             * reads the payloads of received lines that hold an erased member
+             * and nothing else: the rest cross PCIe as headers only. */
+            const uint64_t e0 = ~m0, e1 = ~m1; /* (line masks hold members only) */
+            uint64_t n0 = 0, n1 = 0, pn = 0;
+            for (uint32_t l = 0; l < n; ++l)
+                if ((pm >> l & 1) && ((M.mask[l][0] & e0) | (M.mask[l][1] & e1))) {
+                    n0 |= M.mask[l][0];
+                    n1 |= M.mask[l][1];
+                    pn |= 1ull << l;
+                }
+            for (uint32_t i = 0; i < k; ++i)
+                if (spt[(size_t)g * k + i] && !((i < 64 ? n0 >> i : n1 >> (i - 64)) & 1))
+                    spt[(size_t)g * k + i] |= 1;
+            for (uint32_t l = 0; l < n; ++l)
+                if (fpt[(size_t)g * n + l] && !(pn >> l & 1))
+                    fpt[(size_t)g * n + l] |= 1;
+        }
+        tab_us += now_us() - tt;
+        hipError_t e;
+        if ((e = hipEventRecord(c->ev[s][0], st)) != hipSuccess ||
+            (e = hipMemcpyAsync(dv, h, L.in_bytes, hipMemcpyHostToDevice, st)) != hipSuccess ||
+            (e = hipEventRecord(c->ev[s][1], st)) != hipSuccess) {
+            rc = set_err(RFEC_EDEVICE, "zero-copy recover H2D", e);
+            break;
+        }
+        int ke = rfec_launch_host_gather(0, (const uint64_t*)(dv + L.sp), ng * k, DI_STRIDE, dv + L.shards,
+                                         (rfec_hdr*)(dv + L.hdr), NULL, NULL, SIM_VIDEO_SIZE, st);
+        if (!ke)
+            ke = rfec_launch_host_gather(1, (const uint64_t*)(dv + L.fp), ng * n, DI_STRIDE, dv + L.parity,
+                                         (rfec_hdr*)(dv + L.meta), (uint16_t*)(dv + L.fsize),
+                                         (uint16_t*)(dv + L.fecid), SIM_VIDEO_SIZE, st);
+        const rfec_dense_out D = {dv + L.out_shards, (rfec_hdr*)(dv + L.out_hdr), dv + L.out_index, E};
+        if (!ke)
+            ke = rfec_launch_recover_out(&M, ng, DI_STRIDE, SIM_VIDEO_SIZE, dv + L.shards,
+                                         (const rfec_hdr*)(dv + L.hdr), (const uint64_t*)(dv + L.present),
+                                         dv + L.parity, (const rfec_hdr*)(dv + L.meta), (const uint16_t*)(dv + L.fsize),
+                                         (const uint64_t*)(dv + L.ppm), (uint64_t*)(dv + L.recovered), dv + L.ws, st,
+                                         g_tuning, &D);
+        if (!ke && (e = hipEventRecord(c->ev[s][2], st)) != hipSuccess)
+            ke = (int)e;
+        if (!ke)
+            ke = rfec_launch_host_scatter_seg((const uint64_t*)(dv + L.op), ng, E, DI_STRIDE, dv + L.out_shards,
+                                              (const rfec_hdr*)(dv + L.out_hdr), dv + L.out_index,
+                                              (const uint16_t*)(dv + L.fecid), (const uint64_t*)(dv + L.ppm), n,
+                                              SIM_VIDEO_SIZE, st);
+        if (ke || (e = hipMemcpyAsync(h + L.oidx, dv + L.out_index, (size_t)ng * E, hipMemcpyDeviceToHost, st)) !=
+                      hipSuccess ||
+            (e = hipMemcpyAsync(h + L.rec, dv + L.recovered, (size_t)ng * 16, hipMemcpyDeviceToHost, st)) !=
+                hipSuccess ||
+            (e = hipEventRecord(c->ev[s][3], st)) != hipSuccess) {
+            rc = set_err(RFEC_EDEVICE, "zero-copy recover launch", ke ? ke : (int)e);
+            break;
+        }
+    }
+    if (rc != RFEC_OK) {
+        (void)hipStreamSynchronize(c->bstream[0]);
+        (void)hipStreamSynchronize(c->bstream[1]);
+        return rc;
+    }
+    if (timing) { /* gather: tables + masks; kernel: device gathers + decode; d2h: the scatter + small copies */
+        timing->gather_us = tab_us;
+        timing->h2d_us = h2d_us;
+        timing->kernel_us = kernel_us;
+        timing->d2h_us = d2h_us;
+        timing->scatter_us = out_us;
+        timing->total_us = now_us() - t0;
+        timing->zero_copy = 1;
+        timing->reserved = 0;
+    }
+    return RFEC_OK;
+}
+
 int rfec_host_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,
                              sim_fec_t* const* fecs, uint32_t per_group, sim_segment_t* const* out,
                              uint8_t* out_index, uint64_t* recovered, rfec_host_timing* timing)
@@ -446,6 +878,12 @@ int rfec_host_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
         return set_err(RFEC_EINVAL, "per_group above k", 0);
     if ((rc = check_geometry(groups, DI_STRIDE, SIM_VIDEO_SIZE, plan->k)))
         return rc;
+    intptr_t ds = 0, df = 0, dout = 0;
+    if (zerocopy_enabled() &&
+        pinned_span((const void* const*)segs, (size_t)groups * plan->k, sizeof(sim_segment_t), &ds) &&
+        pinned_span((const void* const*)fecs, (size_t)groups * plan->n_lines, sizeof(sim_fec_t), &df) &&
+        pinned_span((const void* const*)out, (size_t)groups * per_group, sizeof(sim_segment_t), &dout))
+        return zc_recover_groups(plan, groups, segs, fecs, per_group, out, out_index, recovered, timing, ds, df, dout);
     di_ctx* c = di_get();
     if (!c)
         return RFEC_EDEVICE;
@@ -567,6 +1005,8 @@ int rfec_host_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
         timing->d2h_us = d2h_us;
         timing->scatter_us = scatter_us;
         timing->total_us = now_us() - t0;
+        timing->zero_copy = 0;
+        timing->reserved = 0;
     }
     return RFEC_OK;
 }

@@ -1233,24 +1233,7 @@ int rfec_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payloa
 /* ------------------------------------------------------------------------ */
 /* Received datagrams (host) -> recovered segments (host)                    */
 /* ------------------------------------------------------------------------ */
-void* rfec_pinned_alloc(size_t bytes)
-{
-    void* p = NULL;
-    hipError_t e;
-    if (bytes == 0)
-        return NULL;
-    if ((e = hipHostMalloc(&p, bytes, hipHostMallocDefault)) != hipSuccess) {
-        set_err(RFEC_ENOMEM, "pinned alloc", e);
-        return NULL;
-    }
-    return p;
-}
-
-void rfec_pinned_free(void* p)
-{
-    if (p)
-        (void)hipHostFree(p);
-}
+/* rfec_pinned_alloc / rfec_pinned_free: rfec_hostmem.c (the registry of pinned blocks the device maps) */
 
 typedef struct {
     uint8_t* d;

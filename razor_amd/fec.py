@@ -142,7 +142,8 @@ class rfec_plan(C.Structure):
 
 class rfec_host_timing(C.Structure):
     _fields_ = [("gather_us", C.c_double), ("h2d_us", C.c_double), ("kernel_us", C.c_double),
-                ("d2h_us", C.c_double), ("scatter_us", C.c_double), ("total_us", C.c_double)]
+                ("d2h_us", C.c_double), ("scatter_us", C.c_double), ("total_us", C.c_double),
+                ("zero_copy", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 def seg_dtype(video_size: int) -> np.dtype:

@@ -256,6 +256,33 @@ int rfec_launch_zero_tails(uint32_t slots, uint32_t stride, uint8_t* shards, con
     return 0;
 }
 
+/* the zero-copy host-memory paths: not exercised here (no pinned blocks are
+ * registered through the stub), refused if reached */
+int rfec_launch_host_gather(int kind, const uint64_t* ptrs, uint32_t n, uint32_t stride, uint8_t* dst, rfec_hdr* hdr,
+                            uint16_t* fsize, uint16_t* fecid, uint32_t video, void* stream)
+{
+    (void)kind, (void)ptrs, (void)n, (void)stride, (void)dst, (void)hdr, (void)fsize, (void)fecid, (void)video,
+        (void)stream;
+    return (int)hipErrorNotSupported;
+}
+int rfec_launch_host_scatter_fec(const uint64_t* fptrs, uint32_t groups, const rfec_kplan* P, uint32_t stride,
+                                 const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fsize,
+                                 const int8_t* status, const rfec_hdr* hdr, uint16_t fec_id0, uint32_t g0,
+                                 uint32_t video, void* stream)
+{
+    (void)fptrs, (void)groups, (void)P, (void)stride, (void)parity, (void)meta, (void)fsize, (void)status,
+        (void)hdr, (void)fec_id0, (void)g0, (void)video, (void)stream;
+    return (int)hipErrorNotSupported;
+}
+int rfec_launch_host_scatter_seg(const uint64_t* optrs, uint32_t groups, uint32_t E, uint32_t stride,
+                                 const uint8_t* out_shards, const rfec_hdr* out_hdr, const uint8_t* out_index,
+                                 const uint16_t* fecid, const uint64_t* ppm, uint32_t n_lines, uint32_t video,
+                                 void* stream)
+{
+    (void)optrs, (void)groups, (void)E, (void)stride, (void)out_shards, (void)out_hdr, (void)out_index,
+        (void)fecid, (void)ppm, (void)n_lines, (void)video, (void)stream;
+    return (int)hipErrorNotSupported;
+}
 const char* rfec_hip_error_string(int code) { return code ? "stub error" : "no error"; }
 
 /* HBM probes: not available without a device */

@@ -310,27 +310,65 @@ def test_capacity_status(product):
     assert fs.cpu().numpy()[1, 1] == 60
 
 
-def test_host_encode_groups(product1200, oracle1200):
-    """rfec_host_encode_groups (host AoS in, host sim_fec_t out) vs the oracle's
-    reference-shaped AoS path (flex_fec_generate per line + sender stamps)."""
-    from razor_amd.fec import fec_dtype, seg_dtype
+def _host_arrays(lib, n, dtype, mem, fill=0):
+    """n structs of `dtype` in pageable numpy memory, or in an rfec_pinned_alloc
+    block (the zero-copy path); `fill` pre-sets every byte (stale contents a
+    caller's buffers may hold)."""
+    if mem == "pinned":
+        a, keep = lib.pinned_array((n,), dtype)
+    else:
+        a, keep = np.zeros(n, dtype), None
+    a.view(np.uint8)[...] = fill
+    return a, keep
 
-    lib, o = product1200, oracle1200
-    G, k, S = 37, 10, 1200
-    shards, hdr = o.fill_groups(202, G, k, S, ragged=True)
-    plan = o.plan_from_fraction(k, 80, 3)  # full 3x4 plan: 7 parities
-    segs = np.zeros(G * k, seg_dtype(1200))
+
+def _ptrs(a):
+    return a.ctypes.data + np.arange(a.shape[0], dtype=np.uint64) * a.dtype.itemsize
+
+
+def _host_segs(lib, o, seed, G, k, S, mem):
+    from razor_amd.fec import seg_dtype
+
+    shards, hdr = o.fill_groups(seed, G, k, S, ragged=True)
+    segs, keep = _host_arrays(lib, G * k, seg_dtype(1200), mem)
     h = hdr.reshape(-1)
     for a, b in (("seq", "packet_id"), ("fid", "fid"), ("ts", "timestamp"), ("index", "index"),
                  ("total", "total"), ("ftype", "ftype"), ("payload_type", "payload_type"), ("size", "data_size")):
         segs[b] = h[a]
     segs["data"] = shards.reshape(G * k, S)
+    return shards, hdr, segs, keep
+
+
+def _fields_equal(got, want, size_field, data_field):
+    """Every named field equal, the payload compared up to its size field
+    (bytes past it are unspecified in the reference's structs)."""
+    for f in got.dtype.names:
+        if f != data_field:
+            assert np.array_equal(got[f], want[f]), f
+    for j in range(got.shape[0]):
+        L = int(want[size_field][j])
+        L = 0 if L == 0xFFFF else L
+        assert np.array_equal(got[data_field][j, :L], want[data_field][j, :L]), j
+
+
+@pytest.mark.parametrize("mem", ["pageable", "pinned"])
+def test_host_encode_groups(product1200, oracle1200, mem):
+    """rfec_host_encode_groups (host AoS in, host sim_fec_t out) vs the oracle's
+    reference-shaped AoS path (flex_fec_generate per line + sender stamps).
+    "pinned": segments and parities in rfec_pinned_alloc memory, so the device
+    gathers and scatters the structs itself (timing.zero_copy); its output
+    equals the staged path's field for field and zero past fec_data_size; a
+    line whose flex_fec_generate fails (oversize data_size) gets 0xFFFF."""
+    from razor_amd.fec import fec_dtype
+
+    lib, o = product1200, oracle1200
+    G, k, S = 37, 10, 1200
+    shards, hdr, segs, ks = _host_segs(lib, o, 202, G, k, S, mem)
+    plan = o.plan_from_fraction(k, 80, 3)  # full 3x4 plan: 7 parities
     n = plan.n_lines
-    fecs = np.zeros(G * n, fec_dtype(1200))
-    sp = segs.ctypes.data + np.arange(G * k, dtype=np.uint64) * segs.dtype.itemsize
-    fp = fecs.ctypes.data + np.arange(G * n, dtype=np.uint64) * fecs.dtype.itemsize
-    t = lib.host_encode_groups(plan, G, sp, fp, fec_id0=1)
-    assert t["total_us"] > 0
+    fecs, kf = _host_arrays(lib, G * n, fec_dtype(1200), mem, fill=0xA5)
+    t = lib.host_encode_groups(plan, G, _ptrs(segs), _ptrs(fecs), fec_id0=1)
+    assert t["total_us"] > 0 and t["zero_copy"] == (mem == "pinned")
     nref, ref = o.encode_aos(plan, G, o.to_aos(shards, hdr))
     assert nref == G * n
     ref = ref.view(fec_dtype(1200)).reshape(-1)
@@ -340,10 +378,29 @@ def test_host_encode_groups(product1200, oracle1200):
     for j in range(G * n):
         L = int(ref["fec_data_size"][j])
         assert np.array_equal(fecs["fec_data"][j, :L], ref["fec_data"][j, :L])
+    if mem != "pinned":
+        return
+    for j in range(G * n):
+        assert not fecs["fec_data"][j, int(fecs["fec_data_size"][j]):].any(), j
+    # against the staged path, fec_id0 wrapping past 65535 and failing lines
+    segs["data_size"][3 * k + 2] = 1300  # > SIM_VIDEO_SIZE: its row and column lines fail
+    stale = np.zeros(G * n, fec_dtype(1200))
+    stale.view(np.uint8)[...] = 0x5A
+    fecs.view(np.uint8)[...] = 0x5A
+    t = lib.host_encode_groups(plan, G, _ptrs(segs), _ptrs(fecs), fec_id0=65520)
+    assert t["zero_copy"] == 1
+    pg = np.zeros(G * k, segs.dtype)
+    pg[...] = segs
+    t = lib.host_encode_groups(plan, G, _ptrs(pg), _ptrs(stale), fec_id0=65520)
+    assert t["zero_copy"] == 0
+    assert (stale["fec_data_size"] == 0xFFFF).sum() >= 2
+    assert stale["fec_id"].min() >= 1 and stale["fec_id"].max() == 65535
+    _fields_equal(fecs, stale, "fec_data_size", "fec_data")
 
 
+@pytest.mark.parametrize("mem", ["pageable", "pinned"])
 @pytest.mark.parametrize("k,layers,G", [(10, 1, 301), (10, 3, 301), (10, 3, 4500), (128, 1, 3000)])
-def test_host_recover_groups(product1200, oracle1200, k, layers, G):
+def test_host_recover_groups(product1200, oracle1200, k, layers, G, mem):
     """rfec_host_recover_groups (host AoS in, flex_fec_recover-style out_seg
     out): groups encoded by rfec_host_encode_groups (checked above), 1-3
     segments and 0-2 parities of each lost; out_index / recovered masks equal
@@ -352,24 +409,20 @@ def test_host_recover_groups(product1200, oracle1200, k, layers, G):
     and carries the group's fec_id.  4,500 groups: three double-buffered
     chunks of packed received rows (2,048, 2,048, 404).  k = 128 with a
     64-line plan (64 rows of 2): chunks sized by bytes (~1,400 groups of
-    ~470 KB device staging each), not by the group count alone."""
+    ~470 KB device staging each), not by the group count alone.  "pinned":
+    every struct in rfec_pinned_alloc memory (the zero-copy path, with some
+    out pointers NULL), output equal to the staged path's field for field,
+    out structs not recovered into left as they were."""
     from razor_amd.fec import fec_dtype, seg_dtype
 
     lib, o = product1200, oracle1200
     S, E = 1200, 3
-    shards, hdr = o.fill_groups(203, G, k, S, ragged=True)
+    shards, hdr, segs, ks = _host_segs(lib, o, 203, G, k, S, mem)
     plan = o.plan_from_fraction(k, 80, layers) if k <= 10 else o.plan_matrix(k, 64, 2, layers)
     assert plan.n_lines == ({1: 3, 3: 7}[layers] if k == 10 else 64)
     n = plan.n_lines
-    segs = np.zeros(G * k, seg_dtype(1200))
-    h = hdr.reshape(-1)
-    for a, b in (("seq", "packet_id"), ("fid", "fid"), ("ts", "timestamp"), ("index", "index"),
-                 ("total", "total"), ("ftype", "ftype"), ("payload_type", "payload_type"), ("size", "data_size")):
-        segs[b] = h[a]
-    segs["data"] = shards.reshape(G * k, S)
-    fecs = np.zeros(G * n, fec_dtype(1200))
-    sp = segs.ctypes.data + np.arange(G * k, dtype=np.uint64) * segs.dtype.itemsize
-    fp = fecs.ctypes.data + np.arange(G * n, dtype=np.uint64) * fecs.dtype.itemsize
+    fecs, kf = _host_arrays(lib, G * n, fec_dtype(1200), mem)
+    sp, fp = _ptrs(segs), _ptrs(fecs)
     lib.host_encode_groups(plan, G, sp, fp, fec_id0=1)
     rng = np.random.default_rng(layers)
     present = np.zeros((G, 2), np.uint64)
@@ -383,10 +436,12 @@ def test_host_recover_groups(product1200, oracle1200, k, layers, G):
         plost = rng.choice(n, int(rng.integers(0, 3)), replace=False)
         fp_rx[g * n + plost] = 0
         ppm[g] = sum(1 << l for l in range(n) if l not in plost)
-    out = np.zeros(G * E, seg_dtype(1200))
-    op = out.ctypes.data + np.arange(G * E, dtype=np.uint64) * out.dtype.itemsize
+    out, ko = _host_arrays(lib, G * E, seg_dtype(1200), mem, fill=0xA5 if mem == "pinned" else 0)
+    op = _ptrs(out)
+    if mem == "pinned":
+        op[::7] = 0  # out_seg NULL: skipped
     oi, rec, t = lib.host_recover_groups(plan, G, sp_rx, fp_rx, E, op)
-    assert t["total_us"] > 0
+    assert t["total_us"] > 0 and t["zero_copy"] == (mem == "pinned")
     # the oracle on the same received set (lost members' slots / headers zero)
     rx_sh = shards.copy()
     rx_h = hdr.copy()
@@ -404,7 +459,7 @@ def test_host_recover_groups(product1200, oracle1200, k, layers, G):
     for g in range(G):
         for e in range(E):
             i = int(oi[g, e])
-            if i == 0xFF:
+            if i == 0xFF or op[g * E + e] == 0:
                 continue
             got, want = out[g * E + e], segs[g * k + i]
             for f in ("packet_id", "fid", "timestamp", "index", "total", "ftype", "payload_type", "data_size"):
@@ -412,6 +467,25 @@ def test_host_recover_groups(product1200, oracle1200, k, layers, G):
             nb = int(want["data_size"])
             assert np.array_equal(got["data"][:nb], want["data"][:nb]) and not got["data"][nb:].any()
             assert got["fec_id"] == fecs["fec_id"][g * n]
+    if mem != "pinned":
+        return
+    # the staged path on pageable copies of the same structs and stale out contents
+    pseg = np.zeros(G * k, segs.dtype)
+    pseg[...] = segs
+    pfec = np.zeros(G * n, fecs.dtype)
+    pfec[...] = fecs
+    pout = np.zeros(G * E, out.dtype)
+    pout.view(np.uint8)[...] = 0xA5
+    pop = _ptrs(pout)
+    pop[::7] = 0
+    psp = np.where(sp_rx == 0, 0, _ptrs(pseg))
+    pfp = np.where(fp_rx == 0, 0, _ptrs(pfec))
+    oi2, rec2, t2 = lib.host_recover_groups(plan, G, psp, pfp, E, pop)
+    assert t2["zero_copy"] == 0
+    assert np.array_equal(oi2, oi) and np.array_equal(rec2, rec)
+    _fields_equal(out, pout, "data_size", "data")
+    untouched = (oi.reshape(-1) == 0xFF) | (op == 0)
+    assert (out.view(np.uint8).reshape(G * E, -1)[untouched] == 0xA5).all()
 
 
 @pytest.mark.parametrize("name", ["c2_k10_rows_S1200_G65536", "c3_k10_full_S1200_G65536",

@@ -13,7 +13,7 @@ O=razor_amd/lib/obj; D=tools/bin/ab; mkdir -p $D
 SRCFILE=${SRCFILE:-razor_amd/csrc/$SRC.hip}
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Iinclude -Irazor_amd/csrc "$@" -c -x hip "$SRCFILE" -o $D/${SRC}_$name.o
 objs=""
-for s in rfec_kernels rfec_probe rfec_wire rfec_fill rfec_service; do
+for s in rfec_kernels rfec_probe rfec_wire rfec_fill rfec_service rfec_hostio; do
   if [ $s = $SRC ]; then objs="$objs $D/${SRC}_$name.o"; else objs="$objs $O/$s.o"; fi
 done
 hipcc -shared -fPIC $objs $O/rfec_net.o $O/*_v$VS.o -o $D/${LIB}_$name.so -Wl,-soname,$LIB.so -lpthread -lm

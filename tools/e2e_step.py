@@ -11,6 +11,10 @@ sim_segment_t / sim_fec_t structs in host memory (AoS, payload at offset 34).
           scatter into flex_fec_recover-style out_seg structs
 
 Both chunked and double-buffered (copies, kernels and host threads overlap).
+--mem pinned: the structs in rfec_pinned_alloc memory, so both directions
+take the zero-copy path -- no host gather or scatter, the device reads the
+sim_segment_t and writes the sim_fec_t / out_seg structs over PCIe itself
+(rfec_hostio.hip); only the pointer tables are staged.
 Prints one JSON line per workload: per-stage times (summed over chunks) and
 the wall time of each direction, GiB/s over the bench's algorithmic bytes
 (bench.py: encode (k + r) S per group, decode the peel's bytes), every
@@ -18,6 +22,7 @@ recovered segment checked against the original.  The device-resident rate
 is bench.py's `value`; this one is PCIe-bound.
 
 Usage: python tools/e2e_step.py [--groups 65536] [--reps 3] [--config c3|c3full|both]
+                                [--mem pageable|pinned|both]
 """
 from __future__ import annotations
 
@@ -35,12 +40,22 @@ from bench import distinct_row_pairs, peel_bytes  # noqa: E402
 from razor_amd.fec import fec_dtype, native, seg_dtype  # noqa: E402
 
 
-def run(lib, G, full, reps):
+def alloc(lib, n, dtype, mem, keep):
+    if mem != "pinned":
+        return np.zeros(n, dtype)
+    a, kp = lib.pinned_array((n,), dtype)
+    a.view(np.uint8)[...] = 0
+    keep.append(kp)
+    return a
+
+
+def run(lib, G, full, reps, mem):
     k, S = 10, 1200
     plan = lib.plan_from_fraction(k, 80, 3 if full else 1)
     n = plan.n_lines
     rng = np.random.default_rng(5)
-    segs = np.zeros(G * k, seg_dtype(1200))
+    keep = []
+    segs = alloc(lib, G * k, seg_dtype(1200), mem, keep)
     segs["data"] = rng.integers(0, 256, (G * k, S), dtype=np.uint8)
     gi = np.repeat(np.arange(G, dtype=np.uint64), k)
     ii = np.tile(np.arange(k, dtype=np.uint64), G)
@@ -51,7 +66,7 @@ def run(lib, G, full, reps):
     segs["total"] = k
     segs["ftype"] = gi % 60 == 0
     segs["data_size"] = S
-    fecs = np.zeros(G * n, fec_dtype(1200))
+    fecs = alloc(lib, G * n, fec_dtype(1200), mem, keep)
     sp = segs.ctypes.data + np.arange(G * k, dtype=np.uint64) * segs.dtype.itemsize
     fp = fecs.ctypes.data + np.arange(G * n, dtype=np.uint64) * fecs.dtype.itemsize
     # the bench's erasures: 2 per group, distinct-row pairs (rows) / every recoverable pair (full plan)
@@ -66,7 +81,7 @@ def run(lib, G, full, reps):
     sp_rx = sp.copy().reshape(G, k)
     sp_rx[np.arange(G), erased[:, 0]] = 0
     sp_rx[np.arange(G), erased[:, 1]] = 0
-    out = np.zeros(G * 2, seg_dtype(1200))
+    out = alloc(lib, G * 2, seg_dtype(1200), mem, keep)
     op = out.ctypes.data + np.arange(G * 2, dtype=np.uint64) * out.dtype.itemsize
     lib.host_encode_groups(plan, G, sp, fp)  # warm: staging
     lib.host_recover_groups(plan, G, sp_rx.reshape(-1), fp, 2, op)
@@ -78,19 +93,27 @@ def run(lib, G, full, reps):
     for f in ("packet_id", "fid", "timestamp", "index", "data_size", "data"):
         ok = ok and bool(np.array_equal(out[f].reshape(G, 2, *out[f].shape[1:]), want[f]))
     med = lambda runs, key: float(np.median([r[key] for r in runs]))  # noqa: E731
-    e_t = {key: med(enc, key) for key in enc[0]}
-    d_t = {key: med([r[2] for r in dec], key) for key in dec[0][2]}
+    e_t = {key: med(enc, key) for key in enc[0] if key.endswith("_us")}
+    d_t = {key: med([r[2] for r in dec], key) for key in dec[0][2] if key.endswith("_us")}
     wall = e_t["total_us"] + d_t["total_us"]
-    return {"workload": f"{'c3full' if full else 'c3'}: k10_r{n}_S1200_G{G}, host AoS in / out",
+    zc = all(r["zero_copy"] for r in enc) and all(r[2]["zero_copy"] for r in dec)
+    assert zc == (mem == "pinned") and (zc or not any(r["zero_copy"] for r in enc)), mem
+    if zc:  # the structs themselves cross PCIe (16-B chunks from the data's dword), + 8-B pointers
+        ss, fs = segs.dtype.itemsize, fecs.dtype.itemsize
+        pcie = {"encode_h2d": G * k * (ss + 8) + G * n * 8, "encode_d2h": G * n * fs,
+                "decode_h2d": G * ((k - 2) * ss + n * fs + (k + n + 2) * 8 + 24), "decode_d2h": G * 2 * ss + 16 * G}
+    else:  # decode H2D: the received payloads only, in 1,216-B slots (2 of k lost), + headers, masks, row maps
+        pcie = {"encode_h2d": G * k * (S + 20), "encode_d2h": G * n * (S + 23),
+                "decode_h2d": G * ((k - 2 + n) * 1216 + k * 20 + n * 22 + 24 + (k + n) * 4),
+                "decode_d2h": G * 2 * (S + 21) + 16 * G}
+    return {"workload": f"{'c3full' if full else 'c3'}: k10_r{n}_S1200_G{G}, host AoS in / out, {mem}",
+            "zero_copy": zc,
             "encode_us": {x: round(v, 1) for x, v in e_t.items()},
             "decode_us": {x: round(v, 1) for x, v in d_t.items()},
             "encode_e2e_gibps": round(enc_bytes / (e_t["total_us"] * 1e-6) / 2**30, 2),
             "decode_e2e_gibps": round(dec_bytes / (d_t["total_us"] * 1e-6) / 2**30, 2),
             "step_e2e_gibps": round((enc_bytes + dec_bytes) / (wall * 1e-6) / 2**30, 2),
-            # decode H2D: the received payloads only, in 1,216-B slots (2 of k lost), + headers, masks, row maps
-            "pcie_bytes": {"encode_h2d": G * k * (S + 20), "encode_d2h": G * n * (S + 23),
-                           "decode_h2d": G * ((k - 2 + n) * 1216 + k * 20 + n * 22 + 24 + (k + n) * 4),
-                           "decode_d2h": G * 2 * (S + 21) + 16 * G},
+            "pcie_bytes": pcie,
             "bytes": {"encode": enc_bytes, "decode": dec_bytes}, "reps": reps, "verified": ok}
 
 
@@ -99,10 +122,12 @@ def main():
     ap.add_argument("--groups", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--config", default="both", choices=("c3", "c3full", "both"))
+    ap.add_argument("--mem", default="pageable", choices=("pageable", "pinned", "both"))
     args = ap.parse_args()
     lib = native(1200)
-    for full in ((False, True) if args.config == "both" else (args.config == "c3full",)):
-        print(json.dumps(run(lib, args.groups, full, args.reps)), flush=True)
+    for mem in (("pageable", "pinned") if args.mem == "both" else (args.mem,)):
+        for full in ((False, True) if args.config == "both" else (args.config == "c3full",)):
+            print(json.dumps(run(lib, args.groups, full, args.reps, mem)), flush=True)
 
 
 if __name__ == "__main__":
