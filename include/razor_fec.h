@@ -235,7 +235,9 @@ int rfec_recover_batch_out(const rfec_plan* plan, uint32_t groups, uint32_t stri
  * rfec_pinned_alloc (and RFEC_HOST_ZEROCOPY is not "0"), no host gather or
  * scatter runs -- the device reads the sim_segment_t and writes the sim_fec_t
  * through the block's device mapping over PCIe, and only the pointer tables
- * are staged (timing->zero_copy = 1; gather_us is then the table build).
+ * are staged (timing->zero_copy = 1; gather_us is then the host's table
+ * build, h2d_us the device's gathers over PCIe, kernel_us the encode / decode,
+ * d2h_us the device's scatter, scatter_us the copy of out_index / recovered).
  */
 typedef struct {
     double gather_us, h2d_us, kernel_us, d2h_us, scatter_us, total_us;
@@ -572,7 +574,10 @@ int rfec_host_recv_datagrams(uint32_t n, uint32_t dstride, const uint8_t* dgram,
                              rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out,
                              rfec_rx_report* report);
 
-/* Pinned host memory for datagram slots (hipHostMalloc / hipHostFree). */
+/* Pinned host memory the device maps (hipHostMalloc / hipHostFree): datagram
+ * slots, and struct pools for the zero-copy form of rfec_host_encode_groups /
+ * rfec_host_recover_groups (each block is registered with its device address
+ * until rfec_pinned_free). */
 void* rfec_pinned_alloc(size_t bytes);
 void rfec_pinned_free(void* p);
 

@@ -47,6 +47,7 @@ typedef struct {
     /* rfec_host_encode_groups: two pinned host staging slots + their HBM
      * mirrors, one stream and four events per slot */
     uint8_t* bh;
+    uint8_t* bh_dev; /* the device's address of bh (the zero-copy kernels read / write it) */
     uint8_t* bd;
     size_t bh_bytes, bd_bytes; /* the two pinned / device staging slots, together */
     hipStream_t bstream[2];

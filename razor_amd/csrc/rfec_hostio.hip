@@ -95,17 +95,23 @@ __device__ __forceinline__ v4u keep16(v4u v, int n)
 // A pointer with bit 0 set is header only: the struct's header fields are
 // read, its payload is not (the slot is zeroed) -- the receive side marks so
 // the structs on no line that can fire, whose bytes the decode never reads.
+struct GatherSide {
+    const uint64_t* ptrs; // device addresses of the structs (0: lost, bit 0: header only)
+    uint32_t total;       // lanes: structs x C
+    v4u* dst;             // slots [n][C]
+    uint32_t* hdr_dw;     // 20-byte header records
+    uint16_t* fsize;      // KIND 1: fec_data_size, fec_id
+    uint16_t* fecid;
+};
+
 template <int KIND>
-__global__ __launch_bounds__(kBlock) void k_host_gather(const uint64_t* __restrict__ ptrs, uint32_t total, uint32_t C,
-                                                        FastDiv divC, v4u* __restrict__ dst,
-                                                        uint32_t* __restrict__ hdr_dw, uint16_t* __restrict__ fsize,
-                                                        uint16_t* __restrict__ fecid, uint32_t video)
+__device__ __forceinline__ void gather_lane(const GatherSide& S, uint32_t t, uint32_t C, const FastDiv& divC,
+                                            uint32_t video)
 {
     constexpr uint32_t DOFF = KIND ? 42u : 34u; // data
-    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    const bool live = t < total;
+    const bool live = t < S.total;
     const uint32_t slot = live ? fdiv(t, divC) : 0u, j = live ? t - slot * C : 0u;
-    const uint64_t raw = live ? ptrs[slot] : 0u;
+    const uint64_t raw = live ? S.ptrs[slot] : 0u;
     const uint8_t* p = reinterpret_cast<const uint8_t*>(raw & ~(uint64_t)3);
     const uint32_t nload = (video + 15u) / 16u; // chunks that hold struct bytes
     const bool ld = p && !(raw & 1u) && j < nload;
@@ -121,7 +127,7 @@ __global__ __launch_bounds__(kBlock) void k_host_gather(const uint64_t* __restri
     if (!live)
         return;
     const int n = (int)min(sz, video) - (int)(16u * j);
-    __builtin_nontemporal_store(keep16(shift2(x, nx), n), dst + (size_t)slot * C + j);
+    __builtin_nontemporal_store(keep16(shift2(x, nx), n), S.dst + (size_t)slot * C + j);
     if (j != 0)
         return;
     uint32_t h[5] = {0, 0, 0, 0, 0};
@@ -139,14 +145,31 @@ __global__ __launch_bounds__(kBlock) void k_host_gather(const uint64_t* __restri
             id = ld_host4(p) & 0xFFFFu;
         }
     }
-    uint32_t* o = hdr_dw + (size_t)slot * 5;
+    uint32_t* o = S.hdr_dw + (size_t)slot * 5;
 #pragma unroll
     for (int d = 0; d < 5; ++d)
         o[d] = h[d];
     if constexpr (KIND == 1) {
-        fsize[slot] = (uint16_t)fs;
-        fecid[slot] = (uint16_t)id;
+        S.fsize[slot] = (uint16_t)fs;
+        S.fecid[slot] = (uint16_t)id;
     }
+}
+
+// One launch for both kinds: blocks [0, b1) gather the segments (side 0),
+// the rest the parities (side 1), so the receive side's two gathers share one
+// tail; the first aux_n lanes also copy aux_src -> aux_dst (the masks into HBM).
+__global__ __launch_bounds__(kBlock) void k_host_gather(GatherSide s0, GatherSide s1, uint32_t b1, uint32_t C,
+                                                        FastDiv divC, uint32_t video,
+                                                        const uint64_t* __restrict__ aux_src,
+                                                        uint64_t* __restrict__ aux_dst, uint32_t aux_n)
+{
+    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+    if (g < aux_n)
+        aux_dst[g] = aux_src[g];
+    if (blockIdx.x < b1)
+        gather_lane<0>(s0, g, C, divC, video);
+    else
+        gather_lane<1>(s1, (blockIdx.x - b1) * kBlock + threadIdx.x, C, divC, video);
 }
 
 // Parity slots [G][n][C] + meta / fsize / status -> the callers' sim_fec_t.
@@ -200,7 +223,8 @@ __global__ __launch_bounds__(kBlock) void k_host_scatter_fec(const uint64_t* __r
 }
 
 // Recovered segments (dense output [G][E][C], headers, out_index) -> the
-// callers' sim_segment_t (NULL or out_index 0xFF: left alone).
+// callers' sim_segment_t (NULL or out_index 0xFF: left alone); out_index and
+// the recovered masks also into host memory (oidx_host, rec_host).
 __global__ __launch_bounds__(kBlock) void k_host_scatter_seg(const uint64_t* __restrict__ optrs, uint32_t total,
                                                              uint32_t C, FastDiv divC, FastDiv divE,
                                                              const v4u* __restrict__ out_sh,
@@ -208,14 +232,25 @@ __global__ __launch_bounds__(kBlock) void k_host_scatter_seg(const uint64_t* __r
                                                              const uint8_t* __restrict__ out_index,
                                                              const uint16_t* __restrict__ fecid,
                                                              const uint64_t* __restrict__ ppm, uint32_t n,
-                                                             uint32_t video)
+                                                             uint32_t video, uint8_t* __restrict__ oidx_host,
+                                                             const uint64_t* __restrict__ rec,
+                                                             uint64_t* __restrict__ rec_host)
 {
     const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
     const bool live = t < total;
     const uint32_t o = live ? fdiv(t, divC) : 0u, j = live ? t - o * C : 0u;
     const uint32_t nch = (video + 15u) / 16u;
     uint8_t* p = live ? reinterpret_cast<uint8_t*>(optrs[o]) : nullptr;
-    const bool on = p && out_index[o] != 0xFFu;
+    const uint32_t oi = live ? out_index[o] : 0xFFu;
+    if (live && j == 0) {
+        oidx_host[o] = (uint8_t)oi;
+        const uint32_t g = fdiv(o, divE);
+        if (o == g * divE.d) {
+            rec_host[2 * g] = rec[2 * g];
+            rec_host[2 * g + 1] = rec[2 * g + 1];
+        }
+    }
+    const bool on = p && oi != 0xFFu;
     const bool dat = on && j < nch;
     v4u c = {0, 0, 0, 0};
     if (dat)
@@ -245,19 +280,21 @@ inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kB
 
 extern "C" {
 
-int rfec_launch_host_gather(int kind, const uint64_t* ptrs, uint32_t n, uint32_t stride, uint8_t* dst, rfec_hdr* hdr,
-                            uint16_t* fsize, uint16_t* fecid, uint32_t video, void* stream)
+int rfec_launch_host_gather(const uint64_t* sptrs, uint32_t ns, uint8_t* shards, rfec_hdr* hdr,
+                            const uint64_t* fptrs, uint32_t nf, uint8_t* parity, rfec_hdr* meta, uint16_t* fsize,
+                            uint16_t* fecid, uint32_t stride, uint32_t video, const uint64_t* aux_src,
+                            uint64_t* aux_dst, uint32_t aux_n, void* stream)
 {
-    const uint32_t C = stride / 16, total = n * C;
-    if (!total)
+    const uint32_t C = stride / 16;
+    const GatherSide s0{sptrs, ns * C, reinterpret_cast<v4u*>(shards), reinterpret_cast<uint32_t*>(hdr), nullptr,
+                        nullptr};
+    const GatherSide s1{fptrs, nf * C, reinterpret_cast<v4u*>(parity), reinterpret_cast<uint32_t*>(meta), fsize,
+                        fecid};
+    const uint32_t b1 = blocks_for(s0.total > aux_n ? s0.total : aux_n), nb = b1 + blocks_for(s1.total);
+    if (!nb)
         return 0;
-    hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
-    if (kind == 0)
-        RFEC_LAUNCH(k_host_gather<0>, dim3(blocks_for(total)), dim3(kBlock), 0, sm, ptrs, total, C, make_fastdiv(C),
-                    reinterpret_cast<v4u*>(dst), reinterpret_cast<uint32_t*>(hdr), fsize, fecid, video);
-    else
-        RFEC_LAUNCH(k_host_gather<1>, dim3(blocks_for(total)), dim3(kBlock), 0, sm, ptrs, total, C, make_fastdiv(C),
-                    reinterpret_cast<v4u*>(dst), reinterpret_cast<uint32_t*>(hdr), fsize, fecid, video);
+    RFEC_LAUNCH(k_host_gather, dim3(nb), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), s0, s1, b1, C,
+                make_fastdiv(C), video, aux_src, aux_dst, aux_n);
     return (int)hipGetLastError();
 }
 
@@ -280,14 +317,15 @@ int rfec_launch_host_scatter_fec(const uint64_t* fptrs, uint32_t groups, const r
 int rfec_launch_host_scatter_seg(const uint64_t* optrs, uint32_t groups, uint32_t E, uint32_t stride,
                                  const uint8_t* out_shards, const rfec_hdr* out_hdr, const uint8_t* out_index,
                                  const uint16_t* fecid, const uint64_t* ppm, uint32_t n_lines, uint32_t video,
-                                 void* stream)
+                                 uint8_t* oidx_host, const uint64_t* recovered, uint64_t* rec_host, void* stream)
 {
     const uint32_t C = stride / 16, total = groups * E * C;
     if (!total)
         return 0;
     RFEC_LAUNCH(k_host_scatter_seg, dim3(blocks_for(total)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
                 optrs, total, C, make_fastdiv(C), make_fastdiv(E), reinterpret_cast<const v4u*>(out_shards),
-                reinterpret_cast<const uint32_t*>(out_hdr), out_index, fecid, ppm, n_lines, video);
+                reinterpret_cast<const uint32_t*>(out_hdr), out_index, fecid, ppm, n_lines, video, oidx_host,
+                recovered, rec_host);
     return (int)hipGetLastError();
 }
 

@@ -69,10 +69,17 @@ static int hb_reserve(di_ctx* c, size_t host_slot, size_t dev_slot)
     if (c->bh_bytes < 2 * host_slot) {
         if (c->bh)
             (void)hipHostFree(c->bh);
-        c->bh = NULL;
+        c->bh = c->bh_dev = NULL;
         c->bh_bytes = 0;
         if ((e = hipHostMalloc((void**)&c->bh, 2 * host_slot, hipHostMallocDefault)) != hipSuccess)
             return set_err(RFEC_ENOMEM, "pinned staging", e);
+        void* d = NULL;
+        if ((e = hipHostGetDevicePointer(&d, c->bh, 0)) != hipSuccess || !d) {
+            (void)hipHostFree(c->bh);
+            c->bh = NULL;
+            return set_err(RFEC_EDEVICE, "pinned staging: no device address", e);
+        }
+        c->bh_dev = (uint8_t*)d;
         c->bh_bytes = 2 * host_slot;
     }
     if (c->bd_bytes < 2 * dev_slot) {
@@ -182,6 +189,16 @@ static int zerocopy_enabled(void)
     return !(v && v[0] == '0');
 }
 
+/* groups per zero-copy chunk: RFEC_ZC_CHUNK (measurement knob) or G / 8, at least 2,048 */
+static uint32_t zc_chunk(uint32_t groups)
+{
+    const char* v = getenv("RFEC_ZC_CHUNK");
+    uint32_t chunk = v && atoi(v) > 0 ? (uint32_t)atoi(v) : (groups + 7) / 8;
+    if (!(v && atoi(v) > 0) && chunk < 2048)
+        chunk = 2048;
+    return chunk;
+}
+
 /* device addresses of structs (0 for NULL) into a pinned table */
 static void dev_ptrs(uint64_t* out, const void* const* ptrs, size_t n, intptr_t delta)
 {
@@ -252,11 +269,14 @@ static void hb_scatter(void* arg, size_t lo, size_t hi)
     }
 }
 
-/* The zero-copy encode: per chunk on slot s's stream, the pointer tables
- * H2D, then on the device the segments gathered from the callers' structs,
- * the encode, the parities scattered into the callers' sim_fec_t.  Chunks
- * alternate between two streams, so one chunk's PCIe reads overlap the
- * previous one's PCIe writes. */
+/* The zero-copy encode: per chunk, the host writes the structs' device
+ * addresses into pinned slot s; on the device the gather stream reads the
+ * segments from the callers' structs into HBM slot s, and the second stream
+ * (after that gather's event) encodes and scatters the parities into the
+ * callers' sim_fec_t.  Gathers follow each other on their own stream, so
+ * chunk c's PCIe writes run beside chunk c+1's PCIe reads (with one stream
+ * per slot, both slots' gathers ran together and then both scatters: the
+ * link saw reads, then writes, 20.3 vs ~18 ms for c3). */
 typedef struct {
     size_t sp, fp, shards, hdr, parity, meta, fsize, status, total, host_total;
 } hz_layout;
@@ -292,8 +312,7 @@ static int zc_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
     if (!c)
         return RFEC_EDEVICE;
     const uint32_t k = plan->k, n = plan->n_lines;
-    uint32_t chunk = (groups + 7) / 8;
-    chunk = chunk < 2048 ? 2048 : chunk;
+    uint32_t chunk = zc_chunk(groups);
     chunk = chunk > groups ? groups : chunk;
     const uint32_t nch = (groups + chunk - 1) / chunk;
     const hz_layout L = hz_offsets(chunk, k, n);
@@ -323,33 +342,37 @@ static int zc_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
         const uint32_t s = it & 1, g0 = it * chunk, ng = it == nch - 1 ? groups - g0 : chunk;
         uint8_t* h = c->bh + (size_t)s * L.host_total;
         uint8_t* dv = c->bd + (size_t)s * L.total;
-        hipStream_t st = c->bstream[s];
+        hipStream_t ga = c->bstream[0], gb = c->bstream[1]; /* gathers; encode + scatter */
         const double tt = now_us();
         dev_ptrs((uint64_t*)(h + L.sp), (const void* const*)(segs + (size_t)g0 * k), (size_t)ng * k, ds);
         dev_ptrs((uint64_t*)(h + L.fp), (const void* const*)(fecs + (size_t)g0 * n), (size_t)ng * n, df);
         tab_us += now_us() - tt;
+        /* the kernels read the pointer tables where the host wrote them (a DMA
+         * copy queued beside the PCIe-bound kernels started ~1.4 ms late) */
+        const uint8_t* hd = c->bh_dev + (size_t)s * L.host_total;
         hipError_t e;
         int ke = 0;
-        if ((e = hipEventRecord(c->ev[s][0], st)) != hipSuccess ||
-            (e = hipMemcpyAsync(dv, h, L.host_total, hipMemcpyHostToDevice, st)) != hipSuccess ||
-            (e = hipEventRecord(c->ev[s][1], st)) != hipSuccess) {
-            rc = set_err(RFEC_EDEVICE, "zero-copy encode H2D", e);
+        if ((e = hipEventRecord(c->ev[s][0], ga)) != hipSuccess) {
+            rc = set_err(RFEC_EDEVICE, "zero-copy encode event", e);
             break;
         }
-        ke = rfec_launch_host_gather(0, (const uint64_t*)(dv + L.sp), ng * k, DI_STRIDE, dv + L.shards,
-                                     (rfec_hdr*)(dv + L.hdr), NULL, NULL, SIM_VIDEO_SIZE, st);
+        ke = rfec_launch_host_gather((const uint64_t*)(hd + L.sp), ng * k, dv + L.shards, (rfec_hdr*)(dv + L.hdr),
+                                     NULL, 0, NULL, NULL, NULL, NULL, DI_STRIDE, SIM_VIDEO_SIZE, NULL, NULL, 0, ga);
+        if (!ke && ((e = hipEventRecord(c->ev[s][1], ga)) != hipSuccess ||
+                    (e = hipStreamWaitEvent(gb, c->ev[s][1], 0)) != hipSuccess))
+            ke = (int)e;
         if (!ke)
             ke = rfec_launch_encode(plan, ng, DI_STRIDE, SIM_VIDEO_SIZE, dv + L.shards, (const rfec_hdr*)(dv + L.hdr),
                                     dv + L.parity, (rfec_hdr*)(dv + L.meta), (uint16_t*)(dv + L.fsize),
-                                    (int8_t*)(dv + L.status), st, g_tuning);
-        if (!ke && (e = hipEventRecord(c->ev[s][2], st)) != hipSuccess)
+                                    (int8_t*)(dv + L.status), gb, g_tuning);
+        if (!ke && (e = hipEventRecord(c->ev[s][2], gb)) != hipSuccess)
             ke = (int)e;
         if (!ke)
-            ke = rfec_launch_host_scatter_fec((const uint64_t*)(dv + L.fp), ng, plan, DI_STRIDE, dv + L.parity,
+            ke = rfec_launch_host_scatter_fec((const uint64_t*)(hd + L.fp), ng, plan, DI_STRIDE, dv + L.parity,
                                               (const rfec_hdr*)(dv + L.meta), (const uint16_t*)(dv + L.fsize),
                                               (const int8_t*)(dv + L.status), (const rfec_hdr*)(dv + L.hdr), fec_id0,
-                                              g0, SIM_VIDEO_SIZE, st);
-        if (ke || (e = hipEventRecord(c->ev[s][3], st)) != hipSuccess) {
+                                              g0, SIM_VIDEO_SIZE, gb);
+        if (ke || (e = hipEventRecord(c->ev[s][3], gb)) != hipSuccess) {
             rc = set_err(RFEC_EDEVICE, "zero-copy encode launch", ke ? ke : (int)e);
             break;
         }
@@ -359,7 +382,7 @@ static int zc_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
         (void)hipStreamSynchronize(c->bstream[1]);
         return rc;
     }
-    if (timing) { /* gather: the host's pointer tables; kernel: device gather + encode; d2h: the scatter */
+    if (timing) { /* gather: the host's pointer tables; h2d: the device's gather; d2h: its scatter */
         timing->gather_us = tab_us;
         timing->h2d_us = h2d_us;
         timing->kernel_us = kernel_us;
@@ -665,11 +688,14 @@ static void hr_scatter(void* arg, size_t lo, size_t hi)
     }
 }
 
-/* The zero-copy recover: per chunk, the pointer tables and the received
- * masks (from which pointers are NULL) H2D; on the device the received
+/* The zero-copy recover: per chunk, the host writes the pointer tables and
+ * the received masks (from which pointers are NULL) into pinned slot s; on
+ * the gather stream the received
  * segments and parities gathered from the callers' structs into the dense
  * slots (a lost one zero), the dense decode, the recovered segments scattered
- * into the callers' out_seg structs; out_index and the recovered masks D2H. */
+ * into the callers' out_seg structs, out_index and the recovered masks into
+ * the pinned slot -- the decode and the scatter on the second stream, so one
+ * chunk's PCIe writes run beside the next chunk's reads (as the encode). */
 typedef struct {
     size_t sp, fp, op, present, ppm, in_bytes;       /* host -> device */
     size_t oidx, rec, host_total;                    /* device -> host (pinned) */
@@ -722,8 +748,8 @@ static int zc_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
     const uint32_t k = plan->k, n = plan->n_lines;
     const size_t group_bytes = hy_offsets(plan, 1024, E).total / 1024 + 1;
     const size_t by_bytes = RFEC_HR_SLOT_BYTES / group_bytes;
-    uint32_t chunk = (groups + 7) / 8;
-    chunk = chunk < 2048 ? 2048 : chunk > 16384 ? 16384 : chunk;
+    uint32_t chunk = zc_chunk(groups);
+    chunk = chunk > 16384 ? 16384 : chunk;
     chunk = (size_t)chunk > by_bytes ? (uint32_t)(by_bytes ? by_bytes : 1) : chunk;
     chunk = chunk > groups ? groups : chunk;
     const uint32_t nch = (groups + chunk - 1) / chunk;
@@ -764,7 +790,7 @@ static int zc_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
         const uint32_t s = it & 1, g0 = it * chunk, ng = it == nch - 1 ? groups - g0 : chunk;
         uint8_t* h = c->bh + (size_t)s * L.host_total;
         uint8_t* dv = c->bd + (size_t)s * L.total;
-        hipStream_t st = c->bstream[s];
+        hipStream_t ga = c->bstream[0], gb = c->bstream[1]; /* gathers; decode + scatter */
         const double tt = now_us();
         sim_segment_t* const* sg = segs + (size_t)g0 * k;
         sim_fec_t* const* fg = fecs + (size_t)g0 * n;
@@ -809,38 +835,40 @@ static int zc_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
                     fpt[(size_t)g * n + l] |= 1;
         }
         tab_us += now_us() - tt;
+        /* no DMA: the kernels read the tables from the pinned slot, the first
+         * gather copies the masks into HBM for the decode, the scatter writes
+         * out_index and the recovered masks back */
+        const uint8_t* hd = c->bh_dev + (size_t)s * L.host_total;
         hipError_t e;
-        if ((e = hipEventRecord(c->ev[s][0], st)) != hipSuccess ||
-            (e = hipMemcpyAsync(dv, h, L.in_bytes, hipMemcpyHostToDevice, st)) != hipSuccess ||
-            (e = hipEventRecord(c->ev[s][1], st)) != hipSuccess) {
-            rc = set_err(RFEC_EDEVICE, "zero-copy recover H2D", e);
+        if ((e = hipEventRecord(c->ev[s][0], ga)) != hipSuccess) {
+            rc = set_err(RFEC_EDEVICE, "zero-copy recover event", e);
             break;
         }
-        int ke = rfec_launch_host_gather(0, (const uint64_t*)(dv + L.sp), ng * k, DI_STRIDE, dv + L.shards,
-                                         (rfec_hdr*)(dv + L.hdr), NULL, NULL, SIM_VIDEO_SIZE, st);
-        if (!ke)
-            ke = rfec_launch_host_gather(1, (const uint64_t*)(dv + L.fp), ng * n, DI_STRIDE, dv + L.parity,
-                                         (rfec_hdr*)(dv + L.meta), (uint16_t*)(dv + L.fsize),
-                                         (uint16_t*)(dv + L.fecid), SIM_VIDEO_SIZE, st);
+        int ke = rfec_launch_host_gather((const uint64_t*)(hd + L.sp), ng * k, dv + L.shards, (rfec_hdr*)(dv + L.hdr),
+                                         (const uint64_t*)(hd + L.fp), ng * n, dv + L.parity, (rfec_hdr*)(dv + L.meta),
+                                         (uint16_t*)(dv + L.fsize), (uint16_t*)(dv + L.fecid), DI_STRIDE,
+                                         SIM_VIDEO_SIZE, (const uint64_t*)(hd + L.present),
+                                         (uint64_t*)(dv + L.present), (uint32_t)((L.in_bytes - L.present) / 8), ga);
+        if (!ke && ((e = hipEventRecord(c->ev[s][1], ga)) != hipSuccess ||
+                    (e = hipStreamWaitEvent(gb, c->ev[s][1], 0)) != hipSuccess))
+            ke = (int)e;
         const rfec_dense_out D = {dv + L.out_shards, (rfec_hdr*)(dv + L.out_hdr), dv + L.out_index, E};
         if (!ke)
             ke = rfec_launch_recover_out(&M, ng, DI_STRIDE, SIM_VIDEO_SIZE, dv + L.shards,
                                          (const rfec_hdr*)(dv + L.hdr), (const uint64_t*)(dv + L.present),
                                          dv + L.parity, (const rfec_hdr*)(dv + L.meta), (const uint16_t*)(dv + L.fsize),
-                                         (const uint64_t*)(dv + L.ppm), (uint64_t*)(dv + L.recovered), dv + L.ws, st,
+                                         (const uint64_t*)(dv + L.ppm), (uint64_t*)(dv + L.recovered), dv + L.ws, gb,
                                          g_tuning, &D);
-        if (!ke && (e = hipEventRecord(c->ev[s][2], st)) != hipSuccess)
+        if (!ke && (e = hipEventRecord(c->ev[s][2], gb)) != hipSuccess)
             ke = (int)e;
         if (!ke)
-            ke = rfec_launch_host_scatter_seg((const uint64_t*)(dv + L.op), ng, E, DI_STRIDE, dv + L.out_shards,
+            ke = rfec_launch_host_scatter_seg((const uint64_t*)(hd + L.op), ng, E, DI_STRIDE, dv + L.out_shards,
                                               (const rfec_hdr*)(dv + L.out_hdr), dv + L.out_index,
                                               (const uint16_t*)(dv + L.fecid), (const uint64_t*)(dv + L.ppm), n,
-                                              SIM_VIDEO_SIZE, st);
-        if (ke || (e = hipMemcpyAsync(h + L.oidx, dv + L.out_index, (size_t)ng * E, hipMemcpyDeviceToHost, st)) !=
-                      hipSuccess ||
-            (e = hipMemcpyAsync(h + L.rec, dv + L.recovered, (size_t)ng * 16, hipMemcpyDeviceToHost, st)) !=
-                hipSuccess ||
-            (e = hipEventRecord(c->ev[s][3], st)) != hipSuccess) {
+                                              SIM_VIDEO_SIZE, c->bh_dev + (size_t)s * L.host_total + L.oidx,
+                                              (const uint64_t*)(dv + L.recovered),
+                                              (uint64_t*)(c->bh_dev + (size_t)s * L.host_total + L.rec), gb);
+        if (ke || (e = hipEventRecord(c->ev[s][3], gb)) != hipSuccess) {
             rc = set_err(RFEC_EDEVICE, "zero-copy recover launch", ke ? ke : (int)e);
             break;
         }
@@ -850,7 +878,7 @@ static int zc_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
         (void)hipStreamSynchronize(c->bstream[1]);
         return rc;
     }
-    if (timing) { /* gather: tables + masks; kernel: device gathers + decode; d2h: the scatter + small copies */
+    if (timing) { /* gather: tables + masks; h2d: the device gathers; kernel: decode; d2h: the scatter */
         timing->gather_us = tab_us;
         timing->h2d_us = h2d_us;
         timing->kernel_us = kernel_us;

@@ -81,21 +81,25 @@ int rfec_launch_line_jobs(const rfec_line_job* jobs, uint32_t n_jobs, const int3
 int rfec_launch_zero_tails(uint32_t slots, uint32_t stride, uint8_t* shards, const rfec_hdr* hdr, void* stream);
 /* rfec_hostio.hip: razor's structs in device-mapped host memory <-> the slot
  * layout (pointer tables hold device addresses, 0 = a lost struct, bit 0 set =
- * header only: the payload is not read and its slot is zeroed).
- * kind 0: sim_segment_t -> shards + header records; kind 1: sim_fec_t ->
- * parity slots + fec_meta records + fec_data_size + fec_id. */
-int rfec_launch_host_gather(int kind, const uint64_t* ptrs, uint32_t n, uint32_t stride, uint8_t* dst, rfec_hdr* hdr,
-                            uint16_t* fsize, uint16_t* fecid, uint32_t video, void* stream);
+ * header only: the payload is not read and its slot is zeroed).  One launch
+ * gathers ns sim_segment_t (-> shards + header records) and nf sim_fec_t (->
+ * parity slots + fec_meta records + fec_data_size + fec_id; nf may be 0) and
+ * copies aux_n u64 words aux_src -> aux_dst (may be 0: none). */
+int rfec_launch_host_gather(const uint64_t* sptrs, uint32_t ns, uint8_t* shards, rfec_hdr* hdr,
+                            const uint64_t* fptrs, uint32_t nf, uint8_t* parity, rfec_hdr* meta, uint16_t* fsize,
+                            uint16_t* fecid, uint32_t stride, uint32_t video, const uint64_t* aux_src,
+                            uint64_t* aux_dst, uint32_t aux_n, void* stream);
 /* parity slots of `groups` groups -> their sim_fec_t, stamped as flex_fec_sender_update does */
 int rfec_launch_host_scatter_fec(const uint64_t* fptrs, uint32_t groups, const rfec_kplan* P, uint32_t stride,
                                  const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fsize,
                                  const int8_t* status, const rfec_hdr* hdr, uint16_t fec_id0, uint32_t g0,
                                  uint32_t video, void* stream);
-/* dense recover output -> the callers' out_seg structs (flex_fec_recover's fields + fec_id) */
+/* dense recover output -> the callers' out_seg structs (flex_fec_recover's
+ * fields + fec_id); out_index and the recovered masks into oidx_host / rec_host */
 int rfec_launch_host_scatter_seg(const uint64_t* optrs, uint32_t groups, uint32_t E, uint32_t stride,
                                  const uint8_t* out_shards, const rfec_hdr* out_hdr, const uint8_t* out_index,
                                  const uint16_t* fecid, const uint64_t* ppm, uint32_t n_lines, uint32_t video,
-                                 void* stream);
+                                 uint8_t* oidx_host, const uint64_t* recovered, uint64_t* rec_host, void* stream);
 const char* rfec_hip_error_string(int code);
 
 /* Group-level drop-in (rfec_flex.c) over the per-thread pinned, device-mapped

@@ -258,11 +258,13 @@ int rfec_launch_zero_tails(uint32_t slots, uint32_t stride, uint8_t* shards, con
 
 /* the zero-copy host-memory paths: not exercised here (no pinned blocks are
  * registered through the stub), refused if reached */
-int rfec_launch_host_gather(int kind, const uint64_t* ptrs, uint32_t n, uint32_t stride, uint8_t* dst, rfec_hdr* hdr,
-                            uint16_t* fsize, uint16_t* fecid, uint32_t video, void* stream)
+int rfec_launch_host_gather(const uint64_t* sptrs, uint32_t ns, uint8_t* shards, rfec_hdr* hdr,
+                            const uint64_t* fptrs, uint32_t nf, uint8_t* parity, rfec_hdr* meta, uint16_t* fsize,
+                            uint16_t* fecid, uint32_t stride, uint32_t video, const uint64_t* aux_src,
+                            uint64_t* aux_dst, uint32_t aux_n, void* stream)
 {
-    (void)kind, (void)ptrs, (void)n, (void)stride, (void)dst, (void)hdr, (void)fsize, (void)fecid, (void)video,
-        (void)stream;
+    (void)sptrs, (void)ns, (void)shards, (void)hdr, (void)fptrs, (void)nf, (void)parity, (void)meta, (void)fsize,
+        (void)fecid, (void)stride, (void)video, (void)aux_src, (void)aux_dst, (void)aux_n, (void)stream;
     return (int)hipErrorNotSupported;
 }
 int rfec_launch_host_scatter_fec(const uint64_t* fptrs, uint32_t groups, const rfec_kplan* P, uint32_t stride,
@@ -277,10 +279,11 @@ int rfec_launch_host_scatter_fec(const uint64_t* fptrs, uint32_t groups, const r
 int rfec_launch_host_scatter_seg(const uint64_t* optrs, uint32_t groups, uint32_t E, uint32_t stride,
                                  const uint8_t* out_shards, const rfec_hdr* out_hdr, const uint8_t* out_index,
                                  const uint16_t* fecid, const uint64_t* ppm, uint32_t n_lines, uint32_t video,
-                                 void* stream)
+                                 uint8_t* oidx_host, const uint64_t* recovered, uint64_t* rec_host, void* stream)
 {
     (void)optrs, (void)groups, (void)E, (void)stride, (void)out_shards, (void)out_hdr, (void)out_index,
-        (void)fecid, (void)ppm, (void)n_lines, (void)video, (void)stream;
+        (void)fecid, (void)ppm, (void)n_lines, (void)video, (void)oidx_host, (void)recovered, (void)rec_host,
+        (void)stream;
     return (int)hipErrorNotSupported;
 }
 const char* rfec_hip_error_string(int code) { return code ? "stub error" : "no error"; }

@@ -100,8 +100,21 @@ def run(lib, G, full, reps, mem):
     assert zc == (mem == "pinned") and (zc or not any(r["zero_copy"] for r in enc)), mem
     if zc:  # the structs themselves cross PCIe (16-B chunks from the data's dword), + 8-B pointers
         ss, fs = segs.dtype.itemsize, fecs.dtype.itemsize
+        # receive side: whole structs only on lines that hold an erased member, the rest as a 64-B header
+        lm = [set(plan.members(l)) for l in range(n)]
+        cnt = {}
+        for a, b in erased.tolist():
+            cnt[(a, b)] = cnt.get((a, b), 0) + 1
+        nseg = nfec = nhdr = 0
+        for (a, b), m in cnt.items():
+            lines = [l for l in range(n) if a in lm[l] or b in lm[l]]
+            need = set().union(*(lm[l] for l in lines)) - {a, b}
+            nseg += m * len(need)
+            nfec += m * len(lines)
+            nhdr += m * (k - 2 - len(need) + n - len(lines))
         pcie = {"encode_h2d": G * k * (ss + 8) + G * n * 8, "encode_d2h": G * n * fs,
-                "decode_h2d": G * ((k - 2) * ss + n * fs + (k + n + 2) * 8 + 24), "decode_d2h": G * 2 * ss + 16 * G}
+                "decode_h2d": nseg * ss + nfec * fs + nhdr * 64 + G * ((k + n + 2) * 8 + 24),
+                "decode_d2h": G * 2 * ss + 17 * G * 2}
     else:  # decode H2D: the received payloads only, in 1,216-B slots (2 of k lost), + headers, masks, row maps
         pcie = {"encode_h2d": G * k * (S + 20), "encode_d2h": G * n * (S + 23),
                 "decode_h2d": G * ((k - 2 + n) * 1216 + k * 20 + n * 22 + 24 + (k + n) * 4),
