@@ -73,11 +73,11 @@ static void di_free(void* p)
         (void)hipHostFree(c->bh);
     if (c->bd)
         (void)hipFree(c->bd);
-    for (int s = 0; c->have_ev && s < 2; ++s) {
+    for (int s = 0; c->have_ev && s < RFEC_HB_SLOTS; ++s)
         for (int i = 0; i < 4; ++i)
             (void)hipEventDestroy(c->ev[s][i]);
+    for (int s = 0; c->have_ev && s < 2; ++s)
         (void)hipStreamDestroy(c->bstream[s]);
-    }
     if (c->stream)
         (void)hipStreamDestroy(c->stream);
     free(c);

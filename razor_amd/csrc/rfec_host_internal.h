@@ -38,6 +38,10 @@ void parallel_for(size_t n, int threads, pf_fn fn, void* arg);
 #define DI_MAXK RFEC_MAX_K_ENCODE /* staging slots: a whole encode group, or the recover jobs' slots */
 
 /* one pinned, device-mapped staging area per calling thread */
+/* staging slots of the host-memory batch paths: 2 for the staged forms, 3
+ * for the zero-copy forms (chunk c+2 is queued while chunk c still decodes
+ * and scatters) */
+#define RFEC_HB_SLOTS 3
 typedef struct {
     int device;
     hipStream_t stream;
@@ -51,7 +55,7 @@ typedef struct {
     uint8_t* bd;
     size_t bh_bytes, bd_bytes; /* the two pinned / device staging slots, together */
     hipStream_t bstream[2];
-    hipEvent_t ev[2][4];
+    hipEvent_t ev[RFEC_HB_SLOTS][4];
     int have_ev;
 } di_ctx;
 di_ctx* di_get(void);

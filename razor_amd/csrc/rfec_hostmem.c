@@ -53,25 +53,35 @@ static hb_layout hb_offsets(uint32_t G, uint32_t k, uint32_t n)
 /* two staging slots: host_slot bytes of pinned memory and dev_slot bytes of
  * device memory each (the recover path keeps device-only regions past the
  * host-mirrored ones, so dev_slot >= host_slot there) */
-static int hb_reserve(di_ctx* c, size_t host_slot, size_t dev_slot)
+static int hb_reserve(di_ctx* c, size_t host_slot, size_t dev_slot, uint32_t nslot)
 {
     hipError_t e;
     if (!c->have_ev) {
-        for (int s = 0; s < 2; ++s) {
-            if ((e = hipStreamCreateWithFlags(&c->bstream[s], hipStreamNonBlocking)) != hipSuccess)
+        /* stream 0 at the lowest priority: the zero-copy paths run their PCIe-bound
+         * gathers on it, and the encode / decode and scatters queued on stream 1
+         * then get CUs at once instead of waiting behind the gathers' waves (the
+         * highest priority is the resident service's queue) */
+        int prio_lo = 0, prio_hi = 0;
+        if ((e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi)) != hipSuccess)
+            return set_err(RFEC_EDEVICE, "stream priorities", e);
+        for (int s = 0; s < 2; ++s)
+            if ((e = s == 0 ? hipStreamCreateWithPriority(&c->bstream[s], hipStreamNonBlocking, prio_lo)
+                            : hipStreamCreateWithFlags(&c->bstream[s], hipStreamNonBlocking)) != hipSuccess)
                 return set_err(RFEC_EDEVICE, "stream create", e);
+        for (int s = 0; s < RFEC_HB_SLOTS; ++s)
             for (int i = 0; i < 4; ++i)
                 if ((e = hipEventCreate(&c->ev[s][i])) != hipSuccess)
                     return set_err(RFEC_EDEVICE, "event create", e);
-        }
         c->have_ev = 1;
     }
-    if (c->bh_bytes < 2 * host_slot) {
+    host_slot *= nslot;
+    dev_slot *= nslot;
+    if (c->bh_bytes < host_slot) {
         if (c->bh)
             (void)hipHostFree(c->bh);
         c->bh = c->bh_dev = NULL;
         c->bh_bytes = 0;
-        if ((e = hipHostMalloc((void**)&c->bh, 2 * host_slot, hipHostMallocDefault)) != hipSuccess)
+        if ((e = hipHostMalloc((void**)&c->bh, host_slot, hipHostMallocDefault)) != hipSuccess)
             return set_err(RFEC_ENOMEM, "pinned staging", e);
         void* d = NULL;
         if ((e = hipHostGetDevicePointer(&d, c->bh, 0)) != hipSuccess || !d) {
@@ -80,16 +90,16 @@ static int hb_reserve(di_ctx* c, size_t host_slot, size_t dev_slot)
             return set_err(RFEC_EDEVICE, "pinned staging: no device address", e);
         }
         c->bh_dev = (uint8_t*)d;
-        c->bh_bytes = 2 * host_slot;
+        c->bh_bytes = host_slot;
     }
-    if (c->bd_bytes < 2 * dev_slot) {
+    if (c->bd_bytes < dev_slot) {
         if (c->bd)
             (void)hipFree(c->bd);
         c->bd = NULL;
         c->bd_bytes = 0;
-        if ((e = hipMalloc((void**)&c->bd, 2 * dev_slot)) != hipSuccess)
+        if ((e = hipMalloc((void**)&c->bd, dev_slot)) != hipSuccess)
             return set_err(RFEC_ENOMEM, "device staging", e);
-        c->bd_bytes = 2 * dev_slot;
+        c->bd_bytes = dev_slot;
     }
     return RFEC_OK;
 }
@@ -316,14 +326,14 @@ static int zc_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
     chunk = chunk > groups ? groups : chunk;
     const uint32_t nch = (groups + chunk - 1) / chunk;
     const hz_layout L = hz_offsets(chunk, k, n);
-    int rc = hb_reserve(c, L.host_total, L.total);
+    int rc = hb_reserve(c, L.host_total, L.total, RFEC_HB_SLOTS);
     if (rc)
         return rc;
     double tab_us = 0, h2d_us = 0, kernel_us = 0, d2h_us = 0;
     const double t0 = now_us();
-    for (uint32_t it = 0; it < nch + 2 && rc == RFEC_OK; ++it) {
-        if (it >= 2) { /* retire chunk it - 2: its slot may be refilled */
-            const uint32_t s = (it - 2) & 1;
+    for (uint32_t it = 0; it < nch + RFEC_HB_SLOTS && rc == RFEC_OK; ++it) {
+        if (it >= RFEC_HB_SLOTS) { /* retire chunk it - RFEC_HB_SLOTS: its slot may be refilled */
+            const uint32_t s = (it - RFEC_HB_SLOTS) % RFEC_HB_SLOTS;
             const hipError_t e = hipEventSynchronize(c->ev[s][3]);
             if (e != hipSuccess) {
                 rc = set_err(RFEC_EDEVICE, "zero-copy encode wait", e);
@@ -339,7 +349,7 @@ static int zc_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
         }
         if (it >= nch)
             continue;
-        const uint32_t s = it & 1, g0 = it * chunk, ng = it == nch - 1 ? groups - g0 : chunk;
+        const uint32_t s = it % RFEC_HB_SLOTS, g0 = it * chunk, ng = it == nch - 1 ? groups - g0 : chunk;
         uint8_t* h = c->bh + (size_t)s * L.host_total;
         uint8_t* dv = c->bd + (size_t)s * L.total;
         hipStream_t ga = c->bstream[0], gb = c->bstream[1]; /* gathers; encode + scatter */
@@ -433,7 +443,7 @@ int rfec_host_encode_groups(const rfec_plan* plan, uint32_t groups, sim_segment_
     chunk = chunk > groups ? groups : chunk;
     const uint32_t nch = (groups + chunk - 1) / chunk;
     const hb_layout L = hb_offsets(chunk, k, n);
-    if ((rc = hb_reserve(c, L.total, L.total)))
+    if ((rc = hb_reserve(c, L.total, L.total, 2)))
         return rc;
     const int threads = host_threads();
     double gather_us = 0, scatter_us = 0, h2d_us = 0, kernel_us = 0, d2h_us = 0;
@@ -754,17 +764,17 @@ static int zc_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
     chunk = chunk > groups ? groups : chunk;
     const uint32_t nch = (groups + chunk - 1) / chunk;
     const hy_layout L = hy_offsets(plan, chunk, E);
-    int rc = hb_reserve(c, L.host_total, L.total);
+    int rc = hb_reserve(c, L.host_total, L.total, RFEC_HB_SLOTS);
     if (rc)
         return rc;
     rfec_kmask M;
     make_masks(plan, &M);
     double tab_us = 0, h2d_us = 0, kernel_us = 0, d2h_us = 0, out_us = 0;
     const double t0 = now_us();
-    for (uint32_t it = 0; it < nch + 2 && rc == RFEC_OK; ++it) {
-        if (it >= 2) { /* retire chunk it - 2: its out_index / recovered masks to the caller */
-            const uint32_t s = (it - 2) & 1, g0 = (it - 2) * chunk;
-            const uint32_t ng = it - 2 == nch - 1 ? groups - g0 : chunk;
+    for (uint32_t it = 0; it < nch + RFEC_HB_SLOTS && rc == RFEC_OK; ++it) {
+        if (it >= RFEC_HB_SLOTS) { /* retire chunk it - RFEC_HB_SLOTS: its out_index / recovered masks to the caller */
+            const uint32_t s = (it - RFEC_HB_SLOTS) % RFEC_HB_SLOTS, g0 = (it - RFEC_HB_SLOTS) * chunk;
+            const uint32_t ng = it - RFEC_HB_SLOTS == nch - 1 ? groups - g0 : chunk;
             const hipError_t e = hipEventSynchronize(c->ev[s][3]);
             if (e != hipSuccess) {
                 rc = set_err(RFEC_EDEVICE, "zero-copy recover wait", e);
@@ -787,7 +797,7 @@ static int zc_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
         }
         if (it >= nch)
             continue;
-        const uint32_t s = it & 1, g0 = it * chunk, ng = it == nch - 1 ? groups - g0 : chunk;
+        const uint32_t s = it % RFEC_HB_SLOTS, g0 = it * chunk, ng = it == nch - 1 ? groups - g0 : chunk;
         uint8_t* h = c->bh + (size_t)s * L.host_total;
         uint8_t* dv = c->bd + (size_t)s * L.total;
         hipStream_t ga = c->bstream[0], gb = c->bstream[1]; /* gathers; decode + scatter */
@@ -927,7 +937,7 @@ int rfec_host_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
     chunk = chunk > groups ? groups : chunk;
     const uint32_t nch = (groups + chunk - 1) / chunk;
     const hr_layout L = hr_offsets(plan, chunk, E);
-    if ((rc = hb_reserve(c, L.host_total, L.total)))
+    if ((rc = hb_reserve(c, L.host_total, L.total, 2)))
         return rc;
     rfec_kmask M;
     make_masks(plan, &M);
