@@ -104,6 +104,10 @@ __device__ __forceinline__ v4u bld16(__amdgpu_buffer_rsrc_t r, uint32_t off)
 {
     return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxNT));
 }
+__device__ __forceinline__ v4u bld16_l2(__amdgpu_buffer_rsrc_t r, uint32_t off) // default policy (kept in L2)
+{
+    return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
 
 // Payload-block index, XCD-swizzled.  Workgroups are dispatched round-robin
 // over the 8 XCDs (block b runs on XCD b % 8, each XCD with its own L2); the
@@ -313,8 +317,10 @@ struct MatrixShape {
 // NR: members l COL + q; column c = l - NR: c + q COL (K >= 2 COL here, so no
 // column has fewer than 2 members).  Loads take the default policy: the
 // column lanes' second reads are meant to hit L2.  At c3 full (10 reads : 7
-// writes per group) 233-235 us, the time of a 10 : 7 streaming probe over
-// contiguous streams (rfec_probe_mix: 235 us): the mix's HBM ceiling.
+// writes per group) 228-230 us with the unused member slots predicated off
+// through a buffer descriptor (round 5; 234-237 us when they re-read member
+// 0; non-temporal loads on the rows, the columns or both: 239-242 us,
+// profiles/r05/ab/encode_pred/).
 // Measured slower: one lane per (group, chunk) loading each member once, all
 // seven parity chunks through LDS and stored as one contiguous run per block
 // (238-239 us, round 4); the same with seven direct stores per lane (252-260
@@ -343,15 +349,20 @@ __global__ __launch_bounds__(kBlock) void k_encode_matrix_out(const v4u* __restr
     const uint32_t c = l - NR;
     const uint32_t first = row ? l * COL : c, step = row ? 1u : (uint32_t)COL;
     const uint32_t count = row ? min((uint32_t)COL, K - l * COL) : (K - c + COL - 1) / COL;
-    const v4u* s = shards + ((size_t)g * K + first) * C + j;
+    // member loads through a descriptor over the wave's first group, an unused
+    // slot predicated off (kNoLoad reads 0 without a memory access), default
+    // policy: the column lanes' second reads are meant to hit L2
+    const uint32_t gb = (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
+    const __amdgpu_buffer_rsrc_t rs = wave_rsrc(shards + (size_t)gb * K * C);
+    const uint32_t o0 = (((g - gb) * K + first) * C + j) * 16u;
     v4u v[M];
 #pragma unroll
-    for (int q = 0; q < M; ++q) // unconditional (an unused slot re-reads member 0), default policy
-        v[q] = s[(uint32_t)q < count ? (size_t)q * step * C : 0];
+    for (int q = 0; q < M; ++q)
+        v[q] = bld16_l2(rs, (uint32_t)q < count ? o0 + (uint32_t)q * step * C * 16u : kNoLoad);
     v4u acc = v[0];
 #pragma unroll
     for (int q = 1; q < M; ++q)
-        acc ^= (uint32_t)q < count ? v[q] : v4u{0, 0, 0, 0};
+        acc ^= v[q];
     st16(parity + ((size_t)g * (NR + COL) + l) * C + j, acc);
 }
 
@@ -366,7 +377,9 @@ __global__ __launch_bounds__(kBlock) void k_encode_matrix_out(const v4u* __restr
 // edge.  Row layouts have no member in two lines, so no chunk is loaded twice.
 // 165-171 us vs 178-211 us flat at k = 10 / 1,200 B, equal to a 10-read :
 // 3-write probe over contiguous streams; XCD-swizzled blocks: 168 vs 172 us,
-// HBM traffic 1.029 vs 1.059 x algorithmic.
+// HBM traffic 1.029 vs 1.059 x algorithmic.  Round 5: the last row's absent
+// members predicated off through a buffer descriptor instead of per-load
+// branches: 163-166 vs 166-168 us (profiles/r05/ab/encode_pred/).
 // ---------------------------------------------------------------------------
 template <int K, int COL>
 __global__ __launch_bounds__(kBlock) void k_encode_out(const v4u* __restrict__ shards, v4u* __restrict__ parity,
@@ -385,17 +398,19 @@ __global__ __launch_bounds__(kBlock) void k_encode_out(const v4u* __restrict__ s
     const uint32_t rem = t - g * divRC.d;
     const uint32_t r = fdiv(rem, divC);
     const uint32_t j = rem - r * divC.d;
-    const v4u* s = shards + ((size_t)g * K + (size_t)r * COL) * C + j;
+    // member loads predicated through a descriptor (the last row's missing
+    // members read 0 without a memory access), not per-load branches
+    const uint32_t gb = (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
+    const __amdgpu_buffer_rsrc_t rs = wave_rsrc(shards + (size_t)gb * K * C);
+    const uint32_t o0 = (((g - gb) * K + r * COL) * C + j) * 16u;
     v4u v[COL];
 #pragma unroll
     for (int q = 0; q < COL; ++q)
-        if (q < LAST || r < (uint32_t)(R - 1))
-            v[q] = ld16(s + (size_t)q * C);
+        v[q] = bld16(rs, (q < LAST || r < (uint32_t)(R - 1)) ? o0 + (uint32_t)q * C * 16u : kNoLoad);
     v4u acc = v[0];
 #pragma unroll
     for (int q = 1; q < COL; ++q)
-        if (q < LAST || r < (uint32_t)(R - 1))
-            acc ^= v[q];
+        acc ^= v[q];
     st16(parity + ((size_t)g * R + r) * C + j, acc);
 }
 
