@@ -33,11 +33,11 @@ step bench_c5 400 python bench.py --config c5 --no-cpu
 step rocprof_stats_c3full 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c3full" -o run -- python bench.py --config c3full --no-cpu --steps 20 --warmup 5
 step rocprof_stats_c5 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5" -o run -- python bench.py --config c5 --no-cpu --steps 20 --warmup 5
 step mix 200 python tools/mix_probe.py
-if [ -n "$LOCAL" ]; then step e2e 400 taskset -c "$LOCAL" python tools/e2e_step.py
-else step e2e 400 python tools/e2e_step.py; fi
+if [ -n "$LOCAL" ]; then step e2e 400 taskset -c "$LOCAL" python tools/e2e_step.py --mem both
+else step e2e 400 python tools/e2e_step.py --mem both; fi
 step wire_bench 300 python tools/wire_bench.py --out "$OUT/wire.json"
 step rocprof_wire 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_wire" -o run -- python tools/wire_bench.py --reps 5
-step pmc_c3 600 python tools/pmc_traffic.py --out "$OUT/traffic_c3.json" -- --steps 10 --warmup 2 --c4-steps 0
+step pmc_c3 600 python tools/pmc_traffic.py --out "$OUT/traffic_c3.json" -- --steps 10 --warmup 2 --c4-steps 0 --sub-steps 0
 step pmc_c5 600 python tools/pmc_traffic.py --out "$OUT/traffic_c5.json" -- --config c5 --steps 10 --warmup 2
 step pmc_c3full 600 python tools/pmc_traffic.py --out "$OUT/traffic_c3full.json" -- --config c3full --steps 10 --warmup 2
 echo done | tee -a "$OUT/steps.log"
