@@ -169,6 +169,11 @@ hipError_t hipEventRecord(hipEvent_t e, hipStream_t s)
     (void)e, (void)s;
     return hipSuccess;
 }
+hipError_t hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned int flags)
+{
+    (void)s, (void)e, (void)flags;
+    return hipSuccess;
+}
 hipError_t hipEventSynchronize(hipEvent_t e)
 {
     (void)e;
