@@ -802,20 +802,30 @@ struct CSched {
 __device__ __forceinline__ uint32_t cs_line(const CSched& S, uint32_t s) { return (S.lines >> (4 * s)) & 15u; }
 __device__ __forceinline__ uint32_t cs_tg(const CSched& S, uint32_t s) { return (uint32_t)(S.tg >> (8 * s)) & 0xffu; }
 
+// Line records (first | stride << 8 | count << 16) and member masks of a plan:
+// from the kernel arguments (any plan; KArgLines), from LDS copies (LdsLines),
+// or arithmetic in the line index for the sender's matrix shapes (MatLines).
+struct KArgLines {
+    const rfec_kmask& M;
+    __device__ uint32_t rec(uint32_t l) const { return reinterpret_cast<const uint32_t*>(M.plan.line)[l]; }
+    __device__ uint64_t mask(uint32_t l) const { return M.mask[l][0]; }
+    __device__ uint32_t nl(uint32_t n) const { return n; }
+};
+
 // The canonical schedule over the masks: a line fires with its parity
 // received, exactly one member missing and one present; lines in `banned`
 // never fire; dense (E > 0): only erased segments of rank < E are targets.
 // MT: the mask word, uint32_t for k <= 32 (half the VALU work), else uint64_t.
-template <typename MT>
-__device__ CSched cascade_schedule(const rfec_kmask& M, uint32_t NL, MT have, uint64_t ppm, uint32_t banned, MT erased,
+template <typename MT, class Lines>
+__device__ CSched cascade_schedule(const Lines& LL, uint32_t NL, MT have, uint64_t ppm, uint32_t banned, MT erased,
                                    uint32_t E)
 {
     CSched S = {0, 0, 0};
     bool progress = true;
     while (progress) {
         progress = false;
-        for (uint32_t l = 0; l < NL; ++l) { // uniform: the masks stay scalar kernel-argument loads
-            const MT m = (MT)M.mask[l][0];
+        for (uint32_t l = 0; l < NL; ++l) { // uniform: the masks stay scalar kernel-argument loads (or constants)
+            const MT m = (MT)LL.mask(l);
             const MT x = m & ~have;
             if (!((ppm >> l) & 1ull) || ((banned >> l) & 1u) || __popcll((uint64_t)x) != 1 || (m & have) == 0)
                 continue;
@@ -862,7 +872,7 @@ __device__ CSched cascade_check(const CascArgs& A, const rfec_kmask& M, uint32_t
     CSched S;
 #pragma unroll 1
     for (uint32_t attempt = 0; attempt <= NL; ++attempt) {
-        S = cascade_schedule<uint64_t>(M, NL, have, ppm, banned, erased, A.E);
+        S = cascade_schedule<uint64_t>(KArgLines{M}, NL, have, ppm, banned, erased, A.E);
         int bad = -1;
 #pragma unroll 1
         for (uint32_t s = 0; s < S.n; ++s) {
@@ -985,9 +995,9 @@ __device__ __forceinline__ CSched cs_unpack(const v4u r)
 // schedule packed.  A group of more than LPG steps (more than LPG erasures
 // recovered) takes the serial exact peel.  Dead lanes (live false) join the
 // shuffles only.
-template <typename MT, int LPG, bool kTasks = true>
-__device__ v4u cascade_check_lanes(const CascArgs& A, const rfec_kmask& M, uint32_t g, bool live, uint32_t s,
-                                   uint32_t base)
+template <typename MT, int LPG, bool kTasks, class Lines>
+__device__ v4u cascade_check_lanes(const CascArgs& A, const rfec_kmask& M, const Lines& LL, uint32_t g, bool live,
+                                   uint32_t s, uint32_t base)
 {
     const uint32_t gg = live ? g : 0u;
     const rfec_kplan& P = M.plan;
@@ -996,10 +1006,10 @@ __device__ v4u cascade_check_lanes(const CascArgs& A, const rfec_kmask& M, uint3
     const MT have = (MT)A.present[2 * gg] & kmask;
     const MT erased = ~have & kmask;
     const uint64_t ppm = A.parity_present[gg];
-    const CSched S = cascade_schedule<MT>(M, NL, have, ppm, 0u, erased, A.E);
+    const CSched S = cascade_schedule<MT>(LL, LL.nl(NL), have, ppm, 0u, erased, A.E);
     const bool on = live && s < S.n;
     const uint32_t l = on ? cs_line(S, s) : 0u, t = cs_tg(S, s);
-    const uint32_t ln = reinterpret_cast<const uint32_t*>(P.line)[l];
+    const uint32_t ln = LL.rec(l);
     const uint32_t first = ln & 0xff, stride = (ln >> 8) & 0xff, count = (ln >> 16) & 0xff;
     const uint32_t* gh = A.hdr_dw + (size_t)gg * K * 5;
     const uint32_t* gm = A.meta_dw + (size_t)gg * NL * 5;
@@ -1032,7 +1042,7 @@ __device__ v4u cascade_check_lanes(const CascArgs& A, const rfec_kmask& M, uint3
     }
     // cascades: the members recovered by earlier steps, folded in step order (step r's record is
     // final before round r); only waves that hold one take the shuffles
-    const MT depm = on ? ((MT)M.mask[l][0] & erased & ~(MT(1) << t)) : MT(0);
+    const MT depm = on ? ((MT)LL.mask(l) & erased & ~(MT(1) << t)) : MT(0);
     if (__ballot(depm != 0)) {
 #pragma unroll
         for (int r = 0; r < LPG - 1; ++r) {
@@ -1094,7 +1104,7 @@ __device__ v4u cascade_check_lanes(const CascArgs& A, const rfec_kmask& M, uint3
             uint32_t w = 0;
             if (ss < 8) {
                 const uint32_t tl = cs_line(X, ss), tt = cs_tg(X, ss);
-                const bool casc = (M.mask[tl][0] & (uint64_t)erased & ~(1ull << tt)) != 0;
+                const bool casc = (LL.mask(tl) & (uint64_t)erased & ~(1ull << tt)) != 0;
                 w = kTaskValid | (casc ? kTaskCascade : 0u) | tl | (tt << 8);
             }
             if (kTasks)
@@ -1117,7 +1127,7 @@ __global__ __launch_bounds__(kBlock) void k_cascade_check(CascArgs A, rfec_kmask
     const uint32_t gt = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t g = gt / kCheckLanes, s = gt % kCheckLanes;
     const bool live = g < A.groups;
-    const v4u r = cascade_check_lanes<MT, kCheckLanes>(A, M, live ? g : 0u, live, s,
+    const v4u r = cascade_check_lanes<MT, kCheckLanes, true>(A, M, KArgLines{M}, live ? g : 0u, live, s,
                                                        (threadIdx.x & (kWave - 1)) & ~(uint32_t)(kCheckLanes - 1));
     if (live && s == 0)
         *reinterpret_cast<v4u*>(A.ws + (size_t)g * A.ws_stride) = r;
@@ -1198,12 +1208,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
 // A dense payload lane whose target no line recovers at once (a cascade):
 // the group's mask schedule (cascade_schedule without the header checks),
 // the steps the target's step reads, transitively, replayed in registers.
-template <typename MT, class Lines>
-__device__ __forceinline__ void cascade_dense_tail(const CascArgs& A, const rfec_kmask& M, uint32_t NL, uint64_t have,
+// (SL: the schedule's masks -- kernel arguments or constants; LL: the replay's)
+template <typename MT, class SLines, class Lines>
+__device__ __forceinline__ void cascade_dense_tail(const CascArgs& A, const SLines& SL, uint32_t NL, uint64_t have,
                                                    uint64_t erased, uint64_t ppm, uint32_t tgt, const v4u* grp,
                                                    const v4u* par, v4u* slot0, v4u* dst, const Lines& LL)
 {
-    const CSched S = cascade_schedule<MT>(M, NL, (MT)have, ppm, 0u, (MT)erased, A.E);
+    const CSched S = cascade_schedule<MT>(SL, NL, (MT)have, ppm, 0u, (MT)erased, A.E);
     uint32_t ss = 8;
 #pragma unroll
     for (int s = 0; s < 8; ++s)
@@ -1253,7 +1264,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         const uint32_t gt = hb * kBlock + threadIdx.x;
         const uint32_t g = gt / kCheckLanes, s = gt % kCheckLanes;
         const bool live = g < A.groups;
-        cascade_check_lanes<MT, kCheckLanes, false>(A, M, live ? g : 0u, live, s,
+        cascade_check_lanes<MT, kCheckLanes, false>(A, M, KArgLines{M}, live ? g : 0u, live, s,
                                                     (threadIdx.x & (kWave - 1)) & ~(uint32_t)(kCheckLanes - 1));
         return;
     }
@@ -1321,7 +1332,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         st16(dst, acc);
         return;
     }
-    cascade_dense_tail<MT>(A, M, NL, have, erased, ppm, tgt, grp, par, slot0, dst, LdsLines{lplan, lmask});
+    cascade_dense_tail<MT>(A, KArgLines{M}, NL, have, erased, ppm, tgt, grp, par, slot0, dst, LdsLines{lplan, lmask});
 }
 
 // The sender's full matrix plans (rows of COL consecutive segments, then the
@@ -1361,6 +1372,7 @@ struct MatLines {
     {
         return l < (uint32_t)NR ? (ROW << (l * COL)) & KM : (COL0 << (l - NR)) & KM;
     }
+    __device__ uint32_t nl(uint32_t) const { return NR + COL; }
 };
 
 template <int K, int COL>
@@ -1375,7 +1387,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         const uint32_t gt = hb * kBlock + threadIdx.x;
         const uint32_t g = gt / kCheckLanes, s = gt % kCheckLanes;
         const bool live = g < A.groups;
-        cascade_check_lanes<uint32_t, kCheckLanes, false>(A, M, live ? g : 0u, live, s,
+        cascade_check_lanes<uint32_t, kCheckLanes, false>(A, M, LL{}, live ? g : 0u, live, s,
                                                           (threadIdx.x & (kWave - 1)) & ~(uint32_t)(kCheckLanes - 1));
         return;
     }
@@ -1427,7 +1439,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         st16(dst, acc);
         return;
     }
-    cascade_dense_tail<uint32_t>(A, M, NL, hv, er, pp, tgt, grp, par, slot0, dst, LL{});
+    cascade_dense_tail<uint32_t>(A, LL{}, NL, hv, er, pp, tgt, grp, par, slot0, dst, LL{});
 }
 
 // ---------------------------------------------------------------------------
