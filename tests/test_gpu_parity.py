@@ -398,6 +398,37 @@ def test_host_encode_groups(product1200, oracle1200, mem):
     _fields_equal(fecs, stale, "fec_data_size", "fec_data")
 
 
+def test_host_zero_copy_eligibility(product1200, oracle1200, monkeypatch):
+    """The zero-copy form runs only when every struct pointer of an array lies
+    in ONE rfec_pinned_alloc block and RFEC_HOST_ZEROCOPY is not "0"; segments
+    split over two pinned blocks, or the variable set, take the staged form --
+    same parities either way (and the oracle's)."""
+    from razor_amd.fec import fec_dtype, seg_dtype
+
+    lib, o = product1200, oracle1200
+    G, k, S = 64, 10, 1200
+    shards, hdr, segs, ks = _host_segs(lib, o, 204, G, k, S, "pinned")
+    plan = o.plan_from_fraction(k, 80, 3)
+    n = plan.n_lines
+    nref, ref = o.encode_aos(plan, G, o.to_aos(shards, hdr))
+    ref = ref.view(fec_dtype(1200)).reshape(-1)
+
+    def run(sp, expect_zc):
+        fecs, kf = _host_arrays(lib, G * n, fec_dtype(1200), "pinned", fill=0x33)
+        t = lib.host_encode_groups(plan, G, sp, _ptrs(fecs), fec_id0=1)
+        assert t["zero_copy"] == expect_zc
+        _fields_equal(fecs, ref, "fec_data_size", "fec_data")
+
+    run(_ptrs(segs), 1)
+    half, kh = _host_arrays(lib, G * k // 2, seg_dtype(1200), "pinned")
+    half[...] = segs[G * k // 2:]
+    split = _ptrs(segs).copy()
+    split[G * k // 2:] = _ptrs(half)
+    run(split, 0)  # two blocks: staged
+    monkeypatch.setenv("RFEC_HOST_ZEROCOPY", "0")
+    run(_ptrs(segs), 0)
+
+
 @pytest.mark.parametrize("mem", ["pageable", "pinned"])
 @pytest.mark.parametrize("k,layers,G", [(10, 1, 301), (10, 3, 301), (10, 3, 4500), (128, 1, 3000)])
 def test_host_recover_groups(product1200, oracle1200, k, layers, G, mem):
