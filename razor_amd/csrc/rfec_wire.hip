@@ -1044,8 +1044,14 @@ __device__ __forceinline__ void store_payload20(const uint32_t* wb, uint8_t* __r
     }
 }
 
-// parse: registers capped for 8 waves per SIMD (two 16-wave blocks per CU)
-constexpr int kParseWaves = 8;
+// parse: 4 waves per SIMD (one 16-wave block per CU), registers for a
+// three-deep datagram pipeline without spills (107 VGPRs).  At the 64-register
+// cap of 8 waves the two-deep kernel spilled 39 VGPRs to scratch; 5 waves
+// (96 registers, no spill) ran as fast as it, 6-7 waves (19-22 spills) slower;
+// three deep at 4 waves: parse_seg 395-400 vs 404-410 us, parse_fec 120-124 vs
+// 125-126 us; four or five deep: no further gain
+// (profiles/r05/ab/parse_occupancy/).
+constexpr int kParseWaves = 4;
 
 template <int B>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWaves))) void k_parse(const uint8_t* __restrict__ dgram,
@@ -1144,12 +1150,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
             store_slot<B>(slot, stride, lane, pay);
         }
     };
-    // Datagrams d0, d0 + nw, ... one per step, the next one's loads issued
-    // before the current one is processed (ping-pong buffers).  A batch's
-    // header pass runs first in its first step (it waits on its own loads
-    // and the current datagram's, already in flight).
+    // Datagrams d0, d0 + nw, ... one per step, the loads of the datagram two
+    // steps ahead issued before the current one is processed (three buffers in
+    // rotation).  A batch's header pass runs first in its first step (it waits
+    // on its own loads and the current datagram's, already in flight).
     auto step = [&](const PW& cur, PW& nxt, uint32_t d) {
-        const uint32_t d1 = d + nw;
+        const uint32_t d1 = d + nw, d2 = d + 2 * nw;
         if (i == (uint32_t)kWave) { // (a batch short of kWave is the wave's last)
             const uint32_t cnt = min((uint32_t)kWave, (n - 1 - d) / nw + 1);
             HdrIn in;
@@ -1160,14 +1166,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kParseWa
             __builtin_amdgcn_s_setprio(0);
             i = 0;
         }
-        load(min(d1, n - 1), nxt); // past the end: the last datagram again (branch-free)
+        load(min(d2, n - 1), nxt); // two ahead; past the end: the last datagram again (branch-free)
         proc(cur, d);
         return d1 < n;
     };
-    PW a, b;
+    PW a, b, c; // datagrams d, d + nw in flight while d is processed, d + 2 nw issued
     load(d0, a);
-    for (uint32_t d = d0;; d += 2 * nw) {
-        if (!step(a, b, d) || !step(b, a, d + nw))
+    load(min(d0 + nw, n - 1), b);
+    for (uint32_t d = d0;; d += 3 * nw) {
+        if (!step(a, c, d) || !step(b, a, d + nw) || !step(c, b, d + 2 * nw))
             break;
     }
 }
