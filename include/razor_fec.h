@@ -333,7 +333,11 @@ typedef struct {
  * `status` may be NULL; a slot with status -1 gets length 0 (the reference
  * never emits that parity).  `order` may be NULL; otherwise datagram i is
  * written to slot order[i] of dgram / dlen (a permutation).  Needs
- * fec_size <= capacity <= stride and dstride >= capacity + 49. */
+ * fec_size <= capacity <= stride and dstride >= capacity + 49.  Datagram
+ * slots whose stride is a multiple of 128 bytes (1,280 for 1,200-byte
+ * payloads) are written in whole 128-byte lines: 0.60 of HBM peak against
+ * 0.52 for the minimal 16-byte multiples, whose slot edges split lines
+ * (DESIGN.md §4). */
 int rfec_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
                         const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,
                         const rfec_fec_stamp* stamps, const uint32_t* order, uint32_t dstride, uint8_t* dgram,

@@ -26,7 +26,7 @@ sys.path[:0] = [str(ROOT), str(ROOT / "oracle")]
 
 from razor_amd.fec import FRAME_DTYPE, WIRE_REC_DTYPE, native  # noqa: E402
 
-S, K, DSTRIDE, STRIDE = 1200, 10, 1264, 1200
+S, K, DSTRIDE, STRIDE = 1200, 10, 1280, 1200
 
 
 def stream(lib, F, loss, window, seed=1):

@@ -46,7 +46,7 @@ def main():
     frames["payload_type"] = 96
     frames["protect_fraction"] = 80
     frames["now_ms"] = 1_700_000_000_000 + np.arange(F) * 33
-    dstride = 1264
+    dstride = 1280  # 10 x 128 B: whole-line datagram stores
     bufs, keep_alive = None, []
     if not args.pageable:  # datagram slots in pinned memory, reused across calls (what a sender hands to sendmmsg)
         ms, mp = CH * k + 128, CH * 8 + 64

@@ -62,11 +62,13 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--lib", default="", help="another build of the library (A/B)")
     ap.add_argument("--dstride", type=int, default=0, help="datagram slot width for both kinds (e.g. 1504: 1500-B receive slots, 32-byte lanes)")
+    ap.add_argument("--stride", type=int, default=0, help="payload slot stride (framing input, parse output; default 1216)")
     ap.add_argument("--out", default="")
     ap.add_argument("--tuning", type=int, default=0, help="rfec_set_tuning bits")
     ap.add_argument("--only", default="", help="comma list of kernels to time (frame_fec,frame_seg,parse_fec,parse_seg)")
     args = ap.parse_args()
     G, k, n, S = args.groups, 10, 3, 1200
+    P = args.stride or 1216  # payload slot stride: the engine's 16-B-aligned FEC slots
     lib = Native(1200, args.lib) if args.lib else native(1200)
     lib.set_tuning(args.tuning)
     dev = torch.device("cuda:0")
@@ -75,8 +77,8 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(5)
     NF, NS = G * n, G * k
-    parity = torch.randint(0, 256, (NF, S), dtype=torch.uint8, device=dev, generator=gen)
-    shards = torch.randint(0, 256, (NS, S), dtype=torch.uint8, device=dev, generator=gen)
+    parity = torch.randint(0, 256, (NF, P), dtype=torch.uint8, device=dev, generator=gen)
+    shards = torch.randint(0, 256, (NS, P), dtype=torch.uint8, device=dev, generator=gen)
     rng = np.random.default_rng(3)
     meta = np.zeros(NF, HDR_DTYPE)
     meta["seq"] = rng.integers(0, 2**31, NF)
@@ -99,29 +101,31 @@ def main():
     sstamp["transport_seq"] = np.arange(NS)
     to = lambda a: torch.from_numpy(a.view(np.uint8).reshape(-1).copy()).to(dev)  # noqa: E731
     d_meta, d_fs, d_fst, d_hdr, d_sst = to(meta), to(np.full(NF, S, np.uint16)), to(fstamp), to(hdr), to(sstamp)
-    DF, DS = (args.dstride, args.dstride) if args.dstride else (1264, 1248)  # slots: >= 1249 / >= 1236, multiples of 16
+    # datagram slots: 1,280 B (10 x 128: whole-line stores; the minimal 16-B multiples, 1,264 / 1,248, leave
+    # slot edges inside 128-B lines and frame at 0.52-0.53 of peak against 0.60-0.61)
+    DF, DS = (args.dstride, args.dstride) if args.dstride else (1280, 1280)
     dg_f = torch.empty((NF, DF), dtype=torch.uint8, device=dev)
     dl_f = torch.empty((NF,), dtype=torch.int16, device=dev)
     dg_s = torch.empty((NS, DS), dtype=torch.uint8, device=dev)
     dl_s = torch.empty((NS,), dtype=torch.int16, device=dev)
     rec_f = torch.empty((NF, 64), dtype=torch.uint8, device=dev)
-    pay_f = torch.empty((NF, S), dtype=torch.uint8, device=dev)
+    pay_f = torch.empty((NF, P), dtype=torch.uint8, device=dev)
     rec_s = torch.empty((NS, 64), dtype=torch.uint8, device=dev)
-    pay_s = torch.empty((NS, S), dtype=torch.uint8, device=dev)
+    pay_s = torch.empty((NS, P), dtype=torch.uint8, device=dev)
 
     def frame_fec():
-        lib.wire_frame_fec(NF, S, S, parity.data_ptr(), d_meta.data_ptr(), d_fs.data_ptr(), None, d_fst.data_ptr(),
+        lib.wire_frame_fec(NF, P, S, parity.data_ptr(), d_meta.data_ptr(), d_fs.data_ptr(), None, d_fst.data_ptr(),
                            DF, dg_f.data_ptr(), dl_f.data_ptr(), sp)
 
     def frame_seg():
-        lib.wire_frame_seg(NS, S, S, shards.data_ptr(), d_hdr.data_ptr(), d_sst.data_ptr(), DS, dg_s.data_ptr(),
+        lib.wire_frame_seg(NS, P, S, shards.data_ptr(), d_hdr.data_ptr(), d_sst.data_ptr(), DS, dg_s.data_ptr(),
                            dl_s.data_ptr(), sp)
 
     def parse_f():
-        lib.wire_parse(NF, DF, dg_f.data_ptr(), dl_f.data_ptr(), S, S, rec_f.data_ptr(), pay_f.data_ptr(), sp)
+        lib.wire_parse(NF, DF, dg_f.data_ptr(), dl_f.data_ptr(), P, S, rec_f.data_ptr(), pay_f.data_ptr(), sp)
 
     def parse_s():
-        lib.wire_parse(NS, DS, dg_s.data_ptr(), dl_s.data_ptr(), S, S, rec_s.data_ptr(), pay_s.data_ptr(), sp)
+        lib.wire_parse(NS, DS, dg_s.data_ptr(), dl_s.data_ptr(), P, S, rec_s.data_ptr(), pay_s.data_ptr(), sp)
 
     with torch.cuda.stream(st):
         for f in (frame_fec, frame_seg, parse_f, parse_s):
@@ -143,7 +147,8 @@ def main():
                          "algorithmic_bytes": alg[name], "GBps": round(alg[name] / med / 1e9, 1),
                          "frac_of_hbm_peak": round(alg[name] / med / 1e9 / HBM_PEAK, 4)}
     # verification: parse(frame(x)) == x everywhere
-    ok = bool(torch.equal(pay_f, parity) and torch.equal(pay_s, shards))
+    ok = bool(torch.equal(pay_f[:, :S], parity[:, :S]) and torch.equal(pay_s[:, :S], shards[:, :S]))
+    ok = ok and not bool(pay_f[:, S:].any()) and not bool(pay_s[:, S:].any())  # slot tails zeroed
     rf = rec_f.cpu().numpy()
     rs = rec_s.cpu().numpy()
     ok = ok and bool((rf[:, 0] == 0).all() and (rs[:, 0] == 0).all())
@@ -152,13 +157,13 @@ def main():
     from pyoracle import Oracle
     o = Oracle(1200)
     idx = np.r_[0:64, NF // 2:NF // 2 + 64, NF - 64:NF]
-    og, ol = o.frame_fec_batch(parity[idx].cpu().numpy(), meta[idx], np.full(len(idx), S, np.uint16), None,
+    og, ol = o.frame_fec_batch(np.ascontiguousarray(parity[idx, :S].cpu().numpy()), meta[idx], np.full(len(idx), S, np.uint16), None,
                                fstamp[idx], S, DF)
     ok = ok and bool(np.array_equal(dg_f[idx].cpu().numpy(), og))
     idx = np.r_[0:64, 65530:65600, NS - 64:NS]
-    og, ol = o.frame_seg_batch(shards[idx].cpu().numpy(), hdr[idx], sstamp[idx], S, DS)
+    og, ol = o.frame_seg_batch(np.ascontiguousarray(shards[idx, :S].cpu().numpy()), hdr[idx], sstamp[idx], S, DS)
     ok = ok and bool(np.array_equal(dg_s[idx].cpu().numpy(), og))
-    out = {"groups": G, "k": k, "r": n, "payload": S, "fec_datagrams": NF, "seg_datagrams": NS,
+    out = {"groups": G, "k": k, "r": n, "payload": S, "payload_stride": P, "fec_datagrams": NF, "seg_datagrams": NS,
            "dstride": {"fec": DF, "seg": DS}, "kernels": res, "verified": ok,
            "timing": ("the kernel's own start / stop (rfec_timing_events)" if hasattr(lib.lib, "rfec_timing_events")
                       else "stream events around each call")}
