@@ -655,6 +655,9 @@ int rfec_rx_session_get_info(const rfec_rx_session* s, rfec_rx_session_info* inf
  * (k = 6..16) takes the plan-driven cascade kernel instead of the one
  * compiled for its shape (the A/B and cross-check of the latter). */
 #define RFEC_TUNE_PLAN_CASCADE (1u << 2)
+/* RFEC_TUNE_WAVE_PARSE: rfec_wire_parse takes the wave-per-datagram kernel
+ * instead of the quarter-wave one (the A/B and cross-check of the latter). */
+#define RFEC_TUNE_WAVE_PARSE (1u << 3)
 /* RFEC_TUNE_NO_SERVICE: the drop-in symbols (flex_fec_generate / _recover, the
  * group-level sender and receiver) launch their kernels per call instead of
  * posting to the resident service (process-wide; also RFEC_SERVICE=0 in the

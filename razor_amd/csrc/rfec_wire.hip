@@ -9,9 +9,10 @@
 //                 yield 0 without advancing (cf_stream.c mach_*_read)
 //   crc32         cf_crc32.c:56-68, seed 0x0e3dfc0a (sim_proto.c:11)
 //
-// Framing into datagram slots of at most 1,280 bytes: the quarter-wave
-// kernels at the end of this file (k_frame_seg_q, k_frame_fec_q: 16 lanes per
-// datagram, four datagrams per wave).  The parse, and framing into wider
+// Framing into, and parsing of, datagram slots of at most 1,280 bytes: the
+// quarter-wave kernels at the end of this file (k_frame_seg_q, k_frame_fec_q,
+// k_parse_q: 16 lanes per datagram, four datagrams per wave).  The parse of
+// wider payload slots (and with RFEC_TUNE_WAVE_PARSE), and framing into wider
 // slots: one wavefront per datagram; lane j owns bytes [B j, B j + B) of it,
 // B = 20 when the slot holds at most 1,280 bytes (a 1,249-byte SIM_FEC or
 // 1,236-byte SIM_SEG at 1,200-byte payloads then keeps 63 of 64 lanes busy),
@@ -1704,6 +1705,221 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     }
 }
 
+// ---------------------------------------------------------------------------
+// Quarter-wave parse (slots of at most 1,280 bytes, or datagrams that fit
+// 1,280 bytes; payload slots of at most 1,280 bytes): the framing's layout
+// run backwards.  A wave parses four consecutive datagrams, 16 lanes each;
+// lane s of group g holds 16-byte chunks c = 16 k + s (k = 0..4) of datagram
+// 4 q + g, aligned b128 loads, no LDS staging.
+//
+// Headers: a per-lane pass over the wave's next 64 datagrams (lane 4 t + g =
+// quad t's datagram g) decodes each header as if its CRC matched (decode_lane,
+// as k_parse), writes the record and keeps the packed facts (length, data
+// position, data size) and the big-endian trailer (one b64 load at the
+// trailer's dword); each quad takes its datagram's two dwords by ds_bpermute.
+//
+// CRC32 over [0, len - 4): the framing's (Horner over the five rows, one carry
+// by column s + Dq, one x^(-8 Dr) correction, row-level DPP XORs) on the
+// chunks with the bytes from len - 4 on masked, against the trailer.
+//
+// Payload: the data starts at byte `at` = 16 A + r of the datagram (26-32 for
+// a SIM_SEG, 45 for a SIM_FEC).  The lane that holds datagram chunk C produces
+// payload chunk j = (C - A) mod 80: its own chunk and the next one (lane s + 1
+// of the row, a row_ror:15 DPP move; lane 15 takes lane 0's of the next row)
+// shifted down by r bytes in registers, masked at the data size, one aligned
+// b128 store -- every payload chunk of the slot is produced by exactly one
+// lane, so the zeros to the slot's end come out of the same stores (the A
+// chunks that wrap round are past any data).  The payload is stored as if the
+// CRC matched; a group whose CRC fails (rare) zeroes its slot afterwards and
+// rewrites its record as EBADCRC.
+// ---------------------------------------------------------------------------
+// (rin: a descriptor over the whole batch, per-lane offsets < 2^32; the second
+// dword may lie in the next slot, or past the batch: 0)
+__device__ __forceinline__ uint32_t load_trailer(__amdgpu_buffer_rsrc_t rin, uint32_t d, uint32_t len, bool active,
+                                                 uint32_t dstride)
+{
+    if (!active || len < 4 || len > dstride)
+        return 0;
+    const uint32_t tp = len - 4;
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rin, d * dstride + (tp & ~3u), 0, kAuxNT);
+    return bswap(__builtin_amdgcn_alignbyte(v[1], v[0], tp & 3u));
+}
+
+// bytes >= m of one 16-byte chunk (byte offset c0 in its message) zeroed
+__device__ __forceinline__ uint32_t keep_below(uint32_t v, int j, int e)
+{
+    const uint32_t t8 = 8u * (uint32_t)min(max(e - 4 * j, 0), 4);
+    return v & ~(uint32_t)(0xFFFFFFFFull << t8);
+}
+
+// 4 waves per SIMD: the next quad's rows in flight beside this quad's (125
+// VGPRs, no spill).  Capped at 64 VGPRs for 8 waves it spilled 53 and ran
+// 8-13 % slower than the wave-per-datagram parse; at 4 waves: parse_seg
+// 361 vs 386-389 us, parse_fec 111-113 vs 122-123 us against that kernel's
+// three-deep 4-wave form (profiles/r05/ab/parse_occupancy/).
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_parse_q(
+    const uint8_t* __restrict__ dgram, const uint16_t* __restrict__ dlen, rfec_wire_rec* __restrict__ recs,
+    uint8_t* __restrict__ payload, uint32_t n, uint32_t dstride, uint32_t stride, uint32_t capacity)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t T[kQTabDwords];
+    {
+        const v4u* src = reinterpret_cast<const v4u*>(&kCrcQ);
+        v4u* dst = reinterpret_cast<v4u*>(T);
+        for (int i = threadIdx.x; i < kQTabDwords / 4; i += kBlock)
+            dst[i] = src[i];
+        __syncthreads();
+    }
+    const uint32_t lane = threadIdx.x & (kWave - 1), g = lane >> 4, s = lane & 15u;
+    const uint32_t nquads = (n + 3u) / 4u;
+    const uint32_t nw = gridDim.x * kWavesPerBlock;
+    uint32_t q = wave_id();
+    if (q >= nquads)
+        return;
+    const __amdgpu_buffer_rsrc_t rin = rsrc64(dgram, (uint64_t)n * dstride);
+    const __amdgpu_buffer_rsrc_t rout = rsrc64(payload, (uint64_t)n * stride);
+    constexpr uint32_t kOut = 0xFFFFFFF0u;
+    const uint32_t rows_in = min(dstride, kQWindow); // the slot's bytes a lane may load
+    uint32_t F = 0, TR = 0, bt = 0;
+    // the headers of quads q0, q0 + nw, ... (16 of them), one datagram per lane
+    auto header_pass = [&](uint32_t q0) {
+        const uint32_t dd = 4u * (q0 + (lane >> 2) * nw) + (lane & 3u);
+        const bool a = dd < n;
+        __builtin_amdgcn_s_setprio(3);
+        HdrIn in;
+        load_header(dgram, dlen, dd, a, dstride, in);
+        TR = load_trailer(rin, dd, in.len, a, dstride);
+        F = decode_header<20>(in, recs, dd, a, dstride, capacity);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    // row k of quad qq's datagram (a lane past the batch or the slot reads 0 without a memory access)
+    auto load_row = [&](uint32_t qq, int k) {
+        const uint32_t dd = 4u * qq + g, o = 16u * (16u * k + s);
+        return __builtin_bit_cast(
+            v4u, __builtin_amdgcn_raw_buffer_load_b128(rin, qq < nquads && dd < n && o < rows_in ? dd * dstride + o
+                                                                                             : kOut,
+                                                       0, kAuxNT));
+    };
+    // The next quad's rows are loaded as soon as this quad's are consumed, and
+    // before this quad's payload stores: vmcnt counts loads and stores in issue
+    // order, so a load issued after a store can only be waited for together
+    // with that store (loads issued after the previous quad's stores wait for
+    // their write acknowledgements).  Only a batch's first quad, whose header
+    // pass runs after the stores (no row registers live across it), loads after.
+    header_pass(q);
+    v4u X[kQRows];
+#pragma unroll
+    for (int k = 0; k < kQRows; ++k)
+        X[k] = load_row(q, k);
+    for (;;) {
+        const uint32_t d = 4u * q + g;
+        const bool act = d < n;
+        const uint32_t src = 4u * bt + g;
+        const uint32_t f = bperm(F, src), tr = bperm(TR, src);
+        ++bt;
+        const bool valid = (f & kPkValid) != 0;
+        const uint32_t len = f & 0xfffu, at1 = (f >> 12) & 63u, dsize = (f >> 18) & 0xfffu;
+        const uint32_t nb = valid ? len - 4u : 0u;
+        const uint32_t at = at1 ? at1 - 1u : 0u, A = at >> 4, r = at & 15u;
+        const uint32_t dsz = at1 ? dsize : 0u;
+        // One pass over the rows: row k's CRC (Horner, the bytes from nb on
+        // masked, the seed folded into the first dword) and its payload chunk
+        // (j = (C - A) mod 80 from chunks C, C + 1 shifted down by r; stored
+        // as if the CRC matched).
+        __builtin_amdgcn_s_setprio(3);
+        uint32_t acc = 0;
+        v4u Y[kQRows]; // the payload chunks
+        uint32_t PO[kQRows];
+#pragma unroll
+        for (int k = 0; k < kQRows; ++k) {
+            {
+                const int e = (int)nb - (int)(16u * (16u * k + s));
+                uint32_t x[4] = {X[k][0], X[k][1], X[k][2], X[k][3]};
+                if (__builtin_amdgcn_ballot_w64(e < 16) != 0) { // (wave-uniform: a message ends in this row)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        x[j] = keep_below(x[j], j, e);
+                }
+                x[0] ^= k == 0 && s == 0 ? ~RFEC_WIRE_CRC_SEED : 0u;
+                acc = (k ? mul_row(T, acc) : 0u) ^ slice16(T, x[0], x[1], x[2], x[3]);
+            }
+            // window: own chunk w[0..3], the next one w[4..7] (lane s + 1 of the row; lane 15: lane 0 of
+            // the next row, which row_ror:15 of that row's register brings to lane 15)
+            uint32_t w[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                w[i] = X[k][i];
+                const uint32_t a = dpp(X[k][i], kDppRowRor15);
+                const uint32_t b = k + 1 < kQRows ? dpp(X[k + 1 < kQRows ? k + 1 : k][i], kDppRowRor15) : 0u;
+                w[4 + i] = s == 15 ? b : a;
+            }
+            // shift down by r: 8 bytes, 4 bytes, then the byte funnel.  The selects are byte permutes with a
+            // per-lane selector (all bytes of one operand or the other): selects over array elements are
+            // otherwise folded into an indexed access, i.e. the window in scratch
+            const uint32_t s8 = (r & 8u) ? 0x07060504u : 0x03020100u, s4 = (r & 4u) ? 0x07060504u : 0x03020100u;
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+                w[i] = __builtin_amdgcn_perm(w[i + 2], w[i], s8);
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+                w[i] = __builtin_amdgcn_perm(w[i + 1], w[i], s4);
+            const uint32_t C = 16u * k + s;
+            const uint32_t jj = C >= A ? C - A : C + kQChunks - A; // payload chunk
+            const int e = (int)dsz - (int)(16u * jj);               // its data bytes
+            uint32_t y[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                y[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], r & 3u);
+            if (__builtin_amdgcn_ballot_w64(e < 16) != 0) { // (wave-uniform: some lane's data ends here)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    y[i] = keep_below(y[i], i, e);
+            }
+            const uint32_t po = 16u * jj;
+            Y[k] = v4u{y[0], y[1], y[2], y[3]};
+            PO[k] = act && po < stride ? d * stride + po : kOut;
+        }
+        const uint32_t D = kQWindow - nb, Dq = D >> 4, Dr = D & 15u;
+        const uint32_t R = row_xor(carry_q(T, acc, s + Dq));
+        const uint32_t* iv = T + kQInv + Dr * 32u;
+        const uint32_t b = (((R >> s) & 1u) ? iv[s] : 0u) ^ (((R >> (s + 16u)) & 1u) ? iv[s + 16u] : 0u);
+        const bool ok = valid && ~row_xor(b) == tr;
+        __builtin_amdgcn_s_setprio(0);
+        const uint32_t qn = q + nw;
+        const bool batch_end = bt == 16; // (wave-uniform) the next quad starts a header batch
+        if (!batch_end) {
+#pragma unroll
+            for (int k = 0; k < kQRows; ++k)
+                X[k] = load_row(qn, k);
+        }
+#pragma unroll
+        for (int k = 0; k < kQRows; ++k)
+            __builtin_amdgcn_raw_buffer_store_b128(Y[k], rout, PO[k], 0, kAuxST);
+        if (valid && !ok && act) { // rare: a CRC mismatch -- zero the slot, the record reads EBADCRC
+            __builtin_amdgcn_s_waitcnt(0); // after this wave's header-pass record and payload stores
+#pragma unroll
+            for (int k = 0; k < kQRows; ++k) {
+                const uint32_t po = 16u * (16u * k + s);
+                __builtin_amdgcn_raw_buffer_store_b128(v4u{0, 0, 0, 0}, rout, po < stride ? d * stride + po : kOut,
+                                                       0, kAuxST);
+            }
+            if (s < 4) { // the record's four 16-byte pieces: status EBADCRC (byte 0), every other field 0
+                static_assert(RFEC_WIRE_EBADCRC == -1 && offsetof(rfec_wire_rec, status) == 0, "record layout");
+                reinterpret_cast<v4u*>(recs + d)[s] = v4u{s == 0 ? 0xFFu : 0u, 0u, 0u, 0u};
+            }
+        }
+        q = qn;
+        if (q >= nquads)
+            break;
+        if (batch_end) {
+            header_pass(q);
+            bt = 0;
+#pragma unroll
+            for (int k = 0; k < kQRows; ++k)
+                X[k] = load_row(q, k);
+        }
+    }
+}
+
 // Persistent grid: exactly the blocks that are resident at once (occupancy
 // from the kernel's registers / LDS x CUs), so no block waits for a second
 // round; fewer when the batch is small.  TAG: one cache per kernel instance.
@@ -1776,6 +1992,16 @@ int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, c
                            uint32_t max_len, void* stream)
 {
     hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
+    // quarter-wave: the first 1,280 bytes of a slot, enough when the slot or every datagram fits;
+    // payload slots of at most 1,280 bytes; both arrays within 32-bit buffer offsets
+    const bool fits = dstride <= kQWindow || (max_len && max_len <= kQWindow);
+    if (fits && stride <= kQWindow && !(rfec_get_tuning() & RFEC_TUNE_WAVE_PARSE) &&
+        (uint64_t)n * dstride + kQWindow < 0xFFFFFFF0ull && (uint64_t)n * stride < 0xFFFFFFF0ull) {
+        const uint32_t quads = (n + 3u) / 4u;
+        RFEC_LAUNCH(k_parse_q, dim3(grid_for<8>((const void*)k_parse_q, quads)), dim3(kBlock), 0, sm, dgram, dlen,
+                    recs, payload, n, dstride, stride, capacity);
+        return (int)hipGetLastError();
+    }
     // 20-byte lanes cover 1,280 bytes of a slot: enough when the slot or every datagram fits
     if (narrow(dstride) || (max_len && max_len <= (uint32_t)(kWave * 20)))
         RFEC_LAUNCH(k_parse<20>, dim3(grid_for<4>((const void*)k_parse<20>, n)), dim3(kBlock), 0, sm, dgram,

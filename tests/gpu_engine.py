@@ -110,7 +110,7 @@ class GpuWire:
     def __init__(self, video_size=1000, device="cuda:0", tuning=0):
         self.lib = native(video_size)
         self.device = torch.device(device)
-        self.tuning = tuning  # rfec_set_tuning bits for the parse
+        self.tuning = tuning  # RFEC_TUNE_WAVE_PARSE: the wave-per-datagram parse
 
     def _run(self, fn, *args):
         fn(*args, torch.cuda.current_stream(self.device).cuda_stream)

@@ -79,6 +79,19 @@ def gwire():
     return GpuWire()
 
 
+RFEC_TUNE_WAVE_PARSE = 1 << 3
+
+
+@pytest.fixture(params=["quarter", "wave"])
+def pwire(request):
+    """The parse both ways: the quarter-wave kernel (default) and the
+    wave-per-datagram one (RFEC_TUNE_WAVE_PARSE), the cross-check."""
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the -m gpu suite must run on an MI355X")
+    from gpu_engine import GpuWire
+    return GpuWire(tuning=0 if request.param == "quarter" else RFEC_TUNE_WAVE_PARSE)
+
+
 @pytest.mark.gpu
 def test_wire_frame_fec_gpu(gwire):
     wc.check_frame_fec(gwire)
@@ -90,12 +103,13 @@ def test_wire_frame_seg_gpu(gwire):
 
 
 @pytest.mark.gpu
-def test_wire_parse_gpu(gwire):
-    wc.check_parse(gwire)
+def test_wire_parse_gpu(pwire):
+    wc.check_parse(pwire)
 
 
 @pytest.mark.gpu
-def test_wire_short_datagram_gpu(gwire):
+def test_wire_short_datagram_gpu(pwire):
+    gwire = pwire
     dgram = np.full((5, 64), 0xAB, np.uint8)
     recs, pay = gwire.parse(dgram, np.array([0, 1, 2, 3, 4], np.uint16), wc.STRIDE, wc.CAP)
     assert (recs["status"][:4] == -1).all() and not pay.any()
@@ -112,13 +126,15 @@ def test_wire_short_datagram_gpu(gwire):
                                                        (1000, 1008, 1056, 3001), (230, 240, 288, 2051),
                                                        (1200, 1280, 1280, 2050), (1200, 1200, 1504, 2049),
                                                        (1300, 1312, 1360, 1025)])
-def test_wire_parse_mixed_gpu(gwire, oracle1000, capacity, stride, dstride, N):
+def test_wire_parse_mixed_gpu(pwire, oracle1000, capacity, stride, dstride, N):
     """The parse against the oracle on batches that mix SIM_SEG (every header
     width: data at bytes 26-32) and SIM_FEC (data at 45) datagrams in random
-    order with flipped bytes (CRC mismatches: record EBADCRC, slot zero), lengths
+    order -- a quarter-wave quad holds datagrams with different data offsets
+    -- with flipped bytes (CRC mismatches: record EBADCRC, slot zero), lengths
     cut short or past the slot, data sizes that overrun the datagram, control
-    messages and bad message ids; slots of 1,056-1,504 bytes, payload slots
-    up to 1,280 bytes."""
+    messages and bad message ids; slots of 1,248-1,504 bytes (wider than 1,280:
+    the datagrams still fit, the quarter-wave parse reads the first 1,280),
+    payload slots up to 1,280 bytes, N not a multiple of 4."""
     rng = np.random.default_rng(capacity + stride * 3 + dstride * 7 + N)
     frames, lens = [], []
     for seg in (True, False):
@@ -149,7 +165,7 @@ def test_wire_parse_mixed_gpu(gwire, oracle1000, capacity, stride, dstride, N):
         dgram[i, 1] = rng.choice([0x10, 0x12, 0x1D, 0x05, 0x40])
         crc = oracle1000.crc32(dgram[i, :L - 4].tobytes())
         dgram[i, L - 4:L] = np.frombuffer(crc.to_bytes(4, "big"), np.uint8)
-    recs, pay = gwire.parse(dgram, dlen, stride, capacity)
+    recs, pay = pwire.parse(dgram, dlen, stride, capacity)
     orecs, opay = oracle1000.parse_batch(dgram, dlen, stride, capacity)
     bad = np.nonzero((recs.view(np.uint8).reshape(n, 64) != orecs.view(np.uint8).reshape(n, 64)).any(1))[0]
     assert len(bad) == 0, (bad[:8], recs[bad[:2]], orecs[bad[:2]])
