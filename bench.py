@@ -621,7 +621,8 @@ def kernel_desc(w, k, S, full_plan):
         dec_kernels = (f"{dense_k} (one launch: checker blocks spread over the payload lanes, one "
                        "lane per (group, output slot, chunk))" if w.dense else
                        "k_cascade_check + k_decode_cascade (one lane per (group, schedule step, chunk))")
-    elif cd >= 64 and rows_layout and (k, lines[0]) in ((10, 4), (32, 4)):
+    elif rows_layout and (k, lines[0]) in ((10, 4), (32, 4)) and (cd >= 64 or (w.dense and 2 <= len(lines)
+                                                                              and cd >= 16)):
         dec_kernels = f"k_decode_rows<{k},{lines[0]}> ({per}; header blocks spread)"
     elif cd >= 64:
         dec_kernels = f"k_decode_out ({per}; header blocks spread)"

@@ -2313,12 +2313,15 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
         const FusedArgs F = {sh, pp, total, C, f, n_hdr, st, DO};
         // output-mapped (a lane per (group, line or slot, chunk)) where a line's slot spans at least a wave
         // of chunks; below that most of its lanes would sit on lines that do not fire (k = 32 / 256 B, 2
-        // erasures: 6 of 8 rows idle, 60.0 vs 41.6 us flat), so the flat form
-        if (cd >= (uint32_t)kWave && (uint64_t)groups * P.n_lines * cd < (1ull << 32)) {
-            uint32_t col = 0;
-            // dense output: lanes per output slot (no lane on a line that does not fire)
-            const bool slots = F.D.E && F.D.E <= P.n_lines;
-            if (!generic && is_row_layout(&P, &col) && col <= 4 && P.k <= 64) {
+        // erasures: 6 of 8 rows idle, 60.0 vs 41.6 us flat), so the flat form -- except a dense output of
+        // row layouts with slots of >= 16 chunks: lanes per output slot sit on no idle line (k = 32 /
+        // 256 B: 33.2-33.9 vs 34.6-34.9 us flat, round 5)
+        uint32_t col = 0;
+        const bool slots = F.D.E && F.D.E <= P.n_lines; // dense output: lanes per output slot
+        const bool rows = !generic && is_row_layout(&P, &col) && col <= 4 && P.k <= 64;
+        if ((cd >= (uint32_t)kWave || (slots && rows && cd >= 16)) &&
+            (uint64_t)groups * P.n_lines * cd < (1ull << 32)) {
+            if (rows) {
                 if (P.k == 10 && col == 4)
                     launch_fused_rows<10, 4>(F, B, *M, cd, slots);
                 else if (P.k == 32 && col == 4)
