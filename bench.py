@@ -179,11 +179,39 @@ class Workload:
             self.out_hdr = torch.empty((G, 2, 20), dtype=torch.uint8, device=dev)
             self.out_index = torch.empty((G, 2), dtype=torch.uint8, device=dev)
         self.ws = torch.empty((lib.workspace_size(self.plan, launch_groups or G),), dtype=torch.uint8, device=dev)
+        # packed erasure records (rfec_recover_packed_out), for row layouts: see use_packed
+        self.packed = False
+        self.pks = lib.packed_stride(self.plan, 2) if self.dense else 0
+        self.packed_rec = None
         # algorithmic payload bytes (headers excluded): encode reads k*S, writes r*S
         self.enc_bytes = G * (k + self.n) * S
         # decode: per recovered segment read its line's other members + the parity, write 1
         pair_bytes = np.array([peel_bytes(self.plan, k, tuple(p), S) for p in pairs.tolist()], np.int64)
         self.dec_bytes = int(pair_bytes[pick].sum())
+
+    def use_packed(self, on):
+        """Decode from packed erasure records (rfec_pack_erasures' layout: per
+        group the masks, then per output slot its row's meta, fec_data_size
+        and other members' records) instead of the batch layout's header
+        arrays.  The records are built once the parity exists (prepare(), before
+        timing: a receiver writes them as segments arrive, as the batch layout's
+        arrays are written).  The outputs are poisoned so verify() sees this
+        path's results."""
+        assert not on or self.pks, "packed records need a dense row-layout decode"
+        self.packed = on
+        if on and self.packed_rec is None:
+            self.packed_rec = torch.empty((self.G, self.pks), dtype=torch.uint8, device=self.shards.device)
+        if on:
+            for t in (self.out_shards, self.out_hdr, self.out_index, self.recovered):
+                t.view(torch.uint8).fill_(0xEE)
+
+    def prepare(self, stream):
+        """Untimed, after the priming encode: the packed records from this set's
+        received headers, masks and the encode's meta / fec_data_size."""
+        if self.packed:
+            self.lib.pack_erasures(self.plan, self.G, self.rx_hdr.data_ptr(), self.present.data_ptr(),
+                                   self.meta.data_ptr(), self.fsize.data_ptr(), self.parity_present.data_ptr(), 2,
+                                   self.packed_rec.data_ptr(), stream)
 
     def _chunks(self):
         """(first group, groups) of each launch: the whole batch, or launches of
@@ -203,7 +231,15 @@ class Workload:
     def decode(self, stream):
         k, n, st = self.k, self.n, self.stride
         for g0, g in self._chunks():
-            if self.dense:
+            if self.packed:
+                self.lib.recover_packed_out(self.plan, g, st, self.S, self.rx.data_ptr() + g0 * k * st,
+                                            self.parity.data_ptr() + g0 * n * st,
+                                            self.packed_rec.data_ptr() + g0 * self.pks,
+                                            self.recovered.data_ptr() + g0 * 16, 2,
+                                            self.out_shards.data_ptr() + g0 * 2 * st,
+                                            self.out_hdr.data_ptr() + g0 * 40, self.out_index.data_ptr() + g0 * 2,
+                                            stream)
+            elif self.dense:
                 self.lib.recover_batch_out(self.plan, g, st, self.S, self.rx.data_ptr() + g0 * k * st,
                                            self.rx_hdr.data_ptr() + g0 * k * 20, self.present.data_ptr() + g0 * 16,
                                            self.parity.data_ptr() + g0 * n * st, self.meta.data_ptr() + g0 * n * 20,
@@ -484,6 +520,8 @@ def time_steps(lib, sets, steps, warmup, stream, dist, timing, hot):
 
     for ws in sets:  # every set holds its parity before the first (cold) decode
         ws.encode(sp)
+    for ws in sets:
+        ws.prepare(sp)
     for i in range(warmup):
         sets[i % nset].encode(sp)
         dec_set(i).decode(sp)
@@ -613,6 +651,11 @@ def kernel_desc(w, k, S, full_plan):
     else:
         enc_kernel = "k_encode (plan-driven)"
     cd = (S + 15) // 16
+    if w.packed:
+        kt = f"{k},{lines[0]}" if (k, lines[0]) in ((10, 4), (32, 4)) else "0,4 (run-time k, col)"
+        return enc_kernel, (f"k_decode_rows<{kt}> packed (rfec_recover_packed_out: one lane per (group, output "
+                            "slot, chunk); header lanes per (group, output slot) on the packed erasure records, "
+                            "spread)"), lines, rows_layout
     per = ("one lane per (group, output slot, chunk)" if w.dense and 2 <= len(lines)
            else "one lane per (group, line, chunk)")
     if full_plan:
@@ -657,8 +700,21 @@ def config_sub(lib, name, device, stream, dist, world, rank, pf, steps, warmup, 
             want = golden_digest(cfg["golden"], 1, 0)
             digest_ok = None if want is None else w.digest() == want
             verified = verified and digest_ok is not False
+    # row layouts: the same steps again with the decode on packed erasure records (rfec_recover_packed_out)
+    t_pk, pk_ok = 0.0, -1
+    if w.pks:
+        for ws in sets:
+            ws.use_packed(True)
+        _, _, t_dec_pk, _, own_pk = time_steps(lib, sets, steps, warmup, stream, dist, "own", False)
+        t_pk = float(t_dec_pk.mean()) * 1e6 if own_pk else -1.0
+        if verify:
+            pk_ok = int(all(ws.verify() for ws in sets))
+            verified = verified and bool(pk_ok)
+        pk_kernels = kernel_desc(w, k, S, full_plan)[1]
+        for ws in sets:
+            ws.use_packed(False)
     per_rank = torch.tensor([w.enc_bytes + w.dec_bytes, float(t_enc.mean()) * 1e6, float(t_dec.mean()) * 1e6,
-                             -1 if verified is None else int(verified)], dtype=torch.float64)
+                             -1 if verified is None else int(verified), t_pk, pk_ok], dtype=torch.float64)
     rows = [per_rank]
     if dist:
         rows = [torch.zeros_like(per_rank) for _ in range(world)]
@@ -686,6 +742,15 @@ def config_sub(lib, name, device, stream, dist, world, rank, pf, steps, warmup, 
                "decode": {"kernels": dec_kernels, "launch_us": round(dec_us, 2),
                           "frac": round(w.dec_bytes / (dec_us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
                           "traffic": load_traffic(wn, "decode")},
+               "decode_packed": None if not w.pks else {
+                   "kernels": pk_kernels, "input": "packed erasure records (rfec_pack_erasures layout, "
+                   f"{w.pks} B per group), built before timing; the same steps and outputs",
+                   "launch_us": round(float(rows[0][4]), 2) if float(rows[0][4]) > 0 else None,
+                   "frac": round(w.dec_bytes / (float(rows[0][4]) * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
+                   if float(rows[0][4]) > 0 else None,
+                   "traffic": load_traffic(wn + "+packed", "decode"),
+                   "launch_us_per_rank": [round(float(r[4]), 2) for r in rows],
+                   "verified": None if not verify else all(int(r[5]) == 1 for r in rows)},
                "encode_us_per_rank": [round(float(r[1]), 2) for r in rows],
                "decode_us_per_rank": [round(float(r[2]), 2) for r in rows],
                "timing": "per launch: " + (TIMING_OWN if own_enc and own_dec else TIMING_BRACKET),
@@ -724,6 +789,8 @@ def main():
     ap.add_argument("--full-plan", action="store_true", help="custom: rows + columns of the reference plan")
     ap.add_argument("--in-place", action="store_true",
                     help="decode into the received shards (rfec_recover_batch) instead of a dense output")
+    ap.add_argument("--packed-decode", action="store_true",
+                    help="dense row-layout decodes from packed erasure records (rfec_recover_packed_out)")
     ap.add_argument("--hot-decode", action="store_true",
                     help="decode the set encoded in the same step (its parity still MALL-resident)")
     ap.add_argument("--c4-steps", type=int, default=10,
@@ -787,6 +854,11 @@ def main():
                      stride=args.stride or None, col=col, full_plan=full_plan, config_id=cfg["config_id"],
                      in_place=args.in_place)
             for _ in range(max(1, args.sets))]
+    if args.packed_decode:
+        if not sets[0].pks:
+            raise SystemExit("bench.py: --packed-decode needs a dense decode of a row layout (rows of <= 4, k <= 64)")
+        for ws in sets:
+            ws.use_packed(True)
     w = sets[0]
     nset = len(sets)
     stream = torch.cuda.current_stream(device)
@@ -911,13 +983,14 @@ def main():
             "encode_read_only_frac": round(w.G * w.k * w.S / enc_mean / 1e9 / HBM_PEAK_GBPS, 4),
             "decode_gibps": round(w.dec_bytes / dec_mean / 2**30, 2),
             "decode_output": ("dense: rfec_recover_batch_out, recovered segments to [G][2] slots (flex_fec_recover's "
-                              "out_seg); the received shards read only" if w.dense else "in place: rfec_recover_batch"),
+                              "out_seg); the received shards read only" if w.dense else "in place: rfec_recover_batch")
+            + ("; header input: packed erasure records (rfec_recover_packed_out)" if w.packed else ""),
             "decode_roofline": {"achieved": round(w.dec_bytes / dec_mean / 1e9, 1), "frac":
                                 round(w.dec_bytes / dec_mean / 1e9 / HBM_PEAK_GBPS, 4),
                                 "launch_us": round(dec_mean * 1e6, 2),
                                 "launch_us_median": round(float(np.median(t_dec)) * 1e6, 2),
                                 "timing": TIMING_OWN if own_dec else TIMING_BRACKET,
-                                "traffic": load_traffic(workload_name, "decode"),
+                                "traffic": load_traffic(workload_name + ("+packed" if w.packed else ""), "decode"),
                                 "kernels": dec_kernels,
                                 "parity_operand": "cold: written one step (>= 1.7 GB of traffic) before"
                                 if not (args.hot_decode or nset == 1) else "hot: written by this step's encode"},

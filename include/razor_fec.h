@@ -219,6 +219,41 @@ int rfec_recover_batch_out(const rfec_plan* plan, uint32_t groups, uint32_t stri
                            void* stream);
 
 /*
+ * Packed erasure records: the header input of rfec_recover_batch_out for row
+ * layouts (rows of `col` consecutive segments and no columns -- strip mode or
+ * the row layer alone, flex_fec_sender.c:166-190; k <= 64, col <= 4) laid out
+ * per erased segment, so a decode reads one contiguous run per group instead
+ * of the present / parity_present / fec_size / meta / hdr arrays, whose
+ * sectors it shares with the rows that do not fire.  Group g's record,
+ * rfec_packed_stride(plan, per_group) bytes (a multiple of 64) at
+ * packed + g * stride:
+ *   +0   u64 present         bit i = segment i was received
+ *   +8   u64 parity_present  bit r = row r's parity was received
+ *   +16 + e * S, e < per_group, S = 24 + 20 (col - 1): the group's e-th erased
+ *        segment (index order), in row r:
+ *        rfec_hdr meta of row r; u16 fec_data_size of row r; u16 0;
+ *        rfec_hdr of row r's other members in index order (zeros past the
+ *        row's end).  All zeros where the group has fewer than e + 1 erasures.
+ *   zeros up to the stride.
+ * A receiver that knows the plan can write these as segments and parities
+ * arrive (each segment's record goes to the slot of every erased segment of
+ * its row); rfec_pack_erasures builds them from the batch layout.
+ * rfec_recover_packed_out then gives rfec_recover_batch_out's results for the
+ * same batch (out_shards, out_hdr, out_index, recovered) with no workspace.
+ * rfec_packed_stride returns 0 for a plan outside the row layouts above or a
+ * per_group outside [1, k].  (razor's flex_fec_receiver.c:105-206 reads the
+ * same fields per line; the layout is this library's.)
+ */
+size_t rfec_packed_stride(const rfec_plan* plan, uint32_t per_group);
+int rfec_pack_erasures(const rfec_plan* plan, uint32_t groups, const rfec_hdr* hdr, const uint64_t* present,
+                       const rfec_hdr* meta, const uint16_t* fec_size, const uint64_t* parity_present,
+                       uint32_t per_group, uint8_t* packed, void* stream);
+int rfec_recover_packed_out(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
+                            const uint8_t* shards, const uint8_t* parity, const uint8_t* packed,
+                            uint64_t* recovered, uint32_t per_group, uint8_t* out_shards, rfec_hdr* out_hdr,
+                            uint8_t* out_index, void* stream);
+
+/*
  * Host-resident batch: the path that starts and ends in host memory (segments
  * built from UDP socket buffers, sim_session.c).  Gathers G groups of
  * sim_segment_t (segs[g*k + i], this library's SIM_VIDEO_SIZE layout) into a

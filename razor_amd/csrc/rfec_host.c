@@ -311,6 +311,99 @@ int rfec_recover_batch_out(const rfec_plan* plan, uint32_t groups, uint32_t stri
     return e ? set_err(RFEC_EDEVICE, "recover launch", e) : RFEC_OK;
 }
 
+/* the row width of a plan the packed records cover (rows of col <= 4 consecutive segments, no columns,
+ * k <= 64), else 0 */
+static uint32_t packed_col(const rfec_plan* p)
+{
+    if (!p || p->k == 0 || p->k > 64 || p->n_lines == 0)
+        return 0;
+    const uint32_t col = p->line[0].count;
+    if (col < 2 || col > 4 || p->n_lines != (p->k + col - 1) / col)
+        return 0;
+    for (uint32_t l = 0; l < p->n_lines; ++l) {
+        const uint32_t first = l * col, count = p->k - first < col ? p->k - first : col;
+        if (p->line[l].first != first || p->line[l].stride != 1 || p->line[l].count != count)
+            return 0;
+    }
+    return col;
+}
+
+size_t rfec_packed_stride(const rfec_plan* plan, uint32_t per_group)
+{
+    const uint32_t col = packed_col(plan);
+    if (!col || per_group == 0 || per_group > plan->k)
+        return 0;
+    return ((16u + per_group * (24u + 20u * (col - 1u))) + 63u) & ~(size_t)63u;
+}
+
+/* the checks both packed entry points share; sets *col and *pk_stride */
+static int packed_check(const rfec_plan* plan, uint32_t groups, uint32_t per_group, const void* packed,
+                        uint32_t* col, size_t* pk_stride)
+{
+    int rc = check_plan(plan, RFEC_MAX_K);
+    if (rc)
+        return rc;
+    *col = packed_col(plan);
+    if (!*col)
+        return set_err(RFEC_EINVAL, "packed records need a row layout (rows of <= 4 segments, k <= 64)", 0);
+    if (per_group == 0 || per_group > plan->k)
+        return set_err(RFEC_EINVAL, "per_group must be in [1, k]", 0);
+    *pk_stride = rfec_packed_stride(plan, per_group);
+    unsigned lg = 0;
+    while ((1u << lg) < per_group)
+        ++lg;
+    if (((uint64_t)groups << lg) >= (1ull << 32) || (uint64_t)groups * *pk_stride >= (1ull << 40))
+        return set_err(RFEC_EINVAL, "batch too large for one launch (groups x slots)", 0);
+    if (groups && (!packed || (uintptr_t)packed % 16))
+        return set_err(RFEC_EINVAL, "packed records: NULL or not 16-byte aligned", 0);
+    return RFEC_OK;
+}
+
+int rfec_pack_erasures(const rfec_plan* plan, uint32_t groups, const rfec_hdr* hdr, const uint64_t* present,
+                       const rfec_hdr* meta, const uint16_t* fec_size, const uint64_t* parity_present,
+                       uint32_t per_group, uint8_t* packed, void* stream)
+{
+    uint32_t col;
+    size_t pks;
+    int rc = packed_check(plan, groups, per_group, packed, &col, &pks);
+    if (rc)
+        return rc;
+    if (groups == 0)
+        return RFEC_OK;
+    if (!hdr || !present || !meta || !fec_size || !parity_present)
+        return set_err(RFEC_EINVAL, "NULL buffer", 0);
+    const int e = rfec_launch_pack_rows(plan, col, groups, hdr, present, meta, fec_size, parity_present, per_group,
+                                        packed, (uint32_t)pks, 24u + 20u * (col - 1u), stream);
+    return e ? set_err(RFEC_EDEVICE, "pack launch", e) : RFEC_OK;
+}
+
+int rfec_recover_packed_out(const rfec_plan* plan, uint32_t groups, uint32_t stride, uint32_t capacity,
+                            const uint8_t* shards, const uint8_t* parity, const uint8_t* packed,
+                            uint64_t* recovered, uint32_t per_group, uint8_t* out_shards, rfec_hdr* out_hdr,
+                            uint8_t* out_index, void* stream)
+{
+    uint32_t col;
+    size_t pks;
+    int rc = packed_check(plan, groups, per_group, packed, &col, &pks);
+    if (rc)
+        return rc;
+    if ((rc = check_geometry(groups, stride, capacity, plan->k)))
+        return rc;
+    const uint32_t cd = capacity ? (capacity + 15) / 16 : 1;
+    if ((uint64_t)groups * per_group * cd >= (1ull << 32) || (uint64_t)65 * plan->k * stride >= 0x7FFFFFF0ull)
+        return set_err(RFEC_EINVAL, "batch too large for one launch (groups x slots x chunks)", 0);
+    if (groups == 0)
+        return RFEC_OK;
+    if (!shards || !parity || !recovered || !out_shards || !out_hdr || !out_index)
+        return set_err(RFEC_EINVAL, "NULL buffer", 0);
+    static __thread rfec_kmask M;
+    make_masks(plan, &M);
+    const rfec_dense_out D = {out_shards, out_hdr, out_index, per_group};
+    const int e = rfec_launch_recover_packed(&M, col, groups, stride, capacity, shards, parity, packed, (uint32_t)pks,
+                                             24u + 20u * (col - 1u), recovered, &D, stream);
+    return e ? set_err(RFEC_EDEVICE, "recover launch", e) : RFEC_OK;
+}
+
 int rfec_zero_tails(uint32_t groups, uint32_t k, uint32_t stride, uint8_t* shards, const rfec_hdr* hdr,
                     void* stream)
 {

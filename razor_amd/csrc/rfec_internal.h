@@ -55,6 +55,16 @@ static inline size_t rfec_ws_bytes(uint32_t k, uint32_t n_lines, uint32_t groups
 {
     return (size_t)groups * rfec_sched_record_bytes(k, n_lines);
 }
+/* packed erasure records (rfec_pack_erasures / rfec_recover_packed_out): row layouts, rows of `col` <= 4,
+ * k <= 64; group records of pk_stride bytes, slot records of pk_slot = 24 + 20 (col - 1) bytes */
+int rfec_launch_pack_rows(const rfec_kplan* P, uint32_t col, uint32_t groups, const rfec_hdr* hdr,
+                          const uint64_t* present, const rfec_hdr* meta, const uint16_t* fsize,
+                          const uint64_t* parity_present, uint32_t per_group, uint8_t* packed, uint32_t pk_stride,
+                          uint32_t pk_slot, void* stream);
+int rfec_launch_recover_packed(const rfec_kmask* M, uint32_t col, uint32_t groups, uint32_t stride,
+                               uint32_t capacity, const uint8_t* shards, const uint8_t* parity, const uint8_t* packed,
+                               uint32_t pk_stride, uint32_t pk_slot, uint64_t* recovered,
+                               const rfec_dense_out* out, void* stream);
 int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
                                const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,
                                const rfec_fec_stamp* stamps, const uint32_t* order, uint32_t dstride,

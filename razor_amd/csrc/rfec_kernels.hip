@@ -488,6 +488,10 @@ struct PeelArgs {
     rfec_hdr* out_hdr;
     uint8_t* out_index;
     uint32_t out_per_group;
+    // packed erasure records (rfec_recover_packed_out): group g's record at
+    // packed + g * pk_stride, slot e's at + 16 + e * pk_slot; null: the batch layout
+    const uint8_t* packed;
+    uint32_t pk_stride, pk_slot;
 };
 
 // Payload side of the dense output: out slot (g * E + e) of `sh` (E == 0: in place).
@@ -1563,6 +1567,69 @@ __device__ void line_headers(const PeelArgs& A, const rfec_kmask& M, uint32_t bl
     }
 }
 
+// Header lanes of the packed decode (rfec_recover_packed_out), one per (group,
+// output slot e): 2^nlp_log2 >= E consecutive lanes per group.  Slot e's
+// record holds the fec_meta, fec_data_size and the other members' records of
+// the row of the group's e-th erased segment, so a lane's header bytes are one
+// contiguous run after the group's two masks (line_headers reads them from
+// three arrays: the meta and member runs in sectors shared with the lines that
+// do not fire).  The checks and the recovered record are line_headers'.
+template <int COL>
+__device__ void packed_headers(const PeelArgs& A, uint32_t blk, uint32_t KK, uint32_t CC)
+{
+    const uint32_t ep = 1u << A.nlp_log2;
+    const uint32_t hl = blk * kBlock + threadIdx.x;
+    const uint32_t g = hl >> A.nlp_log2, e = hl & (ep - 1);
+    uint64_t rec = 0;
+    if (g < A.groups && e < A.out_per_group) {
+        const uint8_t* pg = A.packed + (size_t)g * A.pk_stride;
+        const uint64_t h = reinterpret_cast<const uint64_t*>(pg)[0], pp = reinterpret_cast<const uint64_t*>(pg)[1];
+        uint64_t m = ~h & (KK == 64 ? ~0ull : (1ull << KK) - 1ull);
+        for (uint32_t u = 0; u < e; ++u) // the e-th erased segment
+            m &= m - 1ull;
+        uint32_t v = 0xFF;
+        if (m) {
+            const uint32_t tgt = (uint32_t)__ffsll((long long)m) - 1, r = tgt / CC;
+            const uint32_t R = (KK + CC - 1) / CC, cnt = r + 1 < R ? CC : KK - (R - 1) * CC;
+            const uint64_t rm = ((1ull << cnt) - 1ull) << (r * CC);
+            if (__popcll(rm & ~h) == 1 && (rm & h) && ((pp >> r) & 1ull)) {
+                const uint32_t* sr = reinterpret_cast<const uint32_t*>(pg + 16 + (size_t)e * A.pk_slot);
+                uint32_t r0 = sr[0], r1 = sr[1], r2 = sr[2], r3 = sr[3], r4 = sr[4];
+                const uint32_t L = sr[5] & 0xFFFFu;
+                uint32_t w[COL - 1][5];
+#pragma unroll
+                for (int q = 0; q < COL - 1; ++q) // one round of loads, as line_headers
+#pragma unroll
+                    for (int d = 0; d < 5; ++d)
+                        w[q][d] = (uint32_t)q + 1 < cnt ? sr[6 + 5 * q + d] : 0u;
+                bool ok = L <= A.capacity;
+#pragma unroll
+                for (int q = 0; q < COL - 1; ++q) {
+                    r0 ^= w[q][0];
+                    r1 ^= w[q][1];
+                    r2 ^= w[q][2];
+                    r3 ^= w[q][3];
+                    r4 ^= w[q][4];
+                    ok = ok && (w[q][4] >> 16) <= L;
+                }
+                if (ok && (r4 >> 16) <= L) {
+                    uint32_t* ht = reinterpret_cast<uint32_t*>(A.out_hdr + (size_t)g * A.out_per_group + e);
+                    ht[0] = r0, ht[1] = r1, ht[2] = r2, ht[3] = r3, ht[4] = r4;
+                    v = tgt;
+                    rec = 1ull << tgt;
+                }
+            }
+        }
+        A.out_index[(size_t)g * A.out_per_group + e] = (uint8_t)v;
+    }
+    for (uint32_t sh = 1; sh < ep; sh <<= 1)
+        rec |= __shfl_xor(rec, sh);
+    if (g < A.groups && e == 0) {
+        A.recovered[2 * g] = rec;
+        A.recovered[2 * g + 1] = 0;
+    }
+}
+
 // Header blocks of the fused decodes: every (every + 1)-th block until they
 // run out (every == 0: the first n_hdr of the grid), spread over the grid so
 // their latency-bound chains overlap the payload stream (cold: k = 32 / 256 B
@@ -1811,7 +1878,9 @@ __global__ __launch_bounds__(kBlock) void k_decode_out(v4u* shards, const v4u* _
 // (traffic 1.077 vs 1.107 x algorithmic at k = 10 / 1,200 B).
 // K = 0: k and col at run time (k_rt <= 64, col_rt <= COL), the member loads
 // unrolled to COL and predicated on the row's size (the strip-mode plans).
-template <int K, int COL, bool SLOTS>
+// PK (with SLOTS): the masks and header records from the packed erasure
+// records (rfec_recover_packed_out), header lanes packed_headers.
+template <int K, int COL, bool SLOTS, bool PK = false>
 __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* __restrict__ parity, uint32_t total,
                                                         uint32_t C, FastDiv divC, FastDiv divRC,
                                                         uint32_t n_hdr_blocks, uint32_t hdr_every, PeelArgs A,
@@ -1819,13 +1888,18 @@ __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* 
                                                         uint32_t col_rt, FastDiv divCol)
 {
     static_assert(K <= 64, "row decode keeps the present mask in one word");
+    static_assert(!PK || SLOTS, "packed records are per output slot");
+    const uint32_t KK = K ? (uint32_t)K : k_rt, CC = K ? (uint32_t)COL : col_rt;
     uint32_t hb, pb;
     if (header_block_xcd((n_hdr_blocks + 7u) >> 3, hdr_every, npay8, &hb, &pb)) {
-        if (hb < n_hdr_blocks)
-            line_headers(A, M, hb);
+        if (hb < n_hdr_blocks) {
+            if constexpr (PK)
+                packed_headers<COL>(A, hb, KK, CC);
+            else
+                line_headers(A, M, hb);
+        }
         return;
     }
-    const uint32_t KK = K ? (uint32_t)K : k_rt, CC = K ? (uint32_t)COL : col_rt;
     const uint32_t R = (KK + CC - 1) / CC, LAST = KK - (R - 1) * CC;
     const uint32_t t = pb * kBlock + threadIdx.x;
     if (t >= total)
@@ -1834,7 +1908,14 @@ __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* 
     const uint32_t rem = t - g * divRC.d;
     const uint32_t q0 = fdiv(rem, divC); // row, or output slot (SLOTS)
     const uint32_t j = rem - q0 * divC.d;
-    const uint64_t h = A.present[2 * g];
+    uint64_t h, ppm = 0;
+    if constexpr (PK) { // the record's two masks: one 16-B load
+        const uint64_t* pg = reinterpret_cast<const uint64_t*>(A.packed + (size_t)g * A.pk_stride);
+        h = pg[0];
+        ppm = pg[1];
+    } else {
+        h = A.present[2 * g];
+    }
     uint32_t r, tgt;
     if constexpr (SLOTS) {
         uint64_t m = ~h & (KK == 64 ? ~0ull : (1ull << KK) - 1ull);
@@ -1850,7 +1931,7 @@ __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* 
     const uint32_t cnt = r + 1 < R ? CC : LAST;
     const uint64_t rm = ((1ull << cnt) - 1ull) << (r * CC);
     const uint64_t miss = rm & ~h;
-    if (__popcll(miss) != 1 || !((A.parity_present[g] >> r) & 1ull))
+    if (__popcll(miss) != 1 || !(((PK ? ppm : A.parity_present[g]) >> r) & 1ull))
         return;
     if constexpr (!SLOTS)
         tgt = (uint32_t)__ffsll((long long)miss) - 1;
@@ -1876,6 +1957,61 @@ __global__ __launch_bounds__(kBlock) void k_decode_rows(v4u* shards, const v4u* 
     for (int q = 0; q < COL; ++q)
         acc ^= mv[q];
     st16(dst, acc);
+}
+
+// The batch layout -> packed erasure records (rfec_pack_erasures): one lane
+// per (group, output slot e), 2^lg >= E lanes per group.  Slot e: the fec_meta
+// and fec_data_size of the row of the group's e-th erased segment and the
+// row's other members' records in index order (zeros past the row's end);
+// all zeros where the group has no e-th erased segment.  Lane 0 writes the
+// masks and zeros the record's tail.
+__global__ __launch_bounds__(kBlock) void k_pack_rows(uint8_t* __restrict__ packed, const uint32_t* __restrict__ hdr,
+                                                      const uint64_t* __restrict__ present,
+                                                      const uint32_t* __restrict__ meta,
+                                                      const uint16_t* __restrict__ fsize,
+                                                      const uint64_t* __restrict__ parity_present, uint32_t groups,
+                                                      uint32_t KK, uint32_t CC, uint32_t NL, uint32_t E, uint32_t lg,
+                                                      uint32_t pk_stride, uint32_t pk_slot)
+{
+    const uint32_t hl = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t g = hl >> lg, e = hl & ((1u << lg) - 1u);
+    if (g >= groups || e >= E)
+        return;
+    uint8_t* pg = packed + (size_t)g * pk_stride;
+    const uint64_t h = present[2 * g];
+    if (e == 0) {
+        reinterpret_cast<uint64_t*>(pg)[0] = h;
+        reinterpret_cast<uint64_t*>(pg)[1] = parity_present[g];
+        for (uint32_t o = 16 + E * pk_slot; o < pk_stride; o += 4)
+            *reinterpret_cast<uint32_t*>(pg + o) = 0;
+    }
+    uint64_t m = ~h & (KK == 64 ? ~0ull : (1ull << KK) - 1ull);
+    for (uint32_t u = 0; u < e; ++u)
+        m &= m - 1ull;
+    uint32_t* so = reinterpret_cast<uint32_t*>(pg + 16 + (size_t)e * pk_slot);
+    const uint32_t nd = pk_slot / 4;
+    if (!m) {
+        for (uint32_t d = 0; d < nd; ++d)
+            so[d] = 0;
+        return;
+    }
+    const uint32_t tgt = (uint32_t)__ffsll((long long)m) - 1, r = tgt / CC;
+    const uint32_t first = r * CC, cnt = KK - first < CC ? KK - first : CC;
+    const uint32_t* mr = meta + ((size_t)g * NL + r) * 5;
+    for (uint32_t d = 0; d < 5; ++d)
+        so[d] = mr[d];
+    so[5] = fsize[(size_t)g * NL + r];
+    uint32_t o = 6;
+    for (uint32_t i = first; i < first + cnt; ++i) {
+        if (i == tgt)
+            continue;
+        const uint32_t* hr = hdr + ((size_t)g * KK + i) * 5;
+        for (uint32_t d = 0; d < 5; ++d)
+            so[o + d] = hr[d];
+        o += 5;
+    }
+    for (; o < nd; ++o)
+        so[o] = 0;
 }
 
 // dst row r <- src row map[r] (all `C` 16-B chunks), or zeros for map[r] < 0:
@@ -2191,6 +2327,21 @@ void launch_fused_rows(const FusedArgs& F, const PeelArgs& B, const rfec_kmask& 
                     dC, dRC, F.n_hdr, every, B, M, F.D, npay8, kk, cc, dCol);
 }
 
+// packed dense decode of row layouts: lanes per (group, output slot, chunk column), header lanes per
+// (group, output slot)
+template <int K, int COL>
+void launch_packed_rows(const FusedArgs& F, const PeelArgs& B, const rfec_kmask& M, uint32_t cd, uint32_t col_rt)
+{
+    const uint32_t kk = K ? (uint32_t)K : M.plan.k, cc = K ? (uint32_t)COL : col_rt;
+    const uint32_t total = B.groups * F.D.E * cd; // < 2^32: checked by the caller
+    const uint32_t npay = blocks_for(total), npay8 = (npay + 7u) & ~7u, nhr = (F.n_hdr + 7u) >> 3;
+    const dim3 grid(8u * nhr + npay8);
+    const uint32_t every = nhr ? (npay8 >> 3) / nhr : 0u;
+    const FastDiv dC = make_fastdiv(cd), dRC = make_fastdiv(F.D.E * cd), dCol = make_fastdiv(cc);
+    RFEC_LAUNCH((k_decode_rows<K, COL, true, true>), grid, dim3(kBlock), 0, F.stream, F.shards, F.parity, total, F.C,
+                dC, dRC, F.n_hdr, every, B, M, F.D, npay8, kk, cc, dCol);
+}
+
 template <int MAXC>
 void launch_fused_flat(const FusedArgs& F, const PeelArgs& B, const rfec_kmask& M)
 {
@@ -2263,6 +2414,8 @@ int launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32
     B.out_hdr = dense ? out->hdr : nullptr;
     B.out_index = dense ? out->index : nullptr;
     B.out_per_group = dense ? out->per_group : 0u;
+    B.packed = nullptr;
+    B.pk_stride = B.pk_slot = 0;
     const DenseOut DO = {dense ? reinterpret_cast<v4u*>(out->shards) : nullptr, dense ? out->per_group : 0u};
     uint64_t seen0 = 0, seen1 = 0;
     B.disjoint = 1;
@@ -2398,6 +2551,55 @@ int rfec_launch_recover_out(const rfec_kmask* M, uint32_t groups, uint32_t strid
     // the fused decodes only read the shards and headers when the output is dense
     return launch_recover(M, groups, stride, capacity, const_cast<uint8_t*>(shards), const_cast<rfec_hdr*>(hdr),
                           present, parity, meta, fsize, parity_present, recovered, ws, stream, flags, out);
+}
+
+int rfec_launch_pack_rows(const rfec_kplan* P, uint32_t col, uint32_t groups, const rfec_hdr* hdr,
+                          const uint64_t* present, const rfec_hdr* meta, const uint16_t* fsize,
+                          const uint64_t* parity_present, uint32_t per_group, uint8_t* packed, uint32_t pk_stride,
+                          uint32_t pk_slot, void* stream)
+{
+    uint32_t lg = 0;
+    while ((1u << lg) < per_group)
+        ++lg;
+    const uint32_t lanes = groups << lg; // < 2^32: host-checked
+    RFEC_LAUNCH(k_pack_rows, dim3(blocks_for(lanes)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), packed,
+                reinterpret_cast<const uint32_t*>(hdr), present, reinterpret_cast<const uint32_t*>(meta), fsize,
+                parity_present, groups, P->k, col, P->n_lines, per_group, lg, pk_stride, pk_slot);
+    return (int)hipGetLastError();
+}
+
+int rfec_launch_recover_packed(const rfec_kmask* M, uint32_t col, uint32_t groups, uint32_t stride,
+                               uint32_t capacity, const uint8_t* shards, const uint8_t* parity, const uint8_t* packed,
+                               uint32_t pk_stride, uint32_t pk_slot, uint64_t* recovered,
+                               const rfec_dense_out* out, void* stream)
+{
+    const rfec_kplan* P = &M->plan;
+    PeelArgs B = {};
+    B.recovered = recovered;
+    B.groups = groups;
+    B.capacity = capacity;
+    B.out_hdr = out->hdr;
+    B.out_index = out->index;
+    B.out_per_group = out->per_group;
+    B.packed = packed;
+    B.pk_stride = pk_stride;
+    B.pk_slot = pk_slot;
+    uint32_t lg = 0;
+    while ((1u << lg) < out->per_group)
+        ++lg;
+    B.nlp_log2 = lg;
+    const uint32_t cd = capacity ? (capacity + 15) / 16 : 1;
+    const uint32_t n_hdr = (uint32_t)((((uint64_t)groups << lg) + kBlock - 1) / kBlock);
+    const DenseOut DO = {reinterpret_cast<v4u*>(out->shards), out->per_group};
+    const FusedArgs F = {const_cast<v4u*>(reinterpret_cast<const v4u*>(shards)), reinterpret_cast<const v4u*>(parity),
+                         groups * cd, stride / 16, make_fastdiv(cd), n_hdr, reinterpret_cast<hipStream_t>(stream), DO};
+    if (P->k == 10 && col == 4)
+        launch_packed_rows<10, 4>(F, B, *M, cd, col);
+    else if (P->k == 32 && col == 4)
+        launch_packed_rows<32, 4>(F, B, *M, cd, col);
+    else
+        launch_packed_rows<0, 4>(F, B, *M, cd, col);
+    return (int)hipGetLastError();
 }
 
 int rfec_launch_line_jobs(const rfec_line_job* jobs, uint32_t n_jobs, const int32_t* members, const uint8_t* rows,

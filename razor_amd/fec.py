@@ -205,6 +205,10 @@ _SIGS = {
                                      _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rfec_recover_batch_out": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, C.c_uint32, C.c_uint32,
                                          _P, _P, _P, _P, _P, _P, _P, _P, C.c_uint32, _P, _P, _P, _P, _P]),
+    "rfec_packed_stride": (C.c_size_t, [C.POINTER(rfec_plan), C.c_uint32]),
+    "rfec_pack_erasures": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, _P, _P, _P, _P, _P, C.c_uint32, _P, _P]),
+    "rfec_recover_packed_out": (C.c_int, [C.POINTER(rfec_plan), C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P, _P,
+                                          C.c_uint32, _P, _P, _P, _P]),
     "rfec_zero_tails": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _P, _P]),
     "rfec_timing_events": (C.c_int, [_P, _P]),
     "rfec_timing_launches": (C.c_uint32, []),
@@ -353,6 +357,21 @@ class Native:
                                                     present, parity, meta, fec_size, parity_present, recovered,
                                                     per_group, out_shards, out_hdr, out_index, workspace, stream),
                     "rfec_recover_batch_out")
+
+    def packed_stride(self, plan, per_group) -> int:
+        """rfec_packed_stride: bytes per group record (0: not a packed layout)."""
+        return self.lib.rfec_packed_stride(C.byref(as_plan(plan)), per_group)
+
+    def pack_erasures(self, plan, groups, hdr, present, meta, fec_size, parity_present, per_group, packed,
+                      stream=None):
+        self._check(self.lib.rfec_pack_erasures(C.byref(as_plan(plan)), groups, hdr, present, meta, fec_size,
+                                                parity_present, per_group, packed, stream), "rfec_pack_erasures")
+
+    def recover_packed_out(self, plan, groups, stride, capacity, shards, parity, packed, recovered, per_group,
+                           out_shards, out_hdr, out_index, stream=None):
+        self._check(self.lib.rfec_recover_packed_out(C.byref(as_plan(plan)), groups, stride, capacity, shards, parity,
+                                                     packed, recovered, per_group, out_shards, out_hdr, out_index,
+                                                     stream), "rfec_recover_packed_out")
 
     def host_encode_groups(self, plan, groups, seg_ptrs, fec_ptrs, fec_id0=1):
         """seg_ptrs / fec_ptrs: host addresses (uint64 numpy arrays) of the

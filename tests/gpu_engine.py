@@ -104,6 +104,41 @@ class GpuEngine:
                 _host(d_rec, np.uint64, (G, 2)))
 
 
+    def recover_packed(self, plan, shards, hdr, present, parity, meta, fsize, pp, capacity, per_group, packed=None):
+        """rfec_pack_erasures (on the device, unless `packed` gives the records)
+        then rfec_recover_packed_out: returns (out_shards, out_hdr, out_index,
+        recovered, packed records [G][stride] as built)."""
+        G, k, stride = shards.shape
+        E = per_group
+        pks = self.lib.packed_stride(plan, E)
+        assert pks > 0
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        d_sh = _dev(shards, self.device)
+        d_p = _dev(parity, self.device)
+        if packed is None:
+            d_h = _dev(hdr, self.device)
+            d_pr = _dev(np.ascontiguousarray(present, np.uint64), self.device)
+            d_m = _dev(meta, self.device)
+            d_f = _dev(np.ascontiguousarray(fsize, np.uint16), self.device)
+            d_pp = _dev(np.ascontiguousarray(pp, np.uint64), self.device)
+            d_pk = torch.full((G * pks,), 0x77, dtype=torch.uint8, device=self.device)
+            self.lib.pack_erasures(plan, G, d_h.data_ptr(), d_pr.data_ptr(), d_m.data_ptr(), d_f.data_ptr(),
+                                   d_pp.data_ptr(), E, d_pk.data_ptr(), st)
+        else:
+            assert packed.shape == (G, pks)
+            d_pk = _dev(packed, self.device)
+        d_rec = torch.full((G * 16,), 0xEE, dtype=torch.uint8, device=self.device)
+        o_sh = torch.full((G * E * stride,), 0x3C, dtype=torch.uint8, device=self.device)
+        o_h = torch.full((G * E * 20,), 0x3C, dtype=torch.uint8, device=self.device)
+        o_i = torch.full((G * E,), 0x3C, dtype=torch.uint8, device=self.device)
+        self.lib.recover_packed_out(plan, G, stride, capacity, d_sh.data_ptr(), d_p.data_ptr(), d_pk.data_ptr(),
+                                    d_rec.data_ptr(), E, o_sh.data_ptr(), o_h.data_ptr(), o_i.data_ptr(), st)
+        torch.cuda.synchronize(self.device)
+        assert np.array_equal(_host(d_sh, np.uint8, (G, k, stride)), shards), "shards written"
+        return (_host(o_sh, np.uint8, (G, E, stride)), _host(o_h, HDR_DTYPE, (G, E)), _host(o_i, np.uint8, (G, E)),
+                _host(d_rec, np.uint64, (G, 2)), _host(d_pk, np.uint8, (G, pks)))
+
+
 class GpuWire:
     """The wire codec (rfec_wire_*) on numpy inputs."""
 

@@ -222,6 +222,27 @@ int rfec_launch_recover_out(const rfec_kmask* M, uint32_t groups, uint32_t strid
     return (int)hipErrorInvalidValue;
 }
 
+/* packed erasure records: not used by the host control plane; refused */
+int rfec_launch_pack_rows(const rfec_kplan* P, uint32_t col, uint32_t groups, const rfec_hdr* hdr,
+                          const uint64_t* present, const rfec_hdr* meta, const uint16_t* fsize,
+                          const uint64_t* parity_present, uint32_t per_group, uint8_t* packed, uint32_t pk_stride,
+                          uint32_t pk_slot, void* stream)
+{
+    (void)P, (void)col, (void)groups, (void)hdr, (void)present, (void)meta, (void)fsize, (void)parity_present;
+    (void)per_group, (void)packed, (void)pk_stride, (void)pk_slot, (void)stream;
+    return (int)hipErrorInvalidValue;
+}
+
+int rfec_launch_recover_packed(const rfec_kmask* M, uint32_t col, uint32_t groups, uint32_t stride,
+                               uint32_t capacity, const uint8_t* shards, const uint8_t* parity, const uint8_t* packed,
+                               uint32_t pk_stride, uint32_t pk_slot, uint64_t* recovered,
+                               const rfec_dense_out* out, void* stream)
+{
+    (void)M, (void)col, (void)groups, (void)stride, (void)capacity, (void)shards, (void)parity, (void)packed;
+    (void)pk_stride, (void)pk_slot, (void)recovered, (void)out, (void)stream;
+    return (int)hipErrorInvalidValue;
+}
+
 int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* parity,
                                const rfec_hdr* meta, const uint16_t* fec_size, const int8_t* status,
                                const rfec_fec_stamp* stamps, const uint32_t* order, uint32_t dstride,

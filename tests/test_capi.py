@@ -87,6 +87,42 @@ def test_argument_validation(product):
         product.zero_tails(1 << 30, 8, 1200, 1, 1, None)
 
 
+def test_packed_records_geometry(product, oracle1000):
+    """rfec_packed_stride and the packed entry points' checks (no launch): row
+    layouts of rows <= 4 and k <= 64 only; the host packer (parity_cases) has
+    the same stride."""
+    from razor_amd.fec import RfecError
+    from parity_cases import pack_erasures_np
+    c5 = product.plan_matrix(32, 8, 4, 1)
+    assert product.packed_stride(c5, 2) == 192  # 16 + 2 x 84 -> 3 x 64 B
+    assert product.packed_stride(product.plan_matrix(10, 3, 4, 1), 2) == 192
+    assert product.packed_stride(product.plan_matrix(12, 6, 2, 1), 5) == 256  # 16 + 5 x 44 = 236
+    assert product.packed_stride(c5, 32) == (16 + 32 * 84 + 63) // 64 * 64
+    assert product.packed_stride(c5, 0) == 0 and product.packed_stride(c5, 33) == 0
+    assert product.packed_stride(product.plan_matrix(10, 3, 4, 3), 2) == 0  # rows + columns
+    assert product.packed_stride(product.plan_matrix(16, 2, 8, 1), 2) == 0  # rows of 8
+    assert product.packed_stride(product.plan_matrix(96, 24, 4, 1), 2) == 0  # k > 64
+    G, k, col, E = 3, 10, 4, 2
+    hdr = np.zeros((G, k), po.HDR_DTYPE)
+    meta = np.zeros((G, 3), po.HDR_DTYPE)
+    rec = pack_erasures_np(k, col, hdr, np.zeros((G, 2), np.uint64), meta, np.zeros((G, 3), np.uint16),
+                           np.zeros(G, np.uint64), E)
+    assert rec.shape == (G, product.packed_stride(product.plan_matrix(10, 3, 4, 1), E))
+    full = product.plan_matrix(10, 3, 4, 3)
+    with pytest.raises(RfecError):  # not a row layout
+        product.recover_packed_out(full, 4, 1200, 1200, 16, 16, 16, 16, 2, 16, 16, 16)
+    with pytest.raises(RfecError):  # per_group 0
+        product.recover_packed_out(c5, 4, 256, 256, 16, 16, 16, 16, 0, 16, 16, 16)
+    with pytest.raises(RfecError):  # records not 16-byte aligned
+        product.recover_packed_out(c5, 4, 256, 256, 16, 16, 24, 16, 2, 16, 16, 16)
+    with pytest.raises(RfecError):  # NULL buffers
+        product.recover_packed_out(c5, 4, 256, 256, None, None, 16, None, 2, None, None, None)
+    with pytest.raises(RfecError):
+        product.pack_erasures(c5, 4, None, None, None, None, None, 2, 16)
+    with pytest.raises(RfecError):  # groups x slots beyond 32 bits
+        product.pack_erasures(c5, 1 << 30, 16, 16, 16, 16, 16, 32, 16)
+
+
 def test_dropin_fails_loudly_without_gpu():
     """No CPU path: without a HIP device the drop-in symbols print and return -1."""
     code = r'''

@@ -155,6 +155,11 @@ def _check_subs(d, n):
         assert 0 < c["encode"]["frac"] < 1 and 0 < c["decode"]["frac"] < 1
         assert c["encode"]["mix_ceiling"]["kernel_vs_ceiling"] > 0
     assert d["c3full"]["decode"]["kernels"].startswith("k_decode_matrix_dense<10,4>")
+    # c5 (a row layout) also decodes from packed erasure records; c3full has none
+    pk = d["c5"]["decode_packed"]
+    assert pk["verified"] is True and pk["kernels"].startswith("k_decode_rows<32,4> packed")
+    assert len(pk["launch_us_per_rank"]) == n and all(t > 0 for t in pk["launch_us_per_rank"])
+    assert d["c3full"]["decode_packed"] is None
     assert d["c5"]["encode"]["mix_ceiling"]["probe"].startswith("rfec_probe_mix 4 reads : 1 writes")
     assert d["c3full"]["encode"]["mix_ceiling"]["probe"].startswith("rfec_probe_mix 10 reads : 7 writes")
 

@@ -109,7 +109,7 @@ def main():
         if "check" in res:  # the cascade decode's two launches together
             entry["decode_with_check_traffic_over_algorithmic"] = (res["decode"]["hbm_bytes"] +
                                                                    res["check"]["hbm_bytes"]) / dec_alg
-    name = f"k{k}_r{r}_S{S}_G{groups}"
+    name = f"k{k}_r{r}_S{S}_G{groups}" + ("+packed" if "--packed-decode" in bench_args else "")
     Path(args.out).write_text(json.dumps({name: entry}, indent=1))
     print(json.dumps({name: entry}, indent=1))
 
