@@ -3,7 +3,7 @@
 #   bash tools/measure.sh <tag>
 # pytest -m gpu, smoke, drop-in group bench, the default bench (the driver's command) and the
 # rocprofv3 kernel stats of that same command, c3full / c5 lines + stats, the r:w mix probe, the
-# end-to-end step, wire bench + stats, PMC traffic passes (FETCH_SIZE / WRITE_SIZE) for c3, c5, c3full.  Every GPU step has its own limit; a crash /
+# end-to-end step, wire bench + stats, PMC traffic passes (FETCH_SIZE / WRITE_SIZE) for c3, c5, c3full and c5's packed-record decode.  Every GPU step has its own limit; a crash /
 # fault / timeout stops the script.
 set -u
 TAG=${1:-m}; OUT=gpurun_out/$TAG
@@ -40,4 +40,5 @@ step rocprof_wire 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$
 step pmc_c3 600 python tools/pmc_traffic.py --out "$OUT/traffic_c3.json" -- --steps 10 --warmup 2 --c4-steps 0 --sub-steps 0
 step pmc_c5 600 python tools/pmc_traffic.py --out "$OUT/traffic_c5.json" -- --config c5 --steps 10 --warmup 2
 step pmc_c3full 600 python tools/pmc_traffic.py --out "$OUT/traffic_c3full.json" -- --config c3full --steps 10 --warmup 2
+step pmc_c5p 600 python tools/pmc_traffic.py --out "$OUT/traffic_c5p.json" -- --config c5 --packed-decode --steps 10 --warmup 2
 echo done | tee -a "$OUT/steps.log"
