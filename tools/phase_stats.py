@@ -37,7 +37,8 @@ def main():
     if cur:
         blocks.append(cur)
     blocks = [b for b in blocks if len(b) >= args.min_block]
-    names = ["headline (prime, warm-up, timed steps)", "c4_strong (65,536-group launches)"]
+    names = ["headline (prime, warm-up, timed steps)", "c4_strong (65,536-group launches)", "c5 sub-object",
+             "c5 sub-object, packed-record decode", "c3full sub-object"]
     out = []
     for i, b in enumerate(blocks):
         per = {}
