@@ -122,6 +122,42 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
     return (b & 7u) * (nb8 >> 3) + (b >> 3);
 }
 
+// Header / meta blocks spread in rounds of 8 blocks (one per XCD: block b runs on XCD
+// b % 8) for the XCD-swizzled decodes: the first round of every (every + 1) is
+// a round of 8 header blocks until n_hr of them ran, so the payload blocks fill
+// whole rounds and payload block p (in payload order) runs on XCD p % 8; it
+// then takes logical block xcd_block(p): consecutive logical blocks share an
+// XCD's L2 (the 128-B lines split between neighbouring slots are fetched once)
+// and XCD x sweeps its eighth of the groups in order.  XCD x's header blocks
+// are x n_hr + 0, 1, ...: the groups its own payload rounds reach next, so the
+// header blocks' reads of the masks come in through the same L2 just before
+// the payload lanes read them (the cascade decode: 128.3-128.8 vs 129.4-130.3
+// us with header block per * 8 + x, last in each period).
+// npay8: payload blocks rounded up to a multiple of 8.
+__device__ __forceinline__ bool header_block_xcd(uint32_t n_hr, uint32_t every, uint32_t npay8, uint32_t* hb,
+                                                 uint32_t* pb)
+{
+    const uint32_t R = blockIdx.x >> 3, x = blockIdx.x & 7u;
+    uint32_t pr;
+    if (!every) {
+        if (R < n_hr) {
+            *hb = x * n_hr + R;
+            return true;
+        }
+        pr = R - n_hr;
+    } else {
+        const uint32_t per = R / (every + 1);
+        if (per < n_hr && R == per * (every + 1)) {
+            *hb = x * n_hr + per;
+            return true;
+        }
+        pr = R - min(per + 1, n_hr);
+    }
+    *pb = xcd_block(pr * 8u + x, npay8);
+    return false;
+}
+
+
 // Copies n dwords global -> LDS with the whole block (nt lanes), several loads
 // in flight per lane: the loads go through a buffer descriptor over exactly
 // the n dwords, so a lane past the end reads zeros with no branch around the
@@ -229,18 +265,24 @@ struct EncMeta {
     uint32_t groups, capacity, gpb, n_meta_blocks;
 };
 
-// Grid of the swizzled encodes: the meta blocks first, padded to `head` (a
-// multiple of 8) so that payload block p runs on XCD p % 8.  Returns false
-// for meta / padding blocks (meta work done), else the logical payload block.
+// Grid of the swizzled encodes: head / 8 rounds of 8 meta blocks spread over
+// the payload rounds (header_block_xcd; the payload part of the grid is whole
+// rounds of 8), so the meta blocks' latency-bound header stages overlap the
+// payload stream instead of holding the whole GPU at the start of the launch:
+// c5 (k = 32 / 256 B, 8 % header bytes) 113.4-113.6 vs 117.9-119.4 us, c3
+// 161.7-162.2 vs 162.8-163.4 us (round 5, profiles/r05/ab/enc_meta_spread/).
+// Returns false for meta / padding blocks (meta work done), else the logical
+// payload block.
 __device__ __forceinline__ bool enc_payload_block(const EncMeta& E, uint32_t head, const rfec_kplan& P, uint32_t* b)
 {
-    if (blockIdx.x < E.n_meta_blocks) {
-        meta_block(blockIdx.x, E.hdr_dw, E.meta_dw, E.fsize, E.status, E.groups, E.capacity, E.gpb, P);
+    const uint32_t n_mr = head >> 3, npay8 = gridDim.x - head;
+    const uint32_t every = n_mr ? (npay8 >> 3) / n_mr : 0u;
+    uint32_t mb;
+    if (header_block_xcd(n_mr, every, npay8, &mb, b)) {
+        if (mb < E.n_meta_blocks)
+            meta_block(mb, E.hdr_dw, E.meta_dw, E.fsize, E.status, E.groups, E.capacity, E.gpb, P);
         return false;
     }
-    if (blockIdx.x < head)
-        return false;
-    *b = xcd_block(blockIdx.x - head, gridDim.x - head);
     return true;
 }
 
@@ -1256,8 +1298,6 @@ __device__ __forceinline__ void cascade_dense_tail(const CascArgs& A, const SLin
 // the kernel arguments: 131 us; checker rounds 3 or 8 rounds further ahead: no
 // change).  The payload lanes wait on the masks where k_decode_cascade waited
 // on its task word (L2).
-__device__ __forceinline__ bool header_block_xcd(uint32_t n_hr, uint32_t every, uint32_t npay8, uint32_t* hb,
-                                                 uint32_t* pb);
 
 template <typename MT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_decode_cascade_dense(
@@ -1650,40 +1690,6 @@ __device__ __forceinline__ bool header_block(uint32_t n_hdr, uint32_t every, uin
     return per < n_hdr && b - per * (every + 1) == every;
 }
 
-// The same spread in rounds of 8 blocks (one per XCD: block b runs on XCD
-// b % 8) for the XCD-swizzled decodes: the first round of every (every + 1) is
-// a round of 8 header blocks until n_hr of them ran, so the payload blocks fill
-// whole rounds and payload block p (in payload order) runs on XCD p % 8; it
-// then takes logical block xcd_block(p): consecutive logical blocks share an
-// XCD's L2 (the 128-B lines split between neighbouring slots are fetched once)
-// and XCD x sweeps its eighth of the groups in order.  XCD x's header blocks
-// are x n_hr + 0, 1, ...: the groups its own payload rounds reach next, so the
-// header blocks' reads of the masks come in through the same L2 just before
-// the payload lanes read them (the cascade decode: 128.3-128.8 vs 129.4-130.3
-// us with header block per * 8 + x, last in each period).
-// npay8: payload blocks rounded up to a multiple of 8.
-__device__ __forceinline__ bool header_block_xcd(uint32_t n_hr, uint32_t every, uint32_t npay8, uint32_t* hb,
-                                                 uint32_t* pb)
-{
-    const uint32_t R = blockIdx.x >> 3, x = blockIdx.x & 7u;
-    uint32_t pr;
-    if (!every) {
-        if (R < n_hr) {
-            *hb = x * n_hr + R;
-            return true;
-        }
-        pr = R - n_hr;
-    } else {
-        const uint32_t per = R / (every + 1);
-        if (per < n_hr && R == per * (every + 1)) {
-            *hb = x * n_hr + per;
-            return true;
-        }
-        pr = R - min(per + 1, n_hr);
-    }
-    *pb = xcd_block(pr * 8u + x, npay8);
-    return false;
-}
 
 // Flat form, slots under 64 chunks (k = 32 / 256 B): one lane per (group,
 // chunk column) XORs every fired line of its group, two lines' loads in
@@ -2121,6 +2127,8 @@ struct EncLaunch {
 
 // meta blocks + padding to a multiple of 8 (the swizzled grids)
 inline uint32_t enc_head(const EncLaunch& a) { return (a.E.n_meta_blocks + 7u) & ~7u; }
+// payload blocks for `total` lanes, in whole rounds of 8 (enc_payload_block)
+inline uint32_t enc_rounds(uint64_t total) { return (blocks_for(total) + 7u) & ~7u; }
 
 template <int K, int COL>
 hipError_t launch_rows_out(const EncLaunch& a)
@@ -2128,7 +2136,7 @@ hipError_t launch_rows_out(const EncLaunch& a)
     constexpr uint32_t R = (K + COL - 1) / COL;
     const uint64_t total = (uint64_t)a.groups * R * a.cd; // < 2^32: checked by the caller
     const uint32_t head = enc_head(a);
-    RFEC_LAUNCH((k_encode_out<K, COL>), dim3(head + blocks_for(total)), dim3(kBlock), 0, a.stream, a.s, a.p,
+    RFEC_LAUNCH((k_encode_out<K, COL>), dim3(head + enc_rounds(total)), dim3(kBlock), 0, a.stream, a.s, a.p,
                 (uint32_t)total, a.stride / 16, make_fastdiv(a.cd), make_fastdiv(R * a.cd), head, a.E, *a.P);
     return hipGetLastError();
 }
@@ -2139,7 +2147,7 @@ hipError_t launch_rows_out_rt(const EncLaunch& a, uint32_t col)
     const uint32_t K = a.P->k, R = (K + col - 1) / col;
     const uint64_t total = (uint64_t)a.groups * R * a.cd; // < 2^32: checked by the caller
     const uint32_t head = enc_head(a);
-    RFEC_LAUNCH((k_encode_out_rt<CMAX>), dim3(head + blocks_for(total)), dim3(kBlock), 0, a.stream, a.s, a.p,
+    RFEC_LAUNCH((k_encode_out_rt<CMAX>), dim3(head + enc_rounds(total)), dim3(kBlock), 0, a.stream, a.s, a.p,
                 (uint32_t)total, a.stride / 16, make_fastdiv(a.cd), make_fastdiv(R * a.cd), K, col, head, a.E,
                 *a.P);
     return hipGetLastError();
@@ -2206,7 +2214,7 @@ hipError_t launch_encode(const EncLaunch& a, unsigned flags)
     if (!generic && P->k >= 6 && P->k <= 16 && is_full_matrix(P, P->k <= 9 ? 3 : 4)) {
         const uint32_t head = enc_head(a);
         const uint32_t nl = P->n_lines, tot = a.groups * nl * a.cd;
-        const dim3 grid_o(head + blocks_for(tot));
+        const dim3 grid_o(head + enc_rounds(tot));
 #define RFEC_MX(KK, CC)                                                                                           \
     case KK:                                                                                                      \
         RFEC_LAUNCH((k_encode_matrix_out<KK, CC>), grid_o, dim3(kBlock), 0, a.stream, a.s, a.p, tot, C,          \
