@@ -271,6 +271,20 @@ for mem in ("pinned", "pageable"):
         except RfecError:
             pass
 print("hostmem ok")
+
+# 8. packed erasure records (rfec_host.c): the stride and argument checks, up to
+#    the launches the stub refuses
+c5 = lib.plan_matrix(32, 8, 4, 1)
+assert lib.packed_stride(c5, 2) == 192 and lib.packed_stride(lib.plan_matrix(10, 3, 4, 3), 2) == 0
+for call in (lambda: lib.pack_erasures(c5, 4, 16, 16, 16, 16, 16, 2, 16),
+             lambda: lib.recover_packed_out(c5, 4, 256, 256, 16, 16, 16, 16, 2, 16, 16, 16),
+             lambda: lib.recover_packed_out(lib.plan_matrix(10, 3, 4, 3), 4, 1200, 1200, 16, 16, 16, 16, 2, 16, 16,
+                                            16)):
+    try:
+        call()
+    except RfecError:
+        pass
+print("packed ok")
 """
 
 
@@ -283,4 +297,4 @@ def test_host_control_plane_under_asan(stub_lib, tmp_path):
     env["UBSAN_OPTIONS"] = "print_stacktrace=1:halt_on_error=1"
     r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-8000:]
-    assert "sender ok" in r.stdout and "udp ok" in r.stdout and "hostmem ok" in r.stdout
+    assert "sender ok" in r.stdout and "udp ok" in r.stdout and "hostmem ok" in r.stdout and "packed ok" in r.stdout
