@@ -502,9 +502,10 @@ TIMING_BRACKET = ("HIP events recorded on the launch stream before and after the
 # stream events); the windows are still those of launches inside the timed
 # region.
 TIMING_EVERY = 8
+SUB_EVERY = 2  # the c5 / c3full sub-objects (20 steps)
 
 
-def time_steps(lib, sets, steps, warmup, stream, dist, timing, hot):
+def time_steps(lib, sets, steps, warmup, stream, dist, timing, hot, every=TIMING_EVERY):
     """Primes every set's parity, runs `warmup` untimed steps, then times
     `steps` steps (encode one set, decode the set encoded one step earlier, or
     the same set when `hot` or one set) between a barrier + device
@@ -549,7 +550,7 @@ def time_steps(lib, sets, steps, warmup, stream, dist, timing, hot):
     for i in range(steps):
         # sampled steps: the kernels' own events where a call is one launch (no marker between launches),
         # else a bracket
-        smp = i % TIMING_EVERY == 0
+        smp = i % every == 0
         ka, kb, kc, kd = kev[i]
         a, b, c, d = ev[i]
         if smp and own_enc:
@@ -570,7 +571,7 @@ def time_steps(lib, sets, steps, warmup, stream, dist, timing, hot):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    sampled = list(zip(kev, ev))[::TIMING_EVERY]
+    sampled = list(zip(kev, ev))[::every]
     t_enc = np.array([(q if own_enc else e)[0].elapsed_time((q if own_enc else e)[1]) for q, e in sampled]) / 1e3
     t_dec = np.array([(q if own_dec else e)[2].elapsed_time((q if own_dec else e)[3]) for q, e in sampled]) / 1e3
     if dist:
@@ -692,7 +693,9 @@ def config_sub(lib, name, device, stream, dist, world, rank, pf, steps, warmup, 
     sets = [Workload(lib, G, k, S, pf, device, rank * G, seed=2000 + 17 * rank, col=col, full_plan=full_plan,
                      config_id=cfg["config_id"]) for _ in range(2)]
     w = sets[0]
-    elapsed, t_enc, t_dec, own_enc, own_dec = time_steps(lib, sets, steps, warmup, stream, dist, "own", False)
+    # (kernel windows on every SUB_EVERY-th step: the sub-objects' few steps still give ~10 samples)
+    elapsed, t_enc, t_dec, own_enc, own_dec = time_steps(lib, sets, steps, warmup, stream, dist, "own", False,
+                                                         SUB_EVERY)
     verified = digest_ok = None
     if verify:
         verified = all(ws.verify() for ws in sets)
@@ -705,7 +708,7 @@ def config_sub(lib, name, device, stream, dist, world, rank, pf, steps, warmup, 
     if w.pks:
         for ws in sets:
             ws.use_packed(True)
-        _, _, t_dec_pk, _, own_pk = time_steps(lib, sets, steps, warmup, stream, dist, "own", False)
+        _, _, t_dec_pk, _, own_pk = time_steps(lib, sets, steps, warmup, stream, dist, "own", False, SUB_EVERY)
         t_pk = float(t_dec_pk.mean()) * 1e6 if own_pk else -1.0
         if verify:
             pk_ok = int(all(ws.verify() for ws in sets))
@@ -753,7 +756,8 @@ def config_sub(lib, name, device, stream, dist, world, rank, pf, steps, warmup, 
                    "verified": None if not verify else all(int(r[5]) == 1 for r in rows)},
                "encode_us_per_rank": [round(float(r[1]), 2) for r in rows],
                "decode_us_per_rank": [round(float(r[2]), 2) for r in rows],
-               "timing": "per launch: " + (TIMING_OWN if own_enc and own_dec else TIMING_BRACKET),
+               "timing": "per launch: " + (TIMING_OWN if own_enc and own_dec else TIMING_BRACKET).replace(
+                   "every 8th timed step", "every 2nd timed step"),
                "verified": None if not verify else all(int(r[3]) == 1 for r in rows),
                "verified_vs_reference_digest": digest_ok,
                "digest_scope": "rank 0's groups [0, 65,536) = the reference's full-size digest case "
