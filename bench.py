@@ -502,7 +502,7 @@ TIMING_BRACKET = ("HIP events recorded on the launch stream before and after the
 # stream events); the windows are still those of launches inside the timed
 # region.
 TIMING_EVERY = 8
-SUB_EVERY = 2  # the c5 / c3full sub-objects (20 steps)
+SUB_EVERY = TIMING_EVERY  # the c5 / c3full sub-objects (80 steps: 10 samples)
 
 
 def time_steps(lib, sets, steps, warmup, stream, dist, timing, hot, every=TIMING_EVERY):
@@ -693,7 +693,7 @@ def config_sub(lib, name, device, stream, dist, world, rank, pf, steps, warmup, 
     sets = [Workload(lib, G, k, S, pf, device, rank * G, seed=2000 + 17 * rank, col=col, full_plan=full_plan,
                      config_id=cfg["config_id"]) for _ in range(2)]
     w = sets[0]
-    # (kernel windows on every SUB_EVERY-th step: the sub-objects' few steps still give ~10 samples)
+    # (kernel windows on every SUB_EVERY-th step: 10 samples of the default 80 steps)
     elapsed, t_enc, t_dec, own_enc, own_dec = time_steps(lib, sets, steps, warmup, stream, dist, "own", False,
                                                          SUB_EVERY)
     verified = digest_ok = None
@@ -756,8 +756,7 @@ def config_sub(lib, name, device, stream, dist, world, rank, pf, steps, warmup, 
                    "verified": None if not verify else all(int(r[5]) == 1 for r in rows)},
                "encode_us_per_rank": [round(float(r[1]), 2) for r in rows],
                "decode_us_per_rank": [round(float(r[2]), 2) for r in rows],
-               "timing": "per launch: " + (TIMING_OWN if own_enc and own_dec else TIMING_BRACKET).replace(
-                   "every 8th timed step", "every 2nd timed step"),
+               "timing": "per launch: " + (TIMING_OWN if own_enc and own_dec else TIMING_BRACKET),
                "verified": None if not verify else all(int(r[3]) == 1 for r in rows),
                "verified_vs_reference_digest": digest_ok,
                "digest_scope": "rank 0's groups [0, 65,536) = the reference's full-size digest case "
@@ -799,7 +798,7 @@ def main():
                     help="decode the set encoded in the same step (its parity still MALL-resident)")
     ap.add_argument("--c4-steps", type=int, default=10,
                     help="timed steps of the c4_strong sub-object (config c3 only; 0 = skip it)")
-    ap.add_argument("--sub-steps", type=int, default=20,
+    ap.add_argument("--sub-steps", type=int, default=80,
                     help="timed steps of the c5 / c3full sub-objects (config c3 only; 0 = skip them)")
     args = ap.parse_args()
 
