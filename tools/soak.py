@@ -7,6 +7,8 @@ the exact peel reject lines, the generic or the default kernels -- and checks:
   encode: parities, metas, fec_data_size, status == oracle
   recover (in place): recovered masks, headers and data == oracle's peel
   recover_out (dense, E random): out slots, headers, indices, masks == oracle
+  recover_packed_out (row layouts of rows <= 4, k <= 64; a third of the
+    iterations draw the row layer alone): the same, from packed erasure records
 and, every other iteration, the wire codec on a random batch (SIM_SEG or
 SIM_FEC, capacity 16-1999, 1-20k datagrams): framed bytes and lengths ==
 oracle, then parse of the datagrams with random bytes flipped in ~5 % of them
@@ -125,6 +127,24 @@ def check_dense(o, eng, plan, E, args):
     return None
 
 
+def check_packed(o, eng, plan, E, args):
+    """rfec_pack_erasures + rfec_recover_packed_out == the oracle's dense recovery"""
+    rx, rh, present, parity, meta, fs, pp, cap = args
+    e_s, e_h, e_i, e_rec = o.recover_batch_out(plan, rx, rh, present, parity, meta, fs, pp, cap, E)
+    g_s, g_h, g_i, g_rec, _ = eng.recover_packed(plan, rx, rh, present, parity, meta, fs, pp, cap, E)
+    if not np.array_equal(g_rec, e_rec):
+        return "packed recovered masks"
+    if not np.array_equal(g_i, e_i):
+        return "packed out_index"
+    for gi, e in zip(*np.nonzero(e_i != 0xFF)):
+        if g_h[gi, e] != e_h[gi, e]:
+            return f"packed header g{gi} e{e}"
+        L = int(e_h[gi, e]["size"])
+        if not np.array_equal(g_s[gi, e, :L], e_s[gi, e, :L]):
+            return f"packed data g{gi} e{e}"
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=120.0)
@@ -136,7 +156,7 @@ def main():
     engines = {t: GpuEngine(1000, tuning=t) for t in (0, 1)}
     gw = GpuWire(1000)
     t0 = time.time()
-    it, fails, groups, cfgs, wit, dgrams = 0, [], 0, set(), 0, 0
+    it, fails, groups, cfgs, wit, dgrams, pk_groups = 0, [], 0, set(), 0, 0, 0
     while time.time() - t0 < args.seconds:
         if (it + wit) % 2 == 1:
             what, (cap_w, N, seg) = check_wire(o, gw, rng)
@@ -150,7 +170,7 @@ def main():
             continue
         k = int(rng.integers(2, 65))
         pf = int(rng.choice([5, 10, 20, 40, 80, 120, 200, 255]))
-        plan = o.plan_from_fraction(k, pf, 3)
+        plan = o.plan_from_fraction(k, pf, 1 if rng.random() < 1 / 3 else 3)
         if plan.n_lines == 0:
             continue
         S = int(rng.choice([16, 64, 200, 256, 512, 1000]))
@@ -163,17 +183,20 @@ def main():
             corrupt=float(rng.choice([0.0, 0.2, 0.45])))
         rargs = (rx, rh, present, parity, meta, fs, pp, cap)
         E = int(rng.integers(1, min(k, 6) + 1))
+        packed = eng.lib.packed_stride(plan, E) > 0
         what = (check_encode(o, eng, plan, shards, hdr, cap) or check_recover(o, eng, plan, k, rargs)
-                or check_dense(o, eng, plan, E, rargs))
+                or check_dense(o, eng, plan, E, rargs) or (packed and check_packed(o, eng, plan, E, rargs)) or None)
+        pk_groups += G if packed else 0
         it += 1
         groups += G
         cfgs.add((k, plan.n_lines))
-        line = f"{it} k={k} pf={pf} lines={plan.n_lines} S={S} G={G} E={E} tuning={tuning} " + ("ok" if not what
-                                                                                              else "FAIL " + what)
+        line = (f"{it} k={k} pf={pf} lines={plan.n_lines} S={S} G={G} E={E} tuning={tuning} packed={int(packed)} "
+                + ("ok" if not what else "FAIL " + what))
         print(line, flush=True)
         if what:
             fails.append(line)
-    out = {"iterations": it, "groups": groups, "distinct_k_lines": len(cfgs), "wire_iterations": wit,
+    out = {"iterations": it, "groups": groups, "packed_groups": pk_groups, "distinct_k_lines": len(cfgs),
+           "wire_iterations": wit,
            "datagrams": dgrams, "seconds": round(time.time() - t0, 1), "seed": args.seed, "failures": fails}
     print(json.dumps(out))
     if args.out:
