@@ -123,6 +123,32 @@ def test_packed_records_geometry(product, oracle1000):
         product.pack_erasures(c5, 1 << 30, 16, 16, 16, 16, 16, 32, 16)
 
 
+def test_packed_records_layout():
+    """The host restatement of the packed erasure records (what the GPU tests
+    compare rfec_pack_erasures against) follows razor_fec.h's layout: k = 8 in
+    rows of 4, segments 1 and 6 lost, two slots."""
+    from parity_cases import pack_erasures_np
+    k, col, E = 8, 4, 2
+    hdr = np.zeros((1, k), po.HDR_DTYPE)
+    hdr["seq"] = np.arange(100, 100 + k)
+    meta = np.zeros((1, 2), po.HDR_DTYPE)
+    meta["seq"] = [7, 9]
+    fs = np.array([[300, 400]], np.uint16)
+    present = np.array([[0xFF & ~(1 << 1) & ~(1 << 6), 0]], np.uint64)
+    pp = np.array([3], np.uint64)
+    rec = pack_erasures_np(k, col, hdr, present, meta, fs, pp, E)
+    assert rec.shape == (1, 192)  # 16 + 2 x (24 + 3 x 20) = 184 -> 192
+    u64 = rec[0, :16].view(np.uint64)
+    assert u64[0] == present[0, 0] and u64[1] == 3
+    for e, (row, members) in enumerate(((0, (0, 2, 3)), (1, (4, 5, 7)))):
+        o = 16 + e * 84
+        assert rec[0, o:o + 20].view(po.HDR_DTYPE)[0]["seq"] == meta[0, row]["seq"]
+        assert rec[0, o + 20:o + 22].view(np.uint16)[0] == fs[0, row] and not rec[0, o + 22:o + 24].any()
+        seqs = [int(rec[0, o + 24 + 20 * q:o + 44 + 20 * q].view(po.HDR_DTYPE)[0]["seq"]) for q in range(3)]
+        assert seqs == [100 + i for i in members]
+    assert not rec[0, 184:].any()
+
+
 def test_dropin_fails_loudly_without_gpu():
     """No CPU path: without a HIP device the drop-in symbols print and return -1."""
     code = r'''
