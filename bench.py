@@ -58,7 +58,7 @@ import torch
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-from razor_amd.dist import shard_groups  # noqa: E402
+from razor_amd.dist import StepWindow, device_identity, gather_objects, shard_groups  # noqa: E402
 from razor_amd.fec import HDR_DTYPE, Native, native  # noqa: E402
 
 METRIC = "FEC encode+decode GiB/s (device-resident), 1200B pkts k=10/r=3; % HBM peak"
@@ -509,9 +509,11 @@ def time_steps(lib, sets, steps, warmup, stream, dist, timing, hot, every=TIMING
     """Primes every set's parity, runs `warmup` untimed steps, then times
     `steps` steps (encode one set, decode the set encoded one step earlier, or
     the same set when `hot` or one set) between a barrier + device
-    synchronize on both sides.  Returns (elapsed wall seconds, max over ranks;
+    synchronize on both sides (razor_amd/dist.StepWindow).  Returns (the job's
+    wall seconds: max over ranks of t1 - min over ranks of t0, CLOCK_MONOTONIC;
     encode / decode launch seconds of the sampled steps (every TIMING_EVERY-th,
-    from the first); whether each is the kernel's own window)."""
+    from the first); whether each is the kernel's own window; the window's
+    per-rank readings and skews)."""
     nset = len(sets)
     sp = stream.cuda_stream
     device = stream.device
@@ -543,10 +545,8 @@ def time_steps(lib, sets, steps, warmup, stream, dist, timing, hot, every=TIMING
     own_enc = timing == "own" and n_enc == 1
     own_dec = timing == "own" and n_dec == 1
     torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
+    win = StepWindow(dist, lambda: torch.cuda.synchronize(device))
+    win.start()  # barrier, synchronize, t0 (CLOCK_MONOTONIC)
     for i in range(steps):
         # sampled steps: the kernels' own events where a call is one launch (no marker between launches),
         # else a bracket
@@ -567,18 +567,12 @@ def time_steps(lib, sets, steps, warmup, stream, dist, timing, hot, every=TIMING
         dec_set(warmup + i).decode(sp)
         if smp and not own_dec:
             d.record(stream)
-    torch.cuda.synchronize(device)
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    win.stop()  # synchronize, t1, barrier
     sampled = list(zip(kev, ev))[::every]
     t_enc = np.array([(q if own_enc else e)[0].elapsed_time((q if own_enc else e)[1]) for q, e in sampled]) / 1e3
     t_dec = np.array([(q if own_dec else e)[2].elapsed_time((q if own_dec else e)[3]) for q, e in sampled]) / 1e3
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    return elapsed, t_enc, t_dec, own_enc, own_dec
+    window = win.reduce()  # every rank's (t0, t1): the job's window is max(t1) - min(t0)
+    return window["elapsed_s"], t_enc, t_dec, own_enc, own_dec, window
 
 
 def c4_strong(lib, device, stream, dist, world, rank, pf, steps, warmup, verify):
@@ -600,7 +594,7 @@ def c4_strong(lib, device, stream, dist, world, rank, pf, steps, warmup, verify)
     sets = [Workload(lib, my, cfg["k"], cfg["S"], pf, device, group0, seed=3000 + rank, config_id=cfg["config_id"],
                      launch_groups=CONFIGS["c3"]["groups"]) for _ in range(2)]
     w = sets[0]
-    elapsed, t_enc, t_dec, own_enc, own_dec = time_steps(lib, sets, steps, warmup, stream, dist, "own", False)
+    elapsed, t_enc, t_dec, own_enc, own_dec, _ = time_steps(lib, sets, steps, warmup, stream, dist, "own", False)
     verified = digest_ok = None
     if verify:
         verified = all(ws.verify() for ws in sets)
@@ -694,7 +688,7 @@ def config_sub(lib, name, device, stream, dist, world, rank, pf, steps, warmup, 
                      config_id=cfg["config_id"]) for _ in range(2)]
     w = sets[0]
     # (kernel windows on every SUB_EVERY-th step: 10 samples of the default 80 steps)
-    elapsed, t_enc, t_dec, own_enc, own_dec = time_steps(lib, sets, steps, warmup, stream, dist, "own", False,
+    elapsed, t_enc, t_dec, own_enc, own_dec, _ = time_steps(lib, sets, steps, warmup, stream, dist, "own", False,
                                                          SUB_EVERY)
     verified = digest_ok = None
     if verify:
@@ -708,7 +702,7 @@ def config_sub(lib, name, device, stream, dist, world, rank, pf, steps, warmup, 
     if w.pks:
         for ws in sets:
             ws.use_packed(True)
-        _, _, t_dec_pk, _, own_pk = time_steps(lib, sets, steps, warmup, stream, dist, "own", False, SUB_EVERY)
+        _, _, t_dec_pk, _, own_pk, _ = time_steps(lib, sets, steps, warmup, stream, dist, "own", False, SUB_EVERY)
         t_pk = float(t_dec_pk.mean()) * 1e6 if own_pk else -1.0
         if verify:
             pk_ok = int(all(ws.verify() for ws in sets))
@@ -868,8 +862,9 @@ def main():
     sp = stream.cuda_stream
     torch.cuda.synchronize(device)
 
-    elapsed, t_enc, t_dec, own_enc, own_dec = time_steps(lib, sets, args.steps, args.warmup, stream, dist,
-                                                         args.timing, args.hot_decode)
+    elapsed, t_enc, t_dec, own_enc, own_dec, window = time_steps(lib, sets, args.steps, args.warmup, stream, dist,
+                                                                 args.timing, args.hot_decode)
+    ranks = gather_objects(dist, dict(rank=rank, local_rank=local, **device_identity(device)))
 
     verified, digest_ok = None, None
     if not args.no_verify:
@@ -998,6 +993,14 @@ def main():
                                 "parity_operand": "cold: written one step (>= 1.7 GB of traffic) before"
                                 if not (args.hot_decode or nset == 1) else "hot: written by this step's encode"},
             "copy_ceiling_GBps": round(ceiling, 1),  # rfec_probe_copy, read + write bytes
+            "timing_window": {"rule": "value = all ranks' bytes x steps / (max over ranks of t1 - min over ranks "
+                                      "of t0); t0 after the opening barrier + synchronize, t1 after the closing "
+                                      "synchronize (before the closing barrier), CLOCK_MONOTONIC",
+                              **{kk: window[kk] for kk in ("start_skew_us", "stop_skew_us", "t0_us", "t1_us",
+                                                            "clock")},
+                              "rank_elapsed_max_ms": round(window["rank_elapsed_max_s"] * 1e3, 4)},
+            "ranks": ranks,
+            "distinct_devices": len({r["pci_bus_id"] for r in ranks}),
             "verified": verified,
             "verified_vs_reference_digest": digest_ok,
             "tuning": args.tuning,

@@ -91,6 +91,13 @@ int flex_fec_recover(sim_segment_t* segs[], int segs_count, sim_fec_t* fec, sim_
 /* SIM_VIDEO_SIZE this library's drop-in symbols were compiled with. */
 int rfec_sim_video_size(void);
 
+/* ABI version of this header / library.  A caller compiled against one
+ * header checks rfec_abi_version() == RFEC_ABI_VERSION before using structs
+ * whose size changed.  History: 5 -- rfec_host_timing grew from 48 to 56
+ * bytes (zero_copy, reserved); 6 -- rfec_abi_version itself. */
+#define RFEC_ABI_VERSION 6
+uint32_t rfec_abi_version(void);
+
 /* ------------------------------------------------------------------------ */
 /* Batched device API                                                        */
 /* ------------------------------------------------------------------------ */

@@ -64,6 +64,9 @@ int rfec_set_error_sys(int code, const char* what, int err)
 
 int rfec_sim_video_size(void) { return SIM_VIDEO_SIZE; }
 
+uint32_t rfec_abi_version(void) { return RFEC_ABI_VERSION; }
+_Static_assert(sizeof(rfec_host_timing) == 56, "rfec_host_timing: ABI 5 layout (bump RFEC_ABI_VERSION)");
+
 unsigned g_tuning = 0;
 void rfec_set_tuning(unsigned flags) { g_tuning = flags; }
 unsigned rfec_get_tuning(void) { return g_tuning; }

@@ -71,6 +71,38 @@ __device__ __forceinline__ void st_host16(uint8_t* p, v4u v) { __builtin_memcpy(
 __device__ __forceinline__ void st_host4(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
 __device__ __forceinline__ void st_host2(uint8_t* p, uint32_t v) { *reinterpret_cast<uint16_t*>(p) = (uint16_t)v; }
 
+// The part of a 16-byte access that lies inside a struct: `avail` = the
+// struct's bytes from the access on (a multiple of 4, the structs' sizes and
+// the accesses' offsets being so).  With SIM_VIDEO_SIZE % 16 != 0 (1000: 63
+// chunks = 1,008 bytes of data lanes) a struct's last chunk reaches past its
+// end; those dwords are neither read nor written (the next struct's header,
+// or past the pinned block for the last one).
+__device__ __forceinline__ v4u ld_host_part(const uint8_t* p, int avail)
+{
+    if (avail >= 16)
+        return ld_host16(p);
+    v4u v = {0, 0, 0, 0};
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+        if (4 * d < avail)
+            v[d] = ld_host4(p + 4 * d);
+    return v;
+}
+__device__ __forceinline__ void st_host_part(uint8_t* p, v4u v, int avail)
+{
+    if (avail >= 16) {
+        st_host16(p, v);
+        return;
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d)
+        if (4 * d < avail)
+            st_host4(p + 4 * d, v[d]);
+}
+// sizeof(sim_segment_t) / sizeof(sim_fec_t) for a SIM_VIDEO_SIZE: the data
+// offset + video, up to the structs' 4-byte alignment (sim_proto.h:80-99,157-174)
+__device__ __forceinline__ int struct_bytes(uint32_t doff, uint32_t video) { return (int)((doff + video + 3u) & ~3u); }
+
 // bytes [2, 18) of the 20 bytes (x0..x3, nx)
 __device__ __forceinline__ v4u shift2(const v4u& x, uint32_t nx)
 {
@@ -115,15 +147,16 @@ __device__ __forceinline__ void gather_lane(const GatherSide& S, uint32_t t, uin
     const uint8_t* p = reinterpret_cast<const uint8_t*>(raw & ~(uint64_t)3);
     const uint32_t nload = (video + 15u) / 16u; // chunks that hold struct bytes
     const bool ld = p && !(raw & 1u) && j < nload;
+    const int avail = struct_bytes(DOFF, video) - (int)(DOFF - 2u + 16u * j); // struct bytes from the load on
     v4u x = {0, 0, 0, 0};
     uint32_t sz = 0;
     if (ld)
-        x = ld_host16(p + DOFF - 2u + 16u * j);
+        x = ld_host_part(p + DOFF - 2u + 16u * j, avail);
     if (p && (ld || j == 0))
         sz = *reinterpret_cast<const uint16_t*>(p + DOFF - 2u); // (one address per struct: coalesced)
     uint32_t nx = next_lane(x[0]);
     if (ld && ((threadIdx.x & 63u) == 63u || j + 1u >= nload))
-        nx = ld_host4(p + DOFF + 14u + 16u * j); // (still inside the struct: its size covers data + 2)
+        nx = avail >= 20 ? ld_host4(p + DOFF + 14u + 16u * j) : 0u; // (only inside the struct)
     if (!live)
         return;
     const int n = (int)min(sz, video) - (int)(16u * j);
@@ -200,8 +233,8 @@ __global__ __launch_bounds__(kBlock) void k_host_scatter_fec(const uint64_t* __r
     if (!live)
         return;
     uint8_t* p = reinterpret_cast<uint8_t*>(fptrs[o]);
-    if (dat)
-        st_host16(p + 44u + 16u * j, shift2(c, nx));
+    if (dat) // (the last chunk only up to the struct's end: 1,044 B at SIM_VIDEO_SIZE 1000)
+        st_host_part(p + 44u + 16u * j, shift2(c, nx), struct_bytes(42u, video) - (int)(44u + 16u * j));
     if (j != 0)
         return;
     const uint32_t g = fdiv(o, divN), l = o - g * divN.d;
@@ -262,7 +295,7 @@ __global__ __launch_bounds__(kBlock) void k_host_scatter_seg(const uint64_t* __r
         nx = 0; // past data: the struct's padding
     if (!dat)
         return;
-    st_host16(p + 36u + 16u * j, shift2(c, nx));
+    st_host_part(p + 36u + 16u * j, shift2(c, nx), struct_bytes(34u, video) - (int)(36u + 16u * j));
     if (j != 0)
         return;
     const uint32_t* h = out_hdr_dw + (size_t)o * 5;

@@ -167,18 +167,22 @@ void rfec_pinned_free(void* p)
 
 /* 1 when every non-NULL pointer of ptrs[0, n) addresses `obj` bytes inside one
  * registered block (its device offset in *delta); 1 with delta 0 when all are
- * NULL */
+ * NULL.  0 when a pointer is not 4-byte aligned: the zero-copy kernels move
+ * the structs in dwords and use the pointers' low 2 bits as flags
+ * (rfec_hostio.hip), so such a batch takes the staged form. */
 static int pinned_span(const void* const* ptrs, size_t n, size_t obj, intptr_t* delta)
 {
     uintptr_t lo = UINTPTR_MAX, hi = 0;
+    *delta = 0;
     for (size_t i = 0; i < n; ++i) {
         const uintptr_t a = (uintptr_t)ptrs[i];
         if (!a)
             continue;
+        if (a & 3u)
+            return 0;
         lo = a < lo ? a : lo;
         hi = a > hi ? a : hi;
     }
-    *delta = 0;
     if (lo == UINTPTR_MAX)
         return 1;
     hi += obj;

@@ -2196,10 +2196,14 @@ hipError_t launch_encode(const EncLaunch& a, unsigned flags)
     const rfec_kplan* P = a.P;
     const bool generic = (flags & RFEC_KFLAG_GENERIC) != 0;
     uint32_t col = 0;
+    // k_encode_out / k_encode_matrix_out address a wave's groups (at most kWave + 1 of them) through one
+    // buffer descriptor of range kNoLoad: per-lane offsets must stay below it, or a large stride would
+    // read zeros past the range (the same bound as the fused decodes, launch_recover)
+    const bool rsrc_ok = (uint64_t)(kWave + 1) * P->k * a.stride < kNoLoad;
     if (!generic && is_row_layout(P, &col) && (uint64_t)a.groups * ((P->k + col - 1) / col) * a.cd < (1ull << 32)) {
-        if (P->k == 10 && col == 4)
+        if (P->k == 10 && col == 4 && rsrc_ok)
             return launch_rows_out<10, 4>(a);
-        if (P->k == 32 && col == 4)
+        if (P->k == 32 && col == 4 && rsrc_ok)
             return launch_rows_out<32, 4>(a);
         // other row layouts: the same output-mapped lanes with k and col at run time
         // (an 8-wide instantiation compiled to 230 VGPRs, two waves per SIMD: 0.33 of 8 TB/s at k = 20,
@@ -2211,7 +2215,7 @@ hipError_t launch_encode(const EncLaunch& a, unsigned flags)
     }
     const uint32_t C = a.stride / 16;
     const uint32_t total = a.groups * a.cd;
-    if (!generic && P->k >= 6 && P->k <= 16 && is_full_matrix(P, P->k <= 9 ? 3 : 4)) {
+    if (!generic && rsrc_ok && P->k >= 6 && P->k <= 16 && is_full_matrix(P, P->k <= 9 ? 3 : 4)) {
         const uint32_t head = enc_head(a);
         const uint32_t nl = P->n_lines, tot = a.groups * nl * a.cd;
         const dim3 grid_o(head + enc_rounds(tot));

@@ -146,6 +146,9 @@ class rfec_host_timing(C.Structure):
                 ("zero_copy", C.c_uint32), ("reserved", C.c_uint32)]
 
 
+RFEC_ABI_VERSION = 6  # include/razor_fec.h
+
+
 def seg_dtype(video_size: int) -> np.dtype:
     """numpy mirror of sim_segment_t (sim_proto.h:80-99)."""
     size = ((34 + video_size + 3) // 4) * 4
@@ -195,6 +198,7 @@ _SIGS = {
     "flex_fec_generate": (C.c_int, [_P, C.c_int, _P]),
     "flex_fec_recover": (C.c_int, [_P, C.c_int, _P, _P]),
     "rfec_sim_video_size": (C.c_int, []),
+    "rfec_abi_version": (C.c_uint32, []),
     "rfec_num_packets": (C.c_int, [C.c_uint16, C.c_uint8, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8)]),
     "rfec_plan_from_fraction": (C.c_int, [C.c_uint16, C.c_uint8, C.c_uint, C.POINTER(rfec_plan)]),
     "rfec_plan_matrix": (C.c_int, [C.c_uint16, C.c_uint8, C.c_uint8, C.c_uint, C.POINTER(rfec_plan)]),
@@ -311,6 +315,9 @@ class Native:
         self.video_size = self.lib.rfec_sim_video_size()
         if self.video_size != video_size:
             raise RfecError(f"{self.path} was built with SIM_VIDEO_SIZE={self.video_size}")
+        abi = self.lib.rfec_abi_version() if hasattr(self.lib, "rfec_abi_version") else RFEC_ABI_VERSION
+        if abi != RFEC_ABI_VERSION:
+            raise RfecError(f"{self.path}: ABI {abi}, these bindings expect {RFEC_ABI_VERSION}")
         self.sim_segment_t, self.sim_fec_t = sim_types(self.video_size)
 
     # -- planner -------------------------------------------------------------

@@ -287,6 +287,37 @@ def test_empty_and_degenerate(product):
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("layers", [1, 3])
+def test_encode_large_stride_small_capacity(product1200, oracle1200, layers):
+    """A legal batch whose slot stride is far larger than its capacity (16-B
+    payloads in 40 MiB slots): the fused encodes address a wave's groups through
+    one buffer descriptor whose range is ~2 GiB, and one wave here spans all 8
+    groups (2.9 GB of offsets), so launch_encode must take the generic kernel.
+    Parities / meta / sizes equal the oracle's on the compact layout."""
+    lib, o = product1200, oracle1200
+    G, k, cap, stride = 8, 10, 16, 40 << 20
+    sh_c, hdr = o.fill_groups(307, G, k, cap, ragged=True)
+    plan = o.plan_from_fraction(k, 80, layers)
+    n = plan.n_lines
+    par_c, meta_c, fs_c, st_c = o.encode_batch(plan, sh_c, hdr, cap)
+    sh = torch.zeros((G, k, stride), dtype=torch.uint8, device="cuda")
+    sh[:, :, :16] = torch.from_numpy(sh_c).cuda()
+    dh = torch.from_numpy(hdr.view(np.uint8).reshape(-1).copy()).cuda()
+    par = torch.full((G, n, stride), 0x5A, dtype=torch.uint8, device="cuda")
+    meta = torch.empty((G, n, 20), dtype=torch.uint8, device="cuda")
+    fs = torch.empty((G, n), dtype=torch.int16, device="cuda")
+    st = torch.empty((G, n), dtype=torch.int8, device="cuda")
+    lib.encode_batch(plan, G, stride, cap, sh.data_ptr(), dh.data_ptr(), par.data_ptr(), meta.data_ptr(),
+                     fs.data_ptr(), st.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(par[:, :, :16].cpu().numpy(), par_c[:, :, :16])
+    assert np.array_equal(meta.cpu().numpy().reshape(-1), meta_c.view(np.uint8).reshape(-1))
+    assert np.array_equal(fs.cpu().numpy().view(np.uint16), fs_c)
+    assert np.array_equal(st.cpu().numpy(), st_c)
+    del sh, par
+    torch.cuda.empty_cache()
+
+
 def test_capacity_status(product):
     """status -1 where a line's fec_data_size exceeds capacity (flex_fec_xor.c:27-28)."""
     lib = product
@@ -517,6 +548,126 @@ def test_host_recover_groups(product1200, oracle1200, k, layers, G, mem):
     _fields_equal(out, pout, "data_size", "data")
     untouched = (oi.reshape(-1) == 0xFF) | (op == 0)
     assert (out.view(np.uint8).reshape(G * E, -1)[untouched] == 0xA5).all()
+
+
+def _gapped(lib, n, dtype, gap, fill, canary):
+    """n structs of `dtype` in ONE rfec_pinned_alloc block, `gap` canary bytes
+    after each (the last struct ends exactly at the block's end): returns the
+    block's bytes, the structs' addresses and a structured view per struct."""
+    isz = np.dtype(dtype).itemsize
+    step = isz + gap
+    raw, keep = lib.pinned_array((n * step - gap,), np.uint8)
+    raw[...] = canary
+    for i in range(n):
+        raw[i * step:i * step + isz] = fill
+    ptrs = raw.ctypes.data + np.arange(n, dtype=np.uint64) * step
+    return raw, keep, ptrs, step, isz
+
+
+def _gaps_intact(raw, n, step, isz, canary):
+    g = np.ones(raw.shape[0], bool)
+    for i in range(n):
+        g[i * step:i * step + isz] = False
+    return (raw[g] == canary).all()
+
+
+def test_host_zero_copy_1000_struct_bounds(product, oracle1000):
+    """The zero-copy kernels at SIM_VIDEO_SIZE 1000 (librazor_fec.so): the
+    data runs 1,000 bytes = 62.5 chunks, so a struct's last 16-byte chunk
+    reaches past sizeof(sim_fec_t) = 1,044 / sizeof(sim_segment_t) = 1,036.
+    Structs placed with 16-byte canary gaps between them (and the last one
+    ending at the pinned block's end): encode parities and recovered out_seg
+    equal the oracle's, and no byte outside a written struct changes."""
+    from razor_amd.fec import fec_dtype, seg_dtype
+
+    lib, o = product, oracle1000
+    G, k, S, E, CAN = 29, 10, 1000, 3, 0xC3
+    shards, hdr = o.fill_groups(301, G, k, S, ragged=True)
+    sdt, fdt = seg_dtype(1000), fec_dtype(1000)
+    assert sdt.itemsize == 1036 and fdt.itemsize == 1044
+    plan = o.plan_from_fraction(k, 80, 3)
+    n = plan.n_lines
+    aos = o.to_aos(shards, hdr)
+    sraw, ks, sp, sstep, ssz = _gapped(lib, G * k, sdt, 16, 0, CAN)
+    for i in range(G * k):
+        sraw[i * sstep:i * sstep + ssz] = aos[i:i + 1].view(np.uint8)
+    fraw, kf, fp, fstep, fsz = _gapped(lib, G * n, fdt, 16, 0xA5, CAN)
+    t = lib.host_encode_groups(plan, G, sp, fp, fec_id0=7)
+    assert t["zero_copy"] == 1
+    assert _gaps_intact(fraw, G * n, fstep, fsz, CAN)
+    assert _gaps_intact(sraw, G * k, sstep, ssz, CAN)
+    nref, ref = o.encode_aos(plan, G, aos)
+    ref = ref.view(fdt).reshape(-1)
+    got = np.stack([fraw[i * fstep:i * fstep + fsz] for i in range(G * n)]).reshape(-1).view(fdt)
+    for f in ("fec_id", "row", "col", "index", "count", "base_id", "fec_data_size", "meta"):
+        assert np.array_equal(got[f], ref[f]), f
+    for j in range(G * n):
+        L = int(ref["fec_data_size"][j])
+        assert np.array_equal(got["fec_data"][j, :L], ref["fec_data"][j, :L]), j
+        assert not got["fec_data"][j, L:].any(), j
+    # receive: 1-3 segments and 0-1 parities lost per group, out_seg structs gapped too
+    rng = np.random.default_rng(11)
+    present = np.zeros((G, 2), np.uint64)
+    ppm = np.zeros(G, np.uint64)
+    sp_rx, fp_rx = sp.copy(), fp.copy()
+    for g in range(G):
+        lost = rng.choice(k, int(rng.integers(1, 4)), replace=False)
+        sp_rx[g * k + lost] = 0
+        present[g, 0] = sum(1 << i for i in range(k) if i not in lost)
+        plost = rng.choice(n, int(rng.integers(0, 2)), replace=False)
+        fp_rx[g * n + plost] = 0
+        ppm[g] = sum(1 << l for l in range(n) if l not in plost)
+    oraw, ko, op, ostep, osz = _gapped(lib, G * E, sdt, 16, 0xA5, CAN)
+    oi, rec, t = lib.host_recover_groups(plan, G, sp_rx, fp_rx, E, op)
+    assert t["zero_copy"] == 1
+    assert _gaps_intact(oraw, G * E, ostep, osz, CAN)
+    rx_sh, rx_h = shards.copy(), hdr.copy()
+    for g in range(G):
+        for i in range(k):
+            if not (int(present[g, 0]) >> i) & 1:
+                rx_sh[g, i] = 0
+                rx_h[g, i] = 0
+    par = got["fec_data"].reshape(G, n, S)
+    par = np.pad(par, ((0, 0), (0, 0), (0, shards.shape[2] - S)))
+    meta = np.ascontiguousarray(got["meta"].reshape(G, n))
+    _, _, o_i, o_rec = o.recover_batch_out(plan, rx_sh, rx_h, present, par, meta,
+                                           got["fec_data_size"].reshape(G, n), ppm, S, E)
+    assert np.array_equal(oi, o_i) and np.array_equal(rec, o_rec)
+    assert (oi != 0xFF).sum() > G // 2
+    for g in range(G):
+        for e in range(E):
+            i = int(oi[g, e])
+            blk = oraw[(g * E + e) * ostep:(g * E + e) * ostep + osz]
+            if i == 0xFF:
+                assert (blk == 0xA5).all(), (g, e)
+                continue
+            got_s, want = blk.view(sdt)[0], aos[g * k + i]
+            for f in ("packet_id", "fid", "timestamp", "index", "total", "ftype", "payload_type", "data_size"):
+                assert got_s[f] == want[f], (g, e, f)
+            nb = int(want["data_size"])
+            assert np.array_equal(got_s["data"][:nb], want["data"][:nb]) and not got_s["data"][nb:].any()
+
+
+def test_host_zero_copy_unaligned_takes_staged(product1200, oracle1200):
+    """A struct pointer that is not 4-byte aligned inside a pinned block: the
+    zero-copy kernels move dwords and use the low pointer bits as flags, so
+    the batch takes the staged form (timing.zero_copy = 0), same parities."""
+    from razor_amd.fec import fec_dtype, seg_dtype
+
+    lib, o = product1200, oracle1200
+    G, k, S = 8, 10, 1200
+    shards, hdr = o.fill_groups(305, G, k, S, ragged=True)
+    aos = o.to_aos(shards, hdr)
+    sdt, fdt = seg_dtype(1200), fec_dtype(1200)
+    raw, keep = lib.pinned_array((G * k * sdt.itemsize + 8,), np.uint8)
+    raw[2:2 + aos.nbytes] = aos.view(np.uint8)
+    sp = raw.ctypes.data + 2 + np.arange(G * k, dtype=np.uint64) * sdt.itemsize
+    plan = o.plan_from_fraction(k, 80, 3)
+    fecs, kf = _host_arrays(lib, G * plan.n_lines, fdt, "pinned")
+    t = lib.host_encode_groups(plan, G, sp, _ptrs(fecs), fec_id0=1)
+    assert t["zero_copy"] == 0
+    _, ref = o.encode_aos(plan, G, aos)
+    _fields_equal(fecs, ref.view(fdt).reshape(-1), "fec_data_size", "fec_data")
 
 
 @pytest.mark.parametrize("name", ["c2_k10_rows_S1200_G65536", "c3_k10_full_S1200_G65536",

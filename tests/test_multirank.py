@@ -50,13 +50,13 @@ def _worker(rank, world, port, total, outdir):
     def step():
         out["r"] = o.encode_batch(plan, shards[lo:lo + n], hdr[lo:lo + n], 1200)
 
-    elapsed = timed_steps(step, steps=3, warmup=1, sync=lambda: None, dist=dist)
+    win = timed_steps(step, steps=3, warmup=1, sync=lambda: None, dist=dist)
     parity, meta, fsize, status = out["r"]
     digs = [None] * world
     dist.all_gather_object(digs, {"lo": lo, "n": n, "digest": [_digest(parity[g], meta[g], fsize[g])
                                                                for g in range(n)]})
     if rank == 0:
-        Path(outdir, "result.json").write_text(json.dumps({"shards": digs, "elapsed": elapsed}))
+        Path(outdir, "result.json").write_text(json.dumps({"shards": digs, "window": win}))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -81,7 +81,14 @@ def test_batch_split_world2(tmp_path, total):
         got += s["digest"]
     assert expect_lo == total
     assert got == whole
-    assert res["elapsed"] > 0
+    # the window bench.py's time_steps uses (razor_amd/dist.StepWindow): every rank's CLOCK_MONOTONIC t0 / t1,
+    # the job's time from the first start to the last stop, skews >= 0
+    w = res["window"]
+    assert len(w["t0_us"]) == len(w["t1_us"]) == world
+    assert min(w["t0_us"]) == 0 and w["start_skew_us"] == max(w["t0_us"]) >= 0 and w["stop_skew_us"] >= 0
+    assert all(b >= a for a, b in zip(w["t0_us"], w["t1_us"]))
+    assert w["elapsed_s"] >= w["rank_elapsed_max_s"] > 0
+    assert abs(w["elapsed_s"] * 1e6 - max(w["t1_us"])) < 1.0
 
 
 def test_shard_groups_cover():

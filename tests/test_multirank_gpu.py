@@ -124,6 +124,7 @@ def test_bench_two_ranks_one_gpu():
     assert d["config"]["workload"].startswith("c3: k10_r3_S1200_G65536 per GPU x 2")
     assert d["verified"] is True and d["verified_vs_reference_digest"] is True
     assert d["value"] > 0
+    _check_window(d, 2)
     # one kernel per call: the roofline takes each kernel's own start / stop events
     for key in ("roofline", "decode_roofline"):
         assert d[key]["timing"].startswith("the kernel's own") and d[key]["launch_us"] > 0
@@ -194,8 +195,24 @@ def test_bench_n_ranks_one_gpu(n):
     assert d["config"]["total_groups"] == n * 65536
     assert d["config"]["workload"].startswith(f"c3: k10_r3_S1200_G65536 per GPU x {n}")
     assert d["verified"] is True and d["verified_vs_reference_digest"] is True
+    _check_window(d, n)
     _check_c4_strong(d["c4_strong"], n)
     _check_subs(d, n)
+
+
+def _check_window(d, n):
+    """The line's clock (razor_amd/dist.StepWindow): every rank's CLOCK_MONOTONIC
+    t0 / t1, ms_per_step = (max t1 - min t0) / steps, the start skew, and every
+    rank's physical device (here all share the one leased GPU)."""
+    w = d["timing_window"]
+    assert len(w["t0_us"]) == len(w["t1_us"]) == n and min(w["t0_us"]) == 0
+    assert w["start_skew_us"] == max(w["t0_us"]) and w["start_skew_us"] >= 0 and w["stop_skew_us"] >= 0
+    assert abs(max(w["t1_us"]) / 1e3 / d["steps"] - d["ms_per_step"]) < 1e-3
+    assert w["rank_elapsed_max_ms"] <= max(w["t1_us"]) / 1e3 + 1e-6
+    assert [r["rank"] for r in d["ranks"]] == list(range(n))
+    for r in d["ranks"]:
+        assert len(r["pci_bus_id"].split(":")) == 3 and r["name"]
+    assert d["distinct_devices"] == 1
 
 
 @pytest.mark.timeout(900)
