@@ -94,7 +94,8 @@ int rfec_sim_video_size(void);
 /* ABI version of this header / library.  A caller compiled against one
  * header checks rfec_abi_version() == RFEC_ABI_VERSION before using structs
  * whose size changed.  History: 5 -- rfec_host_timing grew from 48 to 56
- * bytes (zero_copy, reserved); 6 -- rfec_abi_version itself. */
+ * bytes (zero_copy, reserved); 6 -- rfec_abi_version, rfec_rx_session_info grew
+ * from 24 to 40 bytes (threads, batches_*), rfec_rx_session_set_threads. */
 #define RFEC_ABI_VERSION 6
 uint32_t rfec_abi_version(void);
 
@@ -651,10 +652,26 @@ typedef struct {
     uint32_t rows_held;       /* HBM payload rows allocated */
     uint32_t pending;         /* datagrams of the batch the last _async call
                                  started: the records its next call writes */
+    uint32_t threads;         /* control-plane shards (1: serial) */
+    uint32_t batches_parallel;    /* batches replayed by the shards in parallel */
+    uint32_t batches_serial;      /* batches replayed in arrival order */
+    uint32_t batches_rolled_back; /* parallel replays undone (then replayed in order) */
 } rfec_rx_session_info;
 
-/* NULL on bad arguments (stride % 16, capacity > stride) or no memory. */
+/* NULL on bad arguments (stride % 16, capacity > stride) or no memory.
+ *
+ * The control plane is sharded by fec_id over RFEC_RX_THREADS (default 8)
+ * shards, each replayed in arrival order by its own thread: groups are
+ * independent in the reference (sim_fec.c:141-207 keys a flex by fec_id).
+ * Deliveries are those of the serial replay, always: a batch runs in parallel
+ * only while every packet id belongs to one fec_id and no parity of the batch
+ * can meet the 3 s drop (sim_fec.c:148) through max_ts; one that breaks either
+ * is rolled back and replayed in arrival order (a packet id under two fec_ids
+ * merges the shards into one for the rest of the session). */
 rfec_rx_session* rfec_rx_session_create(uint32_t stride, uint32_t capacity);
+/* Control-plane shards / threads (1..64) of a session that has not been
+ * pushed to yet; 1 = the serial replay. */
+int rfec_rx_session_set_threads(rfec_rx_session* s, uint32_t threads);
 void rfec_rx_session_destroy(rfec_rx_session* s);
 /* recs / payload: DEVICE (rfec_wire_parse output, rows of the session's
  * stride), n records in arrival order; out / out_payload: HOST, the segments

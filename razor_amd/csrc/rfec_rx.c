@@ -36,7 +36,18 @@ typedef struct { /* open addressing u32 -> u32, value 0 = empty */
     uint32_t mask, n;
 } hmap;
 
-static uint32_t hm_home(const hmap* m, uint32_t k) { return (k * 0x9E3779B1u) & m->mask; }
+/* Home slot: keys in blocks of 16 (consecutive keys, consecutive slots: one
+ * cache line serves several lookups, as packet ids and fec_ids arrive nearly
+ * in sequence), the blocks spread by Fibonacci hashing on the table's bit
+ * width.  (A multiplicative hash of each key sent every lookup of the c3
+ * stream to a new line; the key's low bits alone alias a shard's keys, which
+ * take every T-th group, onto a quarter of the table.) */
+static uint32_t key_home(uint32_t mask, uint32_t k)
+{
+    const uint32_t bits = 32u - (uint32_t)__builtin_clz(mask); /* log2(capacity), >= 6 */
+    return ((((k >> 4) * 0x9E3779B1u) >> (36u - bits)) << 4 | (k & 15u)) & mask;
+}
+static uint32_t hm_home(const hmap* m, uint32_t k) { return key_home(m->mask, k); }
 
 static int hm_init(hmap* m, uint32_t n)
 {
@@ -123,12 +134,55 @@ typedef struct {
     uint32_t fec_ts;       /* flex->fec_ts = send_ts of the parity that created it (sim_fec.c:157) */
     int ref_ok;            /* col >= 2 && row >= 1 && count >= 1 (flex_fec_receiver.c:214, 250) */
     uint32_t gstamp;       /* == rx_sim.epoch: gslot is this device call's group slot */
+    uint32_t jstamp;       /* == rx_sim.jepoch: saved in this batch's journal (rx_touch) */
 } rx_inst;
 
 typedef struct {
     rfec_hdr hdr;
     uint32_t inst;
+    uint32_t shard; /* rx_device's merged list: the shard holding inst */
 } rx_event; /* a recovered segment: pending, then delivered */
+
+/* ------------------------------------------------------------------------ */
+/* Sharded sessions (rfec_rx_session_*): the control plane partitioned by     */
+/* fec_id over T shards, each a full rx_sim replayed by its own thread in     */
+/* arrival order.  Groups are independent in the reference (the receiver     */
+/* keys a flex by fec_id, sim_fec.c:141-207), and every other piece of       */
+/* state is keyed by packet id: first-arrival dedupe, the segment cache a    */
+/* new flex replays (sim_fec.c:121-138), the recovered-id map (:104-119).    */
+/* Those stay inside one shard as long as every packet id belongs to one     */
+/* fec_id -- its segments carry it, the parity ranges [base_id, base_id +    */
+/* count) claim it, and recovery stays inside its flex's range -- which is  */
+/* checked after each batch (each shard logs its claims; T threads insert    */
+/* them into the owner tables, partitioned by packet-id block, so no two     */
+/* threads write one table; recovery ranges as they happen).  The one global */
+/* quantity is max_ts, which gates the 3 s parity drop (sim_fec.c:148): a    */
+/* batch runs in parallel only when no parity can be dropped by it (its      */
+/* send_ts + 3000 >= every earlier segment timestamp of the batch, checked   */
+/* before the replay, and >= every segment recovered before it, checked as   */
+/* recoveries happen).  A batch that breaks either rule is rolled back       */
+/* (journal below) and replayed in arrival order: over the shards with one   */
+/* max_ts, or, when a packet id crossed fec_ids, after merging the shards    */
+/* into one (the session then stays serial).                                */
+/* ------------------------------------------------------------------------ */
+#define RX_MAX_THREADS 64 /* shards (= replay threads) of a session */
+
+
+#define RX_CONFLICT_OWNER 1
+#define RX_CONFLICT_TS 2
+
+typedef struct { /* one batch's parallel replay, shared by the shards */
+    uint32_t T;           /* shards */
+    const uint32_t* smin; /* [n]: min over the batch's later parities of send_ts + 3000 (by batch position) */
+    uint32_t a0;          /* the batch's first record */
+    int ts_check;         /* recoveries checked against smin (the parallel replay) */
+    int conflict;         /* RX_CONFLICT_* (atomic) */
+} rx_par;
+
+typedef struct {
+    uint8_t map; /* 0 seen, 1 cache, 2 flex_of, 3 shape_of */
+    uint32_t key, old; /* old value, 0 = absent */
+} rx_jop;
 
 typedef struct {
     const rfec_wire_rec* R;
@@ -149,19 +203,28 @@ typedef struct {
     uint32_t nout, outcap;
     rfec_hdr* rh;          /* headers of delivered (recovered) segments the cache refers to */
     uint32_t nrh, rhcap;
-    uint32_t* dl;          /* instances that deliver in this device call */
-    uint32_t ndl, dlcap;
-    rfec_line_job* jobs;   /* groups above RFEC_MAX_K: this call's line jobs (rx_big_peel) */
-    uint32_t njobs, jobcap;
-    uint16_t* jlevel;      /* a job's dependency level (1 = arrived members only) */
-    uint32_t jlevelcap;
-    int32_t* jmem;         /* member codes: record >= 0, job j as -1 - j */
-    uint32_t njmem, jmemcap;
     uint32_t epoch;        /* device call counter (rx_inst.gstamp) */
     int oom;
+    /* sharded sessions: the batch's shared context, and the journal that rolls
+       this shard back to the batch's start (map operations, the instances the
+       batch touched -- saved on first touch with their slot / line tables --,
+       and the tables' lengths) */
+    rx_par* P;
+    uint64_t* claims;   /* this batch's packet-id claims: seq << 32 | fec_id + 1 */
+    uint32_t nclaims, claimcap;
+    uint64_t* cpart;    /* the claims by owner-table partition (rx_bucket_claims), offsets in coff */
+    uint32_t cpartcap;
+    uint32_t coff[RX_MAX_THREADS + 1];
+    uint32_t* claimed;  /* [65536 / T + 1][2]: the range last claimed per fec_id / T (base, count + 1) */
+    int jon;
+    uint32_t jepoch, j_ng, j_nslot, j_nline, j_ns, j_nrh, j_max_ts, j_dropped, j_unmod;
+    rx_jop* jops;
+    uint32_t njops, jopcap;
+    uint8_t* jsave;
+    size_t njsave, jsavecap;
 } rx_sim;
 
-#define RX_GROW(ptr, n, cap, need, T)                                                   \
+#define RX_GROW_F(flag, ptr, n, cap, need, T)                                          \
     do {                                                                                \
         if ((n) + (need) > (cap)) {                                                     \
             uint32_t c_ = (cap) ? 2 * (cap) : 1024;                                     \
@@ -169,13 +232,188 @@ typedef struct {
                 c_ *= 2;                                                                \
             T* p_ = (T*)realloc((ptr), (size_t)c_ * sizeof(T));                         \
             if (!p_) {                                                                  \
-                X->oom = 1;                                                             \
+                (flag) = 1;                                                             \
                 break;                                                                  \
             }                                                                           \
             (ptr) = p_;                                                                 \
             (cap) = c_;                                                                 \
         }                                                                               \
     } while (0)
+#define RX_GROW(ptr, n, cap, need, T) RX_GROW_F(X->oom, ptr, n, cap, need, T)
+
+/* -- the journal (sharded sessions) ------------------------------------------ */
+static hmap* rx_map(rx_sim* X, int m)
+{
+    return m == 0 ? &X->seen : m == 1 ? &X->cache : m == 2 ? &X->flex_of : &X->shape_of;
+}
+
+static void rx_jlog(rx_sim* X, int m, uint32_t k, uint32_t old)
+{
+    RX_GROW(X->jops, X->njops, X->jopcap, 1, rx_jop);
+    if (X->oom)
+        return;
+    X->jops[X->njops++] = (rx_jop){(uint8_t)m, k, old};
+}
+
+/* hm_put / hm_del on one of X's maps, journaled while a batch may roll back */
+static int rx_put(rx_sim* X, int m, uint32_t k, uint32_t v)
+{
+    if (X->jon)
+        rx_jlog(X, m, k, hm_get(rx_map(X, m), k));
+    return hm_put(rx_map(X, m), k, v);
+}
+static void rx_del(rx_sim* X, int m, uint32_t k)
+{
+    if (X->jon) {
+        const uint32_t o = hm_get(rx_map(X, m), k);
+        if (!o)
+            return;
+        rx_jlog(X, m, k, o);
+    }
+    hm_del(rx_map(X, m), k);
+}
+
+/* Saves instance ii (and its slot / line tables) the first time this batch
+ * changes it; instances the batch created are dropped whole on rollback. */
+static void rx_touch(rx_sim* X, uint32_t ii)
+{
+    if (!X->jon || ii >= X->j_ng || X->G[ii].jstamp == X->jepoch)
+        return;
+    rx_inst* g = &X->G[ii];
+    const int sh = g->shape != UINT32_MAX;
+    const uint32_t nc = sh ? g->count : 0, nl = sh ? X->S[g->shape].n_lines : 0;
+    const size_t need = 4 + sizeof(rx_inst) + (size_t)nc * (4 + sizeof(rfec_hdr)) + (size_t)nl * 4;
+    if (X->njsave + need > X->jsavecap) {
+        size_t c = X->jsavecap ? 2 * X->jsavecap : 1 << 16;
+        while (c < X->njsave + need)
+            c *= 2;
+        uint8_t* p = (uint8_t*)realloc(X->jsave, c);
+        if (!p) {
+            X->oom = 1;
+            return;
+        }
+        X->jsave = p;
+        X->jsavecap = c;
+    }
+    uint8_t* w = X->jsave + X->njsave;
+    memcpy(w, &ii, 4);
+    memcpy(w + 4, g, sizeof(rx_inst));
+    w += 4 + sizeof(rx_inst);
+    memcpy(w, X->slot_src + g->slot0, (size_t)nc * 4);
+    memcpy(w + (size_t)nc * 4, X->slot_hdr + g->slot0, (size_t)nc * sizeof(rfec_hdr));
+    memcpy(w + (size_t)nc * (4 + sizeof(rfec_hdr)), X->line_par + g->line0, (size_t)nl * 4);
+    X->njsave += need;
+    g->jstamp = X->jepoch;
+}
+
+static void rx_journal_begin(rx_sim* X)
+{
+    X->jon = 1;
+    if (++X->jepoch == 0) { /* wrapped: no instance may carry a stale stamp */
+        for (uint32_t i = 0; i < X->ng; ++i)
+            X->G[i].jstamp = 0;
+        X->jepoch = 1;
+    }
+    X->njops = 0;
+    X->njsave = 0;
+    X->j_ng = X->ng;
+    X->j_nslot = X->nslot;
+    X->j_nline = X->nline;
+    X->j_ns = X->ns;
+    X->j_nrh = X->nrh;
+    X->j_max_ts = X->max_ts;
+    X->j_dropped = X->dropped;
+    X->j_unmod = X->unmodelled;
+}
+
+static void rx_journal_end(rx_sim* X)
+{
+    X->jon = 0;
+    X->njops = 0;
+    X->njsave = 0;
+}
+
+/* Back to the state rx_journal_begin saw. */
+static void rx_rollback(rx_sim* X)
+{
+    X->jon = 0;
+    for (uint32_t q = X->njops; q-- > 0;) {
+        const rx_jop* o = &X->jops[q];
+        if (o->old) {
+            if (hm_put(rx_map(X, o->map), o->key, o->old))
+                X->oom = 1;
+        } else {
+            hm_del(rx_map(X, o->map), o->key);
+        }
+    }
+    for (size_t off = 0; off < X->njsave;) {
+        uint32_t ii;
+        memcpy(&ii, X->jsave + off, 4);
+        rx_inst* g = &X->G[ii];
+        memcpy(g, X->jsave + off + 4, sizeof(rx_inst));
+        const int sh = g->shape != UINT32_MAX;
+        const uint32_t nc = sh ? g->count : 0, nl = sh ? X->S[g->shape].n_lines : 0;
+        const uint8_t* r = X->jsave + off + 4 + sizeof(rx_inst);
+        memcpy(X->slot_src + g->slot0, r, (size_t)nc * 4);
+        memcpy(X->slot_hdr + g->slot0, r + (size_t)nc * 4, (size_t)nc * sizeof(rfec_hdr));
+        memcpy(X->line_par + g->line0, r + (size_t)nc * (4 + sizeof(rfec_hdr)), (size_t)nl * 4);
+        off += 4 + sizeof(rx_inst) + (size_t)nc * (4 + sizeof(rfec_hdr)) + (size_t)nl * 4;
+    }
+    X->ng = X->j_ng;
+    X->nslot = X->j_nslot;
+    X->nline = X->j_nline;
+    X->ns = X->j_ns;
+    X->nrh = X->j_nrh;
+    X->max_ts = X->j_max_ts;
+    X->dropped = X->j_dropped;
+    X->unmodelled = X->j_unmod;
+    X->npend = X->nout = 0;
+    X->njops = 0;
+    X->njsave = 0;
+}
+
+/* -- packet-id ownership (sharded sessions) ---------------------------------- */
+static void rx_conflict(rx_sim* X, int what) { __atomic_fetch_or(&X->P->conflict, what, __ATOMIC_RELAXED); }
+
+/* owner-table partition of a packet id: blocks of 256 ids, round robin */
+static uint32_t rx_part(uint32_t seq, uint32_t T) { return (seq >> 8) % T; }
+
+/* the claims grouped by partition (counting sort), for the T verifiers */
+static void rx_bucket_claims(rx_sim* X, uint32_t T)
+{
+    uint32_t cnt[RX_MAX_THREADS + 1] = {0};
+    RX_GROW(X->cpart, 0, X->cpartcap, X->nclaims + 1, uint64_t);
+    if (X->oom)
+        return;
+    for (uint32_t q = 0; q < X->nclaims; ++q)
+        cnt[rx_part((uint32_t)(X->claims[q] >> 32), T)]++;
+    X->coff[0] = 0;
+    for (uint32_t j = 0; j < T; ++j)
+        X->coff[j + 1] = X->coff[j] + cnt[j];
+    uint32_t pos[RX_MAX_THREADS];
+    memcpy(pos, X->coff, T * sizeof(uint32_t));
+    for (uint32_t q = 0; q < X->nclaims; ++q)
+        X->cpart[pos[rx_part((uint32_t)(X->claims[q] >> 32), T)]++] = X->claims[q];
+}
+
+static void rx_claim(rx_sim* X, uint32_t seq, uint32_t code)
+{
+    RX_GROW(X->claims, X->nclaims, X->claimcap, 1, uint64_t);
+    if (!X->oom)
+        X->claims[X->nclaims++] = (uint64_t)seq << 32 | code;
+}
+
+/* a parity's range [base_id, base_id + count) for its fec_id (logged once per range) */
+static void rx_claim_range(rx_sim* X, const rfec_wire_rec* r)
+{
+    uint32_t* c = X->claimed + 2u * (r->fec_id / X->P->T);
+    if (c[0] == r->base_id && c[1] == (uint32_t)r->count + 1u)
+        return;
+    for (uint32_t i = 0; i < r->count; ++i)
+        rx_claim(X, r->base_id + i, (uint32_t)r->fec_id + 1u);
+    c[0] = r->base_id;
+    c[1] = (uint32_t)r->count + 1u;
+}
 
 static rfec_hdr rec_hdr(const rfec_wire_rec* r)
 {
@@ -298,6 +536,7 @@ static void rx_on_segment(rx_sim* X, uint32_t ii, const rfec_hdr* h, int32_t src
         X->unmodelled++;
         return;
     }
+    rx_touch(X, ii);
     const uint32_t t = h->seq - g->base;
     if (t < g->count) {
         if (rx_has(X, g, t))
@@ -326,8 +565,8 @@ static void rx_remove(rx_sim* X, uint32_t ii) /* sim_fec_evict_segment + flex re
 {
     const rx_inst* g = &X->G[ii];
     for (uint32_t i = 0; i < g->count; ++i)
-        hm_del(&X->cache, g->base + i);
-    hm_del(&X->flex_of, g->fec_id);
+        rx_del(X, 1, g->base + i);
+    rx_del(X, 2, g->fec_id);
 }
 
 /* sim_fec_put_segment (sim_fec.c:171-207); cache values: record + 1, or 0x80000000 | index into X->rh */
@@ -336,7 +575,7 @@ static void rx_put_segment(rx_sim* X, const rfec_hdr* h, uint16_t fec_id, uint32
     if (h->seq == 0 || hm_get(&X->cache, h->seq))
         return;
     X->max_ts = h->ts > X->max_ts ? h->ts : X->max_ts;
-    if (hm_put(&X->cache, h->seq, cval)) {
+    if (rx_put(X, 1, h->seq, cval)) {
         X->oom = 1;
         return;
     }
@@ -431,7 +670,7 @@ static uint32_t rx_shape_of(rx_sim* X, uint32_t count, uint32_t row, uint32_t co
         for (uint32_t l = 0; l < sh->n_lines; ++l)
             sh->line_of[sh->plan.line[l].index] = (int16_t)l;
     }
-    if (!extended && hm_put(&X->shape_of, key, X->ns + 1)) {
+    if (!extended && rx_put(X, 3, key, X->ns + 1)) {
         X->oom = 1;
         return UINT32_MAX;
     }
@@ -444,6 +683,7 @@ static uint32_t rx_shape_of(rx_sim* X, uint32_t count, uint32_t row, uint32_t co
  * the new shape, or -1 (no room: the parity stays unmodelled). */
 static int rx_extend(rx_sim* X, uint32_t ii, uint32_t c)
 {
+    rx_touch(X, ii);
     rx_inst* g = &X->G[ii];
     uint64_t xcol[2] = {X->S[g->shape].xcol[0], X->S[g->shape].xcol[1]};
     xcol[c >> 6] |= 1ull << (c & 63);
@@ -498,8 +738,7 @@ static void rx_put_fec(rx_sim* X, uint32_t a)
         static const uint64_t no_xcol[2] = {0, 0};
         g->shape = g->ref_ok ? rx_shape_of(X, g->count, g->row, g->col, no_xcol) : UINT32_MAX;
         if (g->shape != UINT32_MAX) {
-            rx_shape* sh = &X->S[g->shape];
-            g->gslot = sh->n_groups++;
+            const rx_shape* sh = &X->S[g->shape];
             RX_GROW(X->slot_src, X->nslot, X->slotcap, g->count, int32_t);
             RX_GROW(X->slot_hdr, X->nslot, X->slothcap, g->count, rfec_hdr);
             RX_GROW(X->line_par, X->nline, X->linecap, sh->n_lines, int32_t);
@@ -519,7 +758,7 @@ static void rx_put_fec(rx_sim* X, uint32_t a)
             X->unmodelled++;
         }
         fi = ++X->ng;
-        if (hm_put(&X->flex_of, f->fec_id, fi)) {
+        if (rx_put(X, 2, f->fec_id, fi)) {
             X->oom = 1;
             return;
         }
@@ -538,6 +777,8 @@ static void rx_put_fec(rx_sim* X, uint32_t a)
     rx_inst* g = &X->G[fi - 1];
     if (!g->ref_ok || g->shape == UINT32_MAX)
         return;
+    rx_touch(X, fi - 1);
+    g = &X->G[fi - 1];
     int l = X->S[g->shape].line_of[f->index];
     if (X->S[g->shape].huge) { /* line = index; the parity registered once */
         uint32_t first, stride;
@@ -571,8 +812,12 @@ static void rx_put_fec(rx_sim* X, uint32_t a)
     rx_check_line(X, fi - 1, l);
 }
 
-/* sim_receiver_recover (sim_receiver.c:780-804): lowest packet_id first, cascading */
-static void rx_drain(rx_sim* X)
+/* sim_receiver_recover (sim_receiver.c:780-804): lowest packet_id first,
+ * cascading; the recoveries of record a.  In a sharded batch each delivered
+ * packet must lie in its flex's range (so its id stays in this shard) and,
+ * in the parallel replay, raise max_ts no higher than any later parity of
+ * the batch can take (smin): else the batch is replayed otherwise. */
+static void rx_drain(rx_sim* X, uint32_t a)
 {
     while (X->npend && !X->oom) {
         uint32_t b = 0;
@@ -583,9 +828,20 @@ static void rx_drain(rx_sim* X)
         X->pend[b] = X->pend[--X->npend];
         if (hm_get(&X->seen, e.hdr.seq))
             continue;
+        if (X->P) {
+            const rx_inst* g = &X->G[e.inst];
+            if (e.hdr.seq - g->base >= g->count) {
+                rx_conflict(X, RX_CONFLICT_OWNER);
+                return;
+            }
+            if (X->P->ts_check && e.hdr.ts > X->P->smin[a - X->P->a0]) {
+                rx_conflict(X, RX_CONFLICT_TS);
+                return;
+            }
+        }
         RX_GROW(X->out, X->nout, X->outcap, 1, rx_event);
         RX_GROW(X->rh, X->nrh, X->rhcap, 1, rfec_hdr);
-        if (X->oom || hm_put(&X->seen, e.hdr.seq, 1)) {
+        if (X->oom || rx_put(X, 0, e.hdr.seq, 1)) {
             X->oom = 1;
             return;
         }
@@ -610,10 +866,11 @@ static void rx_sim_free(rx_sim* X)
     free(X->pend);
     free(X->out);
     free(X->rh);
-    free(X->dl);
-    free(X->jobs);
-    free(X->jlevel);
-    free(X->jmem);
+    free(X->jops);
+    free(X->jsave);
+    free(X->claims);
+    free(X->cpart);
+    free(X->claimed);
 }
 
 static int cmp_u32(const void* a, const void* b)
@@ -748,30 +1005,80 @@ static int rx_tables_init(rx_sim* X, uint32_t n)
     return hm_init(&X->seen, n) || hm_init(&X->cache, n) || hm_init(&X->flex_of, 1024) || hm_init(&X->shape_of, 64);
 }
 
-/* The control plane, in arrival order, over records [a0, a0 + n) of X->R:
- * sim_receiver_put / sim_receiver_put_fec and the recovery cascade. */
+/* One record of X->R in arrival order: sim_receiver_put /
+ * sim_receiver_put_fec and the recovery cascade.  In a sharded batch the
+ * record first claims its packet ids for its fec_id. */
+static void rx_arrival(rx_sim* X, uint32_t a)
+{
+    const rfec_wire_rec* r = &X->R[a];
+    if (r->status != RFEC_WIRE_OK)
+        return;
+    if (r->mid == RFEC_WIRE_SEG) { /* sim_receiver_put (sim_receiver.c:811-827) */
+        if (X->P) /* (a segment outside FEC claims its id for fec_id 0) */
+            rx_claim(X, r->hdr.seq, (uint32_t)r->fec_id + 1u);
+        if (hm_get(&X->seen, r->hdr.seq))
+            return;
+        if (rx_put(X, 0, r->hdr.seq, 1)) {
+            X->oom = 1;
+            return;
+        }
+        if (r->fec_id == 0)
+            return;
+        const rfec_hdr h = rec_hdr(r);
+        rx_put_segment(X, &h, r->fec_id, a + 1, (int32_t)a);
+    } else if (r->mid == RFEC_WIRE_FEC) {
+        if (X->P)
+            rx_claim_range(X, r);
+        rx_put_fec(X, a);
+    }
+    rx_drain(X, a);
+}
+
+/* The control plane over records [a0, a0 + n) of X->R. */
 static void rx_run(rx_sim* X, uint32_t a0, uint32_t n)
 {
-    for (uint32_t a = a0; a < a0 + n && !X->oom; ++a) {
-        const rfec_wire_rec* r = &X->R[a];
-        if (r->status != RFEC_WIRE_OK)
-            continue;
-        if (r->mid == RFEC_WIRE_SEG) { /* sim_receiver_put (sim_receiver.c:811-827) */
-            if (hm_get(&X->seen, r->hdr.seq))
-                continue;
-            if (hm_put(&X->seen, r->hdr.seq, 1)) {
-                X->oom = 1;
-                break;
-            }
-            if (r->fec_id == 0)
-                continue;
-            const rfec_hdr h = rec_hdr(r);
-            rx_put_segment(X, &h, r->fec_id, a + 1, (int32_t)a);
-        } else if (r->mid == RFEC_WIRE_FEC) {
-            rx_put_fec(X, a);
-        }
-        rx_drain(X);
-    }
+    for (uint32_t a = a0; a < a0 + n && !X->oom; ++a)
+        rx_arrival(X, a);
+}
+
+/* The device side of one ingestion call over T shards (one for rfec_rx_recover
+ * and a merged session): the shards' deliveries merged in packet-id order, the
+ * delivering groups laid out by device shape (the same geometry on several
+ * shards is one launch), the line jobs of the large groups. */
+typedef struct {
+    const rx_shape* sh; /* any shard's shape of this geometry (plans are a function of it) */
+    uint32_t n_groups, row0, prow0, group0;
+} rx_dclass;
+
+typedef struct {
+    rx_event* ev;          /* this call's deliveries, all shards, ascending packet id */
+    uint32_t nev, evcap;
+    uint64_t* dl;          /* delivering groups: shard << 32 | instance */
+    uint32_t ndl, dlcap;
+    rx_dclass* C;          /* device shapes */
+    uint32_t nc, ccap;
+    uint32_t* cls;         /* per (shard, shape): its device shape */
+    uint32_t clscap;
+    rfec_line_job* jobs;   /* groups above RFEC_MAX_K: this call's line jobs (rx_big_peel) */
+    uint32_t njobs, jobcap;
+    uint16_t* jlevel;      /* a job's dependency level (1 = arrived members only) */
+    uint32_t jlevelcap;
+    int32_t* jmem;         /* member codes: record >= 0, job j as -1 - j */
+    uint32_t njmem, jmemcap;
+    uint32_t unmodelled;
+    int oom;
+} rx_dev;
+
+static void rx_dev_free(rx_dev* D)
+{
+    free(D->ev);
+    free(D->dl);
+    free(D->C);
+    free(D->cls);
+    free(D->jobs);
+    free(D->jlevel);
+    free(D->jmem);
+    memset(D, 0, sizeof(*D));
 }
 
 /* A group recovered by line jobs (rx_line_jobs: above RFEC_MAX_K segments or a
@@ -781,7 +1088,7 @@ static void rx_run(rx_sim* X, uint32_t a0, uint32_t n)
  * members and registered parities, over headers on the host; each firing
  * becomes a line job the device runs (rfec_launch_line_jobs).  job_of[t]: the
  * job recovering member t, or -1.  Returns -1 when out of memory. */
-static int rx_big_peel(rx_sim* X, uint32_t gi, int32_t* job_of)
+static int rx_big_peel(const rx_sim* X, rx_dev* D, uint32_t gi, int32_t* job_of)
 {
     const rx_inst* g = &X->G[gi];
     const rx_shape* sh = &X->S[g->shape];
@@ -805,9 +1112,9 @@ static int rx_big_peel(rx_sim* X, uint32_t gi, int32_t* job_of)
         if (have[i])
             hd[i] = X->slot_hdr[g->slot0 + i];
     }
-    for (int progress = 1; progress && !X->oom;) {
+    for (int progress = 1; progress && !D->oom;) {
         progress = 0;
-        for (uint32_t l = 0; l < NL && !X->oom; ++l) {
+        for (uint32_t l = 0; l < NL && !D->oom; ++l) {
             uint32_t first, stride;
             int reg;
             const uint32_t n = rx_line(X, g, l, &first, &stride, &reg);
@@ -850,28 +1157,28 @@ static int rx_big_peel(rx_sim* X, uint32_t gi, int32_t* job_of)
             }
             if (!ok || h.size > L)
                 continue;
-            RX_GROW(X->jobs, X->njobs, X->jobcap, 1, rfec_line_job);
-            RX_GROW(X->jlevel, X->njobs, X->jlevelcap, 1, uint16_t);
-            RX_GROW(X->jmem, X->njmem, X->jmemcap, present, int32_t);
-            if (X->oom)
+            RX_GROW_F(D->oom, D->jobs, D->njobs, D->jobcap, 1, rfec_line_job);
+            RX_GROW_F(D->oom, D->jlevel, D->njobs, D->jlevelcap, 1, uint16_t);
+            RX_GROW_F(D->oom, D->jmem, D->njmem, D->jmemcap, present, int32_t);
+            if (D->oom)
                 break;
-            rfec_line_job* J = &X->jobs[X->njobs];
-            J->out = (int32_t)X->njobs;
+            rfec_line_job* J = &D->jobs[D->njobs];
+            J->out = (int32_t)D->njobs;
             J->parity = X->line_par[g->line0 + l];
-            J->member0 = X->njmem;
+            J->member0 = D->njmem;
             J->n_members = present;
             for (uint32_t q = 0; q < n; ++q) {
                 const uint32_t i = first + q * stride;
                 if (i != t)
-                    X->jmem[X->njmem++] = src[i];
+                    D->jmem[D->njmem++] = src[i];
             }
-            X->jlevel[X->njobs] = (uint16_t)(level + 1);
-            job_of[t] = (int32_t)X->njobs;
-            src[t] = -1 - (int32_t)X->njobs;
+            D->jlevel[D->njobs] = (uint16_t)(level + 1);
+            job_of[t] = (int32_t)D->njobs;
+            src[t] = -1 - (int32_t)D->njobs;
             lvl[t] = (uint16_t)(level + 1);
             hd[t] = h;
             have[t] = 1;
-            X->njobs++;
+            D->njobs++;
             progress = 1;
         }
     }
@@ -879,7 +1186,7 @@ static int rx_big_peel(rx_sim* X, uint32_t gi, int32_t* job_of)
     free(src);
     free(lvl);
     free(have);
-    return X->oom ? -1 : 0;
+    return D->oom ? -1 : 0;
 }
 
 #define RX_MAX_LEVEL 256u
@@ -891,116 +1198,162 @@ static int rx_big_peel(rx_sim* X, uint32_t gi, int32_t* job_of)
  * 64 lines; its parity rows sit at a 256-line stride). */
 static int rx_line_jobs(const rx_shape* sh) { return sh->count > RFEC_MAX_K || sh->huge; }
 
+static int same_geometry(const rx_shape* a, const rx_shape* b)
+{
+    return a->count == b->count && a->row == b->row && a->col == b->col && a->xcol[0] == b->xcol[0] &&
+           a->xcol[1] == b->xcol[1];
+}
+
 /* The device side of one call: the groups that delivered something in this
- * call, rebuilt from their arrived members and registered parities (rows of
- * `rows`, DEVICE, indexed by record), peeled by rfec_recover_batch, and the
- * delivered rows copied out.  The pinned tables go after the first `hoff`
- * bytes of t_rx.h, which survive a grow (X->R may live there). */
-static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t capacity, size_t hoff,
-                     rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out, rfec_rx_report* rep,
-                     hipStream_t sm)
+ * call (over the T shards XS), rebuilt from their arrived members and
+ * registered parities (rows of `rows`, DEVICE, indexed by record), peeled by
+ * rfec_recover_batch, and the delivered rows copied out.  The pinned tables
+ * go after the first `hoff` bytes of t_rx.h, which survive a grow (the
+ * shards' R may live there: `r_stage`). */
+static int rx_device(rx_sim* const* XS, uint32_t T, rx_dev* D, const uint8_t* rows, uint32_t stride,
+                     uint32_t capacity, size_t hoff, int r_stage, rfec_rx_seg* out, uint8_t* out_payload,
+                     uint32_t max_out, uint32_t* n_out, rfec_rx_report* rep, hipStream_t sm)
 {
     hipError_t e = hipSuccess;
     int rc = RFEC_OK, ke = 0;
     const double th = now_us();
     *n_out = 0;
-    if (X->nout)
-        qsort(X->out, X->nout, sizeof(rx_event), cmp_event);
-    if (X->nout == 0) { /* nothing recovered: no device work */
+    D->nev = D->ndl = D->nc = D->njobs = D->njmem = 0;
+    /* 1. the deliveries of every shard, ascending packet id */
+    uint32_t total = 0, nshape = 0;
+    for (uint32_t t = 0; t < T; ++t) {
+        total += XS[t]->nout;
+        nshape += XS[t]->ns;
+    }
+    if (total == 0) { /* nothing recovered: no device work */
         rep->host_us += now_us() - th;
         return RFEC_OK;
     }
-    /* group tables, shape-major, for the groups that deliver something (work
-     * proportional to the deliveries, not to the open flexes) */
-    for (uint32_t s = 0; s < X->ns; ++s)
-        X->S[s].n_groups = 0;
-    if (++X->epoch == 0) { /* wrapped: no instance may carry a stale stamp */
-        for (uint32_t gi = 0; gi < X->ng; ++gi)
-            X->G[gi].gstamp = 0;
-        X->epoch = 1;
+    RX_GROW_F(D->oom, D->ev, 0, D->evcap, total, rx_event);
+    RX_GROW_F(D->oom, D->cls, 0, D->clscap, nshape + 1, uint32_t);
+    if (D->oom)
+        return set_err(RFEC_ENOMEM, "rx: delivery list", 0);
+    uint32_t sbase[RX_MAX_THREADS + 1];
+    sbase[0] = 0;
+    for (uint32_t t = 0; t < T; ++t) {
+        const rx_sim* X = XS[t];
+        for (uint32_t q = 0; q < X->nout; ++q) {
+            D->ev[D->nev] = X->out[q];
+            D->ev[D->nev++].shard = t;
+        }
+        sbase[t + 1] = sbase[t] + X->ns;
     }
-    X->ndl = 0;
-    for (uint32_t q = 0; q < X->nout; ++q) {
-        const uint32_t gi = X->out[q].inst;
-        rx_inst* g = &X->G[gi];
-        if (g->gstamp != X->epoch) {
-            RX_GROW(X->dl, X->ndl, X->dlcap, 1, uint32_t);
-            if (X->oom)
-                return set_err(RFEC_ENOMEM, "rx: delivery list", 0);
-            g->gstamp = X->epoch;
-            g->gslot = X->S[g->shape].n_groups++;
-            X->dl[X->ndl++] = gi;
+    if (D->nev > 1)
+        qsort(D->ev, D->nev, sizeof(rx_event), cmp_event);
+    memset(D->cls, 0, (size_t)nshape * sizeof(uint32_t));
+    /* 2. delivering groups, by device shape (work proportional to the deliveries, not to the open flexes) */
+    for (uint32_t t = 0; t < T; ++t) {
+        rx_sim* X = XS[t];
+        if (++X->epoch == 0) { /* wrapped: no instance may carry a stale stamp */
+            for (uint32_t gi = 0; gi < X->ng; ++gi)
+                X->G[gi].gstamp = 0;
+            X->epoch = 1;
         }
     }
-    uint32_t nrows = 0, prows = 0, ngs = 0;
-    for (uint32_t s = 0; s < X->ns; ++s) {
-        rx_shape* sh = &X->S[s];
-        sh->row0 = nrows;
-        sh->prow0 = prows;
-        sh->group0 = ngs;
-        if (rx_line_jobs(sh)) /* line jobs instead (below) */
+    for (uint32_t q = 0; q < D->nev; ++q) {
+        rx_sim* X = XS[D->ev[q].shard];
+        rx_inst* g = &X->G[D->ev[q].inst];
+        if (g->gstamp == X->epoch)
             continue;
-        nrows += sh->n_groups * sh->count;
-        prows += sh->n_groups * sh->n_lines;
-        ngs += sh->n_groups;
+        g->gstamp = X->epoch;
+        RX_GROW_F(D->oom, D->dl, D->ndl, D->dlcap, 1, uint64_t);
+        if (D->oom)
+            return set_err(RFEC_ENOMEM, "rx: delivery list", 0);
+        D->dl[D->ndl++] = (uint64_t)D->ev[q].shard << 32 | D->ev[q].inst;
+        uint32_t* c = &D->cls[sbase[D->ev[q].shard] + g->shape];
+        if (!*c) { /* this shard's shape: an existing device shape of the same geometry, or a new one */
+            const rx_shape* sh = &X->S[g->shape];
+            uint32_t k = 0;
+            while (k < D->nc && !same_geometry(D->C[k].sh, sh))
+                ++k;
+            if (k == D->nc) {
+                RX_GROW_F(D->oom, D->C, D->nc, D->ccap, 1, rx_dclass);
+                if (D->oom)
+                    return set_err(RFEC_ENOMEM, "rx: device shapes", 0);
+                D->C[D->nc++] = (rx_dclass){sh, 0, 0, 0, 0};
+            }
+            *c = k + 1;
+        }
+        g->gslot = D->C[*c - 1].n_groups++;
     }
+    uint32_t nrows = 0, prows = 0, ngs = 0;
+    for (uint32_t k = 0; k < D->nc; ++k) {
+        rx_dclass* C = &D->C[k];
+        C->row0 = nrows;
+        C->prow0 = prows;
+        C->group0 = ngs;
+        if (rx_line_jobs(C->sh)) /* line jobs instead (below) */
+            continue;
+        nrows += C->n_groups * C->sh->count;
+        prows += C->n_groups * C->sh->n_lines;
+        ngs += C->n_groups;
+    }
+#define RX_CLASS(t, g) (&D->C[D->cls[sbase[t] + (g)->shape] - 1])
     /* groups above RFEC_MAX_K: the host peel's line jobs, output rows after
      * the batched peel's rows, launched level by level (jobs sorted by level) */
-    X->njobs = X->njmem = 0;
     uint32_t nbig = 0, maxlvl = 0;
-    for (uint32_t d = 0; d < X->ndl; ++d)
-        if (rx_line_jobs(&X->S[X->G[X->dl[d]].shape]))
-            nbig += X->G[X->dl[d]].count;
+    for (uint32_t d = 0; d < D->ndl; ++d) {
+        const rx_sim* X = XS[D->dl[d] >> 32];
+        const rx_inst* g = &X->G[(uint32_t)D->dl[d]];
+        if (rx_line_jobs(&X->S[g->shape]))
+            nbig += g->count;
+    }
     int32_t* job_of = nbig ? (int32_t*)malloc((size_t)nbig * sizeof(int32_t)) : NULL;
     uint32_t* jperm = NULL;
     if (nbig && !job_of)
         return set_err(RFEC_ENOMEM, "rx: large groups", 0);
-    for (uint32_t d = 0, off = 0; d < X->ndl; ++d) {
-        rx_inst* g = &X->G[X->dl[d]];
+    for (uint32_t d = 0, off = 0; d < D->ndl; ++d) {
+        rx_sim* X = XS[D->dl[d] >> 32];
+        rx_inst* g = &X->G[(uint32_t)D->dl[d]];
         if (!rx_line_jobs(&X->S[g->shape]))
             continue;
         g->gslot = off; /* (a large group's slot: its job_of range) */
-        if (rx_big_peel(X, X->dl[d], job_of + off))
-            X->oom = 1;
+        if (rx_big_peel(X, D, (uint32_t)D->dl[d], job_of + off))
+            D->oom = 1;
         off += g->count;
     }
-    if (X->oom) {
+    if (D->oom) {
         free(job_of);
         return set_err(RFEC_ENOMEM, "rx: line jobs", 0);
     }
     /* a line fires at most once, so a chain is at most as deep as a group has lines (256 FEC indices) */
     uint32_t lvl_n[RX_MAX_LEVEL + 1] = {0};
-    if (X->njobs) { /* stable sort by level; codes and job_of follow */
-        for (uint32_t j = 0; j < X->njobs; ++j) {
-            if (X->jlevel[j] > RX_MAX_LEVEL) {
+    if (D->njobs) { /* stable sort by level; codes and job_of follow */
+        for (uint32_t j = 0; j < D->njobs; ++j) {
+            if (D->jlevel[j] > RX_MAX_LEVEL) {
                 free(job_of);
                 return set_err(RFEC_EINVAL, "rx: line job chain too deep", 0);
             }
-            maxlvl = X->jlevel[j] > maxlvl ? X->jlevel[j] : maxlvl;
-            lvl_n[X->jlevel[j]]++;
+            maxlvl = D->jlevel[j] > maxlvl ? D->jlevel[j] : maxlvl;
+            lvl_n[D->jlevel[j]]++;
         }
         uint32_t start[RX_MAX_LEVEL + 2] = {0};
         for (uint32_t v = 1; v <= maxlvl; ++v)
             start[v + 1] = start[v] + lvl_n[v];
-        jperm = (uint32_t*)malloc((size_t)X->njobs * sizeof(uint32_t));
-        rfec_line_job* sorted = (rfec_line_job*)malloc((size_t)X->njobs * sizeof(rfec_line_job));
+        jperm = (uint32_t*)malloc((size_t)D->njobs * sizeof(uint32_t));
+        rfec_line_job* sorted = (rfec_line_job*)malloc((size_t)D->njobs * sizeof(rfec_line_job));
         if (!jperm || !sorted) {
             free(jperm);
             free(sorted);
             free(job_of);
             return set_err(RFEC_ENOMEM, "rx: line jobs", 0);
         }
-        for (uint32_t j = 0; j < X->njobs; ++j)
-            jperm[j] = start[X->jlevel[j]]++;
-        for (uint32_t j = 0; j < X->njobs; ++j) {
-            sorted[jperm[j]] = X->jobs[j];
+        for (uint32_t j = 0; j < D->njobs; ++j)
+            jperm[j] = start[D->jlevel[j]]++;
+        for (uint32_t j = 0; j < D->njobs; ++j) {
+            sorted[jperm[j]] = D->jobs[j];
             sorted[jperm[j]].out = (int32_t)jperm[j];
         }
-        memcpy(X->jobs, sorted, (size_t)X->njobs * sizeof(rfec_line_job));
+        memcpy(D->jobs, sorted, (size_t)D->njobs * sizeof(rfec_line_job));
         free(sorted);
-        for (uint32_t m = 0; m < X->njmem; ++m)
-            if (X->jmem[m] < 0)
-                X->jmem[m] = -1 - (int32_t)jperm[-1 - X->jmem[m]];
+        for (uint32_t m = 0; m < D->njmem; ++m)
+            if (D->jmem[m] < 0)
+                D->jmem[m] = -1 - (int32_t)jperm[-1 - D->jmem[m]];
         for (uint32_t i = 0; i < nbig; ++i)
             if (job_of[i] >= 0)
                 job_of[i] = (int32_t)jperm[job_of[i]];
@@ -1009,25 +1362,25 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
     const size_t o_meta = RX_ALIGN(o_hdr + (size_t)nrows * sizeof(rfec_hdr));
     const size_t o_fs = RX_ALIGN(o_meta + (size_t)prows * sizeof(rfec_hdr));
     const size_t o_pres = RX_ALIGN(o_fs + (size_t)prows * 2), o_pp = RX_ALIGN(o_pres + (size_t)ngs * 16);
-    const size_t o_omap = RX_ALIGN(o_pp + (size_t)ngs * 8), o_jobs = RX_ALIGN(o_omap + (size_t)X->nout * 4);
-    const size_t o_jmem = RX_ALIGN(o_jobs + (size_t)X->njobs * sizeof(rfec_line_job));
-    const size_t o_in_end = RX_ALIGN(o_jmem + (size_t)X->njmem * 4);
+    const size_t o_omap = RX_ALIGN(o_pp + (size_t)ngs * 8), o_jobs = RX_ALIGN(o_omap + (size_t)D->nev * 4);
+    const size_t o_jmem = RX_ALIGN(o_jobs + (size_t)D->njobs * sizeof(rfec_line_job));
+    const size_t o_in_end = RX_ALIGN(o_jmem + (size_t)D->njmem * 4);
     const size_t o_rec = o_in_end, host_bytes = RX_ALIGN(o_rec + (size_t)ngs * 16);
     size_t ws_bytes = 0;
-    for (uint32_t s = 0; s < X->ns; ++s)
-        if (!rx_line_jobs(&X->S[s]))
-            ws_bytes += RX_ALIGN(rfec_recover_workspace_size(&X->S[s].plan, X->S[s].n_groups));
-    const size_t d_shards = o_in_end, d_par = RX_ALIGN(d_shards + ((size_t)nrows + X->njobs) * stride);
+    for (uint32_t k = 0; k < D->nc; ++k)
+        if (!rx_line_jobs(D->C[k].sh))
+            ws_bytes += RX_ALIGN(rfec_recover_workspace_size(&D->C[k].sh->plan, D->C[k].n_groups));
+    const size_t d_shards = o_in_end, d_par = RX_ALIGN(d_shards + ((size_t)nrows + D->njobs) * stride);
     const size_t d_ws = RX_ALIGN(d_par + (size_t)prows * stride), d_rec = RX_ALIGN(d_ws + ws_bytes);
-    const size_t d_out = RX_ALIGN(d_rec + (size_t)ngs * 16), dev_bytes = RX_ALIGN(d_out + (size_t)X->nout * stride);
-    const int r_in_stage = (const uint8_t*)X->R == t_rx.h;
+    const size_t d_out = RX_ALIGN(d_rec + (size_t)ngs * 16), dev_bytes = RX_ALIGN(d_out + (size_t)D->nev * stride);
     if ((rc = rx_reserve(hoff + host_bytes, dev_bytes, hoff))) {
         free(job_of);
         free(jperm);
         return rc;
     }
-    if (r_in_stage)
-        X->R = (const rfec_wire_rec*)t_rx.h;
+    if (r_stage) /* the records live at the start of the pinned block, which may have moved */
+        for (uint32_t t = 0; t < T; ++t)
+            XS[t]->R = (const rfec_wire_rec*)t_rx.h;
     uint8_t* H = t_rx.h + hoff;
     memset(H, 0, o_in_end);
     int32_t* smap = (int32_t*)(H + o_smap);
@@ -1038,17 +1391,20 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
     uint64_t* pres = (uint64_t*)(H + o_pres);
     uint64_t* ppm = (uint64_t*)(H + o_pp);
     int32_t* omap = (int32_t*)(H + o_omap);
-    if (X->njobs) {
-        memcpy(H + o_jobs, X->jobs, (size_t)X->njobs * sizeof(rfec_line_job));
-        memcpy(H + o_jmem, X->jmem, (size_t)X->njmem * 4);
+    if (D->njobs) {
+        memcpy(H + o_jobs, D->jobs, (size_t)D->njobs * sizeof(rfec_line_job));
+        memcpy(H + o_jmem, D->jmem, (size_t)D->njmem * 4);
     }
-    for (uint32_t d = 0; d < X->ndl; ++d) {
-        const rx_inst* g = &X->G[X->dl[d]];
+    for (uint32_t d = 0; d < D->ndl; ++d) {
+        const uint32_t t = (uint32_t)(D->dl[d] >> 32);
+        const rx_sim* X = XS[t];
+        const rx_inst* g = &X->G[(uint32_t)D->dl[d]];
         const rx_shape* sh = &X->S[g->shape];
         if (rx_line_jobs(sh))
             continue;
-        const uint32_t gg = sh->group0 + g->gslot, r0 = sh->row0 + g->gslot * sh->count;
-        const uint32_t p0 = sh->prow0 + g->gslot * sh->n_lines;
+        const rx_dclass* C = RX_CLASS(t, g);
+        const uint32_t gg = C->group0 + g->gslot, r0 = C->row0 + g->gslot * sh->count;
+        const uint32_t p0 = C->prow0 + g->gslot * sh->n_lines;
         pres[2 * gg] = g->arrived[0];
         pres[2 * gg + 1] = g->arrived[1];
         ppm[gg] = g->ppm;
@@ -1069,73 +1425,77 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
     }
     /* output rows: the recovering group's slot */
     uint32_t nok = 0;
-    for (uint32_t q = 0; q < X->nout; ++q) {
-        const rx_event* ev = &X->out[q];
+    for (uint32_t q = 0; q < D->nev; ++q) {
+        const rx_event* ev = &D->ev[q];
+        const rx_sim* X = XS[ev->shard];
         const rx_inst* g = &X->G[ev->inst];
         const rx_shape* sh = &X->S[g->shape];
         const uint32_t t = ev->hdr.seq - g->base;
         if (rx_line_jobs(sh)) /* the job that recovers t */
             omap[q] = t < g->count && job_of[g->gslot + t] >= 0 ? (int32_t)(nrows + (uint32_t)job_of[g->gslot + t]) : -1;
         else
-            omap[q] = t < g->count ? (int32_t)(sh->row0 + g->gslot * sh->count + t) : -1;
+            omap[q] = t < g->count ? (int32_t)(RX_CLASS(ev->shard, g)->row0 + g->gslot * sh->count + t) : -1;
     }
     free(job_of);
     free(jperm);
     rep->host_us += now_us() - th;
     rep->n_groups = ngs;
-    for (uint32_t s = 0; s < X->ns; ++s)
-        rep->n_shapes += X->S[s].n_groups != 0;
-    /* the device: rows in place, one peel per shape, the delivered rows compacted */
-    uint8_t* D = t_rx.d;
+    for (uint32_t k = 0; k < D->nc; ++k)
+        rep->n_shapes += D->C[k].n_groups != 0;
+    /* the device: rows in place, one peel per device shape, the delivered rows compacted */
+    uint8_t* Dv = t_rx.d;
     double tt = now_us();
-    if ((e = hipMemcpyAsync(D, H, o_in_end, hipMemcpyHostToDevice, sm)) != hipSuccess)
+    if ((e = hipMemcpyAsync(Dv, H, o_in_end, hipMemcpyHostToDevice, sm)) != hipSuccess)
         return set_err(RFEC_EDEVICE, "rx: H2D", e);
-    ke = rfec_launch_gather_rows(D + d_shards, rows, (const int32_t*)(D + o_smap), nrows, stride, sm);
+    ke = rfec_launch_gather_rows(Dv + d_shards, rows, (const int32_t*)(Dv + o_smap), nrows, stride, sm);
     if (!ke)
-        ke = rfec_launch_gather_rows(D + d_par, rows, (const int32_t*)(D + o_pmap), prows, stride, sm);
+        ke = rfec_launch_gather_rows(Dv + d_par, rows, (const int32_t*)(Dv + o_pmap), prows, stride, sm);
     for (uint32_t v = 1, lo = 0; v <= maxlvl && !ke; lo += lvl_n[v], ++v) /* the large groups' line jobs */
-        ke = rfec_launch_line_jobs((const rfec_line_job*)(D + o_jobs) + lo, lvl_n[v], (const int32_t*)(D + o_jmem),
-                                   rows, D + d_shards + (size_t)nrows * stride, stride, sm);
+        ke = rfec_launch_line_jobs((const rfec_line_job*)(Dv + o_jobs) + lo, lvl_n[v], (const int32_t*)(Dv + o_jmem),
+                                   rows, Dv + d_shards + (size_t)nrows * stride, stride, sm);
     size_t wso = 0;
-    for (uint32_t s = 0; s < X->ns && !ke; ++s) {
-        const rx_shape* sh = &X->S[s];
-        if (!sh->n_groups || rx_line_jobs(sh))
+    for (uint32_t k = 0; k < D->nc && !ke; ++k) {
+        const rx_dclass* C = &D->C[k];
+        if (!C->n_groups || rx_line_jobs(C->sh))
             continue;
         rfec_kmask M;
-        make_masks(&sh->plan, &M);
-        ke = rfec_launch_recover(&M, sh->n_groups, stride, capacity, D + d_shards + (size_t)sh->row0 * stride,
-                                 (rfec_hdr*)(D + o_hdr) + sh->row0, (const uint64_t*)(D + o_pres) + 2 * sh->group0,
-                                 D + d_par + (size_t)sh->prow0 * stride, (const rfec_hdr*)(D + o_meta) + sh->prow0,
-                                 (const uint16_t*)(D + o_fs) + sh->prow0, (const uint64_t*)(D + o_pp) + sh->group0,
-                                 (uint64_t*)(D + d_rec) + 2 * sh->group0, D + d_ws + wso, sm, g_tuning);
-        wso += RX_ALIGN(rfec_recover_workspace_size(&sh->plan, sh->n_groups));
+        make_masks(&C->sh->plan, &M);
+        ke = rfec_launch_recover(&M, C->n_groups, stride, capacity, Dv + d_shards + (size_t)C->row0 * stride,
+                                 (rfec_hdr*)(Dv + o_hdr) + C->row0, (const uint64_t*)(Dv + o_pres) + 2 * C->group0,
+                                 Dv + d_par + (size_t)C->prow0 * stride, (const rfec_hdr*)(Dv + o_meta) + C->prow0,
+                                 (const uint16_t*)(Dv + o_fs) + C->prow0, (const uint64_t*)(Dv + o_pp) + C->group0,
+                                 (uint64_t*)(Dv + d_rec) + 2 * C->group0, Dv + d_ws + wso, sm, g_tuning);
+        wso += RX_ALIGN(rfec_recover_workspace_size(&C->sh->plan, C->n_groups));
     }
     /* delivered rows: straight into the caller's output when it is pinned and
        large enough (no second round trip; rows the peel did not cover are
        squeezed out on the host below), else into the device staging */
-    uint8_t* outd = X->nout && X->nout <= max_out ? (uint8_t*)host_mapped(out_payload) : NULL;
-    if (!ke && X->nout)
-        ke = rfec_launch_gather_rows(outd ? outd : D + d_out, D + d_shards, (const int32_t*)(D + o_omap), X->nout,
+    uint8_t* outd = D->nev && D->nev <= max_out ? (uint8_t*)host_mapped(out_payload) : NULL;
+    if (!ke && D->nev)
+        ke = rfec_launch_gather_rows(outd ? outd : Dv + d_out, Dv + d_shards, (const int32_t*)(Dv + o_omap), D->nev,
                                      stride, sm);
     uint64_t* rec = (uint64_t*)(H + o_rec);
-    if (ke || (e = hipMemcpyAsync(rec, D + d_rec, (size_t)ngs * 16, hipMemcpyDeviceToHost, sm)) != hipSuccess ||
+    if (ke || (e = hipMemcpyAsync(rec, Dv + d_rec, (size_t)ngs * 16, hipMemcpyDeviceToHost, sm)) != hipSuccess ||
         (e = hipStreamSynchronize(sm)) != hipSuccess)
         return set_err(RFEC_EDEVICE, "rx: recover", ke ? ke : (int)e);
     rep->kernel_us += now_us() - tt;
     /* the device peel covers every packet the arrival-order pass delivered (same lines, a superset of
        the members at each firing); anything else is reported, not delivered */
-    for (uint32_t q = 0; q < X->nout; ++q) {
-        const rx_event* ev = &X->out[q];
+    for (uint32_t q = 0; q < D->nev; ++q) {
+        const rx_event* ev = &D->ev[q];
+        const rx_sim* X = XS[ev->shard];
         const rx_inst* g = &X->G[ev->inst];
-        const uint32_t t = ev->hdr.seq - g->base, gg = X->S[g->shape].group0 + g->gslot;
         const int big = rx_line_jobs(&X->S[g->shape]);
+        const uint32_t t = ev->hdr.seq - g->base;
+        const uint32_t gg = big ? 0 : RX_CLASS(ev->shard, g)->group0 + g->gslot;
         if (big ? omap[q] < 0 : t >= g->count || !((rec[2 * gg + (t >> 6)] >> (t & 63)) & 1ull)) {
-            X->unmodelled++;
+            D->unmodelled++;
             omap[q] = -1;
             continue;
         }
         nok++;
     }
+#undef RX_CLASS
     if (nok > max_out) {
         *n_out = nok;
         return set_err(RFEC_EINVAL, "rx: output too small", 0);
@@ -1143,28 +1503,28 @@ static int rx_device(rx_sim* X, const uint8_t* rows, uint32_t stride, uint32_t c
     tt = now_us();
     uint32_t o = 0;
     if (outd) { /* the rows are in out_payload already (the sync above) */
-        for (uint32_t q = 0; q < X->nout; ++q) {
+        for (uint32_t q = 0; q < D->nev; ++q) {
             if (omap[q] < 0)
                 continue;
             if (o != q)
                 memmove(out_payload + (size_t)o * stride, out_payload + (size_t)q * stride, stride);
-            X->out[o++] = X->out[q];
+            D->ev[o++] = D->ev[q];
         }
-    } else if (nok == X->nout) { /* the usual case: one copy */
+    } else if (nok == D->nev) { /* the usual case: one copy */
         if (nok)
-            e = hipMemcpyAsync(out_payload, D + d_out, (size_t)nok * stride, hipMemcpyDeviceToHost, sm);
+            e = hipMemcpyAsync(out_payload, Dv + d_out, (size_t)nok * stride, hipMemcpyDeviceToHost, sm);
         o = nok;
     }
-    for (uint32_t q = 0; q < X->nout && !outd && nok != X->nout && e == hipSuccess; ++q) {
+    for (uint32_t q = 0; q < D->nev && !outd && nok != D->nev && e == hipSuccess; ++q) {
         if (omap[q] < 0)
             continue;
-        e = hipMemcpyAsync(out_payload + (size_t)o * stride, D + d_out + (size_t)q * stride, stride,
+        e = hipMemcpyAsync(out_payload + (size_t)o * stride, Dv + d_out + (size_t)q * stride, stride,
                            hipMemcpyDeviceToHost, sm);
-        X->out[o++] = X->out[q];
+        D->ev[o++] = D->ev[q];
     }
     for (uint32_t q = 0; q < o; ++q) {
-        out[q].hdr = X->out[q].hdr;
-        out[q].fec_id = (uint16_t)X->G[X->out[q].inst].fec_id;
+        out[q].hdr = D->ev[q].hdr;
+        out[q].fec_id = (uint16_t)XS[D->ev[q].shard]->G[D->ev[q].inst].fec_id;
         out[q].reserved = 0;
     }
     if (e == hipSuccess && !outd)
@@ -1223,8 +1583,12 @@ int rfec_rx_recover(uint32_t n, const rfec_wire_rec* recs, const uint8_t* payloa
     rep->n_fec_dropped = X.dropped;
     rep->host_us += now_us() - th;
     /* 3. the device: the records stay at the start of the pinned block */
-    rc = rx_device(&X, payload, stride, capacity, rec_bytes, out, out_payload, max_out, n_out, rep, sm);
-    rep->n_unmodelled = X.unmodelled;
+    rx_sim* XS[1] = {&X};
+    rx_dev D;
+    memset(&D, 0, sizeof(D));
+    rc = rx_device(XS, 1, &D, payload, stride, capacity, rec_bytes, 1, out, out_payload, max_out, n_out, rep, sm);
+    rep->n_unmodelled = X.unmodelled + D.unmodelled;
+    rx_dev_free(&D);
     rx_sim_free(&X);
     rep->total_us = now_us() - t0;
     return rc;
@@ -1305,8 +1669,9 @@ int rfec_host_recv_datagrams(uint32_t n, uint32_t dstride, const uint8_t* dgram,
 }
 
 /* ------------------------------------------------------------------------ */
-/* Receiver session: rx_sim kept across calls, records by id in a host store, */
-/* their payload rows by id in an HBM arena                                   */
+/* Receiver session: the control plane kept across calls, sharded by fec_id   */
+/* (above: rx_owners, the journal) over T shards replayed by a thread pool;   */
+/* records by id in a host store, their payload rows by id in an HBM arena    */
 /* ------------------------------------------------------------------------ */
 /* a batch of the pipelined push: its parse in flight on the session's stream */
 typedef struct {
@@ -1318,9 +1683,131 @@ typedef struct {
     hipEvent_t done;
 } rx_stage;
 
+/* The replay threads: T - 1 workers beside the calling thread, woken per
+ * batch (a generation counter; a short spin, then a condition variable). */
+typedef struct rx_pool rx_pool;
+typedef struct {
+    rx_pool* pool;
+    uint32_t idx;
+} rx_worker;
+struct rx_pool {
+    pthread_t th[RX_MAX_THREADS];
+    rx_worker w[RX_MAX_THREADS];
+    uint32_t nth; /* workers started */
+    pthread_mutex_t mu;
+    pthread_cond_t go, fin;
+    uint32_t gen, done; /* atomics */
+    int stop;
+    void (*fn)(void*, uint32_t);
+    void* arg;
+};
+
+#define RX_SPIN_US 200.0 /* a worker or the caller spins this long before sleeping */
+
+static void cpu_relax(void)
+{
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#endif
+}
+
+static void* pool_main(void* p)
+{
+    rx_worker* W = (rx_worker*)p;
+    rx_pool* P = W->pool;
+    uint32_t seen = 0;
+    for (;;) {
+        const double t0 = now_us();
+        for (uint32_t i = 0; __atomic_load_n(&P->gen, __ATOMIC_ACQUIRE) == seen && !P->stop; ++i) {
+            cpu_relax();
+            if ((i & 63) == 63 && now_us() - t0 > RX_SPIN_US) {
+                pthread_mutex_lock(&P->mu);
+                while (__atomic_load_n(&P->gen, __ATOMIC_ACQUIRE) == seen && !P->stop)
+                    pthread_cond_wait(&P->go, &P->mu);
+                pthread_mutex_unlock(&P->mu);
+            }
+        }
+        if (P->stop)
+            return NULL;
+        seen = __atomic_load_n(&P->gen, __ATOMIC_ACQUIRE);
+        P->fn(P->arg, W->idx);
+        if (__atomic_add_fetch(&P->done, 1u, __ATOMIC_ACQ_REL) == P->nth) {
+            pthread_mutex_lock(&P->mu);
+            pthread_cond_broadcast(&P->fin);
+            pthread_mutex_unlock(&P->mu);
+        }
+    }
+}
+
+static int pool_start(rx_pool* P, uint32_t workers)
+{
+    memset(P, 0, sizeof(*P));
+    pthread_mutex_init(&P->mu, NULL);
+    pthread_cond_init(&P->go, NULL);
+    pthread_cond_init(&P->fin, NULL);
+    for (uint32_t i = 0; i < workers; ++i) {
+        P->w[i] = (rx_worker){P, i + 1};
+        if (pthread_create(&P->th[i], NULL, pool_main, &P->w[i]))
+            return -1;
+        P->nth = i + 1;
+    }
+    return 0;
+}
+
+static void pool_stop(rx_pool* P)
+{
+    pthread_mutex_lock(&P->mu);
+    P->stop = 1;
+    pthread_cond_broadcast(&P->go);
+    pthread_mutex_unlock(&P->mu);
+    for (uint32_t i = 0; i < P->nth; ++i)
+        pthread_join(P->th[i], NULL);
+    pthread_mutex_destroy(&P->mu);
+    pthread_cond_destroy(&P->go);
+    pthread_cond_destroy(&P->fin);
+    P->nth = 0;
+}
+
+/* fn(arg, 0) here and fn(arg, i) on worker i, 1 <= i <= nth; returns when all are done */
+static void pool_run(rx_pool* P, void (*fn)(void*, uint32_t), void* arg)
+{
+    P->fn = fn;
+    P->arg = arg;
+    __atomic_store_n(&P->done, 0u, __ATOMIC_RELEASE);
+    pthread_mutex_lock(&P->mu);
+    __atomic_add_fetch(&P->gen, 1u, __ATOMIC_ACQ_REL);
+    pthread_cond_broadcast(&P->go);
+    pthread_mutex_unlock(&P->mu);
+    fn(arg, 0);
+    const double t0 = now_us();
+    for (uint32_t i = 0; __atomic_load_n(&P->done, __ATOMIC_ACQUIRE) < P->nth; ++i) {
+        cpu_relax();
+        if ((i & 63) == 63 && now_us() - t0 > RX_SPIN_US) {
+            pthread_mutex_lock(&P->mu);
+            while (__atomic_load_n(&P->done, __ATOMIC_ACQUIRE) < P->nth)
+                pthread_cond_wait(&P->fin, &P->mu);
+            pthread_mutex_unlock(&P->mu);
+        }
+    }
+}
+
 struct rfec_rx_session {
-    rx_sim X;
-    rfec_wire_rec* store; /* X.R */
+    rx_sim* XS[RX_MAX_THREADS]; /* the shards: fec_id % T (T = 1: one serial state) */
+    uint32_t T;
+    uint32_t max_ts;            /* sim_receiver_fec_t.max_ts, over the shards */
+    rx_pool pool;
+    int pool_on;
+    hmap vown[RX_MAX_THREADS];  /* sharded: packet id -> fec_id + 1, partition (seq >> 8) % T */
+    int vown_on;
+    rx_par par;
+    uint8_t* pshard;            /* per batch record: its shard (0xFF: no control-plane effect) */
+    uint32_t* lst;              /* per shard, its records of the batch in arrival order */
+    uint32_t* smin;
+    uint32_t lcap;
+    uint32_t loff[RX_MAX_THREADS + 1];
+    uint32_t n_parallel, n_serial, n_rollback; /* batches by replay (rfec_rx_session_info) */
+    rx_dev dev;
+    rfec_wire_rec* store; /* every shard's R */
     uint32_t nstore, storecap;
     uint8_t* arena; /* [arows][stride]: rows [0, nstore) ingested, then the pending batch's */
     uint32_t arows;
@@ -1332,6 +1819,49 @@ struct rfec_rx_session {
     int pend;        /* its stage, -1: none */
 };
 
+static void rx_shards_free(rfec_rx_session* S)
+{
+    for (uint32_t t = 0; t < S->T; ++t)
+        if (S->XS[t]) {
+            rx_sim_free(S->XS[t]);
+            free(S->XS[t]);
+            S->XS[t] = NULL;
+        }
+}
+
+/* T empty shards (and, for T > 1, the replay threads) */
+static int rx_shards_init(rfec_rx_session* S, uint32_t T)
+{
+    if (S->pool_on) {
+        pool_stop(&S->pool);
+        S->pool_on = 0;
+    }
+    rx_shards_free(S);
+    S->T = T;
+    for (uint32_t t = 0; t < T; ++t) {
+        rx_sim* X = (rx_sim*)calloc(1, sizeof(rx_sim));
+        S->XS[t] = X;
+        if (!X || rx_tables_init(X, 1024))
+            return -1;
+        X->capacity = S->capacity;
+    }
+    if (T > 1) {
+        if (pool_start(&S->pool, T - 1)) {
+            S->pool_on = 1;
+            return -1;
+        }
+        S->pool_on = 1;
+    }
+    return 0;
+}
+
+static uint32_t rx_default_threads(void)
+{
+    const char* v = getenv("RFEC_RX_THREADS");
+    const int t = v ? atoi(v) : 8;
+    return t < 1 ? 1u : t > RX_MAX_THREADS ? (uint32_t)RX_MAX_THREADS : (uint32_t)t;
+}
+
 rfec_rx_session* rfec_rx_session_create(uint32_t stride, uint32_t capacity)
 {
     if (stride == 0 || stride % 16 || capacity > stride) {
@@ -1339,18 +1869,32 @@ rfec_rx_session* rfec_rx_session_create(uint32_t stride, uint32_t capacity)
         return NULL;
     }
     rfec_rx_session* s = (rfec_rx_session*)calloc(1, sizeof(*s));
-    if (!s || rx_tables_init(&s->X, 1024)) {
-        if (s)
-            rx_sim_free(&s->X);
-        free(s);
-        set_err(RFEC_ENOMEM, "rx session: host tables", 0);
+    if (!s) {
+        set_err(RFEC_ENOMEM, "rx session", 0);
         return NULL;
     }
-    s->X.capacity = capacity;
     s->stride = stride;
     s->capacity = capacity;
     s->pend = -1;
+    if (rx_shards_init(s, rx_default_threads())) {
+        rfec_rx_session_destroy(s);
+        set_err(RFEC_ENOMEM, "rx session: host tables / threads", 0);
+        return NULL;
+    }
     return s;
+}
+
+int rfec_rx_session_set_threads(rfec_rx_session* s, uint32_t threads)
+{
+    if (!s || threads < 1 || threads > RX_MAX_THREADS)
+        return set_err(RFEC_EINVAL, "rx session: threads must be in [1, 64]", 0);
+    if (s->nstore || s->pend >= 0 || s->max_ts)
+        return set_err(RFEC_EINVAL, "rx session: threads are set before the first push", 0);
+    if (threads == s->T)
+        return RFEC_OK;
+    if (rx_shards_init(s, threads))
+        return set_err(RFEC_ENOMEM, "rx session: host tables / threads", 0);
+    return RFEC_OK;
 }
 
 void rfec_rx_session_destroy(rfec_rx_session* s)
@@ -1369,109 +1913,491 @@ void rfec_rx_session_destroy(rfec_rx_session* s)
     }
     if (s->sa)
         (void)hipStreamDestroy(s->sa);
-    rx_sim_free(&s->X);
+    if (s->pool_on)
+        pool_stop(&s->pool);
+    rx_shards_free(s);
+    rx_dev_free(&s->dev);
+    if (s->vown_on)
+        for (uint32_t t = 0; t < s->T; ++t)
+            hm_free(&s->vown[t]);
+    free(s->pshard);
+    free(s->lst);
+    free(s->smin);
     free(s->store);
     if (s->arena)
         (void)hipFree(s->arena);
     free(s);
 }
 
+/* The shards merged into one serial state, for good: a batch broke the
+ * partition (a packet id under two fec_ids, a recovery outside its flex, or
+ * parity ranges too large to claim).  Instances, shapes, slot / line tables
+ * and recovered headers are concatenated; map values follow. */
+static int rx_merge(rfec_rx_session* S)
+{
+    const uint32_t T = S->T;
+    if (T == 1)
+        return RFEC_OK;
+    rx_sim* M = (rx_sim*)calloc(1, sizeof(rx_sim));
+    uint32_t ng = 0, nslot = 0, nline = 0, ns = 0, nrh = 0, nseen = 0, ncache = 0;
+    for (uint32_t t = 0; t < T; ++t) {
+        const rx_sim* X = S->XS[t];
+        ng += X->ng, nslot += X->nslot, nline += X->nline, ns += X->ns, nrh += X->nrh;
+        nseen += X->seen.n, ncache += X->cache.n;
+    }
+    if (!M || hm_init(&M->seen, nseen) || hm_init(&M->cache, ncache) || hm_init(&M->flex_of, 1024) ||
+        hm_init(&M->shape_of, 64))
+        goto oom;
+    M->R = S->store;
+    M->capacity = S->capacity;
+    M->max_ts = S->max_ts;
+    M->G = (rx_inst*)malloc(((size_t)ng + 1) * sizeof(rx_inst));
+    M->S = (rx_shape*)malloc(((size_t)ns + 1) * sizeof(rx_shape));
+    M->slot_src = (int32_t*)malloc(((size_t)nslot + 1) * sizeof(int32_t));
+    M->slot_hdr = (rfec_hdr*)malloc(((size_t)nslot + 1) * sizeof(rfec_hdr));
+    M->line_par = (int32_t*)malloc(((size_t)nline + 1) * sizeof(int32_t));
+    M->rh = (rfec_hdr*)malloc(((size_t)nrh + 1) * sizeof(rfec_hdr));
+    if (!M->G || !M->S || !M->slot_src || !M->slot_hdr || !M->line_par || !M->rh)
+        goto oom;
+    M->gcap = ng + 1, M->scap = ns + 1, M->slotcap = M->slothcap = nslot + 1, M->linecap = nline + 1;
+    M->rhcap = nrh + 1;
+    for (uint32_t t = 0; t < T; ++t) {
+        const rx_sim* X = S->XS[t];
+        const uint32_t og = M->ng, os = M->ns, oslot = M->nslot, oline = M->nline, orh = M->nrh;
+        for (uint32_t i = 0; i < X->ng; ++i) {
+            rx_inst g = X->G[i];
+            g.slot0 += oslot;
+            g.line0 += oline;
+            if (g.shape != UINT32_MAX)
+                g.shape += os;
+            g.gstamp = g.jstamp = 0;
+            M->G[M->ng++] = g;
+        }
+        for (uint32_t i = 0; i < X->ns; ++i) {
+            const rx_shape* sh = &X->S[i];
+            M->S[M->ns++] = *sh;
+            const uint32_t key = sh->count << 16 | sh->row << 8 | sh->col;
+            if (!sh->xcol[0] && !sh->xcol[1] && !hm_get(&M->shape_of, key) && hm_put(&M->shape_of, key, os + i + 1))
+                goto oom;
+        }
+        memcpy(M->slot_src + oslot, X->slot_src, (size_t)X->nslot * sizeof(int32_t));
+        memcpy(M->slot_hdr + oslot, X->slot_hdr, (size_t)X->nslot * sizeof(rfec_hdr));
+        memcpy(M->line_par + oline, X->line_par, (size_t)X->nline * sizeof(int32_t));
+        memcpy(M->rh + orh, X->rh, (size_t)X->nrh * sizeof(rfec_hdr));
+        M->nslot += X->nslot, M->nline += X->nline, M->nrh += X->nrh;
+        for (uint32_t i = 0; i <= X->seen.mask; ++i)
+            if (X->seen.v[i] && hm_put(&M->seen, X->seen.k[i], X->seen.v[i]))
+                goto oom;
+        for (uint32_t i = 0; i <= X->cache.mask; ++i) {
+            const uint32_t c = X->cache.v[i];
+            if (c && hm_put(&M->cache, X->cache.k[i], (c & 0x80000000u) ? (0x80000000u | ((c & 0x7FFFFFFFu) + orh)) : c))
+                goto oom;
+        }
+        for (uint32_t i = 0; i <= X->flex_of.mask; ++i)
+            if (X->flex_of.v[i] && hm_put(&M->flex_of, X->flex_of.k[i], X->flex_of.v[i] + og))
+                goto oom;
+    }
+    if (S->vown_on)
+        for (uint32_t t = 0; t < T; ++t)
+            hm_free(&S->vown[t]);
+    S->vown_on = 0;
+    rx_shards_free(S);
+    if (S->pool_on) {
+        pool_stop(&S->pool);
+        S->pool_on = 0;
+    }
+    S->XS[0] = M;
+    S->T = 1;
+    return RFEC_OK;
+oom:
+    if (M) {
+        rx_sim_free(M);
+        free(M);
+    }
+    return set_err(RFEC_ENOMEM, "rx session: merge", 0);
+}
+
+/* Phase 0 of a sharded batch, serial over the records [a0, a0 + n): each
+ * record's shard, the per-shard lists, smin, whether a parity of the batch
+ * could meet the 3 s drop through a segment timestamp before it (`risky`). */
+static int rx_phase0(rfec_rx_session* S, uint32_t a0, uint32_t n, int* risky)
+{
+    if (S->lcap < n) {
+        const uint32_t c = n + n / 4 + 64;
+        uint8_t* ps = (uint8_t*)realloc(S->pshard, c);
+        if (ps)
+            S->pshard = ps;
+        uint32_t* l = (uint32_t*)realloc(S->lst, (size_t)c * 4);
+        if (l)
+            S->lst = l;
+        uint32_t* m = (uint32_t*)realloc(S->smin, (size_t)c * 4);
+        if (m)
+            S->smin = m;
+        if (!ps || !l || !m)
+            return set_err(RFEC_ENOMEM, "rx session: batch lists", 0);
+        S->lcap = c;
+    }
+    const uint32_t T = S->T;
+    const rfec_wire_rec* R = S->store + a0;
+    uint32_t cnt[RX_MAX_THREADS] = {0};
+    uint32_t pm = S->max_ts;
+    int rk = 0;
+    for (uint32_t p = 0; p < n; ++p) {
+        const rfec_wire_rec* r = &R[p];
+        uint32_t t = 0xFF;
+        if (r->status == RFEC_WIRE_OK && r->mid == RFEC_WIRE_SEG) {
+            t = r->fec_id ? r->fec_id % T : r->hdr.seq % T;
+            if (r->fec_id && r->hdr.seq && r->hdr.ts > pm) /* (an upper bound of what raises max_ts) */
+                pm = r->hdr.ts;
+        } else if (r->status == RFEC_WIRE_OK && r->mid == RFEC_WIRE_FEC) {
+            t = r->fec_id % T;
+            if (r->send_ts + 3000u < pm) /* sim_fec.c:148 could drop it */
+                rk = 1;
+        }
+        S->pshard[p] = (uint8_t)t;
+        if (t != 0xFF)
+            cnt[t]++;
+    }
+    uint32_t m = UINT32_MAX;
+    for (uint32_t p = n; p-- > 0;) {
+        S->smin[p] = m;
+        const rfec_wire_rec* r = &R[p];
+        if (r->status == RFEC_WIRE_OK && r->mid == RFEC_WIRE_FEC && r->send_ts + 3000u < m)
+            m = r->send_ts + 3000u;
+    }
+    S->loff[0] = 0;
+    for (uint32_t t = 0; t < T; ++t)
+        S->loff[t + 1] = S->loff[t] + cnt[t];
+    uint32_t pos[RX_MAX_THREADS];
+    memcpy(pos, S->loff, T * sizeof(uint32_t));
+    for (uint32_t p = 0; p < n; ++p)
+        if (S->pshard[p] != 0xFF)
+            S->lst[pos[S->pshard[p]]++] = a0 + p;
+    *risky = rk;
+    return RFEC_OK;
+}
+
+/* shard t replays its records of the batch in arrival order */
+static void rx_shard_job(void* arg, uint32_t t)
+{
+    rfec_rx_session* S = (rfec_rx_session*)arg;
+    rx_sim* X = S->XS[t];
+    const uint32_t* L = S->lst + S->loff[t];
+    const uint32_t n = S->loff[t + 1] - S->loff[t];
+    for (uint32_t i = 0; i < n && !X->oom; ++i) {
+        if ((i & 15) == 0 && __atomic_load_n(&S->par.conflict, __ATOMIC_RELAXED))
+            return;
+        rx_arrival(X, L[i]);
+    }
+    rx_bucket_claims(X, S->T);
+}
+
+/* the batch's packet-id claims into the owner tables: thread j takes the ids
+ * of its partition from every shard's log; an id under two fec_ids is a
+ * conflict */
+static void rx_verify_job(void* arg, uint32_t j)
+{
+    rfec_rx_session* S = (rfec_rx_session*)arg;
+    hmap* V = &S->vown[j];
+    const uint32_t T = S->T;
+    for (uint32_t u = 0; u < T; ++u) {
+        const rx_sim* X = S->XS[u];
+        for (uint32_t q = X->coff[j]; q < X->coff[j + 1]; ++q) {
+            const uint32_t seq = (uint32_t)(X->cpart[q] >> 32), code = (uint32_t)X->cpart[q];
+            const uint32_t v = hm_get(V, seq);
+            if (!v) {
+                if (hm_put(V, seq, code))
+                    __atomic_fetch_or(&S->par.conflict, RX_CONFLICT_OWNER, __ATOMIC_RELAXED); /* (no memory: serial) */
+            } else if (v != code) {
+                __atomic_fetch_or(&S->par.conflict, RX_CONFLICT_OWNER, __ATOMIC_RELAXED);
+                return;
+            }
+        }
+    }
+}
+
+/* the batch in arrival order over the shards, one max_ts (then the claims bucketed) */
+static void rx_serial_over_shards(rfec_rx_session* S, uint32_t a0, uint32_t n)
+{
+    uint32_t m = S->max_ts;
+    for (uint32_t p = 0; p < n; ++p) {
+        if (S->pshard[p] == 0xFF)
+            continue;
+        rx_sim* X = S->XS[S->pshard[p]];
+        X->max_ts = m;
+        rx_arrival(X, a0 + p);
+        m = X->max_ts;
+        if (X->oom || __atomic_load_n(&S->par.conflict, __ATOMIC_RELAXED))
+            break;
+    }
+    for (uint32_t t = 0; t < S->T; ++t)
+        rx_bucket_claims(S->XS[t], S->T);
+}
+
+static int rx_any_oom(const rfec_rx_session* S)
+{
+    for (uint32_t t = 0; t < S->T; ++t)
+        if (S->XS[t]->oom)
+            return 1;
+    return 0;
+}
+
+/* The control plane over the session's records [a0, a0 + n). */
+static int rx_ingest(rfec_rx_session* S, uint32_t a0, uint32_t n)
+{
+    for (uint32_t t = 0; t < S->T; ++t) {
+        rx_sim* X = S->XS[t];
+        X->R = S->store;
+        X->nout = X->dropped = X->unmodelled = 0;
+    }
+    int rc, risky = 0;
+    if (S->T > 1) {
+        if (!S->vown_on) {
+            for (uint32_t t = 0; t < S->T; ++t)
+                if (hm_init(&S->vown[t], 4096))
+                    return set_err(RFEC_ENOMEM, "rx session: packet ids", 0);
+            S->vown_on = 1;
+        }
+        for (uint32_t t = 0; t < S->T; ++t) {
+            rx_sim* X = S->XS[t];
+            if (!X->claimed && !(X->claimed = (uint32_t*)calloc(2u * (65536u / S->T + 1u), sizeof(uint32_t))))
+                return set_err(RFEC_ENOMEM, "rx session: claims", 0);
+            X->nclaims = 0;
+        }
+        if ((rc = rx_phase0(S, a0, n, &risky)))
+            return rc;
+    }
+    if (S->T == 1) {
+        rx_sim* X = S->XS[0];
+        X->P = NULL;
+        X->R = S->store;
+        X->nout = X->dropped = X->unmodelled = 0;
+        X->max_ts = S->max_ts;
+        rx_run(X, a0, n);
+        S->max_ts = X->max_ts;
+        S->n_serial++;
+        return X->oom ? set_err(RFEC_ENOMEM, "rx session: host tables", 0) : RFEC_OK;
+    }
+    rx_par* P = &S->par;
+    P->T = S->T;
+    P->smin = S->smin;
+    P->a0 = a0;
+    P->ts_check = !risky;
+    P->conflict = 0;
+    for (uint32_t t = 0; t < S->T; ++t) {
+        rx_sim* X = S->XS[t];
+        X->P = P;
+        X->max_ts = S->max_ts;
+        rx_journal_begin(X);
+    }
+    if (!risky)
+        pool_run(&S->pool, rx_shard_job, S);
+    else
+        rx_serial_over_shards(S, a0, n);
+    int c = __atomic_load_n(&P->conflict, __ATOMIC_RELAXED);
+    if (!c && !rx_any_oom(S)) {
+        pool_run(&S->pool, rx_verify_job, S); /* every packet id under one fec_id? */
+        c = __atomic_load_n(&P->conflict, __ATOMIC_RELAXED);
+        if (!c)
+            ++*(risky ? &S->n_serial : &S->n_parallel);
+    } else if ((c & RX_CONFLICT_TS) && !(c & RX_CONFLICT_OWNER) && !rx_any_oom(S)) {
+        /* a recovery raised max_ts past a later parity's limit: again, in arrival order */
+        S->n_rollback++;
+        for (uint32_t t = 0; t < S->T; ++t) {
+            rx_rollback(S->XS[t]);
+            rx_journal_begin(S->XS[t]);
+        }
+        P->ts_check = 0;
+        P->conflict = 0;
+        rx_serial_over_shards(S, a0, n); /* (the claim logs keep the first try's claims too) */
+        c = __atomic_load_n(&P->conflict, __ATOMIC_RELAXED);
+        if (!c && !rx_any_oom(S)) {
+            pool_run(&S->pool, rx_verify_job, S);
+            c = __atomic_load_n(&P->conflict, __ATOMIC_RELAXED);
+        }
+        if (!c)
+            S->n_serial++;
+    }
+    if (rx_any_oom(S))
+        return set_err(RFEC_ENOMEM, "rx session: host tables", 0);
+    if (c) { /* a packet id crossed fec_ids: back to the batch's start, one serial state from here on */
+        S->n_rollback++;
+        for (uint32_t t = 0; t < S->T; ++t) {
+            rx_rollback(S->XS[t]);
+            S->XS[t]->P = NULL;
+        }
+        if (rx_any_oom(S) || (rc = rx_merge(S)))
+            return set_err(RFEC_ENOMEM, "rx session: merge", 0);
+        rx_sim* X = S->XS[0];
+        X->nout = X->dropped = X->unmodelled = 0;
+        X->max_ts = S->max_ts;
+        rx_run(X, a0, n);
+        S->max_ts = X->max_ts;
+        S->n_serial++;
+        return X->oom ? set_err(RFEC_ENOMEM, "rx session: host tables", 0) : RFEC_OK;
+    }
+    uint32_t m = S->max_ts;
+    for (uint32_t t = 0; t < S->T; ++t) {
+        rx_sim* X = S->XS[t];
+        rx_journal_end(X);
+        X->P = NULL;
+        m = X->max_ts > m ? X->max_ts : m;
+    }
+    S->max_ts = m;
+    return RFEC_OK;
+}
+
 /* Keeps only what the open state refers to: the flexes still registered (with
  * their slot / line tables), the records of cached segments and of those
  * flexes' members and parities (their rows gathered into a fresh arena with
- * room for `extra` more), the headers of cached recovered segments.  The rows
- * of a pending pipelined batch (parsed, not ingested) move along behind the
- * kept ones. */
+ * room for `extra` more), the headers of cached recovered segments -- over
+ * every shard; records are renumbered in arrival order.  The rows of a
+ * pending pipelined batch (parsed, not ingested) move along behind the kept
+ * ones. */
+typedef struct {
+    rx_inst* NG;
+    int32_t* nsrc;
+    rfec_hdr* nhdr;
+    int32_t* npar;
+    uint32_t* hmap_; /* old rh -> new + 1 */
+    uint32_t ng, ns, nl, nh;
+} rx_kept;
+
 static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
 {
     const uint32_t tail = S->pend >= 0 ? S->pend_n : 0;
     hipError_t e;
     if (tail && (e = hipEventSynchronize(S->st[S->pend].done)) != hipSuccess)
         return set_err(RFEC_EDEVICE, "rx session: pending parse", e);
-    rx_sim* X = &S->X;
+    const uint32_t T = S->T;
     int rc = RFEC_OK;
-    const uint32_t ng_live = X->flex_of.n;
-    rx_inst* NG = (rx_inst*)malloc(((size_t)ng_live + 1) * sizeof(rx_inst));
-    uint32_t nslot = 0, nline = 0;
-    for (uint32_t i = 0; i <= X->flex_of.mask; ++i)
-        if (X->flex_of.v[i]) {
-            const rx_inst* g = &X->G[X->flex_of.v[i] - 1];
-            if (g->shape != UINT32_MAX) {
-                nslot += g->count;
-                nline += X->S[g->shape].n_lines;
-            }
-        }
-    int32_t* nsrc = (int32_t*)malloc(((size_t)nslot + 1) * sizeof(int32_t));
-    rfec_hdr* nhdr = (rfec_hdr*)malloc(((size_t)nslot + 1) * sizeof(rfec_hdr));
-    int32_t* npar = (int32_t*)malloc(((size_t)nline + 1) * sizeof(int32_t));
+    rx_kept K[RX_MAX_THREADS];
+    memset(K, 0, sizeof(K));
     uint32_t* rmap = (uint32_t*)calloc((size_t)S->nstore + 1, sizeof(uint32_t)); /* old record -> new + 1 */
-    uint32_t* hmap_ = (uint32_t*)calloc((size_t)X->nrh + 1, sizeof(uint32_t));  /* old rh -> new + 1 */
-    if (!NG || !nsrc || !nhdr || !npar || !rmap || !hmap_) {
-        rc = set_err(RFEC_ENOMEM, "rx session: compaction", 0);
+    uint32_t* gmap = NULL;
+    uint8_t* arena = NULL;
+    if (!rmap)
+        goto oom;
+    /* 1. per shard: live flexes and their tables; mark the records they refer to */
+    for (uint32_t t = 0; t < T; ++t) {
+        const rx_sim* X = S->XS[t];
+        rx_kept* k = &K[t];
+        uint32_t nslot = 0, nline = 0;
+        for (uint32_t i = 0; i <= X->flex_of.mask; ++i)
+            if (X->flex_of.v[i]) {
+                const rx_inst* g = &X->G[X->flex_of.v[i] - 1];
+                if (g->shape != UINT32_MAX) {
+                    nslot += g->count;
+                    nline += X->S[g->shape].n_lines;
+                }
+            }
+        k->NG = (rx_inst*)malloc(((size_t)X->flex_of.n + 1) * sizeof(rx_inst));
+        k->nsrc = (int32_t*)malloc(((size_t)nslot + 1) * sizeof(int32_t));
+        k->nhdr = (rfec_hdr*)malloc(((size_t)nslot + 1) * sizeof(rfec_hdr));
+        k->npar = (int32_t*)malloc(((size_t)nline + 1) * sizeof(int32_t));
+        k->hmap_ = (uint32_t*)calloc((size_t)X->nrh + 1, sizeof(uint32_t));
+        if (!k->NG || !k->nsrc || !k->nhdr || !k->npar || !k->hmap_)
+            goto oom;
+        /* the records the live state refers to (read only: nothing changes before the arena is allocated) */
+        for (uint32_t i = 0; i <= X->flex_of.mask; ++i)
+            if (X->flex_of.v[i]) {
+                const rx_inst* g = &X->G[X->flex_of.v[i] - 1];
+                if (g->shape == UINT32_MAX)
+                    continue;
+                for (uint32_t q = 0; q < g->count; ++q)
+                    if (X->slot_src[g->slot0 + q] >= 0)
+                        rmap[X->slot_src[g->slot0 + q]] = 1;
+                for (uint32_t q = 0; q < X->S[g->shape].n_lines; ++q)
+                    if (X->line_par[g->line0 + q] >= 0)
+                        rmap[X->line_par[g->line0 + q]] = 1;
+            }
+        for (uint32_t i = 0; i <= X->cache.mask; ++i) {
+            const uint32_t c = X->cache.v[i];
+            if (c && !(c & 0x80000000u))
+                rmap[c - 1] = 1;
+        }
+    }
+    uint32_t nr = 0;
+    for (uint32_t r = 0; r < S->nstore; ++r)
+        nr += rmap[r] != 0;
+    gmap = (uint32_t*)malloc(((size_t)nr + tail + 1) * sizeof(uint32_t)); /* new -> old */
+    const uint32_t arows = 2 * (nr + tail + extra) > 4096 ? 2 * (nr + tail + extra) : 4096;
+    if (!gmap)
+        goto oom;
+    if ((e = hipMalloc((void**)&arena, (size_t)arows * S->stride)) != hipSuccess) {
+        rc = set_err(RFEC_ENOMEM, "rx session: arena", e);
         goto done;
     }
-    /* 1. live flexes, their tables; the records they refer to */
-    uint32_t ng = 0, ns = 0, nl = 0;
-    for (uint32_t i = 0; i <= X->flex_of.mask; ++i) {
-        if (!X->flex_of.v[i])
-            continue;
-        rx_inst g = X->G[X->flex_of.v[i] - 1];
-        if (g.shape != UINT32_MAX) {
-            const uint32_t nlines = X->S[g.shape].n_lines;
-            memcpy(nsrc + ns, X->slot_src + g.slot0, g.count * sizeof(int32_t));
-            memcpy(nhdr + ns, X->slot_hdr + g.slot0, g.count * sizeof(rfec_hdr));
-            memcpy(npar + nl, X->line_par + g.line0, nlines * sizeof(int32_t));
-            for (uint32_t q = 0; q < g.count; ++q)
-                if (nsrc[ns + q] >= 0)
-                    rmap[nsrc[ns + q]] = 1;
-            for (uint32_t q = 0; q < nlines; ++q)
-                if (npar[nl + q] >= 0)
-                    rmap[npar[nl + q]] = 1;
-            g.slot0 = ns;
-            g.line0 = nl;
-            ns += g.count;
-            nl += nlines;
+    for (uint32_t t = 0; t < T; ++t) {
+        rx_sim* X = S->XS[t];
+        rx_kept* k = &K[t];
+        for (uint32_t i = 0; i <= X->flex_of.mask; ++i) {
+            if (!X->flex_of.v[i])
+                continue;
+            rx_inst g = X->G[X->flex_of.v[i] - 1];
+            if (g.shape != UINT32_MAX) {
+                const uint32_t nlines = X->S[g.shape].n_lines;
+                memcpy(k->nsrc + k->ns, X->slot_src + g.slot0, g.count * sizeof(int32_t));
+                memcpy(k->nhdr + k->ns, X->slot_hdr + g.slot0, g.count * sizeof(rfec_hdr));
+                memcpy(k->npar + k->nl, X->line_par + g.line0, nlines * sizeof(int32_t));
+                g.slot0 = k->ns;
+                g.line0 = k->nl;
+                k->ns += g.count;
+                k->nl += nlines;
+            }
+            k->NG[k->ng] = g;
+            X->flex_of.v[i] = ++k->ng;
         }
-        NG[ng] = g;
-        X->flex_of.v[i] = ++ng;
-    }
-    /* 2. cached segments: arrived ones keep their record, recovered ones their header */
-    for (uint32_t i = 0; i <= X->cache.mask; ++i) {
-        const uint32_t c = X->cache.v[i];
-        if (!c)
-            continue;
-        if (c & 0x80000000u)
-            hmap_[c & 0x7FFFFFFFu] = 1;
-        else
-            rmap[c - 1] = 1;
+        /* 2. cached recovered segments keep their header */
+        for (uint32_t i = 0; i <= X->cache.mask; ++i) {
+            const uint32_t c = X->cache.v[i];
+            if (c & 0x80000000u)
+                k->hmap_[c & 0x7FFFFFFFu] = 1;
+        }
     }
     /* 3. new ids, in arrival order */
-    uint32_t nr = 0, nh = 0;
+    nr = 0;
     for (uint32_t r = 0; r < S->nstore; ++r)
         if (rmap[r])
             rmap[r] = ++nr;
-    for (uint32_t h = 0; h < X->nrh; ++h)
-        if (hmap_[h])
-            hmap_[h] = ++nh;
-    for (uint32_t q = 0; q < ns; ++q)
-        if (nsrc[q] >= 0)
-            nsrc[q] = (int32_t)rmap[nsrc[q]] - 1;
-    for (uint32_t q = 0; q < nl; ++q)
-        if (npar[q] >= 0)
-            npar[q] = (int32_t)rmap[npar[q]] - 1;
-    for (uint32_t i = 0; i <= X->cache.mask; ++i) {
-        const uint32_t c = X->cache.v[i];
-        if (c)
-            X->cache.v[i] = (c & 0x80000000u) ? (0x80000000u | (hmap_[c & 0x7FFFFFFFu] - 1)) : rmap[c - 1];
+    for (uint32_t t = 0; t < T; ++t) {
+        rx_sim* X = S->XS[t];
+        rx_kept* k = &K[t];
+        for (uint32_t h = 0; h < X->nrh; ++h)
+            if (k->hmap_[h])
+                k->hmap_[h] = ++k->nh;
+        for (uint32_t q = 0; q < k->ns; ++q)
+            if (k->nsrc[q] >= 0)
+                k->nsrc[q] = (int32_t)rmap[k->nsrc[q]] - 1;
+        for (uint32_t q = 0; q < k->nl; ++q)
+            if (k->npar[q] >= 0)
+                k->npar[q] = (int32_t)rmap[k->npar[q]] - 1;
+        for (uint32_t i = 0; i <= X->cache.mask; ++i) {
+            const uint32_t c = X->cache.v[i];
+            if (c)
+                X->cache.v[i] = (c & 0x80000000u) ? (0x80000000u | (k->hmap_[c & 0x7FFFFFFFu] - 1)) : rmap[c - 1];
+        }
+        for (uint32_t h = 0; h < X->nrh; ++h)
+            if (k->hmap_[h])
+                X->rh[k->hmap_[h] - 1] = X->rh[h];
+        X->nrh = k->nh;
+        /* the group tables */
+        free(X->G);
+        free(X->slot_src);
+        free(X->slot_hdr);
+        free(X->line_par);
+        X->G = k->NG;
+        X->ng = X->gcap = k->ng;
+        X->slot_src = k->nsrc;
+        X->slot_hdr = k->nhdr;
+        X->nslot = X->slotcap = X->slothcap = k->ns;
+        X->line_par = k->npar;
+        X->nline = X->linecap = k->nl;
+        k->NG = NULL;
+        k->nsrc = k->npar = NULL;
+        k->nhdr = NULL;
     }
     /* 4. records (host) and rows (device) */
-    uint32_t* gmap = (uint32_t*)malloc(((size_t)nr + tail + 1) * sizeof(uint32_t)); /* new -> old */
-    const uint32_t arows = 2 * (nr + tail + extra) > 4096 ? 2 * (nr + tail + extra) : 4096;
-    uint8_t* arena = NULL;
-    if (!gmap) {
-        rc = set_err(RFEC_ENOMEM, "rx session: compaction", 0);
-        goto done;
-    }
     for (uint32_t r = 0; r < S->nstore; ++r)
         if (rmap[r]) {
             gmap[rmap[r] - 1] = r;
@@ -1480,16 +2406,8 @@ static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
     for (uint32_t t = 0; t < tail; ++t)
         gmap[nr + t] = S->nstore + t;
     S->nstore = nr;
-    X->R = S->store;
-    for (uint32_t h = 0; h < X->nrh; ++h)
-        if (hmap_[h])
-            X->rh[hmap_[h] - 1] = X->rh[h];
-    X->nrh = nh;
-    if ((e = hipMalloc((void**)&arena, (size_t)arows * S->stride)) != hipSuccess) {
-        free(gmap);
-        rc = set_err(RFEC_ENOMEM, "rx session: arena", e);
-        goto done;
-    }
+    for (uint32_t t = 0; t < T; ++t)
+        S->XS[t]->R = S->store;
     if (nr + tail) {
         int32_t* dmap = NULL;
         int ke = 0;
@@ -1501,39 +2419,31 @@ static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
             if (dmap)
                 (void)hipFree(dmap);
             (void)hipFree(arena);
-            free(gmap);
+            arena = NULL;
             rc = set_err(RFEC_EDEVICE, "rx session: row compaction", ke ? ke : (int)e);
             goto done;
         }
         (void)hipFree(dmap);
     }
-    free(gmap);
     if (S->arena)
         (void)hipFree(S->arena);
     S->arena = arena;
     S->arows = arows;
-    /* 5. the group tables */
-    free(X->G);
-    free(X->slot_src);
-    free(X->slot_hdr);
-    free(X->line_par);
-    X->G = NG;
-    X->ng = X->gcap = ng;
-    X->slot_src = nsrc;
-    X->slot_hdr = nhdr;
-    X->nslot = X->slotcap = X->slothcap = ns;
-    X->line_par = npar;
-    X->nline = X->linecap = nl;
-    NG = NULL;
-    nsrc = npar = NULL;
-    nhdr = NULL;
+    goto done;
+oom:
+    rc = set_err(RFEC_ENOMEM, "rx session: compaction", 0);
+    if (arena)
+        (void)hipFree(arena);
 done:
-    free(NG);
-    free(nsrc);
-    free(nhdr);
-    free(npar);
+    for (uint32_t t = 0; t < T; ++t) {
+        free(K[t].NG);
+        free(K[t].nsrc);
+        free(K[t].nhdr);
+        free(K[t].npar);
+        free(K[t].hmap_);
+    }
+    free(gmap);
     free(rmap);
-    free(hmap_);
     return rc;
 }
 
@@ -1565,12 +2475,10 @@ static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const rfec_wir
                                   rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out,
                                   rfec_rx_report* rep, hipStream_t sm)
 {
-    rx_sim* X = &S->X;
     hipError_t e;
     int rc;
     if (payload && (rc = rx_session_room(S, n, sm)))
         return rc;
-    X->R = S->store;
     memcpy(S->store + S->nstore, rh, (size_t)n * sizeof(rfec_wire_rec));
     if (payload) {
         double tt = now_us();
@@ -1582,16 +2490,18 @@ static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const rfec_wir
     const uint32_t a0 = S->nstore;
     S->nstore += n;
     const double th = now_us();
-    X->nout = 0;
-    X->dropped = 0;
-    X->unmodelled = 0;
-    rx_run(X, a0, n);
-    if (X->oom)
-        return set_err(RFEC_ENOMEM, "rx session: host tables", 0);
-    rep->n_fec_dropped = X->dropped;
+    if ((rc = rx_ingest(S, a0, n)))
+        return rc;
+    uint32_t dropped = 0, unmod = 0;
+    for (uint32_t t = 0; t < S->T; ++t) {
+        dropped += S->XS[t]->dropped;
+        unmod += S->XS[t]->unmodelled;
+    }
+    rep->n_fec_dropped = dropped;
     rep->host_us += now_us() - th;
-    rc = rx_device(X, S->arena, S->stride, S->capacity, 0, out, out_payload, max_out, n_out, rep, sm);
-    rep->n_unmodelled = X->unmodelled;
+    rc = rx_device(S->XS, S->T, &S->dev, S->arena, S->stride, S->capacity, 0, 0, out, out_payload, max_out, n_out,
+                   rep, sm);
+    rep->n_unmodelled = unmod + S->dev.unmodelled;
     return rc;
 }
 
@@ -1797,13 +2707,73 @@ int rfec_rx_session_push_datagrams_async(rfec_rx_session* S, uint32_t n, uint32_
     return RFEC_OK;
 }
 
+static int cmp_u64(const void* a, const void* b)
+{
+    const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+/* every shard's keys of one map, key << 32 | shard, ascending (the skiplists' order) */
+static uint64_t* rx_keys(rfec_rx_session* S, int m, uint32_t* n)
+{
+    size_t tot = 0;
+    for (uint32_t t = 0; t < S->T; ++t)
+        tot += rx_map(S->XS[t], m)->n;
+    uint64_t* k = (uint64_t*)malloc((tot + 1) * sizeof(uint64_t));
+    *n = 0;
+    if (!k)
+        return NULL;
+    for (uint32_t t = 0; t < S->T; ++t) {
+        const hmap* h = rx_map(S->XS[t], m);
+        for (uint32_t i = 0; i <= h->mask; ++i)
+            if (h->v[i])
+                k[(*n)++] = (uint64_t)h->k[i] << 32 | t;
+    }
+    qsort(k, *n, sizeof(uint64_t), cmp_u64);
+    return k;
+}
+
+/* sim_fec_evict (sim_fec.c:209-241) over the shards: flexes in fec_id order
+ * while stale (fec_ts + 3000 <= max_ts) or full, removed with their members'
+ * cache entries; then cached segments in packet_id order while older than 6 s
+ * (timestamp + 6000 < max_ts); both walks stop at the first entry that stays
+ * (rx_evict's rules over the union of the shards). */
 int rfec_rx_session_evict(rfec_rx_session* S, void* stream)
 {
     if (!S)
         return set_err(RFEC_EINVAL, "rx session: NULL", 0);
-    rx_evict(&S->X);
-    if (S->X.oom)
+    for (uint32_t t = 0; t < S->T; ++t)
+        S->XS[t]->max_ts = S->max_ts;
+    if (S->T == 1) {
+        rx_evict(S->XS[0]);
+        if (S->XS[0]->oom)
+            return set_err(RFEC_ENOMEM, "rx session: evict", 0);
+        return rx_compact(S, 0, (hipStream_t)stream);
+    }
+    uint32_t n = 0;
+    uint64_t* k = rx_keys(S, 2, &n);
+    if (!k)
         return set_err(RFEC_ENOMEM, "rx session: evict", 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        rx_sim* X = S->XS[(uint32_t)k[i]];
+        const uint32_t fi = hm_get(&X->flex_of, (uint32_t)(k[i] >> 32)) - 1;
+        const rx_inst* g = &X->G[fi];
+        if (!(g->fec_ts + 3000u <= S->max_ts || g->nsegs >= g->count))
+            break;
+        rx_remove(X, fi);
+    }
+    free(k);
+    if (!(k = rx_keys(S, 1, &n)))
+        return set_err(RFEC_ENOMEM, "rx session: evict", 0);
+    for (uint32_t i = 0; i < n; ++i) {
+        rx_sim* X = S->XS[(uint32_t)k[i]];
+        const uint32_t seq = (uint32_t)(k[i] >> 32), c = hm_get(&X->cache, seq);
+        const uint32_t ts = (c & 0x80000000u) ? X->rh[c & 0x7FFFFFFFu].ts : X->R[c - 1].hdr.ts;
+        if (!(ts + 6000u < S->max_ts))
+            break;
+        hm_del(&X->cache, seq);
+    }
+    free(k);
     return rx_compact(S, 0, (hipStream_t)stream);
 }
 
@@ -1812,11 +2782,17 @@ int rfec_rx_session_get_info(const rfec_rx_session* S, rfec_rx_session_info* inf
     if (!S || !info)
         return set_err(RFEC_EINVAL, "rx session: NULL", 0);
     memset(info, 0, sizeof(*info));
-    info->max_ts = S->X.max_ts;
-    info->open_flexes = S->X.flex_of.n;
-    info->cached_segments = S->X.cache.n;
+    info->max_ts = S->max_ts;
+    for (uint32_t t = 0; t < S->T; ++t) {
+        info->open_flexes += S->XS[t]->flex_of.n;
+        info->cached_segments += S->XS[t]->cache.n;
+    }
     info->records_held = S->nstore;
     info->rows_held = S->arows;
     info->pending = S->pend >= 0 ? S->pend_n : 0;
+    info->threads = S->T;
+    info->batches_parallel = S->n_parallel;
+    info->batches_serial = S->n_serial;
+    info->batches_rolled_back = S->n_rollback;
     return RFEC_OK;
 }

@@ -86,7 +86,9 @@ class rfec_send_report(C.Structure):
 
 class rfec_rx_session_info(C.Structure):
     _fields_ = [("max_ts", C.c_uint32), ("open_flexes", C.c_uint32), ("cached_segments", C.c_uint32),
-                ("records_held", C.c_uint32), ("rows_held", C.c_uint32), ("pending", C.c_uint32)]
+                ("records_held", C.c_uint32), ("rows_held", C.c_uint32), ("pending", C.c_uint32),
+                ("threads", C.c_uint32), ("batches_parallel", C.c_uint32), ("batches_serial", C.c_uint32),
+                ("batches_rolled_back", C.c_uint32)]
 
 
 class rfec_service_info(C.Structure):
@@ -261,6 +263,7 @@ _SIGS = {
                                                        C.POINTER(C.c_uint32), C.POINTER(rfec_rx_report)]),
     "rfec_rx_session_evict": (C.c_int, [_P, _P]),
     "rfec_rx_session_get_info": (C.c_int, [_P, C.POINTER(rfec_rx_session_info)]),
+    "rfec_rx_session_set_threads": (C.c_int, [_P, C.c_uint32]),
     "rfec_pinned_free": (None, [_P]),
 }
 
@@ -511,8 +514,9 @@ class Native:
         keeper.arr = arr
         return arr, keeper
 
-    def rx_session(self, stride, capacity):
-        return RxSession(self, stride, capacity)
+    def rx_session(self, stride, capacity, threads=0):
+        """threads: control-plane shards (0: the library's default, RFEC_RX_THREADS or 8; 1: serial)."""
+        return RxSession(self, stride, capacity, threads)
 
     # -- batched UDP I/O (host memory) -------------------------------------------
     def udp_open(self, ip="127.0.0.1", port=0, flags=RFEC_UDP_SERVER, buf_bytes=0):
@@ -588,11 +592,13 @@ class _Pinned:
 class RxSession:
     """rfec_rx_session: receiver-side FEC state kept across batches."""
 
-    def __init__(self, native: Native, stride: int, capacity: int):
+    def __init__(self, native: Native, stride: int, capacity: int, threads: int = 0):
         self.n, self.stride = native, stride
         self.h = native.lib.rfec_rx_session_create(stride, capacity)
         if not self.h:
             raise RfecError(f"rfec_rx_session_create failed: {native.last_error()}")
+        if threads:
+            native._check(native.lib.rfec_rx_session_set_threads(self.h, threads), "rfec_rx_session_set_threads")
 
     def push(self, n, recs, payload, max_out=1 << 16, stream=None):
         """recs / payload: DEVICE addresses.  Returns (segments, payload rows, report)."""

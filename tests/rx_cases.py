@@ -205,3 +205,76 @@ def single_group_stream(oracle, k, pf, erase, tamper=None, seed=0, video_size=10
         recs.append(r)
         rows.append(p)
     return np.array(recs, po.WIRE_REC), np.array(rows, np.uint8)
+
+
+C3_LINES = [(0, 1, 4, 0), (4, 1, 4, 1), (8, 1, 2, 2), (0, 4, 3, 0x80), (1, 4, 3, 0x81), (2, 4, 2, 0x82),
+            (3, 4, 2, 0x83)]  # the sender's 3 x 4 plan at k = 10: rows, then columns (first, stride, count, index)
+
+
+def c3_groups(G, k=10, cap=16):
+    """Parsed-datagram records of G groups of the sender's 3 x 4 plan, in
+    order: segments [G][k] (packet ids 1 + g k + i, timestamp 33 g, data_size
+    cap) and parities [G][7] (send_ts 33 g, meta = XOR of the members'
+    headers).  Headers only: for the control plane (tests/test_rx_shards.py,
+    tools/rx_host_bench.py)."""
+    from razor_amd.fec import RFEC_WIRE_FEC, RFEC_WIRE_SEG, WIRE_REC_DTYPE
+    seg = np.zeros((G, k), WIRE_REC_DTYPE)
+    seg["mid"], seg["ver"], seg["remb"] = RFEC_WIRE_SEG, 1, 0xFF
+    g = np.arange(G)[:, None]
+    i = np.arange(k)[None, :]
+    seg["hdr"]["seq"] = 1 + g * k + i
+    seg["hdr"]["fid"] = 1 + g
+    seg["hdr"]["ts"] = 33 * g
+    seg["hdr"]["index"] = i
+    seg["hdr"]["total"] = k
+    seg["hdr"]["payload_type"] = 96
+    seg["hdr"]["size"] = cap
+    seg["data_size"] = cap
+    seg["fec_id"] = (np.arange(G)[:, None] % 65535 + 1) * np.ones((1, k), np.int64)
+    fec = np.zeros((G, len(C3_LINES)), WIRE_REC_DTYPE)
+    fec["mid"], fec["ver"] = RFEC_WIRE_FEC, 1
+    fec["fec_id"] = seg["fec_id"][:, :1]
+    fec["base_id"] = seg["hdr"]["seq"][:, :1]
+    fec["count"], fec["row"], fec["col"] = k, 3, 4
+    fec["send_ts"] = 33 * g
+    fec["data_size"] = cap
+    c3_metas(seg, fec)
+    return seg, fec
+
+
+def c3_metas(seg, fec):
+    """fec[:, l].hdr = XOR of line l's members' headers (flex_fec_xor.c:13-44)."""
+    from razor_amd.fec import HDR_DTYPE
+    G, k = seg.shape
+    hv = seg["hdr"].copy().view(np.uint32).reshape(G, k, 5)
+    for l, (first, stride, cnt, idx) in enumerate(C3_LINES):
+        x = np.bitwise_xor.reduce(hv[:, first:first + stride * cnt:stride], axis=1)
+        fec["hdr"][:, l] = x.view(HDR_DTYPE).reshape(G)
+        fec["index"][:, l] = idx
+
+
+def c3_shuffle(seg, fec, loss, window, seed=1, dup=0.02):
+    """The arrival order: each group's parities after its last segment,
+    independent loss, reordering within `window` arrivals, `dup` duplicates
+    (arriving up to 3 windows late)."""
+    rng = np.random.default_rng(seed)
+    G, k = seg.shape
+    nl = fec.shape[1]
+    g = np.arange(G)[:, None]
+    recs = np.concatenate([seg, fec], axis=1).reshape(-1)
+    pos = (np.concatenate([np.broadcast_to(np.arange(k, dtype=np.float64), (G, k)),
+                           np.broadcast_to(k - 1 + (np.arange(nl) + 1) / (nl + 1), (G, nl))], axis=1)
+           + g * (k + 1)).reshape(-1)
+    keep = rng.random(len(recs)) >= loss
+    recs, pos = recs[keep], pos[keep]
+    d = rng.random(len(recs)) < dup
+    key = np.concatenate([pos + rng.integers(0, window, len(pos)),
+                          pos[d] + rng.integers(window, 3 * window, int(d.sum()))])
+    recs = np.concatenate([recs, recs[d]])
+    return recs[np.argsort(key, kind="stable")]
+
+
+def c3_records(G, loss, window, seed=1, k=10, cap=16):
+    """c3_groups shuffled by c3_shuffle: a lossy, reordered c3 stream with duplicates."""
+    seg, fec = c3_groups(G, k, cap)
+    return c3_shuffle(seg, fec, loss, window, seed)

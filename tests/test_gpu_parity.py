@@ -592,7 +592,7 @@ def test_host_zero_copy_1000_struct_bounds(product, oracle1000):
     for i in range(G * k):
         sraw[i * sstep:i * sstep + ssz] = aos[i:i + 1].view(np.uint8)
     fraw, kf, fp, fstep, fsz = _gapped(lib, G * n, fdt, 16, 0xA5, CAN)
-    t = lib.host_encode_groups(plan, G, sp, fp, fec_id0=7)
+    t = lib.host_encode_groups(plan, G, sp, fp, fec_id0=1)
     assert t["zero_copy"] == 1
     assert _gaps_intact(fraw, G * n, fstep, fsz, CAN)
     assert _gaps_intact(sraw, G * k, sstep, ssz, CAN)
