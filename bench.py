@@ -59,7 +59,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 from razor_amd.dist import StepWindow, device_identity, gather_objects, shard_groups  # noqa: E402
-from razor_amd.fec import HDR_DTYPE, Native, native  # noqa: E402
+from razor_amd.fec import FEC_STAMP_DTYPE, HDR_DTYPE, SEG_STAMP_DTYPE, Native, native  # noqa: E402
 
 METRIC = "FEC encode+decode GiB/s (device-resident), 1200B pkts k=10/r=3; % HBM peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -96,6 +96,44 @@ def make_headers(G, k, S, group0):
     hdr["ftype"] = (gi % 60 == 0)
     hdr["size"] = S
     return hdr
+
+
+WIRE_DSTRIDE = 1280  # datagram slots of 10 x 128 B: whole-line stores
+WIRE_GOLDEN = ROOT / "tests" / "golden" / "wire_c3_digest.json"
+
+
+def wire_stamps(hdr, plan, n):
+    """The sender's fields around the FEC of the c3 workload's datagrams
+    (sim_sender.c:103-122 / sim_proto.inl:83-307): parities get uid, fec_id
+    (+1 per group, 0 skipped), base_id, count, row, col, index, send_ts and a
+    running transport_seq; segments uid, fec_id, send_ts, transport_seq."""
+    G, k = hdr.shape
+    fid = (np.arange(G) % 65535 + 1).astype(np.uint16)
+    f = np.zeros((G, n), FEC_STAMP_DTYPE)
+    f["uid"] = 0x52415A4F
+    f["fec_id"] = fid[:, None]
+    f["base_id"] = hdr["seq"][:, :1]
+    f["count"] = k
+    f["row"], f["col"] = plan.row, plan.col
+    f["index"] = [plan.line[l].index for l in range(n)]
+    f["send_ts"] = hdr["ts"][:, :1]
+    f["transport_seq"] = (np.arange(G * n) & 0xFFFF).reshape(G, n)
+    s = np.zeros((G, k), SEG_STAMP_DTYPE)
+    s["uid"] = 0x52415A4F
+    s["fec_id"] = fid[:, None]
+    s["send_ts"] = hdr["ts"] & 0xFFFF
+    s["transport_seq"] = (np.arange(G * k) & 0xFFFF).reshape(G, k)
+    s["remb"] = 0xFF
+    return f.reshape(-1), s.reshape(-1)
+
+
+def wire_digest(dg, dl):
+    """SHA-256 of datagrams (host arrays [N][dstride], lengths [N]): the
+    lengths, then each datagram's bytes in order."""
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(dl, np.uint16).tobytes())
+    h.update(dg[np.arange(dg.shape[1])[None, :] < dl.astype(np.int64)[:, None]].tobytes())
+    return h.hexdigest()
 
 
 def distinct_row_pairs(plan):
@@ -632,6 +670,93 @@ def c4_strong(lib, device, stream, dist, world, rank, pf, steps, warmup, verify)
                 False if any(f[1] == 0 for f in flags) else (True if all(f[1] == 1 for f in flags) else None))}
 
 
+def wire_sub(lib, w, device, reps=10):
+    """§8(f1) on the default line: the c3 workload's datagrams -- its 196,608
+    parities as SIM_FEC (rfec_wire_frame_fec) and 655,360 segments as SIM_SEG
+    (rfec_wire_frame_seg), into 1,280-B slots -- and both parsed back
+    (rfec_wire_parse), each kernel timed by its own start / stop events over
+    `reps` launches.  Algorithmic bytes per datagram (tools/wire_bench.py):
+    frame read payload + header + stamp, write the datagram + its length;
+    parse read datagram + length, write the 64-B record + the payload slot.
+    Checked: parse(frame(x)) = x on every datagram, and the datagrams of the
+    first 4,096 groups against the oracle's bytes for the same groups
+    (tests/golden/wire_c3_digest.json, made by oracle/gen_wire_digest.py)."""
+    G, k, n, S, P = w.G, w.k, w.n, w.S, w.stride
+    NF, NS, D = G * n, G * k, WIRE_DSTRIDE
+    st = torch.cuda.current_stream(device)
+    sp = st.cuda_stream
+    fst, sst = wire_stamps(w.hdr_np, w.plan, n)
+    d_fst = torch.from_numpy(fst.view(np.uint8).copy()).to(device)
+    d_sst = torch.from_numpy(sst.view(np.uint8).copy()).to(device)
+    dg_f = torch.empty((NF, D), dtype=torch.uint8, device=device)
+    dl_f = torch.empty((NF,), dtype=torch.int16, device=device)
+    dg_s = torch.empty((NS, D), dtype=torch.uint8, device=device)
+    dl_s = torch.empty((NS,), dtype=torch.int16, device=device)
+    rec_f = torch.empty((NF, 64), dtype=torch.uint8, device=device)
+    pay_f = torch.empty((NF, P), dtype=torch.uint8, device=device)
+    rec_s = torch.empty((NS, 64), dtype=torch.uint8, device=device)
+    pay_s = torch.empty((NS, P), dtype=torch.uint8, device=device)
+    calls = {
+        "frame_fec": lambda: lib.wire_frame_fec(NF, P, S, w.parity.data_ptr(), w.meta.data_ptr(), w.fsize.data_ptr(),
+                                                w.status.data_ptr(), d_fst.data_ptr(), D, dg_f.data_ptr(),
+                                                dl_f.data_ptr(), sp),
+        "frame_seg": lambda: lib.wire_frame_seg(NS, P, S, w.shards.data_ptr(), w.hdr.data_ptr(), d_sst.data_ptr(), D,
+                                                dg_s.data_ptr(), dl_s.data_ptr(), sp),
+        "parse_fec": lambda: lib.wire_parse(NF, D, dg_f.data_ptr(), dl_f.data_ptr(), P, S, rec_f.data_ptr(),
+                                            pay_f.data_ptr(), sp),
+        "parse_seg": lambda: lib.wire_parse(NS, D, dg_s.data_ptr(), dl_s.data_ptr(), P, S, rec_s.data_ptr(),
+                                            pay_s.data_ptr(), sp)}
+    for f in calls.values():
+        f()
+    torch.cuda.synchronize(device)
+    lf = dl_f.cpu().numpy().view(np.uint16).astype(np.int64)
+    ls = dl_s.cpu().numpy().view(np.uint16).astype(np.int64)
+    alg = {"frame_fec": int(NF * (S + 20 + 24 + 2) + lf.sum() + 2 * NF),
+           "frame_seg": int(NS * (S + 20 + 12) + ls.sum() + 2 * NS),
+           "parse_fec": int(lf.sum() + 2 * NF + NF * (64 + S)),
+           "parse_seg": int(ls.sum() + 2 * NS + NS * (64 + S))}
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps * 4)]
+    for a, b in ev:
+        a.record(st)
+        b.record(st)
+    torch.cuda.synchronize(device)
+    kern = {}
+    for i, (name, f) in enumerate(calls.items()):
+        for r in range(reps):
+            a, b = ev[i * reps + r]
+            lib.timing_events(a.cuda_event, b.cuda_event)
+            f()
+        torch.cuda.synchronize(device)
+        t = np.array([a.elapsed_time(b) * 1e-3 for a, b in ev[i * reps:(i + 1) * reps]])
+        kern[name] = {"launch_us": round(float(t.mean()) * 1e6, 2), "launch_us_median": round(float(np.median(t)) * 1e6, 2),
+                      "algorithmic_bytes": alg[name], "GBps": round(alg[name] / t.mean() / 1e9, 1),
+                      "frac": round(alg[name] / t.mean() / 1e9 / HBM_PEAK_GBPS, 4)}
+    kern["frame_fec"]["kernel"] = kern["frame_seg"]["kernel"] = "k_frame_{fec,seg}_q (quarter-wave, slice-by-16 CRC)"
+    kern["parse_fec"]["kernel"] = kern["parse_seg"]["kernel"] = "k_parse_q (quarter-wave, CRC by row)"
+    # parse(frame(x)) = x: payload bytes, zero slot tails, OK records with the input headers
+    ok = bool(torch.equal(pay_f.view(NF, P)[:, :S], w.parity.view(NF, P)[:, :S]) and
+              torch.equal(pay_s.view(NS, P)[:, :S], w.shards.view(NS, P)[:, :S]))
+    ok = ok and (S == P or not (bool(pay_f[:, S:].any()) or bool(pay_s[:, S:].any())))
+    ok = ok and bool((rec_f[:, 0] == 0).all()) and bool((rec_s[:, 0] == 0).all())
+    ok = ok and torch.equal(rec_s[:, 8:28], w.hdr.view(NS, 20)) and torch.equal(rec_f[:, 8:28], w.meta.view(NF, 20))
+    digest_ok = None
+    if WIRE_GOLDEN.exists():
+        gold = json.loads(WIRE_GOLDEN.read_text())
+        g = gold["groups"]
+        if gold["dstride"] == D and gold["payload_stride"] == P and g <= G:
+            got_f = wire_digest(dg_f[:g * n].cpu().numpy(), lf[:g * n])
+            got_s = wire_digest(dg_s[:g * k].cpu().numpy(), ls[:g * k])
+            digest_ok = got_f == gold["fec_sha256"] and got_s == gold["seg_sha256"]
+    res = {"workload": f"c3 datagrams: {NF} SIM_FEC + {NS} SIM_SEG of {S} B in {D}-B slots, parsed back",
+           "kernels": kern, "reps": reps, "timing": TIMING_OWN.split(" (")[0],
+           "verified_round_trip": ok, "verified_vs_oracle_digest": digest_ok,
+           "digest_scope": "the datagrams of groups [0, 4,096) (both kinds) = the oracle's framing of the same "
+                           "groups (pinned to the reference's datagrams at S <= 1,000: tests/golden/wire_*.bin)"}
+    del dg_f, dg_s, rec_f, rec_s, pay_f, pay_s
+    torch.cuda.empty_cache()
+    return res
+
+
 def kernel_desc(w, k, S, full_plan):
     """(encode kernel, decode kernels) the library launches for this workload
     (rfec_launch_encode / rfec_launch_recover_out dispatch, rfec_kernels.hip)."""
@@ -704,14 +829,27 @@ def config_sub(lib, name, device, stream, dist, world, rank, pf, steps, warmup, 
             ws.use_packed(True)
         _, _, t_dec_pk, _, own_pk, _ = time_steps(lib, sets, steps, warmup, stream, dist, "own", False, SUB_EVERY)
         t_pk = float(t_dec_pk.mean()) * 1e6 if own_pk else -1.0
+        # the records' producer here: rfec_pack_erasures (k_pack_rows) from the batch layout, outside the
+        # decode's time; timed the same way so the line shows what the records cost to build
+        pev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+        for a, b in pev:
+            a.record(stream)
+            b.record(stream)
+        for a, b in pev:
+            lib.timing_events(a.cuda_event, b.cuda_event)
+            w.prepare(stream.cuda_stream)
+        torch.cuda.synchronize(device)
+        t_pack = float(np.mean([a.elapsed_time(b) for a, b in pev])) * 1e3
         if verify:
             pk_ok = int(all(ws.verify() for ws in sets))
             verified = verified and bool(pk_ok)
         pk_kernels = kernel_desc(w, k, S, full_plan)[1]
         for ws in sets:
             ws.use_packed(False)
+    else:
+        t_pack = -1.0
     per_rank = torch.tensor([w.enc_bytes + w.dec_bytes, float(t_enc.mean()) * 1e6, float(t_dec.mean()) * 1e6,
-                             -1 if verified is None else int(verified), t_pk, pk_ok], dtype=torch.float64)
+                             -1 if verified is None else int(verified), t_pk, pk_ok, t_pack], dtype=torch.float64)
     rows = [per_rank]
     if dist:
         rows = [torch.zeros_like(per_rank) for _ in range(world)]
@@ -747,7 +885,12 @@ def config_sub(lib, name, device, stream, dist, world, rank, pf, steps, warmup, 
                    if float(rows[0][4]) > 0 else None,
                    "traffic": load_traffic(wn + "+packed", "decode"),
                    "launch_us_per_rank": [round(float(r[4]), 2) for r in rows],
-                   "verified": None if not verify else all(int(r[5]) == 1 for r in rows)},
+                   "verified": None if not verify else all(int(r[5]) == 1 for r in rows),
+                   "producer": {"call": "rfec_pack_erasures (kernel k_pack_rows) from the batch layout's headers, "
+                                        "masks and the encode's meta, before the timed steps (not in launch_us)",
+                                "launch_us": round(float(rows[0][6]), 2),
+                                "frac_with_pack": round(w.dec_bytes / ((float(rows[0][4]) + float(rows[0][6])) * 1e-6)
+                                                        / 1e9 / HBM_PEAK_GBPS, 4) if float(rows[0][4]) > 0 else None}},
                "encode_us_per_rank": [round(float(r[1]), 2) for r in rows],
                "decode_us_per_rank": [round(float(r[2]), 2) for r in rows],
                "timing": "per launch: " + (TIMING_OWN if own_enc and own_dec else TIMING_BRACKET),
@@ -792,6 +935,7 @@ def main():
                     help="decode the set encoded in the same step (its parity still MALL-resident)")
     ap.add_argument("--c4-steps", type=int, default=10,
                     help="timed steps of the c4_strong sub-object (config c3 only; 0 = skip it)")
+    ap.add_argument("--no-wire", action="store_true", help="skip the wire sub-object (§8(f1) kernels)")
     ap.add_argument("--sub-steps", type=int, default=80,
                     help="timed steps of the c5 / c3full sub-objects (config c3 only; 0 = skip them)")
     args = ap.parse_args()
@@ -1005,6 +1149,11 @@ def main():
             "verified_vs_reference_digest": digest_ok,
             "tuning": args.tuning,
         }
+        if cfg_name == "c3" and not args.no_wire and not args.lib:
+            log("wire ...")
+            res["wire"] = wire_sub(lib, w, device)
+            if res["wire"]["verified_round_trip"] is False or res["wire"]["verified_vs_oracle_digest"] is False:
+                verified = res["verified"] = False
         if c4 is not None:
             res["c4_strong"] = c4
         for sub, d in subs.items():

@@ -95,7 +95,8 @@ int rfec_sim_video_size(void);
  * header checks rfec_abi_version() == RFEC_ABI_VERSION before using structs
  * whose size changed.  History: 5 -- rfec_host_timing grew from 48 to 56
  * bytes (zero_copy, reserved); 6 -- rfec_abi_version, rfec_rx_session_info grew
- * from 24 to 40 bytes (threads, batches_*), rfec_rx_session_set_threads. */
+ * from 24 to 88 bytes (threads, batches_*, the host time split),
+ * rfec_rx_session_set_threads. */
 #define RFEC_ABI_VERSION 6
 uint32_t rfec_abi_version(void);
 
@@ -656,6 +657,13 @@ typedef struct {
     uint32_t batches_parallel;    /* batches replayed by the shards in parallel */
     uint32_t batches_serial;      /* batches replayed in arrival order */
     uint32_t batches_rolled_back; /* parallel replays undone (then replayed in order) */
+    uint32_t reserved;
+    /* host time, microseconds, summed over the session's batches: */
+    double split_us;   /* the batch split over the shards (serial) */
+    double replay_us;  /* the control plane's replay (the shards in parallel, or in order) */
+    double verify_us;  /* the packet-id ownership check (parallel) */
+    double tables_us;  /* the device tables of the delivering groups (rx_device, host part) */
+    double compact_us; /* record / row compaction (rfec_rx_session_evict, and when the arena fills) */
 } rfec_rx_session_info;
 
 /* NULL on bad arguments (stride % 16, capacity > stride) or no memory.

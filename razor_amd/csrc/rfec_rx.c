@@ -112,6 +112,152 @@ static void hm_del(hmap* m, uint32_t k) /* backward-shift deletion */
         }
 }
 
+/* Packet-id maps (first-arrival dedupe, the segment cache, fec_id -> flex,
+ * packet-id ownership): u32 key -> u32 value (0 = absent) in a radix table,
+ * 14 + 10 + 8 key bits: a directory of mids, a mid of leaves, a leaf of 256
+ * values, allocated on first use and freed when empty.  Ids arrive nearly in
+ * sequence, so consecutive lookups hit one leaf (the last one is cached): no
+ * hashing, no probing, no rehash, and the key order is the walk order (the
+ * evictions' sorted walks).  (An open-addressing hash spent 35-70 % of the
+ * control plane in probes that missed the cache, and its growth in page
+ * faults.) */
+#define PM_LEAF_BITS 8
+#define PM_MID_BITS 10
+#define PM_DIR_BITS (32 - PM_LEAF_BITS - PM_MID_BITS)
+#define PM_LEAF (1u << PM_LEAF_BITS)
+#define PM_MID (1u << PM_MID_BITS)
+typedef struct {
+    uint32_t n;
+    uint32_t v[PM_LEAF];
+} pm_leaf;
+typedef struct {
+    pm_leaf* leaf[PM_MID];
+    uint32_t nleaf;
+} pm_mid;
+typedef struct {
+    pm_mid** dir; /* [1 << PM_DIR_BITS] */
+    uint32_t n;   /* entries */
+    uint32_t last_pg;
+    pm_leaf* last; /* the leaf of page last_pg (key >> PM_LEAF_BITS), or NULL */
+} pmap;
+
+static int pm_init(pmap* m)
+{
+    memset(m, 0, sizeof(*m));
+    m->dir = (pm_mid**)calloc((size_t)1 << PM_DIR_BITS, sizeof(pm_mid*));
+    return m->dir ? 0 : -1;
+}
+
+static void pm_free(pmap* m)
+{
+    if (m->dir)
+        for (uint32_t d = 0; d < (1u << PM_DIR_BITS); ++d)
+            if (m->dir[d]) {
+                for (uint32_t l = 0; l < PM_MID; ++l)
+                    free(m->dir[d]->leaf[l]);
+                free(m->dir[d]);
+            }
+    free(m->dir);
+    memset(m, 0, sizeof(*m));
+}
+
+static pm_leaf* pm_find(pmap* m, uint32_t k)
+{
+    const uint32_t pg = k >> PM_LEAF_BITS;
+    if (m->last && m->last_pg == pg)
+        return m->last;
+    const pm_mid* d = m->dir[pg >> PM_MID_BITS];
+    pm_leaf* f = d ? d->leaf[pg & (PM_MID - 1)] : NULL;
+    if (f) {
+        m->last = f;
+        m->last_pg = pg;
+    }
+    return f;
+}
+
+static uint32_t pm_get(pmap* m, uint32_t k)
+{
+    const pm_leaf* f = pm_find(m, k);
+    return f ? f->v[k & (PM_LEAF - 1)] : 0u;
+}
+
+static int pm_put(pmap* m, uint32_t k, uint32_t v) /* v != 0 */
+{
+    pm_leaf* f = pm_find(m, k);
+    if (!f) {
+        const uint32_t pg = k >> PM_LEAF_BITS;
+        pm_mid** d = &m->dir[pg >> PM_MID_BITS];
+        if (!*d && !(*d = (pm_mid*)calloc(1, sizeof(pm_mid))))
+            return -1;
+        if (!(f = (pm_leaf*)calloc(1, sizeof(pm_leaf))))
+            return -1;
+        (*d)->leaf[pg & (PM_MID - 1)] = f;
+        (*d)->nleaf++;
+        m->last = f;
+        m->last_pg = pg;
+    }
+    uint32_t* s = &f->v[k & (PM_LEAF - 1)];
+    f->n += *s == 0;
+    m->n += *s == 0;
+    *s = v;
+    return 0;
+}
+
+static void pm_del(pmap* m, uint32_t k)
+{
+    pm_leaf* f = pm_find(m, k);
+    uint32_t* s = f ? &f->v[k & (PM_LEAF - 1)] : NULL;
+    if (!s || !*s)
+        return;
+    *s = 0;
+    m->n--;
+    if (--f->n == 0) { /* the leaf (and an empty mid) go */
+        const uint32_t pg = k >> PM_LEAF_BITS;
+        pm_mid** d = &m->dir[pg >> PM_MID_BITS];
+        (*d)->leaf[pg & (PM_MID - 1)] = NULL;
+        free(f);
+        if (--(*d)->nleaf == 0) {
+            free(*d);
+            *d = NULL;
+        }
+        m->last = NULL;
+    }
+}
+
+/* In key order: the next entry at or after *key (its value's address, the key
+ * in *key), NULL past the last.  Start with *key = 0; continue from key + 1. */
+static uint32_t* pm_next(const pmap* m, uint32_t* key, uint32_t* done)
+{
+    uint64_t k = *key;
+    while (k < (1ull << 32)) {
+        const uint32_t pg = (uint32_t)(k >> PM_LEAF_BITS);
+        const pm_mid* d = m->dir[pg >> PM_MID_BITS];
+        if (!d) {
+            k = ((uint64_t)(pg >> PM_MID_BITS) + 1) << (PM_MID_BITS + PM_LEAF_BITS);
+            continue;
+        }
+        pm_leaf* f = d->leaf[pg & (PM_MID - 1)];
+        if (!f) {
+            k = ((uint64_t)pg + 1) << PM_LEAF_BITS;
+            continue;
+        }
+        for (uint32_t i = (uint32_t)k & (PM_LEAF - 1); i < PM_LEAF; ++i)
+            if (f->v[i]) {
+                *key = (pg << PM_LEAF_BITS) | i;
+                return &f->v[i];
+            }
+        k = ((uint64_t)pg + 1) << PM_LEAF_BITS;
+    }
+    *done = 1;
+    return NULL;
+}
+/* for (PM_EACH(m, key, val)) { ... *val ... } -- entries in key order; the body
+ * may change *val (not to 0) but not insert or delete */
+#define PM_EACH(m, key, val)                                                                        \
+    uint32_t key = 0, *val = NULL, pm_d_ = 0;                                                       \
+    !pm_d_ && (val = pm_next((m), &key, &pm_d_)) != NULL;                                           \
+    key = key == UINT32_MAX ? (pm_d_ = 1, key) : key + 1
+
 typedef struct {
     uint32_t count, row, col, n_groups, n_lines, row0, prow0, group0;
     uint32_t huge;        /* count > RX_MAX_COUNT or more than RFEC_MAX_LINES lines: no plan; line l = FEC
@@ -187,7 +333,8 @@ typedef struct {
 typedef struct {
     const rfec_wire_rec* R;
     uint32_t capacity, max_ts, dropped, unmodelled;
-    hmap seen, cache, flex_of, shape_of;
+    pmap seen, cache, flex_of; /* packet id -> 1; packet id -> record + 1 | 0x80000000 + rh index; fec_id -> instance + 1 */
+    hmap shape_of;
     rx_inst* G;
     uint32_t ng, gcap;
     rx_shape* S;
@@ -242,9 +389,13 @@ typedef struct {
 #define RX_GROW(ptr, n, cap, need, T) RX_GROW_F(X->oom, ptr, n, cap, need, T)
 
 /* -- the journal (sharded sessions) ------------------------------------------ */
-static hmap* rx_map(rx_sim* X, int m)
+static pmap* rx_map(rx_sim* X, int m) /* 0 seen, 1 cache, 2 flex_of (3: shape_of, a hash map) */
 {
-    return m == 0 ? &X->seen : m == 1 ? &X->cache : m == 2 ? &X->flex_of : &X->shape_of;
+    return m == 0 ? &X->seen : m == 1 ? &X->cache : &X->flex_of;
+}
+static uint32_t rx_get(rx_sim* X, int m, uint32_t k)
+{
+    return m == 3 ? hm_get(&X->shape_of, k) : pm_get(rx_map(X, m), k);
 }
 
 static void rx_jlog(rx_sim* X, int m, uint32_t k, uint32_t old)
@@ -255,22 +406,25 @@ static void rx_jlog(rx_sim* X, int m, uint32_t k, uint32_t old)
     X->jops[X->njops++] = (rx_jop){(uint8_t)m, k, old};
 }
 
-/* hm_put / hm_del on one of X's maps, journaled while a batch may roll back */
+/* put / delete on one of X's maps, journaled while a batch may roll back */
 static int rx_put(rx_sim* X, int m, uint32_t k, uint32_t v)
 {
     if (X->jon)
-        rx_jlog(X, m, k, hm_get(rx_map(X, m), k));
-    return hm_put(rx_map(X, m), k, v);
+        rx_jlog(X, m, k, rx_get(X, m, k));
+    return m == 3 ? hm_put(&X->shape_of, k, v) : pm_put(rx_map(X, m), k, v);
 }
 static void rx_del(rx_sim* X, int m, uint32_t k)
 {
     if (X->jon) {
-        const uint32_t o = hm_get(rx_map(X, m), k);
+        const uint32_t o = rx_get(X, m, k);
         if (!o)
             return;
         rx_jlog(X, m, k, o);
     }
-    hm_del(rx_map(X, m), k);
+    if (m == 3)
+        hm_del(&X->shape_of, k);
+    else
+        pm_del(rx_map(X, m), k);
 }
 
 /* Saves instance ii (and its slot / line tables) the first time this batch
@@ -340,10 +494,12 @@ static void rx_rollback(rx_sim* X)
     for (uint32_t q = X->njops; q-- > 0;) {
         const rx_jop* o = &X->jops[q];
         if (o->old) {
-            if (hm_put(rx_map(X, o->map), o->key, o->old))
+            if (o->map == 3 ? hm_put(&X->shape_of, o->key, o->old) : pm_put(rx_map(X, o->map), o->key, o->old))
                 X->oom = 1;
+        } else if (o->map == 3) {
+            hm_del(&X->shape_of, o->key);
         } else {
-            hm_del(rx_map(X, o->map), o->key);
+            pm_del(rx_map(X, o->map), o->key);
         }
     }
     for (size_t off = 0; off < X->njsave;) {
@@ -572,14 +728,14 @@ static void rx_remove(rx_sim* X, uint32_t ii) /* sim_fec_evict_segment + flex re
 /* sim_fec_put_segment (sim_fec.c:171-207); cache values: record + 1, or 0x80000000 | index into X->rh */
 static void rx_put_segment(rx_sim* X, const rfec_hdr* h, uint16_t fec_id, uint32_t cval, int32_t src)
 {
-    if (h->seq == 0 || hm_get(&X->cache, h->seq))
+    if (h->seq == 0 || pm_get(&X->cache, h->seq))
         return;
     X->max_ts = h->ts > X->max_ts ? h->ts : X->max_ts;
     if (rx_put(X, 1, h->seq, cval)) {
         X->oom = 1;
         return;
     }
-    const uint32_t fi = hm_get(&X->flex_of, fec_id);
+    const uint32_t fi = pm_get(&X->flex_of, fec_id);
     if (!fi)
         return;
     rx_on_segment(X, fi - 1, h, src, 1);
@@ -721,7 +877,7 @@ static void rx_put_fec(rx_sim* X, uint32_t a)
         X->dropped++;
         return;
     }
-    uint32_t fi = hm_get(&X->flex_of, f->fec_id);
+    uint32_t fi = pm_get(&X->flex_of, f->fec_id);
     if (!fi) { /* flex_fec_receiver_active (flex_fec_receiver.c:69-88) */
         RX_GROW(X->G, X->ng, X->gcap, 1, rx_inst);
         if (X->oom)
@@ -763,7 +919,7 @@ static void rx_put_fec(rx_sim* X, uint32_t a)
             return;
         }
         for (uint32_t i = 0; i < g->count && g->shape != UINT32_MAX; ++i) { /* sim_fec_add_segment_to_flex */
-            const uint32_t c = hm_get(&X->cache, g->base + i);
+            const uint32_t c = pm_get(&X->cache, g->base + i);
             if (!c)
                 continue;
             if (c & 0x80000000u) {
@@ -826,7 +982,7 @@ static void rx_drain(rx_sim* X, uint32_t a)
                 b = i;
         const rx_event e = X->pend[b];
         X->pend[b] = X->pend[--X->npend];
-        if (hm_get(&X->seen, e.hdr.seq))
+        if (pm_get(&X->seen, e.hdr.seq))
             continue;
         if (X->P) {
             const rx_inst* g = &X->G[e.inst];
@@ -854,9 +1010,9 @@ static void rx_drain(rx_sim* X, uint32_t a)
 
 static void rx_sim_free(rx_sim* X)
 {
-    hm_free(&X->seen);
-    hm_free(&X->cache);
-    hm_free(&X->flex_of);
+    pm_free(&X->seen);
+    pm_free(&X->cache);
+    pm_free(&X->flex_of);
     hm_free(&X->shape_of);
     free(X->G);
     free(X->S);
@@ -873,60 +1029,36 @@ static void rx_sim_free(rx_sim* X)
     free(X->claimed);
 }
 
-static int cmp_u32(const void* a, const void* b)
-{
-    const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
-    return x < y ? -1 : x > y;
-}
-
-/* keys of a map, ascending (the skiplists' iteration order); NULL on OOM */
-static uint32_t* hm_sorted_keys(const hmap* m, uint32_t* n)
-{
-    uint32_t* k = (uint32_t*)malloc(((size_t)m->n + 1) * sizeof(uint32_t));
-    *n = 0;
-    if (!k)
-        return NULL;
-    for (uint32_t i = 0; i <= m->mask; ++i)
-        if (m->v[i])
-            k[(*n)++] = m->k[i];
-    qsort(k, *n, sizeof(uint32_t), cmp_u32);
-    return k;
-}
-
 /* sim_fec_evict (sim_fec.c:209-241) past its 300 ms wall-clock gate: flexes in
  * fec_id order while stale (fec_ts + 3000 <= max_ts) or full, removed with
  * their members' cache entries; then cached segments in packet_id order while
  * older than 6 s (timestamp + 6000 < max_ts).  Both walks stop at the first
- * entry that stays, as the skiplist walks do. */
+ * entry that stays, as the skiplist walks do (pmap: key order; each step
+ * looks up the next key afresh, so removals are safe). */
 static void rx_evict(rx_sim* X)
 {
-    uint32_t n = 0;
-    uint32_t* k = hm_sorted_keys(&X->flex_of, &n);
-    if (!k) {
-        X->oom = 1;
-        return;
-    }
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t fi = hm_get(&X->flex_of, k[i]) - 1;
+    uint32_t key = 0, done = 0;
+    for (uint32_t* v; (v = pm_next(&X->flex_of, &key, &done)) != NULL;) {
+        const uint32_t fi = *v - 1;
         const rx_inst* g = &X->G[fi];
         if (!(g->fec_ts + 3000u <= X->max_ts || g->nsegs >= g->count))
             break;
         rx_remove(X, fi);
+        if (key == UINT32_MAX)
+            break;
+        ++key;
     }
-    free(k);
-    k = hm_sorted_keys(&X->cache, &n);
-    if (!k) {
-        X->oom = 1;
-        return;
-    }
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t c = hm_get(&X->cache, k[i]);
+    key = done = 0;
+    for (uint32_t* v; (v = pm_next(&X->cache, &key, &done)) != NULL;) {
+        const uint32_t c = *v;
         const uint32_t ts = (c & 0x80000000u) ? X->rh[c & 0x7FFFFFFFu].ts : X->R[c - 1].hdr.ts;
         if (!(ts + 6000u < X->max_ts))
             break;
-        hm_del(&X->cache, k[i]);
+        pm_del(&X->cache, key);
+        if (key == UINT32_MAX)
+            break;
+        ++key;
     }
-    free(k);
 }
 
 static int cmp_event(const void* a, const void* b)
@@ -1002,7 +1134,8 @@ static int rx_reserve(size_t host_bytes, size_t dev_bytes, size_t keep)
 
 static int rx_tables_init(rx_sim* X, uint32_t n)
 {
-    return hm_init(&X->seen, n) || hm_init(&X->cache, n) || hm_init(&X->flex_of, 1024) || hm_init(&X->shape_of, 64);
+    (void)n;
+    return pm_init(&X->seen) || pm_init(&X->cache) || pm_init(&X->flex_of) || hm_init(&X->shape_of, 64);
 }
 
 /* One record of X->R in arrival order: sim_receiver_put /
@@ -1016,7 +1149,7 @@ static void rx_arrival(rx_sim* X, uint32_t a)
     if (r->mid == RFEC_WIRE_SEG) { /* sim_receiver_put (sim_receiver.c:811-827) */
         if (X->P) /* (a segment outside FEC claims its id for fec_id 0) */
             rx_claim(X, r->hdr.seq, (uint32_t)r->fec_id + 1u);
-        if (hm_get(&X->seen, r->hdr.seq))
+        if (pm_get(&X->seen, r->hdr.seq))
             return;
         if (rx_put(X, 0, r->hdr.seq, 1)) {
             X->oom = 1;
@@ -1702,7 +1835,8 @@ struct rx_pool {
     void* arg;
 };
 
-#define RX_SPIN_US 200.0 /* a worker or the caller spins this long before sleeping */
+#define RX_SPIN_US 2000.0 /* a worker spins this long before sleeping: batches come back to back, and a
+                             condition-variable wake costs ~10-50 us */
 
 static void cpu_relax(void)
 {
@@ -1797,7 +1931,7 @@ struct rfec_rx_session {
     uint32_t max_ts;            /* sim_receiver_fec_t.max_ts, over the shards */
     rx_pool pool;
     int pool_on;
-    hmap vown[RX_MAX_THREADS];  /* sharded: packet id -> fec_id + 1, partition (seq >> 8) % T */
+    pmap vown[RX_MAX_THREADS];  /* sharded: packet id -> fec_id + 1, partition (seq >> 8) % T */
     int vown_on;
     rx_par par;
     uint8_t* pshard;            /* per batch record: its shard (0xFF: no control-plane effect) */
@@ -1805,7 +1939,9 @@ struct rfec_rx_session {
     uint32_t* smin;
     uint32_t lcap;
     uint32_t loff[RX_MAX_THREADS + 1];
+    uint8_t shard_of[65536];    /* fec_id % T (no division per record) */
     uint32_t n_parallel, n_serial, n_rollback; /* batches by replay (rfec_rx_session_info) */
+    double t_split, t_replay, t_verify, t_tables, t_compact; /* host time split (rfec_rx_session_info) */
     rx_dev dev;
     rfec_wire_rec* store; /* every shard's R */
     uint32_t nstore, storecap;
@@ -1818,6 +1954,18 @@ struct rfec_rx_session {
     uint32_t pend_n; /* rows of the pending batch (arena rows [nstore, nstore + pend_n)) */
     int pend;        /* its stage, -1: none */
 };
+
+/* a shard's state on cache lines of its own: the replay threads write their
+ * shard's counters on every record (two shards on one line ping-pong it) */
+static rx_sim* rx_sim_alloc(void)
+{
+    const size_t sz = (sizeof(rx_sim) + 127) & ~(size_t)127;
+    void* p = NULL;
+    if (posix_memalign(&p, 128, sz))
+        return NULL;
+    memset(p, 0, sz);
+    return (rx_sim*)p;
+}
 
 static void rx_shards_free(rfec_rx_session* S)
 {
@@ -1838,8 +1986,10 @@ static int rx_shards_init(rfec_rx_session* S, uint32_t T)
     }
     rx_shards_free(S);
     S->T = T;
+    for (uint32_t f = 0; f < 65536; ++f)
+        S->shard_of[f] = (uint8_t)(f % T);
     for (uint32_t t = 0; t < T; ++t) {
-        rx_sim* X = (rx_sim*)calloc(1, sizeof(rx_sim));
+        rx_sim* X = rx_sim_alloc();
         S->XS[t] = X;
         if (!X || rx_tables_init(X, 1024))
             return -1;
@@ -1919,7 +2069,7 @@ void rfec_rx_session_destroy(rfec_rx_session* s)
     rx_dev_free(&s->dev);
     if (s->vown_on)
         for (uint32_t t = 0; t < s->T; ++t)
-            hm_free(&s->vown[t]);
+            pm_free(&s->vown[t]);
     free(s->pshard);
     free(s->lst);
     free(s->smin);
@@ -1938,15 +2088,13 @@ static int rx_merge(rfec_rx_session* S)
     const uint32_t T = S->T;
     if (T == 1)
         return RFEC_OK;
-    rx_sim* M = (rx_sim*)calloc(1, sizeof(rx_sim));
-    uint32_t ng = 0, nslot = 0, nline = 0, ns = 0, nrh = 0, nseen = 0, ncache = 0;
+    rx_sim* M = rx_sim_alloc();
+    uint32_t ng = 0, nslot = 0, nline = 0, ns = 0, nrh = 0;
     for (uint32_t t = 0; t < T; ++t) {
         const rx_sim* X = S->XS[t];
         ng += X->ng, nslot += X->nslot, nline += X->nline, ns += X->ns, nrh += X->nrh;
-        nseen += X->seen.n, ncache += X->cache.n;
     }
-    if (!M || hm_init(&M->seen, nseen) || hm_init(&M->cache, ncache) || hm_init(&M->flex_of, 1024) ||
-        hm_init(&M->shape_of, 64))
+    if (!M || rx_tables_init(M, 0))
         goto oom;
     M->R = S->store;
     M->capacity = S->capacity;
@@ -1985,21 +2133,19 @@ static int rx_merge(rfec_rx_session* S)
         memcpy(M->line_par + oline, X->line_par, (size_t)X->nline * sizeof(int32_t));
         memcpy(M->rh + orh, X->rh, (size_t)X->nrh * sizeof(rfec_hdr));
         M->nslot += X->nslot, M->nline += X->nline, M->nrh += X->nrh;
-        for (uint32_t i = 0; i <= X->seen.mask; ++i)
-            if (X->seen.v[i] && hm_put(&M->seen, X->seen.k[i], X->seen.v[i]))
+        for (PM_EACH(&X->seen, k, v))
+            if (pm_put(&M->seen, k, *v))
                 goto oom;
-        for (uint32_t i = 0; i <= X->cache.mask; ++i) {
-            const uint32_t c = X->cache.v[i];
-            if (c && hm_put(&M->cache, X->cache.k[i], (c & 0x80000000u) ? (0x80000000u | ((c & 0x7FFFFFFFu) + orh)) : c))
+        for (PM_EACH(&X->cache, k, v))
+            if (pm_put(&M->cache, k, (*v & 0x80000000u) ? (0x80000000u | ((*v & 0x7FFFFFFFu) + orh)) : *v))
                 goto oom;
-        }
-        for (uint32_t i = 0; i <= X->flex_of.mask; ++i)
-            if (X->flex_of.v[i] && hm_put(&M->flex_of, X->flex_of.k[i], X->flex_of.v[i] + og))
+        for (PM_EACH(&X->flex_of, k, v))
+            if (pm_put(&M->flex_of, k, *v + og))
                 goto oom;
     }
     if (S->vown_on)
         for (uint32_t t = 0; t < T; ++t)
-            hm_free(&S->vown[t]);
+            pm_free(&S->vown[t]);
     S->vown_on = 0;
     rx_shards_free(S);
     if (S->pool_on) {
@@ -2046,11 +2192,11 @@ static int rx_phase0(rfec_rx_session* S, uint32_t a0, uint32_t n, int* risky)
         const rfec_wire_rec* r = &R[p];
         uint32_t t = 0xFF;
         if (r->status == RFEC_WIRE_OK && r->mid == RFEC_WIRE_SEG) {
-            t = r->fec_id ? r->fec_id % T : r->hdr.seq % T;
+            t = r->fec_id ? S->shard_of[r->fec_id] : r->hdr.seq % T;
             if (r->fec_id && r->hdr.seq && r->hdr.ts > pm) /* (an upper bound of what raises max_ts) */
                 pm = r->hdr.ts;
         } else if (r->status == RFEC_WIRE_OK && r->mid == RFEC_WIRE_FEC) {
-            t = r->fec_id % T;
+            t = S->shard_of[r->fec_id];
             if (r->send_ts + 3000u < pm) /* sim_fec.c:148 could drop it */
                 rk = 1;
         }
@@ -2098,15 +2244,15 @@ static void rx_shard_job(void* arg, uint32_t t)
 static void rx_verify_job(void* arg, uint32_t j)
 {
     rfec_rx_session* S = (rfec_rx_session*)arg;
-    hmap* V = &S->vown[j];
+    pmap* V = &S->vown[j];
     const uint32_t T = S->T;
     for (uint32_t u = 0; u < T; ++u) {
         const rx_sim* X = S->XS[u];
         for (uint32_t q = X->coff[j]; q < X->coff[j + 1]; ++q) {
             const uint32_t seq = (uint32_t)(X->cpart[q] >> 32), code = (uint32_t)X->cpart[q];
-            const uint32_t v = hm_get(V, seq);
+            const uint32_t v = pm_get(V, seq);
             if (!v) {
-                if (hm_put(V, seq, code))
+                if (pm_put(V, seq, code))
                     __atomic_fetch_or(&S->par.conflict, RX_CONFLICT_OWNER, __ATOMIC_RELAXED); /* (no memory: serial) */
             } else if (v != code) {
                 __atomic_fetch_or(&S->par.conflict, RX_CONFLICT_OWNER, __ATOMIC_RELAXED);
@@ -2154,7 +2300,7 @@ static int rx_ingest(rfec_rx_session* S, uint32_t a0, uint32_t n)
     if (S->T > 1) {
         if (!S->vown_on) {
             for (uint32_t t = 0; t < S->T; ++t)
-                if (hm_init(&S->vown[t], 4096))
+                if (pm_init(&S->vown[t]))
                     return set_err(RFEC_ENOMEM, "rx session: packet ids", 0);
             S->vown_on = 1;
         }
@@ -2164,9 +2310,12 @@ static int rx_ingest(rfec_rx_session* S, uint32_t a0, uint32_t n)
                 return set_err(RFEC_ENOMEM, "rx session: claims", 0);
             X->nclaims = 0;
         }
+        const double ts = now_us();
         if ((rc = rx_phase0(S, a0, n, &risky)))
             return rc;
+        S->t_split += now_us() - ts;
     }
+    const double tr = now_us();
     if (S->T == 1) {
         rx_sim* X = S->XS[0];
         X->P = NULL;
@@ -2176,6 +2325,7 @@ static int rx_ingest(rfec_rx_session* S, uint32_t a0, uint32_t n)
         rx_run(X, a0, n);
         S->max_ts = X->max_ts;
         S->n_serial++;
+        S->t_replay += now_us() - tr;
         return X->oom ? set_err(RFEC_ENOMEM, "rx session: host tables", 0) : RFEC_OK;
     }
     rx_par* P = &S->par;
@@ -2195,8 +2345,11 @@ static int rx_ingest(rfec_rx_session* S, uint32_t a0, uint32_t n)
     else
         rx_serial_over_shards(S, a0, n);
     int c = __atomic_load_n(&P->conflict, __ATOMIC_RELAXED);
+    S->t_replay += now_us() - tr;
     if (!c && !rx_any_oom(S)) {
+        const double tv = now_us();
         pool_run(&S->pool, rx_verify_job, S); /* every packet id under one fec_id? */
+        S->t_verify += now_us() - tv;
         c = __atomic_load_n(&P->conflict, __ATOMIC_RELAXED);
         if (!c)
             ++*(risky ? &S->n_serial : &S->n_parallel);
@@ -2263,7 +2416,23 @@ typedef struct {
     uint32_t ng, ns, nl, nh;
 } rx_kept;
 
+static uint32_t rx_min_rows(void)
+{
+    const char* v = getenv("RFEC_RX_ARENA_ROWS");
+    const long r = v ? atol(v) : 1l << 18;
+    return r < 4096 ? 4096u : r > (1l << 26) ? (1u << 26) : (uint32_t)r;
+}
+
+static int rx_compact_(rfec_rx_session* S, uint32_t extra, hipStream_t sm);
 static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
+{
+    const double t0 = now_us();
+    const int rc = rx_compact_(S, extra, sm);
+    S->t_compact += now_us() - t0;
+    return rc;
+}
+
+static int rx_compact_(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
 {
     const uint32_t tail = S->pend >= 0 ? S->pend_n : 0;
     hipError_t e;
@@ -2283,14 +2452,13 @@ static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
         const rx_sim* X = S->XS[t];
         rx_kept* k = &K[t];
         uint32_t nslot = 0, nline = 0;
-        for (uint32_t i = 0; i <= X->flex_of.mask; ++i)
-            if (X->flex_of.v[i]) {
-                const rx_inst* g = &X->G[X->flex_of.v[i] - 1];
-                if (g->shape != UINT32_MAX) {
-                    nslot += g->count;
-                    nline += X->S[g->shape].n_lines;
-                }
+        for (PM_EACH(&X->flex_of, fk, fv)) {
+            const rx_inst* g = &X->G[*fv - 1];
+            if (g->shape != UINT32_MAX) {
+                nslot += g->count;
+                nline += X->S[g->shape].n_lines;
             }
+        }
         k->NG = (rx_inst*)malloc(((size_t)X->flex_of.n + 1) * sizeof(rx_inst));
         k->nsrc = (int32_t*)malloc(((size_t)nslot + 1) * sizeof(int32_t));
         k->nhdr = (rfec_hdr*)malloc(((size_t)nslot + 1) * sizeof(rfec_hdr));
@@ -2299,9 +2467,8 @@ static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
         if (!k->NG || !k->nsrc || !k->nhdr || !k->npar || !k->hmap_)
             goto oom;
         /* the records the live state refers to (read only: nothing changes before the arena is allocated) */
-        for (uint32_t i = 0; i <= X->flex_of.mask; ++i)
-            if (X->flex_of.v[i]) {
-                const rx_inst* g = &X->G[X->flex_of.v[i] - 1];
+        for (PM_EACH(&X->flex_of, fk, fv)) {
+                const rx_inst* g = &X->G[*fv - 1];
                 if (g->shape == UINT32_MAX)
                     continue;
                 for (uint32_t q = 0; q < g->count; ++q)
@@ -2311,17 +2478,19 @@ static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
                     if (X->line_par[g->line0 + q] >= 0)
                         rmap[X->line_par[g->line0 + q]] = 1;
             }
-        for (uint32_t i = 0; i <= X->cache.mask; ++i) {
-            const uint32_t c = X->cache.v[i];
-            if (c && !(c & 0x80000000u))
-                rmap[c - 1] = 1;
-        }
+        for (PM_EACH(&X->cache, ck, cv))
+            if (!(*cv & 0x80000000u))
+                rmap[*cv - 1] = 1;
     }
     uint32_t nr = 0;
     for (uint32_t r = 0; r < S->nstore; ++r)
         nr += rmap[r] != 0;
     gmap = (uint32_t*)malloc(((size_t)nr + tail + 1) * sizeof(uint32_t)); /* new -> old */
-    const uint32_t arows = 2 * (nr + tail + extra) > 4096 ? 2 * (nr + tail + extra) : 4096;
+    /* room for 4 x what stays (compaction's host work is proportional to the open state: it comes back
+       after >= 3 x that many records), at least RFEC_RX_ARENA_ROWS rows (default 2^18: ~320 MB of HBM at
+       1,216-B rows; with razor's 300 ms evictions the open state stays far below it) */
+    const uint64_t want = 4ull * (nr + tail + extra);
+    const uint32_t arows = (uint32_t)(want > rx_min_rows() ? (want < 0xFFFFFFFFull ? want : 0xFFFFFFFFull) : rx_min_rows());
     if (!gmap)
         goto oom;
     if ((e = hipMalloc((void**)&arena, (size_t)arows * S->stride)) != hipSuccess) {
@@ -2331,10 +2500,8 @@ static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
     for (uint32_t t = 0; t < T; ++t) {
         rx_sim* X = S->XS[t];
         rx_kept* k = &K[t];
-        for (uint32_t i = 0; i <= X->flex_of.mask; ++i) {
-            if (!X->flex_of.v[i])
-                continue;
-            rx_inst g = X->G[X->flex_of.v[i] - 1];
+        for (PM_EACH(&X->flex_of, fk, fv)) {
+            rx_inst g = X->G[*fv - 1];
             if (g.shape != UINT32_MAX) {
                 const uint32_t nlines = X->S[g.shape].n_lines;
                 memcpy(k->nsrc + k->ns, X->slot_src + g.slot0, g.count * sizeof(int32_t));
@@ -2346,14 +2513,12 @@ static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
                 k->nl += nlines;
             }
             k->NG[k->ng] = g;
-            X->flex_of.v[i] = ++k->ng;
+            *fv = ++k->ng;
         }
         /* 2. cached recovered segments keep their header */
-        for (uint32_t i = 0; i <= X->cache.mask; ++i) {
-            const uint32_t c = X->cache.v[i];
-            if (c & 0x80000000u)
-                k->hmap_[c & 0x7FFFFFFFu] = 1;
-        }
+        for (PM_EACH(&X->cache, ck, cv))
+            if (*cv & 0x80000000u)
+                k->hmap_[*cv & 0x7FFFFFFFu] = 1;
     }
     /* 3. new ids, in arrival order */
     nr = 0;
@@ -2372,11 +2537,8 @@ static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
         for (uint32_t q = 0; q < k->nl; ++q)
             if (k->npar[q] >= 0)
                 k->npar[q] = (int32_t)rmap[k->npar[q]] - 1;
-        for (uint32_t i = 0; i <= X->cache.mask; ++i) {
-            const uint32_t c = X->cache.v[i];
-            if (c)
-                X->cache.v[i] = (c & 0x80000000u) ? (0x80000000u | (k->hmap_[c & 0x7FFFFFFFu] - 1)) : rmap[c - 1];
-        }
+        for (PM_EACH(&X->cache, ck, cv))
+            *cv = (*cv & 0x80000000u) ? (0x80000000u | (k->hmap_[*cv & 0x7FFFFFFFu] - 1)) : rmap[*cv - 1];
         for (uint32_t h = 0; h < X->nrh; ++h)
             if (k->hmap_[h])
                 X->rh[k->hmap_[h] - 1] = X->rh[h];
@@ -2499,8 +2661,10 @@ static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const rfec_wir
     }
     rep->n_fec_dropped = dropped;
     rep->host_us += now_us() - th;
+    const double h0 = rep->host_us;
     rc = rx_device(S->XS, S->T, &S->dev, S->arena, S->stride, S->capacity, 0, 0, out, out_payload, max_out, n_out,
                    rep, sm);
+    S->t_tables += rep->host_us - h0;
     rep->n_unmodelled = unmod + S->dev.unmodelled;
     return rc;
 }
@@ -2724,10 +2888,8 @@ static uint64_t* rx_keys(rfec_rx_session* S, int m, uint32_t* n)
     if (!k)
         return NULL;
     for (uint32_t t = 0; t < S->T; ++t) {
-        const hmap* h = rx_map(S->XS[t], m);
-        for (uint32_t i = 0; i <= h->mask; ++i)
-            if (h->v[i])
-                k[(*n)++] = (uint64_t)h->k[i] << 32 | t;
+        for (PM_EACH(rx_map(S->XS[t], m), key, v))
+            k[(*n)++] = (uint64_t)key << 32 | t;
     }
     qsort(k, *n, sizeof(uint64_t), cmp_u64);
     return k;
@@ -2756,7 +2918,7 @@ int rfec_rx_session_evict(rfec_rx_session* S, void* stream)
         return set_err(RFEC_ENOMEM, "rx session: evict", 0);
     for (uint32_t i = 0; i < n; ++i) {
         rx_sim* X = S->XS[(uint32_t)k[i]];
-        const uint32_t fi = hm_get(&X->flex_of, (uint32_t)(k[i] >> 32)) - 1;
+        const uint32_t fi = pm_get(&X->flex_of, (uint32_t)(k[i] >> 32)) - 1;
         const rx_inst* g = &X->G[fi];
         if (!(g->fec_ts + 3000u <= S->max_ts || g->nsegs >= g->count))
             break;
@@ -2767,11 +2929,11 @@ int rfec_rx_session_evict(rfec_rx_session* S, void* stream)
         return set_err(RFEC_ENOMEM, "rx session: evict", 0);
     for (uint32_t i = 0; i < n; ++i) {
         rx_sim* X = S->XS[(uint32_t)k[i]];
-        const uint32_t seq = (uint32_t)(k[i] >> 32), c = hm_get(&X->cache, seq);
+        const uint32_t seq = (uint32_t)(k[i] >> 32), c = pm_get(&X->cache, seq);
         const uint32_t ts = (c & 0x80000000u) ? X->rh[c & 0x7FFFFFFFu].ts : X->R[c - 1].hdr.ts;
         if (!(ts + 6000u < S->max_ts))
             break;
-        hm_del(&X->cache, seq);
+        pm_del(&X->cache, seq);
     }
     free(k);
     return rx_compact(S, 0, (hipStream_t)stream);
@@ -2794,5 +2956,10 @@ int rfec_rx_session_get_info(const rfec_rx_session* S, rfec_rx_session_info* inf
     info->batches_parallel = S->n_parallel;
     info->batches_serial = S->n_serial;
     info->batches_rolled_back = S->n_rollback;
+    info->split_us = S->t_split;
+    info->replay_us = S->t_replay;
+    info->verify_us = S->t_verify;
+    info->tables_us = S->t_tables;
+    info->compact_us = S->t_compact;
     return RFEC_OK;
 }

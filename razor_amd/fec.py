@@ -88,7 +88,12 @@ class rfec_rx_session_info(C.Structure):
     _fields_ = [("max_ts", C.c_uint32), ("open_flexes", C.c_uint32), ("cached_segments", C.c_uint32),
                 ("records_held", C.c_uint32), ("rows_held", C.c_uint32), ("pending", C.c_uint32),
                 ("threads", C.c_uint32), ("batches_parallel", C.c_uint32), ("batches_serial", C.c_uint32),
-                ("batches_rolled_back", C.c_uint32)]
+                ("batches_rolled_back", C.c_uint32), ("reserved", C.c_uint32), ("split_us", C.c_double),
+                ("replay_us", C.c_double), ("verify_us", C.c_double), ("tables_us", C.c_double),
+                ("compact_us", C.c_double)]
+
+
+assert C.sizeof(rfec_rx_session_info) == 88
 
 
 class rfec_service_info(C.Structure):

@@ -328,3 +328,17 @@ def test_mask_only_peel_equals_reference_peel(oracle1000, k, pf):
                                 np.repeat(meta1, G, axis=0), np.repeat(fsize1, G, axis=0), pp, 1000)
     for g in range(G):
         assert int(rec[g, 0]) == _mask_only_peel(plan, k, present[g, 0], pp[g]), f"pattern {pats[g]}"
+
+
+def test_wire_c3_digest_regenerates():
+    """tests/golden/wire_c3_digest.json (bench.py's wire sub-object checks the
+    device datagrams against it) is what oracle/gen_wire_digest.py computes
+    from the oracle's framing, over headers equal to the bench's."""
+    import importlib.util
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    spec = importlib.util.spec_from_file_location("gen_wire_digest", root / "oracle" / "gen_wire_digest.py")
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    assert gen.digests() == json.loads((root / "tests" / "golden" / "wire_c3_digest.json").read_text())

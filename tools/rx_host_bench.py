@@ -78,7 +78,9 @@ def main():
         dev += rep.kernel_us + rep.h2d_us + rep.d2h_us
         tot += rep.total_us
     wall = time.perf_counter() - t0
-    print("session:", sess.info())
+    info = sess.info()
+    print("session:", info)
+    print("split ms:", {k: round(v / 1e3, 2) for k, v in info.items() if k.endswith("_us")})
     got = np.concatenate(got)
     print(f"arrivals {n}  recovered {len(got)}  wall {wall * 1e3:.1f} ms  host_us {host:.0f} "
           f"({host * 1e3 / n:.1f} ns/arrival)  stub-device {dev:.0f} us  total {tot:.0f} us  "
