@@ -79,6 +79,19 @@ int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, c
                            uint32_t max_len, void* stream);
 int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map, uint32_t rows, uint32_t stride,
                             void* stream);
+/* The receiver session's batch split, per parsed record (rfec_rx.c rx_phase0): its shard (fec_id % T, a
+ * segment outside FEC by packet id; 0xFF: no effect on the control plane), its kind (RX_SPLIT_*) and the
+ * value the replay's max_ts rules read (a segment's timestamp, a parity's send_ts + 3000). */
+#define RX_SPLIT_NONE 0
+#define RX_SPLIT_SEG_TS 1 /* SIM_SEG with fec_id and packet id: may raise max_ts */
+#define RX_SPLIT_SEG 2
+#define RX_SPLIT_FEC 3
+typedef struct {
+    uint8_t shard, kind;
+    uint16_t reserved;
+    uint32_t value;
+} rfec_rx_split; /* 8 bytes */
+int rfec_launch_rx_split(const rfec_wire_rec* recs, uint32_t n, uint32_t T, rfec_rx_split* out, void* stream);
 /* receiver groups above RFEC_MAX_K segments: out row = parity row ^ member rows (one dependency level per call) */
 typedef struct {
     int32_t out;       /* output row */

@@ -2023,6 +2023,41 @@ __global__ __launch_bounds__(kBlock) void k_pack_rows(uint8_t* __restrict__ pack
 // dst row r <- src row map[r] (all `C` 16-B chunks), or zeros for map[r] < 0:
 // the receiver's scatter of parsed payloads into group slots and its gather
 // of recovered segments.  One lane per chunk, streaming.
+// The receiver session's batch split (rfec_rx.c rx_phase0), one lane per
+// parsed record: the host then reads 8 bytes per record instead of the 64-B
+// records the parse just wrote (cache-cold on the host), and the replay
+// threads take those cache misses in parallel.  Reads only the fields the
+// split needs (status, mid, seq, ts, send_ts, fec_id; rfec_wire_rec layout).
+__global__ __launch_bounds__(kBlock) void k_rx_split(const rfec_wire_rec* __restrict__ recs, uint32_t n, uint32_t T,
+                                                    rfec_rx_split* __restrict__ out)
+{
+    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n)
+        return;
+    static_assert(offsetof(rfec_wire_rec, mid) == 2 && offsetof(rfec_wire_rec, hdr) == 8 &&
+                      offsetof(rfec_wire_rec, send_ts) == 32 && offsetof(rfec_wire_rec, fec_id) == 36 &&
+                      sizeof(rfec_rx_split) == 8,
+                  "record layout");
+    const uint32_t* r = reinterpret_cast<const uint32_t*>(recs + p);
+    const uint32_t w0 = r[0], seq = r[2], ts = r[4], send_ts = r[8], fec_id = r[9] & 0xFFFFu;
+    const int8_t status = (int8_t)(w0 & 0xFFu);
+    const uint32_t mid = (w0 >> 16) & 0xFFu;
+    uint32_t shard = 0xFFu, kind = RX_SPLIT_NONE, value = 0;
+    if (status == RFEC_WIRE_OK && mid == RFEC_WIRE_SEG) {
+        shard = (fec_id ? fec_id : seq) % T;
+        kind = fec_id && seq ? RX_SPLIT_SEG_TS : RX_SPLIT_SEG;
+        value = ts;
+    } else if (status == RFEC_WIRE_OK && mid == RFEC_WIRE_FEC) {
+        shard = fec_id % T;
+        kind = RX_SPLIT_FEC;
+        value = send_ts + 3000u;
+    }
+    uint2 o;
+    o.x = shard | kind << 8;
+    o.y = value;
+    *reinterpret_cast<uint2*>(out + p) = o;
+}
+
 __global__ __launch_bounds__(kBlock) void k_gather_rows(v4u* __restrict__ dst, const v4u* __restrict__ src,
                                                         const int32_t* __restrict__ map, uint32_t total, uint32_t C,
                                                         FastDiv divC)
@@ -2635,6 +2670,15 @@ int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map
         return 0;
     RFEC_LAUNCH(k_gather_rows, dim3(blocks_for(total)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
                 reinterpret_cast<v4u*>(dst), reinterpret_cast<const v4u*>(src), map, total, C, make_fastdiv(C));
+    return (int)hipGetLastError();
+}
+
+int rfec_launch_rx_split(const rfec_wire_rec* recs, uint32_t n, uint32_t T, rfec_rx_split* out, void* stream)
+{
+    if (!n)
+        return 0;
+    RFEC_LAUNCH(k_rx_split, dim3(blocks_for(n)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), recs, n, T,
+                out);
     return (int)hipGetLastError();
 }
 

@@ -4,7 +4,7 @@
  * plane of sim_fec.c:104-241 / flex_fec_receiver.c:69-280 runs on the host
  * over headers; the bytes are peeled on the device.
  */
-#define _POSIX_C_SOURCE 200809L
+#define _GNU_SOURCE /* sched_getcpu, CPU_SET, pthread_attr_setaffinity_np: the replay threads' placement */
 #ifndef __HIP_PLATFORM_AMD__
 #define __HIP_PLATFORM_AMD__ 1
 #endif
@@ -12,6 +12,7 @@
 
 #include <math.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -316,10 +317,14 @@ typedef struct {
 
 #define RX_CONFLICT_OWNER 1
 #define RX_CONFLICT_TS 2
+#define RX_CONFLICT_RISKY 4 /* a parity of the batch could meet the 3 s drop (found by the replay threads) */
 
 typedef struct { /* one batch's parallel replay, shared by the shards */
     uint32_t T;           /* shards */
-    const uint32_t* smin; /* [n]: min over the batch's later parities of send_ts + 3000 (by batch position) */
+    const uint32_t* smin; /* [n]: min over the batch's later parities of send_ts + 3000 (by batch position);
+                             NULL: each shard computes its own from `sum` */
+    const rfec_rx_split* sum; /* the batch's split summary (k_rx_split), or NULL (host lists) */
+    uint32_t n, max0;     /* the batch's records; max_ts at its start */
     uint32_t a0;          /* the batch's first record */
     int ts_check;         /* recoveries checked against smin (the parallel replay) */
     int conflict;         /* RX_CONFLICT_* (atomic) */
@@ -357,6 +362,9 @@ typedef struct {
        batch touched -- saved on first touch with their slot / line tables --,
        and the tables' lengths) */
     rx_par* P;
+    const uint32_t* sminp; /* this batch's smin: P->smin, or sminl (computed by this shard's thread) */
+    uint32_t* sminl;
+    uint32_t sminlcap;
     uint64_t* claims;   /* this batch's packet-id claims: seq << 32 | fec_id + 1 */
     uint32_t nclaims, claimcap;
     uint64_t* cpart;    /* the claims by owner-table partition (rx_bucket_claims), offsets in coff */
@@ -990,7 +998,7 @@ static void rx_drain(rx_sim* X, uint32_t a)
                 rx_conflict(X, RX_CONFLICT_OWNER);
                 return;
             }
-            if (X->P->ts_check && e.hdr.ts > X->P->smin[a - X->P->a0]) {
+            if (X->P->ts_check && e.hdr.ts > X->sminp[a - X->P->a0]) {
                 rx_conflict(X, RX_CONFLICT_TS);
                 return;
             }
@@ -1025,6 +1033,7 @@ static void rx_sim_free(rx_sim* X)
     free(X->jops);
     free(X->jsave);
     free(X->claims);
+    free(X->sminl);
     free(X->cpart);
     free(X->claimed);
 }
@@ -1202,6 +1211,43 @@ typedef struct {
     int oom;
 } rx_dev;
 
+/* D->ev by packet id: an LSD radix sort of (packet id, position) keys, 4 x 8
+ * bits, then one permutation (qsort's comparisons were ~20 % of the device
+ * tables' host time at ~900 deliveries a batch); stable */
+static int rx_sort_events(rx_dev* D)
+{
+    const uint32_t n = D->nev;
+    uint64_t* k = (uint64_t*)malloc((size_t)n * 2 * sizeof(uint64_t));
+    rx_event* tmp = (rx_event*)malloc((size_t)n * sizeof(rx_event));
+    if (!k || !tmp) {
+        free(k);
+        free(tmp);
+        return -1;
+    }
+    uint64_t* src = k;
+    uint64_t* dst = k + n;
+    for (uint32_t i = 0; i < n; ++i)
+        src[i] = (uint64_t)D->ev[i].hdr.seq << 32 | i;
+    for (uint32_t sh = 32; sh < 64; sh += 8) {
+        uint32_t cnt[257] = {0};
+        for (uint32_t i = 0; i < n; ++i)
+            cnt[((src[i] >> sh) & 0xFFu) + 1]++;
+        for (uint32_t b = 1; b <= 256; ++b)
+            cnt[b] += cnt[b - 1];
+        for (uint32_t i = 0; i < n; ++i)
+            dst[cnt[(src[i] >> sh) & 0xFFu]++] = src[i];
+        uint64_t* t = src;
+        src = dst;
+        dst = t;
+    }
+    for (uint32_t i = 0; i < n; ++i)
+        tmp[i] = D->ev[(uint32_t)src[i]];
+    memcpy(D->ev, tmp, (size_t)n * sizeof(rx_event));
+    free(k);
+    free(tmp);
+    return 0;
+}
+
 static void rx_dev_free(rx_dev* D)
 {
     free(D->ev);
@@ -1376,8 +1422,8 @@ static int rx_device(rx_sim* const* XS, uint32_t T, rx_dev* D, const uint8_t* ro
         }
         sbase[t + 1] = sbase[t] + X->ns;
     }
-    if (D->nev > 1)
-        qsort(D->ev, D->nev, sizeof(rx_event), cmp_event);
+    if (D->nev > 1 && rx_sort_events(D)) /* ascending packet id (each shard's list is in its arrival order) */
+        return set_err(RFEC_ENOMEM, "rx: delivery list", 0);
     memset(D->cls, 0, (size_t)nshape * sizeof(uint32_t));
     /* 2. delivering groups, by device shape (work proportional to the deliveries, not to the open flexes) */
     for (uint32_t t = 0; t < T; ++t) {
@@ -1808,9 +1854,9 @@ int rfec_host_recv_datagrams(uint32_t n, uint32_t dstride, const uint8_t* dgram,
 /* ------------------------------------------------------------------------ */
 /* a batch of the pipelined push: its parse in flight on the session's stream */
 typedef struct {
-    rfec_wire_rec* rec;  /* pinned, device-mapped records */
-    rfec_wire_rec* recd; /* rec as the device addresses it */
-    uint32_t reccap;
+    rfec_rx_split* sum;  /* pinned, device-mapped: the batch's split summary (k_rx_split) */
+    rfec_rx_split* sumd; /* sum as the device addresses it */
+    uint32_t sumcap;
     uint8_t* dg; /* device copy of pageable datagram slots + lengths */
     size_t dgb;
     hipEvent_t done;
@@ -1835,8 +1881,19 @@ struct rx_pool {
     void* arg;
 };
 
-#define RX_SPIN_US 2000.0 /* a worker spins this long before sleeping: batches come back to back, and a
-                             condition-variable wake costs ~10-50 us */
+/* how long a worker (or the caller) spins before sleeping on the condition
+ * variable: RFEC_RX_SPIN_US, default 50 us (spinning threads share the
+ * process's CPU quota and cores with the caller's serial work) */
+static double rx_spin_us(void)
+{
+    static double v = -1.0;
+    if (v < 0) {
+        const char* e = getenv("RFEC_RX_SPIN_US");
+        v = e ? atof(e) : 50.0;
+    }
+    return v;
+}
+#define RX_SPIN_US rx_spin_us()
 
 static void cpu_relax(void)
 {
@@ -1873,18 +1930,79 @@ static void* pool_main(void* p)
     }
 }
 
+/* The CPUs the replay threads run on: RFEC_RX_CPUS ("a-b,c,..."), else those
+ * sharing the last-level cache with the creating thread's CPU (one CCD of an
+ * EPYC: the records, the shards and the device tables pass between the
+ * threads through that L3; across CCDs every such line is a fabric round
+ * trip, and the replay ran slower in parallel than alone), within the
+ * process's affinity.  RFEC_RX_PIN=0: no placement.  0 when nothing applies. */
+static int parse_cpus(const char* s, cpu_set_t* set)
+{
+    CPU_ZERO(set);
+    int n = 0;
+    while (s && *s) {
+        char* e;
+        long a = strtol(s, &e, 10), b = a;
+        if (e == s)
+            break;
+        if (*e == '-')
+            b = strtol(e + 1, &e, 10);
+        for (long c = a; c <= b && c < CPU_SETSIZE; ++c, ++n)
+            CPU_SET((int)c, set);
+        s = *e == ',' ? e + 1 : e;
+        if (*s == '\n')
+            break;
+    }
+    return n;
+}
+
+static int rx_worker_cpus(cpu_set_t* set)
+{
+    const char* pin = getenv("RFEC_RX_PIN");
+    if (pin && pin[0] == '0')
+        return 0;
+    const char* cpus = getenv("RFEC_RX_CPUS");
+    if (cpus)
+        return parse_cpus(cpus, set) > 0;
+    const int cpu = sched_getcpu();
+    if (cpu < 0)
+        return 0;
+    char path[96], buf[512];
+    snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", cpu);
+    FILE* f = fopen(path, "r");
+    if (!f)
+        return 0;
+    const int ok = fgets(buf, sizeof(buf), f) != NULL;
+    fclose(f);
+    if (!ok || parse_cpus(buf, set) < 2)
+        return 0;
+    cpu_set_t mine;
+    if (pthread_getaffinity_np(pthread_self(), sizeof(mine), &mine))
+        return 0;
+    CPU_AND(set, set, &mine);
+    return CPU_COUNT(set) >= 2;
+}
+
 static int pool_start(rx_pool* P, uint32_t workers)
 {
     memset(P, 0, sizeof(*P));
     pthread_mutex_init(&P->mu, NULL);
     pthread_cond_init(&P->go, NULL);
     pthread_cond_init(&P->fin, NULL);
+    cpu_set_t cpus;
+    pthread_attr_t attr;
+    pthread_attr_init(&attr);
+    if (rx_worker_cpus(&cpus))
+        pthread_attr_setaffinity_np(&attr, sizeof(cpus), &cpus);
     for (uint32_t i = 0; i < workers; ++i) {
         P->w[i] = (rx_worker){P, i + 1};
-        if (pthread_create(&P->th[i], NULL, pool_main, &P->w[i]))
+        if (pthread_create(&P->th[i], &attr, pool_main, &P->w[i])) {
+            pthread_attr_destroy(&attr);
             return -1;
+        }
         P->nth = i + 1;
     }
+    pthread_attr_destroy(&attr);
     return 0;
 }
 
@@ -1943,7 +2061,8 @@ struct rfec_rx_session {
     uint32_t n_parallel, n_serial, n_rollback; /* batches by replay (rfec_rx_session_info) */
     double t_split, t_replay, t_verify, t_tables, t_compact; /* host time split (rfec_rx_session_info) */
     rx_dev dev;
-    rfec_wire_rec* store; /* every shard's R */
+    rfec_wire_rec* store;   /* every shard's R: pinned, the parse writes the records straight in */
+    rfec_wire_rec* store_d; /* store as the device addresses it */
     uint32_t nstore, storecap;
     uint8_t* arena; /* [arows][stride]: rows [0, nstore) ingested, then the pending batch's */
     uint32_t arows;
@@ -1966,6 +2085,8 @@ static rx_sim* rx_sim_alloc(void)
     memset(p, 0, sz);
     return (rx_sim*)p;
 }
+
+static int rx_compact(rfec_rx_session* S, uint32_t extra, hipStream_t sm);
 
 static void rx_shards_free(rfec_rx_session* S)
 {
@@ -2031,6 +2152,12 @@ rfec_rx_session* rfec_rx_session_create(uint32_t stride, uint32_t capacity)
         set_err(RFEC_ENOMEM, "rx session: host tables / threads", 0);
         return NULL;
     }
+    /* the row arena and the record store now (RFEC_RX_ARENA_ROWS), not inside the first push */
+    if (rx_compact(s, 0, NULL)) {
+        rfec_rx_session_destroy(s);
+        return NULL;
+    }
+    s->t_compact = 0;
     return s;
 }
 
@@ -2054,8 +2181,8 @@ void rfec_rx_session_destroy(rfec_rx_session* s)
     if (s->sa) /* a pending parse still writes into the arena */
         (void)hipStreamSynchronize(s->sa);
     for (int i = 0; i < 2; ++i) {
-        if (s->st[i].rec)
-            (void)hipHostFree(s->st[i].rec);
+        if (s->st[i].sum)
+            (void)hipHostFree(s->st[i].sum);
         if (s->st[i].dg)
             (void)hipFree(s->st[i].dg);
         if (s->st[i].done)
@@ -2073,7 +2200,8 @@ void rfec_rx_session_destroy(rfec_rx_session* s)
     free(s->pshard);
     free(s->lst);
     free(s->smin);
-    free(s->store);
+    if (s->store)
+        (void)hipHostFree(s->store);
     if (s->arena)
         (void)hipFree(s->arena);
     free(s);
@@ -2166,7 +2294,7 @@ oom:
 /* Phase 0 of a sharded batch, serial over the records [a0, a0 + n): each
  * record's shard, the per-shard lists, smin, whether a parity of the batch
  * could meet the 3 s drop through a segment timestamp before it (`risky`). */
-static int rx_phase0(rfec_rx_session* S, uint32_t a0, uint32_t n, int* risky)
+static int rx_phase0(rfec_rx_session* S, uint32_t a0, uint32_t n, const rfec_rx_split* sum, int* risky)
 {
     if (S->lcap < n) {
         const uint32_t c = n + n / 4 + 64;
@@ -2188,7 +2316,25 @@ static int rx_phase0(rfec_rx_session* S, uint32_t a0, uint32_t n, int* risky)
     uint32_t cnt[RX_MAX_THREADS] = {0};
     uint32_t pm = S->max_ts;
     int rk = 0;
-    for (uint32_t p = 0; p < n; ++p) {
+    if (sum) { /* the device's split (k_rx_split): 8 bytes per record */
+        for (uint32_t p = 0; p < n; ++p) {
+            const rfec_rx_split e = sum[p];
+            if (e.kind == RX_SPLIT_SEG_TS && e.value > pm)
+                pm = e.value;
+            else if (e.kind == RX_SPLIT_FEC && e.value < pm)
+                rk = 1;
+            S->pshard[p] = e.shard;
+            if (e.shard != 0xFF)
+                cnt[e.shard]++;
+        }
+        uint32_t m = UINT32_MAX;
+        for (uint32_t p = n; p-- > 0;) {
+            S->smin[p] = m;
+            if (sum[p].kind == RX_SPLIT_FEC && sum[p].value < m)
+                m = sum[p].value;
+        }
+    }
+    for (uint32_t p = 0; p < n && !sum; ++p) {
         const rfec_wire_rec* r = &R[p];
         uint32_t t = 0xFF;
         if (r->status == RFEC_WIRE_OK && r->mid == RFEC_WIRE_SEG) {
@@ -2205,7 +2351,7 @@ static int rx_phase0(rfec_rx_session* S, uint32_t a0, uint32_t n, int* risky)
             cnt[t]++;
     }
     uint32_t m = UINT32_MAX;
-    for (uint32_t p = n; p-- > 0;) {
+    for (uint32_t p = n; !sum && p-- > 0;) {
         S->smin[p] = m;
         const rfec_wire_rec* r = &R[p];
         if (r->status == RFEC_WIRE_OK && r->mid == RFEC_WIRE_FEC && r->send_ts + 3000u < m)
@@ -2228,12 +2374,47 @@ static void rx_shard_job(void* arg, uint32_t t)
 {
     rfec_rx_session* S = (rfec_rx_session*)arg;
     rx_sim* X = S->XS[t];
-    const uint32_t* L = S->lst + S->loff[t];
-    const uint32_t n = S->loff[t + 1] - S->loff[t];
-    for (uint32_t i = 0; i < n && !X->oom; ++i) {
-        if ((i & 15) == 0 && __atomic_load_n(&S->par.conflict, __ATOMIC_RELAXED))
+    const rx_par* P = &S->par;
+    if (P->sum) {
+        /* the device's split: this thread walks the whole summary (8 B a record), replays its own records,
+           keeps the batch's running segment timestamp (a parity below it: the batch replays in order) and
+           its own copy of smin (no serial split on the calling thread) */
+        const rfec_rx_split* sum = P->sum;
+        const uint32_t n = P->n;
+        RX_GROW(X->sminl, 0, X->sminlcap, n, uint32_t);
+        if (X->oom)
             return;
-        rx_arrival(X, L[i]);
+        uint32_t m = UINT32_MAX;
+        for (uint32_t p = n; p-- > 0;) {
+            X->sminl[p] = m;
+            if (sum[p].kind == RX_SPLIT_FEC && sum[p].value < m)
+                m = sum[p].value;
+        }
+        X->sminp = X->sminl;
+        uint32_t pm = P->max0, k = 0;
+        for (uint32_t p = 0; p < n && !X->oom; ++p) {
+            const rfec_rx_split e = sum[p];
+            if (e.kind == RX_SPLIT_SEG_TS && e.value > pm) {
+                pm = e.value;
+            } else if (e.kind == RX_SPLIT_FEC && e.value < pm) {
+                rx_conflict(X, RX_CONFLICT_RISKY);
+                return;
+            }
+            if (e.shard != t)
+                continue;
+            if ((k++ & 15) == 0 && __atomic_load_n(&S->par.conflict, __ATOMIC_RELAXED))
+                return;
+            rx_arrival(X, P->a0 + p);
+        }
+    } else {
+        const uint32_t* L = S->lst + S->loff[t];
+        const uint32_t n = S->loff[t + 1] - S->loff[t];
+        X->sminp = P->smin;
+        for (uint32_t i = 0; i < n && !X->oom; ++i) {
+            if ((i & 15) == 0 && __atomic_load_n(&S->par.conflict, __ATOMIC_RELAXED))
+                return;
+            rx_arrival(X, L[i]);
+        }
     }
     rx_bucket_claims(X, S->T);
 }
@@ -2266,10 +2447,12 @@ static void rx_verify_job(void* arg, uint32_t j)
 static void rx_serial_over_shards(rfec_rx_session* S, uint32_t a0, uint32_t n)
 {
     uint32_t m = S->max_ts;
+    const rfec_rx_split* sum = S->par.sum;
     for (uint32_t p = 0; p < n; ++p) {
-        if (S->pshard[p] == 0xFF)
+        const uint32_t t = sum ? sum[p].shard : S->pshard[p];
+        if (t == 0xFF)
             continue;
-        rx_sim* X = S->XS[S->pshard[p]];
+        rx_sim* X = S->XS[t];
         X->max_ts = m;
         rx_arrival(X, a0 + p);
         m = X->max_ts;
@@ -2289,7 +2472,7 @@ static int rx_any_oom(const rfec_rx_session* S)
 }
 
 /* The control plane over the session's records [a0, a0 + n). */
-static int rx_ingest(rfec_rx_session* S, uint32_t a0, uint32_t n)
+static int rx_ingest(rfec_rx_session* S, uint32_t a0, uint32_t n, const rfec_rx_split* sum)
 {
     for (uint32_t t = 0; t < S->T; ++t) {
         rx_sim* X = S->XS[t];
@@ -2310,10 +2493,12 @@ static int rx_ingest(rfec_rx_session* S, uint32_t a0, uint32_t n)
                 return set_err(RFEC_ENOMEM, "rx session: claims", 0);
             X->nclaims = 0;
         }
-        const double ts = now_us();
-        if ((rc = rx_phase0(S, a0, n, &risky)))
-            return rc;
-        S->t_split += now_us() - ts;
+        if (!sum) { /* (with the device's split the replay threads take the batch apart themselves) */
+            const double ts = now_us();
+            if ((rc = rx_phase0(S, a0, n, NULL, &risky)))
+                return rc;
+            S->t_split += now_us() - ts;
+        }
     }
     const double tr = now_us();
     if (S->T == 1) {
@@ -2330,7 +2515,10 @@ static int rx_ingest(rfec_rx_session* S, uint32_t a0, uint32_t n)
     }
     rx_par* P = &S->par;
     P->T = S->T;
-    P->smin = S->smin;
+    P->sum = sum;
+    P->n = n;
+    P->max0 = S->max_ts;
+    P->smin = sum ? NULL : S->smin;
     P->a0 = a0;
     P->ts_check = !risky;
     P->conflict = 0;
@@ -2353,8 +2541,9 @@ static int rx_ingest(rfec_rx_session* S, uint32_t a0, uint32_t n)
         c = __atomic_load_n(&P->conflict, __ATOMIC_RELAXED);
         if (!c)
             ++*(risky ? &S->n_serial : &S->n_parallel);
-    } else if ((c & RX_CONFLICT_TS) && !(c & RX_CONFLICT_OWNER) && !rx_any_oom(S)) {
-        /* a recovery raised max_ts past a later parity's limit: again, in arrival order */
+    } else if ((c & (RX_CONFLICT_TS | RX_CONFLICT_RISKY)) && !(c & RX_CONFLICT_OWNER) && !rx_any_oom(S)) {
+        /* a recovery raised max_ts past a later parity's limit, or a parity could meet the drop through a
+           segment timestamp before it: again, in arrival order */
         S->n_rollback++;
         for (uint32_t t = 0; t < S->T; ++t) {
             rx_rollback(S->XS[t]);
@@ -2497,6 +2686,22 @@ static int rx_compact_(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
         rc = set_err(RFEC_ENOMEM, "rx session: arena", e);
         goto done;
     }
+    /* the record store: the same capacity, pinned and device-mapped (the parse writes records in) */
+    rfec_wire_rec* nst = S->store;
+    rfec_wire_rec* nst_d = S->store_d;
+    if (S->storecap < arows) {
+        void* d = NULL;
+        nst = NULL;
+        if ((e = hipHostMalloc((void**)&nst, (size_t)arows * sizeof(rfec_wire_rec), hipHostMallocMapped)) !=
+                hipSuccess ||
+            (e = hipHostGetDevicePointer(&d, nst, 0)) != hipSuccess) {
+            if (nst)
+                (void)hipHostFree(nst);
+            rc = set_err(RFEC_ENOMEM, "rx session: record store", e);
+            goto oom_arena;
+        }
+        nst_d = (rfec_wire_rec*)d;
+    }
     for (uint32_t t = 0; t < T; ++t) {
         rx_sim* X = S->XS[t];
         rx_kept* k = &K[t];
@@ -2559,14 +2764,23 @@ static int rx_compact_(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
         k->nsrc = k->npar = NULL;
         k->nhdr = NULL;
     }
-    /* 4. records (host) and rows (device) */
+    /* 4. records (host: in place, rmap[r] - 1 <= r, ascending, or into the larger store) and rows (device) */
     for (uint32_t r = 0; r < S->nstore; ++r)
         if (rmap[r]) {
             gmap[rmap[r] - 1] = r;
-            S->store[rmap[r] - 1] = S->store[r]; /* rmap[r] - 1 <= r: in place, ascending */
+            nst[rmap[r] - 1] = S->store[r];
         }
-    for (uint32_t t = 0; t < tail; ++t)
+    for (uint32_t t = 0; t < tail; ++t) { /* the pending batch's records and rows follow */
         gmap[nr + t] = S->nstore + t;
+        nst[nr + t] = S->store[S->nstore + t];
+    }
+    if (nst != S->store) {
+        if (S->store)
+            (void)hipHostFree(S->store);
+        S->store = nst;
+        S->store_d = nst_d;
+        S->storecap = arows;
+    }
     S->nstore = nr;
     for (uint32_t t = 0; t < T; ++t)
         S->XS[t]->R = S->store;
@@ -2594,6 +2808,7 @@ static int rx_compact_(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
     goto done;
 oom:
     rc = set_err(RFEC_ENOMEM, "rx session: compaction", 0);
+oom_arena:
     if (arena)
         (void)hipFree(arena);
 done:
@@ -2615,33 +2830,24 @@ static int rx_session_room(rfec_rx_session* S, uint32_t n, hipStream_t sm)
 {
     int rc;
     const uint32_t tail = S->pend >= 0 ? S->pend_n : 0; /* a pending pipelined batch's rows */
-    if (S->nstore + tail + n > S->arows && (rc = rx_compact(S, n, sm)))
-        return rc;
-    if (S->nstore + tail + n > S->storecap) {
-        uint32_t c = S->storecap ? S->storecap : 4096;
-        while (c < S->nstore + tail + n)
-            c *= 2;
-        rfec_wire_rec* p = (rfec_wire_rec*)realloc(S->store, (size_t)c * sizeof(rfec_wire_rec));
-        if (!p)
-            return set_err(RFEC_ENOMEM, "rx session: record store", 0);
-        S->store = p;
-        S->storecap = c;
-    }
+    if ((S->nstore + tail + n > S->arows || S->nstore + tail + n > S->storecap) && (rc = rx_compact(S, n, sm)))
+        return rc; /* (compaction sizes both: room for 4 x what stays) */
     return RFEC_OK;
 }
 
-/* records already on the host (rh[0, n)), payload rows on the device at
- * `payload`, or already in the arena's next n rows (payload NULL; the caller
- * made the room) */
-static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const rfec_wire_rec* rh, const uint8_t* payload,
+static int rx_stage_reserve(rx_stage* st, uint32_t n, size_t dg_bytes);
+
+/* The batch's records are at store[nstore, nstore + n) already (the parse or
+ * the D2H wrote them there); payload rows on the device at `payload`, or
+ * already in the arena's next n rows (payload NULL; the caller made the
+ * room); `sum`: the batch's split summary (k_rx_split), or NULL (split on the
+ * host from the records) */
+static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const uint8_t* payload, const rfec_rx_split* sum,
                                   rfec_rx_seg* out, uint8_t* out_payload, uint32_t max_out, uint32_t* n_out,
                                   rfec_rx_report* rep, hipStream_t sm)
 {
     hipError_t e;
     int rc;
-    if (payload && (rc = rx_session_room(S, n, sm)))
-        return rc;
-    memcpy(S->store + S->nstore, rh, (size_t)n * sizeof(rfec_wire_rec));
     if (payload) {
         double tt = now_us();
         if ((e = hipMemcpyAsync(S->arena + (size_t)S->nstore * S->stride, payload, (size_t)n * S->stride,
@@ -2652,7 +2858,7 @@ static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const rfec_wir
     const uint32_t a0 = S->nstore;
     S->nstore += n;
     const double th = now_us();
-    if ((rc = rx_ingest(S, a0, n)))
+    if ((rc = rx_ingest(S, a0, n, sum)))
         return rc;
     uint32_t dropped = 0, unmod = 0;
     for (uint32_t t = 0; t < S->T; ++t) {
@@ -2667,6 +2873,14 @@ static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const rfec_wir
     S->t_tables += rep->host_us - h0;
     rep->n_unmodelled = unmod + S->dev.unmodelled;
     return rc;
+}
+
+/* the split summary of records the device can read at `recs_d` into stage st (sharded sessions) */
+static int rx_split_launch(rfec_rx_session* S, rx_stage* st, const rfec_wire_rec* recs_d, uint32_t n, hipStream_t sm)
+{
+    if (S->T == 1 || n > (1u << 20)) /* (one serial state; or a huge push: split on the host) */
+        return 0;
+    return rfec_launch_rx_split(recs_d, n, S->T, st->sumd, sm);
 }
 
 int rfec_rx_session_push(rfec_rx_session* S, uint32_t n, const rfec_wire_rec* recs, const uint8_t* payload,
@@ -2684,17 +2898,18 @@ int rfec_rx_session_push(rfec_rx_session* S, uint32_t n, const rfec_wire_rec* re
         return RFEC_OK;
     hipStream_t sm = (hipStream_t)stream;
     hipError_t e;
-    int rc;
-    if ((rc = rx_reserve(RX_ALIGN((size_t)n * sizeof(rfec_wire_rec)), 0, 0)))
+    int rc, ke = 0;
+    if ((rc = rx_session_room(S, n, sm)) || (rc = rx_stage_reserve(&S->st[0], n, 0)))
         return rc;
     double tt = now_us();
-    if ((e = hipMemcpyAsync(t_rx.h, recs, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost, sm)) !=
-            hipSuccess ||
-        (e = hipStreamSynchronize(sm)) != hipSuccess)
-        return set_err(RFEC_EDEVICE, "rx session: records D2H", e);
+    /* the records into the store, their split beside */
+    if ((e = hipMemcpyAsync(S->store + S->nstore, recs, (size_t)n * sizeof(rfec_wire_rec), hipMemcpyDeviceToHost,
+                            sm)) != hipSuccess ||
+        (ke = rx_split_launch(S, &S->st[0], recs, n, sm)) != 0 || (e = hipStreamSynchronize(sm)) != hipSuccess)
+        return set_err(RFEC_EDEVICE, "rx session: records D2H", ke ? ke : (int)e);
     rep->d2h_us += now_us() - tt;
-    rc = rx_session_push_staged(S, n, (const rfec_wire_rec*)t_rx.h, payload, out, out_payload, max_out, n_out, rep,
-                                sm);
+    rc = rx_session_push_staged(S, n, payload, S->T > 1 && n <= (1u << 20) ? S->st[0].sum : NULL, out, out_payload,
+                                max_out, n_out, rep, sm);
     rep->total_us = now_us() - t0;
     return rc;
 }
@@ -2718,48 +2933,36 @@ int rfec_rx_session_push_datagrams(rfec_rx_session* S, uint32_t n, uint32_t dstr
     if (!t_rv.sm && (e = hipStreamCreateWithFlags(&t_rv.sm, hipStreamNonBlocking)) != hipSuccess)
         return set_err(RFEC_EDEVICE, "recv: stream", e);
     const uint32_t stride = S->stride;
-    const size_t o_dl = RX_ALIGN((size_t)n * dstride), need = RX_ALIGN(o_dl + (size_t)n * 2);
-    if (t_rv.db < need) {
-        if (t_rv.d)
-            (void)hipFree(t_rv.d);
-        t_rv.d = NULL;
-        t_rv.db = 0;
-        const size_t b = need + need / 4;
-        if ((e = hipMalloc((void**)&t_rv.d, b)) != hipSuccess)
-            return set_err(RFEC_ENOMEM, "recv: device staging", e);
-        t_rv.db = b;
-    }
-    uint8_t* D = t_rv.d;
+    const size_t o_dl = RX_ALIGN((size_t)n * dstride);
     int rc;
-    if ((rc = rx_reserve(RX_ALIGN((size_t)n * sizeof(rfec_wire_rec)), 0, 0)))
+    /* the records are parsed straight into the store, the payload rows into the arena's next n rows */
+    if ((rc = rx_session_room(S, n, t_rv.sm)) || (rc = rx_stage_reserve(&S->st[0], n, o_dl + (size_t)n * 2)))
         return rc;
-    /* the payload rows are parsed straight into the arena's next n rows */
-    if ((rc = rx_session_room(S, n, t_rv.sm)))
-        return rc;
+    rx_stage* st = &S->st[0];
     double tt = now_us();
     /* datagrams in pinned memory (the UDP batch slots) are read by the parse
-     * itself; pageable ones are copied first.  The records go straight to the
-     * pinned staging area. */
+     * itself; pageable ones are copied first */
     const uint8_t* dg = host_mapped(dgram);
     const uint8_t* dl = host_mapped(dlen);
     if (!dg || !dl) {
-        if ((e = hipMemcpyAsync(D, dgram, (size_t)n * dstride, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess ||
-            (e = hipMemcpyAsync(D + o_dl, dlen, (size_t)n * 2, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess)
+        if ((e = hipMemcpyAsync(st->dg, dgram, (size_t)n * dstride, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess ||
+            (e = hipMemcpyAsync(st->dg + o_dl, dlen, (size_t)n * 2, hipMemcpyHostToDevice, t_rv.sm)) != hipSuccess)
             return set_err(RFEC_EDEVICE, "recv: datagrams H2D", e);
-        dg = D;
-        dl = D + o_dl;
+        dg = st->dg;
+        dl = st->dg + o_dl;
     }
     const double h2d_issue = now_us() - tt;
-    int ke = rfec_launch_wire_parse(n, dstride, dg, (const uint16_t*)dl, stride, S->capacity,
-                                    (rfec_wire_rec*)t_rx.hd, S->arena + (size_t)S->nstore * stride,
-                                    max_dlen(dlen, n), t_rv.sm);
+    int ke = rfec_launch_wire_parse(n, dstride, dg, (const uint16_t*)dl, stride, S->capacity, S->store_d + S->nstore,
+                                    S->arena + (size_t)S->nstore * stride, max_dlen(dlen, n), t_rv.sm);
+    if (!ke)
+        ke = rx_split_launch(S, st, S->store_d + S->nstore, n, t_rv.sm);
     if (ke || (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
         return set_err(RFEC_EDEVICE, "recv: parse", ke ? ke : (int)e);
     const double staged = now_us() - tt;
     if (recs_out)
-        memcpy(recs_out, t_rx.h, (size_t)n * sizeof(rfec_wire_rec));
-    rc = rx_session_push_staged(S, n, (const rfec_wire_rec*)t_rx.h, NULL, out, out_payload, max_out, n_out, rep,
-                                t_rv.sm);
+        memcpy(recs_out, S->store + S->nstore, (size_t)n * sizeof(rfec_wire_rec));
+    rc = rx_session_push_staged(S, n, NULL, S->T > 1 && n <= (1u << 20) ? st->sum : NULL, out, out_payload, max_out,
+                                n_out, rep, t_rv.sm);
     rep->h2d_us += h2d_issue;
     rep->kernel_us += staged - h2d_issue; /* the H2D completes inside this interval too */
     rep->total_us = now_us() - t0;
@@ -2767,29 +2970,30 @@ int rfec_rx_session_push_datagrams(rfec_rx_session* S, uint32_t n, uint32_t dstr
 }
 
 /* The pipelined push: this call starts batch i (H2D if pageable, parse into
- * the arena's rows after the pending batch's, records into its stage's mapped
- * area, on the session's own stream) and then ingests batch i-1 (control
- * plane, peel on the thread's stream) while the device parses batch i. */
+ * the store's records and the arena's rows after the pending batch's, its
+ * split summary into its stage, on the session's own stream) and then
+ * ingests batch i-1 (control plane, peel on the thread's stream) while the
+ * device parses batch i. */
 static int rx_stage_reserve(rx_stage* st, uint32_t n, size_t dg_bytes)
 {
     hipError_t e;
     if (!st->done && (e = hipEventCreateWithFlags(&st->done, hipEventDisableTiming)) != hipSuccess)
         return set_err(RFEC_EDEVICE, "rx session: event", e);
-    if (st->reccap < n) {
+    if (st->sumcap < n) {
         const uint32_t c = n + n / 4 + 64;
         void* h = NULL;
         void* d = NULL;
-        if ((e = hipHostMalloc(&h, (size_t)c * sizeof(rfec_wire_rec), hipHostMallocMapped)) != hipSuccess)
-            return set_err(RFEC_ENOMEM, "rx session: record stage", e);
+        if ((e = hipHostMalloc(&h, (size_t)c * sizeof(rfec_rx_split), hipHostMallocMapped)) != hipSuccess)
+            return set_err(RFEC_ENOMEM, "rx session: split stage", e);
         if ((e = hipHostGetDevicePointer(&d, h, 0)) != hipSuccess) {
             (void)hipHostFree(h);
-            return set_err(RFEC_EDEVICE, "rx session: record stage device view", e);
+            return set_err(RFEC_EDEVICE, "rx session: split stage device view", e);
         }
-        if (st->rec)
-            (void)hipHostFree(st->rec);
-        st->rec = (rfec_wire_rec*)h;
-        st->recd = (rfec_wire_rec*)d;
-        st->reccap = c;
+        if (st->sum)
+            (void)hipHostFree(st->sum);
+        st->sum = (rfec_rx_split*)h;
+        st->sumd = (rfec_rx_split*)d;
+        st->sumcap = c;
     }
     if (dg_bytes > st->dgb) {
         if (st->dg)
@@ -2842,9 +3046,11 @@ int rfec_rx_session_push_datagrams_async(rfec_rx_session* S, uint32_t n, uint32_
             dl = st->dg + o_dl;
         }
         rep->h2d_us += now_us() - tt;
-        const int ke = rfec_launch_wire_parse(n, dstride, dg, (const uint16_t*)dl, S->stride, S->capacity, st->recd,
-                                              S->arena + (size_t)(S->nstore + p) * S->stride, max_dlen(dlen, n),
-                                              S->sa);
+        int ke = rfec_launch_wire_parse(n, dstride, dg, (const uint16_t*)dl, S->stride, S->capacity,
+                                        S->store_d + S->nstore + p, S->arena + (size_t)(S->nstore + p) * S->stride,
+                                        max_dlen(dlen, n), S->sa);
+        if (!ke)
+            ke = rx_split_launch(S, st, S->store_d + S->nstore + p, n, S->sa);
         if (ke || (e = hipEventRecord(st->done, S->sa)) != hipSuccess)
             return set_err(RFEC_EDEVICE, "rx session: parse", ke ? ke : (int)e);
     }
@@ -2856,9 +3062,10 @@ int rfec_rx_session_push_datagrams_async(rfec_rx_session* S, uint32_t n, uint32_
             return set_err(RFEC_EDEVICE, "rx session: parse", e);
         rep->kernel_us += now_us() - tt;
         if (recs_out)
-            memcpy(recs_out, ps->rec, (size_t)p * sizeof(rfec_wire_rec));
-        S->pend = -1; /* its rows are the arena's next p rows now */
-        rc = rx_session_push_staged(S, p, ps->rec, NULL, out, out_payload, max_out, n_out, rep, t_rv.sm);
+            memcpy(recs_out, S->store + S->nstore, (size_t)p * sizeof(rfec_wire_rec));
+        S->pend = -1; /* its records and rows are the store's and the arena's next p now */
+        rc = rx_session_push_staged(S, p, NULL, S->T > 1 && p <= (1u << 20) ? ps->sum : NULL, out, out_payload,
+                                    max_out, n_out, rep, t_rv.sm);
         if (rc) {
             S->pend = cur; /* batch i stays pending behind whatever was ingested */
             S->pend_n = n;

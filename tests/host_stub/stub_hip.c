@@ -277,6 +277,27 @@ int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map
     return 0;
 }
 
+/* the receiver session's batch split (k_rx_split): the same summary on the host */
+int rfec_launch_rx_split(const rfec_wire_rec* recs, uint32_t n, uint32_t T, rfec_rx_split* out, void* stream)
+{
+    (void)stream;
+    for (uint32_t p = 0; p < n; ++p) {
+        const rfec_wire_rec* r = &recs[p];
+        rfec_rx_split e = {0xFF, RX_SPLIT_NONE, 0, 0};
+        if (r->status == RFEC_WIRE_OK && r->mid == RFEC_WIRE_SEG) {
+            e.shard = (uint8_t)((r->fec_id ? r->fec_id : r->hdr.seq) % T);
+            e.kind = r->fec_id && r->hdr.seq ? RX_SPLIT_SEG_TS : RX_SPLIT_SEG;
+            e.value = r->hdr.ts;
+        } else if (r->status == RFEC_WIRE_OK && r->mid == RFEC_WIRE_FEC) {
+            e.shard = (uint8_t)(r->fec_id % T);
+            e.kind = RX_SPLIT_FEC;
+            e.value = r->send_ts + 3000u;
+        }
+        out[p] = e;
+    }
+    return 0;
+}
+
 int rfec_launch_zero_tails(uint32_t slots, uint32_t stride, uint8_t* shards, const rfec_hdr* hdr, void* stream)
 {
     return 0;

@@ -1,4 +1,4 @@
-# GPU box: host-plane sweep (stub lib, the box's CPUs), session bench sweep
+# GPU box: kernel trace of the receiver session (async, 16 shards)
 set -o pipefail
-for t in 1 4 8 16; do timeout -k 10 120 python -u tools/rx_host_bench.py --groups 65536 --no-verify --lib tools/bin/librazor_fec_rxhost.so --threads $t >> gpurun_out/rxh.log 2>&1 || exit 1; done && \
-RFEC_RX_ARENA_ROWS=1048576 timeout -k 10 400 python -u tools/rx_session_bench.py --frames 32768 --threads 1,8,16 --modes async,sync --out gpurun_out/rxs4.json > gpurun_out/rxs4.log 2>&1
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+RFEC_RX_SPIN_US=0 RFEC_RX_ARENA_ROWS=1048576 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/rxprof -o rx -- python3 tools/rx_session_bench.py --frames 32768 --threads 16 --modes async --reps 1 > gpurun_out/rxprof.log 2>&1
