@@ -79,6 +79,10 @@ int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, c
                            uint32_t max_len, void* stream);
 int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map, uint32_t rows, uint32_t stride,
                             void* stream);
+/* the receiver session's device stage (rfec_rx.c rx_device): dst row r <- src row map[r] (zeros for
+ * map[r] < 0; `map` may be pinned host memory), and tbytes (a multiple of 16) of tables tsrc -> tdst */
+int rfec_launch_rx_stage(uint8_t* dst, const uint8_t* src, const int32_t* map, uint32_t rows, uint32_t stride,
+                         void* tdst, const void* tsrc, size_t tbytes, void* stream);
 /* The receiver session's batch split, per parsed record (rfec_rx.c rx_phase0): its shard (fec_id % T, a
  * segment outside FEC by packet id; 0xFF: no effect on the control plane), its kind (RX_SPLIT_*) and the
  * value the replay's max_ts rules read (a segment's timestamp, a parity's send_ts + 3000). */

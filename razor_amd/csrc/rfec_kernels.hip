@@ -2072,6 +2072,33 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows(v4u* __restrict__ dst, c
     st16(dst + (size_t)r * C + j, v);
 }
 
+// The receiver session's device stage of one ingestion call (rfec_rx.c
+// rx_device): the delivering groups' member and parity rows gathered from the
+// row arena by a map the host wrote into pinned memory (read over PCIe by the
+// lanes themselves), and, by the lanes after them, the host's tables (header
+// records, masks, sizes, the output map) copied from pinned into device
+// memory -- one launch where an H2D copy and two gathers ran in sequence (each
+// step a few us of dispatch latency for ~5 MB of rows per 4,096-datagram
+// batch).  The rows are stored with the default policy: the decode reads them
+// next.
+__global__ __launch_bounds__(kBlock) void k_rx_stage(v4u* __restrict__ dst, const v4u* __restrict__ src,
+                                                     const int32_t* __restrict__ map, uint32_t total, uint32_t C,
+                                                     FastDiv divC, v4u* __restrict__ tdst,
+                                                     const v4u* __restrict__ tsrc, uint32_t tchunks)
+{
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t < total) {
+        const uint32_t r = fdiv(t, divC);
+        const uint32_t j = t - r * C;
+        const int32_t s = map[r];
+        dst[(size_t)r * C + j] = s >= 0 ? ld16(src + (size_t)s * C + j) : v4u{0, 0, 0, 0};
+        return;
+    }
+    const uint32_t u = t - total;
+    if (u < tchunks)
+        tdst[u] = tsrc[u];
+}
+
 // Receiver groups above RFEC_MAX_K segments (a foreign peer's flexes): one
 // line job per recovered segment, recovered = parity ^ the line's present
 // members (flex_fec_xor.c:73-95), the host's peel in dependency levels (one
@@ -2670,6 +2697,22 @@ int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map
         return 0;
     RFEC_LAUNCH(k_gather_rows, dim3(blocks_for(total)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
                 reinterpret_cast<v4u*>(dst), reinterpret_cast<const v4u*>(src), map, total, C, make_fastdiv(C));
+    return (int)hipGetLastError();
+}
+
+int rfec_launch_rx_stage(uint8_t* dst, const uint8_t* src, const int32_t* map, uint32_t rows, uint32_t stride,
+                         void* tdst, const void* tsrc, size_t tbytes, void* stream)
+{
+    const uint32_t C = stride / 16;
+    const uint64_t total = (uint64_t)rows * C, tchunks = (tbytes + 15) / 16;
+    if (total + tchunks >= (1ull << 32) || stride % 16)
+        return (int)hipErrorInvalidValue;
+    if (!(total + tchunks))
+        return 0;
+    RFEC_LAUNCH(k_rx_stage, dim3(blocks_for(total + tchunks)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream),
+                reinterpret_cast<v4u*>(dst), reinterpret_cast<const v4u*>(src), map, (uint32_t)total, C,
+                make_fastdiv(C ? C : 1), reinterpret_cast<v4u*>(tdst), reinterpret_cast<const v4u*>(tsrc),
+                (uint32_t)tchunks);
     return (int)hipGetLastError();
 }
 

@@ -121,22 +121,30 @@ static void hm_del(hmap* m, uint32_t k) /* backward-shift deletion */
  * hashing, no probing, no rehash, and the key order is the walk order (the
  * evictions' sorted walks).  (An open-addressing hash spent 35-70 % of the
  * control plane in probes that missed the cache, and its growth in page
- * faults.) */
+ * faults.)  Each level keeps a bitmap of what is occupied below it, so a walk
+ * (pm_next) skips empty directory slots, leaves and values by bit scans: the
+ * evictions and compaction walk the open state, not the key space (the
+ * directory scan from key 0 was ~30 % of the control plane with an eviction
+ * per batch). */
 #define PM_LEAF_BITS 8
 #define PM_MID_BITS 10
 #define PM_DIR_BITS (32 - PM_LEAF_BITS - PM_MID_BITS)
 #define PM_LEAF (1u << PM_LEAF_BITS)
 #define PM_MID (1u << PM_MID_BITS)
+#define PM_DIR (1u << PM_DIR_BITS)
 typedef struct {
     uint32_t n;
+    uint64_t bits[PM_LEAF / 64]; /* values != 0 */
     uint32_t v[PM_LEAF];
 } pm_leaf;
 typedef struct {
     pm_leaf* leaf[PM_MID];
+    uint64_t bits[PM_MID / 64]; /* leaves present */
     uint32_t nleaf;
 } pm_mid;
 typedef struct {
-    pm_mid** dir; /* [1 << PM_DIR_BITS] */
+    pm_mid** dir; /* [PM_DIR] */
+    uint64_t* dbits; /* [PM_DIR / 64]: mids present */
     uint32_t n;   /* entries */
     uint32_t last_pg;
     pm_leaf* last; /* the leaf of page last_pg (key >> PM_LEAF_BITS), or NULL */
@@ -145,20 +153,22 @@ typedef struct {
 static int pm_init(pmap* m)
 {
     memset(m, 0, sizeof(*m));
-    m->dir = (pm_mid**)calloc((size_t)1 << PM_DIR_BITS, sizeof(pm_mid*));
-    return m->dir ? 0 : -1;
+    m->dir = (pm_mid**)calloc(PM_DIR, sizeof(pm_mid*));
+    m->dbits = (uint64_t*)calloc(PM_DIR / 64, sizeof(uint64_t));
+    return m->dir && m->dbits ? 0 : -1;
 }
 
 static void pm_free(pmap* m)
 {
     if (m->dir)
-        for (uint32_t d = 0; d < (1u << PM_DIR_BITS); ++d)
+        for (uint32_t d = 0; d < PM_DIR; ++d)
             if (m->dir[d]) {
                 for (uint32_t l = 0; l < PM_MID; ++l)
                     free(m->dir[d]->leaf[l]);
                 free(m->dir[d]);
             }
     free(m->dir);
+    free(m->dbits);
     memset(m, 0, sizeof(*m));
 }
 
@@ -186,20 +196,28 @@ static int pm_put(pmap* m, uint32_t k, uint32_t v) /* v != 0 */
 {
     pm_leaf* f = pm_find(m, k);
     if (!f) {
-        const uint32_t pg = k >> PM_LEAF_BITS;
-        pm_mid** d = &m->dir[pg >> PM_MID_BITS];
-        if (!*d && !(*d = (pm_mid*)calloc(1, sizeof(pm_mid))))
-            return -1;
+        const uint32_t pg = k >> PM_LEAF_BITS, di = pg >> PM_MID_BITS, li = pg & (PM_MID - 1);
+        pm_mid** d = &m->dir[di];
+        if (!*d) {
+            if (!(*d = (pm_mid*)calloc(1, sizeof(pm_mid))))
+                return -1;
+            m->dbits[di >> 6] |= 1ull << (di & 63);
+        }
         if (!(f = (pm_leaf*)calloc(1, sizeof(pm_leaf))))
             return -1;
-        (*d)->leaf[pg & (PM_MID - 1)] = f;
+        (*d)->leaf[li] = f;
+        (*d)->bits[li >> 6] |= 1ull << (li & 63);
         (*d)->nleaf++;
         m->last = f;
         m->last_pg = pg;
     }
-    uint32_t* s = &f->v[k & (PM_LEAF - 1)];
-    f->n += *s == 0;
-    m->n += *s == 0;
+    const uint32_t i = k & (PM_LEAF - 1);
+    uint32_t* s = &f->v[i];
+    if (*s == 0) {
+        f->n++;
+        m->n++;
+        f->bits[i >> 6] |= 1ull << (i & 63);
+    }
     *s = v;
     return 0;
 }
@@ -207,47 +225,72 @@ static int pm_put(pmap* m, uint32_t k, uint32_t v) /* v != 0 */
 static void pm_del(pmap* m, uint32_t k)
 {
     pm_leaf* f = pm_find(m, k);
-    uint32_t* s = f ? &f->v[k & (PM_LEAF - 1)] : NULL;
+    const uint32_t i = k & (PM_LEAF - 1);
+    uint32_t* s = f ? &f->v[i] : NULL;
     if (!s || !*s)
         return;
     *s = 0;
+    f->bits[i >> 6] &= ~(1ull << (i & 63));
     m->n--;
     if (--f->n == 0) { /* the leaf (and an empty mid) go */
-        const uint32_t pg = k >> PM_LEAF_BITS;
-        pm_mid** d = &m->dir[pg >> PM_MID_BITS];
-        (*d)->leaf[pg & (PM_MID - 1)] = NULL;
+        const uint32_t pg = k >> PM_LEAF_BITS, di = pg >> PM_MID_BITS, li = pg & (PM_MID - 1);
+        pm_mid** d = &m->dir[di];
+        (*d)->leaf[li] = NULL;
+        (*d)->bits[li >> 6] &= ~(1ull << (li & 63));
         free(f);
         if (--(*d)->nleaf == 0) {
             free(*d);
             *d = NULL;
+            m->dbits[di >> 6] &= ~(1ull << (di & 63));
         }
         m->last = NULL;
     }
+}
+
+/* the first set bit of bits[0, nbits) at or after `from`, or nbits */
+static uint32_t pm_scan(const uint64_t* bits, uint32_t nbits, uint32_t from)
+{
+    if (from >= nbits)
+        return nbits;
+    uint32_t w = from >> 6;
+    uint64_t x = bits[w] & (~0ull << (from & 63));
+    while (!x) {
+        if (++w >= nbits / 64)
+            return nbits;
+        x = bits[w];
+    }
+    return w * 64 + (uint32_t)__builtin_ctzll(x);
 }
 
 /* In key order: the next entry at or after *key (its value's address, the key
  * in *key), NULL past the last.  Start with *key = 0; continue from key + 1. */
 static uint32_t* pm_next(const pmap* m, uint32_t* key, uint32_t* done)
 {
-    uint64_t k = *key;
-    while (k < (1ull << 32)) {
-        const uint32_t pg = (uint32_t)(k >> PM_LEAF_BITS);
-        const pm_mid* d = m->dir[pg >> PM_MID_BITS];
-        if (!d) {
-            k = ((uint64_t)(pg >> PM_MID_BITS) + 1) << (PM_MID_BITS + PM_LEAF_BITS);
+    uint32_t pg = *key >> PM_LEAF_BITS, i = *key & (PM_LEAF - 1);
+    uint32_t di = pg >> PM_MID_BITS, li = pg & (PM_MID - 1);
+    if (!m->dir) {
+        *done = 1;
+        return NULL;
+    }
+    for (;;) {
+        const pm_mid* d = m->dir[di];
+        if (!d) { /* the next mid */
+            if ((di = pm_scan(m->dbits, PM_DIR, di + 1)) >= PM_DIR)
+                break;
+            li = i = 0;
             continue;
         }
-        pm_leaf* f = d->leaf[pg & (PM_MID - 1)];
-        if (!f) {
-            k = ((uint64_t)pg + 1) << PM_LEAF_BITS;
-            continue;
+        pm_leaf* f = d->leaf[li];
+        if (f && (i = pm_scan(f->bits, PM_LEAF, i)) < PM_LEAF) {
+            *key = (di << (PM_MID_BITS + PM_LEAF_BITS)) | (li << PM_LEAF_BITS) | i;
+            return &f->v[i];
         }
-        for (uint32_t i = (uint32_t)k & (PM_LEAF - 1); i < PM_LEAF; ++i)
-            if (f->v[i]) {
-                *key = (pg << PM_LEAF_BITS) | i;
-                return &f->v[i];
-            }
-        k = ((uint64_t)pg + 1) << PM_LEAF_BITS;
+        i = 0;
+        if ((li = pm_scan(d->bits, PM_MID, li + 1)) < PM_MID)
+            continue;
+        if ((di = pm_scan(m->dbits, PM_DIR, di + 1)) >= PM_DIR)
+            break;
+        li = 0;
     }
     *done = 1;
     return NULL;
@@ -313,6 +356,7 @@ typedef struct {
 /* into one (the session then stays serial).                                */
 /* ------------------------------------------------------------------------ */
 #define RX_MAX_THREADS 64 /* shards (= replay threads) of a session */
+#define RX_PREFETCH 8     /* records prefetched ahead by a shard's replay */
 
 
 #define RX_CONFLICT_OWNER 1
@@ -328,6 +372,7 @@ typedef struct { /* one batch's parallel replay, shared by the shards */
     uint32_t a0;          /* the batch's first record */
     int ts_check;         /* recoveries checked against smin (the parallel replay) */
     int conflict;         /* RX_CONFLICT_* (atomic) */
+    double t0;            /* the replay's start (now_us), for the per-shard timings */
 } rx_par;
 
 typedef struct {
@@ -365,6 +410,8 @@ typedef struct {
     const uint32_t* sminp; /* this batch's smin: P->smin, or sminl (computed by this shard's thread) */
     uint32_t* sminl;
     uint32_t sminlcap;
+    uint32_t* mine;     /* this shard's records of the batch (the device's split) */
+    uint32_t minecap;
     uint64_t* claims;   /* this batch's packet-id claims: seq << 32 | fec_id + 1 */
     uint32_t nclaims, claimcap;
     uint64_t* cpart;    /* the claims by owner-table partition (rx_bucket_claims), offsets in coff */
@@ -377,6 +424,8 @@ typedef struct {
     uint32_t njops, jopcap;
     uint8_t* jsave;
     size_t njsave, jsavecap;
+    double tw_wake, tw_run; /* parallel replays: this shard's start after the replay's, and its run (us, summed) */
+    uint32_t tw_n, tw_recs;
 } rx_sim;
 
 #define RX_GROW_F(flag, ptr, n, cap, need, T)                                          \
@@ -1034,6 +1083,7 @@ static void rx_sim_free(rx_sim* X)
     free(X->jsave);
     free(X->claims);
     free(X->sminl);
+    free(X->mine);
     free(X->cpart);
     free(X->claimed);
 }
@@ -1190,6 +1240,7 @@ static void rx_run(rx_sim* X, uint32_t a0, uint32_t n)
 typedef struct {
     const rx_shape* sh; /* any shard's shape of this geometry (plans are a function of it) */
     uint32_t n_groups, row0, prow0, group0;
+    uint32_t E, dense0; /* dense output slots per group, the shape's first dense row */
 } rx_dclass;
 
 typedef struct {
@@ -1454,7 +1505,7 @@ static int rx_device(rx_sim* const* XS, uint32_t T, rx_dev* D, const uint8_t* ro
                 RX_GROW_F(D->oom, D->C, D->nc, D->ccap, 1, rx_dclass);
                 if (D->oom)
                     return set_err(RFEC_ENOMEM, "rx: device shapes", 0);
-                D->C[D->nc++] = (rx_dclass){sh, 0, 0, 0, 0};
+                D->C[D->nc++] = (rx_dclass){sh, 0, 0, 0, 0, 0, 0};
             }
             *c = k + 1;
         }
@@ -1537,7 +1588,32 @@ static int rx_device(rx_sim* const* XS, uint32_t T, rx_dev* D, const uint8_t* ro
             if (job_of[i] >= 0)
                 job_of[i] = (int32_t)jperm[job_of[i]];
     }
-    const size_t o_smap = 0, o_pmap = RX_ALIGN((size_t)nrows * 4), o_hdr = RX_ALIGN(o_pmap + (size_t)prows * 4);
+    /* dense output per device shape: E slots per group, the shape's largest erasure count among its
+       delivering groups (the e-th erased member of a group, index order, goes to slot e) */
+    for (uint32_t k = 0; k < D->nc; ++k)
+        D->C[k].E = 0;
+    for (uint32_t d = 0; d < D->ndl; ++d) {
+        const uint32_t t = (uint32_t)(D->dl[d] >> 32);
+        const rx_sim* X = XS[t];
+        const rx_inst* g = &X->G[(uint32_t)D->dl[d]];
+        if (rx_line_jobs(&X->S[g->shape]))
+            continue;
+        rx_dclass* C = RX_CLASS(t, g);
+        const uint32_t er = g->count - (uint32_t)(__builtin_popcountll(g->arrived[0]) + __builtin_popcountll(g->arrived[1]));
+        C->E = er > C->E ? er : C->E;
+    }
+    uint32_t ndense = 0;
+    for (uint32_t k = 0; k < D->nc; ++k) {
+        rx_dclass* C = &D->C[k];
+        if (rx_line_jobs(C->sh) || !C->n_groups)
+            continue;
+        C->E = C->E < 1 ? 1 : C->E > C->sh->count ? C->sh->count : C->E;
+        C->dense0 = ndense;
+        ndense += C->n_groups * C->E;
+    }
+    /* rows on the device, one region: [nrows members][njobs line-job outputs][prows parities][ndense] */
+    const uint32_t r_job = nrows, r_par = nrows + D->njobs, r_dense = r_par + prows, nmap = r_dense;
+    const size_t o_map = 0, o_hdr = RX_ALIGN((size_t)nmap * 4);
     const size_t o_meta = RX_ALIGN(o_hdr + (size_t)nrows * sizeof(rfec_hdr));
     const size_t o_fs = RX_ALIGN(o_meta + (size_t)prows * sizeof(rfec_hdr));
     const size_t o_pres = RX_ALIGN(o_fs + (size_t)prows * 2), o_pp = RX_ALIGN(o_pres + (size_t)ngs * 16);
@@ -1549,9 +1625,9 @@ static int rx_device(rx_sim* const* XS, uint32_t T, rx_dev* D, const uint8_t* ro
     for (uint32_t k = 0; k < D->nc; ++k)
         if (!rx_line_jobs(D->C[k].sh))
             ws_bytes += RX_ALIGN(rfec_recover_workspace_size(&D->C[k].sh->plan, D->C[k].n_groups));
-    const size_t d_shards = o_in_end, d_par = RX_ALIGN(d_shards + ((size_t)nrows + D->njobs) * stride);
-    const size_t d_ws = RX_ALIGN(d_par + (size_t)prows * stride), d_rec = RX_ALIGN(d_ws + ws_bytes);
-    const size_t d_out = RX_ALIGN(d_rec + (size_t)ngs * 16), dev_bytes = RX_ALIGN(d_out + (size_t)D->nev * stride);
+    const size_t d_rows = o_in_end, d_ws = RX_ALIGN(d_rows + ((size_t)r_dense + ndense) * stride);
+    const size_t d_ohdr = RX_ALIGN(d_ws + ws_bytes), d_oidx = RX_ALIGN(d_ohdr + (size_t)ndense * sizeof(rfec_hdr));
+    const size_t d_out = RX_ALIGN(d_oidx + ndense), dev_bytes = RX_ALIGN(d_out + (size_t)D->nev * stride);
     if ((rc = rx_reserve(hoff + host_bytes, dev_bytes, hoff))) {
         free(job_of);
         free(jperm);
@@ -1561,15 +1637,16 @@ static int rx_device(rx_sim* const* XS, uint32_t T, rx_dev* D, const uint8_t* ro
         for (uint32_t t = 0; t < T; ++t)
             XS[t]->R = (const rfec_wire_rec*)t_rx.h;
     uint8_t* H = t_rx.h + hoff;
-    memset(H, 0, o_in_end);
-    int32_t* smap = (int32_t*)(H + o_smap);
-    int32_t* pmap = (int32_t*)(H + o_pmap);
+    uint8_t* Hd = t_rx.hd + hoff; /* H as the device addresses it */
+    int32_t* map = (int32_t*)(H + o_map);
     rfec_hdr* hh = (rfec_hdr*)(H + o_hdr);
     rfec_hdr* mh = (rfec_hdr*)(H + o_meta);
     uint16_t* fsz = (uint16_t*)(H + o_fs);
     uint64_t* pres = (uint64_t*)(H + o_pres);
     uint64_t* ppm = (uint64_t*)(H + o_pp);
     int32_t* omap = (int32_t*)(H + o_omap);
+    for (uint32_t j = 0; j < D->njobs; ++j)
+        map[r_job + j] = -1;
     if (D->njobs) {
         memcpy(H + o_jobs, D->jobs, (size_t)D->njobs * sizeof(rfec_line_job));
         memcpy(H + o_jmem, D->jmem, (size_t)D->njmem * 4);
@@ -1589,20 +1666,26 @@ static int rx_device(rx_sim* const* XS, uint32_t T, rx_dev* D, const uint8_t* ro
         ppm[gg] = g->ppm;
         for (uint32_t i = 0; i < sh->count; ++i) {
             const int32_t src = X->slot_src[g->slot0 + i];
-            smap[r0 + i] = src;
+            map[r0 + i] = src;
             if (src >= 0)
                 hh[r0 + i] = X->slot_hdr[g->slot0 + i];
+            else
+                memset(&hh[r0 + i], 0, sizeof(rfec_hdr));
         }
         for (uint32_t l = 0; l < sh->n_lines; ++l) {
             const int32_t src = X->line_par[g->line0 + l];
-            pmap[p0 + l] = src;
+            map[r_par + p0 + l] = src;
             if (src >= 0) {
                 mh[p0 + l] = X->R[src].hdr;
                 fsz[p0 + l] = X->R[src].data_size;
+            } else {
+                memset(&mh[p0 + l], 0, sizeof(rfec_hdr));
+                fsz[p0 + l] = 0;
             }
         }
     }
-    /* output rows: the recovering group's slot */
+    /* output rows: the recovering group's dense slot (its rank among the group's erased members), or the
+       line job that recovers it */
     uint32_t nok = 0;
     for (uint32_t q = 0; q < D->nev; ++q) {
         const rx_event* ev = &D->ev[q];
@@ -1610,10 +1693,18 @@ static int rx_device(rx_sim* const* XS, uint32_t T, rx_dev* D, const uint8_t* ro
         const rx_inst* g = &X->G[ev->inst];
         const rx_shape* sh = &X->S[g->shape];
         const uint32_t t = ev->hdr.seq - g->base;
-        if (rx_line_jobs(sh)) /* the job that recovers t */
-            omap[q] = t < g->count && job_of[g->gslot + t] >= 0 ? (int32_t)(nrows + (uint32_t)job_of[g->gslot + t]) : -1;
-        else
-            omap[q] = t < g->count ? (int32_t)(RX_CLASS(ev->shard, g)->row0 + g->gslot * sh->count + t) : -1;
+        if (rx_line_jobs(sh)) { /* the job that recovers t */
+            omap[q] = t < g->count && job_of[g->gslot + t] >= 0 ? (int32_t)(r_job + (uint32_t)job_of[g->gslot + t]) : -1;
+            continue;
+        }
+        const rx_dclass* C = RX_CLASS(ev->shard, g);
+        uint32_t e = UINT32_MAX;
+        if (t < g->count && !((g->arrived[t >> 6] >> (t & 63)) & 1ull)) {
+            const uint64_t lo = t >= 64 ? ~g->arrived[0] : ~g->arrived[0] & ((1ull << t) - 1);
+            const uint64_t hi = t >= 64 ? ~g->arrived[1] & ((1ull << (t - 64)) - 1) : 0;
+            e = (uint32_t)(__builtin_popcountll(lo) + __builtin_popcountll(hi));
+        }
+        omap[q] = e < C->E ? (int32_t)(r_dense + C->dense0 + g->gslot * C->E + e) : -1;
     }
     free(job_of);
     free(jperm);
@@ -1621,29 +1712,30 @@ static int rx_device(rx_sim* const* XS, uint32_t T, rx_dev* D, const uint8_t* ro
     rep->n_groups = ngs;
     for (uint32_t k = 0; k < D->nc; ++k)
         rep->n_shapes += D->C[k].n_groups != 0;
-    /* the device: rows in place, one peel per device shape, the delivered rows compacted */
+    /* the device: rows and tables staged in one launch, one dense peel per device shape writing its
+       recovered masks into pinned memory, the delivered rows gathered out; one synchronisation */
     uint8_t* Dv = t_rx.d;
+    uint8_t* rows_d = Dv + d_rows;
     double tt = now_us();
-    if ((e = hipMemcpyAsync(Dv, H, o_in_end, hipMemcpyHostToDevice, sm)) != hipSuccess)
-        return set_err(RFEC_EDEVICE, "rx: H2D", e);
-    ke = rfec_launch_gather_rows(Dv + d_shards, rows, (const int32_t*)(Dv + o_smap), nrows, stride, sm);
-    if (!ke)
-        ke = rfec_launch_gather_rows(Dv + d_par, rows, (const int32_t*)(Dv + o_pmap), prows, stride, sm);
+    ke = rfec_launch_rx_stage(rows_d, rows, (const int32_t*)(Hd + o_map), nmap, stride, Dv, Hd, o_in_end, sm);
     for (uint32_t v = 1, lo = 0; v <= maxlvl && !ke; lo += lvl_n[v], ++v) /* the large groups' line jobs */
         ke = rfec_launch_line_jobs((const rfec_line_job*)(Dv + o_jobs) + lo, lvl_n[v], (const int32_t*)(Dv + o_jmem),
-                                   rows, Dv + d_shards + (size_t)nrows * stride, stride, sm);
+                                   rows, rows_d + (size_t)r_job * stride, stride, sm);
     size_t wso = 0;
+    uint64_t* rec_d = (uint64_t*)(Hd + o_rec);
     for (uint32_t k = 0; k < D->nc && !ke; ++k) {
         const rx_dclass* C = &D->C[k];
         if (!C->n_groups || rx_line_jobs(C->sh))
             continue;
         rfec_kmask M;
         make_masks(&C->sh->plan, &M);
-        ke = rfec_launch_recover(&M, C->n_groups, stride, capacity, Dv + d_shards + (size_t)C->row0 * stride,
-                                 (rfec_hdr*)(Dv + o_hdr) + C->row0, (const uint64_t*)(Dv + o_pres) + 2 * C->group0,
-                                 Dv + d_par + (size_t)C->prow0 * stride, (const rfec_hdr*)(Dv + o_meta) + C->prow0,
-                                 (const uint16_t*)(Dv + o_fs) + C->prow0, (const uint64_t*)(Dv + o_pp) + C->group0,
-                                 (uint64_t*)(Dv + d_rec) + 2 * C->group0, Dv + d_ws + wso, sm, g_tuning);
+        const rfec_dense_out DO = {rows_d + ((size_t)r_dense + C->dense0) * stride,
+                                   (rfec_hdr*)(Dv + d_ohdr) + C->dense0, Dv + d_oidx + C->dense0, C->E};
+        ke = rfec_launch_recover_out(&M, C->n_groups, stride, capacity, rows_d + (size_t)C->row0 * stride,
+                                     (const rfec_hdr*)(Dv + o_hdr) + C->row0, (const uint64_t*)(Dv + o_pres) + 2 * C->group0,
+                                     rows_d + ((size_t)r_par + C->prow0) * stride, (const rfec_hdr*)(Dv + o_meta) + C->prow0,
+                                     (const uint16_t*)(Dv + o_fs) + C->prow0, (const uint64_t*)(Dv + o_pp) + C->group0,
+                                     rec_d + 2 * C->group0, Dv + d_ws + wso, sm, g_tuning, &DO);
         wso += RX_ALIGN(rfec_recover_workspace_size(&C->sh->plan, C->n_groups));
     }
     /* delivered rows: straight into the caller's output when it is pinned and
@@ -1651,11 +1743,10 @@ static int rx_device(rx_sim* const* XS, uint32_t T, rx_dev* D, const uint8_t* ro
        squeezed out on the host below), else into the device staging */
     uint8_t* outd = D->nev && D->nev <= max_out ? (uint8_t*)host_mapped(out_payload) : NULL;
     if (!ke && D->nev)
-        ke = rfec_launch_gather_rows(outd ? outd : Dv + d_out, Dv + d_shards, (const int32_t*)(Dv + o_omap), D->nev,
-                                     stride, sm);
+        ke = rfec_launch_gather_rows(outd ? outd : Dv + d_out, rows_d, (const int32_t*)(Dv + o_omap), D->nev, stride,
+                                     sm);
     uint64_t* rec = (uint64_t*)(H + o_rec);
-    if (ke || (e = hipMemcpyAsync(rec, Dv + d_rec, (size_t)ngs * 16, hipMemcpyDeviceToHost, sm)) != hipSuccess ||
-        (e = hipStreamSynchronize(sm)) != hipSuccess)
+    if (ke || (e = hipStreamSynchronize(sm)) != hipSuccess)
         return set_err(RFEC_EDEVICE, "rx: recover", ke ? ke : (int)e);
     rep->kernel_us += now_us() - tt;
     /* the device peel covers every packet the arrival-order pass delivered (same lines, a superset of
@@ -1667,7 +1758,7 @@ static int rx_device(rx_sim* const* XS, uint32_t T, rx_dev* D, const uint8_t* ro
         const int big = rx_line_jobs(&X->S[g->shape]);
         const uint32_t t = ev->hdr.seq - g->base;
         const uint32_t gg = big ? 0 : RX_CLASS(ev->shard, g)->group0 + g->gslot;
-        if (big ? omap[q] < 0 : t >= g->count || !((rec[2 * gg + (t >> 6)] >> (t & 63)) & 1ull)) {
+        if (omap[q] < 0 || (!big && !((rec[2 * gg + (t >> 6)] >> (t & 63)) & 1ull))) {
             D->unmodelled++;
             omap[q] = -1;
             continue;
@@ -1873,6 +1964,7 @@ struct rx_pool {
     pthread_t th[RX_MAX_THREADS];
     rx_worker w[RX_MAX_THREADS];
     uint32_t nth; /* workers started */
+    uint32_t base; /* the first worker's index: 1 (the caller runs fn(arg, 0)) or 0 (workers run every index) */
     pthread_mutex_t mu;
     pthread_cond_t go, fin;
     uint32_t gen, done; /* atomics */
@@ -1983,9 +2075,10 @@ static int rx_worker_cpus(cpu_set_t* set)
     return CPU_COUNT(set) >= 2;
 }
 
-static int pool_start(rx_pool* P, uint32_t workers)
+static int pool_start(rx_pool* P, uint32_t workers, uint32_t base)
 {
     memset(P, 0, sizeof(*P));
+    P->base = base;
     pthread_mutex_init(&P->mu, NULL);
     pthread_cond_init(&P->go, NULL);
     pthread_cond_init(&P->fin, NULL);
@@ -1995,7 +2088,7 @@ static int pool_start(rx_pool* P, uint32_t workers)
     if (rx_worker_cpus(&cpus))
         pthread_attr_setaffinity_np(&attr, sizeof(cpus), &cpus);
     for (uint32_t i = 0; i < workers; ++i) {
-        P->w[i] = (rx_worker){P, i + 1};
+        P->w[i] = (rx_worker){P, i + P->base};
         if (pthread_create(&P->th[i], &attr, pool_main, &P->w[i])) {
             pthread_attr_destroy(&attr);
             return -1;
@@ -2020,7 +2113,7 @@ static void pool_stop(rx_pool* P)
     P->nth = 0;
 }
 
-/* fn(arg, 0) here and fn(arg, i) on worker i, 1 <= i <= nth; returns when all are done */
+/* fn(arg, 0) here (base 1) and fn(arg, i) on the workers; returns when all are done */
 static void pool_run(rx_pool* P, void (*fn)(void*, uint32_t), void* arg)
 {
     P->fn = fn;
@@ -2030,7 +2123,8 @@ static void pool_run(rx_pool* P, void (*fn)(void*, uint32_t), void* arg)
     __atomic_add_fetch(&P->gen, 1u, __ATOMIC_ACQ_REL);
     pthread_cond_broadcast(&P->go);
     pthread_mutex_unlock(&P->mu);
-    fn(arg, 0);
+    if (P->base)
+        fn(arg, 0);
     const double t0 = now_us();
     for (uint32_t i = 0; __atomic_load_n(&P->done, __ATOMIC_ACQUIRE) < P->nth; ++i) {
         cpu_relax();
@@ -2066,6 +2160,10 @@ struct rfec_rx_session {
     uint32_t nstore, storecap;
     uint8_t* arena; /* [arows][stride]: rows [0, nstore) ingested, then the pending batch's */
     uint32_t arows;
+    uint8_t* spare; /* the previous arena ([sprows][stride]): the next compaction's target when large enough */
+    uint32_t sprows;
+    int32_t* dmap;  /* compaction's row map on the device, [dmapcap] */
+    uint32_t dmapcap;
     uint32_t stride, capacity;
     /* pipelined push (rfec_rx_session_push_datagrams_async) */
     hipStream_t sa;
@@ -2117,7 +2215,11 @@ static int rx_shards_init(rfec_rx_session* S, uint32_t T)
         X->capacity = S->capacity;
     }
     if (T > 1) {
-        if (pool_start(&S->pool, T - 1)) {
+        /* RFEC_RX_CALLER=0: the calling thread replays no shard (every shard on the pinned workers, which
+           share one last-level cache; the caller may run elsewhere) */
+        const char* c = getenv("RFEC_RX_CALLER");
+        const uint32_t base = c && c[0] == '0' ? 0u : 1u;
+        if (pool_start(&S->pool, T - base, base)) {
             S->pool_on = 1;
             return -1;
         }
@@ -2192,6 +2294,12 @@ void rfec_rx_session_destroy(rfec_rx_session* s)
         (void)hipStreamDestroy(s->sa);
     if (s->pool_on)
         pool_stop(&s->pool);
+    if (getenv("RFEC_RX_TRACE"))
+        for (uint32_t t = 0; t < s->T; ++t)
+            if (s->XS[t] && s->XS[t]->tw_n)
+                fprintf(stderr, "rx shard %u: %u replays, start +%.1f us, run %.1f us, %.1f journal ops (per replay)\n",
+                        t, s->XS[t]->tw_n, s->XS[t]->tw_wake / s->XS[t]->tw_n, s->XS[t]->tw_run / s->XS[t]->tw_n,
+                        (double)s->XS[t]->tw_recs / s->XS[t]->tw_n);
     rx_shards_free(s);
     rx_dev_free(&s->dev);
     if (s->vown_on)
@@ -2204,6 +2312,10 @@ void rfec_rx_session_destroy(rfec_rx_session* s)
         (void)hipHostFree(s->store);
     if (s->arena)
         (void)hipFree(s->arena);
+    if (s->spare)
+        (void)hipFree(s->spare);
+    if (s->dmap)
+        (void)hipFree(s->dmap);
     free(s);
 }
 
@@ -2370,11 +2482,23 @@ static int rx_phase0(rfec_rx_session* S, uint32_t a0, uint32_t n, const rfec_rx_
 }
 
 /* shard t replays its records of the batch in arrival order */
+static void rx_shard_replay(rfec_rx_session* S, rx_sim* X, const rx_par* P, uint32_t t);
 static void rx_shard_job(void* arg, uint32_t t)
 {
     rfec_rx_session* S = (rfec_rx_session*)arg;
     rx_sim* X = S->XS[t];
     const rx_par* P = &S->par;
+    const double ts = now_us();
+    const uint32_t ng0 = X->njops;
+    X->tw_wake += ts - P->t0;
+    X->tw_n++;
+    rx_shard_replay(S, X, P, t);
+    X->tw_recs += X->njops - ng0;
+    X->tw_run += now_us() - ts;
+}
+
+static void rx_shard_replay(rfec_rx_session* S, rx_sim* X, const rx_par* P, uint32_t t)
+{
     if (P->sum) {
         /* the device's split: this thread walks the whole summary (8 B a record), replays its own records,
            keeps the batch's running segment timestamp (a parity below it: the batch replays in order) and
@@ -2391,8 +2515,12 @@ static void rx_shard_job(void* arg, uint32_t t)
                 m = sum[p].value;
         }
         X->sminp = X->sminl;
-        uint32_t pm = P->max0, k = 0;
-        for (uint32_t p = 0; p < n && !X->oom; ++p) {
+        /* this shard's records of the batch, and the drop check over the whole batch */
+        RX_GROW(X->mine, 0, X->minecap, n, uint32_t);
+        if (X->oom)
+            return;
+        uint32_t pm = P->max0, nm = 0;
+        for (uint32_t p = 0; p < n; ++p) {
             const rfec_rx_split e = sum[p];
             if (e.kind == RX_SPLIT_SEG_TS && e.value > pm) {
                 pm = e.value;
@@ -2400,11 +2528,21 @@ static void rx_shard_job(void* arg, uint32_t t)
                 rx_conflict(X, RX_CONFLICT_RISKY);
                 return;
             }
-            if (e.shard != t)
-                continue;
-            if ((k++ & 15) == 0 && __atomic_load_n(&S->par.conflict, __ATOMIC_RELAXED))
+            X->mine[nm] = P->a0 + p;
+            nm += e.shard == t;
+        }
+        /* the records, prefetched a few arrivals ahead: the device wrote them (cache-cold here) and a shard's
+           records are scattered over the batch, so the hardware prefetcher does not follow them (each one a
+           DRAM round trip: a shard replayed 3-4 x slower per arrival than one thread over the whole batch) */
+        const rfec_wire_rec* R = X->R;
+        for (uint32_t i = 0; i < nm && i < RX_PREFETCH; ++i)
+            __builtin_prefetch(&R[X->mine[i]]);
+        for (uint32_t i = 0; i < nm && !X->oom; ++i) {
+            if (i + RX_PREFETCH < nm)
+                __builtin_prefetch(&R[X->mine[i + RX_PREFETCH]]);
+            if ((i & 15) == 0 && __atomic_load_n(&S->par.conflict, __ATOMIC_RELAXED))
                 return;
-            rx_arrival(X, P->a0 + p);
+            rx_arrival(X, X->mine[i]);
         }
     } else {
         const uint32_t* L = S->lst + S->loff[t];
@@ -2522,6 +2660,7 @@ static int rx_ingest(rfec_rx_session* S, uint32_t a0, uint32_t n, const rfec_rx_
     P->a0 = a0;
     P->ts_check = !risky;
     P->conflict = 0;
+    P->t0 = now_us();
     for (uint32_t t = 0; t < S->T; ++t) {
         rx_sim* X = S->XS[t];
         X->P = P;
@@ -2682,7 +2821,12 @@ static int rx_compact_(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
     const uint32_t arows = (uint32_t)(want > rx_min_rows() ? (want < 0xFFFFFFFFull ? want : 0xFFFFFFFFull) : rx_min_rows());
     if (!gmap)
         goto oom;
-    if ((e = hipMalloc((void**)&arena, (size_t)arows * S->stride)) != hipSuccess) {
+    /* the previous arena when it is large enough (no allocation per compaction: an eviction per batch
+       compacts per batch), else a fresh one */
+    if (S->spare && S->sprows >= arows) {
+        arena = S->spare;
+        S->spare = NULL;
+    } else if ((e = hipMalloc((void**)&arena, (size_t)arows * S->stride)) != hipSuccess) {
         rc = set_err(RFEC_ENOMEM, "rx session: arena", e);
         goto done;
     }
@@ -2785,24 +2929,36 @@ static int rx_compact_(rfec_rx_session* S, uint32_t extra, hipStream_t sm)
     for (uint32_t t = 0; t < T; ++t)
         S->XS[t]->R = S->store;
     if (nr + tail) {
-        int32_t* dmap = NULL;
         int ke = 0;
         const uint32_t nm = nr + tail;
-        if ((e = hipMalloc((void**)&dmap, (size_t)nm * sizeof(int32_t))) != hipSuccess ||
-            (e = hipMemcpyAsync(dmap, gmap, (size_t)nm * sizeof(int32_t), hipMemcpyHostToDevice, sm)) != hipSuccess ||
-            (ke = rfec_launch_gather_rows(arena, S->arena, dmap, nm, S->stride, sm)) != 0 ||
+        if (S->dmapcap < nm) {
+            if (S->dmap)
+                (void)hipFree(S->dmap);
+            S->dmap = NULL;
+            S->dmapcap = 0;
+            if ((e = hipMalloc((void**)&S->dmap, ((size_t)nm + nm / 2) * sizeof(int32_t))) == hipSuccess)
+                S->dmapcap = nm + nm / 2;
+        }
+        if (!S->dmap ||
+            (e = hipMemcpyAsync(S->dmap, gmap, (size_t)nm * sizeof(int32_t), hipMemcpyHostToDevice, sm)) != hipSuccess ||
+            (ke = rfec_launch_gather_rows(arena, S->arena, S->dmap, nm, S->stride, sm)) != 0 ||
             (e = hipStreamSynchronize(sm)) != hipSuccess) {
-            if (dmap)
-                (void)hipFree(dmap);
             (void)hipFree(arena);
             arena = NULL;
             rc = set_err(RFEC_EDEVICE, "rx session: row compaction", ke ? ke : (int)e);
             goto done;
         }
-        (void)hipFree(dmap);
     }
-    if (S->arena)
-        (void)hipFree(S->arena);
+    if (S->arena) { /* the old arena is the next compaction's target (the larger of it and the spare) */
+        if (S->spare && S->sprows >= S->arows) {
+            (void)hipFree(S->arena);
+        } else {
+            if (S->spare)
+                (void)hipFree(S->spare);
+            S->spare = S->arena;
+            S->sprows = S->arows;
+        }
+    }
     S->arena = arena;
     S->arows = arows;
     goto done;
@@ -3078,35 +3234,58 @@ int rfec_rx_session_push_datagrams_async(rfec_rx_session* S, uint32_t n, uint32_
     return RFEC_OK;
 }
 
-static int cmp_u64(const void* a, const void* b)
+/* One eviction walk over the union of the shards' maps m (2 flex_of, 1
+ * cache), in key order: the shards' own walks (each in key order) merged, so
+ * the cost is the entries evicted, not the open state (a sort of every
+ * shard's keys per eviction cost ~10-20 % of a batch's host time).  Stops at
+ * the first entry that stays, as the skiplist walks do. */
+static void rx_evict_walk(rfec_rx_session* S, int m)
 {
-    const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
-    return x < y ? -1 : x > y;
-}
-
-/* every shard's keys of one map, key << 32 | shard, ascending (the skiplists' order) */
-static uint64_t* rx_keys(rfec_rx_session* S, int m, uint32_t* n)
-{
-    size_t tot = 0;
-    for (uint32_t t = 0; t < S->T; ++t)
-        tot += rx_map(S->XS[t], m)->n;
-    uint64_t* k = (uint64_t*)malloc((tot + 1) * sizeof(uint64_t));
-    *n = 0;
-    if (!k)
-        return NULL;
-    for (uint32_t t = 0; t < S->T; ++t) {
-        for (PM_EACH(rx_map(S->XS[t], m), key, v))
-            k[(*n)++] = (uint64_t)key << 32 | t;
+    const uint32_t T = S->T;
+    uint32_t key[RX_MAX_THREADS], done[RX_MAX_THREADS];
+    uint32_t* val[RX_MAX_THREADS];
+    for (uint32_t t = 0; t < T; ++t) {
+        key[t] = done[t] = 0;
+        val[t] = pm_next(rx_map(S->XS[t], m), &key[t], &done[t]);
     }
-    qsort(k, *n, sizeof(uint64_t), cmp_u64);
-    return k;
+    for (;;) {
+        uint32_t b = UINT32_MAX;
+        for (uint32_t t = 0; t < T; ++t)
+            if (val[t] && (b == UINT32_MAX || key[t] < key[b]))
+                b = t;
+        if (b == UINT32_MAX)
+            return;
+        rx_sim* X = S->XS[b];
+        const uint32_t v = *val[b];
+        if (m == 2) {
+            const rx_inst* g = &X->G[v - 1];
+            if (!(g->fec_ts + 3000u <= S->max_ts || g->nsegs >= g->count))
+                return;
+            rx_remove(X, v - 1);
+        } else {
+            const uint32_t ts = (v & 0x80000000u) ? X->rh[v & 0x7FFFFFFFu].ts : X->R[v - 1].hdr.ts;
+            if (!(ts + 6000u < S->max_ts))
+                return;
+            pm_del(&X->cache, key[b]);
+        }
+        if (key[b] == UINT32_MAX) {
+            val[b] = NULL;
+            continue;
+        }
+        ++key[b];
+        val[b] = pm_next(rx_map(X, m), &key[b], &done[b]);
+    }
 }
 
 /* sim_fec_evict (sim_fec.c:209-241) over the shards: flexes in fec_id order
  * while stale (fec_ts + 3000 <= max_ts) or full, removed with their members'
  * cache entries; then cached segments in packet_id order while older than 6 s
  * (timestamp + 6000 < max_ts); both walks stop at the first entry that stays
- * (rx_evict's rules over the union of the shards). */
+ * (rx_evict's rules over the union of the shards).  The records and rows the
+ * evicted state held are dropped by the next compaction: here once the
+ * session holds more than half its arena (an eviction per batch compacted per
+ * batch, ~50 us of host time and a device gather each), else when a push
+ * needs the room. */
 int rfec_rx_session_evict(rfec_rx_session* S, void* stream)
 {
     if (!S)
@@ -3115,34 +3294,16 @@ int rfec_rx_session_evict(rfec_rx_session* S, void* stream)
         S->XS[t]->max_ts = S->max_ts;
     if (S->T == 1) {
         rx_evict(S->XS[0]);
-        if (S->XS[0]->oom)
+    } else {
+        rx_evict_walk(S, 2);
+        rx_evict_walk(S, 1);
+    }
+    for (uint32_t t = 0; t < S->T; ++t)
+        if (S->XS[t]->oom)
             return set_err(RFEC_ENOMEM, "rx session: evict", 0);
-        return rx_compact(S, 0, (hipStream_t)stream);
-    }
-    uint32_t n = 0;
-    uint64_t* k = rx_keys(S, 2, &n);
-    if (!k)
-        return set_err(RFEC_ENOMEM, "rx session: evict", 0);
-    for (uint32_t i = 0; i < n; ++i) {
-        rx_sim* X = S->XS[(uint32_t)k[i]];
-        const uint32_t fi = pm_get(&X->flex_of, (uint32_t)(k[i] >> 32)) - 1;
-        const rx_inst* g = &X->G[fi];
-        if (!(g->fec_ts + 3000u <= S->max_ts || g->nsegs >= g->count))
-            break;
-        rx_remove(X, fi);
-    }
-    free(k);
-    if (!(k = rx_keys(S, 1, &n)))
-        return set_err(RFEC_ENOMEM, "rx session: evict", 0);
-    for (uint32_t i = 0; i < n; ++i) {
-        rx_sim* X = S->XS[(uint32_t)k[i]];
-        const uint32_t seq = (uint32_t)(k[i] >> 32), c = pm_get(&X->cache, seq);
-        const uint32_t ts = (c & 0x80000000u) ? X->rh[c & 0x7FFFFFFFu].ts : X->R[c - 1].hdr.ts;
-        if (!(ts + 6000u < S->max_ts))
-            break;
-        pm_del(&X->cache, seq);
-    }
-    free(k);
+    const uint32_t tail = S->pend >= 0 ? S->pend_n : 0;
+    if (2ull * (S->nstore + tail) < S->arows)
+        return RFEC_OK;
     return rx_compact(S, 0, (hipStream_t)stream);
 }
 

@@ -210,16 +210,34 @@ int rfec_launch_recover(const rfec_kmask* M, uint32_t groups, uint32_t stride, u
     return 0;
 }
 
-/* dense output form: not used by the host control plane; refused */
+/* dense output form (the receiver session's device peel): as rfec_launch_recover, for the erased members
+ * of rank < per_group; out_index names them */
 int rfec_launch_recover_out(const rfec_kmask* M, uint32_t groups, uint32_t stride, uint32_t capacity,
                             const uint8_t* shards, const rfec_hdr* hdr, const uint64_t* present,
                             const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fsize,
                             const uint64_t* parity_present, uint64_t* recovered, void* ws, void* stream,
                             unsigned flags, const rfec_dense_out* out)
 {
-    (void)M, (void)groups, (void)stride, (void)capacity, (void)shards, (void)hdr, (void)present, (void)parity;
-    (void)meta, (void)fsize, (void)parity_present, (void)recovered, (void)ws, (void)stream, (void)flags, (void)out;
-    return (int)hipErrorInvalidValue;
+    (void)stride, (void)capacity, (void)shards, (void)hdr, (void)parity, (void)meta, (void)fsize;
+    (void)parity_present, (void)ws, (void)stream, (void)flags;
+    uint64_t all[2] = {0, 0};
+    for (uint32_t l = 0; l < M->plan.n_lines; ++l) {
+        all[0] |= M->mask[l][0];
+        all[1] |= M->mask[l][1];
+    }
+    for (uint32_t g = 0; g < groups; ++g) {
+        uint32_t e = 0;
+        recovered[2 * g] = recovered[2 * g + 1] = 0;
+        for (uint32_t i = 0; i < M->plan.k && e < out->per_group; ++i) {
+            if ((present[2 * g + (i >> 6)] >> (i & 63)) & 1ull)
+                continue;
+            const int ok = (int)((all[i >> 6] >> (i & 63)) & 1ull);
+            if (ok)
+                recovered[2 * g + (i >> 6)] |= 1ull << (i & 63);
+            out->index[(size_t)g * out->per_group + e++] = ok ? (uint8_t)i : 0xFF;
+        }
+    }
+    return 0;
 }
 
 /* packed erasure records: not used by the host control plane; refused */
@@ -274,6 +292,16 @@ int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map
         else
             memset(dst + (size_t)r * stride, 0, stride);
     }
+    return 0;
+}
+
+/* the receiver session's device stage: the gather and the table copy */
+int rfec_launch_rx_stage(uint8_t* dst, const uint8_t* src, const int32_t* map, uint32_t rows, uint32_t stride,
+                         void* tdst, const void* tsrc, size_t tbytes, void* stream)
+{
+    rfec_launch_gather_rows(dst, src, map, rows, stride, stream);
+    if (tbytes)
+        memcpy(tdst, tsrc, tbytes);
     return 0;
 }
 

@@ -220,11 +220,15 @@ def test_rx_session_reference_fixture(lib, name):
 
 
 @pytest.mark.parametrize("evict_every", [0, 300])
-def test_rx_session_split_invariance(lib, oracle1000, evict_every):
+def test_rx_session_split_invariance(lib, oracle1000, evict_every, monkeypatch):
     """A product-sender stream pushed in random batches (evict_every == 0) or
     in batches of evict_every with evictions between: the union of what the
     batches deliver == the oracle on the whole stream with the same evictions
-    -- including groups whose datagrams straddle batches."""
+    -- including groups whose datagrams straddle batches.  The arena is the
+    smallest (RFEC_RX_ARENA_ROWS=4096), so compactions run (an eviction
+    compacts once the session holds half its arena, a push when it needs the
+    room) and the session keeps only what the open state refers to."""
+    monkeypatch.setenv("RFEC_RX_ARENA_ROWS", "4096")
     order, dg, _ = _sender_stream(lib, 2500, 5, (3, 6, 10), (20, 80, 100))
     arrivals = _network(order, np.random.default_rng(13), loss=0.15, window=60, dup=0.03, late=0.05,
                         late_by=2500)

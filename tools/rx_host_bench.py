@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--lib", default="")
     ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--evict", type=int, default=1,
+                    help="rfec_rx_session_evict after every push (the heartbeat's sim_fec_evict); 0: never")
     args = ap.parse_args()
     so = Path(args.lib) if args.lib else build_stub(Path("/tmp/librazor_fec_rxhost.so"))
     lib = Native(1200, path=str(so))
@@ -74,6 +76,8 @@ def main():
                                                 out.ctypes.data, outp.ctypes.data, max_out, C.byref(nout),
                                                 C.byref(rep), None), "push")
         got.append(out[:nout.value].copy())
+        if args.evict and m == args.batch:
+            lib._check(lib.lib.rfec_rx_session_evict(sess.h, None), "evict")
         host += rep.host_us
         dev += rep.kernel_us + rep.h2d_us + rep.d2h_us
         tot += rep.total_us
@@ -89,7 +93,8 @@ def main():
         import pyoracle as po
 
         o = po.Oracle(1200)
-        eo, _, emts, edrop = o.rx_recover(recs, np.zeros((n, CAP), np.uint8), CAP, max_out=1 << 22)
+        eo, _, emts, edrop = o.rx_recover(recs, np.zeros((n, CAP), np.uint8), CAP, max_out=1 << 22,
+                                    evict_every=args.batch if args.evict else 0)
         i, j = np.argsort(got["hdr"]["seq"], kind="stable"), np.argsort(eo["hdr"]["seq"], kind="stable")
         ok = len(got) == len(eo) and np.array_equal(got["hdr"][i], eo["hdr"][j]) and np.array_equal(
             got["fec_id"][i], eo["fec_id"][j]) and sess.info()["max_ts"] == emts

@@ -39,7 +39,7 @@ REP_FIELDS = ("host_us", "h2d_us", "kernel_us", "d2h_us", "total_us")
 OUT = OUTP = None  # pinned outputs, one row per datagram at most (main)
 
 
-def run(lib, mode, n, dg, dl, batch, max_out, threads):
+def run(lib, mode, n, dg, dl, batch, max_out, threads, evict):
     """One pass of the whole stream through a fresh session (`threads`
     control-plane shards); returns the delivered (segments, rows) in delivery
     order, the wall seconds and the summed report."""
@@ -69,12 +69,18 @@ def run(lib, mode, n, dg, dl, batch, max_out, threads):
             tot[f] += getattr(rep, f)
         tot["calls"] += 1
 
+    ev = lib.lib.rfec_rx_session_evict
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for a0 in range(0, n, batch):
         call(a0, min(batch, n - a0))
+        # the heartbeat's sim_fec_evict once per ingested full batch (the async call ingests the previous one)
+        if evict and (mode == "sync" and a0 + batch <= n or mode == "async" and a0 > 0):
+            lib._check(ev(sess.h, None), "evict")
     if mode == "async":
         call(0, 0)  # flush the last pending batch
+        if evict and n % batch == 0:
+            lib._check(ev(sess.h, None), "evict")
     wall = time.perf_counter() - t0
     info = sess.info()
     sess.close()
@@ -90,6 +96,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--modes", default="async,sync")
     ap.add_argument("--threads", default="1,8", help="control-plane shards to measure (rfec_rx_session_set_threads)")
+    ap.add_argument("--evict", type=int, default=1, help="rfec_rx_session_evict after every ingested batch "
+                    "(the heartbeat's sim_fec_evict, sim_receiver.c:881; the oracle evicts at the same points); 0: never")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     lib = native(1200)
@@ -116,20 +124,20 @@ def main():
     o = Oracle(1200)
     t0 = time.perf_counter()
     eo, eop, emts, edrop = o.rx_recover(recs.cpu().numpy().view(WIRE_REC_DTYPE), pay.cpu().numpy().reshape(-1, STRIDE),
-                                        S, max_out=1 << 20)
+                                        S, max_out=1 << 20, evict_every=args.batch if args.evict else 0)
     t_or = time.perf_counter() - t0
     del d_dg, d_dl, recs, pay
     res = {"stream": {"frames": args.frames, "segments_sent": ns, "parities_sent": nf, "datagrams": n,
                       "datagram_GB": round(gb, 4), "loss": args.loss, "window": args.window, "duplicates": 0.02,
                       "k": 10, "payload": S, "plan": "3 x 4 (3 rows + 4 columns)", "dstride": DSTRIDE},
-           "batch": args.batch, "oracle": {"recovered": int(len(eo)), "s": round(t_or, 3),
+           "batch": args.batch, "evict_every_batch": bool(args.evict), "oracle": {"recovered": int(len(eo)), "s": round(t_or, 3),
                                            "datagrams_per_s": round(n / t_or), "cores": 1},
            "pid_cpus": len(os.sched_getaffinity(0))}
     ok_all = True
     for mode, threads in [(m, int(t)) for m in args.modes.split(",") for t in args.threads.split(",")]:
         best = None
         for _ in range(args.reps):
-            r = run(lib, mode, n, dg, dl, args.batch, max(2 * args.batch, 8192), threads)
+            r = run(lib, mode, n, dg, dl, args.batch, max(2 * args.batch, 8192), threads, args.evict)
             if best is None or r[2] < best[2]:
                 best = r
         seg, row, wall, tot, info = best
