@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--counters", required=True)
     ap.add_argument("--match", required=True)
     ap.add_argument("--timeout", type=int, default=120)
+    ap.add_argument("--by-grid", action="store_true", help="one entry per (kernel, grid size): launches of one "
+                    "kernel over different batches (e.g. the SIM_FEC and SIM_SEG parses) kept apart")
     args = ap.parse_args(argv)
     d = ROOT / "gpurun_out" / "pmc_sq" / args.tag
     d.mkdir(parents=True, exist_ok=True)
@@ -49,6 +51,8 @@ def main():
                 pat = next((p for p in pats if p in name), None)
                 if pat is None:
                     continue
+                if args.by_grid:
+                    pat = f"{pat}@grid{row.get('Grid_Size', row.get('Grid_Size_X', ''))}"
                 acc[(pat, row.get("Dispatch_Id", ""))][row["Counter_Name"]] += float(row["Counter_Value"])
     out = defaultdict(lambda: defaultdict(list))
     for (pat, _), cs in acc.items():
