@@ -96,8 +96,9 @@ int rfec_sim_video_size(void);
  * whose size changed.  History: 5 -- rfec_host_timing grew from 48 to 56
  * bytes (zero_copy, reserved); 6 -- rfec_abi_version, rfec_rx_session_info grew
  * from 24 to 88 bytes (threads, batches_*, the host time split),
- * rfec_rx_session_set_threads. */
-#define RFEC_ABI_VERSION 6
+ * rfec_rx_session_set_threads; 7 -- rfec_send_report grew from 64 to 72 bytes
+ * (zero_copy, reserved). */
+#define RFEC_ABI_VERSION 7
 uint32_t rfec_abi_version(void);
 
 /* ------------------------------------------------------------------------ */
@@ -505,10 +506,18 @@ int rfec_sender_plan(rfec_sender_state* st, const rfec_frame* frames, uint32_t n
  * after the segment that closed it); send_ts is that of an immediate send
  * (sim_sender.c:88-91, 111-113).  seg_size is this library's SIM_VIDEO_SIZE;
  * the segments of a group still open at the end are kept (per calling thread)
- * and encoded by the call that closes it. */
+ * and encoded by the call that closes it.
+ *
+ * Zero copy (RFEC_HOST_ZEROCOPY not "0"): when every frame's bytes lie inside
+ * one rfec_pinned_alloc block, the device reads the segments out of the frames
+ * itself (no host copy into the staging slots, no bulk H2D: h2d_us is then the
+ * tables' copy and the device's reads); when the four datagram outputs lie in
+ * such blocks, the framing writes the datagrams there (no D2H; the writes fall
+ * in kernel_us).  report->zero_copy: bit 0 input, bit 1 output. */
 typedef struct {
     uint32_t n_segs, n_groups, n_parities, n_shapes;
     double plan_us, stage_us, h2d_us, kernel_us, d2h_us, total_us;
+    uint32_t zero_copy, reserved;
 } rfec_send_report;
 
 int rfec_host_send_frames(rfec_sender_state* st, const rfec_frame* frames, uint32_t n_frames, uint32_t uid,

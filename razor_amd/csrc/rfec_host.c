@@ -66,6 +66,7 @@ int rfec_sim_video_size(void) { return SIM_VIDEO_SIZE; }
 
 uint32_t rfec_abi_version(void) { return RFEC_ABI_VERSION; }
 _Static_assert(sizeof(rfec_host_timing) == 56, "rfec_host_timing: ABI 5 layout (bump RFEC_ABI_VERSION)");
+_Static_assert(sizeof(rfec_send_report) == 72, "rfec_send_report: ABI 7 layout (bump RFEC_ABI_VERSION)");
 
 unsigned g_tuning = 0;
 void rfec_set_tuning(unsigned flags) { g_tuning = flags; }
@@ -470,7 +471,7 @@ int rfec_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacity, cons
     if (!shards || !hdr || !stamps || !dgram || !dlen)
         return set_err(RFEC_EINVAL, "NULL buffer", 0);
     const int e = rfec_launch_wire_frame_seg(count, stride, capacity, shards, hdr, stamps, order, dstride, dgram,
-                                             dlen, stream);
+                                             dlen, count, stream);
     return e ? set_err(RFEC_EDEVICE, "wire_frame_seg launch", e) : RFEC_OK;
 }
 

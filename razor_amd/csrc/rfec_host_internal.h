@@ -59,6 +59,10 @@ typedef struct {
     int have_ev;
 } di_ctx;
 di_ctx* di_get(void);
+/* rfec_hostmem.c: the pinned-block registry (rfec_pinned_alloc): 1 when [lo, hi) lies inside one block,
+ * its device offset (device address - host address) in *delta; RFEC_HOST_ZEROCOPY != "0" */
+int pinned_range(uintptr_t lo, uintptr_t hi, intptr_t* delta);
+int zerocopy_on(void);
 void seg_to_hdr(const sim_segment_t* s, rfec_hdr* h);
 void stage_payload(uint8_t* slot, const uint8_t* data, uint32_t size);
 

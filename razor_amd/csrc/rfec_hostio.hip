@@ -309,6 +309,38 @@ __global__ __launch_bounds__(kBlock) void k_host_scatter_seg(const uint64_t* __r
 
 inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
 
+// Sender staging without a host copy (rfec_sender.c rfec_host_send_frames,
+// frames in rfec_pinned_alloc memory): slot s <- the segment bytes [src[s],
+// src[s] + size[s]) read over PCIe by the lanes themselves, zeros past size
+// (src 0: a zero slot).  The bytes lie at any alignment (sim_split_frame's
+// offsets): a lane loads the 4-byte-aligned 16 bytes at or before its chunk --
+// only the dwords holding segment bytes, so no load leaves the segment's last
+// dword -- and takes the bytes past them from the next lane (DPP wave_shl:1;
+// the wave's last lane and a slot's last chunk load that dword themselves).
+__global__ __launch_bounds__(kBlock) void k_send_gather(const uint64_t* __restrict__ src,
+                                                        const uint16_t* __restrict__ size, uint32_t total, uint32_t C,
+                                                        FastDiv divC, v4u* __restrict__ dst)
+{
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    const bool live = t < total;
+    const uint32_t slot = live ? fdiv(t, divC) : 0u, j = live ? t - slot * C : 0u;
+    const uint64_t a = live ? src[slot] : 0u;
+    const uint32_t n = a ? size[slot] : 0u, mis = (uint32_t)a & 3u;
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(a - mis) + 16u * j;
+    const int need = (int)(mis + n) - (int)(16u * j); // window bytes from this lane's load on that are wanted
+    v4u x = {0, 0, 0, 0};
+    if (need > 0)
+        x = ld_host_part(base, (need + 3) & ~3);
+    uint32_t nx = next_lane(x[0]);
+    if (mis && need > 16 && ((threadIdx.x & 63u) == 63u || j + 1u == C))
+        nx = ld_host4(base + 16);
+    if (!live)
+        return;
+    const v4u v = {__builtin_amdgcn_alignbyte(x[1], x[0], mis), __builtin_amdgcn_alignbyte(x[2], x[1], mis),
+                   __builtin_amdgcn_alignbyte(x[3], x[2], mis), __builtin_amdgcn_alignbyte(nx, x[3], mis)};
+    dst[(size_t)slot * C + j] = keep16(v, (int)n - (int)(16u * j));
+}
+
 } // namespace
 
 extern "C" {
@@ -328,6 +360,17 @@ int rfec_launch_host_gather(const uint64_t* sptrs, uint32_t ns, uint8_t* shards,
         return 0;
     RFEC_LAUNCH(k_host_gather, dim3(nb), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), s0, s1, b1, C,
                 make_fastdiv(C), video, aux_src, aux_dst, aux_n);
+    return (int)hipGetLastError();
+}
+
+int rfec_launch_send_gather(const uint64_t* src, const uint16_t* size, uint32_t slots, uint32_t stride, uint8_t* dst,
+                            void* stream)
+{
+    const uint32_t C = stride / 16, total = slots * C; // slots * C < 2^32: host-bounded
+    if (!total)
+        return 0;
+    RFEC_LAUNCH(k_send_gather, dim3(blocks_for(total)), dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), src,
+                size, total, C, make_fastdiv(C), reinterpret_cast<v4u*>(dst));
     return (int)hipGetLastError();
 }
 

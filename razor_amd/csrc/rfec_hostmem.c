@@ -203,6 +203,23 @@ static int zerocopy_enabled(void)
     return !(v && v[0] == '0');
 }
 
+int zerocopy_on(void) { return zerocopy_enabled(); }
+
+/* 1 when [lo, hi) lies inside one registered block (its device offset in *delta) */
+int pinned_range(uintptr_t lo, uintptr_t hi, intptr_t* delta)
+{
+    int ok = 0;
+    *delta = 0;
+    pthread_mutex_lock(&g_pin_mu);
+    for (size_t i = 0; i < g_npin && !ok; ++i)
+        if (lo >= g_pin[i].lo && hi <= g_pin[i].hi) {
+            ok = 1;
+            *delta = g_pin[i].delta;
+        }
+    pthread_mutex_unlock(&g_pin_mu);
+    return ok;
+}
+
 /* groups per zero-copy chunk: RFEC_ZC_CHUNK (measurement knob) or G / 8, at least 2,048 */
 static uint32_t zc_chunk(uint32_t groups)
 {
@@ -752,6 +769,67 @@ static hy_layout hy_offsets(const rfec_plan* plan, uint32_t G, uint32_t E)
     return L;
 }
 
+/* The plans whose dense recovery takes the cascade decodes (rfec_kernels.hip
+ * launch_recover: lines cross, <= 4 members a line, <= 8 lines, k <= 64, not
+ * forced generic), whose payload lanes read only the lines zc_lines_read
+ * names. */
+static int zc_cascade_plan(const rfec_plan* p, const rfec_kmask* M)
+{
+    if (p->k > 64 || p->n_lines > 8 || (g_tuning & RFEC_KFLAG_GENERIC))
+        return 0;
+    uint64_t seen = 0;
+    int cross = 0;
+    for (uint32_t l = 0; l < p->n_lines; ++l) {
+        if (p->line[l].count > 4)
+            return 0;
+        cross |= (seen & M->mask[l][0]) != 0;
+        seen |= M->mask[l][0];
+    }
+    return cross;
+}
+
+/* The lines a dense cascade decode reads for one group (k <= 64): for each
+ * erased member of rank < E, the first line in plan order that fires at once
+ * for it (parity received, it the line's only missing member, one member
+ * present); if some target has none, every step of the canonical mask
+ * schedule (lines in plan order to a fixpoint, targets of rank < E) --
+ * cascade_schedule's rules. */
+static uint64_t zc_lines_read(const rfec_kmask* M, uint32_t n, uint64_t have, uint64_t ppm, uint32_t E)
+{
+    const uint32_t k = M->plan.k;
+    const uint64_t km = k >= 64 ? ~0ull : (1ull << k) - 1ull;
+    const uint64_t er = ~have & km;
+    uint64_t lines = 0, e = er;
+    int casc = 0;
+    for (uint32_t q = 0; q < E && e; ++q, e &= e - 1) {
+        const uint64_t tb = e & (~e + 1);
+        uint32_t l = 0;
+        while (l < n && !((ppm >> l & 1) && (M->mask[l][0] & er) == tb && (M->mask[l][0] & have)))
+            ++l;
+        if (l < n)
+            lines |= 1ull << l;
+        else
+            casc = 1;
+    }
+    if (casc) {
+        uint64_t h = have;
+        for (int progress = 1; progress;) {
+            progress = 0;
+            for (uint32_t l = 0; l < n; ++l) {
+                const uint64_t m = M->mask[l][0], x = m & ~h;
+                if (!(ppm >> l & 1) || __builtin_popcountll(x) != 1 || !(m & h))
+                    continue;
+                if ((uint32_t)__builtin_popcountll(er & (x - 1)) >= E)
+                    continue;
+                lines |= 1ull << l;
+                h |= x;
+                progress = 1;
+            }
+        }
+    }
+    return lines;
+}
+
 static int zc_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment_t* const* segs,
                              sim_fec_t* const* fecs, uint32_t E, sim_segment_t* const* out, uint8_t* out_index,
                              uint64_t* recovered, rfec_host_timing* timing, intptr_t ds, intptr_t df, intptr_t dout)
@@ -773,6 +851,7 @@ static int zc_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
         return rc;
     rfec_kmask M;
     make_masks(plan, &M);
+    const int trim = zc_cascade_plan(plan, &M);
     double tab_us = 0, h2d_us = 0, kernel_us = 0, d2h_us = 0, out_us = 0;
     const double t0 = now_us();
     for (uint32_t it = 0; it < nch + RFEC_HB_SLOTS && rc == RFEC_OK; ++it) {
@@ -832,15 +911,28 @@ static int zc_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
             ppm[g] = pm;
             /* A line fires only to rebuild a member it lacks, so the decode
              * reads the payloads of received lines that hold an erased member
-             * and nothing else: the rest cross PCIe as headers only. */
+             * and nothing else: the rest cross PCIe as headers only.  Plans
+             * with cascades on the dense cascade decodes read fewer: a payload
+             * lane takes the first line that fires at once for its target, else
+             * the steps of the canonical mask schedule (k_decode_cascade_dense,
+             * k_decode_matrix_dense; the header checks pick only out_index and
+             * the recovered masks) -- those lines' members and parities cross
+             * whole, every other struct as its header. */
             const uint64_t e0 = ~m0, e1 = ~m1; /* (line masks hold members only) */
             uint64_t n0 = 0, n1 = 0, pn = 0;
-            for (uint32_t l = 0; l < n; ++l)
-                if ((pm >> l & 1) && ((M.mask[l][0] & e0) | (M.mask[l][1] & e1))) {
-                    n0 |= M.mask[l][0];
-                    n1 |= M.mask[l][1];
-                    pn |= 1ull << l;
-                }
+            if (trim) {
+                pn = zc_lines_read(&M, n, m0, pm, E);
+                for (uint32_t l = 0; l < n; ++l)
+                    if (pn >> l & 1)
+                        n0 |= M.mask[l][0];
+            } else {
+                for (uint32_t l = 0; l < n; ++l)
+                    if ((pm >> l & 1) && ((M.mask[l][0] & e0) | (M.mask[l][1] & e1))) {
+                        n0 |= M.mask[l][0];
+                        n1 |= M.mask[l][1];
+                        pn |= 1ull << l;
+                    }
+            }
             for (uint32_t i = 0; i < k; ++i)
                 if (spt[(size_t)g * k + i] && !((i < 64 ? n0 >> i : n1 >> (i - 64)) & 1))
                     spt[(size_t)g * k + i] |= 1;

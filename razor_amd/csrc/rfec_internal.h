@@ -71,7 +71,7 @@ int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacit
                                uint8_t* dgram, uint16_t* dlen, void* stream);
 int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* shards,
                                const rfec_hdr* hdr, const rfec_seg_stamp* stamps, const uint32_t* order,
-                               uint32_t dstride, uint8_t* dgram, uint16_t* dlen, void* stream);
+                               uint32_t dstride, uint8_t* dgram, uint16_t* dlen, uint32_t rows_out, void* stream);
 /* max_len: the longest datagram when the caller knows it (host-side lengths), else 0; slots
  * wider than 1,280 B still take the 20-byte-lane parse when every datagram fits 1,280 B */
 int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
@@ -116,6 +116,10 @@ int rfec_launch_host_gather(const uint64_t* sptrs, uint32_t ns, uint8_t* shards,
                             const uint64_t* fptrs, uint32_t nf, uint8_t* parity, rfec_hdr* meta, uint16_t* fsize,
                             uint16_t* fecid, uint32_t stride, uint32_t video, const uint64_t* aux_src,
                             uint64_t* aux_dst, uint32_t aux_n, void* stream);
+/* sender staging (rfec_sender.c): slot s of `stride` bytes <- src[s] (device address of host bytes, any
+ * alignment; 0: zeros) for size[s] bytes, zeros past them */
+int rfec_launch_send_gather(const uint64_t* src, const uint16_t* size, uint32_t slots, uint32_t stride, uint8_t* dst,
+                            void* stream);
 /* parity slots of `groups` groups -> their sim_fec_t, stamped as flex_fec_sender_update does */
 int rfec_launch_host_scatter_fec(const uint64_t* fptrs, uint32_t groups, const rfec_kplan* P, uint32_t stride,
                                  const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fsize,

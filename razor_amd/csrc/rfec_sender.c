@@ -154,6 +154,7 @@ int rfec_sender_plan(rfec_sender_state* st, const rfec_frame* frames, uint32_t n
 /* ---- frames -> datagrams ------------------------------------------------- */
 typedef struct {
     uint8_t* h;     /* pinned host */
+    uint8_t* hd;    /* h as the device addresses it (NULL: not mapped) */
     uint8_t* d;     /* device */
     size_t bytes;
     uint8_t* carry; /* the open group's segments (slots then headers), host */
@@ -177,6 +178,9 @@ static int sd_reserve(size_t bytes)
     bytes += bytes / 4;
     if ((e = hipHostMalloc((void**)&t_sd.h, bytes, hipHostMallocDefault)) != hipSuccess)
         return set_err(RFEC_ENOMEM, "send staging (host)", e);
+    void* hd = NULL;
+    t_sd.hd = hipHostGetDevicePointer(&hd, t_sd.h, 0) == hipSuccess ? (uint8_t*)hd : NULL;
+    (void)hipGetLastError();
     if ((e = hipMalloc((void**)&t_sd.d, bytes)) != hipSuccess)
         return set_err(RFEC_ENOMEM, "send staging (device)", e);
     t_sd.bytes = bytes;
@@ -184,7 +188,7 @@ static int sd_reserve(size_t bytes)
 }
 
 typedef struct { /* byte offsets in the staging block (host and device alike) */
-    size_t slots, hdr, sstamp, sorder, fstamp, forder, in_end;
+    size_t slots, hdr, sstamp, sorder, fstamp, forder, src, ssz, in_end;
     size_t parity, meta, fsize, status, sdg, sdl, fdg, fdl, total;
 } sd_layout;
 
@@ -203,7 +207,9 @@ static sd_layout sd_offsets(uint32_t n_slots, uint32_t n_par, uint32_t dstride)
     SD_TAKE(sorder, (size_t)n_slots * sizeof(uint32_t));
     SD_TAKE(fstamp, (size_t)n_par * sizeof(rfec_fec_stamp));
     SD_TAKE(forder, (size_t)n_par * sizeof(uint32_t));
-    L.in_end = o; /* everything above goes host -> device in one copy */
+    SD_TAKE(src, (size_t)n_slots * sizeof(uint64_t)); /* zero copy: each slot's bytes (device address), size */
+    SD_TAKE(ssz, (size_t)n_slots * sizeof(uint16_t));
+    L.in_end = o; /* everything above goes host -> device in one copy (zero copy: from hdr on) */
     SD_TAKE(parity, (size_t)n_par * DI_STRIDE);
     SD_TAKE(meta, (size_t)n_par * sizeof(rfec_hdr));
     SD_TAKE(fsize, (size_t)n_par * sizeof(uint16_t));
@@ -225,6 +231,9 @@ typedef struct {
     sd_layout L;
     uint32_t uid, n_segs;
     const uint16_t* tseq;       /* transport_seq per segment */
+    int zc;                     /* zero copy: the device reads the frames (din: their device offset) */
+    intptr_t din;
+    const uint8_t* hd;          /* the staging block as the device addresses it */
 } sd_stage_job;
 
 static void sd_stage(void* arg, size_t lo, size_t hi)
@@ -233,17 +242,26 @@ static void sd_stage(void* arg, size_t lo, size_t hi)
     rfec_hdr* hh = (rfec_hdr*)(J->h + J->L.hdr);
     rfec_seg_stamp* ss = (rfec_seg_stamp*)(J->h + J->L.sstamp);
     uint32_t* so = (uint32_t*)(J->h + J->L.sorder);
+    uint64_t* src = (uint64_t*)(J->h + J->L.src);
+    uint16_t* ssz = (uint16_t*)(J->h + J->L.ssz);
     for (size_t s = lo; s < hi; ++s) {
         uint8_t* slot = J->h + J->L.slots + s * DI_STRIDE;
         const uint32_t i = J->seg_of_slot[s];
         if (i >= J->n_segs) { /* carried from the previous call: bytes and header already in place */
             so[s] = J->n_segs + (UINT32_MAX - i); /* framed into scratch rows past the real ones */
             memset(&ss[s], 0, sizeof(ss[s]));
+            src[s] = J->zc ? (uint64_t)(uintptr_t)(J->hd + J->L.slots + s * DI_STRIDE) : 0u;
+            ssz[s] = DI_STRIDE;
             continue;
         }
         const rfec_seg_plan* g = &J->segs[i];
-        memcpy(slot, J->frames[g->frame].data + g->offset, g->data_size);
-        memset(slot + g->data_size, 0, DI_STRIDE - g->data_size);
+        if (J->zc) { /* the device gathers the bytes from the frame itself */
+            src[s] = (uint64_t)((uintptr_t)(J->frames[g->frame].data + g->offset) + J->din);
+            ssz[s] = g->data_size;
+        } else {
+            memcpy(slot, J->frames[g->frame].data + g->offset, g->data_size);
+            memset(slot + g->data_size, 0, DI_STRIDE - g->data_size);
+        }
         rfec_hdr* h = &hh[s];
         h->seq = g->packet_id;
         h->fid = g->fid;
@@ -353,6 +371,26 @@ int rfec_host_send_frames(rfec_sender_state* st, const rfec_frame* frames, uint3
     const sd_layout L = sd_offsets(n_slots, n_par, dstride);
     if ((rc = sd_reserve(L.total)))
         goto out;
+    /* Zero copy: frames inside one rfec_pinned_alloc block -> the device reads their bytes itself (no host
+       copy into the staging slots, no bulk H2D); datagram outputs inside such blocks -> the framing writes
+       them there (no D2H).  Either side independently; RFEC_HOST_ZEROCOPY=0 turns both off. */
+    intptr_t din = 0, dsg = 0, dsl = 0, dfg = 0, dfl = 0;
+    int zc_in = 0, zc_out = 0;
+    if (zerocopy_on()) {
+        uintptr_t lo = UINTPTR_MAX, hi = 0;
+        for (uint32_t f = 0; f < n_frames; ++f)
+            if (frames[f].size) {
+                const uintptr_t a = (uintptr_t)frames[f].data;
+                lo = a < lo ? a : lo;
+                hi = a + frames[f].size > hi ? a + frames[f].size : hi;
+            }
+        zc_in = t_sd.hd && lo < hi && pinned_range(lo, hi, &din);
+        zc_out = pinned_range((uintptr_t)seg_dgram, (uintptr_t)seg_dgram + (size_t)ns * dstride, &dsg) &&
+                 pinned_range((uintptr_t)seg_dlen, (uintptr_t)(seg_dlen + ns), &dsl) &&
+                 (!n_par || (pinned_range((uintptr_t)fec_dgram, (uintptr_t)fec_dgram + (size_t)n_par * dstride, &dfg) &&
+                             pinned_range((uintptr_t)fec_dlen, (uintptr_t)(fec_dlen + n_par), &dfl)));
+    }
+    rep->zero_copy = (uint32_t)(zc_in | zc_out << 1);
     di_ctx* c = di_get();
     if (!c) {
         rc = RFEC_EDEVICE;
@@ -370,7 +408,7 @@ int rfec_host_send_frames(rfec_sender_state* st, const rfec_frame* frames, uint3
         memcpy(t_sd.h + L.hdr + (size_t)s * sizeof(rfec_hdr),
                t_sd.carry + (size_t)RFEC_MAX_K * DI_STRIDE + (size_t)j * sizeof(rfec_hdr), sizeof(rfec_hdr));
     }
-    sd_stage_job J = {frames, segs, seg_of_slot, t_sd.h, L, uid, ns, tseq};
+    sd_stage_job J = {frames, segs, seg_of_slot, t_sd.h, L, uid, ns, tseq, zc_in, din, t_sd.hd};
     parallel_for(n_slots, host_threads(), sd_stage, &J);
     /* parity stamps / order, shape by shape */
     {
@@ -418,7 +456,13 @@ int rfec_host_send_frames(rfec_sender_state* st, const rfec_frame* frames, uint3
             if (pos < first)
                 continue;
             const int32_t j = pos - first;
-            memcpy(tmp + (size_t)j * DI_STRIDE, t_sd.h + L.slots + (size_t)s * DI_STRIDE, DI_STRIDE);
+            if (zc_in && i < ns) { /* (the staging slot holds no bytes: from the frame) */
+                const rfec_seg_plan* g = &segs[i];
+                memcpy(tmp + (size_t)j * DI_STRIDE, frames[g->frame].data + g->offset, g->data_size);
+                memset(tmp + (size_t)j * DI_STRIDE + g->data_size, 0, DI_STRIDE - g->data_size);
+            } else {
+                memcpy(tmp + (size_t)j * DI_STRIDE, t_sd.h + L.slots + (size_t)s * DI_STRIDE, DI_STRIDE);
+            }
             memcpy(tmp + (size_t)RFEC_MAX_K * DI_STRIDE + (size_t)j * sizeof(rfec_hdr),
                    t_sd.h + L.hdr + (size_t)s * sizeof(rfec_hdr), sizeof(rfec_hdr));
         }
@@ -441,7 +485,14 @@ int rfec_host_send_frames(rfec_sender_state* st, const rfec_frame* frames, uint3
             }
         uint8_t* D = t_sd.d;
         (void)hipEventRecord(ev[0], sm);
-        e = hipMemcpyAsync(D, t_sd.h, L.in_end, hipMemcpyHostToDevice, sm);
+        const size_t c0 = zc_in ? L.hdr : 0; /* zero copy: the tables only, then the device's frame reads */
+        e = hipMemcpyAsync(D + c0, t_sd.h + c0, L.in_end - c0, hipMemcpyHostToDevice, sm);
+        if (e == hipSuccess && zc_in && n_slots) {
+            const int ke = rfec_launch_send_gather((const uint64_t*)(D + L.src), (const uint16_t*)(D + L.ssz), n_slots,
+                                                   DI_STRIDE, D + L.slots, sm);
+            if (ke)
+                rc = set_err(RFEC_EDEVICE, "send gather launch", ke);
+        }
         (void)hipEventRecord(ev[1], sm);
         uint32_t slot0 = 0, p0 = 0;
         for (uint32_t q = 0; q < ng && e == hipSuccess && !rc;) {
@@ -468,18 +519,22 @@ int rfec_host_send_frames(rfec_sender_state* st, const rfec_frame* frames, uint3
         if (!rc && e == hipSuccess && n_slots)
             ke = rfec_launch_wire_frame_seg(n_slots, DI_STRIDE, SIM_VIDEO_SIZE, D + L.slots,
                                             (const rfec_hdr*)(D + L.hdr), (const rfec_seg_stamp*)(D + L.sstamp),
-                                            (const uint32_t*)(D + L.sorder), dstride, D + L.sdg,
-                                            (uint16_t*)(D + L.sdl), sm);
+                                            (const uint32_t*)(D + L.sorder), dstride,
+                                            zc_out ? (uint8_t*)((uintptr_t)seg_dgram + dsg) : D + L.sdg,
+                                            zc_out ? (uint16_t*)((uintptr_t)seg_dlen + dsl) : (uint16_t*)(D + L.sdl),
+                                            zc_out ? ns : n_slots, sm); /* (zero copy: the carried rows dropped) */
         if (!rc && !ke && e == hipSuccess && n_par)
             ke = rfec_launch_wire_frame_fec(n_par, DI_STRIDE, SIM_VIDEO_SIZE, D + L.parity,
                                             (const rfec_hdr*)(D + L.meta), (const uint16_t*)(D + L.fsize),
                                             (const int8_t*)(D + L.status), (const rfec_fec_stamp*)(D + L.fstamp),
-                                            (const uint32_t*)(D + L.forder), dstride, D + L.fdg,
-                                            (uint16_t*)(D + L.fdl), sm);
+                                            (const uint32_t*)(D + L.forder), dstride,
+                                            zc_out ? (uint8_t*)((uintptr_t)fec_dgram + dfg) : D + L.fdg,
+                                            zc_out ? (uint16_t*)((uintptr_t)fec_dlen + dfl) : (uint16_t*)(D + L.fdl),
+                                            sm);
         if (ke && !rc)
             rc = set_err(RFEC_EDEVICE, "frame launch", ke);
         (void)hipEventRecord(ev[2], sm);
-        if (!rc && e == hipSuccess) {
+        if (!rc && e == hipSuccess && !zc_out) {
             e = hipMemcpyAsync(seg_dgram, D + L.sdg, (size_t)ns * dstride, hipMemcpyDeviceToHost, sm);
             if (e == hipSuccess)
                 e = hipMemcpyAsync(seg_dlen, D + L.sdl, (size_t)ns * sizeof(uint16_t), hipMemcpyDeviceToHost, sm);

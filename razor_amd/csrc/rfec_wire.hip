@@ -624,7 +624,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                                                       const uint32_t* __restrict__ order,
                                                       uint8_t* __restrict__ dgram, uint16_t* __restrict__ dlen,
                                                       uint32_t count, uint32_t stride, uint32_t capacity,
-                                                      uint32_t dstride)
+                                                      uint32_t dstride, uint32_t rows_out)
 {
     constexpr int ND = B / 4;
     static_assert(B == 32, "slots up to 1,280 bytes take k_frame_seg_q");
@@ -645,6 +645,8 @@ __global__ __launch_bounds__(kBlock) void k_frame_seg(const uint8_t* __restrict_
                               },
                               [&](const PW& P, uint32_t d) {
             const uint32_t o = order ? order[d] : d; // output slot
+            if (o >= rows_out) // (a row the caller's output does not hold: not framed)
+                return;
             uint8_t* slot = dgram + (size_t)o * dstride;
             rfec_hdr h;
             {
@@ -1412,7 +1414,7 @@ __device__ __forceinline__ void load_rows_q(__amdgpu_buffer_rsrc_t rin, uint32_t
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_frame_seg_q(
     const uint8_t* __restrict__ shards, const rfec_hdr* __restrict__ hdr, const rfec_seg_stamp* __restrict__ stamps,
     const uint32_t* __restrict__ order, uint8_t* __restrict__ dgram, uint16_t* __restrict__ dlen, uint32_t count,
-    uint32_t stride, uint32_t capacity, uint32_t dstride)
+    uint32_t stride, uint32_t capacity, uint32_t dstride, uint32_t rows_out)
 {
     __shared__ __attribute__((aligned(16))) uint32_t T[kQTabDwords];
     {
@@ -1429,7 +1431,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     if (q >= nquads)
         return;
     const __amdgpu_buffer_rsrc_t rin = rsrc64(shards, (uint64_t)count * stride);
-    const __amdgpu_buffer_rsrc_t rout = rsrc64(dgram, (uint64_t)count * dstride);
+    const __amdgpu_buffer_rsrc_t rout = rsrc64(dgram, (uint64_t)rows_out * dstride); // (rows >= rows_out: dropped)
     // the batch: lane 4 t + g holds quad q + t nw's datagram g
     SegHdrQ B;
     auto pass = [&](uint32_t q0) {
@@ -1531,7 +1533,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
                     __builtin_amdgcn_raw_buffer_store_b128(v4u{out[k][0], out[k][1], out[k][2], out[k][3]}, rout,
                                                            obase + 16u * c, 0, kAuxST);
             }
-            if (s == 0)
+            if (s == 0 && o < rows_out)
                 dlen[o] = (uint16_t)(valid ? n + 4u : 0u);
         }
         q += nw;
@@ -1974,16 +1976,16 @@ int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacit
 
 int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* shards,
                                const rfec_hdr* hdr, const rfec_seg_stamp* stamps, const uint32_t* order,
-                               uint32_t dstride, uint8_t* dgram, uint16_t* dlen, void* stream)
+                               uint32_t dstride, uint8_t* dgram, uint16_t* dlen, uint32_t rows_out, void* stream)
 {
     hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
     if (quarter_ok(count, stride, dstride)) {
         const uint32_t quads = (count + 3u) / 4u;
         RFEC_LAUNCH(k_frame_seg_q, dim3(grid_for<6>((const void*)k_frame_seg_q, quads)), dim3(kBlock), 0, sm, shards,
-                    hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride);
+                    hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride, rows_out);
     } else // slots above 1,280 bytes (or a batch past 32-bit buffer offsets): 32-byte lanes
         RFEC_LAUNCH(k_frame_seg<32>, dim3(grid_for<3>((const void*)k_frame_seg<32>, count)), dim3(kBlock), 0, sm,
-                           shards, hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride);
+                           shards, hdr, stamps, order, dgram, dlen, count, stride, capacity, dstride, rows_out);
     return (int)hipGetLastError();
 }
 

@@ -81,7 +81,7 @@ class rfec_send_report(C.Structure):
     _fields_ = [("n_segs", C.c_uint32), ("n_groups", C.c_uint32), ("n_parities", C.c_uint32),
                 ("n_shapes", C.c_uint32), ("plan_us", C.c_double), ("stage_us", C.c_double),
                 ("h2d_us", C.c_double), ("kernel_us", C.c_double), ("d2h_us", C.c_double),
-                ("total_us", C.c_double)]
+                ("total_us", C.c_double), ("zero_copy", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class rfec_rx_session_info(C.Structure):
@@ -153,7 +153,7 @@ class rfec_host_timing(C.Structure):
                 ("zero_copy", C.c_uint32), ("reserved", C.c_uint32)]
 
 
-RFEC_ABI_VERSION = 6  # include/razor_fec.h
+RFEC_ABI_VERSION = 7  # include/razor_fec.h
 
 
 def seg_dtype(video_size: int) -> np.dtype:

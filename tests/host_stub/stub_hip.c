@@ -271,7 +271,7 @@ int rfec_launch_wire_frame_fec(uint32_t count, uint32_t stride, uint32_t capacit
 
 int rfec_launch_wire_frame_seg(uint32_t count, uint32_t stride, uint32_t capacity, const uint8_t* shards,
                                const rfec_hdr* hdr, const rfec_seg_stamp* stamps, const uint32_t* order,
-                               uint32_t dstride, uint8_t* dgram, uint16_t* dlen, void* stream)
+                               uint32_t dstride, uint8_t* dgram, uint16_t* dlen, uint32_t rows_out, void* stream)
 {
     return 0;
 }
@@ -341,6 +341,17 @@ int rfec_launch_host_gather(const uint64_t* sptrs, uint32_t ns, uint8_t* shards,
     (void)sptrs, (void)ns, (void)shards, (void)hdr, (void)fptrs, (void)nf, (void)parity, (void)meta, (void)fsize,
         (void)fecid, (void)stride, (void)video, (void)aux_src, (void)aux_dst, (void)aux_n, (void)stream;
     return (int)hipErrorNotSupported;
+}
+int rfec_launch_send_gather(const uint64_t* src, const uint16_t* size, uint32_t slots, uint32_t stride, uint8_t* dst,
+                            void* stream)
+{
+    (void)stream;
+    for (uint32_t s = 0; s < slots; ++s) {
+        memset(dst + (size_t)s * stride, 0, stride);
+        if (src[s])
+            memcpy(dst + (size_t)s * stride, (const void*)(uintptr_t)src[s], size[s]);
+    }
+    return 0;
 }
 int rfec_launch_host_scatter_fec(const uint64_t* fptrs, uint32_t groups, const rfec_kplan* P, uint32_t stride,
                                  const uint8_t* parity, const rfec_hdr* meta, const uint16_t* fsize,

@@ -32,13 +32,32 @@ def _fnv(b: bytes) -> int:
     return h
 
 
-def _check_scenario(lib, oracle, scn, splits):
+def _check_scenario(lib, oracle, scn, splits, zero_copy=False):
     frames, blob = po.stage_frames(scn)
+    keep = []
+    if zero_copy:  # frames and datagram outputs in rfec_pinned_alloc blocks: the device reads / writes them
+        pb, k = lib.pinned_array(blob.shape, np.uint8)
+        pb[...] = blob
+        frames["data"] = frames["data"] - np.uint64(blob.ctypes.data) + np.uint64(pb.ctypes.data)
+        blob = pb
+        keep.append(k)
     st = lib.sender_init()
     segs, groups, sdg, sdl, fdg, fdl = [], [], [], [], [], []
     seg_base = 0
     for lo, hi in zip(splits[:-1], splits[1:]):
-        s, g, a, al, b, bl, rep = lib.send_frames(st, frames[lo:hi], UID, DSTRIDE)
+        bufs, kw = None, {}
+        if zero_copy:
+            ms = 64 * (hi - lo) + 256
+            mp = 2 * ms
+            out = [lib.pinned_array(shape, dt) for shape, dt in (((ms, DSTRIDE), np.uint8), ((ms,), np.uint16),
+                                                                 ((mp, DSTRIDE), np.uint8), ((mp,), np.uint16))]
+            keep += [o[1] for o in out]
+            bufs = tuple(o[0] for o in out)
+            kw = dict(max_segs=ms, max_parities=mp, bufs=bufs)
+        s, g, a, al, b, bl, rep = lib.send_frames(st, frames[lo:hi], UID, DSTRIDE, **kw)
+        if zero_copy:
+            assert rep.zero_copy == 3 or (rep.n_segs == 0 and rep.zero_copy & 2), rep.zero_copy
+            a, al, b, bl = a.copy(), al.copy(), b.copy(), bl.copy()
         s = s.copy()
         s["frame"] += lo
         g = g.copy()
@@ -98,16 +117,23 @@ def _check_scenario(lib, oracle, scn, splits):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("zero_copy", [False, True])
 @pytest.mark.parametrize("name", ["steady_k10_pf80", "mixed", "fractions"])
-def test_send_frames_gpu(lib, oracle1000, name):
+def test_send_frames_gpu(lib, oracle1000, name, zero_copy):
+    """zero_copy: the frames and the datagram outputs in pinned blocks (the
+    device gathers the segments out of the frames at their byte offsets and
+    frames straight into the outputs)."""
     scn = {s["name"]: s for s in po.stage_fixture()["scenarios"]}[name]
-    _check_scenario(lib, oracle1000, scn, [0, len(scn["frames"])])
+    _check_scenario(lib, oracle1000, scn, [0, len(scn["frames"])], zero_copy)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("zero_copy", [False, True])
 @pytest.mark.parametrize("name", ["mixed", "fractions"])
-def test_send_frames_split_calls_gpu(lib, oracle1000, name):
-    """The same frames over several calls: open groups are carried across."""
+def test_send_frames_split_calls_gpu(lib, oracle1000, name, zero_copy):
+    """The same frames over several calls: open groups are carried across
+    (zero copy: the carried segments from the pinned staging, the rows of
+    their datagrams past the caller's output not written)."""
     scn = {s["name"]: s for s in po.stage_fixture()["scenarios"]}[name]
     n = len(scn["frames"])
-    _check_scenario(lib, oracle1000, scn, [0, 1, 2, 5, n // 2, n // 2 + 1, n])
+    _check_scenario(lib, oracle1000, scn, [0, 1, 2, 5, n // 2, n // 2 + 1, n], zero_copy)

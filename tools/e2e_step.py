@@ -100,14 +100,20 @@ def run(lib, G, full, reps, mem):
     assert zc == (mem == "pinned") and (zc or not any(r["zero_copy"] for r in enc)), mem
     if zc:  # the structs themselves cross PCIe (16-B chunks from the data's dword), + 8-B pointers
         ss, fs = segs.dtype.itemsize, fecs.dtype.itemsize
-        # receive side: whole structs only on lines that hold an erased member, the rest as a 64-B header
+        # receive side: whole structs only on the lines the decode reads (row layouts: the lines that hold an
+        # erased member; the matrix plan: the first line firing at once per target, else the mask schedule),
+        # the rest as a 64-B header
         lm = [set(plan.members(l)) for l in range(n)]
         cnt = {}
         for a, b in erased.tolist():
             cnt[(a, b)] = cnt.get((a, b), 0) + 1
         nseg = nfec = nhdr = 0
+        cascade = full  # the sender's matrix plan: the dense cascade decode (rfec_hostmem.c zc_lines_read)
         for (a, b), m in cnt.items():
-            lines = [l for l in range(n) if a in lm[l] or b in lm[l]]
+            if cascade:
+                lines = lines_read(lm, k, {a, b}, 2)
+            else:
+                lines = [l for l in range(n) if a in lm[l] or b in lm[l]]
             need = set().union(*(lm[l] for l in lines)) - {a, b}
             nseg += m * len(need)
             nfec += m * len(lines)
@@ -128,6 +134,35 @@ def run(lib, G, full, reps, mem):
             "step_e2e_gibps": round((enc_bytes + dec_bytes) / (wall * 1e-6) / 2**30, 2),
             "pcie_bytes": pcie,
             "bytes": {"encode": enc_bytes, "decode": dec_bytes}, "reps": reps, "verified": ok}
+
+
+def lines_read(lm, k, erased, E):
+    """rfec_hostmem.c zc_lines_read with every parity received: per erased member of rank < E, the first
+    line (plan order) that fires at once for it; if one has none, every step of the canonical mask schedule."""
+    n = len(lm)
+    have = set(range(k)) - set(erased)
+    lines, casc = set(), False
+    for t in sorted(erased)[:E]:
+        l = next((l for l in range(n) if t in lm[l] and (lm[l] - have) == {t} and lm[l] & have), None)
+        if l is None:
+            casc = True
+        else:
+            lines.add(l)
+    if casc:
+        h, er, progress = set(have), sorted(erased), True
+        while progress:
+            progress = False
+            for l in range(n):
+                x = lm[l] - h
+                if len(x) != 1 or not (lm[l] & h):
+                    continue
+                t = next(iter(x))
+                if er.index(t) >= E:
+                    continue
+                lines.add(l)
+                h.add(t)
+                progress = True
+    return sorted(lines)
 
 
 def main():

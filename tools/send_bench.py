@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=8192)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--pageable", action="store_true", help="datagrams into fresh pageable numpy arrays per call")
+    ap.add_argument("--frames-mem", default="pinned", choices=("pinned", "pageable"),
+                    help="frame bytes in an rfec_pinned_alloc block (the device gathers the segments itself) or not")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     lib = native(1200)
@@ -46,6 +48,12 @@ def main():
     frames["payload_type"] = 96
     frames["protect_fraction"] = 80
     frames["now_ms"] = 1_700_000_000_000 + np.arange(F) * 33
+    keep_frames = None
+    if args.frames_mem == "pinned":  # what a capture / encoder hands over: frames in pinned, device-mapped memory
+        pb, keep_frames = lib.pinned_array(blob.shape, np.uint8)
+        pb[...] = blob
+        frames["data"] = pb.ctypes.data + np.arange(F, dtype=np.uint64) * (k * S)
+        blob = pb
     dstride = 1280  # 10 x 128 B: whole-line datagram stores
     bufs, keep_alive = None, []
     if not args.pageable:  # datagram slots in pinned memory, reused across calls (what a sender hands to sendmmsg)
@@ -70,8 +78,9 @@ def main():
                 tot[key] += getattr(r, key)
             nseg += r.n_segs
             npar += r.n_parities
+            zc = r.zero_copy
             if c0 == 0:
-                keep = (segs.copy(), groups.copy(), fdg[:64].copy(), fdl[:64].copy())
+                keep = (segs.copy(), groups.copy(), fdg[:64].copy(), fdl[:64].copy(), sdg[:256].copy(), sdl[:256].copy())
         wall = time.perf_counter() - t0
         if best is None or wall < best[0]:
             best = (wall, tot, nseg, npar, keep)
@@ -79,8 +88,15 @@ def main():
     # verify: the first groups' SIM_FEC datagrams against the oracle
     from pyoracle import FEC_STAMP, HDR_DTYPE, Oracle
     o = Oracle(1200)
-    segs, groups, fdg0, fdl0 = keep
+    segs, groups, fdg0, fdl0, sdg0, sdl0 = keep
     ok = True
+    # the first SIM_SEG datagrams: parsed back, payload = the frame bytes
+    recs, pay = o.parse_batch(sdg0, sdl0, 1216, S)
+    for i in range(len(sdl0)):
+        off = int(frames["data"][segs["frame"][i]]) - blob.ctypes.data + int(segs["offset"][i])
+        ds = int(segs["data_size"][i])
+        ok = ok and int(recs["status"][i]) == 0 and int(recs["hdr"]["seq"][i]) == int(segs["packet_id"][i]) and \
+            bool(np.array_equal(pay[i, :ds], blob[off:off + ds]))
     p = 0
     for g in groups[:8]:
         plan = o.plan_from_fraction(int(g["count"]), int(g["protect_fraction"]), 3)
@@ -106,7 +122,10 @@ def main():
         p += n
     frame_bytes = F * k * S
     dgram_bytes = nseg * (S + 32) + npar * (S + 49)
-    res = {"frames": F, "chunk": CH, "output_memory": "pageable" if args.pageable else "pinned", "segments": nseg, "parities": npar, "frame_bytes": frame_bytes,
+    res = {"frames": F, "chunk": CH, "output_memory": "pageable" if args.pageable else "pinned",
+           "frames_memory": args.frames_mem, "zero_copy": {"in": bool(zc & 1), "out": bool(zc & 2)},
+           "segments": nseg, "parities": npar, "frame_bytes": frame_bytes,
+           "pcie_GBps": (frame_bytes + dgram_bytes) / wall / 1e9,
            "datagram_bytes": dgram_bytes, "wall_s": wall, "stage_us": tot, "frames_GiBps": frame_bytes / wall / 2**30,
            "datagrams_per_s": (nseg + npar) / wall, "gpu_only_GiBps": frame_bytes / (tot["kernel_us"] * 1e-6) / 2**30,
            "verified_sample": ok}
