@@ -152,6 +152,7 @@ int rfec_sender_plan(rfec_sender_state* st, const rfec_frame* frames, uint32_t n
 }
 
 /* ---- frames -> datagrams ------------------------------------------------- */
+#define SD_CHUNKS 16 /* slot chunks of one call at most */
 typedef struct {
     uint8_t* h;     /* pinned host */
     uint8_t* hd;    /* h as the device addresses it (NULL: not mapped) */
@@ -159,6 +160,9 @@ typedef struct {
     size_t bytes;
     uint8_t* carry; /* the open group's segments (slots then headers), host */
     uint32_t n_carry;
+    hipStream_t sg;                  /* the slots' arrival (chunks), beside the framing's stream */
+    hipEvent_t evc[SD_CHUNKS + 1];   /* chunk c arrived; [SD_CHUNKS]: the tables copied */
+    int have_ev;
 } sd_ctx;
 
 static __thread sd_ctx t_sd;
@@ -484,16 +488,58 @@ int rfec_host_send_frames(rfec_sender_state* st, const rfec_frame* frames, uint3
                 goto out;
             }
         uint8_t* D = t_sd.d;
-        (void)hipEventRecord(ev[0], sm);
-        const size_t c0 = zc_in ? L.hdr : 0; /* zero copy: the tables only, then the device's frame reads */
-        e = hipMemcpyAsync(D + c0, t_sd.h + c0, L.in_end - c0, hipMemcpyHostToDevice, sm);
-        if (e == hipSuccess && zc_in && n_slots) {
-            const int ke = rfec_launch_send_gather((const uint64_t*)(D + L.src), (const uint16_t*)(D + L.ssz), n_slots,
-                                                   DI_STRIDE, D + L.slots, sm);
-            if (ke)
-                rc = set_err(RFEC_EDEVICE, "send gather launch", ke);
+        /* The slots arrive in chunks on a second stream (the device's reads of the frames, or the slots'
+           H2D) while the SIM_SEG framing of the chunks before writes on this one: the link carries reads
+           and writes together.  The encode and the SIM_FEC framing follow the last chunk. */
+        uint32_t K = zc_in && n_slots >= 8192 ? n_slots / 2048 : 1; /* (staged: one H2D measured faster) */
+        {
+            const char* v = getenv("RFEC_SEND_CHUNKS");
+            K = v ? (uint32_t)atoi(v) : K;
+            K = K < 1 ? 1 : K > SD_CHUNKS ? SD_CHUNKS : K;
         }
+        if (!t_sd.sg && (e = hipStreamCreateWithFlags(&t_sd.sg, hipStreamNonBlocking)) != hipSuccess) {
+            rc = set_err(RFEC_EDEVICE, "send stream", e);
+            goto out;
+        }
+        for (uint32_t c = 0; c <= SD_CHUNKS && !t_sd.have_ev; ++c)
+            if ((e = hipEventCreate(&t_sd.evc[c])) != hipSuccess) {
+                rc = set_err(RFEC_EDEVICE, "send event", e);
+                goto out;
+            }
+        t_sd.have_ev = 1;
+        (void)hipEventRecord(ev[0], sm);
+        e = hipMemcpyAsync(D + L.hdr, t_sd.h + L.hdr, L.in_end - L.hdr, hipMemcpyHostToDevice, sm); /* tables */
+        (void)hipEventRecord(t_sd.evc[SD_CHUNKS], sm);
         (void)hipEventRecord(ev[1], sm);
+        if (e == hipSuccess)
+            e = hipStreamWaitEvent(t_sd.sg, t_sd.evc[SD_CHUNKS], 0);
+        for (uint32_t c = 0; c < K && e == hipSuccess && !rc; ++c) {
+            const uint32_t s0 = (uint32_t)((uint64_t)n_slots * c / K), s1 = (uint32_t)((uint64_t)n_slots * (c + 1) / K);
+            if (zc_in) {
+                const int ke = rfec_launch_send_gather((const uint64_t*)(D + L.src) + s0, (const uint16_t*)(D + L.ssz) + s0,
+                                                       s1 - s0, DI_STRIDE, D + L.slots + (size_t)s0 * DI_STRIDE, t_sd.sg);
+                if (ke)
+                    rc = set_err(RFEC_EDEVICE, "send gather launch", ke);
+            } else {
+                e = hipMemcpyAsync(D + L.slots + (size_t)s0 * DI_STRIDE, t_sd.h + L.slots + (size_t)s0 * DI_STRIDE,
+                                   (size_t)(s1 - s0) * DI_STRIDE, hipMemcpyHostToDevice, t_sd.sg);
+            }
+            if (e == hipSuccess)
+                e = hipEventRecord(t_sd.evc[c], t_sd.sg);
+            if (e == hipSuccess)
+                e = hipStreamWaitEvent(sm, t_sd.evc[c], 0);
+            int ke = 0;
+            if (e == hipSuccess && !rc && s1 > s0) /* (zero copy: the carried rows, past ns, dropped) */
+                ke = rfec_launch_wire_frame_seg(s1 - s0, DI_STRIDE, SIM_VIDEO_SIZE, D + L.slots + (size_t)s0 * DI_STRIDE,
+                                                (const rfec_hdr*)(D + L.hdr) + s0,
+                                                (const rfec_seg_stamp*)(D + L.sstamp) + s0,
+                                                (const uint32_t*)(D + L.sorder) + s0, dstride,
+                                                zc_out ? (uint8_t*)((uintptr_t)seg_dgram + dsg) : D + L.sdg,
+                                                zc_out ? (uint16_t*)((uintptr_t)seg_dlen + dsl) : (uint16_t*)(D + L.sdl),
+                                                zc_out ? ns : n_slots, sm);
+            if (ke)
+                rc = set_err(RFEC_EDEVICE, "frame launch", ke);
+        }
         uint32_t slot0 = 0, p0 = 0;
         for (uint32_t q = 0; q < ng && e == hipSuccess && !rc;) {
             const uint32_t key = shape[2 * q];
@@ -516,14 +562,7 @@ int rfec_host_send_frames(rfec_sender_state* st, const rfec_frame* frames, uint3
             q = q1;
         }
         int ke = 0;
-        if (!rc && e == hipSuccess && n_slots)
-            ke = rfec_launch_wire_frame_seg(n_slots, DI_STRIDE, SIM_VIDEO_SIZE, D + L.slots,
-                                            (const rfec_hdr*)(D + L.hdr), (const rfec_seg_stamp*)(D + L.sstamp),
-                                            (const uint32_t*)(D + L.sorder), dstride,
-                                            zc_out ? (uint8_t*)((uintptr_t)seg_dgram + dsg) : D + L.sdg,
-                                            zc_out ? (uint16_t*)((uintptr_t)seg_dlen + dsl) : (uint16_t*)(D + L.sdl),
-                                            zc_out ? ns : n_slots, sm); /* (zero copy: the carried rows dropped) */
-        if (!rc && !ke && e == hipSuccess && n_par)
+        if (!rc && e == hipSuccess && n_par)
             ke = rfec_launch_wire_frame_fec(n_par, DI_STRIDE, SIM_VIDEO_SIZE, D + L.parity,
                                             (const rfec_hdr*)(D + L.meta), (const uint16_t*)(D + L.fsize),
                                             (const int8_t*)(D + L.status), (const rfec_fec_stamp*)(D + L.fstamp),
@@ -548,8 +587,9 @@ int rfec_host_send_frames(rfec_sender_state* st, const rfec_frame* frames, uint3
         hipError_t e2 = hipStreamSynchronize(sm);
         if (!rc && (e != hipSuccess || e2 != hipSuccess))
             rc = set_err(RFEC_EDEVICE, "send frames: copy / sync", e != hipSuccess ? e : e2);
-        float a = 0, b = 0, d = 0;
-        (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+        float a = 0, b = 0, d = 0; /* h2d: the tables and the slots' arrival (overlapped with the SIM_SEG
+                                       framing, in kernel_us too) */
+        (void)hipEventElapsedTime(&a, ev[0], t_sd.evc[K - 1]);
         (void)hipEventElapsedTime(&b, ev[1], ev[2]);
         (void)hipEventElapsedTime(&d, ev[2], ev[3]);
         rep->h2d_us = a * 1e3;
