@@ -933,12 +933,29 @@ static int zc_recover_groups(const rfec_plan* plan, uint32_t groups, sim_segment
                         pn |= 1ull << l;
                     }
             }
-            for (uint32_t i = 0; i < k; ++i)
-                if (spt[(size_t)g * k + i] && !((i < 64 ? n0 >> i : n1 >> (i - 64)) & 1))
-                    spt[(size_t)g * k + i] |= 1;
-            for (uint32_t l = 0; l < n; ++l)
-                if (fpt[(size_t)g * n + l] && !(pn >> l & 1))
-                    fpt[(size_t)g * n + l] |= 1;
+            /* a struct on no received line that holds an erased member is read by no peel, not even the
+               exact one after a rejected line: it does not cross at all (pointer 0; the masks above still
+               say it arrived) -- except the group's first parity, whose fec_id the scatter stamps */
+            uint64_t a0 = 0, a1 = 0, pa = 0;
+            if (trim)
+                for (uint32_t l = 0; l < n; ++l)
+                    if ((pm >> l & 1) && ((M.mask[l][0] & e0) | (M.mask[l][1] & e1))) {
+                        a0 |= M.mask[l][0];
+                        a1 |= M.mask[l][1];
+                        pa |= 1ull << l;
+                    }
+            pa |= pm & (~pm + 1);
+            for (uint32_t i = 0; i < k; ++i) {
+                uint64_t* sp = &spt[(size_t)g * k + i];
+                if (!*sp || ((i < 64 ? n0 >> i : n1 >> (i - 64)) & 1))
+                    continue;
+                *sp = trim && !((i < 64 ? a0 >> i : a1 >> (i - 64)) & 1) ? 0 : *sp | 1;
+            }
+            for (uint32_t l = 0; l < n; ++l) {
+                uint64_t* fp = &fpt[(size_t)g * n + l];
+                if (*fp && !(pn >> l & 1))
+                    *fp = trim && !(pa >> l & 1) ? 0 : *fp | 1;
+            }
         }
         tab_us += now_us() - tt;
         /* no DMA: the kernels read the tables from the pinned slot, the first

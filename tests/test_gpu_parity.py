@@ -550,6 +550,52 @@ def test_host_recover_groups(product1200, oracle1200, k, layers, G, mem):
     assert (out.view(np.uint8).reshape(G * E, -1)[untouched] == 0xA5).all()
 
 
+def test_host_recover_groups_rejections_zero_copy(product1200, oracle1200):
+    """The zero-copy recover on the sender's 3 x 4 plan sends whole only the
+    lines the dense cascade decode reads, as headers the rest of the lines
+    holding an erased member, and nothing of the others (rfec_hostmem.c
+    zc_lines_read).  With header rejections (a parity whose fec_data_size is
+    below its members' sizes: the exact peel bans the line and recovers
+    through another, whose members may have crossed as headers only) the
+    out_index / recovered masks / out_seg structs equal the staged path's on
+    pageable copies of the same structs, field for field."""
+    from razor_amd.fec import fec_dtype, seg_dtype
+
+    lib, o = product1200, oracle1200
+    G, k, S, E = 3000, 10, 1200, 3
+    shards, hdr, segs, ks = _host_segs(lib, o, 205, G, k, S, "pinned")
+    plan = o.plan_from_fraction(k, 80, 3)
+    n = plan.n_lines
+    fecs, kf = _host_arrays(lib, G * n, fec_dtype(1200), "pinned")
+    sp, fp = _ptrs(segs), _ptrs(fecs)
+    lib.host_encode_groups(plan, G, sp, fp, fec_id0=1)
+    rng = np.random.default_rng(11)
+    sp_rx, fp_rx = sp.copy(), fp.copy()
+    for g in range(G):
+        lost = rng.choice(k, int(rng.integers(1, 4)), replace=False)
+        sp_rx[g * k + lost] = 0
+        fp_rx[g * n + rng.choice(n, int(rng.integers(0, 2)), replace=False)] = 0
+    bad = rng.choice(G * n, G // 3, replace=False)  # their lines fail the size check when they fire
+    fecs["fec_data_size"][bad] = 600
+    out, ko = _host_arrays(lib, G * E, seg_dtype(1200), "pinned", fill=0xA5)
+    oi, rec, t = lib.host_recover_groups(plan, G, sp_rx, fp_rx, E, _ptrs(out))
+    assert t["zero_copy"] == 1
+    pseg = np.zeros(G * k, segs.dtype)
+    pseg[...] = segs
+    pfec = np.zeros(G * n, fecs.dtype)
+    pfec[...] = fecs
+    pout = np.zeros(G * E, out.dtype)
+    pout.view(np.uint8)[...] = 0xA5
+    oi2, rec2, t2 = lib.host_recover_groups(plan, G, np.where(sp_rx == 0, 0, _ptrs(pseg)),
+                                            np.where(fp_rx == 0, 0, _ptrs(pfec)), E, _ptrs(pout))
+    assert t2["zero_copy"] == 0
+    assert np.array_equal(oi2, oi) and np.array_equal(rec2, rec)
+    _fields_equal(out, pout, "data_size", "data")
+    # the header checks changed the peel in a good share of the groups
+    mask_only = np.array([bin(int(r)).count("1") for r in rec[:, 0]])
+    assert (oi != 0xFF).sum() > G // 2 and mask_only.sum() > 0
+
+
 def _gapped(lib, n, dtype, gap, fill, canary):
     """n structs of `dtype` in ONE rfec_pinned_alloc block, `gap` canary bytes
     after each (the last struct ends exactly at the block's end): returns the

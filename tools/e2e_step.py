@@ -110,14 +110,17 @@ def run(lib, G, full, reps, mem):
         nseg = nfec = nhdr = 0
         cascade = full  # the sender's matrix plan: the dense cascade decode (rfec_hostmem.c zc_lines_read)
         for (a, b), m in cnt.items():
-            if cascade:
-                lines = lines_read(lm, k, {a, b}, 2)
-            else:
-                lines = [l for l in range(n) if a in lm[l] or b in lm[l]]
+            held = [l for l in range(n) if a in lm[l] or b in lm[l]]  # received lines holding an erased member
+            lines = lines_read(lm, k, {a, b}, 2) if cascade else held
             need = set().union(*(lm[l] for l in lines)) - {a, b}
             nseg += m * len(need)
             nfec += m * len(lines)
-            nhdr += m * (k - 2 - len(need) + n - len(lines))
+            if cascade:  # headers: the rest of the held lines (+ the first parity); nothing else crosses
+                hs = set().union(*(lm[l] for l in held)) - {a, b} - need
+                hf = (set(held) | {0}) - set(lines)
+                nhdr += m * (len(hs) + len(hf))
+            else:
+                nhdr += m * (k - 2 - len(need) + n - len(lines))
         pcie = {"encode_h2d": G * k * (ss + 8) + G * n * 8, "encode_d2h": G * n * fs,
                 "decode_h2d": nseg * ss + nfec * fs + nhdr * 64 + G * ((k + n + 2) * 8 + 24),
                 "decode_d2h": G * 2 * ss + 17 * G * 2}
