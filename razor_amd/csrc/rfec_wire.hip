@@ -1737,16 +1737,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
 // ---------------------------------------------------------------------------
 // (rin: a descriptor over the whole batch, per-lane offsets < 2^32; the second
 // dword may lie in the next slot, or past the batch: 0)
-__device__ __forceinline__ uint32_t load_trailer(__amdgpu_buffer_rsrc_t rin, uint32_t d, uint32_t len, bool active,
-                                                 uint32_t dstride)
-{
-    if (!active || len < 4 || len > dstride)
-        return 0;
-    const uint32_t tp = len - 4;
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rin, d * dstride + (tp & ~3u), 0, kAuxNT);
-    return bswap(__builtin_amdgcn_alignbyte(v[1], v[0], tp & 3u));
-}
-
 // bytes >= m of one 16-byte chunk (byte offset c0 in its message) zeroed
 __device__ __forceinline__ uint32_t keep_below(uint32_t v, int j, int e)
 {
@@ -1781,7 +1771,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const __amdgpu_buffer_rsrc_t rout = rsrc64(payload, (uint64_t)n * stride);
     constexpr uint32_t kOut = 0xFFFFFFF0u;
     const uint32_t rows_in = min(dstride, kQWindow); // the slot's bytes a lane may load
-    uint32_t F = 0, TR = 0, bt = 0;
+    uint32_t F = 0, bt = 0;
     // the headers of quads q0, q0 + nw, ... (16 of them), one datagram per lane
     auto header_pass = [&](uint32_t q0) {
         const uint32_t dd = 4u * (q0 + (lane >> 2) * nw) + (lane & 3u);
@@ -1789,7 +1779,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         __builtin_amdgcn_s_setprio(3);
         HdrIn in;
         load_header(dgram, dlen, dd, a, dstride, in);
-        TR = load_trailer(rin, dd, in.len, a, dstride);
         F = decode_header<20>(in, recs, dd, a, dstride, capacity);
         __builtin_amdgcn_s_setprio(0);
     };
@@ -1816,7 +1805,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         const uint32_t d = 4u * q + g;
         const bool act = d < n;
         const uint32_t src = 4u * bt + g;
-        const uint32_t f = bperm(F, src), tr = bperm(TR, src);
+        const uint32_t f = bperm(F, src);
         ++bt;
         const bool valid = (f & kPkValid) != 0;
         const uint32_t len = f & 0xfffu, at1 = (f >> 12) & 63u, dsize = (f >> 18) & 0xfffu;
@@ -1828,7 +1817,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         // (j = (C - A) mod 80 from chunks C, C + 1 shifted down by r; stored
         // as if the CRC matched).
         __builtin_amdgcn_s_setprio(3);
-        uint32_t acc = 0;
+        uint32_t acc = 0, trl = 0; // trl: the trailer (the datagram's CRC32), from the lane whose chunk holds it
         v4u Y[kQRows]; // the payload chunks
         uint32_t PO[kQRows];
 #pragma unroll
@@ -1853,6 +1842,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                 const uint32_t a = dpp(X[k][i], kDppRowRor15);
                 const uint32_t b = k + 1 < kQRows ? dpp(X[k + 1 < kQRows ? k + 1 : k][i], kDppRowRor15) : 0u;
                 w[4 + i] = s == 15 ? b : a;
+            }
+            // the trailer, bytes [nb, nb + 4), from the rows already in registers (a separate load of the
+            // datagram's last line was a second HBM fetch of it: the parse fetched 1.17 x its reads)
+            if (16u * k + s == (nb >> 4)) {
+                const uint32_t i0 = (nb >> 2) & 3u;
+                const uint32_t lo = i0 == 0 ? w[0] : i0 == 1 ? w[1] : i0 == 2 ? w[2] : w[3];
+                const uint32_t hi = i0 == 0 ? w[1] : i0 == 1 ? w[2] : i0 == 2 ? w[3] : w[4];
+                trl = bswap(__builtin_amdgcn_alignbyte(hi, lo, nb & 3u));
             }
             // shift down by r: 8 bytes, 4 bytes, then the byte funnel.  The selects are byte permutes with a
             // per-lane selector (all bytes of one operand or the other): selects over array elements are
@@ -1884,7 +1881,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         const uint32_t R = row_xor(carry_q(T, acc, s + Dq));
         const uint32_t* iv = T + kQInv + Dr * 32u;
         const uint32_t b = (((R >> s) & 1u) ? iv[s] : 0u) ^ (((R >> (s + 16u)) & 1u) ? iv[s + 16u] : 0u);
-        const bool ok = valid && ~row_xor(b) == tr;
+        const bool ok = valid && ~row_xor(b) == row_xor(trl);
         __builtin_amdgcn_s_setprio(0);
         const uint32_t qn = q + nw;
         const bool batch_end = bt == 16; // (wave-uniform) the next quad starts a header batch
