@@ -96,6 +96,11 @@ typedef struct {
     uint32_t value;
 } rfec_rx_split; /* 8 bytes */
 int rfec_launch_rx_split(const rfec_wire_rec* recs, uint32_t n, uint32_t T, rfec_rx_split* out, void* stream);
+/* rfec_launch_wire_parse with the receiver session's split entries of the parsed records (T shards) written
+ * beside them (the quarter-wave parse writes them itself; the wave parses are followed by k_rx_split) */
+int rfec_launch_wire_parse_split(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
+                                 uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload,
+                                 uint32_t max_len, rfec_rx_split* split, uint32_t shards, void* stream);
 /* receiver groups above RFEC_MAX_K segments: out row = parity row ^ member rows (one dependency level per call) */
 typedef struct {
     int32_t out;       /* output row */

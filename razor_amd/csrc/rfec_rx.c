@@ -3185,6 +3185,12 @@ static int rx_session_push_staged(rfec_rx_session* S, uint32_t n, const uint8_t*
     return rc;
 }
 
+/* where a batch's split summary goes (sharded sessions), or NULL (one serial state; a huge push: split on the host) */
+static rfec_rx_split* rx_split_of(const rfec_rx_session* S, rx_stage* st, uint32_t n)
+{
+    return S->T == 1 || n > (1u << 20) ? NULL : st->sumd;
+}
+
 /* the split summary of records the device can read at `recs_d` into stage st (sharded sessions) */
 static int rx_split_launch(rfec_rx_session* S, rx_stage* st, const rfec_wire_rec* recs_d, uint32_t n, hipStream_t sm)
 {
@@ -3262,10 +3268,9 @@ int rfec_rx_session_push_datagrams(rfec_rx_session* S, uint32_t n, uint32_t dstr
         dl = st->dg + o_dl;
     }
     const double h2d_issue = now_us() - tt;
-    int ke = rfec_launch_wire_parse(n, dstride, dg, (const uint16_t*)dl, stride, S->capacity, S->store_d + S->nstore,
-                                    S->arena + (size_t)S->nstore * stride, max_dlen(dlen, n), t_rv.sm);
-    if (!ke)
-        ke = rx_split_launch(S, st, S->store_d + S->nstore, n, t_rv.sm);
+    const int ke = rfec_launch_wire_parse_split(n, dstride, dg, (const uint16_t*)dl, stride, S->capacity,
+                                                S->store_d + S->nstore, S->arena + (size_t)S->nstore * stride,
+                                                max_dlen(dlen, n), rx_split_of(S, st, n), S->T, t_rv.sm);
     if (ke || (e = hipStreamSynchronize(t_rv.sm)) != hipSuccess)
         return set_err(RFEC_EDEVICE, "recv: parse", ke ? ke : (int)e);
     const double staged = now_us() - tt;
@@ -3356,11 +3361,11 @@ int rfec_rx_session_push_datagrams_async(rfec_rx_session* S, uint32_t n, uint32_
             dl = st->dg + o_dl;
         }
         rep->h2d_us += now_us() - tt;
-        int ke = rfec_launch_wire_parse(n, dstride, dg, (const uint16_t*)dl, S->stride, S->capacity,
-                                        S->store_d + S->nstore + p, S->arena + (size_t)(S->nstore + p) * S->stride,
-                                        max_dlen(dlen, n), S->sa);
-        if (!ke)
-            ke = rx_split_launch(S, st, S->store_d + S->nstore + p, n, S->sa);
+        /* the parse writes the split entries beside the records (k_parse_q; the wave parses: k_rx_split) */
+        const int ke = rfec_launch_wire_parse_split(n, dstride, dg, (const uint16_t*)dl, S->stride, S->capacity,
+                                                    S->store_d + S->nstore + p,
+                                                    S->arena + (size_t)(S->nstore + p) * S->stride, max_dlen(dlen, n),
+                                                    rx_split_of(S, st, n), S->T, S->sa);
         if (ke || (e = hipEventRecord(st->done, S->sa)) != hipSuccess)
             return set_err(RFEC_EDEVICE, "rx session: parse", ke ? ke : (int)e);
     }

@@ -925,9 +925,26 @@ __device__ __forceinline__ void load_header(const uint8_t* __restrict__ dgram, c
     }
 }
 
+// the receiver session's split entry of a record (rfec_rx.c; k_rx_split's rules, rfec_kernels.hip)
+__device__ __forceinline__ void split_entry(const rfec_wire_rec& rec, uint32_t T, rfec_rx_split* __restrict__ out)
+{
+    uint32_t shard = 0xFFu, kind = RX_SPLIT_NONE, value = 0;
+    if (rec.status == RFEC_WIRE_OK && rec.mid == RFEC_WIRE_SEG) {
+        shard = (rec.fec_id ? rec.fec_id : rec.hdr.seq) % T;
+        kind = rec.fec_id && rec.hdr.seq ? RX_SPLIT_SEG_TS : RX_SPLIT_SEG;
+        value = rec.hdr.ts;
+    } else if (rec.status == RFEC_WIRE_OK && rec.mid == RFEC_WIRE_FEC) {
+        shard = rec.fec_id % T;
+        kind = RX_SPLIT_FEC;
+        value = rec.send_ts + 3000u;
+    }
+    *reinterpret_cast<uint2*>(out) = uint2{shard | kind << 8, value};
+}
+
 template <int B>
 __device__ __forceinline__ uint32_t decode_header(const HdrIn& in, rfec_wire_rec* __restrict__ recs, uint32_t d,
-                                                  bool active, uint32_t dstride, uint32_t capacity)
+                                                  bool active, uint32_t dstride, uint32_t capacity,
+                                                  rfec_rx_split* __restrict__ split = nullptr, uint32_t T = 1)
 {
     if (!active)
         return 0;
@@ -944,6 +961,8 @@ __device__ __forceinline__ uint32_t decode_header(const HdrIn& in, rfec_wire_rec
 #pragma unroll
     for (int t = 0; t < 4; ++t)
         o[t] = s[t]; // plain stores: the four 16-byte pieces merge in L2 (nontemporal ones measured slower)
+    if (split) // (a CRC mismatch found later rewrites the entry)
+        split_entry(rec, T, split + d);
     return pk;
 }
 
@@ -1751,7 +1770,8 @@ __device__ __forceinline__ uint32_t keep_below(uint32_t v, int j, int e)
 // three-deep 4-wave form (profiles/r05/ab/parse_occupancy/).
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_parse_q(
     const uint8_t* __restrict__ dgram, const uint16_t* __restrict__ dlen, rfec_wire_rec* __restrict__ recs,
-    uint8_t* __restrict__ payload, uint32_t n, uint32_t dstride, uint32_t stride, uint32_t capacity)
+    uint8_t* __restrict__ payload, uint32_t n, uint32_t dstride, uint32_t stride, uint32_t capacity,
+    rfec_rx_split* __restrict__ split, uint32_t shards)
 {
     __shared__ __attribute__((aligned(16))) uint32_t T[kQTabDwords];
     {
@@ -1779,7 +1799,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         __builtin_amdgcn_s_setprio(3);
         HdrIn in;
         load_header(dgram, dlen, dd, a, dstride, in);
-        F = decode_header<20>(in, recs, dd, a, dstride, capacity);
+        F = decode_header<20>(in, recs, dd, a, dstride, capacity, split, shards);
         __builtin_amdgcn_s_setprio(0);
     };
     // row k of quad qq's datagram (a lane past the batch or the slot reads 0 without a memory access)
@@ -1905,6 +1925,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                 static_assert(RFEC_WIRE_EBADCRC == -1 && offsetof(rfec_wire_rec, status) == 0, "record layout");
                 reinterpret_cast<v4u*>(recs + d)[s] = v4u{s == 0 ? 0xFFu : 0u, 0u, 0u, 0u};
             }
+            if (split && s == 0) // no control-plane effect
+                *reinterpret_cast<uint2*>(split + d) = uint2{0xFFu | RX_SPLIT_NONE << 8, 0u};
         }
         q = qn;
         if (q >= nquads)
@@ -1990,6 +2012,14 @@ int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, c
                            uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload,
                            uint32_t max_len, void* stream)
 {
+    return rfec_launch_wire_parse_split(n, dstride, dgram, dlen, stride, capacity, recs, payload, max_len, nullptr, 1,
+                                        stream);
+}
+
+int rfec_launch_wire_parse_split(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
+                                 uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload,
+                                 uint32_t max_len, rfec_rx_split* split, uint32_t shards, void* stream)
+{
     hipStream_t sm = reinterpret_cast<hipStream_t>(stream);
     // quarter-wave: the first 1,280 bytes of a slot, enough when the slot or every datagram fits;
     // payload slots of at most 1,280 bytes; both arrays within 32-bit buffer offsets
@@ -1998,7 +2028,7 @@ int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, c
         (uint64_t)n * dstride + kQWindow < 0xFFFFFFF0ull && (uint64_t)n * stride < 0xFFFFFFF0ull) {
         const uint32_t quads = (n + 3u) / 4u;
         RFEC_LAUNCH(k_parse_q, dim3(grid_for<8>((const void*)k_parse_q, quads)), dim3(kBlock), 0, sm, dgram, dlen,
-                    recs, payload, n, dstride, stride, capacity);
+                    recs, payload, n, dstride, stride, capacity, split, shards ? shards : 1u);
         return (int)hipGetLastError();
     }
     // 20-byte lanes cover 1,280 bytes of a slot: enough when the slot or every datagram fits
@@ -2008,7 +2038,9 @@ int rfec_launch_wire_parse(uint32_t n, uint32_t dstride, const uint8_t* dgram, c
     else
         RFEC_LAUNCH(k_parse<32>, dim3(grid_for<5>((const void*)k_parse<32>, n)), dim3(kBlock), 0, sm, dgram,
                            dlen, recs, payload, n, dstride, stride, capacity);
-    return (int)hipGetLastError();
+    const int e = (int)hipGetLastError();
+    // the wave parses write no split entries: the split kernel after them
+    return e || !split ? e : rfec_launch_rx_split(recs, n, shards ? shards : 1u, split, stream);
 }
 
 } // extern "C"

@@ -295,6 +295,14 @@ int rfec_launch_gather_rows(uint8_t* dst, const uint8_t* src, const int32_t* map
     return 0;
 }
 
+int rfec_launch_wire_parse_split(uint32_t n, uint32_t dstride, const uint8_t* dgram, const uint16_t* dlen,
+                                 uint32_t stride, uint32_t capacity, rfec_wire_rec* recs, uint8_t* payload,
+                                 uint32_t max_len, rfec_rx_split* split, uint32_t shards, void* stream)
+{
+    rfec_launch_wire_parse(n, dstride, dgram, dlen, stride, capacity, recs, payload, max_len, stream);
+    return split ? rfec_launch_rx_split(recs, n, shards, split, stream) : 0;
+}
+
 /* the receiver session's device stage: the gather and the table copy */
 int rfec_launch_rx_stage(uint8_t* dst, const uint8_t* src, const int32_t* map, uint32_t rows, uint32_t stride,
                          void* tdst, const void* tsrc, size_t tbytes, void* stream)
