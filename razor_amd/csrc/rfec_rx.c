@@ -444,6 +444,7 @@ typedef struct {
     size_t njsave, jsavecap;
     double tw_wake, tw_run, tw_pre; /* parallel replays: this shard's start after the replay's, its run and the
                                        part of it before the first arrival (us, summed) */
+    double tw_start;
     uint32_t tw_n, tw_recs;
 } rx_sim;
 
@@ -2574,7 +2575,7 @@ static void rx_shard_job(void* arg, uint32_t t)
     const double ts = now_us();
     X->tw_wake += ts - P->t0;
     X->tw_n++;
-    X->tw_pre -= ts;
+    X->tw_start = ts;
     rx_shard_replay(S, X, P, t);
     X->tw_run += now_us() - ts;
 }
@@ -2619,7 +2620,7 @@ static void rx_shard_replay(rfec_rx_session* S, rx_sim* X, const rx_par* P, uint
         const uint32_t pf = rx_prefetch();
         for (uint32_t i = 0; i < nm && i < pf; ++i)
             __builtin_prefetch(&R[X->mine[i]]);
-        X->tw_pre += now_us();
+        X->tw_pre += now_us() - X->tw_start;
         X->tw_recs += nm;
         for (uint32_t i = 0; i < nm && !X->oom; ++i) {
             if (i + pf < nm)
@@ -2632,7 +2633,7 @@ static void rx_shard_replay(rfec_rx_session* S, rx_sim* X, const rx_par* P, uint
     } else {
         const uint32_t* L = S->lst + S->loff[t];
         const uint32_t n = S->loff[t + 1] - S->loff[t];
-        X->tw_pre += now_us();
+        X->tw_pre += now_us() - X->tw_start;
         for (uint32_t i = 0; i < n && !X->oom; ++i) {
             if ((i & 15) == 0 && __atomic_load_n(&S->par.conflict, __ATOMIC_RELAXED))
                 return;
