@@ -1304,6 +1304,28 @@ __device__ const CrcQTables kCrcQ = make_crcq_tables();
 constexpr int kQTabDwords = (int)(sizeof(CrcQTables) / 4);
 constexpr int kQM = 16 * 256, kQNib = kQM + 4 * 256, kQInv = kQNib + 8 * 16 * kQCols;
 
+// The tables into the block's LDS (no barrier: the caller's): every thread's
+// loads in flight before its first LDS write -- the rolled copy waited for each
+// 16-byte load in turn, five round trips at the kernels' start.
+__device__ __forceinline__ void fill_tables(uint32_t* T)
+{
+    constexpr int N = kQTabDwords / 4, U = (N + kBlock - 1) / kBlock;
+    const v4u* src = reinterpret_cast<const v4u*>(&kCrcQ);
+    v4u* dst = reinterpret_cast<v4u*>(T);
+    v4u v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = (int)threadIdx.x + u * kBlock;
+        v[u] = src[i < N ? i : N - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int i = (int)threadIdx.x + u * kBlock;
+        if (i < N)
+            dst[i] = v[u];
+    }
+}
+
 // v * x^(8 * 256): four byte lookups
 __device__ __forceinline__ uint32_t mul_row(const uint32_t* T, uint32_t v)
 {
@@ -1436,13 +1458,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
     uint32_t stride, uint32_t capacity, uint32_t dstride, uint32_t rows_out)
 {
     __shared__ __attribute__((aligned(16))) uint32_t T[kQTabDwords];
-    {
-        const v4u* src = reinterpret_cast<const v4u*>(&kCrcQ);
-        v4u* dst = reinterpret_cast<v4u*>(T);
-        for (int i = threadIdx.x; i < kQTabDwords / 4; i += kBlock)
-            dst[i] = src[i];
-        __syncthreads();
-    }
+    fill_tables(T);
+    __syncthreads();
     const uint32_t lane = threadIdx.x & (kWave - 1), g = lane >> 4, s = lane & 15u;
     const uint32_t nquads = (count + 3u) / 4u;
     const uint32_t nw = gridDim.x * kWavesPerBlock;
@@ -1627,13 +1644,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
         fv |= __builtin_amdgcn_raw_buffer_load_b16(rfs, s == 11 ? 2u * dd : kOut, 0, kAuxNT);
         fv |= (uint32_t)(int32_t)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(rsu, s == 12 ? dd : kOut, 0, kAuxNT);
     };
-    {
-        const v4u* src = reinterpret_cast<const v4u*>(&kCrcQ);
-        v4u* dst = reinterpret_cast<v4u*>(T);
-        for (int i = threadIdx.x; i < kQTabDwords / 4; i += kBlock)
-            dst[i] = src[i];
-        __syncthreads();
-    }
+    fill_tables(T);
+    __syncthreads();
     if (q >= nquads)
         return;
     load(q);
@@ -1774,32 +1786,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     rfec_rx_split* __restrict__ split, uint32_t shards)
 {
     __shared__ __attribute__((aligned(16))) uint32_t T[kQTabDwords];
-    {
-        const v4u* src = reinterpret_cast<const v4u*>(&kCrcQ);
-        v4u* dst = reinterpret_cast<v4u*>(T);
-        for (int i = threadIdx.x; i < kQTabDwords / 4; i += kBlock)
-            dst[i] = src[i];
-        __syncthreads();
-    }
     const uint32_t lane = threadIdx.x & (kWave - 1), g = lane >> 4, s = lane & 15u;
     const uint32_t nquads = (n + 3u) / 4u;
     const uint32_t nw = gridDim.x * kWavesPerBlock;
     uint32_t q = wave_id();
-    if (q >= nquads)
-        return;
+    const bool live = q < nquads; // (the others still fill the tables)
     const __amdgpu_buffer_rsrc_t rin = rsrc64(dgram, (uint64_t)n * dstride);
     const __amdgpu_buffer_rsrc_t rout = rsrc64(payload, (uint64_t)n * stride);
     constexpr uint32_t kOut = 0xFFFFFFF0u;
     const uint32_t rows_in = min(dstride, kQWindow); // the slot's bytes a lane may load
     uint32_t F = 0, bt = 0;
-    // the headers of quads q0, q0 + nw, ... (16 of them), one datagram per lane
-    auto header_pass = [&](uint32_t q0) {
+    // the headers of quads q0, q0 + nw, ... (16 of them), one datagram per lane:
+    // loads, then the decode and the records (a batch's loads are issued before
+    // the previous quad's payload stores)
+    HdrIn hin;
+    auto header_load = [&](uint32_t q0) {
         const uint32_t dd = 4u * (q0 + (lane >> 2) * nw) + (lane & 3u);
-        const bool a = dd < n;
+        load_header(dgram, dlen, dd, dd < n, dstride, hin);
+    };
+    auto header_decode = [&](uint32_t q0) {
+        const uint32_t dd = 4u * (q0 + (lane >> 2) * nw) + (lane & 3u);
         __builtin_amdgcn_s_setprio(3);
-        HdrIn in;
-        load_header(dgram, dlen, dd, a, dstride, in);
-        F = decode_header<20>(in, recs, dd, a, dstride, capacity, split, shards);
+        F = decode_header<20>(hin, recs, dd, dd < n, dstride, capacity, split, shards);
         __builtin_amdgcn_s_setprio(0);
     };
     // row k of quad qq's datagram (a lane past the batch or the slot reads 0 without a memory access)
@@ -1814,13 +1822,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     // before this quad's payload stores: vmcnt counts loads and stores in issue
     // order, so a load issued after a store can only be waited for together
     // with that store (loads issued after the previous quad's stores wait for
-    // their write acknowledgements).  Only a batch's first quad, whose header
-    // pass runs after the stores (no row registers live across it), loads after.
-    header_pass(q);
+    // their write acknowledgements).  At a batch's end the next batch's header
+    // loads take the rows' place before the stores (fewer registers live across
+    // them); its first quad's rows are loaded after the stores, in flight while
+    // the headers decode.
+    // the first batch: the tables first (row loads issued ahead of them held
+    // the block's barrier back: SIM_FEC parse +2 %), then its header loads and
+    // the first quad's rows, in flight together while the headers decode
     v4u X[kQRows];
+    fill_tables(T);
+    __syncthreads();
+    if (!live)
+        return;
+    header_load(q);
 #pragma unroll
     for (int k = 0; k < kQRows; ++k)
         X[k] = load_row(q, k);
+    header_decode(q);
     for (;;) {
         const uint32_t d = 4u * q + g;
         const bool act = d < n;
@@ -1909,6 +1927,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
 #pragma unroll
             for (int k = 0; k < kQRows; ++k)
                 X[k] = load_row(qn, k);
+        } else if (qn < nquads) {
+            header_load(qn);
         }
 #pragma unroll
         for (int k = 0; k < kQRows; ++k)
@@ -1932,11 +1952,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (q >= nquads)
             break;
         if (batch_end) {
-            header_pass(q);
-            bt = 0;
 #pragma unroll
             for (int k = 0; k < kQRows; ++k)
                 X[k] = load_row(q, k);
+            header_decode(q);
+            bt = 0;
         }
     }
 }
